@@ -1,0 +1,310 @@
+"""Observation encoders: scalar (+ build-order transformer), entity, spatial, value-feature.
+
+Parameter names/shapes match ``distar/agent/default/model/obs_encoder/*.py`` and
+``model/encoder.py``.  The compute graph is restructured for MI355X:
+
+* entity one-hot/binary/scalar fields are never concatenated into a 997-wide tensor on the GPU:
+  ``ops.entity_embed`` sums the selected weight rows (one-hot @ W == row gather);
+* the entity transformer runs on packed real entities (no padding work);
+* the spatial one-hot planes + effect points + entity scatter are assembled by
+  ``ops.spatial_embed`` directly into the 1x1-projected 32-channel map.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..lib import game_data as gd
+from ..lib.features import (ENTITY_FIELDS, SPATIAL_ONE_HOT, EFFECT_KEYS, SPATIAL_SIZE, ENTITY_EMBED_DIM,
+                            BEGINNING_ORDER_LENGTH)
+from .blocks import FCBlock, ConvBlock, ResBlock, OneHotTable, binary_table, eye_table
+from .transformer import Transformer
+
+SPATIAL_Y, SPATIAL_X = SPATIAL_SIZE
+
+
+def _denominator(dim: int) -> torch.Tensor:
+    x = torch.arange(dim, dtype=torch.float)
+    x = torch.div(x, 2, rounding_mode='floor') * 2
+    return 1.0 / torch.pow(10000.0, x / dim)
+
+
+class BeginningBuildOrderEncoder(nn.Module):
+    """20-token pre-LN transformer over (action one-hot 174 | position one-hot 20 | 2x10-bit location)
+    -> mean -> fc 64 (scalar_encoder.py:19-53)."""
+
+    def __init__(self, output_dim: int = 64, head_dim: int = 8, binary_dim: int = 10):
+        super().__init__()
+        self.action_dim = gd.NUM_BEGINNING_ORDER_ACTIONS
+        in_dim = self.action_dim + BEGINNING_ORDER_LENGTH + 2 * binary_dim
+        self.transformer = Transformer(in_dim, head_dim=head_dim, hidden_dim=output_dim * 2, output_dim=output_dim,
+                                       ln_type='pre')
+        self.embedd_fc = FCBlock(output_dim, output_dim, act=True)
+        self.action_one_hot = OneHotTable(eye_table(self.action_dim))
+        self.order_one_hot = OneHotTable(eye_table(BEGINNING_ORDER_LENGTH))
+        self.location_binary = OneHotTable(binary_table(binary_dim))
+
+    def forward(self, bo: torch.Tensor, bo_location: torch.Tensor) -> torch.Tensor:
+        B, L = bo.shape
+        dev = bo.device
+        act = F.one_hot(bo.long().clamp(0, self.action_dim - 1), self.action_dim).float()
+        pos = torch.eye(L, device=dev).expand(B, L, L)
+        loc = bo_location.long()
+        lx = self.location_binary.weight[loc % SPATIAL_X]
+        ly = self.location_binary.weight[torch.div(loc, SPATIAL_X, rounding_mode='floor').clamp(max=1023)]
+        x = torch.cat([act, pos, lx, ly], dim=2)
+        x = self.transformer.forward_dense(x)
+        return self.embedd_fc(x.mean(dim=1))
+
+
+# (name, kind, in_dim/num, out_dim, scalar_context, baseline_feature) in reference module order
+SCALAR_MODULES = [
+    ('agent_statistics', 'fc', 10, 64, False, True),
+    ('home_race', 'emb', 5, 32, True, False),
+    ('away_race', 'emb', 5, 32, True, False),
+    ('upgrades', 'fc', gd.NUM_UPGRADES, 128, False, True),
+    ('unit_counts_bow', 'fc', gd.NUM_UNIT_TYPES, 128, False, True),
+    ('last_delay', 'emb', 128, 64, False, False),
+    ('last_queued', 'emb', 2, 32, False, False),
+    ('last_action_type', 'emb', gd.NUM_ACTIONS, 128, False, False),
+    ('cumulative_stat', 'fc', gd.NUM_CUMULATIVE_STAT_ACTIONS, 128, True, True),
+    ('beginning_order', 'bo', 0, 64, True, True),
+    ('unit_type_bool', 'fc', gd.NUM_UNIT_TYPES, 64, True, False),
+    ('enemy_unit_type_bool', 'fc', gd.NUM_UNIT_TYPES, 64, True, False),
+    ('unit_order_type', 'fc', gd.NUM_UNIT_MIX_ABILITIES, 64, True, False),
+]
+TIME_DIM = 32
+
+
+class ScalarEncoder(nn.Module):
+    """13 scalar fields -> embedded_scalar [B,1024], scalar_context [B,448], baseline_feature [B,512]."""
+
+    def __init__(self):
+        super().__init__()
+        self.encode_modules = nn.ModuleDict()
+        for name, kind, n_in, n_out, _, _ in SCALAR_MODULES:
+            if kind == 'fc':
+                self.encode_modules[name] = FCBlock(n_in, n_out, act=True)
+            elif kind == 'emb':
+                emb = nn.Embedding(n_in, n_out)
+                nn.init.xavier_uniform_(emb.weight)
+                self.encode_modules[name] = emb
+        self.position_array = nn.Parameter(_denominator(TIME_DIM), requires_grad=False)
+        # the reference registers the build-order transformer after the loop -> last in state_dict
+        self.encode_modules['beginning_order'] = BeginningBuildOrderEncoder(64)
+
+    def time_encoder(self, t: torch.Tensor) -> torch.Tensor:
+        ang = t.float().unsqueeze(1) * self.position_array
+        out = torch.empty_like(ang)
+        out[:, 0::2] = torch.sin(ang[:, 0::2])
+        out[:, 1::2] = torch.cos(ang[:, 1::2])
+        return out
+
+    def forward(self, x: Dict[str, torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        embedded, context, baseline = [], [], []
+        for name, kind, n_in, n_out, is_ctx, is_base in SCALAR_MODULES:
+            m = self.encode_modules[name]
+            if kind == 'emb':
+                e = F.relu(m(x[name].long().clamp(max=n_in - 1)))
+            elif kind == 'bo':
+                e = m(x['beginning_order'], x['bo_location'])
+            else:
+                e = m(x[name].float())
+            embedded.append(e)
+            if is_ctx:
+                context.append(e)
+            if is_base:
+                baseline.append(e)
+        embedded.append(self.time_encoder(x['time']).to(embedded[0].dtype))
+        return torch.cat(embedded, 1), torch.cat(context, 1), torch.cat(baseline, 1)
+
+
+def entity_field_layout() -> List[Tuple[str, str, int, int]]:
+    """[(name, encoding, column offset into the 997-wide input, width)]."""
+    out, off = [], 0
+    for name, _, enc, width in ENTITY_FIELDS:
+        out.append((name, enc, off, width))
+        off += width
+    return out
+
+
+ENTITY_LAYOUT = entity_field_layout()
+
+
+def entity_one_hot_input(entity_info: Dict[str, torch.Tensor], index: torch.Tensor, dtype) -> torch.Tensor:
+    """Reference construction of the 997-wide entity input for the selected (packed) entity rows."""
+    T = index.numel()
+    x = torch.zeros(T, ENTITY_EMBED_DIM, dtype=dtype, device=index.device)
+    rows = torch.arange(T, device=index.device)
+    for name, enc, off, width in ENTITY_LAYOUT:
+        v = entity_info[name].reshape(-1)[index]
+        if enc == 'one_hot':
+            x[rows, off + v.long().clamp(0, width - 1)] = 1
+        elif enc == 'binary':
+            bits = (v.long().unsqueeze(1) >> torch.arange(width - 1, -1, -1, device=v.device)) & 1
+            x[:, off:off + width] = bits.to(dtype)
+        else:
+            x[:, off] = v.to(dtype)
+    return x
+
+
+class EntityEncoder(nn.Module):
+    """Entity transformer (entity_encoder.py:20-96): 997 -> 256, 3 post-LN layers, 2 heads x 128."""
+
+    def __init__(self, reduce_type: str = 'selected_units_num'):
+        super().__init__()
+        self.encode_modules = nn.ModuleDict()
+        for name, enc, _, width in ENTITY_LAYOUT:
+            if enc == 'one_hot':
+                self.encode_modules[name] = OneHotTable(eye_table(width))
+            elif enc == 'binary':
+                self.encode_modules[name] = OneHotTable(binary_table(width))
+        self.transformer = Transformer(ENTITY_EMBED_DIM, head_dim=128, hidden_dim=1024, output_dim=256, head_num=2,
+                                       mlp_num=2, layer_num=3, ln_type='post')
+        self.entity_fc = FCBlock(256, 256, act=True)
+        self.embed_fc = FCBlock(256, 256, act=True)
+        self.reduce_type = reduce_type
+
+    def embed(self, entity_info, flat_index):
+        lin = self.transformer.embedding[0]
+        n = ops._native(lin.weight) if flat_index.is_cuda else None
+        if n is not None and n.has('entity_embed'):
+            return n.entity_embed(entity_info, flat_index, lin.weight, lin.bias)
+        x = entity_one_hot_input(entity_info, flat_index, lin.weight.dtype)
+        return ops.linear(x, lin.weight, lin.bias, act='relu')
+
+    def forward(self, entity_info: Dict[str, torch.Tensor], entity_num: torch.Tensor):
+        B, N = entity_info['unit_type'].shape
+        valid = ops.sequence_mask(entity_num, N)                     # [B,N]
+        flat_index = valid.reshape(-1).nonzero().squeeze(1)         # packed row -> padded row
+        lens = entity_num.clamp(max=N).to(torch.int32)
+        cu = F.pad(torch.cumsum(lens, 0, dtype=torch.int32), (1, 0))
+        x = self.embed(entity_info, flat_index)                      # [T,256]
+        x = self.transformer.forward_packed_embedded(x, cu, N)       # [T,256]
+        # the reference's inplace ReLU (entity_encoder.py:84) also rectifies x used by the mean below
+        x = F.relu(x)
+        ee = self.entity_fc(x)
+        entity_embeddings = x.new_zeros(B * N, ee.shape[-1])
+        entity_embeddings = entity_embeddings.index_copy(0, flat_index, ee).view(B, N, -1)
+        # masked mean of relu(transformer output) over real entities (entity_encoder.py:85-87)
+        seg = torch.repeat_interleave(torch.arange(B, device=x.device), lens.long(), output_size=x.shape[0])
+        summed = x.new_zeros(B, x.shape[-1]).index_add(0, seg, x)
+        if self.reduce_type == 'constant':
+            mean = summed / 512
+        else:
+            mean = summed / entity_num.clamp(min=1).unsqueeze(1).to(summed.dtype)
+        embedded_entity = self.embed_fc(mean)
+        return entity_embeddings, embedded_entity, valid
+
+
+class SpatialEncoder(nn.Module):
+    """spatial_encoder.py:9-90: 56 input planes -> 1x1 conv 32 -> 3x[maxpool2, conv3x3] (64,128,128)
+    -> 4 ResBlocks(128) @19x20 -> fc 48640 -> 256. Returns (embedding, map_skip[7])."""
+
+    def __init__(self):
+        super().__init__()
+        self.project = ConvBlock(56, 32, 1, act=True)
+        self.encode_modules = nn.ModuleDict({k: OneHotTable(eye_table(n)) for k, n in SPATIAL_ONE_HOT})
+        dims = [32, 64, 128, 128]
+        self.downsample = nn.ModuleList([ConvBlock(dims[i], dims[i + 1], 3, 1, 1, act=True) for i in range(3)])
+        self.res = nn.ModuleList([ResBlock(128) for _ in range(4)])
+        self.fc = FCBlock(128 * (SPATIAL_Y // 8) * (SPATIAL_X // 8), 256, act=True)
+
+    @staticmethod
+    def input_planes(spatial_info, scatter_map):
+        """Reference assembly of the 56 input planes [B,56,H,W] (spatial_encoder.py:51-70)."""
+        planes = [spatial_info['height_map'].unsqueeze(1).float() / 256]
+        for k, n in SPATIAL_ONE_HOT:
+            planes.append(F.one_hot(spatial_info[k].long().clamp(0, n - 1), n).permute(0, 3, 1, 2).float())
+        B = scatter_map.shape[0]
+        for k in EFFECT_KEYS:
+            m = torch.zeros(B, SPATIAL_Y * SPATIAL_X, device=scatter_map.device)
+            m.scatter_(1, spatial_info[k].long().clamp(0, SPATIAL_Y * SPATIAL_X - 1), 1.0)
+            planes.append(m.view(B, 1, SPATIAL_Y, SPATIAL_X))
+        planes.append(scatter_map.float())
+        return torch.cat(planes, 1)
+
+    def forward(self, spatial_info, scatter_map):
+        x = self.input_planes(spatial_info, scatter_map).to(self.project[0].weight.dtype)
+        x = self.project(x)
+        map_skip = []
+        for conv in self.downsample:
+            map_skip.append(x)
+            x = conv(F.max_pool2d(x, 2, 2))
+        for block in self.res:
+            map_skip.append(x)
+            x = block(x)
+        x = self.fc(x.reshape(x.shape[0], -1))
+        return x, map_skip
+
+
+class Encoder(nn.Module):
+    def __init__(self, reduce_type: str = 'selected_units_num'):
+        super().__init__()
+        self.scalar_encoder = ScalarEncoder()
+        self.spatial_encoder = SpatialEncoder()
+        self.entity_encoder = EntityEncoder(reduce_type)
+        self.scatter_project = FCBlock(256, 32, act=True)
+
+    def forward(self, spatial_info, entity_info, scalar_info, entity_num):
+        embedded_scalar, scalar_context, baseline_feature = self.scalar_encoder(scalar_info)
+        entity_embeddings, embedded_entity, entity_mask = self.entity_encoder(entity_info, entity_num)
+        proj = self.scatter_project(entity_embeddings) * entity_mask.unsqueeze(2).to(entity_embeddings.dtype)
+        scatter_map = ops.scatter_connection(proj, entity_info['x'], entity_info['y'], SPATIAL_Y, SPATIAL_X)
+        embedded_spatial, map_skip = self.spatial_encoder(spatial_info, scatter_map)
+        lstm_input = torch.cat([embedded_scalar, embedded_entity.to(embedded_scalar.dtype),
+                                embedded_spatial.to(embedded_scalar.dtype)], dim=-1)
+        return lstm_input, scalar_context, baseline_feature, entity_embeddings, map_skip
+
+
+VALUE_FC_MODULES = [('enemy_unit_counts_bow', gd.NUM_UNIT_TYPES, 64), ('enemy_unit_type_bool', gd.NUM_UNIT_TYPES, 64),
+                    ('enemy_agent_statistics', 10, 64), ('enemy_upgrades', gd.NUM_UPGRADES, 32),
+                    ('cumulative_stat', gd.NUM_CUMULATIVE_STAT_ACTIONS, 128)]
+
+
+class ValueEncoder(nn.Module):
+    """Opponent-aware critic features -> [B,544] (value_encoder.py:12-74)."""
+
+    def __init__(self):
+        super().__init__()
+        self.encode_modules = nn.ModuleDict()
+        for name, n_in, n_out in VALUE_FC_MODULES[:4]:
+            self.encode_modules[name] = FCBlock(n_in, n_out, act=True)
+        self.encode_modules['unit_alliance'] = nn.Embedding(2, 16)
+        self.encode_modules['unit_type'] = nn.Embedding(gd.NUM_UNIT_TYPES, 48)
+        self.encode_modules['beginning_order'] = BeginningBuildOrderEncoder(64)
+        name, n_in, n_out = VALUE_FC_MODULES[4]
+        self.encode_modules[name] = FCBlock(n_in, n_out, act=True)
+        self.scatter_project = FCBlock(64, 8, act=True)
+        self.project = ConvBlock(10, 16, 1, act=True)
+        dims = [16, 16, 32, 32]
+        layers = []
+        for i in range(3):
+            layers += [nn.MaxPool2d(2, 2), ConvBlock(dims[i], dims[i + 1], 3, 1, 1, act=True)]
+        self.downsample = nn.Sequential(*layers)
+        self.res = nn.ModuleList([ResBlock(32) for _ in range(4)])
+        self.spatial_fc = FCBlock(32 * (SPATIAL_Y // 8) * (SPATIAL_X // 8), 128, act=True)
+
+    def forward(self, x):
+        fc = [self.encode_modules[n](x[n].float()) for n, _, _ in VALUE_FC_MODULES]
+        bo = self.encode_modules['beginning_order'](x['beginning_order'], x['bo_location'])
+        emb = torch.cat([self.encode_modules['unit_alliance'](x['unit_alliance'].long()),
+                         self.encode_modules['unit_type'](x['unit_type'].long().clamp(0, gd.NUM_UNIT_TYPES - 1))], -1)
+        proj = self.scatter_project(emb)
+        U = proj.shape[1]
+        mask = ops.sequence_mask(x['total_unit_count'], U)
+        proj = proj * mask.unsqueeze(2).to(proj.dtype)
+        H, W = x['own_units_spatial'].shape[-2:]
+        sc = ops.scatter_connection(proj, x['unit_x'], x['unit_y'], H, W)
+        sp = torch.cat([sc.to(proj.dtype), x['own_units_spatial'].to(proj.dtype),
+                        x['enemy_units_spatial'].to(proj.dtype)], 1)
+        sp = self.downsample(self.project(sp))
+        for blk in self.res:
+            sp = blk(sp)
+        sp = self.spatial_fc(sp.reshape(sp.shape[0], -1))
+        fc_cat = torch.cat(fc, -1)
+        return torch.cat([fc_cat, sp.to(fc_cat.dtype), bo.to(fc_cat.dtype)], -1)

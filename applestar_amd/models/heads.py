@@ -1,0 +1,271 @@
+"""Autoregressive action heads: action_type -> delay -> queued -> selected_units -> target_unit ->
+target_location (``distar/agent/default/model/head/*.py``, ``policy.py:22-73``).
+
+Two execution modes per head:
+
+* **sampling** (actor inference): draw the action from ``softmax(logits / T)``.  Sampling uses an
+  explicit uniform ``u`` (inverse CDF), so given the same noise the native and reference paths pick
+  bit-identical actions.
+* **teacher-forced** (learner / teacher / SL): the behaviour action is given.  The selected-units
+  pointer network is *not* unrolled step by step here: because every step's autoregressive
+  embedding depends only on the (known) labels, all 64 steps' inputs are formed in parallel
+  (prefix sets of labelled keys), then one batched query MLP, one 32-d LN-LSTM scan and one batched
+  logits GEMM.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..lib import game_data as gd
+from ..lib.features import MAX_SELECTED_UNITS_NUM, SPATIAL_SIZE, MAX_ENTITY_NUM
+from .blocks import FCBlock, ResFCBlock, GLU, GatedResBlock, ConvBlock, glorot_uniform_
+from .lstm import StackedLNLSTM
+
+NEG = -1e9
+
+
+def sample_from_logits(logits: torch.Tensor, u: Optional[torch.Tensor] = None, generator=None) -> torch.Tensor:
+    """Inverse-CDF categorical sample over the last dim (rows of ``logits`` are already scaled).
+    ``u`` [rows] uniform in [0,1); drawn if not given."""
+    p = torch.softmax(logits.float(), dim=-1)
+    cdf = torch.cumsum(p, dim=-1)
+    if u is None:
+        u = torch.rand(p.shape[:-1], device=p.device, generator=generator)
+    x = (u.to(cdf.dtype) * cdf[..., -1]).unsqueeze(-1)
+    idx = torch.searchsorted(cdf, x, right=True).squeeze(-1)
+    return idx.clamp(max=p.shape[-1] - 1)
+
+
+class ActionTypeHead(nn.Module):
+    def __init__(self, input_dim=384, res_dim=256, action_num=gd.NUM_ACTIONS, context_dim=448, gate_dim=1024,
+                 action_map_dim=256):
+        super().__init__()
+        self.action_num = action_num
+        self.project = FCBlock(input_dim, res_dim, act=True)
+        self.res = nn.Sequential(ResFCBlock(res_dim), ResFCBlock(res_dim))
+        self.action_fc = GLU(res_dim, action_num, context_dim)
+        self.action_map_fc1 = FCBlock(action_num, action_map_dim, act=True)
+        self.action_map_fc2 = FCBlock(action_map_dim, action_map_dim)
+        self.glu1 = GLU(action_map_dim, gate_dim, context_dim)
+        self.glu2 = GLU(input_dim, gate_dim, context_dim)
+
+    def forward(self, lstm_output, scalar_context, temperature: float = 1.0, action_type=None,
+                race_mask: Optional[torch.Tensor] = None, u=None):
+        x = self.res(self.project(lstm_output))
+        logits = self.action_fc(x, scalar_context) / temperature
+        if race_mask is not None:
+            logits = logits.masked_fill(~race_mask.to(logits.device).unsqueeze(0), NEG)
+        if action_type is None:
+            action_type = sample_from_logits(logits, u)
+        # one-hot(a) @ W^T == column gather of action_map_fc1's weight
+        w1 = self.action_map_fc1[0]
+        e1 = F.relu(w1.weight.t()[action_type.long()] + w1.bias)
+        e1 = self.action_map_fc2(e1)
+        embedding = self.glu1(e1, scalar_context) + self.glu2(lstm_output, scalar_context)
+        return logits, action_type, embedding
+
+
+class _ArgMLPHead(nn.Module):
+    """Shared shape of DelayHead / QueuedHead (action_arg_head.py:27-86)."""
+
+    def __init__(self, n_out: int, input_dim=1024, decode_dim=256, map_dim=256, use_temperature=True):
+        super().__init__()
+        self.n_out = n_out
+        self.use_temperature = use_temperature
+        self.fc1 = FCBlock(input_dim, decode_dim, act=True)
+        self.fc2 = FCBlock(decode_dim, decode_dim, act=True)
+        self.fc3 = FCBlock(decode_dim, n_out)
+        self.embed_fc1 = FCBlock(n_out, map_dim, act=True)
+        self.embed_fc2 = FCBlock(map_dim, input_dim)
+
+    def forward(self, embedding, temperature: float = 1.0, action=None, u=None):
+        logits = self.fc3(self.fc2(self.fc1(embedding)))
+        if self.use_temperature:
+            logits = logits / temperature
+        if action is None:
+            action = sample_from_logits(logits, u)
+        w = self.embed_fc1[0]
+        e = F.relu(w.weight.t()[action.long()] + w.bias)
+        return logits, action, embedding + self.embed_fc2(e)
+
+
+class DelayHead(_ArgMLPHead):
+    def __init__(self):
+        super().__init__(128, use_temperature=False)  # reference never divides delay logits by T
+
+
+class QueuedHead(_ArgMLPHead):
+    def __init__(self):
+        super().__init__(2, use_temperature=True)
+
+
+class SelectedUnitsHead(nn.Module):
+    """Pointer network over entities + end token (action_arg_head.py:89-328)."""
+
+    def __init__(self, input_dim=1024, entity_dim=256, key_dim=32, func_dim=256, hidden_dim=32, num_layers=1,
+                 extra_units: bool = False):
+        super().__init__()
+        self.key_dim = key_dim
+        self.key_fc = FCBlock(entity_dim, key_dim)
+        self.query_fc1 = FCBlock(input_dim, func_dim, act=True)
+        self.query_fc2 = FCBlock(func_dim, key_dim)
+        self.embed_fc1 = FCBlock(key_dim, func_dim, act=True)
+        self.embed_fc2 = FCBlock(func_dim, input_dim)
+        self.lstm = StackedLNLSTM(key_dim, hidden_dim, num_layers)
+        self.end_embedding = nn.Parameter(torch.empty(1, key_dim))
+        glorot_uniform_(self.end_embedding)
+        self.extra_units = extra_units
+
+    def keys(self, entity_embedding, entity_num):
+        """key [B,N+1,32] with the learned end embedding at position entity_num; logits mask."""
+        B, N, _ = entity_embedding.shape
+        key = self.key_fc(entity_embedding)
+        key = F.pad(key, (0, 0, 0, 1))
+        ar = torch.arange(N + 1, device=key.device)
+        is_end = (ar[None, :] == entity_num[:, None]).unsqueeze(2)
+        key = torch.where(is_end, self.end_embedding.to(key.dtype).expand_as(key), key)
+        mask = ar[None, :] < (entity_num + 1)[:, None]
+        return key, mask
+
+    def _ae_update(self, ae0, emb):
+        return ae0 + self.embed_fc2(self.embed_fc1(emb))
+
+    # ------------------------------------------------------------------ teacher forced (parallel)
+    def forward_teacher(self, ae0, entity_embedding, entity_num, selected_units_num, selected_units):
+        key, base_mask = self.keys(entity_embedding, entity_num)          # [B,N+1,32], [B,N+1]
+        B, N1, C = key.shape
+        S = max(int(selected_units_num.max()), 1)
+        labels = selected_units[:, :S].long()                             # [B,S]
+        en = entity_num.long()
+        # end_flag after label i; a label is added to the selected set iff no end at or before i
+        is_end = labels == en[:, None]
+        ended = torch.cumsum(is_end.int(), 1) > 0
+        added = ~ended
+        # first occurrence among added labels (set semantics of the reference one-hot)
+        same = labels[:, :, None] == labels[:, None, :]                   # [B,S(i),S(j)]
+        earlier = torch.tril(torch.ones(S, S, dtype=torch.bool, device=key.device), -1)
+        dup = (same & earlier[None] & added[:, None, :]).any(-1)
+        new = added & ~dup
+        gathered = key.gather(1, labels.clamp(max=N1 - 1).unsqueeze(-1).expand(B, S, C))
+        run_sum = torch.cumsum(gathered * new.unsqueeze(-1).to(gathered.dtype), 1)
+        run_cnt = torch.cumsum(new.int(), 1)
+        div = torch.where((selected_units_num != 0)[:, None], run_cnt.clamp(min=1), torch.ones_like(run_cnt))
+        emb = run_sum / div.unsqueeze(-1).to(run_sum.dtype)              # embedding after step i
+        ae_after = self._ae_update(ae0.unsqueeze(1), emb)                # [B,S,1024]
+        ae_in = torch.cat([ae0.unsqueeze(1).to(ae_after.dtype), ae_after[:, :-1]], 1)
+        q_in = self.query_fc2(self.query_fc1(ae_in))                     # [B,S,32]
+        state = self.lstm.zero_state(B, q_in.device, torch.float32)
+        q, _ = self.lstm(q_in.transpose(0, 1), state)                    # [S,B,32]
+        logits = torch.bmm(q.transpose(0, 1).float(), key.float().transpose(1, 2))  # [B,S,N+1]
+        # mask: base, end disabled at step 0, labels[:i] masked at step i
+        prev = F.one_hot(labels.clamp(max=N1 - 1), N1).bool()            # [B,S,N+1]
+        prev_cum = torch.cumsum(prev.int(), 1) > 0
+        prev_excl = torch.cat([torch.zeros_like(prev_cum[:, :1]), prev_cum[:, :-1]], 1)
+        mask = base_mask[:, None, :] & ~prev_excl
+        end_pos = F.one_hot(en.clamp(max=N1 - 1), N1).bool()
+        mask[:, 0] &= ~end_pos
+        logits = logits.masked_fill(~mask, NEG)
+        return logits, selected_units, ae_after[:, -1], selected_units_num
+
+    # ------------------------------------------------------------------ sampling (actor)
+    def forward_sample(self, ae0, entity_embedding, entity_num, su_mask, temperature: float = 1.0,
+                       u: Optional[torch.Tensor] = None):
+        key, mask = self.keys(entity_embedding, entity_num)
+        B, N1, _ = key.shape
+        dev = key.device
+        ar_b = torch.arange(B, device=dev)
+        en = entity_num.long()
+        mask = mask.clone()
+        mask[ar_b, en] = False
+        end_flag = ~su_mask.bool()
+        su_num = torch.where(su_mask.bool(), torch.full_like(en, MAX_SELECTED_UNITS_NUM), torch.zeros_like(en))
+        one_hot = torch.zeros(B, N1, device=dev, dtype=key.dtype)
+        state = self.lstm.zero_state(B, dev, torch.float32)
+        ae = ae0
+        results, logits_list = [], []
+        result = None
+        step_logits = None
+        for i in range(MAX_SELECTED_UNITS_NUM):
+            if i == 1:
+                mask[ar_b, en] = True
+            if result is not None:
+                mask[ar_b, result] = False
+            q_in = self.query_fc2(self.query_fc1(ae)).unsqueeze(0)
+            q, state = self.lstm(q_in, state)
+            step_logits = torch.einsum('bc,bnc->bn', q[0].float(), key.float()).masked_fill(~mask, NEG) / temperature
+            ui = None if u is None else u[:, i]
+            result = sample_from_logits(step_logits, ui)
+            newly_end = (result == en) & ~end_flag
+            su_num = torch.where(newly_end, torch.full_like(su_num, i + 1), su_num)
+            end_flag = end_flag | (result == en)
+            results.append(result)
+            logits_list.append(step_logits)
+            keep = ~end_flag
+            one_hot[ar_b[keep], result[keep]] = 1
+            emb = (key * one_hot.unsqueeze(-1)).sum(1)
+            cnt = one_hot.sum(1, keepdim=True)
+            emb = torch.where(cnt > 0, emb / cnt.clamp(min=1), emb)
+            ae = self._ae_update(ae0, emb)
+            if bool(end_flag.all()):
+                break
+        extra = torch.zeros(B, MAX_ENTITY_NUM + 1, device=dev)
+        if self.extra_units:
+            end_logit = step_logits[ar_b, en]
+            ex = (step_logits > end_logit[:, None]) & ~end_flag[:, None]
+            extra[:, :N1] = ex.float()
+        return torch.stack(logits_list, 1), torch.stack(results, 1), ae, su_num, extra
+
+
+class TargetUnitHead(nn.Module):
+    def __init__(self, input_dim=1024, entity_dim=256, key_dim=32):
+        super().__init__()
+        self.key_fc = FCBlock(entity_dim, key_dim)
+        self.query_fc1 = FCBlock(input_dim, key_dim, act=True)
+        self.query_fc2 = FCBlock(key_dim, key_dim)
+
+    def forward(self, embedding, entity_embedding, entity_num, temperature: float = 1.0, target_unit=None, u=None):
+        key = self.key_fc(entity_embedding)
+        q = self.query_fc2(self.query_fc1(embedding))
+        logits = torch.einsum('bc,bnc->bn', q.float(), key.float())
+        mask = ops.sequence_mask(entity_num, key.shape[1])
+        logits = logits.masked_fill(~mask, NEG) / temperature
+        if target_unit is None:
+            target_unit = sample_from_logits(logits, u)
+        return logits, target_unit
+
+
+class LocationHead(nn.Module):
+    """fc 1024->1520 -> [B,4,19,20] || map_skip[-1] -> 1x1 conv 128 -> 4 gated res-blocks (+skips)
+    -> 3 x (bilinear x2, conv3x3) 128->64->32->1 -> 24,320 logits (action_arg_head.py:366-450)."""
+
+    def __init__(self, input_dim=1024, res_dim=128, res_num=4, reshape_channel=4, map_skip_dim=128,
+                 upsample_dims=(64, 32, 1)):
+        super().__init__()
+        self.reshape_channel = reshape_channel
+        self.hy, self.hx = SPATIAL_SIZE[0] // 8, SPATIAL_SIZE[1] // 8
+        self.conv1 = ConvBlock(map_skip_dim + reshape_channel, res_dim, 1, act=True)
+        self.res = nn.ModuleList()  # registered before project_embed, as in the reference
+        self.project_embed = FCBlock(input_dim, self.hy * self.hx * reshape_channel, act=True)
+        self.res.extend([GatedResBlock(res_dim) for _ in range(res_num)])
+        dims = [res_dim] + list(upsample_dims)
+        self.upsample = nn.ModuleList([ConvBlock(dims[i], dims[i + 1], 3, 1, 1, act=(i < len(upsample_dims) - 1))
+                                       for i in range(len(upsample_dims))])
+
+    def forward(self, embedding, map_skip: List[torch.Tensor], temperature: float = 1.0, location=None, u=None):
+        B = embedding.shape[0]
+        p = self.project_embed(embedding).reshape(B, self.reshape_channel, self.hy, self.hx)
+        x = F.relu(torch.cat([p.to(map_skip[-1].dtype), map_skip[-1]], 1))
+        x = self.conv1(x)
+        for i, blk in enumerate(self.res):
+            x = blk(x + map_skip[len(map_skip) - 1 - i])
+        for conv in self.upsample:
+            x = conv(F.interpolate(x, scale_factor=2.0, mode='bilinear', align_corners=False))
+        logits = x.reshape(B, -1).float() / temperature
+        if location is None:
+            location = sample_from_logits(logits, u)
+        return logits, location

@@ -1,0 +1,220 @@
+"""AlphaStar policy/value model.
+
+Module tree and parameter names are those of ``distar/agent/default/model/model.py:22-189`` so
+released ``rl_model.pth`` / ``sl_model.pth`` state dicts load unchanged.  Public forwards:
+
+* :meth:`Model.compute_logp_action` — actor inference (sample + log-prob)        (model.py:56-74)
+* :meth:`Model.compute_teacher_logit` — teacher-forced logits for the KL teacher (model.py:76-93)
+* :meth:`Model.rl_learner_forward` — flattened (T+1)*B learner forward          (model.py:95-168)
+* :meth:`Model.sl_train` — supervised forward over [B,T] chunks                  (model.py:170-189)
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..lib import game_data as gd
+from ..lib.features import MAX_SELECTED_UNITS_NUM, ACTION_HEADS
+from ..utils.config import AttrDict, deep_merge_dicts
+from .blocks import FCBlock, ResFCBlock2
+from .encoders import Encoder, ValueEncoder
+from .heads import (ActionTypeHead, DelayHead, QueuedHead, SelectedUnitsHead, TargetUnitHead, LocationHead,
+                    NEG)
+from .lstm import StackedLNLSTM
+
+BASELINE_NAMES = ['winloss', 'build_order', 'built_unit', 'effect', 'upgrade', 'battle']
+
+DEFAULT_MODEL_CONFIG = AttrDict({
+    'learner': {'use_value_feature': False},
+    'agent': {'extra_units': False},
+    'common': {'type': 'train'},
+    'model': {
+        'temperature': 1.0,
+        'enable_baselines': list(BASELINE_NAMES),
+        'entity_reduce_type': 'selected_units_num',
+        'only_update_baseline': False,
+        'value': {'res_dim': 256, 'res_num': 16, 'input_dim': 384},
+        'lstm': {'input_size': 1536, 'hidden_size': 384, 'num_layers': 3},
+    },
+})
+
+
+class ValueBaseline(nn.Module):
+    """fc(in->256, ReLU) -> 16 x ResFCBlock2 -> fc(256->1, gain .1) [-> (2/pi) atan(pi/2 x)] (value.py:9-39)."""
+
+    def __init__(self, input_dim: int, res_dim: int = 256, res_num: int = 16, atan: bool = False):
+        super().__init__()
+        self.project = FCBlock(input_dim, res_dim, act=True)
+        self.res = nn.Sequential(*[ResFCBlock2(res_dim) for _ in range(res_num)])
+        self.value_fc = FCBlock(res_dim, 1, init='xavier_uniform', gain=0.1)
+        self.atan = atan
+
+    def forward(self, x):
+        v = self.value_fc(self.res(self.project(x))).squeeze(1).float()
+        if self.atan:
+            v = (2.0 / torch.pi) * torch.atan((torch.pi / 2.0) * v)
+        return v
+
+
+class Policy(nn.Module):
+    def __init__(self, extra_units: bool = False):
+        super().__init__()
+        self.action_type_head = ActionTypeHead()
+        self.delay_head = DelayHead()
+        self.queued_head = QueuedHead()
+        self.selected_units_head = SelectedUnitsHead(extra_units=extra_units)
+        self.target_unit_head = TargetUnitHead()
+        self.location_head = LocationHead()
+
+    def forward(self, lstm_output, entity_embeddings, map_skip, scalar_context, entity_num, temperature=1.0,
+                race_mask=None, noise: Optional[Dict[str, torch.Tensor]] = None):
+        noise = noise or {}
+        logit, action = {}, {}
+        logit['action_type'], action['action_type'], emb = self.action_type_head(
+            lstm_output, scalar_context, temperature, race_mask=race_mask, u=noise.get('action_type'))
+        logit['delay'], action['delay'], emb = self.delay_head(emb, temperature, u=noise.get('delay'))
+        logit['queued'], action['queued'], emb = self.queued_head(emb, temperature, u=noise.get('queued'))
+        su_mask = gd.SELECTED_UNITS_MASK.to(action['action_type'].device)[action['action_type']]
+        logit['selected_units'], action['selected_units'], emb, su_num, extra = \
+            self.selected_units_head.forward_sample(emb, entity_embeddings, entity_num, su_mask, temperature,
+                                                    u=noise.get('selected_units'))
+        logit['target_unit'], action['target_unit'] = self.target_unit_head(
+            emb, entity_embeddings, entity_num, temperature, u=noise.get('target_unit'))
+        logit['target_location'], action['target_location'] = self.location_head(
+            emb, map_skip, temperature, u=noise.get('target_location'))
+        return action, su_num, logit, extra
+
+    def train_forward(self, lstm_output, entity_embeddings, map_skip, scalar_context, entity_num, action_info,
+                      selected_units_num, temperature=1.0):
+        logit, action = {}, {}
+        logit['action_type'], action['action_type'], emb = self.action_type_head(
+            lstm_output, scalar_context, temperature, action_type=action_info['action_type'])
+        logit['delay'], action['delay'], emb = self.delay_head(emb, temperature, action=action_info['delay'])
+        logit['queued'], action['queued'], emb = self.queued_head(emb, temperature, action=action_info['queued'])
+        logit['selected_units'], action['selected_units'], emb, su_num = \
+            self.selected_units_head.forward_teacher(emb, entity_embeddings, entity_num, selected_units_num,
+                                                     action_info['selected_units'])
+        logit['target_unit'], action['target_unit'] = self.target_unit_head(
+            emb, entity_embeddings, entity_num, temperature, target_unit=action_info['target_unit'])
+        logit['target_location'], action['target_location'] = self.location_head(
+            emb, map_skip, temperature, location=action_info['target_location'])
+        return action, su_num, logit
+
+
+class Model(nn.Module):
+    def __init__(self, cfg: Optional[dict] = None, use_value_network: bool = False, temperature: Optional[float] = None):
+        super().__init__()
+        self.whole_cfg = deep_merge_dicts(DEFAULT_MODEL_CONFIG, cfg or {})
+        mcfg = self.whole_cfg.model
+        if temperature is not None:
+            mcfg.temperature = temperature
+        self.cfg = mcfg
+        self.temperature = float(mcfg.temperature)
+        self.encoder = Encoder(mcfg.entity_reduce_type)
+        self.policy = Policy(extra_units=bool(self.whole_cfg.get('agent', {}).get('extra_units', False)))
+        self._use_value_feature = bool(self.whole_cfg.learner.get('use_value_feature', False))
+        self.use_value_network = use_value_network
+        if use_value_network:
+            if self._use_value_feature:
+                self.value_encoder = ValueEncoder()
+            self.value_networks = nn.ModuleDict()
+            in_dim = mcfg.value.input_dim + (1056 if self._use_value_feature else 0)
+            for name in BASELINE_NAMES:
+                if name in mcfg.enable_baselines:
+                    self.value_networks[name] = ValueBaseline(in_dim, mcfg.value.res_dim, mcfg.value.res_num,
+                                                              atan=(name == 'winloss'))
+        self.only_update_baseline = bool(mcfg.get('only_update_baseline', False))
+        lc = mcfg.lstm
+        self.core_lstm = StackedLNLSTM(lc.input_size, lc.hidden_size, lc.num_layers)
+        self.race_mask: Optional[torch.Tensor] = None  # set by the agent in play mode (action_type_head.py:52)
+
+    # ------------------------------------------------------------------ helpers
+    def _encode(self, spatial_info, entity_info, scalar_info, entity_num):
+        return self.encoder(spatial_info, entity_info, scalar_info, entity_num)
+
+    def _core(self, lstm_input_seq, hidden_state):
+        state = [(h.float(), c.float()) for h, c in hidden_state]
+        return self.core_lstm(lstm_input_seq, state)
+
+    # ------------------------------------------------------------------ actor inference
+    @torch.no_grad()
+    def compute_logp_action(self, spatial_info, entity_info, scalar_info, entity_num, hidden_state,
+                            noise: Optional[Dict[str, torch.Tensor]] = None, **kwargs):
+        lstm_input, scalar_context, _, entity_embeddings, map_skip = self._encode(
+            spatial_info, entity_info, scalar_info, entity_num)
+        out, out_state = self._core(lstm_input.unsqueeze(0), hidden_state)
+        action, su_num, logit, extra = self.policy(out[0], entity_embeddings, map_skip, scalar_context, entity_num,
+                                                   self.temperature, self.race_mask, noise)
+        logp = {}
+        for k, a in action.items():
+            lp = torch.log_softmax(logit[k].float(), dim=-1)
+            logp[k] = lp.gather(-1, a.long().unsqueeze(-1)).squeeze(-1)
+        return {'action_info': action, 'action_logp': logp, 'selected_units_num': su_num,
+                'entity_num': entity_num, 'hidden_state': out_state, 'logit': logit, 'extra_units': extra}
+
+    @torch.no_grad()
+    def compute_teacher_logit(self, spatial_info, entity_info, scalar_info, entity_num, hidden_state,
+                              selected_units_num, action_info, **kwargs):
+        lstm_input, scalar_context, _, entity_embeddings, map_skip = self._encode(
+            spatial_info, entity_info, scalar_info, entity_num)
+        out, out_state = self._core(lstm_input.unsqueeze(0), hidden_state)
+        _, su_num, logit = self.policy.train_forward(out[0], entity_embeddings, map_skip, scalar_context,
+                                                     entity_num, action_info, selected_units_num, self.temperature)
+        return {'logit': logit, 'hidden_state': out_state, 'entity_num': entity_num, 'selected_units_num': su_num}
+
+    # ------------------------------------------------------------------ learners
+    def rl_learner_forward(self, spatial_info, entity_info, scalar_info, entity_num, hidden_state, action_info,
+                           selected_units_num, batch_size: int, unroll_len: int, behaviour_logp=None,
+                           teacher_logit=None, mask=None, reward=None, step=None, value_feature=None, **kwargs):
+        """Observations are flattened time-major: index t*B + b for t in [0, T] (T+1 steps)."""
+        B, T = batch_size, unroll_len
+        flat_action = {k: v.flatten(0, 1) for k, v in action_info.items()}
+        flat_su_num = selected_units_num.flatten(0, 1)
+        lstm_input, scalar_context, baseline_feature, entity_embeddings, map_skip = self._encode(
+            spatial_info, entity_info, scalar_info, entity_num)
+        H = hidden_state[0][0].shape[-1]
+        h0 = [(h.view(-1, B, H)[0], c.view(-1, B, H)[0]) for h, c in hidden_state]
+        out, _ = self._core(lstm_input.view(T + 1, B, -1), h0)
+        lstm_output = out.reshape((T + 1) * B, -1)
+        n = T * B
+        _, _, logits = self.policy.train_forward(
+            lstm_output[:n], entity_embeddings[:n], [m[:n] for m in map_skip], scalar_context[:n],
+            entity_num[:n], flat_action, flat_su_num, self.temperature)
+        critic_input = lstm_output
+        if self.only_update_baseline:
+            critic_input = critic_input.detach()
+            baseline_feature = baseline_feature.detach()
+        if self._use_value_feature:
+            vf = self.value_encoder(value_feature)
+            critic_input = torch.cat([critic_input.to(vf.dtype), vf, baseline_feature.to(vf.dtype)], 1)
+        values = {k: v(critic_input).view(T + 1, B) for k, v in self.value_networks.items()}
+        for k in list(logits):
+            logits[k] = logits[k].view(T, B, *logits[k].shape[1:])
+        su = logits['selected_units']
+        logits['selected_units'] = F.pad(su, (0, 0, 0, MAX_SELECTED_UNITS_NUM - su.shape[2]), value=NEG)
+        return {'unroll_len': T, 'batch_size': B, 'selected_units_num': selected_units_num,
+                'target_logit': logits, 'value': values, 'action_log_prob': behaviour_logp,
+                'teacher_logit': teacher_logit, 'mask': mask, 'action': action_info, 'reward': reward,
+                'step': step}
+
+    def sl_train(self, spatial_info, entity_info, scalar_info, entity_num, selected_units_num, traj_lens,
+                 hidden_state, action_info, **kwargs):
+        """Inputs flattened batch-major [B*T]; hidden_state per layer [B,H]."""
+        B = len(traj_lens)
+        lstm_input, scalar_context, _, entity_embeddings, map_skip = self._encode(
+            spatial_info, entity_info, scalar_info, entity_num)
+        T = lstm_input.shape[0] // B
+        seq = lstm_input.view(B, T, -1).transpose(0, 1)
+        out, out_state = self._core(seq, hidden_state)
+        lstm_output = out.transpose(0, 1).reshape(B * T, -1)
+        action, su_num, logits = self.policy.train_forward(lstm_output, entity_embeddings, map_skip, scalar_context,
+                                                           entity_num, action_info, selected_units_num,
+                                                           self.temperature)
+        return logits, action, out_state
+
+    def policy_state_dict(self):
+        """Actor-facing weights (everything except value networks / value encoder)."""
+        return {k: v for k, v in self.state_dict().items() if 'value_networks' not in k and 'value_encoder' not in k}

@@ -1,0 +1,86 @@
+"""Transformer used by the entity encoder (post-LN, packed variable-length entity sets) and the
+beginning-build-order encoder (pre-LN, 20 tokens).
+
+Keys follow ``distar/agent/default/model/module_utils.py:71-199`` (``embedding.0``,
+``layers.i.attention.attention_pre.0``, ``.project.0``, ``layernorm1``, ``mlp.{0,1}.0``,
+``layernorm2``).  Unlike the reference (dense [B,2,N,N] scores over the padded batch), the entity
+path runs on *packed* tokens: GEMMs see only real entities and attention is a varlen kernel driven
+by ``cu_seqlens`` — identical outputs on every real token, no work on padding.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from .blocks import FCBlock
+
+
+class Attention(nn.Module):
+    def __init__(self, input_dim: int, head_dim: int, output_dim: int, head_num: int):
+        super().__init__()
+        self.head_num = head_num
+        self.head_dim = head_dim
+        self.attention_pre = FCBlock(input_dim, head_dim * head_num * 3)
+        self.project = FCBlock(head_dim * head_num, output_dim)
+
+    def forward_packed(self, x, cu_seqlens, max_len: int):
+        qkv = self.attention_pre(x)
+        a = ops.varlen_attention(qkv, cu_seqlens, max_len, self.head_num, self.head_dim)
+        return self.project(a)
+
+    def forward_dense(self, x, key_mask=None):
+        B, N, _ = x.shape
+        qkv = self.attention_pre(x).view(B, N, 3, self.head_num, self.head_dim).permute(2, 0, 3, 1, 4)
+        a = ops.masked_attention(qkv[0], qkv[1], qkv[2], key_mask)
+        a = a.permute(0, 2, 1, 3).reshape(B, N, self.head_num * self.head_dim)
+        return self.project(a)
+
+
+class TransformerLayer(nn.Module):
+    def __init__(self, dim: int, head_dim: int, hidden_dim: int, head_num: int, mlp_num: int, ln_type: str):
+        super().__init__()
+        self.attention = Attention(dim, head_dim, dim, head_num)
+        self.layernorm1 = nn.LayerNorm(dim)
+        dims = [dim] + [hidden_dim] * (mlp_num - 1) + [dim]
+        self.mlp = nn.Sequential(*[FCBlock(dims[i], dims[i + 1], act=True) for i in range(mlp_num)])
+        self.layernorm2 = nn.LayerNorm(dim)
+        self.ln_type = ln_type
+
+    def _ln(self, ln, x, residual=None):
+        return ops.layer_norm(x, ln.weight, ln.bias, residual=residual)
+
+    def forward_packed(self, x, cu_seqlens, max_len: int):
+        assert self.ln_type == 'post'
+        a = self.attention.forward_packed(x, cu_seqlens, max_len)
+        x = self._ln(self.layernorm1, a, residual=x)
+        m = self.mlp(x)
+        return self._ln(self.layernorm2, m, residual=x)
+
+    def forward_dense(self, x, key_mask=None):
+        if self.ln_type == 'post':
+            x = self._ln(self.layernorm1, self.attention.forward_dense(x, key_mask), residual=x)
+            return self._ln(self.layernorm2, self.mlp(x), residual=x)
+        x = x + self.attention.forward_dense(self._ln(self.layernorm1, x), key_mask)
+        return x + self.mlp(self._ln(self.layernorm2, x))
+
+
+class Transformer(nn.Module):
+    def __init__(self, input_dim: int, head_dim: int = 128, hidden_dim: int = 1024, output_dim: int = 256,
+                 head_num: int = 2, mlp_num: int = 2, layer_num: int = 3, ln_type: str = 'pre'):
+        super().__init__()
+        self.embedding = FCBlock(input_dim, output_dim, act=True)
+        self.layers = nn.ModuleList([TransformerLayer(output_dim, head_dim, hidden_dim, head_num, mlp_num, ln_type)
+                                     for _ in range(layer_num)])
+
+    def forward_dense(self, x, key_mask=None):
+        x = self.embedding(x)
+        for layer in self.layers:
+            x = layer.forward_dense(x, key_mask)
+        return x
+
+    def forward_packed_embedded(self, x, cu_seqlens, max_len: int):
+        """``x`` is the already-embedded packed token matrix [T, output_dim]."""
+        for layer in self.layers:
+            x = layer.forward_packed(x, cu_seqlens, max_len)
+        return x

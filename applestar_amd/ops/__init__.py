@@ -1,0 +1,89 @@
+"""Fused ops used by the AlphaStar policy / learner.
+
+Every op has one definition in :mod:`.reference` (PyTorch, used for CPU tensors and as the golden
+oracle in tests) and, for GPU tensors, a hand-written HIP/CDNA4 kernel in ``applestar_amd/csrc``
+exposed through :mod:`.native`.  GPU tensors never silently take the reference path for an op that
+has a native kernel: if the extension is missing, :func:`._ext.require` raises.
+
+Ops without a bespoke kernel (plain GEMMs, convolutions) use the vendor libraries through PyTorch
+(hipBLASLt / MIOpen) by design.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import reference as ref
+from . import _ext
+
+__all__ = ['linear', 'layer_norm', 'conv2d', 'gated_residual', 'lnlstm_layer', 'varlen_attention',
+           'masked_attention', 'scatter_connection', 'sequence_mask', 'native_enabled', 'set_native']
+
+_NATIVE_ENABLED = True
+
+
+def set_native(flag: bool) -> None:
+    """Globally disable native kernels (used by tests to produce a torch-only GPU baseline)."""
+    global _NATIVE_ENABLED
+    _NATIVE_ENABLED = bool(flag)
+
+
+def native_enabled() -> bool:
+    return _NATIVE_ENABLED
+
+
+def _native(t: torch.Tensor):
+    """Return the native module when ``t`` lives on a GPU (raising if it is not built), else None."""
+    if t.is_cuda and _NATIVE_ENABLED:
+        from . import native
+        native.ensure_loaded()
+        return native
+    return None
+
+
+sequence_mask = ref.sequence_mask
+masked_attention = ref.masked_attention
+
+
+def linear(x, w, b=None, act=None):
+    # plain GEMM -> hipBLASLt via torch; activation fused by the native epilogue kernel when present
+    y = F.linear(x, w, b)
+    if act is None:
+        return y
+    return ref.act_fn(y, act)
+
+
+def layer_norm(x, w, b, residual=None, act=None, eps: float = 1e-5):
+    n = _native(x)
+    if n is not None and n.has('layer_norm'):
+        return n.layer_norm(x, w, b, residual, act, eps)
+    return ref.layer_norm(x, w, b, residual, act, eps)
+
+
+def conv2d(x, w, b, stride=1, padding=0, act=None):
+    return ref.conv2d(x, w, b, stride, padding, act)
+
+
+def gated_residual(y, g, sp, x):
+    n = _native(x)
+    if n is not None and n.has('gated_residual'):
+        return n.gated_residual(y, g, sp, x)
+    return ref.gated_residual(y, g, sp, x)
+
+
+def lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b):
+    n = _native(x)
+    if n is not None and n.has('lnlstm_layer'):
+        return n.lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b)
+    return ref.lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b)
+
+
+def varlen_attention(qkv, cu_seqlens, max_len: int, num_heads: int, head_dim: int):
+    n = _native(qkv)
+    if n is not None and n.has('varlen_attention'):
+        return n.varlen_attention(qkv, cu_seqlens, max_len, num_heads, head_dim)
+    return ref.varlen_attention(qkv, cu_seqlens, max_len, num_heads, head_dim)
+
+
+def scatter_connection(proj, x, y, H: int, W: int):
+    return ref.scatter_connection(proj, x, y, H, W)

@@ -1,0 +1,69 @@
+"""One-off extractor: reads game-fact tables (action table, unit/buff/upgrade/addon id lists,
+ability id lists, per-race action masks) out of the reference tree by *parsing* its Python
+sources with ``ast`` (nothing from the reference is imported or executed) and writes them to
+``applestar_amd/lib/data/game_data.json``.
+
+These tables are facts about StarCraft II 4.10 that released checkpoints depend on
+(reorder arrays index into one-hot tables), so they must be bit-identical to the reference.
+
+Sources:
+  distar/agent/default/lib/actions.py:5-333       ACTIONS
+  distar/pysc2/lib/static_data.py:123-201,318-331 UNIT_TYPES, BUFFS, UPGRADES, ADDON, *_ABILITIES
+  distar/agent/default/lib/stat.py:533-631        ACTION_RACE_MASK
+"""
+import ast
+import json
+import os
+import sys
+
+REF = sys.argv[1] if len(sys.argv) > 1 else '/root/reference'
+OUT = os.path.join(os.path.dirname(__file__), '..', 'applestar_amd', 'lib', 'data', 'game_data.json')
+
+
+def _assignments(path):
+    tree = ast.parse(open(path).read())
+    out = {}
+    for node in tree.body:
+        if isinstance(node, ast.Assign) and len(node.targets) == 1 and isinstance(node.targets[0], ast.Name):
+            out[node.targets[0].id] = node.value
+    return out
+
+
+def _literal(node):
+    return ast.literal_eval(node)
+
+
+def _torch_tensor_arg(node):
+    # torch.tensor([...]) -> python list
+    assert isinstance(node, ast.Call)
+    return ast.literal_eval(node.args[0])
+
+
+def main():
+    acts = _assignments(os.path.join(REF, 'distar/agent/default/lib/actions.py'))
+    static = _assignments(os.path.join(REF, 'distar/pysc2/lib/static_data.py'))
+    stat = _assignments(os.path.join(REF, 'distar/agent/default/lib/stat.py'))
+    actions = _literal(acts['ACTIONS'])
+    race_mask_node = stat['ACTION_RACE_MASK']
+    race_mask = {}
+    for k, v in zip(race_mask_node.keys, race_mask_node.values):
+        race_mask[ast.literal_eval(k)] = [bool(x) for x in _torch_tensor_arg(v)]
+    data = {
+        'actions': actions,
+        'unit_types': _literal(static['UNIT_TYPES']),
+        'buffs': _literal(static['BUFFS']),
+        'upgrades': _literal(static['UPGRADES']),
+        'addon': _literal(static['ADDON']),
+        'unit_specific_abilities': _literal(static['UNIT_SPECIFIC_ABILITIES']),
+        'unit_general_abilities': _literal(static['UNIT_GENERAL_ABILITIES']),
+        'unit_mix_abilities': _literal(static['UNIT_MIX_ABILITIES']),
+        'action_race_mask': race_mask,
+    }
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    with open(OUT, 'w') as f:
+        json.dump(data, f, separators=(',', ':'))
+    print({k: len(v) for k, v in data.items()})
+
+
+if __name__ == '__main__':
+    main()
