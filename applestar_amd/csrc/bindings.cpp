@@ -1,0 +1,133 @@
+// PyTorch bindings for the applestar_amd HIP kernels.  Tensor checks happen here; the launchers in
+// kernels/*.hip only see raw pointers and the current HIP stream (graph-capturable).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "kernels.h"
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+int dt(const at::Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return as::DT_F32;
+  if (t.scalar_type() == at::kBFloat16) return as::DT_BF16;
+  TORCH_CHECK(false, "applestar_amd: unsupported dtype ", t.scalar_type());
+}
+
+void check_cuda(const at::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "applestar_amd: ", name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), "applestar_amd: ", name, " must be contiguous");
+}
+
+// ---------------------------------------------------------------- layer norm
+std::vector<at::Tensor> layer_norm_fwd(const at::Tensor& x, const c10::optional<at::Tensor>& res,
+                                       const at::Tensor& w, const at::Tensor& b, int64_t out_dtype, double eps,
+                                       int64_t act, bool save_sum) {
+  check_cuda(x, "x");
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 64 == 0 && C <= 1536, "layer_norm: cols must be a multiple of 64 and <= 1536");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat, "layer_norm: fp32 affine");
+  const int64_t rows = x.numel() / C;
+  c10::hip::HIPGuard g(x.device().index());
+  auto y = at::empty(x.sizes(), x.options().dtype(out_dtype == 1 ? at::kBFloat16 : at::kFloat));
+  auto mean = at::empty({rows}, x.options().dtype(at::kFloat));
+  auto rstd = at::empty({rows}, x.options().dtype(at::kFloat));
+  at::Tensor xsum;
+  const void* rp = nullptr;
+  int rdt = as::DT_F32;
+  if (res.has_value()) {
+    check_cuda(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes(), "layer_norm: residual shape");
+    rp = res->data_ptr();
+    rdt = dt(*res);
+    if (save_sum) xsum = at::empty(x.sizes(), x.options().dtype(at::kFloat));
+  }
+  as::layer_norm_fwd(x.data_ptr(), dt(x), rp, rdt, w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr(), dt(y),
+                     xsum.defined() ? xsum.data_ptr<float>() : nullptr, mean.data_ptr<float>(),
+                     rstd.data_ptr<float>(), rows, static_cast<int>(C), static_cast<float>(eps),
+                     static_cast<int>(act), stream());
+  return {y, mean, rstd, xsum.defined() ? xsum : at::Tensor()};
+}
+
+std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& xin, const at::Tensor& y,
+                                       const at::Tensor& w, const at::Tensor& mean, const at::Tensor& rstd,
+                                       int64_t dx_dtype, int64_t act) {
+  check_cuda(dy, "dy");
+  check_cuda(xin, "xin");
+  const int64_t C = xin.size(-1);
+  const int64_t rows = xin.numel() / C;
+  c10::hip::HIPGuard g(xin.device().index());
+  auto dx = at::empty(xin.sizes(), xin.options().dtype(dx_dtype == 1 ? at::kBFloat16 : at::kFloat));
+  const int nblk = as::layer_norm_bwd_blocks(rows);
+  auto part = at::empty({2, nblk, C}, xin.options().dtype(at::kFloat));
+  auto dw = at::empty({C}, xin.options().dtype(at::kFloat));
+  auto db = at::empty({C}, xin.options().dtype(at::kFloat));
+  const at::Tensor& yy = act != 0 ? y : dy;
+  as::layer_norm_bwd(dy.data_ptr(), dt(dy), xin.data_ptr(), dt(xin), yy.data_ptr(), dt(yy), w.data_ptr<float>(),
+                     mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dt(dx),
+                     part[0].data_ptr<float>(), part[1].data_ptr<float>(), rows, static_cast<int>(C),
+                     static_cast<int>(act), nblk, stream());
+  as::column_reduce(part[0].data_ptr<float>(), dw.data_ptr<float>(), nblk, static_cast<int>(C), stream());
+  as::column_reduce(part[1].data_ptr<float>(), db.data_ptr<float>(), nblk, static_cast<int>(C), stream());
+  return {dx, dw, db};
+}
+
+// ---------------------------------------------------------------- reverse scan
+at::Tensor reverse_scan(const at::Tensor& a, const at::Tensor& b, const at::Tensor& init) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  check_cuda(init, "init");
+  TORCH_CHECK(a.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat && init.scalar_type() == at::kFloat,
+              "reverse_scan: fp32");
+  TORCH_CHECK(a.sizes() == b.sizes() && a.dim() >= 2, "reverse_scan: a/b shape");
+  const int64_t B = a.size(-1), T = a.size(-2);
+  const int64_t K = a.numel() / (B * T);
+  TORCH_CHECK(init.numel() == K * B, "reverse_scan: init shape");
+  c10::hip::HIPGuard g(a.device().index());
+  auto y = at::empty_like(b);
+  as::reverse_scan(a.data_ptr<float>(), b.data_ptr<float>(), init.data_ptr<float>(), y.data_ptr<float>(),
+                   static_cast<int>(K), static_cast<int>(T), static_cast<int>(B), stream());
+  return y;
+}
+
+// ---------------------------------------------------------------- gated residual
+at::Tensor gated_residual_fwd(const at::Tensor& y, const at::Tensor& gt, const at::Tensor& sp, const at::Tensor& x) {
+  check_cuda(y, "y");
+  check_cuda(gt, "g");
+  check_cuda(x, "x");
+  TORCH_CHECK(y.scalar_type() == gt.scalar_type() && y.scalar_type() == x.scalar_type(), "gated_residual: dtypes");
+  TORCH_CHECK(y.sizes() == gt.sizes() && y.sizes() == x.sizes(), "gated_residual: shapes");
+  TORCH_CHECK(sp.scalar_type() == at::kFloat, "gated_residual: sp fp32");
+  c10::hip::HIPGuard g(y.device().index());
+  auto out = at::empty_like(y);
+  as::gated_residual_fwd(y.data_ptr(), gt.data_ptr(), sp.data_ptr<float>(), x.data_ptr(), out.data_ptr(), dt(y),
+                         y.numel(), stream());
+  return out;
+}
+
+std::vector<at::Tensor> gated_residual_bwd(const at::Tensor& dout, const at::Tensor& y, const at::Tensor& gt,
+                                           const at::Tensor& sp, const at::Tensor& out) {
+  check_cuda(dout, "dout");
+  TORCH_CHECK(dout.scalar_type() == y.scalar_type(), "gated_residual_bwd: dtype");
+  c10::hip::HIPGuard g(y.device().index());
+  auto dy = at::empty_like(y), dg = at::empty_like(y), dx = at::empty_like(y);
+  const int nblk = as::elementwise_blocks(y.numel());
+  auto part = at::empty({nblk}, y.options().dtype(at::kFloat));
+  as::gated_residual_bwd(dout.data_ptr(), y.data_ptr(), gt.data_ptr(), sp.data_ptr<float>(), out.data_ptr(), dt(y),
+                         dy.data_ptr(), dg.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), y.numel(), nblk,
+                         stream());
+  return {dy, dg, dx, part.sum().reshape({1})};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "applestar_amd HIP kernels for gfx950 (MI355X)";
+  m.def("layer_norm_fwd", &layer_norm_fwd);
+  m.def("layer_norm_bwd", &layer_norm_bwd);
+  m.def("reverse_scan", &reverse_scan);
+  m.def("gated_residual_fwd", &gated_residual_fwd);
+  m.def("gated_residual_bwd", &gated_residual_bwd);
+}

@@ -1,0 +1,106 @@
+"""Build the in-tree native extension ``applestar_amd/_C.<abi>.so`` for gfx950.
+
+* ``csrc/kernels/*.hip`` -> ``hipcc --offload-arch=gfx950 -O3`` (pure HIP, no torch headers: fast)
+* ``csrc/bindings.cpp``  -> ``g++`` against the PyTorch-ROCm headers (pybind11 + ATen)
+* link with libtorch / c10_hip / amdhip64.
+
+Incremental via ninja (a build.ninja is generated under ``build/csrc``).  No hipify, no CUDA
+sources: kernels are written for CDNA4 directly.  Usage: ``python -m applestar_amd.csrc.build``.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+ROOT = os.path.dirname(PKG)
+BUILD = os.path.join(ROOT, 'build', 'csrc')
+ARCH = os.environ.get('APPLESTAR_OFFLOAD_ARCH', 'gfx950')
+ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
+
+
+def _torch_paths():
+    import torch
+    tdir = os.path.dirname(torch.__file__)
+    inc = [os.path.join(tdir, 'include'), os.path.join(tdir, 'include', 'torch', 'csrc', 'api', 'include')]
+    lib = os.path.join(tdir, 'lib')
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return inc, lib, abi
+
+
+def ext_filename() -> str:
+    suffix = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
+    return os.path.join(PKG, '_C' + suffix)
+
+
+def write_ninja() -> str:
+    inc, lib, abi = _torch_paths()
+    py_inc = sysconfig.get_paths()['include']
+    kernels = sorted(glob.glob(os.path.join(HERE, 'kernels', '*.hip')))
+    hipcc = os.path.join(ROCM, 'bin', 'hipcc')
+    hip_flags = (f'--offload-arch={ARCH} -O3 -fPIC -std=c++17 -ffast-math -fno-gpu-rdc -I{HERE} '
+                 f'-D__HIP_PLATFORM_AMD__ -Wno-unused-result')
+    cxx_flags = ' '.join([
+        '-O2 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -DTORCH_EXTENSION_NAME=_C',
+        '-DTORCH_API_INCLUDE_EXTENSION_H', f'-D_GLIBCXX_USE_CXX11_ABI={abi}', f'-I{HERE}',
+        ' '.join(f'-isystem {p}' for p in inc), f'-isystem {py_inc}', f'-isystem {ROCM}/include',
+        '-Wno-deprecated-declarations'])
+    ldflags = ' '.join([f'-L{lib}', '-lc10', '-ltorch', '-ltorch_cpu', '-ltorch_python', '-lc10_hip', '-ltorch_hip',
+                        f'-L{ROCM}/lib', '-lamdhip64', f'-Wl,-rpath,{lib}', f'-Wl,-rpath,{ROCM}/lib'])
+    lines = [
+        'ninja_required_version = 1.3',
+        f'hipcc = {hipcc}',
+        f'hipflags = {hip_flags}',
+        f'cxxflags = {cxx_flags}',
+        f'ldflags = {ldflags}',
+        'rule hip',
+        '  command = $hipcc $hipflags -c $in -o $out -MD -MF $out.d',
+        '  depfile = $out.d',
+        '  deps = gcc',
+        '  description = HIPCC $in',
+        'rule cxx',
+        '  command = g++ $cxxflags -c $in -o $out -MD -MF $out.d',
+        '  depfile = $out.d',
+        '  deps = gcc',
+        '  description = CXX $in',
+        'rule link',
+        '  command = g++ -shared $in -o $out $ldflags',
+        '  description = LINK $out',
+    ]
+    objs = []
+    for k in kernels:
+        o = os.path.join(BUILD, os.path.basename(k) + '.o')
+        lines.append(f'build {o}: hip {k}')
+        objs.append(o)
+    b_o = os.path.join(BUILD, 'bindings.o')
+    lines.append(f'build {b_o}: cxx {os.path.join(HERE, "bindings.cpp")}')
+    objs.append(b_o)
+    lines.append(f'build {ext_filename()}: link {" ".join(objs)}')
+    lines.append(f'default {ext_filename()}')
+    os.makedirs(BUILD, exist_ok=True)
+    path = os.path.join(BUILD, 'build.ninja')
+    with open(path, 'w') as f:
+        f.write('\n'.join(lines) + '\n')
+    return path
+
+
+def build(verbose: bool = False, jobs: int | None = None) -> str:
+    path = write_ninja()
+    ninja = shutil.which('ninja')
+    if ninja is None:
+        import ninja as _ninja  # wheel
+        ninja = os.path.join(_ninja.BIN_DIR, 'ninja')
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    cmd = [ninja, '-f', path, f'-j{jobs}'] + (['-v'] if verbose else [])
+    subprocess.run(cmd, check=True, cwd=BUILD)
+    return ext_filename()
+
+
+if __name__ == '__main__':
+    out = build(verbose='-v' in sys.argv)
+    print(out)

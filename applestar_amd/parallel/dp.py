@@ -1,0 +1,121 @@
+"""Bucketed, backward-overlapped gradient all-reduce for the data-parallel learner.
+
+The reference (``dist_helper.py:421-431``) all-reduces each of 394-474 parameter tensors one by one
+after backward.  Here every parameter's ``.grad`` is a *view* into a small number of flat buckets;
+a post-accumulate-grad hook counts arrivals and, as soon as a bucket is complete, launches one async
+RCCL all-reduce for it while backward continues into earlier layers.  ``synchronize()`` (called
+before clip/optimizer) only waits for the tail bucket.
+
+Bucket size is chosen for xGMI rings (7 point-to-point links at ~153 GB/s per MI355X): a ring
+all-reduce moves 2(n-1)/n of the bucket over each link, so fewer, larger buckets (default 32 MB)
+amortise RCCL launch latency while still leaving several buckets to overlap with backward on a
+~33 M-parameter model (132 MB of fp32 gradients -> ~5 buckets).
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import dist as pdist
+
+
+class _Bucket:
+    __slots__ = ('params', 'flat', 'ready', 'handle', 'comm')
+
+    def __init__(self, params: List[torch.nn.Parameter], dtype, device):
+        self.params = params
+        n = sum(p.numel() for p in params)
+        self.flat = torch.zeros(n, dtype=dtype, device=device)
+        self.ready = 0
+        self.handle = None
+        self.comm = None
+
+
+class GradientReducer:
+    def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 32.0,
+                 comm_dtype: Optional[torch.dtype] = None, group=None, overlap: bool = True):
+        self.group = group
+        self.world = pdist.get_world_size()
+        self.overlap = overlap
+        self.comm_dtype = comm_dtype
+        params = [p for p in params if p.requires_grad]
+        self.params = params
+        self.buckets: List[_Bucket] = []
+        self._owner = {}
+        # backward visits layers roughly in reverse registration order
+        cur, cur_bytes = [], 0
+        limit = int(bucket_mb * 1024 * 1024)
+        for p in reversed(params):
+            key = (p.dtype, p.device)
+            if cur and ((cur[0].dtype, cur[0].device) != key or cur_bytes + p.numel() * p.element_size() > limit):
+                self._add_bucket(cur)
+                cur, cur_bytes = [], 0
+            cur.append(p)
+            cur_bytes += p.numel() * p.element_size()
+        if cur:
+            self._add_bucket(cur)
+        self._hooks = []
+        if self.world > 1 and overlap:
+            for p in params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+        self.use_avg = self.world > 1 and dist.get_backend(group) == 'nccl'
+
+    def _add_bucket(self, params):
+        b = _Bucket(params, params[0].dtype, params[0].device)
+        off = 0
+        for p in params:
+            n = p.numel()
+            p.grad = b.flat[off:off + n].view_as(p)
+            self._owner[p] = b
+            off += n
+        self.buckets.append(b)
+
+    @property
+    def num_buckets(self) -> int:
+        return len(self.buckets)
+
+    def _launch(self, b: _Bucket):
+        if b.handle is not None or self.world == 1:
+            return
+        buf = b.flat
+        if self.comm_dtype is not None and self.comm_dtype != buf.dtype:
+            b.comm = buf.to(self.comm_dtype)
+            buf = b.comm
+        op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
+        b.handle = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
+
+    def _on_grad(self, p):
+        b = self._owner[p]
+        b.ready += 1
+        if b.ready == len(b.params):
+            self._launch(b)
+
+    def zero_grad(self):
+        for b in self.buckets:
+            b.flat.zero_()
+            b.ready = 0
+            b.handle = None
+            b.comm = None
+        for p in self.params:  # re-attach in case someone set grads to None
+            if p.grad is None or p.grad.data_ptr() == 0:
+                raise RuntimeError('gradient view detached from its bucket; use GradientReducer.zero_grad()')
+
+    def synchronize(self):
+        if self.world == 1:
+            return
+        for b in self.buckets:
+            self._launch(b)  # buckets with unused params (or overlap disabled) go now
+        for b in self.buckets:
+            b.handle.wait()
+            if b.comm is not None:
+                b.flat.copy_(b.comm)
+            if not self.use_avg:
+                b.flat.div_(self.world)
+            b.handle = None
+
+    def remove(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

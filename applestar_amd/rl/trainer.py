@@ -1,0 +1,94 @@
+"""One RL learner iteration (forward -> loss -> backward -> all-reduce -> clip -> Adam).
+
+Step semantics of ``RLLearner._train`` (``distar/agent/default/rl_learner.py:82-145``): Adam with
+betas (0, 0.99), eps 1e-5, ``pytorch_norm`` clip at 1.0, value pre-training phase that trains only
+the critic for ``value_pretrain_iters`` iterations.  MI355X specifics: bf16 autocast for every GEMM /
+conv (fp32 master weights, fp32 LayerNorm/softmax/loss), gradients all-reduced in overlapped buckets
+over RCCL, sync-free logging.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import Dict, Optional
+
+import torch
+
+from ..models.model import Model
+from ..parallel import dist as pdist
+from ..parallel.dp import GradientReducer
+from ..utils.config import AttrDict, deep_merge_dicts
+from ..utils.grad_clip import build_grad_clip
+from .loss import ReinforcementLoss
+
+DEFAULT_LEARNER_CONFIG = AttrDict({
+    'learner': {
+        'player_id': 'MP0',
+        'learning_rate': 1e-5,
+        'weight_decay': 0.0,
+        'use_value_feature': True,
+        'value_pretrain_iters': -1,
+        'grad_clip': {'type': 'pytorch_norm', 'threshold': 1.0},
+        'bucket_mb': 32,
+        'comm_dtype': None,
+        'amp_dtype': 'bfloat16',
+    },
+    'model': {'enable_baselines': ['winloss']},
+})
+
+
+def _amp(device: torch.device, dtype_name: Optional[str]):
+    if device.type != 'cuda' or not dtype_name:
+        return contextlib.nullcontext()
+    return torch.autocast('cuda', dtype=getattr(torch, dtype_name))
+
+
+class RLTrainer:
+    def __init__(self, cfg: Optional[dict] = None, device='cpu', model: Optional[Model] = None):
+        self.cfg = deep_merge_dicts(DEFAULT_LEARNER_CONFIG, cfg or {})
+        lc = self.cfg.learner
+        self.device = torch.device(device)
+        self.model = model if model is not None else Model(self.cfg, use_value_network=True)
+        self.model.to(self.device)
+        pdist.broadcast_module(self.model)
+        self.params = [p for p in self.model.parameters() if p.requires_grad]
+        comm = getattr(torch, lc.comm_dtype) if lc.get('comm_dtype') else None
+        self.reducer = GradientReducer(self.params, bucket_mb=lc.bucket_mb, comm_dtype=comm)
+        fused = self.device.type == 'cuda'
+        self.optimizer = torch.optim.Adam(self.params, lr=lc.learning_rate, betas=(0.0, 0.99), eps=1e-5,
+                                          weight_decay=lc.weight_decay, fused=fused)
+        self.grad_clip = build_grad_clip(lc.grad_clip)
+        self.loss = ReinforcementLoss(lc, lc.player_id)
+        self.iter = 0
+        self.remain_value_pretrain = int(lc.get('value_pretrain_iters', -1))
+        self.amp_dtype = lc.get('amp_dtype')
+
+    def _value_pretrain_toggle(self):
+        active = self.remain_value_pretrain > 0
+        self.model.only_update_baseline = active
+        self.loss.only_update_value = active
+        if active:
+            self.remain_value_pretrain -= 1
+
+    def step(self, batch: Dict) -> Dict[str, torch.Tensor]:
+        self._value_pretrain_toggle()
+        self.model.train()
+        with _amp(self.device, self.amp_dtype):
+            out = self.model.rl_learner_forward(**batch)
+        info = self.loss.compute_loss(out)
+        self.reducer.zero_grad()
+        info['total_loss'].backward()
+        self.reducer.synchronize()
+        info['gradient'] = self.grad_clip.apply(self.params)
+        self.optimizer.step()
+        self.iter += 1
+        return info
+
+    def state_dict(self):
+        return {'model': self.model.state_dict(), 'optimizer': self.optimizer.state_dict(),
+                'last_iter': self.iter, 'grad_clip': self.grad_clip.state_dict()}
+
+    def load_state_dict(self, sd, load_optimizer=True):
+        self.model.load_state_dict(sd['model'], strict=False)
+        if load_optimizer and 'optimizer' in sd:
+            self.optimizer.load_state_dict(sd['optimizer'])
+        self.iter = int(sd.get('last_iter', 0))

@@ -1,0 +1,109 @@
+"""Gradient clipping policies (``distar/ctools/torch_utils/grad_clip.py:7-150``):
+``none``, ``max_norm`` (EMA-scaled), ``momentum_norm`` (per-parameter norm vs its EMA, used by SL),
+``clip_value`` (Adam-like second-moment clamp), ``clip_const`` and ``pytorch_norm`` (RL, threshold 1).
+
+All policies are device-side and sync-free: per-tensor norms come from one ``_foreach_norm`` and the
+EMA state lives on the device, so a clip never forces a host round trip (the reference calls
+``.item()`` once per parameter).  ``apply`` returns the pre-clip global norm as a 0-d tensor.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterable, List
+
+import torch
+
+CLIP_TYPES = ('none', 'max_norm', 'momentum_norm', 'clip_value', 'clip_const', 'pytorch_norm', 'clip_norm')
+
+
+def build_grad_clip(cfg) -> 'GradClip':
+    cfg = cfg or {}
+    norm_type = cfg.get('norm_type', 2)
+    if norm_type == 'inf':
+        norm_type = math.inf
+    return GradClip(cfg.get('type', 'none'), cfg.get('threshold', 1.4), norm_type, cfg.get('begin_step', 100),
+                    cfg.get('ignore_threshold', 3))
+
+
+def _grads(parameters) -> List[torch.Tensor]:
+    if isinstance(parameters, torch.Tensor):
+        parameters = [parameters]
+    return [p.grad for p in parameters if p.grad is not None]
+
+
+def _global_norm(norms: List[torch.Tensor], norm_type: float) -> torch.Tensor:
+    st = torch.stack(norms)
+    if math.isinf(norm_type):
+        return st.max()
+    return st.pow(norm_type).sum().pow(1.0 / norm_type)
+
+
+class GradClip:
+    def __init__(self, clip_type='none', threshold=1.4, norm_type=2, begin_step=100, ignore_threshold=3):
+        assert clip_type in CLIP_TYPES, clip_type
+        self.clip_type = clip_type
+        self.threshold = float(threshold)
+        self.norm_type = float(norm_type)
+        self.begin_step = begin_step
+        self.ignore_threshold = ignore_threshold
+        self.beta1, self.beta2 = 0.95, 0.999
+        self.step = 0
+        self.clip_value = None       # max_norm EMA (device scalar)
+        self.norm_mom = None         # momentum_norm per-parameter EMA (device vector)
+        self.exp_avg_sq = None       # clip_value second moments
+
+    def state_dict(self):
+        return {'step': self.step, 'clip_value': self.clip_value, 'norm_mom': self.norm_mom,
+                'exp_avg_sq': self.exp_avg_sq}
+
+    def load_state_dict(self, sd):
+        self.step = sd.get('step', 0)
+        self.clip_value = sd.get('clip_value')
+        self.norm_mom = sd.get('norm_mom')
+        self.exp_avg_sq = sd.get('exp_avg_sq')
+
+    @torch.no_grad()
+    def apply(self, parameters: Iterable[torch.nn.Parameter]) -> torch.Tensor:
+        self.step += 1
+        grads = _grads(list(parameters))
+        if not grads:
+            return torch.zeros(())
+        norms = list(torch._foreach_norm(grads, self.norm_type))
+        total = _global_norm(norms, self.norm_type)
+        t = self.clip_type
+        if t in ('pytorch_norm', 'clip_norm'):
+            coef = (self.threshold / (total + 1e-6)).clamp(max=1.0)
+            torch._foreach_mul_(grads, coef)
+        elif t == 'max_norm':
+            bc1 = 1 - self.beta1 ** self.step
+            if self.clip_value is None:
+                self.clip_value = torch.zeros_like(total)
+            if self.step > self.begin_step:
+                coef = ((self.clip_value / bc1) * self.threshold / (total + 1e-6)).clamp(max=1.0)
+                torch._foreach_mul_(grads, coef)
+            self.clip_value = self.beta1 * self.clip_value + (1 - self.beta1) * total
+        elif t == 'momentum_norm':
+            g = torch.stack(norms)
+            if self.norm_mom is None:
+                scale = torch.ones_like(g)
+            else:
+                scale = torch.where(g < self.threshold * self.norm_mom, torch.ones_like(g),
+                                    self.threshold * self.norm_mom / (g + 1e-6))
+            torch._foreach_mul_(grads, list(scale.unbind()))
+            new = g * scale
+            self.norm_mom = new.clone() if self.norm_mom is None else self.norm_mom * 0.99 + new * 0.01
+            total = _global_norm(list(new.unbind()), self.norm_type)
+        elif t == 'clip_value':
+            bc2 = 1 - self.beta2 ** self.step
+            if self.exp_avg_sq is None:
+                self.exp_avg_sq = [torch.zeros_like(g) for g in grads]
+            torch._foreach_mul_(self.exp_avg_sq, self.beta2)
+            torch._foreach_addcmul_(self.exp_avg_sq, grads, grads, 1 - self.beta2)
+            if self.step >= 100:
+                for g, s in zip(grads, self.exp_avg_sq):
+                    lim = s.sqrt() / math.sqrt(bc2) * 5
+                    g.copy_(torch.where(g.abs() > lim, lim, g))
+        elif t == 'clip_const':
+            for g in grads:
+                g.clamp_(-self.threshold, self.threshold)
+        return total

@@ -1,0 +1,82 @@
+"""Native HIP kernels vs plain-PyTorch fp32 references (run on an MI355X)."""
+import pytest
+import torch
+
+from applestar_amd.ops import reference as R
+from applestar_amd.ops import native as N
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _load():
+    N.ensure_loaded()
+
+
+def _err(a, b):
+    return (a.float() - b.float()).abs().max().item()
+
+
+@pytest.mark.parametrize('cols', [64, 256, 384, 1536])
+@pytest.mark.parametrize('x_dtype,res_dtype', [(torch.float32, None), (torch.bfloat16, torch.float32),
+                                               (torch.bfloat16, torch.bfloat16), (torch.float32, torch.float32)])
+@pytest.mark.parametrize('act', [None, 'relu'])
+def test_layer_norm_matches_reference(cols, x_dtype, res_dtype, act):
+    torch.manual_seed(0)
+    rows = 1031
+    x = torch.randn(rows, cols, device=DEV).to(x_dtype).requires_grad_()
+    res = torch.randn(rows, cols, device=DEV).to(res_dtype).requires_grad_() if res_dtype else None
+    w = (1 + 0.1 * torch.randn(cols, device=DEV)).requires_grad_()
+    b = (0.1 * torch.randn(cols, device=DEV)).requires_grad_()
+    y = N.layer_norm(x, w, b, residual=res, act=act)
+    xr = x.detach().float().requires_grad_()
+    rr = res.detach().float().requires_grad_() if res is not None else None
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    yr = R.layer_norm(xr, wr, br, rr, act)
+    assert _err(y, yr) < 2e-5 * 10
+    g = torch.randn_like(yr)
+    y.backward(g.to(y.dtype))
+    yr.backward(g)
+    tol = 3e-2 if x_dtype == torch.bfloat16 else 1e-4
+    assert _err(x.grad, xr.grad) < tol * max(1.0, xr.grad.abs().max().item())
+    if res is not None:
+        assert _err(res.grad, rr.grad) < tol * max(1.0, rr.grad.abs().max().item())
+    assert _err(w.grad, wr.grad) < 1e-3 * max(1.0, wr.grad.abs().max().item())
+    assert _err(b.grad, br.grad) < 1e-3 * max(1.0, br.grad.abs().max().item())
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_gated_residual(dtype):
+    torch.manual_seed(1)
+    shape = (5, 128, 19, 20)
+    y, g, x = (torch.randn(shape, device=DEV).to(dtype).requires_grad_() for _ in range(3))
+    sp = torch.full((1,), 0.1, device=DEV, requires_grad=True)
+    out = N.gated_residual(y, g, sp, x)
+    ys, gs, xs = (t.detach().float().requires_grad_() for t in (y, g, x))
+    sps = sp.detach().clone().requires_grad_()
+    ref = R.gated_residual(ys, gs, sps, xs)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert _err(out, ref) < tol
+    d = torch.randn_like(ref)
+    out.backward(d.to(dtype))
+    ref.backward(d)
+    for a, b in ((y.grad, ys.grad), (g.grad, gs.grad), (x.grad, xs.grad)):
+        assert _err(a, b) < tol * 4
+    assert abs(sp.grad.item() - sps.grad.item()) < 1e-2 * max(1, abs(sps.grad.item()))
+
+
+def test_reverse_scan():
+    torch.manual_seed(2)
+    K, T, B = 6, 64, 6
+    a = torch.rand(K, T, B, device=DEV)
+    b = torch.randn(K, T, B, device=DEV)
+    init = torch.randn(K, B, device=DEV)
+    y = N.reverse_scan(a, b, init)
+    ref = torch.empty_like(b)
+    acc = init.clone()
+    for t in range(T - 1, -1, -1):
+        acc = a[:, t] * acc + b[:, t]
+        ref[:, t] = acc
+    assert _err(y, ref) < 1e-5
