@@ -121,6 +121,63 @@ std::vector<at::Tensor> gated_residual_bwd(const at::Tensor& dout, const at::Ten
   return {dy, dg, dx, part.sum().reshape({1})};
 }
 
+// ---------------------------------------------------------------- LN-LSTM recurrence
+std::vector<at::Tensor> lnlstm_fwd(const at::Tensor& xp, const at::Tensor& h0, const at::Tensor& c0,
+                                   const at::Tensor& wT, const at::Tensor& lnh_w, const at::Tensor& lnh_b,
+                                   const at::Tensor& lnc_w, const at::Tensor& lnc_b, double eps) {
+  for (auto* t : {&xp, &h0, &c0, &wT, &lnh_w, &lnh_b, &lnc_w, &lnc_b}) check_cuda(*t, "lnlstm input");
+  TORCH_CHECK(xp.scalar_type() == at::kFloat && h0.scalar_type() == at::kFloat && c0.scalar_type() == at::kFloat,
+              "lnlstm: fp32 activations");
+  const int64_t T = xp.size(0), B = xp.size(1), G = xp.size(2), H = G / 4;
+  TORCH_CHECK(as::lnlstm_supported(static_cast<int>(H)), "lnlstm: unsupported hidden size ", H);
+  TORCH_CHECK(wT.size(0) == H && wT.size(1) == G, "lnlstm: wT must be [H, 4H]");
+  TORCH_CHECK(h0.size(0) == B && h0.size(1) == H && c0.sizes() == h0.sizes(), "lnlstm: state shape");
+  c10::hip::HIPGuard g(xp.device().index());
+  auto f = xp.options().dtype(at::kFloat);
+  auto out = at::empty({T, B, H}, f);
+  auto c_all = at::empty({T + 1, B, H}, f);
+  auto xhat_h = at::empty({T, B, G}, f);
+  auto gates = at::empty({T, B, G}, f);
+  auto xhat_c = at::empty({T, B, H}, f);
+  auto rstd_h = at::empty({T, B}, f);
+  auto rstd_c = at::empty({T, B}, f);
+  auto hT = at::empty({B, H}, f);
+  auto cT = at::empty({B, H}, f);
+  as::lnlstm_fwd(xp.data_ptr<float>(), h0.data_ptr<float>(), c0.data_ptr<float>(), wT.data_ptr(), dt(wT),
+                 lnh_w.data_ptr<float>(), lnh_b.data_ptr<float>(), lnc_w.data_ptr<float>(), lnc_b.data_ptr<float>(),
+                 static_cast<int>(T), static_cast<int>(B), static_cast<int>(H), static_cast<float>(eps),
+                 out.data_ptr<float>(), c_all.data_ptr<float>(), xhat_h.data_ptr<float>(), rstd_h.data_ptr<float>(),
+                 gates.data_ptr<float>(), xhat_c.data_ptr<float>(), rstd_c.data_ptr<float>(), hT.data_ptr<float>(),
+                 cT.data_ptr<float>(), stream());
+  return {out, hT, cT, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c};
+}
+
+std::vector<at::Tensor> lnlstm_bwd(const at::Tensor& dout, const at::Tensor& dhT, const at::Tensor& dcT,
+                                   const at::Tensor& gates, const at::Tensor& c_all, const at::Tensor& xhat_c,
+                                   const at::Tensor& rstd_c, const at::Tensor& xhat_h, const at::Tensor& rstd_h,
+                                   const at::Tensor& w, const at::Tensor& lnh_w, const at::Tensor& lnc_w) {
+  for (auto* t : {&dout, &dhT, &dcT, &gates, &c_all, &xhat_c, &rstd_c, &xhat_h, &rstd_h, &w, &lnh_w, &lnc_w})
+    check_cuda(*t, "lnlstm_bwd input");
+  const int64_t T = gates.size(0), B = gates.size(1), G = gates.size(2), H = G / 4;
+  TORCH_CHECK(w.size(0) == G && w.size(1) == H, "lnlstm_bwd: w must be [4H, H]");
+  TORCH_CHECK(dout.scalar_type() == at::kFloat && dout.size(0) == T && dout.size(1) == B && dout.size(2) == H,
+              "lnlstm_bwd: dout");
+  c10::hip::HIPGuard g(gates.device().index());
+  auto f = gates.options().dtype(at::kFloat);
+  auto dgates = at::empty({T, B, G}, f);
+  auto dhg = at::empty({T, B, G}, f);
+  auto dc_ln = at::empty({T, B, H}, f);
+  auto dh0 = at::empty({B, H}, f);
+  auto dc0 = at::empty({B, H}, f);
+  as::lnlstm_bwd(dout.data_ptr<float>(), dhT.data_ptr<float>(), dcT.data_ptr<float>(), gates.data_ptr<float>(),
+                 c_all.data_ptr<float>(), xhat_c.data_ptr<float>(), rstd_c.data_ptr<float>(), xhat_h.data_ptr<float>(),
+                 rstd_h.data_ptr<float>(), w.data_ptr(), dt(w), lnh_w.data_ptr<float>(), lnc_w.data_ptr<float>(),
+                 static_cast<int>(T), static_cast<int>(B), static_cast<int>(H), dgates.data_ptr<float>(),
+                 dhg.data_ptr<float>(), dc_ln.data_ptr<float>(), dh0.data_ptr<float>(), dc0.data_ptr<float>(),
+                 stream());
+  return {dgates, dhg, dc_ln, dh0, dc0};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -130,4 +187,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("reverse_scan", &reverse_scan);
   m.def("gated_residual_fwd", &gated_residual_fwd);
   m.def("gated_residual_bwd", &gated_residual_bwd);
+  m.def("lnlstm_fwd", &lnlstm_fwd);
+  m.def("lnlstm_bwd", &lnlstm_bwd);
 }

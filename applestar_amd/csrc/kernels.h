@@ -35,4 +35,19 @@ void gated_residual_bwd(const void* dout, const void* y, const void* g, const fl
                         void* dy, void* dg, void* dx, float* dsp_part, long n, int nblk, hipStream_t s);
 int elementwise_blocks(long n);
 
+// ---- lstm.hip --------------------------------------------------------------------------------
+// LayerNorm-LSTM recurrence for H in {384, 32}. xp [T,B,4H] = LN_i(x W_ih^T); wT = W_hh^T [H][4H]
+// (fp32 or bf16). Saves what BPTT needs: c_all [T+1,B,H], xhat_h/gates [T,B,4H], xhat_c [T,B,H],
+// rstd_h/rstd_c [T,B].
+bool lnlstm_supported(int H);
+void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* wT, int w_dt, const float* lnh_w,
+                const float* lnh_b, const float* lnc_w, const float* lnc_b, int T, int B, int H, float eps, float* out,
+                float* c_all, float* xhat_h, float* rstd_h, float* gates, float* xhat_c, float* rstd_c, float* hT,
+                float* cT, hipStream_t s);
+// w = W_hh [4H][H]. Outputs d(xp) [T,B,4H], d(h W_hh^T) [T,B,4H], dL/d(LN_c out) [T,B,H], dh0, dc0.
+void lnlstm_bwd(const float* dout, const float* dhT, const float* dcT, const float* gates, const float* c_all,
+                const float* xhat_c, const float* rstd_c, const float* xhat_h, const float* rstd_h, const void* w,
+                int w_dt, const float* lnh_w, const float* lnc_w, int T, int B, int H, float* dgates, float* dhg,
+                float* dc_ln, float* dh0, float* dc0, hipStream_t s);
+
 }  // namespace as

@@ -1,0 +1,304 @@
+// Persistent LayerNorm-LSTM recurrence (forward + BPTT) for gfx950.
+//
+// Cell (lstm.py:138-153): gates = xp[t] + LN_h(h W_hh^T); i,f,g,o = chunk(gates)
+//                         c' = LN_c(sig(f) c + sig(i) tanh(g));  h' = sig(o) tanh(c')
+// xp[t] = LN_i(x[t] W_ih^T) has no recurrence and is computed for all T by one GEMM outside.
+//
+// One workgroup owns one batch row for the whole sequence (rows are independent), so a launch
+// replaces T x ~12 torch kernels per layer.  Thread t computes COLS contiguous columns of the
+// recurrent GEMV (8-byte bf16 / 16-byte fp32 loads of W^T rows, coalesced across the workgroup),
+// LN statistics are two-pass block reductions (wave shuffles + LDS), the hidden state lives in LDS.
+// Core LSTM: H=384 -> 384 threads x 4 columns; selected-units LSTM: H=32 -> 64 threads x 2.
+// The backward walks t = T-1..0 and emits d(xp), d(h_{t-1} W^T) (for one dW GEMM afterwards) and
+// the LN_c output gradient (for the affine-parameter reductions).
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* scratch) {
+  constexpr int NW = NT / kWave;
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();  // scratch reuse guard
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) s += scratch[i];
+  return s;
+}
+
+template <typename TW, int COLS> struct WLoad;
+template <> struct WLoad<bf16_t, 4> {
+  __device__ static void load(const bf16_t* p, float* v) {
+    const uint2 t = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
+    v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
+  }
+};
+template <> struct WLoad<bf16_t, 2> {
+  __device__ static void load(const bf16_t* p, float* v) {
+    const uint32_t t = *reinterpret_cast<const uint32_t*>(p);
+    v[0] = __uint_as_float(t << 16); v[1] = __uint_as_float(t & 0xffff0000u);
+  }
+};
+template <> struct WLoad<float, 4> {
+  __device__ static void load(const float* p, float* v) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+};
+template <> struct WLoad<float, 2> {
+  __device__ static void load(const float* p, float* v) {
+    const float2 t = *reinterpret_cast<const float2*>(p);
+    v[0] = t.x; v[1] = t.y;
+  }
+};
+
+// wT: W_hh transposed, [H][4H] row-major
+template <int H, int NT, int COLS, typename TW>
+__global__ __launch_bounds__(NT) void lnlstm_fwd_kernel(
+    const float* __restrict__ xp, const float* __restrict__ h0, const float* __restrict__ c0,
+    const TW* __restrict__ wT, const float* __restrict__ lnh_w, const float* __restrict__ lnh_b,
+    const float* __restrict__ lnc_w, const float* __restrict__ lnc_b, int T, int B, float eps,
+    float* __restrict__ out, float* __restrict__ c_all, float* __restrict__ xhat_h, float* __restrict__ rstd_h,
+    float* __restrict__ gates_out, float* __restrict__ xhat_c, float* __restrict__ rstd_c, float* __restrict__ hT,
+    float* __restrict__ cT) {
+  static_assert(NT * COLS == 4 * H, "tiling");
+  static_assert(NT >= H, "one thread per hidden unit");
+  constexpr int G = 4 * H;
+  __shared__ float h_s[H];
+  __shared__ float g_s[G];
+  __shared__ float red[NT / kWave];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const bool unit = tid < H;
+  float c = 0.f, lcw = 0.f, lcb = 0.f;
+  if (unit) {
+    h_s[tid] = h0[static_cast<long>(b) * H + tid];
+    c = c0[static_cast<long>(b) * H + tid];
+    lcw = lnc_w[tid];
+    lcb = lnc_b[tid];
+    c_all[static_cast<long>(b) * H + tid] = c;  // c_all[0] = c0
+  }
+  float lw[COLS], lb[COLS];
+#pragma unroll
+  for (int k = 0; k < COLS; ++k) { lw[k] = lnh_w[tid * COLS + k]; lb[k] = lnh_b[tid * COLS + k]; }
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    float acc[COLS];
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) acc[k] = 0.f;
+    const TW* wp = wT + tid * COLS;
+#pragma unroll 8
+    for (int i = 0; i < H; ++i) {
+      float wv[COLS];
+      WLoad<TW, COLS>::load(wp + static_cast<long>(i) * G, wv);
+      const float hv = h_s[i];
+#pragma unroll
+      for (int k = 0; k < COLS; ++k) acc[k] = fmaf(hv, wv[k], acc[k]);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) s += acc[k];
+    const float mu = block_sum<NT>(s, red) * (1.f / G);
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) { const float d = acc[k] - mu; q += d * d; }
+    const float rs = rsqrtf(block_sum<NT>(q, red) * (1.f / G) + eps);
+    const long row = static_cast<long>(t) * B + b;
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) {
+      const int j = tid * COLS + k;
+      const float xh = (acc[k] - mu) * rs;
+      const float gv = xp[row * G + j] + xh * lw[k] + lb[k];
+      xhat_h[row * G + j] = xh;
+      gates_out[row * G + j] = gv;
+      g_s[j] = gv;
+    }
+    if (tid == 0) rstd_h[row] = rs;
+    __syncthreads();
+    float cpre = 0.f, og = 0.f;
+    if (unit) {
+      const float ig = sigmoidf_(g_s[tid]);
+      const float fg = sigmoidf_(g_s[H + tid]);
+      const float gg = tanhf(g_s[2 * H + tid]);
+      og = sigmoidf_(g_s[3 * H + tid]);
+      cpre = fg * c + ig * gg;
+    }
+    const float muc = block_sum<NT>(unit ? cpre : 0.f, red) * (1.f / H);
+    const float dc = unit ? cpre - muc : 0.f;
+    const float rsc = rsqrtf(block_sum<NT>(dc * dc, red) * (1.f / H) + eps);
+    if (unit) {
+      const float xc = dc * rsc;
+      c = xc * lcw + lcb;
+      const float hv = og * tanhf(c);
+      out[row * H + tid] = hv;
+      c_all[(row + B) * H + tid] = c;
+      xhat_c[row * H + tid] = xc;
+      h_s[tid] = hv;
+      if (t == T - 1) { hT[static_cast<long>(b) * H + tid] = hv; cT[static_cast<long>(b) * H + tid] = c; }
+    }
+    if (tid == 0) rstd_c[row] = rsc;
+    __syncthreads();
+  }
+  if (T == 0 && unit) { hT[static_cast<long>(b) * H + tid] = h_s[tid]; cT[static_cast<long>(b) * H + tid] = c; }
+}
+
+// w: W_hh [4H][H] row-major (dh_{t-1} = dhg @ W)
+template <int H, int NT, int COLS, typename TW>
+__global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
+    const float* __restrict__ dout, const float* __restrict__ dhT, const float* __restrict__ dcT,
+    const float* __restrict__ gates, const float* __restrict__ c_all, const float* __restrict__ xhat_c,
+    const float* __restrict__ rstd_c, const float* __restrict__ xhat_h, const float* __restrict__ rstd_h,
+    const TW* __restrict__ w, const float* __restrict__ lnh_w, const float* __restrict__ lnc_w, int T, int B,
+    float* __restrict__ dgates, float* __restrict__ dhg, float* __restrict__ dc_ln, float* __restrict__ dh0,
+    float* __restrict__ dc0) {
+  constexpr int G = 4 * H;
+  __shared__ float dh_s[H];
+  __shared__ float dg_s[G];
+  __shared__ float red[NT / kWave];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const bool unit = tid < H;
+  float dc = 0.f, lcw = 0.f;
+  if (unit) {
+    dh_s[tid] = dhT[static_cast<long>(b) * H + tid];
+    dc = dcT[static_cast<long>(b) * H + tid];
+    lcw = lnc_w[tid];
+  }
+  float lw[COLS];
+#pragma unroll
+  for (int k = 0; k < COLS; ++k) lw[k] = lnh_w[tid * COLS + k];
+  __syncthreads();
+  for (int t = T - 1; t >= 0; --t) {
+    const long row = static_cast<long>(t) * B + b;
+    // ---- cell: h = o tanh(c), c = LN_c(cpre)
+    float dxh = 0.f, xc = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, cprev = 0.f;
+    if (unit) {
+      const float dh = dout[row * H + tid] + dh_s[tid];
+      const float cc = c_all[(row + B) * H + tid];
+      const float tc = tanhf(cc);
+      const float og = sigmoidf_(gates[row * G + 3 * H + tid]);
+      const float do_pre = dh * tc * og * (1.f - og);
+      const float dct = dc + dh * og * (1.f - tc * tc);
+      dc_ln[row * H + tid] = dct;
+      dxh = dct * lcw;
+      xc = xhat_c[row * H + tid];
+      ig = sigmoidf_(gates[row * G + tid]);
+      fg = sigmoidf_(gates[row * G + H + tid]);
+      gg = tanhf(gates[row * G + 2 * H + tid]);
+      cprev = c_all[row * H + tid];
+      dg_s[3 * H + tid] = do_pre;
+    }
+    const float m1 = block_sum<NT>(dxh, red) * (1.f / H);
+    const float m2 = block_sum<NT>(dxh * xc, red) * (1.f / H);
+    if (unit) {
+      const float dcpre = rstd_c[row] * (dxh - m1 - xc * m2);
+      dg_s[tid] = dcpre * gg * ig * (1.f - ig);
+      dg_s[H + tid] = dcpre * cprev * fg * (1.f - fg);
+      dg_s[2 * H + tid] = dcpre * ig * (1.f - gg * gg);
+      dc = dcpre * fg;
+    }
+    __syncthreads();
+    // ---- LN_h backward over the 4H gate pre-activations
+    float dx[COLS], xh[COLS];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) {
+      const int j = tid * COLS + k;
+      const float dgv = dg_s[j];
+      dgates[row * G + j] = dgv;
+      xh[k] = xhat_h[row * G + j];
+      dx[k] = dgv * lw[k];
+      s1 += dx[k];
+      s2 += dx[k] * xh[k];
+    }
+    s1 = block_sum<NT>(s1, red) * (1.f / G);
+    s2 = block_sum<NT>(s2, red) * (1.f / G);
+    const float rs = rstd_h[row];
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) {
+      const int j = tid * COLS + k;
+      const float v = rs * (dx[k] - s1 - xh[k] * s2);
+      dhg[row * G + j] = v;
+      dg_s[j] = v;  // each thread overwrites only its own columns
+    }
+    __syncthreads();
+    // ---- dh_{t-1} = dhg @ W  (W [G][H])
+    if (unit) {
+      float acc = 0.f;
+#pragma unroll 8
+      for (int j = 0; j < G; ++j) acc = fmaf(dg_s[j], Cvt<TW>::load(w, static_cast<long>(j) * H + tid), acc);
+      dh_s[tid] = acc;
+    }
+    __syncthreads();
+  }
+  if (unit) {
+    dh0[static_cast<long>(b) * H + tid] = dh_s[tid];
+    dc0[static_cast<long>(b) * H + tid] = dc;
+  }
+}
+
+template <int H, int NT, int COLS>
+void fwd_launch(const float* xp, const float* h0, const float* c0, const void* wT, int w_dt, const float* lnh_w,
+                const float* lnh_b, const float* lnc_w, const float* lnc_b, int T, int B, float eps, float* out,
+                float* c_all, float* xhat_h, float* rstd_h, float* gates, float* xhat_c, float* rstd_c, float* hT,
+                float* cT, hipStream_t s) {
+  if (w_dt == DT_BF16)
+    hipLaunchKernelGGL((lnlstm_fwd_kernel<H, NT, COLS, bf16_t>), dim3(B), dim3(NT), 0, s, xp, h0, c0,
+                       static_cast<const bf16_t*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, eps, out, c_all, xhat_h,
+                       rstd_h, gates, xhat_c, rstd_c, hT, cT);
+  else
+    hipLaunchKernelGGL((lnlstm_fwd_kernel<H, NT, COLS, float>), dim3(B), dim3(NT), 0, s, xp, h0, c0,
+                       static_cast<const float*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, eps, out, c_all, xhat_h,
+                       rstd_h, gates, xhat_c, rstd_c, hT, cT);
+}
+
+template <int H, int NT, int COLS>
+void bwd_launch(const float* dout, const float* dhT, const float* dcT, const float* gates, const float* c_all,
+                const float* xhat_c, const float* rstd_c, const float* xhat_h, const float* rstd_h, const void* w,
+                int w_dt, const float* lnh_w, const float* lnc_w, int T, int B, float* dgates, float* dhg,
+                float* dc_ln, float* dh0, float* dc0, hipStream_t s) {
+  if (w_dt == DT_BF16)
+    hipLaunchKernelGGL((lnlstm_bwd_kernel<H, NT, COLS, bf16_t>), dim3(B), dim3(NT), 0, s, dout, dhT, dcT, gates,
+                       c_all, xhat_c, rstd_c, xhat_h, rstd_h, static_cast<const bf16_t*>(w), lnh_w, lnc_w, T, B,
+                       dgates, dhg, dc_ln, dh0, dc0);
+  else
+    hipLaunchKernelGGL((lnlstm_bwd_kernel<H, NT, COLS, float>), dim3(B), dim3(NT), 0, s, dout, dhT, dcT, gates,
+                       c_all, xhat_c, rstd_c, xhat_h, rstd_h, static_cast<const float*>(w), lnh_w, lnc_w, T, B,
+                       dgates, dhg, dc_ln, dh0, dc0);
+}
+
+}  // namespace
+
+bool lnlstm_supported(int H) { return H == 384 || H == 32; }
+
+void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* wT, int w_dt, const float* lnh_w,
+                const float* lnh_b, const float* lnc_w, const float* lnc_b, int T, int B, int H, float eps, float* out,
+                float* c_all, float* xhat_h, float* rstd_h, float* gates, float* xhat_c, float* rstd_c, float* hT,
+                float* cT, hipStream_t s) {
+  if (H == 384)
+    fwd_launch<384, 384, 4>(xp, h0, c0, wT, w_dt, lnh_w, lnh_b, lnc_w, lnc_b, T, B, eps, out, c_all, xhat_h, rstd_h,
+                            gates, xhat_c, rstd_c, hT, cT, s);
+  else if (H == 32)
+    fwd_launch<32, 64, 2>(xp, h0, c0, wT, w_dt, lnh_w, lnh_b, lnc_w, lnc_b, T, B, eps, out, c_all, xhat_h, rstd_h,
+                          gates, xhat_c, rstd_c, hT, cT, s);
+}
+
+void lnlstm_bwd(const float* dout, const float* dhT, const float* dcT, const float* gates, const float* c_all,
+                const float* xhat_c, const float* rstd_c, const float* xhat_h, const float* rstd_h, const void* w,
+                int w_dt, const float* lnh_w, const float* lnc_w, int T, int B, int H, float* dgates, float* dhg,
+                float* dc_ln, float* dh0, float* dc0, hipStream_t s) {
+  if (H == 384)
+    bwd_launch<384, 384, 4>(dout, dhT, dcT, gates, c_all, xhat_c, rstd_c, xhat_h, rstd_h, w, w_dt, lnh_w, lnc_w, T, B,
+                            dgates, dhg, dc_ln, dh0, dc0, s);
+  else if (H == 32)
+    bwd_launch<32, 64, 2>(dout, dhT, dcT, gates, c_all, xhat_c, rstd_c, xhat_h, rstd_h, w, w_dt, lnh_w, lnc_w, T, B,
+                          dgates, dhg, dc_ln, dh0, dc0, s);
+}
+
+}  // namespace as

@@ -20,7 +20,7 @@ def ensure_loaded():
     return _C
 
 
-_IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan'}
+_IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer'}
 
 
 def has(name: str) -> bool:
@@ -98,3 +98,48 @@ def reverse_scan(a, b, init):
     b = b.float().contiguous()
     init = init.float().contiguous().expand(b.shape[:-2] + b.shape[-1:]).contiguous()
     return _C.reverse_scan(a, b, init)
+
+
+# ---------------------------------------------------------------------------- LN-LSTM layer
+class _LNLSTMRecurrence(torch.autograd.Function):
+    """Recurrent part of an LN-LSTM layer: xp [T,B,4H] (already LN_i(x W_ih^T)) -> h [T,B,H]."""
+
+    @staticmethod
+    def forward(ctx, xp, h0, c0, w_hh, lnh_w, lnh_b, lnc_w, lnc_b, w_dtype):
+        wq = w_hh.detach().to(w_dtype)
+        wT = wq.t().contiguous()
+        out, hT, cT, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c = _C.lnlstm_fwd(
+            xp.contiguous(), h0.contiguous(), c0.contiguous(), wT, lnh_w.detach(), lnh_b.detach(),
+            lnc_w.detach(), lnc_b.detach(), 1e-5)
+        ctx.save_for_backward(h0, out, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c, wq.contiguous(), lnh_w, lnc_w)
+        return out, hT, cT
+
+    @staticmethod
+    def backward(ctx, dout, dhT, dcT):
+        h0, out, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c, wq, lnh_w, lnc_w = ctx.saved_tensors
+        T, B, H = out.shape
+        z = lambda t: torch.zeros(B, H, device=out.device) if t is None else t.float().contiguous()
+        dout = torch.zeros_like(out) if dout is None else dout.float().contiguous()
+        dgates, dhg, dc_ln, dh0, dc0 = _C.lnlstm_bwd(dout, z(dhT), z(dcT), gates, c_all, xhat_c, rstd_c, xhat_h,
+                                                     rstd_h, wq, lnh_w.detach(), lnc_w.detach())
+        h_prev = torch.cat([h0.float().unsqueeze(0), out[:-1]], 0).view(T * B, H)
+        dw = dhg.view(T * B, 4 * H).t() @ h_prev
+        dlnh_w = (dgates * xhat_h).sum((0, 1))
+        dlnh_b = dgates.sum((0, 1))
+        dlnc_w = (dc_ln * xhat_c).sum((0, 1))
+        dlnc_b = dc_ln.sum((0, 1))
+        return dgates, dh0, dc0, dw, dlnh_w, dlnh_b, dlnc_w, dlnc_b, None
+
+
+def lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b):
+    """x [T,B,I] -> (out [T,B,H], h_T, c_T).  Input GEMM (+ LN_i) for all T at once; recurrence native."""
+    T, B, _ = x.shape
+    H = w_hh.shape[1]
+    if H not in (384, 32):
+        from . import reference
+        return reference.lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b)
+    xg = torch.nn.functional.linear(x.reshape(T * B, -1), w_ih)
+    xp = layer_norm(xg, lni_w, lni_b, out_dtype=torch.float32).view(T, B, 4 * H)
+    w_dtype = torch.bfloat16 if torch.is_autocast_enabled() else torch.float32
+    out, hT, cT = _LNLSTMRecurrence.apply(xp, h0.float(), c0.float(), w_hh, lnh_w, lnh_b, lnc_w, lnc_b, w_dtype)
+    return out, hT, cT

@@ -80,3 +80,31 @@ def test_reverse_scan():
         acc = a[:, t] * acc + b[:, t]
         ref[:, t] = acc
     assert _err(y, ref) < 1e-5
+
+
+@pytest.mark.parametrize('H,I,T,B', [(384, 1536, 9, 6), (32, 32, 13, 37)])
+@pytest.mark.parametrize('autocast', [False, True])
+def test_lnlstm_layer_matches_reference(H, I, T, B, autocast):
+    torch.manual_seed(3)
+    x = torch.randn(T, B, I, device=DEV, requires_grad=True)
+    h0 = (0.5 * torch.randn(B, H, device=DEV)).requires_grad_()
+    c0 = (0.5 * torch.randn(B, H, device=DEV)).requires_grad_()
+    params = [torch.randn(4 * H, I, device=DEV) / I ** 0.5, torch.randn(4 * H, H, device=DEV) / H ** 0.5,
+              1 + 0.1 * torch.randn(4 * H, device=DEV), 0.1 * torch.randn(4 * H, device=DEV),
+              1 + 0.1 * torch.randn(4 * H, device=DEV), 0.1 * torch.randn(4 * H, device=DEV),
+              1 + 0.1 * torch.randn(H, device=DEV), 0.1 * torch.randn(H, device=DEV)]
+    params = [p.requires_grad_() for p in params]
+    ref_in = [t.detach().clone().requires_grad_() for t in [x, h0, c0] + params]
+    with torch.autocast('cuda', dtype=torch.bfloat16, enabled=autocast):
+        out, hT, cT = N.lnlstm_layer(x, h0, c0, *params)
+    r_out, r_h, r_c = R.lnlstm_layer(*ref_in)
+    tol = 5e-2 if autocast else 2e-4
+    assert _err(out, r_out) < tol
+    assert _err(cT, r_c) < tol * 4
+    g = torch.randn_like(r_out)
+    gh = torch.randn_like(r_h)
+    (out * g).sum().add_((hT * gh).sum()).backward()
+    (r_out * g).sum().add_((r_h * gh).sum()).backward()
+    for a, b in zip([x, h0, c0] + params, ref_in):
+        scale = max(1.0, b.grad.abs().max().item())
+        assert _err(a.grad, b.grad) < tol * 4 * scale
