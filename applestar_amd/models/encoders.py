@@ -188,7 +188,7 @@ class EntityEncoder(nn.Module):
         # the reference's inplace ReLU (entity_encoder.py:84) also rectifies x used by the mean below
         x = F.relu(x)
         ee = self.entity_fc(x)
-        entity_embeddings = x.new_zeros(B * N, ee.shape[-1])
+        entity_embeddings = ee.new_zeros(B * N, ee.shape[-1])
         entity_embeddings = entity_embeddings.index_copy(0, flat_index, ee).view(B, N, -1)
         # masked mean of relu(transformer output) over real entities (entity_encoder.py:85-87)
         seg = torch.repeat_interleave(torch.arange(B, device=x.device), lens.long(), output_size=x.shape[0])

@@ -59,12 +59,14 @@ def test_gated_residual(dtype):
     ref = R.gated_residual(ys, gs, sps, xs)
     tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
     assert _err(out, ref) < tol
-    d = torch.randn_like(ref)
-    out.backward(d.to(dtype))
-    ref.backward(d)
+    d = torch.randn_like(ref).to(dtype)
+    out.backward(d)
+    ref.backward(d.float())
     for a, b in ((y.grad, ys.grad), (g.grad, gs.grad), (x.grad, xs.grad)):
         assert _err(a, b) < tol * 4
-    assert abs(sp.grad.item() - sps.grad.item()) < 1e-2 * max(1, abs(sps.grad.item()))
+    # d(sp) is a sum of ~2.4e5 signed terms: bound the error by the sum of |terms|
+    mag = (d.float().abs() * torch.tanh(ys * torch.sigmoid(gs)).abs()).sum().item()
+    assert abs(sp.grad.item() - sps.grad.item()) < 1e-3 * mag
 
 
 def test_reverse_scan():
