@@ -178,6 +178,155 @@ std::vector<at::Tensor> lnlstm_bwd(const at::Tensor& dout, const at::Tensor& dhT
   return {dgates, dhg, dc_ln, dh0, dc0};
 }
 
+// ---------------------------------------------------------------- entity embedding
+int src_dt(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kByte: case at::kBool: return as::SRC_U8;
+    case at::kChar: return as::SRC_I8;
+    case at::kShort: return as::SRC_I16;
+    case at::kInt: return as::SRC_I32;
+    case at::kLong: return as::SRC_I64;
+    case at::kHalf: return as::SRC_F16;
+    case at::kFloat: return as::SRC_F32;
+    default: TORCH_CHECK(false, "entity field dtype ", t.scalar_type());
+  }
+}
+
+as::EntityFields make_fields(const std::vector<at::Tensor>& fields, const std::vector<int64_t>& kind,
+                             const std::vector<int64_t>& offset, const std::vector<int64_t>& width, int64_t numel) {
+  TORCH_CHECK(fields.size() <= as::kMaxFields && fields.size() == kind.size() && kind.size() == offset.size() &&
+                  offset.size() == width.size(), "entity fields table");
+  as::EntityFields f{};
+  f.n = static_cast<int>(fields.size());
+  for (size_t i = 0; i < fields.size(); ++i) {
+    check_cuda(fields[i], "entity field");
+    TORCH_CHECK(fields[i].numel() == numel, "entity field numel mismatch");
+    f.ptr[i] = fields[i].data_ptr();
+    f.dtype[i] = src_dt(fields[i]);
+    f.kind[i] = static_cast<int>(kind[i]);
+    f.offset[i] = static_cast<int>(offset[i]);
+    f.width[i] = static_cast<int>(width[i]);
+  }
+  return f;
+}
+
+at::Tensor entity_embed_fwd(const std::vector<at::Tensor>& fields, const std::vector<int64_t>& kind,
+                            const std::vector<int64_t>& offset, const std::vector<int64_t>& width,
+                            const at::Tensor& index, const at::Tensor& wT, const at::Tensor& bias, int64_t out_dtype) {
+  check_cuda(index, "index");
+  check_cuda(wT, "wT");
+  TORCH_CHECK(index.scalar_type() == at::kLong, "index int64");
+  TORCH_CHECK(wT.size(1) == 256 && bias.numel() == 256 && bias.scalar_type() == at::kFloat, "entity embed: 256 channels");
+  auto f = make_fields(fields, kind, offset, width, fields.empty() ? 0 : fields[0].numel());
+  for (int i = 0; i < f.n; ++i) TORCH_CHECK(f.offset[i] + (f.kind[i] == as::FIELD_SCALAR ? 1 : f.width[i]) <= wT.size(0), "field offset");
+  c10::hip::HIPGuard g(wT.device().index());
+  const int64_t T = index.numel();
+  auto out = at::empty({T, 256}, wT.options().dtype(out_dtype == 1 ? at::kBFloat16 : at::kFloat));
+  if (T > 0)
+    as::entity_embed_fwd(f, index.data_ptr<int64_t>(), wT.data_ptr(), dt(wT), bias.data_ptr<float>(), out.data_ptr(),
+                         dt(out), T, stream());
+  return out;
+}
+
+at::Tensor entity_onehot(const std::vector<at::Tensor>& fields, const std::vector<int64_t>& kind,
+                         const std::vector<int64_t>& offset, const std::vector<int64_t>& width, const at::Tensor& index,
+                         int64_t k_in, int64_t out_dtype) {
+  check_cuda(index, "index");
+  auto f = make_fields(fields, kind, offset, width, fields.empty() ? 0 : fields[0].numel());
+  c10::hip::HIPGuard g(index.device().index());
+  const int64_t T = index.numel();
+  auto X = at::zeros({T, k_in}, index.options().dtype(out_dtype == 1 ? at::kBFloat16 : at::kFloat));
+  as::entity_onehot(f, index.data_ptr<int64_t>(), X.data_ptr(), dt(X), T, static_cast<int>(k_in), stream());
+  return X;
+}
+
+// ---------------------------------------------------------------- spatial path (NHWC)
+at::Tensor upsample2x_fwd(const at::Tensor& x) {  // x [B,H,W,C]
+  check_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 4 == 0, "upsample2x: NHWC with C % 4 == 0");
+  c10::hip::HIPGuard g(x.device().index());
+  auto y = at::empty({x.size(0), 2 * x.size(1), 2 * x.size(2), x.size(3)}, x.options());
+  as::upsample2x_fwd(x.data_ptr(), y.data_ptr(), dt(x), x.size(0), x.size(1), x.size(2), x.size(3), stream());
+  return y;
+}
+
+at::Tensor upsample2x_bwd(const at::Tensor& dy) {  // dy [B,2H,2W,C]
+  check_cuda(dy, "dy");
+  TORCH_CHECK(dy.dim() == 4 && dy.size(3) % 4 == 0 && dy.size(1) % 2 == 0 && dy.size(2) % 2 == 0, "upsample2x_bwd");
+  c10::hip::HIPGuard g(dy.device().index());
+  auto dx = at::empty({dy.size(0), dy.size(1) / 2, dy.size(2) / 2, dy.size(3)}, dy.options());
+  as::upsample2x_bwd(dy.data_ptr(), dx.data_ptr(), dt(dy), dx.size(0), dx.size(1), dx.size(2), dx.size(3), stream());
+  return dx;
+}
+
+as::SpatialPlanes make_planes(const std::vector<at::Tensor>& planes, const std::vector<at::Tensor>& effects) {
+  TORCH_CHECK(planes.size() == 7 && effects.size() == 6, "spatial: 7 planes (height + 6 one-hot) and 6 effects");
+  as::SpatialPlanes sp{};
+  for (const auto& t : planes) {
+    check_cuda(t, "plane");
+    TORCH_CHECK(t.scalar_type() == at::kByte, "spatial planes must be uint8");
+  }
+  for (const auto& t : effects) {
+    check_cuda(t, "effect");
+    TORCH_CHECK(t.scalar_type() == at::kShort, "effects must be int16");
+  }
+  sp.height = planes[0].data_ptr<uint8_t>();
+  for (int k = 0; k < 6; ++k) {
+    TORCH_CHECK(planes[k + 1].numel() == planes[0].numel(), "plane size");
+    sp.plane[k] = planes[k + 1].data_ptr<uint8_t>();
+    sp.effect[k] = effects[k].data_ptr<int16_t>();
+  }
+  return sp;
+}
+
+// returns (effect bits [B,HW] u8, out [B,H,W,32] relu'd)
+std::vector<at::Tensor> spatial_embed_fwd(const std::vector<at::Tensor>& planes, const std::vector<at::Tensor>& effects,
+                                          const at::Tensor& w_dense, const at::Tensor& bias, const at::Tensor& rows,
+                                          const at::Tensor& ex, const at::Tensor& ey, const at::Tensor& entity_num,
+                                          int64_t out_dtype) {
+  auto sp = make_planes(planes, effects);
+  const int64_t B = planes[0].size(0), H = planes[0].size(1), W = planes[0].size(2), HW = H * W;
+  const int64_t L = effects[0].size(1);
+  TORCH_CHECK(w_dense.size(0) == 32 && w_dense.size(1) == 24 && w_dense.scalar_type() == at::kFloat, "w_dense [32,24]");
+  TORCH_CHECK((B * HW) % 4 == 0, "spatial: B*H*W % 4");
+  check_cuda(rows, "rows");
+  TORCH_CHECK(rows.dim() == 3 && rows.size(0) == B && rows.size(2) == 32, "rows [B,N,32]");
+  TORCH_CHECK(ex.scalar_type() == at::kByte && ey.scalar_type() == at::kByte && entity_num.scalar_type() == at::kLong,
+              "entity x/y uint8, entity_num int64");
+  c10::hip::HIPGuard g(rows.device().index());
+  auto bits = at::zeros({B, HW}, planes[0].options());
+  as::spatial_effect_bits(sp, bits.data_ptr<uint8_t>(), B, L, HW, stream());
+  auto pre = at::empty({B, H, W, 32}, rows.options().dtype(at::kFloat));
+  as::spatial_dense(sp, bits.data_ptr<uint8_t>(), w_dense.data_ptr<float>(), bias.data_ptr<float>(), pre.data_ptr<float>(),
+                    B * HW, stream());
+  as::scatter_add_rows(rows.data_ptr(), dt(rows), ex.data_ptr<uint8_t>(), ey.data_ptr<uint8_t>(),
+                       entity_num.data_ptr<int64_t>(), pre.data_ptr<float>(), B, rows.size(1), H, W, stream());
+  auto out = at::empty({B, H, W, 32}, rows.options().dtype(out_dtype == 1 ? at::kBFloat16 : at::kFloat));
+  as::relu_cast(pre.data_ptr<float>(), out.data_ptr(), dt(out), pre.numel(), stream());
+  return {bits, out};
+}
+
+at::Tensor spatial_gather_rows(const at::Tensor& dpre, const at::Tensor& ex, const at::Tensor& ey,
+                               const at::Tensor& entity_num, int64_t N) {
+  check_cuda(dpre, "dpre");
+  const int64_t B = dpre.size(0), H = dpre.size(1), W = dpre.size(2);
+  c10::hip::HIPGuard g(dpre.device().index());
+  auto drows = at::empty({B, N, 32}, dpre.options());
+  as::gather_rows(dpre.data_ptr(), dt(dpre), ex.data_ptr<uint8_t>(), ey.data_ptr<uint8_t>(),
+                  entity_num.data_ptr<int64_t>(), drows.data_ptr(), B, N, H, W, stream());
+  return drows;
+}
+
+at::Tensor spatial_dense_input(const std::vector<at::Tensor>& planes, const std::vector<at::Tensor>& effects,
+                               const at::Tensor& bits, int64_t x_dtype) {
+  auto sp = make_planes(planes, effects);
+  const int64_t npix = planes[0].numel();
+  c10::hip::HIPGuard g(bits.device().index());
+  auto X = at::empty({npix, 24}, bits.options().dtype(x_dtype == 1 ? at::kBFloat16 : at::kFloat));
+  as::spatial_dense_input(sp, bits.data_ptr<uint8_t>(), X.data_ptr(), dt(X), npix, stream());
+  return X;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -189,4 +338,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gated_residual_bwd", &gated_residual_bwd);
   m.def("lnlstm_fwd", &lnlstm_fwd);
   m.def("lnlstm_bwd", &lnlstm_bwd);
+  m.def("entity_embed_fwd", &entity_embed_fwd);
+  m.def("entity_onehot", &entity_onehot);
+  m.def("upsample2x_fwd", &upsample2x_fwd);
+  m.def("upsample2x_bwd", &upsample2x_bwd);
+  m.def("spatial_embed_fwd", &spatial_embed_fwd);
+  m.def("spatial_gather_rows", &spatial_gather_rows);
+  m.def("spatial_dense_input", &spatial_dense_input);
 }

@@ -9,6 +9,20 @@ namespace as {
 
 // dtype codes shared with the bindings
 enum DType : int { DT_F32 = 0, DT_BF16 = 1 };
+// source dtypes of raw observation fields
+enum SrcType : int { SRC_U8 = 0, SRC_I8 = 1, SRC_I16 = 2, SRC_I32 = 3, SRC_I64 = 4, SRC_F16 = 5, SRC_F32 = 6 };
+enum FieldKind : int { FIELD_ONE_HOT = 0, FIELD_BINARY = 1, FIELD_SCALAR = 2 };
+
+constexpr int kMaxFields = 40;
+// Kernel-argument table describing the per-entity observation fields (passed by value).
+struct EntityFields {
+  const void* ptr[kMaxFields];
+  int dtype[kMaxFields];
+  int kind[kMaxFields];
+  int offset[kMaxFields];
+  int width[kMaxFields];
+  int n;
+};
 
 // ---- layernorm.hip -------------------------------------------------------------------------
 // y = act(LN(x + residual) * w + b); saves per-row mean/rstd and (if residual) the fp32 sum.
@@ -49,5 +63,34 @@ void lnlstm_bwd(const float* dout, const float* dhT, const float* dcT, const flo
                 const float* xhat_c, const float* rstd_c, const float* xhat_h, const float* rstd_h, const void* w,
                 int w_dt, const float* lnh_w, const float* lnc_w, int T, int B, int H, float* dgates, float* dhg,
                 float* dc_ln, float* dh0, float* dc0, hipStream_t s);
+
+// ---- entity.hip ------------------------------------------------------------------------------
+// out[t] = relu(bias + sum_fields W^T[row(field value)]) for packed entity t (source row index[t]).
+void entity_embed_fwd(const EntityFields& f, const int64_t* index, const void* wT, int w_dt, const float* bias,
+                      void* out, int out_dt, long T, hipStream_t s);
+// X[t, :] = 997-wide sparse encoding of entity t (X must be zeroed).
+void entity_onehot(const EntityFields& f, const int64_t* index, void* X, int x_dt, long T, int K_in, hipStream_t s);
+
+// ---- spatial.hip -----------------------------------------------------------------------------
+struct SpatialPlanes {
+  const uint8_t* height;     // [B*H*W]
+  const uint8_t* plane[6];   // visibility, creep, player_relative, alerts, pathable, buildable
+  const int16_t* effect[6];  // [B*L] flat pixel indices (0-padded)
+};
+// NHWC bilinear x2 (align_corners=False); C % 4 == 0
+void upsample2x_fwd(const void* x, void* y, int dt, int B, int H, int W, int C, hipStream_t s);
+void upsample2x_bwd(const void* dy, void* dx, int dt, int B, int H, int W, int C, hipStream_t s);
+// bits [B*H*W] (zeroed, size % 4 == 0): bit e set where effect e has a point
+void spatial_effect_bits(const SpatialPlanes& sp, uint8_t* bits, int B, int L, int HW, hipStream_t s);
+// pre [npix][32] = bias + Wd . dense(pixel);  Wd [32][24]
+void spatial_dense(const SpatialPlanes& sp, const uint8_t* bits, const float* wd, const float* bias, float* pre, long npix,
+                   hipStream_t s);
+void spatial_dense_input(const SpatialPlanes& sp, const uint8_t* bits, void* X, int x_dt, long npix, hipStream_t s);
+// pre[b, y*W+x, :] += rows[b, n, :] (32 channels) for n < entity_num[b]; and its transpose (gather)
+void scatter_add_rows(const void* rows, int dt, const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num,
+                      float* pre, int B, int N, int H, int W, hipStream_t s);
+void gather_rows(const void* dpre, int dt, const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num,
+                 void* drows, int B, int N, int H, int W, hipStream_t s);
+void relu_cast(const float* x, void* y, int dt, long n, hipStream_t s);
 
 }  // namespace as

@@ -174,12 +174,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
   }
 }
 
-__global__ void column_reduce_kernel(const float* __restrict__ part, float* __restrict__ out, int nrows, int cols) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= cols) return;
+__global__ __launch_bounds__(256) void column_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                            int nrows, int cols) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
   float s = 0.f;
-  for (int r = 0; r < nrows; ++r) s += part[static_cast<long>(r) * cols + c];
-  out[c] = s;
+  if (c < cols)
+    for (int r = g; r < nrows; r += 4) s += part[static_cast<long>(r) * cols + c];
+  red[g][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (g == 0 && c < cols) out[c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
 }
 
 int fwd_blocks(long rows) {
@@ -232,8 +237,8 @@ void bwd_dispatch(const void* dy, int dy_dt, const void* xin, int xin_dt, const 
 }  // namespace
 
 int layer_norm_bwd_blocks(long rows) {
-  long b = (rows + 15) / 16;  // >= 4 rows per wave to amortise the dgamma/dbeta partials
-  return static_cast<int>(b < 1024 ? (b < 1 ? 1 : b) : 1024);
+  long b = (rows + 31) / 32;  // >= 8 rows per wave to amortise the dgamma/dbeta partials
+  return static_cast<int>(b < 512 ? (b < 1 ? 1 : b) : 512);
 }
 
 #define VPT_SWITCH(cols, F, ...)                      \
@@ -262,7 +267,7 @@ void layer_norm_bwd(const void* dy, int dy_dt, const void* xin, int xin_dt, cons
 }
 
 void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s) {
-  hipLaunchKernelGGL(column_reduce_kernel, dim3((cols + 255) / 256), dim3(256), 0, s, part, out, nrows, cols);
+  hipLaunchKernelGGL(column_reduce_kernel, dim3((cols + 63) / 64), dim3(256), 0, s, part, out, nrows, cols);
 }
 
 }  // namespace as

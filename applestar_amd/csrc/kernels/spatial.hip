@@ -1,0 +1,313 @@
+// Spatial-path kernels for the encoder and the location head (NHWC / channels_last, bf16 or fp32).
+//
+// upsample2x: bilinear x2, align_corners=False (F.interpolate(scale_factor=2, mode='bilinear')),
+//   the location head's 3 upsampling stages (action_arg_head.py:440-446).  torch runs this in fp32
+//   under autocast with a generic NCHW kernel (21.6 % of the first learner profile); here it is a
+//   bf16 NHWC gather with the fixed 0.25/0.75 stencil, channels contiguous per lane.  The backward is
+//   a deterministic gather (each input pixel pulls its <= 4x4 outputs), no atomics.
+// spatial_embed: the spatial encoder input planes + 1x1 projection (spatial_encoder.py:51-72) in
+//   one pass: one thread per pixel reads height/6 categorical planes/effect bits and writes the 32
+//   pre-activation channels; entity contributions (the scatter connection pre-multiplied by the
+//   scatter columns of the 1x1 conv) are added by scatter_add_rows; relu_cast finishes.
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+// 1-D source taps of output index o (align_corners=False, scale 2)
+__device__ __forceinline__ void taps(int o, int n_in, int& i0, int& i1, float& l) {
+  float src = (o + 0.5f) * 0.5f - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = static_cast<int>(src);
+  if (i0 > n_in - 1) i0 = n_in - 1;
+  i1 = i0 + 1 < n_in ? i0 + 1 : n_in - 1;
+  l = src - static_cast<float>(i0);
+}
+
+__device__ __forceinline__ float tap_weight(int o, int k, int n_in) {
+  int i0, i1;
+  float l;
+  taps(o, n_in, i0, i1, l);
+  return (k == i0 ? 1.f - l : 0.f) + (k == i1 ? l : 0.f);
+}
+
+// x [B][H][W][C] -> y [B][2H][2W][C]; thread handles 4 channels
+template <typename T>
+__global__ __launch_bounds__(256) void upsample2x_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int B, int H,
+                                                             int W, int C) {
+  const int C4 = C / 4;
+  const long total = static_cast<long>(B) * 2 * H * 2 * W * C4;
+  for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int c4 = static_cast<int>(i % C4);
+    long r = i / C4;
+    const int ox = static_cast<int>(r % (2 * W));
+    r /= 2 * W;
+    const int oy = static_cast<int>(r % (2 * H));
+    const int b = static_cast<int>(r / (2 * H));
+    int y0, y1, x0, x1;
+    float ly, lx;
+    taps(oy, H, y0, y1, ly);
+    taps(ox, W, x0, x1, lx);
+    const long base = static_cast<long>(b) * H * W;
+    const long p00 = ((base + static_cast<long>(y0) * W + x0) * C) + c4 * 4;
+    const long p01 = ((base + static_cast<long>(y0) * W + x1) * C) + c4 * 4;
+    const long p10 = ((base + static_cast<long>(y1) * W + x0) * C) + c4 * 4;
+    const long p11 = ((base + static_cast<long>(y1) * W + x1) * C) + c4 * 4;
+    const float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx, w10 = ly * (1.f - lx), w11 = ly * lx;
+    const long o = ((static_cast<long>(b) * 2 * H + oy) * 2 * W + ox) * C + c4 * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float v = w00 * Cvt<T>::load(x, p00 + k) + w01 * Cvt<T>::load(x, p01 + k) +
+                      w10 * Cvt<T>::load(x, p10 + k) + w11 * Cvt<T>::load(x, p11 + k);
+      Cvt<T>::store(y, o + k, v);
+    }
+  }
+}
+
+// dy [B][2H][2W][C] -> dx [B][H][W][C]
+template <typename T>
+__global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int B, int H,
+                                                             int W, int C) {
+  const int C4 = C / 4;
+  const long total = static_cast<long>(B) * H * W * C4;
+  for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int c4 = static_cast<int>(i % C4);
+    long r = i / C4;
+    const int kx = static_cast<int>(r % W);
+    r /= W;
+    const int ky = static_cast<int>(r % H);
+    const int b = static_cast<int>(r / H);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int oy = 2 * ky - 1; oy <= 2 * ky + 2; ++oy) {
+      if (oy < 0 || oy >= 2 * H) continue;
+      const float wy = tap_weight(oy, ky, H);
+      if (wy == 0.f) continue;
+      for (int ox = 2 * kx - 1; ox <= 2 * kx + 2; ++ox) {
+        if (ox < 0 || ox >= 2 * W) continue;
+        const float w = wy * tap_weight(ox, kx, W);
+        if (w == 0.f) continue;
+        const long o = ((static_cast<long>(b) * 2 * H + oy) * 2 * W + ox) * C + c4 * 4;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) acc[k] = fmaf(w, Cvt<T>::load(dy, o + k), acc[k]);
+      }
+    }
+    const long d = ((static_cast<long>(b) * H + ky) * W + kx) * C + c4 * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Cvt<T>::store(dx, d + k, acc[k]);
+  }
+}
+
+// pre [B][H*W][32] fp32 = bias + W_dense . dense_input(pixel)
+// dense columns: 0 height/256 | 1..4 visibility | 5..6 creep | 7..11 player_relative | 12..13 alerts |
+//                14..15 pathable | 16..17 buildable | 18..23 effects
+__global__ __launch_bounds__(256) void spatial_dense_kernel(SpatialPlanes sp, const uint8_t* __restrict__ effect_bits,
+                                                            const float* __restrict__ wd, const float* __restrict__ bias,
+                                                            float* __restrict__ pre, long npix) {
+  __shared__ float w_s[24][32];
+  __shared__ float b_s[32];
+  for (int i = threadIdx.x; i < 24 * 32; i += blockDim.x) w_s[i % 24][i / 24] = wd[(i / 24) * 24 + (i % 24)];
+  if (threadIdx.x < 32) b_s[threadIdx.x] = bias[threadIdx.x];
+  __syncthreads();
+  const int widths[6] = {4, 2, 5, 2, 2, 2};
+  for (long p = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; p < npix;
+       p += static_cast<long>(gridDim.x) * blockDim.x) {
+    float acc[32];
+    const float h = static_cast<float>(sp.height[p]) * (1.f / 256.f);
+#pragma unroll
+    for (int c = 0; c < 32; ++c) acc[c] = b_s[c] + w_s[0][c] * h;
+    int off = 1;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      int v = sp.plane[k][p];
+      v = v < widths[k] ? v : widths[k] - 1;
+      const int col = off + v;
+#pragma unroll
+      for (int c = 0; c < 32; ++c) acc[c] += w_s[col][c];
+      off += widths[k];
+    }
+    const uint8_t eb = effect_bits[p];
+#pragma unroll
+    for (int e = 0; e < 6; ++e)
+      if ((eb >> e) & 1) {
+#pragma unroll
+        for (int c = 0; c < 32; ++c) acc[c] += w_s[18 + e][c];
+      }
+    float4* dst = reinterpret_cast<float4*>(pre + p * 32);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) dst[c] = make_float4(acc[4 * c], acc[4 * c + 1], acc[4 * c + 2], acc[4 * c + 3]);
+  }
+}
+
+// effect_bits[b][pix] |= 1 << e for each effect point (int16 flat index, zero padded -> pixel 0)
+__global__ void effect_bits_kernel(SpatialPlanes sp, uint32_t* __restrict__ bits_words, int B, int L, int HW) {
+  const long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<long>(B) * 6 * L) return;
+  const int e = static_cast<int>((i / L) % 6);
+  const int b = static_cast<int>(i / (6L * L));
+  const int j = static_cast<int>(i % L);
+  int p = sp.effect[e][static_cast<long>(b) * L + j];
+  p = p < 0 ? 0 : (p >= HW ? HW - 1 : p);
+  const long byte = static_cast<long>(b) * HW + p;
+  atomicOr(bits_words + (byte >> 2), 1u << (8 * (byte & 3) + e));
+}
+
+// pre[b, y*W+x, c] += rows[b, n, c] for n < entity_num[b]
+template <typename T>
+__global__ __launch_bounds__(256) void scatter_add_rows_kernel(const T* __restrict__ rows, const uint8_t* __restrict__ ex,
+                                                               const uint8_t* __restrict__ ey,
+                                                               const int64_t* __restrict__ entity_num,
+                                                               float* __restrict__ pre, int B, int N, int H, int W) {
+  const long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<long>(B) * N * 32) return;
+  const int c = static_cast<int>(i & 31);
+  const long bn = i >> 5;
+  const int b = static_cast<int>(bn / N);
+  const int n = static_cast<int>(bn % N);
+  if (n >= entity_num[b]) return;
+  int x = ex[bn], y = ey[bn];
+  x = x < W ? x : W - 1;
+  y = y < H ? y : H - 1;
+  atomicAdd(pre + (static_cast<long>(b) * H * W + static_cast<long>(y) * W + x) * 32 + c, Cvt<T>::load(rows, i));
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gather_rows_kernel(const T* __restrict__ dpre, const uint8_t* __restrict__ ex,
+                                                          const uint8_t* __restrict__ ey,
+                                                          const int64_t* __restrict__ entity_num, T* __restrict__ drows,
+                                                          int B, int N, int H, int W) {
+  const long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<long>(B) * N * 32) return;
+  const int c = static_cast<int>(i & 31);
+  const long bn = i >> 5;
+  const int b = static_cast<int>(bn / N);
+  const int n = static_cast<int>(bn % N);
+  float v = 0.f;
+  if (n < entity_num[b]) {
+    int x = ex[bn], y = ey[bn];
+    x = x < W ? x : W - 1;
+    y = y < H ? y : H - 1;
+    v = Cvt<T>::load(dpre, (static_cast<long>(b) * H * W + static_cast<long>(y) * W + x) * 32 + c);
+  }
+  Cvt<T>::store(drows, i, v);
+}
+
+template <typename TO>
+__global__ __launch_bounds__(256) void relu_cast_kernel(const float* __restrict__ x, TO* __restrict__ y, long n) {
+  for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<long>(gridDim.x) * blockDim.x)
+    Cvt<TO>::store(y, i, fmaxf(x[i], 0.f));
+}
+
+// dense input materialised for the 1x1 conv weight gradient: X [npix][24]
+template <typename TX>
+__global__ __launch_bounds__(256) void spatial_dense_input_kernel(SpatialPlanes sp, const uint8_t* __restrict__ effect_bits,
+                                                                  TX* __restrict__ X, long npix) {
+  const int widths[6] = {4, 2, 5, 2, 2, 2};
+  for (long p = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; p < npix;
+       p += static_cast<long>(gridDim.x) * blockDim.x) {
+    float v[24];
+#pragma unroll
+    for (int i = 0; i < 24; ++i) v[i] = 0.f;
+    v[0] = static_cast<float>(sp.height[p]) * (1.f / 256.f);
+    int off = 1;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      int c = sp.plane[k][p];
+      c = c < widths[k] ? c : widths[k] - 1;
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        if (j < widths[k] && j == c) v[off + j] = 1.f;
+      off += widths[k];
+    }
+    const uint8_t eb = effect_bits[p];
+#pragma unroll
+    for (int e = 0; e < 6; ++e) v[18 + e] = static_cast<float>((eb >> e) & 1);
+#pragma unroll
+    for (int i = 0; i < 24; ++i) Cvt<TX>::store(X, p * 24 + i, v[i]);
+  }
+}
+
+int grid_for(long n) {
+  long b = (n + 255) / 256;
+  return static_cast<int>(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+}
+
+}  // namespace
+
+void upsample2x_fwd(const void* x, void* y, int dt, int B, int H, int W, int C, hipStream_t s) {
+  const long n = static_cast<long>(B) * 4 * H * W * (C / 4);
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(upsample2x_fwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const bf16_t*>(x),
+                       static_cast<bf16_t*>(y), B, H, W, C);
+  else
+    hipLaunchKernelGGL(upsample2x_fwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const float*>(x),
+                       static_cast<float*>(y), B, H, W, C);
+}
+
+void upsample2x_bwd(const void* dy, void* dx, int dt, int B, int H, int W, int C, hipStream_t s) {
+  const long n = static_cast<long>(B) * H * W * (C / 4);
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(upsample2x_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s,
+                       static_cast<const bf16_t*>(dy), static_cast<bf16_t*>(dx), B, H, W, C);
+  else
+    hipLaunchKernelGGL(upsample2x_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const float*>(dy),
+                       static_cast<float*>(dx), B, H, W, C);
+}
+
+void spatial_effect_bits(const SpatialPlanes& sp, uint8_t* bits, int B, int L, int HW, hipStream_t s) {
+  const long n = static_cast<long>(B) * 6 * L;
+  hipLaunchKernelGGL(effect_bits_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, sp,
+                     reinterpret_cast<uint32_t*>(bits), B, L, HW);
+}
+
+void spatial_dense(const SpatialPlanes& sp, const uint8_t* bits, const float* wd, const float* bias, float* pre, long npix,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(spatial_dense_kernel, dim3(grid_for(npix)), dim3(256), 0, s, sp, bits, wd, bias, pre, npix);
+}
+
+void spatial_dense_input(const SpatialPlanes& sp, const uint8_t* bits, void* X, int x_dt, long npix, hipStream_t s) {
+  if (x_dt == DT_BF16)
+    hipLaunchKernelGGL(spatial_dense_input_kernel<bf16_t>, dim3(grid_for(npix)), dim3(256), 0, s, sp, bits,
+                       static_cast<bf16_t*>(X), npix);
+  else
+    hipLaunchKernelGGL(spatial_dense_input_kernel<float>, dim3(grid_for(npix)), dim3(256), 0, s, sp, bits,
+                       static_cast<float*>(X), npix);
+}
+
+void scatter_add_rows(const void* rows, int dt, const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num,
+                      float* pre, int B, int N, int H, int W, hipStream_t s) {
+  const long n = static_cast<long>(B) * N * 32;
+  if (n == 0) return;
+  dim3 grid(static_cast<unsigned>((n + 255) / 256));
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(scatter_add_rows_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(rows), ex,
+                       ey, entity_num, pre, B, N, H, W);
+  else
+    hipLaunchKernelGGL(scatter_add_rows_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(rows), ex, ey,
+                       entity_num, pre, B, N, H, W);
+}
+
+void gather_rows(const void* dpre, int dt, const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num,
+                 void* drows, int B, int N, int H, int W, hipStream_t s) {
+  const long n = static_cast<long>(B) * N * 32;
+  if (n == 0) return;
+  dim3 grid(static_cast<unsigned>((n + 255) / 256));
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(gather_rows_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(dpre), ex, ey,
+                       entity_num, static_cast<bf16_t*>(drows), B, N, H, W);
+  else
+    hipLaunchKernelGGL(gather_rows_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(dpre), ex, ey,
+                       entity_num, static_cast<float*>(drows), B, N, H, W);
+}
+
+void relu_cast(const float* x, void* y, int dt, long n, hipStream_t s) {
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(relu_cast_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s, x, static_cast<bf16_t*>(y), n);
+  else
+    hipLaunchKernelGGL(relu_cast_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, x, static_cast<float*>(y), n);
+}
+
+}  // namespace as

@@ -231,6 +231,18 @@ class SpatialEncoder(nn.Module):
     def forward(self, spatial_info, scatter_map):
         x = self.input_planes(spatial_info, scatter_map).to(self.project[0].weight.dtype)
         x = self.project(x)
+        return self.trunk(x)
+
+    def forward_native(self, spatial_info, proj, entity_x, entity_y, entity_num, native):
+        """GPU path: input planes + entity scatter + 1x1 projection fused (ops.native.spatial_embed).
+        The 1x1 conv is linear, so its 32 scatter-map columns are applied per entity *before* the
+        scatter-add (W_s . sum_e p_e == sum_e W_s . p_e) and no 32-channel scatter map is built."""
+        w = self.project[0].weight[:, :, 0, 0]                        # [32, 56]
+        rows = ops.linear(proj, w[:, 24:])                            # [B,N,32]
+        x = native.spatial_embed(spatial_info, rows, entity_x, entity_y, entity_num, w[:, :24], self.project[0].bias)
+        return self.trunk(x)
+
+    def trunk(self, x):
         map_skip = []
         for conv in self.downsample:
             map_skip.append(x)
@@ -254,8 +266,13 @@ class Encoder(nn.Module):
         embedded_scalar, scalar_context, baseline_feature = self.scalar_encoder(scalar_info)
         entity_embeddings, embedded_entity, entity_mask = self.entity_encoder(entity_info, entity_num)
         proj = self.scatter_project(entity_embeddings) * entity_mask.unsqueeze(2).to(entity_embeddings.dtype)
-        scatter_map = ops.scatter_connection(proj, entity_info['x'], entity_info['y'], SPATIAL_Y, SPATIAL_X)
-        embedded_spatial, map_skip = self.spatial_encoder(spatial_info, scatter_map)
+        n = ops._native(proj) if proj.is_cuda else None
+        if n is not None and n.has('spatial_embed'):
+            embedded_spatial, map_skip = self.spatial_encoder.forward_native(
+                spatial_info, proj, entity_info['x'], entity_info['y'], entity_num, n)
+        else:
+            scatter_map = ops.scatter_connection(proj, entity_info['x'], entity_info['y'], SPATIAL_Y, SPATIAL_X)
+            embedded_spatial, map_skip = self.spatial_encoder(spatial_info, scatter_map)
         lstm_input = torch.cat([embedded_scalar, embedded_entity.to(embedded_scalar.dtype),
                                 embedded_spatial.to(embedded_scalar.dtype)], dim=-1)
         return lstm_input, scalar_context, baseline_feature, entity_embeddings, map_skip
@@ -302,6 +319,8 @@ class ValueEncoder(nn.Module):
         sc = ops.scatter_connection(proj, x['unit_x'], x['unit_y'], H, W)
         sp = torch.cat([sc.to(proj.dtype), x['own_units_spatial'].to(proj.dtype),
                         x['enemy_units_spatial'].to(proj.dtype)], 1)
+        if sp.is_cuda:
+            sp = sp.contiguous(memory_format=torch.channels_last)
         sp = self.downsample(self.project(sp))
         for blk in self.res:
             sp = blk(sp)

@@ -259,12 +259,15 @@ class LocationHead(nn.Module):
     def forward(self, embedding, map_skip: List[torch.Tensor], temperature: float = 1.0, location=None, u=None):
         B = embedding.shape[0]
         p = self.project_embed(embedding).reshape(B, self.reshape_channel, self.hy, self.hx)
-        x = F.relu(torch.cat([p.to(map_skip[-1].dtype), map_skip[-1]], 1))
+        skip = map_skip[-1]
+        if skip.is_contiguous(memory_format=torch.channels_last):
+            p = p.contiguous(memory_format=torch.channels_last)
+        x = F.relu(torch.cat([p.to(skip.dtype), skip], 1))
         x = self.conv1(x)
         for i, blk in enumerate(self.res):
             x = blk(x + map_skip[len(map_skip) - 1 - i])
         for conv in self.upsample:
-            x = conv(F.interpolate(x, scale_factor=2.0, mode='bilinear', align_corners=False))
+            x = conv(ops.upsample2x(x))
         logits = x.reshape(B, -1).float() / temperature
         if location is None:
             location = sample_from_logits(logits, u)

@@ -17,7 +17,7 @@ from . import reference as ref
 from . import _ext
 
 __all__ = ['linear', 'layer_norm', 'conv2d', 'gated_residual', 'lnlstm_layer', 'varlen_attention',
-           'masked_attention', 'scatter_connection', 'sequence_mask', 'native_enabled', 'set_native']
+           'masked_attention', 'scatter_connection', 'sequence_mask', 'native_enabled', 'set_native', 'upsample2x']
 
 _NATIVE_ENABLED = True
 
@@ -87,3 +87,10 @@ def varlen_attention(qkv, cu_seqlens, max_len: int, num_heads: int, head_dim: in
 
 def scatter_connection(proj, x, y, H: int, W: int):
     return ref.scatter_connection(proj, x, y, H, W)
+
+
+def upsample2x(x):
+    n = _native(x)
+    if n is not None and n.has('upsample2x') and x.shape[1] % 4 == 0:
+        return n.upsample2x(x)
+    return F.interpolate(x, scale_factor=2.0, mode='bilinear', align_corners=False)

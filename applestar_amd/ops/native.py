@@ -20,12 +20,23 @@ def ensure_loaded():
     return _C
 
 
-_IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer'}
+_IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
+                'spatial_embed'}
 
 
 def has(name: str) -> bool:
     """True when this wrapper module implements ``name`` (the extension is loaded by ensure_loaded)."""
     return name in _IMPLEMENTED
+
+
+def nhwc(t):
+    """[B,C,H,W] (any layout) -> contiguous [B,H,W,C]; free for channels_last tensors."""
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def from_nhwc(t):
+    """contiguous [B,H,W,C] -> [B,C,H,W] view with channels_last strides."""
+    return t.permute(0, 3, 1, 2)
 
 
 def _dt_code(dtype) -> int:
@@ -88,6 +99,9 @@ class _GatedResidual(torch.autograd.Function):
 
 def gated_residual(y, g, sp, x):
     dt = torch.promote_types(torch.promote_types(y.dtype, g.dtype), x.dtype)
+    if x.dim() == 4:  # NCHW logical, run on the NHWC storage (channels_last end to end)
+        y, g, x = (nhwc(t.to(dt)) for t in (y, g, x))
+        return from_nhwc(_GatedResidual.apply(y, g, sp.float(), x))
     y, g, x = (t.to(dt).contiguous() for t in (y, g, x))
     return _GatedResidual.apply(y, g, sp.float(), x)
 
@@ -143,3 +157,113 @@ def lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b
     w_dtype = torch.bfloat16 if torch.is_autocast_enabled() else torch.float32
     out, hT, cT = _LNLSTMRecurrence.apply(xp, h0.float(), c0.float(), w_hh, lnh_w, lnh_b, lnc_w, lnc_b, w_dtype)
     return out, hT, cT
+
+
+# ---------------------------------------------------------------------------- entity embedding
+_KIND = {'one_hot': 0, 'binary': 1, 'scalar': 2}
+
+
+def _entity_table(entity_info):
+    from ..models.encoders import ENTITY_LAYOUT
+    fields, kind, offset, width = [], [], [], []
+    for name, enc, off, w in ENTITY_LAYOUT:
+        fields.append(entity_info[name].contiguous())
+        kind.append(_KIND[enc])
+        offset.append(off)
+        width.append(w)
+    return fields, kind, offset, width
+
+
+class _EntityEmbed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, w, b, index, out_dtype, *fields):
+        from ..models.encoders import ENTITY_LAYOUT
+        kind = [_KIND[e] for _, e, _, _ in ENTITY_LAYOUT]
+        offset = [o for _, _, o, _ in ENTITY_LAYOUT]
+        width = [x for _, _, _, x in ENTITY_LAYOUT]
+        wq = w.detach().to(out_dtype).t().contiguous()       # [997, 256]
+        out = _C.entity_embed_fwd(list(fields), kind, offset, width, index, wq, b.detach().float(),
+                                  _dt_code(out_dtype))
+        ctx.save_for_backward(out, index, *fields)
+        ctx.meta = (kind, offset, width, w.shape[1], out_dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        out, index, *fields = ctx.saved_tensors
+        kind, offset, width, k_in, out_dtype = ctx.meta
+        dpre = (dout * (out > 0)).to(out_dtype)
+        X = _C.entity_onehot(list(fields), kind, offset, width, index, k_in, _dt_code(out_dtype))
+        dw = (dpre.t() @ X).float()
+        db = dpre.float().sum(0)
+        return (dw, db, None, None) + (None,) * len(fields)
+
+
+def entity_embed(entity_info, flat_index, w, b):
+    """relu(one_hot_997(entity rows flat_index) @ w^T + b) without materialising the 997-wide input."""
+    fields, _, _, _ = _entity_table(entity_info)
+    flat = [f.reshape(-1) for f in fields]
+    out_dtype = torch.bfloat16 if torch.is_autocast_enabled() else torch.float32
+    return _EntityEmbed.apply(w, b, flat_index.contiguous(), out_dtype, *flat)
+
+
+# ---------------------------------------------------------------------------- bilinear x2 (NHWC)
+class _Upsample2x(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_nhwc):
+        return _C.upsample2x_fwd(x_nhwc)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _C.upsample2x_bwd(dy.contiguous())
+
+
+def upsample2x(x):
+    """F.interpolate(x, scale_factor=2, mode='bilinear', align_corners=False) for [B,C,H,W] with C%4==0;
+    computed in x's dtype (bf16 stays bf16) on the channels_last storage."""
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    return from_nhwc(_Upsample2x.apply(nhwc(x)))
+
+
+# ---------------------------------------------------------------------------- spatial input embedding
+class _SpatialEmbed(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, w_dense, bias, rows, ex, ey, entity_num, out_dtype, n_planes, *tensors):
+        planes = list(tensors[:n_planes])
+        effects = list(tensors[n_planes:])
+        bits, out = _C.spatial_embed_fwd(planes, effects, w_dense.detach().float().contiguous(),
+                                         bias.detach().float(), rows.contiguous(), ex, ey, entity_num,
+                                         _dt_code(out_dtype))
+        ctx.save_for_backward(out, bits, ex, ey, entity_num, *tensors)
+        ctx.n_planes = n_planes
+        ctx.N = rows.shape[1]
+        ctx.rows_dtype = rows.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        out, bits, ex, ey, entity_num, *tensors = ctx.saved_tensors
+        planes, effects = list(tensors[:ctx.n_planes]), list(tensors[ctx.n_planes:])
+        dpre = (dout * (out > 0)).to(out.dtype).contiguous()                    # [B,H,W,32]
+        drows = _C.spatial_gather_rows(dpre, ex, ey, entity_num, ctx.N).to(ctx.rows_dtype)
+        X = _C.spatial_dense_input(planes, effects, bits, _dt_code(out.dtype))  # [npix,24]
+        d2 = dpre.view(-1, 32)
+        dw = (d2.t() @ X).float()
+        db = d2.float().sum(0)
+        return (dw, db, drows) + (None,) * (5 + len(tensors))
+
+
+def spatial_embed(spatial_info, rows, entity_x, entity_y, entity_num, w_dense, bias):
+    """relu(1x1conv(56 input planes)) where the 32 scatter channels arrive pre-multiplied per entity
+    (``rows`` = scatter_project(entity) @ W[:, 24:56]^T).  Returns [B,32,H,W] channels_last."""
+    from ..lib.features import SPATIAL_ONE_HOT, EFFECT_KEYS
+    planes = [spatial_info['height_map']] + [spatial_info[k] for k, _ in SPATIAL_ONE_HOT]
+    planes = [p.to(torch.uint8).contiguous() for p in planes]
+    effects = [spatial_info[k].to(torch.int16).contiguous() for k in EFFECT_KEYS]
+    out_dtype = torch.bfloat16 if torch.is_autocast_enabled() else torch.float32
+    ex = entity_x.to(torch.uint8).contiguous()
+    ey = entity_y.to(torch.uint8).contiguous()
+    out = _SpatialEmbed.apply(w_dense, bias, rows, ex, ey, entity_num.long().contiguous(), out_dtype, len(planes),
+                              *planes, *effects)
+    return from_nhwc(out)

@@ -67,7 +67,9 @@ class GradientReducer:
         off = 0
         for p in params:
             n = p.numel()
-            p.grad = b.flat[off:off + n].view_as(p)
+            # same strides as the parameter (channels_last conv weights) so fused optimizers that walk
+            # param and grad storage in lockstep see matching elements
+            p.grad = b.flat[off:off + n].as_strided(p.shape, p.stride())
             self._owner[p] = b
             off += n
         self.buckets.append(b)

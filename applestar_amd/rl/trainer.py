@@ -49,6 +49,8 @@ class RLTrainer:
         self.device = torch.device(device)
         self.model = model if model is not None else Model(self.cfg, use_value_network=True)
         self.model.to(self.device)
+        if self.device.type == 'cuda':  # NHWC convolutions end to end (MIOpen igemm kernels are NHWC)
+            self.model.to(memory_format=torch.channels_last)
         pdist.broadcast_module(self.model)
         self.params = [p for p in self.model.parameters() if p.requires_grad]
         comm = getattr(torch, lc.comm_dtype) if lc.get('comm_dtype') else None

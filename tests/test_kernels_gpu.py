@@ -110,3 +110,77 @@ def test_lnlstm_layer_matches_reference(H, I, T, B, autocast):
     for a, b in zip([x, h0, c0] + params, ref_in):
         scale = max(1.0, b.grad.abs().max().item())
         assert _err(a.grad, b.grad) < tol * 4 * scale
+
+
+@pytest.mark.parametrize('autocast', [False, True])
+def test_entity_embed_matches_one_hot_linear(autocast):
+    from applestar_amd.lib.features import random_obs
+    from applestar_amd.models.encoders import entity_one_hot_input
+    torch.manual_seed(4)
+    obs = random_obs(5, max_entities=70, generator=torch.Generator().manual_seed(4))
+    info = {k: v.cuda() for k, v in obs['entity_info'].items()}
+    en = obs['entity_num'].cuda()
+    N = info['unit_type'].shape[1]
+    idx = (torch.arange(N, device=DEV)[None] < en[:, None]).reshape(-1).nonzero().squeeze(1)
+    w = (torch.randn(256, 997, device=DEV) * 0.05).requires_grad_()
+    b = (torch.randn(256, device=DEV) * 0.1).requires_grad_()
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    with torch.autocast('cuda', dtype=torch.bfloat16, enabled=autocast):
+        out = N.entity_embed(info, idx, w, b)
+    X = entity_one_hot_input(info, idx, torch.float32)
+    ref = torch.relu(X @ wr.t() + br)
+    tol = 3e-2 if autocast else 1e-4
+    assert _err(out, ref) < tol * max(1, ref.abs().max().item())
+    g = torch.randn_like(ref)
+    out.backward(g.to(out.dtype))
+    ref.backward(g)
+    assert _err(w.grad, wr.grad) < tol * max(1, wr.grad.abs().max().item()) * 2
+    assert _err(b.grad, br.grad) < tol * max(1, br.grad.abs().max().item()) * 2
+
+
+@pytest.mark.parametrize('C,H,W', [(128, 19, 20), (32, 76, 80), (4, 3, 5)])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_upsample2x_matches_interpolate(C, H, W, dtype):
+    torch.manual_seed(5)
+    x = torch.randn(3, C, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    xr = x.detach().float().requires_grad_()
+    y = N.upsample2x(x)
+    yr = torch.nn.functional.interpolate(xr, scale_factor=2.0, mode='bilinear', align_corners=False)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    assert _err(y, yr) < tol
+    g = torch.randn_like(yr).to(dtype)
+    y.backward(g)
+    yr.backward(g.float())
+    assert _err(x.grad, xr.grad) < tol * 4
+
+
+@pytest.mark.parametrize('autocast', [False, True])
+def test_spatial_embed_matches_reference_planes(autocast):
+    from applestar_amd.lib.features import random_obs
+    from applestar_amd.models.encoders import SpatialEncoder
+    from applestar_amd.ops.reference import scatter_connection
+    torch.manual_seed(6)
+    obs = random_obs(3, max_entities=40, generator=torch.Generator().manual_seed(6))
+    sp = {k: v.cuda() for k, v in obs['spatial_info'].items()}
+    ent = {k: v.cuda() for k, v in obs['entity_info'].items()}
+    en = obs['entity_num'].cuda()
+    B, Nn = ent['x'].shape
+    proj = torch.relu(torch.randn(B, Nn, 32, device=DEV))
+    proj = proj * (torch.arange(Nn, device=DEV)[None] < en[:, None]).unsqueeze(2)
+    w = (torch.randn(32, 56, device=DEV) * 0.2).requires_grad_()
+    b = (torch.randn(32, device=DEV) * 0.1).requires_grad_()
+    proj = proj.requires_grad_()
+    wr, br, pr = (t.detach().clone().requires_grad_() for t in (w, b, proj))
+    with torch.autocast('cuda', dtype=torch.bfloat16, enabled=autocast):
+        rows = torch.nn.functional.linear(proj, w[:, 24:])
+        out = N.spatial_embed(sp, rows, ent['x'], ent['y'], en, w[:, :24], b)
+    smap = scatter_connection(pr, ent['x'], ent['y'], 152, 160)
+    planes = SpatialEncoder.input_planes(sp, smap)
+    ref = torch.relu(torch.nn.functional.conv2d(planes, wr[:, :, None, None], br))
+    tol = 5e-2 if autocast else 1e-4
+    assert _err(out, ref) < tol * max(1, ref.abs().max().item())
+    g = torch.randn_like(ref)
+    out.backward(g.to(out.dtype))
+    ref.backward(g)
+    for a, r in ((w.grad, wr.grad), (b.grad, br.grad), (proj.grad, pr.grad)):
+        assert _err(a, r) < tol * max(1, r.abs().max().item()) * 2
