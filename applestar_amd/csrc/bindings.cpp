@@ -327,6 +327,37 @@ at::Tensor spatial_dense_input(const std::vector<at::Tensor>& planes, const std:
   return X;
 }
 
+// ---------------------------------------------------------------- varlen attention
+std::vector<at::Tensor> varlen_attn_fwd(const at::Tensor& qkv, const at::Tensor& cu, int64_t max_len, int64_t H) {
+  check_cuda(qkv, "qkv");
+  check_cuda(cu, "cu_seqlens");
+  TORCH_CHECK(qkv.scalar_type() == at::kBFloat16 && qkv.dim() == 2 && qkv.size(1) == 3 * H * 128,
+              "varlen_attn: qkv bf16 [T, 3*H*128]");
+  TORCH_CHECK(cu.scalar_type() == at::kInt, "cu_seqlens int32");
+  const int64_t T = qkv.size(0), S = cu.numel() - 1;
+  c10::hip::HIPGuard g(qkv.device().index());
+  auto out = at::empty({T, H * 128}, qkv.options());
+  auto lse = at::empty({H, T}, qkv.options().dtype(at::kFloat));
+  if (T > 0 && S > 0)
+    as::varlen_attn_fwd(qkv.data_ptr(), cu.data_ptr<int>(), out.data_ptr(), lse.data_ptr<float>(), S, max_len, H, T,
+                        1.0f / std::sqrt(128.0f), stream());
+  return {out, lse};
+}
+
+at::Tensor varlen_attn_bwd(const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& dout, const at::Tensor& lse,
+                           const at::Tensor& cu, int64_t max_len, int64_t H) {
+  check_cuda(dout, "dout");
+  TORCH_CHECK(dout.scalar_type() == at::kBFloat16 && dout.sizes() == out.sizes(), "varlen_attn_bwd: dout");
+  const int64_t T = qkv.size(0), S = cu.numel() - 1;
+  c10::hip::HIPGuard g(qkv.device().index());
+  auto dqkv = at::empty_like(qkv);
+  auto delta = at::empty({H, T}, qkv.options().dtype(at::kFloat));
+  if (T > 0 && S > 0)
+    as::varlen_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), cu.data_ptr<int>(),
+                        dqkv.data_ptr(), delta.data_ptr<float>(), S, max_len, H, T, 1.0f / std::sqrt(128.0f), stream());
+  return dqkv;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -345,4 +376,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spatial_embed_fwd", &spatial_embed_fwd);
   m.def("spatial_gather_rows", &spatial_gather_rows);
   m.def("spatial_dense_input", &spatial_dense_input);
+  m.def("varlen_attn_fwd", &varlen_attn_fwd);
+  m.def("varlen_attn_bwd", &varlen_attn_bwd);
 }

@@ -43,7 +43,7 @@ def write_ninja() -> str:
     py_inc = sysconfig.get_paths()['include']
     kernels = sorted(glob.glob(os.path.join(HERE, 'kernels', '*.hip')))
     hipcc = os.path.join(ROCM, 'bin', 'hipcc')
-    hip_flags = (f'--offload-arch={ARCH} -O3 -fPIC -std=c++17 -ffast-math -fno-gpu-rdc -I{HERE} '
+    hip_flags = (f'--offload-arch={ARCH} -O3 -fPIC -std=c++17 -fno-gpu-rdc -I{HERE} '
                  f'-D__HIP_PLATFORM_AMD__ -Wno-unused-result')
     cxx_flags = ' '.join([
         '-O2 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -DTORCH_EXTENSION_NAME=_C',

@@ -93,4 +93,12 @@ void gather_rows(const void* dpre, int dt, const uint8_t* ex, const uint8_t* ey,
                  void* drows, int B, int N, int H, int W, hipStream_t s);
 void relu_cast(const float* x, void* y, int dt, long n, hipStream_t s);
 
+// ---- attention.hip ---------------------------------------------------------------------------
+// Packed varlen MHA, head dim 128, bf16. qkv [T][3][H][128], cu [S+1] int32, out [T][H][128],
+// lse2 [H][T] (log2 domain).  Backward writes dqkv [T][3][H][128]; delta scratch [H][T].
+void varlen_attn_fwd(const void* qkv, const int* cu, void* out, float* lse2, int S, int max_len, int H, long Ttot,
+                     float scale, hipStream_t s);
+void varlen_attn_bwd(const void* qkv, const void* out, const void* dout, const float* lse2, const int* cu, void* dqkv,
+                     float* delta, int S, int max_len, int H, long Ttot, float scale, hipStream_t s);
+
 }  // namespace as

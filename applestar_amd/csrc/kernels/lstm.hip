@@ -93,7 +93,8 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_kernel(
 #pragma unroll
     for (int k = 0; k < COLS; ++k) acc[k] = 0.f;
     const TW* wp = wT + tid * COLS;
-#pragma unroll 8
+    // deep unroll: the W^T stream is L2-latency bound at B=6, keep many 8-16 B loads in flight
+#pragma unroll 32
     for (int i = 0; i < H; ++i) {
       float wv[COLS];
       WLoad<TW, COLS>::load(wp + static_cast<long>(i) * G, wv);
@@ -228,12 +229,37 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
       dg_s[j] = v;  // each thread overwrites only its own columns
     }
     __syncthreads();
-    // ---- dh_{t-1} = dhg @ W  (W [G][H])
-    if (unit) {
-      float acc = 0.f;
-#pragma unroll 8
-      for (int j = 0; j < G; ++j) acc = fmaf(dg_s[j], Cvt<TW>::load(w, static_cast<long>(j) * H + tid), acc);
-      dh_s[tid] = acc;
+    // ---- dh_{t-1} = dhg @ W  (W [G][H]): 2-D split, each thread owns KV consecutive outputs and
+    // 1/JG of the reduction (coalesced KV*2-byte loads along k), partials combined through LDS
+    {
+      constexpr int KV = (H % 4 == 0 && (H / 4) * 4 <= NT) ? 4 : 1;
+      constexpr int KT = H / KV;              // threads along k
+      constexpr int JG = NT / KT;             // reduction groups
+      const int kq = tid % KT, jg = tid / KT;
+      float acc[KV];
+#pragma unroll
+      for (int v = 0; v < KV; ++v) acc[v] = 0.f;
+      if (jg < JG) {
+        const int j0 = jg * (G / JG), j1 = j0 + G / JG;
+#pragma unroll 32
+        for (int j = j0; j < j1; ++j) {
+          const float d = dg_s[j];
+#pragma unroll
+          for (int v = 0; v < KV; ++v) acc[v] = fmaf(d, Cvt<TW>::load(w, static_cast<long>(j) * H + kq * KV + v), acc[v]);
+        }
+      }
+      __shared__ float part[JG > 0 ? JG : 1][H];
+      if (jg < JG) {
+#pragma unroll
+        for (int v = 0; v < KV; ++v) part[jg][kq * KV + v] = acc[v];
+      }
+      __syncthreads();
+      if (unit) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int g2 = 0; g2 < JG; ++g2) sacc += part[g2][tid];
+        dh_s[tid] = sacc;
+      }
     }
     __syncthreads();
   }

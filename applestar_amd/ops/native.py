@@ -21,7 +21,7 @@ def ensure_loaded():
 
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
-                'spatial_embed'}
+                'spatial_embed', 'varlen_attention'}
 
 
 def has(name: str) -> bool:
@@ -248,9 +248,11 @@ class _SpatialEmbed(torch.autograd.Function):
         dpre = (dout * (out > 0)).to(out.dtype).contiguous()                    # [B,H,W,32]
         drows = _C.spatial_gather_rows(dpre, ex, ey, entity_num, ctx.N).to(ctx.rows_dtype)
         X = _C.spatial_dense_input(planes, effects, bits, _dt_code(out.dtype))  # [npix,24]
-        d2 = dpre.view(-1, 32)
-        dw = (d2.t() @ X).float()
-        db = d2.float().sum(0)
+        B = dpre.shape[0]
+        # K = B*H*W ~ 1e7 is far too deep for one GEMM tile: batch over observations, then sum
+        d3 = dpre.view(B, -1, 32)
+        dw = torch.bmm(d3.transpose(1, 2), X.view(B, -1, 24)).float().sum(0)
+        db = d3.float().sum((0, 1))
         return (dw, db, drows) + (None,) * (5 + len(tensors))
 
 
@@ -267,3 +269,30 @@ def spatial_embed(spatial_info, rows, entity_x, entity_y, entity_num, w_dense, b
     out = _SpatialEmbed.apply(w_dense, bias, rows, ex, ey, entity_num.long().contiguous(), out_dtype, len(planes),
                               *planes, *effects)
     return from_nhwc(out)
+
+
+# ---------------------------------------------------------------------------- varlen attention
+class _VarlenAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, cu, max_len, heads):
+        out, lse = _C.varlen_attn_fwd(qkv, cu, max_len, heads)
+        ctx.save_for_backward(qkv, out, lse, cu)
+        ctx.max_len, ctx.heads = max_len, heads
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse, cu = ctx.saved_tensors
+        dqkv = _C.varlen_attn_bwd(qkv, out, dout.to(torch.bfloat16).contiguous(), lse, cu, ctx.max_len, ctx.heads)
+        return dqkv, None, None, None
+
+
+def varlen_attention(qkv, cu_seqlens, max_len: int, num_heads: int, head_dim: int):
+    """Packed self-attention over variable-length entity sets (bf16 flash kernel, head_dim 128)."""
+    if head_dim != 128:
+        from . import reference
+        return reference.varlen_attention(qkv, cu_seqlens, max_len, num_heads, head_dim)
+    dtype = qkv.dtype
+    out = _VarlenAttention.apply(qkv.to(torch.bfloat16).contiguous(), cu_seqlens.to(torch.int32).contiguous(),
+                                 int(max_len), int(num_heads))
+    return out if dtype == torch.bfloat16 else out.to(dtype)

@@ -120,8 +120,8 @@ def test_entity_embed_matches_one_hot_linear(autocast):
     obs = random_obs(5, max_entities=70, generator=torch.Generator().manual_seed(4))
     info = {k: v.cuda() for k, v in obs['entity_info'].items()}
     en = obs['entity_num'].cuda()
-    N = info['unit_type'].shape[1]
-    idx = (torch.arange(N, device=DEV)[None] < en[:, None]).reshape(-1).nonzero().squeeze(1)
+    n_ent = info['unit_type'].shape[1]
+    idx = (torch.arange(n_ent, device=DEV)[None] < en[:, None]).reshape(-1).nonzero().squeeze(1)
     w = (torch.randn(256, 997, device=DEV) * 0.05).requires_grad_()
     b = (torch.randn(256, device=DEV) * 0.1).requires_grad_()
     wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
@@ -184,3 +184,21 @@ def test_spatial_embed_matches_reference_planes(autocast):
     ref.backward(g)
     for a, r in ((w.grad, wr.grad), (b.grad, br.grad), (proj.grad, pr.grad)):
         assert _err(a, r) < tol * max(1, r.abs().max().item()) * 2
+
+
+@pytest.mark.parametrize('lens', [[1, 64, 65, 200, 511], [37], [128, 3, 300]])
+def test_varlen_attention_matches_reference(lens):
+    torch.manual_seed(7)
+    H, Dh = 2, 128
+    T = sum(lens)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    qkv = (torch.randn(T, 3 * H * Dh, device=DEV) * 0.5).to(torch.bfloat16).requires_grad_()
+    ref_in = qkv.detach().float().requires_grad_()
+    out = N.varlen_attention(qkv, cu, max(lens), H, Dh)
+    ref = R.varlen_attention(ref_in, cu, max(lens), H, Dh)
+    assert _err(out, ref) < 2e-2
+    g = torch.randn_like(ref)
+    out.backward(g.to(torch.bfloat16))
+    ref.backward(g)
+    scale = ref_in.grad.abs().max().item()
+    assert _err(qkv.grad, ref_in.grad) < 3e-2 * max(1.0, scale)

@@ -16,3 +16,7 @@ if [ "${PROFILE:-0}" = "1" ]; then
   cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 2 --warmup 1 > $GRAFT_REPO_ROOT/gpurun_out/${TAG}_prof.log 2>&1
   echo "prof exit $?"
 fi
+if [ "${PHASES:-0}" = "1" ]; then
+  timeout -k 10 600 python tools/phase_timing.py > gpurun_out/${TAG}_phases.log 2>&1; echo "phases exit $?"
+  cat gpurun_out/${TAG}_phases.log | tail -15
+fi

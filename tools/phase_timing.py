@@ -1,0 +1,74 @@
+"""Per-phase GPU timing of one RL learner iteration (forward sub-modules, loss, backward, optimizer).
+Usage: python tools/phase_timing.py [--no-native]"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from applestar_amd import ops  # noqa: E402
+from applestar_amd.rl.trainer import RLTrainer  # noqa: E402
+from applestar_amd.rl.synthetic import rl_batch, to_device  # noqa: E402
+
+
+def timeit(fn, reps=5):
+    fn()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for _ in range(reps):
+        out = fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t) / reps * 1000, out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--no-native', action='store_true')
+    args = ap.parse_args()
+    if args.no_native:
+        ops.set_native(False)
+    dev = torch.device('cuda', 0)
+    tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}, device=dev)
+    b = to_device(rl_batch(6, 64, seed=0), dev)
+    m = tr.model
+    B, T = 6, 64
+    amp = torch.autocast('cuda', dtype=torch.bfloat16)
+    res = {}
+    with torch.no_grad(), amp:
+        res['scalar_encoder'], _ = timeit(lambda: m.encoder.scalar_encoder(b['scalar_info']))
+        res['entity_encoder'], ent = timeit(lambda: m.encoder.entity_encoder(b['entity_info'], b['entity_num']))
+        res['encoder(total)'], enc = timeit(lambda: m.encoder(b['spatial_info'], b['entity_info'], b['scalar_info'], b['entity_num']))
+        lstm_in = enc[0]
+        h0 = [(h.view(-1, B, 384)[0].float(), c.view(-1, B, 384)[0].float()) for h, c in b['hidden_state']]
+        res['core_lstm'], core = timeit(lambda: m.core_lstm(lstm_in.view(T + 1, B, -1), h0))
+        lo = core[0].reshape((T + 1) * B, -1)
+        n = T * B
+        fa = {k: v.flatten(0, 1) for k, v in b['action_info'].items()}
+        res['policy.train_forward'], _ = timeit(lambda: m.policy.train_forward(
+            lo[:n], enc[3][:n], [x[:n] for x in enc[4]], enc[1][:n], b['entity_num'][:n], fa,
+            b['selected_units_num'].flatten(0, 1)))
+        res['value_encoder'], vf = timeit(lambda: m.value_encoder(b['value_feature']))
+        crit = torch.cat([lo.to(vf.dtype), vf, enc[2].to(vf.dtype)], 1)
+        res['value_networks'], _ = timeit(lambda: m.value_networks['winloss'](crit))
+    with amp:
+        res['forward(total)'], out = timeit(lambda: m.rl_learner_forward(**b))
+    res['loss'], info = timeit(lambda: tr.loss.compute_loss(out))
+
+    def fb():
+        with amp:
+            o = m.rl_learner_forward(**b)
+        i = tr.loss.compute_loss(o)
+        tr.reducer.zero_grad()
+        i['total_loss'].backward()
+        return i
+    res['fwd+loss+bwd'], _ = timeit(fb, reps=3)
+    res['clip+adam'], _ = timeit(lambda: (tr.grad_clip.apply(tr.params), tr.optimizer.step()))
+    res['full step'], _ = timeit(lambda: tr.step(b), reps=3)
+    for k, v in res.items():
+        print(f'{k:28s} {v:8.2f} ms')
+
+
+if __name__ == '__main__':
+    main()
