@@ -170,7 +170,8 @@ class SelectedUnitsHead(nn.Module):
         end_pos = F.one_hot(en.clamp(max=N1 - 1), N1).bool()
         mask[:, 0] &= ~end_pos
         logits = logits.masked_fill(~mask, NEG)
-        return logits, selected_units, ae_after[:, -1], selected_units_num
+        # the reference returns no sampled units in teacher-forced mode (test_iou off): None
+        return logits, None, ae_after[:, -1], selected_units_num
 
     # ------------------------------------------------------------------ sampling (actor)
     def forward_sample(self, ae0, entity_embedding, entity_num, su_mask, temperature: float = 1.0,
