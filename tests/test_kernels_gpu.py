@@ -133,9 +133,11 @@ def test_entity_embed_matches_one_hot_linear(autocast):
     assert _err(out, ref) < tol * max(1, ref.abs().max().item())
     g = torch.randn_like(ref)
     out.backward(g.to(out.dtype))
-    ref.backward(g)
-    assert _err(w.grad, wr.grad) < tol * max(1, wr.grad.abs().max().item()) * 2
-    assert _err(b.grad, br.grad) < tol * max(1, br.grad.abs().max().item()) * 2
+    # relu-boundary flips between bf16 and fp32 pre-activations are not kernel errors: take the
+    # mask from the native output and check dW = dpre^T X, db = sum dpre exactly against fp32
+    dpre = g * (out.float() > 0)
+    assert _err(w.grad, dpre.t() @ X) < tol * max(1, (dpre.t() @ X).abs().max().item())
+    assert _err(b.grad, dpre.sum(0)) < tol * max(1, dpre.sum(0).abs().max().item())
 
 
 @pytest.mark.parametrize('C,H,W', [(128, 19, 20), (32, 76, 80), (4, 3, 5)])
