@@ -52,6 +52,39 @@ def main():
         res['value_encoder'], vf = timeit(lambda: m.value_encoder(b['value_feature']))
         crit = torch.cat([lo.to(vf.dtype), vf, enc[2].to(vf.dtype)], 1)
         res['value_networks'], _ = timeit(lambda: m.value_networks['winloss'](crit))
+    # forward+backward per sub-module (scalar = sum of outputs)
+    def fb_sub(fn):
+        def run():
+            with amp:
+                outs = fn()
+            flat = []
+            def collect(o):
+                if torch.is_tensor(o):
+                    if o.requires_grad:
+                        flat.append(o.float().sum())
+                elif isinstance(o, (list, tuple)):
+                    for x in o:
+                        collect(x)
+                elif isinstance(o, dict):
+                    for x in o.values():
+                        collect(x)
+            collect(outs)
+            sum(flat).backward()
+        return run
+    res['fb:entity_encoder'], _ = timeit(fb_sub(lambda: m.encoder.entity_encoder(b['entity_info'], b['entity_num'])))
+    res['fb:encoder(total)'], _ = timeit(fb_sub(lambda: m.encoder(b['spatial_info'], b['entity_info'], b['scalar_info'], b['entity_num'])))
+    lstm_in_g = lstm_in.detach().float().requires_grad_()
+    res['fb:core_lstm'], _ = timeit(fb_sub(lambda: m.core_lstm(lstm_in_g.view(T + 1, B, -1), h0)[0]))
+    lo_g = lo.detach().float().requires_grad_()
+    ee_g = enc[3].detach().float().requires_grad_()
+    ms_g = [x.detach().float().requires_grad_() for x in enc[4]]
+    sc_g = enc[1].detach().float().requires_grad_()
+    res['fb:policy'], _ = timeit(fb_sub(lambda: m.policy.train_forward(
+        lo_g[:n], ee_g[:n], [x[:n] for x in ms_g], sc_g[:n], b['entity_num'][:n], fa,
+        b['selected_units_num'].flatten(0, 1))[2]))
+    res['fb:value_encoder'], _ = timeit(fb_sub(lambda: m.value_encoder(b['value_feature'])))
+    crit_g = crit.detach().float().requires_grad_()
+    res['fb:value_networks'], _ = timeit(fb_sub(lambda: m.value_networks['winloss'](crit_g)))
     with amp:
         res['forward(total)'], out = timeit(lambda: m.rl_learner_forward(**b))
     res['loss'], info = timeit(lambda: tr.loss.compute_loss(out))
