@@ -10,6 +10,9 @@ Sources:
   distar/agent/default/lib/actions.py:5-333       ACTIONS
   distar/pysc2/lib/static_data.py:123-201,318-331 UNIT_TYPES, BUFFS, UPGRADES, ADDON, *_ABILITIES
   distar/agent/default/lib/stat.py:533-631        ACTION_RACE_MASK
+  distar/agent/default/lib/stat.py:73-330         unit_dict, cum_dict, action_result_dict (league stats)
+  distar/pysc2/lib/units.py, upgrades.py          unit / upgrade enum names (ids -> names for logs)
+  distar/envs/map_info.py:8-258                   MAPS (bnet name, path, cropped / full size)
 """
 import ast
 import json
@@ -39,6 +42,16 @@ def _torch_tensor_arg(node):
     return ast.literal_eval(node.args[0])
 
 
+def _enum_classes(path):
+    tree = ast.parse(open(path).read())
+    out = {}
+    for node in tree.body:
+        if isinstance(node, ast.ClassDef):
+            out[node.name] = {t.targets[0].id: ast.literal_eval(t.value) for t in node.body
+                              if isinstance(t, ast.Assign) and isinstance(t.targets[0], ast.Name)}
+    return out
+
+
 def main():
     acts = _assignments(os.path.join(REF, 'distar/agent/default/lib/actions.py'))
     static = _assignments(os.path.join(REF, 'distar/pysc2/lib/static_data.py'))
@@ -58,6 +71,12 @@ def main():
         'unit_general_abilities': _literal(static['UNIT_GENERAL_ABILITIES']),
         'unit_mix_abilities': _literal(static['UNIT_MIX_ABILITIES']),
         'action_race_mask': race_mask,
+        'unit_dict': {race: {str(k): v for k, v in d.items()} for race, d in _literal(stat['unit_dict']).items()},
+        'cum_dict': _literal(stat['cum_dict']),
+        'action_result_dict': _literal(stat['action_result_dict']),
+        'unit_enums': _enum_classes(os.path.join(REF, 'distar/pysc2/lib/units.py')),
+        'upgrade_enums': _enum_classes(os.path.join(REF, 'distar/pysc2/lib/upgrades.py'))['Upgrades'],
+        'maps': {k: list(v) for k, v in _literal(_assignments(os.path.join(REF, 'distar/envs/map_info.py'))['MAPS']).items()},
     }
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     with open(OUT, 'w') as f:
