@@ -1,0 +1,80 @@
+"""Actor <-> league / learner communication (``distar/ctools/worker/actor/actor_comm.py``).
+
+* ``ask_for_job``: POST ``league/actor_ask_for_job`` until a job is returned (retry with back-off);
+* ``update_model``: every ``actor_model_update_interval`` seconds pull each trained player's newest
+  ``<player>model`` broadcast from the data plane and hot-load it (into the GPU inference server's
+  resident model when batching, else into the local models); a ``reset_flag`` edge restarts envs;
+* ``send_result``: POST ``league/actor_send_result``.
+Trajectories are pushed by the env workers themselves (see :mod:`applestar_amd.actor.actor`).
+"""
+from __future__ import annotations
+
+import time
+from collections import deque
+
+from ..comm.adapter import Adapter
+from ..league.api import HttpClient
+
+
+class ActorComm:
+    def __init__(self, cfg, actor_uid: str, logger=None):
+        c = cfg.communication
+        self._cfg = cfg
+        self._uid = actor_uid
+        self._logger = logger
+        self._league = HttpClient(c.league_ip, c.league_port)
+        self._adapter = Adapter(c.coordinator_ip, c.coordinator_port)
+        self._interval = float(c.actor_model_update_interval)
+        self._last_update = -1.0
+        self._last_reset = {}
+        self.update_times = deque(maxlen=100)
+        self.job = None
+
+    def ask_for_job(self, actor=None) -> dict:
+        delay = 1.0
+        while True:
+            try:
+                job = self._league.post('/league/actor_ask_for_job', {'job_type': self._cfg.actor.league_job_type})
+                if job:
+                    self.job = job
+                    return job
+            except (ConnectionError, RuntimeError) as e:
+                if self._logger:
+                    self._logger.warning(f'ask_for_job failed: {e}')
+            time.sleep(delay)
+            delay = min(delay * 2, 30.0)
+
+    def update_model(self, actor) -> None:
+        if not self.job or not self.job.get('update_players'):
+            return
+        now = time.time()
+        if self._last_update > 0 and now - self._last_update < self._interval:
+            return
+        self._last_update = now
+        reset = False
+        for pid in self.job['update_players']:
+            t0 = time.time()
+            got = self._adapter.pull(pid + 'model', size=1, block=False)
+            if not got:
+                continue
+            sd = got[0]
+            server = getattr(actor, '_server', None)
+            if server is not None and pid in server.models:
+                server.load_state_dict(pid, sd['model'], last_iter=sd.get('model_last_iter', 0))
+            self.update_times.append(time.time() - t0)
+            flag = bool(sd.get('reset_flag', False))
+            if flag and not self._last_reset.get(pid, False):
+                reset = True
+            self._last_reset[pid] = flag
+        if reset:
+            actor.reset_env()
+
+    def send_result(self, result: dict) -> None:
+        try:
+            self._league.post('/league/actor_send_result', result)
+        except (ConnectionError, RuntimeError) as e:
+            if self._logger:
+                self._logger.error(f'send_result failed: {e}')
+
+    def close(self):
+        self._adapter.close()

@@ -1,0 +1,174 @@
+"""Batched GPU inference server for actors (the reference's ``gpu_batch_inference``).
+
+Reference (``agent.py:145-158,364-385,781-805``, ``actor.py:268-299``): every env process writes its
+observation into a shared-memory slot and bumps a signal; a GPU loop runs ``compute_logp_action`` on
+*all* slots (active or not) and copies flagged rows back; env processes poll with ``sleep(0.01)``.
+
+MI355X design:
+* one server per GPU owns every model (policy per player, teacher per player) on the device;
+* env workers send one serialized request (``utils.serialize``: one buffer, no pickling) over a
+  pipe and block on the reply — no polling;
+* dynamic batching: the server waits on all pipes (``connection.wait``), then keeps collecting until
+  either every live worker has a request queued or ``max_wait_ms`` passed, and runs ONE forward per
+  (player, kind) group over only the rows that asked — padded to the group's max entity count;
+* the batched input is assembled in pinned host memory and copied with ``non_blocking``;
+  outputs come back with one D2H copy per group.
+"""
+from __future__ import annotations
+
+import threading
+import time
+from collections import defaultdict
+from multiprocessing.connection import Connection, wait
+from typing import Dict, List, Optional
+
+import torch
+
+from ..agent.collate import collate_obs, decollate_output
+from ..utils import serialize
+
+
+def _to(tree, device, non_blocking=True):
+    if isinstance(tree, torch.Tensor):
+        if device.type == 'cuda':
+            return tree.pin_memory().to(device, non_blocking=non_blocking)
+        return tree
+    if isinstance(tree, dict):
+        return {k: _to(v, device, non_blocking) for k, v in tree.items()}
+    if isinstance(tree, (list, tuple)):
+        return type(tree)(_to(v, device, non_blocking) for v in tree)
+    return tree
+
+
+class InferenceClient:
+    """Worker-side handle: ``infer(model_input) -> per-sample output`` (blocking)."""
+
+    def __init__(self, conn: Connection, player_id: str, kind: str = 'policy'):
+        self._conn = conn
+        self.player_id = player_id
+        self.kind = kind
+
+    def infer(self, model_input: Dict) -> Dict:
+        self._conn.send_bytes(serialize.dumps({'player_id': self.player_id, 'kind': self.kind, 'input': model_input}))
+        return serialize.loads(self._conn.recv_bytes())
+
+
+class InferenceServer:
+    def __init__(self, device='cuda', max_wait_ms: float = 2.0, amp_dtype: Optional[torch.dtype] = torch.bfloat16):
+        self.device = torch.device(device)
+        self.max_wait = max_wait_ms / 1000.0
+        self.amp_dtype = amp_dtype if self.device.type == 'cuda' else None
+        self.models: Dict[str, torch.nn.Module] = {}
+        self.teachers: Dict[str, torch.nn.Module] = {}
+        self.model_iter: Dict[str, int] = defaultdict(int)
+        self._conns: List[Connection] = []
+        self._lock = threading.Lock()
+        self._stop = False
+        self.stats = defaultdict(float)
+
+    # ------------------------------------------------------------------ models
+    def set_model(self, player_id: str, model: torch.nn.Module, teacher: bool = False):
+        model = model.to(self.device).eval()
+        with self._lock:
+            (self.teachers if teacher else self.models)[player_id] = model
+
+    def load_state_dict(self, player_id: str, state_dict: Dict, teacher: bool = False, last_iter: int = 0):
+        """Hot model update (weights pulled from the learner) without rebuilding the module."""
+        with self._lock:
+            m = (self.teachers if teacher else self.models)[player_id]
+            own = m.state_dict()
+            with torch.no_grad():
+                for k, v in state_dict.items():
+                    if k in own and own[k].shape == v.shape:
+                        own[k].copy_(v, non_blocking=True)
+            if not teacher:
+                self.model_iter[player_id] = int(last_iter)
+
+    def add_connection(self, conn: Connection):
+        with self._lock:
+            self._conns.append(conn)
+
+    # ------------------------------------------------------------------ serving
+    def _forward(self, player_id: str, kind: str, inputs: List[Dict]) -> List[Dict]:
+        batch = _to(collate_obs(inputs), self.device)
+        with self._lock:
+            model = self.models[player_id] if kind == 'policy' else self.teachers[player_id]
+        ctx = torch.autocast('cuda', dtype=self.amp_dtype) if self.amp_dtype else _null()
+        with torch.no_grad(), ctx:
+            out = model.compute_logp_action(**batch) if kind == 'policy' else model.compute_teacher_logit(**batch)
+        out = _to_cpu(out)
+        res = [decollate_output(out, i) for i in range(len(inputs))]
+        if kind == 'policy':
+            for r in res:
+                r['model_last_iter'] = self.model_iter[player_id]
+        return res
+
+    def serve_once(self, timeout: float = 0.1) -> int:
+        """Collect one dynamic batch and answer it; returns the number of requests served."""
+        with self._lock:
+            conns = list(self._conns)
+        if not conns:
+            time.sleep(timeout)
+            return 0
+        ready = wait(conns, timeout=timeout)
+        if not ready:
+            return 0
+        pending: Dict[Connection, Dict] = {}
+        deadline = time.time() + self.max_wait
+        while True:
+            for c in ready:
+                if c in pending:
+                    continue
+                try:
+                    pending[c] = serialize.loads(c.recv_bytes())
+                except (EOFError, OSError):
+                    with self._lock:
+                        if c in self._conns:
+                            self._conns.remove(c)
+            live = len(self._conns)
+            left = deadline - time.time()
+            if len(pending) >= live or left <= 0:
+                break
+            ready = [c for c in wait([c for c in conns if c not in pending and c in self._conns], timeout=left)]
+            if not ready:
+                break
+        groups = defaultdict(list)
+        for c, req in pending.items():
+            groups[(req['player_id'], req['kind'])].append((c, req['input']))
+        t0 = time.time()
+        for (pid, kind), items in groups.items():
+            outs = self._forward(pid, kind, [x for _, x in items])
+            for (c, _), o in zip(items, outs):
+                try:
+                    c.send_bytes(serialize.dumps(o))
+                except (BrokenPipeError, OSError):
+                    pass
+        self.stats['batches'] += len(groups)
+        self.stats['requests'] += len(pending)
+        self.stats['forward_s'] += time.time() - t0
+        return len(pending)
+
+    def serve_forever(self, stop_event: Optional[threading.Event] = None):
+        while not self._stop and not (stop_event is not None and stop_event.is_set()):
+            self.serve_once()
+
+    def stop(self):
+        self._stop = True
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def _to_cpu(tree):
+    if isinstance(tree, torch.Tensor):
+        return tree.detach().to('cpu', non_blocking=False)
+    if isinstance(tree, dict):
+        return {k: _to_cpu(v) for k, v in tree.items()}
+    if isinstance(tree, (list, tuple)):
+        return type(tree)(_to_cpu(v) for v in tree)
+    return tree

@@ -279,6 +279,7 @@ class Agent:
                               self._game_step)
         if self._client is not None:
             out = self._client.infer(self._model_input(agent_obs))
+            self._model_last_iter = int(out.pop('model_last_iter', self._model_last_iter))
         else:
             batch = collate_obs([self._model_input(agent_obs)])
             if self._use_cuda:

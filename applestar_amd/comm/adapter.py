@@ -1,0 +1,281 @@
+"""Data plane: coordinator (metadata broker) + adapter (producer-side payload server, consumer pull).
+
+Same topology as ``distar/ctools/worker/coordinator/{coordinator,adapter}.py``: producers keep the
+serialized payload locally and publish only ``{token, ip, port, key}`` to the coordinator; consumers
+pop metadata (LIFO, newest first, bounded deques) and fetch the bytes directly from the producer, so
+the coordinator never touches trajectory/model bytes.
+
+Differences (by design):
+* one persistent listening socket per adapter (the reference binds a fresh port per payload);
+* payloads use :mod:`applestar_amd.utils.serialize` (safe, 64 B-aligned raw tensor frames; no
+  pickle), so the learner can ``frombuffer`` the bytes straight into pinned memory;
+* "broadcast" tokens (model weights) are *peeked*, not popped: every actor reads the newest model
+  and the producer replaces it in place (the reference's ``maxlen 1`` model deque + re-push).
+"""
+from __future__ import annotations
+
+import http.client
+import json
+import socket
+import struct
+import threading
+import time
+import uuid
+from collections import defaultdict, deque
+from functools import partial
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Any, Dict, List, Optional
+
+from ..utils import serialize
+
+_LEN = struct.Struct('<Q')
+
+
+# ----------------------------------------------------------------------------- coordinator
+class Coordinator:
+    def __init__(self, maxlen: int = 1000):
+        self._lock = threading.Lock()
+        self._meta: Dict[str, deque] = defaultdict(partial(deque, maxlen=maxlen))
+        self._broadcast: Dict[str, dict] = {}
+        self.push_count = defaultdict(int)
+        self.pull_count = defaultdict(int)
+
+    def push(self, info: dict) -> bool:
+        token = info['token']
+        with self._lock:
+            if info.get('broadcast'):
+                self._broadcast[token] = info
+            else:
+                self._meta[token].append(info)
+            self.push_count[token] += 1
+        return True
+
+    def pull(self, token: str, size: int = 1) -> List[dict]:
+        with self._lock:
+            if token in self._broadcast:
+                return [self._broadcast[token]]
+            q = self._meta.get(token)
+            out = []
+            while q and len(out) < size:
+                out.append(q.pop())
+            self.pull_count[token] += len(out)
+            return out
+
+    def stats(self) -> dict:
+        with self._lock:
+            return {'queued': {k: len(v) for k, v in self._meta.items()},
+                    'broadcast': sorted(self._broadcast), 'push': dict(self.push_count),
+                    'pull': dict(self.pull_count)}
+
+
+def serve_coordinator(coord: Coordinator, host: str = '0.0.0.0', port: int = 0) -> ThreadingHTTPServer:
+    class Handler(BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def _reply(self, obj):
+            body = json.dumps({'code': 0, 'info': obj}).encode()
+            self.send_response(200)
+            self.send_header('Content-Type', 'application/json')
+            self.send_header('Content-Length', str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def do_POST(self):
+            n = int(self.headers.get('Content-Length', 0))
+            req = json.loads(self.rfile.read(n) or b'{}')
+            if self.path == '/coordinator/push':
+                self._reply(coord.push(req))
+            elif self.path == '/coordinator/pull':
+                self._reply(coord.pull(req['token'], int(req.get('size', 1))))
+            else:
+                self.send_error(404)
+
+        def do_GET(self):
+            if self.path == '/coordinator/stats':
+                self._reply(coord.stats())
+            else:
+                self.send_error(404)
+
+    srv = ThreadingHTTPServer((host, port), Handler)
+    srv.daemon_threads = True
+    threading.Thread(target=srv.serve_forever, daemon=True, name='coordinator').start()
+    return srv
+
+
+def _post_json(ip: str, port: int, path: str, obj: dict, timeout: float = 30.0):
+    conn = http.client.HTTPConnection(ip, port, timeout=timeout)
+    try:
+        body = json.dumps(obj)
+        conn.request('POST', path, body=body, headers={'Content-Type': 'application/json'})
+        r = conn.getresponse()
+        data = json.loads(r.read())
+        if data.get('code', 0) != 0:
+            raise RuntimeError(data)
+        return data['info']
+    finally:
+        conn.close()
+
+
+# ----------------------------------------------------------------------------- payload server
+def _recv_exact(sock: socket.socket, n: int) -> bytearray:
+    buf = bytearray(n)
+    view = memoryview(buf)
+    got = 0
+    while got < n:
+        k = sock.recv_into(view[got:], n - got)
+        if k == 0:
+            raise ConnectionError('peer closed')
+        got += k
+    return buf
+
+
+class _PayloadServer:
+    def __init__(self, host: str, max_items: int = 4096):
+        self._items: Dict[str, bytes] = {}
+        self._keep = set()
+        self._order = deque()
+        self._max = max_items
+        self._lock = threading.Lock()
+        self._sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        self._sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self._sock.bind((host, 0))
+        self._sock.listen(64)
+        self.port = self._sock.getsockname()[1]
+        self._closed = False
+        threading.Thread(target=self._accept_loop, daemon=True, name='payload-server').start()
+
+    def put(self, key: str, data: bytes, keep: bool = False) -> None:
+        with self._lock:
+            self._items[key] = data
+            if keep:
+                self._keep.add(key)
+            else:
+                self._order.append(key)
+                while len(self._order) > self._max:  # bounded: drop the oldest unread payload
+                    self._items.pop(self._order.popleft(), None)
+
+    def drop(self, key: str) -> None:
+        with self._lock:
+            self._items.pop(key, None)
+            self._keep.discard(key)
+
+    def _accept_loop(self):
+        while not self._closed:
+            try:
+                conn, _ = self._sock.accept()
+            except OSError:
+                return
+            threading.Thread(target=self._serve, args=(conn,), daemon=True).start()
+
+    def _serve(self, conn: socket.socket):
+        with conn:
+            conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+            try:
+                while True:
+                    (klen,) = _LEN.unpack(_recv_exact(conn, 8))
+                    key = bytes(_recv_exact(conn, klen)).decode()
+                    with self._lock:
+                        data = self._items.get(key) if key in self._keep else self._items.pop(key, None)
+                    if data is None:
+                        conn.sendall(_LEN.pack(0))
+                    else:
+                        conn.sendall(_LEN.pack(len(data)))
+                        conn.sendall(data)
+            except (ConnectionError, OSError, struct.error):
+                return
+
+    def close(self):
+        self._closed = True
+        try:
+            self._sock.close()
+        except OSError:
+            pass
+
+
+def fetch(ip: str, port: int, key: str, timeout: float = 60.0) -> Optional[bytearray]:
+    with socket.create_connection((ip, port), timeout=timeout) as s:
+        s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        k = key.encode()
+        s.sendall(_LEN.pack(len(k)) + k)
+        (n,) = _LEN.unpack(_recv_exact(s, 8))
+        return _recv_exact(s, n) if n else None
+
+
+# ----------------------------------------------------------------------------- adapter
+class Adapter:
+    """``push(obj, token)`` / ``pull(token, size)`` against a coordinator."""
+
+    def __init__(self, coordinator_ip: str = '127.0.0.1', coordinator_port: int = 0, host_ip: Optional[str] = None,
+                 compress: bool = False):
+        self._cip, self._cport = coordinator_ip, int(coordinator_port)
+        self._ip = host_ip or self._local_ip()
+        self._compress = compress
+        self._server: Optional[_PayloadServer] = None
+        self._broadcast_keys: Dict[str, str] = {}
+
+    def _local_ip(self) -> str:
+        if self._cip in ('127.0.0.1', 'localhost'):
+            return '127.0.0.1'
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        try:
+            s.connect((self._cip, self._cport or 80))
+            return s.getsockname()[0]
+        finally:
+            s.close()
+
+    def push(self, data: Any, token: str, broadcast: bool = False, retries: int = 20) -> str:
+        if self._server is None:
+            self._server = _PayloadServer('0.0.0.0' if self._ip != '127.0.0.1' else '127.0.0.1')
+        payload = data if isinstance(data, (bytes, bytearray)) else serialize.dumps(data, compress=self._compress)
+        key = f'{token}/{uuid.uuid4().hex}'
+        self._server.put(key, bytes(payload), keep=broadcast)
+        meta = {'token': token, 'ip': self._ip, 'port': self._server.port, 'key': key, 'size': len(payload),
+                'broadcast': broadcast, 'time': time.time()}
+        for i in range(retries + 1):
+            try:
+                _post_json(self._cip, self._cport, '/coordinator/push', meta)
+                break
+            except (ConnectionError, OSError):
+                if i == retries:
+                    raise
+                time.sleep(min(2 ** i * 0.1, 5.0))
+        if broadcast:
+            old = self._broadcast_keys.get(token)
+            self._broadcast_keys[token] = key
+            if old is not None:
+                # keep the previous version briefly for readers that already hold its metadata
+                threading.Timer(30.0, self._server.drop, args=(old,)).start()
+        return key
+
+    def pull(self, token: str, size: int = 1, block: bool = True, sleep_time: float = 0.05,
+             timeout: Optional[float] = None, raw: bool = False) -> List[Any]:
+        out: List[Any] = []
+        t0 = time.time()
+        while len(out) < size:
+            metas = _post_json(self._cip, self._cport, '/coordinator/pull', {'token': token, 'size': size - len(out)})
+            for m in metas:
+                try:
+                    data = fetch(m['ip'], m['port'], m['key'])
+                except OSError:
+                    data = None
+                if data is not None:
+                    out.append(data if raw else serialize.loads(data))
+                if m.get('broadcast'):
+                    return out
+            if len(out) >= size or not block or (timeout is not None and time.time() - t0 > timeout):
+                break
+            time.sleep(sleep_time)
+        return out
+
+    def stats(self) -> dict:
+        conn = http.client.HTTPConnection(self._cip, self._cport, timeout=10)
+        try:
+            conn.request('GET', '/coordinator/stats')
+            return json.loads(conn.getresponse().read())['info']
+        finally:
+            conn.close()
+
+    def close(self):
+        if self._server is not None:
+            self._server.close()

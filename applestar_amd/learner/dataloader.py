@@ -1,0 +1,131 @@
+"""Learner data pipelines.
+
+``RLDataLoader`` (``rl_dataloader.py:79-245``): background threads pull trajectories for
+``<player>traj`` from the data plane into a replay buffer of ``buffer_size`` trajectories; each batch
+takes ``batch_size`` of them; the remainder is shuffled and topped up with new data that is inserted
+twice (``new + old + new``), so each trajectory is reused ~2x exactly like the reference.  Collation
+(:func:`collate_trajectories`) happens on the pulling thread, the batch is pinned, and the H2D copy
+runs on a side HIP stream one batch ahead of compute (:class:`DevicePrefetcher`).
+
+``SyntheticRLDataLoader`` / ``FakeSLDataLoader``: synthetic batches with the exact learner layout
+(``sl_dataloader.py:167-189`` FakeDataloader) for benchmarks and tests.
+"""
+from __future__ import annotations
+
+import queue
+import random
+import threading
+from typing import Iterator, List, Optional
+
+import torch
+
+from ..agent.collate import collate_trajectories
+from ..runtime.prefetch import DevicePrefetcher, pin_tree
+
+
+class RLDataLoader:
+    def __init__(self, adapter, player_id: str, batch_size: int, buffer_size: Optional[int] = None,
+                 device='cpu', queue_size: int = 2, pull_timeout: Optional[float] = None, seed: int = 0):
+        self._adapter = adapter
+        self._token = player_id + 'traj'
+        self.batch_size = int(batch_size)
+        self.buffer_size = max(int(buffer_size or batch_size), self.batch_size)
+        self._q: queue.Queue = queue.Queue(maxsize=queue_size)
+        self._stop = threading.Event()
+        self._rng = random.Random(seed)
+        self._timeout = pull_timeout
+        self.device = torch.device(device)
+        self._thread = threading.Thread(target=self._loop, daemon=True, name='rl-dataloader')
+        self._thread.start()
+        self._iter = DevicePrefetcher(self._host_batches(), self.device) if self.device.type == 'cuda' else \
+            self._host_batches()
+
+    def _pull(self, n: int) -> List:
+        out: List = []
+        while len(out) < n and not self._stop.is_set():
+            try:
+                out += self._adapter.pull(self._token, size=n - len(out), block=True, sleep_time=0.1, timeout=1.0)
+            except (ConnectionError, OSError):  # coordinator restarting / shutting down: retry until stopped
+                self._stop.wait(1.0)
+        return out
+
+    def _loop(self):
+        torch.set_num_threads(1)
+        data = self._pull(self.buffer_size)
+        data = data + data[:self.batch_size // 2 + 1]
+        while not self._stop.is_set():
+            batch = collate_trajectories(data[:self.batch_size])
+            if self.device.type == 'cuda':
+                batch = pin_tree(batch)
+            while not self._stop.is_set():
+                try:
+                    self._q.put(batch, timeout=0.5)
+                    break
+                except queue.Full:
+                    continue
+            data = data[self.batch_size:]
+            self._rng.shuffle(data)
+            left = self.buffer_size - len(data)
+            if left > 0:
+                new = self._pull(left)
+                data = new + data + new
+
+    def _host_batches(self) -> Iterator:
+        while True:
+            yield self._q.get()
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        return next(self._iter)
+
+    def close(self):
+        self._stop.set()
+
+
+class SyntheticRLDataLoader:
+    """Endless synthetic RL batches (fixed seed set, cycled) moved to ``device``."""
+
+    def __init__(self, batch_size: int, unroll_len: int, device='cpu', use_value_feature: bool = True,
+                 n_distinct: int = 2, max_entities: int = 512):
+        from ..rl.synthetic import rl_batch
+        self._batches = [pin_tree(rl_batch(batch_size, unroll_len, max_entities=max_entities, seed=s,
+                                           use_value_feature=use_value_feature))
+                         if torch.device(device).type == 'cuda' else
+                         rl_batch(batch_size, unroll_len, max_entities=max_entities, seed=s,
+                                  use_value_feature=use_value_feature) for s in range(n_distinct)]
+        self.device = torch.device(device)
+
+        def gen():
+            i = 0
+            while True:
+                yield self._batches[i % len(self._batches)]
+                i += 1
+        self._iter = DevicePrefetcher(gen(), self.device) if self.device.type == 'cuda' else gen()
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        return next(self._iter)
+
+
+class FakeSLDataLoader:
+    """Synthetic supervised batches (``FakeDataloader``), batch-major [B*T]."""
+
+    def __init__(self, batch_size: int, traj_len: int, device='cpu', n_distinct: int = 2, max_entities: int = 512):
+        from ..rl.synthetic import sl_batch, to_device
+        self._batches = [sl_batch(batch_size, traj_len, max_entities=max_entities, seed=s)
+                         for s in range(n_distinct)]
+        self.device = torch.device(device)
+        self._to = to_device
+        self._i = 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        b = self._batches[self._i % len(self._batches)]
+        self._i += 1
+        return self._to(b, self.device) if self.device.type != 'cpu' else b

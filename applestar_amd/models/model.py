@@ -47,6 +47,7 @@ class ValueBaseline(nn.Module):
 
     def __init__(self, input_dim: int, res_dim: int = 256, res_num: int = 16, atan: bool = False):
         super().__init__()
+        self.input_dim, self.res_dim, self.res_num = input_dim, res_dim, res_num
         self.project = FCBlock(input_dim, res_dim, act=True)
         self.res = nn.Sequential(*[ResFCBlock2(res_dim) for _ in range(res_num)])
         self.value_fc = FCBlock(res_dim, 1, init='xavier_uniform', gain=0.1)

@@ -108,8 +108,11 @@ def allreduce_scalars(values: Dict[str, torch.Tensor], average: bool = True) -> 
     if not values:
         return {}
     keys = sorted(values)
-    dev = torch.device('cuda', torch.cuda.current_device()) if (
-        is_initialized() and dist.get_backend() == 'nccl') else next(iter(values.values())).device
+    first = next(iter(values.values()))
+    if is_initialized() and dist.get_backend() == 'nccl':
+        dev = torch.device('cuda', torch.cuda.current_device())
+    else:
+        dev = first.device if torch.is_tensor(first) else torch.device('cpu')
     vec = torch.stack([torch.as_tensor(values[k], dtype=torch.float32, device=dev).reshape(()) for k in keys])
     if get_world_size() > 1:
         dist.all_reduce(vec)

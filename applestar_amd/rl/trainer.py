@@ -55,14 +55,19 @@ class RLTrainer:
         self.params = [p for p in self.model.parameters() if p.requires_grad]
         comm = getattr(torch, lc.comm_dtype) if lc.get('comm_dtype') else None
         self.reducer = GradientReducer(self.params, bucket_mb=lc.bucket_mb, comm_dtype=comm)
-        fused = self.device.type == 'cuda'
-        self.optimizer = torch.optim.Adam(self.params, lr=lc.learning_rate, betas=(0.0, 0.99), eps=1e-5,
-                                          weight_decay=lc.weight_decay, fused=fused)
+        self.reset_optimizer()
         self.grad_clip = build_grad_clip(lc.grad_clip)
         self.loss = ReinforcementLoss(lc, lc.player_id)
         self.iter = 0
         self.remain_value_pretrain = int(lc.get('value_pretrain_iters', -1))
         self.amp_dtype = lc.get('amp_dtype')
+
+    def reset_optimizer(self):
+        """Fresh Adam(betas=(0, 0.99), eps=1e-5) state (also used after a league reset)."""
+        lc = self.cfg.learner
+        self.optimizer = torch.optim.Adam(self.params, lr=lc.learning_rate, betas=(0.0, 0.99), eps=1e-5,
+                                          weight_decay=lc.weight_decay, fused=self.device.type == 'cuda')
+        self.lr_scheduler = None
 
     def _value_pretrain_toggle(self):
         active = self.remain_value_pretrain > 0

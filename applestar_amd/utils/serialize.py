@@ -59,10 +59,12 @@ def dumps(tree: Any, compress: bool = False) -> bytes:
     offset = [0]
     header = json.dumps(_encode(tree, blobs, offset)).encode()
     body = bytearray(offset[0])
+    dst = np.frombuffer(body, dtype=np.uint8)
     for off, t in blobs:
         if t.numel():
-            raw = t.view(torch.uint8).reshape(-1) if t.dtype != torch.bool else t.to(torch.uint8).reshape(-1)
-            body[off:off + raw.numel()] = raw.numpy().tobytes()
+            flat = t.reshape(-1)
+            raw = flat.view(torch.uint8) if t.dtype != torch.bool else flat.to(torch.uint8)
+            dst[off:off + raw.numel()] = raw.numpy()
     pre = MAGIC + struct.pack('<QB', len(header), 1 if compress else 0)
     pad = (-(len(pre) + len(header))) % _ALIGN
     frame = bytes(pre) + header + b'\0' * pad

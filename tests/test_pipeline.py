@@ -1,0 +1,80 @@
+"""Full RL pipeline on CPU: league HTTP + coordinator + actor (train job, spawned env workers with
+batched inference) -> trajectories over the data plane -> RL learner iterations -> model broadcast
+back to the actor -> results reach the league."""
+import socket
+import threading
+import time
+
+import pytest
+import torch
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(600)
+def test_rl_pipeline_end_to_end(tmp_path, monkeypatch):
+    pytest.importorskip('flask')
+    monkeypatch.chdir(tmp_path)
+    from werkzeug.serving import make_server
+    from applestar_amd.comm.adapter import Coordinator, serve_coordinator
+    from applestar_amd.league.league import League
+    from applestar_amd.league.api import create_league_app
+    from applestar_amd.actor.actor import Actor
+    from applestar_amd.learner.rl_learner import RLLearner
+
+    coord = serve_coordinator(Coordinator(), '127.0.0.1', 0)
+    cport = coord.server_address[1]
+    league = League({'league': {'active_players': {'checkpoint_path': ['none'], 'player_id': ['MP0'],
+                                                   'pipeline': ['default'], 'frac_id': [1], 'z_prob': [0.0],
+                                                   'teacher_id': ['none'], 'teacher_path': ['none'],
+                                                   'z_path': ['3map.json'], 'one_phase_step': [1e9],
+                                                   'chosen_weight': [1]},
+                                'vs_bot': True, 'bot_probs': [0, 0, 0, 0, 0, 0, 0, 1.0, 0, 0, 0]}},
+                    root=str(tmp_path))
+    lport = _free_port()
+    srv = make_server('127.0.0.1', lport, create_league_app(league), threaded=True)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    comm = {'coordinator_ip': '127.0.0.1', 'coordinator_port': cport, 'league_ip': '127.0.0.1',
+            'league_port': lport, 'learner_send_model_freq': 1, 'learner_send_train_info_freq': 2,
+            'actor_ask_for_job_interval': 40, 'actor_model_update_interval': 1}
+    T = 3
+    learner_holder = {}
+
+    def run_learner():
+        lrn = RLLearner({'common': {'experiment_name': 'e2e'},
+                         'learner': {'use_cuda': False, 'player_id': 'MP0', 'use_value_feature': False,
+                                     'data': {'batch_size': 2, 'trajectory_length': T, 'buffer_size': 2},
+                                     'hook': {'log_show': {'name': 'log_show', 'type': 'log_show', 'priority': 20,
+                                                           'position': 'after_iter', 'ext_args': {'freq': 1}}},
+                                     'log_to_stdout': False},
+                         'communication': comm})
+        learner_holder['l'] = lrn
+        lrn.run(max_iterations=3)
+    t = threading.Thread(target=run_learner, daemon=True)
+    t.start()
+    actor = Actor({'common': {'experiment_name': 'e2e'},
+                   'actor': {'job_type': 'train', 'env_num': 2, 'gpu_batch_inference': True, 'traj_len': T,
+                             'episode_num': 1},
+                   'env': {'game_steps_per_episode': 700, 'fake': True},
+                   'communication': comm})
+    results = actor.run(max_jobs=1)
+    t.join(timeout=300)
+    lrn = learner_holder.get('l')
+    assert lrn is not None and lrn.last_iter.val == 3
+    assert results and all(r['0']['player_id'] == 'MP0' for r in results)
+    league.drain_results()
+    assert sum(league.active_players['MP0'].payoff.games(o) for o in
+               league.active_players['MP0'].payoff.record) == len(results)
+    from applestar_amd.comm.adapter import Adapter
+    st = Adapter('127.0.0.1', cport).stats()
+    assert 'MP0model' in st['broadcast'] and st['pull'].get('MP0traj', 0) >= 2
+    actor.close()
+    lrn.close()
+    srv.shutdown()
+    coord.shutdown()
