@@ -23,6 +23,7 @@ from .map_info import get_map_size
 from ..agent.features import transform_action, MINIMAP_LAYERS
 from ..lib.game_data import UNIT_TYPES, UNIT_SPECIFIC_ABILITIES, ABILITY_TO_QUEUE_ACTION, BUFFS, ACTIONS
 
+RANDOM_MAPS = ['KairosJunction', 'KingsCove', 'NewRepugnancy']  # env.py:64
 POSSIBLE_RESULTS = {R.RESULT_VICTORY: 1, R.RESULT_DEFEAT: -1, R.RESULT_TIE: 0, R.RESULT_UNDECIDED: 0}
 BASES = {'zerg': 86, 'terran': 18, 'protoss': 59}
 WORKERS = {'zerg': 104, 'terran': 45, 'protoss': 84}
@@ -105,7 +106,8 @@ class FakeSC2Env:
         self._cfg = env
         self._player_ids = list(env.get('player_ids', ['agent1', 'bot7']))
         self._races = list(env.get('races', ['zerg', 'zerg']))
-        self._map_name = env.get('map_name', 'KairosJunction').split('_')[0]
+        self._ori_map_name = env.get('map_name', 'KairosJunction').split('_')[0]
+        self._map_name = self._ori_map_name
         self._episode_length = int(env.get('game_steps_per_episode', 100000))
         self._realtime = bool(env.get('realtime', False))
         self._random_delay_weights = env.get('random_delay_weights', [0, 0.7, 0.2, 0.1])
@@ -180,6 +182,8 @@ class FakeSC2Env:
         if players is not None:
             self._player_ids = list(players)
         self._episode_count += 1
+        if self._ori_map_name == 'random':
+            self._map_name = random.choice(RANDOM_MAPS)
         self._map_xy = get_map_size(self._map_name)
         mx, my = self._map_xy
         locs = [(mx * 0.2, my * 0.8), (mx * 0.8, my * 0.2)]

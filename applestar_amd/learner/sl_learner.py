@@ -15,7 +15,7 @@ DEFAULT_SL_LEARNER_CONFIG = {
     'learner': {'learning_rate': 1e-3, 'weight_decay': 1e-5, 'ignore_steps': 6,
                 'grad_clip': {'type': 'momentum_norm', 'threshold': 1.0},
                 'data': {'batch_size': 6, 'trajectory_length': 64, 'fake_data': True, 'num_workers': 1,
-                         'replay_dir': ''}},
+                         'train_data_file': ''}},
 }
 
 
@@ -30,7 +30,7 @@ class SLLearner(BaseLearner):
 
     def _setup_dataloader(self):
         d = self.cfg.learner.data
-        if d.get('fake_data', True) or not d.get('replay_dir'):
+        if d.get('fake_data', False) or not d.get('train_data_file'):
             return FakeSLDataLoader(d.batch_size, d.trajectory_length, self.device)
         from .replay_dataloader import ReplayDataLoader
         return ReplayDataLoader(self.cfg, self.device, rank=self.rank, world_size=self.world_size)

@@ -178,12 +178,14 @@ def test_spatial_embed_matches_reference_planes(autocast):
         out = N.spatial_embed(sp, rows, ent['x'], ent['y'], en, w[:, :24], b)
     smap = scatter_connection(pr, ent['x'], ent['y'], 152, 160)
     planes = SpatialEncoder.input_planes(sp, smap)
-    ref = torch.relu(torch.nn.functional.conv2d(planes, wr[:, :, None, None], br))
+    pre = torch.nn.functional.conv2d(planes, wr[:, :, None, None], br)
+    ref = torch.relu(pre)
     tol = 5e-2 if autocast else 1e-4
     assert _err(out, ref) < tol * max(1, ref.abs().max().item())
     g = torch.randn_like(ref)
     out.backward(g.to(out.dtype))
-    ref.backward(g)
+    # gradients through the ReLU mask the kernel actually applied (bf16 flips values near 0)
+    (pre * (out.detach().float() > 0)).backward(g)
     # padded entity rows are never scattered by the native kernel (the model masks them before the
     # projection anyway), so only the valid rows carry a gradient
     valid = (torch.arange(Nn, device=DEV)[None] < en[:, None]).unsqueeze(2)
