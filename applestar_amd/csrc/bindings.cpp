@@ -358,6 +358,53 @@ at::Tensor varlen_attn_bwd(const at::Tensor& qkv, const at::Tensor& out, const a
   return dqkv;
 }
 
+
+// ---------------------------------------------------------------- selected-units sampler
+std::vector<at::Tensor> su_sample(const at::Tensor& key, const at::Tensor& c0, const at::Tensor& u,
+                                  const at::Tensor& entity_num, const at::Tensor& su_mask, const at::Tensor& wf,
+                                  const at::Tensor& bf, const at::Tensor& wq2, const at::Tensor& bq2,
+                                  const at::Tensor& wih, const at::Tensor& whh, const at::Tensor& lni_w,
+                                  const at::Tensor& lni_b, const at::Tensor& lnh_w, const at::Tensor& lnh_b,
+                                  const at::Tensor& lnc_w, const at::Tensor& lnc_b, const at::Tensor& we1,
+                                  const at::Tensor& be1, double temperature, double eps, int64_t max_steps,
+                                  bool extra_units) {
+  for (auto* t : {&key, &c0, &u, &entity_num, &su_mask, &wf, &bf, &wq2, &bq2, &wih, &whh, &lni_w, &lni_b, &lnh_w,
+                  &lnh_b, &lnc_w, &lnc_b, &we1, &be1})
+    check_cuda(*t, "su_sample input");
+  const int64_t B = key.size(0), N1 = key.size(1);
+  TORCH_CHECK(key.dim() == 3 && key.size(2) == 32, "su_sample: key must be [B, N+1, 32]");
+  TORCH_CHECK(N1 >= 1 && N1 <= 513, "su_sample: N+1 must be in [1, 513]");
+  TORCH_CHECK(c0.scalar_type() == at::kFloat && c0.size(0) == B && c0.size(1) == 256, "su_sample: c0 [B,256] fp32");
+  TORCH_CHECK(u.scalar_type() == at::kFloat && u.size(0) == B && u.size(1) == max_steps, "su_sample: u [B,steps]");
+  TORCH_CHECK(entity_num.scalar_type() == at::kLong && entity_num.numel() == B, "su_sample: entity_num int64 [B]");
+  TORCH_CHECK(su_mask.scalar_type() == at::kByte && su_mask.numel() == B, "su_sample: su_mask uint8 [B]");
+  TORCH_CHECK(wf.scalar_type() == at::kBFloat16 && wf.size(0) == 256 && wf.size(1) == 256, "su_sample: wf bf16");
+  TORCH_CHECK(wq2.size(0) == 32 && wq2.size(1) == 256 && wih.size(0) == 128 && wih.size(1) == 32 &&
+              whh.size(0) == 128 && whh.size(1) == 32 && we1.size(0) == 256 && we1.size(1) == 32,
+              "su_sample: weight shapes");
+  for (auto* t : {&bf, &wq2, &bq2, &wih, &whh, &lni_w, &lni_b, &lnh_w, &lnh_b, &lnc_w, &lnc_b, &we1, &be1})
+    TORCH_CHECK(t->scalar_type() == at::kFloat, "su_sample: fp32 weights");
+  c10::hip::HIPGuard g(key.device().index());
+  auto f = key.options().dtype(at::kFloat);
+  auto logits = at::full({B, max_steps, N1}, -1e9, f);
+  auto results = at::zeros({B, max_steps}, key.options().dtype(at::kLong));
+  auto logp = at::zeros({B, max_steps}, f);
+  auto su_num = at::empty({B}, key.options().dtype(at::kLong));
+  auto emb = at::empty({B, 32}, f);
+  auto extra = at::zeros({B, extra_units ? N1 : 1}, f);
+  as::su_sample(key.data_ptr(), dt(key), N1 * 32, c0.data_ptr<float>(), u.data_ptr<float>(),
+                entity_num.data_ptr<int64_t>(), su_mask.data_ptr<uint8_t>(),
+                reinterpret_cast<const uint16_t*>(wf.data_ptr()), bf.data_ptr<float>(), wq2.data_ptr<float>(),
+                bq2.data_ptr<float>(), wih.data_ptr<float>(), whh.data_ptr<float>(), lni_w.data_ptr<float>(),
+                lni_b.data_ptr<float>(), lnh_w.data_ptr<float>(), lnh_b.data_ptr<float>(), lnc_w.data_ptr<float>(),
+                lnc_b.data_ptr<float>(), we1.data_ptr<float>(), be1.data_ptr<float>(),
+                static_cast<float>(1.0 / temperature), static_cast<float>(eps), static_cast<int>(B),
+                static_cast<int>(N1), static_cast<int>(max_steps), extra_units ? 1 : 0, logits.data_ptr<float>(),
+                results.data_ptr<int64_t>(), logp.data_ptr<float>(), su_num.data_ptr<int64_t>(), emb.data_ptr<float>(),
+                extra.data_ptr<float>(), stream());
+  return {logits, results, logp, su_num, emb, extra};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -378,4 +425,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spatial_dense_input", &spatial_dense_input);
   m.def("varlen_attn_fwd", &varlen_attn_fwd);
   m.def("varlen_attn_bwd", &varlen_attn_bwd);
+  m.def("su_sample", &su_sample);
 }

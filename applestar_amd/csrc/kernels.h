@@ -102,3 +102,18 @@ void varlen_attn_bwd(const void* qkv, const void* out, const void* dout, const f
                      float* delta, int S, int max_len, int H, long Ttot, float scale, hipStream_t s);
 
 }  // namespace as
+
+namespace as {
+// ---- pointer.hip -----------------------------------------------------------------------------
+// Persistent selected-units sampler: one workgroup per batch row runs every pointer step on-chip.
+// key [B, key_bstride/32, 32] (f32|bf16), c0 [B,256] = Wq1 ae0 + bq1, u [B,max_steps] uniforms,
+// wf [256,256] bf16 = Wq1 We2, bf [256] = Wq1 be2.  Outputs: logits [B,max_steps,n1_stride] (rows
+// after a row's end are left untouched), results/logp [B,max_steps], su_num [B], emb [B,32] (mean of
+// selected keys, for the final autoregressive embedding), extra [B,n1_stride] (if extra_units).
+void su_sample(const void* key, int key_dt, long key_bstride, const float* c0, const float* u, const int64_t* entity_num,
+               const uint8_t* su_mask, const uint16_t* wf, const float* bf, const float* wq2, const float* bq2,
+               const float* wih, const float* whh, const float* lni_w, const float* lni_b, const float* lnh_w,
+               const float* lnh_b, const float* lnc_w, const float* lnc_b, const float* we1, const float* be1,
+               float inv_temp, float eps, int B, int n1_stride, int max_steps, int extra_units, float* logits,
+               int64_t* results, float* logp, int64_t* su_num, float* emb, float* extra, hipStream_t s);
+}  // namespace as

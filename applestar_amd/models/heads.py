@@ -174,8 +174,42 @@ class SelectedUnitsHead(nn.Module):
         return logits, None, ae_after[:, -1], selected_units_num
 
     # ------------------------------------------------------------------ sampling (actor)
+    def _folded_query(self):
+        """(Wq1 We2 [256,256] bf16, Wq1 be2 [256]) cached per weight version (pointer.hip fold)."""
+        q1, e2 = self.query_fc1[0], self.embed_fc2[0]
+        tag = (q1.weight.data_ptr(), q1.weight._version, e2.weight.data_ptr(), e2.weight._version, e2.bias._version)
+        if getattr(self, '_fold_tag', None) != tag:
+            with torch.no_grad():
+                wq1 = q1.weight.float()
+                self._fold = ((wq1 @ e2.weight.float()).to(torch.bfloat16).contiguous(), wq1 @ e2.bias.float())
+            self._fold_tag = tag
+        return self._fold
+
+    def forward_sample_native(self, native, ae0, entity_embedding, entity_num, su_mask, temperature: float = 1.0,
+                              u: Optional[torch.Tensor] = None):
+        key, _ = self.keys(entity_embedding, entity_num)
+        B, N1, _ = key.shape
+        q1 = self.query_fc1[0]
+        c0 = F.linear(ae0.float(), q1.weight.float(), q1.bias.float())
+        if u is None:
+            u = torch.rand(B, MAX_SELECTED_UNITS_NUM, device=key.device)
+        wf, bf = self._folded_query()
+        logits, results, _, su_num, emb, extra = native.su_sample(
+            key, c0, u, entity_num, su_mask, wf, bf, self.query_fc2[0].weight, self.query_fc2[0].bias,
+            self.lstm.layers[0].cell, self.embed_fc1[0].weight, self.embed_fc1[0].bias, temperature,
+            MAX_SELECTED_UNITS_NUM, self.extra_units)
+        ae = self._ae_update(ae0, emb.to(ae0.dtype))
+        ex = torch.zeros(B, MAX_ENTITY_NUM + 1, device=key.device)
+        if self.extra_units:
+            ex[:, :N1] = extra
+        return logits, results, ae, su_num, ex
+
     def forward_sample(self, ae0, entity_embedding, entity_num, su_mask, temperature: float = 1.0,
                        u: Optional[torch.Tensor] = None):
+        native = ops._native(entity_embedding)
+        if native is not None and native.has('su_sample') and not torch.is_grad_enabled() \
+                and self.lstm.num_layers == 1:
+            return self.forward_sample_native(native, ae0, entity_embedding, entity_num, su_mask, temperature, u)
         key, mask = self.keys(entity_embedding, entity_num)
         B, N1, _ = key.shape
         dev = key.device

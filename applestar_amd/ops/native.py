@@ -21,7 +21,7 @@ def ensure_loaded():
 
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
-                'spatial_embed', 'varlen_attention'}
+                'spatial_embed', 'varlen_attention', 'su_sample'}
 
 
 def has(name: str) -> bool:
@@ -296,3 +296,19 @@ def varlen_attention(qkv, cu_seqlens, max_len: int, num_heads: int, head_dim: in
     out = _VarlenAttention.apply(qkv.to(torch.bfloat16).contiguous(), cu_seqlens.to(torch.int32).contiguous(),
                                  int(max_len), int(num_heads))
     return out if dtype == torch.bfloat16 else out.to(dtype)
+
+
+def su_sample(key, c0, u, entity_num, su_mask, wf_bf16, bf, wq2, bq2, cell, we1, be1, temperature: float,
+              max_steps: int, extra_units: bool):
+    """Persistent selected-units sampler (inference only; see csrc/kernels/pointer.hip)."""
+    C = ensure_loaded()
+    f = lambda t: t.detach().float().contiguous()
+    key = key.detach()
+    if key.dtype not in (torch.float32, torch.bfloat16):
+        key = key.float()
+    return C.su_sample(key.contiguous(), f(c0), f(u), entity_num.long().contiguous(),
+                       su_mask.to(torch.uint8).contiguous(), wf_bf16.contiguous(), f(bf), f(wq2), f(bq2),
+                       f(cell.weight_ih), f(cell.weight_hh), f(cell.layernorm_i.weight), f(cell.layernorm_i.bias),
+                       f(cell.layernorm_h.weight), f(cell.layernorm_h.bias), f(cell.layernorm_c.weight),
+                       f(cell.layernorm_c.bias), f(we1), f(be1), float(temperature), 1e-5, int(max_steps),
+                       bool(extra_units))

@@ -209,3 +209,49 @@ def test_varlen_attention_matches_reference(lens):
     ref.backward(g)
     scale = ref_in.grad.abs().max().item()
     assert _err(qkv.grad, ref_in.grad) < 3e-2 * max(1.0, scale)
+
+
+def test_su_sample_kernel_matches_teacher_forcing_and_torch_sampler():
+    """Persistent pointer-network sampler: its logits must equal the teacher-forced logits of the
+    units it picked, its picks must follow inverse-CDF sampling of those logits, and (fp32) it should
+    pick the same units as the step-by-step torch loop given the same uniforms."""
+    from applestar_amd import ops
+    from applestar_amd.models.heads import SelectedUnitsHead, sample_from_logits
+    torch.manual_seed(11)
+    head = SelectedUnitsHead(extra_units=True).to(DEV).eval()
+    B, N = 12, 70
+    ae0 = torch.randn(B, 1024, device=DEV)
+    ent = torch.randn(B, N, 256, device=DEV)
+    en = torch.tensor([70, 1, 5, 33, 64, 69, 2, 40, 10, 70, 17, 50], device=DEV)
+    su_mask = torch.tensor([1, 1, 1, 1, 0, 1, 1, 1, 1, 1, 0, 1], device=DEV).bool()
+    u = torch.rand(B, 64, device=DEV)
+    with torch.no_grad():
+        lg, res, ae, su_num, extra = head.forward_sample(ae0, ent, en, su_mask, 1.0, u=u)
+        assert lg.shape == (B, 64, N + 1) and res.shape == (B, 64)
+        assert (su_num[~su_mask] == 0).all() and (su_num[su_mask] >= 2).all()
+        for b in range(B):
+            s = int(su_num[b])
+            if s:
+                assert int(res[b, s - 1]) == int(en[b])            # ended with the end token
+                assert len(set(res[b, :s - 1].tolist())) == s - 1  # no unit twice
+                # each pick is the inverse-CDF sample of its own logits row
+                pick = sample_from_logits(lg[b, :s, :int(en[b]) + 1], u[b, :s])
+                assert torch.equal(pick, res[b, :s])
+        lt, _, ae_t, _ = head.forward_teacher(ae0, ent, en, su_num, res)
+        for b in range(B):
+            s, n1 = int(su_num[b]), int(en[b]) + 1
+            if s:
+                a, r = lg[b, :s, :n1], lt[b, :s, :n1]
+                valid = r > -1e8
+                assert torch.equal(valid, a > -1e8)
+                assert (a[valid] - r[valid]).abs().max() < 2e-2 * max(1.0, r[valid].abs().max().item())
+        rows = su_num > 0  # rows without a unit selection keep ae0 + embed(0) (not teacher-forced labels)
+        assert (ae[rows] - ae_t[rows]).abs().max() < 2e-2 * ae_t[rows].abs().max()
+        # step-by-step torch loop with the same noise
+        ops.set_native(False)
+        try:
+            lg2, res2, ae2, su2, _ = head.forward_sample(ae0, ent, en, su_mask, 1.0, u=u)
+        finally:
+            ops.set_native(True)
+        same = sum(int(torch.equal(res[b, :int(su_num[b])], res2[b, :int(su2[b])])) for b in range(B))
+        assert same >= B - 1, (same, B)
