@@ -49,7 +49,10 @@ class RLTrainer:
         self.device = torch.device(device)
         self.model = model if model is not None else Model(self.cfg, use_value_network=True)
         self.model.to(self.device)
-        if self.device.type == 'cuda':  # NHWC convolutions end to end (MIOpen igemm kernels are NHWC)
+        if self.device.type == 'cuda':
+            # conv shapes depend only on (T+1)*B, so MIOpen find-mode autotuning pays off after one step
+            torch.backends.cudnn.benchmark = bool(lc.get('conv_autotune', True))
+            # NHWC convolutions end to end (MIOpen igemm kernels are NHWC)
             self.model.to(memory_format=torch.channels_last)
         pdist.broadcast_module(self.model)
         self.params = [p for p in self.model.parameters() if p.requires_grad]

@@ -36,6 +36,8 @@ class SLTrainer:
         self.model = model if model is not None else Model(self.cfg, temperature=1.0)
         self.model.to(self.device)
         if self.device.type == 'cuda':
+            # conv shapes depend only on (T+1)*B, so MIOpen find-mode autotuning pays off after one step
+            torch.backends.cudnn.benchmark = bool(lc.get('conv_autotune', True))
             self.model.to(memory_format=torch.channels_last)
         pdist.broadcast_module(self.model)
         self.params = [p for p in self.model.parameters() if p.requires_grad]

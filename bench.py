@@ -35,6 +35,8 @@ def main():
     ap.add_argument('--n-batches', type=int, default=2, help='distinct synthetic batches cycled')
     ap.add_argument('--no-native', action='store_true', help='disable HIP kernels (torch-only baseline)')
     ap.add_argument('--profile-steps', type=int, default=0)
+    ap.add_argument('--conv-benchmark', type=int, default=-1,
+                    help='1/0: force MIOpen find-mode autotuning of convolutions on/off (-1: trainer default)')
     args = ap.parse_args()
 
     from applestar_amd.parallel import dist as pdist
@@ -50,6 +52,8 @@ def main():
     device = torch.device('cuda', torch.cuda.current_device()) if gpu else torch.device('cpu')
     if args.no_native:
         ops.set_native(False)
+    if args.conv_benchmark >= 0:
+        torch.backends.cudnn.benchmark = bool(args.conv_benchmark)
     torch.manual_seed(1234 + rank)
 
     trainer = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}},
