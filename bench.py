@@ -86,7 +86,7 @@ def main():
         info = trainer.step(next(it))
     sync()
     elapsed = time.perf_counter() - t0
-    loss = float(info['total_loss'])
+    loss = float(info['total_loss'].detach())
     t = torch.tensor([elapsed], dtype=torch.float64, device=device if gpu else 'cpu')
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
