@@ -13,6 +13,7 @@ Sources:
   distar/agent/default/lib/stat.py:73-330         unit_dict, cum_dict, action_result_dict (league stats)
   distar/pysc2/lib/units.py, upgrades.py          unit / upgrade enum names (ids -> names for logs)
   distar/envs/map_info.py:8-258                   MAPS (bnet name, path, cropped / full size)
+  distar/pysc2/run_configs/lib.py:36-…            SC2 VERSIONS (game version -> build, data hash)
 """
 import ast
 import json
@@ -52,6 +53,15 @@ def _enum_classes(path):
     return out
 
 
+def _versions(path):
+    tree = ast.parse(open(path).read())
+    out = []
+    for node in ast.walk(tree):
+        if isinstance(node, ast.Call) and getattr(node.func, 'id', None) == 'Version' and len(node.args) == 4:
+            out.append([ast.literal_eval(a) for a in node.args])
+    return out
+
+
 def main():
     acts = _assignments(os.path.join(REF, 'distar/agent/default/lib/actions.py'))
     static = _assignments(os.path.join(REF, 'distar/pysc2/lib/static_data.py'))
@@ -76,6 +86,7 @@ def main():
         'action_result_dict': _literal(stat['action_result_dict']),
         'unit_enums': _enum_classes(os.path.join(REF, 'distar/pysc2/lib/units.py')),
         'upgrade_enums': _enum_classes(os.path.join(REF, 'distar/pysc2/lib/upgrades.py'))['Upgrades'],
+        'sc2_versions': _versions(os.path.join(REF, 'distar/pysc2/run_configs/lib.py')),
         'maps': {k: list(v) for k, v in _literal(_assignments(os.path.join(REF, 'distar/envs/map_info.py'))['MAPS']).items()},
     }
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
