@@ -35,3 +35,43 @@ def test_sl_trainer_steps_cpu():
     info1 = tr.step(b)
     assert torch.isfinite(info1['total_loss'])
     assert 'gradient' in info1 and 'gradient' not in info0
+
+
+def test_replay_dataloader_slots_carry_and_pad():
+    """Slots consume consecutive chunks of one trajectory (new_episodes on the first), short tails are
+    padded with masked steps, and the batch trains."""
+    import torch
+    from applestar_amd.learner.replay_dataloader import ReplayDataLoader
+    from applestar_amd.lib.features import random_obs, random_actions, actions_mask
+    from applestar_amd.utils.config import AttrDict
+
+    def traj(L, seed):
+        g = torch.Generator().manual_seed(seed)
+        steps = []
+        for i in range(L):
+            o = random_obs(1, max_entities=12, generator=g)
+            a, su = random_actions(1, o['entity_num'], generator=g)
+            one = lambda t: t[0]
+            s = {'spatial_info': {k: one(v) for k, v in o['spatial_info'].items()},
+                 'entity_info': {k: one(v)[:int(o['entity_num'][0])] for k, v in o['entity_info'].items()},
+                 'scalar_info': {k: one(v) for k, v in o['scalar_info'].items()},
+                 'entity_num': o['entity_num'][0], 'selected_units_num': su[0],
+                 'action_info': {k: one(v)[:max(int(su[0]), 1)] if k == 'selected_units' else one(v)
+                                 for k, v in a.items()},
+                 'action_mask': {'action_type': torch.tensor(True), 'delay': torch.tensor(True),
+                                 **{k: one(v).bool() for k, v in actions_mask(a['action_type']).items()}}}
+            steps.append(s)
+        return steps
+    src = iter([traj(5, 0), traj(3, 1), traj(4, 2), traj(6, 3), traj(4, 4)])
+    cfg = AttrDict({'learner': {'data': {'batch_size': 2, 'trajectory_length': 4}}})
+    dl = ReplayDataLoader(cfg, source=src)
+    b1 = next(dl)
+    assert b1['traj_lens'] == [4, 3] and b1['new_episodes'] == [True, True]
+    assert b1['entity_info']['unit_type'].shape[0] == 8
+    assert not bool(b1['action_mask']['action_type'][7])   # padded step of slot 1
+    b2 = next(dl)
+    assert b2['traj_lens'] == [1, 4] and b2['new_episodes'] == [False, True]
+    from applestar_amd.sl.trainer import SLTrainer
+    tr = SLTrainer({'learner': {'data': {'batch_size': 2, 'trajectory_length': 4}, 'ignore_steps': 0}}, device='cpu')
+    info = tr.step(b1)
+    assert torch.isfinite(info['total_loss'])
