@@ -35,6 +35,7 @@ import torch
 
 from ..agent.agent import Agent
 from ..league.players import FRAC_ID
+from ..utils import faults
 from ..utils.config import AttrDict, deep_merge_dicts
 from ..utils.log import TextLogger, VariableRecord
 
@@ -150,6 +151,7 @@ def run_episodes(cfg, job: dict, env_id: int = 0, clients=None, send_traj=None, 
     try:
         for ep in range(n_ep):
             t_game = time.time()
+            faults.inject('env_reset')
             obs, game_info, map_name = env.reset()
             # env observation index == agent order among non-bot seats
             by_slot = {i: a for i, a in enumerate(agents)}
@@ -161,6 +163,8 @@ def run_episodes(cfg, job: dict, env_id: int = 0, clients=None, send_traj=None, 
                     cmd = ctrl.recv()
                     if cmd in ('reset', 'close'):
                         return results
+                faults.inject('actor_step')
+                faults.inject(f'actor_step@{env_id}')
                 t0 = time.time()
                 actions = {i: by_slot[i].step(o) for i, o in obs.items()}
                 t1 = time.time()
@@ -323,7 +327,14 @@ class Actor:
     def _drain(self, deadline: float) -> bool:
         """Serve inference + forward results until all workers finish or the deadline passes."""
         done = 0
+        finished = set()
         while done < len(self._processes) and time.time() < deadline:
+            # a worker that died without reporting (crash, OOM kill, injected fault) counts as finished
+            for i, p in enumerate(self._processes):
+                if i not in finished and not p.is_alive() and p.exitcode not in (0, None):
+                    finished.add(i)
+                    done += 1
+                    self._logger.error(f'env worker {i} died with exit code {p.exitcode}')
             if self._server is not None:
                 self._server.serve_once(timeout=0.01)
             else:
@@ -342,7 +353,9 @@ class Actor:
                 elif kind == 'error':
                     self._logger.error(f'env worker error: {payload}')
                 elif kind == 'done':
-                    done += 1
+                    if payload not in finished:
+                        finished.add(payload)
+                        done += 1
         return done >= len(self._processes)
 
     def run(self, max_jobs: Optional[int] = None):

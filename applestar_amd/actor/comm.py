@@ -29,12 +29,15 @@ class ActorComm:
         self._last_reset = {}
         self.update_times = deque(maxlen=100)
         self.job = None
+        from ..runtime.health import HeartbeatSender
+        self._heartbeat = HeartbeatSender(self._league, 'actor', actor_uid, float(c.get('heartbeat_interval', 10.0)))
 
     def ask_for_job(self, actor=None) -> dict:
         delay = 1.0
         while True:
             try:
-                job = self._league.post('/league/actor_ask_for_job', {'job_type': self._cfg.actor.league_job_type})
+                job = self._league.post('/league/actor_ask_for_job', {'job_type': self._cfg.actor.league_job_type,
+                                                                   'actor_id': self._uid})
                 if job:
                     self.job = job
                     return job
@@ -77,4 +80,5 @@ class ActorComm:
                 self._logger.error(f'send_result failed: {e}')
 
     def close(self):
+        self._heartbeat.stop()
         self._adapter.close()

@@ -7,6 +7,7 @@ The control plane is low-rate JSON (jobs, results, train info); the high-rate da
 from __future__ import annotations
 
 import json
+import os
 import time
 from typing import Any, Dict, Optional
 
@@ -42,6 +43,28 @@ def create_league_app(league: League):
     @app.route('/league/actor_send_result', methods=['POST'])
     def actor_send_result():
         return ok(league.actor_send_result(request.json))
+
+    @app.route('/league/heartbeat', methods=['POST'])
+    def heartbeat():
+        d = request.json or {}
+        league.health.beat(d.get('role', 'unknown'), str(d.get('id')), d.get('info'))
+        return ok(True)
+
+    @app.route('/league/health', methods=['GET'])
+    def health():
+        return ok({'members': league.health.status(), 'dead': league.health.dead()})
+
+    @app.route('/league/update_config', methods=['GET'])
+    def reload_config():
+        """Hot reload: re-read ``experiments/<exp>/user_config.yaml`` and merge its league section."""
+        from ..utils.config import read_config, deep_update
+        path = os.path.join(league.root, 'user_config.yaml')
+        if not os.path.exists(path):
+            return bad(f'{path} not found')
+        new = read_config(path)
+        with league.lock:
+            deep_update(league.cfg, new.get('league', {}))
+        return ok(True)
 
     @app.route('/league/save_resume', methods=['GET', 'POST'])
     def save_resume():

@@ -67,6 +67,8 @@ class League:
         os.makedirs(self.resume_dir, exist_ok=True)
         self.logger = TextLogger(os.path.join(self.root, 'log'), 'league', to_stdout=False)
         self.lock = threading.RLock()
+        from ..runtime.health import HeartbeatRegistry
+        self.health = HeartbeatRegistry(float(self.cfg.get('heartbeat_timeout', 120.0)))
         self.elo = ELORating()
         self.active_players: Dict[str, ActivePlayer] = {}
         self.historical_players: Dict[str, HistoricalPlayer] = {}
@@ -130,6 +132,7 @@ class League:
         pid = info['player_id']
         if pid not in self.active_players:
             raise KeyError(f'{pid} not an active player ({list(self.active_players)})')
+        self.health.beat('learner', f"{pid}/rank{info.get('rank', 0)}", info)
         self.learner_info.setdefault(pid, []).append({k: info.get(k) for k in ('ip', 'port', 'rank', 'world_size')})
         return {'ckpt_path': self.active_players[pid].checkpoint_path}
 
@@ -177,6 +180,8 @@ class League:
 
     def actor_ask_for_job(self, info: Dict) -> Dict:
         job_type = info.get('job_type', 'train')
+        if info.get('actor_id'):
+            self.health.beat('actor', info['actor_id'])
         with self.lock:
             if job_type == 'ladder':
                 branch, job = self._ladder_job()

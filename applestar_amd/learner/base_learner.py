@@ -17,6 +17,7 @@ from typing import Dict, Iterator, Optional
 import torch
 
 from ..parallel import dist as pdist
+from ..utils import faults
 from ..utils.checkpoint import CheckpointHelper, CountVar, auto_checkpoint
 from ..utils.config import AttrDict, deep_merge_dicts
 from ..utils.log import LogDict, ScalarLogger, TextLogger, VariableRecord
@@ -57,7 +58,8 @@ class BaseLearner:
         self.last_iter = CountVar(0)
         self.checkpoint_helper = CheckpointHelper()
         self.last_checkpoint_path = ''
-        self.load_path = lc.get('load_path', '')
+        # a supervisor restart passes the newest checkpoint (runtime/supervisor.py)
+        self.load_path = os.environ.get('APPLESTAR_RESUME_PATH') or lc.get('load_path', '')
         self.trainer = self._setup_trainer()
         self.dataloader: Optional[Iterator] = self._setup_dataloader()
         self.hooks = build_learner_hooks(lc.hook)
@@ -114,9 +116,9 @@ class BaseLearner:
 
     @auto_checkpoint('save_checkpoint')
     def run(self, max_iterations: Optional[int] = None):
-        n = self._max_iterations if max_iterations is None else int(max_iterations)
         self.call_hooks('before_run')
-        end = self.last_iter.val + n
+        # config max_iterations is the run's total (resumes continue to it); an explicit argument is relative
+        end = self._max_iterations if max_iterations is None else self.last_iter.val + int(max_iterations)
         while self.last_iter.val < end:
             t0 = time.time()
             data = self._next_data()
@@ -128,6 +130,7 @@ class BaseLearner:
             self.log_buffer['data_time'] = t1 - t0
             self.log_buffer['train_time'] = time.time() - t1
             self.call_hooks('after_iter')
+            faults.inject('learner_iter')
         self.call_hooks('after_run')
 
     def _log_info(self, info: Dict):

@@ -61,6 +61,12 @@ class LearnerComm:
         self._event = None
         if self._adapter is not None:
             threading.Thread(target=self._publish_loop, daemon=True, name='model-publisher').start()
+        self._heartbeat = None
+        if self._league is not None:
+            from ..runtime.health import HeartbeatSender
+            self._heartbeat = HeartbeatSender(self._league, 'learner', f'{self.player_id}/rank{learner.rank}',
+                                              float(c.get('heartbeat_interval', 10.0)),
+                                              info_fn=lambda: {'iter': learner.last_iter.val})
 
     def register(self, learner) -> None:
         if self._league is None:
@@ -133,6 +139,8 @@ class LearnerComm:
 
     def close(self):
         self._stop = True
+        if self._heartbeat is not None:
+            self._heartbeat.stop()
         if self._adapter is not None:
             self._adapter.close()
 

@@ -31,6 +31,7 @@ class SLLearner(BaseLearner):
     def _setup_dataloader(self):
         d = self.cfg.learner.data
         if d.get('fake_data', False) or not d.get('train_data_file'):
-            return FakeSLDataLoader(d.batch_size, d.trajectory_length, self.device)
+            return FakeSLDataLoader(d.batch_size, d.trajectory_length, self.device,
+                                    max_entities=int(d.get('fake_max_entities', 512)))
         from .replay_dataloader import ReplayDataLoader
         return ReplayDataLoader(self.cfg, self.device, rank=self.rank, world_size=self.world_size)

@@ -47,6 +47,8 @@ def init(backend: Optional[str] = None, init_method: Optional[str] = None, rank:
     if world_size <= 1 and init_method is None:
         return 0, 1
     rank = int(os.environ.get('RANK', '0')) if rank is None else rank
+    # surface a dead / hung peer as an error after `timeout_s` instead of a silent hang (RCCL honours it)
+    os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '1')
     use_gpu = torch.cuda.is_available()
     if backend is None:
         backend = 'nccl' if use_gpu else 'gloo'

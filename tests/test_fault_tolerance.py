@@ -1,0 +1,81 @@
+"""Failure detection and recovery: heartbeats, supervised learner restart from the newest checkpoint
+after an injected crash, actor survival of a dying env worker."""
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_heartbeat_registry_marks_silent_members_dead():
+    from applestar_amd.runtime.health import HeartbeatRegistry
+    now = [100.0]
+    reg = HeartbeatRegistry(timeout=10, clock=lambda: now[0])
+    reg.beat('learner', 'MP0/rank0')
+    reg.beat('actor', 'a1')
+    now[0] = 105
+    reg.beat('actor', 'a1')
+    now[0] = 112
+    assert reg.dead() == ['learner/MP0/rank0']
+    assert reg.status()['actor/a1']['alive'] and reg.status()['actor/a1']['beats'] == 2
+
+
+def test_league_health_endpoint(tmp_path):
+    pytest.importorskip('flask')
+    from applestar_amd.league.league import League
+    from applestar_amd.league.api import create_league_app
+    lg = League({}, root=str(tmp_path), start_threads=False)
+    c = create_league_app(lg).test_client()
+    assert c.post('/league/heartbeat', json={'role': 'actor', 'id': 'x'}).json['code'] == 0
+    c.post('/league/register_learner', json={'player_id': 'MP0', 'rank': 0})
+    h = c.get('/league/health').json['info']
+    assert set(h['members']) == {'actor/x', 'learner/MP0/rank0'} and h['dead'] == []
+
+
+@pytest.mark.timeout(900)
+def test_supervised_learner_restarts_from_checkpoint(tmp_path):
+    from applestar_amd.runtime.supervisor import Supervisor, latest_checkpoint
+    cfg = tmp_path / 'sl.yaml'
+    cfg.write_text("""
+common: {experiment_name: ft}
+learner:
+  use_cuda: false
+  max_iterations: 5
+  ignore_steps: 0
+  log_to_stdout: false
+  data: {fake_data: true, batch_size: 1, trajectory_length: 2, fake_max_entities: 8}
+  hook:
+    save_ckpt_after_iter: {name: save_ckpt_after_iter, type: save_ckpt, priority: 40, position: after_iter, ext_args: {freq: 2}}
+""")
+    env = dict(os.environ, APPLESTAR_FAULT='learner_iter:3', APPLESTAR_FAULT_ONCE=str(tmp_path / 'fired'),
+               PYTHONPATH=REPO)
+    sup = Supervisor([sys.executable, '-m', 'applestar_amd.bin.sl_train', '--config', str(cfg)], max_restarts=2,
+                     backoff=0.1, env=env, resume_dir=str(tmp_path / 'experiments' / 'ft'))
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        rc = sup.run()
+    finally:
+        os.chdir(cwd)
+    assert rc == 0 and sup.exit_codes == [17, 0]
+    assert latest_checkpoint(str(tmp_path / 'experiments' / 'ft')).endswith('_iteration_5.pth.tar')
+    import torch
+    ck = torch.load(latest_checkpoint(str(tmp_path / 'experiments' / 'ft')), weights_only=True)
+    assert ck['last_iter'] == 5
+
+
+@pytest.mark.timeout(600)
+def test_actor_survives_dead_env_worker(tmp_path, monkeypatch):
+    monkeypatch.chdir(tmp_path)
+    monkeypatch.setenv('APPLESTAR_FAULT', 'actor_step@0:3')
+    from applestar_amd.actor.actor import Actor
+    actor = Actor({'actor': {'job_type': 'eval', 'env_num': 2, 'gpu_batch_inference': True, 'episode_num': 1},
+                   'env': {'game_steps_per_episode': 300, 'fake': True, 'player_ids': ['agent1', 'bot7']},
+                   'communication': {'actor_ask_for_job_interval': 120}})
+    t0 = time.time()
+    res = actor.run()
+    assert len(res) == 1 and time.time() - t0 < 200
+    actor.close()
