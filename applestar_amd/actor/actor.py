@@ -102,6 +102,15 @@ def build_agents(cfg, job: dict, clients: Optional[Dict] = None) -> List[Agent]:
             continue
         acfg = deep_merge_dicts(cfg, {'agent': {'z_path': job['z_path'][idx]}})
         tid = job['teacher_player_ids'][idx]
+        pipeline = job['pipelines'][idx]
+        if pipeline != 'default':  # plugin agent (registry name / module path)
+            from ..agent.registry import import_agent
+            agent = import_agent(pipeline)(acfg)
+            agent.player_id, agent.side_id, agent.slot = pid, job['side_ids'][idx], idx
+            agent.opponent_id = job.get('bot_id') or 'none'
+            agent._fake_reward_prob = job['z_prob'][idx]
+            agents.append(agent)
+            continue
         tkey = tid if tid != 'none' else pid  # no teacher configured: KL against the player's own policy
         if clients is not None:
             agent = Agent(acfg, inference_client=clients.get((pid, 'policy')),
@@ -173,6 +182,8 @@ def run_episodes(cfg, job: dict, env_id: int = 0, clients=None, send_traj=None, 
                 if train:
                     for i, o in nobs.items():
                         a = by_slot[i]
+                        if not hasattr(a, 'collect_data'):
+                            continue
                         if cfg.actor.job_type == 'train_test' or a.player_id in job['send_data_players']:
                             traj = a.collect_data(o, reward[i], done, i)
                             if traj is not None and send_traj is not None:
@@ -191,9 +202,11 @@ def run_episodes(cfg, job: dict, env_id: int = 0, clients=None, send_traj=None, 
                 info = {'game_steps': env._game_loop if hasattr(env, '_game_loop') else game_iters,
                         'game_iters': game_iters, 'game_duration': time.time() - t_game}
                 for i, a in by_slot.items():
-                    side = {'race': a.race, 'player_id': a.player_id, 'opponent_id': a.opponent_id,
-                            'winloss': reward[i], 'agent_iters': a.iter_count}
-                    side.update({k: v for k, v in a.get_stat_data().items()})
+                    side = {'race': getattr(a, 'race', None), 'player_id': a.player_id,
+                            'opponent_id': a.opponent_id, 'winloss': reward[i],
+                            'agent_iters': getattr(a, 'iter_count', game_iters)}
+                    if hasattr(a, 'get_stat_data'):
+                        side.update(a.get_stat_data())
                     info[str(a.side_id)] = side
                 results.append(info)
                 if send_result is not None:

@@ -162,3 +162,16 @@ def test_agent_train_trajectories_collate_and_learn():
     info = tr.step(b)
     assert all(torch.isfinite(torch.as_tensor(v)).all() for v in info.values() if torch.is_tensor(v) or
                isinstance(v, float))
+
+
+def test_agent_registry_and_template_plugin():
+    from applestar_amd.agent.registry import import_agent, register_agent
+    from applestar_amd.agent.template import Agent as T
+    from applestar_amd.actor.actor import run_episodes, _job_from_config, DEFAULT_ACTOR_CONFIG
+    from applestar_amd.utils.config import deep_merge_dicts
+    assert import_agent('default') is Agent and import_agent('template') is T
+    register_agent('noop', T)
+    cfg = deep_merge_dicts(DEFAULT_ACTOR_CONFIG, {'actor': {'agents': {'model1': 'noop'}},
+                                                  'env': {'game_steps_per_episode': 200, 'fake': True}})
+    res = run_episodes(cfg, _job_from_config(cfg))
+    assert len(res) == 1 and res[0]['0']['player_id'] == 'model1'
