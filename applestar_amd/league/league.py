@@ -66,6 +66,9 @@ class League:
         os.makedirs(self.model_dir, exist_ok=True)
         os.makedirs(self.resume_dir, exist_ok=True)
         self.logger = TextLogger(os.path.join(self.root, 'log'), 'league', to_stdout=False)
+        from ..utils.log import ScalarLogger
+        self.scalar_logger = ScalarLogger(os.path.join(self.root, 'league_scalars')) \
+            if self.cfg.get('scalar_log', True) else None
         self.lock = threading.RLock()
         from ..runtime.health import HeartbeatRegistry
         self.health = HeartbeatRegistry(float(self.cfg.get('heartbeat_timeout', 120.0)))
@@ -276,10 +279,25 @@ class League:
                     race = r.get('race_id', 'unknown')
                     p.dist_stat.update(race, {k: v for k, v in r.items() if k.startswith('dist')})
                     p.cum_stat.update(race, {k: v for k, v in r.items() if k.startswith('cum')})
+                    p.unit_num_stat.update(race, {k: v for k, v in r.items() if k.startswith('units/')})
+                    self._log_player(p, opp)
             first = info.get('0') or next(iter(info.values()))
             self.elo.update(first['player_id'], first['opponent_id'], int(first['winloss']))
             if self.elo.game_count % max(int(self.cfg.print_freq), 1) == 0:
                 self.logger.info('ELO\n' + self.elo.text())
+
+    def _log_player(self, p, opp: str) -> None:
+        """Per-player scalars (league.py:351-375): win rate / game length per opponent, Z distances,
+        cumulative-stat in/out rates, unit counts; step = games played by the player."""
+        if self.scalar_logger is None:
+            return
+        step = p.total_game_count
+        for k, v in p.payoff.stat_info_dict().get(opp, {}).items():
+            self.scalar_logger.add_scalar(f'{p.player_id}/{opp}/{k}', v, step)
+        for stat in (p.dist_stat, p.cum_stat, p.unit_num_stat):
+            for race, vals in stat.stat_info_dict().items():
+                for k, v in vals.items():
+                    self.scalar_logger.add_scalar(f'{p.player_id}/{race}/{k}', v, step)
 
     def _result_loop(self):
         while not self._stop.is_set():
