@@ -405,6 +405,18 @@ std::vector<at::Tensor> su_sample(const at::Tensor& key, const at::Tensor& c0, c
   return {logits, results, logp, su_num, emb, extra};
 }
 
+
+// ---------------------------------------------------------------- trajectory ring gather
+void segment_copy(const at::Tensor& arena, const at::Tensor& out, const at::Tensor& seg) {
+  check_cuda(arena, "arena");
+  check_cuda(out, "out");
+  check_cuda(seg, "seg");
+  TORCH_CHECK(arena.scalar_type() == at::kByte && out.scalar_type() == at::kByte, "segment_copy: uint8 buffers");
+  TORCH_CHECK(seg.scalar_type() == at::kLong && seg.dim() == 2 && seg.size(1) == 3, "segment_copy: seg [n,3] int64");
+  c10::hip::HIPGuard g(arena.device().index());
+  as::segment_copy(arena.data_ptr<uint8_t>(), out.data_ptr<uint8_t>(), seg.data_ptr<int64_t>(), seg.size(0), stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -426,4 +438,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("varlen_attn_fwd", &varlen_attn_fwd);
   m.def("varlen_attn_bwd", &varlen_attn_bwd);
   m.def("su_sample", &su_sample);
+  m.def("segment_copy", &segment_copy);
 }

@@ -117,3 +117,9 @@ void su_sample(const void* key, int key_dt, long key_bstride, const float* c0, c
                float inv_temp, float eps, int B, int n1_stride, int max_steps, int extra_units, float* logits,
                int64_t* results, float* logp, int64_t* su_num, float* emb, float* extra, hipStream_t s);
 }  // namespace as
+
+namespace as {
+// ---- gather.hip --------------------------------------------------------------------------------
+// seg [nseg, 3] int64 = (src byte offset in arena, dst byte offset in out, byte count)
+void segment_copy(const uint8_t* arena, uint8_t* out, const int64_t* seg, long nseg, hipStream_t s);
+}  // namespace as

@@ -24,31 +24,74 @@ from ..runtime.prefetch import DevicePrefetcher, pin_tree
 
 
 class RLDataLoader:
+    """Replay buffer over the data plane.  On a GPU the trajectories live in an HBM
+    :class:`TrajectoryRing` and batches are assembled on device; on CPU (tests) the host collate path
+    is used.  Both keep the reference's reuse policy (each trajectory trains ~``max_reuse`` times)."""
+
     def __init__(self, adapter, player_id: str, batch_size: int, buffer_size: Optional[int] = None,
-                 device='cpu', queue_size: int = 2, pull_timeout: Optional[float] = None, seed: int = 0):
+                 device='cpu', queue_size: int = 2, pull_timeout: Optional[float] = None, seed: int = 0,
+                 ring_bytes: int = 16 << 30, max_reuse: int = 2, device_collate: Optional[bool] = None):
         self._adapter = adapter
         self._token = player_id + 'traj'
         self.batch_size = int(batch_size)
         self.buffer_size = max(int(buffer_size or batch_size), self.batch_size)
+        self.max_reuse = int(max_reuse)
         self._q: queue.Queue = queue.Queue(maxsize=queue_size)
         self._stop = threading.Event()
         self._rng = random.Random(seed)
         self._timeout = pull_timeout
         self.device = torch.device(device)
-        self._thread = threading.Thread(target=self._loop, daemon=True, name='rl-dataloader')
-        self._thread.start()
-        self._iter = DevicePrefetcher(self._host_batches(), self.device) if self.device.type == 'cuda' else \
-            self._host_batches()
+        self.device_collate = (self.device.type == 'cuda') if device_collate is None else device_collate
+        if self.device_collate:
+            from ..runtime.traj_ring import TrajectoryRing
+            self._ring = TrajectoryRing(ring_bytes, self.device)
+            self._avail = threading.Condition()
+            self._thread = threading.Thread(target=self._ring_loop, daemon=True, name='rl-ring-ingest')
+            self._thread.start()
+            self._iter = self._ring_batches()
+        else:
+            self._thread = threading.Thread(target=self._loop, daemon=True, name='rl-dataloader')
+            self._thread.start()
+            self._iter = DevicePrefetcher(self._host_batches(), self.device) if self.device.type == 'cuda' else \
+                self._host_batches()
 
-    def _pull(self, n: int) -> List:
+    def _pull(self, n: int, raw: bool = False) -> List:
         out: List = []
         while len(out) < n and not self._stop.is_set():
             try:
-                out += self._adapter.pull(self._token, size=n - len(out), block=True, sleep_time=0.1, timeout=1.0)
+                out += self._adapter.pull(self._token, size=n - len(out), block=True, sleep_time=0.1, timeout=1.0,
+                                          raw=raw)
             except (ConnectionError, OSError):  # coordinator restarting / shutting down: retry until stopped
                 self._stop.wait(1.0)
         return out
 
+    # ---------------------------------------------------------------- HBM ring path
+    def _ring_loop(self):
+        torch.set_num_threads(1)
+        while not self._stop.is_set():
+            with self._avail:
+                while len(self._ring) >= self.buffer_size and not self._stop.is_set():
+                    self._avail.wait(0.5)
+            for frame in self._pull(1, raw=True):
+                self._ring.put(frame)
+                with self._avail:
+                    self._avail.notify_all()
+
+    def _ring_batches(self) -> Iterator:
+        while True:
+            with self._avail:
+                while len(self._ring) < self.batch_size:
+                    self._avail.wait(0.5)
+            ids = self._ring.least_used(self.batch_size)
+            batch = self._ring.batch(ids)
+            for tid in ids:
+                if self._ring._trajs.get(tid) is not None and self._ring._trajs[tid].uses >= self.max_reuse:
+                    self._ring.drop(tid)
+            with self._avail:
+                self._avail.notify_all()
+            yield batch
+
+    # ---------------------------------------------------------------- host path
     def _loop(self):
         torch.set_num_threads(1)
         data = self._pull(self.buffer_size)

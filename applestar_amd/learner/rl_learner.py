@@ -178,7 +178,9 @@ class RLLearner(BaseLearner):
             return SyntheticRLDataLoader(lc.data.batch_size, lc.data.trajectory_length, self.device,
                                          use_value_feature=lc.use_value_feature)
         return RLDataLoader(Adapter(c.coordinator_ip, c.coordinator_port), lc.player_id, lc.data.batch_size,
-                            lc.data.get('buffer_size'), self.device)
+                            lc.data.get('buffer_size'), self.device,
+                            ring_bytes=int(float(lc.data.get('ring_gb', 16)) * (1 << 30)),
+                            max_reuse=int(lc.data.get('max_reuse', 2)))
 
     def _train(self, data: Dict) -> Dict:
         mli = data.pop('model_last_iter', None)

@@ -1,0 +1,257 @@
+"""HBM-resident trajectory ring with on-device batch assembly.
+
+The reference learner unpickles every trajectory on the host, pads and stacks it with per-tensor
+Python collate and copies the batch to the GPU (``rl_dataloader.py:45-127``) — ~2 s of host work
+per 6x64 batch here, ~25x a learner step.  Instead:
+
+* ``put(frame)``: a trajectory arrives as one :mod:`utils.serialize` frame (list of T+1 step
+  dicts).  Its JSON header is parsed (no tensor decoding) into per-leaf descriptors and the raw
+  body is copied ONCE, host pinned staging -> HBM arena, on a dedicated copy stream.  The arena
+  is a ring (oldest trajectories are evicted when it wraps); 288 GB/GPU holds ~10^4 trajectories.
+* ``batch(ids)``: the padded learner batch (``collate_trajectories`` layout: observations
+  time-major (T+1)*B padded to the batch max entity count, actions/logits [T,B,...], SU / target
+  logits padded with -1e9, masks) is assembled by ONE ``segment_copy`` kernel launch that moves
+  every row of every leaf of every step from the arena into one pre-filled batch buffer; masks are
+  derived on device.  Host work is numpy arithmetic on descriptor tables.
+* reuse: trajectories stay resident, so the reference's ~2x replay reuse costs no copies.
+"""
+from __future__ import annotations
+
+import threading
+import warnings
+from collections import OrderedDict, deque
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..lib.features import MAX_SELECTED_UNITS_NUM
+from ..utils import serialize
+
+NEG = -1e9
+_ALIGN = 256
+OBS_TOP = ('spatial_info', 'entity_info', 'scalar_info', 'entity_num', 'value_feature')
+NEG_FILL = {('behaviour_logp', 'selected_units'), ('teacher_logit', 'selected_units'), ('teacher_logit', 'target_unit'),
+            ('successive_logit', 'selected_units'), ('successive_logit', 'target_unit')}
+SU_PAD = {('action_info', 'selected_units'), ('behaviour_logp', 'selected_units')}
+SU_2D = {('teacher_logit', 'selected_units'), ('successive_logit', 'selected_units')}
+ENTITY_N = {('teacher_logit', 'target_unit'), ('successive_logit', 'target_unit')}
+
+
+def _leaves(node, path=()):
+    """Yield (path, descriptor) for every tensor leaf of a header tree (hidden_state indexed by ints)."""
+    if '__t__' in node:
+        yield path, node['__t__']
+    elif '__d__' in node:
+        for k, v in node['__d__']:
+            yield from _leaves(v, path + (k,))
+    elif '__l__' in node or '__tu__' in node:
+        for i, v in enumerate(node.get('__l__', node.get('__tu__'))):
+            yield from _leaves(v, path + (i,))
+
+
+class _Traj:
+    __slots__ = ('start', 'size', 'T', 'leaves', 'entity_counts', 'event', 'uses')
+
+    def __init__(self, start, size, steps):
+        self.start, self.size = start, size
+        self.T = len(steps) - 1
+        self.leaves: Dict[tuple, List] = {}
+        for t, st in enumerate(steps):
+            for path, d in _leaves(st):
+                self.leaves.setdefault(path, [None] * len(steps))[t] = d
+        ex = self.leaves[('entity_info', 'x')]
+        self.entity_counts = np.array([d[1][0] for d in ex], dtype=np.int64)
+        self.event = None
+        self.uses = 0
+
+
+class TrajectoryRing:
+    def __init__(self, capacity_bytes: int, device='cuda', staging_buffers: int = 4):
+        self.device = torch.device(device)
+        self.capacity = int(capacity_bytes)
+        self.arena = torch.empty(self.capacity, dtype=torch.uint8, device=self.device)
+        self._head = 0
+        self._trajs: 'OrderedDict[int, _Traj]' = OrderedDict()
+        self._next_id = 0
+        self._lock = threading.Lock()
+        cuda = self.device.type == 'cuda'
+        self._stream = torch.cuda.Stream(self.device) if cuda else None
+        self._staging = deque([[None, None] for _ in range(staging_buffers)])  # [pinned tensor, event]
+        self._native = None
+        if cuda:
+            from ..ops import native
+            native.ensure_loaded()
+            self._native = native._C
+
+    # ------------------------------------------------------------------ ingest
+    def _alloc(self, size: int) -> int:
+        size = (size + _ALIGN - 1) // _ALIGN * _ALIGN
+        if size > self.capacity:
+            raise ValueError(f'trajectory of {size} B exceeds the ring ({self.capacity} B)')
+        start = self._head if self._head + size <= self.capacity else 0
+        end = start + size
+        for tid in [k for k, tr in self._trajs.items() if tr.start < end and start < tr.start + tr.size]:
+            del self._trajs[tid]  # overwritten: evict
+        self._head = end
+        return start
+
+    def put(self, frame) -> int:
+        header, body = serialize.parse(frame)
+        steps = header['__l__']
+        n = len(body)
+        with self._lock:
+            start = self._alloc(n)
+            tr = _Traj(start, (n + _ALIGN - 1) // _ALIGN * _ALIGN, steps)
+            with warnings.catch_warnings():  # read-only source: only ever copied from
+                warnings.simplefilter('ignore')
+                src = torch.frombuffer(body, dtype=torch.uint8) if n else torch.empty(0, dtype=torch.uint8)
+            if self._stream is None:
+                self.arena[start:start + n].copy_(src)
+            else:
+                slot = self._staging[0]
+                self._staging.rotate(-1)
+                if slot[1] is not None:
+                    slot[1].synchronize()  # previous async copy from this staging buffer is done
+                if slot[0] is None or slot[0].numel() < n:
+                    slot[0] = torch.empty(max(n, 1 << 20), dtype=torch.uint8, pin_memory=True)
+                slot[0][:n].copy_(src)
+                with torch.cuda.stream(self._stream):
+                    self.arena[start:start + n].copy_(slot[0][:n], non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self._stream)
+                slot[1] = ev
+                tr.event = ev
+            tid = self._next_id
+            self._next_id += 1
+            self._trajs[tid] = tr
+            return tid
+
+    def __len__(self):
+        return len(self._trajs)
+
+    def ids(self) -> List[int]:
+        return list(self._trajs)
+
+    def least_used(self, k: int) -> List[int]:
+        with self._lock:
+            order = sorted(self._trajs.items(), key=lambda kv: (kv[1].uses, kv[0]))
+            return [tid for tid, _ in order[:k]]
+
+    def drop(self, tid: int) -> None:
+        with self._lock:
+            self._trajs.pop(tid, None)
+
+    # ------------------------------------------------------------------ batch assembly
+    def batch(self, ids: Sequence[int]) -> Dict:
+        with self._lock:
+            trs = [self._trajs[i] for i in ids]
+            for tr in trs:
+                tr.uses += 1
+        B, T = len(trs), trs[0].T
+        assert all(tr.T == T for tr in trs), 'trajectories in a batch must share the unroll length'
+        N = int(max(tr.entity_counts.max() for tr in trs))
+        layout, segs = [], []
+        offset = 0
+        paths = list(trs[0].leaves)
+        for path in paths:
+            d0 = trs[0].leaves[path][0]
+            if d0 is None:
+                continue
+            dt = serialize.DTYPES[d0[0]]
+            esize = torch.empty(0, dtype=torch.uint8 if dt == torch.bool else dt).element_size()
+            is_obs = path[0] in OBS_TOP
+            is_hidden = path[0] == 'hidden_state'
+            steps = 1 if is_hidden else (T + 1 if is_obs else T)
+            if path[0] == 'entity_info':
+                row_shape = (N,)
+            elif path in SU_PAD:
+                row_shape = (MAX_SELECTED_UNITS_NUM,)
+            elif path in SU_2D:
+                row_shape = (MAX_SELECTED_UNITS_NUM, N + 1)
+            elif path in ENTITY_N:
+                row_shape = (N,)
+            else:
+                row_shape = tuple(d0[1])
+            row_bytes = int(np.prod(row_shape, dtype=np.int64)) * esize
+            offset = (offset + _ALIGN - 1) // _ALIGN * _ALIGN
+            layout.append((path, dt, (steps * B,) + row_shape, offset, steps))
+            # per (t, b) segments
+            for b, tr in enumerate(trs):
+                descs = tr.leaves[path][:steps]
+                offs = np.array([d[2] for d in descs], dtype=np.int64) + tr.start
+                nb = np.array([d[3] for d in descs], dtype=np.int64)
+                rows = np.arange(steps, dtype=np.int64) * B + b
+                dst = offset + rows * row_bytes
+                if path in SU_2D:  # [s, n+1] -> [64, N+1]: one segment per source row
+                    for t, d in enumerate(descs):
+                        s, c = (d[1][0], d[1][1]) if len(d[1]) == 2 and d[3] else (0, 0)
+                        if s == 0:
+                            continue
+                        r = np.arange(s, dtype=np.int64)
+                        segs.append(np.stack([offs[t] + r * c * esize, dst[t] + r * (N + 1) * esize,
+                                              np.full(s, c * esize, dtype=np.int64)], 1))
+                else:
+                    keep = nb > 0
+                    segs.append(np.stack([offs[keep], dst[keep], nb[keep]], 1))
+            offset += steps * B * row_bytes
+        total = max(offset, 1)
+        seg = np.concatenate(segs, 0) if segs else np.zeros((0, 3), dtype=np.int64)
+        # bounds check on the host before any device access (kernel reads arena[src:src+n])
+        if len(seg):
+            assert seg[:, 0].min() >= 0 and (seg[:, 0] + seg[:, 2]).max() <= self.capacity
+            assert seg[:, 1].min() >= 0 and (seg[:, 1] + seg[:, 2]).max() <= total
+        buf = torch.zeros(total, dtype=torch.uint8, device=self.device)
+        out = {}
+        for path, dt, shape, off, steps in layout:
+            store = torch.uint8 if dt == torch.bool else dt
+            n = int(np.prod(shape, dtype=np.int64))
+            es = torch.empty(0, dtype=store).element_size()
+            view = buf[off:off + n * es].view(store).view(shape)
+            if path in NEG_FILL:
+                view.fill_(NEG)
+            out[path] = view.view(torch.bool) if dt == torch.bool else view
+        if self._stream is not None:
+            cur = torch.cuda.current_stream(self.device)
+            for tr in trs:
+                if tr.event is not None:
+                    cur.wait_event(tr.event)
+        if len(seg):
+            seg_t = torch.from_numpy(seg)
+            if self.device.type == 'cuda':
+                seg_t = seg_t.pin_memory().to(self.device, non_blocking=True)
+                self._native.segment_copy(self.arena, buf, seg_t)
+            else:  # host fallback (tests): same semantics
+                a = self.arena.numpy()
+                o = buf.numpy()
+                for s_, d_, n_ in seg:
+                    o[d_:d_ + n_] = a[s_:s_ + n_]
+        return self._tree(out, B, T, N)
+
+    @staticmethod
+    def _tree(flat: Dict[tuple, torch.Tensor], B: int, T: int, N: int) -> Dict:
+        batch: Dict = {}
+        hidden: Dict[int, Dict[int, torch.Tensor]] = {}
+        for path, t in flat.items():
+            if path[0] == 'hidden_state':
+                hidden.setdefault(path[1], {})[path[2]] = t
+                continue
+            if path[0] not in OBS_TOP:
+                t = t.view(T, B, *t.shape[1:])
+            node = batch
+            for k in path[:-1]:
+                node = node.setdefault(k, {})
+            node[path[-1]] = t
+        if hidden:
+            batch['hidden_state'] = [(hidden[l][0], hidden[l][1]) for l in sorted(hidden)]
+        en = batch['entity_num'].view(T + 1, B)[:T].long()
+        dev = en.device
+        m = batch.setdefault('mask', {})
+        if 'selected_units_num' in batch:
+            m['selected_units_mask'] = torch.arange(MAX_SELECTED_UNITS_NUM, device=dev) < \
+                batch['selected_units_num'].long().unsqueeze(-1)
+        m['selected_units_logits_mask'] = torch.arange(N + 1, device=dev) < (en + 1).unsqueeze(-1)
+        m['target_units_logits_mask'] = torch.arange(N, device=dev) < en.unsqueeze(-1)
+        batch['batch_size'] = B
+        batch['unroll_len'] = T
+        return batch

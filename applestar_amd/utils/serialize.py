@@ -117,6 +117,24 @@ def loads(data, copy: bool = True) -> Any:
     return _decode(header, body, copy)
 
 
+def parse(data):
+    """(header tree, body memoryview) of an uncompressed frame without decoding any tensor; tensor
+    leaves stay ``{'__t__': [dtype, shape, body_offset, nbytes]}`` descriptors (trajectory ring)."""
+    mv = memoryview(data)
+    if bytes(mv[:len(MAGIC)]) != MAGIC:
+        raise ValueError('not an applestar frame')
+    hlen, comp = struct.unpack('<QB', mv[len(MAGIC):len(MAGIC) + 9])
+    if comp:
+        raise ValueError('compressed frames cannot be parsed in place')
+    hstart = len(MAGIC) + 9
+    header = json.loads(bytes(mv[hstart:hstart + hlen]))
+    body_start = hstart + hlen + ((-(hstart + hlen)) % _ALIGN)
+    return header, mv[body_start:]
+
+
+DTYPES = _DT_INV
+
+
 def save(tree: Any, path: str, compress: bool = False) -> None:
     with open(path, 'wb') as f:
         f.write(dumps(tree, compress))

@@ -175,3 +175,36 @@ def test_agent_registry_and_template_plugin():
                                                   'env': {'game_steps_per_episode': 200, 'fake': True}})
     res = run_episodes(cfg, _job_from_config(cfg))
     assert len(res) == 1 and res[0]['0']['player_id'] == 'model1'
+
+
+def test_trajectory_ring_matches_host_collate():
+    """The HBM ring's on-device batch assembly reproduces collate_trajectories exactly (host path)."""
+    from applestar_amd.runtime.traj_ring import TrajectoryRing
+    from applestar_amd.utils import serialize
+    _, trajs, _, _ = _run_episode('train_test', traj_len=3, value_feature=True)
+    full = [t for t in trajs if len(t) == 4][:3]
+    ref = collate_trajectories(full)
+    ring = TrajectoryRing(64 << 20, device='cpu')
+    ids = [ring.put(serialize.dumps(t)) for t in full]
+    got = ring.batch(ids)
+
+    def cmp(a, b, path=''):
+        if isinstance(a, dict):
+            for k in a:
+                if k in ('batch_size', 'unroll_len'):
+                    assert a[k] == b[k]
+                    continue
+                assert k in b, path + '/' + str(k)
+                cmp(a[k], b[k], path + '/' + str(k))
+        elif isinstance(a, (list, tuple)):
+            for x, y in zip(a, b):
+                cmp(x, y, path)
+        elif torch.is_tensor(a):
+            assert a.shape == b.shape, (path, a.shape, b.shape)
+            assert torch.equal(a.to(b.dtype), b), path
+    cmp(ref, got)
+    # eviction when the ring wraps
+    frames = [serialize.dumps(t) for t in full]
+    small = TrajectoryRing(max(len(f) for f in frames) * 2 + 4096, device='cpu')
+    tids = [small.put(f) for f in frames]
+    assert tids[-1] in small.ids() and tids[0] not in small.ids() and 1 <= len(small) <= 2

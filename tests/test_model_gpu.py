@@ -39,3 +39,32 @@ def test_trainer_step_updates_weights():
     assert torch.isfinite(info['total_loss']).item()
     changed = sum(int(not torch.equal(before[k], v)) for k, v in tr.model.named_parameters())
     assert changed > 100
+
+
+def test_trajectory_ring_on_gpu_matches_host_collate():
+    """HBM ring + native segment_copy kernel vs the host collate of the same trajectories."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_agent import _run_episode
+    from applestar_amd.agent.collate import collate_trajectories
+    from applestar_amd.runtime.traj_ring import TrajectoryRing
+    from applestar_amd.utils import serialize
+    _, trajs, _, _ = _run_episode('train_test', traj_len=3, value_feature=True)
+    full = [t for t in trajs if len(t) == 4][:3]
+    ref = collate_trajectories(full)
+    ring = TrajectoryRing(256 << 20, device='cuda')
+    got = ring.batch([ring.put(serialize.dumps(t)) for t in full])
+    torch.cuda.synchronize()
+
+    def cmp(a, b, path=''):
+        if isinstance(a, dict):
+            for k in a:
+                if k not in ('batch_size', 'unroll_len'):
+                    cmp(a[k], b[k], f'{path}/{k}')
+        elif isinstance(a, (list, tuple)):
+            for x, y in zip(a, b):
+                cmp(x, y, path)
+        elif torch.is_tensor(a):
+            assert a.shape == b.shape, path
+            assert torch.equal(a.to(b.dtype), b.cpu()), path
+    cmp(ref, got)

@@ -78,3 +78,30 @@ def test_rl_pipeline_end_to_end(tmp_path, monkeypatch):
     lrn.close()
     srv.shutdown()
     coord.shutdown()
+
+
+def test_rl_dataloader_ring_mode_cpu():
+    """Ring-mode replay buffer (device collate path, run on the host here): batches come from the
+    trajectory ring, each trajectory is reused max_reuse times then dropped."""
+    import torch
+    from applestar_amd.comm.adapter import Coordinator, serve_coordinator, Adapter
+    from applestar_amd.learner.dataloader import RLDataLoader
+    from test_agent import _run_episode
+    _, trajs, _, _ = _run_episode('train_test', traj_len=3)
+    full = [t for t in trajs if len(t) == 4][:4]
+    srv = serve_coordinator(Coordinator(), '127.0.0.1', 0)
+    port = srv.server_address[1]
+    prod = Adapter('127.0.0.1', port)
+    for t in full:
+        prod.push(t, 'MP0traj')
+    dl = RLDataLoader(Adapter('127.0.0.1', port), 'MP0', batch_size=2, buffer_size=4, device='cpu',
+                      device_collate=True, max_reuse=2)
+    seen = []
+    for _ in range(4):
+        b = next(dl)
+        assert b['entity_info']['x'].shape[0] == 4 * 2 and b['action_info']['action_type'].shape == (3, 2)
+        seen.append(b)
+    assert len(dl._ring) == 0  # 4 trajectories x 2 uses = 4 batches of 2
+    dl.close()
+    prod.close()
+    srv.shutdown()
