@@ -50,8 +50,9 @@ class RLTrainer:
         self.model = model if model is not None else Model(self.cfg, use_value_network=True)
         self.model.to(self.device)
         if self.device.type == 'cuda':
-            # conv shapes depend only on (T+1)*B, so MIOpen find-mode autotuning pays off after one step
-            torch.backends.cudnn.benchmark = bool(lc.get('conv_autotune', True))
+            # MIOpen find-mode autotuning (cudnn.benchmark) is opt-in: it measured ~10% faster convs on the
+            # bench shapes, but two runs that used it left the GPU in a memory-fault state
+            torch.backends.cudnn.benchmark = bool(lc.get('conv_autotune', False))
             # NHWC convolutions end to end (MIOpen igemm kernels are NHWC)
             self.model.to(memory_format=torch.channels_last)
         pdist.broadcast_module(self.model)
