@@ -22,6 +22,7 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
+from ..utils.stopwatch import sw
 from ..lib.features import (SPATIAL_SIZE, SPATIAL_INFO, ENTITY_INFO, EFFECT_LEN, MAX_ENTITY_NUM,
                             MAX_SELECTED_UNITS_NUM, BEGINNING_ORDER_LENGTH, UPGRADE_LENGTH)
 from ..lib.game_data import (ACTIONS, NUM_UNIT_TYPES, NUM_UPGRADES, NUM_UNIT_MIX_ABILITIES,
@@ -195,6 +196,7 @@ class Features:
         return bo, cum, n, bo_loc
 
     # ------------------------------------------------------------------ observation
+    @sw.decorate('transform_obs')
     def transform_obs(self, obs, padding_spatial: bool = False, opponent_obs=None) -> Dict:
         o = obs.observation
         raw = o.raw_data
@@ -324,6 +326,7 @@ class Features:
                 'enemy_units_spatial': (d == 1).unsqueeze(0)}
 
     # ------------------------------------------------------------------ replay action -> labels
+    @sw.decorate('reverse_raw_action')
     def reverse_raw_action(self, action, raw_tags: List[int]):
         """Replay ``ActionRaw`` -> (labels, mask, selected_units_num, last_su_tags, last_tu_tag, invalid)."""
         ret = {'action_type': None, 'delay': torch.tensor(0, dtype=torch.long), 'queued': None,
@@ -418,6 +421,7 @@ def action_type_from_ability(ability_id: int, kind: str) -> Optional[int]:
     return _ACTION_BY_GABILITY.get(g, {}).get(kind)
 
 
+@sw.decorate('transform_action')
 def transform_action(action: dict, map_size=None):
     """Agent action dict -> (list of RawUnitCommand, skip_steps) (env.py:457-480)."""
     from ..envs.raw import RawUnitCommand, Point

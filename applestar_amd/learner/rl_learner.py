@@ -167,6 +167,9 @@ class RLLearner(BaseLearner):
             add_learner_hook(self.hooks, SendModelHook('send_model', 30, 'after_iter'))
             add_learner_hook(self.hooks, SendTrainInfoHook('send_train_info', 35, 'after_iter'))
         self._admin_flags = {}
+        if self.cfg.learner.get('var_record_type', 'alphastar') == 'alphastar':
+            from ..utils.log import AlphaStarVarRecord
+            self.record = AlphaStarVarRecord(self.record.length)
 
     def _setup_trainer(self):
         return RLTrainer(self.cfg, device=self.device)

@@ -16,7 +16,7 @@ from collections import defaultdict, deque
 from typing import Dict, Iterable, Optional
 
 __all__ = ['build_logger', 'TextLogger', 'ScalarLogger', 'AverageMeter', 'EmaMeter', 'MoveAverageMeter',
-           'VariableRecord', 'LogDict', 'pretty_table']
+           'VariableRecord', 'LogDict', 'pretty_table', 'AlphaStarVarRecord']
 
 
 class TextLogger:
@@ -183,3 +183,27 @@ def build_logger(path: str, name: str = 'learner', need_scalar: bool = True, to_
     text = TextLogger(path, name, to_stdout=to_stdout)
     scalar = ScalarLogger(os.path.join(path, 'scalars'), name) if need_scalar else None
     return text, scalar
+
+
+class AlphaStarVarRecord(VariableRecord):
+    """RL learner table layout (``log_helper.py:689-749``): rows = loss families (winloss, bo, bu,
+    effect, upgrade, battle, upgo, kl, ent), columns = per-head / value / reward terms."""
+    ROWS = ['winloss', 'build_order', 'built_unit', 'effect', 'upgrade', 'battle', 'upgo', 'kl', 'entropy']
+    COLS = ['reward', 'value', 'td', 'action_type', 'delay', 'queued', 'selected_units', 'target_unit',
+            'target_location', 'total']
+    GENERAL = ['cur_lr', 'data_time', 'train_time', 'total_loss', 'gradient', 'kl/extra_at',
+               'staleness/mean', 'staleness/max']
+
+    def get_vars_text(self) -> str:
+        vals = self.get_vars_dict()
+        head = ['name', 'val', 'loss'] + [c[:8] for c in self.COLS]
+        rows = [head]
+        for i in range(max(len(self.ROWS), len(self.GENERAL))):
+            g = self.GENERAL[i] if i < len(self.GENERAL) else ''
+            row = [g, f'{vals[g]:.5g}' if g in vals else '']
+            if i < len(self.ROWS):
+                r = self.ROWS[i]
+                row += [r] + [f'{vals[f"{r}/{c}"]:.4g}' if f'{r}/{c}' in vals else '' for c in self.COLS]
+            rows.append(row)
+        w = [max(len(r[j]) if j < len(r) else 0 for r in rows) for j in range(len(head))]
+        return '\n'.join(' | '.join((r[j] if j < len(r) else '').ljust(w[j]) for j in range(len(head))) for r in rows)

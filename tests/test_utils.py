@@ -144,3 +144,24 @@ def test_meters():
     r.update_var({'a': 1.0, 'b': 2.0})
     r.update_var({'a': 3.0})
     assert r.get_vars_dict()['a'] == 2.0 and 'a' in r.get_vars_text()
+
+
+def test_stopwatch_and_alphastar_table():
+    from applestar_amd.utils.stopwatch import StopWatch
+    from applestar_amd.utils.log import AlphaStarVarRecord
+    s = StopWatch(enabled=True)
+    for _ in range(3):
+        with s('outer'):
+            with s('inner'):
+                pass
+
+    @s.decorate('fn')
+    def f():
+        return 1
+    f()
+    assert s.times['outer'].num == 3 and s.times['outer.inner'].num == 3 and s.times['fn'].num == 1
+    assert 'outer.inner' in s.str()
+    r = AlphaStarVarRecord(4)
+    r.update_var({'winloss/action_type': 0.5, 'total_loss': 2.0, 'kl/total': 0.1})
+    txt = r.get_vars_text()
+    assert 'winloss' in txt and '0.5' in txt and 'total_loss' in txt
