@@ -19,7 +19,13 @@ import sysconfig
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 ROOT = os.path.dirname(PKG)
-BUILD = os.path.join(ROOT, 'build', 'csrc')
+# Build variants: APPLESTAR_BUILD=debug adds -g and device-side bounds asserts (AS_DEBUG);
+# APPLESTAR_HOST_SANITIZE=address|undefined|thread instruments the HOST code only (bindings + the host
+# halves of the .hip launchers, via -Xarch_host); GPU sanitizers / xnack are not used on this pool.
+VARIANT = os.environ.get('APPLESTAR_BUILD', 'release')
+SANITIZE = os.environ.get('APPLESTAR_HOST_SANITIZE', '')
+BUILD = os.path.join(ROOT, 'build', 'csrc' + ('' if VARIANT == 'release' and not SANITIZE else
+                                              f'-{VARIANT}{"-" + SANITIZE if SANITIZE else ""}'))
 ARCH = os.environ.get('APPLESTAR_OFFLOAD_ARCH', 'gfx950')
 ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
 
@@ -34,8 +40,12 @@ def _torch_paths():
 
 
 def ext_filename() -> str:
+    """Release builds land in-tree (what the package imports); debug / sanitizer variants stay in
+    their build directory and are loaded with ``APPLESTAR_EXT_PATH=<that .so>``."""
     suffix = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
-    return os.path.join(PKG, '_C' + suffix)
+    if VARIANT == 'release' and not SANITIZE:
+        return os.path.join(PKG, '_C' + suffix)
+    return os.path.join(BUILD, '_C' + suffix)
 
 
 def write_ninja() -> str:
@@ -45,13 +55,19 @@ def write_ninja() -> str:
     hipcc = os.path.join(ROCM, 'bin', 'hipcc')
     hip_flags = (f'--offload-arch={ARCH} -O3 -fPIC -std=c++17 -fno-gpu-rdc -I{HERE} '
                  f'-D__HIP_PLATFORM_AMD__ -Wno-unused-result')
+    if VARIANT == 'debug':
+        hip_flags += ' -g -DAS_DEBUG'
+    if SANITIZE:
+        hip_flags += f' -Xarch_host -fsanitize={SANITIZE}'
     cxx_flags = ' '.join([
         '-O2 -fPIC -std=c++17 -D__HIP_PLATFORM_AMD__=1 -DUSE_ROCM=1 -DTORCH_EXTENSION_NAME=_C',
         '-DTORCH_API_INCLUDE_EXTENSION_H', f'-D_GLIBCXX_USE_CXX11_ABI={abi}', f'-I{HERE}',
         ' '.join(f'-isystem {p}' for p in inc), f'-isystem {py_inc}', f'-isystem {ROCM}/include',
-        '-Wno-deprecated-declarations'])
+        '-Wno-deprecated-declarations'] + ([f'-fsanitize={SANITIZE} -fno-omit-frame-pointer'] if SANITIZE else [])
+        + (['-g -DAS_DEBUG'] if VARIANT == 'debug' else []))
     ldflags = ' '.join([f'-L{lib}', '-lc10', '-ltorch', '-ltorch_cpu', '-ltorch_python', '-lc10_hip', '-ltorch_hip',
-                        f'-L{ROCM}/lib', '-lamdhip64', f'-Wl,-rpath,{lib}', f'-Wl,-rpath,{ROCM}/lib'])
+                        f'-L{ROCM}/lib', '-lamdhip64', f'-Wl,-rpath,{lib}', f'-Wl,-rpath,{ROCM}/lib']
+                       + ([f'-fsanitize={SANITIZE}'] if SANITIZE else []))
     lines = [
         'ninja_required_version = 1.3',
         f'hipcc = {hipcc}',

@@ -14,6 +14,9 @@ __global__ __launch_bounds__(256) void segment_copy_kernel(const uint8_t* __rest
                                                            const int64_t* __restrict__ seg, long nseg) {
   for (long s = blockIdx.x; s < nseg; s += gridDim.x) {
     const int64_t src = seg[3 * s], dst = seg[3 * s + 1], n = seg[3 * s + 2];
+#ifdef AS_DEBUG
+    assert(src >= 0 && dst >= 0 && n >= 0);
+#endif
     const uint8_t* a = arena + src;
     uint8_t* o = out + dst;
     if (((src | dst | n) & 15) == 0) {

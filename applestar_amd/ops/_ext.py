@@ -22,7 +22,8 @@ def _load():
     global _C, _ERR
     if _C is not None or _ERR is not None:
         return _C
-    cands = sorted(glob.glob(os.path.join(_PKG_DIR, '_C*.so')))
+    override = os.environ.get('APPLESTAR_EXT_PATH')  # debug / host-sanitizer build variants
+    cands = [override] if override else sorted(glob.glob(os.path.join(_PKG_DIR, '_C*.so')))
     if not cands:
         _ERR = f'applestar_amd native extension not built (no _C*.so in {_PKG_DIR}); run `python -m applestar_amd.csrc.build`'
         return None
