@@ -193,13 +193,27 @@ class _PayloadServer:
             pass
 
 
-def fetch(ip: str, port: int, key: str, timeout: float = 60.0) -> Optional[bytearray]:
+def fetch(ip: str, port: int, key: str, timeout: float = 60.0, alloc=None):
+    """Receive one payload.  ``alloc(n)`` may supply the destination (e.g. a pinned staging buffer
+    of the trajectory ring) so the bytes land where the H2D copy reads them, with no extra copy."""
     with socket.create_connection((ip, port), timeout=timeout) as s:
         s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         k = key.encode()
         s.sendall(_LEN.pack(len(k)) + k)
         (n,) = _LEN.unpack(_recv_exact(s, 8))
-        return _recv_exact(s, n) if n else None
+        if not n:
+            return None
+        if alloc is None:
+            return _recv_exact(s, n)
+        buf = alloc(n)
+        view = memoryview(buf)[:n]
+        got = 0
+        while got < n:
+            r = s.recv_into(view[got:], n - got)
+            if r == 0:
+                raise ConnectionError('peer closed')
+            got += r
+        return view
 
 
 # ----------------------------------------------------------------------------- adapter
@@ -249,14 +263,14 @@ class Adapter:
         return key
 
     def pull(self, token: str, size: int = 1, block: bool = True, sleep_time: float = 0.05,
-             timeout: Optional[float] = None, raw: bool = False) -> List[Any]:
+             timeout: Optional[float] = None, raw: bool = False, alloc=None) -> List[Any]:
         out: List[Any] = []
         t0 = time.time()
         while len(out) < size:
             metas = _post_json(self._cip, self._cport, '/coordinator/pull', {'token': token, 'size': size - len(out)})
             for m in metas:
                 try:
-                    data = fetch(m['ip'], m['port'], m['key'])
+                    data = fetch(m['ip'], m['port'], m['key'], alloc=alloc)
                 except OSError:
                     data = None
                 if data is not None:

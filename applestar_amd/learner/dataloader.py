@@ -55,12 +55,12 @@ class RLDataLoader:
             self._iter = DevicePrefetcher(self._host_batches(), self.device) if self.device.type == 'cuda' else \
                 self._host_batches()
 
-    def _pull(self, n: int, raw: bool = False) -> List:
+    def _pull(self, n: int, raw: bool = False, alloc=None) -> List:
         out: List = []
         while len(out) < n and not self._stop.is_set():
             try:
                 out += self._adapter.pull(self._token, size=n - len(out), block=True, sleep_time=0.1, timeout=1.0,
-                                          raw=raw)
+                                          raw=raw, alloc=alloc)
             except (ConnectionError, OSError):  # coordinator restarting / shutting down: retry until stopped
                 self._stop.wait(1.0)
         return out
@@ -72,7 +72,7 @@ class RLDataLoader:
             with self._avail:
                 while len(self._ring) >= self.buffer_size and not self._stop.is_set():
                     self._avail.wait(0.5)
-            for frame in self._pull(1, raw=True):
+            for frame in self._pull(1, raw=True, alloc=self._ring.stage):  # bytes land in pinned staging
                 self._ring.put(frame)
                 with self._avail:
                     self._avail.notify_all()

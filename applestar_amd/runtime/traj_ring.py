@@ -96,28 +96,47 @@ class TrajectoryRing:
         self._head = end
         return start
 
+    def _next_slot(self, n: int):
+        slot = self._staging[0]
+        self._staging.rotate(-1)
+        if slot[1] is not None:
+            slot[1].synchronize()  # the previous async copy out of this staging buffer has finished
+        if slot[0] is None or slot[0].numel() < n:
+            slot[0] = torch.empty(max(n, 1 << 20), dtype=torch.uint8, pin_memory=self._stream is not None)
+        return slot
+
+    def stage(self, n: int):
+        """Receive target for a frame of ``n`` bytes (pass as ``alloc`` to ``Adapter.pull``): a pinned
+        staging buffer, so :meth:`put` can DMA it to HBM without another host copy."""
+        slot = self._next_slot(n)
+        view = memoryview(slot[0].numpy())[:n]
+        self._staged = (view, slot)
+        return view
+
     def put(self, frame) -> int:
+        staged = getattr(self, '_staged', None)
+        slot = staged[1] if staged is not None and frame is staged[0] else None
+        self._staged = None
         header, body = serialize.parse(frame)
         steps = header['__l__']
         n = len(body)
+        body_off = len(frame) - n
         with self._lock:
             start = self._alloc(n)
             tr = _Traj(start, (n + _ALIGN - 1) // _ALIGN * _ALIGN, steps)
-            with warnings.catch_warnings():  # read-only source: only ever copied from
-                warnings.simplefilter('ignore')
-                src = torch.frombuffer(body, dtype=torch.uint8) if n else torch.empty(0, dtype=torch.uint8)
+            if slot is None:
+                with warnings.catch_warnings():  # read-only source: only ever copied from
+                    warnings.simplefilter('ignore')
+                    src = torch.frombuffer(body, dtype=torch.uint8) if n else torch.empty(0, dtype=torch.uint8)
             if self._stream is None:
-                self.arena[start:start + n].copy_(src)
+                self.arena[start:start + n].copy_(src if slot is None else slot[0][body_off:body_off + n])
             else:
-                slot = self._staging[0]
-                self._staging.rotate(-1)
-                if slot[1] is not None:
-                    slot[1].synchronize()  # previous async copy from this staging buffer is done
-                if slot[0] is None or slot[0].numel() < n:
-                    slot[0] = torch.empty(max(n, 1 << 20), dtype=torch.uint8, pin_memory=True)
-                slot[0][:n].copy_(src)
+                if slot is None:
+                    slot = self._next_slot(n)
+                    slot[0][:n].copy_(src)
+                    body_off = 0
                 with torch.cuda.stream(self._stream):
-                    self.arena[start:start + n].copy_(slot[0][:n], non_blocking=True)
+                    self.arena[start:start + n].copy_(slot[0][body_off:body_off + n], non_blocking=True)
                     ev = torch.cuda.Event()
                     ev.record(self._stream)
                 slot[1] = ev
