@@ -100,10 +100,18 @@ class BaseLearner:
             return os.path.join(d, f'{self.experiment_name}_{pid}_iteration_{it}.pth.tar')
         return os.path.join(self.exp_dir, 'checkpoint', f'{self.experiment_name}_iteration_{it}.pth.tar')
 
+    def model_state_dict(self):
+        f = getattr(self.trainer, 'model_state_dict', None)
+        return f() if f else self.model.state_dict()
+
+    def model_loader(self):
+        return getattr(self.trainer, 'load_model_state_dict', None)
+
     def save_checkpoint(self):
         if self.rank == 0:
             path = self.checkpoint_path(self.last_iter.val)
-            self.checkpoint_helper.save(path, self.model, self.optimizer, last_iter=self.last_iter.val)
+            self.checkpoint_helper.save(path, self.model, self.optimizer, last_iter=self.last_iter.val,
+                                        state_dict=self.model_state_dict())
             self.last_checkpoint_path = path
 
     def call_hooks(self, position: str):

@@ -45,7 +45,7 @@ class LoadCkptHook(LearnerHook):
             return
         obj = engine.checkpoint_helper.load(path, engine.model, engine.optimizer,
                                             load_optimizer=engine.cfg.learner.get('load_optimizer', True),
-                                            logger=engine.logger)
+                                            logger=engine.logger, loader=engine.model_loader())
         engine.last_iter.update(int(obj.get('last_iter', 0)))
         if engine.lr_scheduler is not None:
             engine.lr_scheduler.last_epoch = engine.last_iter.val
@@ -57,7 +57,8 @@ class SaveCkptHook(LearnerHook):
         if engine.rank != 0 or engine.last_iter.val % self.freq != 0:
             return
         path = engine.checkpoint_path(engine.last_iter.val)
-        engine.checkpoint_helper.save(path, engine.model, engine.optimizer, last_iter=engine.last_iter.val)
+        engine.checkpoint_helper.save(path, engine.model, engine.optimizer, last_iter=engine.last_iter.val,
+                                      state_dict=engine.model_state_dict())
         engine.last_checkpoint_path = path
         engine.info(f'{engine.name} saved checkpoint {path}')
 

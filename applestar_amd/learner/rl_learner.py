@@ -85,7 +85,8 @@ class LearnerComm:
             self._model_count += 1
         if not due or self._adapter is None or learner.rank != 0:
             return
-        sd = learner.model.policy_state_dict()
+        sd = {k: v for k, v in learner.model_state_dict().items()
+              if 'value_networks' not in k and 'value_encoder' not in k}
         with self._lock:
             if self._snapshot is None:
                 self._snapshot = {k: torch.empty(v.shape, dtype=v.dtype, pin_memory=v.is_cuda) for k, v in sd.items()}
@@ -207,9 +208,11 @@ class RLLearner(BaseLearner):
                     next(net.parameters()).device)
                 net.load_state_dict(fresh.state_dict())
         pdist.broadcast_module(self.model)
+        self.trainer.on_model_changed()
 
     def reset_from_checkpoint(self, path: str) -> None:
-        self.checkpoint_helper.load(path, self.model, None, load_optimizer=False, logger=self.logger)
+        self.checkpoint_helper.load(path, self.model, None, load_optimizer=False, logger=self.logger,
+                                    loader=self.model_loader())
         self.reset_value()
         self.trainer.remain_value_pretrain = int(self.cfg.learner.get('value_pretrain_iters', -1))
         self.trainer.reset_optimizer()

@@ -40,22 +40,31 @@ class GradientReducer:
         self.world = pdist.get_world_size()
         self.overlap = overlap
         self.comm_dtype = comm_dtype
+        self.keep_comm = False  # master-weight mode reads the fp32 reduction directly (reduced())
         params = [p for p in params if p.requires_grad]
         self.params = params
         self.buckets: List[_Bucket] = []
         self._owner = {}
-        # backward visits layers roughly in reverse registration order
-        cur, cur_bytes = [], 0
+        # backward visits layers roughly in reverse registration order; parameters of different dtypes
+        # (bf16 GEMM weights + fp32 norm affines under master weights) go to separate bucket chains so
+        # the interleaving does not fragment the buckets
         limit = int(bucket_mb * 1024 * 1024)
+        keys = []
         for p in reversed(params):
-            key = (p.dtype, p.device)
-            if cur and ((cur[0].dtype, cur[0].device) != key or cur_bytes + p.numel() * p.element_size() > limit):
+            if (p.dtype, p.device) not in keys:
+                keys.append((p.dtype, p.device))
+        for key in keys:
+            cur, cur_bytes = [], 0
+            for p in reversed(params):
+                if (p.dtype, p.device) != key:
+                    continue
+                if cur and cur_bytes + p.numel() * p.element_size() > limit:
+                    self._add_bucket(cur)
+                    cur, cur_bytes = [], 0
+                cur.append(p)
+                cur_bytes += p.numel() * p.element_size()
+            if cur:
                 self._add_bucket(cur)
-                cur, cur_bytes = [], 0
-            cur.append(p)
-            cur_bytes += p.numel() * p.element_size()
-        if cur:
-            self._add_bucket(cur)
         self._hooks = []
         if self.world > 1 and overlap:
             for p in params:
@@ -82,8 +91,11 @@ class GradientReducer:
         if b.handle is not None or self.world == 1:
             return
         buf = b.flat
-        if self.comm_dtype is not None and self.comm_dtype != buf.dtype:
-            b.comm = buf.to(self.comm_dtype)
+        comm_dtype = self.comm_dtype
+        if comm_dtype is None and buf.dtype == torch.bfloat16 and self.keep_comm:
+            comm_dtype = torch.float32  # bf16 gradients are summed across ranks in fp32
+        if comm_dtype is not None and comm_dtype != buf.dtype:
+            b.comm = buf.to(comm_dtype)
             buf = b.comm
         op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
         b.handle = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
@@ -112,10 +124,17 @@ class GradientReducer:
         for b in self.buckets:
             b.handle.wait()
             if b.comm is not None:
-                b.flat.copy_(b.comm)
-            if not self.use_avg:
+                if not self.use_avg:
+                    b.comm.div_(self.world)
+                if not self.keep_comm:
+                    b.flat.copy_(b.comm)
+            elif not self.use_avg:
                 b.flat.div_(self.world)
             b.handle = None
+
+    def reduced(self, b: _Bucket) -> torch.Tensor:
+        """The bucket's averaged gradient (the fp32 communication copy when one was used)."""
+        return b.comm if b.comm is not None else b.flat
 
     def remove(self):
         for h in self._hooks:

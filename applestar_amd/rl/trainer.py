@@ -16,6 +16,7 @@ import torch
 from ..models.model import Model
 from ..parallel import dist as pdist
 from ..parallel.dp import GradientReducer
+from ..parallel.mixed import MasterWeights
 from ..utils.config import AttrDict, deep_merge_dicts
 from ..utils.grad_clip import build_grad_clip
 from .loss import ReinforcementLoss
@@ -58,7 +59,17 @@ class RLTrainer:
         pdist.broadcast_module(self.model)
         self.params = [p for p in self.model.parameters() if p.requires_grad]
         comm = getattr(torch, lc.comm_dtype) if lc.get('comm_dtype') else None
-        self.reducer = GradientReducer(self.params, bucket_mb=lc.bucket_mb, comm_dtype=comm)
+        use_master = lc.get('master_weights', None)
+        if use_master is None:
+            use_master = self.device.type == 'cuda' and lc.get('amp_dtype') == 'bfloat16'
+        self.master = None
+        if use_master:
+            self.master = MasterWeights(self.model, bucket_mb=lc.bucket_mb, comm_dtype=comm)
+            self.reducer = self.master.reducer
+            self.opt_params = self.master.opt_params
+        else:
+            self.reducer = GradientReducer(self.params, bucket_mb=lc.bucket_mb, comm_dtype=comm)
+            self.opt_params = self.params
         self.reset_optimizer()
         self.grad_clip = build_grad_clip(lc.grad_clip)
         self.loss = ReinforcementLoss(lc, lc.player_id)
@@ -69,7 +80,7 @@ class RLTrainer:
     def reset_optimizer(self):
         """Fresh Adam(betas=(0, 0.99), eps=1e-5) state (also used after a league reset)."""
         lc = self.cfg.learner
-        self.optimizer = torch.optim.Adam(self.params, lr=lc.learning_rate, betas=(0.0, 0.99), eps=1e-5,
+        self.optimizer = torch.optim.Adam(self.opt_params, lr=lc.learning_rate, betas=(0.0, 0.99), eps=1e-5,
                                           weight_decay=lc.weight_decay, fused=self.device.type == 'cuda')
         self.lr_scheduler = None
 
@@ -88,18 +99,37 @@ class RLTrainer:
         info = self.loss.compute_loss(out)
         self.reducer.zero_grad()
         info['total_loss'].backward()
-        self.reducer.synchronize()
-        info['gradient'] = self.grad_clip.apply(self.params)
+        if self.master is not None:
+            self.master.synchronize()
+        else:
+            self.reducer.synchronize()
+        info['gradient'] = self.grad_clip.apply(self.opt_params)
         self.optimizer.step()
+        if self.master is not None:
+            self.master.after_step()
         self.iter += 1
         return info
 
+    def model_state_dict(self):
+        """fp32 model weights (the master copies when the compute weights are bf16)."""
+        return self.master.state_dict() if self.master is not None else self.model.state_dict()
+
+    def load_model_state_dict(self, sd):
+        if self.master is not None:
+            return self.master.load_state_dict(sd)
+        return self.model.load_state_dict(sd, strict=False)
+
+    def on_model_changed(self):
+        """Call after editing model weights in place (e.g. a value-network reset)."""
+        if self.master is not None:
+            self.master.sync_from_model()
+
     def state_dict(self):
-        return {'model': self.model.state_dict(), 'optimizer': self.optimizer.state_dict(),
+        return {'model': self.model_state_dict(), 'optimizer': self.optimizer.state_dict(),
                 'last_iter': self.iter, 'grad_clip': self.grad_clip.state_dict()}
 
     def load_state_dict(self, sd, load_optimizer=True):
-        self.model.load_state_dict(sd['model'], strict=False)
+        self.load_model_state_dict(sd['model'])
         if load_optimizer and 'optimizer' in sd:
             self.optimizer.load_state_dict(sd['optimizer'])
         self.iter = int(sd.get('last_iter', 0))

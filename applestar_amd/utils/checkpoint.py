@@ -38,7 +38,7 @@ def save_file(obj: Dict, path: str) -> None:
 
 
 def load_state_dict_matched(module: torch.nn.Module, state: Dict[str, torch.Tensor],
-                            drop: Iterable[str] = (), prefix_strip: str = 'module.') -> Dict[str, list]:
+                            drop: Iterable[str] = (), prefix_strip: str = 'module.', loader=None) -> Dict[str, list]:
     """Copy every key whose name and shape match; report the rest."""
     own = module.state_dict()
     matched, mismatched, unexpected = {}, [], []
@@ -53,14 +53,14 @@ def load_state_dict_matched(module: torch.nn.Module, state: Dict[str, torch.Tens
         else:
             matched[kk] = v
     missing = [k for k in own if k not in matched and not any(d in k for d in drop)]
-    module.load_state_dict(matched, strict=False)
+    (loader or (lambda sd: module.load_state_dict(sd, strict=False)))(matched)
     return {'missing': missing, 'unexpected': unexpected, 'mismatched': mismatched, 'loaded': list(matched)}
 
 
 class CheckpointHelper:
     def save(self, path: str, model: torch.nn.Module, optimizer=None, last_iter: Optional[int] = None,
-             extra: Optional[Dict] = None, policy_only: bool = False) -> None:
-        sd = model.state_dict()
+             extra: Optional[Dict] = None, policy_only: bool = False, state_dict: Optional[Dict] = None) -> None:
+        sd = model.state_dict() if state_dict is None else state_dict
         if policy_only:
             sd = {k: v for k, v in sd.items() if 'value_networks' not in k and 'value_encoder' not in k}
         obj = {'model': {k: v.detach().cpu() for k, v in sd.items()}}
@@ -73,10 +73,11 @@ class CheckpointHelper:
         save_file(obj, path)
 
     def load(self, path: str, model: torch.nn.Module, optimizer=None, load_optimizer: bool = True,
-             drop: Iterable[str] = (), logger=None) -> Dict:
+             drop: Iterable[str] = (), logger=None, loader=None) -> Dict:
+        """``loader(matched_state_dict)`` replaces ``model.load_state_dict`` (master-weight trainers)."""
         obj = load_file(path)
         sd = obj['model'] if 'model' in obj else obj
-        report = load_state_dict_matched(model, sd, drop=drop)
+        report = load_state_dict_matched(model, sd, drop=drop, loader=loader)
         if logger is not None:
             for k in ('missing', 'unexpected', 'mismatched'):
                 if report[k]:

@@ -59,3 +59,65 @@ def test_gradient_reducer_world2():
     for a, b in zip(g0, g1):
         assert torch.allclose(a, b)       # all-reduced gradients identical on both ranks
     assert sc0 == sc1 and abs(sc0['a'] - 0.5) < 1e-6 and abs(sc0['b'] - 2.0) < 1e-6
+
+
+class _Tiny(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.fc1 = torch.nn.Linear(6, 16)
+        self.ln = torch.nn.LayerNorm(16)
+        self.fc2 = torch.nn.Linear(16, 3)
+        self.conv = torch.nn.Conv2d(2, 4, 3)
+
+    def forward(self, x, img):
+        return self.fc2(torch.relu(self.ln(self.fc1(x)))).square().sum() + self.conv(img).square().sum()
+
+
+def _master_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from applestar_amd.parallel import dist as pdist
+    from applestar_amd.parallel.mixed import MasterWeights
+    pdist.init(backend='gloo')
+    torch.manual_seed(0)
+    m = _Tiny()
+    m.conv.to(memory_format=torch.channels_last)
+    ref = {k: v.clone() for k, v in m.state_dict().items()}
+    mw = MasterWeights(m, bucket_mb=0.0005)
+    opt = torch.optim.SGD(mw.opt_params, lr=0.1)
+    torch.manual_seed(100 + rank)
+    x, img = torch.randn(5, 6), torch.randn(2, 2, 5, 5).contiguous(memory_format=torch.channels_last)
+    mw.zero_grad()
+    with torch.autocast('cpu', dtype=torch.bfloat16):
+        loss = m(x, img)
+    loss.backward()
+    mw.synchronize()
+    opt.step()
+    mw.after_step()
+    npy = lambda d: {k: v.detach().float().numpy().copy() for k, v in d.items()}  # plain pickles
+    q.put((rank, npy(mw.state_dict()), npy(ref), [str(b.flat.dtype) for b in mw.reducer.buckets],
+           str(m.fc1.weight.dtype), str(m.ln.weight.dtype), {k: str(v.dtype) for k, v in mw.state_dict().items()}))
+    pdist.finalize()
+
+
+def test_master_weights_world2():
+    """bf16 compute weights + flat fp32 masters: masters stay identical across ranks, updates use the
+    rank-averaged gradient, norm params stay fp32, bf16 and fp32 params get separate bucket chains."""
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_master_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    import numpy as np
+    (_, s0, ref, dts, wdt, lndt, sdt), (_, s1, _, _, _, _, _) = res
+    assert wdt == 'torch.bfloat16' and lndt == 'torch.float32'
+    assert 'torch.bfloat16' in dts and 'torch.float32' in dts
+    assert all(v == 'torch.float32' for v in sdt.values())   # checkpoints carry fp32 masters
+    for k in s0:
+        assert np.array_equal(s0[k], s1[k]), k
+    # the update moved every weight by lr * averaged grad (non-zero)
+    assert all(np.abs(s0[k] - ref[k]).max() > 0 for k in ('fc1.weight', 'fc2.weight', 'conv.weight', 'ln.weight'))
