@@ -58,6 +58,132 @@ template <> struct WLoad<float, 2> {
   }
 };
 
+// one 16-byte load: 8 bf16 or 4 fp32 values
+template <typename TW> struct WLoad16;
+template <> struct WLoad16<bf16_t> {
+  __device__ static void load(const bf16_t* p, float* v) {
+    const uint4 t = *reinterpret_cast<const uint4*>(p);
+    v[0] = __uint_as_float(t.x << 16); v[1] = __uint_as_float(t.x & 0xffff0000u);
+    v[2] = __uint_as_float(t.y << 16); v[3] = __uint_as_float(t.y & 0xffff0000u);
+    v[4] = __uint_as_float(t.z << 16); v[5] = __uint_as_float(t.z & 0xffff0000u);
+    v[6] = __uint_as_float(t.w << 16); v[7] = __uint_as_float(t.w & 0xffff0000u);
+  }
+};
+template <> struct WLoad16<float> {
+  __device__ static void load(const float* p, float* v) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+};
+
+// Forward for the wide (H = 384) core LSTM: the h W^T GEMV is split over SPLIT groups of rows with
+// 16-byte loads (8 bf16 columns per thread), so ~4x more bytes are in flight than the one-thread-per-
+// 4-columns layout; the per-row recurrence is unchanged (one workgroup per batch row).
+template <int H, int NT, typename TW>
+__global__ __launch_bounds__(NT) void lnlstm_fwd_wide_kernel(
+    const float* __restrict__ xp, const float* __restrict__ h0, const float* __restrict__ c0,
+    const TW* __restrict__ wT, const float* __restrict__ lnh_w, const float* __restrict__ lnh_b,
+    const float* __restrict__ lnc_w, const float* __restrict__ lnc_b, int T, int B, float eps,
+    float* __restrict__ out, float* __restrict__ c_all, float* __restrict__ xhat_h, float* __restrict__ rstd_h,
+    float* __restrict__ gates_out, float* __restrict__ xhat_c, float* __restrict__ rstd_c, float* __restrict__ hT,
+    float* __restrict__ cT) {
+  constexpr int G = 4 * H;
+  constexpr int VW = sizeof(TW) == 2 ? 8 : 4;   // columns per 16-byte load
+  constexpr int CG = G / VW;                    // column groups
+  constexpr int SPLIT = NT / CG;                // row splits of the reduction
+  constexpr int COLS = G / NT;                  // columns per thread in the LN / gate phase
+  static_assert(NT % CG == 0 && H % SPLIT == 0 && G % NT == 0 && NT >= H, "wide tiling");
+  constexpr int RS = H / SPLIT;
+  __shared__ float h_s[H];
+  __shared__ float g_s[G];
+  __shared__ float part[SPLIT][G];
+  __shared__ float red[NT / kWave];
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const bool unit = tid < H;
+  const int cg = tid % CG, sp = tid / CG;
+  float c = 0.f, lcw = 0.f, lcb = 0.f;
+  if (unit) {
+    h_s[tid] = h0[static_cast<long>(b) * H + tid];
+    c = c0[static_cast<long>(b) * H + tid];
+    lcw = lnc_w[tid];
+    lcb = lnc_b[tid];
+    c_all[static_cast<long>(b) * H + tid] = c;
+  }
+  float lw[COLS], lb[COLS];
+#pragma unroll
+  for (int k = 0; k < COLS; ++k) { lw[k] = lnh_w[tid * COLS + k]; lb[k] = lnh_b[tid * COLS + k]; }
+  __syncthreads();
+  for (int t = 0; t < T; ++t) {
+    float acc[VW];
+#pragma unroll
+    for (int v = 0; v < VW; ++v) acc[v] = 0.f;
+    const TW* wp = wT + cg * VW;
+#pragma unroll 16
+    for (int i = sp * RS; i < sp * RS + RS; ++i) {
+      float wv[VW];
+      WLoad16<TW>::load(wp + static_cast<long>(i) * G, wv);
+      const float hv = h_s[i];
+#pragma unroll
+      for (int v = 0; v < VW; ++v) acc[v] = fmaf(hv, wv[v], acc[v]);
+    }
+#pragma unroll
+    for (int v = 0; v < VW; ++v) part[sp][cg * VW + v] = acc[v];
+    __syncthreads();
+    float a[COLS];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < SPLIT; ++q) v += part[q][tid * COLS + k];
+      a[k] = v;
+      s += v;
+    }
+    const float mu = block_sum<NT>(s, red) * (1.f / G);
+    float q2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) { const float d = a[k] - mu; q2 += d * d; }
+    const float rs = rsqrtf(block_sum<NT>(q2, red) * (1.f / G) + eps);
+    const long row = static_cast<long>(t) * B + b;
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) {
+      const int j = tid * COLS + k;
+      const float xh = (a[k] - mu) * rs;
+      const float gv = xp[row * G + j] + xh * lw[k] + lb[k];
+      xhat_h[row * G + j] = xh;
+      gates_out[row * G + j] = gv;
+      g_s[j] = gv;
+    }
+    if (tid == 0) rstd_h[row] = rs;
+    __syncthreads();
+    float cpre = 0.f, og = 0.f;
+    if (unit) {
+      const float ig = sigmoidf_(g_s[tid]);
+      const float fg = sigmoidf_(g_s[H + tid]);
+      const float gg = tanhf(g_s[2 * H + tid]);
+      og = sigmoidf_(g_s[3 * H + tid]);
+      cpre = fg * c + ig * gg;
+    }
+    const float muc = block_sum<NT>(unit ? cpre : 0.f, red) * (1.f / H);
+    const float dc = unit ? cpre - muc : 0.f;
+    const float rsc = rsqrtf(block_sum<NT>(dc * dc, red) * (1.f / H) + eps);
+    if (unit) {
+      const float xc = dc * rsc;
+      c = xc * lcw + lcb;
+      const float hv = og * tanhf(c);
+      out[row * H + tid] = hv;
+      c_all[(row + B) * H + tid] = c;
+      xhat_c[row * H + tid] = xc;
+      h_s[tid] = hv;
+      if (t == T - 1) { hT[static_cast<long>(b) * H + tid] = hv; cT[static_cast<long>(b) * H + tid] = c; }
+    }
+    if (tid == 0) rstd_c[row] = rsc;
+    __syncthreads();
+  }
+  if (T == 0 && unit) { hT[static_cast<long>(b) * H + tid] = h_s[tid]; cT[static_cast<long>(b) * H + tid] = c; }
+}
+
 // wT: W_hh transposed, [H][4H] row-major
 template <int H, int NT, int COLS, typename TW>
 __global__ __launch_bounds__(NT) void lnlstm_fwd_kernel(
@@ -229,26 +355,29 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
       dg_s[j] = v;  // each thread overwrites only its own columns
     }
     __syncthreads();
-    // ---- dh_{t-1} = dhg @ W  (W [G][H]): 2-D split, each thread owns KV consecutive outputs and
-    // 1/JG of the reduction (coalesced KV*2-byte loads along k), partials combined through LDS
+    // ---- dh_{t-1} = dhg @ W  (W [G][H]): 2-D split, each thread owns KV consecutive outputs (one
+    // 16-byte load per j) and 1/JG of the reduction; partials combined through LDS
     {
-      constexpr int KV = (H % 4 == 0 && (H / 4) * 4 <= NT) ? 4 : 1;
+      constexpr int KV = sizeof(TW) == 2 ? 8 : 4;
       constexpr int KT = H / KV;              // threads along k
       constexpr int JG = NT / KT;             // reduction groups
+      static_assert(H % KV == 0 && JG >= 1 && G % JG == 0, "dh tiling");
       const int kq = tid % KT, jg = tid / KT;
       float acc[KV];
 #pragma unroll
       for (int v = 0; v < KV; ++v) acc[v] = 0.f;
       if (jg < JG) {
         const int j0 = jg * (G / JG), j1 = j0 + G / JG;
-#pragma unroll 32
+#pragma unroll 16
         for (int j = j0; j < j1; ++j) {
           const float d = dg_s[j];
+          float wv[KV];
+          WLoad16<TW>::load(w + static_cast<long>(j) * H + kq * KV, wv);
 #pragma unroll
-          for (int v = 0; v < KV; ++v) acc[v] = fmaf(d, Cvt<TW>::load(w, static_cast<long>(j) * H + kq * KV + v), acc[v]);
+          for (int v = 0; v < KV; ++v) acc[v] = fmaf(d, wv[v], acc[v]);
         }
       }
-      __shared__ float part[JG > 0 ? JG : 1][H];
+      __shared__ float part[JG][H];
       if (jg < JG) {
 #pragma unroll
         for (int v = 0; v < KV; ++v) part[jg][kq * KV + v] = acc[v];
@@ -307,9 +436,16 @@ void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* w
                 const float* lnh_b, const float* lnc_w, const float* lnc_b, int T, int B, int H, float eps, float* out,
                 float* c_all, float* xhat_h, float* rstd_h, float* gates, float* xhat_c, float* rstd_c, float* hT,
                 float* cT, hipStream_t s) {
-  if (H == 384)
-    fwd_launch<384, 384, 4>(xp, h0, c0, wT, w_dt, lnh_w, lnh_b, lnc_w, lnc_b, T, B, eps, out, c_all, xhat_h, rstd_h,
-                            gates, xhat_c, rstd_c, hT, cT, s);
+  if (H == 384) {
+    if (w_dt == DT_BF16)
+      hipLaunchKernelGGL((lnlstm_fwd_wide_kernel<384, 768, bf16_t>), dim3(B), dim3(768), 0, s, xp, h0, c0,
+                         static_cast<const bf16_t*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, eps, out, c_all, xhat_h,
+                         rstd_h, gates, xhat_c, rstd_c, hT, cT);
+    else
+      hipLaunchKernelGGL((lnlstm_fwd_wide_kernel<384, 768, float>), dim3(B), dim3(768), 0, s, xp, h0, c0,
+                         static_cast<const float*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, eps, out, c_all, xhat_h,
+                         rstd_h, gates, xhat_c, rstd_c, hT, cT);
+  }
   else if (H == 32)
     fwd_launch<32, 64, 2>(xp, h0, c0, wT, w_dt, lnh_w, lnh_b, lnc_w, lnc_b, T, B, eps, out, c_all, xhat_h, rstd_h,
                           gates, xhat_c, rstd_c, hT, cT, s);
@@ -320,7 +456,7 @@ void lnlstm_bwd(const float* dout, const float* dhT, const float* dcT, const flo
                 int w_dt, const float* lnh_w, const float* lnc_w, int T, int B, int H, float* dgates, float* dhg,
                 float* dc_ln, float* dh0, float* dc0, hipStream_t s) {
   if (H == 384)
-    bwd_launch<384, 384, 4>(dout, dhT, dcT, gates, c_all, xhat_c, rstd_c, xhat_h, rstd_h, w, w_dt, lnh_w, lnc_w, T, B,
+    bwd_launch<384, 768, 2>(dout, dhT, dcT, gates, c_all, xhat_c, rstd_c, xhat_h, rstd_h, w, w_dt, lnh_w, lnc_w, T, B,
                             dgates, dhg, dc_ln, dh0, dc0, s);
   else if (H == 32)
     bwd_launch<32, 64, 2>(dout, dhT, dcT, gates, c_all, xhat_c, rstd_c, xhat_h, rstd_h, w, w_dt, lnh_w, lnc_w, T, B,
