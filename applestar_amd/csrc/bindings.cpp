@@ -417,6 +417,41 @@ void segment_copy(const at::Tensor& arena, const at::Tensor& out, const at::Tens
   as::segment_copy(arena.data_ptr<uint8_t>(), out.data_ptr<uint8_t>(), seg.data_ptr<int64_t>(), seg.size(0), stream());
 }
 
+
+// ---------------------------------------------------------------- fused upsample x2 + conv3x3 -> 1 channel
+at::Tensor upconv1_fwd(const at::Tensor& x_nhwc, const at::Tensor& w, const at::Tensor& bias) {
+  check_cuda(x_nhwc, "x");
+  check_cuda(w, "w");
+  TORCH_CHECK(x_nhwc.dim() == 4 && x_nhwc.size(3) == as::upconv1_channels(), "upconv1: x must be NHWC [B,H,W,32]");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.numel() == as::upconv1_channels() * 9, "upconv1: w fp32 [32*9]");
+  check_cuda(bias, "bias");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() == 1, "upconv1: bias fp32 [1]");
+  const int64_t B = x_nhwc.size(0), H = x_nhwc.size(1), W = x_nhwc.size(2);
+  c10::hip::HIPGuard g(x_nhwc.device().index());
+  auto y = at::empty({B, 2 * H, 2 * W}, x_nhwc.options().dtype(at::kFloat));
+  as::upconv1_fwd(x_nhwc.data_ptr(), dt(x_nhwc), w.data_ptr<float>(), bias.data_ptr<float>(), y.data_ptr<float>(),
+                  static_cast<int>(B), static_cast<int>(H), static_cast<int>(W), stream());
+  return y;
+}
+
+std::vector<at::Tensor> upconv1_bwd(const at::Tensor& x_nhwc, const at::Tensor& w, const at::Tensor& dy) {
+  check_cuda(x_nhwc, "x");
+  check_cuda(w, "w");
+  check_cuda(dy, "dy");
+  const int64_t B = x_nhwc.size(0), H = x_nhwc.size(1), W = x_nhwc.size(2);
+  TORCH_CHECK(x_nhwc.size(3) == as::upconv1_channels(), "upconv1_bwd: channels");
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && dy.numel() == B * 4 * H * W, "upconv1_bwd: dy [B,2H,2W] fp32");
+  c10::hip::HIPGuard g(x_nhwc.device().index());
+  auto dx = at::empty_like(x_nhwc);
+  const int64_t tiles = as::upconv1_tiles(static_cast<int>(B), static_cast<int>(H), static_cast<int>(W));
+  auto part = at::empty({tiles, as::upconv1_channels() * 9 + 1}, dy.options());
+  auto dwb = at::empty({as::upconv1_channels() * 9 + 1}, dy.options());
+  as::upconv1_bwd(x_nhwc.data_ptr(), dt(x_nhwc), w.data_ptr<float>(), dy.data_ptr<float>(), dx.data_ptr(),
+                  part.data_ptr<float>(), dwb.data_ptr<float>(), static_cast<int>(B), static_cast<int>(H),
+                  static_cast<int>(W), stream());
+  return {dx, dwb};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -439,4 +474,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("varlen_attn_bwd", &varlen_attn_bwd);
   m.def("su_sample", &su_sample);
   m.def("segment_copy", &segment_copy);
+  m.def("upconv1_fwd", &upconv1_fwd);
+  m.def("upconv1_bwd", &upconv1_bwd);
 }

@@ -123,3 +123,15 @@ namespace as {
 // seg [nseg, 3] int64 = (src byte offset in arena, dst byte offset in out, byte count)
 void segment_copy(const uint8_t* arena, uint8_t* out, const int64_t* seg, long nseg, hipStream_t s);
 }  // namespace as
+
+namespace as {
+// ---- upconv.hip --------------------------------------------------------------------------------
+// y [B, 2Hl, 2Wl] fp32 = conv3x3(upsample_bilinear_x2(x), w[32,3,3]) + bias; x NHWC [B,Hl,Wl,32]
+int upconv1_channels();
+long upconv1_tiles(int B, int Hl, int Wl);
+void upconv1_fwd(const void* x, int x_dt, const float* w, const float* bias, float* y, int B, int Hl, int Wl,
+                 hipStream_t s);
+// dx NHWC (x's dtype), dwb [289] = (dW[32*9], db); part [upconv1_tiles, 289] scratch
+void upconv1_bwd(const void* x, int x_dt, const float* w, const float* dy, void* dx, float* part, float* dwb, int B,
+                 int Hl, int Wl, hipStream_t s);
+}  // namespace as

@@ -301,9 +301,10 @@ class LocationHead(nn.Module):
         x = self.conv1(x)
         for i, blk in enumerate(self.res):
             x = blk(x + map_skip[len(map_skip) - 1 - i])
-        for conv in self.upsample:
+        for conv in self.upsample[:-1]:
             x = conv(ops.upsample2x(x))
-        logits = x.reshape(B, -1).float() / temperature
+        last = self.upsample[-1][0]  # 32 -> 1: fused upsample + conv, the 32-ch map never hits HBM
+        logits = ops.upsample_conv_out(x, last.weight, last.bias) / temperature
         if location is None:
             location = sample_from_logits(logits, u)
         return logits, location

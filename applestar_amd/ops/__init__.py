@@ -17,7 +17,8 @@ from . import reference as ref
 from . import _ext
 
 __all__ = ['linear', 'layer_norm', 'conv2d', 'gated_residual', 'lnlstm_layer', 'varlen_attention',
-           'masked_attention', 'scatter_connection', 'sequence_mask', 'native_enabled', 'set_native', 'upsample2x']
+           'masked_attention', 'scatter_connection', 'sequence_mask', 'native_enabled', 'set_native', 'upsample2x',
+           'upsample_conv_out']
 
 _NATIVE_ENABLED = True
 
@@ -94,3 +95,13 @@ def upsample2x(x):
     if n is not None and n.has('upsample2x') and x.shape[1] % 4 == 0:
         return n.upsample2x(x)
     return F.interpolate(x, scale_factor=2.0, mode='bilinear', align_corners=False)
+
+
+def upsample_conv_out(x, w, b):
+    """conv3x3(bilinear_x2(x), w, b, padding=1) with ONE output channel, flattened to [B, 4HW] fp32
+    (the location head's last stage, action_arg_head.py:445-450).  Fused on the GPU for 32 channels."""
+    n = _native(x)
+    if n is not None and n.has('upsample_conv_out') and tuple(w.shape) == (1, 32, 3, 3):
+        return n.upsample_conv_out(x, w, b)
+    y = ref.conv2d(upsample2x(x), w, b, 1, 1)
+    return y.reshape(x.shape[0], -1).float()

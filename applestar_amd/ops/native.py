@@ -21,7 +21,7 @@ def ensure_loaded():
 
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
-                'spatial_embed', 'varlen_attention', 'su_sample'}
+                'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out'}
 
 
 def has(name: str) -> bool:
@@ -312,3 +312,32 @@ def su_sample(key, c0, u, entity_num, su_mask, wf_bf16, bf, wq2, bq2, cell, we1,
                        f(cell.layernorm_h.weight), f(cell.layernorm_h.bias), f(cell.layernorm_c.weight),
                        f(cell.layernorm_c.bias), f(we1), f(be1), float(temperature), 1e-5, int(max_steps),
                        bool(extra_units))
+
+
+# ---------------------------------------------------------------------------- upsample x2 + conv -> 1 ch
+class _UpsampleConvOut(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_nhwc, w, b):
+        w32 = w.detach().float().reshape(-1).contiguous()
+        bias = b.detach().float().reshape(1).contiguous() if b is not None else w32.new_zeros(1)
+        y = _C.upconv1_fwd(x_nhwc, w32, bias)
+        ctx.save_for_backward(x_nhwc, w32)
+        ctx.has_bias = b is not None
+        ctx.w_shape, ctx.w_dtype = w.shape, w.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x_nhwc, w32 = ctx.saved_tensors
+        dx, dwb = _C.upconv1_bwd(x_nhwc, w32, dy.float().contiguous())
+        dw = dwb[:-1].view(ctx.w_shape).to(ctx.w_dtype)
+        db = dwb[-1:].to(ctx.w_dtype) if ctx.has_bias else None
+        return dx, dw, db
+
+
+def upsample_conv_out(x, weight, bias):
+    """conv3x3(upsample_bilinear_x2(x), weight[1,32,3,3], padding 1) + bias for [B,32,H,W] -> [B,2H*2W]
+    fp32 logits, fused (the 32-channel upsampled map never reaches HBM)."""
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    return _UpsampleConvOut.apply(nhwc(x), weight, bias).reshape(x.shape[0], -1)

@@ -255,3 +255,29 @@ def test_su_sample_kernel_matches_teacher_forcing_and_torch_sampler():
             ops.set_native(True)
         same = sum(int(torch.equal(res[b, :int(su_num[b])], res2[b, :int(su2[b])])) for b in range(B))
         assert same >= B - 1, (same, B)
+
+
+@pytest.mark.parametrize('H,W,dtype', [(76, 80, torch.float32), (76, 80, torch.bfloat16), (5, 9, torch.float32),
+                                       (1, 1, torch.float32)])
+def test_upsample_conv_out_matches_interpolate_conv(H, W, dtype):
+    """Fused bilinear x2 + conv3x3 (32 -> 1) vs F.interpolate + F.conv2d in fp32: output, dx, dw, db."""
+    torch.manual_seed(11)
+    B = 3
+    x = torch.randn(B, 32, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    w = (torch.randn(1, 32, 3, 3, device=DEV) * 0.2).requires_grad_()
+    b = (torch.randn(1, device=DEV) * 0.1).requires_grad_()
+    xr, wr, br = (t.detach().float().clone().requires_grad_() for t in (x, w, b))
+    y = N.upsample_conv_out(x, w, b)
+    up = torch.nn.functional.interpolate(xr, scale_factor=2.0, mode='bilinear', align_corners=False)
+    yr = torch.nn.functional.conv2d(up, wr, br, padding=1).reshape(B, -1)
+    assert y.shape == yr.shape and y.dtype == torch.float32
+    tol = 1e-4 if dtype == torch.float32 else 1e-2
+    assert _err(y, yr) < tol
+    g = torch.randn_like(yr)
+    y.backward(g)
+    yr.backward(g)
+    rel = lambda a, r: _err(a, r) / max(1.0, r.abs().max().item())
+    assert rel(x.grad.float(), xr.grad) < tol * 10
+    assert rel(w.grad, wr.grad) < tol * 10
+    assert rel(b.grad, br.grad) < tol * 10
