@@ -419,11 +419,19 @@ void segment_copy(const at::Tensor& arena, const at::Tensor& out, const at::Tens
 
 
 // ---------------------------------------------------------------- fused upsample x2 + conv3x3 -> 1 channel
+void check_upconv_x(const at::Tensor& x) {
+  TORCH_CHECK(x.dim() == 4 && x.size(3) == as::upconv1_channels() && x.is_contiguous(),
+              "upconv1: x must be contiguous NHWC [B,H,W,32]");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "upconv1: x fp32 or bf16");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "upconv1: x must be 16-byte aligned");
+}
+
 at::Tensor upconv1_fwd(const at::Tensor& x_nhwc, const at::Tensor& w, const at::Tensor& bias) {
   check_cuda(x_nhwc, "x");
   check_cuda(w, "w");
-  TORCH_CHECK(x_nhwc.dim() == 4 && x_nhwc.size(3) == as::upconv1_channels(), "upconv1: x must be NHWC [B,H,W,32]");
-  TORCH_CHECK(w.scalar_type() == at::kFloat && w.numel() == as::upconv1_channels() * 9, "upconv1: w fp32 [32*9]");
+  check_upconv_x(x_nhwc);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == as::upconv1_channels() * 9,
+              "upconv1: w fp32 contiguous [32*9]");
   check_cuda(bias, "bias");
   TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() == 1, "upconv1: bias fp32 [1]");
   const int64_t B = x_nhwc.size(0), H = x_nhwc.size(1), W = x_nhwc.size(2);
@@ -439,8 +447,11 @@ std::vector<at::Tensor> upconv1_bwd(const at::Tensor& x_nhwc, const at::Tensor& 
   check_cuda(w, "w");
   check_cuda(dy, "dy");
   const int64_t B = x_nhwc.size(0), H = x_nhwc.size(1), W = x_nhwc.size(2);
-  TORCH_CHECK(x_nhwc.size(3) == as::upconv1_channels(), "upconv1_bwd: channels");
-  TORCH_CHECK(dy.scalar_type() == at::kFloat && dy.numel() == B * 4 * H * W, "upconv1_bwd: dy [B,2H,2W] fp32");
+  check_upconv_x(x_nhwc);
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.is_contiguous() && w.numel() == as::upconv1_channels() * 9,
+              "upconv1_bwd: w fp32 contiguous [32*9]");
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && dy.is_contiguous() && dy.numel() == B * 4 * H * W,
+              "upconv1_bwd: dy contiguous [B,2H,2W] fp32");
   c10::hip::HIPGuard g(x_nhwc.device().index());
   auto dx = at::empty_like(x_nhwc);
   const int64_t tiles = as::upconv1_tiles(static_cast<int>(B), static_cast<int>(H), static_cast<int>(W));
