@@ -19,7 +19,7 @@ import torch.nn.functional as F
 
 from .. import ops
 from ..lib import game_data as gd
-from ..lib.features import (ENTITY_FIELDS, SPATIAL_ONE_HOT, EFFECT_KEYS, SPATIAL_SIZE, ENTITY_EMBED_DIM,
+from ..lib.features import (MAX_ENTITY_NUM, ENTITY_FIELDS, SPATIAL_ONE_HOT, EFFECT_KEYS, SPATIAL_SIZE, ENTITY_EMBED_DIM,
                             BEGINNING_ORDER_LENGTH)
 from .blocks import FCBlock, ConvBlock, ResBlock, OneHotTable, binary_table, eye_table
 from .transformer import Transformer
@@ -168,6 +168,12 @@ class EntityEncoder(nn.Module):
         self.entity_fc = FCBlock(256, 256, act=True)
         self.embed_fc = FCBlock(256, 256, act=True)
         self.reduce_type = reduce_type
+        if reduce_type.startswith('attention_pool'):  # entity_encoder.py:54-57
+            from .optional import AttentionPool
+            self.attention_pool = AttentionPool(256, 2, 256, max_num=MAX_ENTITY_NUM + 1
+                                                if reduce_type == 'attention_pool_add_num' else None)
+        elif reduce_type not in ('entity_num', 'selected_units_num', 'constant'):
+            raise NotImplementedError(f'entity_reduce_type {reduce_type!r}')
 
     def embed(self, entity_info, flat_index):
         lin = self.transformer.embedding[0]
@@ -190,6 +196,10 @@ class EntityEncoder(nn.Module):
         ee = self.entity_fc(x)
         entity_embeddings = ee.new_zeros(B * N, ee.shape[-1])
         entity_embeddings = entity_embeddings.index_copy(0, flat_index, ee).view(B, N, -1)
+        if self.reduce_type.startswith('attention_pool'):
+            xp = x.new_zeros(B * N, x.shape[-1]).index_copy(0, flat_index, x).view(B, N, -1)
+            pooled = self.attention_pool(xp, num=entity_num, mask=valid)
+            return entity_embeddings, self.embed_fc(pooled.to(x.dtype)), valid
         # masked mean of relu(transformer output) over real entities (entity_encoder.py:85-87)
         seg = torch.repeat_interleave(torch.arange(B, device=x.device), lens.long(), output_size=x.shape[0])
         summed = x.new_zeros(B, x.shape[-1]).index_add(0, seg, x)

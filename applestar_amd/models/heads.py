@@ -107,9 +107,15 @@ class QueuedHead(_ArgMLPHead):
 class SelectedUnitsHead(nn.Module):
     """Pointer network over entities + end token (action_arg_head.py:89-328)."""
 
+    REDUCE_TYPES = ('selected_units_num', 'attention_pool', 'attention_pool_add_num')
+
     def __init__(self, input_dim=1024, entity_dim=256, key_dim=32, func_dim=256, hidden_dim=32, num_layers=1,
-                 extra_units: bool = False):
+                 extra_units: bool = False, reduce_type: str = 'selected_units_num'):
         super().__init__()
+        # 'entity_num' / 'constant' call an undefined embed_fc in the reference (action_arg_head.py:130-135)
+        if reduce_type not in self.REDUCE_TYPES:
+            raise NotImplementedError(f'selected-units entity_reduce_type {reduce_type!r}')
+        self.reduce_type = reduce_type
         self.key_dim = key_dim
         self.key_fc = FCBlock(entity_dim, key_dim)
         self.query_fc1 = FCBlock(input_dim, func_dim, act=True)
@@ -120,6 +126,10 @@ class SelectedUnitsHead(nn.Module):
         self.end_embedding = nn.Parameter(torch.empty(1, key_dim))
         glorot_uniform_(self.end_embedding)
         self.extra_units = extra_units
+        if reduce_type != 'selected_units_num':
+            from .optional import AttentionPool
+            self.attention_pool = AttentionPool(key_dim, 2, input_dim, max_num=MAX_SELECTED_UNITS_NUM + 1
+                                                if reduce_type == 'attention_pool_add_num' else None)
 
     def keys(self, entity_embedding, entity_num):
         """key [B,N+1,32] with the learned end embedding at position entity_num; logits mask."""
@@ -151,12 +161,16 @@ class SelectedUnitsHead(nn.Module):
         earlier = torch.tril(torch.ones(S, S, dtype=torch.bool, device=key.device), -1)
         dup = (same & earlier[None] & added[:, None, :]).any(-1)
         new = added & ~dup
-        gathered = key.gather(1, labels.clamp(max=N1 - 1).unsqueeze(-1).expand(B, S, C))
-        run_sum = torch.cumsum(gathered * new.unsqueeze(-1).to(gathered.dtype), 1)
-        run_cnt = torch.cumsum(new.int(), 1)
-        div = torch.where((selected_units_num != 0)[:, None], run_cnt.clamp(min=1), torch.ones_like(run_cnt))
-        emb = run_sum / div.unsqueeze(-1).to(run_sum.dtype)              # embedding after step i
-        ae_after = self._ae_update(ae0.unsqueeze(1), emb)                # [B,S,1024]
+        if self.reduce_type == 'selected_units_num':
+            gathered = key.gather(1, labels.clamp(max=N1 - 1).unsqueeze(-1).expand(B, S, C))
+            run_sum = torch.cumsum(gathered * new.unsqueeze(-1).to(gathered.dtype), 1)
+            run_cnt = torch.cumsum(new.int(), 1)
+            div = torch.where((selected_units_num != 0)[:, None], run_cnt.clamp(min=1), torch.ones_like(run_cnt))
+            emb = run_sum / div.unsqueeze(-1).to(run_sum.dtype)          # embedding after step i
+            ae_after = self._ae_update(ae0.unsqueeze(1), emb)            # [B,S,1024]
+        else:  # attention pooling over the selected set after each step (prefix softmax, all steps at once)
+            pooled = self.attention_pool.prefix(key, labels.clamp(max=N1 - 1), new)
+            ae_after = ae0.unsqueeze(1) + pooled.to(ae0.dtype)
         ae_in = torch.cat([ae0.unsqueeze(1).to(ae_after.dtype), ae_after[:, :-1]], 1)
         q_in = self.query_fc2(self.query_fc1(ae_in))                     # [B,S,32]
         state = self.lstm.zero_state(B, q_in.device, torch.float32)
@@ -208,7 +222,7 @@ class SelectedUnitsHead(nn.Module):
                        u: Optional[torch.Tensor] = None):
         native = ops._native(entity_embedding)
         if native is not None and native.has('su_sample') and not torch.is_grad_enabled() \
-                and self.lstm.num_layers == 1:
+                and self.lstm.num_layers == 1 and self.reduce_type == 'selected_units_num':
             return self.forward_sample_native(native, ae0, entity_embedding, entity_num, su_mask, temperature, u)
         key, mask = self.keys(entity_embedding, entity_num)
         B, N1, _ = key.shape
@@ -242,10 +256,13 @@ class SelectedUnitsHead(nn.Module):
             logits_list.append(step_logits)
             keep = ~end_flag
             one_hot[ar_b[keep], result[keep]] = 1
-            emb = (key * one_hot.unsqueeze(-1)).sum(1)
-            cnt = one_hot.sum(1, keepdim=True)
-            emb = torch.where(cnt > 0, emb / cnt.clamp(min=1), emb)
-            ae = self._ae_update(ae0, emb)
+            if self.reduce_type == 'selected_units_num':
+                emb = (key * one_hot.unsqueeze(-1)).sum(1)
+                cnt = one_hot.sum(1, keepdim=True)
+                emb = torch.where(cnt > 0, emb / cnt.clamp(min=1), emb)
+                ae = self._ae_update(ae0, emb)
+            else:
+                ae = ae0 + self.attention_pool(key, num=one_hot.sum(1), mask=one_hot).to(ae0.dtype)
             if bool(end_flag.all()):
                 break
         extra = torch.zeros(B, MAX_ENTITY_NUM + 1, device=dev)

@@ -61,12 +61,12 @@ class ValueBaseline(nn.Module):
 
 
 class Policy(nn.Module):
-    def __init__(self, extra_units: bool = False):
+    def __init__(self, extra_units: bool = False, entity_reduce_type: str = 'selected_units_num'):
         super().__init__()
         self.action_type_head = ActionTypeHead()
         self.delay_head = DelayHead()
         self.queued_head = QueuedHead()
-        self.selected_units_head = SelectedUnitsHead(extra_units=extra_units)
+        self.selected_units_head = SelectedUnitsHead(extra_units=extra_units, reduce_type=entity_reduce_type)
         self.target_unit_head = TargetUnitHead()
         self.location_head = LocationHead()
 
@@ -115,7 +115,8 @@ class Model(nn.Module):
         self.cfg = mcfg
         self.temperature = float(mcfg.temperature)
         self.encoder = Encoder(mcfg.entity_reduce_type)
-        self.policy = Policy(extra_units=bool(self.whole_cfg.get('agent', {}).get('extra_units', False)))
+        self.policy = Policy(extra_units=bool(self.whole_cfg.get('agent', {}).get('extra_units', False)),
+                             entity_reduce_type=mcfg.entity_reduce_type)
         self._use_value_feature = bool(self.whole_cfg.learner.get('use_value_feature', False))
         self.use_value_network = use_value_network
         if use_value_network:

@@ -85,3 +85,20 @@ def test_rl_learner_forward_matches_reference():
     for k in r['target_logit']:
         _close(r['target_logit'][k], m['target_logit'][k])
     _close(r['value']['winloss'], m['value']['winloss'])
+
+
+@pytest.mark.parametrize('reduce_type', ['attention_pool', 'attention_pool_add_num'])
+def test_attention_pool_selected_units_match_reference(reduce_type):
+    """entity_reduce_type attention variants: our prefix-softmax (all steps at once) vs the reference's
+    per-step masked attention pooling (action_arg_head.py:201-206)."""
+    rm, mm = _pair({'model': {'entity_reduce_type': reduce_type}}, use_value_network=False)
+    assert 'policy.head.selected_units_head.attention_pool.queries' in mm.state_dict() or \
+        any('attention_pool.queries' in k for k in mm.state_dict())
+    obs, act, su_num, hidden = _inputs(B=4, seed=3)
+    with torch.no_grad():
+        r = rm.compute_teacher_logit(**copy.deepcopy(obs), hidden_state=copy.deepcopy(hidden),
+                                     selected_units_num=su_num.clone(), action_info=copy.deepcopy(act))
+        m = mm.compute_teacher_logit(**copy.deepcopy(obs), hidden_state=copy.deepcopy(hidden),
+                                     selected_units_num=su_num.clone(), action_info=copy.deepcopy(act))
+    for k in ['selected_units', 'target_unit', 'target_location']:
+        _close(r['logit'][k], m['logit'][k], atol=5e-4, rtol=5e-4)
