@@ -13,6 +13,7 @@ from typing import Dict, Optional
 
 import torch
 
+from ..utils.optim import build_optimizer
 from ..models.model import Model
 from ..parallel import dist as pdist
 from ..parallel.dp import GradientReducer
@@ -80,8 +81,7 @@ class RLTrainer:
     def reset_optimizer(self):
         """Fresh Adam(betas=(0, 0.99), eps=1e-5) state (also used after a league reset)."""
         lc = self.cfg.learner
-        self.optimizer = torch.optim.Adam(self.opt_params, lr=lc.learning_rate, betas=(0.0, 0.99), eps=1e-5,
-                                          weight_decay=lc.weight_decay, fused=self.device.type == 'cuda')
+        self.optimizer = build_optimizer(self.opt_params, lc, betas=(0.0, 0.99), eps=1e-5, device=self.device)
         self.lr_scheduler = None
 
     def _value_pretrain_toggle(self):

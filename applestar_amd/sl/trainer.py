@@ -9,6 +9,7 @@ from typing import Dict, Optional
 
 import torch
 
+from ..utils.optim import build_optimizer
 from ..models.model import Model
 from ..parallel import dist as pdist
 from ..parallel.dp import GradientReducer
@@ -43,8 +44,7 @@ class SLTrainer:
         pdist.broadcast_module(self.model)
         self.params = [p for p in self.model.parameters() if p.requires_grad]
         self.reducer = GradientReducer(self.params, bucket_mb=lc.bucket_mb)
-        self.optimizer = torch.optim.Adam(self.params, lr=lc.learning_rate, weight_decay=lc.weight_decay,
-                                          fused=self.device.type == 'cuda')
+        self.optimizer = build_optimizer(self.params, lc, device=self.device)
         self.lr_scheduler = build_lr_scheduler(self.optimizer, lc.lr_scheduler)
         self.grad_clip = build_grad_clip(lc.grad_clip)
         self.loss = SupervisedLoss(lc)
