@@ -130,3 +130,69 @@ def broadcast_object(obj, src: int = 0):
     lst = [obj]
     dist.broadcast_object_list(lst, src)
     return lst[0]
+
+
+# ---------------------------------------------------------------------------------------------- extras
+def allreduce(x: torch.Tensor, average: bool = True, group=None) -> torch.Tensor:
+    """In-place all-reduce (``dist_helper.py:272-289``); AVG is done inside RCCL on the nccl backend."""
+    if not is_initialized() or dist.get_world_size(group) == 1:
+        return x
+    if average and dist.get_backend(group) == 'nccl':
+        dist.all_reduce(x, op=dist.ReduceOp.AVG, group=group)
+    else:
+        dist.all_reduce(x, group=group)
+        if average:
+            x.div_(dist.get_world_size(group))
+    return x
+
+
+def broadcast(x: torch.Tensor, src: int = 0, group=None) -> torch.Tensor:
+    if is_initialized():
+        dist.broadcast(x, src, group=group)
+    return x
+
+
+def simple_group_split(world_size: int, rank: int, num_groups: int):
+    """Create ``num_groups`` process groups of consecutive ranks (every rank must call this with the same
+    arguments, as ``new_group`` is collective) and return the one containing ``rank``
+    (``dist_helper.py:292-366``)."""
+    assert world_size % num_groups == 0, (world_size, num_groups)
+    size = world_size // num_groups
+    groups = [dist.new_group(list(range(i * size, (i + 1) * size))) for i in range(num_groups)]
+    return groups[rank // size]
+
+
+def get_group(group_size: int):
+    """Process group of ``group_size`` consecutive ranks containing this rank (None when not distributed)."""
+    if not is_initialized():
+        return None
+    world = get_world_size()
+    return simple_group_split(world, get_rank(), world // group_size)
+
+
+def _slurm_master(nodelist: str) -> str:
+    """First host of a SLURM nodelist such as ``node[03-05,07],gpu1`` -> ``node03``."""
+    head = nodelist.split(',')[0] if '[' not in nodelist.split(',')[0] else nodelist[:nodelist.index(']') + 1]
+    if '[' in head:
+        prefix, rng = head.split('[', 1)
+        first = rng.rstrip(']').split(',')[0].split('-')[0]
+        return prefix + first
+    return head
+
+
+def init_from_method(method: str = 'torch', port: int = 29500, backend: Optional[str] = None) -> tuple:
+    """``dist_init(method)`` of the reference (``dist_helper.py:321-344``): 'torch' (torchrun env),
+    'single_node' (RANK/WORLD_SIZE with 127.0.0.1) or 'slurm' (SLURM_PROCID/SLURM_NTASKS/SLURM_LOCALID,
+    master = first node of SLURM_NODELIST)."""
+    if method == 'slurm':
+        os.environ.setdefault('RANK', os.environ['SLURM_PROCID'])
+        os.environ.setdefault('WORLD_SIZE', os.environ['SLURM_NTASKS'])
+        os.environ.setdefault('LOCAL_RANK', os.environ.get('SLURM_LOCALID', '0'))
+        os.environ.setdefault('MASTER_ADDR', _slurm_master(os.environ.get('SLURM_NODELIST', '127.0.0.1')))
+        os.environ.setdefault('MASTER_PORT', str(port))
+    elif method == 'single_node':
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', str(port))
+    elif method != 'torch':
+        raise ValueError(f'unknown dist init method {method!r}')
+    return init(backend=backend)

@@ -121,3 +121,53 @@ def test_master_weights_world2():
         assert np.array_equal(s0[k], s1[k]), k
     # the update moved every weight by lr * averaged grad (non-zero)
     assert all(np.abs(s0[k] - ref[k]).max() > 0 for k in ('fc1.weight', 'fc2.weight', 'conv.weight', 'ln.weight'))
+
+
+def _distmodule_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from applestar_amd.parallel import dist as pdist
+    from applestar_amd.parallel.dist_module import DistModule
+    pdist.init_from_method('single_node', port=port, backend='gloo')
+    torch.manual_seed(rank)
+    dm = DistModule(_Tiny(), bucket_mb=0.0005)
+    torch.manual_seed(200 + rank)
+    x, img = torch.randn(5, 6), torch.randn(2, 2, 5, 5)
+    dm.zero_grad()
+    dm(x, img).backward()
+    dm.sync_gradients()
+    # single-process reference: mean of the two ranks' gradients on the same (broadcast) weights
+    ref = _Tiny()
+    ref.load_state_dict(dm.state_dict())
+    tot = [torch.zeros_like(p) for p in ref.parameters()]
+    for r in range(world):
+        torch.manual_seed(200 + r)
+        xr, ir = torch.randn(5, 6), torch.randn(2, 2, 5, 5)
+        ref.zero_grad()
+        ref(xr, ir).backward()
+        tot = [t + p.grad / world for t, p in zip(tot, ref.parameters())]
+    ok = all(torch.allclose(p.grad, t, atol=1e-5) for p, t in zip(dm.parameters(), tot))
+    grp = pdist.get_group(1)  # world split into singleton groups
+    v = torch.tensor([float(rank + 1)])
+    pdist.allreduce(v, group=grp)   # singleton group: unchanged
+    w = torch.tensor([float(rank + 1)])
+    pdist.allreduce(w)              # world: mean 1.5
+    q.put((rank, ok, list(dm.state_dict())[:2], float(v), float(w), pdist._slurm_master('gpu[07-09,12],x')))
+    pdist.finalize()
+
+
+def test_dist_module_and_groups_world2():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_distmodule_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, keys, v, w, master in res:
+        assert ok
+        assert keys == ['fc1.weight', 'fc1.bias']
+        assert v == rank + 1 and abs(w - 1.5) < 1e-6
+        assert master == 'gpu07'
