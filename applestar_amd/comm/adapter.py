@@ -33,12 +33,18 @@ _LEN = struct.Struct('<Q')
 
 # ----------------------------------------------------------------------------- coordinator
 class Coordinator:
-    def __init__(self, maxlen: int = 1000):
+    def __init__(self, maxlen: int = 1000, host: str = '127.0.0.1'):
         self._lock = threading.Lock()
         self._meta: Dict[str, deque] = defaultdict(partial(deque, maxlen=maxlen))
         self._broadcast: Dict[str, dict] = {}
         self.push_count = defaultdict(int)
         self.pull_count = defaultdict(int)
+        self._host = host
+        # metadata shards ("workers", coordinator.py:20-57,156-165) and stream-server registry
+        self._workers: Dict[str, List[dict]] = defaultdict(list)
+        self._worker_servers = []
+        self._servers = {'put': defaultdict(list), 'get': defaultdict(list)}
+        self._remove_count = defaultdict(int)
 
     def push(self, info: dict) -> bool:
         token = info['token']
@@ -61,6 +67,53 @@ class Coordinator:
             self.pull_count[token] += len(out)
             return out
 
+    def start_worker(self, token: str, worker_num: int) -> List[dict]:
+        """Shard ``token``'s metadata over ``worker_num`` extra brokers (maxlen 256 each, as the
+        reference's workers); idempotent per token.  Each shard is its own HTTP server thread."""
+        with self._lock:
+            if not self._workers[token]:
+                for _ in range(int(worker_num)):
+                    srv = serve_coordinator(Coordinator(maxlen=256), host=self._host, port=0)
+                    self._worker_servers.append(srv)
+                    self._workers[token].append({'ip': self._host, 'port': srv.server_address[1]})
+            return list(self._workers[token])
+
+    def register(self, info: dict):
+        """Stream-channel registry (coordinator.py:75-109): a server registers itself under
+        (token, type); a client asks for the servers of the opposite type."""
+        info = dict(info)
+        typ, token = info.pop('type'), info.pop('token')
+        server = info.pop('server', typ == 'get')
+        with self._lock:
+            if server:
+                entry = {'ip': info['ip'], 'port': int(info['port'])}
+                if entry not in self._servers[typ][token]:
+                    self._servers[typ][token].append(entry)
+                return True
+            other = 'get' if typ == 'put' else 'put'
+            return list(self._servers[other][token]) or False
+
+    def remove_server(self, info: dict) -> bool:
+        """A client reports an unreachable server; it is dropped after 5 reports (coordinator.py:111-124)."""
+        typ = 'put' if info['type'] == 'get' else 'get'
+        entry = {'ip': info['ip'], 'port': int(info['port'])}
+        with self._lock:
+            lst = self._servers[typ][info['token']]
+            if entry in lst:
+                key = f"{entry['ip']}:{entry['port']}"
+                self._remove_count[key] += 1
+                if self._remove_count[key] > 5:
+                    lst.remove(entry)
+                    self._remove_count.pop(key)
+                    return True
+        return False
+
+    def close_workers(self):
+        for srv in self._worker_servers:
+            srv.shutdown()
+            srv.server_close()
+        self._worker_servers = []
+
     def stats(self) -> dict:
         with self._lock:
             return {'queued': {k: len(v) for k, v in self._meta.items()},
@@ -69,6 +122,8 @@ class Coordinator:
 
 
 def serve_coordinator(coord: Coordinator, host: str = '0.0.0.0', port: int = 0) -> ThreadingHTTPServer:
+    if host not in ('0.0.0.0', ''):
+        coord._host = host
     class Handler(BaseHTTPRequestHandler):
         def log_message(self, *a):
             pass
@@ -88,6 +143,12 @@ def serve_coordinator(coord: Coordinator, host: str = '0.0.0.0', port: int = 0) 
                 self._reply(coord.push(req))
             elif self.path == '/coordinator/pull':
                 self._reply(coord.pull(req['token'], int(req.get('size', 1))))
+            elif self.path == '/coordinator/start_worker':
+                self._reply(coord.start_worker(req['token'], int(req['worker_num'])))
+            elif self.path == '/coordinator/register':
+                self._reply(coord.register(req))
+            elif self.path == '/coordinator/remove_server':
+                self._reply(coord.remove_server(req))
             else:
                 self.send_error(404)
 
@@ -227,6 +288,7 @@ class Adapter:
         self._compress = compress
         self._server: Optional[_PayloadServer] = None
         self._broadcast_keys: Dict[str, str] = {}
+        self._worker_addr: Dict[str, List[tuple]] = {}
 
     def _local_ip(self) -> str:
         if self._cip in ('127.0.0.1', 'localhost'):
@@ -238,7 +300,18 @@ class Adapter:
         finally:
             s.close()
 
-    def push(self, data: Any, token: str, broadcast: bool = False, retries: int = 20) -> str:
+    def _shards(self, token: str, worker_num: Optional[int]) -> List[tuple]:
+        """Metadata brokers for ``token``: the coordinator itself, or its ``worker_num`` shards."""
+        if not worker_num:
+            return [(self._cip, self._cport)]
+        if token not in self._worker_addr:
+            ws = _post_json(self._cip, self._cport, '/coordinator/start_worker',
+                            {'token': token, 'worker_num': int(worker_num)})
+            self._worker_addr[token] = [(w['ip'], int(w['port'])) for w in ws]
+        return self._worker_addr[token]
+
+    def push(self, data: Any, token: str, broadcast: bool = False, retries: int = 20,
+             worker_num: Optional[int] = None) -> str:
         if self._server is None:
             self._server = _PayloadServer('0.0.0.0' if self._ip != '127.0.0.1' else '127.0.0.1')
         payload = data if isinstance(data, (bytes, bytearray)) else serialize.dumps(data, compress=self._compress)
@@ -246,9 +319,11 @@ class Adapter:
         self._server.put(key, bytes(payload), keep=broadcast)
         meta = {'token': token, 'ip': self._ip, 'port': self._server.port, 'key': key, 'size': len(payload),
                 'broadcast': broadcast, 'time': time.time()}
+        shards = self._shards(token, None if broadcast else worker_num)
+        cip, cport = shards[hash(key) % len(shards)]
         for i in range(retries + 1):
             try:
-                _post_json(self._cip, self._cport, '/coordinator/push', meta)
+                _post_json(cip, cport, '/coordinator/push', meta)
                 break
             except (ConnectionError, OSError):
                 if i == retries:
@@ -263,11 +338,16 @@ class Adapter:
         return key
 
     def pull(self, token: str, size: int = 1, block: bool = True, sleep_time: float = 0.05,
-             timeout: Optional[float] = None, raw: bool = False, alloc=None) -> List[Any]:
+             timeout: Optional[float] = None, raw: bool = False, alloc=None,
+             worker_num: Optional[int] = None) -> List[Any]:
         out: List[Any] = []
         t0 = time.time()
+        shards = self._shards(token, worker_num)
+        turn = 0
         while len(out) < size:
-            metas = _post_json(self._cip, self._cport, '/coordinator/pull', {'token': token, 'size': size - len(out)})
+            cip, cport = shards[turn % len(shards)]
+            turn += 1
+            metas = _post_json(cip, cport, '/coordinator/pull', {'token': token, 'size': size - len(out)})
             for m in metas:
                 try:
                     data = fetch(m['ip'], m['port'], m['key'], alloc=alloc)
@@ -277,9 +357,12 @@ class Adapter:
                     out.append(data if raw else serialize.loads(data))
                 if m.get('broadcast'):
                     return out
-            if len(out) >= size or not block or (timeout is not None and time.time() - t0 > timeout):
+            if len(out) >= size or (timeout is not None and time.time() - t0 > timeout):
                 break
-            time.sleep(sleep_time)
+            if turn % len(shards) == 0:  # every shard visited once this round
+                if not block:
+                    break
+                time.sleep(sleep_time)
         return out
 
     def stats(self) -> dict:

@@ -31,7 +31,8 @@ from .lstm import LNLSTMCell, StackedLNLSTM, _Layer
 
 __all__ = ['AttentionPool', 'FiLM', 'FiLMedResBlock', 'NormLSTM', 'PytorchLSTM', 'get_lstm', 'LSTMCell',
            'RecurrentStack', 'BidirLayer', 'script_lstm', 'script_lnlstm', 'build_normalization', 'conv2d_block',
-           'deconv2d_block', 'fc_block', 'fc_block2', 'GroupSyncBatchNorm']
+           'deconv2d_block', 'fc_block', 'fc_block2', 'GroupSyncBatchNorm', 'SoftArgmax', 'ScatterConnection',
+           'Swish', 'build_activation']
 
 
 # ---------------------------------------------------------------------------------------------- pooling
@@ -463,3 +464,58 @@ def script_lnlstm(input_size, hidden_size, num_layers, bias=True, batch_first=Fa
     if not bidirectional:
         return StackedLNLSTM(input_size, hidden_size, num_layers)
     return RecurrentStack(_Layer, input_size, hidden_size, num_layers, bidirectional=True)
+
+
+# ---------------------------------------------------------------------------------------------- misc
+class SoftArgmax(nn.Module):
+    """Expected (y, x) location under softmax of a 1-channel heat map [B,1,H,W] -> [B,2]
+    (``torch_utils/network/soft_argmax.py``)."""
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        assert C == 1
+        p = torch.softmax(x.reshape(B, -1).float(), -1).view(B, H, W)
+        ys = torch.arange(H, device=x.device, dtype=p.dtype)
+        xs = torch.arange(W, device=x.device, dtype=p.dtype)
+        return torch.stack([(p.sum(2) * ys).sum(1), (p.sum(1) * xs).sum(1)], 1).to(x.dtype)
+
+
+class ScatterConnection(nn.Module):
+    """Scatter per-entity features [B,M,N] to a [B,N,H,W] map at (y, x) locations [B,M,2]
+    (``torch_utils/network/scatter_connection.py``).  'add' sums collisions, 'cover' keeps one."""
+
+    def __init__(self, scatter_type: str):
+        super().__init__()
+        assert scatter_type in ('cover', 'add')
+        self.scatter_type = scatter_type
+
+    def forward(self, x, spatial_size, location):
+        B, M, N = x.shape
+        H, W = spatial_size
+        idx = (location[..., 0].long() * W + location[..., 1].long()) + \
+            torch.arange(B, device=x.device)[:, None] * (H * W)
+        out = x.new_zeros(B * H * W, N)
+        flat = idx.reshape(-1)
+        if self.scatter_type == 'add':
+            out.index_add_(0, flat, x.reshape(-1, N))
+        else:
+            out.index_copy_(0, flat, x.reshape(-1, N))
+        return out.view(B, H, W, N).permute(0, 3, 1, 2)
+
+
+class Swish(nn.Module):
+    def forward(self, x):
+        return x * torch.sigmoid(x)
+
+
+def build_activation(activation: str, inplace: Optional[bool] = None):
+    """Activation by name (``torch_utils/network/activation.py:72``); 'glu' returns the GLU class."""
+    from .blocks import GLU
+    if inplace is not None:
+        assert activation == 'relu', f'inplace is not compatible with {activation}'
+    table = {'relu': lambda: nn.ReLU(inplace=True if inplace is None else inplace), 'glu': lambda: GLU,
+             'prelu': lambda: nn.PReLU(), 'swish': lambda: Swish(), 'tanh': lambda: nn.Tanh(),
+             'sigmoid': lambda: nn.Sigmoid()}
+    if activation not in table:
+        raise KeyError(f'invalid key for activation: {activation}')
+    return table[activation]()
