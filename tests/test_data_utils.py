@@ -107,3 +107,27 @@ def test_network_misc():
     assert isinstance(build_activation('relu'), torch.nn.ReLU)
     with pytest.raises(KeyError):
         build_activation('nope')
+
+
+@pytest.mark.parametrize('fs_type', ['applestar', 'torch', 'numpy', 'nppickle'])
+@pytest.mark.parametrize('compress', [False, True])
+def test_file_helper_round_trip(tmp_path, fs_type, compress):
+    from applestar_amd.utils import file_helper as F
+    tree = {'obs': {'x': torch.arange(6, dtype=torch.float32).view(2, 3)}, 'steps': [1, 2], 'name': 'traj'}
+    back = F.loads(F.dumps(tree, fs_type, compress), fs_type, compress)
+    x = back['obs']['x']
+    assert np.array_equal(np.asarray(x), np.arange(6, dtype=np.float32).reshape(2, 3))
+    assert list(back['steps']) == [1, 2] and back['name'] == 'traj'
+    if not compress:
+        p = str(tmp_path / f'f.{fs_type}')
+        F.save_file(p, tree, fs_type)
+        assert F.read_file(p, fs_type)['name'] == 'traj'
+        F.remove_file(p)
+
+
+def test_file_helper_refuses_pickle_by_default():
+    from applestar_amd.utils import file_helper as F
+    raw = F.dumps({'a': 1}, 'pickle')
+    with pytest.raises(PermissionError):
+        F.loads(raw, 'pickle')
+    assert F.loads(raw, 'pickle', allow_pickle=True) == {'a': 1}
