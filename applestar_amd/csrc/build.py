@@ -105,7 +105,34 @@ def write_ninja() -> str:
     return path
 
 
+def host_ext_filename() -> str:
+    suffix = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
+    if VARIANT == 'release' and not SANITIZE:
+        return os.path.join(PKG, '_host' + suffix)
+    return os.path.join(BUILD, '_host' + suffix)
+
+
+def build_host() -> str:
+    """Host-only runtime extension (``csrc/host/*.cpp``: shm channels), plain g++ + pybind11, no torch."""
+    import pybind11
+    out = host_ext_filename()
+    srcs = sorted(glob.glob(os.path.join(HERE, 'host', '*.cpp')))
+    deps = srcs + sorted(glob.glob(os.path.join(HERE, 'host', '*.h')))
+    if os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(s) for s in deps):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    flags = ['-O2', '-shared', '-fPIC', '-std=c++17', '-Wall', '-pthread', f'-I{pybind11.get_include()}',
+             f'-I{sysconfig.get_paths()["include"]}']
+    if VARIANT == 'debug':
+        flags += ['-g', '-O0']
+    if SANITIZE:
+        flags += [f'-fsanitize={SANITIZE}', '-fno-omit-frame-pointer', '-g']
+    subprocess.run(['g++', *flags, *srcs, '-o', out, '-lrt'], check=True)
+    return out
+
+
 def build(verbose: bool = False, jobs: int | None = None) -> str:
+    build_host()
     path = write_ninja()
     ninja = shutil.which('ninja')
     if ninja is None:
