@@ -1,0 +1,248 @@
+// 3x3 / stride 1 / pad 1 convolution as an implicit GEMM on the MFMA matrix cores (gfx950), NHWC bf16,
+// with the bias, residual add and ReLU fused into the epilogue.  SURVEY K7/K8: the spatial-encoder
+// downsample convs and ResBlocks (spatial_encoder.py:74-86, res_block.py:50-65), the location head's
+// gated res-blocks and upsample convs (action_arg_head.py:417-446, module_utils.py:204-231).
+//
+//   out[m, n] = act( bias[n] + res[m, n] + sum_{tap, c} x[shift_tap(m), c] * w[n, tap, c] )
+//
+// GEMM view: M = B*H*W output pixels, N = Cout, K = 9*Cin (tap-major, channel-minor: exactly the
+// memory order of a channels_last [Cout, Cin, 3, 3] weight, so the weight needs no repacking).
+// The A operand is gathered on the fly: K-step (tap, c0..c0+BK) of tile row m reads BK contiguous
+// channels of input pixel (y+dy, x+dx) - one 16-B load per 8 channels, zeros outside the image.
+//
+// Tiling (per 256-thread workgroup): BM = 128 pixels x BN (128 / 64 / 32) output channels, BK = 64
+// (or 32 when Cin = 32).  Register-staged double buffer: the global loads of K-step k+1 are issued
+// before the MFMAs of step k and written to the other LDS buffer after them (one barrier per step).
+// LDS rows are padded by 16 B so each 16-lane ds_read_b128 group of an MFMA fragment read hits 16
+// distinct 4-bank groups.  v_mfma_f32_16x16x32_bf16: lane l holds A[row l&15][k 8(l>>4)..+8] and
+// B[k 8(l>>4)..+8][col l&15]; C[row 4(l>>4)+i][col l&15].  Epilogue: fp32 accumulators -> LDS ->
+// 16-B coalesced rows (+bias +residual, ReLU, bf16).  Workgroup ids are remapped so consecutive
+// M-tiles (which share input halo rows) run on one XCD's L2.
+// The input gradient of a conv is the same operation on dy with the flipped, transposed weight.
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+__device__ __forceinline__ bf8v as_bf8(const uint4& u) {
+  bf8v r;
+  __builtin_memcpy(&r, &u, 16);
+  return r;
+}
+
+template <int BN_, int BK_>
+struct ConvCfg {
+  static constexpr int BM = 128, BN = BN_, BK = BK_;
+  static constexpr int NT = 256;
+  static constexpr int WN = BN_ >= 128 ? 2 : 1;  // waves along N
+  static constexpr int WM = 4 / WN;              // waves along M
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int LDK = BK + 8;             // padded LDS row, bf16 elements
+  static constexpr int CH = BK / 8;              // 16-B chunks per row
+  static constexpr int A_IT = (BM * CH + NT - 1) / NT;
+  static constexpr int B_IT = (BN * CH + NT - 1) / NT;
+  static constexpr int STAGE = (BM + BN) * LDK;  // bf16 elements per pipeline stage
+  static constexpr int CPAD = BN + 4;            // fp32 epilogue tile pitch
+  static constexpr int SMEM_BYTES = (2 * STAGE * 2 > BM * CPAD * 4) ? 2 * STAGE * 2 : BM * CPAD * 4;
+  static_assert((BM * CH) % NT == 0, "A tile chunks");
+};
+
+template <int BN, int BK>
+__global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                      const float* __restrict__ bias, const bf16_t* __restrict__ res,
+                                                      bf16_t* __restrict__ out, int B, int H, int W, int Cin, int Cout,
+                                                      int act) {
+  using C = ConvCfg<BN, BK>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM_BYTES];
+  bf16_t* st = reinterpret_cast<bf16_t*>(smem);
+
+  const int HW = H * W;
+  const long M = static_cast<long>(B) * HW;
+  const int K = 9 * Cin;
+  const int ntn = Cout / BN;
+  // XCD-aware bijective remap of the flat workgroup id (8 XCDs, round-robin dispatch)
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int tn = wg % ntn;
+  const long m0 = static_cast<long>(wg / ntn) * C::BM;
+  const int n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  // per-thread A rows (fixed across K-steps)
+  int a_b[C::A_IT], a_y[C::A_IT], a_x[C::A_IT], a_row[C::A_IT], a_ch[C::A_IT];
+#pragma unroll
+  for (int i = 0; i < C::A_IT; ++i) {
+    const int idx = tid + i * C::NT;
+    a_row[i] = idx / C::CH;
+    a_ch[i] = idx % C::CH;
+    const long m = m0 + a_row[i];
+    if (m < M) {
+      a_b[i] = static_cast<int>(m / HW);
+      const int rem = static_cast<int>(m - static_cast<long>(a_b[i]) * HW);
+      a_y[i] = rem / W;
+      a_x[i] = rem - a_y[i] * W;
+    } else {
+      a_b[i] = -1; a_y[i] = 0; a_x[i] = 0;
+    }
+  }
+
+  uint4 ra[C::A_IT], rb[C::B_IT];
+  auto load_regs = [&](int kt) {
+    const int k0 = kt * BK;
+    const int tap = k0 / Cin, c0 = k0 - tap * Cin;
+    const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) {
+      const int yy = a_y[i] + dy, xx = a_x[i] + dx;
+      const bool ok = a_b[i] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
+      ra[i] = ok ? *reinterpret_cast<const uint4*>(
+                       x + ((static_cast<long>(a_b[i]) * H + yy) * W + xx) * Cin + c0 + 8 * a_ch[i])
+                 : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const int idx = tid + i * C::NT;
+      if (idx < BN * C::CH) {
+        const int n = idx / C::CH, ch = idx % C::CH;
+        rb[i] = *reinterpret_cast<const uint4*>(w + static_cast<long>(n0 + n) * K + k0 + 8 * ch);
+      }
+    }
+  };
+  auto store_lds = [&](int s) {
+    bf16_t* A = st + s * C::STAGE;
+    bf16_t* Bs = A + C::BM * C::LDK;
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i)
+      *reinterpret_cast<uint4*>(A + a_row[i] * C::LDK + 8 * a_ch[i]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const int idx = tid + i * C::NT;
+      if (idx < BN * C::CH) {
+        const int n = idx / C::CH, ch = idx % C::CH;
+        *reinterpret_cast<uint4*>(Bs + n * C::LDK + 8 * ch) = rb[i];
+      }
+    }
+  };
+
+  f4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int KT = K / BK;
+  load_regs(0);
+  store_lds(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) load_regs(kt + 1);
+    const bf16_t* A = st + cur * C::STAGE;
+    const bf16_t* Bs = A + C::BM * C::LDK;
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf8v af[C::FM], bfr[C::FN];
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+        af[i] = as_bf8(*reinterpret_cast<const uint4*>(A + (wm * C::TM + i * 16 + lr) * C::LDK + ks * 32 + 8 * lg));
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+        bfr[j] = as_bf8(*reinterpret_cast<const uint4*>(Bs + (wn * C::TN + j * 16 + lr) * C::LDK + ks * 32 + 8 * lg));
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < KT) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: accumulators -> LDS (fp32) -> coalesced 16-B rows with bias / residual / activation
+  float* cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        cs[(wm * C::TM + i * 16 + 4 * lg + e) * C::CPAD + wn * C::TN + j * 16 + lr] = acc[i][j][e];
+  __syncthreads();
+  constexpr int CPR = BN / 8;  // 8-channel chunks per row
+  for (int idx = tid; idx < C::BM * CPR; idx += C::NT) {
+    const int rr = idx / CPR, c8 = idx % CPR;
+    const long m = m0 + rr;
+    if (m >= M) continue;
+    const int n = n0 + 8 * c8;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = cs[rr * C::CPAD + 8 * c8 + e] + (bias ? bias[n + e] : 0.f);
+    const long o = m * Cout + n;
+    if (res) {
+      const uint4 u = *reinterpret_cast<const uint4*>(res + o);
+      const uint32_t q4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] += __uint_as_float(q4[e] << 16);
+        v[2 * e + 1] += __uint_as_float(q4[e] & 0xffff0000u);
+      }
+    }
+    if (act == ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    uint4 u;
+    u.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
+    u.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
+    u.z = static_cast<uint32_t>(f2bf(v[4])) | (static_cast<uint32_t>(f2bf(v[5])) << 16);
+    u.w = static_cast<uint32_t>(f2bf(v[6])) | (static_cast<uint32_t>(f2bf(v[7])) << 16);
+    *reinterpret_cast<uint4*>(out + o) = u;
+  }
+}
+
+template <int BN, int BK>
+void launch(const bf16_t* x, const bf16_t* w, const float* bias, const bf16_t* res, bf16_t* out, int B, int H, int W,
+            int Cin, int Cout, int act, hipStream_t s) {
+  const long M = static_cast<long>(B) * H * W;
+  const long mt = (M + 127) / 128;
+  const long nwg = mt * (Cout / BN);
+  if (nwg == 0) return;
+  hipLaunchKernelGGL((conv3x3_kernel<BN, BK>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias, res, out,
+                     B, H, W, Cin, Cout, act);
+}
+
+}  // namespace
+
+bool conv3x3_supported(int Cin, int Cout) {
+  return Cin % 32 == 0 && Cin >= 32 && (Cout % 128 == 0 || Cout == 64 || Cout == 32);
+}
+
+void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* res, void* out, int B, int H, int W,
+                 int Cin, int Cout, int act, hipStream_t s) {
+  const bf16_t* xp = static_cast<const bf16_t*>(x);
+  const bf16_t* wp = static_cast<const bf16_t*>(w);
+  const bf16_t* rp = static_cast<const bf16_t*>(res);
+  bf16_t* op = static_cast<bf16_t*>(out);
+  const bool k64 = Cin % 64 == 0;
+  if (Cout % 128 == 0) {
+    if (k64) launch<128, 64>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    else launch<128, 32>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+  } else if (Cout == 64) {
+    if (k64) launch<64, 64>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    else launch<64, 32>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+  } else {
+    if (k64) launch<32, 64>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    else launch<32, 32>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+  }
+}
+
+}  // namespace as

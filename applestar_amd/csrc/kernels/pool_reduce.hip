@@ -1,0 +1,294 @@
+// NHWC 2x2 max-pool (forward + backward), sorted-segment row sums, small-table row-gather
+// gradients and the partial-sum column reduction, for gfx950.
+//
+// maxpool2: the spatial and value encoders downsample with max_pool2d(x, 2, 2) three times each
+//   (spatial_encoder.py:74-80, value_encoder.py:43-50).  torch's channels_last kernels cost ~3 ms
+//   per learner step (the backward zero-fills dx, then scatters through int64 argmax indices).  Here
+//   one thread owns 8 channels (16 B) of one output pixel: the forward reads the 2x2 window with four
+//   16-B loads and writes y plus the window position per channel (one byte); the backward writes
+//   every dx element exactly once (dy where the position matches, else 0): no memset, no atomics.
+//   Selection matches torch: scan (0,0),(0,1),(1,0),(1,1), replace on (v > max) || isnan(v).
+// segment_sum: out[s, c] = sum_{t in [cu[s], cu[s+1])} x[t, c] over packed entity rows (the entity
+//   encoder's masked mean, entity_encoder.py:85-87): one workgroup per segment, no atomics.
+// table_grad: dT[v, :] = sum_u [idx[u] == v] src[u, :] for tiny lookup tables (the value encoder's
+//   unit-type / alliance tables, value_encoder.py:32-41): block-private LDS accumulators (LDS float
+//   atomics), one global atomic per table entry per block - instead of ~2e5 contended bf16 CAS
+//   atomics into 260 (or 2) rows.
+// column_reduce: out[c] = sum_r part[r][c] for the per-block partials of the LayerNorm / upconv
+//   weight gradients.  <= 1024 rows: one 1024-thread block per 64 columns (16 row groups x 4
+//   independent accumulators).  More rows: 256-row slabs per block, fp32 atomics into a zeroed out.
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+struct V8 {
+  float v[8];
+};
+
+template <typename T> __device__ __forceinline__ V8 load8(const T* p);
+template <> __device__ __forceinline__ V8 load8<bf16_t>(const bf16_t* p) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+  V8 r;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    r.v[2 * j] = __uint_as_float(w[j] << 16);
+    r.v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+  }
+  return r;
+}
+template <> __device__ __forceinline__ V8 load8<float>(const float* p) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  V8 r;
+  r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+  r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+  return r;
+}
+
+template <typename T> __device__ __forceinline__ void store8(T* p, const V8& r);
+template <> __device__ __forceinline__ void store8<bf16_t>(bf16_t* p, const V8& r) {
+  uint4 u;
+  u.x = static_cast<uint32_t>(f2bf(r.v[0])) | (static_cast<uint32_t>(f2bf(r.v[1])) << 16);
+  u.y = static_cast<uint32_t>(f2bf(r.v[2])) | (static_cast<uint32_t>(f2bf(r.v[3])) << 16);
+  u.z = static_cast<uint32_t>(f2bf(r.v[4])) | (static_cast<uint32_t>(f2bf(r.v[5])) << 16);
+  u.w = static_cast<uint32_t>(f2bf(r.v[6])) | (static_cast<uint32_t>(f2bf(r.v[7])) << 16);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+template <> __device__ __forceinline__ void store8<float>(float* p, const V8& r) {
+  *reinterpret_cast<float4*>(p) = make_float4(r.v[0], r.v[1], r.v[2], r.v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(r.v[4], r.v[5], r.v[6], r.v[7]);
+}
+
+int grid_for(long n) {
+  long b = (n + 255) / 256;
+  return static_cast<int>(b < 1 ? 1 : (b > 16384 ? 16384 : b));
+}
+
+// x [B][H][W][C] -> y [B][H/2][W/2][C], pos (window position 0..3 per element); C % 8 == 0
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool2_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                           uint8_t* __restrict__ pos, int B, int H, int W, int C) {
+  const int Ho = H >> 1, Wo = W >> 1, C8 = C >> 3;
+  const long total = static_cast<long>(B) * Ho * Wo * C8;
+  const long rowstride = static_cast<long>(W) * C;
+  for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int c8 = static_cast<int>(i % C8);
+    long r = i / C8;
+    const int ox = static_cast<int>(r % Wo);
+    r /= Wo;
+    const int oy = static_cast<int>(r % Ho);
+    const long b = r / Ho;
+    const long p00 = ((b * H + 2 * oy) * W + 2 * ox) * C + 8 * c8;
+    const V8 a = load8<T>(x + p00), q1 = load8<T>(x + p00 + C), q2 = load8<T>(x + p00 + rowstride),
+             q3 = load8<T>(x + p00 + rowstride + C);
+    V8 o;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float m = a.v[k];
+      uint32_t p = 0;
+      if (q1.v[k] > m || isnan(q1.v[k])) { m = q1.v[k]; p = 1; }
+      if (q2.v[k] > m || isnan(q2.v[k])) { m = q2.v[k]; p = 2; }
+      if (q3.v[k] > m || isnan(q3.v[k])) { m = q3.v[k]; p = 3; }
+      o.v[k] = m;
+      if (k < 4) lo |= p << (8 * k);
+      else hi |= p << (8 * (k - 4));
+    }
+    store8<T>(y + i * 8, o);
+    *reinterpret_cast<uint2*>(pos + i * 8) = make_uint2(lo, hi);
+  }
+}
+
+// dy [B][Ho][Wo][C], pos -> dx [B][H][W][C] (every element written; an odd trailing row/col gets 0)
+template <typename T>
+__global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ pos,
+                                                           T* __restrict__ dx, int B, int H, int W, int C) {
+  const int Ho = H >> 1, Wo = W >> 1, C8 = C >> 3;
+  const long total = static_cast<long>(B) * H * W * C8;
+  for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const int c8 = static_cast<int>(i % C8);
+    long r = i / C8;
+    const int ix = static_cast<int>(r % W);
+    r /= W;
+    const int iy = static_cast<int>(r % H);
+    const long b = r / H;
+    const int oy = iy >> 1, ox = ix >> 1;
+    V8 o;
+    if (oy < Ho && ox < Wo) {
+      const long oi = ((b * Ho + oy) * Wo + ox) * C + 8 * c8;
+      const V8 g = load8<T>(dy + oi);
+      const uint2 pp = *reinterpret_cast<const uint2*>(pos + oi);
+      const uint32_t me = static_cast<uint32_t>((iy & 1) * 2 + (ix & 1));
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t p = ((k < 4 ? pp.x : pp.y) >> (8 * (k & 3))) & 0xffu;
+        o.v[k] = p == me ? g.v[k] : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) o.v[k] = 0.f;
+    }
+    store8<T>(dx + i * 8, o);
+  }
+}
+
+// one workgroup (256 threads = 4 waves) per segment; each lane covers 4 channels per pass, C <= 1024
+template <typename T>
+__global__ __launch_bounds__(256) void segment_sum_kernel(const T* __restrict__ x, const int* __restrict__ cu,
+                                                          float* __restrict__ out, int C) {
+  __shared__ float red[4][1024];
+  const int s = blockIdx.x;
+  const int t0 = cu[s], t1 = cu[s + 1];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (int c0 = 4 * l; c0 < C; c0 += 256) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int t = t0 + w; t < t1; t += 4) {
+      const long base = static_cast<long>(t) * C + c0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += Cvt<T>::load(x, base + k);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) red[w][c0 + k] = acc[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256)
+    out[static_cast<long>(s) * C + c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+// out [V][D] fp32 (zeroed) += rows of src [U][D] grouped by idx[u]; rows with idx outside [0, V) skipped.
+// V * D floats of dynamic LDS (<= 64 KiB).
+template <typename T>
+__global__ __launch_bounds__(256) void table_grad_kernel(const T* __restrict__ src, const int64_t* __restrict__ idx,
+                                                         float* __restrict__ out, long U, int V, int D) {
+  extern __shared__ float acc[];
+  const int VD = V * D;
+  for (int i = threadIdx.x; i < VD; i += blockDim.x) acc[i] = 0.f;
+  __syncthreads();
+  const long total = U * D;
+  for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const long u = i / D;
+    const int d = static_cast<int>(i - u * D);
+    const int64_t v = idx[u];
+    if (v >= 0 && v < V) atomicAdd(&acc[v * D + d], Cvt<T>::load(src, i));
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < VD; i += blockDim.x) {
+    const float a = acc[i];
+    if (a != 0.f) atomicAdd(out + i, a);
+  }
+}
+
+__global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                             int nrows, int cols) {
+  __shared__ float red[16][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < cols) {
+    int r = g;
+    for (; r + 48 < nrows; r += 64) {
+      s0 += part[static_cast<long>(r) * cols + c];
+      s1 += part[static_cast<long>(r + 16) * cols + c];
+      s2 += part[static_cast<long>(r + 32) * cols + c];
+      s3 += part[static_cast<long>(r + 48) * cols + c];
+    }
+    for (; r < nrows; r += 16) s0 += part[static_cast<long>(r) * cols + c];
+  }
+  red[g][threadIdx.x & 63] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && c < cols) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
+    out[c] = s;
+  }
+}
+
+// grid (ceil(cols/64), ceil(nrows/256)); out zeroed beforehand
+__global__ __launch_bounds__(256) void column_reduce_atomic_kernel(const float* __restrict__ part,
+                                                                   float* __restrict__ out, int nrows, int cols) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int g = threadIdx.x >> 6;
+  const int r0 = blockIdx.y * 256, r1 = min(r0 + 256, nrows);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < cols) {
+    int r = r0 + g;
+    for (; r + 12 < r1; r += 16) {
+      s0 += part[static_cast<long>(r) * cols + c];
+      s1 += part[static_cast<long>(r + 4) * cols + c];
+      s2 += part[static_cast<long>(r + 8) * cols + c];
+      s3 += part[static_cast<long>(r + 12) * cols + c];
+    }
+    for (; r < r1; r += 4) s0 += part[static_cast<long>(r) * cols + c];
+  }
+  red[g][threadIdx.x & 63] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && c < cols) atomicAdd(out + c, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                                 red[3][threadIdx.x]);
+}
+
+}  // namespace
+
+void maxpool2_fwd(const void* x, void* y, uint8_t* pos, int dt, int B, int H, int W, int C, hipStream_t s) {
+  const long n = static_cast<long>(B) * (H / 2) * (W / 2) * (C / 8);
+  if (n == 0) return;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const bf16_t*>(x),
+                       static_cast<bf16_t*>(y), pos, B, H, W, C);
+  else
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const float*>(x),
+                       static_cast<float*>(y), pos, B, H, W, C);
+}
+
+void maxpool2_bwd(const void* dy, const uint8_t* pos, void* dx, int dt, int B, int H, int W, int C, hipStream_t s) {
+  const long n = static_cast<long>(B) * H * W * (C / 8);
+  if (n == 0) return;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(maxpool2_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const bf16_t*>(dy),
+                       pos, static_cast<bf16_t*>(dx), B, H, W, C);
+  else
+    hipLaunchKernelGGL(maxpool2_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const float*>(dy),
+                       pos, static_cast<float*>(dx), B, H, W, C);
+}
+
+void segment_sum(const void* x, int dt, const int* cu, float* out, int S, int C, hipStream_t s) {
+  if (S == 0) return;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(segment_sum_kernel<bf16_t>, dim3(S), dim3(256), 0, s, static_cast<const bf16_t*>(x), cu, out, C);
+  else
+    hipLaunchKernelGGL(segment_sum_kernel<float>, dim3(S), dim3(256), 0, s, static_cast<const float*>(x), cu, out, C);
+}
+
+void table_grad(const void* src, int dt, const int64_t* idx, float* out, long U, int V, int D, hipStream_t s) {
+  const long n = U * D;
+  if (n == 0) return;
+  long blocks = (n + 4095) / 4096;  // >= 16 elements per thread before the per-block flush
+  if (blocks > 256) blocks = 256;
+  if (blocks < 1) blocks = 1;
+  const size_t lds = static_cast<size_t>(V) * D * sizeof(float);
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(table_grad_kernel<bf16_t>, dim3(static_cast<unsigned>(blocks)), dim3(256), lds, s,
+                       static_cast<const bf16_t*>(src), idx, out, U, V, D);
+  else
+    hipLaunchKernelGGL(table_grad_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(256), lds, s,
+                       static_cast<const float*>(src), idx, out, U, V, D);
+}
+
+void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s) {
+  if (nrows <= 1024) {
+    hipLaunchKernelGGL(column_reduce_kernel, dim3((cols + 63) / 64), dim3(1024), 0, s, part, out, nrows, cols);
+    return;
+  }
+  hipMemsetAsync(out, 0, static_cast<size_t>(cols) * sizeof(float), s);
+  hipLaunchKernelGGL(column_reduce_atomic_kernel, dim3((cols + 63) / 64, (nrows + 255) / 256), dim3(256), 0, s, part,
+                     out, nrows, cols);
+}
+
+}  // namespace as
