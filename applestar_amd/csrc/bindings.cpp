@@ -463,6 +463,86 @@ std::vector<at::Tensor> upconv1_bwd(const at::Tensor& x_nhwc, const at::Tensor& 
   return {dx, dwb};
 }
 
+// ---------------------------------------------------------------- max-pool 2x2 (NHWC)
+std::vector<at::Tensor> maxpool2_fwd(const at::Tensor& x) {  // x [B,H,W,C]
+  check_cuda(x, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "maxpool2: NHWC with C % 8 == 0");
+  c10::hip::HIPGuard g(x.device().index());
+  auto y = at::empty({x.size(0), x.size(1) / 2, x.size(2) / 2, x.size(3)}, x.options());
+  auto pos = at::empty(y.sizes(), x.options().dtype(at::kByte));
+  as::maxpool2_fwd(x.data_ptr(), y.data_ptr(), pos.data_ptr<uint8_t>(), dt(x), x.size(0), x.size(1), x.size(2),
+                   x.size(3), stream());
+  return {y, pos};
+}
+
+at::Tensor maxpool2_bwd(const at::Tensor& dy, const at::Tensor& pos, int64_t H, int64_t W) {
+  check_cuda(dy, "dy");
+  check_cuda(pos, "pos");
+  TORCH_CHECK(dy.dim() == 4 && dy.sizes() == pos.sizes() && dy.size(1) == H / 2 && dy.size(2) == W / 2,
+              "maxpool2_bwd: shapes");
+  c10::hip::HIPGuard g(dy.device().index());
+  auto dx = at::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
+  as::maxpool2_bwd(dy.data_ptr(), pos.data_ptr<uint8_t>(), dx.data_ptr(), dt(dy), dy.size(0), H, W, dy.size(3),
+                   stream());
+  return dx;
+}
+
+// ---------------------------------------------------------------- segment sum / table gradient
+at::Tensor segment_sum(const at::Tensor& x, const at::Tensor& cu) {  // x [T,C], cu [S+1] int32 -> [S,C] fp32
+  check_cuda(x, "x");
+  check_cuda(cu, "cu");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 4 == 0 && x.size(1) <= 1024, "segment_sum: x [T, C<=1024]");
+  TORCH_CHECK(cu.scalar_type() == at::kInt, "segment_sum: cu int32");
+  c10::hip::HIPGuard g(x.device().index());
+  const int64_t S = cu.numel() - 1;
+  auto out = at::empty({S, x.size(1)}, x.options().dtype(at::kFloat));
+  as::segment_sum(x.data_ptr(), dt(x), cu.data_ptr<int>(), out.data_ptr<float>(), S, x.size(1), stream());
+  return out;
+}
+
+at::Tensor table_grad(const at::Tensor& src, const at::Tensor& idx, int64_t V) {  // src [U,D], idx [U] int64
+  check_cuda(src, "src");
+  check_cuda(idx, "idx");
+  TORCH_CHECK(src.dim() == 2 && idx.scalar_type() == at::kLong && idx.numel() == src.size(0), "table_grad: shapes");
+  TORCH_CHECK(V * src.size(1) <= 16384, "table_grad: table too large for LDS accumulation");
+  c10::hip::HIPGuard g(src.device().index());
+  auto out = at::zeros({V, src.size(1)}, src.options().dtype(at::kFloat));
+  as::table_grad(src.data_ptr(), dt(src), idx.data_ptr<int64_t>(), out.data_ptr<float>(), src.size(0), V, src.size(1),
+                 stream());
+  return out;
+}
+
+// ---------------------------------------------------------------- conv3x3 implicit GEMM (NHWC bf16)
+at::Tensor conv3x3_fwd(const at::Tensor& x, const at::Tensor& wk, const c10::optional<at::Tensor>& bias,
+                       const c10::optional<at::Tensor>& res, int64_t act) {
+  check_cuda(x, "x");
+  check_cuda(wk, "w");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && wk.scalar_type() == at::kBFloat16, "conv3x3: bf16 x / w");
+  TORCH_CHECK(x.dim() == 4 && wk.dim() == 4 && wk.size(1) == 3 && wk.size(2) == 3 && wk.size(3) == x.size(3),
+              "conv3x3: x NHWC [B,H,W,Cin], w [Cout,3,3,Cin]");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = wk.size(0);
+  TORCH_CHECK(as::conv3x3_supported(Cin, Cout), "conv3x3: unsupported channels ", Cin, "->", Cout);
+  TORCH_CHECK(B * H * W < (1LL << 31) / 128, "conv3x3: too many pixels");
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == Cout, "conv3x3: bias fp32 [Cout]");
+    bp = bias->data_ptr<float>();
+  }
+  const void* rp = nullptr;
+  if (res.has_value()) {
+    check_cuda(*res, "residual");
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->dim() == 4 && res->size(0) == B && res->size(1) == H &&
+                    res->size(2) == W && res->size(3) == Cout, "conv3x3: residual NHWC bf16 [B,H,W,Cout]");
+    rp = res->data_ptr();
+  }
+  c10::hip::HIPGuard g(x.device().index());
+  auto out = at::empty({B, H, W, Cout}, x.options());
+  as::conv3x3_fwd(x.data_ptr(), wk.data_ptr(), bp, rp, out.data_ptr(), B, H, W, Cin, Cout, static_cast<int>(act),
+                  stream());
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -487,4 +567,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("segment_copy", &segment_copy);
   m.def("upconv1_fwd", &upconv1_fwd);
   m.def("upconv1_bwd", &upconv1_bwd);
+  m.def("maxpool2_fwd", &maxpool2_fwd);
+  m.def("maxpool2_bwd", &maxpool2_bwd);
+  m.def("segment_sum", &segment_sum);
+  m.def("table_grad", &table_grad);
+  m.def("conv3x3_fwd", &conv3x3_fwd);
 }

@@ -135,3 +135,20 @@ void upconv1_fwd(const void* x, int x_dt, const float* w, const float* bias, flo
 void upconv1_bwd(const void* x, int x_dt, const float* w, const float* dy, void* dx, float* part, float* dwb, int B,
                  int Hl, int Wl, hipStream_t s);
 }  // namespace as
+
+namespace as {
+// ---- pool_reduce.hip ---------------------------------------------------------------------------
+// NHWC 2x2/stride-2 max-pool; pos [B,H/2,W/2,C] uint8 window position; C % 8 == 0
+void maxpool2_fwd(const void* x, void* y, uint8_t* pos, int dt, int B, int H, int W, int C, hipStream_t s);
+void maxpool2_bwd(const void* dy, const uint8_t* pos, void* dx, int dt, int B, int H, int W, int C, hipStream_t s);
+// out [S, C] fp32 = per-segment row sums of x [T, C] (segments cu[s]..cu[s+1]); C <= 1024, C % 4 == 0
+void segment_sum(const void* x, int dt, const int* cu, float* out, int S, int C, hipStream_t s);
+// out [V, D] fp32 (zeroed) += src rows grouped by idx (V * D <= 16384)
+void table_grad(const void* src, int dt, const int64_t* idx, float* out, long U, int V, int D, hipStream_t s);
+
+// ---- conv3x3.hip -------------------------------------------------------------------------------
+// out NHWC [B,H,W,Cout] bf16 = act(conv3x3_pad1(x NHWC bf16, w [Cout][3][3][Cin] bf16) + bias + res)
+bool conv3x3_supported(int Cin, int Cout);
+void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* res, void* out, int B, int H, int W,
+                 int Cin, int Cout, int act, hipStream_t s);
+}  // namespace as

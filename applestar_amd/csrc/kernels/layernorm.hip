@@ -174,19 +174,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
   }
 }
 
-__global__ __launch_bounds__(256) void column_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
-                                                            int nrows, int cols) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int g = threadIdx.x >> 6;
-  float s = 0.f;
-  if (c < cols)
-    for (int r = g; r < nrows; r += 4) s += part[static_cast<long>(r) * cols + c];
-  red[g][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (g == 0 && c < cols) out[c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-}
-
 int fwd_blocks(long rows) {
   long b = (rows + 3) / 4;
   return static_cast<int>(b < 4096 ? (b < 1 ? 1 : b) : 4096);
@@ -264,10 +251,6 @@ void layer_norm_bwd(const void* dy, int dy_dt, const void* xin, int xin_dt, cons
                     long rows, int cols, int act, int nblk, hipStream_t s) {
   VPT_SWITCH(cols, bwd_dispatch, dy, dy_dt, xin, xin_dt, y, y_dt, w, mean, rstd, dx, dx_dt, dw_part, db_part, rows,
              act, nblk, s);
-}
-
-void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s) {
-  hipLaunchKernelGGL(column_reduce_kernel, dim3((cols + 63) / 64), dim3(256), 0, s, part, out, nrows, cols);
 }
 
 }  // namespace as

@@ -18,7 +18,7 @@ import torch.nn.functional as F
 
 from .. import ops
 
-__all__ = ['FCBlock', 'ConvBlock', 'ResFCBlock', 'ResFCBlock2', 'ResBlock', 'GLU', 'GatedResBlock',
+__all__ = ['FCBlock', 'ConvBlock', 'ResFCBlock', 'ResFCBlock2', 'ResBlock', 'MaxPool2x2', 'GLU', 'GatedResBlock',
            'OneHotTable', 'binary_table']
 
 
@@ -67,10 +67,10 @@ class ConvBlock(nn.Sequential):
         super().__init__(*layers)
         self.act = act
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual=None) -> torch.Tensor:
         c = self[0]
         return ops.conv2d(x, c.weight, c.bias, stride=c.stride[0], padding=c.padding[0],
-                          act='relu' if self.act else None)
+                          act='relu' if self.act else None, residual=residual)
 
 
 class ResFCBlock(nn.Module):
@@ -109,8 +109,15 @@ class ResBlock(nn.Module):
         self.conv2 = ConvBlock(dim, dim, 3, 1, 1, act=False)
 
     def forward(self, x):
-        y = self.conv2(self.conv1(x))
-        return F.relu(y + x)
+        c = self.conv2[0]  # relu(conv2(y) + x): residual and ReLU fused into the conv epilogue on the GPU
+        return ops.conv2d(self.conv1(x), c.weight, c.bias, 1, 1, act='relu', residual=x)
+
+
+class MaxPool2x2(nn.Module):
+    """max_pool2d(x, 2, 2) (parameter-free: keeps the reference's Sequential indices)."""
+
+    def forward(self, x):
+        return ops.max_pool2x2(x)
 
 
 class GLU(nn.Module):

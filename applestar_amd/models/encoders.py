@@ -21,7 +21,7 @@ from .. import ops
 from ..lib import game_data as gd
 from ..lib.features import (MAX_ENTITY_NUM, ENTITY_FIELDS, SPATIAL_ONE_HOT, EFFECT_KEYS, SPATIAL_SIZE, ENTITY_EMBED_DIM,
                             BEGINNING_ORDER_LENGTH)
-from .blocks import FCBlock, ConvBlock, ResBlock, OneHotTable, binary_table, eye_table
+from .blocks import FCBlock, ConvBlock, ResBlock, MaxPool2x2, OneHotTable, binary_table, eye_table
 from .transformer import Transformer
 
 SPATIAL_Y, SPATIAL_X = SPATIAL_SIZE
@@ -202,7 +202,7 @@ class EntityEncoder(nn.Module):
             return entity_embeddings, self.embed_fc(pooled.to(x.dtype)), valid
         # masked mean of relu(transformer output) over real entities (entity_encoder.py:85-87)
         seg = torch.repeat_interleave(torch.arange(B, device=x.device), lens.long(), output_size=x.shape[0])
-        summed = x.new_zeros(B, x.shape[-1]).index_add(0, seg, x)
+        summed = ops.segment_sum(x, cu, seg).to(x.dtype)
         if self.reduce_type == 'constant':
             mean = summed / 512
         else:
@@ -256,7 +256,7 @@ class SpatialEncoder(nn.Module):
         map_skip = []
         for conv in self.downsample:
             map_skip.append(x)
-            x = conv(F.max_pool2d(x, 2, 2))
+            x = conv(ops.max_pool2x2(x))
         for block in self.res:
             map_skip.append(x)
             x = block(x)
@@ -311,7 +311,7 @@ class ValueEncoder(nn.Module):
         dims = [16, 16, 32, 32]
         layers = []
         for i in range(3):
-            layers += [nn.MaxPool2d(2, 2), ConvBlock(dims[i], dims[i + 1], 3, 1, 1, act=True)]
+            layers += [MaxPool2x2(), ConvBlock(dims[i], dims[i + 1], 3, 1, 1, act=True)]
         self.downsample = nn.Sequential(*layers)
         self.res = nn.ModuleList([ResBlock(32) for _ in range(4)])
         self.spatial_fc = FCBlock(32 * (SPATIAL_Y // 8) * (SPATIAL_X // 8), 128, act=True)
@@ -328,7 +328,7 @@ class ValueEncoder(nn.Module):
         tt = et @ lin.weight[:, ea.shape[1]:].t()
         ia = x['unit_alliance'].long().reshape(-1)
         it = x['unit_type'].long().clamp(0, gd.NUM_UNIT_TYPES - 1).reshape(-1)
-        pre = tt.index_select(0, it) + ta.index_select(0, ia) + lin.bias.to(tt.dtype)
+        pre = ops.gather_rows(tt, it) + ops.gather_rows(ta, ia) + lin.bias.to(tt.dtype)
         proj = torch.relu(pre).view(*x['unit_type'].shape, -1)
         U = proj.shape[1]
         mask = ops.sequence_mask(x['total_unit_count'], U)

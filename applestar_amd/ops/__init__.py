@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from . import reference as ref
 from . import _ext
 
-__all__ = ['linear', 'layer_norm', 'conv2d', 'gated_residual', 'lnlstm_layer', 'varlen_attention',
+__all__ = ['linear', 'layer_norm', 'conv2d', 'max_pool2x2', 'segment_sum', 'gather_rows', 'gated_residual', 'lnlstm_layer', 'varlen_attention',
            'masked_attention', 'scatter_connection', 'sequence_mask', 'native_enabled', 'set_native', 'upsample2x',
            'upsample_conv_out']
 
@@ -61,8 +61,39 @@ def layer_norm(x, w, b, residual=None, act=None, eps: float = 1e-5):
     return ref.layer_norm(x, w, b, residual, act, eps)
 
 
-def conv2d(x, w, b, stride=1, padding=0, act=None):
-    return ref.conv2d(x, w, b, stride, padding, act)
+def conv2d(x, w, b, stride=1, padding=0, act=None, residual=None):
+    """act(conv2d(x, w, b) + residual).  GPU: MFMA implicit-GEMM 3x3 kernel / NHWC GEMM for 1x1 (fused
+    bias, residual, ReLU); other shapes go to MIOpen."""
+    n = _native(x)
+    if n is not None and n.has('conv2d'):
+        y = n.conv2d(x, w, b, stride, padding, act, residual)
+        if y is not None:
+            return y
+    return ref.conv2d(x, w, b, stride, padding, act, residual)
+
+
+def max_pool2x2(x):
+    n = _native(x)
+    if n is not None and n.has('maxpool2x2') and x.dim() == 4 and x.shape[1] % 8 == 0:
+        return n.maxpool2x2(x)
+    return F.max_pool2d(x, 2, 2)
+
+
+def segment_sum(x, cu_seqlens, seg):
+    """Per-segment row sums of packed rows x [T,C] -> fp32 [S,C] (seg [T] = segment id of each row)."""
+    n = _native(x)
+    if n is not None and n.has('segment_sum') and x.shape[-1] % 4 == 0 and x.shape[-1] <= 1024:
+        return n.segment_sum(x, cu_seqlens, seg)
+    S = cu_seqlens.numel() - 1
+    return x.float().new_zeros(S, x.shape[-1]).index_add(0, seg, x.float())
+
+
+def gather_rows(table, idx):
+    """table[idx] for small lookup tables (native backward: LDS-accumulated row gradients)."""
+    n = _native(table)
+    if n is not None and n.has('gather_rows') and table.dim() == 2:
+        return n.gather_rows(table, idx)
+    return table.index_select(0, idx)
 
 
 def gated_residual(y, g, sp, x):

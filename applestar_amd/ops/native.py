@@ -21,7 +21,8 @@ def ensure_loaded():
 
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
-                'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out'}
+                'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
+                'gather_rows', 'conv2d'}
 
 
 def has(name: str) -> bool:
@@ -341,3 +342,144 @@ def upsample_conv_out(x, weight, bias):
     if x.dtype not in (torch.float32, torch.bfloat16):
         x = x.float()
     return _UpsampleConvOut.apply(nhwc(x), weight, bias).reshape(x.shape[0], -1)
+
+
+# ---------------------------------------------------------------------------- max-pool 2x2 (NHWC)
+class _MaxPool2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_nhwc):
+        y, pos = _C.maxpool2_fwd(x_nhwc)
+        ctx.save_for_backward(pos)
+        ctx.hw = (x_nhwc.shape[1], x_nhwc.shape[2])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        pos, = ctx.saved_tensors
+        return _C.maxpool2_bwd(dy.contiguous(), pos, *ctx.hw)
+
+
+def maxpool2x2(x):
+    """F.max_pool2d(x, 2, 2) for [B,C,H,W] (C % 8 == 0) on the channels_last storage."""
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    return from_nhwc(_MaxPool2.apply(nhwc(x)))
+
+
+# ---------------------------------------------------------------------------- packed-segment sum
+class _SegmentSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cu, seg):
+        ctx.save_for_backward(seg)
+        ctx.dtype = x.dtype
+        return _C.segment_sum(x.contiguous(), cu)
+
+    @staticmethod
+    def backward(ctx, dout):
+        seg, = ctx.saved_tensors
+        return dout.index_select(0, seg).to(ctx.dtype), None, None
+
+
+def segment_sum(x, cu, seg):
+    """Row sums of packed x [T,C] per segment (cu int32 [S+1]; seg [T] = segment of each row) -> fp32 [S,C]."""
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        x = x.float()
+    return _SegmentSum.apply(x, cu.to(torch.int32).contiguous(), seg)
+
+
+# ---------------------------------------------------------------------------- small-table row gather
+class _GatherRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, table, idx):
+        ctx.save_for_backward(idx)
+        ctx.V, ctx.dtype = table.shape[0], table.dtype
+        return table.index_select(0, idx)
+
+    @staticmethod
+    def backward(ctx, dout):
+        idx, = ctx.saved_tensors
+        d = dout.reshape(idx.numel(), -1)
+        if d.dtype not in (torch.float32, torch.bfloat16):
+            d = d.float()
+        return _C.table_grad(d.contiguous(), idx, ctx.V).to(ctx.dtype), None
+
+
+def gather_rows(table, idx):
+    """table[idx] whose backward accumulates in LDS per block (tiny tables hit by ~1e5 indices)."""
+    if table.shape[0] * table.shape[1] > 16384:
+        return table.index_select(0, idx)
+    return _GatherRows.apply(table, idx.long().contiguous())
+
+
+# ---------------------------------------------------------------------------- conv3x3 implicit GEMM
+class _Conv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x_nhwc, w_lp, b, res_nhwc, act):
+        wk = w_lp.detach().permute(0, 2, 3, 1)          # [Cout,3,3,Cin]: a view for channels_last weights
+        if not wk.is_contiguous():
+            wk = wk.contiguous()
+        bias = b.detach().float().contiguous() if b is not None else None
+        out = _C.conv3x3_fwd(x_nhwc, wk, bias, res_nhwc, _ACT[act])
+        ctx.save_for_backward(x_nhwc, w_lp, out)
+        ctx.act, ctx.has_res = act, res_nhwc is not None
+        ctx.b_dtype = b.dtype if b is not None else None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w, out = ctx.saved_tensors
+        dpre = dout.contiguous()
+        if ctx.act == 'relu':
+            dpre = dpre * (out > 0)
+        dpre = dpre.to(torch.bfloat16).contiguous()
+        wt = w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()   # [Cin,3,3,Cout]
+        dx = _C.conv3x3_fwd(dpre, wt, None, None, 0)
+        has_b = ctx.b_dtype is not None
+        _, dw, db = torch.ops.aten.convolution_backward(
+            from_nhwc(dpre), from_nhwc(x), w.detach(), [w.shape[0]] if has_b else None, [1, 1], [1, 1], [1, 1],
+            False, [0, 0], 1, [False, True, has_b])
+        return (dx, dw, db.to(ctx.b_dtype) if has_b else None, dpre if ctx.has_res else None, None)
+
+
+class _CastWeight(torch.autograd.Function):
+    """bf16 view of an fp32 weight for the native conv (autocast semantics) with an fp32 gradient."""
+
+    @staticmethod
+    def forward(ctx, w):
+        return w.detach().to(torch.bfloat16)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.float()
+
+
+def conv2d(x, w, b, stride, padding, act, residual):
+    """Native convolution paths; returns None when the call should go to MIOpen.
+
+    * 3x3 / stride 1 / pad 1 with Cin, Cout multiples of 32: MFMA implicit GEMM (bf16, under autocast
+      or with bf16 inputs) with bias / residual / ReLU fused;
+    * 1x1 / stride 1 / pad 0: a GEMM over the NHWC pixels (hipBLASLt, bias fused) - no transposes."""
+    if x.dim() != 4 or stride != 1:
+        return None
+    kh, kw = w.shape[2], w.shape[3]
+    cout, cin = w.shape[0], w.shape[1]
+    lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
+    if kh == 3 and kw == 3 and padding == 1 and lowp and _C.conv3x3_supported(cin, cout) \
+            and _C.conv3x3_supported(cout, cin):
+        xl = nhwc(x.to(torch.bfloat16))
+        wl = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
+        rl = nhwc(residual.to(torch.bfloat16)) if residual is not None else None
+        with torch.autocast('cuda', enabled=False):
+            return from_nhwc(_Conv3x3.apply(xl, wl, b, rl, act))
+    if kh == 1 and kw == 1 and padding == 0:
+        B, _, H, W = x.shape
+        y = torch.nn.functional.linear(nhwc(x).view(-1, cin), w.view(cout, cin), b)
+        if residual is not None:
+            y = y + nhwc(residual).view(-1, cout)
+        if act == 'relu':
+            y = torch.relu(y)
+        elif act is not None:
+            from . import reference
+            y = reference.act_fn(y, act)
+        return from_nhwc(y.view(B, H, W, cout))
+    return None

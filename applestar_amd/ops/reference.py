@@ -34,8 +34,11 @@ def layer_norm(x, w, b, residual=None, act=None, eps: float = 1e-5):
     return act_fn(F.layer_norm(x, (x.shape[-1],), w, b, eps), act)
 
 
-def conv2d(x, w, b, stride=1, padding=0, act=None):
-    return act_fn(F.conv2d(x, w, b, stride, padding), act)
+def conv2d(x, w, b, stride=1, padding=0, act=None, residual=None):
+    y = F.conv2d(x, w, b, stride, padding)
+    if residual is not None:
+        y = y + residual
+    return act_fn(y, act)
 
 
 def gated_residual(y, g, sp, x):

@@ -281,3 +281,87 @@ def test_upsample_conv_out_matches_interpolate_conv(H, W, dtype):
     assert rel(x.grad.float(), xr.grad) < tol * 10
     assert rel(w.grad, wr.grad) < tol * 10
     assert rel(b.grad, br.grad) < tol * 10
+
+
+@pytest.mark.parametrize('C,H,W', [(32, 152, 160), (128, 38, 40), (16, 19, 21)])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_maxpool2x2_matches_torch(C, H, W, dtype):
+    torch.manual_seed(5)
+    x = torch.randn(3, C, H, W, device=DEV).to(dtype).contiguous(memory_format=torch.channels_last)
+    x[0, :, :2, :2] = 0.5  # ties resolve to the first window position, like torch
+    xr = x.detach().clone().requires_grad_()
+    x.requires_grad_()
+    y = N.maxpool2x2(x)
+    yr = torch.nn.functional.max_pool2d(xr, 2, 2)
+    assert torch.equal(y, yr)
+    g = torch.randn_like(yr)
+    y.backward(g)
+    yr.backward(g)
+    assert torch.equal(x.grad, xr.grad)
+
+
+def test_segment_sum_and_gather_rows():
+    torch.manual_seed(6)
+    lens = torch.tensor([5, 0, 300, 1, 77], device=DEV)
+    cu = torch.nn.functional.pad(torch.cumsum(lens, 0), (1, 0)).int()
+    T = int(lens.sum())
+    seg = torch.repeat_interleave(torch.arange(5, device=DEV), lens)
+    for dtype in (torch.float32, torch.bfloat16):
+        x = torch.randn(T, 256, device=DEV).to(dtype).requires_grad_()
+        out = N.segment_sum(x, cu, seg)
+        ref = torch.zeros(5, 256, device=DEV).index_add(0, seg, x.float())
+        assert _err(out, ref) < 1e-3
+        g = torch.randn_like(out)
+        out.backward(g)
+        assert _err(x.grad, g[seg]) < 1e-2
+    for V, D, U in [(260, 8, 200000), (2, 8, 200000), (7, 3, 11)]:
+        table = torch.randn(V, D, device=DEV, requires_grad=True)
+        idx = torch.randint(0, V, (U,), device=DEV)
+        y = N.gather_rows(table, idx)
+        assert torch.equal(y, table[idx])
+        g = torch.randn(U, D, device=DEV)
+        y.backward(g)
+        ref = torch.zeros(V, D, device=DEV, dtype=torch.float64).index_add(0, idx, g.double())
+        assert (table.grad.double() - ref).abs().max().item() < 1e-3 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.parametrize('cin,cout,H,W', [(128, 128, 19, 20), (32, 64, 76, 80), (64, 128, 38, 40),
+                                          (128, 64, 38, 40), (64, 32, 19, 21), (32, 32, 7, 5), (256, 128, 9, 9)])
+@pytest.mark.parametrize('act,res', [(None, False), ('relu', False), ('relu', True)])
+def test_conv3x3_mfma_matches_fp32(cin, cout, H, W, act, res):
+    from applestar_amd import ops
+    torch.manual_seed(7)
+    B = 3
+    cl = torch.channels_last
+    x = torch.randn(B, cin, H, W, device=DEV).to(torch.bfloat16).contiguous(memory_format=cl).requires_grad_()
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) / (3 * cin ** 0.5)).to(torch.bfloat16)
+    w = w.contiguous(memory_format=cl).requires_grad_()
+    b = (0.1 * torch.randn(cout, device=DEV)).to(torch.bfloat16).requires_grad_()
+    r = torch.randn(B, cout, H, W, device=DEV).to(torch.bfloat16).contiguous(memory_format=cl).requires_grad_() \
+        if res else None
+    y = ops.conv2d(x, w, b, 1, 1, act=act, residual=r)
+    assert y.dtype == torch.bfloat16 and y.is_contiguous(memory_format=cl)
+    xs, ws, bs = (t.detach().float().requires_grad_() for t in (x, w, b))
+    rs = r.detach().float().requires_grad_() if res else None
+    yr = torch.nn.functional.conv2d(xs, ws, bs, 1, 1)
+    if res:
+        yr = yr + rs
+    if act == 'relu':
+        yr = torch.relu(yr)
+    assert _err(y, yr) < 2e-2 * max(1.0, yr.abs().max().item())
+    g = torch.randn_like(yr).to(torch.bfloat16)
+    y.backward(g)
+    yr.backward(g.float())
+    for a, ref in ((x.grad, xs.grad), (w.grad, ws.grad), (b.grad, bs.grad)) + (((r.grad, rs.grad),) if res else ()):
+        assert _err(a, ref) < 3e-2 * max(1.0, ref.abs().max().item())
+
+
+def test_conv1x1_gemm_path_matches_conv():
+    from applestar_amd import ops
+    torch.manual_seed(8)
+    x = torch.randn(4, 132, 19, 20, device=DEV).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(128, 132, 1, 1, device=DEV) / 12
+    b = torch.randn(128, device=DEV)
+    y = ops.conv2d(x, w, b, 1, 0, act='relu')
+    yr = torch.relu(torch.nn.functional.conv2d(x, w, b))
+    assert _err(y, yr) < 1e-3
