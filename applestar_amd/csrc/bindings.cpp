@@ -572,4 +572,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("segment_sum", &segment_sum);
   m.def("table_grad", &table_grad);
   m.def("conv3x3_fwd", &conv3x3_fwd);
+  m.def("conv3x3_supported", [](int64_t cin, int64_t cout) { return as::conv3x3_supported(static_cast<int>(cin), static_cast<int>(cout)); });
 }

@@ -1,10 +1,13 @@
 #!/bin/bash
-# Session-2 GPU check: gpu tests, bench, rocprofv3 kernel stats of the bench step.
+# Session-2 GPU check: new-kernel tests, all gpu tests, bench, rocprofv3 kernel stats of the bench step.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"
 mkdir -p gpurun_out
 TAG=${TAG:-s2}
+timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread -k "${KSEL:-maxpool or segment or conv}" > gpurun_out/${TAG}_new.log 2>&1; rc=$?
+echo "new-kernel tests exit $rc"; tail -4 gpurun_out/${TAG}_new.log
+[ $rc -eq 0 ] || exit 1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1; rc=$?
 echo "pytest exit $rc"; tail -4 gpurun_out/${TAG}_pytest_gpu.log
 [ $rc -eq 0 ] || exit 1
