@@ -522,7 +522,9 @@ at::Tensor conv3x3_fwd(const at::Tensor& x, const at::Tensor& wk, const c10::opt
               "conv3x3: x NHWC [B,H,W,Cin], w [Cout,3,3,Cin]");
   const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), Cout = wk.size(0);
   TORCH_CHECK(as::conv3x3_supported(Cin, Cout), "conv3x3: unsupported channels ", Cin, "->", Cout);
-  TORCH_CHECK(B * H * W < (1LL << 31) / 128, "conv3x3: too many pixels");
+  TORCH_CHECK(x.is_contiguous() && wk.is_contiguous(), "conv3x3: contiguous NHWC x / w");
+  // 32-bit buffer offsets: every byte offset (and the out-of-range sentinel) must stay below 2^31 - 16
+  TORCH_CHECK(B * H * W * Cin * 2 < 0x7ffffff0LL && Cout * 9 * Cin * 2 < 0x7ffffff0LL, "conv3x3: tensor too large");
   const float* bp = nullptr;
   if (bias.has_value()) {
     check_cuda(*bias, "bias");
@@ -544,6 +546,48 @@ at::Tensor conv3x3_fwd(const at::Tensor& x, const at::Tensor& wk, const c10::opt
 }
 
 }  // namespace
+
+// ---------------------------------------------------------------- split-R MFMA weight gradient
+// dy [R, N] bf16; x [R, K] bf16 (cin == 0) or NHWC [B, H, W, cin] bf16 (3x3 conv, K = 9 cin).
+// Returns (dW fp32 [N, K], db fp32 [N] or undefined).
+std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t cin, bool want_bias) {
+  check_cuda(dy, "dy");
+  check_cuda(x, "x");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "wgrad: bf16 dy / x");
+  TORCH_CHECK(dy.dim() == 2, "wgrad: dy [R, N]");
+  const int64_t R = dy.size(0), N = dy.size(1);
+  int64_t K, H = 1, W = 1;
+  if (cin > 0) {
+    TORCH_CHECK(x.dim() == 4 && x.size(3) == cin && x.size(0) * x.size(1) * x.size(2) == R, "wgrad: x NHWC");
+    H = x.size(1);
+    W = x.size(2);
+    K = 9 * cin;
+    TORCH_CHECK(cin % 8 == 0, "wgrad: Cin % 8");
+  } else {
+    TORCH_CHECK(x.dim() == 2 && x.size(0) == R, "wgrad: x [R, K]");
+    K = x.size(1);
+  }
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0, "wgrad: N and K must be multiples of 8");
+  TORCH_CHECK(R * N * 2 < 0x7ffffff0LL && x.numel() * 2 < 0x7ffffff0LL, "wgrad: tensor too large");
+  c10::hip::HIPGuard g(dy.device().index());
+  const int S = R > 0 ? as::wgrad_splits(R, static_cast<int>(N), static_cast<int>(K)) : 1;
+  auto opts = dy.options().dtype(at::kFloat);
+  if (R == 0) return {at::zeros({N, K}, opts), want_bias ? at::zeros({N}, opts) : at::Tensor()};
+  auto dwp = at::empty({S, N, K}, opts);
+  at::Tensor dbp = want_bias ? at::empty({S, N}, opts) : at::Tensor();
+  as::wgrad(dy.data_ptr(), x.data_ptr(), dwp.data_ptr<float>(), want_bias ? dbp.data_ptr<float>() : nullptr, R,
+            static_cast<int>(N), static_cast<int>(K), static_cast<int>(H), static_cast<int>(W), static_cast<int>(cin),
+            S, stream());
+  if (S == 1) return {dwp.view({N, K}), want_bias ? dbp.view({N}) : at::Tensor()};
+  auto dw = at::empty({N, K}, opts);
+  as::column_reduce(dwp.data_ptr<float>(), dw.data_ptr<float>(), S, static_cast<int>(N * K), stream());
+  at::Tensor db;
+  if (want_bias) {
+    db = at::empty({N}, opts);
+    as::column_reduce(dbp.data_ptr<float>(), db.data_ptr<float>(), S, static_cast<int>(N), stream());
+  }
+  return {dw, db};
+}
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "applestar_amd HIP kernels for gfx950 (MI355X)";
@@ -572,5 +616,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("segment_sum", &segment_sum);
   m.def("table_grad", &table_grad);
   m.def("conv3x3_fwd", &conv3x3_fwd);
+  m.def("wgrad", &wgrad);
   m.def("conv3x3_supported", [](int64_t cin, int64_t cout) { return as::conv3x3_supported(static_cast<int>(cin), static_cast<int>(cout)); });
 }

@@ -151,4 +151,12 @@ void table_grad(const void* src, int dt, const int64_t* idx, float* out, long U,
 bool conv3x3_supported(int Cin, int Cout);
 void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* res, void* out, int B, int H, int W,
                  int Cin, int Cout, int act, hipStream_t s);
+
+// ---- wgrad.hip ---------------------------------------------------------------------------------
+// dw_part [S, N, K] / db_part [S, N] fp32 partials of dW = dY^T X(r, k), db = sum_r dY; dy [R, N] bf16.
+// Cin == 0: x [R, K] bf16 (dense).  Cin > 0: x NHWC [R / (H W), H, W, Cin] bf16, K = 9 Cin (3x3 pad-1 conv).
+// N % 8 == 0, K % 8 == 0 (Cin % 8 == 0), R * max(N, K or Cin) * 2 < 2^31.
+int wgrad_splits(long R, int N, int K);
+void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long R, int N, int K, int H, int W, int Cin,
+           int S, hipStream_t st);
 }  // namespace as

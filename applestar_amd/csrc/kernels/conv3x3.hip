@@ -77,44 +77,59 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__
   const int wm = wid / C::WN, wn = wid % C::WN;
   const int lr = lane & 15, lg = lane >> 4;
 
-  // per-thread A rows (fixed across K-steps)
-  int a_b[C::A_IT], a_y[C::A_IT], a_x[C::A_IT], a_row[C::A_IT], a_ch[C::A_IT];
+  // Operand fetch through buffer descriptors: out-of-image taps and rows past M use an offset beyond
+  // num_records, which the hardware range check turns into zeros - no branches around the loads, so all
+  // A_IT + B_IT loads of a K-step issue back to back and stay in flight under the MFMAs of the previous one.
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(x), 0, static_cast<int>(M * Cin * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(w), 0, static_cast<int>(static_cast<long>(Cout) * K * 2), 0x00020000);
+  constexpr int kOOB = 0x7ffffff0;
+
+  // per-thread A rows (fixed across K-steps): pixel index and a 9-bit in-image mask over the taps
+  int a_pix[C::A_IT], a_row[C::A_IT], a_ch[C::A_IT], a_ok[C::A_IT];
 #pragma unroll
   for (int i = 0; i < C::A_IT; ++i) {
     const int idx = tid + i * C::NT;
     a_row[i] = idx / C::CH;
     a_ch[i] = idx % C::CH;
     const long m = m0 + a_row[i];
+    a_pix[i] = static_cast<int>(m);
+    a_ok[i] = 0;
     if (m < M) {
-      a_b[i] = static_cast<int>(m / HW);
-      const int rem = static_cast<int>(m - static_cast<long>(a_b[i]) * HW);
-      a_y[i] = rem / W;
-      a_x[i] = rem - a_y[i] * W;
-    } else {
-      a_b[i] = -1; a_y[i] = 0; a_x[i] = 0;
+      const int rem = static_cast<int>(m % HW);
+      const int yy = rem / W, xx = rem - yy * W;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int y2 = yy + t / 3 - 1, x2 = xx + t % 3 - 1;
+        a_ok[i] |= (y2 >= 0 && y2 < H && x2 >= 0 && x2 < W) << t;
+      }
     }
+  }
+  int b_off[C::B_IT];
+#pragma unroll
+  for (int i = 0; i < C::B_IT; ++i) {
+    const int idx = tid + i * C::NT;
+    const int n = idx / C::CH, ch = idx % C::CH;
+    b_off[i] = idx < BN * C::CH ? ((n0 + n) * K + 8 * ch) * 2 : kOOB;
   }
 
   uint4 ra[C::A_IT], rb[C::B_IT];
   auto load_regs = [&](int kt) {
     const int k0 = kt * BK;
     const int tap = k0 / Cin, c0 = k0 - tap * Cin;
-    const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+    const int shift = (tap / 3 - 1) * W + (tap % 3 - 1);
 #pragma unroll
     for (int i = 0; i < C::A_IT; ++i) {
-      const int yy = a_y[i] + dy, xx = a_x[i] + dx;
-      const bool ok = a_b[i] >= 0 && yy >= 0 && yy < H && xx >= 0 && xx < W;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(
-                       x + ((static_cast<long>(a_b[i]) * H + yy) * W + xx) * Cin + c0 + 8 * a_ch[i])
-                 : make_uint4(0, 0, 0, 0);
+      const int off = ((a_ok[i] >> tap) & 1) ? ((a_pix[i] + shift) * Cin + c0 + 8 * a_ch[i]) * 2 : kOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
     }
 #pragma unroll
     for (int i = 0; i < C::B_IT; ++i) {
-      const int idx = tid + i * C::NT;
-      if (idx < BN * C::CH) {
-        const int n = idx / C::CH, ch = idx % C::CH;
-        rb[i] = *reinterpret_cast<const uint4*>(w + static_cast<long>(n0 + n) * K + k0 + 8 * ch);
-      }
+      const int off = b_off[i] == kOOB ? kOOB : b_off[i] + k0 * 2;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0);
+      rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
     }
   };
   auto store_lds = [&](int s) {
@@ -126,7 +141,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__
 #pragma unroll
     for (int i = 0; i < C::B_IT; ++i) {
       const int idx = tid + i * C::NT;
-      if (idx < BN * C::CH) {
+      if ((BN * C::CH) % C::NT == 0 || idx < BN * C::CH) {
         const int n = idx / C::CH, ch = idx % C::CH;
         *reinterpret_cast<uint4*>(Bs + n * C::LDK + 8 * ch) = rb[i];
       }
@@ -222,7 +237,7 @@ void launch(const bf16_t* x, const bf16_t* w, const float* bias, const bf16_t* r
 
 }  // namespace
 
-bool conv3x3_supported(int Cin, int Cout) {
+bool conv3x3_supported(int Cin, int Cout) {  // (the host wrapper also bounds B*H*W*Cin*2 < 2^31)
   return Cin % 32 == 0 && Cin >= 32 && (Cout % 128 == 0 || Cout == 64 || Cout == 32);
 }
 

@@ -286,7 +286,7 @@ void column_reduce(const float* part, float* out, int nrows, int cols, hipStream
     hipLaunchKernelGGL(column_reduce_kernel, dim3((cols + 63) / 64), dim3(1024), 0, s, part, out, nrows, cols);
     return;
   }
-  hipMemsetAsync(out, 0, static_cast<size_t>(cols) * sizeof(float), s);
+  (void)hipMemsetAsync(out, 0, static_cast<size_t>(cols) * sizeof(float), s);
   hipLaunchKernelGGL(column_reduce_atomic_kernel, dim3((cols + 63) / 64, (nrows + 255) / 256), dim3(256), 0, s, part,
                      out, nrows, cols);
 }

@@ -1,0 +1,258 @@
+// Weight (and bias) gradients of the tall-skinny GEMMs and 3x3 convolutions on the MFMA matrix cores.
+//
+//   dW[n, k] = sum_r dY[r, n] * X(r, k)          db[n] = sum_r dY[r, n]
+//
+// R (rows = batch * pixels or batch * entities) is 10^4 .. 10^7 while N x K is at most a few hundred
+// squared, so the library GEMM (which tiles only the N x K output) runs a handful of workgroups on a
+// 256-CU part (rocprof r1_v10: 5-workgroup hipBLASLt launches of 0.5 ms each for the 1x1 convs' dW).
+// Here the reduction axis R is split over S slices (grid = N-tiles x K-tiles x S, >= ~1000 workgroups),
+// each slice writes an fp32 partial, and the partials are summed afterwards (deterministic).
+//
+// X(r, k) has two forms:
+//   * dense:   X is [R, K] row-major (nn.Linear / 1x1 conv on NHWC pixels);
+//   * conv3x3: X is an NHWC [B, H, W, Cin] image, k = tap * Cin + c and X(r, k) = x[pixel r shifted by the
+//     tap's (dy, dx)] (zero outside the image) - the implicit-GEMM weight gradient of a pad-1 3x3 conv in
+//     the [Cout, 3, 3, Cin] (channels_last) weight order.  Replaces MIOpen's wrw solvers.
+//
+// Both MFMA operands are reduction-major in memory (row r holds all n / all k), so the tiles are staged
+// row-major in LDS exactly as loaded (16-B chunks) and read back with the gfx950 transposed LDS read
+// ds_read_b64_tr_b16: a 16-lane group receives a 4-row x 16-column block column-major, i.e. 4 consecutive
+// reduction elements of 16 output columns.  The reduction index of fragment element j of lane group g is
+// r = 4g + j (j < 4) and 16 + 4g + (j - 4) (j >= 4) - a permutation of 0..31 applied to both operands -
+// so the two groups of one 32-lane half read 8 consecutive rows; with a row pitch of 72 dwords (BN = 128)
+// or 40 dwords (BN = 64) those 8 rows start on 8 distinct 8-bank groups (conflict-free).
+//
+// Loads go through buffer descriptors: rows past the slice end, columns past N/K and taps outside the
+// image get an out-of-range offset and read as zeros (no branches around loads).  The bias gradient is
+// accumulated from the A fragments by the waves that own K-column 0 of K-tile 0.
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
+typedef __attribute__((ext_vector_type(4))) float f4;
+typedef __attribute__((ext_vector_type(4))) short s4;
+typedef __attribute__((address_space(3))) s4 lds_s4;
+
+constexpr int kOOB = 0x7ffffff0;
+
+template <int BN_, int BK_>
+struct WgCfg {
+  static constexpr int BN = BN_, BK = BK_, BR = 64, NT = 256;
+  static constexpr int TN = BN / 2, TK = BK / 2;       // 2 x 2 waves
+  static constexpr int FN = TN / 16, FK = TK / 16;
+  static constexpr int PA = BN + 16, PB = BK + 16;    // LDS row pitch, bf16 elements (72 / 40 dwords)
+  static constexpr int CHA = BN / 8, CHB = BK / 8;    // 16-B chunks per row
+  static constexpr int A_IT = BR * CHA / NT, B_IT = BR * CHB / NT;
+  static constexpr int STAGE = BR * (PA + PB);        // bf16 elements
+  static constexpr int SMEM = 2 * STAGE * 2;
+  static_assert(A_IT * NT == BR * CHA && B_IT * NT == BR * CHB, "tile / thread mismatch");
+};
+
+__device__ __forceinline__ bf8v tr_frag(const bf16_t* tile, int pitch, int col0, int lane) {
+  // lanes 16g + 4q + p: rows 4g + q (first half) and 16 + 4g + q (second half), columns col0 + 4p .. + 3
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const bf16_t* a0 = tile + (4 * g + q) * pitch + col0 + 4 * p;
+  const s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a0));
+  const s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(a0 + 16 * pitch));
+  typedef __attribute__((ext_vector_type(8))) short s8;
+  const s8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  bf8v r;
+  __builtin_memcpy(&r, &v, 16);
+  return r;
+}
+
+template <int BN, int BK, bool CONV>
+__global__ __launch_bounds__(256) void wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                    float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                    long R, int N, int K, int H, int W, int Cin, long rows_per_split,
+                                                    int tiles_n, int tiles_k) {
+  using C = WgCfg<BN, BK>;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[C::SMEM / 2];
+
+  // XCD-aware remap: consecutive logical ids (the N x K tiles of one row slice, which read the same dY / X
+  // rows) land on one XCD's L2
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tk = wg % tiles_k;
+  const int tn = (wg / tiles_k) % tiles_n;
+  const int s = wg / (tiles_k * tiles_n);
+  const int n0 = tn * BN, k0 = tk * BK;
+  const long r_begin = static_cast<long>(s) * rows_per_split;
+  const long r_end = r_begin + rows_per_split < R ? r_begin + rows_per_split : R;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid >> 1, wk = wid & 1;
+
+  const long HW = static_cast<long>(H) * W;
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(dy), 0,
+                                                                      static_cast<int>(R * N * 2), 0x00020000);
+  const long xbytes = CONV ? R * Cin * 2 : R * K * 2;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x), 0,
+                                                                      static_cast<int>(xbytes), 0x00020000);
+
+  // per-thread fixed chunk columns
+  const int a_ch = tid % C::CHA, b_ch = tid % C::CHB;
+  const int a_col = n0 + 8 * a_ch, b_col = k0 + 8 * b_ch;
+  const bool a_col_ok = a_col < N, b_col_ok = b_col < K;
+  int b_c = b_col, b_shift = 0, b_dy = 0, b_dx = 0;
+  if (CONV) {
+    const int tap = b_col / Cin;
+    b_c = b_col - tap * Cin;
+    b_dy = tap / 3 - 1;
+    b_dx = tap % 3 - 1;
+    b_shift = b_dy * W + b_dx;
+  }
+
+  uint4 ra[C::A_IT], rb[C::B_IT];
+  auto load_regs = [&](long rs) {
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) {
+      const long r = rs + (tid + i * C::NT) / C::CHA;
+      const int off = (a_col_ok && r < r_end) ? static_cast<int>((r * N + a_col) * 2) : kOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0);
+      ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const long r = rs + (tid + i * C::NT) / C::CHB;
+      int off = kOOB;
+      if (CONV) {
+        const int rem = static_cast<int>(r % HW);
+        const int yy = rem / W + b_dy, xx = rem % W + b_dx;
+        if (b_col_ok && r < r_end && yy >= 0 && yy < H && xx >= 0 && xx < W)
+          off = static_cast<int>(((r + b_shift) * Cin + b_c) * 2);
+      } else if (b_col_ok && r < r_end) {
+        off = static_cast<int>((r * K + b_col) * 2);
+      }
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store_lds = [&](int st) {
+    bf16_t* A = smem + st * C::STAGE;
+    bf16_t* Bt = A + C::BR * C::PA;
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i)
+      *reinterpret_cast<uint4*>(A + ((tid + i * C::NT) / C::CHA) * C::PA + 8 * a_ch) = ra[i];
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i)
+      *reinterpret_cast<uint4*>(Bt + ((tid + i * C::NT) / C::CHB) * C::PB + 8 * b_ch) = rb[i];
+  };
+
+  f4 acc[C::FN][C::FK];
+#pragma unroll
+  for (int i = 0; i < C::FN; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FK; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bias = db_part != nullptr && tk == 0 && wk == 0;
+  float bsum[C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FN; ++i) bsum[i] = 0.f;
+
+  const long nsteps = r_end > r_begin ? (r_end - r_begin + C::BR - 1) / C::BR : 0;
+  if (nsteps > 0) {
+    load_regs(r_begin);
+    store_lds(0);
+    __syncthreads();
+  }
+  for (long it = 0; it < nsteps; ++it) {
+    const int cur = static_cast<int>(it & 1);
+    if (it + 1 < nsteps) load_regs(r_begin + (it + 1) * C::BR);
+    const bf16_t* A = smem + cur * C::STAGE;
+    const bf16_t* Bt = A + C::BR * C::PA;
+#pragma unroll
+    for (int ks = 0; ks < C::BR / 32; ++ks) {
+      bf8v af[C::FN], bfr[C::FK];
+#pragma unroll
+      for (int i = 0; i < C::FN; ++i) af[i] = tr_frag(A + ks * 32 * C::PA, C::PA, wn * C::TN + 16 * i, lane);
+#pragma unroll
+      for (int j = 0; j < C::FK; ++j) bfr[j] = tr_frag(Bt + ks * 32 * C::PB, C::PB, wk * C::TK + 16 * j, lane);
+#pragma unroll
+      for (int i = 0; i < C::FN; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FK; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < C::FN; ++i)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) bsum[i] += static_cast<float>(af[i][e]);
+      }
+    }
+    if (it + 1 < nsteps) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: fp32 partial tile; lane (g, i) of fragment (a, b) holds C[n = 16a + 4g + e][k = 16b + i]
+  float* outp = dw_part + static_cast<long>(s) * N * K;
+  const int lr = lane & 15, lg = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < C::FN; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FK; ++j) {
+      const int k = k0 + wk * C::TK + 16 * j + lr;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + wn * C::TN + 16 * i + 4 * lg + e;
+        if (n < N && k < K) outp[static_cast<long>(n) * K + k] = acc[i][j][e];
+      }
+    }
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < C::FN; ++i) {
+      float v = bsum[i];
+      v += __shfl_xor(v, 16, kWave);
+      v += __shfl_xor(v, 32, kWave);
+      const int n = n0 + wn * C::TN + 16 * i + lr;
+      if (lg == 0 && n < N) db_part[static_cast<long>(s) * N + n] = v;
+    }
+  }
+}
+
+template <int BN, int BK, bool CONV>
+void launch(const bf16_t* dy, const bf16_t* x, float* dw, float* db, long R, int N, int K, int H, int W, int Cin,
+            int S, long rps, hipStream_t st) {
+  const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
+  const long nwg = static_cast<long>(tn) * tk * S;
+  hipLaunchKernelGGL((wgrad_kernel<BN, BK, CONV>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x, dw, db,
+                     R, N, K, H, W, Cin, rps, tn, tk);
+}
+
+}  // namespace
+
+int wgrad_splits(long R, int N, int K) {
+  const int BN = N > 64 ? 128 : 64, BK = K > 64 ? 128 : 64;
+  const long tiles = static_cast<long>((N + BN - 1) / BN) * ((K + BK - 1) / BK);
+  long S = (1024 + tiles - 1) / tiles;                 // ~1024 workgroups: 2 resident per CU, 2 rounds
+  const long max_s = (R + 255) / 256;                  // at least 256 rows (4 stages) per slice
+  if (S > max_s) S = max_s;
+  const long max_part = (8L << 20) / (static_cast<long>(N) * K);  // partials <= 32 MB (their sum is a pass)
+  if (S > max_part) S = max_part;
+  if (S < 1) S = 1;
+  if (S > 4096) S = 4096;
+  return static_cast<int>(S);
+}
+
+void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long R, int N, int K, int H, int W, int Cin,
+           int S, hipStream_t st) {
+  long rps = (R + S - 1) / S;
+  rps = (rps + 63) / 64 * 64;
+  const bf16_t* d = static_cast<const bf16_t*>(dy);
+  const bf16_t* xp = static_cast<const bf16_t*>(x);
+  const bool conv = Cin > 0;
+  const bool bn128 = N > 64, bk128 = K > 64;
+#define AS_WG(BNv, BKv)                                                                              \
+  (conv ? launch<BNv, BKv, true>(d, xp, dw_part, db_part, R, N, K, H, W, Cin, S, rps, st)            \
+        : launch<BNv, BKv, false>(d, xp, dw_part, db_part, R, N, K, H, W, Cin, S, rps, st))
+  if (bn128 && bk128) AS_WG(128, 128);
+  else if (bn128) AS_WG(128, 64);
+  else if (bk128) AS_WG(64, 128);
+  else AS_WG(64, 64);
+#undef AS_WG
+}
+
+}  // namespace as

@@ -22,7 +22,7 @@ def ensure_loaded():
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
-                'gather_rows', 'conv2d'}
+                'gather_rows', 'conv2d', 'linear'}
 
 
 def has(name: str) -> bool:
@@ -435,9 +435,9 @@ class _Conv3x3(torch.autograd.Function):
         wt = w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()   # [Cin,3,3,Cout]
         dx = _C.conv3x3_fwd(dpre, wt, None, None, 0)
         has_b = ctx.b_dtype is not None
-        _, dw, db = torch.ops.aten.convolution_backward(
-            from_nhwc(dpre), from_nhwc(x), w.detach(), [w.shape[0]] if has_b else None, [1, 1], [1, 1], [1, 1],
-            False, [0, 0], 1, [False, True, has_b])
+        cout, cin = w.shape[0], w.shape[1]
+        dw, db = _C.wgrad(dpre.view(-1, cout), x, cin, has_b)       # dW in [Cout,3,3,Cin] (channels_last) order
+        dw = dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype)
         return (dx, dw, db.to(ctx.b_dtype) if has_b else None, dpre if ctx.has_res else None, None)
 
 
@@ -473,7 +473,7 @@ def conv2d(x, w, b, stride, padding, act, residual):
             return from_nhwc(_Conv3x3.apply(xl, wl, b, rl, act))
     if kh == 1 and kw == 1 and padding == 0:
         B, _, H, W = x.shape
-        y = torch.nn.functional.linear(nhwc(x).view(-1, cin), w.view(cout, cin), b)
+        y = linear(nhwc(x).view(-1, cin), w.view(cout, cin), b)
         if residual is not None:
             y = y + nhwc(residual).view(-1, cout)
         if act == 'relu':
@@ -483,3 +483,46 @@ def conv2d(x, w, b, stride, padding, act, residual):
             y = reference.act_fn(y, act)
         return from_nhwc(y.view(B, H, W, cout))
     return None
+
+
+# ---------------------------------------------------------------------------- linear with MFMA split-R wgrad
+class _Linear(torch.autograd.Function):
+    """y = x W^T + b on hipBLASLt (forward and dX are well-shaped library GEMMs); dW and db come from the
+    split-R MFMA kernel (``wgrad.hip``): the library tiles only the small N x K output of dW = dY^T X and
+    runs a handful of workgroups for R ~ 10^5..10^7 rows."""
+
+    @staticmethod
+    def forward(ctx, x2, w, b):
+        y = torch.nn.functional.linear(x2, w, b)
+        ctx.save_for_backward(x2, w)
+        ctx.b_dtype = b.dtype if b is not None else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
+        has_b = ctx.b_dtype is not None
+        dw, db = _C.wgrad(dy, x2, 0, has_b)
+        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None)
+
+
+_WGRAD_MIN_ROWS = 4096
+
+
+def linear(x, w, b=None):
+    """bf16 linear over the last dim of x with the native weight gradient when the row count is large.
+    Returns None when the shapes are not covered (the caller uses F.linear)."""
+    N, K = w.shape
+    R = x.numel() // K if K else 0
+    lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
+    if not lowp or R < _WGRAD_MIN_ROWS or N % 8 or K % 8 or R * max(N, K) * 2 >= 0x7ffffff0:
+        return torch.nn.functional.linear(x, w, b)
+    ensure_loaded()
+    xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
+    wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
+    bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
+    with torch.autocast('cuda', enabled=False):
+        y = _Linear.apply(xb, wb, bb)
+    return y.view(*x.shape[:-1], N)

@@ -365,3 +365,59 @@ def test_conv1x1_gemm_path_matches_conv():
     y = ops.conv2d(x, w, b, 1, 0, act='relu')
     yr = torch.relu(torch.nn.functional.conv2d(x, w, b))
     assert _err(y, yr) < 1e-3
+
+
+@pytest.mark.parametrize('R,N,K', [(5000, 128, 128), (100003, 256, 768), (70001, 32, 56), (4097, 1024, 256),
+                                   (300, 64, 64), (145920, 128, 128)])
+def test_wgrad_dense_matches_fp32(R, N, K):
+    from applestar_amd.ops import native
+    C = native.ensure_loaded()
+    torch.manual_seed(11)
+    dy = torch.randn(R, N, device=DEV).to(torch.bfloat16)
+    x = torch.randn(R, K, device=DEV).to(torch.bfloat16)
+    dw, db = C.wgrad(dy, x, 0, True)
+    ref_w = dy.float().t() @ x.float()
+    ref_b = dy.float().sum(0)
+    assert dw.dtype == torch.float32 and dw.shape == (N, K) and db.shape == (N,)
+    scale = R ** 0.5
+    assert _err(dw, ref_w) < 1e-3 * scale, _err(dw, ref_w)
+    assert _err(db, ref_b) < 1e-3 * scale
+    dw2, db2 = C.wgrad(dy, x, 0, False)
+    assert db2 is None
+    assert torch.equal(dw2, dw)            # deterministic (fixed split, ordered partial sum)
+
+
+@pytest.mark.parametrize('B,H,W,cin,cout', [(5, 19, 20, 128, 128), (2, 76, 80, 32, 64), (3, 7, 5, 64, 32),
+                                            (4, 38, 40, 64, 128)])
+def test_wgrad_conv3x3_matches_fp32(B, H, W, cin, cout):
+    from applestar_amd.ops import native
+    C = native.ensure_loaded()
+    torch.manual_seed(12)
+    x = torch.randn(B, H, W, cin, device=DEV).to(torch.bfloat16)
+    dy = torch.randn(B, H, W, cout, device=DEV).to(torch.bfloat16)
+    dw, db = C.wgrad(dy.view(-1, cout), x, cin, True)
+    xs = x.float().permute(0, 3, 1, 2)
+    dys = dy.float().permute(0, 3, 1, 2)
+    ref_w = torch.nn.grad.conv2d_weight(xs, (cout, cin, 3, 3), dys, padding=1)      # [Cout,Cin,3,3]
+    got = dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2)
+    scale = (B * H * W) ** 0.5
+    assert _err(got, ref_w) < 1e-3 * scale, _err(got, ref_w)
+    assert _err(db, dys.sum((0, 2, 3))) < 1e-3 * scale
+
+
+def test_native_linear_autocast_grads_match_fp32():
+    from applestar_amd import ops
+    torch.manual_seed(13)
+    x = torch.randn(9000, 256, device=DEV, requires_grad=True)
+    w = (torch.randn(128, 256, device=DEV) / 16).requires_grad_()
+    b = torch.randn(128, device=DEV, requires_grad=True)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y = ops.linear(x, w, b)     # (no ReLU: bf16 vs fp32 mask flips near 0 would dominate the dX error)
+    assert y.dtype == torch.bfloat16
+    g = torch.randn(9000, 128, device=DEV)
+    y.float().backward(g)
+    xs, ws, bs = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    (xs @ ws.t() + bs).backward(g)
+    assert w.grad.dtype == torch.float32 and b.grad.dtype == torch.float32
+    for a, r in ((x.grad, xs.grad), (w.grad, ws.grad), (b.grad, bs.grad)):
+        assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
