@@ -589,6 +589,32 @@ std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t
   return {dw, db};
 }
 
+// ---------------------------------------------------------------- conv epilogue backward -> NHWC bf16
+// dout: [B, H, W, C] view (NHWC- or NCHW-contiguous underneath); out: NHWC bf16 (used when relu).
+at::Tensor act_grad_nhwc(const at::Tensor& dout, const c10::optional<at::Tensor>& out, bool relu) {
+  TORCH_CHECK(dout.is_cuda() && dout.dim() == 4, "act_grad: dout [B,H,W,C] GPU");
+  const int64_t B = dout.size(0), H = dout.size(1), W = dout.size(2), C = dout.size(3);
+  at::Tensor d = dout;
+  bool nchw = false;
+  if (!d.is_contiguous()) {
+    if (d.permute({0, 3, 1, 2}).is_contiguous() && C % 32 == 0) nchw = true;
+    else d = d.contiguous();
+  }
+  TORCH_CHECK(C % 8 == 0, "act_grad: C % 8");
+  const void* op = nullptr;
+  if (relu) {
+    TORCH_CHECK(out.has_value(), "act_grad: relu needs out");
+    check_cuda(*out, "out");
+    TORCH_CHECK(out->scalar_type() == at::kBFloat16 && out->sizes() == dout.sizes(), "act_grad: out NHWC bf16");
+    op = out->data_ptr();
+  }
+  c10::hip::HIPGuard g(dout.device().index());
+  auto dpre = at::empty({B, H, W, C}, dout.options().dtype(at::kBFloat16));
+  as::act_grad_nhwc(d.data_ptr(), dt(d), nchw, op, dpre.data_ptr(), static_cast<int>(B), static_cast<int>(C),
+                    static_cast<int>(H * W), relu ? 1 : 0, stream());
+  return dpre;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "applestar_amd HIP kernels for gfx950 (MI355X)";
   m.def("layer_norm_fwd", &layer_norm_fwd);
@@ -617,5 +643,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("table_grad", &table_grad);
   m.def("conv3x3_fwd", &conv3x3_fwd);
   m.def("wgrad", &wgrad);
+  m.def("act_grad_nhwc", &act_grad_nhwc);
   m.def("conv3x3_supported", [](int64_t cin, int64_t cout) { return as::conv3x3_supported(static_cast<int>(cin), static_cast<int>(cout)); });
 }

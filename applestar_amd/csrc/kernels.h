@@ -157,6 +157,12 @@ void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* re
 // Cin == 0: x [R, K] bf16 (dense).  Cin > 0: x NHWC [R / (H W), H, W, Cin] bf16, K = 9 Cin (3x3 pad-1 conv).
 // N % 8 == 0, K % 8 == 0 (Cin % 8 == 0), R * max(N, K or Cin) * 2 < 2^31.
 int wgrad_splits(long R, int N, int K);
+
+// ---- act_grad.hip ------------------------------------------------------------------------------
+// dpre NHWC bf16 [B, HW, C] = dout * (out > 0) (relu) or dout; dout fp32/bf16, NHWC or (dout_nchw) NCHW
+// contiguous; out NHWC bf16.  C % 8 == 0 (NHWC) / C % 32 == 0 (NCHW).
+void act_grad_nhwc(const void* dout, int dt, bool dout_nchw, const void* out, void* dpre, int B, int C, int HW, int relu,
+                   hipStream_t s);
 void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long R, int N, int K, int H, int W, int Cin,
            int S, hipStream_t st);
 }  // namespace as

@@ -428,10 +428,7 @@ class _Conv3x3(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         x, w, out = ctx.saved_tensors
-        dpre = dout.contiguous()
-        if ctx.act == 'relu':
-            dpre = dpre * (out > 0)
-        dpre = dpre.to(torch.bfloat16).contiguous()
+        dpre = _C.act_grad_nhwc(dout, out, ctx.act == 'relu')    # one pass: mask + cast + NHWC
         wt = w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()   # [Cin,3,3,Cout]
         dx = _C.conv3x3_fwd(dpre, wt, None, None, 0)
         has_b = ctx.b_dtype is not None

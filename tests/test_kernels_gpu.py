@@ -421,3 +421,25 @@ def test_native_linear_autocast_grads_match_fp32():
     assert w.grad.dtype == torch.float32 and b.grad.dtype == torch.float32
     for a, r in ((x.grad, xs.grad), (w.grad, ws.grad), (b.grad, bs.grad)):
         assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
+
+
+@pytest.mark.parametrize('layout', ['nhwc', 'nchw', 'strided'])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('relu', [False, True])
+def test_act_grad_nhwc(layout, dtype, relu):
+    from applestar_amd.ops import native
+    C = native.ensure_loaded()
+    torch.manual_seed(14)
+    B, H, W, Ch = 3, 19, 21, 64
+    out = torch.randn(B, H, W, Ch, device=DEV).to(torch.bfloat16)
+    g = torch.randn(B, Ch, H, W, device=DEV).to(dtype)
+    if layout == 'nhwc':
+        dout = g.permute(0, 2, 3, 1).contiguous()
+    elif layout == 'nchw':
+        dout = g.permute(0, 2, 3, 1)                     # NCHW-contiguous underneath
+    else:
+        dout = g.permute(0, 2, 3, 1)[:, :, ::1, :].transpose(1, 2).contiguous().transpose(1, 2)
+    got = C.act_grad_nhwc(dout, out, relu)
+    ref = dout.float() * (out > 0) if relu else dout.float()
+    assert got.dtype == torch.bfloat16 and got.is_contiguous()
+    assert _err(got, ref) <= 1e-2 * ref.abs().max().item()
