@@ -42,6 +42,34 @@ DEFAULT_MODEL_CONFIG = AttrDict({
 })
 
 
+_SIDE_STREAMS: Dict[int, 'torch.cuda.Stream'] = {}
+SIDE_STREAMS_ENABLED = True
+
+
+def _side_stream_call(fn, inputs):
+    """Run ``fn(inputs)`` on a per-device side stream (GPU) and return a handle for :func:`_side_stream_join`."""
+    dev = next((v.device for v in inputs.values() if torch.is_tensor(v)), None) if isinstance(inputs, dict) else None
+    if dev is None or dev.type != 'cuda' or not SIDE_STREAMS_ENABLED:
+        return fn(inputs), None
+    main = torch.cuda.current_stream(dev)
+    side = _SIDE_STREAMS.get(dev.index)
+    if side is None:
+        side = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(dev)
+    side.wait_stream(main)                 # inputs were produced on the main stream
+    with torch.cuda.stream(side):
+        out = fn(inputs)
+    return out, side
+
+
+def _side_stream_join(handle):
+    out, side = handle
+    if side is not None:
+        main = torch.cuda.current_stream(out.device)
+        main.wait_stream(side)
+        out.record_stream(main)            # allocated on the side stream, consumed on main
+    return out
+
+
 class ValueBaseline(nn.Module):
     """fc(in->256, ReLU) -> 16 x ResFCBlock2 -> fc(256->1, gain .1) [-> (2/pi) atan(pi/2 x)] (value.py:9-39)."""
 
@@ -175,6 +203,12 @@ class Model(nn.Module):
         B, T = batch_size, unroll_len
         flat_action = {k: v.flatten(0, 1) for k, v in action_info.items()}
         flat_su_num = selected_units_num.flatten(0, 1)
+        # The opponent-aware value encoder depends only on its own inputs: on the GPU it runs on a side HIP
+        # stream, overlapping the policy encoders and the latency-bound core LSTM (which occupies a handful
+        # of CUs); autograd replays its backward on the same side stream, so that overlaps as well.
+        vf = None
+        if self._use_value_feature:
+            vf = _side_stream_call(self.value_encoder, value_feature)
         lstm_input, scalar_context, baseline_feature, entity_embeddings, map_skip = self._encode(
             spatial_info, entity_info, scalar_info, entity_num)
         H = hidden_state[0][0].shape[-1]
@@ -190,7 +224,7 @@ class Model(nn.Module):
             critic_input = critic_input.detach()
             baseline_feature = baseline_feature.detach()
         if self._use_value_feature:
-            vf = self.value_encoder(value_feature)
+            vf = _side_stream_join(vf)
             critic_input = torch.cat([critic_input.to(vf.dtype), vf, baseline_feature.to(vf.dtype)], 1)
         values = {k: v(critic_input).view(T + 1, B) for k, v in self.value_networks.items()}
         for k in list(logits):

@@ -49,7 +49,9 @@ masked_attention = ref.masked_attention
 def linear(x, w, b=None, act=None):
     """act(x W^T + b).  GPU: hipBLASLt forward / dX, MFMA split-R kernel for dW / db of tall inputs."""
     n = _native(x)
-    y = n.linear(x, w, b) if n is not None else F.linear(x, w, b)
+    if n is not None:
+        return n.linear(x, w, b, act)
+    y = F.linear(x, w, b)
     if act is None:
         return y
     return ref.act_fn(y, act)

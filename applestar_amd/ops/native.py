@@ -246,9 +246,16 @@ class _SpatialEmbed(torch.autograd.Function):
     def backward(ctx, dout):
         out, bits, ex, ey, entity_num, *tensors = ctx.saved_tensors
         planes, effects = list(tensors[:ctx.n_planes]), list(tensors[ctx.n_planes:])
-        dpre = (dout * (out > 0)).to(out.dtype).contiguous()                    # [B,H,W,32]
+        lowp = out.dtype == torch.bfloat16
+        if lowp:   # one pass: ReLU mask + cast + NHWC
+            dpre = _C.act_grad_nhwc(dout, out, True)
+        else:
+            dpre = (dout * (out > 0)).to(out.dtype).contiguous()                # [B,H,W,32]
         drows = _C.spatial_gather_rows(dpre, ex, ey, entity_num, ctx.N).to(ctx.rows_dtype)
         X = _C.spatial_dense_input(planes, effects, bits, _dt_code(out.dtype))  # [npix,24]
+        if lowp and X.numel() * 2 < 0x7ffffff0 and dpre.numel() * 2 < 0x7ffffff0:
+            dw, db = _C.wgrad(dpre.view(-1, 32), X.view(-1, 24), 0, True)       # split-R MFMA, bias fused
+            return (dw, db, drows) + (None,) * (5 + len(tensors))
         B = dpre.shape[0]
         # K = B*H*W ~ 1e7 is far too deep for one GEMM tile: batch over observations, then sum
         d3 = dpre.view(B, -1, 32)
@@ -470,56 +477,72 @@ def conv2d(x, w, b, stride, padding, act, residual):
             return from_nhwc(_Conv3x3.apply(xl, wl, b, rl, act))
     if kh == 1 and kw == 1 and padding == 0:
         B, _, H, W = x.shape
-        y = linear(nhwc(x).view(-1, cin), w.view(cout, cin), b)
-        if residual is not None:
-            y = y + nhwc(residual).view(-1, cout)
-        if act == 'relu':
-            y = torch.relu(y)
-        elif act is not None:
-            from . import reference
-            y = reference.act_fn(y, act)
+        if residual is None:
+            y = linear(nhwc(x).view(-1, cin), w.view(cout, cin), b, act)
+        else:
+            y = linear(nhwc(x).view(-1, cin), w.view(cout, cin), b) + nhwc(residual).view(-1, cout)
+            if act is not None:
+                from . import reference
+                y = reference.act_fn(y, act)
         return from_nhwc(y.view(B, H, W, cout))
     return None
 
 
 # ---------------------------------------------------------------------------- linear with MFMA split-R wgrad
 class _Linear(torch.autograd.Function):
-    """y = x W^T + b on hipBLASLt (forward and dX are well-shaped library GEMMs); dW and db come from the
-    split-R MFMA kernel (``wgrad.hip``): the library tiles only the small N x K output of dW = dY^T X and
-    runs a handful of workgroups for R ~ 10^5..10^7 rows."""
+    """y = act(x W^T + b) on hipBLASLt (ReLU fused into the GEMM epilogue via ``_addmm_activation``; dX
+    is a well-shaped library GEMM); dW and db come from the split-R MFMA kernel (``wgrad.hip``): the
+    library tiles only the small N x K output of dW = dY^T X and runs a handful of workgroups for
+    R ~ 10^5..10^7 rows.  The ReLU mask is applied to dY by the one-pass ``act_grad`` kernel."""
 
     @staticmethod
-    def forward(ctx, x2, w, b):
-        y = torch.nn.functional.linear(x2, w, b)
-        ctx.save_for_backward(x2, w)
+    def forward(ctx, x2, w, b, relu):
+        if relu and b is not None:
+            y = torch._addmm_activation(b, x2, w.t(), use_gelu=False)
+        else:
+            y = torch.nn.functional.linear(x2, w, b)
+            if relu:
+                y = torch.relu(y)
+        ctx.save_for_backward(x2, w, y if relu else None)
+        ctx.relu = relu
         ctx.b_dtype = b.dtype if b is not None else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x2, w = ctx.saved_tensors
-        dy = dy.to(torch.bfloat16).contiguous()
+        x2, w, y = ctx.saved_tensors
+        if ctx.relu:
+            R, N = y.shape
+            dy = _C.act_grad_nhwc(dy.view(1, 1, R, N) if dy.is_contiguous() else dy.contiguous().view(1, 1, R, N),
+                                  y.view(1, 1, R, N), True).view(R, N)
+        else:
+            dy = dy.to(torch.bfloat16).contiguous()
         dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
         has_b = ctx.b_dtype is not None
         dw, db = _C.wgrad(dy, x2, 0, has_b)
-        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None)
+        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None), None
 
 
 _WGRAD_MIN_ROWS = 4096
 
 
-def linear(x, w, b=None):
-    """bf16 linear over the last dim of x with the native weight gradient when the row count is large.
-    Returns None when the shapes are not covered (the caller uses F.linear)."""
+def linear(x, w, b=None, act=None):
+    """bf16 act(x W^T + b) over the last dim of x with the native weight gradient when the row count is
+    large; other shapes take F.linear (+ the activation)."""
     N, K = w.shape
     R = x.numel() // K if K else 0
     lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
-    if not lowp or R < _WGRAD_MIN_ROWS or N % 8 or K % 8 or R * max(N, K) * 2 >= 0x7ffffff0:
-        return torch.nn.functional.linear(x, w, b)
+    if not lowp or R < _WGRAD_MIN_ROWS or N % 8 or K % 8 or R * max(N, K) * 2 >= 0x7ffffff0 or \
+            act not in (None, 'relu'):
+        y = torch.nn.functional.linear(x, w, b)
+        if act is None:
+            return y
+        from . import reference
+        return reference.act_fn(y, act)
     ensure_loaded()
     xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
     wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
     bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
     with torch.autocast('cuda', enabled=False):
-        y = _Linear.apply(xb, wb, bb)
+        y = _Linear.apply(xb, wb, bb, act == 'relu')
     return y.view(*x.shape[:-1], N)

@@ -98,7 +98,7 @@ class RLTrainer:
             out = self.model.rl_learner_forward(**batch)
         info = self.loss.compute_loss(out)
         self.reducer.zero_grad()
-        info['total_loss'].backward()
+        self.reducer.backward(info['total_loss'])
         if self.master is not None:
             self.master.synchronize()
         else:

@@ -74,7 +74,7 @@ class SLTrainer:
                                       batch['entity_num'], infer_action)
         if self.iter >= self.ignore_steps:
             self.reducer.zero_grad()
-            info['total_loss'].backward()
+            self.reducer.backward(info['total_loss'])
             self.reducer.synchronize()
             info['gradient'] = self.grad_clip.apply(self.params)
             self.optimizer.step()

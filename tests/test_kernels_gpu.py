@@ -443,3 +443,19 @@ def test_act_grad_nhwc(layout, dtype, relu):
     ref = dout.float() * (out > 0) if relu else dout.float()
     assert got.dtype == torch.bfloat16 and got.is_contiguous()
     assert _err(got, ref) <= 1e-2 * ref.abs().max().item()
+
+
+def test_native_linear_relu_epilogue_grads():
+    from applestar_amd import ops
+    torch.manual_seed(15)
+    x = torch.randn(6000, 256, device=DEV).to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(1024, 256, device=DEV) / 16).to(torch.bfloat16).requires_grad_()
+    b = (0.1 * torch.randn(1024, device=DEV)).to(torch.bfloat16).requires_grad_()
+    y = ops.linear(x, w, b, act='relu')
+    yr = torch.relu(x.float() @ w.float().t() + b.float())
+    assert y.dtype == torch.bfloat16 and _err(y, yr) < 3e-2 * yr.abs().max().item()
+    g = torch.randn(6000, 1024, device=DEV)
+    y.backward(g)
+    dpre = g * (y.detach() > 0)                          # same mask as the bf16 forward
+    for a, r in ((x.grad, dpre @ w.float()), (w.grad, dpre.t() @ x.float()), (b.grad, dpre.sum(0))):
+        assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
