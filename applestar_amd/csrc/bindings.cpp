@@ -1,5 +1,6 @@
 // PyTorch bindings for the applestar_amd HIP kernels.  Tensor checks happen here; the launchers in
 // kernels/*.hip only see raw pointers and the current HIP stream (graph-capturable).
+#include <cstring>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPGuard.h>
@@ -615,6 +616,47 @@ at::Tensor act_grad_nhwc(const at::Tensor& dout, const c10::optional<at::Tensor>
   return dpre;
 }
 
+// ---------------------------------------------------------------- multi-tensor copy (+ dtype conversion)
+// dst[i].copy_(src[i]) for same-shape, same-stride, non-overlapping-and-dense pairs (storage order copy);
+// pairs that do not qualify are copied with copy_.  One H2D upload of the chunk table + one launch.
+void multi_copy(const std::vector<at::Tensor>& dsts, const std::vector<at::Tensor>& srcs) {
+  TORCH_CHECK(dsts.size() == srcs.size(), "multi_copy: list sizes");
+  if (dsts.empty()) return;
+  c10::hip::HIPGuard g(dsts[0].device().index());
+  as::CopyArgs a;
+  a.ntensors = 0;
+  a.chunk_start[0] = 0;
+  auto flush = [&]() {
+    if (a.ntensors > 0) as::multi_copy(a, stream());
+    a.ntensors = 0;
+    a.chunk_start[0] = 0;
+  };
+  for (size_t i = 0; i < dsts.size(); ++i) {
+    const at::Tensor& d = dsts[i];
+    const at::Tensor& s = srcs[i];
+    TORCH_CHECK(d.is_cuda() && s.is_cuda() && d.sizes() == s.sizes(), "multi_copy: GPU tensors of equal shape");
+    const bool ok = d.strides() == s.strides() && d.is_non_overlapping_and_dense() &&
+                    (d.scalar_type() == at::kFloat || d.scalar_type() == at::kBFloat16) &&
+                    (s.scalar_type() == at::kFloat || s.scalar_type() == at::kBFloat16);
+    if (!ok) {
+      at::Tensor dd = d;
+      dd.copy_(s);
+      continue;
+    }
+    const long n = d.numel();
+    if (n == 0) continue;
+    // storage-order copy: the lowest address of a non-overlapping dense tensor is its data_ptr
+    const int t = a.ntensors++;
+    a.src[t] = s.data_ptr();
+    a.dst[t] = d.data_ptr();
+    a.n[t] = n;
+    a.dts[t] = static_cast<unsigned char>((s.scalar_type() == at::kFloat ? 1 : 0) | (d.scalar_type() == at::kFloat ? 2 : 0));
+    a.chunk_start[t + 1] = a.chunk_start[t] + static_cast<int>((n + as::kCopyChunk - 1) / as::kCopyChunk);
+    if (a.ntensors == as::kCopyMaxT) flush();
+  }
+  flush();
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "applestar_amd HIP kernels for gfx950 (MI355X)";
   m.def("layer_norm_fwd", &layer_norm_fwd);
@@ -643,6 +685,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("table_grad", &table_grad);
   m.def("conv3x3_fwd", &conv3x3_fwd);
   m.def("wgrad", &wgrad);
+  m.def("multi_copy", &multi_copy);
   m.def("act_grad_nhwc", &act_grad_nhwc);
   m.def("conv3x3_supported", [](int64_t cin, int64_t cout) { return as::conv3x3_supported(static_cast<int>(cin), static_cast<int>(cout)); });
 }

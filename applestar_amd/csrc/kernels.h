@@ -158,6 +158,19 @@ void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* re
 // N % 8 == 0, K % 8 == 0 (Cin % 8 == 0), R * max(N, K or Cin) * 2 < 2^31.
 int wgrad_splits(long R, int N, int K);
 
+// ---- multi_copy.hip ----------------------------------------------------------------------------
+constexpr int kCopyMaxT = 64;
+constexpr long kCopyChunk = 8192;
+struct CopyArgs {                     // passed by value (< 2 KB of kernel arguments)
+  int ntensors;
+  int chunk_start[kCopyMaxT + 1];     // prefix sums of ceil(n / kCopyChunk)
+  const void* src[kCopyMaxT];
+  void* dst[kCopyMaxT];
+  long n[kCopyMaxT];
+  unsigned char dts[kCopyMaxT];       // bit 0: src fp32, bit 1: dst fp32 (else bf16)
+};
+void multi_copy(const CopyArgs& a, hipStream_t s);
+
 // ---- act_grad.hip ------------------------------------------------------------------------------
 // dpre NHWC bf16 [B, HW, C] = dout * (out > 0) (relu) or dout; dout fp32/bf16, NHWC or (dout_nchw) NCHW
 // contiguous; out NHWC bf16.  C % 8 == 0 (NHWC) / C % 32 == 0 (NCHW).

@@ -73,8 +73,48 @@ class MasterWeights:
     def zero_grad(self):
         self.reducer.zero_grad()
 
+    def backward(self, loss: torch.Tensor):
+        """Backward into the master gradient.  Multi-rank: into the bf16 buckets (hooks overlap the
+        all-reduces with backward; :meth:`synchronize` then gathers them into the fp32 master grad).
+        Single rank: ``autograd.grad`` and ONE native multi-tensor copy that writes every bf16 gradient,
+        converted, straight into its fp32 master-grad slot (and the fp32 ones into their buckets) - no
+        per-parameter accumulate / copy launches, no bucket round trip."""
+        self._direct = False
+        if self.reducer.world > 1 or not loss.is_cuda:
+            self.reducer.backward(loss)
+            return
+        from ..ops import native
+        C = native.ensure_loaded()
+        grads = torch.autograd.grad(loss, self.reducer.params, allow_unused=True)
+        mg = self._master_grad_views()
+        dst, src = [], []
+        for p, g in zip(self.reducer.params, grads):
+            if g is not None:
+                dst.append(mg.get(p, p.grad))
+                src.append(g)
+        if len(dst) < len(self.reducer.params):   # unused parameters (e.g. value pre-training) get zeros
+            self.master.grad.zero_()
+        C.multi_copy(dst, src)
+        self._direct = True
+
+    def _master_grad_views(self):
+        views = getattr(self, '_mg_views', None)
+        if views is None:
+            views = {}
+            g = self.master.grad
+            for b, off, _ in self._slices:
+                o2 = off
+                for p in b.params:
+                    m = p.numel()
+                    views[p] = g[o2:o2 + m].as_strided(p.shape, p.stride(), g.storage_offset() + o2)
+                    o2 += m
+            self._mg_views = views
+        return views
+
     def synchronize(self):
         """All-reduce (if distributed) and gather the bf16 gradients into the flat fp32 master grad."""
+        if getattr(self, '_direct', False):
+            return
         self.reducer.synchronize()
         g = self.master.grad
         for b, off, k in self._slices:

@@ -98,7 +98,10 @@ class RLTrainer:
             out = self.model.rl_learner_forward(**batch)
         info = self.loss.compute_loss(out)
         self.reducer.zero_grad()
-        self.reducer.backward(info['total_loss'])
+        if self.master is not None:
+            self.master.backward(info['total_loss'])
+        else:
+            self.reducer.backward(info['total_loss'])
         if self.master is not None:
             self.master.synchronize()
         else:

@@ -459,3 +459,29 @@ def test_native_linear_relu_epilogue_grads():
     dpre = g * (y.detach() > 0)                          # same mask as the bf16 forward
     for a, r in ((x.grad, dpre @ w.float()), (w.grad, dpre.t() @ x.float()), (b.grad, dpre.sum(0))):
         assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
+
+
+def test_multi_copy_converts_and_handles_many_tensors():
+    from applestar_amd.ops import native
+    C = native.ensure_loaded()
+    torch.manual_seed(16)
+    srcs, dsts = [], []
+    flat = torch.zeros(4 * 10 ** 6, device=DEV)
+    off = 0
+    for i in range(150):                              # > kCopyMaxT tensors -> several launches
+        shape = (int(torch.randint(1, 40, ()).item()), int(torch.randint(1, 700, ()).item()))
+        n = shape[0] * shape[1]
+        s = torch.randn(shape, device=DEV).to(torch.bfloat16 if i % 2 else torch.float32)
+        d = flat[off:off + n].view(shape) if i % 3 else torch.empty(shape, device=DEV, dtype=torch.bfloat16)
+        off += n
+        srcs.append(s)
+        dsts.append(d)
+    conv_w = torch.randn(64, 32, 3, 3, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    conv_d = torch.empty(64, 32, 3, 3, device=DEV).contiguous(memory_format=torch.channels_last)
+    srcs.append(conv_w)
+    dsts.append(conv_d)
+    srcs.append(torch.randn(3, 5, device=DEV).t())     # stride mismatch -> copy_ fallback
+    dsts.append(torch.empty(5, 3, device=DEV))
+    C.multi_copy(dsts, srcs)
+    for d, s in zip(dsts, srcs):
+        assert torch.equal(d, s.to(d.dtype)), (d.shape, d.dtype, s.dtype)

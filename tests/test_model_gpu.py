@@ -68,3 +68,31 @@ def test_trajectory_ring_on_gpu_matches_host_collate():
             assert a.shape == b.shape, path
             assert torch.equal(a.to(b.dtype), b.cpu()), path
     cmp(ref, got)
+
+
+def test_direct_master_grad_matches_bucket_path():
+    """Single-rank autograd.grad + native multi-tensor copy into the fp32 master grad == the bucket path
+    (AccumulateGrad into bf16 bucket views, then bucket -> master copy)."""
+    torch.manual_seed(0)
+    tr = RLTrainer(CFG, device='cuda')
+    batch = to_device(rl_batch(2, 4, max_entities=64, seed=3), 'cuda')
+
+    def loss():
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            out = tr.model.rl_learner_forward(**dict(batch))
+        return tr.loss.compute_loss(out)['total_loss']
+
+    tr.reducer.zero_grad()
+    tr.master.backward(loss())
+    tr.master.synchronize()
+    direct = tr.master.master.grad.clone()
+    fp32_direct = [p.grad.detach().float().clone() for p in tr.master.fp32_params]
+    tr.reducer.zero_grad()
+    loss().backward()                      # AccumulateGrad into the bucket views
+    tr.master._direct = False
+    tr.master.synchronize()
+    ref = tr.master.master.grad
+    scale = ref.abs().max().item()
+    assert (direct - ref).abs().max().item() <= 2e-2 * scale
+    for a, p in zip(fp32_direct, tr.master.fp32_params):
+        assert (a - p.grad.float()).abs().max().item() <= 2e-2 * max(1.0, p.grad.abs().max().item())
