@@ -1,6 +1,9 @@
 // PyTorch bindings for the applestar_amd HIP kernels.  Tensor checks happen here; the launchers in
 // kernels/*.hip only see raw pointers and the current HIP stream (graph-capturable).
 #include <cstring>
+#include <cstdlib>
+#include <map>
+#include <string>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPGuard.h>
@@ -123,6 +126,44 @@ std::vector<at::Tensor> gated_residual_bwd(const at::Tensor& dout, const at::Ten
 }
 
 // ---------------------------------------------------------------- LN-LSTM recurrence
+// ---------------------------------------------------------------- layer-norm LSTM recurrence
+// Split (multi-workgroup) recurrence for H = 384 and small batches; APPLESTAR_LSTM_SPLIT=0 disables it.
+bool lstm_split_enabled(int64_t H, int64_t B) {
+  static const bool env_on = [] {
+    const char* v = std::getenv("APPLESTAR_LSTM_SPLIT");
+    return v == nullptr || std::string(v) != "0";
+  }();
+  return env_on && H == 384 && B >= 1 && B <= 16;
+}
+
+// sticky device-side timeout flag of the split recurrence's cross-workgroup poll (never reset)
+at::Tensor& lstm_split_err(const at::Device& dev) {
+  static std::map<int, at::Tensor> flags;
+  auto it = flags.find(dev.index());
+  if (it == flags.end())
+    it = flags.emplace(dev.index(), at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(dev))).first;
+  return it->second;
+}
+
+at::Tensor lstm_split_error(int64_t device) {
+  return lstm_split_err(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device))).clone();
+}
+
+struct SplitBufs {
+  at::Tensor slab, cnt;
+  as::LstmSplit s;
+};
+
+SplitBufs make_split(const at::Tensor& like, int64_t B, int64_t width) {
+  SplitBufs r;
+  const int64_t Bp = (B + 7) / 8 * 8;
+  r.slab = at::empty({2, Bp, 8, width}, like.options().dtype(at::kFloat));
+  r.cnt = at::zeros({Bp}, like.options().dtype(at::kInt));
+  r.s = {r.slab.data_ptr<float>(), reinterpret_cast<unsigned*>(r.cnt.data_ptr<int>()),
+         lstm_split_err(like.device()).data_ptr<int>()};
+  return r;
+}
+
 std::vector<at::Tensor> lnlstm_fwd(const at::Tensor& xp, const at::Tensor& h0, const at::Tensor& c0,
                                    const at::Tensor& wT, const at::Tensor& lnh_w, const at::Tensor& lnh_b,
                                    const at::Tensor& lnc_w, const at::Tensor& lnc_b, double eps) {
@@ -144,12 +185,15 @@ std::vector<at::Tensor> lnlstm_fwd(const at::Tensor& xp, const at::Tensor& h0, c
   auto rstd_c = at::empty({T, B}, f);
   auto hT = at::empty({B, H}, f);
   auto cT = at::empty({B, H}, f);
+  SplitBufs sb;
+  const bool split = lstm_split_enabled(H, B);
+  if (split) sb = make_split(xp, B, G);
   as::lnlstm_fwd(xp.data_ptr<float>(), h0.data_ptr<float>(), c0.data_ptr<float>(), wT.data_ptr(), dt(wT),
                  lnh_w.data_ptr<float>(), lnh_b.data_ptr<float>(), lnc_w.data_ptr<float>(), lnc_b.data_ptr<float>(),
                  static_cast<int>(T), static_cast<int>(B), static_cast<int>(H), static_cast<float>(eps),
                  out.data_ptr<float>(), c_all.data_ptr<float>(), xhat_h.data_ptr<float>(), rstd_h.data_ptr<float>(),
                  gates.data_ptr<float>(), xhat_c.data_ptr<float>(), rstd_c.data_ptr<float>(), hT.data_ptr<float>(),
-                 cT.data_ptr<float>(), stream());
+                 cT.data_ptr<float>(), stream(), split ? &sb.s : nullptr);
   return {out, hT, cT, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c};
 }
 
@@ -170,12 +214,15 @@ std::vector<at::Tensor> lnlstm_bwd(const at::Tensor& dout, const at::Tensor& dhT
   auto dc_ln = at::empty({T, B, H}, f);
   auto dh0 = at::empty({B, H}, f);
   auto dc0 = at::empty({B, H}, f);
+  SplitBufs sb;
+  const bool split = lstm_split_enabled(H, B);
+  if (split) sb = make_split(gates, B, H);
   as::lnlstm_bwd(dout.data_ptr<float>(), dhT.data_ptr<float>(), dcT.data_ptr<float>(), gates.data_ptr<float>(),
                  c_all.data_ptr<float>(), xhat_c.data_ptr<float>(), rstd_c.data_ptr<float>(), xhat_h.data_ptr<float>(),
                  rstd_h.data_ptr<float>(), w.data_ptr(), dt(w), lnh_w.data_ptr<float>(), lnc_w.data_ptr<float>(),
                  static_cast<int>(T), static_cast<int>(B), static_cast<int>(H), dgates.data_ptr<float>(),
                  dhg.data_ptr<float>(), dc_ln.data_ptr<float>(), dh0.data_ptr<float>(), dc0.data_ptr<float>(),
-                 stream());
+                 stream(), split ? &sb.s : nullptr);
   return {dgates, dhg, dc_ln, dh0, dc0};
 }
 
@@ -685,6 +732,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("table_grad", &table_grad);
   m.def("conv3x3_fwd", &conv3x3_fwd);
   m.def("wgrad", &wgrad);
+  m.def("lstm_split_error", &lstm_split_error);
   m.def("multi_copy", &multi_copy);
   m.def("act_grad_nhwc", &act_grad_nhwc);
   m.def("conv3x3_supported", [](int64_t cin, int64_t cout) { return as::conv3x3_supported(static_cast<int>(cin), static_cast<int>(cout)); });

@@ -54,15 +54,24 @@ int elementwise_blocks(long n);
 // (fp32 or bf16). Saves what BPTT needs: c_all [T+1,B,H], xhat_h/gates [T,B,4H], xhat_c [T,B,H],
 // rstd_h/rstd_c [T,B].
 bool lnlstm_supported(int H);
+// Split recurrence (H = 384): 8 workgroups per row exchange partial products through `slab`
+// ([2, Bp, 8, 4H] fwd / [2, Bp, 8, H] bwd fp32, Bp = B rounded up to 8) with per-row counters `cnt`
+// ([Bp] u32, zeroed before the launch); a poll that times out sets *err.  All Bp * 8 workgroups must be
+// co-resident (callers keep B <= 16).
+struct LstmSplit {
+  float* slab;
+  unsigned* cnt;
+  int* err;
+};
 void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* wT, int w_dt, const float* lnh_w,
                 const float* lnh_b, const float* lnc_w, const float* lnc_b, int T, int B, int H, float eps, float* out,
                 float* c_all, float* xhat_h, float* rstd_h, float* gates, float* xhat_c, float* rstd_c, float* hT,
-                float* cT, hipStream_t s);
+                float* cT, hipStream_t s, const LstmSplit* split = nullptr);
 // w = W_hh [4H][H]. Outputs d(xp) [T,B,4H], d(h W_hh^T) [T,B,4H], dL/d(LN_c out) [T,B,H], dh0, dc0.
 void lnlstm_bwd(const float* dout, const float* dhT, const float* dcT, const float* gates, const float* c_all,
                 const float* xhat_c, const float* rstd_c, const float* xhat_h, const float* rstd_h, const void* w,
                 int w_dt, const float* lnh_w, const float* lnc_w, int T, int B, int H, float* dgates, float* dhg,
-                float* dc_ln, float* dh0, float* dc0, hipStream_t s);
+                float* dc_ln, float* dh0, float* dc0, hipStream_t s, const LstmSplit* split = nullptr);
 
 // ---- entity.hip ------------------------------------------------------------------------------
 // out[t] = relu(bias + sum_fields W^T[row(field value)]) for packed entity t (source row index[t]).

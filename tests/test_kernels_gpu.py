@@ -84,9 +84,13 @@ def test_reverse_scan():
     assert _err(y, ref) < 1e-5
 
 
-@pytest.mark.parametrize('H,I,T,B', [(384, 1536, 9, 6), (32, 32, 13, 37)])
+@pytest.mark.parametrize('H,I,T,B', [(384, 1536, 9, 6), (384, 384, 65, 16), (384, 1536, 3, 20), (32, 32, 13, 37)])
 @pytest.mark.parametrize('autocast', [False, True])
 def test_lnlstm_layer_matches_reference(H, I, T, B, autocast):
+    # H = 384, B <= 16 runs the split (8 workgroups per row, cross-workgroup all-reduce) recurrence;
+    # B = 20 the one-workgroup-per-row kernel
+    if autocast and T > 16:
+        pytest.skip('bf16 weights vs the fp32 oracle diverge chaotically over long sequences; fp32 covers T=65')
     torch.manual_seed(3)
     x = torch.randn(T, B, I, device=DEV, requires_grad=True)
     h0 = (0.5 * torch.randn(B, H, device=DEV)).requires_grad_()
@@ -110,6 +114,8 @@ def test_lnlstm_layer_matches_reference(H, I, T, B, autocast):
     for a, b in zip([x, h0, c0] + params, ref_in):
         scale = max(1.0, b.grad.abs().max().item())
         assert _err(a.grad, b.grad) < tol * 4 * scale
+    torch.cuda.synchronize()
+    assert int(N.ensure_loaded().lstm_split_error(0).item()) == 0, 'split LSTM exchange timed out'
 
 
 @pytest.mark.parametrize('autocast', [False, True])
