@@ -149,7 +149,16 @@ class SelectedUnitsHead(nn.Module):
     def forward_teacher(self, ae0, entity_embedding, entity_num, selected_units_num, selected_units):
         key, base_mask = self.keys(entity_embedding, entity_num)          # [B,N+1,32], [B,N+1]
         B, N1, C = key.shape
-        S = max(int(selected_units_num.max()), 1)
+        step_ok = None
+        if key.is_cuda:
+            # static S = label width (no host sync on max(selected_units_num)); steps at or beyond the
+            # batch max are frozen out of the running selection and their logits masked to NEG, which is
+            # exactly the dynamic-S result padded to the label width
+            S = selected_units.shape[1]
+            smax = selected_units_num.max().clamp(min=1)
+            step_ok = torch.arange(S, device=key.device) < smax
+        else:
+            S = max(int(selected_units_num.max()), 1)
         labels = selected_units[:, :S].long()                             # [B,S]
         en = entity_num.long()
         # end_flag after label i; a label is added to the selected set iff no end at or before i
@@ -161,6 +170,8 @@ class SelectedUnitsHead(nn.Module):
         earlier = torch.tril(torch.ones(S, S, dtype=torch.bool, device=key.device), -1)
         dup = (same & earlier[None] & added[:, None, :]).any(-1)
         new = added & ~dup
+        if step_ok is not None:
+            new = new & step_ok[None, :]
         if self.reduce_type == 'selected_units_num':
             gathered = key.gather(1, labels.clamp(max=N1 - 1).unsqueeze(-1).expand(B, S, C))
             run_sum = torch.cumsum(gathered * new.unsqueeze(-1).to(gathered.dtype), 1)
@@ -183,6 +194,8 @@ class SelectedUnitsHead(nn.Module):
         mask = base_mask[:, None, :] & ~prev_excl
         end_pos = F.one_hot(en.clamp(max=N1 - 1), N1).bool()
         mask[:, 0] &= ~end_pos
+        if step_ok is not None:
+            mask = mask & step_ok[None, :, None]
         logits = logits.masked_fill(~mask, NEG)
         # the reference returns no sampled units in teacher-forced mode (test_iou off): None
         return logits, None, ae_after[:, -1], selected_units_num

@@ -60,7 +60,11 @@ def linear(x, w, b=None, act=None):
 def layer_norm(x, w, b, residual=None, act=None, eps: float = 1e-5):
     n = _native(x)
     if n is not None and n.has('layer_norm'):
-        return n.layer_norm(x, w, b, residual, act, eps)
+        # under autocast the normalised activations are stored in bf16 (statistics and affine in fp32):
+        # every consumer is a bf16 GEMM, so an fp32 output only bought a cast in forward and an fp32
+        # gradient cast + fp32 residual-gradient adds in backward (~0.5 GB per step in the entity encoder)
+        out_dtype = torch.bfloat16 if torch.is_autocast_enabled() else None
+        return n.layer_norm(x, w, b, residual, act, eps, out_dtype=out_dtype)
     return ref.layer_norm(x, w, b, residual, act, eps)
 
 

@@ -63,6 +63,16 @@ class ReinforcementLoss:
         self.only_update_value = False
         self._refresh()
 
+    def _head_weights(self, kind: str, device) -> torch.Tensor:
+        """Per-head pg / upgo weights as a cached device tensor (building it per call is an H2D copy
+        from pageable memory, i.e. a host sync in the middle of the step)."""
+        cache = self.__dict__.setdefault('_hw_cache', {})
+        key = (kind, str(device))
+        if key not in cache:
+            w = self.cfg.pg_head_weights if kind == 'pg' else self.cfg.upgo_head_weights
+            cache[key] = torch.tensor([w.get(h, 1.0) for h in HEADS], device=device)
+        return cache[key]
+
     def compute_loss(self, inputs: Dict) -> Dict[str, torch.Tensor]:
         logits = inputs['target_logit']
         values = dict(inputs['value'])
@@ -103,7 +113,7 @@ class ReinforcementLoss:
 
         # ---------------- V-trace policy gradient, one batched scan per baseline field
         total_pg = 0.0
-        pg_w = torch.tensor([self.cfg.pg_head_weights.get(h, 1.0) for h in HEADS], device=rho_stack.device)
+        pg_w = self._head_weights('pg', rho_stack.device)
         for field, v in values.items():
             wf = self.w.pg.get(field, 0.0)
             with torch.no_grad():
@@ -125,7 +135,7 @@ class ReinforcementLoss:
         with torch.no_grad():
             upgo_adv = rho_stack * (rl_utils.upgo_returns(r, v.detach()) - v.detach()[:-1])
         upgo = (-upgo_adv * logp_stack * head_mask).mean(dim=(1, 2))
-        upgo_w = torch.tensor([self.cfg.upgo_head_weights.get(h, 1.0) for h in HEADS], device=upgo.device)
+        upgo_w = self._head_weights('upgo', upgo.device)
         total_upgo = (upgo * upgo_w).sum() * self.w.upgo.winloss
         for i, h in enumerate(HEADS):
             info['upgo/' + h] = upgo[i].detach()

@@ -82,8 +82,11 @@ def main():
         info = trainer.step(next(it))
     sync()
     t0 = time.perf_counter()
+    host = 0.0
     for _ in range(args.steps):
+        h0 = time.perf_counter()
         info = trainer.step(next(it))
+        host += time.perf_counter() - h0
     sync()
     elapsed = time.perf_counter() - t0
     loss = float(info['total_loss'].detach())
@@ -117,6 +120,7 @@ def main():
                 'baseline_note': 'vs_baseline = per-GPU samples/s / 256 (reference RL learner, A100)',
                 'native_kernels': (not args.no_native) and gpu,
                 'final_loss': loss,
+                'host_ms_per_step': round(1000.0 * host / max(args.steps, 1), 3),
             },
         }
         print(json.dumps(out), flush=True)

@@ -1,0 +1,43 @@
+"""List the host<->device synchronisations of one RL learner step (torch.cuda.set_sync_debug_mode),
+with the applestar_amd source line that triggered each.  Usage: python tools/sync_points.py"""
+import collections
+import os
+import sys
+import traceback
+import warnings
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from applestar_amd.rl.trainer import RLTrainer  # noqa: E402
+from applestar_amd.rl.synthetic import rl_batch, to_device  # noqa: E402
+
+
+def main():
+    dev = torch.device('cuda', 0)
+    tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}, device=dev)
+    b = to_device(rl_batch(6, 64, seed=0), dev)
+    tr.step(dict(b))
+    torch.cuda.synchronize()
+    hits = collections.Counter()
+
+    def showwarning(message, category, filename, lineno, file=None, line=None):
+        where = '?'
+        for fr in reversed(traceback.extract_stack()[:-1]):
+            if 'applestar_amd' in fr.filename:
+                where = f"{fr.filename.split('applestar_amd/')[-1]}:{fr.lineno} {fr.name}: {fr.line}"
+                break
+        hits[where] += 1
+
+    warnings.showwarning = showwarning
+    warnings.simplefilter('always')
+    torch.cuda.set_sync_debug_mode('warn')
+    tr.step(dict(b))
+    torch.cuda.set_sync_debug_mode('default')
+    torch.cuda.synchronize()
+    for where, n in hits.most_common():
+        print(f'{n:4d}  {where}')
+
+
+if __name__ == '__main__':
+    main()
