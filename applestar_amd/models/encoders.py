@@ -11,7 +11,7 @@ Parameter names/shapes match ``distar/agent/default/model/obs_encoder/*.py`` and
 """
 from __future__ import annotations
 
-from typing import Dict, List, Tuple
+from typing import Dict, List, Tuple, Optional
 
 import torch
 import torch.nn as nn
@@ -183,10 +183,16 @@ class EntityEncoder(nn.Module):
         x = entity_one_hot_input(entity_info, flat_index, lin.weight.dtype)
         return ops.linear(x, lin.weight, lin.bias, act='relu')
 
-    def forward(self, entity_info: Dict[str, torch.Tensor], entity_num: torch.Tensor):
+    def forward(self, entity_info: Dict[str, torch.Tensor], entity_num: torch.Tensor,
+                entity_total: Optional[int] = None):
+        """``entity_total`` (optional host int = sum(min(entity_num, N))) lets the packing skip the
+        host<->device sync of a data-dependent ``nonzero``."""
         B, N = entity_info['unit_type'].shape
         valid = ops.sequence_mask(entity_num, N)                     # [B,N]
-        flat_index = valid.reshape(-1).nonzero().squeeze(1)         # packed row -> padded row
+        if entity_total is not None and valid.is_cuda:
+            flat_index = torch.nonzero_static(valid.reshape(-1), size=int(entity_total)).squeeze(1)
+        else:
+            flat_index = valid.reshape(-1).nonzero().squeeze(1)     # packed row -> padded row
         lens = entity_num.clamp(max=N).to(torch.int32)
         cu = F.pad(torch.cumsum(lens, 0, dtype=torch.int32), (1, 0))
         x = self.embed(entity_info, flat_index)                      # [T,256]
@@ -272,9 +278,9 @@ class Encoder(nn.Module):
         self.entity_encoder = EntityEncoder(reduce_type)
         self.scatter_project = FCBlock(256, 32, act=True)
 
-    def forward(self, spatial_info, entity_info, scalar_info, entity_num):
+    def forward(self, spatial_info, entity_info, scalar_info, entity_num, entity_total: Optional[int] = None):
         embedded_scalar, scalar_context, baseline_feature = self.scalar_encoder(scalar_info)
-        entity_embeddings, embedded_entity, entity_mask = self.entity_encoder(entity_info, entity_num)
+        entity_embeddings, embedded_entity, entity_mask = self.entity_encoder(entity_info, entity_num, entity_total)
         proj = self.scatter_project(entity_embeddings) * entity_mask.unsqueeze(2).to(entity_embeddings.dtype)
         n = ops._native(proj) if proj.is_cuda else None
         if n is not None and n.has('spatial_embed'):

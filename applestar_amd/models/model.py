@@ -162,8 +162,8 @@ class Model(nn.Module):
         self.race_mask: Optional[torch.Tensor] = None  # set by the agent in play mode (action_type_head.py:52)
 
     # ------------------------------------------------------------------ helpers
-    def _encode(self, spatial_info, entity_info, scalar_info, entity_num):
-        return self.encoder(spatial_info, entity_info, scalar_info, entity_num)
+    def _encode(self, spatial_info, entity_info, scalar_info, entity_num, entity_total=None):
+        return self.encoder(spatial_info, entity_info, scalar_info, entity_num, entity_total)
 
     def _core(self, lstm_input_seq, hidden_state):
         state = [(h.float(), c.float()) for h, c in hidden_state]
@@ -210,7 +210,7 @@ class Model(nn.Module):
         if self._use_value_feature:
             vf = _side_stream_call(self.value_encoder, value_feature)
         lstm_input, scalar_context, baseline_feature, entity_embeddings, map_skip = self._encode(
-            spatial_info, entity_info, scalar_info, entity_num)
+            spatial_info, entity_info, scalar_info, entity_num, kwargs.get('entity_total'))
         H = hidden_state[0][0].shape[-1]
         h0 = [(h.view(-1, B, H)[0], c.view(-1, B, H)[0]) for h, c in hidden_state]
         out, _ = self._core(lstm_input.view(T + 1, B, -1), h0)

@@ -25,6 +25,18 @@ def pin_tree(x):
     return x
 
 
+def entity_total_hint(batch) -> Optional[int]:
+    """Host-side packed entity count of an RL learner batch (sum of min(entity_num, N)), computed from the
+    host copy before the H2D transfer; the model uses it to pack entities without a device->host sync."""
+    if not isinstance(batch, dict) or not torch.is_tensor(batch.get('entity_num')) or \
+            not isinstance(batch.get('entity_info'), dict) or batch['entity_num'].is_cuda:
+        return None
+    ut = batch['entity_info'].get('unit_type')
+    if not torch.is_tensor(ut) or ut.dim() < 2:
+        return None
+    return int(batch['entity_num'].clamp(max=ut.shape[-1]).sum())
+
+
 def _to(x, device, stream):
     if torch.is_tensor(x):
         y = x.to(device, non_blocking=True)
@@ -61,11 +73,14 @@ class DevicePrefetcher:
             self._next = host
             return
         compute = torch.cuda.current_stream(self.device)
+        hint = entity_total_hint(host)
         with torch.cuda.stream(self.stream):
             # copies are issued on the side stream; record_stream ties lifetime to the compute stream
             self._next = _to_side(host, self.device, compute)
             self._event = torch.cuda.Event()
             self._event.record(self.stream)
+        if hint is not None:
+            self._next['entity_total'] = hint
 
     def __iter__(self):
         return self

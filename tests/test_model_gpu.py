@@ -96,3 +96,22 @@ def test_direct_master_grad_matches_bucket_path():
     assert (direct - ref).abs().max().item() <= 2e-2 * scale
     for a, p in zip(fp32_direct, tr.master.fp32_params):
         assert (a - p.grad.float()).abs().max().item() <= 2e-2 * max(1.0, p.grad.abs().max().item())
+
+
+def test_entity_total_hint_packing_matches_nonzero():
+    """The prefetcher's host-side packed-entity count (nonzero_static, no device sync) gives the same
+    learner forward as the synchronising nonzero path."""
+    from applestar_amd.runtime.prefetch import DevicePrefetcher, entity_total_hint, pin_tree
+    torch.manual_seed(0)
+    m = Model(CFG, use_value_network=True).cuda().eval()
+    host = pin_tree(rl_batch(2, 3, max_entities=48, seed=5))
+    hint = entity_total_hint(host)
+    assert hint is not None and hint > 0
+    staged = next(DevicePrefetcher(iter([host]), torch.device('cuda')))
+    assert staged['entity_total'] == hint
+    with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
+        a = m.rl_learner_forward(**staged)
+        staged.pop('entity_total')
+        b = m.rl_learner_forward(**staged)
+    for k in a['target_logit']:
+        assert torch.equal(a['target_logit'][k], b['target_logit'][k]), k
