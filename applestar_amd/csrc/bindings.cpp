@@ -704,6 +704,27 @@ void multi_copy(const std::vector<at::Tensor>& dsts, const std::vector<at::Tenso
   flush();
 }
 
+// ---------------------------------------------------------------- narrow 1x1 conv on NHWC pixels
+at::Tensor pointwise_conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act) {
+  check_cuda(x, "x");
+  check_cuda(w, "w");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2, "pointwise: x [P, cin] bf16");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.dim() == 2 && w.size(1) == x.size(1), "pointwise: w fp32 [cout, cin]");
+  const int64_t P = x.size(0), cin = x.size(1), cout = w.size(0);
+  TORCH_CHECK(as::pointwise_supported(static_cast<int>(cin), static_cast<int>(cout)), "pointwise: channels");
+  const float* bp = nullptr;
+  if (bias.has_value()) {
+    check_cuda(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == cout, "pointwise: bias fp32 [cout]");
+    bp = bias->data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(x.device().index());
+  auto y = at::empty({P, cout}, x.options());
+  as::pointwise_conv(x.data_ptr(), w.data_ptr<float>(), bp, y.data_ptr(), P, static_cast<int>(cin),
+                     static_cast<int>(cout), static_cast<int>(act), stream());
+  return y;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "applestar_amd HIP kernels for gfx950 (MI355X)";
   m.def("layer_norm_fwd", &layer_norm_fwd);
@@ -732,6 +753,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("table_grad", &table_grad);
   m.def("conv3x3_fwd", &conv3x3_fwd);
   m.def("wgrad", &wgrad);
+  m.def("pointwise_conv", &pointwise_conv);
+  m.def("pointwise_supported", [](int64_t ci, int64_t co) { return as::pointwise_supported(static_cast<int>(ci), static_cast<int>(co)); });
   m.def("lstm_split_error", &lstm_split_error);
   m.def("multi_copy", &multi_copy);
   m.def("act_grad_nhwc", &act_grad_nhwc);

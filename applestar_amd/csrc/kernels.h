@@ -180,6 +180,12 @@ struct CopyArgs {                     // passed by value (< 2 KB of kernel argum
 };
 void multi_copy(const CopyArgs& a, hipStream_t s);
 
+// ---- pointwise.hip -----------------------------------------------------------------------------
+// y [P, cout] bf16 = act(x [P, cin] bf16 . w^T (fp32 [cout, cin]) + bias); cin, cout in {8, 16, 32}
+bool pointwise_supported(int cin, int cout);
+void pointwise_conv(const void* x, const float* w, const float* bias, void* y, long P, int cin, int cout, int act,
+                    hipStream_t s);
+
 // ---- act_grad.hip ------------------------------------------------------------------------------
 // dpre NHWC bf16 [B, HW, C] = dout * (out > 0) (relu) or dout; dout fp32/bf16, NHWC or (dout_nchw) NCHW
 // contiguous; out NHWC bf16.  C % 8 == 0 (NHWC) / C % 32 == 0 (NCHW).

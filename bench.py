@@ -27,8 +27,8 @@ BASELINE_PER_GPU = 256.0  # samples/s/GPU, 32xA100 learner, docs/guidance_to_sma
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=10)
-    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--steps', type=int, default=30)
+    ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--batch', type=int, default=6, help='trajectories per GPU')
     ap.add_argument('--unroll', type=int, default=64)
     ap.add_argument('--max-entities', type=int, default=512)

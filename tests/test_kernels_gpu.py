@@ -491,3 +491,28 @@ def test_multi_copy_converts_and_handles_many_tensors():
     C.multi_copy(dsts, srcs)
     for d, s in zip(dsts, srcs):
         assert torch.equal(d, s.to(d.dtype)), (d.shape, d.dtype, s.dtype)
+
+
+@pytest.mark.parametrize('cin,cout,act', [(16, 16, 'relu'), (32, 8, None), (8, 32, 'relu')])
+def test_pointwise_conv1x1_matches_fp32(cin, cout, act):
+    from applestar_amd import ops
+    torch.manual_seed(17)
+    x = torch.randn(3, cin, 37, 41, device=DEV).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    w = (torch.randn(cout, cin, 1, 1, device=DEV) / cin ** 0.5).requires_grad_()
+    b = (0.1 * torch.randn(cout, device=DEV)).requires_grad_()
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y = ops.conv2d(x, w, b, 1, 0, act=act)
+    assert y.dtype == torch.bfloat16
+    xs, ws, bs = (t.detach().float().requires_grad_() for t in (x, w, b))
+    yr = torch.nn.functional.conv2d(xs, ws, bs)
+    if act == 'relu':
+        yr = torch.relu(yr)
+    assert _err(y, yr) < 3e-2 * max(1.0, yr.abs().max().item())
+    g = torch.randn_like(yr)
+    y.float().backward(g)
+    dpre = g * (y.detach().float() > 0) if act == 'relu' else g    # the bf16 forward's mask
+    dx = torch.nn.grad.conv2d_input(xs.shape, ws, dpre)
+    dw = torch.nn.grad.conv2d_weight(xs, ws.shape, dpre)
+    for a, r in ((x.grad, dx), (w.grad, dw), (b.grad, dpre.sum((0, 2, 3)))):
+        assert _err(a, r) < 3e-2 * max(1.0, r.abs().max().item())
