@@ -228,7 +228,9 @@ int wgrad_splits(long R, int N, int K) {
   const int BN = N > 64 ? 128 : 64, BK = K > 64 ? 128 : 64;
   const long tiles = static_cast<long>((N + BN - 1) / BN) * ((K + BK - 1) / BK);
   long S = (1024 + tiles - 1) / tiles;                 // ~1024 workgroups: 2 resident per CU, 2 rounds
-  const long max_s = (R + 255) / 256;                  // at least 256 rows (4 stages) per slice
+  // at least 256 rows (4 stages) per slice; short reductions (R < 2048, e.g. the 390-row policy / value
+  // MLP gradients) take one slice so no partial-sum pass is launched at all
+  const long max_s = R < 2048 ? 1 : (R + 255) / 256;
   if (S > max_s) S = max_s;
   const long max_part = (8L << 20) / (static_cast<long>(N) * K);  // partials <= 32 MB (their sum is a pass)
   if (S > max_part) S = max_part;
