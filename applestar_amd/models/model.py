@@ -162,6 +162,15 @@ class Model(nn.Module):
         self.race_mask: Optional[torch.Tensor] = None  # set by the agent in play mode (action_type_head.py:52)
 
     # ------------------------------------------------------------------ helpers
+    def _graphed(self, name: str, module: nn.Module):
+        """HIP-graph-captured (forward + backward) view of a static-shape section (runtime/graphs.py);
+        kept outside the module tree so state_dict keys are unchanged."""
+        from ..runtime.graphs import GraphedSection
+        cache = self.__dict__.setdefault('_graph_sections', {})
+        if name not in cache:
+            cache[name] = GraphedSection(module)
+        return cache[name]
+
     def _encode(self, spatial_info, entity_info, scalar_info, entity_num, entity_total=None):
         return self.encoder(spatial_info, entity_info, scalar_info, entity_num, entity_total)
 
@@ -226,7 +235,7 @@ class Model(nn.Module):
         if self._use_value_feature:
             vf = _side_stream_join(vf)
             critic_input = torch.cat([critic_input.to(vf.dtype), vf, baseline_feature.to(vf.dtype)], 1)
-        values = {k: v(critic_input).view(T + 1, B) for k, v in self.value_networks.items()}
+        values = {k: self._graphed(k, v)(critic_input).view(T + 1, B) for k, v in self.value_networks.items()}
         for k in list(logits):
             logits[k] = logits[k].view(T, B, *logits[k].shape[1:])
         su = logits['selected_units']
