@@ -43,12 +43,14 @@ struct WgCfg {
   static constexpr int BN = BN_, BK = BK_, BR = 64, NT = 256;
   static constexpr int TN = BN / 2, TK = BK / 2;       // 2 x 2 waves
   static constexpr int FN = TN / 16, FK = TK / 16;
-  static constexpr int PA = BN + 16, PB = BK + 16;    // LDS row pitch, bf16 elements (72 / 40 dwords)
+  // LDS row pitch, bf16 elements: 72 / 56 / 40 / 24 dwords for 128 / 96 / 64 / 32 columns - each makes the
+  // 8 consecutive rows of a transposed read start on 8 distinct 8-bank groups
+  static constexpr int PA = BN + 16, PB = BK + 16;
   static constexpr int CHA = BN / 8, CHB = BK / 8;    // 16-B chunks per row
   static constexpr int A_IT = BR * CHA / NT, B_IT = BR * CHB / NT;
   static constexpr int STAGE = BR * (PA + PB);        // bf16 elements
   static constexpr int SMEM = 2 * STAGE * 2;
-  static_assert(A_IT * NT == BR * CHA && B_IT * NT == BR * CHB, "tile / thread mismatch");
+  static_assert(A_IT * NT == BR * CHA && B_IT * NT == BR * CHB && NT % CHA == 0, "tile / thread mismatch");
 };
 
 __device__ __forceinline__ bf8v tr_frag(const bf16_t* tile, int pitch, int col0, int lane) {
@@ -94,17 +96,28 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const bf16_t* __restrict__ d
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(x), 0,
                                                                       static_cast<int>(xbytes), 0x00020000);
 
-  // per-thread fixed chunk columns
-  const int a_ch = tid % C::CHA, b_ch = tid % C::CHB;
-  const int a_col = n0 + 8 * a_ch, b_col = k0 + 8 * b_ch;
-  const bool a_col_ok = a_col < N, b_col_ok = b_col < K;
-  int b_c = b_col, b_shift = 0, b_dy = 0, b_dx = 0;
-  if (CONV) {
-    const int tap = b_col / Cin;
-    b_c = b_col - tap * Cin;
-    b_dy = tap / 3 - 1;
-    b_dx = tap % 3 - 1;
-    b_shift = b_dy * W + b_dx;
+  // per-thread chunk columns, fixed across row stages.  A: CHA divides NT, so every A chunk of a thread has
+  // the same column.  B: CHB = 12 (BK = 96) does not divide NT, so each of a thread's B chunks has its own
+  // column (and, for the conv form, its own tap).
+  const int a_ch = tid % C::CHA;
+  const int a_col = n0 + 8 * a_ch;
+  const bool a_col_ok = a_col < N;
+  int b_ch[C::B_IT], b_rr[C::B_IT], b_col[C::B_IT], b_c[C::B_IT], b_shift[C::B_IT], b_dy[C::B_IT], b_dx[C::B_IT];
+#pragma unroll
+  for (int i = 0; i < C::B_IT; ++i) {
+    const int idx = tid + i * C::NT;
+    b_ch[i] = idx % C::CHB;
+    b_rr[i] = idx / C::CHB;
+    b_col[i] = k0 + 8 * b_ch[i];
+    b_c[i] = b_col[i];
+    b_shift[i] = b_dy[i] = b_dx[i] = 0;
+    if (CONV) {
+      const int tap = b_col[i] / Cin;
+      b_c[i] = b_col[i] - tap * Cin;
+      b_dy[i] = tap / 3 - 1;
+      b_dx[i] = tap % 3 - 1;
+      b_shift[i] = b_dy[i] * W + b_dx[i];
+    }
   }
 
   uint4 ra[C::A_IT], rb[C::B_IT];
@@ -118,15 +131,16 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const bf16_t* __restrict__ d
     }
 #pragma unroll
     for (int i = 0; i < C::B_IT; ++i) {
-      const long r = rs + (tid + i * C::NT) / C::CHB;
+      const long r = rs + b_rr[i];
+      const bool ok = b_col[i] < K && r < r_end;
       int off = kOOB;
       if (CONV) {
         const int rem = static_cast<int>(r % HW);
-        const int yy = rem / W + b_dy, xx = rem % W + b_dx;
-        if (b_col_ok && r < r_end && yy >= 0 && yy < H && xx >= 0 && xx < W)
-          off = static_cast<int>(((r + b_shift) * Cin + b_c) * 2);
-      } else if (b_col_ok && r < r_end) {
-        off = static_cast<int>((r * K + b_col) * 2);
+        const int yy = rem / W + b_dy[i], xx = rem % W + b_dx[i];
+        if (ok && yy >= 0 && yy < H && xx >= 0 && xx < W)
+          off = static_cast<int>(((r + b_shift[i]) * Cin + b_c[i]) * 2);
+      } else if (ok) {
+        off = static_cast<int>((r * K + b_col[i]) * 2);
       }
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
       rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
@@ -140,7 +154,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const bf16_t* __restrict__ d
       *reinterpret_cast<uint4*>(A + ((tid + i * C::NT) / C::CHA) * C::PA + 8 * a_ch) = ra[i];
 #pragma unroll
     for (int i = 0; i < C::B_IT; ++i)
-      *reinterpret_cast<uint4*>(Bt + ((tid + i * C::NT) / C::CHB) * C::PB + 8 * b_ch) = rb[i];
+      *reinterpret_cast<uint4*>(Bt + b_rr[i] * C::PB + 8 * b_ch[i]) = rb[i];
   };
 
   f4 acc[C::FN][C::FK];
@@ -224,8 +238,23 @@ void launch(const bf16_t* dy, const bf16_t* x, float* dw, float* db, long R, int
 
 }  // namespace
 
+namespace {
+// tile choice: BN covers N with the least padding (32 / 64 / 128), BK in {64, 96, 128} minimises the padded
+// K (3x3 convs: K = 9 Cin = 288 / 576 / 1152 -> BK 96 has no padding where 128 wastes up to 25 %)
+int pick_bn(int N) { return N <= 32 ? 32 : (N <= 64 ? 64 : 128); }
+int pick_bk(int K) {
+  int best = 128;
+  long best_pad = (K + 127) / 128 * 128L;
+  for (int bk : {96, 64}) {
+    const long pad = (K + bk - 1) / bk * static_cast<long>(bk);
+    if (pad < best_pad) { best = bk; best_pad = pad; }
+  }
+  return best;
+}
+}  // namespace
+
 int wgrad_splits(long R, int N, int K) {
-  const int BN = N > 64 ? 128 : 64, BK = K > 64 ? 128 : 64;
+  const int BN = pick_bn(N), BK = pick_bk(K);
   const long tiles = static_cast<long>((N + BN - 1) / BN) * ((K + BK - 1) / BK);
   long S = (1024 + tiles - 1) / tiles;                 // ~1024 workgroups: 2 resident per CU, 2 rounds
   // at least 256 rows (4 stages) per slice; short reductions (R < 2048, e.g. the 390-row policy / value
@@ -246,14 +275,16 @@ void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long R
   const bf16_t* d = static_cast<const bf16_t*>(dy);
   const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bool conv = Cin > 0;
-  const bool bn128 = N > 64, bk128 = K > 64;
+  const int bn = pick_bn(N), bk = pick_bk(K);
 #define AS_WG(BNv, BKv)                                                                              \
-  (conv ? launch<BNv, BKv, true>(d, xp, dw_part, db_part, R, N, K, H, W, Cin, S, rps, st)            \
-        : launch<BNv, BKv, false>(d, xp, dw_part, db_part, R, N, K, H, W, Cin, S, rps, st))
-  if (bn128 && bk128) AS_WG(128, 128);
-  else if (bn128) AS_WG(128, 64);
-  else if (bk128) AS_WG(64, 128);
-  else AS_WG(64, 64);
+  if (bn == BNv && bk == BKv) {                                                                      \
+    if (conv) launch<BNv, BKv, true>(d, xp, dw_part, db_part, R, N, K, H, W, Cin, S, rps, st);       \
+    else launch<BNv, BKv, false>(d, xp, dw_part, db_part, R, N, K, H, W, Cin, S, rps, st);           \
+    return;                                                                                          \
+  }
+  AS_WG(128, 128) AS_WG(128, 96) AS_WG(128, 64)
+  AS_WG(64, 128) AS_WG(64, 96) AS_WG(64, 64)
+  AS_WG(32, 128) AS_WG(32, 96) AS_WG(32, 64)
 #undef AS_WG
 }
 

@@ -374,7 +374,7 @@ def test_conv1x1_gemm_path_matches_conv():
 
 
 @pytest.mark.parametrize('R,N,K', [(5000, 128, 128), (100003, 256, 768), (70001, 32, 56), (4097, 1024, 256),
-                                   (300, 64, 64), (145920, 128, 128)])
+                                   (300, 64, 64), (145920, 128, 128), (20000, 24, 288), (3000, 40, 200)])
 def test_wgrad_dense_matches_fp32(R, N, K):
     from applestar_amd.ops import native
     C = native.ensure_loaded()
