@@ -51,9 +51,12 @@ def init(backend: Optional[str] = None, init_method: Optional[str] = None, rank:
     os.environ.setdefault('TORCH_NCCL_ASYNC_ERROR_HANDLING', '1')
     use_gpu = torch.cuda.is_available()
     if backend is None:
-        backend = 'nccl' if use_gpu else 'gloo'
+        # APPLESTAR_DIST_BACKEND=gloo rehearses the multi-rank GPU path with several ranks sharing one GPU
+        # (RCCL needs one GPU per rank)
+        backend = os.environ.get('APPLESTAR_DIST_BACKEND') or ('nccl' if use_gpu else 'gloo')
     if use_gpu:
-        torch.cuda.set_device(get_local_rank() if 'LOCAL_RANK' in os.environ else rank % torch.cuda.device_count())
+        local = get_local_rank() if 'LOCAL_RANK' in os.environ else rank
+        torch.cuda.set_device(local % torch.cuda.device_count())
     kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
     if init_method is not None:
         kw.update(init_method=init_method, rank=rank, world_size=world_size)
