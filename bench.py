@@ -22,6 +22,7 @@ import time
 import torch
 
 BASELINE_PER_GPU = 256.0  # samples/s/GPU, 32xA100 learner, docs/guidance_to_small_scale_training.md:280-284
+SL_BASELINE_PER_GPU = 384.0  # samples/s/GPU, 56xA100 SL learner, docs/guidance_to_small_scale_training.md:178-184
 
 
 def main():
@@ -35,6 +36,8 @@ def main():
     ap.add_argument('--n-batches', type=int, default=2, help='distinct synthetic batches cycled')
     ap.add_argument('--no-native', action='store_true', help='disable HIP kernels (torch-only baseline)')
     ap.add_argument('--profile-steps', type=int, default=0)
+    ap.add_argument('--mode', choices=['rl', 'sl'], default='rl',
+                    help='rl: the headline RL learner step; sl: supervised learner step (reference 384 samples/s/GPU)')
     ap.add_argument('--conv-benchmark', type=int, default=-1,
                     help='1/0: force MIOpen find-mode autotuning of convolutions on/off (-1: trainer default)')
     args = ap.parse_args()
@@ -56,12 +59,18 @@ def main():
         torch.backends.cudnn.benchmark = bool(args.conv_benchmark)
     torch.manual_seed(1234 + rank)
 
-    trainer = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}},
-                        device=device)
-    host_batches = [pin_tree(rl_batch(args.batch, args.unroll, max_entities=args.max_entities,
-                                      seed=1000 * rank + i)) if gpu else
-                    rl_batch(args.batch, args.unroll, max_entities=args.max_entities, seed=1000 * rank + i)
-                    for i in range(args.n_batches)]
+    if args.mode == 'rl':
+        trainer = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}},
+                            device=device)
+        make = lambda i: rl_batch(args.batch, args.unroll, max_entities=args.max_entities, seed=1000 * rank + i)  # noqa
+    else:
+        from applestar_amd.sl.trainer import SLTrainer
+        from applestar_amd.rl.synthetic import sl_batch
+        trainer = SLTrainer({'learner': {'ignore_steps': 0, 'data': {'batch_size': args.batch,
+                                                                       'trajectory_length': args.unroll}}},
+                            device=device)
+        make = lambda i: sl_batch(args.batch, args.unroll, max_entities=args.max_entities, seed=1000 * rank + i)  # noqa
+    host_batches = [pin_tree(make(i)) if gpu else make(i) for i in range(args.n_batches)]
 
     def source():
         i = 0
@@ -99,7 +108,8 @@ def main():
     value = samples / elapsed
     if rank == 0:
         out = {
-            'metric': 'learner samples/sec (AlphaStar policy)',
+            'metric': 'learner samples/sec (AlphaStar policy)' if args.mode == 'rl' else
+                      'SL learner samples/sec (AlphaStar policy)',
             'value': round(value, 2),
             'unit': 'samples/s',
             'n_gpus': world,
@@ -108,16 +118,18 @@ def main():
             'ms_per_step': round(ms, 3),
             'higher_is_better': True,
             'scaling': 'weak',
-            'vs_baseline': round(value / (BASELINE_PER_GPU * world), 3),
+            'vs_baseline': round(value / ((BASELINE_PER_GPU if args.mode == 'rl' else SL_BASELINE_PER_GPU) * world), 3),
             'dtype': 'bf16',
             'data': 'synthetic (reference fake-data distribution, entity_num~U[1,512)), random-init weights',
             'config': {
-                'model': 'AlphaStar policy + value encoder + winloss baseline (DI-star rl_model arch)',
+                'model': 'AlphaStar policy + value encoder + winloss baseline (DI-star rl_model arch)' if args.mode == 'rl'
+                         else 'AlphaStar policy (DI-star sl_model arch)',
                 'global_batch': args.batch * world,
                 'seq_len': args.unroll,
                 'parallelism': f'dp{world}',
                 'samples_per_step': args.batch * args.unroll * world,
-                'baseline_note': 'vs_baseline = per-GPU samples/s / 256 (reference RL learner, A100)',
+                'baseline_note': 'vs_baseline = per-GPU samples/s / 256 (reference RL learner, A100)' if args.mode == 'rl'
+                                 else 'vs_baseline = per-GPU samples/s / 384 (reference SL learner, A100)',
                 'native_kernels': (not args.no_native) and gpu,
                 'final_loss': loss,
                 'host_ms_per_step': round(1000.0 * host / max(args.steps, 1), 3),
