@@ -52,7 +52,9 @@ struct ConvCfg {
   static_assert((BM * CH) % NT == 0, "A tile chunks");
 };
 
-template <int BN, int BK>
+// SPLIT_TAP: Cin < BK (Cin = 16), so one K-step spans several taps: every 16-B chunk finds its own tap,
+// and K = 9 Cin is not a multiple of BK (the tail reads zeros).  Cout need not be a multiple of BN.
+template <int BN, int BK, bool SPLIT_TAP>
 __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
                                                       const float* __restrict__ bias, const bf16_t* __restrict__ res,
                                                       bf16_t* __restrict__ out, int B, int H, int W, int Cin, int Cout,
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__
   const int HW = H * W;
   const long M = static_cast<long>(B) * HW;
   const int K = 9 * Cin;
-  const int ntn = Cout / BN;
+  const int ntn = (Cout + BN - 1) / BN;
   // XCD-aware bijective remap of the flat workgroup id (8 XCDs, round-robin dispatch)
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
@@ -111,23 +113,36 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__
   for (int i = 0; i < C::B_IT; ++i) {
     const int idx = tid + i * C::NT;
     const int n = idx / C::CH, ch = idx % C::CH;
-    b_off[i] = idx < BN * C::CH ? ((n0 + n) * K + 8 * ch) * 2 : kOOB;
+    b_off[i] = (idx < BN * C::CH && n0 + n < Cout) ? ((n0 + n) * K + 8 * ch) * 2 : kOOB;
   }
 
   uint4 ra[C::A_IT], rb[C::B_IT];
   auto load_regs = [&](int kt) {
     const int k0 = kt * BK;
-    const int tap = k0 / Cin, c0 = k0 - tap * Cin;
-    const int shift = (tap / 3 - 1) * W + (tap % 3 - 1);
+    if (SPLIT_TAP) {
 #pragma unroll
-    for (int i = 0; i < C::A_IT; ++i) {
-      const int off = ((a_ok[i] >> tap) & 1) ? ((a_pix[i] + shift) * Cin + c0 + 8 * a_ch[i]) * 2 : kOOB;
-      const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-      ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      for (int i = 0; i < C::A_IT; ++i) {
+        const int k = k0 + 8 * a_ch[i];
+        const int tap = k / Cin, c = k - tap * Cin;
+        const int shift = (tap / 3 - 1) * W + (tap % 3 - 1);
+        const int off = (k < K && ((a_ok[i] >> tap) & 1)) ? ((a_pix[i] + shift) * Cin + c) * 2 : kOOB;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+        ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
+    } else {
+      const int tap = k0 / Cin, c0 = k0 - tap * Cin;
+      const int shift = (tap / 3 - 1) * W + (tap % 3 - 1);
+#pragma unroll
+      for (int i = 0; i < C::A_IT; ++i) {
+        const int off = ((a_ok[i] >> tap) & 1) ? ((a_pix[i] + shift) * Cin + c0 + 8 * a_ch[i]) * 2 : kOOB;
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+        ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < C::B_IT; ++i) {
-      const int off = b_off[i] == kOOB ? kOOB : b_off[i] + k0 * 2;
+      const int kc = k0 + 8 * ((tid + i * C::NT) % C::CH);
+      const int off = (b_off[i] == kOOB || (SPLIT_TAP && kc >= K)) ? kOOB : b_off[i] + k0 * 2;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0);
       rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
     }
@@ -154,7 +169,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  const int KT = K / BK;
+  const int KT = (K + BK - 1) / BK;
   load_regs(0);
   store_lds(0);
   __syncthreads();
@@ -196,8 +211,8 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__
   for (int idx = tid; idx < C::BM * CPR; idx += C::NT) {
     const int rr = idx / CPR, c8 = idx % CPR;
     const long m = m0 + rr;
-    if (m >= M) continue;
     const int n = n0 + 8 * c8;
+    if (m >= M || n >= Cout) continue;
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = cs[rr * C::CPAD + 8 * c8 + e] + (bias ? bias[n + e] : 0.f);
@@ -224,21 +239,23 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__
   }
 }
 
-template <int BN, int BK>
+template <int BN, int BK, bool SPLIT_TAP = false>
 void launch(const bf16_t* x, const bf16_t* w, const float* bias, const bf16_t* res, bf16_t* out, int B, int H, int W,
             int Cin, int Cout, int act, hipStream_t s) {
   const long M = static_cast<long>(B) * H * W;
   const long mt = (M + 127) / 128;
-  const long nwg = mt * (Cout / BN);
+  const long nwg = mt * ((Cout + BN - 1) / BN);
   if (nwg == 0) return;
-  hipLaunchKernelGGL((conv3x3_kernel<BN, BK>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias, res, out,
-                     B, H, W, Cin, Cout, act);
+  hipLaunchKernelGGL((conv3x3_kernel<BN, BK, SPLIT_TAP>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w,
+                     bias, res, out, B, H, W, Cin, Cout, act);
 }
 
 }  // namespace
 
 bool conv3x3_supported(int Cin, int Cout) {  // (the host wrapper also bounds B*H*W*Cin*2 < 2^31)
-  return Cin % 32 == 0 && Cin >= 32 && (Cout % 128 == 0 || Cout == 64 || Cout == 32);
+  const bool cin_ok = Cin == 16 || (Cin % 32 == 0 && Cin >= 32);
+  const bool cout_ok = Cout == 16 || Cout == 32 || Cout == 64 || Cout % 128 == 0;
+  return cin_ok && cout_ok;
 }
 
 void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* res, void* out, int B, int H, int W,
@@ -248,6 +265,12 @@ void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* re
   const bf16_t* rp = static_cast<const bf16_t*>(res);
   bf16_t* op = static_cast<bf16_t*>(out);
   const bool k64 = Cin % 64 == 0;
+  if (Cin == 16) {                     // K-steps straddle taps
+    if (Cout % 128 == 0) launch<128, 32, true>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    else if (Cout == 64) launch<64, 32, true>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    else launch<32, 32, true>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    return;
+  }
   if (Cout % 128 == 0) {
     if (k64) launch<128, 64>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
     else launch<128, 32>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
