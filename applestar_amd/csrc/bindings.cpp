@@ -65,17 +65,15 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
   c10::hip::HIPGuard g(xin.device().index());
   auto dx = at::empty(xin.sizes(), xin.options().dtype(dx_dtype == 1 ? at::kBFloat16 : at::kFloat));
   const int nblk = as::layer_norm_bwd_blocks(rows);
-  auto part = at::empty({2, nblk, C}, xin.options().dtype(at::kFloat));
-  auto dw = at::empty({C}, xin.options().dtype(at::kFloat));
-  auto db = at::empty({C}, xin.options().dtype(at::kFloat));
+  auto part = at::empty({nblk, 2 * C}, xin.options().dtype(at::kFloat));
+  auto dwb = at::empty({2 * C}, xin.options().dtype(at::kFloat));
   const at::Tensor& yy = act != 0 ? y : dy;
   as::layer_norm_bwd(dy.data_ptr(), dt(dy), xin.data_ptr(), dt(xin), yy.data_ptr(), dt(yy), w.data_ptr<float>(),
                      mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dt(dx),
-                     part[0].data_ptr<float>(), part[1].data_ptr<float>(), rows, static_cast<int>(C),
+                     part.data_ptr<float>(), part.data_ptr<float>() + C, rows, static_cast<int>(C),
                      static_cast<int>(act), nblk, stream());
-  as::column_reduce(part[0].data_ptr<float>(), dw.data_ptr<float>(), nblk, static_cast<int>(C), stream());
-  as::column_reduce(part[1].data_ptr<float>(), db.data_ptr<float>(), nblk, static_cast<int>(C), stream());
-  return {dx, dw, db};
+  as::column_reduce(part.data_ptr<float>(), dwb.data_ptr<float>(), nblk, static_cast<int>(2 * C), stream());
+  return {dx, dwb.narrow(0, 0, C), dwb.narrow(0, C, C)};
 }
 
 // ---------------------------------------------------------------- reverse scan
@@ -621,20 +619,20 @@ std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t
   const int S = R > 0 ? as::wgrad_splits(R, static_cast<int>(N), static_cast<int>(K)) : 1;
   auto opts = dy.options().dtype(at::kFloat);
   if (R == 0) return {at::zeros({N, K}, opts), want_bias ? at::zeros({N}, opts) : at::Tensor()};
-  auto dwp = at::empty({S, N, K}, opts);
-  at::Tensor dbp = want_bias ? at::empty({S, N}, opts) : at::Tensor();
-  as::wgrad(dy.data_ptr(), x.data_ptr(), dwp.data_ptr<float>(), want_bias ? dbp.data_ptr<float>() : nullptr, R,
-            static_cast<int>(N), static_cast<int>(K), static_cast<int>(H), static_cast<int>(W), static_cast<int>(cin),
-            S, stream());
-  if (S == 1) return {dwp.view({N, K}), want_bias ? dbp.view({N}) : at::Tensor()};
-  auto dw = at::empty({N, K}, opts);
-  as::column_reduce(dwp.data_ptr<float>(), dw.data_ptr<float>(), S, static_cast<int>(N * K), stream());
-  at::Tensor db;
-  if (want_bias) {
-    db = at::empty({N}, opts);
-    as::column_reduce(dbp.data_ptr<float>(), db.data_ptr<float>(), S, static_cast<int>(N), stream());
+  // one [S, N*K (+ N)] partial buffer: dW and db of a slice side by side, reduced by ONE column pass
+  const int64_t NK = N * K, stride = NK + (want_bias ? N : 0);
+  auto part = at::empty({S, stride}, opts);
+  as::wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), want_bias ? part.data_ptr<float>() + NK : nullptr,
+            stride, R, static_cast<int>(N), static_cast<int>(K), static_cast<int>(H), static_cast<int>(W),
+            static_cast<int>(cin), S, stream());
+  at::Tensor flat;
+  if (S == 1) {
+    flat = part.view({stride});
+  } else {
+    flat = at::empty({stride}, opts);
+    as::column_reduce(part.data_ptr<float>(), flat.data_ptr<float>(), S, static_cast<int>(stride), stream());
   }
-  return {dw, db};
+  return {flat.narrow(0, 0, NK).view({N, K}), want_bias ? flat.narrow(0, NK, N) : at::Tensor()};
 }
 
 // ---------------------------------------------------------------- conv epilogue backward -> NHWC bf16

@@ -191,6 +191,7 @@ void pointwise_conv(const void* x, const float* w, const float* bias, void* y, l
 // contiguous; out NHWC bf16.  C % 8 == 0 (NHWC) / C % 32 == 0 (NCHW).
 void act_grad_nhwc(const void* dout, int dt, bool dout_nchw, const void* out, void* dpre, int B, int C, int HW, int relu,
                    hipStream_t s);
-void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long R, int N, int K, int H, int W, int Cin,
-           int S, hipStream_t st);
+// partial slice s of dW at dw_part + s * part_stride, of db at db_part + s * part_stride
+void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
+           int H, int W, int Cin, int S, hipStream_t st);
 }  // namespace as

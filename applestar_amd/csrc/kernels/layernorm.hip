@@ -169,8 +169,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
     const float sw = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
     const float sb = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-    dw_part[static_cast<long>(blockIdx.x) * C + c] = sw;
-    db_part[static_cast<long>(blockIdx.x) * C + c] = sb;
+    // [nblk][2C] layout (db_part = dw_part + C): both affine gradients reduce in ONE column pass
+    dw_part[static_cast<long>(blockIdx.x) * 2 * C + c] = sw;
+    db_part[static_cast<long>(blockIdx.x) * 2 * C + c] = sb;
   }
 }
 

@@ -69,7 +69,7 @@ __device__ __forceinline__ bf8v tr_frag(const bf16_t* tile, int pitch, int col0,
 template <int BN, int BK, bool CONV>
 __global__ __launch_bounds__(256) void wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
                                                     float* __restrict__ dw_part, float* __restrict__ db_part,
-                                                    long R, int N, int K, int H, int W, int Cin, long rows_per_split,
+                                                    long part_stride, long R, int N, int K, int H, int W, int Cin, long rows_per_split,
                                                     int tiles_n, int tiles_k) {
   using C = WgCfg<BN, BK>;
   __shared__ __attribute__((aligned(16))) bf16_t smem[C::SMEM / 2];
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const bf16_t* __restrict__ d
   }
 
   // epilogue: fp32 partial tile; lane (g, i) of fragment (a, b) holds C[n = 16a + 4g + e][k = 16b + i]
-  float* outp = dw_part + static_cast<long>(s) * N * K;
+  float* outp = dw_part + static_cast<long>(s) * part_stride;
   const int lr = lane & 15, lg = lane >> 4;
 #pragma unroll
   for (int i = 0; i < C::FN; ++i)
@@ -222,18 +222,18 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const bf16_t* __restrict__ d
       v += __shfl_xor(v, 16, kWave);
       v += __shfl_xor(v, 32, kWave);
       const int n = n0 + wn * C::TN + 16 * i + lr;
-      if (lg == 0 && n < N) db_part[static_cast<long>(s) * N + n] = v;
+      if (lg == 0 && n < N) db_part[static_cast<long>(s) * part_stride + n] = v;
     }
   }
 }
 
 template <int BN, int BK, bool CONV>
-void launch(const bf16_t* dy, const bf16_t* x, float* dw, float* db, long R, int N, int K, int H, int W, int Cin,
+void launch(const bf16_t* dy, const bf16_t* x, float* dw, float* db, long ps, long R, int N, int K, int H, int W, int Cin,
             int S, long rps, hipStream_t st) {
   const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
   const long nwg = static_cast<long>(tn) * tk * S;
   hipLaunchKernelGGL((wgrad_kernel<BN, BK, CONV>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x, dw, db,
-                     R, N, K, H, W, Cin, rps, tn, tk);
+                     ps, R, N, K, H, W, Cin, rps, tn, tk);
 }
 
 }  // namespace
@@ -268,8 +268,8 @@ int wgrad_splits(long R, int N, int K) {
   return static_cast<int>(S);
 }
 
-void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long R, int N, int K, int H, int W, int Cin,
-           int S, hipStream_t st) {
+void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
+           int H, int W, int Cin, int S, hipStream_t st) {
   long rps = (R + S - 1) / S;
   rps = (rps + 63) / 64 * 64;
   const bf16_t* d = static_cast<const bf16_t*>(dy);
@@ -278,8 +278,8 @@ void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long R
   const int bn = pick_bn(N), bk = pick_bk(K);
 #define AS_WG(BNv, BKv)                                                                              \
   if (bn == BNv && bk == BKv) {                                                                      \
-    if (conv) launch<BNv, BKv, true>(d, xp, dw_part, db_part, R, N, K, H, W, Cin, S, rps, st);       \
-    else launch<BNv, BKv, false>(d, xp, dw_part, db_part, R, N, K, H, W, Cin, S, rps, st);           \
+    if (conv) launch<BNv, BKv, true>(d, xp, dw_part, db_part, part_stride, R, N, K, H, W, Cin, S, rps, st);       \
+    else launch<BNv, BKv, false>(d, xp, dw_part, db_part, part_stride, R, N, K, H, W, Cin, S, rps, st);           \
     return;                                                                                          \
   }
   AS_WG(128, 128) AS_WG(128, 96) AS_WG(128, 64)
