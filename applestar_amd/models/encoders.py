@@ -270,6 +270,9 @@ class SpatialEncoder(nn.Module):
         return x, map_skip
 
 
+SCALAR_SIDE_STREAM = True
+
+
 class Encoder(nn.Module):
     def __init__(self, reduce_type: str = 'selected_units_num'):
         super().__init__()
@@ -279,7 +282,11 @@ class Encoder(nn.Module):
         self.scatter_project = FCBlock(256, 32, act=True)
 
     def forward(self, spatial_info, entity_info, scalar_info, entity_num, entity_total: Optional[int] = None):
-        embedded_scalar, scalar_context, baseline_feature = self.scalar_encoder(scalar_info)
+        # the scalar encoder (incl. the 20-token build-order transformer: many small kernels) is independent
+        # of the entity / spatial path: side stream 1 on the GPU (its backward follows it there)
+        from .model import _side_stream_call, _side_stream_join
+        scalar_h = _side_stream_call(self.scalar_encoder, scalar_info, slot=1) if SCALAR_SIDE_STREAM else \
+            (self.scalar_encoder(scalar_info), None)
         entity_embeddings, embedded_entity, entity_mask = self.entity_encoder(entity_info, entity_num, entity_total)
         proj = self.scatter_project(entity_embeddings) * entity_mask.unsqueeze(2).to(entity_embeddings.dtype)
         n = ops._native(proj) if proj.is_cuda else None
@@ -289,6 +296,7 @@ class Encoder(nn.Module):
         else:
             scatter_map = ops.scatter_connection(proj, entity_info['x'], entity_info['y'], SPATIAL_Y, SPATIAL_X)
             embedded_spatial, map_skip = self.spatial_encoder(spatial_info, scatter_map)
+        embedded_scalar, scalar_context, baseline_feature = _side_stream_join(scalar_h)
         lstm_input = torch.cat([embedded_scalar, embedded_entity.to(embedded_scalar.dtype),
                                 embedded_spatial.to(embedded_scalar.dtype)], dim=-1)
         return lstm_input, scalar_context, baseline_feature, entity_embeddings, map_skip

@@ -42,19 +42,20 @@ DEFAULT_MODEL_CONFIG = AttrDict({
 })
 
 
-_SIDE_STREAMS: Dict[int, 'torch.cuda.Stream'] = {}
+_SIDE_STREAMS: Dict[tuple, 'torch.cuda.Stream'] = {}
 SIDE_STREAMS_ENABLED = True
 
 
-def _side_stream_call(fn, inputs):
-    """Run ``fn(inputs)`` on a per-device side stream (GPU) and return a handle for :func:`_side_stream_join`."""
+def _side_stream_call(fn, inputs, slot: int = 0):
+    """Run ``fn(inputs)`` on side stream ``slot`` of the device (GPU) and return a handle for
+    :func:`_side_stream_join`."""
     dev = next((v.device for v in inputs.values() if torch.is_tensor(v)), None) if isinstance(inputs, dict) else None
     if dev is None or dev.type != 'cuda' or not SIDE_STREAMS_ENABLED:
         return fn(inputs), None
     main = torch.cuda.current_stream(dev)
-    side = _SIDE_STREAMS.get(dev.index)
+    side = _SIDE_STREAMS.get((dev.index, slot))
     if side is None:
-        side = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(dev)
+        side = _SIDE_STREAMS[(dev.index, slot)] = torch.cuda.Stream(dev)
     side.wait_stream(main)                 # inputs were produced on the main stream
     with torch.cuda.stream(side):
         out = fn(inputs)
@@ -64,9 +65,11 @@ def _side_stream_call(fn, inputs):
 def _side_stream_join(handle):
     out, side = handle
     if side is not None:
-        main = torch.cuda.current_stream(out.device)
+        tensors = [t for t in (out if isinstance(out, (tuple, list)) else (out,)) if torch.is_tensor(t)]
+        main = torch.cuda.current_stream(tensors[0].device)
         main.wait_stream(side)
-        out.record_stream(main)            # allocated on the side stream, consumed on main
+        for t in tensors:
+            t.record_stream(main)          # allocated on the side stream, consumed on main
     return out
 
 

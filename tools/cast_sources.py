@@ -36,10 +36,10 @@ class Rec(TorchDispatchMode):
                         where = f"{fr.filename.split('applestar_amd/')[-1]}:{fr.lineno} {fr.name}"
                         break
             numel = out.numel() if torch.is_tensor(out) else 0
-            if where == '<backward>' and torch.is_tensor(out):
+            if torch.is_tensor(out) and (where == '<backward>' or name == '_to_copy'):
                 ins = [f"{tuple(a.shape)}:{str(a.dtype)[6:]}" + ('' if a.is_contiguous() else '(nc)')
                        for a in args if torch.is_tensor(a)]
-                where = f"<backward> out {tuple(out.shape)}:{str(out.dtype)[6:]} in {' '.join(ins)}"
+                where = f"{where} out {tuple(out.shape)}:{str(out.dtype)[6:]} in {' '.join(ins)}"
             a = self.agg[(name, where)]
             a[0] += 1
             a[1] += numel
