@@ -44,6 +44,7 @@ DEFAULT_MODEL_CONFIG = AttrDict({
 
 _SIDE_STREAMS: Dict[tuple, 'torch.cuda.Stream'] = {}
 SIDE_STREAMS_ENABLED = True
+CRITIC_SIDE_STREAM = False   # tools/ab_bench.py --variant critic_side: no gain (+1.9 ms, noisy)
 
 
 def _side_stream_call(fn, inputs, slot: int = 0):
@@ -57,6 +58,9 @@ def _side_stream_call(fn, inputs, slot: int = 0):
     if side is None:
         side = _SIDE_STREAMS[(dev.index, slot)] = torch.cuda.Stream(dev)
     side.wait_stream(main)                 # inputs were produced on the main stream
+    for t in inputs.values():              # ... and are read on the side stream
+        if torch.is_tensor(t) and t.is_cuda:
+            t.record_stream(side)
     with torch.cuda.stream(side):
         out = fn(inputs)
     return out, side
@@ -228,17 +232,27 @@ class Model(nn.Module):
         out, _ = self._core(lstm_input.view(T + 1, B, -1), h0)
         lstm_output = out.reshape((T + 1) * B, -1)
         n = T * B
-        _, _, logits = self.policy.train_forward(
-            lstm_output[:n], entity_embeddings[:n], [m[:n] for m in map_skip], scalar_context[:n],
-            entity_num[:n], flat_action, flat_su_num, self.temperature)
         critic_input = lstm_output
         if self.only_update_baseline:
             critic_input = critic_input.detach()
             baseline_feature = baseline_feature.detach()
-        if self._use_value_feature:
-            vf = _side_stream_join(vf)
-            critic_input = torch.cat([critic_input.to(vf.dtype), vf, baseline_feature.to(vf.dtype)], 1)
-        values = {k: self._graphed(k, v)(critic_input).view(T + 1, B) for k, v in self.value_networks.items()}
+
+        def critic(inp):
+            ci = inp['lstm']
+            if self._use_value_feature:
+                v = inp['vf']
+                ci = torch.cat([ci.to(v.dtype), v, inp['bf'].to(v.dtype)], 1)
+            return [self._graphed(k, m)(ci).view(T + 1, B) for k, m in self.value_networks.items()]
+
+        # the critic MLPs depend only on the LSTM output (+ value features): they run on the value encoder's
+        # side stream (which already holds vf) while the policy heads run on the main stream
+        vf_out = vf[0] if isinstance(vf, tuple) else vf
+        critic_in = {'lstm': critic_input, 'vf': vf_out, 'bf': baseline_feature}
+        values_h = _side_stream_call(critic, critic_in) if CRITIC_SIDE_STREAM else (critic(critic_in), None)
+        _, _, logits = self.policy.train_forward(
+            lstm_output[:n], entity_embeddings[:n], [m[:n] for m in map_skip], scalar_context[:n],
+            entity_num[:n], flat_action, flat_su_num, self.temperature)
+        values = dict(zip(self.value_networks.keys(), _side_stream_join(values_h)))
         for k in list(logits):
             logits[k] = logits[k].view(T, B, *logits[k].shape[1:])
         su = logits['selected_units']
