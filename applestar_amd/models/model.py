@@ -47,6 +47,18 @@ SIDE_STREAMS_ENABLED = True
 CRITIC_SIDE_STREAM = False   # tools/ab_bench.py --variant critic_side: no gain (+1.9 ms, noisy)
 
 
+_DEVICE_TABLES: Dict[tuple, torch.Tensor] = {}
+
+
+def _device_table(name: str, t: torch.Tensor, device) -> torch.Tensor:
+    """Constant lookup table cached per device (a per-call .to(device) is a pageable H2D copy: a host
+    sync, and not capturable in a HIP graph)."""
+    key = (name, str(device))
+    if key not in _DEVICE_TABLES:
+        _DEVICE_TABLES[key] = t.to(device)
+    return _DEVICE_TABLES[key]
+
+
 def _side_stream_call(fn, inputs, slot: int = 0):
     """Run ``fn(inputs)`` on side stream ``slot`` of the device (GPU) and return a handle for
     :func:`_side_stream_join`."""
@@ -113,7 +125,7 @@ class Policy(nn.Module):
             lstm_output, scalar_context, temperature, race_mask=race_mask, u=noise.get('action_type'))
         logit['delay'], action['delay'], emb = self.delay_head(emb, temperature, u=noise.get('delay'))
         logit['queued'], action['queued'], emb = self.queued_head(emb, temperature, u=noise.get('queued'))
-        su_mask = gd.SELECTED_UNITS_MASK.to(action['action_type'].device)[action['action_type']]
+        su_mask = _device_table('su_mask', gd.SELECTED_UNITS_MASK, action['action_type'].device)[action['action_type']]
         logit['selected_units'], action['selected_units'], emb, su_num, extra = \
             self.selected_units_head.forward_sample(emb, entity_embeddings, entity_num, su_mask, temperature,
                                                     u=noise.get('selected_units'))

@@ -74,3 +74,88 @@ class GraphedSection:
             self._graphs[sig] = g
         self.replays += 1
         return g(*args)
+
+
+# ---------------------------------------------------------------------------------------------------
+def _tree_clone(x):
+    if torch.is_tensor(x):
+        return x.clone()
+    if isinstance(x, dict):
+        return {k: _tree_clone(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_tree_clone(v) for v in x)
+    return x
+
+
+def _tree_copy_(dst, src):
+    if torch.is_tensor(dst):
+        if dst.shape != src.shape:
+            raise ValueError(f'graphed input shape {tuple(src.shape)} != captured {tuple(dst.shape)}')
+        dst.copy_(src, non_blocking=True)
+    elif isinstance(dst, dict):
+        for k in dst:
+            _tree_copy_(dst[k], src[k])
+    elif isinstance(dst, (list, tuple)):
+        for a, b in zip(dst, src):
+            _tree_copy_(a, b)
+
+
+def _signature(x):
+    if torch.is_tensor(x):
+        return (tuple(x.shape), x.dtype)
+    if isinstance(x, dict):
+        return tuple((k, _signature(v)) for k, v in sorted(x.items()))
+    if isinstance(x, (list, tuple)):
+        return tuple(_signature(v) for v in x)
+    return x
+
+
+class GraphedPolicy:
+    """Actor inference (``compute_logp_action`` / ``compute_teacher_logit``) replayed from HIP graphs,
+    one graph per input signature (batch size x padded entity count): the B = 1 agent step is ~500
+    small kernels whose launch chain, not the GPU, sets the latency.
+
+    Inputs must keep a fixed padded shape per signature (the inference server pads entities to
+    ``MAX_ENTITY_NUM``); the entity encoder switches to its shape-static dense path while capturing.
+    Outputs are the graph's static tensors: consume (or clone) them before the next call."""
+
+    def __init__(self, model: nn.Module, method: str = 'compute_logp_action', max_graphs: int = 8):
+        self.model = model
+        self.method = method
+        self.max_graphs = max_graphs
+        self._graphs: Dict[Tuple, tuple] = {}
+        self.captures = 0
+
+    def _run(self, kwargs):
+        fn = getattr(self.model, self.method)
+        with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16, cache_enabled=False):
+            return fn(**kwargs)
+
+    def __call__(self, **kwargs):
+        from ..models import encoders, model as model_mod
+        sig = _signature(kwargs)
+        entry = self._graphs.get(sig)
+        if entry is None:
+            if len(self._graphs) >= self.max_graphs:
+                self._graphs.pop(next(iter(self._graphs)))
+            static_in = _tree_clone(kwargs)
+            flags = (encoders.STATIC_SHAPES, encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED)
+            encoders.STATIC_SHAPES, encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED = True, False, False
+            try:
+                side = torch.cuda.Stream()
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    for _ in range(2):                      # warm-up (allocator, lazy tables) off-capture
+                        self._run(static_in)
+                torch.cuda.current_stream().wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    static_out = self._run(static_in)
+            finally:
+                encoders.STATIC_SHAPES, encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED = flags
+            entry = self._graphs[sig] = (g, static_in, static_out)
+            self.captures += 1
+        g, static_in, static_out = entry
+        _tree_copy_(static_in, kwargs)
+        g.replay()
+        return static_out

@@ -21,6 +21,7 @@ def main():
     ap.add_argument('--batches', default='1,16,64')
     ap.add_argument('--iters', type=int, default=30)
     ap.add_argument('--entities', type=int, default=300)
+    ap.add_argument('--graphs', type=int, default=1, help='also time the HIP-graph replay (runtime.graphs.GraphedPolicy)')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     m = Model({'agent': {'extra_units': True}}).to(dev).eval().to(memory_format=torch.channels_last)
@@ -32,17 +33,28 @@ def main():
         obs = to_device(obs, dev)
         act, su_num = random_actions(B, en, generator=g)
         res = {}
-        for name in ('policy', 'teacher'):
+        from applestar_amd.runtime.graphs import GraphedPolicy
+        gp = GraphedPolicy(m, 'compute_logp_action')
+        gt = GraphedPolicy(m, 'compute_teacher_logit')
+        act_d = {k: v.to(dev) for k, v in act.items()}
+        modes = [('policy', False), ('teacher', False)] + ([('policy_graph', True), ('teacher_graph', True)]
+                                                           if args.graphs else [])
+        for name, graphed in modes:
             times = []
             for i in range(args.iters + 3):
                 torch.cuda.synchronize()
                 t = time.perf_counter()
-                with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
-                    if name == 'policy':
-                        out = m.compute_logp_action(**obs)
+                if graphed:
+                    if name.startswith('policy'):
+                        out = gp(**obs)
                     else:
-                        out = m.compute_teacher_logit(**obs, selected_units_num=su_num.to(dev),
-                                                      action_info={k: v.to(dev) for k, v in act.items()})
+                        out = gt(**obs, selected_units_num=su_num.to(dev), action_info=act_d)
+                else:
+                    with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
+                        if name == 'policy':
+                            out = m.compute_logp_action(**obs)
+                        else:
+                            out = m.compute_teacher_logit(**obs, selected_units_num=su_num.to(dev), action_info=act_d)
                 torch.cuda.synchronize()
                 if i >= 3:
                     times.append((time.perf_counter() - t) * 1000)

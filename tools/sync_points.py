@@ -15,8 +15,28 @@ from applestar_amd.rl.synthetic import rl_batch, to_device  # noqa: E402
 
 def main():
     dev = torch.device('cuda', 0)
-    tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}, device=dev)
-    b = to_device(rl_batch(6, 64, seed=0), dev)
+    infer = '--infer' in sys.argv
+    if infer:
+        from applestar_amd.models.model import Model
+        from applestar_amd.lib.features import random_obs
+        m = Model({'agent': {'extra_units': True}}).to(dev).eval().to(memory_format=torch.channels_last)
+        g = torch.Generator().manual_seed(0)
+        obs = to_device(random_obs(1, entity_num=torch.tensor([300]), generator=g), dev)
+        hs = [(torch.zeros(1, 384, device=dev), torch.zeros(1, 384, device=dev)) for _ in range(3)]
+
+        def run():
+            with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
+                m.compute_logp_action(**obs, hidden_state=hs)
+
+        class _T:
+            def step(self, _):
+                run()
+        tr = _T()
+        b = {}
+    else:
+        tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}},
+                       device=dev)
+        b = to_device(rl_batch(6, 64, seed=0), dev)
     tr.step(dict(b))
     torch.cuda.synchronize()
     hits = collections.Counter()
