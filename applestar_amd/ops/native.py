@@ -22,7 +22,7 @@ def ensure_loaded():
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
-                'gather_rows', 'conv2d', 'linear'}
+                'gather_rows', 'conv2d', 'linear', 'resblock'}
 
 
 def has(name: str) -> bool:
@@ -443,6 +443,62 @@ class _Conv3x3(torch.autograd.Function):
         dw, db = _C.wgrad(dpre.view(-1, cout), x, cin, has_b)       # dW in [Cout,3,3,Cin] (channels_last) order
         dw = dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype)
         return (dx, dw, db.to(ctx.b_dtype) if has_b else None, dpre if ctx.has_res else None, None)
+
+
+def _conv_w(w):
+    """[Cout,Cin,3,3] -> [Cout,3,3,Cin] (a view for channels_last weights)."""
+    wk = w.detach().permute(0, 2, 3, 1)
+    return wk if wk.is_contiguous() else wk.contiguous()
+
+
+def _conv_wt(w):
+    """flipped, transposed weight [Cin,3,3,Cout] for the input gradient."""
+    return w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()
+
+
+def _conv_dw(dpre, x, w, has_b):
+    cout, cin = w.shape[0], w.shape[1]
+    dw, db = _C.wgrad(dpre.view(-1, cout), x, cin, has_b)
+    return dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype), db
+
+
+class _ResBlock(torch.autograd.Function):
+    """relu(conv2(relu(conv1(x))) + x) (res_block.py:50-65) as ONE autograd node: the input gradient of
+    conv1 and the skip gradient are summed in the dX conv's epilogue (the residual input of the same MFMA
+    kernel) instead of a separate autograd add over the whole activation."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        y1 = _C.conv3x3_fwd(x, _conv_w(w1), b1.detach().float().contiguous(), None, 1)
+        out = _C.conv3x3_fwd(y1, _conv_w(w2), b2.detach().float().contiguous(), x, 1)
+        ctx.save_for_backward(x, w1, w2, y1, out)
+        ctx.b_dtypes = (b1.dtype, b2.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, w1, w2, y1, out = ctx.saved_tensors
+        dpre2 = _C.act_grad_nhwc(dout, out, True)
+        dy1 = _C.conv3x3_fwd(dpre2, _conv_wt(w2), None, None, 0)
+        dw2, db2 = _conv_dw(dpre2, y1, w2, True)
+        dpre1 = _C.act_grad_nhwc(dy1, y1, True)
+        dx = _C.conv3x3_fwd(dpre1, _conv_wt(w1), None, dpre2, 0)       # + skip gradient, fused
+        dw1, db1 = _conv_dw(dpre1, x, w1, True)
+        return dx, dw1, db1.to(ctx.b_dtypes[0]), dw2, db2.to(ctx.b_dtypes[1])
+
+
+def resblock(x, w1, b1, w2, b2):
+    """Native fused ResBlock; None when the shapes / dtypes are not covered (caller falls back)."""
+    C = x.shape[1]
+    lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
+    if x.dim() != 4 or not lowp or b1 is None or b2 is None or not _C.conv3x3_supported(C, C) or \
+            tuple(w1.shape) != (C, C, 3, 3) or tuple(w2.shape) != (C, C, 3, 3):
+        return None
+    xl = nhwc(x.to(torch.bfloat16))
+    w1l = w1 if w1.dtype == torch.bfloat16 else _CastWeight.apply(w1)
+    w2l = w2 if w2.dtype == torch.bfloat16 else _CastWeight.apply(w2)
+    with torch.autocast('cuda', enabled=False):
+        return from_nhwc(_ResBlock.apply(xl, w1l, b1, w2l, b2))
 
 
 class _CastWeight(torch.autograd.Function):

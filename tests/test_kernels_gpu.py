@@ -517,3 +517,27 @@ def test_pointwise_conv1x1_matches_fp32(cin, cout, act):
     dw = torch.nn.grad.conv2d_weight(xs, ws.shape, dpre)
     for a, r in ((x.grad, dx), (w.grad, dw), (b.grad, dpre.sum((0, 2, 3)))):
         assert _err(a, r) < 3e-2 * max(1.0, r.abs().max().item())
+
+
+@pytest.mark.parametrize('C,H,W', [(128, 19, 20), (32, 19, 20)])
+def test_fused_resblock_matches_unfused(C, H, W):
+    """The one-node ResBlock (skip gradient fused into the dX conv epilogue) vs the two-conv native path
+    (each conv checked against fp32 above): same bf16 forward, so same ReLU masks, and the gradients
+    agree up to bf16 rounding of the separate add."""
+    from applestar_amd import ops
+    from applestar_amd.models.blocks import ResBlock
+    torch.manual_seed(18)
+    blk = ResBlock(C).to(DEV).to(memory_format=torch.channels_last)
+    c1, c2 = blk.conv1[0], blk.conv2[0]
+    x = torch.randn(3, C, H, W, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_()
+    x2 = x.detach().clone().requires_grad_()
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y = blk(x)
+        yu = ops.conv2d(ops.conv2d(x2, c1.weight, c1.bias, 1, 1, act='relu'), c2.weight, c2.bias, 1, 1,
+                        act='relu', residual=x2)
+    assert torch.equal(y, yu)
+    g = torch.randn_like(y.float())
+    gx, gw1, gb2 = torch.autograd.grad(y.float(), [x, c1.weight, c2.bias], g)
+    ux, uw1, ub2 = torch.autograd.grad(yu.float(), [x2, c1.weight, c2.bias], g)
+    for a, r in ((gx, ux), (gw1, uw1), (gb2, ub2)):
+        assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
