@@ -63,3 +63,16 @@ def test_stream_channel_put_server_and_dead_server_removal():
         putter.close()
     finally:
         srv.shutdown()
+
+
+def test_protocol_codec_and_import_helper():
+    import torch
+    from applestar_amd.comm import protocol
+    from applestar_amd.utils import import_helper
+    tree = {'a': torch.arange(10, dtype=torch.int16), 'b': [1.5, 'x', None, {'c': torch.ones(2, 3)}]}
+    out = protocol.decode(protocol.encode(tree, compress=True))
+    assert torch.equal(out['a'], tree['a']) and out['b'][:3] == [1.5, 'x', None]
+    assert torch.equal(out['b'][3]['c'], tree['b'][3]['c'])
+    assert import_helper.try_import_link() is not None
+    assert import_helper.try_import_mc() is None
+    import_helper.import_module(['applestar_amd.utils.config'])
