@@ -139,6 +139,9 @@ class GLU(nn.Module):
         return self.layer2(g * x)
 
 
+FUSED_GATED_RESBLOCK = True
+
+
 class GatedResBlock(nn.Module):
     """Location-head gated residual block (module_utils.py:204-231)::
 
@@ -155,6 +158,11 @@ class GatedResBlock(nn.Module):
         self.UpdateSP = nn.Parameter(torch.full((1,), 0.1))
 
     def forward(self, x):
+        n = ops._native(x)
+        if n is not None and n.has('gated_resblock') and FUSED_GATED_RESBLOCK:
+            out = n.gated_resblock(x, self.conv1[0], self.conv2[0], [m[0] for m in self.GateWeightG], self.UpdateSP)
+            if out is not None:
+                return out
         y = self.conv2(self.conv1(x))
         g = self.GateWeightG(x)
         return ops.gated_residual(y, g, self.UpdateSP, x)

@@ -22,7 +22,7 @@ def ensure_loaded():
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
-                'gather_rows', 'conv2d', 'linear', 'resblock'}
+                'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock'}
 
 
 def has(name: str) -> bool:
@@ -499,6 +499,81 @@ def resblock(x, w1, b1, w2, b2):
     w2l = w2 if w2.dtype == torch.bfloat16 else _CastWeight.apply(w2)
     with torch.autocast('cuda', enabled=False):
         return from_nhwc(_ResBlock.apply(xl, w1l, b1, w2l, b2))
+
+
+class _GatedResBlock(torch.autograd.Function):
+    """Location-head GatedResBlock (module_utils.py:204-231) as one autograd node on NHWC bf16:
+
+        y = conv2(relu(conv1(x)));  g = G4(relu(G3(relu(G2(relu(G1(x)))))))   (G* = 1x1 convs = GEMMs)
+        out = relu(tanh(y * sigmoid(g)) * sp + x)
+
+    x feeds three consumers (conv1, G1, the skip); their input gradients are accumulated inside
+    kernels that run anyway: the G1 dX GEMM adds the skip gradient (addmm), and the conv1 dX kernel adds
+    that sum in its epilogue - no separate whole-activation adds."""
+
+    @staticmethod
+    def forward(ctx, x, sp, w1, b1, w2, b2, *gate):
+        B, H, W, C = x.shape
+        y1 = _C.conv3x3_fwd(x, _conv_w(w1), b1.detach().float().contiguous(), None, 1)
+        y = _C.conv3x3_fwd(y1, _conv_w(w2), b2.detach().float().contiguous(), None, 0)
+        h = x.view(-1, C)
+        acts = [h]
+        for i in range(4):
+            gw, gb = gate[2 * i].detach().view(C, C), gate[2 * i + 1].detach()
+            h = torch._addmm_activation(gb, h, gw.t(), use_gelu=False) if i < 3 else torch.addmm(gb, h, gw.t())
+            acts.append(h)
+        out = _C.gated_residual_fwd(y, h.view(B, H, W, C), sp, x)
+        ctx.save_for_backward(x, sp, w1, w2, y1, y, out, *acts[1:], *gate[0::2])
+        ctx.dtypes = (b1.dtype, b2.dtype, gate[1].dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, sp, w1, w2, y1, y, out, a1, a2, a3, g, gw1, gw2, gw3, gw4 = ctx.saved_tensors
+        B, H, W, C = x.shape
+        dy, dg, dx_res, dsp = _C.gated_residual_bwd(dout.contiguous().to(y.dtype), y, g.view(B, H, W, C), sp, out)
+        # gate chain (1x1 convs as GEMMs over the pixels)
+        grads_g = []
+        d = dg.view(-1, C)
+        acts_in = [x.view(-1, C), a1, a2, a3]
+        gws = [gw1, gw2, gw3, gw4]
+        for i in (3, 2, 1, 0):
+            dw_i, db_i = _C.wgrad(d, acts_in[i], 0, True)
+            grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
+            if i > 0:
+                dh = torch.mm(d, gws[i].view(C, C))
+                P = dh.shape[0]
+                d = _C.act_grad_nhwc(dh.view(1, 1, P, C), acts_in[i].view(1, 1, P, C), True).view(P, C)
+        dx_gate = torch.addmm(dx_res.view(-1, C), d, gw1.view(C, C))          # skip + G1 input gradients
+        # conv path
+        dy1 = _C.conv3x3_fwd(dy, _conv_wt(w2), None, None, 0)
+        dw2, db2 = _conv_dw(dy, y1, w2, True)
+        dpre1 = _C.act_grad_nhwc(dy1, y1, True)
+        dx = _C.conv3x3_fwd(dpre1, _conv_wt(w1), None, dx_gate.view(B, H, W, C).contiguous(), 0)
+        dw1, db1 = _conv_dw(dpre1, x, w1, True)
+        gate_grads = [None] * 8
+        for i, dw_i, db_i in grads_g:
+            gate_grads[2 * i], gate_grads[2 * i + 1] = dw_i, db_i
+        return (dx, dsp.to(sp.dtype), dw1, db1.to(ctx.dtypes[0]), dw2, db2.to(ctx.dtypes[1]), *gate_grads)
+
+
+def gated_resblock(x, conv1, conv2, gates, sp):
+    """Fused GatedResBlock (see _GatedResBlock); None when not covered (caller falls back)."""
+    C = x.shape[1]
+    lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
+    if x.dim() != 4 or not lowp or not _C.conv3x3_supported(C, C) or C % 8:
+        return None
+    ws = [conv1.weight, conv1.bias, conv2.weight, conv2.bias]
+    for gc in gates:
+        ws += [gc.weight, gc.bias]
+    if any(t is None for t in ws):
+        return None
+    # conv / GEMM weights and the GEMM biases in bf16 (the per-op path's casts); the conv biases stay as
+    # given: the conv epilogue adds them in fp32
+    ws = [t if (t.dtype == torch.bfloat16 or i in (1, 3)) else _CastWeight.apply(t) for i, t in enumerate(ws)]
+    xl = nhwc(x.to(torch.bfloat16))
+    with torch.autocast('cuda', enabled=False):
+        return from_nhwc(_GatedResBlock.apply(xl, sp.float(), *ws))
 
 
 class _CastWeight(torch.autograd.Function):

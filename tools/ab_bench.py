@@ -21,6 +21,9 @@ def set_variant(name, on):
         os.environ['APPLESTAR_GRAPHS'] = '1' if on else '0'
     elif name == 'wgrad_small':
         native._WGRAD_MIN_ROWS = 256 if on else 4096
+    elif name == 'gated_fused':
+        from applestar_amd.models import blocks
+        blocks.FUSED_GATED_RESBLOCK = on
     elif name == 'critic_side':
         from applestar_amd.models import model
         model.CRITIC_SIDE_STREAM = on
