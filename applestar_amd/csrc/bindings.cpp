@@ -595,8 +595,9 @@ at::Tensor conv3x3_fwd(const at::Tensor& x, const at::Tensor& wk, const c10::opt
 
 // ---------------------------------------------------------------- split-R MFMA weight gradient
 // dy [R, N] bf16; x [R, K] bf16 (cin == 0) or NHWC [B, H, W, cin] bf16 (3x3 conv, K = 9 cin).
-// Returns (dW fp32 [N, K], db fp32 [N] or undefined).
-std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t cin, bool want_bias) {
+// Returns (dW fp32 [N, K], db fp32 [N] or undefined); bf16_out: both in bf16, the cast fused into the
+// split reduction (the gradients of bf16 compute parameters under master weights).
+std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t cin, bool want_bias, bool bf16_out) {
   check_cuda(dy, "dy");
   check_cuda(x, "x");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "wgrad: bf16 dy / x");
@@ -618,7 +619,10 @@ std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t
   c10::hip::HIPGuard g(dy.device().index());
   const int S = R > 0 ? as::wgrad_splits(R, static_cast<int>(N), static_cast<int>(K)) : 1;
   auto opts = dy.options().dtype(at::kFloat);
-  if (R == 0) return {at::zeros({N, K}, opts), want_bias ? at::zeros({N}, opts) : at::Tensor()};
+  if (R == 0) {
+    auto zo = bf16_out ? dy.options() : opts;
+    return {at::zeros({N, K}, zo), want_bias ? at::zeros({N}, zo) : at::Tensor()};
+  }
   // one [S, N*K (+ N)] partial buffer: dW and db of a slice side by side, reduced by ONE column pass
   const int64_t NK = N * K, stride = NK + (want_bias ? N : 0);
   auto part = at::empty({S, stride}, opts);
@@ -626,12 +630,16 @@ std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t
             stride, R, static_cast<int>(N), static_cast<int>(K), static_cast<int>(H), static_cast<int>(W),
             static_cast<int>(cin), S, stream());
   at::Tensor flat;
-  if (S == 1) {
+  if (bf16_out && S <= 1024) {
+    flat = at::empty({stride}, dy.options());
+    as::column_reduce_bf16(part.data_ptr<float>(), flat.data_ptr(), S, static_cast<int>(stride), stream());
+  } else if (S == 1) {
     flat = part.view({stride});
   } else {
     flat = at::empty({stride}, opts);
     as::column_reduce(part.data_ptr<float>(), flat.data_ptr<float>(), S, static_cast<int>(stride), stream());
   }
+  if (bf16_out && flat.scalar_type() != at::kBFloat16) flat = flat.to(at::kBFloat16);
   return {flat.narrow(0, 0, NK).view({N, K}), want_bias ? flat.narrow(0, NK, N) : at::Tensor()};
 }
 
@@ -750,7 +758,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("segment_sum", &segment_sum);
   m.def("table_grad", &table_grad);
   m.def("conv3x3_fwd", &conv3x3_fwd);
-  m.def("wgrad", &wgrad);
+  m.def("wgrad", &wgrad, py::arg("dy"), py::arg("x"), py::arg("cin"), py::arg("want_bias"),
+        py::arg("bf16_out") = false);
   m.def("pointwise_conv", &pointwise_conv);
   m.def("pointwise_supported", [](int64_t ci, int64_t co) { return as::pointwise_supported(static_cast<int>(ci), static_cast<int>(co)); });
   m.def("lstm_split_error", &lstm_split_error);

@@ -34,6 +34,8 @@ void layer_norm_bwd(const void* dy, int dy_dt, const void* xin, int xin_dt, cons
                     const float* w, const float* mean, const float* rstd, void* dx, int dx_dt,
                     float* dw_part, float* db_part, long rows, int cols, int act, int nblk, hipStream_t s);
 void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s);
+// nrows <= 1024 only (one pass, no atomics): bf16 output
+void column_reduce_bf16(const float* part, void* out, int nrows, int cols, hipStream_t s);
 int layer_norm_bwd_blocks(long rows);
 
 // ---- scan.hip --------------------------------------------------------------------------------

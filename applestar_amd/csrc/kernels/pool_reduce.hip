@@ -184,7 +184,10 @@ __global__ __launch_bounds__(256) void table_grad_kernel(const T* __restrict__ s
   }
 }
 
-__global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+// OutT = bf16_t fuses the cast of the reduced weight gradient to the bf16 compute parameter dtype
+// (one launch instead of reduce + cast, wgrad callers under master weights)
+template <typename OutT>
+__global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __restrict__ part, OutT* __restrict__ out,
                                                              int nrows, int cols) {
   __shared__ float red[16][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
@@ -206,7 +209,8 @@ __global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __rest
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) s += red[k][threadIdx.x];
-    out[c] = s;
+    if constexpr (sizeof(OutT) == 2) out[c] = f2bf(s);
+    else out[c] = s;
   }
 }
 
@@ -283,12 +287,17 @@ void table_grad(const void* src, int dt, const int64_t* idx, float* out, long U,
 
 void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s) {
   if (nrows <= 1024) {
-    hipLaunchKernelGGL(column_reduce_kernel, dim3((cols + 63) / 64), dim3(1024), 0, s, part, out, nrows, cols);
+    hipLaunchKernelGGL(column_reduce_kernel<float>, dim3((cols + 63) / 64), dim3(1024), 0, s, part, out, nrows, cols);
     return;
   }
   (void)hipMemsetAsync(out, 0, static_cast<size_t>(cols) * sizeof(float), s);
   hipLaunchKernelGGL(column_reduce_atomic_kernel, dim3((cols + 63) / 64, (nrows + 255) / 256), dim3(256), 0, s, part,
                      out, nrows, cols);
+}
+
+void column_reduce_bf16(const float* part, void* out, int nrows, int cols, hipStream_t s) {
+  hipLaunchKernelGGL(column_reduce_kernel<bf16_t>, dim3((cols + 63) / 64), dim3(1024), 0, s, part,
+                     static_cast<bf16_t*>(out), nrows, cols);
 }
 
 }  // namespace as

@@ -440,7 +440,8 @@ class _Conv3x3(torch.autograd.Function):
         dx = _C.conv3x3_fwd(dpre, wt, None, None, 0)
         has_b = ctx.b_dtype is not None
         cout, cin = w.shape[0], w.shape[1]
-        dw, db = _C.wgrad(dpre.view(-1, cout), x, cin, has_b)       # dW in [Cout,3,3,Cin] (channels_last) order
+        bf = _bf16_grads(w.dtype, ctx.b_dtype)
+        dw, db = _C.wgrad(dpre.view(-1, cout), x, cin, has_b, bf)   # dW in [Cout,3,3,Cin] (channels_last) order
         dw = dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype)
         return (dx, dw, db.to(ctx.b_dtype) if has_b else None, dpre if ctx.has_res else None, None)
 
@@ -456,9 +457,11 @@ def _conv_wt(w):
     return w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()
 
 
-def _conv_dw(dpre, x, w, has_b):
+def _conv_dw(dpre, x, w, b_dtype):
+    """dW (in w's dtype) and db of a 3x3 conv; callers cast db to b_dtype (a no-op when both are bf16:
+    the cast is then fused into the split reduction)."""
     cout, cin = w.shape[0], w.shape[1]
-    dw, db = _C.wgrad(dpre.view(-1, cout), x, cin, has_b)
+    dw, db = _C.wgrad(dpre.view(-1, cout), x, cin, b_dtype is not None, _bf16_grads(w.dtype, b_dtype))
     return dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype), db
 
 
@@ -480,10 +483,10 @@ class _ResBlock(torch.autograd.Function):
         x, w1, w2, y1, out = ctx.saved_tensors
         dpre2 = _C.act_grad_nhwc(dout, out, True)
         dy1 = _C.conv3x3_fwd(dpre2, _conv_wt(w2), None, None, 0)
-        dw2, db2 = _conv_dw(dpre2, y1, w2, True)
+        dw2, db2 = _conv_dw(dpre2, y1, w2, ctx.b_dtypes[1])
         dpre1 = _C.act_grad_nhwc(dy1, y1, True)
         dx = _C.conv3x3_fwd(dpre1, _conv_wt(w1), None, dpre2, 0)       # + skip gradient, fused
-        dw1, db1 = _conv_dw(dpre1, x, w1, True)
+        dw1, db1 = _conv_dw(dpre1, x, w1, ctx.b_dtypes[0])
         return dx, dw1, db1.to(ctx.b_dtypes[0]), dw2, db2.to(ctx.b_dtypes[1])
 
 
@@ -538,7 +541,7 @@ class _GatedResBlock(torch.autograd.Function):
         acts_in = [x.view(-1, C), a1, a2, a3]
         gws = [gw1, gw2, gw3, gw4]
         for i in (3, 2, 1, 0):
-            dw_i, db_i = _C.wgrad(d, acts_in[i], 0, True)
+            dw_i, db_i = _C.wgrad(d, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
             grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
             if i > 0:
                 dh = torch.mm(d, gws[i].view(C, C))
@@ -547,10 +550,10 @@ class _GatedResBlock(torch.autograd.Function):
         dx_gate = torch.addmm(dx_res.view(-1, C), d, gw1.view(C, C))          # skip + G1 input gradients
         # conv path
         dy1 = _C.conv3x3_fwd(dy, _conv_wt(w2), None, None, 0)
-        dw2, db2 = _conv_dw(dy, y1, w2, True)
+        dw2, db2 = _conv_dw(dy, y1, w2, ctx.dtypes[1])
         dpre1 = _C.act_grad_nhwc(dy1, y1, True)
         dx = _C.conv3x3_fwd(dpre1, _conv_wt(w1), None, dx_gate.view(B, H, W, C).contiguous(), 0)
-        dw1, db1 = _conv_dw(dpre1, x, w1, True)
+        dw1, db1 = _conv_dw(dpre1, x, w1, ctx.dtypes[0])
         gate_grads = [None] * 8
         for i, dw_i, db_i in grads_g:
             gate_grads[2 * i], gate_grads[2 * i + 1] = dw_i, db_i
@@ -647,8 +650,17 @@ class _Pointwise(torch.autograd.Function):
         dx = _C.pointwise_conv(dpre, w.detach().float().t().contiguous(), None, 0) if ctx.needs_input_grad[0] \
             else None
         has_b = ctx.b_dtype is not None
-        dw, db = _C.wgrad(dpre, x2, 0, has_b)
+        dw, db = _C.wgrad(dpre, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
         return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None), None
+
+
+WGRAD_BF16_OUT = True    # tools/ab_bench.py --variant wgrad_bf16
+
+
+def _bf16_grads(w_dtype, b_dtype):
+    """Have wgrad emit dW/db in bf16 (cast fused into its split reduction) when the parameters are the
+    bf16 compute copies of master weights; fp32 parameters keep the fp32 reduction."""
+    return WGRAD_BF16_OUT and w_dtype == torch.bfloat16 and b_dtype in (None, torch.bfloat16)
 
 
 # ---------------------------------------------------------------------------- linear with MFMA split-R wgrad
@@ -682,7 +694,7 @@ class _Linear(torch.autograd.Function):
             dy = dy.to(torch.bfloat16).contiguous()
         dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
         has_b = ctx.b_dtype is not None
-        dw, db = _C.wgrad(dy, x2, 0, has_b)
+        dw, db = _C.wgrad(dy, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
         return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None), None
 
 

@@ -392,6 +392,10 @@ def test_wgrad_dense_matches_fp32(R, N, K):
     dw2, db2 = C.wgrad(dy, x, 0, False)
     assert db2 is None
     assert torch.equal(dw2, dw)            # deterministic (fixed split, ordered partial sum)
+    # bf16 output: the cast is fused into the split reduction -> exactly the rounded fp32 result
+    dw3, db3 = C.wgrad(dy, x, 0, True, True)
+    assert dw3.dtype == torch.bfloat16 and db3.dtype == torch.bfloat16
+    assert torch.equal(dw3, dw.to(torch.bfloat16)) and torch.equal(db3, db.to(torch.bfloat16))
 
 
 @pytest.mark.parametrize('B,H,W,cin,cout', [(5, 19, 20, 128, 128), (2, 76, 80, 32, 64), (3, 7, 5, 64, 32),
@@ -410,6 +414,8 @@ def test_wgrad_conv3x3_matches_fp32(B, H, W, cin, cout):
     scale = (B * H * W) ** 0.5
     assert _err(got, ref_w) < 1e-3 * scale, _err(got, ref_w)
     assert _err(db, dys.sum((0, 2, 3))) < 1e-3 * scale
+    dw3, db3 = C.wgrad(dy.view(-1, cout), x, cin, True, True)
+    assert torch.equal(dw3, dw.to(torch.bfloat16)) and torch.equal(db3, db.to(torch.bfloat16))
 
 
 def test_native_linear_autocast_grads_match_fp32():

@@ -21,6 +21,8 @@ def set_variant(name, on):
         os.environ['APPLESTAR_GRAPHS'] = '1' if on else '0'
     elif name == 'wgrad_small':
         native._WGRAD_MIN_ROWS = 256 if on else 4096
+    elif name == 'wgrad_bf16':
+        native.WGRAD_BF16_OUT = on
     elif name == 'gated_fused':
         from applestar_amd.models import blocks
         blocks.FUSED_GATED_RESBLOCK = on
