@@ -464,6 +464,19 @@ void segment_copy(const at::Tensor& arena, const at::Tensor& out, const at::Tens
 }
 
 
+// ---------------------------------------------------------------- flipped / transposed conv3x3 weight
+at::Tensor conv_wt(const at::Tensor& w) {
+  TORCH_CHECK(w.is_cuda(), "conv_wt: w must be a GPU tensor");   // any strides: read through them
+  TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.dim() == 4 && w.size(2) == 3 && w.size(3) == 3,
+              "conv_wt: bf16 [Cout,Cin,3,3] weight");
+  c10::hip::HIPGuard g(w.device().index());
+  const int cout = (int)w.size(0), cin = (int)w.size(1);
+  auto out = at::empty({cin, 3, 3, cout}, w.options().memory_format(at::MemoryFormat::Contiguous));
+  as::conv_wt(reinterpret_cast<const uint16_t*>(w.data_ptr()), reinterpret_cast<uint16_t*>(out.data_ptr()), cout, cin,
+              w.stride(0), w.stride(1), w.stride(2), w.stride(3), stream());
+  return out;
+}
+
 // ---------------------------------------------------------------- fused upsample x2 + conv3x3 -> 1 channel
 void check_upconv_x(const at::Tensor& x) {
   TORCH_CHECK(x.dim() == 4 && x.size(3) == as::upconv1_channels() && x.is_contiguous(),
@@ -751,6 +764,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("varlen_attn_bwd", &varlen_attn_bwd);
   m.def("su_sample", &su_sample);
   m.def("segment_copy", &segment_copy);
+  m.def("conv_wt", &conv_wt);
   m.def("upconv1_fwd", &upconv1_fwd);
   m.def("upconv1_bwd", &upconv1_bwd);
   m.def("maxpool2_fwd", &maxpool2_fwd);

@@ -133,6 +133,8 @@ namespace as {
 // ---- gather.hip --------------------------------------------------------------------------------
 // seg [nseg, 3] int64 = (src byte offset in arena, dst byte offset in out, byte count)
 void segment_copy(const uint8_t* arena, uint8_t* out, const int64_t* seg, long nseg, hipStream_t s);
+void conv_wt(const uint16_t* w, uint16_t* out, int cout, int cin, long s0, long s1, long s2, long s3,
+             hipStream_t s);
 }  // namespace as
 
 namespace as {

@@ -42,3 +42,30 @@ void segment_copy(const uint8_t* arena, uint8_t* out, const int64_t* seg, long n
 }
 
 }  // namespace as
+
+// Input-gradient weight of a 3x3 conv: out[ci][ky][kx][co] = w[co][ci][2-ky][2-kx] (bf16), read through
+// w's strides so contiguous and channels_last weights both work.  Replaces flip + permute + contiguous
+// (two launches) with one; each thread writes one output element, consecutive threads consecutive co.
+namespace as {
+namespace {
+__global__ __launch_bounds__(256) void conv_wt_kernel(const uint16_t* __restrict__ w, uint16_t* __restrict__ out,
+                                                      int cout, int cin, long s0, long s1, long s2, long s3) {
+  const long n = (long)cout * cin * 9;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int co = (int)(i % cout);
+    const long r = i / cout;              // (ci*3 + ky)*3 + kx
+    const int kx = (int)(r % 3), ky = (int)((r / 3) % 3), ci = (int)(r / 9);
+    out[i] = w[co * s0 + ci * s1 + (2 - ky) * s2 + (2 - kx) * s3];
+  }
+}
+}  // namespace
+
+void conv_wt(const uint16_t* w, uint16_t* out, int cout, int cin, long s0, long s1, long s2, long s3,
+             hipStream_t s) {
+  const long n = (long)cout * cin * 9;
+  if (n <= 0) return;
+  long grid = (n + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(conv_wt_kernel, dim3(grid), dim3(256), 0, s, w, out, cout, cin, s0, s1, s2, s3);
+}
+}  // namespace as

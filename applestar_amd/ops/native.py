@@ -436,8 +436,7 @@ class _Conv3x3(torch.autograd.Function):
     def backward(ctx, dout):
         x, w, out = ctx.saved_tensors
         dpre = _C.act_grad_nhwc(dout, out, ctx.act == 'relu')    # one pass: mask + cast + NHWC
-        wt = w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()   # [Cin,3,3,Cout]
-        dx = _C.conv3x3_fwd(dpre, wt, None, None, 0)
+        dx = _C.conv3x3_fwd(dpre, _conv_wt(w), None, None, 0)
         has_b = ctx.b_dtype is not None
         cout, cin = w.shape[0], w.shape[1]
         bf = _bf16_grads(w.dtype, ctx.b_dtype)
@@ -453,7 +452,9 @@ def _conv_w(w):
 
 
 def _conv_wt(w):
-    """flipped, transposed weight [Cin,3,3,Cout] for the input gradient."""
+    """flipped, transposed weight [Cin,3,3,Cout] for the input gradient (one launch; bf16 weights)."""
+    if w.dtype == torch.bfloat16:
+        return _C.conv_wt(w.detach())
     return w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()
 
 

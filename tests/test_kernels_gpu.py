@@ -576,3 +576,16 @@ def test_fused_gated_resblock_matches_unfused():
     gb = torch.autograd.grad(ref.float(), [x2] + params, gout)
     for a, b in zip(ga, gb):
         assert _err(a, b) < 5e-2 * max(1.0, b.float().abs().max().item())
+
+
+@pytest.mark.parametrize('cout,cin', [(128, 128), (64, 32), (1, 32), (33, 7)])
+@pytest.mark.parametrize('channels_last', [False, True])
+def test_conv_wt_matches_flip_permute(cout, cin, channels_last):
+    """One-launch flipped/transposed conv3x3 weight == w.flip(2,3).permute(1,2,3,0), bit-exact."""
+    w = torch.randn(cout, cin, 3, 3, device=DEV).to(torch.bfloat16)
+    if channels_last:
+        w = w.contiguous(memory_format=torch.channels_last)
+    got = N._C.conv_wt(w)
+    ref = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
+    assert got.shape == ref.shape and got.is_contiguous()
+    assert torch.equal(got, ref)
