@@ -615,6 +615,7 @@ std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t
   check_cuda(x, "x");
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "wgrad: bf16 dy / x");
   TORCH_CHECK(dy.dim() == 2, "wgrad: dy [R, N]");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous(), "wgrad: dy and x must be contiguous");
   const int64_t R = dy.size(0), N = dy.size(1);
   int64_t K, H = 1, W = 1;
   if (cin > 0) {
@@ -639,6 +640,12 @@ std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t
   // one [S, N*K (+ N)] partial buffer: dW and db of a slice side by side, reduced by ONE column pass
   const int64_t NK = N * K, stride = NK + (want_bias ? N : 0);
   auto part = at::empty({S, stride}, opts);
+  // debug: poison the partials so any slot the kernel leaves unwritten shows up as NaN on every run
+  static const bool nan_fill = [] {
+    const char* e = std::getenv("APPLESTAR_WGRAD_NANFILL");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (nan_fill) part.fill_(std::numeric_limits<float>::quiet_NaN());
   as::wgrad(dy.data_ptr(), x.data_ptr(), part.data_ptr<float>(), want_bias ? part.data_ptr<float>() + NK : nullptr,
             stride, R, static_cast<int>(N), static_cast<int>(K), static_cast<int>(H), static_cast<int>(W),
             static_cast<int>(cin), S, stream());

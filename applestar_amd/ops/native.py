@@ -452,10 +452,11 @@ def _conv_w(w):
 
 
 def _conv_wt(w):
-    """flipped, transposed weight [Cin,3,3,Cout] for the input gradient (one launch; bf16 weights)."""
-    if w.dtype == torch.bfloat16:
-        return _C.conv_wt(w.detach())
-    return w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()
+    """flipped, transposed weight [Cin,3,3,Cout] for the input gradient (one launch).  Only bf16 weights
+    reach the native conv (conv3x3_fwd rejects others), so there is no fp32 branch to keep untested."""
+    if w.dtype != torch.bfloat16:
+        raise TypeError(f'native conv3x3 backward needs bf16 weights, got {w.dtype}')
+    return _C.conv_wt(w.detach())
 
 
 def _conv_dw(dpre, x, w, b_dtype):

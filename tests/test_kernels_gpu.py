@@ -374,6 +374,35 @@ def test_conv1x1_gemm_path_matches_conv():
     assert _err(y, yr) < 1e-3
 
 
+def _wgrad_tiles(N, K):
+    """(BN, BK) chosen by wgrad.hip for an N x K gradient (pick_bn / pick_bk)."""
+    bn = 32 if N <= 32 else (64 if N <= 64 else 128)
+    bk, best = 128, (K + 127) // 128 * 128
+    for c in (96, 64):
+        if (K + c - 1) // c * c < best:
+            bk, best = c, (K + c - 1) // c * c
+    return bn, bk
+
+
+def _check_wgrad(got, ref64, ref_gpu, tol, rerun):
+    """Compare against a CPU float64 reference; on a miss, say where (n, k, tile), whether the GPU fp32
+    torch reference is itself off, and whether a second launch reproduces the result (round-1
+    intermittent: docs/OPEN_ISSUES.md)."""
+    d = (got.double().cpu() - ref64).abs()
+    err = float(torch.nan_to_num(d, nan=float('inf')).max())
+    if err < tol:
+        return
+    N, K = ref64.shape
+    n, k = divmod(int(torch.nan_to_num(d, nan=float('inf')).argmax()), K)
+    bn, bk = _wgrad_tiles(N, K)
+    again = rerun().double().cpu()
+    raise AssertionError(
+        f'wgrad max err {err:.4g} (tol {tol:.4g}) at n={n} k={k} tile=({n // bn},{k // bk}) '
+        f'got={float(got[n, k]):.6g} ref={float(ref64[n, k]):.6g}; elements over tol: {int((d >= tol).sum())}; '
+        f'gpu fp32 torch ref err vs f64: {float((ref_gpu.double().cpu() - ref64).abs().max()):.4g}; '
+        f'rerun identical: {torch.equal(again, got.double().cpu())}, rerun err {float((again - ref64).abs().max()):.4g}')
+
+
 @pytest.mark.parametrize('R,N,K', [(5000, 128, 128), (100003, 256, 768), (70001, 32, 56), (4097, 1024, 256),
                                    (300, 64, 64), (145920, 128, 128), (20000, 24, 288), (3000, 40, 200)])
 def test_wgrad_dense_matches_fp32(R, N, K):
@@ -383,12 +412,12 @@ def test_wgrad_dense_matches_fp32(R, N, K):
     dy = torch.randn(R, N, device=DEV).to(torch.bfloat16)
     x = torch.randn(R, K, device=DEV).to(torch.bfloat16)
     dw, db = C.wgrad(dy, x, 0, True)
-    ref_w = dy.float().t() @ x.float()
-    ref_b = dy.float().sum(0)
     assert dw.dtype == torch.float32 and dw.shape == (N, K) and db.shape == (N,)
+    dy64, x64 = dy.double().cpu(), x.double().cpu()
     scale = R ** 0.5
-    assert _err(dw, ref_w) < 1e-3 * scale, _err(dw, ref_w)
-    assert _err(db, ref_b) < 1e-3 * scale
+    _check_wgrad(dw, dy64.t() @ x64, dy.float().t() @ x.float(), 1e-3 * scale,
+                 lambda: C.wgrad(dy, x, 0, True)[0])
+    assert float((db.double().cpu() - dy64.sum(0)).abs().max()) < 1e-3 * scale
     dw2, db2 = C.wgrad(dy, x, 0, False)
     assert db2 is None
     assert torch.equal(dw2, dw)            # deterministic (fixed split, ordered partial sum)
@@ -407,13 +436,14 @@ def test_wgrad_conv3x3_matches_fp32(B, H, W, cin, cout):
     x = torch.randn(B, H, W, cin, device=DEV).to(torch.bfloat16)
     dy = torch.randn(B, H, W, cout, device=DEV).to(torch.bfloat16)
     dw, db = C.wgrad(dy.view(-1, cout), x, cin, True)
-    xs = x.float().permute(0, 3, 1, 2)
-    dys = dy.float().permute(0, 3, 1, 2)
-    ref_w = torch.nn.grad.conv2d_weight(xs, (cout, cin, 3, 3), dys, padding=1)      # [Cout,Cin,3,3]
-    got = dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2)
+    ref64 = torch.nn.grad.conv2d_weight(x.double().cpu().permute(0, 3, 1, 2), (cout, cin, 3, 3),
+                                        dy.double().cpu().permute(0, 3, 1, 2), padding=1)   # [Cout,Cin,3,3]
+    ref_gpu = torch.nn.grad.conv2d_weight(x.float().permute(0, 3, 1, 2), (cout, cin, 3, 3),
+                                          dy.float().permute(0, 3, 1, 2), padding=1)
+    as_k = lambda w: w.permute(0, 2, 3, 1).reshape(cout, 9 * cin)    # noqa: E731  [Cout, 3, 3, Cin] order
     scale = (B * H * W) ** 0.5
-    assert _err(got, ref_w) < 1e-3 * scale, _err(got, ref_w)
-    assert _err(db, dys.sum((0, 2, 3))) < 1e-3 * scale
+    _check_wgrad(dw, as_k(ref64), as_k(ref_gpu), 1e-3 * scale, lambda: C.wgrad(dy.view(-1, cout), x, cin, True)[0])
+    assert float((db.double().cpu() - dy.double().cpu().sum((0, 1, 2))).abs().max()) < 1e-3 * scale
     dw3, db3 = C.wgrad(dy.view(-1, cout), x, cin, True, True)
     assert torch.equal(dw3, dw.to(torch.bfloat16)) and torch.equal(db3, db.to(torch.bfloat16))
 

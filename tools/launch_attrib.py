@@ -40,7 +40,7 @@ def main():
         node = next((c for c in chain if 'autograd::engine' in c or 'Backward' in c), None)
         top = [c for c in chain if not c.startswith('aten::')][:2]
         cnt[(ev.name, node or 'forward', ' <- '.join(top)[:110])] += 1
-    os.makedirs(os.path.dirname(args.out), exist_ok=True)
+    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     with open(args.out, 'w') as f:
         for k, v in cnt.most_common(80):
             f.write(f'{v:5d}  {k[0]:18s} {k[1][:70]:70s} {k[2]}\n')
