@@ -74,13 +74,22 @@ class MasterWeights:
         self.reducer.zero_grad()
 
     def backward(self, loss: torch.Tensor):
-        """Backward into the master gradient.  Multi-rank: into the bf16 buckets (hooks overlap the
-        all-reduces with backward; :meth:`synchronize` then gathers them into the fp32 master grad).
-        Single rank: ``autograd.grad`` and ONE native multi-tensor copy that writes every bf16 gradient,
-        converted, straight into its fp32 master-grad slot (and the fp32 ones into their buckets) - no
-        per-parameter accumulate / copy launches, no bucket round trip."""
+        """Backward straight into the fp32 master gradient (``autograd.grad``: no per-parameter
+        AccumulateGrad ``add_`` into zeroed buckets, ~240 launches per RL step).
+
+        Single rank: ONE native multi-tensor copy writes every bf16 gradient, converted, into its fp32
+        master-grad slot (and the fp32 ones into their buckets).  Multi-rank: a tensor hook per
+        parameter collects the gradients of each bucket as backward produces them; when a bucket is
+        complete, one multi-tensor copy writes them (converted) into the bucket's slice of the fp32 master
+        gradient and ONE async RCCL all-reduce of that slice starts, overlapping the rest of backward
+        (:meth:`synchronize` waits for the tail).  The reduction is fp32 and lands in place: no bf16
+        bucket, no gather into the master afterwards."""
         self._direct = False
-        if self.reducer.world > 1 or not loss.is_cuda:
+        self._overlapped = False
+        if self.reducer.world > 1:
+            self._backward_overlapped(loss)
+            return
+        if not loss.is_cuda:
             self.reducer.backward(loss)
             return
         from ..ops import native
@@ -96,6 +105,69 @@ class MasterWeights:
             self.master.grad.zero_()
         C.multi_copy(dst, src)
         self._direct = True
+
+    # ---------------------------------------------------------------- multi-rank, overlapped
+    def _comm_buffers(self):
+        """Per bucket: the fp32 buffer that is all-reduced (a master-grad slice for bf16 buckets, the
+        bucket itself for fp32 ones) and, per parameter, its destination view in that buffer."""
+        plan = getattr(self, '_plan', None)
+        if plan is None:
+            mg = self._master_grad_views()
+            slot = {id(b): (off, k) for b, off, k in self._slices}
+            plan = {}
+            for b in self.reducer.buckets:
+                if id(b) in slot:
+                    off, k = slot[id(b)]
+                    buf = self.master.grad[off:off + k]
+                else:
+                    buf = b.flat
+                plan[id(b)] = (buf, {p: mg.get(p, p.grad) for p in b.params})
+            self._plan = plan
+            self._bucket_of = {p: b for b in self.reducer.buckets for p in b.params}
+            self._hook_handles = [p.register_hook(self._make_hook(p)) for p in self.reducer.params]
+        return plan
+
+    def _make_hook(self, p):
+        def hook(g):
+            if getattr(self, '_overlapped', False):
+                b = self._bucket_of[p]
+                st = self._pending[id(b)]
+                st.append((p, g))
+                if len(st) == len(b.params):
+                    self._flush(b)
+            return None
+        return hook
+
+    def _flush(self, b):
+        """Copy the collected gradients of bucket ``b`` into its fp32 buffer and start its all-reduce."""
+        import torch.distributed as dist
+        if id(b) in self._handles:
+            return
+        buf, dst_of = self._plan[id(b)]
+        got = self._pending[id(b)]
+        if len(got) < len(b.params):           # unused parameters contribute zeros
+            buf.zero_()
+        dst = [dst_of[p] for p, _ in got]
+        src = [g for _, g in got]
+        if dst:
+            if buf.is_cuda:
+                from ..ops import native
+                native.ensure_loaded().multi_copy(dst, src)
+            else:
+                torch._foreach_copy_(dst, src)
+        op = dist.ReduceOp.AVG if self.reducer.use_avg else dist.ReduceOp.SUM
+        self._handles[id(b)] = dist.all_reduce(buf, op=op, group=self.reducer.group, async_op=True)
+
+    def _backward_overlapped(self, loss: torch.Tensor):
+        self._comm_buffers()
+        self._pending = {id(b): [] for b in self.reducer.buckets}
+        self._handles = {}
+        self._overlapped = True
+        try:
+            torch.autograd.grad(loss, self.reducer.params, allow_unused=True)
+        finally:
+            self._overlapped = False
+        self._overlap_done = True
 
     def _master_grad_views(self):
         views = getattr(self, '_mg_views', None)
@@ -114,6 +186,17 @@ class MasterWeights:
     def synchronize(self):
         """All-reduce (if distributed) and gather the bf16 gradients into the flat fp32 master grad."""
         if getattr(self, '_direct', False):
+            return
+        if getattr(self, '_overlap_done', False):
+            self._overlap_done = False
+            for b in self.reducer.buckets:         # buckets whose parameters all went unused
+                self._flush(b)
+            world = self.reducer.world
+            for b in self.reducer.buckets:
+                self._handles[id(b)].wait()
+                if not self.reducer.use_avg:
+                    self._plan[id(b)][0].div_(world)
+            self._handles = {}
             return
         self.reducer.synchronize()
         g = self.master.grad

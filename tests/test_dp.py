@@ -124,6 +124,65 @@ def test_master_weights_world2():
     assert all(np.abs(s0[k] - ref[k]).max() > 0 for k in ('fc1.weight', 'fc2.weight', 'conv.weight', 'ln.weight'))
 
 
+def _overlap_worker(rank, world, port, q):
+    """MasterWeights.backward at world 2: per-bucket copy + all-reduce from tensor hooks, into the fp32
+    master gradient; compared with the average of both ranks' gradients computed locally."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from applestar_amd.parallel import dist as pdist
+    from applestar_amd.parallel.mixed import MasterWeights
+    pdist.init(backend='gloo')
+    torch.manual_seed(0)
+    m = _Tiny()
+    m.unused = torch.nn.Linear(4, 4)           # a bucket-mate that gets no gradient
+    m.conv.to(memory_format=torch.channels_last)
+    mw = MasterWeights(m, bucket_mb=0.0002)
+
+    def data(r):
+        g = torch.Generator().manual_seed(100 + r)
+        return torch.randn(5, 6, generator=g), torch.randn(2, 2, 5, 5, generator=g).contiguous(
+            memory_format=torch.channels_last)
+
+    def loss_of(r):
+        x, img = data(r)
+        with torch.autocast('cpu', dtype=torch.bfloat16):
+            return m(x, img)
+
+    # reference: both ranks' gradients on this process, averaged in fp32 (master order via the views)
+    ref = {}
+    for r in range(world):
+        gs = torch.autograd.grad(loss_of(r), mw.reducer.params, allow_unused=True)
+        for p, g in zip(mw.reducer.params, gs):
+            g = torch.zeros_like(p, dtype=torch.float32) if g is None else g.float()
+            ref[p] = ref.get(p, 0) + g / world
+    results = []
+    for step in range(2):                        # twice: buffers are fully rewritten each step
+        mw.zero_grad()
+        mw.backward(loss_of(rank))
+        mw.synchronize()
+        views = mw._master_grad_views()
+        results.append(max(float((views.get(p, p.grad).float() - ref[p]).abs().max()) for p in mw.reducer.params))
+    nb = mw.reducer.num_buckets
+    q.put((rank, results, nb, float(views[m.unused.weight].abs().max())))
+    pdist.finalize()
+
+
+def test_master_weights_overlapped_backward_world2():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, errs, nb, unused in res:
+        assert nb > 2
+        assert all(e < 1e-5 for e in errs), (rank, errs)
+        assert unused == 0.0
+
+
 def _distmodule_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     from applestar_amd.parallel import dist as pdist

@@ -15,4 +15,9 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: -float(r['TotalDu
 for r in rows[:60]:
     print(f"{float(r['TotalDurationNs'])/5e6:8.3f} ms/it {int(r['Calls'])//5:6d} calls/it  {r['Name'][:150]}")
 PY
-exit $rc
+[ $rc -eq 0 ] || exit $rc
+t=$(find $R/gpurun_out/${TAG} -name '*kernel_trace.csv' | head -1)
+[ -n "$t" ] && python3 $R/tools/prof_gaps.py "$t" 30 > $R/gpurun_out/${TAG}_gaps.txt && head -8 $R/gpurun_out/${TAG}_gaps.txt
+# the raw trace is large: keep only the summaries
+[ -n "$t" ] && rm -f "$t"
+exit 0
