@@ -663,6 +663,54 @@ std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t
   return {flat.narrow(0, 0, NK).view({N, K}), want_bias ? flat.narrow(0, NK, N) : at::Tensor()};
 }
 
+// ---------------------------------------------------------------- fused categorical head statistics
+// logits [R, C] fp32/bf16, teacher [R, C] fp32/bf16 (optional), action [R] int64
+// -> out [3, R] fp32 (logp_a, entropy, KL(teacher || logits)), stats [R, 6] fp32
+std::vector<at::Tensor> head_stats_fwd(const at::Tensor& logits, const c10::optional<at::Tensor>& teacher,
+                                       const at::Tensor& action) {
+  check_cuda(logits, "logits");
+  check_cuda(action, "action");
+  TORCH_CHECK(logits.dim() == 2 && logits.is_contiguous(), "head_stats: logits [R, C] contiguous");
+  TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16, "head_stats: logits dtype");
+  TORCH_CHECK(action.scalar_type() == at::kLong && action.is_contiguous() && action.numel() == logits.size(0),
+              "head_stats: action int64 [R]");
+  const int64_t R = logits.size(0), C = logits.size(1);
+  TORCH_CHECK(C > 0 && C < (1 << 30), "head_stats: C");
+  const void* tp = nullptr;
+  int tdt = 0;
+  if (teacher.has_value()) {
+    const at::Tensor& t = *teacher;
+    check_cuda(t, "teacher");
+    TORCH_CHECK(t.sizes() == logits.sizes() && t.is_contiguous(), "head_stats: teacher [R, C] contiguous");
+    TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "head_stats: teacher dtype");
+    tp = t.data_ptr();
+    tdt = dt(t);
+  }
+  c10::hip::HIPGuard g(logits.device().index());
+  auto out = at::empty({3, R}, logits.options().dtype(at::kFloat));
+  auto stats = at::empty({R, 6}, logits.options().dtype(at::kFloat));
+  as::head_stats_fwd(logits.data_ptr(), dt(logits), tp, tdt, action.data_ptr<int64_t>(), out.data_ptr<float>(),
+                     stats.data_ptr<float>(), R, static_cast<int>(C), stream());
+  return {out, stats};
+}
+
+at::Tensor head_stats_bwd(const at::Tensor& logits, const c10::optional<at::Tensor>& teacher, const at::Tensor& action,
+                          const at::Tensor& stats, const at::Tensor& grad) {
+  check_cuda(grad, "grad");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat && grad.is_contiguous() && grad.numel() == 3 * logits.size(0),
+              "head_stats_bwd: grad fp32 [3, R]");
+  TORCH_CHECK(stats.scalar_type() == at::kFloat && stats.is_contiguous() && stats.numel() == 6 * logits.size(0),
+              "head_stats_bwd: stats");
+  const int64_t R = logits.size(0), C = logits.size(1);
+  const void* tp = teacher.has_value() ? teacher->data_ptr() : nullptr;
+  const int tdt = teacher.has_value() ? dt(*teacher) : 0;
+  c10::hip::HIPGuard g(logits.device().index());
+  auto dl = at::empty_like(logits);
+  as::head_stats_bwd(logits.data_ptr(), dt(logits), tp, tdt, action.data_ptr<int64_t>(), stats.data_ptr<float>(),
+                     grad.data_ptr<float>(), dl.data_ptr(), R, static_cast<int>(C), stream());
+  return dl;
+}
+
 // ---------------------------------------------------------------- conv epilogue backward -> NHWC bf16
 // dout: [B, H, W, C] view (NHWC- or NCHW-contiguous underneath); out: NHWC bf16 (used when relu).
 at::Tensor act_grad_nhwc(const at::Tensor& dout, const c10::optional<at::Tensor>& out, bool relu) {
@@ -785,6 +833,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pointwise_supported", [](int64_t ci, int64_t co) { return as::pointwise_supported(static_cast<int>(ci), static_cast<int>(co)); });
   m.def("lstm_split_error", &lstm_split_error);
   m.def("multi_copy", &multi_copy);
+  m.def("head_stats_fwd", &head_stats_fwd);
+  m.def("head_stats_bwd", &head_stats_bwd);
   m.def("act_grad_nhwc", &act_grad_nhwc);
   m.def("conv3x3_supported", [](int64_t cin, int64_t cout) { return as::conv3x3_supported(static_cast<int>(cin), static_cast<int>(cout)); });
 }

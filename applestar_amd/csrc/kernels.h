@@ -198,4 +198,13 @@ void act_grad_nhwc(const void* dout, int dt, bool dout_nchw, const void* out, vo
 // partial slice s of dW at dw_part + s * part_stride, of db at db_part + s * part_stride
 void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
            int H, int W, int Cin, int S, hipStream_t st);
+
+// ---- loss.hip ----------------------------------------------------------------------------------
+// per row of logits l [R, C] (+ teacher t [R, C], may be null) and action a [R]:
+// out [3, R] = (logp_a, entropy, KL(t || l)); stats [R, 6] saved for the backward
+void head_stats_fwd(const void* l, int l_dt, const void* t, int t_dt, const long* act, float* out, float* stats, long R,
+                    int C, hipStream_t s);
+// dl [R, C] (l's dtype) = g_a d(logp_a) + g_H dH + g_KL dKL, g [3, R]
+void head_stats_bwd(const void* l, int l_dt, const void* t, int t_dt, const long* act, const float* stats,
+                    const float* g, void* dl, long R, int C, hipStream_t s);
 }  // namespace as

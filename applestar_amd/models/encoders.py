@@ -184,13 +184,17 @@ class EntityEncoder(nn.Module):
         return ops.linear(x, lin.weight, lin.bias, act='relu')
 
     def forward(self, entity_info: Dict[str, torch.Tensor], entity_num: torch.Tensor,
-                entity_total: Optional[int] = None):
+                entity_total: Optional[int] = None, entity_pad: Optional[int] = None):
         """``entity_total`` (optional host int = sum(min(entity_num, N))) lets the packing skip the
-        host<->device sync of a data-dependent ``nonzero``."""
+        host<->device sync of a data-dependent ``nonzero``; ``entity_pad`` (host int, a multiple of
+        ``PAD_SEGMENTS * N`` at least the real count) packs to that fixed row count instead, so the
+        step's shapes do not depend on the data (HIP-graph capture of the learner step)."""
         B, N = entity_info['unit_type'].shape
         valid = ops.sequence_mask(entity_num, N)                     # [B,N]
         if STATIC_SHAPES and valid.is_cuda:
             return self._forward_static(entity_info, entity_num, valid)
+        if entity_pad is not None and not self.reduce_type.startswith('attention_pool'):
+            return self._forward_padded(entity_info, entity_num, valid, int(entity_pad))
         if entity_total is not None and valid.is_cuda:
             flat_index = torch.nonzero_static(valid.reshape(-1), size=int(entity_total)).squeeze(1)
         else:
@@ -218,6 +222,37 @@ class EntityEncoder(nn.Module):
         embedded_entity = self.embed_fc(mean)
         return entity_embeddings, embedded_entity, valid
 
+
+    def _forward_padded(self, entity_info, entity_num, valid, T_pad: int):
+        """Packed path at a fixed row count ``T_pad``: the real entities first (same order as the
+        data-dependent packing), then ``T_pad - total`` padding rows that ride along as PAD_SEGMENTS
+        extra attention segments of <= N rows each (so every row the kernels touch is a well-formed
+        token and stays finite).  Padding rows gather entity row 0, scatter into a trash row and are
+        dropped from the per-observation mean, so they receive zero gradient; real rows see exactly
+        the packed path's math."""
+        B, N = valid.shape
+        P = PAD_SEGMENTS
+        dev = valid.device
+        gidx = torch.nonzero_static(valid.reshape(-1), size=T_pad, fill_value=0).squeeze(1)
+        lens = entity_num.clamp(max=N).to(torch.int32)
+        total = lens.sum()
+        pad_lens = ((T_pad - total) - N * torch.arange(P, device=dev, dtype=torch.int32)).clamp(0, N)
+        all_lens = torch.cat([lens, pad_lens.to(torch.int32)])
+        cu = F.pad(torch.cumsum(all_lens, 0, dtype=torch.int32), (1, 0))
+        rows = torch.arange(T_pad, device=dev)
+        sidx = torch.where(rows < total, gidx, torch.full_like(gidx, B * N))
+        x = self.embed(entity_info, gidx)                            # [T_pad,256]
+        x = self.transformer.forward_packed_embedded(x, cu, N)
+        x = F.relu(x)
+        ee = self.entity_fc(x)
+        entity_embeddings = ee.new_zeros(B * N + 1, ee.shape[-1]).index_copy(0, sidx, ee)[:B * N].view(B, N, -1)
+        seg = torch.repeat_interleave(torch.arange(B + P, device=dev), all_lens.long(), output_size=T_pad)
+        summed = ops.segment_sum(x, cu, seg)[:B].to(x.dtype)
+        if self.reduce_type == 'constant':
+            mean = summed / 512
+        else:
+            mean = summed / entity_num.clamp(min=1).unsqueeze(1).to(summed.dtype)
+        return entity_embeddings, self.embed_fc(mean), valid
 
     def _forward_static(self, entity_info, entity_num, valid):
         """Shape-static variant for HIP-graph capture (inference): every padded slot is embedded and
@@ -299,6 +334,15 @@ class SpatialEncoder(nn.Module):
 SCALAR_SIDE_STREAM = True
 # set by runtime.graphs.GraphedPolicy while capturing / replaying: shape-static entity path
 STATIC_SHAPES = False
+# padded packing (EntityEncoder._forward_padded): the padding rows form this many extra segments
+PAD_SEGMENTS = 8
+
+
+def entity_pad_for(total: int, n: int) -> int:
+    """Fixed packed row count for ``total`` real entities at padded width ``n``: the next multiple of
+    PAD_SEGMENTS * n (so the padding always fits the PAD_SEGMENTS extra segments of <= n rows)."""
+    g = PAD_SEGMENTS * max(int(n), 1)
+    return max(1, (int(total) + g - 1) // g) * g
 
 
 class Encoder(nn.Module):
@@ -309,13 +353,15 @@ class Encoder(nn.Module):
         self.entity_encoder = EntityEncoder(reduce_type)
         self.scatter_project = FCBlock(256, 32, act=True)
 
-    def forward(self, spatial_info, entity_info, scalar_info, entity_num, entity_total: Optional[int] = None):
+    def forward(self, spatial_info, entity_info, scalar_info, entity_num, entity_total: Optional[int] = None,
+                entity_pad: Optional[int] = None):
         # the scalar encoder (incl. the 20-token build-order transformer: many small kernels) is independent
         # of the entity / spatial path: side stream 1 on the GPU (its backward follows it there)
         from .model import _side_stream_call, _side_stream_join
         scalar_h = _side_stream_call(self.scalar_encoder, scalar_info, slot=1) if SCALAR_SIDE_STREAM else \
             (self.scalar_encoder(scalar_info), None)
-        entity_embeddings, embedded_entity, entity_mask = self.entity_encoder(entity_info, entity_num, entity_total)
+        entity_embeddings, embedded_entity, entity_mask = self.entity_encoder(entity_info, entity_num, entity_total,
+                                                                              entity_pad)
         proj = self.scatter_project(entity_embeddings) * entity_mask.unsqueeze(2).to(entity_embeddings.dtype)
         n = ops._native(proj) if proj.is_cuda else None
         if n is not None and n.has('spatial_embed'):

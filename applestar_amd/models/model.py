@@ -190,8 +190,8 @@ class Model(nn.Module):
             cache[name] = GraphedSection(module)
         return cache[name]
 
-    def _encode(self, spatial_info, entity_info, scalar_info, entity_num, entity_total=None):
-        return self.encoder(spatial_info, entity_info, scalar_info, entity_num, entity_total)
+    def _encode(self, spatial_info, entity_info, scalar_info, entity_num, entity_total=None, entity_pad=None):
+        return self.encoder(spatial_info, entity_info, scalar_info, entity_num, entity_total, entity_pad)
 
     def _core(self, lstm_input_seq, hidden_state):
         state = [(h.float(), c.float()) for h, c in hidden_state]
@@ -238,7 +238,7 @@ class Model(nn.Module):
         if self._use_value_feature:
             vf = _side_stream_call(self.value_encoder, value_feature)
         lstm_input, scalar_context, baseline_feature, entity_embeddings, map_skip = self._encode(
-            spatial_info, entity_info, scalar_info, entity_num, kwargs.get('entity_total'))
+            spatial_info, entity_info, scalar_info, entity_num, kwargs.get('entity_total'), kwargs.get('entity_pad'))
         H = hidden_state[0][0].shape[-1]
         h0 = [(h.view(-1, B, H)[0], c.view(-1, B, H)[0]) for h, c in hidden_state]
         out, _ = self._core(lstm_input.view(T + 1, B, -1), h0)
@@ -258,7 +258,9 @@ class Model(nn.Module):
 
         # the critic MLPs depend only on the LSTM output (+ value features): they run on the value encoder's
         # side stream (which already holds vf) while the policy heads run on the main stream
-        vf_out = vf[0] if isinstance(vf, tuple) else vf
+        # join the value encoder's side stream here (after the encoders and the LSTM were issued on the main
+        # stream, so the overlap is kept): the critic below reads vf on the main stream
+        vf_out = _side_stream_join(vf) if isinstance(vf, tuple) else vf
         critic_in = {'lstm': critic_input, 'vf': vf_out, 'bf': baseline_feature}
         values_h = _side_stream_call(critic, critic_in) if CRITIC_SIDE_STREAM else (critic(critic_in), None)
         _, _, logits = self.policy.train_forward(

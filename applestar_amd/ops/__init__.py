@@ -124,6 +124,14 @@ def varlen_attention(qkv, cu_seqlens, max_len: int, num_heads: int, head_dim: in
     return ref.varlen_attention(qkv, cu_seqlens, max_len, num_heads, head_dim)
 
 
+def head_stats(logits, teacher, actions):
+    """(logp(action), entropy, KL(teacher || logits)) per distribution row, fp32 (K19 fused kernel on GPU)."""
+    n = _native(logits)
+    if n is not None and n.has('head_stats'):
+        return n.head_stats(logits, teacher, actions)
+    return ref.head_stats(logits, teacher, actions)
+
+
 def scatter_connection(proj, x, y, H: int, W: int):
     return ref.scatter_connection(proj, x, y, H, W)
 

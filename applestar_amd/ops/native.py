@@ -22,7 +22,7 @@ def ensure_loaded():
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
-                'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock'}
+                'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats'}
 
 
 def has(name: str) -> bool:
@@ -723,3 +723,37 @@ def linear(x, w, b=None, act=None):
     with torch.autocast('cuda', enabled=False):
         y = _Linear.apply(xb, wb, bb, act == 'relu')
     return y.view(*x.shape[:-1], N)
+
+
+# ---------------------------------------------------------------------------- fused loss-head statistics
+class _HeadStats(torch.autograd.Function):
+    """(logp_a, entropy, KL) per row in one kernel; backward one pass over the row (loss.hip)."""
+
+    @staticmethod
+    def forward(ctx, logits, teacher, action):
+        out, stats = _C.head_stats_fwd(logits, teacher, action)
+        ctx.save_for_backward(logits, teacher, action, stats)
+        return out[0], out[1], out[2]
+
+    @staticmethod
+    def backward(ctx, ga, gh, gk):
+        logits, teacher, action, stats = ctx.saved_tensors
+        R = logits.shape[0]
+        z = logits.new_zeros(R, dtype=torch.float32)
+        g = torch.stack([z if x is None else x.float() for x in (ga, gh, gk)]).contiguous()
+        return _C.head_stats_bwd(logits, teacher, action, stats, g), None, None
+
+
+def head_stats(logits, teacher, actions):
+    """Fused ``reference.head_stats`` for fp32 / bf16 logits [..., C]."""
+    C = logits.shape[-1]
+    lead = logits.shape[:-1]
+    l2 = logits if logits.dtype in (torch.float32, torch.bfloat16) else logits.float()
+    l2 = l2.reshape(-1, C).contiguous()
+    t2 = None
+    if teacher is not None:
+        t2 = teacher.detach()
+        t2 = (t2 if t2.dtype in (torch.float32, torch.bfloat16) else t2.float()).reshape(-1, C).contiguous()
+    a = actions.reshape(-1).long().contiguous()
+    logp_a, ent, kl = _HeadStats.apply(l2, t2, a)
+    return logp_a.view(lead), ent.view(lead), kl.view(lead)

@@ -138,6 +138,20 @@ def categorical_stats(logits: torch.Tensor, actions: torch.Tensor):
     return logp, a_logp
 
 
+def head_stats(logits: torch.Tensor, teacher: Optional[torch.Tensor], actions: torch.Tensor):
+    """Per row of ``logits [..., C]``: (logp(action), entropy, KL(softmax(teacher) || softmax(logits))),
+    fp32, shaped like ``actions`` (rl_loss.py:63-90, as_rl_utils.py:52-127).  KL is 0 without a teacher."""
+    lp = torch.log_softmax(logits.float(), dim=-1)
+    a = actions.long().clamp(0, logits.shape[-1] - 1)
+    logp_a = lp.gather(-1, a.unsqueeze(-1)).squeeze(-1)
+    ent = -(lp.exp() * lp).sum(-1)
+    if teacher is None:
+        return logp_a, ent, torch.zeros_like(ent)
+    tlp = torch.log_softmax(teacher.float(), dim=-1)
+    kl = (tlp.exp() * (tlp - lp)).sum(-1)
+    return logp_a, ent, kl
+
+
 def vtrace_advantages(clipped_rhos, clipped_cs, rewards, values, gamma: float = 1.0, lambda_: float = 1.0):
     """as_rl_utils.py:284-312. rhos/cs/rewards [T,B], values [T+1,B] -> advantages [T,B]."""
     T = rewards.shape[0]

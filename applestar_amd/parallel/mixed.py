@@ -68,6 +68,9 @@ class MasterWeights:
             off += k
         self.fp32_params = [p for b in self.reducer.buckets if b.flat.dtype != torch.bfloat16 for p in b.params]
         self.opt_params = [self.master] + self.fp32_params
+        # multi-rank: False = per-bucket all-reduce overlapped with backward (eager step); True = backward
+        # writes the local gradient and synchronize() reduces the flat buffers (graph-captured step)
+        self.defer_allreduce = False
 
     # ---------------------------------------------------------------- per iteration
     def zero_grad(self):
@@ -86,14 +89,13 @@ class MasterWeights:
         bucket, no gather into the master afterwards."""
         self._direct = False
         self._overlapped = False
-        if self.reducer.world > 1:
+        world = self.reducer.world
+        if world > 1 and not self.defer_allreduce:
             self._backward_overlapped(loss)
             return
-        if not loss.is_cuda:
+        if not loss.is_cuda and world == 1:
             self.reducer.backward(loss)
             return
-        from ..ops import native
-        C = native.ensure_loaded()
         grads = torch.autograd.grad(loss, self.reducer.params, allow_unused=True)
         mg = self._master_grad_views()
         dst, src = [], []
@@ -103,8 +105,29 @@ class MasterWeights:
                 src.append(g)
         if len(dst) < len(self.reducer.params):   # unused parameters (e.g. value pre-training) get zeros
             self.master.grad.zero_()
-        C.multi_copy(dst, src)
+            for b in self.reducer.buckets:
+                if b.flat.dtype != torch.bfloat16:
+                    b.flat.zero_()
+        if loss.is_cuda:
+            from ..ops import native
+            native.ensure_loaded().multi_copy(dst, src)
+        else:
+            torch._foreach_copy_(dst, src)
         self._direct = True
+
+    def reduce_flat(self):
+        """All-reduce (average) the whole fp32 master gradient and the fp32 buckets: two RCCL calls,
+        used when backward ran without per-bucket overlap (``defer_allreduce``, e.g. between the two
+        halves of a graph-captured step)."""
+        import torch.distributed as dist
+        if self.reducer.world == 1:
+            return
+        bufs = [self.master.grad] + [b.flat for b in self.reducer.buckets if b.flat.dtype != torch.bfloat16]
+        avg = self.reducer.use_avg
+        for buf in bufs:
+            dist.all_reduce(buf, op=dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM, group=self.reducer.group)
+            if not avg:
+                buf.div_(self.reducer.world)
 
     # ---------------------------------------------------------------- multi-rank, overlapped
     def _comm_buffers(self):
@@ -186,6 +209,7 @@ class MasterWeights:
     def synchronize(self):
         """All-reduce (if distributed) and gather the bf16 gradients into the flat fp32 master grad."""
         if getattr(self, '_direct', False):
+            self.reduce_flat()
             return
         if getattr(self, '_overlap_done', False):
             self._overlap_done = False

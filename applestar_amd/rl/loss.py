@@ -4,7 +4,9 @@ entropy, teacher KL (+ extra action-type KL), optional DAPO.
 Semantics follow ``distar/agent/default/rl_training/rl_loss.py:33-178`` and ``as_rl_utils.py:1-127``.
 Differences by design (not in the math):
 
-* every head's log-softmax is computed once (fp32) and shared by logp / entropy / KL;
+* every head's logp(action), entropy and teacher KL come from ONE fused per-row kernel
+  (``ops.head_stats``, csrc/kernels/loss.hip) with a one-pass backward, instead of log-softmax / exp /
+  gather / product / sum chains over the [T, B, C] logits of both the learner and the teacher;
 * the six heads' V-trace (and UPGO) scans run as one batched reverse scan;
 * nothing calls ``.item()`` — the info dict holds 0-d device tensors that the logger fetches with a
   single device->host copy (the reference syncs ~40 times per iteration).
@@ -17,6 +19,7 @@ from typing import Dict
 import torch
 import torch.nn.functional as F
 
+from .. import ops
 from ..utils.config import AttrDict, deep_merge_dicts
 from . import rl_utils
 
@@ -91,12 +94,9 @@ class ReinforcementLoss:
             values[k] = torch.cat([values[k][:-1], values[k][-1:] * not_done], 0).float()
 
         info: Dict[str, torch.Tensor] = {}
-        logp_all, tgt_logp, rhos = {}, {}, {}
+        tgt_logp, rhos, ent_raw, kl_raw = {}, {}, {}, {}
         for h in HEADS:
-            lp = torch.log_softmax(logits[h].float(), dim=-1)
-            logp_all[h] = lp
-            a = actions[h].long()
-            alp = lp.gather(-1, a.unsqueeze(-1)).squeeze(-1)
+            alp, ent_raw[h], kl_raw[h] = ops.head_stats(logits[h], teacher_logits.get(h), actions[h])
             with torch.no_grad():
                 log_rho = alp - behaviour_logp[h].float()
                 if h == 'selected_units':
@@ -157,8 +157,7 @@ class ReinforcementLoss:
         # ---------------- entropy (normalised per head)
         total_ent = 0.0
         for h in HEADS:
-            lp = logp_all[h]
-            ent = -(lp.exp() * lp).sum(-1)
+            ent = ent_raw[h]
             if h == 'selected_units':
                 n_valid = masks['selected_units_logits_mask'].float().sum(-1)
                 ent = ent / (1e-9 + torch.log(n_valid + 1).unsqueeze(-1))
@@ -167,7 +166,7 @@ class ReinforcementLoss:
                 n_valid = masks['target_units_logits_mask'].float().sum(-1)
                 ent = ent / (1e-9 + torch.log(n_valid + 1))
             else:
-                ent = ent / math.log(lp.shape[-1])
+                ent = ent / math.log(logits[h].shape[-1])
             if h not in ('action_type', 'delay'):
                 ent = ent * am[h].float()
             e = ent.mean()
@@ -180,8 +179,7 @@ class ReinforcementLoss:
         total_kl = 0.0
         at_kl_loss = torch.zeros((), device=v.device)
         for h in ['action_type', 'queued', 'delay', 'selected_units', 'target_unit', 'target_location']:
-            t_lp = torch.log_softmax(teacher_logits[h].float(), dim=-1)
-            kl = (t_lp.exp() * (t_lp - logp_all[h])).sum(-1)
+            kl = kl_raw[h]
             if h == 'selected_units':
                 kl = (kl * su_mask).sum(-1)
             if h not in ('action_type', 'delay'):
@@ -202,8 +200,7 @@ class ReinforcementLoss:
         if self.use_dapo and 'successive_logit' in inputs:
             flag = (game_steps < self.dapo_steps).float()
             for h in HEADS:
-                s_lp = torch.log_softmax(inputs['successive_logit'][h].float(), dim=-1)
-                kl = (s_lp.exp() * (s_lp - logp_all[h])).sum(-1)
+                _, _, kl = ops.head_stats(logits[h], inputs['successive_logit'][h], actions[h])
                 if h == 'selected_units':
                     kl = (kl * su_mask).sum(-1)
                 if h not in ('action_type', 'delay'):

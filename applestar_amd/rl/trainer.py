@@ -33,6 +33,11 @@ DEFAULT_LEARNER_CONFIG = AttrDict({
         'bucket_mb': 32,
         'comm_dtype': None,
         'amp_dtype': 'bfloat16',
+        # HIP-graph capture of the whole step (runtime/step_graph.py); GPU only.  Off by default: on ROCm 7
+        # a replay of the ~2,400-node step graph costs ~23 ms of host time (~9.5 us per node, vs ~16 us
+        # per eager launch) and the replayed step ran 2.6 ms slower on the GPU (bench r2d/r2e:
+        # 45.8 vs 43.2 ms/step), so the eager step wins until the launch count is much lower
+        'graph_step': False,
     },
     'model': {'enable_baselines': ['winloss']},
 })
@@ -41,7 +46,13 @@ DEFAULT_LEARNER_CONFIG = AttrDict({
 def _amp(device: torch.device, dtype_name: Optional[str]):
     if device.type != 'cuda' or not dtype_name:
         return contextlib.nullcontext()
-    return torch.autocast('cuda', dtype=getattr(torch, dtype_name))
+    # no autocast weight cache: the compute weights are already bf16 (master weights), and a cache
+    # must not outlive a HIP-graph capture
+    return torch.autocast('cuda', dtype=getattr(torch, dtype_name), cache_enabled=False)
+
+
+# grad-clip types whose state is all on the device (safe to replay from a graph)
+_GRAPH_SAFE_CLIPS = ('none', 'pytorch_norm', 'clip_norm', 'clip_const')
 
 
 class RLTrainer:
@@ -77,12 +88,28 @@ class RLTrainer:
         self.iter = 0
         self.remain_value_pretrain = int(lc.get('value_pretrain_iters', -1))
         self.amp_dtype = lc.get('amp_dtype')
+        self.graph = None
+        if self._graph_capable():
+            from ..runtime.step_graph import GraphedTrainStep
+            if self.master is not None:
+                self.master.defer_allreduce = True     # the all-reduce runs between the two graphs
+            self.graph = GraphedTrainStep(self._fwd_bwd, self._reduce, self._update, device=self.device)
+
+    def _graph_capable(self) -> bool:
+        lc = self.cfg.learner
+        return (self.device.type == 'cuda' and bool(lc.get('graph_step', False)) and self.master is not None and
+                self.grad_clip.clip_type in _GRAPH_SAFE_CLIPS and isinstance(self.optimizer, torch.optim.Adam) and
+                self.optimizer.defaults.get('capturable', False))
 
     def reset_optimizer(self):
         """Fresh Adam(betas=(0, 0.99), eps=1e-5) state (also used after a league reset)."""
         lc = self.cfg.learner
-        self.optimizer = build_optimizer(self.opt_params, lc, betas=(0.0, 0.99), eps=1e-5, device=self.device)
+        capturable = self.device.type == 'cuda' and bool(lc.get('graph_step', False))
+        self.optimizer = build_optimizer(self.opt_params, lc, betas=(0.0, 0.99), eps=1e-5, device=self.device,
+                                         capturable=capturable)
         self.lr_scheduler = None
+        if getattr(self, 'graph', None) is not None:
+            self.graph.reset()
 
     def _value_pretrain_toggle(self):
         active = self.remain_value_pretrain > 0
@@ -91,8 +118,8 @@ class RLTrainer:
         if active:
             self.remain_value_pretrain -= 1
 
-    def step(self, batch: Dict) -> Dict[str, torch.Tensor]:
-        self._value_pretrain_toggle()
+    # ------------------------------------------------------------------ one iteration, in three parts
+    def _fwd_bwd(self, batch: Dict) -> Dict[str, torch.Tensor]:
         self.model.train()
         with _amp(self.device, self.amp_dtype):
             out = self.model.rl_learner_forward(**batch)
@@ -102,14 +129,35 @@ class RLTrainer:
             self.master.backward(info['total_loss'])
         else:
             self.reducer.backward(info['total_loss'])
+        # detached: a returned loss must not keep this step's autograd graph (and its AccumulateGrad nodes,
+        # bound to the stream they were created on) alive into the next step - or into a graph capture
+        return {k: (v.detach() if torch.is_tensor(v) else v) for k, v in info.items()}
+
+    def _reduce(self):
         if self.master is not None:
             self.master.synchronize()
         else:
             self.reducer.synchronize()
-        info['gradient'] = self.grad_clip.apply(self.opt_params)
+
+    def _update(self) -> torch.Tensor:
+        norm = self.grad_clip.apply(self.opt_params)
         self.optimizer.step()
         if self.master is not None:
             self.master.after_step()
+        return norm
+
+    def step(self, batch: Dict) -> Dict[str, torch.Tensor]:
+        self._value_pretrain_toggle()
+        if self.graph is not None and 'entity_total' in batch:
+            from ..models.encoders import entity_pad_for
+            b = dict(batch)
+            total = b.pop('entity_total')
+            b['entity_pad'] = entity_pad_for(total, b['entity_info']['unit_type'].shape[1])
+            info = self.graph(b, extra_key=(self.model.only_update_baseline,))
+        else:
+            info = self._fwd_bwd(batch)
+            self._reduce()
+            info['gradient'] = self._update()
         self.iter += 1
         return info
 

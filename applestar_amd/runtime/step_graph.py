@@ -1,0 +1,165 @@
+"""Whole learner step as HIP graphs: forward + loss + backward in one graph, clip + Adam + weight
+publish in a second; the data-parallel gradient all-reduce (RCCL) runs eagerly between the two.
+
+An RL learner step is ~2,400 kernel launches; eagerly each costs ~16 us of host time (PyTorch
+dispatch + autograd).  Measured on MI355X / ROCm 7 (profiles/r2e_*): replaying the step graph costs
+~23 ms of host time (~9.5 us per node: the HIP runtime still submits node by node) and the replayed
+step ran 2.6 ms slower on the GPU than the eager one, so RLTrainer keeps this opt-in
+(``learner.graph_step``) until fusion has cut the node count; the machinery (static shapes, eager
+warm-up, shared pool, the DP all-reduce between the two graphs) is tested for equivalence.
+
+Shapes must be static per graph.  The one data-dependent shape of the learner step, the packed entity
+count, is fixed by packing to ``encoders.entity_pad_for(total, N)`` rows (``EntityEncoder._forward_padded``:
+padding rows ride along as extra attention segments and get zero gradient).  Everything else is keyed:
+one graph pair per input signature (tensor shapes/dtypes, python scalars, value-pretrain flag), LRU-bounded,
+all sharing one memory pool (graphs replay strictly one after another).
+
+Protocol per signature: the first occurrence runs eagerly (a real training step that also warms up
+lazily-created state: optimizer moments, library workspaces, cached weight folds); the second
+occurrence captures and then replays.  Outputs are the graph's static tensors, packed and copied once
+so callers may keep them across steps.
+"""
+from __future__ import annotations
+
+import os
+import time
+from collections import OrderedDict
+from typing import Callable, Dict, Optional, Tuple
+
+import torch
+
+__all__ = ['GraphedTrainStep', 'batch_signature']
+
+
+def _tree_clone(x):
+    if torch.is_tensor(x):
+        return x.clone()
+    if isinstance(x, dict):
+        return {k: _tree_clone(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_tree_clone(v) for v in x)
+    return x
+
+
+def _tree_copy_(dst, src, path='batch'):
+    if torch.is_tensor(dst):
+        if dst.shape != src.shape or dst.dtype != src.dtype:
+            raise ValueError(f'{path}: {tuple(src.shape)}/{src.dtype} != captured {tuple(dst.shape)}/{dst.dtype}')
+        dst.copy_(src, non_blocking=True)
+    elif isinstance(dst, dict):
+        for k in dst:
+            _tree_copy_(dst[k], src[k], f'{path}.{k}')
+    elif isinstance(dst, (list, tuple)):
+        for i, (a, b) in enumerate(zip(dst, src)):
+            _tree_copy_(a, b, f'{path}[{i}]')
+
+
+def batch_signature(x):
+    """Hashable description of everything a captured step depends on: tensor shapes/dtypes/devices and
+    plain python values (batch_size, unroll_len, entity_pad...)."""
+    if torch.is_tensor(x):
+        return ('T', tuple(x.shape), str(x.dtype), x.device.type)
+    if isinstance(x, dict):
+        return tuple((k, batch_signature(v)) for k, v in sorted(x.items()))
+    if isinstance(x, (list, tuple)):
+        return tuple(batch_signature(v) for v in x)
+    return x
+
+
+class _Entry:
+    __slots__ = ('fb', 'upd', 'static_in', 'keys', 'packed', 'grad_norm')
+
+
+class GraphedTrainStep:
+    """``GraphedTrainStep(fwd_bwd, reduce, update)(batch, extra_key)``.
+
+    * ``fwd_bwd(batch) -> Dict[str, 0-d tensor]``: forward, loss and backward into the gradient buffers;
+    * ``reduce()``: the cross-rank gradient reduction (eager, between the graphs; no-op on one rank);
+    * ``update() -> 0-d tensor``: clip + optimizer + weight publish, returns the pre-clip gradient norm.
+    """
+
+    def __init__(self, fwd_bwd: Callable[[Dict], Dict[str, torch.Tensor]], reduce: Callable[[], None],
+                 update: Callable[[], torch.Tensor], max_graphs: int = 6, device=None):
+        self.fwd_bwd, self.reduce, self.update = fwd_bwd, reduce, update
+        self.max_graphs = max_graphs
+        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        self._graphs: 'OrderedDict[Tuple, _Entry]' = OrderedDict()
+        self._seen = set()
+        self._pool = None
+        self.captures = 0
+        self.replays = 0
+        self.eager_steps = 0
+        self.host_time: Dict[str, float] = {}     # summed host seconds per replay phase
+        # forked side streams (value / scalar encoders) inside the capture; off: captured on one stream
+        self.side_streams = os.environ.get('APPLESTAR_GRAPH_SIDE_STREAMS', '0') == '1'
+
+    def _eager(self, batch):
+        info = self.fwd_bwd(batch)
+        self.reduce()
+        info['gradient'] = self.update()
+        self.eager_steps += 1
+        return info
+
+    def _capture(self, key, batch) -> _Entry:
+        if len(self._graphs) >= self.max_graphs:
+            self._graphs.popitem(last=False)
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        e = _Entry()
+        e.static_in = _tree_clone(batch)
+        torch.cuda.synchronize(self.device)
+        e.fb = torch.cuda.CUDAGraph()
+        from ..models import encoders, model as model_mod
+        flags = (encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED)
+        if not self.side_streams:
+            encoders.SCALAR_SIDE_STREAM = model_mod.SIDE_STREAMS_ENABLED = False
+        try:
+            with torch.cuda.graph(e.fb, pool=self._pool):
+                info = self.fwd_bwd(e.static_in)
+                e.keys = sorted(k for k, v in info.items() if torch.is_tensor(v) and v.numel() == 1)
+                e.packed = torch.stack([info[k].detach().float().reshape(()) for k in e.keys]) if e.keys else None
+        finally:
+            encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED = flags
+        e.upd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(e.upd, pool=self._pool):
+            e.grad_norm = self.update().detach().float().reshape(())
+        self.captures += 1
+        self._graphs[key] = e
+        return e
+
+    def __call__(self, batch: Dict, extra_key=()) -> Dict[str, torch.Tensor]:
+        key = (batch_signature(batch), extra_key)
+        e = self._graphs.get(key)
+        if e is None:
+            if key not in self._seen:
+                self._seen.add(key)
+                return self._eager(batch)
+            e = self._capture(key, batch)
+        else:
+            self._graphs.move_to_end(key)
+        t = self.host_time
+        t0 = time.perf_counter()
+        _tree_copy_(e.static_in, batch)
+        t1 = time.perf_counter()
+        e.fb.replay()
+        t2 = time.perf_counter()
+        self.reduce()
+        t3 = time.perf_counter()
+        e.upd.replay()
+        t4 = time.perf_counter()
+        for k, dt in (('copy_in', t1 - t0), ('replay_fwd_bwd', t2 - t1), ('reduce', t3 - t2), ('replay_update', t4 - t3)):
+            t[k] = t.get(k, 0.0) + dt
+        self.replays += 1
+        out: Dict[str, torch.Tensor] = {}
+        if e.packed is not None:
+            vals = torch.cat([e.packed, e.grad_norm.reshape(1)]).clone()
+            out = {k: vals[i] for i, k in enumerate(e.keys)}
+            out['gradient'] = vals[-1]
+        else:
+            out['gradient'] = e.grad_norm.clone()
+        return out
+
+    def reset(self):
+        """Drop every captured graph (e.g. after the optimizer or the parameter set was replaced)."""
+        self._graphs.clear()
+        self._seen.clear()

@@ -175,7 +175,8 @@ class Adam(torch.optim.Adam):
         self._thre = {plist[int(i)]: v.to(plist[int(i)].device) for i, v in thre.items()}
 
 
-def build_optimizer(params, lc, betas=(0.9, 0.999), eps: float = 1e-8, device=None) -> torch.optim.Optimizer:
+def build_optimizer(params, lc, betas=(0.9, 0.999), eps: float = 1e-8, device=None,
+                    capturable: bool = False) -> torch.optim.Optimizer:
     """Learner optimizer from the config: plain (fused on the GPU) Adam by default; the extended
     :class:`Adam` when ``learner.optimizer`` asks for AdamW or a clip / ignore variant, e.g.
     ``optimizer: {optim_type: adamw, grad_ignore_type: ignore_norm, ignore_value: 50}``."""
@@ -186,5 +187,6 @@ def build_optimizer(params, lc, betas=(0.9, 0.999), eps: float = 1e-8, device=No
     kw = dict(lr=lc.learning_rate, betas=betas, eps=eps, weight_decay=lc.get('weight_decay', 0.0))
     if not ocfg or (ocfg.get('optim_type', 'adam') == 'adam' and not ocfg.get('grad_clip_type')
                     and not ocfg.get('grad_ignore_type')):
-        return torch.optim.Adam(params, fused=fused, **kw)
+        # capturable: the step counter stays on the device so the update can be replayed from a HIP graph
+        return torch.optim.Adam(params, fused=fused, capturable=bool(capturable and fused), **kw)
     return Adam(params, fused=fused, **kw, **ocfg)

@@ -38,6 +38,7 @@ def main():
     ap.add_argument('--profile-steps', type=int, default=0)
     ap.add_argument('--mode', choices=['rl', 'sl'], default='rl',
                     help='rl: the headline RL learner step; sl: supervised learner step (reference 384 samples/s/GPU)')
+    ap.add_argument('--graph', action='store_true', help='replay the learner step from HIP graphs (runtime/step_graph.py)')
     ap.add_argument('--conv-benchmark', type=int, default=-1,
                     help='1/0: force MIOpen find-mode autotuning of convolutions on/off (-1: trainer default)')
     args = ap.parse_args()
@@ -60,8 +61,8 @@ def main():
     torch.manual_seed(1234 + rank)
 
     if args.mode == 'rl':
-        trainer = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}},
-                            device=device)
+        trainer = RLTrainer({'learner': {'use_value_feature': True, 'graph_step': args.graph},
+                             'model': {'enable_baselines': ['winloss']}}, device=device)
         make = lambda i: rl_batch(args.batch, args.unroll, max_entities=args.max_entities, seed=1000 * rank + i)  # noqa
     else:
         from applestar_amd.sl.trainer import SLTrainer
@@ -133,6 +134,11 @@ def main():
                 'native_kernels': (not args.no_native) and gpu,
                 'final_loss': loss,
                 'host_ms_per_step': round(1000.0 * host / max(args.steps, 1), 3),
+                'graph_step': ({'captures': trainer.graph.captures, 'replays': trainer.graph.replays,
+                                'eager_steps': trainer.graph.eager_steps,
+                                'host_ms_per_replay': {k: round(1000.0 * v / max(trainer.graph.replays, 1), 3)
+                                                       for k, v in trainer.graph.host_time.items()}}
+                               if getattr(trainer, 'graph', None) is not None else None),
             },
         }
         print(json.dumps(out), flush=True)

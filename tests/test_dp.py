@@ -124,7 +124,7 @@ def test_master_weights_world2():
     assert all(np.abs(s0[k] - ref[k]).max() > 0 for k in ('fc1.weight', 'fc2.weight', 'conv.weight', 'ln.weight'))
 
 
-def _overlap_worker(rank, world, port, q):
+def _overlap_worker(rank, world, port, q, defer=False):
     """MasterWeights.backward at world 2: per-bucket copy + all-reduce from tensor hooks, into the fp32
     master gradient; compared with the average of both ranks' gradients computed locally."""
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
@@ -136,6 +136,7 @@ def _overlap_worker(rank, world, port, q):
     m.unused = torch.nn.Linear(4, 4)           # a bucket-mate that gets no gradient
     m.conv.to(memory_format=torch.channels_last)
     mw = MasterWeights(m, bucket_mb=0.0002)
+    mw.defer_allreduce = defer
 
     def data(r):
         g = torch.Generator().manual_seed(100 + r)
@@ -166,12 +167,15 @@ def _overlap_worker(rank, world, port, q):
     pdist.finalize()
 
 
-def test_master_weights_overlapped_backward_world2():
+@pytest.mark.parametrize('defer', [False, True])
+def test_master_weights_overlapped_backward_world2(defer):
+    """defer=False: per-bucket all-reduce from tensor hooks during backward; defer=True: backward writes
+    the local gradient and synchronize() reduces the flat master gradient (graph-captured step)."""
     world = 2
     port = _free_port()
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_overlap_worker, args=(r, world, port, q, defer)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda r: r[0])

@@ -619,3 +619,40 @@ def test_conv_wt_matches_flip_permute(cout, cin, channels_last):
     ref = w.flip(2, 3).permute(1, 2, 3, 0).contiguous()
     assert got.shape == ref.shape and got.is_contiguous()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize('C', [2, 128, 327, 513, 4097, 24320])
+@pytest.mark.parametrize('ldt', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('with_teacher', [True, False])
+def test_head_stats_matches_reference(C, ldt, with_teacher):
+    """Fused (logp_a, entropy, KL) rows and their one-pass backward vs log_softmax chains in fp32,
+    including -1e9-masked columns and fully masked rows (padded selected-units steps)."""
+    torch.manual_seed(21)
+    R = 37
+    logits = (3 * torch.randn(R, C, device=DEV)).to(ldt)
+    teacher = 3 * torch.randn(R, C, device=DEV) if with_teacher else None
+    if C > 4:
+        logits[:, C // 2:] = -1e9                   # masked tail
+        if teacher is not None:
+            teacher[:, C // 2:] = -1e9
+        logits[3] = -1e9                            # fully masked row
+        if teacher is not None:
+            teacher[3] = -1e9
+    act = torch.randint(0, max(1, C // 2), (R,), device=DEV)
+    l1 = logits.detach().clone().requires_grad_()
+    got = N.head_stats(l1, teacher, act)
+    l2 = logits.detach().float().clone().requires_grad_()
+    ref = R_head_stats(l2, teacher, act)
+    for a, b in zip(got, ref):
+        assert a.dtype == torch.float32
+        assert _err(a, b) < 1e-3 * max(1.0, b.abs().max().item()), (_err(a, b))
+    gs = [torch.randn(R, device=DEV) for _ in range(3)]
+    sum((x * g).sum() for x, g in zip(got, gs)).backward()
+    sum((x * g).sum() for x, g in zip(ref, gs)).backward()
+    assert l1.grad.dtype == ldt
+    tol = 2e-2 if ldt == torch.bfloat16 else 1e-4
+    assert _err(l1.grad, l2.grad) < tol * max(1.0, l2.grad.abs().max().item()), _err(l1.grad, l2.grad)
+
+
+def R_head_stats(logits, teacher, act):
+    return R.head_stats(logits, teacher, act)
