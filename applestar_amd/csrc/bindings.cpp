@@ -663,6 +663,93 @@ std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t
   return {flat.narrow(0, 0, NK).view({N, K}), want_bias ? flat.narrow(0, NK, N) : at::Tensor()};
 }
 
+// ---------------------------------------------------------------- fused build-order transformer
+// params: w0, b0, then per layer ln1w, ln1b, wqkv, bqkv, wp, bp, ln2w, ln2b, w1, b1, w2, b2 (38 tensors):
+// linear weights / biases all bf16 or all fp32, LayerNorm affines fp32
+namespace {
+int idx_code(const at::Tensor& t) {
+  if (t.scalar_type() == at::kShort) return 0;
+  if (t.scalar_type() == at::kInt) return 1;
+  TORCH_CHECK(t.scalar_type() == at::kLong, "bo_encoder: index dtype int16 / int32 / int64");
+  return 2;
+}
+
+as::BoWeights bo_weights(const std::vector<at::Tensor>& p, int* wdt) {
+  TORCH_CHECK(p.size() == 2 + 12 * as::kBoLayers, "bo_encoder: 38 parameter tensors");
+  const auto lin_t = p[0].scalar_type();
+  TORCH_CHECK(lin_t == at::kFloat || lin_t == at::kBFloat16, "bo_encoder: linear dtype");
+  auto lin = [&](const at::Tensor& t, int64_t numel) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == lin_t && t.numel() == numel,
+                "bo_encoder: linear parameter (dtype / shape / contiguity)");
+    return static_cast<const void*>(t.data_ptr());
+  };
+  auto ln = [&](const at::Tensor& t) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat && t.numel() == 64,
+                "bo_encoder: LayerNorm parameter fp32 [64]");
+    return t.data_ptr<float>();
+  };
+  as::BoWeights w;
+  w.w0 = lin(p[0], 64 * 214);
+  w.b0 = lin(p[1], 64);
+  for (int l = 0; l < as::kBoLayers; ++l) {
+    const int o = 2 + 12 * l;
+    w.ln1w[l] = ln(p[o]);
+    w.ln1b[l] = ln(p[o + 1]);
+    w.wqkv[l] = lin(p[o + 2], 48 * 64);
+    w.bqkv[l] = lin(p[o + 3], 48);
+    w.wp[l] = lin(p[o + 4], 64 * 16);
+    w.bp[l] = lin(p[o + 5], 64);
+    w.ln2w[l] = ln(p[o + 6]);
+    w.ln2b[l] = ln(p[o + 7]);
+    w.w1[l] = lin(p[o + 8], 128 * 64);
+    w.b1[l] = lin(p[o + 9], 128);
+    w.w2[l] = lin(p[o + 10], 64 * 128);
+    w.b2[l] = lin(p[o + 11], 64);
+  }
+  *wdt = lin_t == at::kBFloat16 ? as::DT_BF16 : as::DT_F32;
+  return w;
+}
+}  // namespace
+
+// bo, loc [B, 20] -> (mean [B, 64] fp32, save [B, 3, kBoRecord] fp32 or undefined)
+std::vector<at::Tensor> bo_encoder_fwd(const at::Tensor& bo, const at::Tensor& loc, const std::vector<at::Tensor>& params,
+                                       bool save) {
+  check_cuda(bo, "bo");
+  check_cuda(loc, "loc");
+  TORCH_CHECK(bo.dim() == 2 && bo.size(1) == as::kBoTokens && bo.is_contiguous() && loc.sizes() == bo.sizes() &&
+                  loc.is_contiguous() && loc.scalar_type() == bo.scalar_type(),
+              "bo_encoder: bo / loc [B, 20] contiguous, same dtype");
+  int wdt = 0;
+  const as::BoWeights w = bo_weights(params, &wdt);
+  const int64_t B = bo.size(0);
+  c10::hip::HIPGuard g(bo.device().index());
+  auto opts = bo.options().dtype(at::kFloat);
+  auto out = at::empty({B, 64}, opts);
+  at::Tensor rec;
+  if (save) rec = at::empty({B, as::kBoLayers, as::kBoRecord}, opts);
+  as::bo_encoder_fwd(bo.data_ptr(), loc.data_ptr(), idx_code(bo), w, wdt, out.data_ptr<float>(),
+                     save ? rec.data_ptr<float>() : nullptr, B, stream());
+  return {out, rec};
+}
+
+// -> flat fp32 parameter gradient [kBoGradSize] in the params order
+at::Tensor bo_encoder_bwd(const at::Tensor& bo, const at::Tensor& loc, const std::vector<at::Tensor>& params,
+                          const at::Tensor& save, const at::Tensor& dmean) {
+  check_cuda(dmean, "dmean");
+  const int64_t B = bo.size(0);
+  TORCH_CHECK(dmean.scalar_type() == at::kFloat && dmean.is_contiguous() && dmean.numel() == B * 64,
+              "bo_encoder_bwd: dmean fp32 [B, 64]");
+  TORCH_CHECK(save.scalar_type() == at::kFloat && save.numel() == B * as::kBoLayers * as::kBoRecord,
+              "bo_encoder_bwd: saved record");
+  int wdt = 0;
+  const as::BoWeights w = bo_weights(params, &wdt);
+  c10::hip::HIPGuard g(bo.device().index());
+  auto grad = at::zeros({as::kBoGradSize}, dmean.options());
+  as::bo_encoder_bwd(bo.data_ptr(), loc.data_ptr(), idx_code(bo), w, wdt, save.data_ptr<float>(),
+                     dmean.data_ptr<float>(), grad.data_ptr<float>(), B, stream());
+  return grad;
+}
+
 // ---------------------------------------------------------------- fused categorical head statistics
 // logits [R, C] fp32/bf16, teacher [R, C] fp32/bf16 (optional), action [R] int64
 // -> out [3, R] fp32 (logp_a, entropy, KL(teacher || logits)), stats [R, 6] fp32
@@ -834,6 +921,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_split_error", &lstm_split_error);
   m.def("multi_copy", &multi_copy);
   m.def("head_stats_fwd", &head_stats_fwd);
+  m.def("bo_encoder_fwd", &bo_encoder_fwd);
+  m.def("bo_encoder_bwd", &bo_encoder_bwd);
   m.def("head_stats_bwd", &head_stats_bwd);
   m.def("act_grad_nhwc", &act_grad_nhwc);
   m.def("conv3x3_supported", [](int64_t cin, int64_t cout) { return as::conv3x3_supported(static_cast<int>(cin), static_cast<int>(cout)); });

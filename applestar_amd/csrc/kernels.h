@@ -199,6 +199,33 @@ void act_grad_nhwc(const void* dout, int dt, bool dout_nchw, const void* out, vo
 void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
            int H, int W, int Cin, int S, hipStream_t st);
 
+// ---- bo_encoder.hip ----------------------------------------------------------------------------
+// fused beginning-build-order transformer (20 tokens, 3 pre-LN layers); weights bf16 or fp32 (wdt),
+// LayerNorm affines fp32; bo / loc indices int16 / int32 / int64 (idt 0 / 1 / 2)
+constexpr int kBoTokens = 20, kBoLayers = 3, kBoRecord = 11120, kBoGradSize = 76880;
+struct BoWeights {
+  const void* w0;
+  const void* b0;
+  const float* ln1w[kBoLayers];
+  const float* ln1b[kBoLayers];
+  const void* wqkv[kBoLayers];
+  const void* bqkv[kBoLayers];
+  const void* wp[kBoLayers];
+  const void* bp[kBoLayers];
+  const float* ln2w[kBoLayers];
+  const float* ln2b[kBoLayers];
+  const void* w1[kBoLayers];
+  const void* b1[kBoLayers];
+  const void* w2[kBoLayers];
+  const void* b2[kBoLayers];
+};
+// out [B, 64] fp32 = mean over tokens of the transformer output; save [B, 3, kBoRecord] (nullable)
+void bo_encoder_fwd(const void* bo, const void* loc, int idt, const BoWeights& w, int wdt, float* out, float* save,
+                    long B, hipStream_t st);
+// grad [kBoGradSize] fp32 (zeroed by the caller) += parameter gradients for dmean [B, 64]
+void bo_encoder_bwd(const void* bo, const void* loc, int idt, const BoWeights& w, int wdt, const float* save,
+                    const float* dmean, float* grad, long B, hipStream_t st);
+
 // ---- loss.hip ----------------------------------------------------------------------------------
 // per row of logits l [R, C] (+ teacher t [R, C], may be null) and action a [R]:
 // out [3, R] = (logp_a, entropy, KL(t || l)); stats [R, 6] saved for the backward

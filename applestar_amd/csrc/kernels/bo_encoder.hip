@@ -1,0 +1,384 @@
+// Beginning-build-order encoder as ONE kernel per direction.
+//
+// BeginningBuildOrderEncoder (scalar_encoder.py:19-53, value_encoder.py): 20 build-order tokens of
+// (one-hot action 174 | one-hot position 20 | 10-bit x | 10-bit y) = 214 inputs -> fc 64 + ReLU ->
+// 3 pre-LN transformer layers (64-d, 2 heads x 8, MLP 64-128-64 with ReLUs) -> mean over tokens.
+// The module is tiny (21 K MACs per token and layer) but, as torch ops, it is ~70 forward and ~125
+// backward kernel launches per use, and the learner uses it twice per step (scalar encoder + value
+// encoder) for every one of the (T+1) B observations (r2i launch attribution: 390 launches, 4.3 ms).
+//
+// Here one 256-thread workgroup owns one observation: the 20 x 64 residual stream lives in LDS, each
+// linear stages its weight (bf16 or fp32, transposed) in LDS and computes in fp32, LayerNorm is one
+// wave per token (64 lanes = 64 features), softmax one thread per (head, query) row.  The embedding
+// never builds the 214-wide input: its pre-activation is the sum of the weight columns the token
+// selects (action, position and the set bits of x and y).  The forward saves per-layer activations
+// (133 KB per observation) for the backward, which replays the layers in reverse and accumulates the
+// parameter gradients with fp32 atomics (no per-observation partial buffers).
+#include <math.h>
+
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+constexpr int L = kBoTokens, D = 64, QD = 48, NH = 2, HDIM = 8, HID = 128, NL = kBoLayers, IN = 214, NACT = 174;
+constexpr float kScale = 0.35355339059327373f;  // 1 / sqrt(8)
+constexpr float kEps = 1e-5f;
+
+// per-layer record of the forward (floats)
+constexpr int R_XIN = 0, R_U1 = R_XIN + L * D, R_MU1 = R_U1 + L * D, R_RS1 = R_MU1 + L, R_QKV = R_RS1 + L,
+              R_P = R_QKV + L * QD, R_O = R_P + NH * L * L, R_XMID = R_O + L * 16, R_U2 = R_XMID + L * D,
+              R_MU2 = R_U2 + L * D, R_RS2 = R_MU2 + L, R_H1 = R_RS2 + L, R_H2 = R_H1 + L * HID, REC = R_H2 + L * D;
+static_assert(REC == kBoRecord, "record size");
+
+// gradient buffer layout (floats): W0, b0, then per layer ln1w ln1b wqkv bqkv wp bp ln2w ln2b w1 b1 w2 b2
+constexpr int G_W0 = 0, G_B0 = D * IN, G_L0 = G_B0 + D;
+constexpr int G_LN1W = 0, G_LN1B = 64, G_WQKV = 128, G_BQKV = G_WQKV + QD * D, G_WP = G_BQKV + QD,
+              G_BP = G_WP + D * 16, G_LN2W = G_BP + D, G_LN2B = G_LN2W + D, G_W1 = G_LN2B + D, G_B1 = G_W1 + HID * D,
+              G_W2 = G_B1 + HID, G_B2 = G_W2 + D * HID, G_LAYER = G_B2 + D;
+static_assert(G_L0 + NL * G_LAYER == kBoGradSize, "grad size");
+
+template <typename T>
+__device__ __forceinline__ float ldw(const void* p, int i) {
+  return Cvt<T>::load(static_cast<const T*>(p), i);
+}
+
+__device__ __forceinline__ long ld_idx(const void* p, long i, int idt) {
+  if (idt == 0) return static_cast<const int16_t*>(p)[i];
+  if (idt == 1) return static_cast<const int32_t*>(p)[i];
+  return static_cast<const long*>(p)[i];
+}
+
+// Y[t][n] = act(sum_k A[t][k] W[n][k] + b[n]); A, Y in LDS; W [N][K] global, staged transposed in wb
+template <int K, int N, typename WT>
+__device__ __forceinline__ void mm_nt(const float* A, const void* W, const void* b, float* Y, bool relu, float* wb) {
+  for (int i = threadIdx.x; i < N * K; i += 256) {
+    const int n = i / K, k = i - n * K;
+    wb[k * (N + 1) + n] = ldw<WT>(W, i);
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < L * N; o += 256) {
+    const int t = o / N, n = o - t * N;
+    float acc = ldw<WT>(b, n);
+#pragma unroll 8
+    for (int k = 0; k < K; ++k) acc += A[t * K + k] * wb[k * (N + 1) + n];
+    Y[o] = relu ? fmaxf(acc, 0.f) : acc;
+  }
+  __syncthreads();
+}
+
+// dA[t][k] = sum_n dY[t][n] W[n][k]; W [N][K] global staged in wb (row pitch K + 1)
+template <int K, int N, typename WT>
+__device__ __forceinline__ void mm_nn(const float* dY, const void* W, float* dA, float* wb) {
+  for (int i = threadIdx.x; i < N * K; i += 256) {
+    const int n = i / K, k = i - n * K;
+    wb[n * (K + 1) + k] = ldw<WT>(W, i);
+  }
+  __syncthreads();
+  for (int o = threadIdx.x; o < L * K; o += 256) {
+    const int t = o / K, k = o - t * K;
+    float acc = 0.f;
+#pragma unroll 8
+    for (int n = 0; n < N; ++n) acc += dY[t * N + n] * wb[n * (K + 1) + k];
+    dA[o] = acc;
+  }
+  __syncthreads();
+}
+
+// G[n][k] += sum_t dY[t][n] A[t][k];  gb[n] += sum_t dY[t][n]   (fp32 atomics)
+template <int K, int N>
+__device__ __forceinline__ void mm_grad(const float* dY, const float* A, float* G, float* gb) {
+  for (int i = threadIdx.x; i < N * K; i += 256) {
+    const int n = i / K, k = i - n * K;
+    float acc = 0.f;
+#pragma unroll 4
+    for (int t = 0; t < L; ++t) acc += dY[t * N + n] * A[t * K + k];
+    atomicAdd(G + i, acc);
+  }
+  for (int n = threadIdx.x; n < N; n += 256) {
+    float acc = 0.f;
+    for (int t = 0; t < L; ++t) acc += dY[t * N + n];
+    atomicAdd(gb + n, acc);
+  }
+}
+
+// LayerNorm over 64 features, one wave per token (lane = feature); saves mean / rstd
+__device__ __forceinline__ void layer_norm64(const float* X, const float* g, const float* bta, float* U, float* mu,
+                                             float* rs) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int t = w; t < L; t += 4) {
+    const float x = X[t * D + lane];
+    const float m = wave_sum(x) * (1.f / D);
+    const float d = x - m;
+    const float r = rsqrtf(wave_sum(d * d) * (1.f / D) + kEps);
+    U[t * D + lane] = d * r * g[lane] + bta[lane];
+    if (lane == 0) {
+      mu[t] = m;
+      rs[t] = r;
+    }
+  }
+  __syncthreads();
+}
+
+// dX[t] += LN backward of dU (through the affine): xhat = (X - mu) rs;  also the affine gradients
+__device__ __forceinline__ void layer_norm64_bwd(const float* X, const float* mu, const float* rs, const float* g,
+                                                 const float* dU, float* dX, float* gw, float* gb) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float aw = 0.f, ab = 0.f;
+  for (int t = w; t < L; t += 4) {
+    const float xh = (X[t * D + lane] - mu[t]) * rs[t];
+    const float du = dU[t * D + lane];
+    aw += du * xh;
+    ab += du;
+    const float gx = du * g[lane];
+    const float m1 = wave_sum(gx) * (1.f / D);
+    const float m2 = wave_sum(gx * xh) * (1.f / D);
+    dX[t * D + lane] += rs[t] * (gx - m1 - xh * m2);
+  }
+  atomicAdd(gw + lane, aw);
+  atomicAdd(gb + lane, ab);
+  __syncthreads();
+}
+
+struct Smem {
+  float X[L * D], U[L * D], QKV[L * QD], O[L * 16], H1[L * HID], P[NH * L * L], T[L * D], mu[L], rs[L];
+  float wb[HID * (D + 1)];
+};
+
+template <typename WT>
+__global__ __launch_bounds__(256) void bo_fwd_kernel(const void* __restrict__ bo, const void* __restrict__ loc, int idt,
+                                                     BoWeights wts, float* __restrict__ out, float* __restrict__ save,
+                                                     long B) {
+  __shared__ Smem s;
+  const long b = blockIdx.x;
+  const int tid = threadIdx.x;
+  // ---- embedding: relu(b0 + W0[:, action] + W0[:, 174 + t] + sum of W0 columns of the set x / y bits)
+  for (int i = tid; i < L * D; i += 256) {
+    const int t = i / D, n = i - t * D;
+    long a = ld_idx(bo, b * L + t, idt);
+    a = a < 0 ? 0 : (a > NACT - 1 ? NACT - 1 : a);
+    long p = ld_idx(loc, b * L + t, idt);
+    p = p < 0 ? 0 : p;
+    const int lx = static_cast<int>(p % 160);
+    int ly = static_cast<int>(p / 160);
+    ly = ly > 1023 ? 1023 : ly;
+    const int row = n * IN;
+    float pre = ldw<WT>(wts.b0, n) + ldw<WT>(wts.w0, row + static_cast<int>(a)) + ldw<WT>(wts.w0, row + NACT + t);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      if ((lx >> (9 - j)) & 1) pre += ldw<WT>(wts.w0, row + 194 + j);
+      if ((ly >> (9 - j)) & 1) pre += ldw<WT>(wts.w0, row + 204 + j);
+    }
+    s.X[i] = fmaxf(pre, 0.f);
+  }
+  __syncthreads();
+  for (int l = 0; l < NL; ++l) {
+    float* rec = save != nullptr ? save + (b * NL + l) * REC : nullptr;
+    if (rec)
+      for (int i = tid; i < L * D; i += 256) rec[R_XIN + i] = s.X[i];
+    layer_norm64(s.X, wts.ln1w[l], wts.ln1b[l], s.U, s.mu, s.rs);
+    if (rec) {
+      for (int i = tid; i < L * D; i += 256) rec[R_U1 + i] = s.U[i];
+      if (tid < L) {
+        rec[R_MU1 + tid] = s.mu[tid];
+        rec[R_RS1 + tid] = s.rs[tid];
+      }
+    }
+    mm_nt<D, QD, WT>(s.U, wts.wqkv[l], wts.bqkv[l], s.QKV, false, s.wb);
+    // scores and softmax: one thread per (head, query) row
+    if (tid < NH * L) {
+      const int h = tid / L, t = tid - h * L;
+      float sc[L];
+      float m = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < L; ++u) {
+        float acc = 0.f;
+#pragma unroll
+        for (int d = 0; d < HDIM; ++d) acc += s.QKV[t * QD + h * HDIM + d] * s.QKV[u * QD + 16 + h * HDIM + d];
+        sc[u] = acc * kScale;
+        m = fmaxf(m, sc[u]);
+      }
+      float sum = 0.f;
+#pragma unroll
+      for (int u = 0; u < L; ++u) {
+        sc[u] = __expf(sc[u] - m);
+        sum += sc[u];
+      }
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int u = 0; u < L; ++u) s.P[tid * L + u] = sc[u] * inv;
+    }
+    __syncthreads();
+    for (int o = tid; o < L * 16; o += 256) {
+      const int t = o / 16, c = o - t * 16, h = c / HDIM;
+      float acc = 0.f;
+#pragma unroll
+      for (int u = 0; u < L; ++u) acc += s.P[(h * L + t) * L + u] * s.QKV[u * QD + 32 + c];
+      s.O[o] = acc;
+    }
+    __syncthreads();
+    if (rec) {
+      for (int i = tid; i < L * QD; i += 256) rec[R_QKV + i] = s.QKV[i];
+      for (int i = tid; i < NH * L * L; i += 256) rec[R_P + i] = s.P[i];
+      for (int i = tid; i < L * 16; i += 256) rec[R_O + i] = s.O[i];
+    }
+    mm_nt<16, D, WT>(s.O, wts.wp[l], wts.bp[l], s.T, false, s.wb);
+    for (int i = tid; i < L * D; i += 256) {
+      s.X[i] += s.T[i];
+      if (rec) rec[R_XMID + i] = s.X[i];
+    }
+    __syncthreads();
+    layer_norm64(s.X, wts.ln2w[l], wts.ln2b[l], s.U, s.mu, s.rs);
+    if (rec) {
+      for (int i = tid; i < L * D; i += 256) rec[R_U2 + i] = s.U[i];
+      if (tid < L) {
+        rec[R_MU2 + tid] = s.mu[tid];
+        rec[R_RS2 + tid] = s.rs[tid];
+      }
+    }
+    mm_nt<D, HID, WT>(s.U, wts.w1[l], wts.b1[l], s.H1, true, s.wb);
+    mm_nt<HID, D, WT>(s.H1, wts.w2[l], wts.b2[l], s.T, true, s.wb);
+    for (int i = tid; i < L * D; i += 256) {
+      s.X[i] += s.T[i];
+      if (rec) {
+        rec[R_H1 + i] = s.H1[i];
+        rec[R_H1 + L * D + i] = s.H1[L * D + i];
+        rec[R_H2 + i] = s.T[i];
+      }
+    }
+    __syncthreads();
+  }
+  if (tid < D) {
+    float acc = 0.f;
+    for (int t = 0; t < L; ++t) acc += s.X[t * D + tid];
+    out[b * D + tid] = acc * (1.f / L);
+  }
+}
+
+struct SmemB {
+  float dX[L * D], dT[L * D], dH[L * HID], A[L * HID], QKV[L * QD], dQKV[L * QD], P[NH * L * L], dS[NH * L * L],
+      dO[L * 16];
+  float wb[HID * (D + 1)];
+};
+
+template <typename WT>
+__global__ __launch_bounds__(256) void bo_bwd_kernel(const void* __restrict__ bo, const void* __restrict__ loc, int idt,
+                                                     BoWeights wts, const float* __restrict__ save,
+                                                     const float* __restrict__ dmean, float* __restrict__ grad,
+                                                     long B) {
+  __shared__ SmemB s;
+  const long b = blockIdx.x;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < L * D; i += 256) s.dX[i] = dmean[b * D + (i % D)] * (1.f / L);
+  __syncthreads();
+  for (int l = NL - 1; l >= 0; --l) {
+    const float* rec = save + (b * NL + l) * REC;
+    float* gl = grad + G_L0 + l * G_LAYER;
+    // ---- MLP branch: x = xmid + relu(relu(u2 W1^T + b1) W2^T + b2)
+    for (int i = tid; i < L * D; i += 256) s.dT[i] = rec[R_H2 + i] > 0.f ? s.dX[i] : 0.f;   // dH2 (pre-act)
+    for (int i = tid; i < L * HID; i += 256) s.A[i] = rec[R_H1 + i];
+    __syncthreads();
+    mm_grad<HID, D>(s.dT, s.A, gl + G_W2, gl + G_B2);
+    mm_nn<HID, D, WT>(s.dT, wts.w2[l], s.dH, s.wb);
+    for (int i = tid; i < L * HID; i += 256) s.dH[i] = s.A[i] > 0.f ? s.dH[i] : 0.f;         // dH1 (pre-act)
+    __syncthreads();
+    for (int i = tid; i < L * D; i += 256) s.A[i] = rec[R_U2 + i];
+    __syncthreads();
+    mm_grad<D, HID>(s.dH, s.A, gl + G_W1, gl + G_B1);
+    mm_nn<D, HID, WT>(s.dH, wts.w1[l], s.dT, s.wb);                                           // dU2
+    layer_norm64_bwd(rec + R_XMID, rec + R_MU2, rec + R_RS2, wts.ln2w[l], s.dT, s.dX, gl + G_LN2W, gl + G_LN2B);
+    // ---- attention branch: xmid = xin + (softmax(q k^T / sqrt 8) v) Wp^T + bp
+    for (int i = tid; i < L * 16; i += 256) s.A[i] = rec[R_O + i];
+    for (int i = tid; i < L * QD; i += 256) s.QKV[i] = rec[R_QKV + i];
+    for (int i = tid; i < NH * L * L; i += 256) s.P[i] = rec[R_P + i];
+    __syncthreads();
+    mm_grad<16, D>(s.dX, s.A, gl + G_WP, gl + G_BP);
+    mm_nn<16, D, WT>(s.dX, wts.wp[l], s.dO, s.wb);
+    for (int i = tid; i < NH * L * L; i += 256) {          // dP[h][t][u] = dO[t][h] . V[u][h]
+      const int h = i / (L * L), t = (i / L) % L, u = i % L;
+      float acc = 0.f;
+#pragma unroll
+      for (int d = 0; d < HDIM; ++d) acc += s.dO[t * 16 + h * HDIM + d] * s.QKV[u * QD + 32 + h * HDIM + d];
+      s.dS[i] = acc;
+    }
+    __syncthreads();
+    if (tid < NH * L) {                                     // dS = P (dP - sum_u P dP), per row
+      float dot = 0.f;
+      for (int u = 0; u < L; ++u) dot += s.P[tid * L + u] * s.dS[tid * L + u];
+      for (int u = 0; u < L; ++u) s.dS[tid * L + u] = s.P[tid * L + u] * (s.dS[tid * L + u] - dot);
+    }
+    __syncthreads();
+    for (int o = tid; o < L * QD; o += 256) {
+      const int t = o / QD, c = o - t * QD;
+      const int part = c / 16, hc = c - part * 16, h = hc / HDIM;
+      float acc = 0.f;
+      if (part == 0) {          // dQ[t] = scale sum_u dS[h][t][u] K[u]
+#pragma unroll
+        for (int u = 0; u < L; ++u) acc += s.dS[(h * L + t) * L + u] * s.QKV[u * QD + 16 + hc];
+        acc *= kScale;
+      } else if (part == 1) {   // dK[t] = scale sum_q dS[h][q][t] Q[q]
+#pragma unroll
+        for (int q = 0; q < L; ++q) acc += s.dS[(h * L + q) * L + t] * s.QKV[q * QD + hc];
+        acc *= kScale;
+      } else {                  // dV[t] = sum_q P[h][q][t] dO[q]
+#pragma unroll
+        for (int q = 0; q < L; ++q) acc += s.P[(h * L + q) * L + t] * s.dO[q * 16 + hc];
+      }
+      s.dQKV[o] = acc;
+    }
+    for (int i = tid; i < L * D; i += 256) s.A[i] = rec[R_U1 + i];
+    __syncthreads();
+    mm_grad<D, QD>(s.dQKV, s.A, gl + G_WQKV, gl + G_BQKV);
+    mm_nn<D, QD, WT>(s.dQKV, wts.wqkv[l], s.dT, s.wb);                                        // dU1
+    layer_norm64_bwd(rec + R_XIN, rec + R_MU1, rec + R_RS1, wts.ln1w[l], s.dT, s.dX, gl + G_LN1W, gl + G_LN1B);
+  }
+  // ---- embedding: x0 = relu(pre); pre = b0 + sum of the selected W0 columns
+  const float* rec0 = save + (b * NL) * REC;
+  for (int i = tid; i < L * D; i += 256) {
+    const int t = i / D, n = i - t * D;
+    if (!(rec0[R_XIN + i] > 0.f)) continue;
+    const float g = s.dX[i];
+    long a = ld_idx(bo, b * L + t, idt);
+    a = a < 0 ? 0 : (a > NACT - 1 ? NACT - 1 : a);
+    long p = ld_idx(loc, b * L + t, idt);
+    p = p < 0 ? 0 : p;
+    const int lx = static_cast<int>(p % 160);
+    int ly = static_cast<int>(p / 160);
+    ly = ly > 1023 ? 1023 : ly;
+    float* gw = grad + G_W0 + n * IN;
+    atomicAdd(grad + G_B0 + n, g);
+    atomicAdd(gw + a, g);
+    atomicAdd(gw + NACT + t, g);
+    for (int j = 0; j < 10; ++j) {
+      if ((lx >> (9 - j)) & 1) atomicAdd(gw + 194 + j, g);
+      if ((ly >> (9 - j)) & 1) atomicAdd(gw + 204 + j, g);
+    }
+  }
+}
+
+}  // namespace
+
+void bo_encoder_fwd(const void* bo, const void* loc, int idt, const BoWeights& w, int wdt, float* out, float* save,
+                    long B, hipStream_t st) {
+  if (B == 0) return;
+  if (wdt == DT_BF16)
+    hipLaunchKernelGGL(bo_fwd_kernel<bf16_t>, dim3(static_cast<unsigned>(B)), dim3(256), 0, st, bo, loc, idt, w, out,
+                       save, B);
+  else
+    hipLaunchKernelGGL(bo_fwd_kernel<float>, dim3(static_cast<unsigned>(B)), dim3(256), 0, st, bo, loc, idt, w, out,
+                       save, B);
+}
+
+void bo_encoder_bwd(const void* bo, const void* loc, int idt, const BoWeights& w, int wdt, const float* save,
+                    const float* dmean, float* grad, long B, hipStream_t st) {
+  if (B == 0) return;
+  if (wdt == DT_BF16)
+    hipLaunchKernelGGL(bo_bwd_kernel<bf16_t>, dim3(static_cast<unsigned>(B)), dim3(256), 0, st, bo, loc, idt, w, save,
+                       dmean, grad, B);
+  else
+    hipLaunchKernelGGL(bo_bwd_kernel<float>, dim3(static_cast<unsigned>(B)), dim3(256), 0, st, bo, loc, idt, w, save,
+                       dmean, grad, B);
+}
+
+}  // namespace as

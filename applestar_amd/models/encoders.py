@@ -48,7 +48,38 @@ class BeginningBuildOrderEncoder(nn.Module):
         self.order_one_hot = OneHotTable(eye_table(BEGINNING_ORDER_LENGTH))
         self.location_binary = OneHotTable(binary_table(binary_dim))
 
+    def fused_params(self):
+        """Parameters in the order of the fused kernel (csrc/kernels/bo_encoder.hip)."""
+        t = self.transformer
+        ps = [t.embedding[0].weight, t.embedding[0].bias]
+        for layer in t.layers:
+            a = layer.attention
+            ps += [layer.layernorm1.weight, layer.layernorm1.bias, a.attention_pre[0].weight, a.attention_pre[0].bias,
+                   a.project[0].weight, a.project[0].bias, layer.layernorm2.weight, layer.layernorm2.bias,
+                   layer.mlp[0][0].weight, layer.mlp[0][0].bias, layer.mlp[1][0].weight, layer.mlp[1][0].bias]
+        return ps
+
+    def _fusable(self, bo) -> bool:
+        if not bo.is_cuda or bo.shape[1] != BEGINNING_ORDER_LENGTH or not FUSED_BO:
+            return False
+        n = ops._native(bo)
+        if n is None or not n.has('bo_encoder'):
+            return False
+        ps = self.fused_params()
+        lin = ps[0].dtype
+        return lin in (torch.float32, torch.bfloat16) and all(
+            p.is_contiguous() and p.dtype == (torch.float32 if i >= 2 and (i - 2) % 12 in (0, 1, 6, 7) else lin)
+            for i, p in enumerate(ps))
+
     def forward(self, bo: torch.Tensor, bo_location: torch.Tensor) -> torch.Tensor:
+        if self._fusable(bo):
+            from ..ops import native
+            mean = native.bo_encoder(bo, bo_location, self.fused_params())          # fp32 [B, 64]
+            return self.embedd_fc(mean)
+        return self.forward_torch(bo, bo_location)
+
+    def forward_torch(self, bo: torch.Tensor, bo_location: torch.Tensor) -> torch.Tensor:
+        """The op-by-op path (CPU, and the reference the fused kernel is tested against)."""
         B, L = bo.shape
         dev = bo.device
         act = F.one_hot(bo.long().clamp(0, self.action_dim - 1), self.action_dim).float()
@@ -59,6 +90,10 @@ class BeginningBuildOrderEncoder(nn.Module):
         x = torch.cat([act, pos, lx, ly], dim=2)
         x = self.transformer.forward_dense(x)
         return self.embedd_fc(x.mean(dim=1))
+
+
+# fused build-order transformer kernel on the GPU (tools/ab_bench / APPLESTAR_FUSED_BO=0 for the op-by-op path)
+FUSED_BO = __import__('os').environ.get('APPLESTAR_FUSED_BO', '1') == '1'
 
 
 # (name, kind, in_dim/num, out_dim, scalar_context, baseline_feature) in reference module order

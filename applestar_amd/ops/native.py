@@ -22,7 +22,7 @@ def ensure_loaded():
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
-                'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats'}
+                'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder'}
 
 
 def has(name: str) -> bool:
@@ -757,3 +757,44 @@ def head_stats(logits, teacher, actions):
     a = actions.reshape(-1).long().contiguous()
     logp_a, ent, kl = _HeadStats.apply(l2, t2, a)
     return logp_a.view(lead), ent.view(lead), kl.view(lead)
+
+
+# ---------------------------------------------------------------------------- fused build-order transformer
+class _BOEncoder(torch.autograd.Function):
+    """Embedding + 3 pre-LN layers + token mean of the beginning-build-order encoder in one kernel per
+    direction (bo_encoder.hip); parameter gradients accumulated in one fp32 buffer, then cast into the
+    parameters' dtypes with one multi-tensor copy."""
+
+    @staticmethod
+    def forward(ctx, bo, loc, *params):
+        out, rec = _C.bo_encoder_fwd(bo, loc, list(params), True)
+        ctx.save_for_backward(bo, loc, rec, *params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dmean):
+        bo, loc, rec, *params = ctx.saved_tensors
+        flat = _C.bo_encoder_bwd(bo, loc, list(params), rec, dmean.float().contiguous())
+        grads, srcs, off = [], [], 0
+        for p in params:
+            n = p.numel()
+            src = flat[off:off + n].view(p.shape)
+            grads.append(src if p.dtype == torch.float32 else torch.empty_like(p))
+            srcs.append(src)
+            off += n
+        dst = [g for g, p in zip(grads, params) if p.dtype != torch.float32]
+        if dst:
+            _C.multi_copy(dst, [s for s, p in zip(srcs, params) if p.dtype != torch.float32])
+        return (None, None) + tuple(grads)
+
+
+def bo_encoder(bo, loc, params):
+    """mean over the 20 tokens of the build-order transformer output, fp32 [B, 64] (params: see
+    BeginningBuildOrderEncoder.fused_params)."""
+    if bo.dtype not in (torch.int16, torch.int32, torch.int64):
+        bo = bo.long()
+    if loc.dtype != bo.dtype:
+        loc = loc.to(bo.dtype)
+    if not torch.is_grad_enabled() or not any(p.requires_grad for p in params):
+        return _C.bo_encoder_fwd(bo.contiguous(), loc.contiguous(), list(params), False)[0]
+    return _BOEncoder.apply(bo.contiguous(), loc.contiguous(), *params)

@@ -656,3 +656,44 @@ def test_head_stats_matches_reference(C, ldt, with_teacher):
 
 def R_head_stats(logits, teacher, act):
     return R.head_stats(logits, teacher, act)
+
+
+@pytest.mark.parametrize('wdtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('idx_dtype', [torch.int16, torch.int64])
+def test_bo_encoder_fused_matches_torch(wdtype, idx_dtype):
+    """Fused build-order transformer (one kernel per direction) vs the op-by-op module in fp32:
+    output and every parameter gradient, with bf16 or fp32 linear weights."""
+    from applestar_amd.models.encoders import BeginningBuildOrderEncoder
+    torch.manual_seed(31)
+    enc = BeginningBuildOrderEncoder(64).to(DEV)
+    ref = BeginningBuildOrderEncoder(64).to(DEV)
+    ref.load_state_dict(enc.state_dict())
+    if wdtype == torch.bfloat16:
+        for ps in (enc.fused_params(),):
+            for i, p in enumerate(ps):
+                if not (i >= 2 and (i - 2) % 12 in (0, 1, 6, 7)):
+                    p.data = p.data.to(torch.bfloat16)
+        with torch.no_grad():   # the reference sees the same bf16-rounded values in fp32
+            for pe, pr in zip(enc.fused_params(), ref.fused_params()):
+                pr.copy_(pe.float())
+    B = 97
+    bo = torch.randint(0, 174, (B, 20), device=DEV).to(idx_dtype)
+    loc = torch.randint(0, 152 * 160, (B, 20), device=DEV).to(idx_dtype)
+    bo[5, 3:] = 0
+    assert enc._fusable(bo)
+    n_before = len(enc.fused_params())
+    out = enc(bo, loc)
+    out_ref = ref.forward_torch(bo, loc)
+    scale = out_ref.abs().max().item()
+    tol = 2e-3 if wdtype == torch.float32 else 2e-2
+    assert _err(out, out_ref) < tol * max(1.0, scale), _err(out, out_ref)
+    g = torch.randn_like(out_ref)
+    out.float().backward(g)
+    out_ref.backward(g)
+    for (pe, pr) in zip(enc.parameters(), ref.parameters()):
+        if pr.grad is None:
+            continue
+        assert pe.grad is not None and pe.grad.dtype == pe.dtype
+        s = pr.grad.abs().max().item()
+        assert _err(pe.grad, pr.grad) < tol * max(1e-3, s), (pe.shape, _err(pe.grad, pr.grad), s)
+    assert n_before == 38
