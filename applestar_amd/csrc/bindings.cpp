@@ -750,6 +750,109 @@ at::Tensor bo_encoder_bwd(const at::Tensor& bo, const at::Tensor& loc, const std
   return grad;
 }
 
+// ---------------------------------------------------------------- residual MLP stack (value baseline)
+// params: per block w1, b1, w2, b2 (bf16 [256,256] / [256]), ln weight, ln bias (fp32 [256])
+namespace {
+as::ResMlpW resmlp_weights(const std::vector<at::Tensor>& p, int* nblk) {
+  TORCH_CHECK(p.size() % 6 == 0 && p.size() / 6 >= 1 && p.size() / 6 <= as::kResMax, "resmlp: 6 tensors per block");
+  const int n = static_cast<int>(p.size() / 6);
+  as::ResMlpW w{};
+  for (int k = 0; k < n; ++k) {
+    for (int j = 0; j < 4; ++j) {
+      const at::Tensor& t = p[6 * k + j];
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kBFloat16 &&
+                      t.numel() == ((j % 2) == 0 ? 256 * 256 : 256),
+                  "resmlp: bf16 contiguous fc weights [256,256] / biases [256]");
+    }
+    for (int j = 4; j < 6; ++j) {
+      const at::Tensor& t = p[6 * k + j];
+      TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == at::kFloat && t.numel() == 256,
+                  "resmlp: fp32 LayerNorm affine [256]");
+    }
+    w.w1[k] = p[6 * k].data_ptr();
+    w.b1[k] = p[6 * k + 1].data_ptr();
+    w.w2[k] = p[6 * k + 2].data_ptr();
+    w.b2[k] = p[6 * k + 3].data_ptr();
+    w.g[k] = p[6 * k + 4].data_ptr<float>();
+    w.be[k] = p[6 * k + 5].data_ptr<float>();
+  }
+  *nblk = n;
+  return w;
+}
+}  // namespace
+
+// x0 [R, 256] fp32 / bf16 -> (out fp32 [R, 256], sv_x, sv_h, sv_xhat, sv_rstd) (saved tensors undefined if !save)
+std::vector<at::Tensor> resmlp_fwd(const at::Tensor& x0, const std::vector<at::Tensor>& params, bool save) {
+  check_cuda(x0, "x0");
+  TORCH_CHECK(x0.dim() == 2 && x0.size(1) == 256 && x0.is_contiguous() &&
+                  (x0.scalar_type() == at::kFloat || x0.scalar_type() == at::kBFloat16),
+              "resmlp: x0 [R, 256] fp32 / bf16 contiguous");
+  int n = 0;
+  const as::ResMlpW w = resmlp_weights(params, &n);
+  const int64_t R = x0.size(0);
+  c10::hip::HIPGuard g(x0.device().index());
+  auto f32 = x0.options().dtype(at::kFloat), b16 = x0.options().dtype(at::kBFloat16);
+  auto out = at::empty({R, 256}, f32);
+  at::Tensor sx, sh, sxh, srs;
+  if (save) {
+    sx = at::empty({n, R, 256}, b16);
+    sh = at::empty({n, R, 256}, b16);
+    sxh = at::empty({n, R, 256}, f32);
+    srs = at::empty({n, R}, f32);
+  }
+  as::resmlp_fwd(x0.data_ptr(), dt(x0), w, n, out.data_ptr<float>(),
+                 save ? reinterpret_cast<uint16_t*>(sx.data_ptr()) : nullptr,
+                 save ? reinterpret_cast<uint16_t*>(sh.data_ptr()) : nullptr, save ? sxh.data_ptr<float>() : nullptr,
+                 save ? srs.data_ptr<float>() : nullptr, R, stream());
+  return {out, sx, sh, sxh, srs};
+}
+
+// -> (dx0 fp32 [R, 256], weight grads fp32 [2n, 256*256 + 256] (W1_k | b1_k, W2_k | b2_k), LN grads fp32 [n, 512])
+std::vector<at::Tensor> resmlp_bwd(const at::Tensor& dout, const std::vector<at::Tensor>& params, const at::Tensor& sx,
+                                   const at::Tensor& sh, const at::Tensor& sxh, const at::Tensor& srs) {
+  check_cuda(dout, "dout");
+  int n = 0;
+  as::ResMlpW w = resmlp_weights(params, &n);
+  const int64_t R = dout.size(0);
+  TORCH_CHECK(dout.scalar_type() == at::kFloat && dout.is_contiguous() && dout.numel() == R * 256,
+              "resmlp_bwd: dout fp32 [R, 256]");
+  TORCH_CHECK(sx.numel() == n * R * 256 && sh.numel() == n * R * 256 && sxh.numel() == n * R * 256 && srs.numel() == n * R,
+              "resmlp_bwd: saved tensors");
+  c10::hip::HIPGuard g(dout.device().index());
+  auto f32 = dout.options(), b16 = dout.options().dtype(at::kBFloat16);
+  auto wt = at::empty({2 * n, 256, 256}, b16);
+  as::resmlp_transpose(w, n, reinterpret_cast<uint16_t*>(wt.data_ptr()), stream());
+  for (int k = 0; k < n; ++k) {
+    w.w1t[k] = static_cast<const uint16_t*>(wt.data_ptr()) + (2L * k) * 65536;
+    w.w2t[k] = static_cast<const uint16_t*>(wt.data_ptr()) + (2L * k + 1) * 65536;
+  }
+  auto dy = at::empty({n, R, 256}, b16), dh = at::empty({n, R, 256}, b16);
+  const int nrb = as::resmlp_row_blocks(R);
+  auto part = at::empty({nrb, n * 512}, f32);
+  auto dx0 = at::empty({R, 256}, f32);
+  as::resmlp_bwd(dout.data_ptr<float>(), w, n, reinterpret_cast<const uint16_t*>(sh.data_ptr()), sxh.data_ptr<float>(),
+                 srs.data_ptr<float>(), reinterpret_cast<uint16_t*>(dy.data_ptr()),
+                 reinterpret_cast<uint16_t*>(dh.data_ptr()), part.data_ptr<float>(), dx0.data_ptr<float>(), R, stream());
+  const int64_t stride = 65536 + 256;
+  auto gw = at::empty({2 * n, stride}, f32);
+  as::WgBatch P;
+  for (int k = 0; k < n; ++k) {
+    const long o = static_cast<long>(k) * R * 256;
+    P.dy[2 * k] = static_cast<const uint16_t*>(dh.data_ptr()) + o;       // W1_k: dH^T x_in
+    P.x[2 * k] = static_cast<const uint16_t*>(sx.data_ptr()) + o;
+    P.dy[2 * k + 1] = static_cast<const uint16_t*>(dy.data_ptr()) + o;   // W2_k: dY^T h
+    P.x[2 * k + 1] = static_cast<const uint16_t*>(sh.data_ptr()) + o;
+    for (int j = 0; j < 2; ++j) {
+      P.dw[2 * k + j] = gw.data_ptr<float>() + (2 * k + j) * stride;
+      P.db[2 * k + j] = gw.data_ptr<float>() + (2 * k + j) * stride + 65536;
+    }
+  }
+  as::wgrad_batched(P, 2 * n, 0, R, 256, 256, 1, 1, 0, 1, stream());
+  auto gln = at::empty({n, 512}, f32);
+  as::column_reduce(part.data_ptr<float>(), gln.data_ptr<float>(), nrb, n * 512, stream());
+  return {dx0, gw, gln};
+}
+
 // ---------------------------------------------------------------- fused categorical head statistics
 // logits [R, C] fp32/bf16, teacher [R, C] fp32/bf16 (optional), action [R] int64
 // -> out [3, R] fp32 (logp_a, entropy, KL(teacher || logits)), stats [R, 6] fp32
@@ -921,6 +1024,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_split_error", &lstm_split_error);
   m.def("multi_copy", &multi_copy);
   m.def("head_stats_fwd", &head_stats_fwd);
+  m.def("resmlp_fwd", &resmlp_fwd);
+  m.def("resmlp_bwd", &resmlp_bwd);
   m.def("bo_encoder_fwd", &bo_encoder_fwd);
   m.def("bo_encoder_bwd", &bo_encoder_bwd);
   m.def("head_stats_bwd", &head_stats_bwd);

@@ -198,6 +198,16 @@ void act_grad_nhwc(const void* dout, int dt, bool dout_nchw, const void* out, vo
 // partial slice s of dW at dw_part + s * part_stride, of db at db_part + s * part_stride
 void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
            int H, int W, int Cin, int S, hipStream_t st);
+// the same for nb <= kWgMaxBatch independent problems of one shape in one launch (grid.y = problem)
+constexpr int kWgMaxBatch = 32;
+struct WgBatch {
+  const void* dy[kWgMaxBatch];
+  const void* x[kWgMaxBatch];
+  float* dw[kWgMaxBatch];
+  float* db[kWgMaxBatch];
+};
+void wgrad_batched(const WgBatch& P, int nb, long part_stride, long R, int N, int K, int H, int W, int Cin, int S,
+                   hipStream_t st);
 
 // ---- bo_encoder.hip ----------------------------------------------------------------------------
 // fused beginning-build-order transformer (20 tokens, 3 pre-LN layers); weights bf16 or fp32 (wdt),
@@ -225,6 +235,31 @@ void bo_encoder_fwd(const void* bo, const void* loc, int idt, const BoWeights& w
 // grad [kBoGradSize] fp32 (zeroed by the caller) += parameter gradients for dmean [B, 64]
 void bo_encoder_bwd(const void* bo, const void* loc, int idt, const BoWeights& w, int wdt, const float* save,
                     const float* dmean, float* grad, long B, hipStream_t st);
+
+// ---- resmlp.hip -------------------------------------------------------------------------------
+// n <= kResMax x ResFCBlock2(256): x <- LN(fc2(relu(fc1(x))) + x); linear weights / biases bf16, LN fp32
+constexpr int kResMax = 16;
+struct ResMlpW {
+  const void* w1[kResMax];
+  const void* b1[kResMax];
+  const void* w2[kResMax];
+  const void* b2[kResMax];
+  const float* g[kResMax];
+  const float* be[kResMax];
+  const void* w1t[kResMax];   // backward: W1^T, W2^T (resmlp_transpose)
+  const void* w2t[kResMax];
+};
+// out [R, 256] fp32; saved (nullable sv_x): sv_x / sv_h bf16 [n, R, 256], sv_xhat fp32 [n, R, 256], sv_rstd [n, R]
+void resmlp_fwd(const void* x0, int x0_dt, const ResMlpW& w, int nblk, float* out, uint16_t* sv_x, uint16_t* sv_h,
+                float* sv_xhat, float* sv_rstd, long R, hipStream_t s);
+// dst [2 n, 256, 256]: W1_0^T, W2_0^T, W1_1^T, ...
+void resmlp_transpose(const ResMlpW& w, int nblk, uint16_t* dst, hipStream_t s);
+int resmlp_row_blocks(long R);
+// dx0 [R, 256] fp32; sv_dy / sv_dh bf16 [n, R, 256] (for the batched weight gradient);
+// ln_part [row_blocks, n, 512] fp32 per-workgroup (dgamma | dbeta) partials
+void resmlp_bwd(const float* dout, const ResMlpW& w, int nblk, const uint16_t* sv_h, const float* sv_xhat,
+                const float* sv_rstd, uint16_t* sv_dy, uint16_t* sv_dh, float* ln_part, float* dx0, long R,
+                hipStream_t s);
 
 // ---- loss.hip ----------------------------------------------------------------------------------
 // per row of logits l [R, C] (+ teacher t [R, C], may be null) and action a [R]:

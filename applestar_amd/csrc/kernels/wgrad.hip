@@ -67,11 +67,14 @@ __device__ __forceinline__ bf8v tr_frag(const bf16_t* tile, int pitch, int col0,
 }
 
 template <int BN, int BK, bool CONV>
-__global__ __launch_bounds__(256) void wgrad_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
-                                                    float* __restrict__ dw_part, float* __restrict__ db_part,
-                                                    long part_stride, long R, int N, int K, int H, int W, int Cin, long rows_per_split,
-                                                    int tiles_n, int tiles_k) {
+__global__ __launch_bounds__(256) void wgrad_kernel(const WgBatch P, long part_stride, long R, int N, int K, int H,
+                                                    int W, int Cin, long rows_per_split, int tiles_n, int tiles_k) {
   using C = WgCfg<BN, BK>;
+  // blockIdx.y selects one of a batch of independent problems of the same shape (one per launch otherwise)
+  const bf16_t* __restrict__ dy = static_cast<const bf16_t*>(P.dy[blockIdx.y]);
+  const bf16_t* __restrict__ x = static_cast<const bf16_t*>(P.x[blockIdx.y]);
+  float* __restrict__ dw_part = P.dw[blockIdx.y];
+  float* __restrict__ db_part = P.db[blockIdx.y];
   __shared__ __attribute__((aligned(16))) bf16_t smem[C::SMEM / 2];
 
   // XCD-aware remap: consecutive logical ids (the N x K tiles of one row slice, which read the same dY / X
@@ -228,12 +231,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const bf16_t* __restrict__ d
 }
 
 template <int BN, int BK, bool CONV>
-void launch(const bf16_t* dy, const bf16_t* x, float* dw, float* db, long ps, long R, int N, int K, int H, int W, int Cin,
-            int S, long rps, hipStream_t st) {
+void launch(const WgBatch& P, int nb, long ps, long R, int N, int K, int H, int W, int Cin, int S, long rps,
+            hipStream_t st) {
   const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
   const long nwg = static_cast<long>(tn) * tk * S;
-  hipLaunchKernelGGL((wgrad_kernel<BN, BK, CONV>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x, dw, db,
-                     ps, R, N, K, H, W, Cin, rps, tn, tk);
+  hipLaunchKernelGGL((wgrad_kernel<BN, BK, CONV>), dim3(static_cast<unsigned>(nwg), static_cast<unsigned>(nb)),
+                     dim3(256), 0, st, P, ps, R, N, K, H, W, Cin, rps, tn, tk);
 }
 
 }  // namespace
@@ -268,24 +271,33 @@ int wgrad_splits(long R, int N, int K) {
   return static_cast<int>(S);
 }
 
-void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
-           int H, int W, int Cin, int S, hipStream_t st) {
+void wgrad_batched(const WgBatch& P, int nb, long part_stride, long R, int N, int K, int H, int W, int Cin, int S,
+                   hipStream_t st) {
+  if (nb <= 0) return;
   long rps = (R + S - 1) / S;
   rps = (rps + 63) / 64 * 64;
-  const bf16_t* d = static_cast<const bf16_t*>(dy);
-  const bf16_t* xp = static_cast<const bf16_t*>(x);
   const bool conv = Cin > 0;
   const int bn = pick_bn(N), bk = pick_bk(K);
 #define AS_WG(BNv, BKv)                                                                              \
   if (bn == BNv && bk == BKv) {                                                                      \
-    if (conv) launch<BNv, BKv, true>(d, xp, dw_part, db_part, part_stride, R, N, K, H, W, Cin, S, rps, st);       \
-    else launch<BNv, BKv, false>(d, xp, dw_part, db_part, part_stride, R, N, K, H, W, Cin, S, rps, st);           \
+    if (conv) launch<BNv, BKv, true>(P, nb, part_stride, R, N, K, H, W, Cin, S, rps, st);            \
+    else launch<BNv, BKv, false>(P, nb, part_stride, R, N, K, H, W, Cin, S, rps, st);                \
     return;                                                                                          \
   }
   AS_WG(128, 128) AS_WG(128, 96) AS_WG(128, 64)
   AS_WG(64, 128) AS_WG(64, 96) AS_WG(64, 64)
   AS_WG(32, 128) AS_WG(32, 96) AS_WG(32, 64)
 #undef AS_WG
+}
+
+void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
+           int H, int W, int Cin, int S, hipStream_t st) {
+  WgBatch P;
+  P.dy[0] = dy;
+  P.x[0] = x;
+  P.dw[0] = dw_part;
+  P.db[0] = db_part;
+  wgrad_batched(P, 1, part_stride, R, N, K, H, W, Cin, S, st);
 }
 
 }  // namespace as

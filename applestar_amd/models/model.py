@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import ops
 from ..lib import game_data as gd
 from ..lib.features import MAX_SELECTED_UNITS_NUM, ACTION_HEADS
 from ..utils.config import AttrDict, deep_merge_dicts
@@ -45,6 +46,8 @@ DEFAULT_MODEL_CONFIG = AttrDict({
 _SIDE_STREAMS: Dict[tuple, 'torch.cuda.Stream'] = {}
 SIDE_STREAMS_ENABLED = True
 CRITIC_SIDE_STREAM = False   # tools/ab_bench.py --variant critic_side: no gain (+1.9 ms, noisy)
+# value baselines' ResFCBlock2 stack as the fused resmlp kernels on the GPU (APPLESTAR_FUSED_RESMLP=0: op by op)
+FUSED_RESMLP = __import__('os').environ.get('APPLESTAR_FUSED_RESMLP', '1') == '1'
 
 
 _DEVICE_TABLES: Dict[tuple, torch.Tensor] = {}
@@ -100,8 +103,30 @@ class ValueBaseline(nn.Module):
         self.value_fc = FCBlock(res_dim, 1, init='xavier_uniform', gain=0.1)
         self.atan = atan
 
+    def fused_params(self):
+        """ResFCBlock2 parameters in the fused kernel's order (csrc/kernels/resmlp.hip)."""
+        ps = []
+        for blk in self.res:
+            ps += [blk.fc1[0].weight, blk.fc1[0].bias, blk.fc2[0].weight, blk.fc2[0].bias, blk.norm.weight, blk.norm.bias]
+        return ps
+
+    def _fusable(self, x) -> bool:
+        if not (x.is_cuda and FUSED_RESMLP and self.res_dim == 256 and 1 <= self.res_num <= 16):
+            return False
+        n = ops._native(x)
+        if n is None or not n.has('resmlp'):
+            return False
+        return all(p.is_contiguous() and p.dtype == (torch.float32 if i % 6 >= 4 else torch.bfloat16)
+                   for i, p in enumerate(self.fused_params()))
+
     def forward(self, x):
-        v = self.value_fc(self.res(self.project(x))).squeeze(1).float()
+        h = self.project(x)
+        if self._fusable(h):
+            from ..ops import native
+            h = native.resmlp(h.reshape(-1, self.res_dim), self.fused_params()).view(*h.shape[:-1], self.res_dim)
+        else:
+            h = self.res(h)
+        v = self.value_fc(h).squeeze(1).float()
         if self.atan:
             v = (2.0 / torch.pi) * torch.atan((torch.pi / 2.0) * v)
         return v

@@ -22,7 +22,7 @@ def ensure_loaded():
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
-                'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder'}
+                'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp'}
 
 
 def has(name: str) -> bool:
@@ -798,3 +798,47 @@ def bo_encoder(bo, loc, params):
     if not torch.is_grad_enabled() or not any(p.requires_grad for p in params):
         return _C.bo_encoder_fwd(bo.contiguous(), loc.contiguous(), list(params), False)[0]
     return _BOEncoder.apply(bo.contiguous(), loc.contiguous(), *params)
+
+
+# ---------------------------------------------------------------------------- residual MLP stack (value baseline)
+class _ResMLP(torch.autograd.Function):
+    """n x ResFCBlock2(256) in one forward kernel; backward = weight transpose + one data-gradient kernel +
+    one batched MFMA weight-gradient launch + one LayerNorm-affine reduction (resmlp.hip)."""
+
+    @staticmethod
+    def forward(ctx, x0, *params):
+        out, sx, sh, sxh, srs = _C.resmlp_fwd(x0, list(params), True)
+        ctx.save_for_backward(sx, sh, sxh, srs, *params)
+        ctx.x_dtype = x0.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        sx, sh, sxh, srs, *params = ctx.saved_tensors
+        dx0, gw, gln = _C.resmlp_bwd(dout.float().contiguous(), list(params), sx, sh, sxh, srs)
+        n = len(params) // 6
+        grads, dst, src = [], [], []
+        for k in range(n):
+            w1, b1, w2, b2 = params[6 * k:6 * k + 4]
+            for j, (w, b) in enumerate(((w1, b1), (w2, b2))):
+                row = gw[2 * k + j]
+                for p, flat in ((w, row[:65536]), (b, row[65536:])):
+                    g = torch.empty_like(p)
+                    dst.append(g)
+                    src.append(flat.view(p.shape))
+                    grads.append(g)
+            grads.append(gln[k, :256])
+            grads.append(gln[k, 256:])
+        _C.multi_copy(dst, src)
+        # reorder to the params order (w1, b1, w2, b2, ln_w, ln_b)
+        dx = dx0 if ctx.x_dtype == torch.float32 else dx0.to(ctx.x_dtype)
+        return (dx,) + tuple(grads)
+
+
+def resmlp(x0, params):
+    """x0 [R, 256] -> fp32 [R, 256] through n ResFCBlock2 blocks (params: 6 per block)."""
+    x0 = x0 if x0.dtype in (torch.float32, torch.bfloat16) else x0.float()
+    x0 = x0.contiguous()
+    if not torch.is_grad_enabled() or not (x0.requires_grad or any(p.requires_grad for p in params)):
+        return _C.resmlp_fwd(x0, list(params), False)[0]
+    return _ResMLP.apply(x0, *params)

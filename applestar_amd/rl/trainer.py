@@ -161,6 +161,21 @@ class RLTrainer:
         self.iter += 1
         return info
 
+    def nonfinite_grads(self):
+        """Names of parameters whose current gradient has a NaN / Inf (debugging aid; syncs)."""
+        bad = []
+        if self.master is not None:
+            views = self.master._master_grad_views()
+            for p in self.master.reducer.params:
+                g = views.get(p, p.grad)
+                if g is not None and not bool(torch.isfinite(g).all()):
+                    bad.append(self.master.names[p])
+        else:
+            for n, p in self.model.named_parameters():
+                if p.grad is not None and not bool(torch.isfinite(p.grad).all()):
+                    bad.append(n)
+        return bad
+
     def model_state_dict(self):
         """fp32 model weights (the master copies when the compute weights are bf16)."""
         return self.master.state_dict() if self.master is not None else self.model.state_dict()

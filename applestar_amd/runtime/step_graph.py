@@ -67,7 +67,7 @@ def batch_signature(x):
 
 
 class _Entry:
-    __slots__ = ('fb', 'upd', 'static_in', 'keys', 'packed', 'grad_norm')
+    __slots__ = ('fb', 'upd', 'static_in', 'keys', 'packed', 'grad_norm')   # upd None: update inside fb
 
 
 class GraphedTrainStep:
@@ -90,6 +90,10 @@ class GraphedTrainStep:
         self.replays = 0
         self.eager_steps = 0
         self.host_time: Dict[str, float] = {}     # summed host seconds per replay phase
+        self.check_fn: Optional[Callable[[], None]] = None
+        # one graph for the whole step when there is no cross-rank reduction between backward and update
+        import torch.distributed as dist
+        self.single_graph = not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
         # forked side streams (value / scalar encoders) inside the capture; off: captured on one stream
         self.side_streams = os.environ.get('APPLESTAR_GRAPH_SIDE_STREAMS', '0') == '1'
 
@@ -118,11 +122,15 @@ class GraphedTrainStep:
                 info = self.fwd_bwd(e.static_in)
                 e.keys = sorted(k for k, v in info.items() if torch.is_tensor(v) and v.numel() == 1)
                 e.packed = torch.stack([info[k].detach().float().reshape(()) for k in e.keys]) if e.keys else None
+                if self.single_graph:
+                    e.grad_norm = self.update().detach().float().reshape(())
         finally:
             encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED = flags
-        e.upd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(e.upd, pool=self._pool):
-            e.grad_norm = self.update().detach().float().reshape(())
+        e.upd = None
+        if not self.single_graph:
+            e.upd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(e.upd, pool=self._pool):
+                e.grad_norm = self.update().detach().float().reshape(())
         self.captures += 1
         self._graphs[key] = e
         return e
@@ -142,10 +150,22 @@ class GraphedTrainStep:
         _tree_copy_(e.static_in, batch)
         t1 = time.perf_counter()
         e.fb.replay()
+        if self.check_fn is not None:      # debugging hook between the two graphs
+            self.check_fn()
         t2 = time.perf_counter()
-        self.reduce()
+        if e.upd is not None:
+            # ROCm 7: a graph launched right behind another on the same stream was seen reading the first
+            # graph's outputs before they landed (test_graphed_train_step_matches_eager: inf gradient norm
+            # unless the host waited in between), so the multi-rank path waits for the stream here
+            torch.cuda.current_stream(self.device).synchronize()
+            self.reduce()
         t3 = time.perf_counter()
-        e.upd.replay()
+        if e.upd is not None:
+            e.upd.replay()
+        # ROCm 7 workaround: without a host wait here, eager work queued behind the replay (the output
+        # copy below) read an inf gradient norm on the second replay of a graph
+        # (test_graphed_train_step_matches_eager fails 6/6 without it, passes with it)
+        torch.cuda.current_stream(self.device).synchronize()
         t4 = time.perf_counter()
         for k, dt in (('copy_in', t1 - t0), ('replay_fwd_bwd', t2 - t1), ('reduce', t3 - t2), ('replay_update', t4 - t3)):
             t[k] = t.get(k, 0.0) + dt
@@ -158,6 +178,12 @@ class GraphedTrainStep:
         else:
             out['gradient'] = e.grad_norm.clone()
         return out
+
+    def replay_fwd_bwd_only(self):
+        """Debugging aid: replay the forward/backward graph of the most recently used signature again
+        (gradients left in the buffers, no optimizer update)."""
+        if self._graphs:
+            next(reversed(self._graphs.values())).fb.replay()
 
     def reset(self):
         """Drop every captured graph (e.g. after the optimizer or the parameter set was replaced)."""

@@ -225,7 +225,13 @@ def test_graphed_train_step_matches_eager():
         ig = graphed.step(dict(b))
         for k in ('total_loss', 'gradient'):
             a, r = float(ig[k]), float(ie[k])
-            assert abs(a - r) <= 2e-2 * max(1.0, abs(r)), (i, k, a, r)
+            if not abs(a - r) <= 2e-2 * max(1.0, abs(r)):
+                graphed.graph.replay_fwd_bwd_only()
+                torch.cuda.synchronize()
+                from applestar_amd.ops import native
+                lstm_err = int(native.ensure_loaded().lstm_split_error(0).item())
+                raise AssertionError((i, k, a, r, 'non-finite after a fwd/bwd replay:', graphed.nonfinite_grads()[:8],
+                                      'lstm split timeout flag', lstm_err))
     torch.cuda.synchronize()
     assert graphed.graph.captures == 2 and graphed.graph.replays == 3 and graphed.graph.eager_steps == 2
     de, dg = eager.master.master.detach() - m0, graphed.master.master.detach() - m0
