@@ -639,6 +639,14 @@ std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t
   }
   // one [S, N*K (+ N)] partial buffer: dW and db of a slice side by side, reduced by ONE column pass
   const int64_t NK = N * K, stride = NK + (want_bias ? N : 0);
+  if (bf16_out && S == 1) {   // one slice: the kernel writes the final bf16 gradient (no reduce / cast pass)
+    auto flat = at::empty({stride}, dy.options());
+    as::wgrad(dy.data_ptr(), x.data_ptr(), reinterpret_cast<float*>(flat.data_ptr()),
+              want_bias ? reinterpret_cast<float*>(static_cast<at::BFloat16*>(flat.data_ptr()) + NK) : nullptr, 0, R,
+              static_cast<int>(N), static_cast<int>(K), static_cast<int>(H), static_cast<int>(W), static_cast<int>(cin),
+              1, stream(), true);
+    return {flat.narrow(0, 0, NK).view({N, K}), want_bias ? flat.narrow(0, NK, N) : at::Tensor()};
+  }
   auto part = at::empty({S, stride}, opts);
   // debug: poison the partials so any slot the kernel leaves unwritten shows up as NaN on every run
   static const bool nan_fill = [] {
@@ -744,9 +752,12 @@ at::Tensor bo_encoder_bwd(const at::Tensor& bo, const at::Tensor& loc, const std
   int wdt = 0;
   const as::BoWeights w = bo_weights(params, &wdt);
   c10::hip::HIPGuard g(bo.device().index());
-  auto grad = at::zeros({as::kBoGradSize}, dmean.options());
+  const int reps = static_cast<int>(std::min<int64_t>(B, 32));
+  auto rep = at::zeros({reps, as::kBoGradSize}, dmean.options());
   as::bo_encoder_bwd(bo.data_ptr(), loc.data_ptr(), idx_code(bo), w, wdt, save.data_ptr<float>(),
-                     dmean.data_ptr<float>(), grad.data_ptr<float>(), B, stream());
+                     dmean.data_ptr<float>(), rep.data_ptr<float>(), B, reps, stream());
+  auto grad = at::empty({as::kBoGradSize}, dmean.options());
+  as::column_reduce(rep.data_ptr<float>(), grad.data_ptr<float>(), reps, as::kBoGradSize, stream());
   return grad;
 }
 

@@ -196,8 +196,9 @@ void pointwise_conv(const void* x, const float* w, const float* bias, void* y, l
 void act_grad_nhwc(const void* dout, int dt, bool dout_nchw, const void* out, void* dpre, int B, int C, int HW, int relu,
                    hipStream_t s);
 // partial slice s of dW at dw_part + s * part_stride, of db at db_part + s * part_stride
+// out_bf16 with S == 1: dw_part / db_part are bf16 buffers receiving the final gradient (cast fused)
 void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
-           int H, int W, int Cin, int S, hipStream_t st);
+           int H, int W, int Cin, int S, hipStream_t st, bool out_bf16 = false);
 // the same for nb <= kWgMaxBatch independent problems of one shape in one launch (grid.y = problem)
 constexpr int kWgMaxBatch = 32;
 struct WgBatch {
@@ -207,7 +208,7 @@ struct WgBatch {
   float* db[kWgMaxBatch];
 };
 void wgrad_batched(const WgBatch& P, int nb, long part_stride, long R, int N, int K, int H, int W, int Cin, int S,
-                   hipStream_t st);
+                   hipStream_t st, bool out_bf16 = false);
 
 // ---- bo_encoder.hip ----------------------------------------------------------------------------
 // fused beginning-build-order transformer (20 tokens, 3 pre-LN layers); weights bf16 or fp32 (wdt),
@@ -232,9 +233,10 @@ struct BoWeights {
 // out [B, 64] fp32 = mean over tokens of the transformer output; save [B, 3, kBoRecord] (nullable)
 void bo_encoder_fwd(const void* bo, const void* loc, int idt, const BoWeights& w, int wdt, float* out, float* save,
                     long B, hipStream_t st);
-// grad [kBoGradSize] fp32 (zeroed by the caller) += parameter gradients for dmean [B, 64]
+// grad [replicas, kBoGradSize] fp32 (zeroed by the caller; observation b adds into replica b % replicas)
+// += parameter gradients for dmean [B, 64]; the caller sums the replicas
 void bo_encoder_bwd(const void* bo, const void* loc, int idt, const BoWeights& w, int wdt, const float* save,
-                    const float* dmean, float* grad, long B, hipStream_t st);
+                    const float* dmean, float* grad, long B, int replicas, hipStream_t st);
 
 // ---- resmlp.hip -------------------------------------------------------------------------------
 // n <= kResMax x ResFCBlock2(256): x <- LN(fc2(relu(fc1(x))) + x); linear weights / biases bf16, LN fp32

@@ -68,7 +68,8 @@ __device__ __forceinline__ bf8v tr_frag(const bf16_t* tile, int pitch, int col0,
 
 template <int BN, int BK, bool CONV>
 __global__ __launch_bounds__(256) void wgrad_kernel(const WgBatch P, long part_stride, long R, int N, int K, int H,
-                                                    int W, int Cin, long rows_per_split, int tiles_n, int tiles_k) {
+                                                    int W, int Cin, long rows_per_split, int tiles_n, int tiles_k,
+                                                    int out_bf16) {
   using C = WgCfg<BN, BK>;
   // blockIdx.y selects one of a batch of independent problems of the same shape (one per launch otherwise)
   const bf16_t* __restrict__ dy = static_cast<const bf16_t*>(P.dy[blockIdx.y]);
@@ -205,7 +206,9 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgBatch P, long part_s
   }
 
   // epilogue: fp32 partial tile; lane (g, i) of fragment (a, b) holds C[n = 16a + 4g + e][k = 16b + i]
+  // out_bf16 (single slice only): the final dW / db in bf16, the cast fused here instead of a pass
   float* outp = dw_part + static_cast<long>(s) * part_stride;
+  bf16_t* outb = reinterpret_cast<bf16_t*>(dw_part);
   const int lr = lane & 15, lg = lane >> 4;
 #pragma unroll
   for (int i = 0; i < C::FN; ++i)
@@ -215,7 +218,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgBatch P, long part_s
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int n = n0 + wn * C::TN + 16 * i + 4 * lg + e;
-        if (n < N && k < K) outp[static_cast<long>(n) * K + k] = acc[i][j][e];
+        if (n < N && k < K) {
+          if (out_bf16) outb[static_cast<long>(n) * K + k] = f2bf(acc[i][j][e]);
+          else outp[static_cast<long>(n) * K + k] = acc[i][j][e];
+        }
       }
     }
   if (do_bias) {
@@ -225,18 +231,21 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgBatch P, long part_s
       v += __shfl_xor(v, 16, kWave);
       v += __shfl_xor(v, 32, kWave);
       const int n = n0 + wn * C::TN + 16 * i + lr;
-      if (lg == 0 && n < N) db_part[static_cast<long>(s) * part_stride + n] = v;
+      if (lg == 0 && n < N) {
+        if (out_bf16) reinterpret_cast<bf16_t*>(db_part)[n] = f2bf(v);
+        else db_part[static_cast<long>(s) * part_stride + n] = v;
+      }
     }
   }
 }
 
 template <int BN, int BK, bool CONV>
 void launch(const WgBatch& P, int nb, long ps, long R, int N, int K, int H, int W, int Cin, int S, long rps,
-            hipStream_t st) {
+            int out_bf16, hipStream_t st) {
   const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
   const long nwg = static_cast<long>(tn) * tk * S;
   hipLaunchKernelGGL((wgrad_kernel<BN, BK, CONV>), dim3(static_cast<unsigned>(nwg), static_cast<unsigned>(nb)),
-                     dim3(256), 0, st, P, ps, R, N, K, H, W, Cin, rps, tn, tk);
+                     dim3(256), 0, st, P, ps, R, N, K, H, W, Cin, rps, tn, tk, out_bf16);
 }
 
 }  // namespace
@@ -272,7 +281,8 @@ int wgrad_splits(long R, int N, int K) {
 }
 
 void wgrad_batched(const WgBatch& P, int nb, long part_stride, long R, int N, int K, int H, int W, int Cin, int S,
-                   hipStream_t st) {
+                   hipStream_t st, bool out_bf16) {
+  const int ob = (out_bf16 && S == 1) ? 1 : 0;
   if (nb <= 0) return;
   long rps = (R + S - 1) / S;
   rps = (rps + 63) / 64 * 64;
@@ -280,8 +290,8 @@ void wgrad_batched(const WgBatch& P, int nb, long part_stride, long R, int N, in
   const int bn = pick_bn(N), bk = pick_bk(K);
 #define AS_WG(BNv, BKv)                                                                              \
   if (bn == BNv && bk == BKv) {                                                                      \
-    if (conv) launch<BNv, BKv, true>(P, nb, part_stride, R, N, K, H, W, Cin, S, rps, st);            \
-    else launch<BNv, BKv, false>(P, nb, part_stride, R, N, K, H, W, Cin, S, rps, st);                \
+    if (conv) launch<BNv, BKv, true>(P, nb, part_stride, R, N, K, H, W, Cin, S, rps, ob, st);        \
+    else launch<BNv, BKv, false>(P, nb, part_stride, R, N, K, H, W, Cin, S, rps, ob, st);            \
     return;                                                                                          \
   }
   AS_WG(128, 128) AS_WG(128, 96) AS_WG(128, 64)
@@ -291,13 +301,13 @@ void wgrad_batched(const WgBatch& P, int nb, long part_stride, long R, int N, in
 }
 
 void wgrad(const void* dy, const void* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
-           int H, int W, int Cin, int S, hipStream_t st) {
+           int H, int W, int Cin, int S, hipStream_t st, bool out_bf16) {
   WgBatch P;
   P.dy[0] = dy;
   P.x[0] = x;
   P.dw[0] = dw_part;
   P.db[0] = db_part;
-  wgrad_batched(P, 1, part_stride, R, N, K, H, W, Cin, S, st);
+  wgrad_batched(P, 1, part_stride, R, N, K, H, W, Cin, S, st, out_bf16);
 }
 
 }  // namespace as
