@@ -19,6 +19,8 @@
 // 16-B coalesced rows (+bias +residual, ReLU, bf16).  Workgroup ids are remapped so consecutive
 // M-tiles (which share input halo rows) run on one XCD's L2.
 // The input gradient of a conv is the same operation on dy with the flipped, transposed weight.
+#include <cstdlib>
+
 #include "../common.h"
 #include "../kernels.h"
 
@@ -239,6 +241,239 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Halo-window variant for narrow maps (W <= 40, Cin % 64 == 0): the implicit GEMM above gathers every
+// input pixel once per tap (9x the image through LDS, and its LDS stores plus fragment reads saturate
+// the LDS port before the MFMAs do).  Here a 128-pixel tile's input is staged ONCE per 64-channel
+// chunk as a window of 128 + 2W + 2 consecutive pixel rows (the tile plus one image row and one pixel
+// of halo on each side); every tap then reads its A fragments from that window at a constant row
+// offset dy*W + dx and zeroes the rows whose neighbour falls outside the image (per-lane 9-bit masks).
+// Only the weight tile is re-staged per (tap, chunk) step, double-buffered through registers.
+template <int BN, int WP>
+struct HaloCfg {
+  static constexpr int BM = 128, CK = 64, NT = 256;
+  static constexpr int WN = BN >= 128 ? 2 : 1, WM = 4 / WN;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int FM = TM / 16, FN = TN / 16;
+  static constexpr int P = CK + 8;                 // LDS row pitch (bf16): conflict-free ds_read_b128 groups
+  static constexpr int NR = WP * NT / 8;           // window rows covered by WP 16-B pieces per thread
+  static constexpr int B_IT = BN * (CK / 8) / NT;  // weight pieces per thread
+  static constexpr int WIN = NR * P, BT = BN * P;  // bf16 elements
+  static constexpr int MAIN = (WIN + 2 * BT) * 2;  // bytes
+  static constexpr int CPAD = BN + 4;
+  static constexpr int SMEM = MAIN > BM * CPAD * 4 ? MAIN : BM * CPAD * 4;
+  static_assert(B_IT * NT == BN * (CK / 8), "weight tile pieces");
+};
+
+template <int BN, int WP>
+__global__ __launch_bounds__(256) void conv3x3_halo_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ w,
+                                                           const float* __restrict__ bias,
+                                                           const bf16_t* __restrict__ res, bf16_t* __restrict__ out,
+                                                           int B, int H, int W, int Cin, int Cout, int act) {
+  using C = HaloCfg<BN, WP>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[C::SMEM];
+  bf16_t* win = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* bts = win + C::WIN;
+
+  const int HW = H * W;
+  const long M = static_cast<long>(B) * HW;
+  const int K = 9 * Cin;
+  const int ntn = (Cout + BN - 1) / BN;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int tn = wg % ntn;
+  const long m0 = static_cast<long>(wg / ntn) * C::BM;
+  const int n0 = tn * BN;
+  const long wb0 = m0 - (W + 1);                    // window row 0 <-> pixel wb0
+  const int nrows = C::BM + 2 * W + 2;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int lr = lane & 15, lg = lane >> 4;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(x), 0, static_cast<int>(M * Cin * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(w), 0, static_cast<int>(static_cast<long>(Cout) * K * 2), 0x00020000);
+  constexpr int kOOB = 0x7ffffff0;
+
+  // 9-bit in-image masks of this lane's A-fragment rows (pixel wm*TM + 16 i + lr of the tile)
+  int ok9[C::FM];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i) {
+    const long m = m0 + wm * C::TM + 16 * i + lr;
+    ok9[i] = 0;
+    if (m < M) {
+      const int rem = static_cast<int>(m % HW);
+      const int yy = rem / W, xx = rem - yy * W;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int y2 = yy + t / 3 - 1, x2 = xx + t % 3 - 1;
+        ok9[i] |= (y2 >= 0 && y2 < H && x2 >= 0 && x2 < W) << t;
+      }
+    }
+  }
+
+  uint4 rw[WP], rb[C::B_IT];
+  auto load_win = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < WP; ++i) {
+      const int piece = tid + i * C::NT;
+      const int row = piece >> 3, ch = (piece & 7) * 8;
+      const long pix = wb0 + row;
+      const int off = (row < nrows && pix >= 0 && pix < M) ? static_cast<int>((pix * Cin + c0 + ch) * 2) : kOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      rw[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store_win = [&]() {
+#pragma unroll
+    for (int i = 0; i < WP; ++i) {
+      const int piece = tid + i * C::NT;
+      const int row = piece >> 3, ch = (piece & 7) * 8;
+      if (row < nrows) *reinterpret_cast<uint4*>(win + row * C::P + ch) = rw[i];
+    }
+  };
+  auto load_b = [&](int step) {
+    const int tap = step % 9, c0 = (step / 9) * C::CK;
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const int piece = tid + i * C::NT;
+      const int n = piece >> 3, ch = (piece & 7) * 8;
+      const int off = n0 + n < Cout ? ((n0 + n) * K + tap * Cin + c0 + ch) * 2 : kOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0);
+      rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store_b = [&](int buf) {
+    bf16_t* Bs = bts + buf * C::BT;
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const int piece = tid + i * C::NT;
+      const int n = piece >> 3, ch = (piece & 7) * 8;
+      *reinterpret_cast<uint4*>(Bs + n * C::P + ch) = rb[i];
+    }
+  };
+
+  f4 acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = 9 * (Cin / C::CK);
+  load_win(0);
+  load_b(0);
+  store_win();
+  store_b(0);
+  __syncthreads();
+  for (int step = 0; step < nsteps; ++step) {
+    const int cur = step & 1;
+    const int tap = step % 9;
+    const bool next = step + 1 < nsteps;
+    const bool new_chunk = next && (step + 1) % 9 == 0;
+    if (next) load_b(step + 1);
+    if (new_chunk) load_win(((step + 1) / 9) * C::CK);
+    const int shift = (W + 1) + (tap / 3 - 1) * W + (tap % 3 - 1);
+    const bf16_t* Bs = bts + cur * C::BT;
+#pragma unroll
+    for (int ks = 0; ks < C::CK / 32; ++ks) {
+      bf8v af[C::FM], bfr[C::FN];
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const int row = wm * C::TM + 16 * i + lr + shift;
+        uint4 u = *reinterpret_cast<const uint4*>(win + row * C::P + ks * 32 + 8 * lg);
+        if (!((ok9[i] >> tap) & 1)) u = make_uint4(0, 0, 0, 0);
+        af[i] = as_bf8(u);
+      }
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+        bfr[j] = as_bf8(*reinterpret_cast<const uint4*>(Bs + (wn * C::TN + 16 * j + lr) * C::P + ks * 32 + 8 * lg));
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (new_chunk) {
+      __syncthreads();           // every wave is done reading the old window
+      store_win();
+    }
+    if (next) store_b(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue (as conv3x3_kernel): fp32 tile in LDS -> 16-B rows with bias / residual / activation
+  float* cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        cs[(wm * C::TM + i * 16 + 4 * lg + e) * C::CPAD + wn * C::TN + j * 16 + lr] = acc[i][j][e];
+  __syncthreads();
+  constexpr int CPR = BN / 8;
+  for (int idx = tid; idx < C::BM * CPR; idx += C::NT) {
+    const int rr = idx / CPR, c8 = idx % CPR;
+    const long m = m0 + rr;
+    const int n = n0 + 8 * c8;
+    if (m >= M || n >= Cout) continue;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = cs[rr * C::CPAD + 8 * c8 + e] + (bias ? bias[n + e] : 0.f);
+    const long o = m * Cout + n;
+    if (res) {
+      const uint4 u = *reinterpret_cast<const uint4*>(res + o);
+      const uint32_t q4[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[2 * e] += __uint_as_float(q4[e] << 16);
+        v[2 * e + 1] += __uint_as_float(q4[e] & 0xffff0000u);
+      }
+    }
+    if (act == ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    uint4 u;
+    u.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
+    u.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
+    u.z = static_cast<uint32_t>(f2bf(v[4])) | (static_cast<uint32_t>(f2bf(v[5])) << 16);
+    u.w = static_cast<uint32_t>(f2bf(v[6])) | (static_cast<uint32_t>(f2bf(v[7])) << 16);
+    *reinterpret_cast<uint4*>(out + o) = u;
+  }
+}
+
+template <int BN, int WP>
+void launch_halo(const bf16_t* x, const bf16_t* w, const float* bias, const bf16_t* res, bf16_t* out, int B, int H,
+                 int W, int Cin, int Cout, int act, hipStream_t s) {
+  const long M = static_cast<long>(B) * H * W;
+  const long nwg = (M + 127) / 128 * ((Cout + BN - 1) / BN);
+  if (nwg == 0) return;
+  hipLaunchKernelGGL((conv3x3_halo_kernel<BN, WP>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias, res,
+                     out, B, H, W, Cin, Cout, act);
+}
+
+// window pieces per thread for a map width: (128 + 2W + 2) rows x 8 pieces over 256 threads
+bool halo_pieces(int W, int* wp) {
+  const int need = ((128 + 2 * W + 2) * 8 + 255) / 256;
+  if (need <= 6) *wp = 6;
+  else if (need <= 8) *wp = 8;
+  else return false;
+  return true;
+}
+
+bool use_halo(int W, int Cin, int Cout) {
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_CONV_HALO");
+    return e == nullptr || e[0] != '0';
+  }();
+  int wp = 0;
+  return on && Cin % 64 == 0 && (Cout % 128 == 0 || Cout == 64) && halo_pieces(W, &wp);
+}
+
 template <int BN, int BK, bool SPLIT_TAP = false>
 void launch(const bf16_t* x, const bf16_t* w, const float* bias, const bf16_t* res, bf16_t* out, int B, int H, int W,
             int Cin, int Cout, int act, hipStream_t s) {
@@ -265,6 +500,18 @@ void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* re
   const bf16_t* rp = static_cast<const bf16_t*>(res);
   bf16_t* op = static_cast<bf16_t*>(out);
   const bool k64 = Cin % 64 == 0;
+  if (use_halo(W, Cin, Cout)) {        // narrow maps: halo window staged once per channel chunk
+    int npc = 0;
+    halo_pieces(W, &npc);
+    if (Cout % 128 == 0) {
+      if (npc == 6) launch_halo<128, 6>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+      else launch_halo<128, 8>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    } else {
+      if (npc == 6) launch_halo<64, 6>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+      else launch_halo<64, 8>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    }
+    return;
+  }
   if (Cin == 16) {                     // K-steps straddle taps
     if (Cout % 128 == 0) launch<128, 32, true>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
     else if (Cout == 64) launch<64, 32, true>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
