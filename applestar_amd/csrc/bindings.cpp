@@ -340,16 +340,33 @@ std::vector<at::Tensor> spatial_embed_fwd(const std::vector<at::Tensor>& planes,
   TORCH_CHECK(ex.scalar_type() == at::kByte && ey.scalar_type() == at::kByte && entity_num.scalar_type() == at::kLong,
               "entity x/y uint8, entity_num int64");
   c10::hip::HIPGuard g(rows.device().index());
-  auto bits = at::zeros({B, HW}, planes[0].options());
-  as::spatial_effect_bits(sp, bits.data_ptr<uint8_t>(), B, L, HW, stream());
-  auto pre = at::empty({B, H, W, 32}, rows.options().dtype(at::kFloat));
-  as::spatial_dense(sp, bits.data_ptr<uint8_t>(), w_dense.data_ptr<float>(), bias.data_ptr<float>(), pre.data_ptr<float>(),
-                    B * HW, stream());
-  as::scatter_add_rows(rows.data_ptr(), dt(rows), ex.data_ptr<uint8_t>(), ey.data_ptr<uint8_t>(),
-                       entity_num.data_ptr<int64_t>(), pre.data_ptr<float>(), B, rows.size(1), H, W, stream());
+  TORCH_CHECK(rows.is_contiguous() && ex.is_contiguous() && ey.is_contiguous() && entity_num.is_contiguous(),
+              "spatial: contiguous rows / entity coordinates");
   auto out = at::empty({B, H, W, 32}, rows.options().dtype(out_dtype == 1 ? at::kBFloat16 : at::kFloat));
-  as::relu_cast(pre.data_ptr<float>(), out.data_ptr(), dt(out), pre.numel(), stream());
-  return {bits, out};
+  as::spatial_embed_fused(sp, w_dense.data_ptr<float>(), bias.data_ptr<float>(), rows.data_ptr(), dt(rows),
+                          ex.data_ptr<uint8_t>(), ey.data_ptr<uint8_t>(), entity_num.data_ptr<int64_t>(),
+                          out.data_ptr(), dt(out), static_cast<int>(B), static_cast<int>(rows.size(1)),
+                          static_cast<int>(H), static_cast<int>(W), static_cast<int>(L), stream());
+  return {at::Tensor(), out};
+}
+
+// (dWd fp32 [32, 24], db fp32 [32]) of the spatial 1x1 projection's dense columns from dpre [B,H,W,32]
+std::vector<at::Tensor> spatial_dense_wgrad(const std::vector<at::Tensor>& planes, const std::vector<at::Tensor>& effects,
+                                            const at::Tensor& dpre) {
+  auto sp = make_planes(planes, effects);
+  const int64_t B = planes[0].size(0), H = planes[0].size(1), W = planes[0].size(2);
+  const int64_t L = effects[0].size(1);
+  check_cuda(dpre, "dpre");
+  TORCH_CHECK(dpre.is_contiguous() && dpre.numel() == B * H * W * 32, "spatial_dense_wgrad: dpre [B,H,W,32] contiguous");
+  c10::hip::HIPGuard g(dpre.device().index());
+  const int nb = as::spatial_wgrad_blocks(static_cast<int>(B));
+  auto f32 = dpre.options().dtype(at::kFloat);
+  auto part = at::empty({nb, 32 * 24 + 32}, f32);
+  as::spatial_dense_wgrad(sp, dpre.data_ptr(), dt(dpre), part.data_ptr<float>(), static_cast<int>(B),
+                          static_cast<int>(H), static_cast<int>(W), static_cast<int>(L), stream());
+  auto red = at::empty({32 * 24 + 32}, f32);
+  as::column_reduce(part.data_ptr<float>(), red.data_ptr<float>(), nb, 32 * 24 + 32, stream());
+  return {red.narrow(0, 0, 32 * 24).view({32, 24}), red.narrow(0, 32 * 24, 32)};
 }
 
 at::Tensor spatial_gather_rows(const at::Tensor& dpre, const at::Tensor& ex, const at::Tensor& ey,
@@ -1016,6 +1033,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spatial_embed_fwd", &spatial_embed_fwd);
   m.def("spatial_gather_rows", &spatial_gather_rows);
   m.def("spatial_dense_input", &spatial_dense_input);
+  m.def("spatial_dense_wgrad", &spatial_dense_wgrad);
   m.def("varlen_attn_fwd", &varlen_attn_fwd);
   m.def("varlen_attn_bwd", &varlen_attn_bwd);
   m.def("su_sample", &su_sample);

@@ -103,6 +103,14 @@ void scatter_add_rows(const void* rows, int dt, const uint8_t* ex, const uint8_t
 void gather_rows(const void* dpre, int dt, const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num,
                  void* drows, int B, int N, int H, int W, hipStream_t s);
 void relu_cast(const float* x, void* y, int dt, long n, hipStream_t s);
+// fused: out [B,H,W,32] = relu(bias + Wd . dense(pixel) + sum of the rows of entities at the pixel)
+void spatial_embed_fused(const SpatialPlanes& sp, const float* wd, const float* bias, const void* rows, int rows_dt,
+                         const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num, void* out, int out_dt, int B,
+                         int N, int H, int W, int L, hipStream_t s);
+// per-workgroup partial rows [spatial_wgrad_blocks(B)][32*24 + 32] of dWd (n-major) and db from dpre [B*H*W, 32]
+int spatial_wgrad_blocks(int B);
+void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, int dt, float* part, int B, int H, int W, int L,
+                         hipStream_t s);
 
 // ---- attention.hip ---------------------------------------------------------------------------
 // Packed varlen MHA, head dim 128, bf16. qkv [T][3][H][128], cu [S+1] int32, out [T][H][128],

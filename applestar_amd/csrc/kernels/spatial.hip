@@ -230,6 +230,154 @@ __global__ __launch_bounds__(256) void spatial_dense_input_kernel(SpatialPlanes 
   }
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Fused spatial input (forward): one workgroup owns a tile of 256 consecutive pixels of ONE
+// observation.  It marks the tile's effect points in LDS, computes every pixel's 24 dense columns
+// (height, 6 one-hot planes, effect bits) against the 1x1 weight into an fp32 LDS tile, adds the
+// pre-projected rows of the observation's entities that fall inside the tile (LDS float atomics), and
+// writes relu(tile) once in the output dtype with 16-B stores.  Replaces effect_bits + spatial_dense
+// (one fp32 [npix, 32] round trip, 128-B strided stores per thread) + scatter_add_rows + relu_cast.
+constexpr int kSpTile = 256;
+
+template <typename TR, typename TO>
+__global__ __launch_bounds__(256) void spatial_embed_fused_kernel(SpatialPlanes sp, const float* __restrict__ wd,
+                                                                  const float* __restrict__ bias,
+                                                                  const TR* __restrict__ rows,
+                                                                  const uint8_t* __restrict__ ex,
+                                                                  const uint8_t* __restrict__ ey,
+                                                                  const int64_t* __restrict__ entity_num,
+                                                                  TO* __restrict__ out, int N, int H, int W, int L,
+                                                                  int tiles) {
+  __shared__ float acc[kSpTile][33];
+  __shared__ float w_s[24][32];
+  __shared__ float b_s[32];
+  __shared__ uint32_t eb[kSpTile];
+  const int HW = H * W;
+  const int b = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int p0 = tile * kSpTile, tid = threadIdx.x;
+  const int np = HW - p0 < kSpTile ? HW - p0 : kSpTile;
+  for (int i = tid; i < 24 * 32; i += 256) w_s[i % 24][i / 24] = wd[(i / 24) * 24 + (i % 24)];
+  if (tid < 32) b_s[tid] = bias[tid];
+  eb[tid] = 0;
+  __syncthreads();
+  for (int i = tid; i < 6 * L; i += 256) {
+    const int e = i / L, j = i - e * L;
+    int p = sp.effect[e][static_cast<long>(b) * L + j];
+    p = p < 0 ? 0 : (p >= HW ? HW - 1 : p);
+    if (p >= p0 && p < p0 + np) atomicOr(&eb[p - p0], 1u << e);
+  }
+  __syncthreads();
+  if (tid < np) {
+    const long pix = static_cast<long>(b) * HW + p0 + tid;
+    const int widths[6] = {4, 2, 5, 2, 2, 2};
+    float a[32];
+    const float h = static_cast<float>(sp.height[pix]) * (1.f / 256.f);
+#pragma unroll
+    for (int c = 0; c < 32; ++c) a[c] = b_s[c] + w_s[0][c] * h;
+    int off = 1;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      int v = sp.plane[k][pix];
+      v = v < widths[k] ? v : widths[k] - 1;
+#pragma unroll
+      for (int c = 0; c < 32; ++c) a[c] += w_s[off + v][c];
+      off += widths[k];
+    }
+    const uint32_t bits = eb[tid];
+#pragma unroll
+    for (int e = 0; e < 6; ++e)
+      if ((bits >> e) & 1) {
+#pragma unroll
+        for (int c = 0; c < 32; ++c) a[c] += w_s[18 + e][c];
+      }
+#pragma unroll
+    for (int c = 0; c < 32; ++c) acc[tid][c] = a[c];
+  }
+  __syncthreads();
+  // entities of this observation inside the tile: add their 32 pre-projected channels
+  const int ne = static_cast<int>(entity_num[b] < N ? entity_num[b] : N);
+  for (int i = tid; i < ne * 32; i += 256) {
+    const int n = i >> 5, c = i & 31;
+    const long bn = static_cast<long>(b) * N + n;
+    int x = ex[bn], y = ey[bn];
+    x = x < W ? x : W - 1;
+    y = y < H ? y : H - 1;
+    const int p = y * W + x - p0;
+    if (p >= 0 && p < np) atomicAdd(&acc[p][c], Cvt<TR>::load(rows, bn * 32 + c));
+  }
+  __syncthreads();
+  const long o0 = (static_cast<long>(b) * HW + p0) * 32;
+  for (int i = tid; i < np * 32; i += 256) {
+    const int p = i >> 5, c = i & 31;
+    Cvt<TO>::store(out, o0 + i, fmaxf(acc[p][c], 0.f));
+  }
+}
+
+// dW_dense [32][24] and db [32] of the spatial 1x1 projection without materialising the dense input:
+// thread (slot = tid / 32, channel n = tid % 32) accumulates dpre[p][n] * X[p][k] over its pixels in
+// registers (X is height + one-hot + effect bits, so every column update is a select-add); the 8 slots
+// are summed in LDS and each workgroup writes one partial row [32 * 24 + 32] (reduced afterwards).
+template <typename TD>
+__global__ __launch_bounds__(256) void spatial_dense_wgrad_kernel(SpatialPlanes sp, const TD* __restrict__ dpre,
+                                                                  float* __restrict__ part, int H, int W, int L,
+                                                                  int tiles, int wg_per_obs) {
+  __shared__ uint32_t eb[kSpTile];
+  __shared__ float red[8][32][25];
+  const int HW = H * W;
+  const int b = blockIdx.x / wg_per_obs, q = blockIdx.x % wg_per_obs;
+  const int tid = threadIdx.x, n = tid & 31, slot = tid >> 5;
+  float acc[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) acc[k] = 0.f;
+  for (int tile = q; tile < tiles; tile += wg_per_obs) {
+    const int p0 = tile * kSpTile;
+    const int np = HW - p0 < kSpTile ? HW - p0 : kSpTile;
+    __syncthreads();
+    eb[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < 6 * L; i += 256) {
+      const int e = i / L, j = i - e * L;
+      int p = sp.effect[e][static_cast<long>(b) * L + j];
+      p = p < 0 ? 0 : (p >= HW ? HW - 1 : p);
+      if (p >= p0 && p < p0 + np) atomicOr(&eb[p - p0], 1u << e);
+    }
+    __syncthreads();
+    for (int pl = slot; pl < np; pl += 8) {
+      const long pix = static_cast<long>(b) * HW + p0 + pl;
+      const float d = Cvt<TD>::load(dpre, pix * 32 + n);
+      acc[24] += d;
+      acc[0] += d * (static_cast<float>(sp.height[pix]) * (1.f / 256.f));
+      const int widths[6] = {4, 2, 5, 2, 2, 2};
+      int off = 1;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        int v = sp.plane[k][pix];
+        v = v < widths[k] ? v : widths[k] - 1;
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+          if (j < widths[k]) acc[off + j] += (v == j) ? d : 0.f;
+        off += widths[k];
+      }
+      const uint32_t bits = eb[pl];
+#pragma unroll
+      for (int e = 0; e < 6; ++e) acc[18 + e] += ((bits >> e) & 1) ? d : 0.f;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 25; ++k) red[slot][n][k] = acc[k];
+  __syncthreads();
+  float* row = part + static_cast<long>(blockIdx.x) * (32 * 24 + 32);
+  for (int i = tid; i < 32 * 25; i += 256) {
+    const int nn = i / 25, k = i % 25;
+    float s = 0.f;
+#pragma unroll
+    for (int sl = 0; sl < 8; ++sl) s += red[sl][nn][k];
+    if (k < 24) row[nn * 24 + k] = s;
+    else row[32 * 24 + nn] = s;
+  }
+}
+
 int grid_for(long n) {
   long b = (n + 255) / 256;
   return static_cast<int>(b < 1 ? 1 : (b > 8192 ? 8192 : b));
@@ -301,6 +449,36 @@ void gather_rows(const void* dpre, int dt, const uint8_t* ex, const uint8_t* ey,
   else
     hipLaunchKernelGGL(gather_rows_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(dpre), ex, ey,
                        entity_num, static_cast<float*>(drows), B, N, H, W);
+}
+
+void spatial_embed_fused(const SpatialPlanes& sp, const float* wd, const float* bias, const void* rows, int rows_dt,
+                         const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num, void* out, int out_dt, int B,
+                         int N, int H, int W, int L, hipStream_t s) {
+  const int tiles = (H * W + kSpTile - 1) / kSpTile;
+  const dim3 grid(static_cast<unsigned>(B) * tiles);
+  if (B == 0) return;
+#define AS_SP(TR, TO)                                                                                              \
+  hipLaunchKernelGGL((spatial_embed_fused_kernel<TR, TO>), grid, dim3(256), 0, s, sp, wd, bias,                    \
+                     static_cast<const TR*>(rows), ex, ey, entity_num, static_cast<TO*>(out), N, H, W, L, tiles)
+  if (rows_dt == DT_BF16 && out_dt == DT_BF16) AS_SP(bf16_t, bf16_t);
+  else if (rows_dt == DT_BF16) AS_SP(bf16_t, float);
+  else if (out_dt == DT_BF16) AS_SP(float, bf16_t);
+  else AS_SP(float, float);
+#undef AS_SP
+}
+
+int spatial_wgrad_blocks(int B) { return B * 4; }
+
+void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, int dt, float* part, int B, int H, int W, int L,
+                         hipStream_t s) {
+  const int tiles = (H * W + kSpTile - 1) / kSpTile;
+  if (B == 0) return;
+  if (dt == DT_BF16)
+    hipLaunchKernelGGL(spatial_dense_wgrad_kernel<bf16_t>, dim3(static_cast<unsigned>(B) * 4), dim3(256), 0, s, sp,
+                       static_cast<const bf16_t*>(dpre), part, H, W, L, tiles, 4);
+  else
+    hipLaunchKernelGGL(spatial_dense_wgrad_kernel<float>, dim3(static_cast<unsigned>(B) * 4), dim3(256), 0, s, sp,
+                       static_cast<const float*>(dpre), part, H, W, L, tiles, 4);
 }
 
 void relu_cast(const float* x, void* y, int dt, long n, hipStream_t s) {

@@ -233,10 +233,10 @@ class _SpatialEmbed(torch.autograd.Function):
     def forward(ctx, w_dense, bias, rows, ex, ey, entity_num, out_dtype, n_planes, *tensors):
         planes = list(tensors[:n_planes])
         effects = list(tensors[n_planes:])
-        bits, out = _C.spatial_embed_fwd(planes, effects, w_dense.detach().float().contiguous(),
-                                         bias.detach().float(), rows.contiguous(), ex, ey, entity_num,
-                                         _dt_code(out_dtype))
-        ctx.save_for_backward(out, bits, ex, ey, entity_num, *tensors)
+        _, out = _C.spatial_embed_fwd(planes, effects, w_dense.detach().float().contiguous(),
+                                      bias.detach().float(), rows.contiguous(), ex, ey, entity_num,
+                                      _dt_code(out_dtype))
+        ctx.save_for_backward(out, ex, ey, entity_num, *tensors)
         ctx.n_planes = n_planes
         ctx.N = rows.shape[1]
         ctx.rows_dtype = rows.dtype
@@ -244,7 +244,7 @@ class _SpatialEmbed(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
-        out, bits, ex, ey, entity_num, *tensors = ctx.saved_tensors
+        out, ex, ey, entity_num, *tensors = ctx.saved_tensors
         planes, effects = list(tensors[:ctx.n_planes]), list(tensors[ctx.n_planes:])
         lowp = out.dtype == torch.bfloat16
         if lowp:   # one pass: ReLU mask + cast + NHWC
@@ -252,15 +252,8 @@ class _SpatialEmbed(torch.autograd.Function):
         else:
             dpre = (dout * (out > 0)).to(out.dtype).contiguous()                # [B,H,W,32]
         drows = _C.spatial_gather_rows(dpre, ex, ey, entity_num, ctx.N).to(ctx.rows_dtype)
-        X = _C.spatial_dense_input(planes, effects, bits, _dt_code(out.dtype))  # [npix,24]
-        if lowp and X.numel() * 2 < 0x7ffffff0 and dpre.numel() * 2 < 0x7ffffff0:
-            dw, db = _C.wgrad(dpre.view(-1, 32), X.view(-1, 24), 0, True)       # split-R MFMA, bias fused
-            return (dw, db, drows) + (None,) * (5 + len(tensors))
-        B = dpre.shape[0]
-        # K = B*H*W ~ 1e7 is far too deep for one GEMM tile: batch over observations, then sum
-        d3 = dpre.view(B, -1, 32)
-        dw = torch.bmm(d3.transpose(1, 2), X.view(B, -1, 24)).float().sum(0)
-        db = d3.float().sum((0, 1))
+        # dense-column weight gradient straight from dpre and the planes (no [npix, 24] input matrix)
+        dw, db = _C.spatial_dense_wgrad(planes, effects, dpre.contiguous())
         return (dw, db, drows) + (None,) * (5 + len(tensors))
 
 
