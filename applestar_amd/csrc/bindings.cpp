@@ -334,7 +334,6 @@ std::vector<at::Tensor> spatial_embed_fwd(const std::vector<at::Tensor>& planes,
   const int64_t B = planes[0].size(0), H = planes[0].size(1), W = planes[0].size(2), HW = H * W;
   const int64_t L = effects[0].size(1);
   TORCH_CHECK(w_dense.size(0) == 32 && w_dense.size(1) == 24 && w_dense.scalar_type() == at::kFloat, "w_dense [32,24]");
-  TORCH_CHECK((B * HW) % 4 == 0, "spatial: B*H*W % 4");
   check_cuda(rows, "rows");
   TORCH_CHECK(rows.dim() == 3 && rows.size(0) == B && rows.size(2) == 32, "rows [B,N,32]");
   TORCH_CHECK(ex.scalar_type() == at::kByte && ey.scalar_type() == at::kByte && entity_num.scalar_type() == at::kLong,

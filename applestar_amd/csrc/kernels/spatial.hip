@@ -12,6 +12,8 @@
 #include "../common.h"
 #include "../kernels.h"
 
+#include <cstdlib>
+
 namespace as {
 namespace {
 
@@ -378,6 +380,250 @@ __global__ __launch_bounds__(256) void spatial_dense_wgrad_kernel(SpatialPlanes 
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// MFMA forms (bf16 activations).  Every dense column except height is 0 or 1 and height/256 has 8
+// significant bits, so the dense input is EXACT in bf16: a pixel is described by one 25-bit column
+// mask (bit c set <=> X[p][c] = 1; bit 24 is the bias / db column) plus its height as bf16 bits.
+//   forward  pre[p][n] = sum_c X[p][c] Wd'[n][c]  — K = 32 columns = ONE 16x16x32 MFMA step per
+//            16 pixels x 16 channels; Wd' (bias in column 24) is split hi + lo bf16 so the product
+//            keeps ~fp32 accuracy (X exact, hi + lo carries 16 mantissa bits).
+//   backward dWd'[n][c] = sum_p dpre[p][n] X[p][c] — K = pixels: dpre^T is staged in LDS per tile,
+//            the X fragments are expanded from the LDS masks on the fly.
+__device__ __forceinline__ uint32_t pixel_mask(const SpatialPlanes& sp, long pix, uint32_t ebits) {
+  const uint32_t v0 = min(static_cast<uint32_t>(sp.plane[0][pix]), 3u), v1 = min(static_cast<uint32_t>(sp.plane[1][pix]), 1u);
+  const uint32_t v2 = min(static_cast<uint32_t>(sp.plane[2][pix]), 4u), v3 = min(static_cast<uint32_t>(sp.plane[3][pix]), 1u);
+  const uint32_t v4 = min(static_cast<uint32_t>(sp.plane[4][pix]), 1u), v5 = min(static_cast<uint32_t>(sp.plane[5][pix]), 1u);
+  return (2u << v0) | (32u << v1) | (128u << v2) | (4096u << v3) | (16384u << v4) | (65536u << v5) |
+         ((ebits & 63u) << 18) | (1u << 24);
+}
+
+// two bf16 words for columns j, j + 1 of the mask byte m (1.0 = 0x3F80)
+__device__ __forceinline__ uint32_t bit_pair(uint32_t m, int j) {
+  return (((m >> j) & 1u) ? 0x3F80u : 0u) | (((m >> (j + 1)) & 1u) ? 0x3F800000u : 0u);
+}
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf8v;
+typedef __attribute__((ext_vector_type(4))) float f4;
+
+__device__ __forceinline__ bf8v as_frag(uint4 u) {
+  bf8v r;
+  __builtin_memcpy(&r, &u, 16);
+  return r;
+}
+
+// effect points of observation b that fall into [p0, p0 + np) -> eb (LDS, zeroed)
+__device__ __forceinline__ void mark_effects(const SpatialPlanes& sp, uint32_t* eb, int b, int L, int HW, int p0,
+                                             int np) {
+  for (int i = threadIdx.x; i < 6 * L; i += blockDim.x) {
+    const int e = i / L, j = i - e * L;
+    int p = sp.effect[e][static_cast<long>(b) * L + j];
+    p = p < 0 ? 0 : (p >= HW ? HW - 1 : p);
+    if (p >= p0 && p < p0 + np) atomicOr(&eb[p - p0], 1u << e);
+  }
+}
+
+__global__ __launch_bounds__(256) void spatial_embed_mfma_kernel(SpatialPlanes sp, const float* __restrict__ wd,
+                                                                 const float* __restrict__ bias,
+                                                                 const bf16_t* __restrict__ rows,
+                                                                 const uint8_t* __restrict__ ex,
+                                                                 const uint8_t* __restrict__ ey,
+                                                                 const int64_t* __restrict__ entity_num,
+                                                                 bf16_t* __restrict__ out, int N, int H, int W, int L,
+                                                                 int tiles) {
+  __shared__ float acc_s[kSpTile][33];
+  __shared__ uint32_t eb[kSpTile];
+  __shared__ uint32_t msk[kSpTile];
+  __shared__ uint32_t hgt[kSpTile];
+  const int HW = H * W;
+  const int b = blockIdx.x / tiles, tile = blockIdx.x % tiles;
+  const int p0 = tile * kSpTile, tid = threadIdx.x, l = tid & 63, w = tid >> 6, g = l >> 4, lr = l & 15;
+  const int np = HW - p0 < kSpTile ? HW - p0 : kSpTile;
+  eb[tid] = 0;
+  // B fragments: B[c = 8 g + j][n = 16 nt + lr] = Wd'[n][c], hi and lo halves
+  bf8v bhi[2], blo[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = 16 * nt + lr;
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      uint32_t h2 = 0, l2 = 0;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int c = 8 * g + j + t;
+        const float v = c < 24 ? wd[n * 24 + c] : (c == 24 ? bias[n] : 0.f);
+        const bf16_t hi = f2bf(v);
+        const bf16_t lo = f2bf(v - bf2f(hi));
+        h2 |= static_cast<uint32_t>(hi) << (16 * t);
+        l2 |= static_cast<uint32_t>(lo) << (16 * t);
+      }
+      hw[j / 2] = h2;
+      lw[j / 2] = l2;
+    }
+    bhi[nt] = as_frag(make_uint4(hw[0], hw[1], hw[2], hw[3]));
+    blo[nt] = as_frag(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+  }
+  __syncthreads();
+  mark_effects(sp, eb, b, L, HW, p0, np);
+  __syncthreads();
+  if (tid < np) {
+    const long pix = static_cast<long>(b) * HW + p0 + tid;
+    msk[tid] = pixel_mask(sp, pix, eb[tid]);
+    hgt[tid] = f2bf(static_cast<float>(sp.height[pix]) * (1.f / 256.f));
+  } else {
+    msk[tid] = 0;
+    hgt[tid] = 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int pr = 64 * w + 16 * m + lr;  // A row (pixel) of this lane
+    const uint32_t mb = (msk[pr] >> (8 * g)) & 0xFFu;
+    uint32_t q0 = bit_pair(mb, 0);
+    if (g == 0) q0 = (q0 & 0xFFFF0000u) | hgt[pr];
+    const bf8v a = as_frag(make_uint4(q0, bit_pair(mb, 2), bit_pair(mb, 4), bit_pair(mb, 6)));
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      f4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bhi[nt], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, blo[nt], c, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc_s[64 * w + 16 * m + 4 * g + i][16 * nt + lr] = c[i];
+    }
+  }
+  __syncthreads();
+  const int ne = static_cast<int>(entity_num[b] < N ? entity_num[b] : N);
+  for (int i = tid; i < ne * 32; i += 256) {
+    const int n = i >> 5, c = i & 31;
+    const long bn = static_cast<long>(b) * N + n;
+    int x = ex[bn], y = ey[bn];
+    x = x < W ? x : W - 1;
+    y = y < H ? y : H - 1;
+    const int p = y * W + x - p0;
+    if (p >= 0 && p < np) atomicAdd(&acc_s[p][c], bf2f(rows[bn * 32 + c]));
+  }
+  __syncthreads();
+  // relu + bf16, 8 channels (16 B) per store
+  uint4* o = reinterpret_cast<uint4*>(out + (static_cast<long>(b) * HW + p0) * 32);
+  for (int i = tid; i < np * 4; i += 256) {
+    const int p = i >> 2, c8 = 8 * (i & 3);
+    uint32_t q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      q[j] = static_cast<uint32_t>(f2bf(fmaxf(acc_s[p][c8 + 2 * j], 0.f))) |
+             (static_cast<uint32_t>(f2bf(fmaxf(acc_s[p][c8 + 2 * j + 1], 0.f))) << 16);
+    o[i] = make_uint4(q[0], q[1], q[2], q[3]);
+  }
+}
+
+constexpr int kSpP = kSpTile + 8;  // padded bf16 LDS row of the dpre^T image
+
+__global__ __launch_bounds__(256) void spatial_dense_wgrad_mfma_kernel(SpatialPlanes sp, const bf16_t* __restrict__ dpre,
+                                                                       float* __restrict__ part, int H, int W, int L,
+                                                                       int tiles, int wg_per_obs) {
+  __shared__ __attribute__((aligned(16))) bf16_t dT[32 * kSpP];
+  __shared__ __attribute__((aligned(16))) uint32_t msk[kSpTile];
+  __shared__ __attribute__((aligned(16))) uint16_t hgt[kSpTile];
+  __shared__ uint32_t eb[kSpTile];
+  static_assert(sizeof(bf16_t) * 32 * kSpP >= sizeof(float) * 4 * 32 * 33, "reduction image aliases dT");
+  const int HW = H * W;
+  const int b = blockIdx.x / wg_per_obs, q = blockIdx.x % wg_per_obs;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, g = l >> 4, lr = l & 15;
+  f4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  eb[tid] = 0;
+  for (int tile = q; tile < tiles; tile += wg_per_obs) {
+    const int p0 = tile * kSpTile;
+    const int np = HW - p0 < kSpTile ? HW - p0 : kSpTile;
+    __syncthreads();  // previous tile consumed, eb zeroed
+    mark_effects(sp, eb, b, L, HW, p0, np);
+    __syncthreads();
+    const long base = static_cast<long>(b) * HW + p0;
+    if (tid < np) {
+      msk[tid] = pixel_mask(sp, base + tid, eb[tid]);
+      hgt[tid] = f2bf(static_cast<float>(sp.height[base + tid]) * (1.f / 256.f));
+    } else {
+      msk[tid] = 0;
+      hgt[tid] = 0;
+    }
+    {  // dpre^T: thread = (pixel pair, 16-channel half); tail pixels are zero
+      const int pp = 2 * (tid & 127), h16 = 16 * (tid >> 7);
+      uint4 r0[2], r1[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        r0[k] = pp < np ? *reinterpret_cast<const uint4*>(dpre + (base + pp) * 32 + h16 + 8 * k) : make_uint4(0, 0, 0, 0);
+        r1[k] = pp + 1 < np ? *reinterpret_cast<const uint4*>(dpre + (base + pp + 1) * 32 + h16 + 8 * k)
+                            : make_uint4(0, 0, 0, 0);
+      }
+      uint32_t* d32 = reinterpret_cast<uint32_t*>(dT);
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const uint32_t a[4] = {r0[k].x, r0[k].y, r0[k].z, r0[k].w}, c[4] = {r1[k].x, r1[k].y, r1[k].z, r1[k].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = h16 + 8 * k + 2 * j;
+          d32[(n * kSpP + pp) >> 1] = (a[j] & 0xFFFFu) | (c[j] << 16);
+          d32[((n + 1) * kSpP + pp) >> 1] = (a[j] >> 16) | (c[j] & 0xFFFF0000u);
+        }
+      }
+    }
+    __syncthreads();
+    eb[tid] = 0;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int p = 64 * w + 32 * ks + 8 * g;
+      const bf8v a0 = as_frag(*reinterpret_cast<const uint4*>(dT + lr * kSpP + p));
+      const bf8v a1 = as_frag(*reinterpret_cast<const uint4*>(dT + (16 + lr) * kSpP + p));
+      const uint4 m0 = *reinterpret_cast<const uint4*>(msk + p), m1 = *reinterpret_cast<const uint4*>(msk + p + 4);
+      const uint4 hh = *reinterpret_cast<const uint4*>(hgt + p);
+      const uint32_t mm[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+      const uint32_t hw[4] = {hh.x, hh.y, hh.z, hh.w};
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const int c = 16 * ct + lr;
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[j] = (((mm[2 * j] >> c) & 1u) ? 0x3F80u : 0u) | (((mm[2 * j + 1] >> c) & 1u) ? 0x3F800000u : 0u);
+        if (c == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = hw[j];
+        }
+        const bf8v bx = as_frag(make_uint4(v[0], v[1], v[2], v[3]));
+        acc[0][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bx, acc[0][ct], 0, 0, 0);
+        acc[1][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bx, acc[1][ct], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(dT);  // [4 waves][32 n][33]
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(w * 32 + 16 * nt + 4 * g + i) * 33 + 16 * ct + lr] = acc[nt][ct][i];
+  __syncthreads();
+  float* row = part + static_cast<long>(blockIdx.x) * (32 * 24 + 32);
+  for (int i = tid; i < 32 * 25; i += 256) {
+    const int nn = i / 25, k = i % 25;
+    const float s = red[nn * 33 + k] + red[(32 + nn) * 33 + k] + red[(64 + nn) * 33 + k] + red[(96 + nn) * 33 + k];
+    if (k < 24) row[nn * 24 + k] = s;
+    else row[32 * 24 + nn] = s;
+  }
+}
+
+// APPLESTAR_SPATIAL_MFMA=0 selects the scalar fp32 kernels (A/B measurements)
+bool spatial_mfma() {
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_SPATIAL_MFMA");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int grid_for(long n) {
   long b = (n + 255) / 256;
   return static_cast<int>(b < 1 ? 1 : (b > 8192 ? 8192 : b));
@@ -460,7 +706,10 @@ void spatial_embed_fused(const SpatialPlanes& sp, const float* wd, const float* 
 #define AS_SP(TR, TO)                                                                                              \
   hipLaunchKernelGGL((spatial_embed_fused_kernel<TR, TO>), grid, dim3(256), 0, s, sp, wd, bias,                    \
                      static_cast<const TR*>(rows), ex, ey, entity_num, static_cast<TO*>(out), N, H, W, L, tiles)
-  if (rows_dt == DT_BF16 && out_dt == DT_BF16) AS_SP(bf16_t, bf16_t);
+  if (rows_dt == DT_BF16 && out_dt == DT_BF16 && spatial_mfma())
+    hipLaunchKernelGGL(spatial_embed_mfma_kernel, grid, dim3(256), 0, s, sp, wd, bias, static_cast<const bf16_t*>(rows), ex,
+                       ey, entity_num, static_cast<bf16_t*>(out), N, H, W, L, tiles);
+  else if (rows_dt == DT_BF16 && out_dt == DT_BF16) AS_SP(bf16_t, bf16_t);
   else if (rows_dt == DT_BF16) AS_SP(bf16_t, float);
   else if (out_dt == DT_BF16) AS_SP(float, bf16_t);
   else AS_SP(float, float);
@@ -473,7 +722,10 @@ void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, int dt, floa
                          hipStream_t s) {
   const int tiles = (H * W + kSpTile - 1) / kSpTile;
   if (B == 0) return;
-  if (dt == DT_BF16)
+  if (dt == DT_BF16 && spatial_mfma())
+    hipLaunchKernelGGL(spatial_dense_wgrad_mfma_kernel, dim3(static_cast<unsigned>(B) * 4), dim3(256), 0, s, sp,
+                       static_cast<const bf16_t*>(dpre), part, H, W, L, tiles, 4);
+  else if (dt == DT_BF16)
     hipLaunchKernelGGL(spatial_dense_wgrad_kernel<bf16_t>, dim3(static_cast<unsigned>(B) * 4), dim3(256), 0, s, sp,
                        static_cast<const bf16_t*>(dpre), part, H, W, L, tiles, 4);
   else

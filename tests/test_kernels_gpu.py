@@ -199,6 +199,49 @@ def test_spatial_embed_matches_reference_planes(autocast):
         assert _err(a, r) < tol * max(1, r.abs().max().item()) * 2
 
 
+def test_spatial_embed_partial_tile():
+    """Map sizes that are not a multiple of the kernels' 256-pixel tile (odd pixel count: the last
+    tile is partial and its pixel pairs straddle the end) against an fp32 reference of the planes."""
+    from applestar_amd.lib.features import SPATIAL_ONE_HOT, EFFECT_KEYS
+    torch.manual_seed(11)
+    B, H, W, Nn, L = 3, 37, 45, 9, 5
+    sp = {'height_map': torch.randint(0, 256, (B, H, W), device=DEV, dtype=torch.uint8)}
+    for k, n in SPATIAL_ONE_HOT:
+        sp[k] = torch.randint(0, n + 1, (B, H, W), device=DEV, dtype=torch.uint8)   # n -> clamped to n-1
+    for k in EFFECT_KEYS:
+        sp[k] = torch.randint(0, H * W, (B, L), device=DEV, dtype=torch.int16)
+    ex = torch.randint(0, W, (B, Nn), device=DEV)
+    ey = torch.randint(0, H, (B, Nn), device=DEV)
+    en = torch.tensor([Nn, 4, 0], device=DEV)
+    rows = torch.randn(B, Nn, 32, device=DEV) * (torch.arange(Nn, device=DEV)[None] < en[:, None]).unsqueeze(2)
+    w = (torch.randn(32, 24, device=DEV) * 0.3).requires_grad_()
+    b = (torch.randn(32, device=DEV) * 0.1).requires_grad_()
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        out = N.spatial_embed(sp, rows.to(torch.bfloat16), ex, ey, en, w, b)
+    planes = [sp['height_map'].float().unsqueeze(1) / 256]
+    for k, n in SPATIAL_ONE_HOT:
+        planes.append(torch.nn.functional.one_hot(sp[k].long().clamp(0, n - 1), n).permute(0, 3, 1, 2).float())
+    for k in EFFECT_KEYS:
+        m = torch.zeros(B, H * W, device=DEV)
+        m.scatter_(1, sp[k].long(), 1.0)
+        planes.append(m.view(B, 1, H, W))
+    X = torch.cat(planes, 1)                                                      # [B,24,H,W]
+    wr, br = w.detach().clone().requires_grad_(), b.detach().clone().requires_grad_()
+    pre = torch.einsum('bkhw,nk->bnhw', X, wr) + br[None, :, None, None]
+    ent = torch.zeros(B, 32, H, W, device=DEV)
+    for i in range(B):
+        for j in range(int(en[i])):
+            ent[i, :, ey[i, j], ex[i, j]] += rows[i, j].to(torch.bfloat16).float()
+    pre = pre + ent
+    ref = torch.relu(pre)
+    assert _err(out, ref) < 2e-2 * max(1, ref.abs().max().item())
+    g = torch.randn_like(ref)
+    out.backward(g.to(out.dtype))
+    (pre * (out.detach().float() > 0)).backward(g.to(torch.bfloat16).float())
+    assert _err(w.grad, wr.grad) < 2e-2 * max(1, wr.grad.abs().max().item())
+    assert _err(b.grad, br.grad) < 2e-2 * max(1, br.grad.abs().max().item())
+
+
 @pytest.mark.parametrize('lens', [[1, 64, 65, 200, 511], [37], [128, 3, 300]])
 def test_varlen_attention_matches_reference(lens):
     torch.manual_seed(7)
