@@ -610,9 +610,11 @@ at::Tensor conv3x3_fwd(const at::Tensor& x, const at::Tensor& wk, const c10::opt
   if (res.has_value()) {
     check_cuda(*res, "residual");
     TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->dim() == 4 && res->size(0) == B && res->size(1) == H &&
-                    res->size(2) == W && res->size(3) == Cout, "conv3x3: residual NHWC bf16 [B,H,W,Cout]");
+                    res->size(2) == W && res->size(3) == Cout && res->is_contiguous(),
+                "conv3x3: residual NHWC bf16 [B,H,W,Cout] contiguous");
     rp = res->data_ptr();
   }
+  TORCH_CHECK(act >= 0 && act <= 4 && (act != 4 || rp != nullptr), "conv3x3: act 0..4; act 4 (ReLU gradient gate) needs res");
   c10::hip::HIPGuard g(x.device().index());
   auto out = at::empty({B, H, W, Cout}, x.options());
   as::conv3x3_fwd(x.data_ptr(), wk.data_ptr(), bp, rp, out.data_ptr(), B, H, W, Cin, Cout, static_cast<int>(act),
@@ -815,11 +817,14 @@ std::vector<at::Tensor> resmlp_fwd(const at::Tensor& x0, const std::vector<at::T
                   (x0.scalar_type() == at::kFloat || x0.scalar_type() == at::kBFloat16),
               "resmlp: x0 [R, 256] fp32 / bf16 contiguous");
   int n = 0;
-  const as::ResMlpW w = resmlp_weights(params, &n);
+  as::ResMlpW w = resmlp_weights(params, &n);
   const int64_t R = x0.size(0);
   c10::hip::HIPGuard g(x0.device().index());
   auto f32 = x0.options().dtype(at::kFloat), b16 = x0.options().dtype(at::kBFloat16);
   auto out = at::empty({R, 256}, f32);
+  auto pk = at::empty({2 * n, 256, 256}, b16);
+  as::resmlp_pack(w, n, false, reinterpret_cast<uint16_t*>(pk.data_ptr()), stream());
+  w.pk = pk.data_ptr();
   at::Tensor sx, sh, sxh, srs;
   if (save) {
     sx = at::empty({n, R, 256}, b16);
@@ -847,12 +852,9 @@ std::vector<at::Tensor> resmlp_bwd(const at::Tensor& dout, const std::vector<at:
               "resmlp_bwd: saved tensors");
   c10::hip::HIPGuard g(dout.device().index());
   auto f32 = dout.options(), b16 = dout.options().dtype(at::kBFloat16);
-  auto wt = at::empty({2 * n, 256, 256}, b16);
-  as::resmlp_transpose(w, n, reinterpret_cast<uint16_t*>(wt.data_ptr()), stream());
-  for (int k = 0; k < n; ++k) {
-    w.w1t[k] = static_cast<const uint16_t*>(wt.data_ptr()) + (2L * k) * 65536;
-    w.w2t[k] = static_cast<const uint16_t*>(wt.data_ptr()) + (2L * k + 1) * 65536;
-  }
+  auto pk = at::empty({2 * n, 256, 256}, b16);
+  as::resmlp_pack(w, n, true, reinterpret_cast<uint16_t*>(pk.data_ptr()), stream());
+  w.pk = pk.data_ptr();
   auto dy = at::empty({n, R, 256}, b16), dh = at::empty({n, R, 256}, b16);
   const int nrb = as::resmlp_row_blocks(R);
   auto part = at::empty({nrb, n * 512}, f32);

@@ -256,14 +256,14 @@ struct ResMlpW {
   const void* b2[kResMax];
   const float* g[kResMax];
   const float* be[kResMax];
-  const void* w1t[kResMax];   // backward: W1^T, W2^T (resmlp_transpose)
-  const void* w2t[kResMax];
+  const void* pk;             // fragment-ordered GEMM operands [2 n][65536] (resmlp_pack)
 };
 // out [R, 256] fp32; saved (nullable sv_x): sv_x / sv_h bf16 [n, R, 256], sv_xhat fp32 [n, R, 256], sv_rstd [n, R]
 void resmlp_fwd(const void* x0, int x0_dt, const ResMlpW& w, int nblk, float* out, uint16_t* sv_x, uint16_t* sv_h,
                 float* sv_xhat, float* sv_rstd, long R, hipStream_t s);
-// dst [2 n, 256, 256]: W1_0^T, W2_0^T, W1_1^T, ...
-void resmlp_transpose(const ResMlpW& w, int nblk, uint16_t* dst, hipStream_t s);
+// dst [2 n][65536]: the GEMM operands in the kernels' per-wave fragment order (one 1-KB contiguous
+// run per wave load instruction): forward W1_0, W2_0, W1_1, ...; backward (bwd) W2_0^T, W1_0^T, W2_1^T, ...
+void resmlp_pack(const ResMlpW& w, int nblk, bool bwd, uint16_t* dst, hipStream_t s);
 int resmlp_row_blocks(long R);
 // dx0 [R, 256] fp32; sv_dy / sv_dh bf16 [n, R, 256] (for the batched weight gradient);
 // ln_part [row_blocks, n, 512] fp32 per-workgroup (dgamma | dbeta) partials

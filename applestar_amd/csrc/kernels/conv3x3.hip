@@ -36,6 +36,53 @@ __device__ __forceinline__ bf8v as_bf8(const uint4& u) {
   return r;
 }
 
+// fp32 tile cs [128][CPAD] (LDS) -> out rows m0.., channels n0..n0+BN in 16-B pieces:
+//   v = cs + bias (+ res | * [res > 0] for ACT_DRELU), then ReLU for ACT_RELU; bf16.
+// ACT_DRELU is the input-gradient form: dpre = dx * (y > 0) with y (the layer's ReLU output) in res.
+template <int BN, int CPAD>
+__device__ __forceinline__ void conv_epilogue(const float* cs, long m0, int n0, long M, int Cout,
+                                              const float* __restrict__ bias, const bf16_t* __restrict__ res,
+                                              bf16_t* __restrict__ out, int act) {
+  constexpr int CPR = BN / 8;  // 8-channel pieces per row
+  for (int idx = threadIdx.x; idx < 128 * CPR; idx += 256) {
+    const int rr = idx / CPR, c8 = idx % CPR;
+    const long m = m0 + rr;
+    const int n = n0 + 8 * c8;
+    if (m >= M || n >= Cout) continue;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = cs[rr * CPAD + 8 * c8 + e] + (bias ? bias[n + e] : 0.f);
+    const long o = m * Cout + n;
+    if (res) {
+      const uint4 u = *reinterpret_cast<const uint4*>(res + o);
+      const uint32_t q4[4] = {u.x, u.y, u.z, u.w};
+      if (act == ACT_DRELU) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (!(__uint_as_float(q4[e] << 16) > 0.f)) v[2 * e] = 0.f;
+          if (!(__uint_as_float(q4[e] & 0xffff0000u) > 0.f)) v[2 * e + 1] = 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += __uint_as_float(q4[e] << 16);
+          v[2 * e + 1] += __uint_as_float(q4[e] & 0xffff0000u);
+        }
+      }
+    }
+    if (act == ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    uint4 u;
+    u.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
+    u.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
+    u.z = static_cast<uint32_t>(f2bf(v[4])) | (static_cast<uint32_t>(f2bf(v[5])) << 16);
+    u.w = static_cast<uint32_t>(f2bf(v[6])) | (static_cast<uint32_t>(f2bf(v[7])) << 16);
+    *reinterpret_cast<uint4*>(out + o) = u;
+  }
+}
+
 template <int BN_, int BK_>
 struct ConvCfg {
   static constexpr int BM = 128, BN = BN_, BK = BK_;
@@ -209,36 +256,7 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__
       for (int e = 0; e < 4; ++e)
         cs[(wm * C::TM + i * 16 + 4 * lg + e) * C::CPAD + wn * C::TN + j * 16 + lr] = acc[i][j][e];
   __syncthreads();
-  constexpr int CPR = BN / 8;  // 8-channel chunks per row
-  for (int idx = tid; idx < C::BM * CPR; idx += C::NT) {
-    const int rr = idx / CPR, c8 = idx % CPR;
-    const long m = m0 + rr;
-    const int n = n0 + 8 * c8;
-    if (m >= M || n >= Cout) continue;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = cs[rr * C::CPAD + 8 * c8 + e] + (bias ? bias[n + e] : 0.f);
-    const long o = m * Cout + n;
-    if (res) {
-      const uint4 u = *reinterpret_cast<const uint4*>(res + o);
-      const uint32_t q4[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[2 * e] += __uint_as_float(q4[e] << 16);
-        v[2 * e + 1] += __uint_as_float(q4[e] & 0xffff0000u);
-      }
-    }
-    if (act == ACT_RELU) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    }
-    uint4 u;
-    u.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
-    u.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
-    u.z = static_cast<uint32_t>(f2bf(v[4])) | (static_cast<uint32_t>(f2bf(v[5])) << 16);
-    u.w = static_cast<uint32_t>(f2bf(v[6])) | (static_cast<uint32_t>(f2bf(v[7])) << 16);
-    *reinterpret_cast<uint4*>(out + o) = u;
-  }
+  conv_epilogue<BN, C::CPAD>(cs, m0, n0, M, Cout, bias, res, out, act);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -414,36 +432,7 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(const bf16_t* __restr
       for (int e = 0; e < 4; ++e)
         cs[(wm * C::TM + i * 16 + 4 * lg + e) * C::CPAD + wn * C::TN + j * 16 + lr] = acc[i][j][e];
   __syncthreads();
-  constexpr int CPR = BN / 8;
-  for (int idx = tid; idx < C::BM * CPR; idx += C::NT) {
-    const int rr = idx / CPR, c8 = idx % CPR;
-    const long m = m0 + rr;
-    const int n = n0 + 8 * c8;
-    if (m >= M || n >= Cout) continue;
-    float v[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = cs[rr * C::CPAD + 8 * c8 + e] + (bias ? bias[n + e] : 0.f);
-    const long o = m * Cout + n;
-    if (res) {
-      const uint4 u = *reinterpret_cast<const uint4*>(res + o);
-      const uint32_t q4[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[2 * e] += __uint_as_float(q4[e] << 16);
-        v[2 * e + 1] += __uint_as_float(q4[e] & 0xffff0000u);
-      }
-    }
-    if (act == ACT_RELU) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-    }
-    uint4 u;
-    u.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
-    u.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
-    u.z = static_cast<uint32_t>(f2bf(v[4])) | (static_cast<uint32_t>(f2bf(v[5])) << 16);
-    u.w = static_cast<uint32_t>(f2bf(v[6])) | (static_cast<uint32_t>(f2bf(v[7])) << 16);
-    *reinterpret_cast<uint4*>(out + o) = u;
-  }
+  conv_epilogue<BN, C::CPAD>(cs, m0, n0, M, Cout, bias, res, out, act);
 }
 
 template <int BN, int WP>

@@ -5,6 +5,8 @@ Shapes/dtypes the kernels do not cover raise instead of silently using torch.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _ext
@@ -452,6 +454,17 @@ def _conv_wt(w):
     return _C.conv_wt(w.detach())
 
 
+FUSED_DRELU = os.environ.get('APPLESTAR_CONV_DRELU', '1') != '0'   # A/B switch
+
+
+def _conv_dx_drelu(dpre, w, y):
+    """Input gradient of a 3x3 conv whose input y is a ReLU output, already gated by (y > 0): the gate
+    is the dX conv's epilogue mode 4 (no separate read-modify-write pass over the activation)."""
+    if FUSED_DRELU:
+        return _C.conv3x3_fwd(dpre, _conv_wt(w), None, y, 4)
+    return _C.act_grad_nhwc(_C.conv3x3_fwd(dpre, _conv_wt(w), None, None, 0), y, True)
+
+
 def _conv_dw(dpre, x, w, b_dtype):
     """dW (in w's dtype) and db of a 3x3 conv; callers cast db to b_dtype (a no-op when both are bf16:
     the cast is then fused into the split reduction)."""
@@ -477,9 +490,8 @@ class _ResBlock(torch.autograd.Function):
     def backward(ctx, dout):
         x, w1, w2, y1, out = ctx.saved_tensors
         dpre2 = _C.act_grad_nhwc(dout, out, True)
-        dy1 = _C.conv3x3_fwd(dpre2, _conv_wt(w2), None, None, 0)
+        dpre1 = _conv_dx_drelu(dpre2, w2, y1)
         dw2, db2 = _conv_dw(dpre2, y1, w2, ctx.b_dtypes[1])
-        dpre1 = _C.act_grad_nhwc(dy1, y1, True)
         dx = _C.conv3x3_fwd(dpre1, _conv_wt(w1), None, dpre2, 0)       # + skip gradient, fused
         dw1, db1 = _conv_dw(dpre1, x, w1, ctx.b_dtypes[0])
         return dx, dw1, db1.to(ctx.b_dtypes[0]), dw2, db2.to(ctx.b_dtypes[1])
@@ -544,9 +556,8 @@ class _GatedResBlock(torch.autograd.Function):
                 d = _C.act_grad_nhwc(dh.view(1, 1, P, C), acts_in[i].view(1, 1, P, C), True).view(P, C)
         dx_gate = torch.addmm(dx_res.view(-1, C), d, gw1.view(C, C))          # skip + G1 input gradients
         # conv path
-        dy1 = _C.conv3x3_fwd(dy, _conv_wt(w2), None, None, 0)
+        dpre1 = _conv_dx_drelu(dy, w2, y1)
         dw2, db2 = _conv_dw(dy, y1, w2, ctx.dtypes[1])
-        dpre1 = _C.act_grad_nhwc(dy1, y1, True)
         dx = _C.conv3x3_fwd(dpre1, _conv_wt(w1), None, dx_gate.view(B, H, W, C).contiguous(), 0)
         dw1, db1 = _conv_dw(dpre1, x, w1, ctx.dtypes[0])
         gate_grads = [None] * 8

@@ -406,6 +406,26 @@ def test_conv3x3_mfma_matches_fp32(cin, cout, H, W, act, res):
         assert _err(a, ref) < 3e-2 * max(1.0, ref.abs().max().item())
 
 
+@pytest.mark.parametrize('cin,cout,H,W', [(128, 128, 19, 20), (64, 128, 38, 40), (128, 64, 38, 40),
+                                          (256, 128, 9, 9), (32, 32, 7, 5), (128, 128, 76, 80)])
+def test_conv3x3_drelu_epilogue(cin, cout, H, W):
+    """act mode 4: out = conv(x) * (res > 0) - the input gradient gated by the ReLU output it flows into
+    (window / halo / implicit-GEMM kernels all share the epilogue)."""
+    from applestar_amd.ops import native
+    C = native.ensure_loaded()
+    torch.manual_seed(9)
+    B = 3
+    x = torch.randn(B, H, W, cin, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(cout, 3, 3, cin, device=DEV) / (3 * cin ** 0.5)).to(torch.bfloat16)
+    y = torch.relu(torch.randn(B, H, W, cout, device=DEV)).to(torch.bfloat16)
+    y[0, 0, 0, :] = -0.0   # negative zero gates like zero
+    out = C.conv3x3_fwd(x, w, None, y, 4)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), None, 1, 1)
+    ref = ref.permute(0, 2, 3, 1) * (y.float() > 0)
+    assert _err(out, ref) < 2e-2 * max(1.0, ref.abs().max().item())
+    assert bool((out[y <= 0] == 0).all())
+
+
 def test_conv1x1_gemm_path_matches_conv():
     from applestar_amd import ops
     torch.manual_seed(8)

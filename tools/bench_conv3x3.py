@@ -1,6 +1,9 @@
 """Microbenchmark of the native 3x3 conv forward on the learner's shapes: halo-window kernel vs the
 per-tap implicit GEMM (the same binary; APPLESTAR_CONV_HALO is read once per process, so the script
-runs itself twice).  Prints one JSON line per shape with us / call and TFLOP/s.
+runs itself once per variant).  r2z also measured a whole-window variant with the weight fragments
+loaded straight from L2 into registers and no loop barriers: 30-100 % SLOWER than the halo kernel
+(profiles/r2z_conv3x3_variants_microbench.jsonl), so it was dropped.  Prints one JSON line per shape with
+us / call and TFLOP/s.
 
     python tools/bench_conv_halo.py
 """
@@ -33,7 +36,7 @@ def run():
         torch.cuda.synchronize()
         us = s.elapsed_time(e) / n * 1e3
         flop = 2.0 * B * H * W * cout * 9 * cin
-        print(json.dumps({'halo': os.environ.get('APPLESTAR_CONV_HALO', '1'), 'shape': [B, H, W, cin, cout],
+        print(json.dumps({'variant': os.environ.get('VARIANT', 'win'), 'shape': [B, H, W, cin, cout],
                           'us': round(us, 1), 'tflops': round(flop / us / 1e6, 1),
                           'checksum': float(y.float().abs().mean())}), flush=True)
 
@@ -42,6 +45,6 @@ if __name__ == '__main__':
     if len(sys.argv) > 1 and sys.argv[1] == 'child':
         run()
     else:
-        for flag in ('0', '1'):
-            env = dict(os.environ, APPLESTAR_CONV_HALO=flag)
+        for name, halo in (('implicit', '0'), ('halo', '1')):
+            env = dict(os.environ, APPLESTAR_CONV_HALO=halo, VARIANT=name)
             subprocess.run([sys.executable, __file__, 'child'], env=env, check=True)
