@@ -18,12 +18,22 @@ __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(static_cast<uint32_t>(v) << 16);
 }
 
-// round-to-nearest-even float -> bf16 (NaN preserved)
+// round-to-nearest-even float -> bf16 (NaN preserved): the fptrunc lowers to gfx950's v_cvt_pk_bf16_f32
+// (the former integer rounding sequence carried a NaN branch - an exec-mask branch per conversion)
 __device__ __forceinline__ bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return static_cast<bf16_t>((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return static_cast<bf16_t>(u >> 16);
+  const __bf16 b = static_cast<__bf16>(f);
+  bf16_t u;
+  __builtin_memcpy(&u, &b, 2);
+  return u;
+}
+
+// two floats -> packed bf16 pair (lo in bits 0..15): one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t f2bf2(float lo, float hi) {
+  typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+  const bf2 b = {static_cast<__bf16>(lo), static_cast<__bf16>(hi)};
+  uint32_t u;
+  __builtin_memcpy(&u, &b, 4);
+  return u;
 }
 
 template <typename T> struct Cvt;

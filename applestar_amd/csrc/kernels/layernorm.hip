@@ -29,8 +29,8 @@ template <> struct VecIO<4> {
   }
   __device__ static void store(bf16_t* p, long i, const float* v) {
     uint2 t;
-    t.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
-    t.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
+    t.x = f2bf2(v[0], v[1]);
+    t.y = f2bf2(v[2], v[3]);
     *reinterpret_cast<uint2*>(p + i) = t;
   }
 };
@@ -48,7 +48,7 @@ template <> struct VecIO<2> {
   }
   __device__ static void store(bf16_t* p, long i, const float* v) {
     *reinterpret_cast<uint32_t*>(p + i) =
-        static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
+        f2bf2(v[0], v[1]);
   }
 };
 template <> struct VecIO<1> {

@@ -45,10 +45,10 @@ __global__ __launch_bounds__(256) void pointwise_kernel(const bf16_t* __restrict
       v[e] = act == ACT_RELU ? fmaxf(a, 0.f) : a;
     }
     uint4 u;
-    u.x = static_cast<uint32_t>(f2bf(v[0])) | (static_cast<uint32_t>(f2bf(v[1])) << 16);
-    u.y = static_cast<uint32_t>(f2bf(v[2])) | (static_cast<uint32_t>(f2bf(v[3])) << 16);
-    u.z = static_cast<uint32_t>(f2bf(v[4])) | (static_cast<uint32_t>(f2bf(v[5])) << 16);
-    u.w = static_cast<uint32_t>(f2bf(v[6])) | (static_cast<uint32_t>(f2bf(v[7])) << 16);
+    u.x = f2bf2(v[0], v[1]);
+    u.y = f2bf2(v[2], v[3]);
+    u.z = f2bf2(v[4], v[5]);
+    u.w = f2bf2(v[6], v[7]);
     *reinterpret_cast<uint4*>(y + p * COUT + o) = u;
   }
 }

@@ -51,10 +51,10 @@ template <> __device__ __forceinline__ V8 load8<float>(const float* p) {
 template <typename T> __device__ __forceinline__ void store8(T* p, const V8& r);
 template <> __device__ __forceinline__ void store8<bf16_t>(bf16_t* p, const V8& r) {
   uint4 u;
-  u.x = static_cast<uint32_t>(f2bf(r.v[0])) | (static_cast<uint32_t>(f2bf(r.v[1])) << 16);
-  u.y = static_cast<uint32_t>(f2bf(r.v[2])) | (static_cast<uint32_t>(f2bf(r.v[3])) << 16);
-  u.z = static_cast<uint32_t>(f2bf(r.v[4])) | (static_cast<uint32_t>(f2bf(r.v[5])) << 16);
-  u.w = static_cast<uint32_t>(f2bf(r.v[6])) | (static_cast<uint32_t>(f2bf(r.v[7])) << 16);
+  u.x = f2bf2(r.v[0], r.v[1]);
+  u.y = f2bf2(r.v[2], r.v[3]);
+  u.z = f2bf2(r.v[4], r.v[5]);
+  u.w = f2bf2(r.v[6], r.v[7]);
   *reinterpret_cast<uint4*>(p) = u;
 }
 template <> __device__ __forceinline__ void store8<float>(float* p, const V8& r) {

@@ -509,8 +509,7 @@ __global__ __launch_bounds__(256) void spatial_embed_mfma_kernel(SpatialPlanes s
     uint32_t q[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      q[j] = static_cast<uint32_t>(f2bf(fmaxf(acc_s[p][c8 + 2 * j], 0.f))) |
-             (static_cast<uint32_t>(f2bf(fmaxf(acc_s[p][c8 + 2 * j + 1], 0.f))) << 16);
+      q[j] = f2bf2(fmaxf(acc_s[p][c8 + 2 * j], 0.f), fmaxf(acc_s[p][c8 + 2 * j + 1], 0.f));
     o[i] = make_uint4(q[0], q[1], q[2], q[3]);
   }
 }

@@ -65,7 +65,7 @@ __device__ __forceinline__ void store_px(bf16_t* __restrict__ p, const float v[k
     uint32_t w4[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
-      w4[j] = static_cast<uint32_t>(f2bf(v[i * 8 + 2 * j])) | (static_cast<uint32_t>(f2bf(v[i * 8 + 2 * j + 1])) << 16);
+      w4[j] = f2bf2(v[i * 8 + 2 * j], v[i * 8 + 2 * j + 1]);
     q[i] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
   }
 }

@@ -1,0 +1,55 @@
+"""Microbenchmark of the packed varlen attention kernels on the learner's shape: 390 observations with
+entity counts U[1, 512), 2 heads x 128.  Runs itself once per kernel generation (APPLESTAR_ATTN_V2 is
+read once per process); one JSON line each with fwd / bwd us and the achieved TFLOP/s.
+
+    python tools/bench_attention.py
+"""
+import json
+import os
+import subprocess
+import sys
+
+import torch
+
+
+def run():
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from applestar_amd.ops import native
+    C = native.ensure_loaded()
+    g = torch.Generator().manual_seed(0)
+    dist = os.environ.get('LENS', 'uniform')
+    lens = torch.randint(1, 512, (390,), generator=g) if dist == 'uniform' else torch.full((130,), 511)
+    H, Dh = 2, 128
+    T = int(lens.sum())
+    cu = torch.cat([torch.zeros(1, dtype=torch.int64), lens.cumsum(0)]).to(torch.int32).cuda()
+    qkv = (torch.randn(T, 3 * H * Dh, device='cuda') * 0.5).to(torch.bfloat16)
+    mx = int(lens.max())
+    out, lse = C.varlen_attn_fwd(qkv, cu, mx, H)
+    dout = torch.randn_like(out)
+
+    def timed(fn, n=20):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(n):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / n * 1e3
+
+    f = timed(lambda: C.varlen_attn_fwd(qkv, cu, mx, H))
+    b = timed(lambda: C.varlen_attn_bwd(qkv, out, dout, lse, cu, mx, H))
+    flop = float((lens.double() ** 2).sum()) * H * Dh * 4        # QK^T + PV
+    print(json.dumps({'variant': os.environ.get('APPLESTAR_ATTN_V2', '1'), 'lens': dist, 'fwd_us': round(f, 1),
+                      'bwd_us': round(b, 1), 'fwd_tflops': round(flop / f / 1e6, 1),
+                      'bwd_tflops': round(2.5 * flop / b / 1e6, 1)}), flush=True)
+
+
+if __name__ == '__main__':
+    if len(sys.argv) > 1 and sys.argv[1] == 'child':
+        run()
+    else:
+        for flag in ('0', '1'):
+            subprocess.run([sys.executable, __file__, 'child'], env=dict(os.environ, APPLESTAR_ATTN_V2=flag), check=True)
