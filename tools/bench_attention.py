@@ -1,6 +1,6 @@
 """Microbenchmark of the packed varlen attention kernels on the learner's shape: 390 observations with
-entity counts U[1, 512), 2 heads x 128.  Runs itself once per kernel generation (APPLESTAR_ATTN_V2 is
-read once per process); one JSON line each with fwd / bwd us and the achieved TFLOP/s.
+entity counts U[1, 512) (LENS=max: 130 x 511), 2 heads x 128.  One JSON line with fwd / bwd us and the
+achieved TFLOP/s.
 
     python tools/bench_attention.py
 """
@@ -42,7 +42,7 @@ def run():
     f = timed(lambda: C.varlen_attn_fwd(qkv, cu, mx, H))
     b = timed(lambda: C.varlen_attn_bwd(qkv, out, dout, lse, cu, mx, H))
     flop = float((lens.double() ** 2).sum()) * H * Dh * 4        # QK^T + PV
-    print(json.dumps({'variant': os.environ.get('APPLESTAR_ATTN_V2', '1'), 'lens': dist, 'fwd_us': round(f, 1),
+    print(json.dumps({'lens': dist, 'fwd_us': round(f, 1),
                       'bwd_us': round(b, 1), 'fwd_tflops': round(flop / f / 1e6, 1),
                       'bwd_tflops': round(2.5 * flop / b / 1e6, 1)}), flush=True)
 
@@ -51,5 +51,4 @@ if __name__ == '__main__':
     if len(sys.argv) > 1 and sys.argv[1] == 'child':
         run()
     else:
-        for flag in ('0', '1'):
-            subprocess.run([sys.executable, __file__, 'child'], env=dict(os.environ, APPLESTAR_ATTN_V2=flag), check=True)
+        subprocess.run([sys.executable, __file__, 'child'], check=True)
