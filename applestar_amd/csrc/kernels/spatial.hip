@@ -255,6 +255,8 @@ __global__ __launch_bounds__(256) void spatial_embed_fused_kernel(SpatialPlanes 
   __shared__ float w_s[24][32];
   __shared__ float b_s[32];
   __shared__ uint32_t eb[kSpTile];
+  __shared__ int2 ent_list[kSpTile];
+  __shared__ int ent_cnt;
   const int HW = H * W;
   const int b = blockIdx.x / tiles, tile = blockIdx.x % tiles;
   const int p0 = tile * kSpTile, tid = threadIdx.x;
@@ -262,6 +264,7 @@ __global__ __launch_bounds__(256) void spatial_embed_fused_kernel(SpatialPlanes 
   for (int i = tid; i < 24 * 32; i += 256) w_s[i % 24][i / 24] = wd[(i / 24) * 24 + (i % 24)];
   if (tid < 32) b_s[tid] = bias[tid];
   eb[tid] = 0;
+  if (tid == 0) ent_cnt = 0;
   __syncthreads();
   for (int i = tid; i < 6 * L; i += 256) {
     const int e = i / L, j = i - e * L;
@@ -298,15 +301,31 @@ __global__ __launch_bounds__(256) void spatial_embed_fused_kernel(SpatialPlanes 
   }
   __syncthreads();
   // entities of this observation inside the tile: add their 32 pre-projected channels
+  // entities of this observation inside the tile: one position test per entity (a compacted LDS list),
+  // then the listed rows' 32 channels in parallel
   const int ne = static_cast<int>(entity_num[b] < N ? entity_num[b] : N);
-  for (int i = tid; i < ne * 32; i += 256) {
-    const int n = i >> 5, c = i & 31;
+  for (int n = tid; n < ne; n += 256) {
     const long bn = static_cast<long>(b) * N + n;
     int x = ex[bn], y = ey[bn];
     x = x < W ? x : W - 1;
     y = y < H ? y : H - 1;
     const int p = y * W + x - p0;
-    if (p >= 0 && p < np) atomicAdd(&acc[p][c], Cvt<TR>::load(rows, bn * 32 + c));
+    if (p >= 0 && p < np) {
+      const int slot = atomicAdd(&ent_cnt, 1);
+      if (slot < kSpTile) {
+        ent_list[slot] = make_int2(n, p);
+      } else {   // list full (> 256 entities in one tile): add this row directly
+        for (int c = 0; c < 32; ++c) atomicAdd(&acc[p][c], Cvt<TR>::load(rows, bn * 32 + c));
+      }
+    }
+  }
+  __syncthreads();
+  const int nl = ent_cnt < kSpTile ? ent_cnt : kSpTile;
+  for (int i = tid; i < nl * 32; i += 256) {
+    const int c = i & 31;
+    const int2 e = ent_list[i >> 5];
+    const long bn = static_cast<long>(b) * N + e.x;
+    atomicAdd(&acc[e.y][c], Cvt<TR>::load(rows, bn * 32 + c));
   }
   __syncthreads();
   const long o0 = (static_cast<long>(b) * HW + p0) * 32;
@@ -434,11 +453,14 @@ __global__ __launch_bounds__(256) void spatial_embed_mfma_kernel(SpatialPlanes s
   __shared__ uint32_t eb[kSpTile];
   __shared__ uint32_t msk[kSpTile];
   __shared__ uint32_t hgt[kSpTile];
+  __shared__ int2 ent_list[kSpTile];
+  __shared__ int ent_cnt;
   const int HW = H * W;
   const int b = blockIdx.x / tiles, tile = blockIdx.x % tiles;
   const int p0 = tile * kSpTile, tid = threadIdx.x, l = tid & 63, w = tid >> 6, g = l >> 4, lr = l & 15;
   const int np = HW - p0 < kSpTile ? HW - p0 : kSpTile;
   eb[tid] = 0;
+  if (tid == 0) ent_cnt = 0;
   // B fragments: B[c = 8 g + j][n = 16 nt + lr] = Wd'[n][c], hi and lo halves
   bf8v bhi[2], blo[2];
 #pragma unroll
@@ -491,15 +513,31 @@ __global__ __launch_bounds__(256) void spatial_embed_mfma_kernel(SpatialPlanes s
     }
   }
   __syncthreads();
+  // entities of this observation inside the tile: one position test per entity (a compacted LDS list),
+  // then the listed rows' 32 channels in parallel
   const int ne = static_cast<int>(entity_num[b] < N ? entity_num[b] : N);
-  for (int i = tid; i < ne * 32; i += 256) {
-    const int n = i >> 5, c = i & 31;
+  for (int n = tid; n < ne; n += 256) {
     const long bn = static_cast<long>(b) * N + n;
     int x = ex[bn], y = ey[bn];
     x = x < W ? x : W - 1;
     y = y < H ? y : H - 1;
     const int p = y * W + x - p0;
-    if (p >= 0 && p < np) atomicAdd(&acc_s[p][c], bf2f(rows[bn * 32 + c]));
+    if (p >= 0 && p < np) {
+      const int slot = atomicAdd(&ent_cnt, 1);
+      if (slot < kSpTile) {
+        ent_list[slot] = make_int2(n, p);
+      } else {   // list full (> 256 entities in one tile): add this row directly
+        for (int c = 0; c < 32; ++c) atomicAdd(&acc_s[p][c], bf2f(rows[bn * 32 + c]));
+      }
+    }
+  }
+  __syncthreads();
+  const int nl = ent_cnt < kSpTile ? ent_cnt : kSpTile;
+  for (int i = tid; i < nl * 32; i += 256) {
+    const int c = i & 31;
+    const int2 e = ent_list[i >> 5];
+    const long bn = static_cast<long>(b) * N + e.x;
+    atomicAdd(&acc_s[e.y][c], bf2f(rows[bn * 32 + c]));
   }
   __syncthreads();
   // relu + bf16, 8 channels (16 B) per store

@@ -199,19 +199,21 @@ def test_spatial_embed_matches_reference_planes(autocast):
         assert _err(a, r) < tol * max(1, r.abs().max().item()) * 2
 
 
-def test_spatial_embed_partial_tile():
+@pytest.mark.parametrize('crowded', [False, True])
+def test_spatial_embed_partial_tile(crowded):
     """Map sizes that are not a multiple of the kernels' 256-pixel tile (odd pixel count: the last
-    tile is partial and its pixel pairs straddle the end) against an fp32 reference of the planes."""
+    tile is partial and its pixel pairs straddle the end) against an fp32 reference of the planes.
+    crowded: 300 entities inside the first tile (more than its 256-entry compacted list)."""
     from applestar_amd.lib.features import SPATIAL_ONE_HOT, EFFECT_KEYS
     torch.manual_seed(11)
-    B, H, W, Nn, L = 3, 37, 45, 9, 5
+    B, H, W, Nn, L = 3, 37, 45, (300 if crowded else 9), 5
     sp = {'height_map': torch.randint(0, 256, (B, H, W), device=DEV, dtype=torch.uint8)}
     for k, n in SPATIAL_ONE_HOT:
         sp[k] = torch.randint(0, n + 1, (B, H, W), device=DEV, dtype=torch.uint8)   # n -> clamped to n-1
     for k in EFFECT_KEYS:
         sp[k] = torch.randint(0, H * W, (B, L), device=DEV, dtype=torch.int16)
-    ex = torch.randint(0, W, (B, Nn), device=DEV)
-    ey = torch.randint(0, H, (B, Nn), device=DEV)
+    ex = torch.randint(0, 8 if crowded else W, (B, Nn), device=DEV)
+    ey = torch.randint(0, 3 if crowded else H, (B, Nn), device=DEV)
     en = torch.tensor([Nn, 4, 0], device=DEV)
     rows = torch.randn(B, Nn, 32, device=DEV) * (torch.arange(Nn, device=DEV)[None] < en[:, None]).unsqueeze(2)
     w = (torch.randn(32, 24, device=DEV) * 0.3).requires_grad_()
