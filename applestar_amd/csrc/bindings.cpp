@@ -148,17 +148,18 @@ at::Tensor lstm_split_error(int64_t device) {
 }
 
 struct SplitBufs {
-  at::Tensor slab, cnt;
+  at::Tensor slab;
   as::LstmSplit s;
 };
 
+// granule slab, zeroed per launch (epoch tags start at 1)
 SplitBufs make_split(const at::Tensor& like, int64_t B, int64_t width) {
   SplitBufs r;
   const int64_t Bp = (B + 7) / 8 * 8;
-  r.slab = at::empty({2, Bp, 8, width}, like.options().dtype(at::kFloat));
-  r.cnt = at::zeros({Bp}, like.options().dtype(at::kInt));
-  r.s = {r.slab.data_ptr<float>(), reinterpret_cast<unsigned*>(r.cnt.data_ptr<int>()),
-         lstm_split_err(like.device()).data_ptr<int>()};
+  // granules [2, Bp, 8, width] u64 (backward) or data [2, Bp, 8, width] u32 + flags [Bp, 8] (forward):
+  // one zeroed buffer sized for either
+  r.slab = at::zeros({2 * Bp * 8 * width + Bp * 8}, like.options().dtype(at::kLong));
+  r.s = {reinterpret_cast<unsigned long long*>(r.slab.data_ptr<int64_t>()), lstm_split_err(like.device()).data_ptr<int>()};
   return r;
 }
 

@@ -57,12 +57,11 @@ int elementwise_blocks(long n);
 // rstd_h/rstd_c [T,B].
 bool lnlstm_supported(int H);
 // Split recurrence (H = 384): 8 workgroups per row exchange partial products through `slab`
-// ([2, Bp, 8, 4H] fwd / [2, Bp, 8, H] bwd fp32, Bp = B rounded up to 8) with per-row counters `cnt`
-// ([Bp] u32, zeroed before the launch); a poll that times out sets *err.  All Bp * 8 workgroups must be
-// co-resident (callers keep B <= 16).
+// ([2, Bp, 8, 4H] fwd / [2, Bp, 8, H] bwd {epoch, fp32} granules, Bp = B rounded up to 8, ZEROED before
+// every launch); a poll that times out sets *err.  All Bp * 8 workgroups must be co-resident (callers
+// keep B <= 16).
 struct LstmSplit {
-  float* slab;
-  unsigned* cnt;
+  unsigned long long* slab;
   int* err;
 };
 void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* wT, int w_dt, const float* lnh_w,

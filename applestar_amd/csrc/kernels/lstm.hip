@@ -31,6 +31,22 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   return s;
 }
 
+// two block sums with one barrier pair (wave shuffles + a float2 LDS slot per wave)
+template <int NT>
+__device__ __forceinline__ float2 block_sum2(float a, float b, float* scratch) {
+  constexpr int NW = NT / kWave;
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();  // scratch reuse guard
+  if ((threadIdx.x & 63) == 0) { scratch[2 * w] = a; scratch[2 * w + 1] = b; }
+  __syncthreads();
+  float2 r = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) { r.x += scratch[2 * i]; r.y += scratch[2 * i + 1]; }
+  return r;
+}
+
 template <typename TW, int COLS> struct WLoad;
 template <> struct WLoad<bf16_t, 4> {
   __device__ static void load(const bf16_t* p, float* v) {
@@ -97,7 +113,7 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_wide_kernel(
   __shared__ float h_s[H];
   __shared__ float g_s[G];
   __shared__ float part[SPLIT][G];
-  __shared__ float red[NT / kWave];
+  __shared__ float red[2 * (NT / kWave)];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const bool unit = tid < H;
@@ -140,11 +156,12 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_wide_kernel(
       a[k] = v;
       s += v;
     }
-    const float mu = block_sum<NT>(s, red) * (1.f / G);
-    float q2 = 0.f;
+    float q2 = 0.f;   // LN_h statistics in one reduction (sum, sum of squares)
 #pragma unroll
-    for (int k = 0; k < COLS; ++k) { const float d = a[k] - mu; q2 += d * d; }
-    const float rs = rsqrtf(block_sum<NT>(q2, red) * (1.f / G) + eps);
+    for (int k = 0; k < COLS; ++k) q2 += a[k] * a[k];
+    const float2 sq = block_sum2<NT>(s, q2, red);
+    const float mu = sq.x * (1.f / G);
+    const float rs = rsqrtf(fmaxf(sq.y * (1.f / G) - mu * mu, 0.f) + eps);
     const long row = static_cast<long>(t) * B + b;
 #pragma unroll
     for (int k = 0; k < COLS; ++k) {
@@ -165,9 +182,11 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_wide_kernel(
       og = sigmoidf_(g_s[3 * H + tid]);
       cpre = fg * c + ig * gg;
     }
-    const float muc = block_sum<NT>(unit ? cpre : 0.f, red) * (1.f / H);
+    // LN_c statistics in one reduction (sum, sum of squares)
+    const float2 sc2 = block_sum2<NT>(unit ? cpre : 0.f, unit ? cpre * cpre : 0.f, red);
+    const float muc = sc2.x * (1.f / H);
     const float dc = unit ? cpre - muc : 0.f;
-    const float rsc = rsqrtf(block_sum<NT>(dc * dc, red) * (1.f / H) + eps);
+    const float rsc = rsqrtf(fmaxf(sc2.y * (1.f / H) - muc * muc, 0.f) + eps);
     if (unit) {
       const float xc = dc * rsc;
       c = xc * lcw + lcb;
@@ -198,7 +217,7 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_kernel(
   constexpr int G = 4 * H;
   __shared__ float h_s[H];
   __shared__ float g_s[G];
-  __shared__ float red[NT / kWave];
+  __shared__ float red[2 * (NT / kWave)];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const bool unit = tid < H;
@@ -231,11 +250,12 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_kernel(
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < COLS; ++k) s += acc[k];
-    const float mu = block_sum<NT>(s, red) * (1.f / G);
-    float q = 0.f;
+    float q = 0.f;   // LN_h statistics in one reduction (sum, sum of squares)
 #pragma unroll
-    for (int k = 0; k < COLS; ++k) { const float d = acc[k] - mu; q += d * d; }
-    const float rs = rsqrtf(block_sum<NT>(q, red) * (1.f / G) + eps);
+    for (int k = 0; k < COLS; ++k) q += acc[k] * acc[k];
+    const float2 sq = block_sum2<NT>(s, q, red);
+    const float mu = sq.x * (1.f / G);
+    const float rs = rsqrtf(fmaxf(sq.y * (1.f / G) - mu * mu, 0.f) + eps);
     const long row = static_cast<long>(t) * B + b;
 #pragma unroll
     for (int k = 0; k < COLS; ++k) {
@@ -256,9 +276,11 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_kernel(
       og = sigmoidf_(g_s[3 * H + tid]);
       cpre = fg * c + ig * gg;
     }
-    const float muc = block_sum<NT>(unit ? cpre : 0.f, red) * (1.f / H);
+    // LN_c statistics in one reduction (sum, sum of squares)
+    const float2 sc2 = block_sum2<NT>(unit ? cpre : 0.f, unit ? cpre * cpre : 0.f, red);
+    const float muc = sc2.x * (1.f / H);
     const float dc = unit ? cpre - muc : 0.f;
-    const float rsc = rsqrtf(block_sum<NT>(dc * dc, red) * (1.f / H) + eps);
+    const float rsc = rsqrtf(fmaxf(sc2.y * (1.f / H) - muc * muc, 0.f) + eps);
     if (unit) {
       const float xc = dc * rsc;
       c = xc * lcw + lcb;
@@ -287,7 +309,7 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
   constexpr int G = 4 * H;
   __shared__ float dh_s[H];
   __shared__ float dg_s[G];
-  __shared__ float red[NT / kWave];
+  __shared__ float red[2 * (NT / kWave)];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const bool unit = tid < H;
@@ -321,8 +343,8 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
       cprev = c_all[row * H + tid];
       dg_s[3 * H + tid] = do_pre;
     }
-    const float m1 = block_sum<NT>(dxh, red) * (1.f / H);
-    const float m2 = block_sum<NT>(dxh * xc, red) * (1.f / H);
+    const float2 mm = block_sum2<NT>(dxh, dxh * xc, red);
+    const float m1 = mm.x * (1.f / H), m2 = mm.y * (1.f / H);
     if (unit) {
       const float dcpre = rstd_c[row] * (dxh - m1 - xc * m2);
       dg_s[tid] = dcpre * gg * ig * (1.f - ig);
@@ -344,8 +366,11 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
       s1 += dx[k];
       s2 += dx[k] * xh[k];
     }
-    s1 = block_sum<NT>(s1, red) * (1.f / G);
-    s2 = block_sum<NT>(s2, red) * (1.f / G);
+    {
+      const float2 ss = block_sum2<NT>(s1, s2, red);
+      s1 = ss.x * (1.f / G);
+      s2 = ss.y * (1.f / G);
+    }
     const float rs = rstd_h[row];
 #pragma unroll
     for (int k = 0; k < COLS; ++k) {
@@ -403,34 +428,68 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
 // 1.2 MB W_hh through ONE CU per step (rocprof r1_v14: ~15 us/step, 3 ms per pass).  Here each batch row
 // is served by KS = 8 workgroups; workgroup ks keeps its 1/8 slice of W_hh resident in REGISTERS for the
 // whole sequence (96 fp32 weights per thread) and computes a partial product; one all-reduce per step
-// (plain fp32 stores -> agent release -> counter add; relaxed poll -> agent acquire -> plain loads: the
-// cdna_hip_programming.md split-K hand-off) gives every workgroup the full vector, after which the LN /
+// gives every workgroup the full vector, after which the LN /
 // gate / cell math runs redundantly (bit-identical) in all KS workgroups, so no further exchange is
 // needed.  Block ids are laid out so the KS workgroups of a row share an XCD (its L2 carries the slabs).
 // Forward: slice = rows of h (W_hh^T rows), partial = 4H gate pre-activations.
 // Backward: slice = gate rows of W_hh, partial = dh_{t-1}.
-// The poll is bounded: after ~0.5 s it sets *err and continues (garbage, but the grid drains).
+// The exchange is the data-is-the-flag hand-off (cdna_hip_programming.md Guideline 16, R2): every
+// partial value travels as an 8-byte {epoch, value} granule written by an agent-scope (write-through)
+// atomic store; each consumer thread re-reads the granules IT needs with agent-scope loads until all
+// carry this step's epoch (epoch = step + 1; the slab is zeroed before every launch and double-buffered
+// by step parity - a producer can run at most one step ahead).  No counter, no fences, no workgroup
+// barrier: the previous counter form (stores -> release -> fetch_add; poll -> acquire -> loads) cost
+// several dependent L2 round trips per step.
+// The poll is bounded: after 2^16 passes (tens of ms) it sets *err and continues (garbage, but the grid drains).
 constexpr int kSplitKS = 8;
 
-__device__ __forceinline__ void split_exchange(unsigned* cnt, unsigned target, int* err) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned spins = 0;
-    while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1u << 24)) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+
+// one wave: lanes < N poll flag[lane] (agent-scope loads) until every flag reaches `epoch`
+template <int N>
+__device__ __forceinline__ void wait_flags(unsigned* flags, unsigned epoch, int* err) {
+  const int l = threadIdx.x & 63;
+  for (unsigned spins = 0;; ++spins) {
+    const unsigned f = l < N ? __hip_atomic_load((gu32*)(flags + l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : epoch;
+    if (__all(f >= epoch)) return;
+    if (spins > (1u << 16)) {
+      if (l == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_sleep(1);
   }
-  __syncthreads();
+}
+
+__device__ __forceinline__ void put_granule(unsigned long long* g, unsigned epoch, float v) {
+  __hip_atomic_store((gu64*)(g), (static_cast<unsigned long long>(epoch) << 32) | __float_as_uint(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// v[q][k] = granule (base + q * qstride + k) once all N carry `epoch` (wave-uniform loop)
+template <int NQ, int NK>
+__device__ __forceinline__ void get_granules(const unsigned long long* base, long qstride, unsigned epoch,
+                                             float (&v)[NQ][NK], int* err) {
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+      for (int k = 0; k < NK; ++k) {
+        const unsigned long long x = __hip_atomic_load(
+            (gu64*)(const_cast<unsigned long long*>(base + q * qstride + k)), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        v[q][k] = __uint_as_float(static_cast<unsigned>(x));
+        ok &= static_cast<unsigned>(x >> 32) == epoch;
+      }
+    if (__all(ok)) return;
+    if (spins > (1u << 16)) {
+      if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
 }
 
 template <int H, int NT, typename TW>
@@ -440,13 +499,13 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
     const float* __restrict__ lnc_w, const float* __restrict__ lnc_b, int T, int B, int Bp, float eps,
     float* __restrict__ out, float* __restrict__ c_all, float* __restrict__ xhat_h, float* __restrict__ rstd_h,
     float* __restrict__ gates_out, float* __restrict__ xhat_c, float* __restrict__ rstd_c, float* __restrict__ hT,
-    float* __restrict__ cT, float* __restrict__ slab, unsigned* __restrict__ cnt, int* __restrict__ err) {
+    float* __restrict__ cT, unsigned long long* __restrict__ slab, int* __restrict__ err) {
   constexpr int KS = kSplitKS;
   constexpr int G = 4 * H, RS = H / KS, COLS = G / NT, GS = G / KS;
   static_assert(G % NT == 0 && H % KS == 0 && NT >= H, "split tiling");
   __shared__ float h_s[H];
   __shared__ float g_s[G];
-  __shared__ float red[NT / kWave];
+  __shared__ float red[2 * (NT / kWave)];
   const int b = blockIdx.x % Bp, ks = blockIdx.x / Bp;   // Bp % 8 == 0: a row's slices share an XCD
   if (b >= B) return;
   const int tid = threadIdx.x;
@@ -479,27 +538,45 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
 #pragma unroll
       for (int k = 0; k < COLS; ++k) acc[k] = fmaf(hv, wv[r][k], acc[k]);
     }
+    // R1 hand-off (the payload is 48 KB per row - too much to poll value by value): write-through data
+    // stores, drain, one flag per producer workgroup; one wave polls the row's 8 flags, then every
+    // thread reads its 16 values with write-through (L1-bypassing) loads - no fences
     const int par = t & 1;
-    float* my = slab + ((static_cast<long>(par) * Bp + b) * KS + ks) * G;
+    const unsigned epoch = static_cast<unsigned>(t + 1);
+    unsigned* data = reinterpret_cast<unsigned*>(slab) + (static_cast<long>(par) * Bp + b) * KS * G;
+    unsigned* flags = reinterpret_cast<unsigned*>(slab) + 2L * Bp * KS * G + static_cast<long>(b) * KS;
 #pragma unroll
-    for (int k = 0; k < COLS; ++k) my[tid * COLS + k] = acc[k];
-    split_exchange(cnt + b, static_cast<unsigned>(KS * (t + 1)), err);
-    const float* all = slab + (static_cast<long>(par) * Bp + b) * KS * G;
+    for (int k = 0; k < COLS; ++k)
+      __hip_atomic_store((gu32*)(data + ks * G + tid * COLS + k), __float_as_uint(acc[k]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store((gu32*)(flags + ks), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < 64) wait_flags<KS>(flags, epoch, err);
+    __syncthreads();
+    float pv[KS][COLS];
+#pragma unroll
+    for (int q = 0; q < KS; ++q)
+#pragma unroll
+      for (int k = 0; k < COLS; ++k)
+        pv[q][k] = __uint_as_float(__hip_atomic_load((gu32*)(data + q * G + tid * COLS + k), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT));
     float a[COLS];
     float sum = 0.f;
 #pragma unroll
     for (int k = 0; k < COLS; ++k) {
       float v = 0.f;
 #pragma unroll
-      for (int q = 0; q < KS; ++q) v += all[q * G + tid * COLS + k];
+      for (int q = 0; q < KS; ++q) v += pv[q][k];
       a[k] = v;
       sum += v;
     }
-    const float mu = block_sum<NT>(sum, red) * (1.f / G);
-    float q2 = 0.f;
+    float q2 = 0.f;   // LN_h statistics in one reduction (sum, sum of squares)
 #pragma unroll
-    for (int k = 0; k < COLS; ++k) { const float d = a[k] - mu; q2 += d * d; }
-    const float rs = rsqrtf(block_sum<NT>(q2, red) * (1.f / G) + eps);
+    for (int k = 0; k < COLS; ++k) q2 += a[k] * a[k];
+    const float2 sq = block_sum2<NT>(sum, q2, red);
+    const float mu = sq.x * (1.f / G);
+    const float rs = rsqrtf(fmaxf(sq.y * (1.f / G) - mu * mu, 0.f) + eps);
     const long row = static_cast<long>(t) * B + b;
 #pragma unroll
     for (int k = 0; k < COLS; ++k) {
@@ -522,9 +599,11 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
       og = sigmoidf_(g_s[3 * H + tid]);
       cpre = fg * c + ig * gg;
     }
-    const float muc = block_sum<NT>(unit ? cpre : 0.f, red) * (1.f / H);
+    // LN_c statistics in one reduction (sum, sum of squares)
+    const float2 sc2 = block_sum2<NT>(unit ? cpre : 0.f, unit ? cpre * cpre : 0.f, red);
+    const float muc = sc2.x * (1.f / H);
     const float dc = unit ? cpre - muc : 0.f;
-    const float rsc = rsqrtf(block_sum<NT>(dc * dc, red) * (1.f / H) + eps);
+    const float rsc = rsqrtf(fmaxf(sc2.y * (1.f / H) - muc * muc, 0.f) + eps);
     if (unit) {
       const float xc = dc * rsc;
       c = xc * lcw + lcb;
@@ -551,14 +630,14 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
     const float* __restrict__ rstd_c, const float* __restrict__ xhat_h, const float* __restrict__ rstd_h,
     const TW* __restrict__ w, const float* __restrict__ lnh_w, const float* __restrict__ lnc_w, int T, int B, int Bp,
     float* __restrict__ dgates, float* __restrict__ dhg, float* __restrict__ dc_ln, float* __restrict__ dh0,
-    float* __restrict__ dc0, float* __restrict__ slab, unsigned* __restrict__ cnt, int* __restrict__ err) {
+    float* __restrict__ dc0, unsigned long long* __restrict__ slab, int* __restrict__ err) {
   constexpr int KS = kSplitKS;
   constexpr int G = 4 * H, COLS = G / NT, JS = G / KS, RH = NT / H, JR = JS / RH, RS = H / KS;
   static_assert(NT % H == 0 && JS % RH == 0 && G % NT == 0, "split tiling");
   __shared__ float dh_s[H];
   __shared__ float dg_s[G];
   __shared__ float part[RH][H];
-  __shared__ float red[NT / kWave];
+  __shared__ float red[2 * (NT / kWave)];
   const int b = blockIdx.x % Bp, ks = blockIdx.x / Bp;
   if (b >= B) return;
   const int tid = threadIdx.x;
@@ -598,8 +677,8 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
       cprev = c_all[row * H + tid];
       dg_s[3 * H + tid] = do_pre;
     }
-    const float m1 = block_sum<NT>(dxh, red) * (1.f / H);
-    const float m2 = block_sum<NT>(dxh * xc, red) * (1.f / H);
+    const float2 mm = block_sum2<NT>(dxh, dxh * xc, red);
+    const float m1 = mm.x * (1.f / H), m2 = mm.y * (1.f / H);
     if (unit) {
       const float dcpre = rstd_c[row] * (dxh - m1 - xc * m2);
       dg_s[tid] = dcpre * gg * ig * (1.f - ig);
@@ -620,8 +699,11 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
       s1 += dx[k];
       s2 += dx[k] * xh[k];
     }
-    s1 = block_sum<NT>(s1, red) * (1.f / G);
-    s2 = block_sum<NT>(s2, red) * (1.f / G);
+    {
+      const float2 ss = block_sum2<NT>(s1, s2, red);
+      s1 = ss.x * (1.f / G);
+      s2 = ss.y * (1.f / G);
+    }
     const float rs = rstd_h[row];
 #pragma unroll
     for (int k = 0; k < COLS; ++k) {
@@ -638,19 +720,23 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
     part[rh][kcol] = acc;
     __syncthreads();
     const int par = t & 1;
+    const unsigned epoch = static_cast<unsigned>(T - t);
+    unsigned long long* row_slab = slab + (static_cast<long>(par) * Bp + b) * KS * H;
     if (unit) {
       float v = 0.f;
 #pragma unroll
       for (int q = 0; q < RH; ++q) v += part[q][tid];
-      slab[((static_cast<long>(par) * Bp + b) * KS + ks) * H + tid] = v;
+      put_granule(row_slab + ks * H + tid, epoch, v);
     }
-    split_exchange(cnt + b, static_cast<unsigned>(KS * (T - t)), err);
-    if (unit) {
-      const float* all = slab + (static_cast<long>(par) * Bp + b) * KS * H;
-      float v = 0.f;
+    if (tid < 64 * ((H + 63) / 64)) {   // whole waves: the poll loop is wave-uniform
+      float pv[KS][1];
+      get_granules<KS, 1>(row_slab + (tid < H ? tid : 0), H, epoch, pv, err);
+      if (unit) {
+        float v = 0.f;
 #pragma unroll
-      for (int q = 0; q < KS; ++q) v += all[q * H + tid];
-      dh_s[tid] = v;
+        for (int q = 0; q < KS; ++q) v += pv[q][0];
+        dh_s[tid] = v;
+      }
     }
     __syncthreads();
   }
@@ -704,11 +790,11 @@ void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* w
     if (w_dt == DT_BF16)
       hipLaunchKernelGGL((lnlstm_fwd_split_kernel<384, 768, bf16_t>), grid, dim3(768), 0, s, xp, h0, c0,
                          static_cast<const bf16_t*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, Bp, eps, out, c_all,
-                         xhat_h, rstd_h, gates, xhat_c, rstd_c, hT, cT, split->slab, split->cnt, split->err);
+                         xhat_h, rstd_h, gates, xhat_c, rstd_c, hT, cT, split->slab, split->err);
     else
       hipLaunchKernelGGL((lnlstm_fwd_split_kernel<384, 768, float>), grid, dim3(768), 0, s, xp, h0, c0,
                          static_cast<const float*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, Bp, eps, out, c_all,
-                         xhat_h, rstd_h, gates, xhat_c, rstd_c, hT, cT, split->slab, split->cnt, split->err);
+                         xhat_h, rstd_h, gates, xhat_c, rstd_c, hT, cT, split->slab, split->err);
   } else if (H == 384) {
     if (w_dt == DT_BF16)
       hipLaunchKernelGGL((lnlstm_fwd_wide_kernel<384, 768, bf16_t>), dim3(B), dim3(768), 0, s, xp, h0, c0,
@@ -734,11 +820,11 @@ void lnlstm_bwd(const float* dout, const float* dhT, const float* dcT, const flo
     if (w_dt == DT_BF16)
       hipLaunchKernelGGL((lnlstm_bwd_split_kernel<384, 768, bf16_t>), grid, dim3(768), 0, s, dout, dhT, dcT, gates,
                          c_all, xhat_c, rstd_c, xhat_h, rstd_h, static_cast<const bf16_t*>(w), lnh_w, lnc_w, T, B, Bp,
-                         dgates, dhg, dc_ln, dh0, dc0, split->slab, split->cnt, split->err);
+                         dgates, dhg, dc_ln, dh0, dc0, split->slab, split->err);
     else
       hipLaunchKernelGGL((lnlstm_bwd_split_kernel<384, 768, float>), grid, dim3(768), 0, s, dout, dhT, dcT, gates,
                          c_all, xhat_c, rstd_c, xhat_h, rstd_h, static_cast<const float*>(w), lnh_w, lnc_w, T, B, Bp,
-                         dgates, dhg, dc_ln, dh0, dc0, split->slab, split->cnt, split->err);
+                         dgates, dhg, dc_ln, dh0, dc0, split->slab, split->err);
   } else if (H == 384)
     bwd_launch<384, 768, 2>(dout, dhT, dcT, gates, c_all, xhat_c, rstd_c, xhat_h, rstd_h, w, w_dt, lnh_w, lnc_w, T, B,
                             dgates, dhg, dc_ln, dh0, dc0, s);
