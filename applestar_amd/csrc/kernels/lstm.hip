@@ -47,6 +47,27 @@ __device__ __forceinline__ float2 block_sum2(float a, float b, float* scratch) {
   return r;
 }
 
+// register-resident weight slice of N values; bf16 weights stay packed two per VGPR (halves the
+// split kernels' weight registers: 96 -> 48, which removed the backward's scratch spill)
+template <typename TW, int N> struct RegW;
+template <int N> struct RegW<float, N> {
+  float v[N];
+  __device__ __forceinline__ void load(int i, const float* p, long off) { v[i] = p[off]; }
+  __device__ __forceinline__ float get(int i) const { return v[i]; }
+};
+template <int N> struct RegW<bf16_t, N> {
+  static_assert(N % 2 == 0, "pairs");
+  uint32_t v[N / 2];
+  __device__ __forceinline__ void load(int i, const bf16_t* p, long off) {
+    const uint32_t x = p[off];
+    if (i & 1) v[i >> 1] |= x << 16;
+    else v[i >> 1] = x;
+  }
+  __device__ __forceinline__ float get(int i) const {
+    return (i & 1) ? __uint_as_float(v[i >> 1] & 0xffff0000u) : __uint_as_float(v[i >> 1] << 16);
+  }
+};
+
 template <typename TW, int COLS> struct WLoad;
 template <> struct WLoad<bf16_t, 4> {
   __device__ static void load(const bf16_t* p, float* v) {
@@ -511,11 +532,11 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
   const int tid = threadIdx.x;
   const bool unit = tid < H;
   const bool own_unit = unit && tid / RS == ks;
-  float wv[RS][COLS];
+  RegW<TW, RS * COLS> wv;
 #pragma unroll
   for (int r = 0; r < RS; ++r)
 #pragma unroll
-    for (int k = 0; k < COLS; ++k) wv[r][k] = Cvt<TW>::load(wT, static_cast<long>(ks * RS + r) * G + tid * COLS + k);
+    for (int k = 0; k < COLS; ++k) wv.load(r * COLS + k, wT, static_cast<long>(ks * RS + r) * G + tid * COLS + k);
   float c = 0.f, lcw = 0.f, lcb = 0.f;
   if (unit) {
     h_s[tid] = h0[static_cast<long>(b) * H + tid];
@@ -527,8 +548,18 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
   float lw[COLS], lb[COLS];
 #pragma unroll
   for (int k = 0; k < COLS; ++k) { lw[k] = lnh_w[tid * COLS + k]; lb[k] = lnh_b[tid * COLS + k]; }
+  // the input projection of step t + 1 is fetched during step t
+  float xpc[COLS];
+#pragma unroll
+  for (int k = 0; k < COLS; ++k) xpc[k] = T > 0 ? xp[static_cast<long>(b) * G + tid * COLS + k] : 0.f;
   __syncthreads();
   for (int t = 0; t < T; ++t) {
+    float xpn[COLS];
+    {
+      const long nrow = static_cast<long>(t + 1 < T ? t + 1 : t) * B + b;
+#pragma unroll
+      for (int k = 0; k < COLS; ++k) xpn[k] = xp[nrow * G + tid * COLS + k];
+    }
     float acc[COLS];
 #pragma unroll
     for (int k = 0; k < COLS; ++k) acc[k] = 0.f;
@@ -536,7 +567,7 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
     for (int r = 0; r < RS; ++r) {
       const float hv = h_s[ks * RS + r];
 #pragma unroll
-      for (int k = 0; k < COLS; ++k) acc[k] = fmaf(hv, wv[r][k], acc[k]);
+      for (int k = 0; k < COLS; ++k) acc[k] = fmaf(hv, wv.get(r * COLS + k), acc[k]);
     }
     // R1 hand-off (the payload is 48 KB per row - too much to poll value by value): write-through data
     // stores, drain, one flag per producer workgroup; one wave polls the row's 8 flags, then every
@@ -582,7 +613,7 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
     for (int k = 0; k < COLS; ++k) {
       const int j = tid * COLS + k;
       const float xh = (a[k] - mu) * rs;
-      const float gv = xp[row * G + j] + xh * lw[k] + lb[k];
+      const float gv = xpc[k] + xh * lw[k] + lb[k];
       if (j / GS == ks) {
         xhat_h[row * G + j] = xh;
         gates_out[row * G + j] = gv;
@@ -617,6 +648,8 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
       }
     }
     if (tid == 0 && ks == 0) rstd_c[row] = rsc;
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) xpc[k] = xpn[k];
     __syncthreads();
   }
   if (T == 0 && own_unit) { hT[static_cast<long>(b) * H + tid] = h_s[tid]; cT[static_cast<long>(b) * H + tid] = c; }
@@ -645,9 +678,9 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
   const bool own_unit = unit && tid / RS == ks;
   const int kcol = tid % H, rh = tid / H;
   const int j0 = ks * JS + rh * JR;
-  float wv[JR];
+  RegW<TW, JR> wv;
 #pragma unroll
-  for (int m = 0; m < JR; ++m) wv[m] = Cvt<TW>::load(w, static_cast<long>(j0 + m) * H + kcol);
+  for (int m = 0; m < JR; ++m) wv.load(m, w, static_cast<long>(j0 + m) * H + kcol);
   float dc = 0.f, lcw = 0.f;
   if (unit) {
     dh_s[tid] = dhT[static_cast<long>(b) * H + tid];
@@ -657,30 +690,53 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
   float lw[COLS];
 #pragma unroll
   for (int k = 0; k < COLS; ++k) lw[k] = lnh_w[tid * COLS + k];
+  // the step's saved activations, fetched one step ahead (their latency hides under the previous
+  // step's exchange instead of opening every step); unit lanes only for the H-wide ones
+  struct StepIn { float dout, cc, go, xc, gi, gf, gg, cprev, rc, xh[COLS], rh; };
+  const int ut = unit ? tid : 0;
+  auto load_in = [&](int t, StepIn& v) {
+    const long row = static_cast<long>(t) * B + b;
+    v.dout = dout[row * H + ut];
+    v.cc = c_all[(row + B) * H + ut];
+    v.go = gates[row * G + 3 * H + ut];
+    v.xc = xhat_c[row * H + ut];
+    v.gi = gates[row * G + ut];
+    v.gf = gates[row * G + H + ut];
+    v.gg = gates[row * G + 2 * H + ut];
+    v.cprev = c_all[row * H + ut];
+    v.rc = rstd_c[row];
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) v.xh[k] = xhat_h[row * G + tid * COLS + k];
+    v.rh = rstd_h[row];
+  };
+  StepIn cur;
+  if (T > 0) load_in(T - 1, cur);
   __syncthreads();
   for (int t = T - 1; t >= 0; --t) {
     const long row = static_cast<long>(t) * B + b;
+    StepIn nxt;
+    load_in(t > 0 ? t - 1 : 0, nxt);
     float dxh = 0.f, xc = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, cprev = 0.f;
     if (unit) {
-      const float dh = dout[row * H + tid] + dh_s[tid];
-      const float cc = c_all[(row + B) * H + tid];
+      const float dh = cur.dout + dh_s[tid];
+      const float cc = cur.cc;
       const float tc = tanhf(cc);
-      const float og = sigmoidf_(gates[row * G + 3 * H + tid]);
+      const float og = sigmoidf_(cur.go);
       const float do_pre = dh * tc * og * (1.f - og);
       const float dct = dc + dh * og * (1.f - tc * tc);
       if (own_unit) dc_ln[row * H + tid] = dct;
       dxh = dct * lcw;
-      xc = xhat_c[row * H + tid];
-      ig = sigmoidf_(gates[row * G + tid]);
-      fg = sigmoidf_(gates[row * G + H + tid]);
-      gg = tanhf(gates[row * G + 2 * H + tid]);
-      cprev = c_all[row * H + tid];
+      xc = cur.xc;
+      ig = sigmoidf_(cur.gi);
+      fg = sigmoidf_(cur.gf);
+      gg = tanhf(cur.gg);
+      cprev = cur.cprev;
       dg_s[3 * H + tid] = do_pre;
     }
     const float2 mm = block_sum2<NT>(dxh, dxh * xc, red);
     const float m1 = mm.x * (1.f / H), m2 = mm.y * (1.f / H);
     if (unit) {
-      const float dcpre = rstd_c[row] * (dxh - m1 - xc * m2);
+      const float dcpre = cur.rc * (dxh - m1 - xc * m2);
       dg_s[tid] = dcpre * gg * ig * (1.f - ig);
       dg_s[H + tid] = dcpre * cprev * fg * (1.f - fg);
       dg_s[2 * H + tid] = dcpre * ig * (1.f - gg * gg);
@@ -694,7 +750,7 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
       const int j = tid * COLS + k;
       const float dgv = dg_s[j];
       if (j / JS == ks) dgates[row * G + j] = dgv;
-      xh[k] = xhat_h[row * G + j];
+      xh[k] = cur.xh[k];
       dx[k] = dgv * lw[k];
       s1 += dx[k];
       s2 += dx[k] * xh[k];
@@ -704,7 +760,7 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
       s1 = ss.x * (1.f / G);
       s2 = ss.y * (1.f / G);
     }
-    const float rs = rstd_h[row];
+    const float rs = cur.rh;
 #pragma unroll
     for (int k = 0; k < COLS; ++k) {
       const int j = tid * COLS + k;
@@ -716,7 +772,7 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
     // partial dh_{t-1}[k] over this workgroup's JS gate rows (two row halves per column, combined in LDS)
     float acc = 0.f;
 #pragma unroll
-    for (int m = 0; m < JR; ++m) acc = fmaf(dg_s[j0 + m], wv[m], acc);
+    for (int m = 0; m < JR; ++m) acc = fmaf(dg_s[j0 + m], wv.get(m), acc);
     part[rh][kcol] = acc;
     __syncthreads();
     const int par = t & 1;
@@ -738,6 +794,7 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
         dh_s[tid] = v;
       }
     }
+    cur = nxt;
     __syncthreads();
   }
   if (own_unit) {
