@@ -287,6 +287,33 @@ at::Tensor entity_onehot(const std::vector<at::Tensor>& fields, const std::vecto
   return X;
 }
 
+// (dW [256, k_in] fp32, db [256] fp32) of relu(X W^T + b) from dout and the ReLU output (same dtype)
+std::vector<at::Tensor> entity_embed_wgrad(const std::vector<at::Tensor>& fields, const std::vector<int64_t>& kind,
+                                           const std::vector<int64_t>& offset, const std::vector<int64_t>& width,
+                                           const at::Tensor& index, const at::Tensor& dout, const at::Tensor& out,
+                                           int64_t k_in) {
+  check_cuda(index, "index");
+  check_cuda(dout, "dout");
+  check_cuda(out, "out");
+  const int64_t T = index.numel();
+  TORCH_CHECK(dout.scalar_type() == out.scalar_type() && dout.is_contiguous() && out.is_contiguous() &&
+                  dout.numel() == T * 256 && out.numel() == T * 256, "entity_embed_wgrad: dout / out [T, 256] contiguous");
+  TORCH_CHECK(k_in >= 1 && k_in <= 1024, "entity_embed_wgrad: K_in <= 1024");
+  auto f = make_fields(fields, kind, offset, width, fields.empty() ? 0 : fields[0].numel());
+  for (int i = 0; i < f.n; ++i)
+    TORCH_CHECK(f.offset[i] + (f.kind[i] == as::FIELD_SCALAR ? 1 : f.width[i]) <= k_in, "field offset");
+  c10::hip::HIPGuard g(index.device().index());
+  auto f32 = dout.options().dtype(at::kFloat);
+  const int nchunk = as::entity_wgrad_chunks(T);
+  const int64_t width_row = 256 * k_in + 256;
+  auto part = at::empty({nchunk, width_row}, f32);
+  as::entity_embed_wgrad(f, index.data_ptr<int64_t>(), dout.data_ptr(), out.data_ptr(), dt(dout), part.data_ptr<float>(),
+                         T, static_cast<int>(k_in), nchunk, stream());
+  auto red = at::empty({width_row}, f32);
+  as::column_reduce(part.data_ptr<float>(), red.data_ptr<float>(), nchunk, width_row, stream());
+  return {red.narrow(0, 0, 256 * k_in).view({256, k_in}), red.narrow(0, 256 * k_in, 256)};
+}
+
 // ---------------------------------------------------------------- spatial path (NHWC)
 at::Tensor upsample2x_fwd(const at::Tensor& x) {  // x [B,H,W,C]
   check_cuda(x, "x");
@@ -1032,6 +1059,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("entity_onehot", &entity_onehot);
   m.def("upsample2x_fwd", &upsample2x_fwd);
   m.def("upsample2x_bwd", &upsample2x_bwd);
+  m.def("entity_embed_wgrad", &entity_embed_wgrad);
   m.def("spatial_embed_fwd", &spatial_embed_fwd);
   m.def("spatial_gather_rows", &spatial_gather_rows);
   m.def("spatial_dense_input", &spatial_dense_input);

@@ -78,6 +78,11 @@ void lnlstm_bwd(const float* dout, const float* dhT, const float* dcT, const flo
 // out[t] = relu(bias + sum_fields W^T[row(field value)]) for packed entity t (source row index[t]).
 void entity_embed_fwd(const EntityFields& f, const int64_t* index, const void* wT, int w_dt, const float* bias,
                       void* out, int out_dt, long T, hipStream_t s);
+// dW partials of the embedding from dpre = dout * [out > 0] (dout / out [T][256], dt): part
+// [nchunk][256 * K_in + 256] (dW row-major | db), reduced over chunks by column_reduce; K_in <= 1024
+int entity_wgrad_chunks(long T);
+void entity_embed_wgrad(const EntityFields& f, const int64_t* index, const void* dout, const void* out, int dt,
+                        float* part, long T, int K_in, int nchunk, hipStream_t s);
 // X[t, :] = 997-wide sparse encoding of entity t (X must be zeroed).
 void entity_onehot(const EntityFields& f, const int64_t* index, void* X, int x_dt, long T, int K_in, hipStream_t s);
 

@@ -177,6 +177,11 @@ def _entity_table(entity_info):
     return fields, kind, offset, width
 
 
+# entity.hip's LDS-atomic scatter for dW measured 7.6 ms (r2aq) vs 0.46 ms for the materialised one-hot
+# + library GEMM: off until it is an MFMA kernel
+ENTITY_SPARSE_WGRAD = os.environ.get('APPLESTAR_ENTITY_SPARSE_WGRAD', '0') == '1'
+
+
 class _EntityEmbed(torch.autograd.Function):
     @staticmethod
     def forward(ctx, w, b, index, out_dtype, *fields):
@@ -195,6 +200,10 @@ class _EntityEmbed(torch.autograd.Function):
     def backward(ctx, dout):
         out, index, *fields = ctx.saved_tensors
         kind, offset, width, k_in, out_dtype = ctx.meta
+        if ENTITY_SPARSE_WGRAD:
+            dw, db = _C.entity_embed_wgrad(list(fields), kind, offset, width, index,
+                                           dout.to(out.dtype).contiguous(), out, k_in)
+            return (dw, db, None, None) + (None,) * len(fields)
         dpre = (dout * (out > 0)).to(out_dtype)
         X = _C.entity_onehot(list(fields), kind, offset, width, index, k_in, _dt_code(out_dtype))
         dw = (dpre.t() @ X).float()
@@ -707,12 +716,54 @@ class _Linear(torch.autograd.Function):
 _WGRAD_MIN_ROWS = 256     # tools/ab_bench.py --variant wgrad_small: -0.7 ms/step vs 4096
 
 
+class _LinearSplitK(torch.autograd.Function):
+    """act(x W^T + b) for a reduction dim the native kernels do not take (K % 8 != 0): library GEMMs
+    for y and dX, dW / db reduced over 64 row chunks with one batched GEMM + a sum."""
+
+    @staticmethod
+    def forward(ctx, x2, w, b, relu):
+        y = torch.nn.functional.linear(x2, w, b)
+        if relu:
+            y = torch.relu(y)
+        ctx.save_for_backward(x2, w, y if relu else None)
+        ctx.relu, ctx.has_b = relu, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, y = ctx.saved_tensors
+        if ctx.relu:
+            dy = dy * (y > 0)
+        dy = dy.to(x2.dtype).contiguous()
+        R, N = dy.shape
+        K = x2.shape[1]
+        dx = dy @ w if ctx.needs_input_grad[0] else None
+        c = 64
+        Rc = R // c
+        dw = torch.bmm(dy[:Rc * c].view(c, Rc, N).transpose(1, 2), x2[:Rc * c].view(c, Rc, K)).float().sum(0)
+        if Rc * c < R:
+            dw += dy[Rc * c:].t().float() @ x2[Rc * c:].float()
+        db = dy.float().sum(0) if ctx.has_b else None
+        return dx, dw.to(w.dtype), (db.to(w.dtype) if db is not None else None), None
+
+
 def linear(x, w, b=None, act=None):
     """bf16 act(x W^T + b) over the last dim of x with the native weight gradient when the row count is
     large; other shapes take F.linear (+ the activation)."""
     N, K = w.shape
     R = x.numel() // K if K else 0
     lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
+    if lowp and K % 8 and R >= 4 * _WGRAD_MIN_ROWS and act in (None, 'relu'):
+        # K not a multiple of 8 (e.g. the location head's 4 + 128 = 132-channel 1x1 conv over 146k
+        # pixels): library forward / dX, weight gradient as a split-K batched GEMM (the plain library
+        # dW = dY^T X on [146k, 132] runs a couple of output tiles for 0.42 ms; zero-padding K to 136
+        # instead made both the dX GEMM and the native dW pick slow tiles: +5 ms, r2ap)
+        with torch.autocast('cuda', enabled=False):
+            xb = x.reshape(R, K).to(torch.bfloat16)
+            wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
+            bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
+            y = _LinearSplitK.apply(xb, wb, bb, act == 'relu')
+        return y.view(*x.shape[:-1], N)
     if not lowp or R < _WGRAD_MIN_ROWS or N % 8 or K % 8 or R * max(N, K) * 2 >= 0x7ffffff0 or \
             act not in (None, 'relu'):
         y = torch.nn.functional.linear(x, w, b)

@@ -531,6 +531,27 @@ def test_native_linear_autocast_grads_match_fp32():
         assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
 
 
+def test_native_linear_pads_odd_k():
+    """K = 132 (not a multiple of 8): the reduction dim is zero-padded so the native weight-gradient
+    kernel runs; grads of x, w (original shapes) and b must match fp32."""
+    from applestar_amd import ops
+    torch.manual_seed(16)
+    x = torch.randn(5000, 132, device=DEV, requires_grad=True)
+    w = (torch.randn(128, 132, device=DEV) / 12).requires_grad_()
+    b = torch.randn(128, device=DEV, requires_grad=True)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y = ops.linear(x, w, b)
+    assert y.shape == (5000, 128)
+    g = torch.randn(5000, 128, device=DEV)
+    y.float().backward(g)
+    xs, ws, bs = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    (xs @ ws.t() + bs).backward(g)
+    assert x.grad.shape == x.shape and w.grad.shape == w.shape
+    for a, r in ((y.float(), xs.detach() @ ws.detach().t() + bs.detach()), (x.grad, xs.grad), (w.grad, ws.grad),
+                 (b.grad, bs.grad)):
+        assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
+
+
 @pytest.mark.parametrize('layout', ['nhwc', 'nchw', 'strided'])
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('relu', [False, True])
