@@ -298,7 +298,7 @@ std::vector<at::Tensor> entity_embed_wgrad(const std::vector<at::Tensor>& fields
   const int64_t T = index.numel();
   TORCH_CHECK(dout.scalar_type() == out.scalar_type() && dout.is_contiguous() && out.is_contiguous() &&
                   dout.numel() == T * 256 && out.numel() == T * 256, "entity_embed_wgrad: dout / out [T, 256] contiguous");
-  TORCH_CHECK(k_in >= 1 && k_in <= 1024, "entity_embed_wgrad: K_in <= 1024");
+  TORCH_CHECK(k_in >= 1 && k_in < 1024, "entity_embed_wgrad: K_in < 1024 (column K_in carries db)");
   auto f = make_fields(fields, kind, offset, width, fields.empty() ? 0 : fields[0].numel());
   for (int i = 0; i < f.n; ++i)
     TORCH_CHECK(f.offset[i] + (f.kind[i] == as::FIELD_SCALAR ? 1 : f.width[i]) <= k_in, "field offset");

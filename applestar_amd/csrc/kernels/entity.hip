@@ -4,10 +4,10 @@
 // [B, N, 997] fp32 tensor and multiplies by W[256, 997] (entity_encoder.py:61-78, K1 in SURVEY).
 // one-hot(v) @ W^T is a row gather of W^T, so the forward here is an embedding-bag: one wave per
 // (packed, real) entity, each lane accumulating 4 of the 256 output channels from the selected
-// W^T rows (8-16 B per lane, L2-resident 0.5 MB table), + bias, ReLU.  The weight gradient is the
-// same sparse structure transposed: entity_embed_wgrad() scatters dpre = dout * [out > 0] into an LDS
-// [997][32] fp32 tile per (32-channel group, token chunk) - ~58 nonzero columns per token instead of
-// the 997-wide materialised one-hot and a [256 x T] x [T x 997] library GEMM (r2an: 0.46 ms).
+// W^T rows (8-16 B per lane, L2-resident 0.5 MB table), + bias, ReLU.  The weight gradient
+// (entity_embed_wgrad) runs on MFMA with the one-hot input generated in registers from the raw fields
+// instead of materialising the [T, 997] input for a library GEMM (r2an: 0.46 ms).  (A first version
+// scattered dpre into an LDS [997][32] tile with float atomics: 7.6 ms - LDS atomics are slow.)
 #include "../common.h"
 #include "../kernels.h"
 #include <hip/hip_fp16.h>
@@ -101,82 +101,115 @@ __global__ __launch_bounds__(256) void entity_onehot_kernel(EntityFields f, cons
 }
 
 
-// dW partials: workgroup (chunk, channel group g) accumulates, for tokens of its chunk, dpre[t][32 g + c]
-// times each nonzero input column of token t into acc[col][c] (LDS float atomics; lanes 0-31 / 32-63
-// take two tokens, lane c = channel), then writes its [32][K_in] block (and the 32 bias sums) into row
-// `chunk` of part [nchunk][256 * K_in + 256] (reduced over chunks afterwards).  Tokens go in passes of
-// 128: the pass's field values are first staged in LDS by all threads (independent loads, so their
-// latency overlaps - read one field at a time per token they serialised: 8.6 ms, r2ap), and each
-// wave fetches its 16 tokens' dpre before scattering.
-constexpr int kEwKin = 1024;   // LDS rows (K_in <= 1024)
-constexpr int kEwPass = 128;   // tokens per pass
+// Weight gradient on the matrix cores: dW [256][K_in] = dpre^T X with the sparse X built per step.
+// Workgroup = (64-channel slice cs, token chunk), 8 waves; wave w owns output columns 128 w .. 128 w + 127
+// (8 column tiles x 4 channel tiles of 16x16x32 MFMA accumulators).  Per 32-token step: dpre = dout *
+// [out > 0] of the slice is staged transposed in LDS ([64 n][32 t], the A operand), and X^T
+// ([1024 cols][32 t] bf16, zeroed each step) receives the step's ~58 nonzeros per token, one thread per
+// (token, field) pair - the B fragments are then plain 16-B row reads.  Column K_in (< 1024) is a ones
+// column whose accumulator is db.  The next step's dout / out / field values are loaded during the
+// current step's MFMAs.  Partials: part[chunk] = [256 * K_in] dW | [256] db, reduced over chunks.
+// (Per-lane generation of X from the field values was VALU-bound: 0.56 ms.)
+typedef __attribute__((ext_vector_type(8))) __bf16 ew_bf8;
+typedef __attribute__((ext_vector_type(4))) float ew_f4;
+constexpr int kEwStep = 32, kEwDP = kEwStep + 8;   // tokens per MFMA step, padded LDS row (bf16)
+
 template <typename TD>
-__global__ __launch_bounds__(256) void entity_wgrad_kernel(EntityFields f, const int64_t* __restrict__ index,
+__global__ __launch_bounds__(512) void entity_wgrad_kernel(EntityFields f, const int64_t* __restrict__ index,
                                                            const TD* __restrict__ dout, const TD* __restrict__ out,
                                                            float* __restrict__ part, long T, int K_in, int nchunk) {
-  __shared__ float acc[kEwKin * 32 + 32];   // [K_in][32] (+ 32 bias sums); static: > 64 KB
-  __shared__ float fv[kMaxFields][kEwPass];
-  const int g = blockIdx.x & 7, chunk = blockIdx.x >> 3;
-  const int tid = threadIdx.x, c = tid & 31, half = (tid >> 5) & 1, w = tid >> 6;
-  for (int i = tid; i < K_in * 32 + 32; i += 256) acc[i] = 0.f;
+  __shared__ __attribute__((aligned(16))) bf16_t dT[64 * kEwDP];
+  __shared__ __attribute__((aligned(16))) bf16_t xT[1024 * kEwDP];
+  const int cs = blockIdx.x & 3, chunk = blockIdx.x >> 2;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, lr = l & 15, lg = l >> 4;
+  ew_f4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = ew_f4{0.f, 0.f, 0.f, 0.f};
   const long per = (T + nchunk - 1) / nchunk;
   const long t0 = chunk * per, t1 = t0 + per < T ? t0 + per : T;
-  float db = 0.f;
-  for (long base = t0; base < t1; base += kEwPass) {
-    __syncthreads();   // previous pass consumed (and acc zeroed)
+  const int tt_d = tid >> 4, c4 = 4 * (tid & 15);
+  float dreg[4], freg[3];
+  auto load_step = [&](long base) {
     {
-      const int tl = tid & (kEwPass - 1), fh = tid >> 7;
-      const long t = base + tl < t1 ? base + tl : t0;
-      const long src = index[t];
-      float vals[kMaxFields / 2];
+      const long t = base + tt_d;
+      const bool ok = t < t1;
+      const long o = (ok ? t : t0) * 256 + 64 * cs + c4;
 #pragma unroll
-      for (int i = 0; i < kMaxFields / 2; ++i) {
-        const int k = 2 * i + fh;
-        vals[i] = k < f.n ? load_field(f.ptr[k], f.dtype[k], src) : 0.f;
+      for (int e = 0; e < 4; ++e) {
+        const float ov = Cvt<TD>::load(out, o + e), dv = Cvt<TD>::load(dout, o + e);
+        dreg[e] = (ok && ov > 0.f) ? dv : 0.f;
       }
-#pragma unroll
-      for (int i = 0; i < kMaxFields / 2; ++i)
-        if (2 * i + fh < f.n) fv[2 * i + fh][tl] = vals[i];
     }
-    // this lane's 16 tokens of the pass: dpre = dout * [out > 0]
-    float dv[kEwPass / 8];
 #pragma unroll
-    for (int j = 0; j < kEwPass / 8; ++j) {
-      const long t = base + 2 * w + half + 8 * j;
-      const long o = (t < t1 ? t : t0) * 256 + 32 * g + c;
-      const float ov = Cvt<TD>::load(out, o), dd = Cvt<TD>::load(dout, o);
-      dv[j] = (t < t1 && ov > 0.f) ? dd : 0.f;
+    for (int r = 0; r < 3; ++r) {
+      const int i = tid + 512 * r;
+      const int k = i / kEwStep, tt = i - k * kEwStep;
+      const long t = base + tt < t1 ? base + tt : t0;
+      freg[r] = k < f.n ? load_field(f.ptr[k], f.dtype[k], index[t]) : 0.f;
     }
+  };
+  static_assert(kMaxFields * kEwStep <= 3 * 512, "field staging: 3 values per thread");
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  if (t0 < t1) load_step(t0);
+  for (long base = t0; base < t1; base += kEwStep) {
+    __syncthreads();   // previous step's tiles consumed
+    // zero X^T (1024 rows x 64 B of data per row; the pad columns are never read)
+    for (int i = tid; i < 1024 * 4; i += 512) *reinterpret_cast<uint4*>(xT + (i >> 2) * kEwDP + 8 * (i & 3)) = z4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dT[(c4 + e) * kEwDP + tt_d] = f2bf(dreg[e]);
     __syncthreads();
-#pragma unroll 1
-    for (int j = 0; j < kEwPass / 8; ++j) {
-      const int tl = 2 * w + half + 8 * j;
-      if (base + tl >= t1) break;
-      const float d = dv[j];
-      db += d;
-      for (int k = 0; k < f.n; ++k) {
-        const float v = fv[k][tl];
+    if (tid < kEwStep) xT[K_in * kEwDP + tid] = base + tid < t1 ? 0x3F80 : 0;   // ones column (db)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {   // scatter the nonzeros of (token tt, field k)
+      const int i = tid + 512 * r;
+      const int k = i / kEwStep, tt = i - k * kEwStep;
+      if (k < f.n && base + tt < t1) {
+        const float v = freg[r];
         const int off = f.offset[k], width = f.width[k];
         if (f.kind[k] == FIELD_ONE_HOT) {
-          atomicAdd(&acc[(off + clampi(static_cast<int>(v), 0, width - 1)) * 32 + c], d);
+          xT[(off + clampi(static_cast<int>(v), 0, width - 1)) * kEwDP + tt] = 0x3F80;
         } else if (f.kind[k] == FIELD_BINARY) {
           const int iv = clampi(static_cast<int>(v), 0, (1 << width) - 1);
           for (int bit = 0; bit < width; ++bit)
-            if ((iv >> (width - 1 - bit)) & 1) atomicAdd(&acc[(off + bit) * 32 + c], d);
-        } else if (v != 0.f) {
-          atomicAdd(&acc[off * 32 + c], d * v);
+            if ((iv >> (width - 1 - bit)) & 1) xT[(off + bit) * kEwDP + tt] = 0x3F80;
+        } else {
+          xT[off * kEwDP + tt] = f2bf(v);
         }
       }
     }
+    __syncthreads();
+    if (base + kEwStep < t1) load_step(base + kEwStep);
+    ew_bf8 af[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const uint4 u = *reinterpret_cast<const uint4*>(dT + (16 * nt + lr) * kEwDP + 8 * lg);
+      __builtin_memcpy(&af[nt], &u, 16);
+    }
+#pragma unroll
+    for (int ct = 0; ct < 8; ++ct) {
+      const uint4 u = *reinterpret_cast<const uint4*>(xT + (128 * w + 16 * ct + lr) * kEwDP + 8 * lg);
+      ew_bf8 bx;
+      __builtin_memcpy(&bx, &u, 16);
+#pragma unroll
+      for (int nt = 0; nt < 4; ++nt) acc[ct][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[nt], bx, acc[ct][nt], 0, 0, 0);
+    }
   }
-  atomicAdd(&acc[K_in * 32 + c], db);
-  __syncthreads();
+  // C[n = 16 nt + 4 lg + i][col = 128 w + 16 ct + lr]
   float* row = part + static_cast<long>(chunk) * (256L * K_in + 256);
-  for (int i = tid; i < 32 * K_in; i += 256) {
-    const int cc = i / K_in, col = i - cc * K_in;   // consecutive threads -> consecutive columns
-    row[static_cast<long>(32 * g + cc) * K_in + col] = acc[col * 32 + cc];
+#pragma unroll
+  for (int ct = 0; ct < 8; ++ct) {
+    const int col = 128 * w + 16 * ct + lr;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = 64 * cs + 16 * nt + 4 * lg + i;
+        if (col < K_in) row[static_cast<long>(n) * K_in + col] = acc[ct][nt][i];
+        else if (col == K_in) row[256L * K_in + n] = acc[ct][nt][i];
+      }
   }
-  if (tid < 32) row[256L * K_in + 32 * g + tid] = acc[K_in * 32 + tid];
 }
 
 }  // namespace
@@ -198,18 +231,18 @@ void entity_embed_fwd(const EntityFields& f, const int64_t* index, const void* w
 }
 
 int entity_wgrad_chunks(long T) {
-  long n = (T + 2047) / 2048;   // ~2k tokens per workgroup, <= 64 chunks (x 8 channel groups)
+  long n = (T + 1023) / 1024;   // ~1k+ tokens per workgroup, <= 64 chunks (x 4 channel slices)
   return static_cast<int>(n < 1 ? 1 : (n > 64 ? 64 : n));
 }
 
 void entity_embed_wgrad(const EntityFields& f, const int64_t* index, const void* dout, const void* out, int dt,
                         float* part, long T, int K_in, int nchunk, hipStream_t s) {
-  const dim3 grid(static_cast<unsigned>(nchunk) * 8);
+  const dim3 grid(static_cast<unsigned>(nchunk) * 4);
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(entity_wgrad_kernel<bf16_t>, grid, dim3(256), 0, s, f, index, static_cast<const bf16_t*>(dout),
+    hipLaunchKernelGGL(entity_wgrad_kernel<bf16_t>, grid, dim3(512), 0, s, f, index, static_cast<const bf16_t*>(dout),
                        static_cast<const bf16_t*>(out), part, T, K_in, nchunk);
   else
-    hipLaunchKernelGGL(entity_wgrad_kernel<float>, grid, dim3(256), 0, s, f, index, static_cast<const float*>(dout),
+    hipLaunchKernelGGL(entity_wgrad_kernel<float>, grid, dim3(512), 0, s, f, index, static_cast<const float*>(dout),
                        static_cast<const float*>(out), part, T, K_in, nchunk);
 }
 
