@@ -287,6 +287,19 @@ at::Tensor entity_onehot(const std::vector<at::Tensor>& fields, const std::vecto
   return X;
 }
 
+// a [R, 32] @ W [32, N] (bf16) given wT = W^T [N, 32]
+at::Tensor mm_k32(const at::Tensor& a, const at::Tensor& wT) {
+  check_cuda(a, "a");
+  check_cuda(wT, "wT");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && wT.scalar_type() == at::kBFloat16 && a.is_contiguous() &&
+                  wT.is_contiguous() && a.dim() == 2 && a.size(1) == 32 && wT.dim() == 2 && wT.size(1) == 32 &&
+                  wT.size(0) % 16 == 0, "mm_k32: a [R, 32], wT [N, 32] bf16 contiguous, N % 16 == 0");
+  c10::hip::HIPGuard g(a.device().index());
+  auto out = at::empty({a.size(0), wT.size(0)}, a.options());
+  as::mm_k32(a.data_ptr(), wT.data_ptr(), out.data_ptr(), a.size(0), static_cast<int>(wT.size(0)), stream());
+  return out;
+}
+
 // (dW [256, k_in] fp32, db [256] fp32) of relu(X W^T + b) from dout and the ReLU output (same dtype)
 std::vector<at::Tensor> entity_embed_wgrad(const std::vector<at::Tensor>& fields, const std::vector<int64_t>& kind,
                                            const std::vector<int64_t>& offset, const std::vector<int64_t>& width,
@@ -1060,6 +1073,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("upsample2x_fwd", &upsample2x_fwd);
   m.def("upsample2x_bwd", &upsample2x_bwd);
   m.def("entity_embed_wgrad", &entity_embed_wgrad);
+  m.def("mm_k32", &mm_k32);
   m.def("spatial_embed_fwd", &spatial_embed_fwd);
   m.def("spatial_gather_rows", &spatial_gather_rows);
   m.def("spatial_dense_input", &spatial_dense_input);

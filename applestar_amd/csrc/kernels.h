@@ -250,6 +250,10 @@ void bo_encoder_fwd(const void* bo, const void* loc, int idt, const BoWeights& w
 void bo_encoder_bwd(const void* bo, const void* loc, int idt, const BoWeights& w, int wdt, const float* save,
                     const float* dmean, float* grad, long B, int replicas, hipStream_t st);
 
+// ---- gemm_k32.hip ------------------------------------------------------------------------------
+// out [R][N] = a [R][32] . W [32][N], bf16; wT = W^T [N][32] contiguous; N % 16 == 0
+void mm_k32(const void* a, const void* wT, void* out, long R, int N, hipStream_t s);
+
 // ---- resmlp.hip -------------------------------------------------------------------------------
 // n <= kResMax x ResFCBlock2(256): x <- LN(fc2(relu(fc1(x))) + x); linear weights / biases bf16, LN fp32
 constexpr int kResMax = 16;

@@ -707,7 +707,14 @@ class _Linear(torch.autograd.Function):
                                   y.view(1, 1, R, N), True).view(R, N)
         else:
             dy = dy.to(torch.bfloat16).contiguous()
-        dx = torch.mm(dy, w) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if dy.shape[1] == 32 and x2.shape[1] % 16 == 0 and dy.is_contiguous():
+                # thin-K product (the heads' 256 -> 32 key projections): one MFMA per output tile, a pure
+                # store stream (gemm_k32.hip); the library took 0.19 ms per 196k-row call
+                dx = _C.mm_k32(dy, w.t().contiguous())
+            else:
+                dx = torch.mm(dy, w)
         has_b = ctx.b_dtype is not None
         dw, db = _C.wgrad(dy, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
         return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None), None

@@ -531,6 +531,31 @@ def test_native_linear_autocast_grads_match_fp32():
         assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
 
 
+@pytest.mark.parametrize('K', [256, 32])
+def test_native_linear_thin_output_dx(K):
+    """N = 32 outputs: the input gradient runs the K = 32 MFMA kernel (gemm_k32.hip); R not a multiple
+    of its 64-row block."""
+    from applestar_amd import ops
+    from applestar_amd.ops import native
+    torch.manual_seed(17)
+    R = 5003
+    x = torch.randn(R, K, device=DEV, requires_grad=True)
+    w = (torch.randn(32, K, device=DEV) / K ** 0.5).requires_grad_()
+    b = torch.randn(32, device=DEV, requires_grad=True)
+    with torch.autocast('cuda', dtype=torch.bfloat16):
+        y = ops.linear(x, w, b)
+    g = torch.randn(R, 32, device=DEV)
+    y.float().backward(g)
+    xs, ws, bs = (t.detach().clone().requires_grad_() for t in (x, w, b))
+    (xs @ ws.t() + bs).backward(g)
+    for a, r in ((x.grad, xs.grad), (w.grad, ws.grad), (b.grad, bs.grad)):
+        assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
+    C = native.ensure_loaded()
+    a = torch.randn(130, 32, device=DEV).to(torch.bfloat16)
+    wt = torch.randn(48, 32, device=DEV).to(torch.bfloat16)
+    assert _err(C.mm_k32(a, wt), a.float() @ wt.float().t()) < 2e-2 * 8
+
+
 def test_native_linear_pads_odd_k():
     """K = 132 (not a multiple of 8): the reduction dim is zero-padded so the native weight-gradient
     kernel runs; grads of x, w (original shapes) and b must match fp32."""
