@@ -391,18 +391,25 @@ std::vector<at::Tensor> spatial_embed_fwd(const std::vector<at::Tensor>& planes,
 }
 
 // (dWd fp32 [32, 24], db fp32 [32]) of the spatial 1x1 projection's dense columns from dpre [B,H,W,32]
+// gate (optional): the embedding's ReLU output; dpre is then dout and the ReLU mask is applied on the fly
 std::vector<at::Tensor> spatial_dense_wgrad(const std::vector<at::Tensor>& planes, const std::vector<at::Tensor>& effects,
-                                            const at::Tensor& dpre) {
+                                            const at::Tensor& dpre, const c10::optional<at::Tensor>& gate) {
   auto sp = make_planes(planes, effects);
   const int64_t B = planes[0].size(0), H = planes[0].size(1), W = planes[0].size(2);
   const int64_t L = effects[0].size(1);
   check_cuda(dpre, "dpre");
   TORCH_CHECK(dpre.is_contiguous() && dpre.numel() == B * H * W * 32, "spatial_dense_wgrad: dpre [B,H,W,32] contiguous");
+  const void* gp = nullptr;
+  if (gate.has_value()) {
+    TORCH_CHECK(gate->is_contiguous() && gate->sizes() == dpre.sizes() && gate->scalar_type() == dpre.scalar_type(),
+                "spatial_dense_wgrad: gate like dpre");
+    gp = gate->data_ptr();
+  }
   c10::hip::HIPGuard g(dpre.device().index());
   const int nb = as::spatial_wgrad_blocks(static_cast<int>(B));
   auto f32 = dpre.options().dtype(at::kFloat);
   auto part = at::empty({nb, 32 * 24 + 32}, f32);
-  as::spatial_dense_wgrad(sp, dpre.data_ptr(), dt(dpre), part.data_ptr<float>(), static_cast<int>(B),
+  as::spatial_dense_wgrad(sp, dpre.data_ptr(), gp, dt(dpre), part.data_ptr<float>(), static_cast<int>(B),
                           static_cast<int>(H), static_cast<int>(W), static_cast<int>(L), stream());
   auto red = at::empty({32 * 24 + 32}, f32);
   as::column_reduce(part.data_ptr<float>(), red.data_ptr<float>(), nb, 32 * 24 + 32, stream());
@@ -410,12 +417,19 @@ std::vector<at::Tensor> spatial_dense_wgrad(const std::vector<at::Tensor>& plane
 }
 
 at::Tensor spatial_gather_rows(const at::Tensor& dpre, const at::Tensor& ex, const at::Tensor& ey,
-                               const at::Tensor& entity_num, int64_t N) {
+                               const at::Tensor& entity_num, int64_t N, const c10::optional<at::Tensor>& gate) {
   check_cuda(dpre, "dpre");
+  TORCH_CHECK(dpre.is_contiguous() && dpre.dim() == 4 && dpre.size(3) == 32, "spatial_gather_rows: dpre [B,H,W,32]");
+  const void* gp = nullptr;
+  if (gate.has_value()) {
+    TORCH_CHECK(gate->is_contiguous() && gate->sizes() == dpre.sizes() && gate->scalar_type() == dpre.scalar_type(),
+                "spatial_gather_rows: gate like dpre");
+    gp = gate->data_ptr();
+  }
   const int64_t B = dpre.size(0), H = dpre.size(1), W = dpre.size(2);
   c10::hip::HIPGuard g(dpre.device().index());
   auto drows = at::empty({B, N, 32}, dpre.options());
-  as::gather_rows(dpre.data_ptr(), dt(dpre), ex.data_ptr<uint8_t>(), ey.data_ptr<uint8_t>(),
+  as::gather_rows(dpre.data_ptr(), gp, dt(dpre), ex.data_ptr<uint8_t>(), ey.data_ptr<uint8_t>(),
                   entity_num.data_ptr<int64_t>(), drows.data_ptr(), B, N, H, W, stream());
   return drows;
 }
@@ -1075,9 +1089,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("entity_embed_wgrad", &entity_embed_wgrad);
   m.def("mm_k32", &mm_k32);
   m.def("spatial_embed_fwd", &spatial_embed_fwd);
-  m.def("spatial_gather_rows", &spatial_gather_rows);
+  m.def("spatial_gather_rows", &spatial_gather_rows, py::arg("dpre"), py::arg("ex"), py::arg("ey"),
+        py::arg("entity_num"), py::arg("N"), py::arg("gate") = py::none());
   m.def("spatial_dense_input", &spatial_dense_input);
-  m.def("spatial_dense_wgrad", &spatial_dense_wgrad);
+  m.def("spatial_dense_wgrad", &spatial_dense_wgrad, py::arg("planes"), py::arg("effects"), py::arg("dpre"),
+        py::arg("gate") = py::none());
   m.def("varlen_attn_fwd", &varlen_attn_fwd);
   m.def("varlen_attn_bwd", &varlen_attn_bwd);
   m.def("su_sample", &su_sample);

@@ -104,8 +104,9 @@ void spatial_dense_input(const SpatialPlanes& sp, const uint8_t* bits, void* X, 
 // pre[b, y*W+x, :] += rows[b, n, :] (32 channels) for n < entity_num[b]; and its transpose (gather)
 void scatter_add_rows(const void* rows, int dt, const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num,
                       float* pre, int B, int N, int H, int W, hipStream_t s);
-void gather_rows(const void* dpre, int dt, const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num,
-                 void* drows, int B, int N, int H, int W, hipStream_t s);
+// gate (nullable): ReLU output; dpre is then treated as dout * [gate > 0]
+void gather_rows(const void* dpre, const void* gate, int dt, const uint8_t* ex, const uint8_t* ey,
+                 const int64_t* entity_num, void* drows, int B, int N, int H, int W, hipStream_t s);
 void relu_cast(const float* x, void* y, int dt, long n, hipStream_t s);
 // fused: out [B,H,W,32] = relu(bias + Wd . dense(pixel) + sum of the rows of entities at the pixel)
 void spatial_embed_fused(const SpatialPlanes& sp, const float* wd, const float* bias, const void* rows, int rows_dt,
@@ -113,8 +114,8 @@ void spatial_embed_fused(const SpatialPlanes& sp, const float* wd, const float* 
                          int N, int H, int W, int L, hipStream_t s);
 // per-workgroup partial rows [spatial_wgrad_blocks(B)][32*24 + 32] of dWd (n-major) and db from dpre [B*H*W, 32]
 int spatial_wgrad_blocks(int B);
-void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, int dt, float* part, int B, int H, int W, int L,
-                         hipStream_t s);
+void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, const void* gate, int dt, float* part, int B, int H,
+                         int W, int L, hipStream_t s);
 
 // ---- attention.hip ---------------------------------------------------------------------------
 // Packed varlen MHA, head dim 128, bf16. qkv [T][3][H][128], cu [S+1] int32, out [T][H][128],

@@ -175,8 +175,10 @@ __global__ __launch_bounds__(256) void scatter_add_rows_kernel(const T* __restri
   atomicAdd(pre + (static_cast<long>(b) * H * W + static_cast<long>(y) * W + x) * 32 + c, Cvt<T>::load(rows, i));
 }
 
+// gate (nullable): the embedding's ReLU output - dpre is then dout * [gate > 0]
 template <typename T>
-__global__ __launch_bounds__(256) void gather_rows_kernel(const T* __restrict__ dpre, const uint8_t* __restrict__ ex,
+__global__ __launch_bounds__(256) void gather_rows_kernel(const T* __restrict__ dpre, const T* __restrict__ gate,
+                                                          const uint8_t* __restrict__ ex,
                                                           const uint8_t* __restrict__ ey,
                                                           const int64_t* __restrict__ entity_num, T* __restrict__ drows,
                                                           int B, int N, int H, int W) {
@@ -191,7 +193,9 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const T* __restrict__ 
     int x = ex[bn], y = ey[bn];
     x = x < W ? x : W - 1;
     y = y < H ? y : H - 1;
-    v = Cvt<T>::load(dpre, (static_cast<long>(b) * H * W + static_cast<long>(y) * W + x) * 32 + c);
+    const long o = (static_cast<long>(b) * H * W + static_cast<long>(y) * W + x) * 32 + c;
+    v = Cvt<T>::load(dpre, o);
+    if (gate != nullptr && !(Cvt<T>::load(gate, o) > 0.f)) v = 0.f;
   }
   Cvt<T>::store(drows, i, v);
 }
@@ -341,6 +345,7 @@ __global__ __launch_bounds__(256) void spatial_embed_fused_kernel(SpatialPlanes 
 // are summed in LDS and each workgroup writes one partial row [32 * 24 + 32] (reduced afterwards).
 template <typename TD>
 __global__ __launch_bounds__(256) void spatial_dense_wgrad_kernel(SpatialPlanes sp, const TD* __restrict__ dpre,
+                                                                  const TD* __restrict__ gate,
                                                                   float* __restrict__ part, int H, int W, int L,
                                                                   int tiles, int wg_per_obs) {
   __shared__ uint32_t eb[kSpTile];
@@ -366,7 +371,7 @@ __global__ __launch_bounds__(256) void spatial_dense_wgrad_kernel(SpatialPlanes 
     __syncthreads();
     for (int pl = slot; pl < np; pl += 8) {
       const long pix = static_cast<long>(b) * HW + p0 + pl;
-      const float d = Cvt<TD>::load(dpre, pix * 32 + n);
+      const float d = (gate == nullptr || Cvt<TD>::load(gate, pix * 32 + n) > 0.f) ? Cvt<TD>::load(dpre, pix * 32 + n) : 0.f;
       acc[24] += d;
       acc[0] += d * (static_cast<float>(sp.height[pix]) * (1.f / 256.f));
       const int widths[6] = {4, 2, 5, 2, 2, 2};
@@ -554,7 +559,22 @@ __global__ __launch_bounds__(256) void spatial_embed_mfma_kernel(SpatialPlanes s
 
 constexpr int kSpP = kSpTile + 8;  // padded bf16 LDS row of the dpre^T image
 
+// 8 bf16 of v kept where the matching bf16 of g is > 0 (sign clear, not +0), zeroed elsewhere
+__device__ __forceinline__ uint4 relu_gate8(uint4 v, uint4 g) {
+  uint32_t a[4] = {v.x, v.y, v.z, v.w};
+  const uint32_t b[4] = {g.x, g.y, g.z, g.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint32_t lo = b[e] & 0xffffu, hi = b[e] >> 16;
+    const uint32_t mlo = (!(lo & 0x8000u) && (lo & 0x7fffu)) ? 0xffffu : 0u;
+    const uint32_t mhi = (!(hi & 0x8000u) && (hi & 0x7fffu)) ? 0xffff0000u : 0u;
+    a[e] &= mlo | mhi;
+  }
+  return make_uint4(a[0], a[1], a[2], a[3]);
+}
+
 __global__ __launch_bounds__(256) void spatial_dense_wgrad_mfma_kernel(SpatialPlanes sp, const bf16_t* __restrict__ dpre,
+                                                                       const bf16_t* __restrict__ gate,
                                                                        float* __restrict__ part, int H, int W, int L,
                                                                        int tiles, int wg_per_obs) {
   __shared__ __attribute__((aligned(16))) bf16_t dT[32 * kSpP];
@@ -593,6 +613,11 @@ __global__ __launch_bounds__(256) void spatial_dense_wgrad_mfma_kernel(SpatialPl
         r0[k] = pp < np ? *reinterpret_cast<const uint4*>(dpre + (base + pp) * 32 + h16 + 8 * k) : make_uint4(0, 0, 0, 0);
         r1[k] = pp + 1 < np ? *reinterpret_cast<const uint4*>(dpre + (base + pp + 1) * 32 + h16 + 8 * k)
                             : make_uint4(0, 0, 0, 0);
+        if (gate != nullptr) {
+          if (pp < np) r0[k] = relu_gate8(r0[k], *reinterpret_cast<const uint4*>(gate + (base + pp) * 32 + h16 + 8 * k));
+          if (pp + 1 < np)
+            r1[k] = relu_gate8(r1[k], *reinterpret_cast<const uint4*>(gate + (base + pp + 1) * 32 + h16 + 8 * k));
+        }
       }
       uint32_t* d32 = reinterpret_cast<uint32_t*>(dT);
 #pragma unroll
@@ -721,17 +746,17 @@ void scatter_add_rows(const void* rows, int dt, const uint8_t* ex, const uint8_t
                        entity_num, pre, B, N, H, W);
 }
 
-void gather_rows(const void* dpre, int dt, const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num,
-                 void* drows, int B, int N, int H, int W, hipStream_t s) {
+void gather_rows(const void* dpre, const void* gate, int dt, const uint8_t* ex, const uint8_t* ey,
+                 const int64_t* entity_num, void* drows, int B, int N, int H, int W, hipStream_t s) {
   const long n = static_cast<long>(B) * N * 32;
   if (n == 0) return;
   dim3 grid(static_cast<unsigned>((n + 255) / 256));
   if (dt == DT_BF16)
-    hipLaunchKernelGGL(gather_rows_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(dpre), ex, ey,
-                       entity_num, static_cast<bf16_t*>(drows), B, N, H, W);
+    hipLaunchKernelGGL(gather_rows_kernel<bf16_t>, grid, dim3(256), 0, s, static_cast<const bf16_t*>(dpre),
+                       static_cast<const bf16_t*>(gate), ex, ey, entity_num, static_cast<bf16_t*>(drows), B, N, H, W);
   else
-    hipLaunchKernelGGL(gather_rows_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(dpre), ex, ey,
-                       entity_num, static_cast<float*>(drows), B, N, H, W);
+    hipLaunchKernelGGL(gather_rows_kernel<float>, grid, dim3(256), 0, s, static_cast<const float*>(dpre),
+                       static_cast<const float*>(gate), ex, ey, entity_num, static_cast<float*>(drows), B, N, H, W);
 }
 
 void spatial_embed_fused(const SpatialPlanes& sp, const float* wd, const float* bias, const void* rows, int rows_dt,
@@ -755,19 +780,19 @@ void spatial_embed_fused(const SpatialPlanes& sp, const float* wd, const float* 
 
 int spatial_wgrad_blocks(int B) { return B * 4; }
 
-void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, int dt, float* part, int B, int H, int W, int L,
-                         hipStream_t s) {
+void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, const void* gate, int dt, float* part, int B, int H,
+                         int W, int L, hipStream_t s) {
   const int tiles = (H * W + kSpTile - 1) / kSpTile;
   if (B == 0) return;
   if (dt == DT_BF16 && spatial_mfma())
     hipLaunchKernelGGL(spatial_dense_wgrad_mfma_kernel, dim3(static_cast<unsigned>(B) * 4), dim3(256), 0, s, sp,
-                       static_cast<const bf16_t*>(dpre), part, H, W, L, tiles, 4);
+                       static_cast<const bf16_t*>(dpre), static_cast<const bf16_t*>(gate), part, H, W, L, tiles, 4);
   else if (dt == DT_BF16)
     hipLaunchKernelGGL(spatial_dense_wgrad_kernel<bf16_t>, dim3(static_cast<unsigned>(B) * 4), dim3(256), 0, s, sp,
-                       static_cast<const bf16_t*>(dpre), part, H, W, L, tiles, 4);
+                       static_cast<const bf16_t*>(dpre), static_cast<const bf16_t*>(gate), part, H, W, L, tiles, 4);
   else
     hipLaunchKernelGGL(spatial_dense_wgrad_kernel<float>, dim3(static_cast<unsigned>(B) * 4), dim3(256), 0, s, sp,
-                       static_cast<const float*>(dpre), part, H, W, L, tiles, 4);
+                       static_cast<const float*>(dpre), static_cast<const float*>(gate), part, H, W, L, tiles, 4);
 }
 
 void relu_cast(const float* x, void* y, int dt, long n, hipStream_t s) {

@@ -237,7 +237,9 @@ def test_spatial_embed_partial_tile(crowded):
     pre = pre + ent
     ref = torch.relu(pre)
     assert _err(out, ref) < 2e-2 * max(1, ref.abs().max().item())
-    g = torch.randn_like(ref)
+    # channels_last gradient: the NHWC-contiguous dout takes the fused ReLU-gate path of the backward
+    # (the NCHW gradient of test_spatial_embed_matches_reference_planes takes the act_grad path)
+    g = torch.randn_like(ref).contiguous(memory_format=torch.channels_last)
     out.backward(g.to(out.dtype))
     (pre * (out.detach().float() > 0)).backward(g.to(torch.bfloat16).float())
     assert _err(w.grad, wr.grad) < 2e-2 * max(1, wr.grad.abs().max().item())
