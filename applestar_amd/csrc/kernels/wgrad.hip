@@ -124,6 +124,19 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgBatch P, long part_s
     }
   }
 
+  // conv form: image coordinates of each B chunk's row, advanced incrementally by BR rows per stage (a
+  // 64-bit modulo + two divisions per chunk per stage were the bulk of the loop's VALU work)
+  int cy[C::B_IT], cx[C::B_IT];
+  const int adv_q = C::BR / W, adv_r = C::BR - (C::BR / W) * W;
+  if (CONV) {
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const long r = r_begin + b_rr[i];
+      const int rem = static_cast<int>(r % HW);
+      cy[i] = rem / W;
+      cx[i] = rem - cy[i] * W;
+    }
+  }
   uint4 ra[C::A_IT], rb[C::B_IT];
   auto load_regs = [&](long rs) {
 #pragma unroll
@@ -139,10 +152,17 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgBatch P, long part_s
       const bool ok = b_col[i] < K && r < r_end;
       int off = kOOB;
       if (CONV) {
-        const int rem = static_cast<int>(r % HW);
-        const int yy = rem / W + b_dy[i], xx = rem % W + b_dx[i];
+        const int yy = cy[i] + b_dy[i], xx = cx[i] + b_dx[i];
         if (ok && yy >= 0 && yy < H && xx >= 0 && xx < W)
           off = static_cast<int>(((r + b_shift[i]) * Cin + b_c[i]) * 2);
+        // advance this chunk's row by BR for the next stage
+        cx[i] += adv_r;
+        cy[i] += adv_q;
+        if (cx[i] >= W) {
+          cx[i] -= W;
+          cy[i] += 1;
+        }
+        while (cy[i] >= H) cy[i] -= H;
       } else if (ok) {
         off = static_cast<int>((r * K + b_col[i]) * 2);
       }
