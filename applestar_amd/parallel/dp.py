@@ -21,6 +21,42 @@ import torch.distributed as dist
 from . import dist as pdist
 
 
+def _cur_stream(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device) if t.is_cuda else None
+
+
+def join_hook_stream(main, t: Optional[torch.Tensor] = None):
+    """Called from a gradient hook.  The autograd engine runs a parameter's hooks on the stream its
+    gradient was produced on: the stream its forward ran on (the scalar encoder runs on a side stream,
+    models/model.py ``_side_stream_call``).  Bucket copies and collectives are always issued on ``main``
+    (the stream backward was started from), so ``main`` must first wait for that producer stream, and a
+    hook-captured gradient ``t`` read later on ``main`` must not be recycled by the allocator early.
+    Without this, a bucket completed from a side-stream hook was copied / reduced while main-stream
+    gradients of the same bucket were still being computed (non-finite gradients with world > 1)."""
+    if main is None:
+        return
+    cur = torch.cuda.current_stream(main.device)
+    if cur != main:
+        main.wait_stream(cur)
+        if t is not None:
+            t.record_stream(main)
+
+
+class _on_stream:
+    """``with torch.cuda.stream(main)`` that is a no-op for CPU (``main`` None)."""
+
+    def __init__(self, main):
+        self.ctx = torch.cuda.stream(main) if main is not None else None
+
+    def __enter__(self):
+        if self.ctx is not None:
+            self.ctx.__enter__()
+
+    def __exit__(self, *exc):
+        if self.ctx is not None:
+            self.ctx.__exit__(*exc)
+
+
 class _Bucket:
     __slots__ = ('params', 'flat', 'ready', 'handle', 'comm')
 
@@ -70,6 +106,7 @@ class GradientReducer:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
         self.use_avg = self.world > 1 and dist.get_backend(group) == 'nccl'
+        self._main = None        # stream backward was started from (bucket collectives are issued there)
 
     def _add_bucket(self, params):
         b = _Bucket(params, params[0].dtype, params[0].device)
@@ -101,10 +138,12 @@ class GradientReducer:
         b.handle = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
 
     def _on_grad(self, p):
+        join_hook_stream(self._main)
         b = self._owner[p]
         b.ready += 1
         if b.ready == len(b.params):
-            self._launch(b)
+            with _on_stream(self._main):
+                self._launch(b)
 
     def backward(self, loss: torch.Tensor):
         """``loss.backward()`` into the bucket views.
@@ -115,6 +154,7 @@ class GradientReducer:
         ``add_`` into the zeroed buckets - ~240 launches per RL step) and written with one multi-tensor
         copy."""
         if self.world > 1:
+            self._main = _cur_stream(loss)
             loss.backward()
             return
         grads = torch.autograd.grad(loss, self.params, allow_unused=True)

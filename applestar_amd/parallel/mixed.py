@@ -16,7 +16,7 @@ from typing import Dict, List
 import torch
 import torch.nn as nn
 
-from .dp import GradientReducer
+from .dp import GradientReducer, join_hook_stream, _on_stream
 
 LOWP_MODULES = (nn.Linear, nn.Conv2d, nn.ConvTranspose2d)
 
@@ -153,11 +153,13 @@ class MasterWeights:
     def _make_hook(self, p):
         def hook(g):
             if getattr(self, '_overlapped', False):
+                join_hook_stream(self._main, g)
                 b = self._bucket_of[p]
                 st = self._pending[id(b)]
                 st.append((p, g))
                 if len(st) == len(b.params):
-                    self._flush(b)
+                    with _on_stream(self._main):
+                        self._flush(b)
             return None
         return hook
 
@@ -185,6 +187,7 @@ class MasterWeights:
         self._comm_buffers()
         self._pending = {id(b): [] for b in self.reducer.buckets}
         self._handles = {}
+        self._main = torch.cuda.current_stream(loss.device) if loss.is_cuda else None
         self._overlapped = True
         try:
             torch.autograd.grad(loss, self.reducer.params, allow_unused=True)

@@ -58,7 +58,15 @@ def rl_batch(batch_size: int, unroll_len: int, max_entities: int = MAX_ENTITY_NU
     tu_valid = sequence_mask(en_tb.reshape(-1), N).view(T, B, N)
     teacher['target_unit'] = teacher['target_unit'].masked_fill(~tu_valid, -1e9)
     su_valid = sequence_mask(en_tb.reshape(-1) + 1, N + 1).view(T, B, 1, N + 1)
-    teacher['selected_units'] = teacher['selected_units'].masked_fill(~su_valid, -1e9)
+    # the teacher runs the same teacher-forced selected-units head as the student (agent.py:569,
+    # model.py:76-162), so its logits carry the same masks: at step i the units already chosen at steps < i,
+    # and the end token at step 0.  Random logits there would put a ~1e9 KL on every masked unit.
+    labels = act['selected_units'].clamp(max=N)                                         # [T,B,S]
+    prev = torch.nn.functional.one_hot(labels, N + 1).bool()                             # [T,B,S,N+1]
+    prev_excl = torch.cat([torch.zeros_like(prev[:, :, :1]), (torch.cumsum(prev.int(), 2) > 0)[:, :, :-1]], 2)
+    end0 = torch.zeros(T, B, MAX_SELECTED_UNITS_NUM, N + 1, dtype=torch.bool)
+    end0[:, :, 0] = torch.nn.functional.one_hot(en_tb.clamp(max=N), N + 1).bool()
+    teacher['selected_units'] = teacher['selected_units'].masked_fill(~su_valid | prev_excl | end0, -1e9)
     mask = {
         'actions_mask': am,
         'selected_units_mask': sequence_mask(su_num.reshape(-1), MAX_SELECTED_UNITS_NUM).view(T, B, -1),

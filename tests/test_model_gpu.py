@@ -1,6 +1,7 @@
 """Whole-model checks on the MI355X: the native/bf16 learner path agrees with the fp32 CPU oracle,
 and a full RL learner iteration (with native kernels) runs and updates weights."""
 import copy
+import math
 
 import pytest
 import torch
@@ -271,3 +272,30 @@ def test_stacked_lstm_pipelined_matches_layer_by_layer():
     assert (a[2] - b[2]).abs().max().item() < 1e-5
     for u, v in zip(a[3], b[3]):
         assert (u - v).abs().max().item() < 1e-4 * max(1.0, u.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_data_parallel_two_ranks_finite_and_identical(tmp_path):
+    """Two ranks (gloo, sharing the one GPU) run the bf16 master-weight learner with backward-overlapped
+    bucket all-reduces: every step's gradient norm is finite and identical on both ranks (the reduced
+    gradient), and the loss stays finite.  Regression test for bucket copies issued from a side-stream
+    gradient hook (parallel/dp.py ``join_hook_stream``)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, APPLESTAR_DIST_BACKEND='gloo')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', '29631', os.path.join(root, 'tools', 'loss_probe.py'),
+           '--steps', '3', '--batch', '2', '--unroll', '8']
+    res = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=400)
+    assert res.returncode == 0, res.stderr[-3000:]
+    recs = [json.loads(l) for l in res.stdout.splitlines() if l.startswith('{')]
+    assert len(recs) == 6, res.stdout[-2000:]
+    for r in recs:
+        assert math.isfinite(r['loss']) and math.isfinite(r['grad_norm']), r
+        assert 'nonfinite_grads' not in r, r
+    for s in range(3):
+        a, b = [r['grad_norm'] for r in recs if r['step'] == s]
+        assert a == b
