@@ -1011,6 +1011,97 @@ at::Tensor act_grad_nhwc(const at::Tensor& dout, const c10::optional<at::Tensor>
   return dpre;
 }
 
+// ---------------------------------------------------------------- value-encoder spatial input (value_spatial.hip)
+// sc [P, 8] bf16 (NHWC scatter map), own / enemy [P] bool or uint8, w [16, 10] fp32, b [16] fp32 -> [P, 16] bf16
+at::Tensor vsp_fwd(const at::Tensor& sc, const at::Tensor& own, const at::Tensor& enemy, const at::Tensor& w,
+                   const at::Tensor& b) {
+  check_cuda(sc, "sc");
+  check_cuda(own, "own");
+  check_cuda(enemy, "enemy");
+  check_cuda(w, "w");
+  check_cuda(b, "b");
+  const int64_t P = sc.size(0);
+  TORCH_CHECK(sc.scalar_type() == at::kBFloat16 && sc.dim() == 2 && sc.size(1) == as::vsp_in_channels() - 2,
+              "vsp: sc [P, 8] bf16");
+  TORCH_CHECK(own.element_size() == 1 && enemy.element_size() == 1 && own.numel() == P && enemy.numel() == P,
+              "vsp: own / enemy [P] bool");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.size(0) == as::vsp_out_channels() && w.size(1) == as::vsp_in_channels()
+              && b.scalar_type() == at::kFloat && b.numel() == as::vsp_out_channels(), "vsp: w [16, 10], b [16] fp32");
+  c10::hip::HIPGuard g(sc.device().index());
+  auto out = at::empty({P, as::vsp_out_channels()}, sc.options());
+  as::vsp_fwd(sc.data_ptr(), own.data_ptr(), enemy.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(),
+              out.data_ptr(), P, stream());
+  return out;
+}
+
+// -> {dSc [P, 8] bf16, [dW | db] [16, 11] fp32}
+std::vector<at::Tensor> vsp_bwd(const at::Tensor& dout, const at::Tensor& out, const at::Tensor& sc,
+                                const at::Tensor& own, const at::Tensor& enemy, const at::Tensor& w) {
+  check_cuda(dout, "dout");
+  check_cuda(out, "out");
+  check_cuda(sc, "sc");
+  check_cuda(own, "own");
+  check_cuda(enemy, "enemy");
+  check_cuda(w, "w");
+  const int64_t P = sc.size(0);
+  TORCH_CHECK(dout.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16 && dout.sizes() == out.sizes()
+              && out.size(0) == P && out.size(1) == as::vsp_out_channels(), "vsp_bwd: dout / out [P, 16] bf16");
+  TORCH_CHECK(sc.scalar_type() == at::kBFloat16 && sc.size(1) == as::vsp_in_channels() - 2, "vsp_bwd: sc [P, 8] bf16");
+  TORCH_CHECK(own.element_size() == 1 && enemy.element_size() == 1 && own.numel() == P && enemy.numel() == P,
+              "vsp_bwd: own / enemy [P] bool");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.size(0) == as::vsp_out_channels() && w.size(1) == as::vsp_in_channels(),
+              "vsp_bwd: w [16, 10] fp32");
+  c10::hip::HIPGuard g(sc.device().index());
+  const int nblk = as::vsp_bwd_blocks(P);
+  auto dsc = at::empty_like(sc);
+  auto part = at::empty({nblk, as::vsp_out_channels() * (as::vsp_in_channels() + 1)}, sc.options().dtype(at::kFloat));
+  as::vsp_bwd(dout.data_ptr(), out.data_ptr(), sc.data_ptr(), own.data_ptr(), enemy.data_ptr(), w.data_ptr<float>(),
+              dsc.data_ptr(), part.data_ptr<float>(), P, nblk, stream());
+  return {dsc, part.sum(0).view({as::vsp_out_channels(), as::vsp_in_channels() + 1})};
+}
+
+// ---------------------------------------------------------------- location-head input (locin.hip)
+// y0 [P, 128] bf16 (skip W_s^T + b), p [B, 4*HW] bf16 (fc output), wp [128, 4] fp32 -> relu(y0 + W_p relu(p))
+at::Tensor loc_in_fwd(const at::Tensor& y0, const at::Tensor& p, const at::Tensor& wp, int64_t HW) {
+  check_cuda(y0, "y0");
+  check_cuda(p, "p");
+  check_cuda(wp, "wp");
+  TORCH_CHECK(y0.scalar_type() == at::kBFloat16 && p.scalar_type() == at::kBFloat16 && wp.scalar_type() == at::kFloat,
+              "loc_in: bf16 y0 / p, fp32 wp");
+  TORCH_CHECK(y0.dim() == 2 && wp.dim() == 2 && as::loc_in_supported(static_cast<int>(y0.size(1)),
+              static_cast<int>(wp.size(1))) && wp.size(0) == y0.size(1), "loc_in: [P,128] x [128,4]");
+  TORCH_CHECK(HW > 0 && y0.size(0) % HW == 0 && p.numel() == (y0.size(0) / HW) * wp.size(1) * HW, "loc_in: p shape");
+  c10::hip::HIPGuard g(y0.device().index());
+  auto out = at::empty_like(y0);
+  as::loc_in_fwd(y0.data_ptr(), p.data_ptr(), wp.data_ptr<float>(), out.data_ptr(), y0.size(0), static_cast<int>(HW),
+                 stream());
+  return out;
+}
+
+// -> {dY * (y > 0) [P,128] bf16, dp [B, 4*HW] bf16, dW_p [128, 4] fp32}
+std::vector<at::Tensor> loc_in_bwd(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& p, const at::Tensor& wp,
+                                   int64_t HW) {
+  check_cuda(dy, "dy");
+  check_cuda(y, "y");
+  check_cuda(p, "p");
+  check_cuda(wp, "wp");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 && dy.sizes() == y.sizes(),
+              "loc_in_bwd: bf16 dy / y of one shape");
+  TORCH_CHECK(p.scalar_type() == at::kBFloat16 && wp.scalar_type() == at::kFloat, "loc_in_bwd: dtypes");
+  TORCH_CHECK(y.dim() == 2 && as::loc_in_supported(static_cast<int>(y.size(1)), static_cast<int>(wp.size(1))) &&
+              wp.size(0) == y.size(1), "loc_in_bwd: [P,128] x [128,4]");
+  TORCH_CHECK(HW > 0 && y.size(0) % HW == 0 && p.numel() == (y.size(0) / HW) * wp.size(1) * HW, "loc_in_bwd: p shape");
+  c10::hip::HIPGuard g(y.device().index());
+  const long P = y.size(0);
+  const int nblk = as::loc_in_bwd_blocks(P);
+  auto dym = at::empty_like(y);
+  auto dp = at::empty_like(p);
+  auto part = at::empty({nblk, wp.size(0) * wp.size(1)}, y.options().dtype(at::kFloat));
+  as::loc_in_bwd(dy.data_ptr(), y.data_ptr(), p.data_ptr(), wp.data_ptr<float>(), dym.data_ptr(), dp.data_ptr(),
+                 part.data_ptr<float>(), P, static_cast<int>(HW), nblk, stream());
+  return {dym, dp, part.sum(0).view({wp.size(0), wp.size(1)})};
+}
+
 // ---------------------------------------------------------------- multi-tensor copy (+ dtype conversion)
 // dst[i].copy_(src[i]) for same-shape, same-stride, non-overlapping-and-dense pairs (storage order copy);
 // pairs that do not qualify are copied with copy_.  One H2D upload of the chunk table + one launch.
@@ -1112,6 +1203,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pointwise_supported", [](int64_t ci, int64_t co) { return as::pointwise_supported(static_cast<int>(ci), static_cast<int>(co)); });
   m.def("lstm_split_error", &lstm_split_error);
   m.def("multi_copy", &multi_copy);
+  m.def("loc_in_fwd", &loc_in_fwd);
+  m.def("vsp_fwd", &vsp_fwd);
+  m.def("vsp_in_channels", []() { return as::vsp_in_channels(); });
+  m.def("vsp_out_channels", []() { return as::vsp_out_channels(); });
+  m.def("vsp_bwd", &vsp_bwd);
+  m.def("loc_in_supported", [](int64_t c, int64_t p) { return as::loc_in_supported(static_cast<int>(c), static_cast<int>(p)); });
+  m.def("loc_in_bwd", &loc_in_bwd);
   m.def("head_stats_fwd", &head_stats_fwd);
   m.def("resmlp_fwd", &resmlp_fwd);
   m.def("resmlp_bwd", &resmlp_bwd);

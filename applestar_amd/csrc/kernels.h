@@ -47,6 +47,20 @@ void reverse_scan(const float* a, const float* b, const float* init, float* y, i
 // out = relu(tanh(y * sigmoid(g)) * sp + x)
 void gated_residual_fwd(const void* y, const void* g, const float* sp, const void* x, void* out, int dt, long n,
                         hipStream_t s);
+// value-encoder spatial input: relu(W [sc(8) | own | enemy] + b) per NHWC pixel, one-pass backward
+int vsp_in_channels();
+int vsp_out_channels();
+void vsp_fwd(const void* sc, const void* own, const void* enemy, const float* w, const float* b, void* out, long P,
+             hipStream_t s);
+int vsp_bwd_blocks(long P);
+void vsp_bwd(const void* dout, const void* out, const void* sc, const void* own, const void* enemy, const float* w,
+             void* dsc, float* part, long P, int nblk, hipStream_t s);
+// location-head input: relu(y0 + W_p relu(p)) per NHWC pixel and its one-pass backward (locin.hip)
+bool loc_in_supported(int C, int P);
+void loc_in_fwd(const void* y0, const void* p, const float* wp, void* out, long npix, int HW, hipStream_t s);
+int loc_in_bwd_blocks(long npix);
+void loc_in_bwd(const void* dy, const void* y, const void* p, const float* wp, void* dym, void* dp, float* part,
+                long npix, int HW, int nblk, hipStream_t s);
 void gated_residual_bwd(const void* dout, const void* y, const void* g, const float* sp, const void* out, int dt,
                         void* dy, void* dg, void* dx, float* dsp_part, long n, int nblk, hipStream_t s);
 int elementwise_blocks(long n);

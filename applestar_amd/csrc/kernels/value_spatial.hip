@@ -1,0 +1,167 @@
+// Value-encoder spatial input (value_encoder.py:52-60 in the reference):
+//
+//     sp = relu(conv1x1(cat([scatter(units -> 8 ch), own_units_spatial, enemy_units_spatial]), 10 -> 16))
+//
+// over B x 152 x 160 = 9.5 M pixels per learner batch.  Here the 10-channel input is never built: each
+// pixel reads its 8 scattered channels (one 16-byte vector of the NHWC scatter map) and the two bool
+// planes and writes the 16 ReLU'd outputs (two lanes per pixel, 8 channels / 16 bytes each).  The cat
+// path wrote a 16-channel zero-padded NHWC copy (303 MB, 0.45 ms, r2bm) and ran the projection as a
+// separate pass.
+//
+// Backward, one pass over dOut: dPre = dOut * (out > 0); dSc = W_sc^T dPre (8 channels per pixel, the
+// scatter's gradient); dW (16 x 10) and db accumulated in registers per lane, reduced across the wave by
+// shuffles and across the block in LDS into one partial row per block.  The unfused chain was act_grad,
+// a pointwise dX pass and a 9.5M-row weight-gradient pass over 16-channel maps.
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+constexpr int kVsSc = 8;               // scattered unit channels
+constexpr int kVsIn = kVsSc + 2;       // + own / enemy planes
+constexpr int kVsOut = 16;             // output channels; two lanes per pixel, 8 each
+constexpr int kVsAcc = 8 * (kVsIn + 1);  // per-lane dW / db accumulators
+
+__device__ __forceinline__ void vs_unpack8(const uint4 v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = bf2f(static_cast<bf16_t>(w[i] & 0xffffu));
+    f[2 * i + 1] = bf2f(static_cast<bf16_t>(w[i] >> 16));
+  }
+}
+
+__device__ __forceinline__ uint4 vs_pack8(const float* f) {
+  uint4 v;
+  v.x = f2bf2(f[0], f[1]);
+  v.y = f2bf2(f[2], f[3]);
+  v.z = f2bf2(f[4], f[5]);
+  v.w = f2bf2(f[6], f[7]);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void vsp_fwd_kernel(const bf16_t* __restrict__ sc, const uint8_t* __restrict__ own,
+                                                      const uint8_t* __restrict__ enemy, const float* __restrict__ w,
+                                                      const float* __restrict__ b, bf16_t* __restrict__ out, long P) {
+  const int h = threadIdx.x & 1;
+  float wr[8][kVsIn], br[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    br[c] = b[8 * h + c];
+#pragma unroll
+    for (int k = 0; k < kVsIn; ++k) wr[c][k] = w[(8 * h + c) * kVsIn + k];
+  }
+  const long step = static_cast<long>(gridDim.x) * (blockDim.x >> 1);
+  for (long pix = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) >> 1; pix < P; pix += step) {
+    float s[kVsSc];
+    vs_unpack8(*reinterpret_cast<const uint4*>(sc + pix * kVsSc), s);
+    const float fo = own[pix] ? 1.f : 0.f, fe = enemy[pix] ? 1.f : 0.f;
+    float v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      float a = fmaf(wr[c][kVsSc], fo, fmaf(wr[c][kVsSc + 1], fe, br[c]));
+#pragma unroll
+      for (int k = 0; k < kVsSc; ++k) a = fmaf(wr[c][k], s[k], a);
+      v[c] = fmaxf(a, 0.f);
+    }
+    *reinterpret_cast<uint4*>(out + pix * kVsOut + 8 * h) = vs_pack8(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void vsp_bwd_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out,
+                                                      const bf16_t* __restrict__ sc, const uint8_t* __restrict__ own,
+                                                      const uint8_t* __restrict__ enemy, const float* __restrict__ w,
+                                                      bf16_t* __restrict__ dsc, float* __restrict__ part, long P) {
+  __shared__ float red[4][2][kVsAcc];
+  const int h = threadIdx.x & 1;
+  float wr[8][kVsSc], acc[8][kVsIn + 1];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int k = 0; k < kVsSc; ++k) wr[c][k] = w[(8 * h + c) * kVsIn + k];
+#pragma unroll
+    for (int k = 0; k <= kVsIn; ++k) acc[c][k] = 0.f;
+  }
+  const long step = static_cast<long>(gridDim.x) * (blockDim.x >> 1);
+  // both lanes of a pixel pair run the same trip count, so the pair shuffle always sees its partner
+  for (long pix = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) >> 1; pix < P; pix += step) {
+    float d[8], o[8], s[kVsSc];
+    vs_unpack8(*reinterpret_cast<const uint4*>(dout + pix * kVsOut + 8 * h), d);
+    vs_unpack8(*reinterpret_cast<const uint4*>(out + pix * kVsOut + 8 * h), o);
+    vs_unpack8(*reinterpret_cast<const uint4*>(sc + pix * kVsSc), s);
+    const float fo = own[pix] ? 1.f : 0.f, fe = enemy[pix] ? 1.f : 0.f;
+    float ds[kVsSc];
+#pragma unroll
+    for (int k = 0; k < kVsSc; ++k) ds[k] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float g = o[c] > 0.f ? d[c] : 0.f;
+#pragma unroll
+      for (int k = 0; k < kVsSc; ++k) {
+        acc[c][k] = fmaf(g, s[k], acc[c][k]);
+        ds[k] = fmaf(wr[c][k], g, ds[k]);
+      }
+      acc[c][kVsSc] = fmaf(g, fo, acc[c][kVsSc]);
+      acc[c][kVsSc + 1] = fmaf(g, fe, acc[c][kVsSc + 1]);
+      acc[c][kVsIn] += g;
+    }
+#pragma unroll
+    for (int k = 0; k < kVsSc; ++k) ds[k] += __shfl_xor(ds[k], 1, 64);
+    if (h == 0) *reinterpret_cast<uint4*>(dsc + pix * kVsSc) = vs_pack8(ds);
+  }
+  // lanes of equal parity hold partial sums of the same 88 entries: fold the 32 of each wave
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+#pragma unroll
+    for (int k = 0; k <= kVsIn; ++k) {
+      float v = acc[c][k];
+#pragma unroll
+      for (int off = 2; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+      acc[c][k] = v;
+    }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < 2) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int k = 0; k <= kVsIn; ++k) red[wv][lane][c * (kVsIn + 1) + k] = acc[c][k];
+  }
+  __syncthreads();
+  // part[block][ch * 11 + k] with ch = 8 * h + c  (== h * 88 + c * 11 + k)
+  for (int e = threadIdx.x; e < 2 * kVsAcc; e += blockDim.x) {
+    const int hh = e / kVsAcc, j = e % kVsAcc;
+    part[static_cast<long>(blockIdx.x) * 2 * kVsAcc + e] = red[0][hh][j] + red[1][hh][j] + red[2][hh][j] + red[3][hh][j];
+  }
+}
+
+}  // namespace
+
+int vsp_in_channels() { return kVsIn; }
+int vsp_out_channels() { return kVsOut; }
+
+void vsp_fwd(const void* sc, const void* own, const void* enemy, const float* w, const float* b, void* out, long P,
+             hipStream_t s) {
+  long blocks = (P * 2 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(vsp_fwd_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
+                     static_cast<const bf16_t*>(sc), static_cast<const uint8_t*>(own),
+                     static_cast<const uint8_t*>(enemy), w, b, static_cast<bf16_t*>(out), P);
+}
+
+int vsp_bwd_blocks(long P) {
+  long blocks = (P * 2 + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  return static_cast<int>(blocks < 1 ? 1 : blocks);
+}
+
+void vsp_bwd(const void* dout, const void* out, const void* sc, const void* own, const void* enemy, const float* w,
+             void* dsc, float* part, long P, int nblk, hipStream_t s) {
+  hipLaunchKernelGGL(vsp_bwd_kernel, dim3(nblk), dim3(256), 0, s, static_cast<const bf16_t*>(dout),
+                     static_cast<const bf16_t*>(out), static_cast<const bf16_t*>(sc),
+                     static_cast<const uint8_t*>(own), static_cast<const uint8_t*>(enemy), w,
+                     static_cast<bf16_t*>(dsc), part, P);
+}
+
+}  // namespace as

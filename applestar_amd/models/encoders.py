@@ -458,7 +458,12 @@ class ValueEncoder(nn.Module):
         proj = proj * mask.unsqueeze(2).to(proj.dtype)
         H, W = x['own_units_spatial'].shape[-2:]
         sc = ops.scatter_connection(proj, x['unit_x'], x['unit_y'], H, W)
-        if sc.is_cuda:
+        c = self.project[0]
+        fused = ops.value_spatial_proj(sc, x['own_units_spatial'], x['enemy_units_spatial'], c.weight, c.bias) \
+            if sc.is_cuda else None
+        if fused is not None:
+            sp = fused
+        elif sc.is_cuda:
             # assembled directly in NHWC, zero-padded 10 -> 16 channels (with a zero-padded 1x1 weight) so
             # the 9.5M-row 1x1 conv's weight gradient takes the split-R MFMA kernel (K % 8 == 0)
             B_ = sc.shape[0]
@@ -466,7 +471,6 @@ class ValueEncoder(nn.Module):
             enemy = x['enemy_units_spatial'].to(proj.dtype).reshape(B_, H, W, 1)
             pad = own.new_zeros(B_, H, W, 6)
             sp = torch.cat([sc.to(proj.dtype).permute(0, 2, 3, 1), own, enemy, pad], -1).permute(0, 3, 1, 2)
-            c = self.project[0]
             sp = ops.conv2d(sp, torch.nn.functional.pad(c.weight, (0, 0, 0, 0, 0, 6)), c.bias, 1, 0, act='relu')
         else:
             sp = torch.cat([sc.to(proj.dtype), x['own_units_spatial'].to(proj.dtype),

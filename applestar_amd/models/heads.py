@@ -323,12 +323,16 @@ class LocationHead(nn.Module):
 
     def forward(self, embedding, map_skip: List[torch.Tensor], temperature: float = 1.0, location=None, u=None):
         B = embedding.shape[0]
-        p = self.project_embed(embedding).reshape(B, self.reshape_channel, self.hy, self.hx)
+        pf = self.project_embed(embedding)
         skip = map_skip[-1]
-        if skip.is_contiguous(memory_format=torch.channels_last):
-            p = p.contiguous(memory_format=torch.channels_last)
-        x = F.relu(torch.cat([p.to(skip.dtype), skip], 1))
-        x = self.conv1(x)
+        # map_skip[-1] is a ResBlock output (ReLU'd) and pf is ReLU'd: the fused stage skips the cat
+        x = ops.location_input(pf, skip, self.conv1[0].weight, self.conv1[0].bias) if self.conv1.act else None
+        if x is None:
+            p = pf.reshape(B, self.reshape_channel, self.hy, self.hx)
+            if skip.is_contiguous(memory_format=torch.channels_last):
+                p = p.contiguous(memory_format=torch.channels_last)
+            x = F.relu(torch.cat([p.to(skip.dtype), skip], 1))
+            x = self.conv1(x)
         for i, blk in enumerate(self.res):
             x = blk(x + map_skip[len(map_skip) - 1 - i])
         for conv in self.upsample[:-1]:

@@ -79,6 +79,24 @@ def conv2d(x, w, b, stride=1, padding=0, act=None, residual=None):
     return ref.conv2d(x, w, b, stride, padding, act, residual)
 
 
+def value_spatial_proj(sc, own, enemy, w, b):
+    """Fused value-encoder spatial input relu(conv1x1(cat([sc, own, enemy]))) on the GPU; None when it does
+    not apply (caller runs the cat path)."""
+    n = _native(sc)
+    if n is not None and n.has('value_spatial_proj'):
+        return n.value_spatial_proj(sc, own, enemy, w, b)
+    return None
+
+
+def location_input(pf, skip, w, b):
+    """Fused location-head input stage relu(conv1x1(relu(cat([pf as [B,P,H,W], skip])))) on the GPU
+    (skip a channels_last ReLU output); None when it does not apply (caller runs the cat path)."""
+    n = _native(skip)
+    if n is not None and n.has('location_input'):
+        return n.location_input(pf, skip, w, b)
+    return None
+
+
 def max_pool2x2(x):
     n = _native(x)
     if n is not None and n.has('maxpool2x2') and x.dim() == 4 and x.shape[1] % 8 == 0:

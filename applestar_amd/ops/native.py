@@ -24,7 +24,8 @@ def ensure_loaded():
 
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
-                'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp'}
+                'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp',
+                'location_input', 'value_spatial_proj'}
 
 
 def has(name: str) -> bool:
@@ -645,6 +646,103 @@ def conv2d(x, w, b, stride, padding, act, residual):
                 y = reference.act_fn(y, act)
         return from_nhwc(y.view(B, H, W, cout))
     return None
+
+
+# ---------------------------------------------------------------------------- value spatial input (value_spatial.hip)
+VSP_FUSED = os.environ.get('APPLESTAR_VSP_FUSED', '1') == '1'
+
+
+class _ValueSpatialProj(torch.autograd.Function):
+    """relu(conv1x1(cat([scatter map (8 ch), own, enemy]))) of the value encoder over the 9.5M-pixel map
+    without building the 10-channel input (value_spatial.hip); backward is one pass for the ReLU mask, the
+    scatter map's gradient and dW / db."""
+
+    @staticmethod
+    def forward(ctx, sc2d, own, enemy, w2, b):
+        wf, bf = w2.detach().float().contiguous(), b.detach().float().contiguous()
+        out = _C.vsp_fwd(sc2d, own, enemy, wf, bf)
+        ctx.save_for_backward(sc2d, own, enemy, wf, out)
+        ctx.dtypes = (w2.dtype, b.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        sc2d, own, enemy, wf, out = ctx.saved_tensors
+        dsc, dwb = _C.vsp_bwd(dout.to(torch.bfloat16).contiguous(), out, sc2d, own, enemy, wf)
+        w_dtype, b_dtype = ctx.dtypes
+        return dsc, None, None, dwb[:, :-1].to(w_dtype), dwb[:, -1].to(b_dtype)
+
+
+def value_spatial_proj(sc, own, enemy, w, b):
+    """sc [B, 8, H, W] (NHWC-contiguous scatter map), own / enemy [B, 1, H, W] bool, 1x1 conv weight
+    [16, 10, 1, 1] + bias -> relu(conv(cat([sc, own, enemy]))) as a channels_last [B, 16, H, W] view;
+    None when the shapes are not the kernel's."""
+    if not VSP_FUSED:
+        return None
+    B, C, H, W = sc.shape
+    cout, cin = w.shape[0], w.shape[1]
+    if cout != _C.vsp_out_channels() or cin != _C.vsp_in_channels() or C != cin - 2 or b is None \
+            or own.dtype != torch.bool or enemy.dtype != torch.bool or own.numel() != B * H * W \
+            or enemy.numel() != B * H * W:
+        return None
+    sc2d = nhwc(sc.to(torch.bfloat16)).view(-1, C)
+    with torch.autocast('cuda', enabled=False):
+        y = _ValueSpatialProj.apply(sc2d, own.reshape(-1).view(torch.uint8), enemy.reshape(-1).view(torch.uint8),
+                                    w.view(cout, cin), b)
+    return from_nhwc(y.view(B, H, W, cout))
+
+
+# ---------------------------------------------------------------------------- location-head input (locin.hip)
+LOC_FUSED = os.environ.get('APPLESTAR_LOC_FUSED', '1') == '1'
+
+
+class _LocationInput(torch.autograd.Function):
+    """relu(conv1x1(relu(cat([p, skip], 1)))) of the location head without the concat: y0 = skip W_s^T + b
+    as a K = 128 library GEMM, then the rank-4 term W_p relu(p) + ReLU per pixel in one pass (locin.hip),
+    reading p in the fc output's [B, 4*HW] layout.  Backward: one pass for the ReLU mask, dP and the
+    128 x 4 dW_p; dSkip on the library, dW_s / db on the split-R MFMA wgrad.  The cat-based path wrote the
+    38 MB concat (0.25 ms on channels_last), ran the K = 132 GEMMs and a ReLU pass each way."""
+
+    @staticmethod
+    def forward(ctx, pf, skip2d, w2, b, HW):
+        C, CP = w2.shape
+        ws = w2[:, CP - C:].contiguous()
+        wp = w2[:, :CP - C].float().contiguous()
+        y0 = torch.addmm(b.to(skip2d.dtype), skip2d, ws.t())
+        y = _C.loc_in_fwd(y0, pf, wp, HW)
+        ctx.save_for_backward(pf, skip2d, ws, wp, y)
+        ctx.meta = (HW, w2.dtype, b.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        pf, skip2d, ws, wp, y = ctx.saved_tensors
+        HW, w_dtype, b_dtype = ctx.meta
+        dym, dp, dwp = _C.loc_in_bwd(dy.to(torch.bfloat16).contiguous(), y, pf, wp, HW)
+        dskip = torch.mm(dym, ws) if ctx.needs_input_grad[1] else None
+        dws, db = _C.wgrad(dym, skip2d, 0, True, _bf16_grads(w_dtype, b_dtype))
+        dw = torch.cat([dwp.to(dws.dtype), dws], 1).to(w_dtype)
+        return dp, dskip, dw, db.to(b_dtype), None
+
+
+def location_input(pf, skip, w, b):
+    """pf [B, P*H*W] (ReLU'd fc output), skip [B, C, H, W] channels_last bf16 (a ReLU output), conv1x1
+    weight [C, P + C, 1, 1] + bias -> relu(conv(relu(cat([pf.view(B, P, H, W), skip], 1)))) as a
+    channels_last [B, C, H, W] view; None when the shapes are not the kernel's."""
+    if not LOC_FUSED:
+        return None
+    B, C, H, W = skip.shape
+    cout, cin = w.shape[0], w.shape[1]
+    if skip.dtype != torch.bfloat16 or not skip.is_contiguous(memory_format=torch.channels_last) or b is None \
+            or cout != C or not _C.loc_in_supported(C, cin - C) or pf.numel() != B * (cin - C) * H * W:
+        return None
+    w2 = w.view(cout, cin)
+    w2 = w2 if w2.dtype == torch.bfloat16 else _CastWeight.apply(w2)
+    bb = b if b.dtype == torch.bfloat16 else _CastWeight.apply(b)
+    with torch.autocast('cuda', enabled=False):
+        y = _LocationInput.apply(pf.to(torch.bfloat16).reshape(B, -1).contiguous(), nhwc(skip).view(-1, C), w2, bb,
+                                 H * W)
+    return from_nhwc(y.view(B, H, W, C))
 
 
 # ---------------------------------------------------------------------------- narrow 1x1 conv (pointwise.hip)

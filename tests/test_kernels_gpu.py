@@ -854,3 +854,70 @@ def test_resmlp_fused_matches_op_by_op():
         assert pa.grad is not None and pa.grad.dtype == pa.dtype, na
         e_f, e_r = _err(pa.grad, pg.grad), _err(pb.grad, pg.grad)
         assert e_f < 2 * e_r + 1e-3 * max(1e-3, pg.grad.abs().max().item()), (na, e_f, e_r)
+
+
+@pytest.mark.parametrize('B', [6, 5])
+def test_location_input_matches_cat_path(B):
+    """locin.hip: relu(conv1x1(relu(cat([fc output as [B,4,H,W], skip])))) without the concat vs the fp32
+    torch cat + conv path, forward and all four gradients (skip gradient where skip > 0: the fused stage
+    leaves the skip map's own ReLU mask to its producer)."""
+    import torch.nn.functional as F
+    torch.manual_seed(0)
+    H, W, C, P = 19, 20, 128, 4
+    pf = torch.relu(torch.randn(B, P * H * W, device=DEV)).bfloat16().requires_grad_()
+    skip = torch.relu(torch.randn(B, C, H, W, device=DEV)).bfloat16()
+    skip = skip.contiguous(memory_format=torch.channels_last).requires_grad_()
+    w = (0.1 * torch.randn(C, P + C, 1, 1, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    y = N.location_input(pf, skip, w, b)
+    assert y is not None and y.is_contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(B, C, H, W, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    pr, sr, wr, br = (t.detach().float().requires_grad_() for t in (pf, skip, w, b))
+    x = torch.relu(torch.cat([pr.view(B, P, H, W), sr], 1))
+    z = F.conv2d(x, wr, br)
+    yr = torch.relu(z)
+    # the output ReLU's mask is taken from the kernel's own output: pre-activations within bf16 rounding of
+    # zero may flip sign between the bf16 and the fp32 paths, and one flipped entry moves dP by |dy w|
+    (z * (y.detach().float() > 0)).backward(dy.float())
+
+    def rel(a, r):
+        return _err(a, r) / max(r.abs().max().item(), 1e-6)
+
+    assert rel(y, yr) < 1e-2
+    assert rel(pf.grad, pr.grad) < 2e-2
+    assert rel(w.grad, wr.grad) < 2e-2
+    assert rel(b.grad, br.grad) < 2e-2
+    assert rel(skip.grad * (skip > 0), sr.grad) < 2e-2
+
+
+@pytest.mark.parametrize('B,H,W', [(3, 152, 160), (2, 7, 9)])
+def test_value_spatial_proj_matches_cat_path(B, H, W):
+    """value_spatial.hip: relu(conv1x1(cat([scatter map (8 ch), own, enemy]))) without the cat vs fp32
+    torch, forward and the scatter-map / weight / bias gradients (output ReLU mask from the kernel's own
+    output, as in the location-input test)."""
+    import torch.nn.functional as F
+    torch.manual_seed(0)
+    sc = torch.zeros(B * H * W, 8, device=DEV)
+    hot = torch.rand(B * H * W, device=DEV) < 0.05          # a sparse unit scatter, like the real map
+    sc[hot] = torch.randn(int(hot.sum()), 8, device=DEV)
+    sc = sc.bfloat16().view(B, H, W, 8).permute(0, 3, 1, 2).requires_grad_()
+    own = torch.rand(B, 1, H, W, device=DEV) < 0.1
+    enemy = torch.rand(B, 1, H, W, device=DEV) < 0.1
+    w = (0.3 * torch.randn(16, 10, 1, 1, device=DEV)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(16, device=DEV)).bfloat16().requires_grad_()
+    y = N.value_spatial_proj(sc, own, enemy, w, b)
+    assert y is not None and y.is_contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(B, 16, H, W, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    sr, wr, br = (t.detach().float().requires_grad_() for t in (sc, w, b))
+    z = F.conv2d(torch.cat([sr, own.float(), enemy.float()], 1), wr, br)
+    (z * (y.detach().float() > 0)).backward(dy.float())
+
+    def rel(a, r):
+        return _err(a, r) / max(r.abs().max().item(), 1e-6)
+
+    assert rel(y, torch.relu(z)) < 1e-2
+    assert rel(sc.grad, sr.grad) < 2e-2
+    assert rel(w.grad, wr.grad) < 2e-2
+    assert rel(b.grad, br.grad) < 2e-2

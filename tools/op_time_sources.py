@@ -16,9 +16,16 @@ from applestar_amd.rl.trainer import RLTrainer, _amp  # noqa: E402
 from applestar_amd.rl.synthetic import rl_batch, to_device  # noqa: E402
 from applestar_amd.runtime.prefetch import entity_total_hint  # noqa: E402
 
-SKIP = ('view', 'reshape', 'permute', 'transpose', 't.default', 'expand', 'slice', 'select', 'unsqueeze', 'squeeze',
-        'as_strided', 'detach', 'alias', 'split', 'chunk', 'unbind', '_unsafe_view', 'narrow', 'is_', 'size', 'stride',
-        'lift_fresh', 'empty', 'sym_', 'dim', '_local_scalar_dense', 'item', 'record_stream')
+# metadata-only ops, matched on the op's base name (a substring match on 'aten.cat.default' would hit 't.default')
+SKIP = ('view', 'reshape', 'permute', 'transpose', 't', 'expand', 'slice', 'select', 'unsqueeze', 'squeeze',
+        'as_strided', 'detach', 'alias', 'split', 'split_with_sizes', 'chunk', 'unbind', '_unsafe_view', 'narrow',
+        'size', 'stride', 'lift_fresh', 'dim', '_local_scalar_dense', 'item', 'record_stream', 'expand_as', 'view_as')
+SKIP_PREFIX = ('is_', 'empty', 'sym_')
+
+
+def _skip(name: str) -> bool:
+    base = name.split('.')[1] if name.count('.') >= 1 else name
+    return base in SKIP or base.startswith(SKIP_PREFIX)
 
 
 class Timer(TorchDispatchMode):
@@ -28,7 +35,7 @@ class Timer(TorchDispatchMode):
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         name = str(func)
-        if any(s in name for s in SKIP):
+        if _skip(name):
             return func(*args, **(kwargs or {}))
         frames = [f for f in traceback.extract_stack()[:-1] if 'applestar_amd' in f.filename]
         where = ' <- '.join(f'{f.filename.split("applestar_amd/")[-1]}:{f.lineno}' for f in frames[-2:][::-1])
