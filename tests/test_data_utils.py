@@ -131,3 +131,33 @@ def test_file_helper_refuses_pickle_by_default():
     with pytest.raises(PermissionError):
         F.loads(raw, 'pickle')
     assert F.loads(raw, 'pickle', allow_pickle=True) == {'a': 1}
+
+
+def test_packed_batch_roundtrip():
+    """pack_tree: every tensor of an RL batch becomes a view of one byte buffer with the same values;
+    to_device rebuilds the same structure (here on the CPU) from one copy of the buffer."""
+    from applestar_amd.rl.synthetic import rl_batch
+    from applestar_amd.runtime.prefetch import pack_tree, PackedBatch
+
+    b = rl_batch(2, 3, max_entities=16, seed=0)
+    pk = pack_tree(b, pin=False)
+    assert isinstance(pk, PackedBatch)
+
+    def leaves(x, out):
+        if torch.is_tensor(x):
+            out.append(x)
+        elif isinstance(x, dict):
+            for v in x.values():
+                leaves(v, out)
+        elif isinstance(x, (list, tuple)):
+            for v in x:
+                leaves(v, out)
+        return out
+
+    ref, got, dev = leaves(b, []), leaves(dict(pk), []), leaves(pk.to_device('cpu'), [])
+    assert len(ref) == len(got) == len(dev) > 50
+    base = pk.buffer.data_ptr()
+    for r, g, d in zip(ref, got, dev):
+        assert g.dtype == r.dtype and g.shape == r.shape and torch.equal(g, r) and torch.equal(d, r)
+        assert base <= g.data_ptr() < base + pk.buffer.numel()
+    assert pk['batch_size'] == b['batch_size'] and pk.to_device('cpu')['unroll_len'] == b['unroll_len']
