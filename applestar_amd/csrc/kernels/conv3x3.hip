@@ -39,23 +39,43 @@ __device__ __forceinline__ bf8v as_bf8(const uint4& u) {
 // fp32 tile cs [128][CPAD] (LDS) -> out rows m0.., channels n0..n0+BN in 16-B pieces:
 //   v = cs + bias (+ res | * [res > 0] for ACT_DRELU), then ReLU for ACT_RELU; bf16.
 // ACT_DRELU is the input-gradient form: dpre = dx * (y > 0) with y (the layer's ReLU output) in res.
+// A thread's 8-channel piece is the same in every row it handles (256 % (BN / 8) == 0): its bias is loaded
+// once and every residual row is requested before the first is used, so the epilogue pays one memory
+// latency, not one per row (the per-row form cost 29 us of an 89 us ResBlock conv, r2bu ablation).
 template <int BN, int CPAD>
 __device__ __forceinline__ void conv_epilogue(const float* cs, long m0, int n0, long M, int Cout,
                                               const float* __restrict__ bias, const bf16_t* __restrict__ res,
                                               bf16_t* __restrict__ out, int act) {
-  constexpr int CPR = BN / 8;  // 8-channel pieces per row
-  for (int idx = threadIdx.x; idx < 128 * CPR; idx += 256) {
-    const int rr = idx / CPR, c8 = idx % CPR;
-    const long m = m0 + rr;
-    const int n = n0 + 8 * c8;
-    if (m >= M || n >= Cout) continue;
-    float v[8];
+  constexpr int CPR = BN / 8;          // 8-channel pieces per row
+  constexpr int RSTEP = 256 / CPR;     // rows between a thread's consecutive pieces
+  constexpr int IT = 128 / RSTEP;
+  static_assert(256 % CPR == 0, "epilogue piece mapping");
+  const int c8 = threadIdx.x % CPR, r0 = threadIdx.x / CPR;
+  const int n = n0 + 8 * c8;
+  if (n >= Cout) return;
+  float bv[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = cs[rr * CPAD + 8 * c8 + e] + (bias ? bias[n + e] : 0.f);
-    const long o = m * Cout + n;
+  for (int e = 0; e < 8; ++e) bv[e] = bias ? bias[n + e] : 0.f;
+  uint4 rv[IT];
+  if (res) {
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+      const long m = m0 + r0 + k * RSTEP;
+      rv[k] = m < M ? *reinterpret_cast<const uint4*>(res + m * Cout + n) : make_uint4(0, 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int rr = r0 + k * RSTEP;
+    const long m = m0 + rr;
+    if (m >= M) break;
+    float v[8];
+    const float4 c0 = *reinterpret_cast<const float4*>(cs + rr * CPAD + 8 * c8);
+    const float4 c1 = *reinterpret_cast<const float4*>(cs + rr * CPAD + 8 * c8 + 4);
+    v[0] = c0.x + bv[0]; v[1] = c0.y + bv[1]; v[2] = c0.z + bv[2]; v[3] = c0.w + bv[3];
+    v[4] = c1.x + bv[4]; v[5] = c1.y + bv[5]; v[6] = c1.z + bv[6]; v[7] = c1.w + bv[7];
     if (res) {
-      const uint4 u = *reinterpret_cast<const uint4*>(res + o);
-      const uint32_t q4[4] = {u.x, u.y, u.z, u.w};
+      const uint32_t q4[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
       if (act == ACT_DRELU) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -79,7 +99,7 @@ __device__ __forceinline__ void conv_epilogue(const float* cs, long m0, int n0, 
     u.y = f2bf2(v[2], v[3]);
     u.z = f2bf2(v[4], v[5]);
     u.w = f2bf2(v[6], v[7]);
-    *reinterpret_cast<uint4*>(out + o) = u;
+    *reinterpret_cast<uint4*>(out + m * Cout + n) = u;
   }
 }
 
@@ -91,7 +111,7 @@ struct ConvCfg {
   static constexpr int WM = 4 / WN;              // waves along M
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 16, FN = TN / 16;
-  static constexpr int LDK = BK + 8;             // padded LDS row, bf16 elements
+  static constexpr int LDK = BK + 16;            // padded LDS row (bf16) = 16 mod 32: conflict-free b128 reads
   static constexpr int CH = BK / 8;              // 16-B chunks per row
   static constexpr int A_IT = (BM * CH + NT - 1) / NT;
   static constexpr int B_IT = (BN * CH + NT - 1) / NT;
@@ -267,13 +287,20 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(const bf16_t* __restrict__
 // of halo on each side); every tap then reads its A fragments from that window at a constant row
 // offset dy*W + dx and zeroes the rows whose neighbour falls outside the image (per-lane 9-bit masks).
 // Only the weight tile is re-staged per (tap, chunk) step, double-buffered through registers.
+// HALO_ABL: timing-ablation bits for tools/native/conv_ablation.cpp only (1: no weight restaging, 2: no window
+// restaging, 8: no loop barriers, 16: two K-steps only, 32: no epilogue, 64: no prologue loads); 0 in every
+// library build
+#ifndef HALO_ABL
+#define HALO_ABL 0
+#endif
+
 template <int BN, int WP>
 struct HaloCfg {
   static constexpr int BM = 128, CK = 64, NT = 256;
   static constexpr int WN = BN >= 128 ? 2 : 1, WM = 4 / WN;
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 16, FN = TN / 16;
-  static constexpr int P = CK + 8;                 // LDS row pitch (bf16): conflict-free ds_read_b128 groups
+  static constexpr int P = CK + 16;                // LDS row pitch (bf16) = 16 mod 32: conflict-free ds_read_b128 groups
   static constexpr int NR = WP * NT / 8;           // window rows covered by WP 16-B pieces per thread
   static constexpr int B_IT = BN * (CK / 8) / NT;  // weight pieces per thread
   static constexpr int WIN = NR * P, BT = BN * P;  // bf16 elements
@@ -380,48 +407,65 @@ __global__ __launch_bounds__(256) void conv3x3_halo_kernel(const bf16_t* __restr
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  const int nsteps = 9 * (Cin / C::CK);
-  load_win(0);
-  load_b(0);
-  store_win();
-  store_b(0);
+  const int nsteps = (HALO_ABL & 16) ? 2 : 9 * (Cin / C::CK);
+  if (!(HALO_ABL & 64)) {
+    load_win(0);
+    load_b(0);
+    store_win();
+    store_b(0);
+  }
   __syncthreads();
   for (int step = 0; step < nsteps; ++step) {
-    const int cur = step & 1;
+    const int cur = (HALO_ABL & 1) ? 0 : (step & 1);
     const int tap = step % 9;
-    const bool next = step + 1 < nsteps;
-    const bool new_chunk = next && (step + 1) % 9 == 0;
+    const bool next = step + 1 < nsteps && !(HALO_ABL & 1);
+    const bool new_chunk = step + 1 < nsteps && (step + 1) % 9 == 0 && !(HALO_ABL & 2);
     if (next) load_b(step + 1);
     if (new_chunk) load_win(((step + 1) / 9) * C::CK);
     const int shift = (W + 1) + (tap / 3 - 1) * W + (tap % 3 - 1);
     const bf16_t* Bs = bts + cur * C::BT;
+    // every fragment of the step is read before the first MFMA: the reads of the second k-slice land while
+    // the first slice's MFMAs run, so the LDS latency is exposed once per step instead of once per slice
+    // (with the loop barrier keeping a CU's waves in phase, the other wave on the SIMD cannot hide it)
+    constexpr int KS = C::CK / 32;
+    uint4 ua[KS][C::FM], ub[KS][C::FN];
 #pragma unroll
-    for (int ks = 0; ks < C::CK / 32; ++ks) {
-      bf8v af[C::FM], bfr[C::FN];
+    for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
-      for (int i = 0; i < C::FM; ++i) {
-        const int row = wm * C::TM + 16 * i + lr + shift;
-        uint4 u = *reinterpret_cast<const uint4*>(win + row * C::P + ks * 32 + 8 * lg);
-        if (!((ok9[i] >> tap) & 1)) u = make_uint4(0, 0, 0, 0);
-        af[i] = as_bf8(u);
-      }
+      for (int i = 0; i < C::FM; ++i)
+        ua[ks][i] = *reinterpret_cast<const uint4*>(win + (wm * C::TM + 16 * i + lr + shift) * C::P + ks * 32 + 8 * lg);
 #pragma unroll
       for (int j = 0; j < C::FN; ++j)
-        bfr[j] = as_bf8(*reinterpret_cast<const uint4*>(Bs + (wn * C::TN + 16 * j + lr) * C::P + ks * 32 + 8 * lg));
+        ub[ks][j] = *reinterpret_cast<const uint4*>(Bs + (wn * C::TN + 16 * j + lr) * C::P + ks * 32 + 8 * lg);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      bf8v af[C::FM];
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) af[i] = as_bf8(((ok9[i] >> tap) & 1) ? ua[ks][i] : make_uint4(0, 0, 0, 0));
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
         for (int j = 0; j < C::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], as_bf8(ub[ks][j]), acc[i][j], 0, 0, 0);
     }
     if (new_chunk) {
-      __syncthreads();           // every wave is done reading the old window
+      if (!(HALO_ABL & 8)) __syncthreads();           // every wave is done reading the old window
       store_win();
     }
     if (next) store_b(cur ^ 1);
-    __syncthreads();
+    if (!(HALO_ABL & 8)) __syncthreads();
   }
 
+  if (HALO_ABL & 32) {            // ablation: no epilogue (one value per lane keeps the MFMAs alive)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) t += acc[i][j][0] + acc[i][j][3];
+    if (t == 12345.f) out[threadIdx.x] = 1;
+    return;
+  }
   // epilogue (as conv3x3_kernel): fp32 tile in LDS -> 16-B rows with bias / residual / activation
   float* cs = reinterpret_cast<float*>(smem);
 #pragma unroll
