@@ -66,6 +66,12 @@ __device__ __forceinline__ bf8v tr_frag(const bf16_t* tile, int pitch, int col0,
   return r;
 }
 
+// WG_ABL: timing-ablation bits for tools/native/wgrad_ablation.cpp only (1: no row-stage loads after the
+// first, 2: no partial-tile stores); 0 in every library build
+#ifndef WG_ABL
+#define WG_ABL 0
+#endif
+
 template <int BN, int BK, bool CONV>
 __global__ __launch_bounds__(256) void wgrad_kernel(const WgBatch P, long part_stride, long R, int N, int K, int H,
                                                     int W, int Cin, long rows_per_split, int tiles_n, int tiles_k,
@@ -198,8 +204,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgBatch P, long part_s
     __syncthreads();
   }
   for (long it = 0; it < nsteps; ++it) {
-    const int cur = static_cast<int>(it & 1);
-    if (it + 1 < nsteps) load_regs(r_begin + (it + 1) * C::BR);
+    const int cur = (WG_ABL & 1) ? 0 : static_cast<int>(it & 1);
+    if (it + 1 < nsteps && !(WG_ABL & 1)) load_regs(r_begin + (it + 1) * C::BR);
     const bf16_t* A = smem + cur * C::STAGE;
     const bf16_t* Bt = A + C::BR * C::PA;
 #pragma unroll
@@ -221,29 +227,62 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgBatch P, long part_s
           for (int e = 0; e < 8; ++e) bsum[i] += static_cast<float>(af[i][e]);
       }
     }
-    if (it + 1 < nsteps) store_lds(cur ^ 1);
+    if (it + 1 < nsteps && !(WG_ABL & 1)) store_lds(cur ^ 1);
     __syncthreads();
   }
+  if (WG_ABL & 2) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < C::FN; ++i)
+#pragma unroll
+      for (int j = 0; j < C::FK; ++j) t += acc[i][j][0] + acc[i][j][3];
+    if (t == 12345.f) dw_part[tid] = 1.f;
+    return;
+  }
 
-  // epilogue: fp32 partial tile; lane (g, i) of fragment (a, b) holds C[n = 16a + 4g + e][k = 16b + i]
-  // out_bf16 (single slice only): the final dW / db in bf16, the cast fused here instead of a pass
+  // epilogue: the fp32 tile goes through LDS (lane (g, i) of fragment (a, b) holds C[n = 16a + 4g + e][k = 16b + i])
+  // and leaves as whole 16-B pieces of each row n, so a wave's stores cover full cache lines.  Scalar stores
+  // straight from the fragments wrote 64-B pieces with 4x the store instructions: 24 of the 91 us of the
+  // ResBlock conv dW (56 slices x 590 KB of partials, r2bx ablation).
   float* outp = dw_part + static_cast<long>(s) * part_stride;
   bf16_t* outb = reinterpret_cast<bf16_t*>(dw_part);
   const int lr = lane & 15, lg = lane >> 4;
+  float* cs = reinterpret_cast<float*>(smem);
+  constexpr int CP = C::BK + 4;                         // fp32 row pitch of the staged tile
+  static_assert(C::BN * CP * 4 <= C::SMEM, "epilogue tile fits the staging LDS");
+  __syncthreads();                                      // (the loop ends on a barrier; explicit for nsteps == 0)
 #pragma unroll
   for (int i = 0; i < C::FN; ++i)
 #pragma unroll
-    for (int j = 0; j < C::FK; ++j) {
-      const int k = k0 + wk * C::TK + 16 * j + lr;
+    for (int j = 0; j < C::FK; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int n = n0 + wn * C::TN + 16 * i + 4 * lg + e;
-        if (n < N && k < K) {
-          if (out_bf16) outb[static_cast<long>(n) * K + k] = f2bf(acc[i][j][e]);
-          else outp[static_cast<long>(n) * K + k] = acc[i][j][e];
-        }
+      for (int e = 0; e < 4; ++e)
+        cs[(wn * C::TN + 16 * i + 4 * lg + e) * CP + wk * C::TK + 16 * j + lr] = acc[i][j][e];
+  __syncthreads();
+  constexpr int PR = C::BK / 4;                         // 4-float pieces per row
+  for (int idx = tid; idx < C::BN * PR; idx += C::NT) {
+    const int nn = idx / PR, kk = 4 * (idx % PR);
+    const int n = n0 + nn, k = k0 + kk;
+    if (n >= N || k >= K) continue;
+    const float4 v = *reinterpret_cast<const float4*>(cs + nn * CP + kk);
+    const long o = static_cast<long>(n) * K + k;
+    if (k + 4 <= K && (K & 3) == 0) {
+      if (out_bf16) {
+        uint2 u;
+        u.x = f2bf2(v.x, v.y);
+        u.y = f2bf2(v.z, v.w);
+        *reinterpret_cast<uint2*>(outb + o) = u;
+      } else {
+        *reinterpret_cast<float4*>(outp + o) = v;
+      }
+    } else {
+      const float vv[4] = {v.x, v.y, v.z, v.w};
+      for (int e = 0; e < 4 && k + e < K; ++e) {
+        if (out_bf16) outb[o + e] = f2bf(vv[e]);
+        else outp[o + e] = vv[e];
       }
     }
+  }
   if (do_bias) {
 #pragma unroll
     for (int i = 0; i < C::FN; ++i) {
