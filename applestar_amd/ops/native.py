@@ -141,7 +141,7 @@ class _LNLSTMRecurrence(torch.autograd.Function):
         dgates, dhg, dc_ln, dh0, dc0 = _C.lnlstm_bwd(dout, z(dhT), z(dcT), gates, c_all, xhat_c, rstd_c, xhat_h,
                                                      rstd_h, wq, lnh_w.detach(), lnc_w.detach())
         h_prev = torch.cat([h0.float().unsqueeze(0), out[:-1]], 0).view(T * B, H)
-        dw = dhg.view(T * B, 4 * H).t() @ h_prev
+        dw = _mm_tn(dhg.view(T * B, 4 * H), h_prev)
         dlnh_w = (dgates * xhat_h).sum((0, 1))
         dlnh_b = dgates.sum((0, 1))
         dlnc_w = (dc_ln * xhat_c).sum((0, 1))
@@ -156,7 +156,11 @@ def lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b
     if H not in (384, 32):
         from . import reference
         return reference.lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b)
-    xg = torch.nn.functional.linear(x.reshape(T * B, -1), w_ih)
+    x2 = x.reshape(T * B, -1)
+    # bf16 input projection through linear(): its dW takes the split-R MFMA kernel, not a library GEMM that
+    # tiles only the 4H x I output over T*B = 24576 rows (the selected-units head's LSTM)
+    xg = linear(x2, w_ih) if (x2.dtype == torch.bfloat16 and w_ih.dtype == torch.bfloat16) else \
+        torch.nn.functional.linear(x2, w_ih)
     xp = layer_norm(xg, lni_w, lni_b, out_dtype=torch.float32).view(T, B, 4 * H)
     w_dtype = torch.bfloat16 if torch.is_autocast_enabled() else torch.float32
     out, hT, cT = _LNLSTMRecurrence.apply(xp, h0.float(), c0.float(), w_hh, lnh_w, lnh_b, lnc_w, lnc_b, w_dtype)
@@ -790,7 +794,18 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x2, w, b, relu):
-        if relu and b is not None:
+        R, K = x2.shape
+        if GEMM_REFORM and R <= 2048 and K >= 16384 and K % (32 * 8) == 0:
+            # few rows, huge reduction (the spatial encoder's 48640 -> 256 fc): the library ran a 256x16 tile
+            # over the whole K (0.14-0.30 ms); 32 K-chunks as one batched GEMM + an fp32 sum: 48 us
+            S = 32
+            kc = K // S
+            p = torch.bmm(x2.view(R, S, kc).transpose(0, 1), w.view(w.shape[0], S, kc).permute(1, 2, 0))
+            y = p.sum(0, dtype=torch.float32)
+            if b is not None:
+                y = y + b.float()
+            y = (torch.relu(y) if relu else y).to(x2.dtype)
+        elif relu and b is not None:
             y = torch._addmm_activation(b, x2, w.t(), use_gelu=False)
         else:
             y = torch.nn.functional.linear(x2, w, b)
@@ -816,6 +831,11 @@ class _Linear(torch.autograd.Function):
                 # thin-K product (the heads' 256 -> 32 key projections): one MFMA per output tile, a pure
                 # store stream (gemm_k32.hip); the library took 0.19 ms per 196k-row call
                 dx = _C.mm_k32(dy, w.t().contiguous())
+            elif GEMM_REFORM and dy.shape[0] * w.shape[1] >= (1 << 22):
+                # dY W as an "NT" product against a transposed weight copy (the layout of the forward):
+                # hipBLASLt's "NN" kernels ran the transformer FFN dX at 132 vs 106 us and the value fc's
+                # 390 x 12160 dX at 32 vs 19 us (tools/bench_gemm_alts.py)
+                dx = torch.nn.functional.linear(dy, w.t().contiguous())
             else:
                 dx = torch.mm(dy, w)
         has_b = ctx.b_dtype is not None
@@ -824,6 +844,16 @@ class _Linear(torch.autograd.Function):
 
 
 _WGRAD_MIN_ROWS = 256     # tools/ab_bench.py --variant wgrad_small: -0.7 ms/step vs 4096
+GEMM_REFORM = os.environ.get('APPLESTAR_GEMM_REFORM', '1') == '1'
+
+
+def _mm_tn(a, b):
+    """a^T b for a [R, M], b [R, N] with R >> M, N (recurrent weight gradients): 32 row chunks as one batched
+    GEMM + a sum when R is large (the library tiled only the small M x N output: 45 vs 25 us at R = 24576)."""
+    R = a.shape[0]
+    if GEMM_REFORM and R >= 8192 and R % 32 == 0 and a.shape[1] * b.shape[1] <= (1 << 18):
+        return torch.bmm(a.view(32, R // 32, -1).transpose(1, 2), b.view(32, R // 32, -1)).sum(0)
+    return a.t() @ b
 
 
 class _LinearSplitK(torch.autograd.Function):

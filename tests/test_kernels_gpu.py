@@ -921,3 +921,27 @@ def test_value_spatial_proj_matches_cat_path(B, H, W):
     assert rel(sc.grad, sr.grad) < 2e-2
     assert rel(w.grad, wr.grad) < 2e-2
     assert rel(b.grad, br.grad) < 2e-2
+
+
+@pytest.mark.parametrize('R,K,N,relu', [(390, 48640, 256, True), (5000, 256, 1024, False)])
+def test_native_linear_reformulated_gemms(R, K, N, relu):
+    """The library-GEMM reformulations in _Linear: a few rows over a huge K run as a 32-chunk split-K batched
+    GEMM (the spatial fc, 48640 -> 256), and large dX products use a transposed weight copy; values and all
+    gradients vs fp32 (ReLU mask from the bf16 output)."""
+    from applestar_amd import ops
+    from applestar_amd.ops import native
+    assert native.GEMM_REFORM
+    torch.manual_seed(23)
+    x = torch.randn(R, K, device=DEV).bfloat16().requires_grad_()
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16().requires_grad_()
+    b = torch.randn(N, device=DEV).bfloat16().requires_grad_()
+    y = ops.linear(x, w, b, act='relu' if relu else None)
+    g = torch.randn(R, N, device=DEV).bfloat16()
+    y.backward(g)
+    xs, ws, bs = (t.detach().float().requires_grad_() for t in (x, w, b))
+    z = xs @ ws.t() + bs
+    ref = torch.relu(z) if relu else z
+    assert _err(y, ref) < 2e-2 * max(1.0, ref.abs().max().item())
+    (z * (y.detach().float() > 0) if relu else z).backward(g.float())
+    for a, r in ((x.grad, xs.grad), (w.grad, ws.grad), (b.grad, bs.grad)):
+        assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())

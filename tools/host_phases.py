@@ -35,7 +35,8 @@ def main():
     for i in range(args.steps + 3):
         torch.cuda.synchronize()
         t = [time.perf_counter()]
-        tr.model.train()
+        if not tr.model.training:
+            tr.model.train()
         with _amp(dev, 'bfloat16'):
             out = tr.model.rl_learner_forward(**b)
         t.append(time.perf_counter())
