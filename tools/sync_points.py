@@ -36,7 +36,10 @@ def main():
     else:
         tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}},
                        device=dev)
-        b = to_device(rl_batch(6, 64, seed=0), dev)
+        from applestar_amd.runtime.prefetch import entity_total_hint
+        h = rl_batch(6, 64, seed=0)
+        b = to_device(h, dev)
+        b['entity_total'] = entity_total_hint(h)   # as the bench's prefetcher supplies it
     tr.step(dict(b))
     torch.cuda.synchronize()
     hits = collections.Counter()
