@@ -102,6 +102,115 @@ __global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const T* __restrict
   }
 }
 
+// bf16, C % 8 == 0: one thread per INPUT pixel and 8 channels (16-B vectors, 32-bit index math).
+// Forward: the 3x3 neighbourhood (clamped) gives the 2x2 outputs of the fixed 0.25 / 0.75 stencil; border
+// clamping reproduces align_corners=False exactly (a clamped neighbour is the pixel itself).  The per-output
+// form above did 64-bit divisions and 16 scalar 2-byte loads per 4 channels (0.14 ms per location-head
+// upsample).  Backward: the input pixel pulls its 4 x 4 output neighbourhood with the 1-D weights
+// 0.25 | 0.75 (+0.25 at the first / last index) | 0.75 (+0.25) | 0.25.
+__device__ __forceinline__ void up_unpack8(const uint4 v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ uint4 up_pack8(const float* f) {
+  uint4 v;
+  v.x = f2bf2(f[0], f[1]);
+  v.y = f2bf2(f[2], f[3]);
+  v.z = f2bf2(f[4], f[5]);
+  v.w = f2bf2(f[6], f[7]);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void upsample2x_fwd_v8_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ y,
+                                                                int B, int H, int W, int C) {
+  const int C8 = C >> 3;
+  const int total = B * H * W * C8;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = i % C8;
+    int p = i / C8;
+    const int xx = p % W;
+    p /= W;
+    const int yy = p % H;
+    const int b = p / H;
+    const int ys[3] = {yy > 0 ? yy - 1 : 0, yy, yy + 1 < H ? yy + 1 : H - 1};
+    const int xs[3] = {xx > 0 ? xx - 1 : 0, xx, xx + 1 < W ? xx + 1 : W - 1};
+    float r0[3][8], r1[3][8];                      // rows 2yy / 2yy+1 interpolated, per source column
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float a[8], m[8], z[8];
+      const long col = static_cast<long>(xs[c]) * C + 8 * c8;
+      up_unpack8(*reinterpret_cast<const uint4*>(x + (static_cast<long>(b * H + ys[0]) * W) * C + col), a);
+      up_unpack8(*reinterpret_cast<const uint4*>(x + (static_cast<long>(b * H + ys[1]) * W) * C + col), m);
+      up_unpack8(*reinterpret_cast<const uint4*>(x + (static_cast<long>(b * H + ys[2]) * W) * C + col), z);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        r0[c][e] = 0.25f * a[e] + 0.75f * m[e];
+        r1[c][e] = 0.75f * m[e] + 0.25f * z[e];
+      }
+    }
+    float o[8];
+    const long W2 = 2L * W;
+    const long base = ((static_cast<long>(b) * 2 * H + 2 * yy) * W2 + 2 * xx) * C + 8 * c8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.25f * r0[0][e] + 0.75f * r0[1][e];
+    *reinterpret_cast<uint4*>(y + base) = up_pack8(o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.75f * r0[1][e] + 0.25f * r0[2][e];
+    *reinterpret_cast<uint4*>(y + base + C) = up_pack8(o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.25f * r1[0][e] + 0.75f * r1[1][e];
+    *reinterpret_cast<uint4*>(y + base + W2 * C) = up_pack8(o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.75f * r1[1][e] + 0.25f * r1[2][e];
+    *reinterpret_cast<uint4*>(y + base + W2 * C + C) = up_pack8(o);
+  }
+}
+
+__device__ __forceinline__ float up_w(int t, int k, int n) {   // weight of output 2k-1+t on input k
+  if (t == 0) return k > 0 ? 0.25f : 0.f;
+  if (t == 1) return k == 0 ? 1.f : 0.75f;
+  if (t == 2) return k == n - 1 ? 1.f : 0.75f;
+  return k < n - 1 ? 0.25f : 0.f;
+}
+
+__global__ __launch_bounds__(256) void upsample2x_bwd_v8_kernel(const bf16_t* __restrict__ dy, bf16_t* __restrict__ dx,
+                                                                int B, int H, int W, int C) {
+  const int C8 = C >> 3;
+  const int total = B * H * W * C8;
+  const long W2 = 2L * W;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = i % C8;
+    int p = i / C8;
+    const int xx = p % W;
+    p /= W;
+    const int yy = p % H;
+    const int b = p / H;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ty = 0; ty < 4; ++ty) {
+      const float wy = up_w(ty, yy, H);
+      if (wy == 0.f) continue;
+      const int oy = 2 * yy - 1 + ty;
+#pragma unroll
+      for (int tx = 0; tx < 4; ++tx) {
+        const float w = wy * up_w(tx, xx, W);
+        if (w == 0.f) continue;
+        const int ox = 2 * xx - 1 + tx;
+        float v[8];
+        up_unpack8(*reinterpret_cast<const uint4*>(dy + ((static_cast<long>(b) * 2 * H + oy) * W2 + ox) * C + 8 * c8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] = fmaf(w, v[e], acc[e]);
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + ((static_cast<long>(b) * H + yy) * W + xx) * C + 8 * c8) = up_pack8(acc);
+  }
+}
+
 // pre [B][H*W][32] fp32 = bias + W_dense . dense_input(pixel)
 // dense columns: 0 height/256 | 1..4 visibility | 5..6 creep | 7..11 player_relative | 12..13 alerts |
 //                14..15 pathable | 16..17 buildable | 18..23 effects
@@ -694,6 +803,12 @@ int grid_for(long n) {
 }  // namespace
 
 void upsample2x_fwd(const void* x, void* y, int dt, int B, int H, int W, int C, hipStream_t s) {
+  const long n8 = static_cast<long>(B) * H * W * (C / 8);
+  if (dt == DT_BF16 && C % 8 == 0 && n8 < (1L << 31) - (1L << 24)) {
+    hipLaunchKernelGGL(upsample2x_fwd_v8_kernel, dim3(grid_for(n8)), dim3(256), 0, s, static_cast<const bf16_t*>(x),
+                       static_cast<bf16_t*>(y), B, H, W, C);
+    return;
+  }
   const long n = static_cast<long>(B) * 4 * H * W * (C / 4);
   if (dt == DT_BF16)
     hipLaunchKernelGGL(upsample2x_fwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const bf16_t*>(x),
@@ -704,6 +819,12 @@ void upsample2x_fwd(const void* x, void* y, int dt, int B, int H, int W, int C, 
 }
 
 void upsample2x_bwd(const void* dy, void* dx, int dt, int B, int H, int W, int C, hipStream_t s) {
+  const long n8 = static_cast<long>(B) * H * W * (C / 8);
+  if (dt == DT_BF16 && C % 8 == 0 && n8 < (1L << 31) - (1L << 24)) {
+    hipLaunchKernelGGL(upsample2x_bwd_v8_kernel, dim3(grid_for(n8)), dim3(256), 0, s, static_cast<const bf16_t*>(dy),
+                       static_cast<bf16_t*>(dx), B, H, W, C);
+    return;
+  }
   const long n = static_cast<long>(B) * H * W * (C / 4);
   if (dt == DT_BF16)
     hipLaunchKernelGGL(upsample2x_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s,
