@@ -390,6 +390,32 @@ std::vector<at::Tensor> spatial_embed_fwd(const std::vector<at::Tensor>& planes,
   return {at::Tensor(), out};
 }
 
+// relu(embed) -> max_pool2x2 fused: {pooled [B,H/2,W/2,32] bf16, pos [B,H/2,W/2,32] uint8}
+std::vector<at::Tensor> spatial_embed_pool_fwd(const std::vector<at::Tensor>& planes, const std::vector<at::Tensor>& effects,
+                                               const at::Tensor& w_dense, const at::Tensor& bias, const at::Tensor& rows,
+                                               const at::Tensor& ex, const at::Tensor& ey, const at::Tensor& entity_num) {
+  auto sp = make_planes(planes, effects);
+  const int64_t B = planes[0].size(0), H = planes[0].size(1), W = planes[0].size(2);
+  const int64_t L = effects[0].size(1);
+  TORCH_CHECK(as::spatial_pool_supported(static_cast<int>(H), static_cast<int>(W)), "spatial_embed_pool: H, W");
+  TORCH_CHECK(w_dense.size(0) == 32 && w_dense.size(1) == 24 && w_dense.scalar_type() == at::kFloat &&
+              bias.scalar_type() == at::kFloat && bias.numel() == 32, "spatial_embed_pool: w_dense [32,24], bias fp32");
+  check_cuda(rows, "rows");
+  TORCH_CHECK(rows.dim() == 3 && rows.size(0) == B && rows.size(2) == 32 && rows.scalar_type() == at::kBFloat16,
+              "spatial_embed_pool: rows [B,N,32] bf16");
+  TORCH_CHECK(ex.scalar_type() == at::kByte && ey.scalar_type() == at::kByte && entity_num.scalar_type() == at::kLong &&
+              ex.is_contiguous() && ey.is_contiguous() && entity_num.is_contiguous(),
+              "spatial_embed_pool: entity x/y uint8, entity_num int64, contiguous");
+  c10::hip::HIPGuard g(rows.device().index());
+  auto pooled = at::empty({B, H / 2, W / 2, 32}, rows.options());
+  auto pos = at::empty({B, H / 2, W / 2, 32}, rows.options().dtype(at::kByte));
+  as::spatial_embed_pool(sp, w_dense.data_ptr<float>(), bias.data_ptr<float>(), rows.data_ptr(), ex.data_ptr<uint8_t>(),
+                         ey.data_ptr<uint8_t>(), entity_num.data_ptr<int64_t>(), pooled.data_ptr(),
+                         pos.data_ptr<uint8_t>(), static_cast<int>(B), static_cast<int>(rows.size(1)),
+                         static_cast<int>(H), static_cast<int>(W), static_cast<int>(L), stream());
+  return {pooled, pos};
+}
+
 // (dWd fp32 [32, 24], db fp32 [32]) of the spatial 1x1 projection's dense columns from dpre [B,H,W,32]
 // gate (optional): the embedding's ReLU output; dpre is then dout and the ReLU mask is applied on the fly
 std::vector<at::Tensor> spatial_dense_wgrad(const std::vector<at::Tensor>& planes, const std::vector<at::Tensor>& effects,
@@ -614,6 +640,21 @@ at::Tensor maxpool2_bwd(const at::Tensor& dy, const at::Tensor& pos, int64_t H, 
   auto dx = at::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
   as::maxpool2_bwd(dy.data_ptr(), pos.data_ptr<uint8_t>(), dx.data_ptr(), dt(dy), dy.size(0), H, W, dy.size(3),
                    stream());
+  return dx;
+}
+
+at::Tensor maxpool2_bwd_relu(const at::Tensor& dy, const at::Tensor& pos, const at::Tensor& y, int64_t H, int64_t W) {
+  check_cuda(dy, "dy");
+  check_cuda(pos, "pos");
+  check_cuda(y, "y");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+              dy.sizes() == pos.sizes() && dy.sizes() == y.sizes() && H % 2 == 0 && W % 2 == 0 &&
+              dy.size(1) == H / 2 && dy.size(2) == W / 2 && dy.size(3) % 8 == 0, "maxpool2_bwd_relu: shapes");
+  TORCH_CHECK(dy.numel() < (1L << 31) - (1L << 24), "maxpool2_bwd_relu: size");
+  c10::hip::HIPGuard g(dy.device().index());
+  auto dx = at::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
+  as::maxpool2_bwd_relu(dy.data_ptr(), pos.data_ptr<uint8_t>(), y.data_ptr(), dx.data_ptr(), dy.size(0), H, W,
+                        dy.size(3), stream());
   return dx;
 }
 
@@ -1194,6 +1235,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("upconv1_bwd", &upconv1_bwd);
   m.def("maxpool2_fwd", &maxpool2_fwd);
   m.def("maxpool2_bwd", &maxpool2_bwd);
+  m.def("maxpool2_bwd_relu", &maxpool2_bwd_relu);
+  m.def("spatial_embed_pool_fwd", &spatial_embed_pool_fwd);
+  m.def("spatial_pool_supported", [](int64_t h, int64_t w) { return as::spatial_pool_supported(static_cast<int>(h), static_cast<int>(w)); });
   m.def("segment_sum", &segment_sum);
   m.def("table_grad", &table_grad);
   m.def("conv3x3_fwd", &conv3x3_fwd);

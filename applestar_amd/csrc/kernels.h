@@ -126,6 +126,12 @@ void relu_cast(const float* x, void* y, int dt, long n, hipStream_t s);
 void spatial_embed_fused(const SpatialPlanes& sp, const float* wd, const float* bias, const void* rows, int rows_dt,
                          const uint8_t* ex, const uint8_t* ey, const int64_t* entity_num, void* out, int out_dt, int B,
                          int N, int H, int W, int L, hipStream_t s);
+// pooled: relu(embed) -> max_pool2x2 in one pass (pixel-row pairs per workgroup); pooled [B,H/2,W/2,32] bf16,
+// pos [B,H/2,W/2,32] argmax bytes (maxpool2 format); needs spatial_pool_supported(H, W)
+bool spatial_pool_supported(int H, int W);
+void spatial_embed_pool(const SpatialPlanes& sp, const float* wd, const float* bias, const void* rows, const uint8_t* ex,
+                        const uint8_t* ey, const int64_t* entity_num, void* pooled, uint8_t* pos, int B, int N, int H,
+                        int W, int L, hipStream_t s);
 // per-workgroup partial rows [spatial_wgrad_blocks(B)][32*24 + 32] of dWd (n-major) and db from dpre [B*H*W, 32]
 int spatial_wgrad_blocks(int B);
 void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, const void* gate, int dt, float* part, int B, int H,
@@ -181,6 +187,9 @@ namespace as {
 // NHWC 2x2/stride-2 max-pool; pos [B,H/2,W/2,C] uint8 window position; C % 8 == 0
 void maxpool2_fwd(const void* x, void* y, uint8_t* pos, int dt, int B, int H, int W, int C, hipStream_t s);
 void maxpool2_bwd(const void* dy, const uint8_t* pos, void* dx, int dt, int B, int H, int W, int C, hipStream_t s);
+// bf16, even H / W: dx = dy at the argmax where the pooled ReLU output y > 0, else 0 (relu -> maxpool2 backward)
+void maxpool2_bwd_relu(const void* dy, const uint8_t* pos, const void* y, void* dx, int B, int H, int W, int C,
+                       hipStream_t s);
 // out [S, C] fp32 = per-segment row sums of x [T, C] (segments cu[s]..cu[s+1]); C <= 1024, C % 4 == 0
 void segment_sum(const void* x, int dt, const int* cu, float* out, int S, int C, hipStream_t s);
 // out [V, D] fp32 (zeroed) += src rows grouped by idx (V * D <= 16384)

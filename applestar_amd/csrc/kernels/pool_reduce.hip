@@ -240,6 +240,61 @@ __global__ __launch_bounds__(256) void column_reduce_atomic_kernel(const float* 
 
 }  // namespace
 
+namespace {
+// Backward of relu -> maxpool2 for even H, W (bf16): one thread per pooled pixel and 8 channels writes its
+// 2x2 input pixels; the gradient passes at the argmax when the pooled value (= the ReLU output there) is
+// positive.  Used by the fused spatial embed + pool stage, which keeps no full-resolution output.
+__global__ __launch_bounds__(256) void maxpool2_bwd_relu_kernel(const bf16_t* __restrict__ dy,
+                                                                const uint8_t* __restrict__ pos,
+                                                                const bf16_t* __restrict__ y, bf16_t* __restrict__ dx,
+                                                                int B, int H, int W, int C) {
+  const int Ho = H >> 1, Wo = W >> 1, C8 = C >> 3;
+  const int total = B * Ho * Wo * C8;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = i % C8;
+    int r = i / C8;
+    const int ox = r % Wo;
+    r /= Wo;
+    const int oy = r % Ho;
+    const int b = r / Ho;
+    const long oi = static_cast<long>(i) * 8;
+    const uint4 g = *reinterpret_cast<const uint4*>(dy + oi);
+    const uint4 yv = *reinterpret_cast<const uint4*>(y + oi);
+    const uint2 pp = *reinterpret_cast<const uint2*>(pos + oi);
+    const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
+    uint32_t outw[4][4];   // [window position][dword]
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) outw[t][j] = 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t p = ((k < 4 ? pp.x : pp.y) >> (8 * (k & 3))) & 3u;
+      const uint32_t raw = (k & 1) ? (gw[k >> 1] >> 16) : (gw[k >> 1] & 0xffffu);     // bf16 bits of dy
+      const float yk = __uint_as_float((k & 1) ? (yw[k >> 1] & 0xffff0000u) : (yw[k >> 1] << 16));
+      const uint32_t bits = yk > 0.f ? raw : 0u;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (p == static_cast<uint32_t>(t)) outw[t][k >> 1] |= bits << ((k & 1) ? 16 : 0);
+    }
+    const long row = static_cast<long>(W) * C;
+    const long i00 = ((static_cast<long>(b) * H + 2 * oy) * W + 2 * ox) * C + 8 * c8;
+    *reinterpret_cast<uint4*>(dx + i00) = make_uint4(outw[0][0], outw[0][1], outw[0][2], outw[0][3]);
+    *reinterpret_cast<uint4*>(dx + i00 + C) = make_uint4(outw[1][0], outw[1][1], outw[1][2], outw[1][3]);
+    *reinterpret_cast<uint4*>(dx + i00 + row) = make_uint4(outw[2][0], outw[2][1], outw[2][2], outw[2][3]);
+    *reinterpret_cast<uint4*>(dx + i00 + row + C) = make_uint4(outw[3][0], outw[3][1], outw[3][2], outw[3][3]);
+  }
+}
+}  // namespace
+
+void maxpool2_bwd_relu(const void* dy, const uint8_t* pos, const void* y, void* dx, int B, int H, int W, int C,
+                       hipStream_t s) {
+  const long n = static_cast<long>(B) * (H / 2) * (W / 2) * (C / 8);
+  if (n == 0) return;
+  hipLaunchKernelGGL(maxpool2_bwd_relu_kernel, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const bf16_t*>(dy), pos,
+                     static_cast<const bf16_t*>(y), static_cast<bf16_t*>(dx), B, H, W, C);
+}
+
 void maxpool2_fwd(const void* x, void* y, uint8_t* pos, int dt, int B, int H, int W, int C, hipStream_t s) {
   const long n = static_cast<long>(B) * (H / 2) * (W / 2) * (C / 8);
   if (n == 0) return;

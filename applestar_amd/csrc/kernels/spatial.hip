@@ -666,6 +666,142 @@ __global__ __launch_bounds__(256) void spatial_embed_mfma_kernel(SpatialPlanes s
   }
 }
 
+// Pooled form: the encoder's first stage is relu(embed) -> max_pool2x2 -> conv, and the full-resolution
+// embed map (B x 152 x 160 x 32 bf16 = 607 MB at the learner batch) feeds only that pool.  A tile here is one
+// pair of image rows (2W <= kPoolTile pixels), so the 2x2 windows are tile-local: the kernel writes the pooled
+// map and the argmax byte per channel (maxpool2's format, for its backward) and never the full map.
+constexpr int kPoolTile = 320;
+constexpr int kPoolMF = kPoolTile / 64;   // 16-pixel MFMA row fragments per wave
+
+__global__ __launch_bounds__(256) void spatial_embed_pool_kernel(SpatialPlanes sp, const float* __restrict__ wd,
+                                                                 const float* __restrict__ bias,
+                                                                 const bf16_t* __restrict__ rows,
+                                                                 const uint8_t* __restrict__ ex,
+                                                                 const uint8_t* __restrict__ ey,
+                                                                 const int64_t* __restrict__ entity_num,
+                                                                 bf16_t* __restrict__ pooled, uint8_t* __restrict__ pos,
+                                                                 int N, int H, int W, int L) {
+  __shared__ float acc_s[kPoolTile][33];
+  __shared__ uint32_t eb[kPoolTile];
+  __shared__ uint32_t msk[kPoolTile];
+  __shared__ uint32_t hgt[kPoolTile];
+  __shared__ int2 ent_list[kSpTile];
+  __shared__ int ent_cnt;
+  const int HW = H * W, Ho = H >> 1, Wo = W >> 1;
+  const int b = blockIdx.x / Ho, rp = blockIdx.x % Ho;
+  const int np = 2 * W, p0 = rp * np;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, g = l >> 4, lr = l & 15;
+  for (int i = tid; i < kPoolTile; i += 256) eb[i] = 0;
+  if (tid == 0) ent_cnt = 0;
+  bf8v bhi[2], blo[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int n = 16 * nt + lr;
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      uint32_t h2 = 0, l2 = 0;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int c = 8 * g + j + t;
+        const float v = c < 24 ? wd[n * 24 + c] : (c == 24 ? bias[n] : 0.f);
+        const bf16_t hi = f2bf(v);
+        const bf16_t lo = f2bf(v - bf2f(hi));
+        h2 |= static_cast<uint32_t>(hi) << (16 * t);
+        l2 |= static_cast<uint32_t>(lo) << (16 * t);
+      }
+      hw[j / 2] = h2;
+      lw[j / 2] = l2;
+    }
+    bhi[nt] = as_frag(make_uint4(hw[0], hw[1], hw[2], hw[3]));
+    blo[nt] = as_frag(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+  }
+  __syncthreads();
+  mark_effects(sp, eb, b, L, HW, p0, np);
+  __syncthreads();
+  for (int i = tid; i < kPoolTile; i += 256) {
+    if (i < np) {
+      const long pix = static_cast<long>(b) * HW + p0 + i;
+      msk[i] = pixel_mask(sp, pix, eb[i]);
+      hgt[i] = f2bf(static_cast<float>(sp.height[pix]) * (1.f / 256.f));
+    } else {
+      msk[i] = 0;
+      hgt[i] = 0;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < kPoolMF; ++m) {
+    const int pr = kPoolMF * 16 * w + 16 * m + lr;  // A row (pixel) of this lane
+    const uint32_t mb = (msk[pr] >> (8 * g)) & 0xFFu;
+    uint32_t q0 = bit_pair(mb, 0);
+    if (g == 0) q0 = (q0 & 0xFFFF0000u) | hgt[pr];
+    const bf8v a = as_frag(make_uint4(q0, bit_pair(mb, 2), bit_pair(mb, 4), bit_pair(mb, 6)));
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      f4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bhi[nt], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, blo[nt], c, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc_s[kPoolMF * 16 * w + 16 * m + 4 * g + i][16 * nt + lr] = c[i];
+    }
+  }
+  __syncthreads();
+  const int ne = static_cast<int>(entity_num[b] < N ? entity_num[b] : N);
+  for (int n = tid; n < ne; n += 256) {
+    const long bn = static_cast<long>(b) * N + n;
+    int x = ex[bn], y = ey[bn];
+    x = x < W ? x : W - 1;
+    y = y < H ? y : H - 1;
+    const int p = y * W + x - p0;
+    if (p >= 0 && p < np) {
+      const int slot = atomicAdd(&ent_cnt, 1);
+      if (slot < kSpTile) {
+        ent_list[slot] = make_int2(n, p);
+      } else {
+        for (int c = 0; c < 32; ++c) atomicAdd(&acc_s[p][c], bf2f(rows[bn * 32 + c]));
+      }
+    }
+  }
+  __syncthreads();
+  const int nl = ent_cnt < kSpTile ? ent_cnt : kSpTile;
+  for (int i = tid; i < nl * 32; i += 256) {
+    const int c = i & 31;
+    const int2 e = ent_list[i >> 5];
+    const long bn = static_cast<long>(b) * N + e.x;
+    atomicAdd(&acc_s[e.y][c], bf2f(rows[bn * 32 + c]));
+  }
+  __syncthreads();
+  // relu + 2x2 max (first maximum in window order wins, NaN propagates: maxpool2_fwd's rule) -> 8 channels
+  // of one pooled pixel per thread: 16-B value store + 8 argmax bytes
+  const long obase = (static_cast<long>(b) * Ho + rp) * Wo;
+  for (int i = tid; i < Wo * 4; i += 256) {
+    const int ox = i >> 2, c8 = 8 * (i & 3);
+    const int q[4] = {2 * ox, 2 * ox + 1, W + 2 * ox, W + 2 * ox + 1};
+    float mv[8];
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      // compared as the bf16 values the unfused map would hold, so ties resolve as max_pool2x2 on that map
+      float m = bf2f(f2bf(fmaxf(acc_s[q[0]][c8 + k], 0.f)));
+      uint32_t pp = 0;
+#pragma unroll
+      for (int t = 1; t < 4; ++t) {
+        const float v = bf2f(f2bf(fmaxf(acc_s[q[t]][c8 + k], 0.f)));
+        if (v > m || isnan(v)) { m = v; pp = t; }
+      }
+      mv[k] = m;
+      if (k < 4) lo |= pp << (8 * k);
+      else hi |= pp << (8 * (k - 4));
+    }
+    uint32_t o4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o4[j] = f2bf2(mv[2 * j], mv[2 * j + 1]);
+    const long o = (obase + ox) * 32 + c8;
+    *reinterpret_cast<uint4*>(pooled + o) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+    *reinterpret_cast<uint2*>(pos + o) = make_uint2(lo, hi);
+  }
+}
+
 constexpr int kSpP = kSpTile + 8;  // padded bf16 LDS row of the dpre^T image
 
 // 8 bf16 of v kept where the matching bf16 of g is > 0 (sign clear, not +0), zeroed elsewhere
@@ -832,6 +968,16 @@ void upsample2x_bwd(const void* dy, void* dx, int dt, int B, int H, int W, int C
   else
     hipLaunchKernelGGL(upsample2x_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const float*>(dy),
                        static_cast<float*>(dx), B, H, W, C);
+}
+
+bool spatial_pool_supported(int H, int W) { return H % 2 == 0 && W % 2 == 0 && 2 * W <= kPoolTile && W >= 2; }
+
+void spatial_embed_pool(const SpatialPlanes& sp, const float* wd, const float* bias, const void* rows, const uint8_t* ex,
+                        const uint8_t* ey, const int64_t* entity_num, void* pooled, uint8_t* pos, int B, int N, int H,
+                        int W, int L, hipStream_t s) {
+  hipLaunchKernelGGL(spatial_embed_pool_kernel, dim3(B * (H / 2)), dim3(256), 0, s, sp, wd, bias,
+                     static_cast<const bf16_t*>(rows), ex, ey, entity_num, static_cast<bf16_t*>(pooled), pos, N, H, W,
+                     L);
 }
 
 void spatial_effect_bits(const SpatialPlanes& sp, uint8_t* bits, int B, int L, int HW, hipStream_t s) {

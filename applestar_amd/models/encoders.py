@@ -351,12 +351,23 @@ class SpatialEncoder(nn.Module):
         scatter-add (W_s . sum_e p_e == sum_e W_s . p_e) and no 32-channel scatter map is built."""
         w = self.project[0].weight[:, :, 0, 0]                        # [32, 56]
         rows = ops.linear(proj, w[:, 24:])                            # [B,N,32]
+        pooled = native.spatial_embed_pool(spatial_info, rows, entity_x, entity_y, entity_num, w[:, :24],
+                                           self.project[0].bias) if native.has('spatial_embed_pool') else None
+        if pooled is not None:
+            return self.trunk(pooled, pooled_first=True)
         x = native.spatial_embed(spatial_info, rows, entity_x, entity_y, entity_num, w[:, :24], self.project[0].bias)
         return self.trunk(x)
 
-    def trunk(self, x):
+    def trunk(self, x, pooled_first: bool = False):
+        """``pooled_first``: x is already relu(embed) -> max_pool2x2 (the fused GPU stage), so the
+        full-resolution map is never built and skip level 0 is None — no consumer reads levels 0-2 (the
+        location head takes the last four)."""
         map_skip = []
-        for conv in self.downsample:
+        for i, conv in enumerate(self.downsample):
+            if i == 0 and pooled_first:
+                map_skip.append(None)
+                x = conv(x)
+                continue
             map_skip.append(x)
             x = conv(ops.max_pool2x2(x))
         for block in self.res:

@@ -112,6 +112,8 @@ class _TakeRows(torch.autograd.Function):
 
 
 def _take_rows(x, n):
+    if x is None:                 # a skip level the fused encoder never materialises (see SpatialEncoder.trunk)
+        return None
     if x.dim() == 4 and x.shape[0] > n and x.is_cuda:
         return _TakeRows.apply(x, n)
     return x[:n]

@@ -25,7 +25,7 @@ def ensure_loaded():
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
                 'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp',
-                'location_input', 'value_spatial_proj'}
+                'location_input', 'value_spatial_proj', 'spatial_embed_pool'}
 
 
 def has(name: str) -> bool:
@@ -290,6 +290,60 @@ def spatial_embed(spatial_info, rows, entity_x, entity_y, entity_num, w_dense, b
     ey = entity_y.to(torch.uint8).contiguous()
     out = _SpatialEmbed.apply(w_dense, bias, rows, ex, ey, entity_num.long().contiguous(), out_dtype, len(planes),
                               *planes, *effects)
+    return from_nhwc(out)
+
+
+SPATIAL_POOL_FUSED = os.environ.get('APPLESTAR_SPATIAL_POOL_FUSED', '1') == '1'
+
+
+class _SpatialEmbedPool(torch.autograd.Function):
+    """relu(embed) -> max_pool2x2 of the spatial encoder's first stage in one kernel (spatial.hip
+    spatial_embed_pool_kernel): the full-resolution map (607 MB at the learner batch) is neither written nor
+    re-read by a separate pool.  Backward: one pass builds the full-resolution dpre from the pooled gradient,
+    the argmax bytes and the pooled ReLU output (maxpool2_bwd_relu), then the unfused gather / dense-wgrad
+    kernels run on it without a gate."""
+
+    @staticmethod
+    def forward(ctx, w_dense, bias, rows, ex, ey, entity_num, n_planes, *tensors):
+        planes = list(tensors[:n_planes])
+        effects = list(tensors[n_planes:])
+        pooled, pos = _C.spatial_embed_pool_fwd(planes, effects, w_dense.detach().float().contiguous(),
+                                                bias.detach().float().contiguous(), rows.contiguous(), ex, ey,
+                                                entity_num)
+        ctx.save_for_backward(pooled, pos, ex, ey, entity_num, *tensors)
+        ctx.n_planes = n_planes
+        ctx.N = rows.shape[1]
+        ctx.rows_dtype = rows.dtype
+        ctx.HW = (planes[0].shape[1], planes[0].shape[2])
+        return pooled
+
+    @staticmethod
+    def backward(ctx, dpooled):
+        pooled, pos, ex, ey, entity_num, *tensors = ctx.saved_tensors
+        planes, effects = list(tensors[:ctx.n_planes]), list(tensors[ctx.n_planes:])
+        H, W = ctx.HW
+        dpre = _C.maxpool2_bwd_relu(dpooled.to(torch.bfloat16).contiguous(), pos, pooled, H, W)
+        drows = _C.spatial_gather_rows(dpre, ex, ey, entity_num, ctx.N).to(ctx.rows_dtype)
+        dw, db = _C.spatial_dense_wgrad(planes, effects, dpre)
+        return (dw, db, drows) + (None,) * (4 + len(tensors))
+
+
+def spatial_embed_pool(spatial_info, rows, entity_x, entity_y, entity_num, w_dense, bias):
+    """max_pool2x2(spatial_embed(...)) as [B,32,H/2,W/2] channels_last bf16, or None when the fused stage
+    does not apply (fp32 compute, odd or wide maps)."""
+    from ..lib.features import SPATIAL_ONE_HOT, EFFECT_KEYS
+    H, W = spatial_info['height_map'].shape[-2:]
+    if not SPATIAL_POOL_FUSED or not torch.is_autocast_enabled() and rows.dtype != torch.bfloat16 or \
+            not _C.spatial_pool_supported(H, W):
+        return None
+    planes = [spatial_info['height_map']] + [spatial_info[k] for k, _ in SPATIAL_ONE_HOT]
+    planes = [p.to(torch.uint8).contiguous() for p in planes]
+    effects = [spatial_info[k].to(torch.int16).contiguous() for k in EFFECT_KEYS]
+    ex = entity_x.to(torch.uint8).contiguous()
+    ey = entity_y.to(torch.uint8).contiguous()
+    with torch.autocast('cuda', enabled=False):
+        out = _SpatialEmbedPool.apply(w_dense, bias, rows.to(torch.bfloat16), ex, ey, entity_num.long().contiguous(),
+                                      len(planes), *planes, *effects)
     return from_nhwc(out)
 
 

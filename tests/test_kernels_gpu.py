@@ -945,3 +945,44 @@ def test_native_linear_reformulated_gemms(R, K, N, relu):
     (z * (y.detach().float() > 0) if relu else z).backward(g.float())
     for a, r in ((x.grad, xs.grad), (w.grad, ws.grad), (b.grad, bs.grad)):
         assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
+
+
+@pytest.mark.parametrize('HW', [(38, 40), (152, 160)])
+@pytest.mark.parametrize('crowded', [False, True])
+def test_spatial_embed_pool_matches_unfused(HW, crowded):
+    """Fused relu(embed) -> max_pool2x2 (pixel-row-pair tiles) vs the unfused native embed + maxpool:
+    pooled output bit-equal (same arithmetic, same argmax rule) and the rows / dense-weight / bias
+    gradients equal up to summation order."""
+    from applestar_amd.lib.features import SPATIAL_ONE_HOT, EFFECT_KEYS
+    from applestar_amd import ops
+    torch.manual_seed(31)
+    B, (H, W), L = 3, HW, 5
+    Nn = 400 if crowded else 37
+    sp = {'height_map': torch.randint(0, 256, (B, H, W), device=DEV, dtype=torch.uint8)}
+    for k, n in SPATIAL_ONE_HOT:
+        sp[k] = torch.randint(0, n + 1, (B, H, W), device=DEV, dtype=torch.uint8)
+    for k in EFFECT_KEYS:
+        sp[k] = torch.randint(0, H * W, (B, L), device=DEV, dtype=torch.int16)
+    ex = torch.randint(0, 6 if crowded else W, (B, Nn), device=DEV)
+    ey = torch.randint(0, 2 if crowded else H, (B, Nn), device=DEV)
+    en = torch.tensor([Nn, 4, 0], device=DEV)
+    rows0 = (torch.randn(B, Nn, 32, device=DEV) * (torch.arange(Nn, device=DEV)[None] < en[:, None]).unsqueeze(2))
+    w0 = torch.randn(32, 24, device=DEV) * 0.3
+    b0 = torch.randn(32, device=DEV) * 0.1
+    outs, grads = [], []
+    for fused in (True, False):
+        rows = rows0.to(torch.bfloat16).requires_grad_()
+        w, b = w0.clone().requires_grad_(), b0.clone().requires_grad_()
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            if fused:
+                y = N.spatial_embed_pool(sp, rows, ex, ey, en, w, b)
+                assert y is not None and y.shape == (B, 32, H // 2, W // 2)
+            else:
+                y = ops.max_pool2x2(N.spatial_embed(sp, rows, ex, ey, en, w, b))
+        g = torch.randn(B, 32, H // 2, W // 2, device=DEV, generator=torch.Generator(DEV).manual_seed(5))
+        y.backward(g.to(y.dtype).contiguous(memory_format=torch.channels_last))
+        outs.append(y.detach().float())
+        grads.append((rows.grad.float(), w.grad, b.grad))
+    assert torch.equal(outs[0], outs[1])
+    for a, r in zip(grads[0], grads[1]):
+        assert _err(a, r) < 1e-2 * max(1, r.abs().max().item())
