@@ -380,7 +380,8 @@ def test_segment_sum_and_gather_rows():
 
 @pytest.mark.parametrize('cin,cout,H,W', [(128, 128, 19, 20), (32, 64, 76, 80), (64, 128, 38, 40),
                                           (128, 64, 38, 40), (64, 32, 19, 21), (32, 32, 7, 5), (256, 128, 9, 9),
-                                          (16, 16, 38, 40), (16, 32, 19, 20), (32, 16, 11, 13), (16, 64, 7, 9)])
+                                          (16, 16, 38, 40), (16, 32, 19, 20), (32, 16, 11, 13), (16, 64, 7, 9),
+                                          (64, 32, 76, 80), (64, 32, 19, 20), (64, 64, 30, 62)])
 @pytest.mark.parametrize('act,res', [(None, False), ('relu', False), ('relu', True)])
 def test_conv3x3_mfma_matches_fp32(cin, cout, H, W, act, res):
     from applestar_amd import ops

@@ -12,7 +12,8 @@ import os
 import subprocess
 import sys
 
-SHAPES = [(390, 19, 20, 128, 128), (384, 19, 20, 128, 128), (390, 38, 40, 64, 128), (384, 38, 40, 128, 64)]
+SHAPES = [(390, 19, 20, 128, 128), (384, 19, 20, 128, 128), (390, 38, 40, 64, 128), (384, 38, 40, 128, 64),
+          (384, 76, 80, 64, 32)]
 
 
 def run():
