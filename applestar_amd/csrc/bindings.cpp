@@ -1101,6 +1101,59 @@ std::vector<at::Tensor> vsp_bwd(const at::Tensor& dout, const at::Tensor& out, c
   return {dsc, part.sum(0).view({as::vsp_out_channels(), as::vsp_in_channels() + 1})};
 }
 
+// pooled forms (even H, W): sc [B*H*W, 8], own / enemy [B*H*W] -> {pooled [B*(H/2)*(W/2), 16] bf16, pos uint8}
+std::vector<at::Tensor> vsp_pool_fwd(const at::Tensor& sc, const at::Tensor& own, const at::Tensor& enemy,
+                                     const at::Tensor& w, const at::Tensor& b, int64_t B, int64_t H, int64_t W) {
+  check_cuda(sc, "sc");
+  check_cuda(own, "own");
+  check_cuda(enemy, "enemy");
+  check_cuda(w, "w");
+  check_cuda(b, "b");
+  const int64_t P = B * H * W;
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && sc.dim() == 2 && sc.size(0) == P && sc.size(1) == as::vsp_in_channels() - 2 &&
+              sc.scalar_type() == at::kBFloat16, "vsp_pool: sc [B*H*W, 8] bf16, even H / W");
+  TORCH_CHECK(own.element_size() == 1 && enemy.element_size() == 1 && own.numel() == P && enemy.numel() == P,
+              "vsp_pool: own / enemy [B*H*W] bool");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.size(0) == as::vsp_out_channels() && w.size(1) == as::vsp_in_channels()
+              && b.scalar_type() == at::kFloat && b.numel() == as::vsp_out_channels(), "vsp_pool: w [16, 10], b [16] fp32");
+  c10::hip::HIPGuard g(sc.device().index());
+  const int64_t Po = B * (H / 2) * (W / 2);
+  auto pooled = at::empty({Po, as::vsp_out_channels()}, sc.options());
+  auto pos = at::empty({Po, as::vsp_out_channels()}, sc.options().dtype(at::kByte));
+  as::vsp_pool_fwd(sc.data_ptr(), own.data_ptr(), enemy.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(),
+                   pooled.data_ptr(), pos.data_ptr<uint8_t>(), static_cast<int>(B), static_cast<int>(H),
+                   static_cast<int>(W), stream());
+  return {pooled, pos};
+}
+
+// -> {dSc [B*H*W, 8] bf16, [dW | db] [16, 11] fp32}
+std::vector<at::Tensor> vsp_pool_bwd(const at::Tensor& dpooled, const at::Tensor& pos, const at::Tensor& pooled,
+                                     const at::Tensor& sc, const at::Tensor& own, const at::Tensor& enemy,
+                                     const at::Tensor& w, int64_t B, int64_t H, int64_t W) {
+  check_cuda(dpooled, "dpooled");
+  check_cuda(pos, "pos");
+  check_cuda(pooled, "pooled");
+  check_cuda(sc, "sc");
+  check_cuda(w, "w");
+  const int64_t P = B * H * W, Po = B * (H / 2) * (W / 2);
+  TORCH_CHECK(dpooled.scalar_type() == at::kBFloat16 && pooled.scalar_type() == at::kBFloat16 &&
+              dpooled.sizes() == pooled.sizes() && pos.sizes() == pooled.sizes() && pooled.size(0) == Po &&
+              pooled.size(1) == as::vsp_out_channels(), "vsp_pool_bwd: dpooled / pooled / pos [Po, 16]");
+  TORCH_CHECK(sc.size(0) == P && sc.size(1) == as::vsp_in_channels() - 2 && own.numel() == P && enemy.numel() == P &&
+              own.element_size() == 1 && enemy.element_size() == 1 && own.is_contiguous() && enemy.is_contiguous(),
+              "vsp_pool_bwd: sc / own / enemy");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.size(0) == as::vsp_out_channels() && w.size(1) == as::vsp_in_channels(),
+              "vsp_pool_bwd: w [16, 10] fp32");
+  c10::hip::HIPGuard g(sc.device().index());
+  const int nblk = as::vsp_bwd_blocks(Po);
+  auto dsc = at::empty_like(sc);
+  auto part = at::empty({nblk, as::vsp_out_channels() * (as::vsp_in_channels() + 1)}, sc.options().dtype(at::kFloat));
+  as::vsp_pool_bwd(dpooled.data_ptr(), pos.data_ptr<uint8_t>(), pooled.data_ptr(), sc.data_ptr(), own.data_ptr(),
+                   enemy.data_ptr(), w.data_ptr<float>(), dsc.data_ptr(), part.data_ptr<float>(), static_cast<int>(B),
+                   static_cast<int>(H), static_cast<int>(W), nblk, stream());
+  return {dsc, part.sum(0).view({as::vsp_out_channels(), as::vsp_in_channels() + 1})};
+}
+
 // ---------------------------------------------------------------- location-head input (locin.hip)
 // y0 [P, 128] bf16 (skip W_s^T + b), p [B, 4*HW] bf16 (fc output), wp [128, 4] fp32 -> relu(y0 + W_p relu(p))
 at::Tensor loc_in_fwd(const at::Tensor& y0, const at::Tensor& p, const at::Tensor& wp, int64_t HW) {
@@ -1249,6 +1302,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("multi_copy", &multi_copy);
   m.def("loc_in_fwd", &loc_in_fwd);
   m.def("vsp_fwd", &vsp_fwd);
+  m.def("vsp_pool_fwd", &vsp_pool_fwd);
+  m.def("vsp_pool_bwd", &vsp_pool_bwd);
   m.def("vsp_in_channels", []() { return as::vsp_in_channels(); });
   m.def("vsp_out_channels", []() { return as::vsp_out_channels(); });
   m.def("vsp_bwd", &vsp_bwd);

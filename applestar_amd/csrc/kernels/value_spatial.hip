@@ -135,6 +135,143 @@ __global__ __launch_bounds__(256) void vsp_bwd_kernel(const bf16_t* __restrict__
   }
 }
 
+// Pooled forms: the value encoder applies max_pool2x2 right after this projection, so (even H, W) one lane pair
+// per POOLED pixel evaluates its 2x2 window and writes the pooled map + maxpool2's argmax bytes; the 303 MB
+// full-resolution map is never written or re-read.  Backward: the gradient reaches only the argmax pixel of
+// each channel, and only where the pooled (ReLU) value is positive.
+__global__ __launch_bounds__(256) void vsp_pool_fwd_kernel(const bf16_t* __restrict__ sc, const uint8_t* __restrict__ own,
+                                                           const uint8_t* __restrict__ enemy, const float* __restrict__ w,
+                                                           const float* __restrict__ b, bf16_t* __restrict__ pooled,
+                                                           uint8_t* __restrict__ pos, int B, int H, int W) {
+  const int h = threadIdx.x & 1;
+  float wr[8][kVsIn], br[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    br[c] = b[8 * h + c];
+#pragma unroll
+    for (int k = 0; k < kVsIn; ++k) wr[c][k] = w[(8 * h + c) * kVsIn + k];
+  }
+  const int Ho = H >> 1, Wo = W >> 1;
+  const long Po = static_cast<long>(B) * Ho * Wo;
+  const long step = static_cast<long>(gridDim.x) * (blockDim.x >> 1);
+  for (long q = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) >> 1; q < Po; q += step) {
+    const int ox = static_cast<int>(q % Wo);
+    const long t = q / Wo;
+    const int oy = static_cast<int>(t % Ho);
+    const long bb = t / Ho;
+    const long p00 = (bb * H + 2 * oy) * W + 2 * ox;
+    const long pix[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
+    float m[8];
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int t4 = 0; t4 < 4; ++t4) {
+      float s[kVsSc];
+      vs_unpack8(*reinterpret_cast<const uint4*>(sc + pix[t4] * kVsSc), s);
+      const float fo = own[pix[t4]] ? 1.f : 0.f, fe = enemy[pix[t4]] ? 1.f : 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        float a = fmaf(wr[c][kVsSc], fo, fmaf(wr[c][kVsSc + 1], fe, br[c]));
+#pragma unroll
+        for (int k = 0; k < kVsSc; ++k) a = fmaf(wr[c][k], s[k], a);
+        const float v = bf2f(f2bf(fmaxf(a, 0.f)));     // the value the unfused bf16 map would hold
+        if (t4 == 0) {
+          m[c] = v;
+        } else if (v > m[c]) {
+          m[c] = v;
+          if (c < 4) lo = (lo & ~(0xffu << (8 * c))) | (static_cast<uint32_t>(t4) << (8 * c));
+          else hi = (hi & ~(0xffu << (8 * (c - 4)))) | (static_cast<uint32_t>(t4) << (8 * (c - 4)));
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(pooled + q * kVsOut + 8 * h) = vs_pack8(m);
+    *reinterpret_cast<uint2*>(pos + q * kVsOut + 8 * h) = make_uint2(lo, hi);
+  }
+}
+
+__global__ __launch_bounds__(256) void vsp_pool_bwd_kernel(const bf16_t* __restrict__ dpooled,
+                                                           const uint8_t* __restrict__ pos,
+                                                           const bf16_t* __restrict__ pooled,
+                                                           const bf16_t* __restrict__ sc, const uint8_t* __restrict__ own,
+                                                           const uint8_t* __restrict__ enemy, const float* __restrict__ w,
+                                                           bf16_t* __restrict__ dsc, float* __restrict__ part, int B,
+                                                           int H, int W) {
+  __shared__ float red[4][2][kVsAcc];
+  const int h = threadIdx.x & 1;
+  float wr[8][kVsSc], acc[8][kVsIn + 1];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int k = 0; k < kVsSc; ++k) wr[c][k] = w[(8 * h + c) * kVsIn + k];
+#pragma unroll
+    for (int k = 0; k <= kVsIn; ++k) acc[c][k] = 0.f;
+  }
+  const int Ho = H >> 1, Wo = W >> 1;
+  const long Po = static_cast<long>(B) * Ho * Wo;
+  const long step = static_cast<long>(gridDim.x) * (blockDim.x >> 1);
+  for (long q = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) >> 1; q < Po; q += step) {
+    const int ox = static_cast<int>(q % Wo);
+    const long t = q / Wo;
+    const int oy = static_cast<int>(t % Ho);
+    const long bb = t / Ho;
+    const long p00 = (bb * H + 2 * oy) * W + 2 * ox;
+    float d[8], y[8];
+    vs_unpack8(*reinterpret_cast<const uint4*>(dpooled + q * kVsOut + 8 * h), d);
+    vs_unpack8(*reinterpret_cast<const uint4*>(pooled + q * kVsOut + 8 * h), y);
+    const uint2 pp = *reinterpret_cast<const uint2*>(pos + q * kVsOut + 8 * h);
+#pragma unroll 1
+    for (int t4 = 0; t4 < 4; ++t4) {
+      float g[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint32_t pc = ((c < 4 ? pp.x : pp.y) >> (8 * (c & 3))) & 0xffu;
+        g[c] = (pc == static_cast<uint32_t>(t4) && y[c] > 0.f) ? d[c] : 0.f;
+      }
+      float ds[kVsSc];
+#pragma unroll
+      for (int k = 0; k < kVsSc; ++k) ds[k] = 0.f;
+      float s[kVsSc];
+      const long px = p00 + (t4 >> 1) * W + (t4 & 1);
+      vs_unpack8(*reinterpret_cast<const uint4*>(sc + px * kVsSc), s);
+      const float fo = own[px] ? 1.f : 0.f, fe = enemy[px] ? 1.f : 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+#pragma unroll
+        for (int k = 0; k < kVsSc; ++k) {
+          acc[c][k] = fmaf(g[c], s[k], acc[c][k]);
+          ds[k] = fmaf(wr[c][k], g[c], ds[k]);
+        }
+        acc[c][kVsSc] = fmaf(g[c], fo, acc[c][kVsSc]);
+        acc[c][kVsSc + 1] = fmaf(g[c], fe, acc[c][kVsSc + 1]);
+        acc[c][kVsIn] += g[c];
+      }
+#pragma unroll
+      for (int k = 0; k < kVsSc; ++k) ds[k] += __shfl_xor(ds[k], 1, 64);
+      if (h == 0) *reinterpret_cast<uint4*>(dsc + px * kVsSc) = vs_pack8(ds);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c)
+#pragma unroll
+    for (int k = 0; k <= kVsIn; ++k) {
+      float v = acc[c][k];
+#pragma unroll
+      for (int off = 2; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+      acc[c][k] = v;
+    }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane < 2) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int k = 0; k <= kVsIn; ++k) red[wv][lane][c * (kVsIn + 1) + k] = acc[c][k];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 2 * kVsAcc; e += blockDim.x) {
+    const int hh = e / kVsAcc, j = e % kVsAcc;
+    part[static_cast<long>(blockIdx.x) * 2 * kVsAcc + e] = red[0][hh][j] + red[1][hh][j] + red[2][hh][j] + red[3][hh][j];
+  }
+}
+
 }  // namespace
 
 int vsp_in_channels() { return kVsIn; }
@@ -154,6 +291,26 @@ int vsp_bwd_blocks(long P) {
   long blocks = (P * 2 + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   return static_cast<int>(blocks < 1 ? 1 : blocks);
+}
+
+void vsp_pool_fwd(const void* sc, const void* own, const void* enemy, const float* w, const float* b, void* pooled,
+                  uint8_t* pos, int B, int H, int W, hipStream_t s) {
+  const long Po = static_cast<long>(B) * (H / 2) * (W / 2);
+  long blocks = (Po * 2 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(vsp_pool_fwd_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
+                     static_cast<const bf16_t*>(sc), static_cast<const uint8_t*>(own),
+                     static_cast<const uint8_t*>(enemy), w, b, static_cast<bf16_t*>(pooled), pos, B, H, W);
+}
+
+void vsp_pool_bwd(const void* dpooled, const uint8_t* pos, const void* pooled, const void* sc, const void* own,
+                  const void* enemy, const float* w, void* dsc, float* part, int B, int H, int W, int nblk,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(vsp_pool_bwd_kernel, dim3(nblk), dim3(256), 0, s, static_cast<const bf16_t*>(dpooled), pos,
+                     static_cast<const bf16_t*>(pooled), static_cast<const bf16_t*>(sc),
+                     static_cast<const uint8_t*>(own), static_cast<const uint8_t*>(enemy), w,
+                     static_cast<bf16_t*>(dsc), part, B, H, W);
 }
 
 void vsp_bwd(const void* dout, const void* out, const void* sc, const void* own, const void* enemy, const float* w,

@@ -470,9 +470,13 @@ class ValueEncoder(nn.Module):
         H, W = x['own_units_spatial'].shape[-2:]
         sc = ops.scatter_connection(proj, x['unit_x'], x['unit_y'], H, W)
         c = self.project[0]
-        fused = ops.value_spatial_proj(sc, x['own_units_spatial'], x['enemy_units_spatial'], c.weight, c.bias) \
-            if sc.is_cuda else None
-        if fused is not None:
+        pooled = ops.value_spatial_proj_pool(sc, x['own_units_spatial'], x['enemy_units_spatial'], c.weight, c.bias) \
+            if sc.is_cuda and isinstance(self.downsample[0], MaxPool2x2) else None
+        fused = None if pooled is not None or not sc.is_cuda else \
+            ops.value_spatial_proj(sc, x['own_units_spatial'], x['enemy_units_spatial'], c.weight, c.bias)
+        if pooled is not None:
+            sp = pooled          # = downsample[0](projection): the first pool is fused into the projection
+        elif fused is not None:
             sp = fused
         elif sc.is_cuda:
             # assembled directly in NHWC, zero-padded 10 -> 16 channels (with a zero-padded 1x1 weight) so
@@ -487,7 +491,7 @@ class ValueEncoder(nn.Module):
             sp = torch.cat([sc.to(proj.dtype), x['own_units_spatial'].to(proj.dtype),
                             x['enemy_units_spatial'].to(proj.dtype)], 1)
             sp = self.project(sp)
-        sp = self.downsample(sp)
+        sp = self.downsample[1:](sp) if pooled is not None else self.downsample(sp)
         for blk in self.res:
             sp = blk(sp)
         sp = self.spatial_fc(sp.reshape(sp.shape[0], -1))

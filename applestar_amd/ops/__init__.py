@@ -88,6 +88,14 @@ def value_spatial_proj(sc, own, enemy, w, b):
     return None
 
 
+def value_spatial_proj_pool(sc, own, enemy, w, b):
+    """max_pool2x2 of the fused value-encoder spatial input on the GPU; None when it does not apply."""
+    n = _native(sc)
+    if n is not None and n.has('value_spatial_proj_pool'):
+        return n.value_spatial_proj_pool(sc, own, enemy, w, b)
+    return None
+
+
 def location_input(pf, skip, w, b):
     """Fused location-head input stage relu(conv1x1(relu(cat([pf as [B,P,H,W], skip])))) on the GPU
     (skip a channels_last ReLU output); None when it does not apply (caller runs the cat path)."""

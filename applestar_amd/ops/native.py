@@ -25,7 +25,7 @@ def ensure_loaded():
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
                 'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp',
-                'location_input', 'value_spatial_proj', 'spatial_embed_pool'}
+                'location_input', 'value_spatial_proj', 'spatial_embed_pool', 'value_spatial_proj_pool'}
 
 
 def has(name: str) -> bool:
@@ -708,6 +708,7 @@ def conv2d(x, w, b, stride, padding, act, residual):
 
 # ---------------------------------------------------------------------------- value spatial input (value_spatial.hip)
 VSP_FUSED = os.environ.get('APPLESTAR_VSP_FUSED', '1') == '1'
+VSP_POOL_FUSED = os.environ.get('APPLESTAR_VSP_POOL_FUSED', '1') == '1'
 
 
 class _ValueSpatialProj(torch.autograd.Function):
@@ -729,6 +730,44 @@ class _ValueSpatialProj(torch.autograd.Function):
         dsc, dwb = _C.vsp_bwd(dout.to(torch.bfloat16).contiguous(), out, sc2d, own, enemy, wf)
         w_dtype, b_dtype = ctx.dtypes
         return dsc, None, None, dwb[:, :-1].to(w_dtype), dwb[:, -1].to(b_dtype)
+
+
+class _ValueSpatialProjPool(torch.autograd.Function):
+    """max_pool2x2(relu(conv1x1(cat([scatter map, own, enemy])))) in one pass per pooled pixel
+    (value_spatial.hip vsp_pool_*): neither the 16-channel full-resolution map nor its pool gradient is built."""
+
+    @staticmethod
+    def forward(ctx, sc2d, own, enemy, w2, b, B, H, W):
+        wf, bf = w2.detach().float().contiguous(), b.detach().float().contiguous()
+        pooled, pos = _C.vsp_pool_fwd(sc2d, own, enemy, wf, bf, B, H, W)
+        ctx.save_for_backward(sc2d, own, enemy, wf, pooled, pos)
+        ctx.meta = (w2.dtype, b.dtype, B, H, W)
+        return pooled
+
+    @staticmethod
+    def backward(ctx, dpooled):
+        sc2d, own, enemy, wf, pooled, pos = ctx.saved_tensors
+        w_dtype, b_dtype, B, H, W = ctx.meta
+        dsc, dwb = _C.vsp_pool_bwd(dpooled.to(torch.bfloat16).contiguous(), pos, pooled, sc2d, own, enemy, wf, B, H, W)
+        return dsc, None, None, dwb[:, :-1].to(w_dtype), dwb[:, -1].to(b_dtype), None, None, None
+
+
+def value_spatial_proj_pool(sc, own, enemy, w, b):
+    """max_pool2x2 of :func:`value_spatial_proj` as a channels_last [B, 16, H/2, W/2] view (even H, W);
+    None when it does not apply."""
+    if not (VSP_FUSED and VSP_POOL_FUSED):
+        return None
+    B, C, H, W = sc.shape
+    cout, cin = w.shape[0], w.shape[1]
+    if H % 2 or W % 2 or cout != _C.vsp_out_channels() or cin != _C.vsp_in_channels() or C != cin - 2 or b is None \
+            or own.dtype != torch.bool or enemy.dtype != torch.bool or own.numel() != B * H * W \
+            or enemy.numel() != B * H * W:
+        return None
+    sc2d = nhwc(sc.to(torch.bfloat16)).view(-1, C)
+    with torch.autocast('cuda', enabled=False):
+        y = _ValueSpatialProjPool.apply(sc2d, own.reshape(-1).view(torch.uint8), enemy.reshape(-1).view(torch.uint8),
+                                        w.view(cout, cin), b, B, H, W)
+    return from_nhwc(y.view(B, H // 2, W // 2, cout))
 
 
 def value_spatial_proj(sc, own, enemy, w, b):

@@ -987,3 +987,31 @@ def test_spatial_embed_pool_matches_unfused(HW, crowded):
     assert torch.equal(outs[0], outs[1])
     for a, r in zip(grads[0], grads[1]):
         assert _err(a, r) < 1e-2 * max(1, r.abs().max().item())
+
+
+@pytest.mark.parametrize('B,H,W', [(3, 152, 160), (2, 6, 10)])
+def test_value_spatial_proj_pool_matches_unfused(B, H, W):
+    """Pooled value-encoder projection (value_spatial.hip vsp_pool_*) vs value_spatial_proj followed by the
+    native max_pool2x2: pooled output bit-equal, scatter-map / weight / bias gradients equal up to order."""
+    from applestar_amd import ops
+    torch.manual_seed(41)
+    sc0 = torch.zeros(B * H * W, 8, device=DEV)
+    hot = torch.rand(B * H * W, device=DEV) < 0.05
+    sc0[hot] = torch.randn(int(hot.sum()), 8, device=DEV)
+    own = torch.rand(B, 1, H, W, device=DEV) < 0.1
+    enemy = torch.rand(B, 1, H, W, device=DEV) < 0.1
+    w0 = 0.3 * torch.randn(16, 10, 1, 1, device=DEV)
+    b0 = 0.1 * torch.randn(16, device=DEV)
+    g = torch.randn(B, 16, H // 2, W // 2, device=DEV).bfloat16().contiguous(memory_format=torch.channels_last)
+    res = []
+    for fused in (True, False):
+        sc = sc0.bfloat16().view(B, H, W, 8).permute(0, 3, 1, 2).requires_grad_()
+        w, b = w0.bfloat16().requires_grad_(), b0.bfloat16().requires_grad_()
+        y = N.value_spatial_proj_pool(sc, own, enemy, w, b) if fused else \
+            ops.max_pool2x2(N.value_spatial_proj(sc, own, enemy, w, b))
+        assert y is not None and y.shape == (B, 16, H // 2, W // 2)
+        y.backward(g)
+        res.append((y.detach().float(), sc.grad.float(), w.grad.float(), b.grad.float()))
+    assert torch.equal(res[0][0], res[1][0])
+    for a, r in zip(res[0][1:], res[1][1:]):
+        assert _err(a, r) < 1e-2 * max(1, r.abs().max().item())
