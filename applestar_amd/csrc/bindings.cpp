@@ -1154,6 +1154,34 @@ std::vector<at::Tensor> vsp_pool_bwd(const at::Tensor& dpooled, const at::Tensor
   return {dsc, part.sum(0).view({as::vsp_out_channels(), as::vsp_in_channels() + 1})};
 }
 
+// ---------------------------------------------------------------- RL loss tail (rl_loss.hip)
+// -> {info [rl_loss_info_size(F)], dalp, dent, dkl [6,T,B], dv [F,T+1,B]}
+std::vector<at::Tensor> rl_loss(const at::Tensor& alp, const at::Tensor& blp, const at::Tensor& hm, const at::Tensor& ent,
+                                const at::Tensor& kl, const at::Tensor& v, const at::Tensor& r, const at::Tensor& wm,
+                                const at::Tensor& atflag, const at::Tensor& sc, int64_t upgo_f, bool only_value) {
+  for (const at::Tensor* t : {&alp, &blp, &hm, &ent, &kl, &v, &r, &wm, &atflag, &sc}) {
+    check_cuda(*t, "rl_loss operand");
+    TORCH_CHECK(t->scalar_type() == at::kFloat, "rl_loss: fp32 operands");
+  }
+  TORCH_CHECK(alp.dim() == 3 && alp.size(0) == 6, "rl_loss: alp [6,T,B]");
+  const int64_t T = alp.size(1), B = alp.size(2), F = v.size(0);
+  TORCH_CHECK(blp.sizes() == alp.sizes() && hm.sizes() == alp.sizes() && ent.sizes() == alp.sizes() &&
+              kl.sizes() == alp.sizes(), "rl_loss: per-head operands [6,T,B]");
+  TORCH_CHECK(F >= 1 && F <= 6 && v.dim() == 3 && v.size(1) == T + 1 && v.size(2) == B && r.dim() == 3 &&
+              r.size(0) == F && r.size(1) == T && r.size(2) == B && wm.sizes() == r.sizes(), "rl_loss: fields");
+  TORCH_CHECK(atflag.numel() == T * B && T * B <= as::rl_loss_max_tb() && T >= 1, "rl_loss: [T,B] size");
+  TORCH_CHECK(sc.numel() == 4 * F + 4 * 6 + 4 && upgo_f >= -1 && upgo_f < F, "rl_loss: scalars");
+  c10::hip::HIPGuard g(alp.device().index());
+  auto info = at::empty({as::rl_loss_info_size(static_cast<int>(F))}, alp.options());
+  auto dalp = at::empty_like(alp), dent = at::empty_like(alp), dkl = at::empty_like(alp), dv = at::empty_like(v);
+  as::rl_loss(alp.data_ptr<float>(), blp.data_ptr<float>(), hm.data_ptr<float>(), ent.data_ptr<float>(),
+              kl.data_ptr<float>(), v.data_ptr<float>(), r.data_ptr<float>(), wm.data_ptr<float>(),
+              atflag.data_ptr<float>(), sc.data_ptr<float>(), static_cast<int>(F), static_cast<int>(T),
+              static_cast<int>(B), static_cast<int>(upgo_f), only_value ? 1 : 0, dalp.data_ptr<float>(),
+              dent.data_ptr<float>(), dkl.data_ptr<float>(), dv.data_ptr<float>(), info.data_ptr<float>(), stream());
+  return {info, dalp, dent, dkl, dv};
+}
+
 // ---------------------------------------------------------------- location-head input (locin.hip)
 // y0 [P, 128] bf16 (skip W_s^T + b), p [B, 4*HW] bf16 (fc output), wp [128, 4] fp32 -> relu(y0 + W_p relu(p))
 at::Tensor loc_in_fwd(const at::Tensor& y0, const at::Tensor& p, const at::Tensor& wp, int64_t HW) {
@@ -1302,6 +1330,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("multi_copy", &multi_copy);
   m.def("loc_in_fwd", &loc_in_fwd);
   m.def("vsp_fwd", &vsp_fwd);
+  m.def("rl_loss", &rl_loss);
   m.def("vsp_pool_fwd", &vsp_pool_fwd);
   m.def("vsp_pool_bwd", &vsp_pool_bwd);
   m.def("vsp_in_channels", []() { return as::vsp_in_channels(); });

@@ -318,4 +318,11 @@ void head_stats_fwd(const void* l, int l_dt, const void* t, int t_dt, const long
 // dl [R, C] (l's dtype) = g_a d(logp_a) + g_H dH + g_KL dKL, g [3, R]
 void head_stats_bwd(const void* l, int l_dt, const void* t, int t_dt, const long* act, const float* stats,
                     const float* g, void* dl, long R, int C, hipStream_t s);
+// ---- rl_loss.hip: the RL loss after the per-head statistics, with its closed-form gradients (one workgroup)
+int rl_loss_info_size(int F);
+int rl_loss_max_tb();
+void rl_loss(const float* alp, const float* blp, const float* hm, const float* ent, const float* kl, const float* v,
+             const float* r, const float* wm, const float* atflag, const float* sc, int F, int T, int B, int upgo_f,
+             int only_value, float* dalp, float* dent, float* dkl, float* dv, float* info, hipStream_t s);
+
 }  // namespace as

@@ -88,6 +88,11 @@ def value_spatial_proj(sc, own, enemy, w, b):
     return None
 
 
+def rl_loss_tail(alp, ent, kl, v, blp, hm, r, wm, atflag, sc, upgo_f, only_value):
+    """Fused RL loss tail (GPU): (total, info vector); callers check _native(...).has('rl_loss') first."""
+    return _native(v).rl_loss_tail(alp, ent, kl, v, blp, hm, r, wm, atflag, sc, upgo_f, only_value)
+
+
 def value_spatial_proj_pool(sc, own, enemy, w, b):
     """max_pool2x2 of the fused value-encoder spatial input on the GPU; None when it does not apply."""
     n = _native(sc)

@@ -25,7 +25,8 @@ def ensure_loaded():
 _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
                 'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp',
-                'location_input', 'value_spatial_proj', 'spatial_embed_pool', 'value_spatial_proj_pool'}
+                'location_input', 'value_spatial_proj', 'spatial_embed_pool', 'value_spatial_proj_pool',
+                'rl_loss'}
 
 
 def has(name: str) -> bool:
@@ -345,6 +346,33 @@ def spatial_embed_pool(spatial_info, rows, entity_x, entity_y, entity_num, w_den
         out = _SpatialEmbedPool.apply(w_dense, bias, rows.to(torch.bfloat16), ex, ey, entity_num.long().contiguous(),
                                       len(planes), *planes, *effects)
     return from_nhwc(out)
+
+
+class _RLLossTail(torch.autograd.Function):
+    """The RL loss after the per-head statistics (rl_loss.hip): one kernel computes the total, the info
+    vector and the closed-form gradients w.r.t. the stacked log-probs / entropies / KLs / values; backward
+    only scales them by the incoming gradient."""
+
+    @staticmethod
+    def forward(ctx, alp, ent, kl, v, blp, hm, r, wm, atflag, sc, upgo_f, only_value):
+        c = lambda t: t.detach().float().contiguous()  # noqa: E731
+        info, dalp, dent, dkl, dv = _C.rl_loss(c(alp), c(blp), c(hm), c(ent), c(kl), c(v), c(r), c(wm), c(atflag),
+                                               sc, int(upgo_f), bool(only_value))
+        ctx.save_for_backward(dalp, dent, dkl, dv)
+        ctx.dtypes = (alp.dtype, ent.dtype, kl.dtype, v.dtype)
+        ctx.mark_non_differentiable(info)
+        return info[-1], info
+
+    @staticmethod
+    def backward(ctx, gtotal, ginfo):
+        dalp, dent, dkl, dv = ctx.saved_tensors
+        da, de, dk, dvv = (g * gtotal for g in (dalp, dent, dkl, dv))
+        return (da.to(ctx.dtypes[0]), de.to(ctx.dtypes[1]), dk.to(ctx.dtypes[2]), dvv.to(ctx.dtypes[3])) + (None,) * 8
+
+
+def rl_loss_tail(alp, ent, kl, v, blp, hm, r, wm, atflag, sc, upgo_f, only_value):
+    """(total loss 0-d, info vector) of the fused RL loss tail; see rl/loss.py _compute_loss_fused."""
+    return _RLLossTail.apply(alp, ent, kl, v, blp, hm, r, wm, atflag, sc, upgo_f, only_value)
 
 
 # ---------------------------------------------------------------------------- varlen attention

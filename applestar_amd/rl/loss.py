@@ -14,6 +14,7 @@ Differences by design (not in the math):
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict
 
 import torch
@@ -24,6 +25,7 @@ from ..utils.config import AttrDict, deep_merge_dicts
 from . import rl_utils
 
 HEADS = ['action_type', 'delay', 'queued', 'selected_units', 'target_unit', 'target_location']
+FUSED_LOSS = os.environ.get('APPLESTAR_FUSED_LOSS', '1') == '1'
 
 DEFAULT_RL_LOSS_CONFIG = AttrDict({
     'loss_weights': {
@@ -76,7 +78,102 @@ class ReinforcementLoss:
             cache[key] = torch.tensor([w.get(h, 1.0) for h in HEADS], device=device)
         return cache[key]
 
+    # ------------------------------------------------------------------ fused GPU tail (rl_loss.hip)
+    _PG_MASKED_FIELDS = ('build_order', 'built_unit', 'effect')
+
+    def _fused_ok(self, inputs: Dict) -> bool:
+        if not FUSED_LOSS:
+            return False
+        v0 = next(iter(inputs['value'].values()))
+        if not v0.is_cuda or (self.use_dapo and 'successive_logit' in inputs):
+            return False
+        n = ops._native(v0)
+        if n is None or not n.has('rl_loss'):
+            return False
+        T, B = inputs['reward']['winloss'].shape if 'winloss' in inputs['reward'] else (0, 0)
+        return 0 < T * B <= 2048 and 1 <= len(inputs['value']) <= 6
+
+    def _scalars(self, fields, device) -> torch.Tensor:
+        cache = self.__dict__.setdefault('_sc_cache', {})
+        key = (tuple(fields), str(device))
+        if key not in cache:
+            c = self.cfg
+            vals = []
+            for f in fields:
+                vals += [self.w.pg.get(f, 0.0), self.w.baseline.get(f, 0.0), float(self.gammas.pg.get(f, 1.0)),
+                         float(self.gammas.baseline.get(f, 1.0))]
+            for table in (c.pg_head_weights, c.upgo_head_weights, c.entropy_head_weights, c.kl_head_weights):
+                vals += [table.get(h, 1.0) for h in HEADS]
+            vals += [self.w.upgo.winloss, self.w.entropy, self.w.kl, self.w.action_type_kl]
+            cache[key] = torch.tensor(vals, dtype=torch.float32, device=device)
+        return cache[key]
+
+    def _compute_loss_fused(self, inputs: Dict) -> Dict[str, torch.Tensor]:
+        """Same loss and info as the torch path below: the per-head statistics and their [T, B] reductions
+        here, everything after them (scans, means, gradients) in one native kernel (ops.native.rl_loss_tail)."""
+        logits = inputs['target_logit']
+        values = inputs['value']
+        behaviour_logp = inputs['action_log_prob']
+        teacher_logits = inputs['teacher_logit']
+        masks = inputs['mask']
+        actions = inputs['action']
+        rewards = inputs['reward']
+        am = masks['actions_mask']
+        su_mask = masks['selected_units_mask'].float()
+        fields = list(values.keys())
+        V = torch.stack([values[k].float() for k in fields], 0)                     # [F, T+1, B]
+        not_done = (rewards['winloss'][-1] == 0).to(V.dtype)
+        V = torch.cat([V[:, :-1], V[:, -1:] * not_done], 1)
+        alps, blps, ents, kls = [], [], [], []
+        for h in HEADS:
+            alp, ent, kl = ops.head_stats(logits[h], teacher_logits.get(h), actions[h])
+            blp = behaviour_logp[h].float()
+            if h == 'selected_units':
+                n_valid = masks['selected_units_logits_mask'].float().sum(-1)
+                alp = (alp * su_mask).sum(-1)
+                blp = (blp * su_mask).sum(-1)
+                ent = (ent / (1e-9 + torch.log(n_valid + 1).unsqueeze(-1)) * su_mask).sum(-1) / (su_mask.sum(-1) + 1e-9)
+                kl = (kl * su_mask).sum(-1)
+            elif h == 'target_unit':
+                ent = ent / (1e-9 + torch.log(masks['target_units_logits_mask'].float().sum(-1) + 1))
+            else:
+                ent = ent / math.log(logits[h].shape[-1])
+            alps.append(alp)
+            blps.append(blp)
+            ents.append(ent)
+            kls.append(kl)
+        ones = torch.ones_like(alps[0])
+        hm = torch.stack([ones, ones] + [am[h].float() for h in ['queued', 'selected_units', 'target_unit',
+                                                                  'target_location']], 0)
+        R = torch.stack([rewards[k].float() for k in fields], 0)
+        WM = torch.stack([masks[k + '_mask'].float() if k in self._PG_MASKED_FIELDS else ones for k in fields], 0)
+        atflag = (inputs['step'] < self.action_type_kl_steps).float() * masks['cum_action_mask'].float()
+        upgo_f = fields.index('winloss') if 'winloss' in fields else -1
+        total, vec = ops.rl_loss_tail(torch.stack(alps, 0), torch.stack(ents, 0), torch.stack(kls, 0), V,
+                                      torch.stack(blps, 0).detach(), hm, R, WM, atflag,
+                                      self._scalars(fields, V.device), upgo_f, self.only_update_value)
+        info: Dict[str, torch.Tensor] = {}
+        o = 0
+        for f in fields:
+            info[f'{f}/total'] = vec[o]
+            for i, h in enumerate(HEADS):
+                info[f'{f}/{h}'] = vec[o + 1 + i]
+            info[f + '/td'], info[f + '/reward'], info[f + '/value'] = vec[o + 7], vec[o + 8], vec[o + 9]
+            o += 10
+        if 'battle' in rewards:
+            info['battle/reward'] = rewards['battle'].float().mean()
+        for name in ('upgo', 'entropy', 'kl'):
+            for i, h in enumerate(HEADS):
+                info[f'{name}/{h}'] = vec[o + i]
+            info[f'{name}/total'] = vec[o + 6]
+            o += 7
+        info['kl/extra_at'] = vec[o]
+        info['total_loss'] = total
+        return info
+
     def compute_loss(self, inputs: Dict) -> Dict[str, torch.Tensor]:
+        if self._fused_ok(inputs):
+            return self._compute_loss_fused(inputs)
         logits = inputs['target_logit']
         values = dict(inputs['value'])
         behaviour_logp = inputs['action_log_prob']

@@ -299,3 +299,55 @@ def test_data_parallel_two_ranks_finite_and_identical(tmp_path):
     for s in range(3):
         a, b = [r['grad_norm'] for r in recs if r['step'] == s]
         assert a == b
+
+
+@pytest.mark.parametrize('only_value', [False, True])
+def test_fused_rl_loss_matches_torch_loss(only_value):
+    """rl_loss.hip (the loss after the per-head statistics, with closed-form gradients) vs the torch
+    ReinforcementLoss path: total loss, every info entry, and the gradients w.r.t. all head logits and the
+    baseline values; two baseline fields (winloss + build_order with its mask)."""
+    from applestar_amd.rl import loss as L
+    dev = torch.device('cuda')
+    T, B = 16, 3
+    batch = to_device(rl_batch(B, T, max_entities=40, seed=3), dev)
+    g = torch.Generator(device=dev).manual_seed(7)
+
+    def make_inputs():
+        logits = {}
+        for h, t in batch['teacher_logit'].items():
+            x = t + 0.5 * torch.randn(t.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(hash(h) % 1000))
+            logits[h] = torch.where(t > -1e8, x, torch.full_like(x, -1e9)).requires_grad_()
+        values = {'winloss': (0.3 * torch.randn(T + 1, B, device=dev, generator=torch.Generator(device=dev).manual_seed(1))).requires_grad_(),
+                  'build_order': (0.3 * torch.randn(T + 1, B, device=dev, generator=torch.Generator(device=dev).manual_seed(2))).requires_grad_()}
+        mask = dict(batch['mask'])
+        mask['build_order_mask'] = (torch.rand(T, B, device=dev, generator=g) < 0.7).float()
+        return {'target_logit': logits, 'value': values, 'action_log_prob': batch['behaviour_logp'],
+                'teacher_logit': batch['teacher_logit'], 'mask': mask, 'action': batch['action_info'],
+                'reward': batch['reward'], 'step': batch['step']}
+
+    cfg = {'loss_weights': {'pg': {'build_order': 0.5}, 'baseline': {'build_order': 2.0}}}
+    results = []
+    inp = make_inputs()
+    for fused in (True, False):
+        L.FUSED_LOSS = fused
+        try:
+            loss = L.ReinforcementLoss(cfg)
+            loss.only_update_value = only_value
+            x = {k: v for k, v in inp.items()}
+            info = loss.compute_loss(x)
+            leaves = list(inp['target_logit'].values()) + list(inp['value'].values())
+            grads = torch.autograd.grad(info['total_loss'], leaves, allow_unused=True)
+            results.append((info, grads))
+        finally:
+            L.FUSED_LOSS = True
+    (fi, fg), (ti, tg) = results
+    assert set(fi) == set(ti)
+    for k in ti:
+        a, r = float(fi[k]), float(ti[k])
+        assert abs(a - r) <= 1e-4 + 1e-4 * abs(r), (k, a, r)
+    for a, r in zip(fg, tg):
+        if r is None:
+            assert a is None or float(a.abs().max()) == 0.0
+            continue
+        a = torch.zeros_like(r) if a is None else a
+        assert float((a - r).abs().max()) <= 1e-5 + 1e-4 * float(r.abs().max())

@@ -25,6 +25,7 @@ def main():
     ap.add_argument('--unroll', type=int, default=2)
     ap.add_argument('--max-entities', type=int, default=16)
     ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--no-sync', action='store_true', help='pipelined steps (no device sync between them): shows where the host blocks')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}, device=dev)
@@ -33,7 +34,8 @@ def main():
     b['entity_total'] = entity_total_hint(h)
     tot = {}
     for i in range(args.steps + 3):
-        torch.cuda.synchronize()
+        if not args.no_sync:
+            torch.cuda.synchronize()
         t = [time.perf_counter()]
         if not tr.model.training:
             tr.model.train()
@@ -48,7 +50,8 @@ def main():
         tr._reduce()
         tr._update()
         t.append(time.perf_counter())
-        torch.cuda.synchronize()
+        if not args.no_sync:
+            torch.cuda.synchronize()
         t.append(time.perf_counter())
         if i >= 3:
             for k, a, z in (('forward', 0, 1), ('loss', 1, 2), ('backward', 2, 3), ('update', 3, 4), ('gpu_tail', 4, 5),

@@ -38,7 +38,10 @@ class Timer(TorchDispatchMode):
         if _skip(name):
             return func(*args, **(kwargs or {}))
         frames = [f for f in traceback.extract_stack()[:-1] if 'applestar_amd' in f.filename]
-        where = ' <- '.join(f'{f.filename.split("applestar_amd/")[-1]}:{f.lineno}' for f in frames[-2:][::-1])
+        depth = int(os.environ.get('OP_FRAMES', '2'))
+        where = ' <- '.join(f'{f.filename.split("applestar_amd/")[-1]}:{f.lineno}' for f in frames[-depth:][::-1])
+        if os.environ.get('OP_SHAPES'):
+            where += ' ' + ' '.join(f'{tuple(a.shape)}{str(a.dtype)[6:]}' for a in args if isinstance(a, torch.Tensor))[:60]
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         out = func(*args, **(kwargs or {}))
