@@ -1154,6 +1154,55 @@ std::vector<at::Tensor> vsp_pool_bwd(const at::Tensor& dpooled, const at::Tensor
   return {dsc, part.sum(0).view({as::vsp_out_channels(), as::vsp_in_channels() + 1})};
 }
 
+// ---------------------------------------------------------------- gate chain (gate_chain.hip)
+// x [P,128] bf16; m: 4 x [128,128] bf16 (row n = output channel); bias: 4 x fp32 [128] or None; mask / res:
+// 4 x bf16 [P,128] or None; relu_mask bit L: ReLU after layer L -> 4 outputs [P,128] bf16
+std::vector<at::Tensor> gate_chain(const at::Tensor& x, const std::vector<at::Tensor>& m,
+                                   const std::vector<c10::optional<at::Tensor>>& bias,
+                                   const std::vector<c10::optional<at::Tensor>>& mask,
+                                   const std::vector<c10::optional<at::Tensor>>& res, int64_t relu_mask) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.size(1) == 128 && x.is_contiguous(),
+              "gate_chain: x [P,128] bf16 contiguous");
+  TORCH_CHECK(m.size() == 4 && bias.size() == 4 && mask.size() == 4 && res.size() == 4, "gate_chain: 4 layers");
+  const int64_t P = x.size(0);
+  as::GateChainArgs a{};
+  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr());
+  a.relu_mask = static_cast<int>(relu_mask);
+  std::vector<at::Tensor> outs;
+  for (int L = 0; L < 4; ++L) {
+    check_cuda(m[L], "m");
+    TORCH_CHECK(m[L].scalar_type() == at::kBFloat16 && m[L].size(0) == 128 && m[L].numel() == 128 * 128 &&
+                m[L].is_contiguous(), "gate_chain: m [128,128] bf16 contiguous");
+    a.m[L] = reinterpret_cast<const uint16_t*>(m[L].data_ptr());
+    a.bias[L] = nullptr;
+    if (bias[L].has_value()) {
+      check_cuda(*bias[L], "bias");
+      TORCH_CHECK(bias[L]->scalar_type() == at::kFloat && bias[L]->numel() == 128, "gate_chain: bias fp32 [128]");
+      a.bias[L] = bias[L]->data_ptr<float>();
+    }
+    a.mask[L] = nullptr;
+    if (mask[L].has_value()) {
+      check_cuda(*mask[L], "mask");
+      TORCH_CHECK(mask[L]->scalar_type() == at::kBFloat16 && mask[L]->sizes() == x.sizes() &&
+                  mask[L]->is_contiguous(), "gate_chain: mask like x");
+      a.mask[L] = reinterpret_cast<const uint16_t*>(mask[L]->data_ptr());
+    }
+    a.res[L] = nullptr;
+    if (res[L].has_value()) {
+      check_cuda(*res[L], "res");
+      TORCH_CHECK(res[L]->scalar_type() == at::kBFloat16 && res[L]->sizes() == x.sizes() &&
+                  res[L]->is_contiguous(), "gate_chain: res like x");
+      a.res[L] = reinterpret_cast<const uint16_t*>(res[L]->data_ptr());
+    }
+    outs.push_back(at::empty_like(x));
+    a.out[L] = reinterpret_cast<uint16_t*>(outs.back().data_ptr());
+  }
+  c10::hip::HIPGuard g(x.device().index());
+  as::gate_chain(a, P, stream());
+  return outs;
+}
+
 // ---------------------------------------------------------------- RL loss tail (rl_loss.hip)
 // -> {info [rl_loss_info_size(F)], dalp, dent, dkl [6,T,B], dv [F,T+1,B]}
 std::vector<at::Tensor> rl_loss(const at::Tensor& alp, const at::Tensor& blp, const at::Tensor& hm, const at::Tensor& ent,
@@ -1331,6 +1380,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("loc_in_fwd", &loc_in_fwd);
   m.def("vsp_fwd", &vsp_fwd);
   m.def("rl_loss", &rl_loss);
+  m.def("gate_chain", &gate_chain);
   m.def("vsp_pool_fwd", &vsp_pool_fwd);
   m.def("vsp_pool_bwd", &vsp_pool_bwd);
   m.def("vsp_in_channels", []() { return as::vsp_in_channels(); });

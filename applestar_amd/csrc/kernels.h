@@ -325,4 +325,18 @@ void rl_loss(const float* alp, const float* blp, const float* hm, const float* e
              const float* r, const float* wm, const float* atflag, const float* sc, int F, int T, int B, int upgo_f,
              int only_value, float* dalp, float* dent, float* dkl, float* dv, float* info, hipStream_t s);
 
+// ---- gate_chain.hip: four chained 128 x 128 pointwise layers, activation tile resident in LDS
+// layer L: out[L] = epilogue(in @ m[L]^T) with m[L] [128 out][128 in] bf16; epilogue: + bias[L] (fp32,
+// nullable), ReLU if bit L of relu_mask, zero where mask[L] (bf16 [P,128], nullable) <= 0, + res[L] (nullable)
+struct GateChainArgs {
+  const uint16_t* x;
+  const uint16_t* m[4];
+  const float* bias[4];
+  const uint16_t* mask[4];
+  const uint16_t* res[4];
+  uint16_t* out[4];
+  int relu_mask;
+};
+void gate_chain(const GateChainArgs& a, long P, hipStream_t s);
+
 }  // namespace as

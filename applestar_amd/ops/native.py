@@ -612,6 +612,9 @@ def resblock(x, w1, b1, w2, b2):
         return from_nhwc(_ResBlock.apply(xl, w1l, b1, w2l, b2))
 
 
+GATE_CHAIN = os.environ.get('APPLESTAR_GATE_CHAIN', '1') == '1'
+
+
 class _GatedResBlock(torch.autograd.Function):
     """Location-head GatedResBlock (module_utils.py:204-231) as one autograd node on NHWC bf16:
 
@@ -629,10 +632,17 @@ class _GatedResBlock(torch.autograd.Function):
         y = _C.conv3x3_fwd(y1, _conv_w(w2), b2.detach().float().contiguous(), None, 0)
         h = x.view(-1, C)
         acts = [h]
-        for i in range(4):
-            gw, gb = gate[2 * i].detach().view(C, C), gate[2 * i + 1].detach()
-            h = torch._addmm_activation(gb, h, gw.t(), use_gelu=False) if i < 3 else torch.addmm(gb, h, gw.t())
-            acts.append(h)
+        if GATE_CHAIN and C == 128:
+            # the four gate layers in one launch, activation tile resident in LDS (gate_chain.hip)
+            acts += _C.gate_chain(h, [gate[2 * i].detach().view(C, C) for i in range(4)],
+                                  [gate[2 * i + 1].detach().float().contiguous() for i in range(4)],
+                                  [None] * 4, [None] * 4, 0b0111)
+            h = acts[-1]
+        else:
+            for i in range(4):
+                gw, gb = gate[2 * i].detach().view(C, C), gate[2 * i + 1].detach()
+                h = torch._addmm_activation(gb, h, gw.t(), use_gelu=False) if i < 3 else torch.addmm(gb, h, gw.t())
+                acts.append(h)
         out = _C.gated_residual_fwd(y, h.view(B, H, W, C), sp, x)
         ctx.save_for_backward(x, sp, w1, w2, y1, y, out, *acts[1:], *gate[0::2])
         ctx.dtypes = (b1.dtype, b2.dtype, gate[1].dtype)
@@ -648,14 +658,24 @@ class _GatedResBlock(torch.autograd.Function):
         d = dg.view(-1, C)
         acts_in = [x.view(-1, C), a1, a2, a3]
         gws = [gw1, gw2, gw3, gw4]
-        for i in (3, 2, 1, 0):
-            dw_i, db_i = _C.wgrad(d, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
-            grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
-            if i > 0:
-                dh = torch.mm(d, gws[i].view(C, C))
-                P = dh.shape[0]
-                d = _C.act_grad_nhwc(dh.view(1, 1, P, C), acts_in[i].view(1, 1, P, C), True).view(P, C)
-        dx_gate = torch.addmm(dx_res.view(-1, C), d, gw1.view(C, C))          # skip + G1 input gradients
+        if GATE_CHAIN and C == 128:
+            # d3, d2, d1 and the gate-path input gradient (+ the skip gradient) in one launch; the weight
+            # gradients from the saved layer inputs and these
+            d3, d2, d1, dx_gate = _C.gate_chain(d, [gws[i].view(C, C).t().contiguous() for i in (3, 2, 1, 0)],
+                                                [None] * 4, [a3, a2, a1, None], [None, None, None, dx_res.view(-1, C)],
+                                                0)
+            for i, di in ((3, d), (2, d3), (1, d2), (0, d1)):
+                dw_i, db_i = _C.wgrad(di, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
+                grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
+        else:
+            for i in (3, 2, 1, 0):
+                dw_i, db_i = _C.wgrad(d, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
+                grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
+                if i > 0:
+                    dh = torch.mm(d, gws[i].view(C, C))
+                    P = dh.shape[0]
+                    d = _C.act_grad_nhwc(dh.view(1, 1, P, C), acts_in[i].view(1, 1, P, C), True).view(P, C)
+            dx_gate = torch.addmm(dx_res.view(-1, C), d, gw1.view(C, C))      # skip + G1 input gradients
         # conv path
         dpre1 = _conv_dx_drelu(dy, w2, y1)
         dw2, db2 = _conv_dw(dy, y1, w2, ctx.dtypes[1])

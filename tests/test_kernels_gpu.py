@@ -693,11 +693,48 @@ def test_fused_resblock_matches_unfused(C, H, W):
         assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
 
 
-def test_fused_gated_resblock_matches_unfused():
+@pytest.mark.parametrize('P', [1520, 128, 77])
+def test_gate_chain_matches_fp32(P):
+    """Four chained 128x128 pointwise layers in one launch (gate_chain.hip), forward form (bias + ReLU on
+    the first three) and backward form (transposed operands, ReLU masks of saved activations, residual
+    gradient added to the last output), vs fp32 torch of the same chain on the same bf16 inputs."""
+    torch.manual_seed(23)
+    C = 128
+    x = torch.randn(P, C, device=DEV).to(torch.bfloat16)
+    ws = [(torch.randn(C, C, device=DEV) / C ** 0.5).to(torch.bfloat16) for _ in range(4)]
+    bs = [0.1 * torch.randn(C, device=DEV) for _ in range(4)]
+    outs = N._C.gate_chain(x, ws, bs, [None] * 4, [None] * 4, 0b0111)
+    h = x.float()
+    for i in range(4):
+        h = h @ ws[i].float().t() + bs[i]
+        if i < 3:
+            h = torch.relu(h)
+        assert _err(outs[i], h) < 2e-2 * max(1.0, h.abs().max().item())
+        h = outs[i].float()                      # continue from the kernel's bf16 rows (mask agreement)
+    a1, a2, a3 = outs[:3]
+    dg = torch.randn(P, C, device=DEV).to(torch.bfloat16)
+    dres = torch.randn(P, C, device=DEV).to(torch.bfloat16)
+    wt = [ws[i].t().contiguous() for i in (3, 2, 1, 0)]
+    d3, d2, d1, dx = N._C.gate_chain(dg, wt, [None] * 4, [a3, a2, a1, None], [None, None, None, dres], 0)
+    d = dg.float()
+    for got, w, m, res in ((d3, ws[3], a3, None), (d2, ws[2], a2, None), (d1, ws[1], a1, None),
+                           (dx, ws[0], None, dres)):
+        r = d @ w.float()
+        if m is not None:
+            r = r * (m.float() > 0)
+        if res is not None:
+            r = r + res.float()
+        assert _err(got, r) < 2e-2 * max(1.0, r.abs().max().item())
+        d = got.float()
+
+
+@pytest.mark.parametrize('gate_chain', [True, False])
+def test_fused_gated_resblock_matches_unfused(gate_chain, monkeypatch):
     """One-node GatedResBlock vs the per-op native path (conv / 1x1 GEMM / gated-residual kernels, each
-    checked against fp32 elsewhere)."""
+    checked against fp32 elsewhere), with the gate path as one gate_chain launch or as four GEMMs."""
     from applestar_amd import ops
     from applestar_amd.models.blocks import GatedResBlock
+    monkeypatch.setattr(N, 'GATE_CHAIN', gate_chain)
     torch.manual_seed(19)
     C = 128
     blk = GatedResBlock(C).to(DEV).to(memory_format=torch.channels_last)
