@@ -42,7 +42,7 @@ def test_rl_pipeline_end_to_end(tmp_path, monkeypatch):
     threading.Thread(target=srv.serve_forever, daemon=True).start()
     comm = {'coordinator_ip': '127.0.0.1', 'coordinator_port': cport, 'league_ip': '127.0.0.1',
             'league_port': lport, 'learner_send_model_freq': 1, 'learner_send_train_info_freq': 2,
-            'actor_ask_for_job_interval': 40, 'actor_model_update_interval': 1}
+            'actor_ask_for_job_interval': 240, 'actor_model_update_interval': 1}
     T = 3
     learner_holder = {}
 
