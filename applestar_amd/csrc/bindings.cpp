@@ -1314,6 +1314,58 @@ void multi_copy(const std::vector<at::Tensor>& dsts, const std::vector<at::Tenso
   flush();
 }
 
+// ---------------------------------------------------------------- strided multi-tensor copy (derived weight forms)
+// dsts[t] (contiguous, fp32/bf16) <- srcs[t] read through spec[9 t .. 9 t + 8] = {size0..3, stride0..3, base}
+// (element units, relative to srcs[t].data_ptr(); strides may be negative).  Every reachable source offset is
+// checked against the source tensor's own extent before anything is launched.
+void multi_strided_copy(const std::vector<at::Tensor>& dsts, const std::vector<at::Tensor>& srcs,
+                        const std::vector<int64_t>& spec) {
+  TORCH_CHECK(dsts.size() == srcs.size() && spec.size() == 9 * dsts.size(), "multi_strided_copy: list sizes");
+  if (dsts.empty()) return;
+  c10::hip::HIPGuard g(dsts[0].device().index());
+  as::StridedCopyArgs a;
+  a.ntensors = 0;
+  a.chunk_start[0] = 0;
+  auto flush = [&]() {
+    if (a.ntensors > 0) as::multi_strided_copy(a, stream());
+    a.ntensors = 0;
+    a.chunk_start[0] = 0;
+  };
+  for (size_t i = 0; i < dsts.size(); ++i) {
+    const at::Tensor& d = dsts[i];
+    const at::Tensor& s = srcs[i];
+    TORCH_CHECK(d.is_cuda() && s.is_cuda() && d.device() == s.device(), "multi_strided_copy: GPU tensors");
+    TORCH_CHECK(d.is_contiguous(), "multi_strided_copy: contiguous destination");
+    TORCH_CHECK((d.scalar_type() == at::kFloat || d.scalar_type() == at::kBFloat16) &&
+                (s.scalar_type() == at::kFloat || s.scalar_type() == at::kBFloat16), "multi_strided_copy: fp32/bf16");
+    const int64_t* sp = spec.data() + 9 * i;
+    int64_t n = 1, lo = sp[8], hi = sp[8];
+    for (int k = 0; k < 4; ++k) {
+      TORCH_CHECK(sp[k] >= 1, "multi_strided_copy: sizes >= 1");
+      n *= sp[k];
+      const int64_t reach = (sp[k] - 1) * sp[4 + k];
+      if (reach < 0) lo += reach; else hi += reach;
+    }
+    TORCH_CHECK(n == d.numel() && n < (int64_t{1} << 31), "multi_strided_copy: spec / destination size");
+    int64_t extent = 1;                 // elements spanned by the source view itself
+    for (int64_t k = 0; k < s.dim(); ++k) extent += (s.size(k) - 1) * s.stride(k);
+    TORCH_CHECK(lo >= 0 && hi < extent, "multi_strided_copy: spec reaches outside the source");
+    const int t = a.ntensors++;
+    a.src[t] = s.data_ptr();
+    a.dst[t] = d.data_ptr();
+    a.n[t] = static_cast<int>(n);
+    for (int k = 0; k < 4; ++k) {
+      a.size[t][k] = static_cast<int>(sp[k]);
+      a.stride[t][k] = sp[4 + k];
+    }
+    a.base[t] = sp[8];
+    a.dts[t] = static_cast<unsigned char>((s.scalar_type() == at::kFloat ? 1 : 0) | (d.scalar_type() == at::kFloat ? 2 : 0));
+    a.chunk_start[t + 1] = a.chunk_start[t] + static_cast<int>((n + as::kCopyChunk - 1) / as::kCopyChunk);
+    if (a.ntensors == as::kSCopyMaxT) flush();
+  }
+  flush();
+}
+
 // ---------------------------------------------------------------- narrow 1x1 conv on NHWC pixels
 at::Tensor pointwise_conv(const at::Tensor& x, const at::Tensor& w, const c10::optional<at::Tensor>& bias, int64_t act) {
   check_cuda(x, "x");
@@ -1377,6 +1429,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pointwise_supported", [](int64_t ci, int64_t co) { return as::pointwise_supported(static_cast<int>(ci), static_cast<int>(co)); });
   m.def("lstm_split_error", &lstm_split_error);
   m.def("multi_copy", &multi_copy);
+  m.def("multi_strided_copy", &multi_strided_copy);
   m.def("loc_in_fwd", &loc_in_fwd);
   m.def("vsp_fwd", &vsp_fwd);
   m.def("rl_loss", &rl_loss);

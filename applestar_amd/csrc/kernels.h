@@ -227,6 +227,24 @@ struct CopyArgs {                     // passed by value (< 2 KB of kernel argum
 };
 void multi_copy(const CopyArgs& a, hipStream_t s);
 
+// Strided multi-tensor copy (+ dtype conversion) into contiguous destinations: dst[t][i] for the dst index
+// i = ((i0 * size1 + i1) * size2 + i2) * size3 + i3 reads src[t][base + sum_k ik * stride_k] (strides may be
+// negative: flipped conv weights).  Rebuilds every derived weight form (fp32 biases, transposed GEMM weights,
+// flipped/transposed conv weights) after an optimizer step in one launch per kSCopyMaxT tensors.
+constexpr int kSCopyMaxT = 24;
+struct StridedCopyArgs {                 // passed by value (~2.1 KB of kernel arguments)
+  int ntensors;
+  int chunk_start[kSCopyMaxT + 1];
+  const void* src[kSCopyMaxT];
+  void* dst[kSCopyMaxT];
+  int n[kSCopyMaxT];
+  int size[kSCopyMaxT][4];
+  long stride[kSCopyMaxT][4];
+  long base[kSCopyMaxT];
+  unsigned char dts[kSCopyMaxT];         // bit 0: src fp32, bit 1: dst fp32 (else bf16)
+};
+void multi_strided_copy(const StridedCopyArgs& a, hipStream_t s);
+
 // ---- pointwise.hip -----------------------------------------------------------------------------
 // y [P, cout] bf16 = act(x [P, cin] bf16 . w^T (fp32 [cout, cin]) + bias); cin, cout in {8, 16, 32}
 bool pointwise_supported(int cin, int cout);

@@ -26,11 +26,43 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyArgs a) {
   }
 }
 
+
+__global__ __launch_bounds__(256) void strided_copy_kernel(const StridedCopyArgs a) {
+  const int b = blockIdx.x;
+  int t = 0;
+  while (t + 1 < a.ntensors && a.chunk_start[t + 1] <= b) ++t;
+  const int i0 = (b - a.chunk_start[t]) * static_cast<int>(kCopyChunk);
+  const int i1 = i0 + static_cast<int>(kCopyChunk) < a.n[t] ? i0 + static_cast<int>(kCopyChunk) : a.n[t];
+  const bool sf = (a.dts[t] & 1) != 0, df = (a.dts[t] & 2) != 0;
+  const int s1 = a.size[t][1], s2 = a.size[t][2], s3 = a.size[t][3];
+  const long st0 = a.stride[t][0], st1 = a.stride[t][1], st2 = a.stride[t][2], st3 = a.stride[t][3];
+  const void* src = a.src[t];
+  void* dst = a.dst[t];
+  for (int i = i0 + threadIdx.x; i < i1; i += 256) {
+    int r = i;
+    const int c3 = r % s3;
+    r /= s3;
+    const int c2 = r % s2;
+    r /= s2;
+    const int c1 = r % s1;
+    const int c0 = r / s1;
+    const long off = a.base[t] + c0 * st0 + c1 * st1 + c2 * st2 + c3 * st3;
+    const float v = sf ? static_cast<const float*>(src)[off] : bf2f(static_cast<const bf16_t*>(src)[off]);
+    if (df) static_cast<float*>(dst)[i] = v;
+    else static_cast<bf16_t*>(dst)[i] = f2bf(v);
+  }
+}
+
 }  // namespace
 
 void multi_copy(const CopyArgs& a, hipStream_t s) {
   const int nblk = a.chunk_start[a.ntensors];
   if (nblk > 0) hipLaunchKernelGGL(multi_copy_kernel, dim3(nblk), dim3(256), 0, s, a);
+}
+
+void multi_strided_copy(const StridedCopyArgs& a, hipStream_t s) {
+  const int nblk = a.chunk_start[a.ntensors];
+  if (nblk > 0) hipLaunchKernelGGL(strided_copy_kernel, dim3(nblk), dim3(256), 0, s, a);
 }
 
 }  // namespace as

@@ -195,7 +195,7 @@ class _EntityEmbed(torch.autograd.Function):
         kind = [_KIND[e] for _, e, _, _ in ENTITY_LAYOUT]
         offset = [o for _, _, o, _ in ENTITY_LAYOUT]
         width = [x for _, _, _, x in ENTITY_LAYOUT]
-        wq = w.detach().to(out_dtype).t().contiguous()       # [997, 256]
+        wq = _wT(w, out_dtype)                              # [997, 256]
         out = _C.entity_embed_fwd(list(fields), kind, offset, width, index, wq, b.detach().float(),
                                   _dt_code(out_dtype))
         ctx.save_for_backward(out, index, *fields)
@@ -250,8 +250,8 @@ class _SpatialEmbed(torch.autograd.Function):
     def forward(ctx, w_dense, bias, rows, ex, ey, entity_num, out_dtype, n_planes, *tensors):
         planes = list(tensors[:n_planes])
         effects = list(tensors[n_planes:])
-        _, out = _C.spatial_embed_fwd(planes, effects, w_dense.detach().float().contiguous(),
-                                      bias.detach().float(), rows.contiguous(), ex, ey, entity_num,
+        _, out = _C.spatial_embed_fwd(planes, effects, _w32(w_dense),
+                                      _w32(bias), rows.contiguous(), ex, ey, entity_num,
                                       _dt_code(out_dtype))
         ctx.save_for_backward(out, ex, ey, entity_num, *tensors)
         ctx.n_planes = n_planes
@@ -308,8 +308,8 @@ class _SpatialEmbedPool(torch.autograd.Function):
     def forward(ctx, w_dense, bias, rows, ex, ey, entity_num, n_planes, *tensors):
         planes = list(tensors[:n_planes])
         effects = list(tensors[n_planes:])
-        pooled, pos = _C.spatial_embed_pool_fwd(planes, effects, w_dense.detach().float().contiguous(),
-                                                bias.detach().float().contiguous(), rows.contiguous(), ex, ey,
+        pooled, pos = _C.spatial_embed_pool_fwd(planes, effects, _w32(w_dense),
+                                                _w32(bias), rows.contiguous(), ex, ey,
                                                 entity_num)
         ctx.save_for_backward(pooled, pos, ex, ey, entity_num, *tensors)
         ctx.n_planes = n_planes
@@ -521,7 +521,7 @@ class _Conv3x3(torch.autograd.Function):
         wk = w_lp.detach().permute(0, 2, 3, 1)          # [Cout,3,3,Cin]: a view for channels_last weights
         if not wk.is_contiguous():
             wk = wk.contiguous()
-        bias = b.detach().float().contiguous() if b is not None else None
+        bias = _w32(b) if b is not None else None
         out = _C.conv3x3_fwd(x_nhwc, wk, bias, res_nhwc, _ACT[act])
         ctx.save_for_backward(x_nhwc, w_lp, out)
         ctx.act, ctx.has_res = act, res_nhwc is not None
@@ -548,11 +548,104 @@ def _conv_w(w):
 
 
 def _conv_wt(w):
-    """flipped, transposed weight [Cin,3,3,Cout] for the input gradient (one launch).  Only bf16 weights
-    reach the native conv (conv3x3_fwd rejects others), so there is no fp32 branch to keep untested."""
+    """flipped, transposed weight [Cin,3,3,Cout] for the input gradient (a derived form: rebuilt once per
+    optimizer step for parameters).  Only bf16 weights reach the native conv (conv3x3_fwd rejects others),
+    so there is no fp32 branch to keep untested."""
     if w.dtype != torch.bfloat16:
         raise TypeError(f'native conv3x3 backward needs bf16 weights, got {w.dtype}')
-    return _C.conv_wt(w.detach())
+
+    def make():
+        s0, s1, s2, s3 = w.stride()
+        return _C.conv_wt(w.detach()), [w.shape[1], 3, 3, w.shape[0], s1, -s2, -s3, s0, 2 * s2 + 2 * s3]
+    return _derived(w, 'convwt', make)
+
+
+# ---------------------------------------------------------------------------- derived weight forms
+class DerivedWeights:
+    """Layout / dtype forms of the compute weights that the kernels consume - fp32 biases and small fp32
+    weights, transposed GEMM weights for the dX products, flipped+transposed conv weights - built ONCE per
+    optimizer step instead of once per layer per step (~110 cast / transpose launches per RL step).
+
+    Owned by :class:`~applestar_amd.parallel.mixed.MasterWeights`, which tags its parameters with it
+    (``p._derived_forms``) and calls :meth:`refresh` after publishing new bf16 weights: one
+    ``multi_strided_copy`` launch per 24 forms rebuilds every form in place (the buffers keep their
+    addresses).  A form is served only while it matches the owner's weight epoch and the parameter's version
+    counter; any other write path (state-dict load, resync) calls :meth:`invalidate`, after which the next
+    use rebuilds the form per call, as the uncached path does.  Untagged tensors (casts of fp32 weights,
+    activations) are never cached."""
+
+    def __init__(self):
+        self.enabled = True
+        self.epoch = 0
+        self.forms = {}          # (id(param), key) -> [param, out, spec, epoch, version]
+
+    def lookup(self, p, key, make):
+        f = self.forms.get((id(p), key))
+        if f is not None and f[3] == self.epoch and f[4] == p._version:
+            return f[1]
+        out, spec = make()
+        if spec is None or out.data_ptr() == p.data_ptr():
+            return out
+        if f is not None and f[1].shape == out.shape and f[1].dtype == out.dtype:
+            f[1].copy_(out)      # rebuilt in the form's own buffer: its address may be baked into a HIP graph
+            out = f[1]
+        self.forms[(id(p), key)] = [p, out, spec, self.epoch, p._version]
+        return out
+
+    def invalidate(self):
+        self.epoch += 1
+
+    def refresh(self):
+        """New weights were published: rebuild every known form in place (same stream as the writer)."""
+        self.epoch += 1
+        if not (self.enabled and self.forms):
+            return
+        fs = list(self.forms.values())
+        spec = []
+        for f in fs:
+            spec += f[2]
+        ensure_loaded().multi_strided_copy([f[1] for f in fs], [f[0].detach() for f in fs], spec)
+        for f in fs:
+            f[3], f[4] = self.epoch, f[0]._version
+
+
+def _derived(p, key, make):
+    reg = getattr(p, '_derived_forms', None) if isinstance(p, torch.nn.Parameter) else None
+    if reg is None or not reg.enabled or not p.is_cuda:
+        return make()[0]
+    return reg.lookup(p, key, make)
+
+
+def _view_spec(view, src):
+    """multi_strided_copy spec of a strided view of ``src`` (<= 4 dims, element units)."""
+    if view.dim() > 4:
+        return None
+    pad = 4 - view.dim()
+    return [1] * pad + list(view.shape) + [0] * pad + list(view.stride()) + \
+        [view.storage_offset() - src.storage_offset()]
+
+
+def _w32(t):
+    """t as a contiguous fp32 tensor (a bias, a small weight); a derived form for parameters."""
+    if t.dtype == torch.float32 and t.is_contiguous():
+        return t.detach()
+    return _derived(t, 'f32', lambda: (t.detach().float().contiguous(), _view_spec(t.detach(), t)))
+
+
+def _wT(t, dtype=None):
+    """t viewed as [shape0, -1], transposed, contiguous, in ``dtype`` (default t's); a derived form for
+    parameters."""
+    dtype = dtype or t.dtype
+
+    def make():
+        v = t.detach().reshape(t.shape[0], -1).t()
+        out = v.to(dtype).contiguous() if dtype != t.dtype else v.contiguous()
+        try:
+            spec = _view_spec(t.detach().view(t.shape[0], -1).t(), t)
+        except RuntimeError:          # not viewable as 2-D: keep the per-call copy
+            spec = None
+        return out, spec
+    return _derived(t, ('T', dtype), make)
 
 
 FUSED_DRELU = os.environ.get('APPLESTAR_CONV_DRELU', '1') != '0'   # A/B switch
@@ -581,8 +674,8 @@ class _ResBlock(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2):
-        y1 = _C.conv3x3_fwd(x, _conv_w(w1), b1.detach().float().contiguous(), None, 1)
-        out = _C.conv3x3_fwd(y1, _conv_w(w2), b2.detach().float().contiguous(), x, 1)
+        y1 = _C.conv3x3_fwd(x, _conv_w(w1), _w32(b1), None, 1)
+        out = _C.conv3x3_fwd(y1, _conv_w(w2), _w32(b2), x, 1)
         ctx.save_for_backward(x, w1, w2, y1, out)
         ctx.b_dtypes = (b1.dtype, b2.dtype)
         return out
@@ -628,14 +721,14 @@ class _GatedResBlock(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, sp, w1, b1, w2, b2, *gate):
         B, H, W, C = x.shape
-        y1 = _C.conv3x3_fwd(x, _conv_w(w1), b1.detach().float().contiguous(), None, 1)
-        y = _C.conv3x3_fwd(y1, _conv_w(w2), b2.detach().float().contiguous(), None, 0)
+        y1 = _C.conv3x3_fwd(x, _conv_w(w1), _w32(b1), None, 1)
+        y = _C.conv3x3_fwd(y1, _conv_w(w2), _w32(b2), None, 0)
         h = x.view(-1, C)
         acts = [h]
         if GATE_CHAIN and C == 128:
             # the four gate layers in one launch, activation tile resident in LDS (gate_chain.hip)
             acts += _C.gate_chain(h, [gate[2 * i].detach().view(C, C) for i in range(4)],
-                                  [gate[2 * i + 1].detach().float().contiguous() for i in range(4)],
+                                  [_w32(gate[2 * i + 1]) for i in range(4)],
                                   [None] * 4, [None] * 4, 0b0111)
             h = acts[-1]
         else:
@@ -661,7 +754,7 @@ class _GatedResBlock(torch.autograd.Function):
         if GATE_CHAIN and C == 128:
             # d3, d2, d1 and the gate-path input gradient (+ the skip gradient) in one launch; the weight
             # gradients from the saved layer inputs and these
-            d3, d2, d1, dx_gate = _C.gate_chain(d, [gws[i].view(C, C).t().contiguous() for i in (3, 2, 1, 0)],
+            d3, d2, d1, dx_gate = _C.gate_chain(d, [_wT(gws[i]) for i in (3, 2, 1, 0)],
                                                 [None] * 4, [a3, a2, a1, None], [None, None, None, dx_res.view(-1, C)],
                                                 0)
             for i, di in ((3, d), (2, d3), (1, d2), (0, d1)):
@@ -898,8 +991,7 @@ class _Pointwise(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x2, w, b, relu):
-        y = _C.pointwise_conv(x2, w.detach().float().contiguous(),
-                              b.detach().float().contiguous() if b is not None else None, 1 if relu else 0)
+        y = _C.pointwise_conv(x2, _w32(w), _w32(b) if b is not None else None, 1 if relu else 0)
         ctx.save_for_backward(x2, w, y)
         ctx.relu = relu
         ctx.b_dtype = b.dtype if b is not None else None
@@ -910,7 +1002,7 @@ class _Pointwise(torch.autograd.Function):
         x2, w, y = ctx.saved_tensors
         P, cout = y.shape
         dpre = _C.act_grad_nhwc(dy.reshape(1, 1, P, cout), y.view(1, 1, P, cout), ctx.relu).view(P, cout)
-        dx = _C.pointwise_conv(dpre, w.detach().float().t().contiguous(), None, 0) if ctx.needs_input_grad[0] \
+        dx = _C.pointwise_conv(dpre, _wT(w, torch.float32), None, 0) if ctx.needs_input_grad[0] \
             else None
         has_b = ctx.b_dtype is not None
         dw, db = _C.wgrad(dpre, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
@@ -971,12 +1063,12 @@ class _Linear(torch.autograd.Function):
             if dy.shape[1] == 32 and x2.shape[1] % 16 == 0 and dy.is_contiguous():
                 # thin-K product (the heads' 256 -> 32 key projections): one MFMA per output tile, a pure
                 # store stream (gemm_k32.hip); the library took 0.19 ms per 196k-row call
-                dx = _C.mm_k32(dy, w.t().contiguous())
+                dx = _C.mm_k32(dy, _wT(w))
             elif GEMM_REFORM and dy.shape[0] * w.shape[1] >= (1 << 22):
                 # dY W as an "NT" product against a transposed weight copy (the layout of the forward):
                 # hipBLASLt's "NN" kernels ran the transformer FFN dX at 132 vs 106 us and the value fc's
                 # 390 x 12160 dX at 32 vs 19 us (tools/bench_gemm_alts.py)
-                dx = torch.nn.functional.linear(dy, w.t().contiguous())
+                dx = torch.nn.functional.linear(dy, _wT(w))
             else:
                 dx = torch.mm(dy, w)
         has_b = ctx.b_dtype is not None

@@ -11,6 +11,7 @@ fp32 end to end.  ``state_dict`` exports the fp32 master values (reference check
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List
 
 import torch
@@ -68,6 +69,14 @@ class MasterWeights:
             off += k
         self.fp32_params = [p for b in self.reducer.buckets if b.flat.dtype != torch.bfloat16 for p in b.params]
         self.opt_params = [self.master] + self.fp32_params
+        # fp32 biases / transposed GEMM weights / flipped conv weights the kernels read: rebuilt in one launch
+        # per step by after_step instead of one cast or transpose per layer (ops/native.py DerivedWeights)
+        self.derived = None
+        if dev.type == 'cuda' and os.environ.get('APPLESTAR_DERIVED_WEIGHTS', '1') != '0':   # A/B switch
+            from ..ops.native import DerivedWeights
+            self.derived = DerivedWeights()
+            for p in self.params:
+                p._derived_forms = self.derived
         # multi-rank: False = per-bucket all-reduce overlapped with backward (eager step); True = backward
         # writes the local gradient and synchronize() reduces the flat buffers (graph-captured step)
         self.defer_allreduce = False
@@ -234,6 +243,8 @@ class MasterWeights:
         """Publish the updated master weights to the bf16 compute weights."""
         with torch.no_grad():
             self.weight_flat.copy_(self.master.detach())
+            if self.derived is not None:
+                self.derived.refresh()
 
     # ---------------------------------------------------------------- state
     def _master_views(self) -> Dict[str, torch.Tensor]:
@@ -271,6 +282,8 @@ class MasterWeights:
 
     def sync_from_model(self):
         """Re-derive the masters from the current (bf16) compute weights, e.g. after an in-place reset."""
+        if self.derived is not None:
+            self.derived.invalidate()
         with torch.no_grad():
             for n, v in self._master_views().items():
                 v.copy_(dict(self.model.named_parameters())[n].data.float())

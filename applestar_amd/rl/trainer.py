@@ -94,6 +94,8 @@ class RLTrainer:
             if self.master is not None:
                 self.master.defer_allreduce = True     # the all-reduce runs between the two graphs
             self.graph = GraphedTrainStep(self._fwd_bwd, self._reduce, self._update, device=self.device)
+            if self.master is not None and self.master.derived is not None:
+                self.master.derived.enabled = False    # per-call forms inside the captured step
 
     def _graph_capable(self) -> bool:
         lc = self.cfg.learner
