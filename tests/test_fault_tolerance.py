@@ -74,8 +74,10 @@ def test_actor_survives_dead_env_worker(tmp_path, monkeypatch):
     from applestar_amd.actor.actor import Actor
     actor = Actor({'actor': {'job_type': 'eval', 'env_num': 2, 'gpu_batch_inference': True, 'episode_num': 1},
                    'env': {'game_steps_per_episode': 300, 'fake': True, 'player_ids': ['agent1', 'bot7']},
-                   'communication': {'actor_ask_for_job_interval': 120}})
+                   'communication': {'actor_ask_for_job_interval': 400}})
     t0 = time.time()
     res = actor.run()
-    assert len(res) == 1 and time.time() - t0 < 200
+    # the job deadline is >= 280 s: finishing well before it means the dead worker was not waited for (a
+    # generous bound, so that a loaded CPU running the surviving episode does not fail the test)
+    assert len(res) == 1 and time.time() - t0 < 250
     actor.close()
