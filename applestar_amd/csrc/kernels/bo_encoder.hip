@@ -52,6 +52,11 @@ __device__ __forceinline__ long ld_idx(const void* p, long i, int idt) {
   return static_cast<const long*>(p)[i];
 }
 
+// The three products below are LDS-bandwidth bound (a scalar loop reads two LDS words per FMA): each
+// thread computes a 2 x 2 (mm_nt / mm_nn) or 4 x 2 (mm_grad) register tile, so an FMA costs one word or
+// less of LDS traffic (docs/PERF_LOG.md).  L = 20 tokens splits into 10 token pairs.
+static_assert(L % 2 == 0, "token pairs");
+
 // Y[t][n] = act(sum_k A[t][k] W[n][k] + b[n]); A, Y in LDS; W [N][K] global, staged transposed in wb
 template <int K, int N, typename WT>
 __device__ __forceinline__ void mm_nt(const float* A, const void* W, const void* b, float* Y, bool relu, float* wb) {
@@ -60,12 +65,31 @@ __device__ __forceinline__ void mm_nt(const float* A, const void* W, const void*
     wb[k * (N + 1) + n] = ldw<WT>(W, i);
   }
   __syncthreads();
-  for (int o = threadIdx.x; o < L * N; o += 256) {
-    const int t = o / N, n = o - t * N;
-    float acc = ldw<WT>(b, n);
+  constexpr int NP = N / 2;
+  static_assert(N % 2 == 0, "pairs");
+  for (int o = threadIdx.x; o < (L / 2) * NP; o += 256) {
+    const int t = 2 * (o / NP), n = 2 * (o % NP);
+    const float b0 = ldw<WT>(b, n), b1 = ldw<WT>(b, n + 1);
+    float a00 = b0, a01 = b1, a10 = b0, a11 = b1;
 #pragma unroll 8
-    for (int k = 0; k < K; ++k) acc += A[t * K + k] * wb[k * (N + 1) + n];
-    Y[o] = relu ? fmaxf(acc, 0.f) : acc;
+    for (int k = 0; k < K; ++k) {
+      const float x0 = A[t * K + k], x1 = A[(t + 1) * K + k];
+      const float w0 = wb[k * (N + 1) + n], w1 = wb[k * (N + 1) + n + 1];
+      a00 += x0 * w0;
+      a01 += x0 * w1;
+      a10 += x1 * w0;
+      a11 += x1 * w1;
+    }
+    if (relu) {
+      a00 = fmaxf(a00, 0.f);
+      a01 = fmaxf(a01, 0.f);
+      a10 = fmaxf(a10, 0.f);
+      a11 = fmaxf(a11, 0.f);
+    }
+    Y[t * N + n] = a00;
+    Y[t * N + n + 1] = a01;
+    Y[(t + 1) * N + n] = a10;
+    Y[(t + 1) * N + n + 1] = a11;
   }
   __syncthreads();
 }
@@ -78,25 +102,57 @@ __device__ __forceinline__ void mm_nn(const float* dY, const void* W, float* dA,
     wb[n * (K + 1) + k] = ldw<WT>(W, i);
   }
   __syncthreads();
-  for (int o = threadIdx.x; o < L * K; o += 256) {
-    const int t = o / K, k = o - t * K;
-    float acc = 0.f;
+  constexpr int KP = K / 2;
+  static_assert(K % 2 == 0, "pairs");
+  for (int o = threadIdx.x; o < (L / 2) * KP; o += 256) {
+    const int t = 2 * (o / KP), k = 2 * (o % KP);
+    float a00 = 0.f, a01 = 0.f, a10 = 0.f, a11 = 0.f;
 #pragma unroll 8
-    for (int n = 0; n < N; ++n) acc += dY[t * N + n] * wb[n * (K + 1) + k];
-    dA[o] = acc;
+    for (int n = 0; n < N; ++n) {
+      const float y0 = dY[t * N + n], y1 = dY[(t + 1) * N + n];
+      const float w0 = wb[n * (K + 1) + k], w1 = wb[n * (K + 1) + k + 1];
+      a00 += y0 * w0;
+      a01 += y0 * w1;
+      a10 += y1 * w0;
+      a11 += y1 * w1;
+    }
+    dA[t * K + k] = a00;
+    dA[t * K + k + 1] = a01;
+    dA[(t + 1) * K + k] = a10;
+    dA[(t + 1) * K + k + 1] = a11;
   }
   __syncthreads();
 }
 
-// G[n][k] += sum_t dY[t][n] A[t][k];  gb[n] += sum_t dY[t][n]   (fp32 atomics)
+// G[n][k] += sum_t dY[t][n] A[t][k];  gb[n] += sum_t dY[t][n]   (fp32 atomics).  A thread owns rows n..n+3 of
+// columns k and k + K/2: consecutive lanes take consecutive k, so every atomic instruction covers contiguous
+// addresses (a 4 x 4 tile per lane spread each instruction over 16-B strides: the backward got slower) and the
+// dY quad is one broadcast 16-B LDS read; 3 LDS reads per 8 FMAs.
 template <int K, int N>
 __device__ __forceinline__ void mm_grad(const float* dY, const float* A, float* G, float* gb) {
-  for (int i = threadIdx.x; i < N * K; i += 256) {
-    const int n = i / K, k = i - n * K;
-    float acc = 0.f;
+  static_assert(N % 4 == 0 && K % 2 == 0, "row quads, column halves");
+  constexpr int KH = K / 2;
+  for (int o = threadIdx.x; o < (N / 4) * KH; o += 256) {
+    const int n = 4 * (o / KH), k = o % KH;
+    float acc[4][2] = {};
 #pragma unroll 4
-    for (int t = 0; t < L; ++t) acc += dY[t * N + n] * A[t * K + k];
-    atomicAdd(G + i, acc);
+    for (int t = 0; t < L; ++t) {
+      const float4 y = *reinterpret_cast<const float4*>(dY + t * N + n);
+      const float a0 = A[t * K + k], a1 = A[t * K + k + KH];
+      acc[0][0] += y.x * a0;
+      acc[0][1] += y.x * a1;
+      acc[1][0] += y.y * a0;
+      acc[1][1] += y.y * a1;
+      acc[2][0] += y.z * a0;
+      acc[2][1] += y.z * a1;
+      acc[3][0] += y.w * a0;
+      acc[3][1] += y.w * a1;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      atomicAdd(G + (n + i) * K + k, acc[i][0]);
+      atomicAdd(G + (n + i) * K + k + KH, acc[i][1]);
+    }
   }
   for (int n = threadIdx.x; n < N; n += 256) {
     float acc = 0.f;
@@ -143,7 +199,7 @@ __device__ __forceinline__ void layer_norm64_bwd(const float* X, const float* mu
   __syncthreads();
 }
 
-struct Smem {
+struct alignas(16) Smem {
   float X[L * D], U[L * D], QKV[L * QD], O[L * 16], H1[L * HID], P[NH * L * L], T[L * D], mu[L], rs[L];
   float wb[HID * (D + 1)];
 };
@@ -258,7 +314,7 @@ __global__ __launch_bounds__(256) void bo_fwd_kernel(const void* __restrict__ bo
   }
 }
 
-struct SmemB {
+struct alignas(16) SmemB {
   float dX[L * D], dT[L * D], dH[L * HID], A[L * HID], QKV[L * QD], dQKV[L * QD], P[NH * L * L], dS[NH * L * L],
       dO[L * 16];
   float wb[HID * (D + 1)];
