@@ -1359,8 +1359,13 @@ void multi_strided_copy(const std::vector<at::Tensor>& dsts, const std::vector<a
       a.stride[t][k] = sp[4 + k];
     }
     a.base[t] = sp[8];
-    a.dts[t] = static_cast<unsigned char>((s.scalar_type() == at::kFloat ? 1 : 0) | (d.scalar_type() == at::kFloat ? 2 : 0));
-    a.chunk_start[t + 1] = a.chunk_start[t] + static_cast<int>((n + as::kCopyChunk - 1) / as::kCopyChunk);
+    // a transpose of the last two dims (dst rows contiguous in the source) of a large tensor: LDS-tiled path,
+    // one 64 x 128 tile per block
+    const bool tiled = sp[0] == 1 && sp[1] == 1 && sp[6] == 1 && sp[7] > 1 && n >= (1 << 16);
+    a.dts[t] = static_cast<unsigned char>((s.scalar_type() == at::kFloat ? 1 : 0) | (d.scalar_type() == at::kFloat ? 2 : 0) |
+                                          (tiled ? 4 : 0));
+    const int64_t chunks = tiled ? ((sp[2] + 63) / 64) * ((sp[3] + 127) / 128) : (n + as::kCopyChunk - 1) / as::kCopyChunk;
+    a.chunk_start[t + 1] = a.chunk_start[t] + static_cast<int>(chunks);
     if (a.ntensors == as::kSCopyMaxT) flush();
   }
   flush();

@@ -241,7 +241,7 @@ struct StridedCopyArgs {                 // passed by value (~2.1 KB of kernel a
   int size[kSCopyMaxT][4];
   long stride[kSCopyMaxT][4];
   long base[kSCopyMaxT];
-  unsigned char dts[kSCopyMaxT];         // bit 0: src fp32, bit 1: dst fp32 (else bf16)
+  unsigned char dts[kSCopyMaxT];         // bit 0: src fp32, bit 1: dst fp32 (else bf16), bit 2: tiled transpose
 };
 void multi_strided_copy(const StridedCopyArgs& a, hipStream_t s);
 

@@ -34,6 +34,34 @@ __global__ __launch_bounds__(256) void strided_copy_kernel(const StridedCopyArgs
   const int i0 = (b - a.chunk_start[t]) * static_cast<int>(kCopyChunk);
   const int i1 = i0 + static_cast<int>(kCopyChunk) < a.n[t] ? i0 + static_cast<int>(kCopyChunk) : a.n[t];
   const bool sf = (a.dts[t] & 1) != 0, df = (a.dts[t] & 2) != 0;
+  if (a.dts[t] & 4) {
+    // transpose form (dst [R, Cc] from src element (r, c) at base + r + c * S): a 64 x 128 tile through LDS,
+    // read along r and written along c, both coalesced (the per-element path reads one row per lane)
+    __shared__ float tile[128][65];
+    const int R = a.size[t][2], Cc = a.size[t][3];
+    const long S = a.stride[t][3];
+    const int tiles_c = (Cc + 127) / 128, tb = b - a.chunk_start[t];
+    const int r0 = (tb / tiles_c) * 64, c0 = (tb % tiles_c) * 128;
+    for (int i = threadIdx.x; i < 128 * 64; i += 256) {
+      const int cc = i >> 6, rr = i & 63, r = r0 + rr, c = c0 + cc;
+      float v = 0.f;
+      if (r < R && c < Cc) {
+        const long off = a.base[t] + r + c * S;
+        v = sf ? static_cast<const float*>(a.src[t])[off] : bf2f(static_cast<const bf16_t*>(a.src[t])[off]);
+      }
+      tile[cc][rr] = v;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64 * 128; i += 256) {
+      const int rr = i >> 7, cc = i & 127, r = r0 + rr, c = c0 + cc;
+      if (r < R && c < Cc) {
+        const long o = static_cast<long>(r) * Cc + c;
+        if (df) static_cast<float*>(a.dst[t])[o] = tile[cc][rr];
+        else static_cast<bf16_t*>(a.dst[t])[o] = f2bf(tile[cc][rr]);
+      }
+    }
+    return;
+  }
   const int s1 = a.size[t][1], s2 = a.size[t][2], s3 = a.size[t][3];
   const long st0 = a.stride[t][0], st1 = a.stride[t][1], st2 = a.stride[t][2], st3 = a.stride[t][3];
   const void* src = a.src[t];

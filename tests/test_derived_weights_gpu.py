@@ -28,7 +28,10 @@ def test_multi_strided_copy_forms_match_torch():
         forms.append((w, torch.empty(w.shape[1], 3, 3, w.shape[0], dtype=torch.bfloat16, device='cuda'),
                       [w.shape[1], 3, 3, w.shape[0], s1, -s2, -s3, s0, 2 * s2 + 2 * s3],
                       w.flip(2, 3).permute(1, 2, 3, 0)))
-    for t, dt in ((lin, torch.bfloat16), (gate, torch.bfloat16), (w32, torch.bfloat16), (lin, torch.float32)):
+    big = torch.randn(250, 1003, device='cuda', generator=g).to(torch.bfloat16)      # tiled transpose path (>= 64 K)
+    big32 = torch.randn(130, 700, device='cuda', generator=g)
+    for t, dt in ((lin, torch.bfloat16), (gate, torch.bfloat16), (w32, torch.bfloat16), (lin, torch.float32),
+                  (big, torch.bfloat16), (big32, torch.bfloat16), (big32, torch.float32)):
         v = t.view(t.shape[0], -1).t()
         forms.append((t, torch.empty(v.shape, dtype=dt, device='cuda'), native._view_spec(v, t), v.to(dt)))
     forms.append((bias, torch.empty(77, dtype=torch.float32, device='cuda'), native._view_spec(bias, bias), bias.float()))
