@@ -1,0 +1,15 @@
+#!/bin/bash
+# deferred GatedResBlock weight gradients: tests, A/B/A/B, overlap around the LSTM backward
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_deferred_wgrad_gpu.py tests/test_derived_weights_gpu.py tests/test_model_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r2dk_tests.log 2>&1 || { tail -40 gpurun_out/r2dk_tests.log; exit 1; }
+tail -2 gpurun_out/r2dk_tests.log
+VAR=APPLESTAR_DEFER_WGRAD bash tools/gpu_ab3.sh || exit 1
+R=$PWD
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace -d $R/gpurun_out/r2dk_prof -o run --output-format csv -- python3 $R/bench.py --steps 3 --warmup 2 > $R/gpurun_out/r2dk_prof.log 2>&1 || exit 1
+t=$(find $R/gpurun_out/r2dk_prof -name '*kernel_trace.csv' | head -1)
+python3 $R/tools/overlap_around.py "$t" 'lnlstm_bwd_split' 8 > $R/gpurun_out/r2dk_overlap.txt
+rm -f "$t"
+cat $R/gpurun_out/r2dk_overlap.txt
