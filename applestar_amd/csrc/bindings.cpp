@@ -225,6 +225,25 @@ std::vector<at::Tensor> lnlstm_bwd(const at::Tensor& dout, const at::Tensor& dhT
   return {dgates, dhg, dc_ln, dh0, dc0};
 }
 
+// ---------------------------------------------------------------- LayerNorm affine gradients (column sums)
+// [2, C] fp32: row 0 = sum_r dy * xh, row 1 = sum_r dy (the LN weight / bias gradients) for fp32 dy, xh of equal
+// shape (rows = every leading dim); one launch (+ one column reduction past 512 rows)
+at::Tensor ln_affine_grads(const at::Tensor& dy, const at::Tensor& xh) {
+  check_cuda(dy, "dy");
+  check_cuda(xh, "xh");
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && xh.scalar_type() == at::kFloat && dy.sizes() == xh.sizes() &&
+                  dy.is_contiguous() && xh.is_contiguous() && dy.dim() >= 1, "ln_affine_grads: contiguous fp32, same shape");
+  c10::hip::HIPGuard g(dy.device().index());
+  const int64_t C = dy.size(-1), R = C ? dy.numel() / C : 0;
+  auto out = at::empty({2, C}, dy.options());
+  if (R == 0) return out.zero_();
+  const int S = as::ln_affine_slices(R);
+  at::Tensor part = S == 1 ? out : at::empty({S, 2 * C}, dy.options());
+  as::ln_affine_grads(dy.data_ptr<float>(), xh.data_ptr<float>(), part.data_ptr<float>(), R, static_cast<int>(C), stream());
+  if (S > 1) as::column_reduce(part.data_ptr<float>(), out.data_ptr<float>(), S, static_cast<int>(2 * C), stream());
+  return out;
+}
+
 // ---------------------------------------------------------------- entity embedding
 int src_dt(const at::Tensor& t) {
   switch (t.scalar_type()) {
@@ -1434,6 +1453,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pointwise_supported", [](int64_t ci, int64_t co) { return as::pointwise_supported(static_cast<int>(ci), static_cast<int>(co)); });
   m.def("lstm_split_error", &lstm_split_error);
   m.def("multi_copy", &multi_copy);
+  m.def("ln_affine_grads", &ln_affine_grads);
   m.def("multi_strided_copy", &multi_strided_copy);
   m.def("loc_in_fwd", &loc_in_fwd);
   m.def("vsp_fwd", &vsp_fwd);

@@ -199,6 +199,10 @@ void maxpool2_bwd_relu(const void* dy, const uint8_t* pos, const void* y, void* 
                        hipStream_t s);
 // out [S, C] fp32 = per-segment row sums of x [T, C] (segments cu[s]..cu[s+1]); C <= 1024, C % 4 == 0
 void segment_sum(const void* x, int dt, const int* cu, float* out, int S, int C, hipStream_t s);
+// LayerNorm affine gradients: per row slice s of ln_affine_slices(R), part[s] = [sum dy*xh (C) | sum dy (C)]
+// (fp32 [R, C] inputs); reduce the slices with column_reduce when there are several
+int ln_affine_slices(long R);
+void ln_affine_grads(const float* dy, const float* xh, float* part, long R, int C, hipStream_t s);
 // out [V, D] fp32 (zeroed) += src rows grouped by idx (V * D <= 16384)
 void table_grad(const void* src, int dt, const int64_t* idx, float* out, long U, int V, int D, hipStream_t s);
 

@@ -238,6 +238,35 @@ __global__ __launch_bounds__(256) void column_reduce_atomic_kernel(const float* 
                                                  red[3][threadIdx.x]);
 }
 
+
+// LayerNorm affine gradients over rows: part[s][c] = sum_r dy[r][c] * xh[r][c], part[s][C + c] = sum_r dy[r][c]
+// for the rows of slice s (kAffRows rows per slice); 64 columns per block, the 4 waves take every 4th row
+constexpr int kAffRows = 512;
+__global__ __launch_bounds__(256) void ln_affine_grads_kernel(const float* __restrict__ dy, const float* __restrict__ xh,
+                                                              float* __restrict__ part, long R, int C) {
+  __shared__ float sw[4][64], sb[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const long r0 = static_cast<long>(blockIdx.y) * kAffRows;
+  const long r1 = r0 + kAffRows < R ? r0 + kAffRows : R;
+  float aw = 0.f, ab = 0.f;
+  if (c < C) {
+#pragma unroll 4
+    for (long r = r0 + w; r < r1; r += 4) {
+      const float g = dy[r * C + c];
+      aw += g * xh[r * C + c];
+      ab += g;
+    }
+  }
+  sw[w][lane] = aw;
+  sb[w][lane] = ab;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    float* o = part + static_cast<long>(blockIdx.y) * 2 * C;
+    o[c] = (sw[0][lane] + sw[1][lane]) + (sw[2][lane] + sw[3][lane]);
+    o[C + c] = (sb[0][lane] + sb[1][lane]) + (sb[2][lane] + sb[3][lane]);
+  }
+}
 }  // namespace
 
 namespace {
@@ -353,6 +382,14 @@ void column_reduce(const float* part, float* out, int nrows, int cols, hipStream
 void column_reduce_bf16(const float* part, void* out, int nrows, int cols, hipStream_t s) {
   hipLaunchKernelGGL(column_reduce_kernel<bf16_t>, dim3((cols + 63) / 64), dim3(1024), 0, s, part,
                      static_cast<bf16_t*>(out), nrows, cols);
+}
+
+int ln_affine_slices(long R) { return static_cast<int>((R + kAffRows - 1) / kAffRows); }
+
+void ln_affine_grads(const float* dy, const float* xh, float* part, long R, int C, hipStream_t s) {
+  const int S = ln_affine_slices(R);
+  if (S == 0 || C == 0) return;
+  hipLaunchKernelGGL(ln_affine_grads_kernel, dim3((C + 63) / 64, S), dim3(256), 0, s, dy, xh, part, R, C);
 }
 
 }  // namespace as

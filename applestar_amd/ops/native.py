@@ -143,10 +143,10 @@ class _LNLSTMRecurrence(torch.autograd.Function):
                                                      rstd_h, wq, lnh_w.detach(), lnc_w.detach())
         h_prev = torch.cat([h0.float().unsqueeze(0), out[:-1]], 0).view(T * B, H)
         dw = _mm_tn(dhg.view(T * B, 4 * H), h_prev)
-        dlnh_w = (dgates * xhat_h).sum((0, 1))
-        dlnh_b = dgates.sum((0, 1))
-        dlnc_w = (dc_ln * xhat_c).sum((0, 1))
-        dlnc_b = dc_ln.sum((0, 1))
+        # LN_h / LN_c affine gradients: one column-sum launch each (four products + reductions as torch ops
+        # were ~17 launches at ~19 us per LSTM backward, r2dl)
+        dlnh_w, dlnh_b = _C.ln_affine_grads(dgates.contiguous(), xhat_h.contiguous()).unbind(0)
+        dlnc_w, dlnc_b = _C.ln_affine_grads(dc_ln.contiguous(), xhat_c.contiguous()).unbind(0)
         return dgates, dh0, dc0, dw, dlnh_w, dlnh_b, dlnc_w, dlnc_b, None
 
 
@@ -1120,6 +1120,49 @@ class _LinearSplitK(torch.autograd.Function):
         return dx, dw.to(w.dtype), (db.to(w.dtype) if db is not None else None), None
 
 
+_SMALL_LINEAR_ROWS = 4096
+_ONES = {}
+
+
+def _ones_row(R, dtype, device):
+    """A cached [1, R] ones row (bias gradients as a GEMV)."""
+    key = (R, dtype, device)
+    t = _ONES.get(key)
+    if t is None:
+        t = _ONES[key] = torch.ones(1, R, dtype=dtype, device=device)
+    return t
+
+
+class _SmallLinear(torch.autograd.Function):
+    """act(x W^T + b) over a few rows, or with K / N not a multiple of 8 (the scalar encoders' one-hot inputs,
+    the 2- and 1-wide head / value outputs): library GEMMs both ways, the bias gradient as a ones-row GEMV
+    (torch's column reduction over a few hundred rows took ~15 us per layer, r2dl) and the ReLU mask as one
+    threshold_backward."""
+
+    @staticmethod
+    def forward(ctx, x2, w, b, relu):
+        if relu and b is not None:
+            y = torch._addmm_activation(b, x2, w.t(), use_gelu=False)
+        else:
+            y = torch.nn.functional.linear(x2, w, b)
+            if relu:
+                y = torch.relu(y)
+        ctx.save_for_backward(x2, w, y if relu else None)
+        ctx.relu, ctx.has_b = relu, b is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, y = ctx.saved_tensors
+        dy = dy.to(x2.dtype)
+        if ctx.relu:
+            dy = torch.ops.aten.threshold_backward(dy, y, 0.0)
+        dx = dy @ w if ctx.needs_input_grad[0] else None
+        dw = dy.t() @ x2
+        db = (_ones_row(dy.shape[0], dy.dtype, dy.device) @ dy).view(-1) if ctx.has_b else None
+        return dx, dw, db, None
+
+
 def linear(x, w, b=None, act=None):
     """bf16 act(x W^T + b) over the last dim of x with the native weight gradient when the row count is
     large; other shapes take F.linear (+ the activation)."""
@@ -1136,6 +1179,14 @@ def linear(x, w, b=None, act=None):
             wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
             bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
             y = _LinearSplitK.apply(xb, wb, bb, act == 'relu')
+        return y.view(*x.shape[:-1], N)
+    if lowp and x.is_cuda and act in (None, 'relu') and R < _SMALL_LINEAR_ROWS and \
+            (R < _WGRAD_MIN_ROWS or N % 8 or K % 8):
+        with torch.autocast('cuda', enabled=False):
+            xb = x.reshape(R, K).to(torch.bfloat16)
+            wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
+            bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
+            y = _SmallLinear.apply(xb, wb, bb, act == 'relu')
         return y.view(*x.shape[:-1], N)
     if not lowp or R < _WGRAD_MIN_ROWS or N % 8 or K % 8 or R * max(N, K) * 2 >= 0x7ffffff0 or \
             act not in (None, 'relu'):
