@@ -237,9 +237,9 @@ class EntityEncoder(nn.Module):
         lens = entity_num.clamp(max=N).to(torch.int32)
         cu = F.pad(torch.cumsum(lens, 0, dtype=torch.int32), (1, 0))
         x = self.embed(entity_info, flat_index)                      # [T,256]
-        x = self.transformer.forward_packed_embedded(x, cu, N)       # [T,256]
-        # the reference's inplace ReLU (entity_encoder.py:84) also rectifies x used by the mean below
-        x = F.relu(x)
+        # the reference's inplace ReLU (entity_encoder.py:84), which also rectifies x used by the mean below,
+        # applied by the transformer's closing LayerNorm kernel (no separate pass / mask pass over [T,256])
+        x = self.transformer.forward_packed_embedded(x, cu, N, final_act='relu')      # [T,256]
         ee = self.entity_fc(x)
         entity_embeddings = ee.new_zeros(B * N, ee.shape[-1])
         entity_embeddings = entity_embeddings.index_copy(0, flat_index, ee).view(B, N, -1)
@@ -277,8 +277,7 @@ class EntityEncoder(nn.Module):
         rows = torch.arange(T_pad, device=dev)
         sidx = torch.where(rows < total, gidx, torch.full_like(gidx, B * N))
         x = self.embed(entity_info, gidx)                            # [T_pad,256]
-        x = self.transformer.forward_packed_embedded(x, cu, N)
-        x = F.relu(x)
+        x = self.transformer.forward_packed_embedded(x, cu, N, final_act='relu')
         ee = self.entity_fc(x)
         entity_embeddings = ee.new_zeros(B * N + 1, ee.shape[-1]).index_copy(0, sidx, ee)[:B * N].view(B, N, -1)
         seg = torch.repeat_interleave(torch.arange(B + P, device=dev), all_lens.long(), output_size=T_pad)

@@ -50,12 +50,13 @@ class TransformerLayer(nn.Module):
     def _ln(self, ln, x, residual=None):
         return ops.layer_norm(x, ln.weight, ln.bias, residual=residual)
 
-    def forward_packed(self, x, cu_seqlens, max_len: int):
+    def forward_packed(self, x, cu_seqlens, max_len: int, act=None):
+        """``act``: an activation applied to the layer output inside the closing LayerNorm kernel."""
         assert self.ln_type == 'post'
         a = self.attention.forward_packed(x, cu_seqlens, max_len)
         x = self._ln(self.layernorm1, a, residual=x)
         m = self.mlp(x)
-        return self._ln(self.layernorm2, m, residual=x)
+        return ops.layer_norm(m, self.layernorm2.weight, self.layernorm2.bias, residual=x, act=act)
 
     def forward_dense(self, x, key_mask=None):
         if self.ln_type == 'post':
@@ -79,8 +80,9 @@ class Transformer(nn.Module):
             x = layer.forward_dense(x, key_mask)
         return x
 
-    def forward_packed_embedded(self, x, cu_seqlens, max_len: int):
-        """``x`` is the already-embedded packed token matrix [T, output_dim]."""
-        for layer in self.layers:
-            x = layer.forward_packed(x, cu_seqlens, max_len)
+    def forward_packed_embedded(self, x, cu_seqlens, max_len: int, final_act=None):
+        """``x`` is the already-embedded packed token matrix [T, output_dim]; ``final_act`` (e.g. the entity
+        encoder's ReLU after the transformer) runs inside the last LayerNorm kernel, forward and backward."""
+        for i, layer in enumerate(self.layers):
+            x = layer.forward_packed(x, cu_seqlens, max_len, act=final_act if i == len(self.layers) - 1 else None)
         return x
