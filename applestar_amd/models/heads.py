@@ -189,16 +189,18 @@ class SelectedUnitsHead(nn.Module):
         state = self.lstm.zero_state(B, q_in.device, torch.float32)
         q, _ = self.lstm(q_in.transpose(0, 1), state)                    # [S,B,32]
         logits = torch.bmm(q.transpose(0, 1).float(), key.float().transpose(1, 2))  # [B,S,N+1]
-        # mask: base, end disabled at step 0, labels[:i] masked at step i
-        prev = F.one_hot(labels.clamp(max=N1 - 1), N1).bool()            # [B,S,N+1]
-        prev_cum = torch.cumsum(prev.int(), 1) > 0
-        prev_excl = torch.cat([torch.zeros_like(prev_cum[:, :1]), prev_cum[:, :-1]], 1)
-        mask = base_mask[:, None, :] & ~prev_excl
+        # mask: base, end disabled at step 0, labels[:i] masked at step i.  Unit n is masked at step i iff its
+        # first label step is < i: one [B, N+1] scatter-min of the label steps and one broadcast compare (a
+        # [B,S,N+1] int64 one-hot + cumsum + shifted cat was ~0.2 GB of traffic per step, r2dn)
+        steps = torch.arange(S, device=labels.device)
+        first = torch.full((B, N1), S, dtype=torch.long, device=labels.device)
+        first.scatter_reduce_(1, labels.clamp(max=N1 - 1), steps.expand(B, S), reduce='amin')
+        mask = base_mask[:, None, :] & (first[:, None, :] >= steps[None, :, None])
         end_pos = F.one_hot(en.clamp(max=N1 - 1), N1).bool()
         mask[:, 0] &= ~end_pos
         if step_ok is not None:
             mask = mask & step_ok[None, :, None]
-        logits = logits.masked_fill(~mask, NEG)
+        logits = torch.where(mask, logits, NEG)
         # the reference returns no sampled units in teacher-forced mode (test_iou off): None
         return logits, None, ae_after[:, -1], selected_units_num
 
