@@ -133,10 +133,12 @@ class SelectedUnitsHead(nn.Module):
             self.attention_pool = AttentionPool(key_dim, 2, input_dim, max_num=MAX_SELECTED_UNITS_NUM + 1
                                                 if reduce_type == 'attention_pool_add_num' else None)
 
-    def keys(self, entity_embedding, entity_num):
-        """key [B,N+1,32] with the learned end embedding at position entity_num; logits mask."""
-        B, N, _ = entity_embedding.shape
-        key = self.key_fc(entity_embedding)
+    def keys(self, entity_embedding, entity_num, key=None):
+        """key [B,N+1,32] with the learned end embedding at position entity_num; logits mask.  ``key``: the
+        key_fc output when the caller already projected the entities (Policy.train_forward)."""
+        if key is None:
+            key = self.key_fc(entity_embedding)
+        B, N, _ = key.shape
         key = F.pad(key, (0, 0, 0, 1))
         ar = torch.arange(N + 1, device=key.device)
         is_end = (ar[None, :] == entity_num[:, None]).unsqueeze(2)
@@ -148,8 +150,8 @@ class SelectedUnitsHead(nn.Module):
         return ae0 + self.embed_fc2(self.embed_fc1(emb))
 
     # ------------------------------------------------------------------ teacher forced (parallel)
-    def forward_teacher(self, ae0, entity_embedding, entity_num, selected_units_num, selected_units):
-        key, base_mask = self.keys(entity_embedding, entity_num)          # [B,N+1,32], [B,N+1]
+    def forward_teacher(self, ae0, entity_embedding, entity_num, selected_units_num, selected_units, key=None):
+        key, base_mask = self.keys(entity_embedding, entity_num, key)     # [B,N+1,32], [B,N+1]
         B, N1, C = key.shape
         step_ok = None
         if key.is_cuda:
@@ -297,8 +299,10 @@ class TargetUnitHead(nn.Module):
         self.query_fc1 = FCBlock(input_dim, key_dim, act=True)
         self.query_fc2 = FCBlock(key_dim, key_dim)
 
-    def forward(self, embedding, entity_embedding, entity_num, temperature: float = 1.0, target_unit=None, u=None):
-        key = self.key_fc(entity_embedding)
+    def forward(self, embedding, entity_embedding, entity_num, temperature: float = 1.0, target_unit=None, u=None,
+                key=None):
+        if key is None:
+            key = self.key_fc(entity_embedding)
         q = self.query_fc2(self.query_fc1(embedding))
         logits = torch.einsum('bc,bnc->bn', q.float(), key.float())
         mask = ops.sequence_mask(entity_num, key.shape[1])

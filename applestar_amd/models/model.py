@@ -10,6 +10,8 @@ released ``rl_model.pth`` / ``sl_model.pth`` state dicts load unchanged.  Public
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -46,6 +48,8 @@ DEFAULT_MODEL_CONFIG = AttrDict({
 _SIDE_STREAMS: Dict[tuple, 'torch.cuda.Stream'] = {}
 SIDE_STREAMS_ENABLED = True
 CRITIC_SIDE_STREAM = False   # tools/ab_bench.py --variant critic_side: no gain (+1.9 ms, noisy)
+# selected-units + target-unit key projections as one product before the row slice (APPLESTAR_JOINT_KEYS=0: per head)
+JOINT_KEYS = os.environ.get('APPLESTAR_JOINT_KEYS', '1') != '0'
 # value baselines' ResFCBlock2 stack as the fused resmlp kernels on the GPU (APPLESTAR_FUSED_RESMLP=0: op by op)
 FUSED_RESMLP = __import__('os').environ.get('APPLESTAR_FUSED_RESMLP', '1') == '1'
 
@@ -187,18 +191,30 @@ class Policy(nn.Module):
             emb, map_skip, temperature, u=noise.get('target_location'))
         return action, su_num, logit, extra
 
+    def joint_keys(self, entity_embeddings, rows: Optional[int] = None):
+        """The selected-units and target-unit key projections (both 256 -> 32 over every entity) as ONE
+        256 -> 64 product over the full padded batch, sliced to ``rows`` afterwards: the backward is one input
+        gradient of the entity embeddings (no sum of two, no full-size zero-padded slice gradient)."""
+        su, tu = self.selected_units_head.key_fc[0], self.target_unit_head.key_fc[0]
+        k = ops.linear(entity_embeddings, torch.cat([su.weight, tu.weight], 0), torch.cat([su.bias, tu.bias], 0))
+        if rows is not None:
+            k = k[:rows]
+        return k.split(su.weight.shape[0], dim=-1)
+
     def train_forward(self, lstm_output, entity_embeddings, map_skip, scalar_context, entity_num, action_info,
-                      selected_units_num, temperature=1.0):
+                      selected_units_num, temperature=1.0, keys=None):
+        """``keys``: (selected-units, target-unit) key projections from :meth:`joint_keys` (else per head)."""
         logit, action = {}, {}
+        su_key, tu_key = keys if keys is not None else (None, None)
         logit['action_type'], action['action_type'], emb = self.action_type_head(
             lstm_output, scalar_context, temperature, action_type=action_info['action_type'])
         logit['delay'], action['delay'], emb = self.delay_head(emb, temperature, action=action_info['delay'])
         logit['queued'], action['queued'], emb = self.queued_head(emb, temperature, action=action_info['queued'])
         logit['selected_units'], action['selected_units'], emb, su_num = \
             self.selected_units_head.forward_teacher(emb, entity_embeddings, entity_num, selected_units_num,
-                                                     action_info['selected_units'])
+                                                     action_info['selected_units'], key=su_key)
         logit['target_unit'], action['target_unit'] = self.target_unit_head(
-            emb, entity_embeddings, entity_num, temperature, target_unit=action_info['target_unit'])
+            emb, entity_embeddings, entity_num, temperature, target_unit=action_info['target_unit'], key=tu_key)
         logit['target_location'], action['target_location'] = self.location_head(
             emb, map_skip, temperature, location=action_info['target_location'])
         return action, su_num, logit
@@ -315,9 +331,10 @@ class Model(nn.Module):
         vf_out = _side_stream_join(vf) if isinstance(vf, tuple) else vf
         critic_in = {'lstm': critic_input, 'vf': vf_out, 'bf': baseline_feature}
         values_h = _side_stream_call(critic, critic_in) if CRITIC_SIDE_STREAM else (critic(critic_in), None)
+        keys = self.policy.joint_keys(entity_embeddings, n) if JOINT_KEYS else None
         _, _, logits = self.policy.train_forward(
             lstm_output[:n], entity_embeddings[:n], [_take_rows(m, n) for m in map_skip], scalar_context[:n],
-            entity_num[:n], flat_action, flat_su_num, self.temperature)
+            entity_num[:n], flat_action, flat_su_num, self.temperature, keys=keys)
         values = dict(zip(self.value_networks.keys(), _side_stream_join(values_h)))
         for k in list(logits):
             logits[k] = logits[k].view(T, B, *logits[k].shape[1:])
