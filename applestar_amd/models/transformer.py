@@ -51,12 +51,21 @@ class TransformerLayer(nn.Module):
         return ops.layer_norm(x, ln.weight, ln.bias, residual=residual)
 
     def forward_packed(self, x, cu_seqlens, max_len: int, act=None):
-        """``act``: an activation applied to the layer output inside the closing LayerNorm kernel."""
+        """``act``: an activation applied to the layer output inside the closing LayerNorm kernel.  On the GPU
+        each residual gradient is added inside the dX GEMM of its branch's first linear (``ops.grad_link``)
+        instead of a separate [T, 256] autograd add."""
         assert self.ln_type == 'post'
-        a = self.attention.forward_packed(x, cu_seqlens, max_len)
-        x = self._ln(self.layernorm1, a, residual=x)
-        m = self.mlp(x)
-        return ops.layer_norm(m, self.layernorm2.weight, self.layernorm2.bias, residual=x, act=act)
+        link1, link2 = ops.grad_link(x), ops.grad_link(x)
+        pre = self.attention.attention_pre[0]
+        qkv = ops.linear(x, pre.weight, pre.bias, grad_link=link1)
+        a = self.attention.project(ops.varlen_attention(qkv, cu_seqlens, max_len, self.attention.head_num,
+                                                        self.attention.head_dim))
+        x = ops.layer_norm(a, self.layernorm1.weight, self.layernorm1.bias, residual=x, grad_link=link1)
+        fc0 = self.mlp[0]
+        m = ops.linear(x, fc0[0].weight, fc0[0].bias, act='relu' if fc0.act else None, grad_link=link2)
+        for blk in self.mlp[1:]:
+            m = blk(m)
+        return ops.layer_norm(m, self.layernorm2.weight, self.layernorm2.bias, residual=x, act=act, grad_link=link2)
 
     def forward_dense(self, x, key_mask=None):
         if self.ln_type == 'post':

@@ -46,25 +46,26 @@ sequence_mask = ref.sequence_mask
 masked_attention = ref.masked_attention
 
 
-def linear(x, w, b=None, act=None):
-    """act(x W^T + b).  GPU: hipBLASLt forward / dX, MFMA split-R kernel for dW / db of tall inputs."""
+def linear(x, w, b=None, act=None, grad_link=None):
+    """act(x W^T + b).  GPU: hipBLASLt forward / dX, MFMA split-R kernel for dW / db of tall inputs.
+    ``grad_link``: native GradLink (residual gradient added in the dX GEMM), ignored elsewhere."""
     n = _native(x)
     if n is not None:
-        return n.linear(x, w, b, act)
+        return n.linear(x, w, b, act, grad_link=grad_link)
     y = F.linear(x, w, b)
     if act is None:
         return y
     return ref.act_fn(y, act)
 
 
-def layer_norm(x, w, b, residual=None, act=None, eps: float = 1e-5):
+def layer_norm(x, w, b, residual=None, act=None, eps: float = 1e-5, grad_link=None):
     n = _native(x)
     if n is not None and n.has('layer_norm'):
         # under autocast the normalised activations are stored in bf16 (statistics and affine in fp32):
         # every consumer is a bf16 GEMM, so an fp32 output only bought a cast in forward and an fp32
         # gradient cast + fp32 residual-gradient adds in backward (~0.5 GB per step in the entity encoder)
         out_dtype = torch.bfloat16 if torch.is_autocast_enabled() else None
-        return n.layer_norm(x, w, b, residual, act, eps, out_dtype=out_dtype)
+        return n.layer_norm(x, w, b, residual, act, eps, out_dtype=out_dtype, grad_link=grad_link)
     return ref.layer_norm(x, w, b, residual, act, eps)
 
 
@@ -182,3 +183,9 @@ def upsample_conv_out(x, w, b):
         return n.upsample_conv_out(x, w, b)
     y = ref.conv2d(upsample2x(x), w, b, 1, 1)
     return y.reshape(x.shape[0], -1).float()
+
+
+def grad_link(x):
+    """A native residual-gradient link for a block ``LN(f(x) + x)`` on the GPU path, else None."""
+    n = _native(x)
+    return n.GradLink() if n is not None and hasattr(n, 'GradLink') else None

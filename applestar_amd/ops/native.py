@@ -49,9 +49,27 @@ def _dt_code(dtype) -> int:
 
 
 # ---------------------------------------------------------------------------- layer norm
+RESID_LINK = os.environ.get('APPLESTAR_RESID_LINK', '1') == '1'   # A/B switch
+
+
+class GradLink:
+    """Hands the residual gradient of ``LN(f(x) + x)`` from the LayerNorm backward to the backward of the
+    branch's first linear (``f = ... o linear(x)``), which adds it in the dX GEMM epilogue
+    (``addmm(g, dY, W)``): x then receives one gradient instead of two that the autograd engine sums with a
+    separate [T, C] add (two per entity-transformer layer).  Autograd runs the LayerNorm backward before the
+    linear's (the linear feeds the LayerNorm), so the hand-off is ordered.  The LayerNorm only hands off
+    when the linear armed the link in forward on the native path with the residual itself as its input
+    (``armed`` is that tensor), so an unarmed link leaves the plain two-gradient path in place."""
+    __slots__ = ('armed', 'g')
+
+    def __init__(self):
+        self.armed = None
+        self.g = None
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, res, w, b, act, eps, out_dtype):
+    def forward(ctx, x, res, w, b, act, eps, out_dtype, link=None):
         x_c = x.contiguous()
         res_c = res.contiguous() if res is not None else None
         y, mean, rstd, xsum = _C.layer_norm_fwd(x_c, res_c, w, b, _dt_code(out_dtype), eps, _ACT[act], True)
@@ -61,6 +79,7 @@ class _LayerNorm(torch.autograd.Function):
         ctx.has_res = res is not None
         ctx.x_dtype = x.dtype
         ctx.res_dtype = res.dtype if res is not None else None
+        ctx.link = link if (link is not None and res is not None and link.armed is res) else None
         return y
 
     @staticmethod
@@ -71,10 +90,12 @@ class _LayerNorm(torch.autograd.Function):
         dres = None
         if ctx.has_res:
             dres = dx if ctx.res_dtype == ctx.x_dtype else dx.to(ctx.res_dtype)
-        return dx, dres, dw, db, None, None, None
+            if ctx.link is not None and ctx.needs_input_grad[1]:
+                ctx.link.g, dres = dres, None      # added by the branch linear's dX GEMM (GradLink)
+        return dx, dres, dw, db, None, None, None, None
 
 
-def layer_norm(x, w, b, residual=None, act=None, eps=1e-5, out_dtype=None):
+def layer_norm(x, w, b, residual=None, act=None, eps=1e-5, out_dtype=None, grad_link=None):
     C = x.shape[-1]
     if C % 64 != 0 or C > 1536 or w.dtype != torch.float32:
         from . import reference
@@ -84,7 +105,7 @@ def layer_norm(x, w, b, residual=None, act=None, eps=1e-5, out_dtype=None):
     if residual is not None and residual.dtype not in (torch.float32, torch.bfloat16):
         residual = residual.float()
     out_dtype = out_dtype or torch.float32
-    return _LayerNorm.apply(x, residual, w, b, act, float(eps), out_dtype)
+    return _LayerNorm.apply(x, residual, w, b, act, float(eps), out_dtype, grad_link if RESID_LINK else None)
 
 
 # ---------------------------------------------------------------------------- gated residual
@@ -1006,7 +1027,7 @@ class _Pointwise(torch.autograd.Function):
             else None
         has_b = ctx.b_dtype is not None
         dw, db = _C.wgrad(dpre, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
-        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None), None
+        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None), None, None
 
 
 WGRAD_BF16_OUT = True    # tools/ab_bench.py --variant wgrad_bf16
@@ -1026,7 +1047,8 @@ class _Linear(torch.autograd.Function):
     R ~ 10^5..10^7 rows.  The ReLU mask is applied to dY by the one-pass ``act_grad`` kernel."""
 
     @staticmethod
-    def forward(ctx, x2, w, b, relu):
+    def forward(ctx, x2, w, b, relu, link=None):
+        ctx.link = link
         R, K = x2.shape
         if GEMM_REFORM and R <= 2048 and K >= 16384 and K % (32 * 8) == 0:
             # few rows, huge reduction (the spatial encoder's 48640 -> 256 fc): the library ran a 256x16 tile
@@ -1059,7 +1081,14 @@ class _Linear(torch.autograd.Function):
         else:
             dy = dy.to(torch.bfloat16).contiguous()
         dx = None
-        if ctx.needs_input_grad[0]:
+        g = None
+        if ctx.link is not None:
+            g, ctx.link.g = ctx.link.g, None
+        if g is not None:
+            # + the residual gradient the closing LayerNorm handed over (GradLink), in the GEMM epilogue
+            wt = _wT(w).t() if GEMM_REFORM and dy.shape[0] * w.shape[1] >= (1 << 22) else w
+            dx = torch.addmm(g.view(dy.shape[0], w.shape[1]), dy, wt)
+        elif ctx.needs_input_grad[0]:
             if dy.shape[1] == 32 and x2.shape[1] % 16 == 0 and dy.is_contiguous():
                 # thin-K product (the heads' 256 -> 32 key projections): one MFMA per output tile, a pure
                 # store stream (gemm_k32.hip); the library took 0.19 ms per 196k-row call
@@ -1073,7 +1102,7 @@ class _Linear(torch.autograd.Function):
                 dx = torch.mm(dy, w)
         has_b = ctx.b_dtype is not None
         dw, db = _C.wgrad(dy, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
-        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None), None
+        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None), None, None
 
 
 _WGRAD_MIN_ROWS = 256     # tools/ab_bench.py --variant wgrad_small: -0.7 ms/step vs 4096
@@ -1163,9 +1192,10 @@ class _SmallLinear(torch.autograd.Function):
         return dx, dw, db, None
 
 
-def linear(x, w, b=None, act=None):
+def linear(x, w, b=None, act=None, grad_link=None):
     """bf16 act(x W^T + b) over the last dim of x with the native weight gradient when the row count is
-    large; other shapes take F.linear (+ the activation)."""
+    large; other shapes take F.linear (+ the activation).  ``grad_link``: a :class:`GradLink` the residual
+    LayerNorm downstream hands x's residual gradient over (armed only on the native path below)."""
     N, K = w.shape
     R = x.numel() // K if K else 0
     lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
@@ -1196,11 +1226,16 @@ def linear(x, w, b=None, act=None):
         from . import reference
         return reference.act_fn(y, act)
     ensure_loaded()
-    xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
+    link = None
+    if grad_link is not None and RESID_LINK and x.dim() == 2 and x.dtype == torch.bfloat16 and \
+            x.is_contiguous() and x.requires_grad:
+        grad_link.armed, link, xb = x, grad_link, x
+    else:
+        xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
     wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
     bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
     with torch.autocast('cuda', enabled=False):
-        y = _Linear.apply(xb, wb, bb, act == 'relu')
+        y = _Linear.apply(xb, wb, bb, act == 'relu', link)
     return y.view(*x.shape[:-1], N)
 
 
