@@ -1086,8 +1086,10 @@ class _Linear(torch.autograd.Function):
             g, ctx.link.g = ctx.link.g, None
         if g is not None:
             # + the residual gradient the closing LayerNorm handed over (GradLink), in the GEMM epilogue
+            # in place: g is the LayerNorm's input gradient, which the branch's later layers (backward
+            # runs earlier, same stream) have already consumed; out-of-place addmm copied g first
             wt = _wT(w).t() if GEMM_REFORM and dy.shape[0] * w.shape[1] >= (1 << 22) else w
-            dx = torch.addmm(g.view(dy.shape[0], w.shape[1]), dy, wt)
+            dx = g.view(dy.shape[0], w.shape[1]).addmm_(dy, wt)
         elif ctx.needs_input_grad[0]:
             if dy.shape[1] == 32 and x2.shape[1] % 16 == 0 and dy.is_contiguous():
                 # thin-K product (the heads' 256 -> 32 key projections): one MFMA per output tile, a pure
