@@ -147,6 +147,12 @@ at::Tensor lstm_split_error(int64_t device) {
   return lstm_split_err(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device))).clone();
 }
 
+// the flag itself (not a copy): the trainers gate the optimizer update on it and log it with the step's
+// other scalars, so a timed-out exchange never reaches the weights unnoticed
+at::Tensor lstm_split_flag(int64_t device) {
+  return lstm_split_err(at::Device(at::kCUDA, static_cast<c10::DeviceIndex>(device)));
+}
+
 struct SplitBufs {
   at::Tensor slab;
   as::LstmSplit s;
@@ -517,6 +523,39 @@ at::Tensor varlen_attn_bwd(const at::Tensor& qkv, const at::Tensor& out, const a
   if (T > 0 && S > 0)
     as::varlen_attn_bwd(qkv.data_ptr(), out.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(), cu.data_ptr<int>(),
                         dqkv.data_ptr(), delta.data_ptr<float>(), S, max_len, H, T, 1.0f / std::sqrt(128.0f), stream());
+  return dqkv;
+}
+
+
+std::vector<at::Tensor> varlen_attn_fwd_f32(const at::Tensor& qkv, const at::Tensor& cu, int64_t max_len, int64_t H) {
+  check_cuda(qkv, "qkv");
+  check_cuda(cu, "cu_seqlens");
+  TORCH_CHECK(qkv.scalar_type() == at::kFloat && qkv.dim() == 2 && qkv.size(1) == 3 * H * 128 && qkv.is_contiguous(),
+              "varlen_attn_f32: qkv fp32 contiguous [T, 3*H*128]");
+  TORCH_CHECK(cu.scalar_type() == at::kInt && cu.is_contiguous(), "cu_seqlens int32");
+  const int64_t T = qkv.size(0), S = cu.numel() - 1;
+  c10::hip::HIPGuard g(qkv.device().index());
+  auto out = at::empty({T, H * 128}, qkv.options());
+  auto lse = at::empty({H, T}, qkv.options());
+  if (T > 0 && S > 0)
+    as::varlen_attn_fwd_f32(qkv.data_ptr<float>(), cu.data_ptr<int>(), out.data_ptr<float>(), lse.data_ptr<float>(), S,
+                            max_len, H, T, 1.0f / std::sqrt(128.0f), stream());
+  return {out, lse};
+}
+
+at::Tensor varlen_attn_bwd_f32(const at::Tensor& qkv, const at::Tensor& out, const at::Tensor& dout,
+                               const at::Tensor& lse, const at::Tensor& cu, int64_t max_len, int64_t H) {
+  check_cuda(dout, "dout");
+  TORCH_CHECK(qkv.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat && dout.scalar_type() == at::kFloat &&
+              dout.sizes() == out.sizes() && dout.is_contiguous() && out.is_contiguous(), "varlen_attn_bwd_f32: fp32");
+  const int64_t T = qkv.size(0), S = cu.numel() - 1;
+  c10::hip::HIPGuard g(qkv.device().index());
+  auto dqkv = at::empty_like(qkv);
+  auto delta = at::empty({H, T}, qkv.options());
+  if (T > 0 && S > 0)
+    as::varlen_attn_bwd_f32(qkv.data_ptr<float>(), out.data_ptr<float>(), dout.data_ptr<float>(), lse.data_ptr<float>(),
+                            cu.data_ptr<int>(), dqkv.data_ptr<float>(), delta.data_ptr<float>(), S, max_len, H, T,
+                            1.0f / std::sqrt(128.0f), stream());
   return dqkv;
 }
 
@@ -1434,6 +1473,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gate") = py::none());
   m.def("varlen_attn_fwd", &varlen_attn_fwd);
   m.def("varlen_attn_bwd", &varlen_attn_bwd);
+  m.def("varlen_attn_fwd_f32", &varlen_attn_fwd_f32);
+  m.def("varlen_attn_bwd_f32", &varlen_attn_bwd_f32);
   m.def("su_sample", &su_sample);
   m.def("segment_copy", &segment_copy);
   m.def("conv_wt", &conv_wt);
@@ -1452,6 +1493,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pointwise_conv", &pointwise_conv);
   m.def("pointwise_supported", [](int64_t ci, int64_t co) { return as::pointwise_supported(static_cast<int>(ci), static_cast<int>(co)); });
   m.def("lstm_split_error", &lstm_split_error);
+  m.def("lstm_split_flag", &lstm_split_flag);
   m.def("multi_copy", &multi_copy);
   m.def("ln_affine_grads", &ln_affine_grads);
   m.def("multi_strided_copy", &multi_strided_copy);

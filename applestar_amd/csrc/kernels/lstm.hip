@@ -464,6 +464,13 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
 // The poll is bounded: after 2^16 passes (tens of ms) it sets *err and continues (garbage, but the grid drains).
 constexpr int kSplitKS = 8;
 
+// poll budget of the cross-workgroup exchange (each pass sleeps ~64 clocks plus one L2 round trip: ~2^20
+// passes is ~1 s).  Running out sets the sticky device flag (bindings: lstm_split_flag), which the trainers
+// read with the step's logged scalars: the optimizer update of that step is gated to zero and the learner
+// raises.  The budget is generous on purpose: side-stream kernels can delay the residency of a row's 8
+// workgroups for milliseconds, and a false timeout costs a whole run.
+constexpr unsigned kSplitPollLimit = 1u << 20;
+
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
@@ -475,7 +482,7 @@ __device__ __forceinline__ void wait_flags(unsigned* flags, unsigned epoch, int*
     const unsigned f = l < N ? __hip_atomic_load((gu32*)(flags + l), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                              : epoch;
     if (__all(f >= epoch)) return;
-    if (spins > (1u << 16)) {
+    if (spins > kSplitPollLimit) {
       if (l == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
@@ -505,7 +512,7 @@ __device__ __forceinline__ void get_granules(const unsigned long long* base, lon
         ok &= static_cast<unsigned>(x >> 32) == epoch;
       }
     if (__all(ok)) return;
-    if (spins > (1u << 16)) {
+    if (spins > kSplitPollLimit) {
       if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }

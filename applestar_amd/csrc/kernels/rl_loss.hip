@@ -102,8 +102,9 @@ __global__ __launch_bounds__(kLossT) void rl_loss_kernel(const float* __restrict
       float up = 0.f;
       for (int t = 0; t < T; ++t) dalp[hb + t * B + b] = 0.f;
       for (int f = 0; f < F; ++f) {
+        // every field's V-trace sum is logged (pg/<field>), also at pg weight 0 (the reference config trains
+        // the policy on winloss only); the weight gates the gradient alone
         const float wpg = fsc[4 * f];
-        if (wpg == 0.f) continue;
         const float gp = fsc[4 * f + 2];
         const float* vf = v + static_cast<long>(f) * (T + 1) * B;
         const float* rf = r + static_cast<long>(f) * TB;

@@ -147,6 +147,11 @@ class BaseLearner:
         if keys:
             vals = torch.stack([info[k].detach().float().reshape(()) for k in keys]).cpu().tolist()
             self.log_buffer.update(dict(zip(keys, vals)))
+            if self.log_buffer.get('lstm_exchange_ok', 1.0) == 0.0:
+                # the split LSTM recurrence's cross-workgroup exchange timed out: this step's update was gated
+                # to zero on the device (trainer._lstm_gate); stop rather than train on garbage
+                raise RuntimeError('LSTM split-recurrence exchange timed out (lstm.hip kSplitPollLimit); '
+                                   'the update of this iteration was dropped')
         for k, v in info.items():
             if isinstance(v, (int, float)):
                 self.log_buffer[k] = float(v)

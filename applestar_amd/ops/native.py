@@ -44,12 +44,18 @@ def from_nhwc(t):
     return t.permute(0, 3, 1, 2)
 
 
+def _lowp(x) -> bool:
+    """True when ``x`` is computed at bf16 precision: a bf16 tensor, or any tensor under bf16 autocast."""
+    return x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
+
+
 def _dt_code(dtype) -> int:
     return 1 if dtype == torch.bfloat16 else 0
 
 
 # ---------------------------------------------------------------------------- layer norm
 RESID_LINK = os.environ.get('APPLESTAR_RESID_LINK', '1') == '1'   # A/B switch
+_DEBUG_GRADLINK = os.environ.get('APPLESTAR_DEBUG_GRADLINK', '0') == '1'
 
 
 class GradLink:
@@ -59,12 +65,21 @@ class GradLink:
     separate [T, C] add (two per entity-transformer layer).  Autograd runs the LayerNorm backward before the
     linear's (the linear feeds the LayerNorm), so the hand-off is ordered.  The LayerNorm only hands off
     when the linear armed the link in forward on the native path with the residual itself as its input
-    (``armed`` is that tensor), so an unarmed link leaves the plain two-gradient path in place."""
-    __slots__ = ('armed', 'g')
+    (``armed`` is that tensor), so an unarmed link leaves the plain two-gradient path in place.
+
+    Aliasing invariant: when the residual has the LayerNorm input's dtype, ``g`` IS the LayerNorm's input
+    gradient, which autograd also passes on as the gradient of the branch output (the attention projection /
+    MLP output).  The linear adds into it in place, so every reader of that gradient must run before the
+    branch's first linear's backward - true for the plain autograd order on one stream (the branch's later
+    layers consume it first).  A ``retain_grad`` / stored tensor hook on the branch output, or a consumer on
+    another stream, would see the sum: do not add either to a GradLink block.  ``APPLESTAR_DEBUG_GRADLINK=1``
+    checks at the hand-over that nothing wrote to ``g`` in between (tensor version counter)."""
+    __slots__ = ('armed', 'g', 'version')
 
     def __init__(self):
         self.armed = None
         self.g = None
+        self.version = None
 
 
 class _LayerNorm(torch.autograd.Function):
@@ -92,6 +107,7 @@ class _LayerNorm(torch.autograd.Function):
             dres = dx if ctx.res_dtype == ctx.x_dtype else dx.to(ctx.res_dtype)
             if ctx.link is not None and ctx.needs_input_grad[1]:
                 ctx.link.g, dres = dres, None      # added by the branch linear's dX GEMM (GradLink)
+                ctx.link.version = ctx.link.g._version if _DEBUG_GRADLINK else None
         return dx, dres, dw, db, None, None, None, None
 
 
@@ -141,6 +157,16 @@ def reverse_scan(a, b, init):
 
 
 # ---------------------------------------------------------------------------- LN-LSTM layer
+def lstm_exchange_ok(device):
+    """Device scalar 1.0 while the split LSTM recurrence's cross-workgroup exchange has never timed out on
+    ``device``, else 0.0 (lstm.hip kSplitPollLimit): the trainers multiply it into the optimizer update and log
+    it, so a timed-out step never reaches the weights.  None off the GPU."""
+    if device.type != 'cuda':
+        return None
+    return (ensure_loaded().lstm_split_flag(device.index or 0) == 0).float().reshape(())
+
+
+
 class _LNLSTMRecurrence(torch.autograd.Function):
     """Recurrent part of an LN-LSTM layer: xp [T,B,4H] (already LN_i(x W_ih^T)) -> h [T,B,H]."""
 
@@ -412,15 +438,37 @@ class _VarlenAttention(torch.autograd.Function):
         return dqkv, None, None, None
 
 
+class _VarlenAttentionF32(torch.autograd.Function):
+    """fp32 operands end to end (attention_f32.hip): the like-for-like path of the fp32 learner step."""
+
+    @staticmethod
+    def forward(ctx, qkv, cu, max_len, heads):
+        out, lse = _C.varlen_attn_fwd_f32(qkv, cu, max_len, heads)
+        ctx.save_for_backward(qkv, out, lse, cu)
+        ctx.max_len, ctx.heads = max_len, heads
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse, cu = ctx.saved_tensors
+        dqkv = _C.varlen_attn_bwd_f32(qkv, out, dout.float().contiguous(), lse, cu, ctx.max_len, ctx.heads)
+        return dqkv, None, None, None
+
+
 def varlen_attention(qkv, cu_seqlens, max_len: int, num_heads: int, head_dim: int):
-    """Packed self-attention over variable-length entity sets (bf16 flash kernel, head_dim 128)."""
-    if head_dim != 128:
+    """Packed self-attention over variable-length entity sets, head_dim 128: the bf16 flash kernel for bf16
+    operands (the mixed-precision step), the fp32 flash kernel (f32-input MFMA) for fp32 operands - an fp32
+    input is never rounded to bf16."""
+    if head_dim != 128 or qkv.dtype not in (torch.float32, torch.bfloat16):
         from . import reference
         return reference.varlen_attention(qkv, cu_seqlens, max_len, num_heads, head_dim)
-    dtype = qkv.dtype
-    out = _VarlenAttention.apply(qkv.to(torch.bfloat16).contiguous(), cu_seqlens.to(torch.int32).contiguous(),
-                                 int(max_len), int(num_heads))
-    return out if dtype == torch.bfloat16 else out.to(dtype)
+    cu = cu_seqlens.to(torch.int32).contiguous()
+    if qkv.dtype == torch.float32:
+        if not hasattr(ensure_loaded(), 'varlen_attn_fwd_f32'):
+            from . import reference
+            return reference.varlen_attention(qkv, cu_seqlens, max_len, num_heads, head_dim)
+        return _VarlenAttentionF32.apply(qkv.contiguous(), cu, int(max_len), int(num_heads))
+    return _VarlenAttention.apply(qkv.contiguous(), cu, int(max_len), int(num_heads))
 
 
 def su_sample(key, c0, u, entity_num, su_mask, wf_bf16, bf, wq2, bq2, cell, we1, be1, temperature: float,
@@ -919,6 +967,8 @@ def value_spatial_proj_pool(sc, own, enemy, w, b):
     None when it does not apply."""
     if not (VSP_FUSED and VSP_POOL_FUSED):
         return None
+    if not _lowp(sc):      # bf16 kernel: an fp32 step takes the fp32 conv path, never a rounded copy
+        return None
     B, C, H, W = sc.shape
     cout, cin = w.shape[0], w.shape[1]
     if H % 2 or W % 2 or cout != _C.vsp_out_channels() or cin != _C.vsp_in_channels() or C != cin - 2 or b is None \
@@ -937,6 +987,8 @@ def value_spatial_proj(sc, own, enemy, w, b):
     [16, 10, 1, 1] + bias -> relu(conv(cat([sc, own, enemy]))) as a channels_last [B, 16, H, W] view;
     None when the shapes are not the kernel's."""
     if not VSP_FUSED:
+        return None
+    if not _lowp(sc):      # bf16 kernel: an fp32 step takes the fp32 conv path, never a rounded copy
         return None
     B, C, H, W = sc.shape
     cout, cin = w.shape[0], w.shape[1]
@@ -1084,6 +1136,8 @@ class _Linear(torch.autograd.Function):
         g = None
         if ctx.link is not None:
             g, ctx.link.g = ctx.link.g, None
+            if _DEBUG_GRADLINK and g is not None and g._version != ctx.link.version:
+                raise RuntimeError('GradLink: the handed-over residual gradient was modified before the dX GEMM')
         if g is not None:
             # + the residual gradient the closing LayerNorm handed over (GradLink), in the GEMM epilogue
             # in place: g is the LayerNorm's input gradient, which the branch's later layers (backward

@@ -1,15 +1,20 @@
-"""Bucketed, backward-overlapped gradient all-reduce for the data-parallel learner.
+"""Bucketed gradient all-reduce for the data-parallel learner (one process per GPU, RCCL over xGMI).
 
-The reference (``dist_helper.py:421-431``) all-reduces each of 394-474 parameter tensors one by one
-after backward.  Here every parameter's ``.grad`` is a *view* into a small number of flat buckets;
-a post-accumulate-grad hook counts arrivals and, as soon as a bucket is complete, launches one async
-RCCL all-reduce for it while backward continues into earlier layers.  ``synchronize()`` (called
-before clip/optimizer) only waits for the tail bucket.
+The reference (``dist_helper.py:421-431``) all-reduces each of its 394-474 parameter tensors one by one
+after backward.  Here every parameter's ``.grad`` is a *view* into a small number of flat buckets.
 
-Bucket size is chosen for xGMI rings (7 point-to-point links at ~153 GB/s per MI355X): a ring
-all-reduce moves 2(n-1)/n of the bucket over each link, so fewer, larger buckets (default 32 MB)
-amortise RCCL launch latency while still leaving several buckets to overlap with backward on a
-~33 M-parameter model (132 MB of fp32 gradients -> ~5 buckets).
+Backward has ONE launch structure at every world size (the single-rank one): ``torch.autograd.grad``
+over all parameters, then one native multi-tensor copy writes every gradient into its bucket slot - no
+per-parameter ``AccumulateGrad`` add into zeroed buckets and no per-parameter Python hook.  ``synchronize``
+then issues one async RCCL all-reduce per bucket (AVG inside RCCL) back to back and waits for them.
+
+Why not overlap the collectives with backward through per-parameter hooks (round 2's design)?  On this
+learner the step is host-issue bound (``profiles/r2dz_*``: ~1,250 launches, host time ~ wall time): ~460
+Python hook calls per step are a few ms of host time on EVERY rank, while the whole exposed collective is
+small - 132 MB of fp32 gradients on an 8-GPU ring moves 2 x 7/8 x 132 MB per link, about 0.8-1.5 ms at
+the 150-300 GB/s an xGMI ring sustains, against a 30-90 ms step.  Buckets default to 32 MB so the copy of
+one bucket and the reduction of the previous one pipeline inside RCCL; the whole reduction is two to five
+calls.
 """
 from __future__ import annotations
 
@@ -21,40 +26,15 @@ import torch.distributed as dist
 from . import dist as pdist
 
 
-def _cur_stream(t: torch.Tensor):
-    return torch.cuda.current_stream(t.device) if t.is_cuda else None
-
-
-def join_hook_stream(main, t: Optional[torch.Tensor] = None):
-    """Called from a gradient hook.  The autograd engine runs a parameter's hooks on the stream its
-    gradient was produced on: the stream its forward ran on (the scalar encoder runs on a side stream,
-    models/model.py ``_side_stream_call``).  Bucket copies and collectives are always issued on ``main``
-    (the stream backward was started from), so ``main`` must first wait for that producer stream, and a
-    hook-captured gradient ``t`` read later on ``main`` must not be recycled by the allocator early.
-    Without this, a bucket completed from a side-stream hook was copied / reduced while main-stream
-    gradients of the same bucket were still being computed (non-finite gradients with world > 1)."""
-    if main is None:
+def copy_into(dst: List[torch.Tensor], src: List[torch.Tensor]):
+    """dst[i].copy_(src[i]) for all i: one native multi-tensor launch on the GPU (dtype-converting)."""
+    if not dst:
         return
-    cur = torch.cuda.current_stream(main.device)
-    if cur != main:
-        main.wait_stream(cur)
-        if t is not None:
-            t.record_stream(main)
-
-
-class _on_stream:
-    """``with torch.cuda.stream(main)`` that is a no-op for CPU (``main`` None)."""
-
-    def __init__(self, main):
-        self.ctx = torch.cuda.stream(main) if main is not None else None
-
-    def __enter__(self):
-        if self.ctx is not None:
-            self.ctx.__enter__()
-
-    def __exit__(self, *exc):
-        if self.ctx is not None:
-            self.ctx.__exit__(*exc)
+    if dst[0].is_cuda:
+        from ..ops import native
+        native.ensure_loaded().multi_copy(dst, src)
+    else:
+        torch._foreach_copy_(dst, src)
 
 
 class _Bucket:
@@ -102,11 +82,7 @@ class GradientReducer:
             if cur:
                 self._add_bucket(cur)
         self._hooks = []
-        if self.world > 1 and overlap:
-            for p in params:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
         self.use_avg = self.world > 1 and dist.get_backend(group) == 'nccl'
-        self._main = None        # stream backward was started from (bucket collectives are issued there)
 
     def _add_bucket(self, params):
         b = _Bucket(params, params[0].dtype, params[0].device)
@@ -137,38 +113,29 @@ class GradientReducer:
         op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
         b.handle = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
 
-    def _on_grad(self, p):
-        join_hook_stream(self._main)
-        b = self._owner[p]
-        b.ready += 1
-        if b.ready == len(b.params):
-            with _on_stream(self._main):
-                self._launch(b)
-
     def backward(self, loss: torch.Tensor):
-        """``loss.backward()`` into the bucket views.
-
-        Multi-rank: plain backward, so the post-accumulate hooks launch each bucket's all-reduce as soon
-        as its last gradient lands (overlap with the rest of backward).  Single rank: there is nothing to
-        overlap, so the gradients are taken with ``autograd.grad`` (no per-parameter AccumulateGrad
-        ``add_`` into the zeroed buckets - ~240 launches per RL step) and written with one multi-tensor
-        copy."""
-        if self.world > 1:
-            self._main = _cur_stream(loss)
-            loss.backward()
-            return
+        """Gradients of ``loss`` into the bucket views: ``autograd.grad`` + one multi-tensor copy (native on
+        the GPU), at every world size; buckets holding a parameter without a gradient are zeroed first."""
         grads = torch.autograd.grad(loss, self.params, allow_unused=True)
         dst, src = [], []
+        stale = set()
         for p, g in zip(self.params, grads):
             if g is not None:
                 dst.append(p.grad)
                 src.append(g)
-        if dst:
-            torch._foreach_copy_(dst, src)
-
-    def zero_grad(self):
+            else:
+                stale.add(id(self._owner[p]))
         for b in self.buckets:
-            b.flat.zero_()
+            if id(b) in stale:
+                b.flat.zero_()
+        copy_into(dst, src)
+
+    def zero_grad(self, buffers: bool = True):
+        """Reset the per-step state; ``buffers=False`` leaves the bucket memory alone (``backward`` overwrites
+        every slot, zeroing the buckets of unused parameters itself)."""
+        for b in self.buckets:
+            if buffers:
+                b.flat.zero_()
             b.ready = 0
             b.handle = None
             b.comm = None

@@ -17,7 +17,7 @@ from typing import Dict, List
 import torch
 import torch.nn as nn
 
-from .dp import GradientReducer, join_hook_stream, _on_stream
+from .dp import GradientReducer, copy_into
 
 LOWP_MODULES = (nn.Linear, nn.Conv2d, nn.ConvTranspose2d)
 
@@ -77,8 +77,8 @@ class MasterWeights:
             self.derived = DerivedWeights()
             for p in self.params:
                 p._derived_forms = self.derived
-        # multi-rank: False = per-bucket all-reduce overlapped with backward (eager step); True = backward
-        # writes the local gradient and synchronize() reduces the flat buffers (graph-captured step)
+        # kept for the graph-captured step (runtime/step_graph.py), which runs the reduction between its two
+        # graphs: backward never launches a collective, so this only documents that contract
         self.defer_allreduce = False
 
     # ---------------------------------------------------------------- per iteration
@@ -86,23 +86,14 @@ class MasterWeights:
         self.reducer.zero_grad()
 
     def backward(self, loss: torch.Tensor):
-        """Backward straight into the fp32 master gradient (``autograd.grad``: no per-parameter
-        AccumulateGrad ``add_`` into zeroed buckets, ~240 launches per RL step).
-
-        Single rank: ONE native multi-tensor copy writes every bf16 gradient, converted, into its fp32
-        master-grad slot (and the fp32 ones into their buckets).  Multi-rank: a tensor hook per
-        parameter collects the gradients of each bucket as backward produces them; when a bucket is
-        complete, one multi-tensor copy writes them (converted) into the bucket's slice of the fp32 master
-        gradient and ONE async RCCL all-reduce of that slice starts, overlapping the rest of backward
-        (:meth:`synchronize` waits for the tail).  The reduction is fp32 and lands in place: no bf16
-        bucket, no gather into the master afterwards."""
+        """Backward straight into the fp32 master gradient, with the same launches at every world size:
+        ``autograd.grad`` (no per-parameter ``AccumulateGrad`` add into zeroed buckets) and ONE native
+        multi-tensor copy that writes every bf16 gradient, converted, into its fp32 master-grad slot (and the
+        fp32 ones into their buckets).  Multi-rank, :meth:`synchronize` then all-reduces the flat fp32
+        buffers (fp32 reduction of the bf16 gradients; parallel/dp.py explains why the collective is not
+        overlapped with backward through per-parameter hooks)."""
         self._direct = False
-        self._overlapped = False
-        world = self.reducer.world
-        if world > 1 and not self.defer_allreduce:
-            self._backward_overlapped(loss)
-            return
-        if not loss.is_cuda and world == 1:
+        if not loss.is_cuda:
             self.reducer.backward(loss)
             return
         grads = torch.autograd.grad(loss, self.reducer.params, allow_unused=True)
@@ -117,92 +108,23 @@ class MasterWeights:
             for b in self.reducer.buckets:
                 if b.flat.dtype != torch.bfloat16:
                     b.flat.zero_()
-        if loss.is_cuda:
-            from ..ops import native
-            native.ensure_loaded().multi_copy(dst, src)
-        else:
-            torch._foreach_copy_(dst, src)
+        copy_into(dst, src)
         self._direct = True
 
     def reduce_flat(self):
-        """All-reduce (average) the whole fp32 master gradient and the fp32 buckets: two RCCL calls,
-        used when backward ran without per-bucket overlap (``defer_allreduce``, e.g. between the two
-        halves of a graph-captured step)."""
+        """All-reduce (average) the whole fp32 master gradient and the fp32 buckets: one RCCL call each,
+        issued back to back (async) and then waited for."""
         import torch.distributed as dist
         if self.reducer.world == 1:
             return
         bufs = [self.master.grad] + [b.flat for b in self.reducer.buckets if b.flat.dtype != torch.bfloat16]
         avg = self.reducer.use_avg
-        for buf in bufs:
-            dist.all_reduce(buf, op=dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM, group=self.reducer.group)
+        op = dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
+        handles = [dist.all_reduce(buf, op=op, group=self.reducer.group, async_op=True) for buf in bufs]
+        for h, buf in zip(handles, bufs):
+            h.wait()
             if not avg:
                 buf.div_(self.reducer.world)
-
-    # ---------------------------------------------------------------- multi-rank, overlapped
-    def _comm_buffers(self):
-        """Per bucket: the fp32 buffer that is all-reduced (a master-grad slice for bf16 buckets, the
-        bucket itself for fp32 ones) and, per parameter, its destination view in that buffer."""
-        plan = getattr(self, '_plan', None)
-        if plan is None:
-            mg = self._master_grad_views()
-            slot = {id(b): (off, k) for b, off, k in self._slices}
-            plan = {}
-            for b in self.reducer.buckets:
-                if id(b) in slot:
-                    off, k = slot[id(b)]
-                    buf = self.master.grad[off:off + k]
-                else:
-                    buf = b.flat
-                plan[id(b)] = (buf, {p: mg.get(p, p.grad) for p in b.params})
-            self._plan = plan
-            self._bucket_of = {p: b for b in self.reducer.buckets for p in b.params}
-            self._hook_handles = [p.register_hook(self._make_hook(p)) for p in self.reducer.params]
-        return plan
-
-    def _make_hook(self, p):
-        def hook(g):
-            if getattr(self, '_overlapped', False):
-                join_hook_stream(self._main, g)
-                b = self._bucket_of[p]
-                st = self._pending[id(b)]
-                st.append((p, g))
-                if len(st) == len(b.params):
-                    with _on_stream(self._main):
-                        self._flush(b)
-            return None
-        return hook
-
-    def _flush(self, b):
-        """Copy the collected gradients of bucket ``b`` into its fp32 buffer and start its all-reduce."""
-        import torch.distributed as dist
-        if id(b) in self._handles:
-            return
-        buf, dst_of = self._plan[id(b)]
-        got = self._pending[id(b)]
-        if len(got) < len(b.params):           # unused parameters contribute zeros
-            buf.zero_()
-        dst = [dst_of[p] for p, _ in got]
-        src = [g for _, g in got]
-        if dst:
-            if buf.is_cuda:
-                from ..ops import native
-                native.ensure_loaded().multi_copy(dst, src)
-            else:
-                torch._foreach_copy_(dst, src)
-        op = dist.ReduceOp.AVG if self.reducer.use_avg else dist.ReduceOp.SUM
-        self._handles[id(b)] = dist.all_reduce(buf, op=op, group=self.reducer.group, async_op=True)
-
-    def _backward_overlapped(self, loss: torch.Tensor):
-        self._comm_buffers()
-        self._pending = {id(b): [] for b in self.reducer.buckets}
-        self._handles = {}
-        self._main = torch.cuda.current_stream(loss.device) if loss.is_cuda else None
-        self._overlapped = True
-        try:
-            torch.autograd.grad(loss, self.reducer.params, allow_unused=True)
-        finally:
-            self._overlapped = False
-        self._overlap_done = True
 
     def _master_grad_views(self):
         views = getattr(self, '_mg_views', None)
@@ -219,22 +141,11 @@ class MasterWeights:
         return views
 
     def synchronize(self):
-        """All-reduce (if distributed) and gather the bf16 gradients into the flat fp32 master grad."""
+        """Average the gradients across ranks (no-op on one rank)."""
         if getattr(self, '_direct', False):
             self.reduce_flat()
             return
-        if getattr(self, '_overlap_done', False):
-            self._overlap_done = False
-            for b in self.reducer.buckets:         # buckets whose parameters all went unused
-                self._flush(b)
-            world = self.reducer.world
-            for b in self.reducer.buckets:
-                self._handles[id(b)].wait()
-                if not self.reducer.use_avg:
-                    self._plan[id(b)][0].div_(world)
-            self._handles = {}
-            return
-        self.reducer.synchronize()
+        self.reducer.synchronize()        # CPU path: the plain bucket reducer, then bucket -> master
         g = self.master.grad
         for b, off, k in self._slices:
             g[off:off + k].copy_(self.reducer.reduced(b))

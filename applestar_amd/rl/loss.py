@@ -62,6 +62,9 @@ class ReinforcementLoss:
         self.gammas = c.gammas
         self.action_type_kl_steps = c.kl.action_type_kl_steps
         self.dapo_steps = c.dapo.dapo_steps
+        # device copies of the weights / gammas are derived from the config: drop them with it
+        self.__dict__.pop('_sc_cache', None)
+        self.__dict__.pop('_hw_cache', None)
 
     def reset(self, learner_cfg):
         self.cfg = deep_merge_dicts(self.cfg, learner_cfg)

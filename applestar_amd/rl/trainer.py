@@ -127,7 +127,7 @@ class RLTrainer:
         with _amp(self.device, self.amp_dtype):
             out = self.model.rl_learner_forward(**batch)
         info = self.loss.compute_loss(out)
-        self.reducer.zero_grad()
+        self.reducer.zero_grad(buffers=False)    # backward overwrites every slot (and zeroes unused ones)
         if self.master is not None:
             self.master.backward(info['total_loss'])
         else:
@@ -143,11 +143,21 @@ class RLTrainer:
             self.reducer.synchronize()
 
     def _update(self) -> torch.Tensor:
-        norm = self.grad_clip.apply(self.opt_params)
+        gate = self._lstm_gate()
+        norm = self.grad_clip.apply(self.opt_params, gate=gate)
         self.optimizer.step()
         if self.master is not None:
             self.master.after_step()
         return norm
+
+    def _lstm_gate(self):
+        """1.0 / 0.0 device scalar: the split LSTM exchange has not / has timed out (ops.native.lstm_exchange_ok);
+        logged with the step's scalars as ``lstm_exchange_ok`` (the learner raises on 0)."""
+        if self.device.type != 'cuda':
+            return None
+        from ..ops import native
+        self._gate = native.lstm_exchange_ok(self.device)
+        return self._gate
 
     def step(self, batch: Dict) -> Dict[str, torch.Tensor]:
         self._value_pretrain_toggle()
@@ -161,6 +171,8 @@ class RLTrainer:
             info = self._fwd_bwd(batch)
             self._reduce()
             info['gradient'] = self._update()
+            if getattr(self, '_gate', None) is not None:
+                info['lstm_exchange_ok'] = self._gate
         self.iter += 1
         return info
 

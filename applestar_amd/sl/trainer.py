@@ -74,10 +74,14 @@ class SLTrainer:
         info = self.loss.compute_loss(logits, batch['action_info'], batch['action_mask'], batch['selected_units_num'],
                                       batch['entity_num'], infer_action)
         if self.iter >= self.ignore_steps:
-            self.reducer.zero_grad()
+            self.reducer.zero_grad(buffers=False)    # backward overwrites every slot
             self.reducer.backward(info['total_loss'])
             self.reducer.synchronize()
-            info['gradient'] = self.grad_clip.apply(self.params)
+            gate = None
+            if self.device.type == 'cuda':
+                from ..ops import native
+                gate = info['lstm_exchange_ok'] = native.lstm_exchange_ok(self.device)
+            info['gradient'] = self.grad_clip.apply(self.params, gate=gate)
             self.optimizer.step()
             self.lr_scheduler.step()
         self.hidden_state = [(h.detach(), c.detach()) for h, c in hidden]

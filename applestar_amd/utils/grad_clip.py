@@ -9,7 +9,7 @@ EMA state lives on the device, so a clip never forces a host round trip (the ref
 from __future__ import annotations
 
 import math
-from typing import Iterable, List
+from typing import Optional, Iterable, List
 
 import torch
 
@@ -63,7 +63,10 @@ class GradClip:
         self.exp_avg_sq = sd.get('exp_avg_sq')
 
     @torch.no_grad()
-    def apply(self, parameters: Iterable[torch.nn.Parameter]) -> torch.Tensor:
+    def apply(self, parameters: Iterable[torch.nn.Parameter], gate: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Clip in place and return the global norm.  ``gate``: an optional device scalar (1 = keep, 0 = drop
+        the whole step's gradient, e.g. a timed-out LSTM exchange), folded into the clip coefficient where
+        there is one; no host sync either way."""
         self.step += 1
         grads = _grads(list(parameters))
         if not grads:
@@ -73,6 +76,9 @@ class GradClip:
         t = self.clip_type
         if t in ('pytorch_norm', 'clip_norm'):
             coef = (self.threshold / (total + 1e-6)).clamp(max=1.0)
+            if gate is not None:
+                coef = coef * gate
+                gate = None
             torch._foreach_mul_(grads, coef)
         elif t == 'max_norm':
             bc1 = 1 - self.beta1 ** self.step
@@ -106,4 +112,6 @@ class GradClip:
         elif t == 'clip_const':
             for g in grads:
                 g.clamp_(-self.threshold, self.threshold)
+        if gate is not None:
+            torch._foreach_mul_(grads, gate)
         return total

@@ -125,8 +125,8 @@ def test_master_weights_world2():
 
 
 def _overlap_worker(rank, world, port, q, defer=False):
-    """MasterWeights.backward at world 2: per-bucket copy + all-reduce from tensor hooks, into the fp32
-    master gradient; compared with the average of both ranks' gradients computed locally."""
+    """MasterWeights.backward + synchronize at world 2 (autograd.grad, one copy into the fp32 master gradient,
+    flat all-reduce); compared with the average of both ranks' gradients computed locally."""
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
     from applestar_amd.parallel import dist as pdist
     from applestar_amd.parallel.mixed import MasterWeights
@@ -169,8 +169,9 @@ def _overlap_worker(rank, world, port, q, defer=False):
 
 @pytest.mark.parametrize('defer', [False, True])
 def test_master_weights_overlapped_backward_world2(defer):
-    """defer=False: per-bucket all-reduce from tensor hooks during backward; defer=True: backward writes
-    the local gradient and synchronize() reduces the flat master gradient (graph-captured step)."""
+    """Both settings of ``defer_allreduce`` (the eager step and the graph-captured step's contract) take the
+    same path: backward writes the local gradient, synchronize() reduces the flat master gradient; the
+    unused bucket-mate ends with an exact zero gradient."""
     world = 2
     port = _free_port()
     ctx = mp.get_context('spawn')

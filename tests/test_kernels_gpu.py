@@ -264,6 +264,34 @@ def test_varlen_attention_matches_reference(lens):
     assert _err(qkv.grad, ref_in.grad) < 3e-2 * max(1.0, scale)
 
 
+@pytest.mark.parametrize('lens', [[1, 64, 65, 200, 511], [37], [128, 3, 300]])
+@pytest.mark.parametrize('score_scale', [0.5, 2.0])
+def test_varlen_attention_fp32_matches_fp64(lens, score_scale):
+    """fp32 operands take the f32-MFMA kernel (attention_f32.hip), never a bf16 copy: forward and all three
+    input gradients within fp32 rounding of a float64 reference."""
+    torch.manual_seed(11)
+    H, Dh = 2, 128
+    T = sum(lens)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    qkv = (torch.randn(T, 3 * H * Dh, device=DEV) * score_scale).requires_grad_()
+    ref_in = qkv.detach().double().cpu().requires_grad_()
+    out = N.varlen_attention(qkv, cu, max(lens), H, Dh)
+    assert out.dtype == torch.float32
+    ref = R.varlen_attention(ref_in, cu.cpu(), max(lens), H, Dh)
+    assert _err(out.cpu(), ref) < 2e-5 * max(1.0, ref.abs().max().item())
+    g = torch.randn(ref.shape, dtype=torch.float64)
+    out.backward(g.float().to(DEV))
+    ref.backward(g)
+    scale = ref_in.grad.abs().max().item()
+    err = (qkv.grad.double().cpu() - ref_in.grad).abs()
+    assert err.max().item() < 5e-5 * max(1.0, scale), err.max().item()
+    # relative Frobenius over each of q / k / v
+    for part in range(3):
+        sl = slice(part * H * Dh, (part + 1) * H * Dh)
+        rel = err[:, sl].norm() / ref_in.grad[:, sl].norm().clamp_min(1e-30)
+        assert rel.item() < 1e-5, (part, rel.item())
+
+
 def test_su_sample_kernel_matches_teacher_forcing_and_torch_sampler():
     """Persistent pointer-network sampler: its logits must equal the teacher-forced logits of the
     units it picked, its picks must follow inverse-CDF sampling of those logits, and (fp32) it should

@@ -302,7 +302,8 @@ def test_data_parallel_two_ranks_finite_and_identical(tmp_path):
 
 
 @pytest.mark.parametrize('only_value', [False, True])
-def test_fused_rl_loss_matches_torch_loss(only_value):
+@pytest.mark.parametrize('bo_pg_weight', [0.5, 0.0])
+def test_fused_rl_loss_matches_torch_loss(only_value, bo_pg_weight):
     """rl_loss.hip (the loss after the per-head statistics, with closed-form gradients) vs the torch
     ReinforcementLoss path: total loss, every info entry, and the gradients w.r.t. all head logits and the
     baseline values; two baseline fields (winloss + build_order with its mask)."""
@@ -325,7 +326,8 @@ def test_fused_rl_loss_matches_torch_loss(only_value):
                 'teacher_logit': batch['teacher_logit'], 'mask': mask, 'action': batch['action_info'],
                 'reward': batch['reward'], 'step': batch['step']}
 
-    cfg = {'loss_weights': {'pg': {'build_order': 0.5}, 'baseline': {'build_order': 2.0}}}
+    # pg weight 0 (the reference config's non-winloss fields): pg/<field> is still logged by both paths
+    cfg = {'loss_weights': {'pg': {'build_order': bo_pg_weight}, 'baseline': {'build_order': 2.0}}}
     results = []
     inp = make_inputs()
     for fused in (True, False):
