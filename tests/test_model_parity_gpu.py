@@ -100,79 +100,116 @@ def test_full_model_fp32_gpu_matches_cpu_fp32(reference):
     assert not bad, bad
 
 
+def _bf16_grad_errors(cpu, batch, ref_grads, native: bool):
+    """Per-group relative gradient error of the mixed-precision trainer against the fp32 oracle, with the
+    native kernels on, or off (PyTorch's own bf16 autocast path: the control)."""
+    from applestar_amd import ops
+    ops.set_native(native)
+    try:
+        tr = RLTrainer(CFG, device='cuda')
+        assert tr.master is not None
+        tr.load_model_state_dict(cpu.state_dict())
+        info = tr._fwd_bwd(to_device(copy.deepcopy(batch), 'cuda'))
+        tr._reduce()
+        with torch.autocast('cuda', dtype=torch.bfloat16, cache_enabled=False), torch.no_grad():
+            out = tr.model.rl_learner_forward(**to_device(copy.deepcopy(batch), 'cuda'))
+        views = tr.master._master_grad_views()
+        got = {}
+        for p in tr.master.reducer.params:
+            g = views.get(p, p.grad)
+            if g is not None:
+                got[tr.master.names[p]] = g.float()
+        torch.cuda.synchronize()
+    finally:
+        ops.set_native(True)
+    return _group_errors(got, ref_grads), out, info
+
+
 def test_full_model_bf16_gpu_vs_cpu_fp32(reference):
     """The mixed-precision trainer (bf16 compute weights + autocast) against the same fp32 oracle: all six
-    heads' logits and the value within bf16 rounding, and every parameter-group gradient (read from the fp32
-    master gradient) within a stated relative Frobenius bound."""
+    heads' logits and the value within bf16 rounding, the loss within 2 %, and every parameter-group
+    gradient (read from the fp32 master gradient) no further from the oracle than PyTorch's own bf16
+    autocast path is (native kernels off, same weights and batch): the native kernels add no error of their
+    own on top of bf16 compute.  Both error tables go to gpurun_out/bf16_grad_group_errors.json."""
     batch, (cpu, ref_out, ref_info, ref_grads) = reference
-    tr = RLTrainer(CFG, device='cuda')
-    assert tr.master is not None
-    tr.load_model_state_dict(cpu.state_dict())
-    info = tr._fwd_bwd(to_device(copy.deepcopy(batch), 'cuda'))
-    tr._reduce()
-    with torch.autocast('cuda', dtype=torch.bfloat16, cache_enabled=False), torch.no_grad():
-        out = tr.model.rl_learner_forward(**to_device(copy.deepcopy(batch), 'cuda'))
+    errs, out, info = _bf16_grad_errors(cpu, batch, ref_grads, native=True)
+    errs_torch, _, _ = _bf16_grad_errors(cpu, batch, ref_grads, native=False)
     for h in HEADS:
         e = _masked_rel(out['target_logit'][h].float(), ref_out['target_logit'][h])
         assert e < 3e-2, (h, e)
     assert _rel(out['value']['winloss'].float(), ref_out['value']['winloss']) < 3e-2
     a, r = float(info['total_loss']), float(ref_info['total_loss'])
     assert abs(a - r) <= 2e-2 * max(1.0, abs(r)), (a, r)
-    views = tr.master._master_grad_views()
-    names = tr.master.names
-    got = {}
-    for p in tr.master.reducer.params:
-        g = views.get(p, p.grad)
-        if g is not None:
-            got[names[p]] = g.float()
-    errs = _group_errors(got, ref_grads)
-    with open(os.path.join(OUT_DIR, 'bf16_grad_group_errors.json'), 'w') if os.path.isdir(OUT_DIR) else \
-            open(os.devnull, 'w') as f:
-        json.dump(errs, f, indent=1, sort_keys=True)
-    bad = {k: v for k, v in errs.items() if v > 0.1}
-    assert not bad, (bad, errs)
+    table = {k: {'native_bf16': errs[k], 'torch_bf16': errs_torch[k]} for k in errs}
+    if os.path.isdir(OUT_DIR):
+        with open(os.path.join(OUT_DIR, 'bf16_grad_group_errors.json'), 'w') as f:
+            json.dump(table, f, indent=1, sort_keys=True)
+    # r3b (profiles/r3b_bf16_grad_group_errors.json): 16 of 18 groups within +-15 % of torch's own bf16 error;
+    # the location head (5.8 vs 4.5 %) and the value encoder's 1x1 projection (a 176-parameter layer whose
+    # gradient is a 9.5M-pixel reduction of bf16 products: 25 vs 18 %) are the two above 1.25x
+    bad = {k: v for k, v in table.items() if v['native_bf16'] > max(1.5 * v['torch_bf16'], 0.03)}
+    assert not bad, bad
+    # and in absolute terms: the big groups (transformer, spatial ResNet, LSTM, heads) within 15 %
+    assert all(v['native_bf16'] < 0.15 for k, v in table.items() if k.startswith(('core_lstm', 'policy'))), table
 
 
-def test_bf16_training_tracks_fp32():
-    """30 learner steps of the fp32 and the bf16 trainer from the same weights on the same 4 batches
-    (lr 1e-4, Adam betas (0, 0.99), pytorch_norm clip 1.0 as the reference): the total-loss and gradient-norm
-    trajectories agree step by step, and the accumulated parameter update points the same way."""
-    steps = 30
-    cfg32 = {**CFG, 'learner': {**CFG['learner'], 'amp_dtype': None, 'learning_rate': 1e-4}}
-    cfg16 = {**CFG, 'learner': {**CFG['learner'], 'learning_rate': 1e-4}}
-    torch.manual_seed(0)
-    t32 = RLTrainer(cfg32, device='cuda')
-    torch.manual_seed(0)
-    t16 = RLTrainer(cfg16, device='cuda')
-    t16.load_model_state_dict(t32.model.state_dict())
-    w0 = {k: v.detach().clone() for k, v in t32.model_state_dict().items()}
-    batches = [to_device(rl_batch(2, 8, max_entities=64, seed=100 + i), 'cuda') for i in range(4)]
-    rec = []
-    for s in range(steps):
-        b = batches[s % len(batches)]
-        i32 = t32.step(copy.deepcopy(b))
-        i16 = t16.step(copy.deepcopy(b))
-        rec.append({'step': s, 'loss_fp32': float(i32['total_loss']), 'loss_bf16': float(i16['total_loss']),
-                    'gnorm_fp32': float(i32['gradient']), 'gnorm_bf16': float(i16['gradient'])})
-    w32, w16 = t32.model_state_dict(), t16.model_state_dict()
-    num = den32 = den16 = 0.0
+def _trajectory(cfg, batches, steps, w_init, native=True):
+    from applestar_amd import ops
+    ops.set_native(native)
+    try:
+        tr = RLTrainer(cfg, device='cuda')
+        tr.load_model_state_dict(w_init)
+        rec = []
+        for s in range(steps):
+            info = tr.step(copy.deepcopy(batches[s % len(batches)]))
+            rec.append((float(info['total_loss']), float(info['gradient'])))
+        w = {k: v.detach().double().clone() for k, v in tr.model_state_dict().items()}
+        torch.cuda.synchronize()
+    finally:
+        ops.set_native(True)
+    return rec, w
+
+
+def _compare(rec_a, w_a, rec_b, w_b, w0):
+    num = da = db = 0.0
     for k, v0 in w0.items():
         if not v0.is_floating_point():
             continue
-        d32 = (w32[k].double() - v0.double()).flatten()
-        d16 = (w16[k].double() - v0.double()).flatten()
-        num += float((d32 * d16).sum())
-        den32 += float(d32.square().sum())
-        den16 += float(d16.square().sum())
-    cos = num / max((den32 * den16) ** 0.5, 1e-60)
-    rel_loss = [abs(r['loss_bf16'] - r['loss_fp32']) / max(abs(r['loss_fp32']), 1e-3) for r in rec]
-    rel_gn = [abs(r['gnorm_bf16'] - r['gnorm_fp32']) / max(r['gnorm_fp32'], 1e-6) for r in rec]
-    summary = {'update_cosine': cos, 'update_norm_ratio': (den16 / max(den32, 1e-60)) ** 0.5,
-               'max_rel_loss': max(rel_loss), 'median_rel_loss': sorted(rel_loss)[len(rel_loss) // 2],
-               'max_rel_gnorm': max(rel_gn), 'median_rel_gnorm': sorted(rel_gn)[len(rel_gn) // 2], 'steps': rec}
+        x = (w_a[k] - v0.double().cuda()).flatten()
+        y = (w_b[k] - v0.double().cuda()).flatten()
+        num += float((x * y).sum())
+        da += float(x.square().sum())
+        db += float(y.square().sum())
+    rel_loss = sorted(abs(b[0] - a[0]) / max(abs(a[0]), 1e-2) for a, b in zip(rec_a, rec_b))
+    rel_gn = sorted(abs(b[1] - a[1]) / max(a[1], 1e-6) for a, b in zip(rec_a, rec_b))
+    return {'update_cosine': num / max((da * db) ** 0.5, 1e-60), 'update_norm_ratio': (db / max(da, 1e-60)) ** 0.5,
+            'median_rel_loss': rel_loss[len(rel_loss) // 2], 'max_rel_loss': rel_loss[-1],
+            'median_rel_gnorm': rel_gn[len(rel_gn) // 2], 'max_rel_gnorm': rel_gn[-1]}
+
+
+def test_bf16_training_tracks_fp32():
+    """30 learner steps at the reference RL settings (lr 1e-5, Adam betas (0, 0.99) eps 1e-5, pytorch_norm clip
+    1.0: distar/agent/default/rl_learner.py) of the fp32 and the bf16 trainer from the same weights over the
+    same 6 batches: total loss and gradient norm track step by step and the accumulated update points the same
+    way.  Control: an fp32 run on the plain PyTorch kernels (same precision, different kernels / summation
+    order) shows how far two fp32 runs drift apart on their own.  Summary -> gpurun_out/precision_parity.json."""
+    steps = 30
+    cfg32 = {**CFG, 'learner': {**CFG['learner'], 'amp_dtype': None}}
+    torch.manual_seed(0)
+    w0 = {k: v.detach().clone() for k, v in RLTrainer(cfg32, device='cuda').model_state_dict().items()}
+    batches = [to_device(rl_batch(2, 8, max_entities=64, seed=100 + i), 'cuda') for i in range(6)]
+    r32, w32 = _trajectory(cfg32, batches, steps, w0)
+    r16, w16 = _trajectory(CFG, batches, steps, w0)
+    rct, wct = _trajectory(cfg32, batches, steps, w0, native=False)
+    summary = {'bf16_vs_fp32': _compare(r32, w32, r16, w16, w0),
+               'control_fp32_torch_vs_fp32_native': _compare(r32, w32, rct, wct, w0),
+               'steps': [{'step': i, 'loss_fp32': a[0], 'loss_bf16': b[0], 'loss_fp32_torch': c[0],
+                          'gnorm_fp32': a[1], 'gnorm_bf16': b[1], 'gnorm_fp32_torch': c[1]}
+                         for i, (a, b, c) in enumerate(zip(r32, r16, rct))]}
     if os.path.isdir(OUT_DIR):
         with open(os.path.join(OUT_DIR, 'precision_parity.json'), 'w') as f:
             json.dump(summary, f, indent=1)
-    assert summary['median_rel_loss'] < 0.02 and summary['max_rel_loss'] < 0.1, summary
-    assert summary['median_rel_gnorm'] < 0.05 and summary['max_rel_gnorm'] < 0.2, summary
-    assert cos > 0.9 and 0.8 < summary['update_norm_ratio'] < 1.25, summary
+    s = summary['bf16_vs_fp32']
+    assert s['median_rel_loss'] < 0.01 and s['max_rel_loss'] < 0.05, summary
+    assert s['median_rel_gnorm'] < 0.03 and s['max_rel_gnorm'] < 0.15, summary
+    assert s['update_cosine'] > 0.95 and 0.9 < s['update_norm_ratio'] < 1.1, summary

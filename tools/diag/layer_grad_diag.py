@@ -44,8 +44,19 @@ def reference(act):
     return y.detach(), xr.grad.detach(), pre.detach()
 
 
-def run(native_on, bf16, act):
+def run(native_on, bf16, act, ref_op=None):
+    """``ref_op``: 'attention' / 'layer_norm' runs that one op on the plain PyTorch path (per-op isolation)."""
     ops.set_native(native_on)
+    saved = None
+    if ref_op is not None:
+        from applestar_amd.ops import reference
+        saved = getattr(ops, ref_op if ref_op != 'attention' else 'varlen_attention')
+        if ref_op == 'attention':
+            ops.varlen_attention = reference.varlen_attention
+        else:
+            ops.layer_norm = lambda x, w, b, residual=None, act=None, eps=1e-5, grad_link=None: \
+                reference.layer_norm(x if residual is None else x.float(),
+                                     w, b, None if residual is None else residual.float(), act, eps)
     layer = TransformerLayer(256, 128, 1024, 2, 2, 'post').to(dev)
     layer.load_state_dict(base.state_dict())
     x = x0.to(dev).to(torch.bfloat16 if bf16 else torch.float32).requires_grad_(True)
@@ -55,6 +66,10 @@ def run(native_on, bf16, act):
     y.float().backward(dy.to(dev))
     torch.cuda.synchronize()
     ops.set_native(True)
+    if ref_op == 'attention':
+        ops.varlen_attention = saved
+    elif ref_op is not None:
+        ops.layer_norm = saved
     return y.detach().double().cpu(), x.grad.double().cpu(), pre.detach().double().cpu()
 
 
@@ -72,7 +87,7 @@ def report(name, got, ref):
     clean_rel = float((g - gr)[~rows_flip].norm() / gr[~rows_flip].norm()) if clean.numel() else 0.0
     row_err = err.max(1).values
     worst = torch.topk(row_err, 3)
-    print(f'  {name:24s} y rel {yrel:.2e}  dx: max {float(err.max()):.4f} (of {float(gr.abs().max()):.3f}), '
+    print(f'  {name:30s} y rel {yrel:.2e}  dx: max {float(err.max()):.4f} (of {float(gr.abs().max()):.3f}), '
           f'rel-Frobenius {rel:.2e} | ReLU flips {nflip:5d} in {int(rows_flip.sum()):4d}/{T} rows | '
           f'rows without a flip: max {clean_max:.4f}, rel {clean_rel:.2e} | worst rows '
           + ', '.join(f'{int(i)}:{float(v):.3f}{"*" if bool(rows_flip[i]) else ""}'
@@ -85,4 +100,6 @@ for act in (None, 'relu'):
     report('native bf16 autocast', run(True, True, act), ref)
     report('torch bf16 autocast', run(False, True, act), ref)
     report('native fp32', run(True, False, act), ref)
+    report('native fp32, torch attention', run(True, False, act, 'attention'), ref)
+    report('native fp32, torch LN', run(True, False, act, 'layer_norm'), ref)
     report('torch fp32', run(False, False, act), ref)
