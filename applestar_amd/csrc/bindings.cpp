@@ -782,6 +782,100 @@ at::Tensor conv3x3_fwd(const at::Tensor& x, const at::Tensor& wk, const c10::opt
 // dy [R, N] bf16; x [R, K] bf16 (cin == 0) or NHWC [B, H, W, cin] bf16 (3x3 conv, K = 9 cin).
 // Returns (dW fp32 [N, K], db fp32 [N] or undefined); bf16_out: both in bf16, the cast fused into the
 // split reduction (the gradients of bf16 compute parameters under master weights).
+// ---------------------------------------------------------------- fused clip + Adam
+void fused_clip_adam(const at::Tensor& table, const at::Tensor& chunks, const at::Tensor& part,
+                     const c10::optional<at::Tensor>& gate, const at::Tensor& norm_out, double max_norm, double lr_bc1,
+                     double b1, double b2, double inv_sqrt_bc2, double eps, double wd, bool decoupled) {
+  check_cuda(table, "table");
+  TORCH_CHECK(table.scalar_type() == at::kLong && chunks.scalar_type() == at::kLong && table.is_contiguous() &&
+              chunks.is_contiguous() && table.numel() % 6 == 0 && chunks.numel() % 2 == 0, "fused_clip_adam: tables");
+  const int64_t nch = chunks.numel() / 2;
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() >= nch, "fused_clip_adam: part");
+  TORCH_CHECK(norm_out.scalar_type() == at::kFloat && norm_out.numel() >= 1, "fused_clip_adam: norm_out");
+  const float* gp = nullptr;
+  if (gate && gate->defined()) {
+    TORCH_CHECK(gate->scalar_type() == at::kFloat && gate->numel() == 1, "fused_clip_adam: gate fp32 scalar");
+    gp = gate->data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(table.device().index());
+  as::fused_clip_adam(table.data_ptr(), reinterpret_cast<const long*>(chunks.data_ptr<int64_t>()),
+                      static_cast<int>(nch), part.data_ptr<float>(), gp, norm_out.data_ptr<float>(),
+                      static_cast<float>(max_norm), static_cast<float>(lr_bc1), static_cast<float>(b1),
+                      static_cast<float>(b2), static_cast<float>(inv_sqrt_bc2), static_cast<float>(eps),
+                      static_cast<float>(wd), decoupled ? 1 : 0, stream());
+}
+
+// ---------------------------------------------------------------- fp32 conv3x3 / weight gradients
+at::Tensor conv3x3_f32(const at::Tensor& x, const at::Tensor& wk, const c10::optional<at::Tensor>& bias,
+                       const c10::optional<at::Tensor>& res, int64_t act) {
+  check_cuda(x, "x");
+  check_cuda(wk, "w");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && wk.scalar_type() == at::kFloat, "conv3x3_f32: fp32 x / w");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(), "conv3x3_f32: x contiguous NHWC [B, H, W, Cin]");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
+  TORCH_CHECK(wk.dim() == 4 && wk.size(1) == 3 && wk.size(2) == 3 && wk.size(3) == Cin && wk.is_contiguous(),
+              "conv3x3_f32: w contiguous [Cout, 3, 3, Cin]");
+  const int64_t Cout = wk.size(0);
+  TORCH_CHECK(as::conv3x3_f32_supported(static_cast<int>(Cin), static_cast<int>(Cout)), "conv3x3_f32: Cin % 16");
+  TORCH_CHECK(B * H * W * std::max(Cin, Cout) * 4 < 0x7ffffff0LL && Cout * 9 * Cin * 4 < 0x7ffffff0LL,
+              "conv3x3_f32: tensor too large for 32-bit buffer offsets");
+  const float* bp = nullptr;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == Cout && bias->is_contiguous(), "conv3x3_f32: bias");
+    bp = bias->data_ptr<float>();
+  }
+  const float* rp = nullptr;
+  if (res && res->defined()) {
+    TORCH_CHECK(res->scalar_type() == at::kFloat && res->dim() == 4 && res->size(0) == B && res->size(1) == H &&
+                res->size(2) == W && res->size(3) == Cout && res->is_contiguous(), "conv3x3_f32: residual NHWC");
+    rp = res->data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(x.device().index());
+  auto out = at::empty({B, H, W, Cout}, x.options());
+  as::conv3x3_f32_fwd(x.data_ptr<float>(), wk.data_ptr<float>(), bp, rp, out.data_ptr<float>(), static_cast<int>(B),
+                      static_cast<int>(H), static_cast<int>(W), static_cast<int>(Cin), static_cast<int>(Cout),
+                      static_cast<int>(act), stream());
+  return out;
+}
+
+std::vector<at::Tensor> wgrad_f32(const at::Tensor& dy, const at::Tensor& x, int64_t cin, bool want_bias) {
+  check_cuda(dy, "dy");
+  check_cuda(x, "x");
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat, "wgrad_f32: fp32 dy / x");
+  TORCH_CHECK(dy.dim() == 2 && dy.is_contiguous() && x.is_contiguous(), "wgrad_f32: contiguous dy [R, N], x");
+  const int64_t R = dy.size(0), N = dy.size(1);
+  int64_t K, H = 1, W = 1;
+  if (cin > 0) {
+    TORCH_CHECK(x.dim() == 4 && x.size(3) == cin && x.size(0) * x.size(1) * x.size(2) == R, "wgrad_f32: x NHWC");
+    H = x.size(1);
+    W = x.size(2);
+    K = 9 * cin;
+    TORCH_CHECK(cin % 4 == 0, "wgrad_f32: Cin % 4");
+  } else {
+    TORCH_CHECK(x.dim() == 2 && x.size(0) == R, "wgrad_f32: x [R, K]");
+    K = x.size(1);
+  }
+  TORCH_CHECK(N % 4 == 0 && K % 4 == 0, "wgrad_f32: N and K must be multiples of 4");
+  TORCH_CHECK(R * N * 4 < 0x7ffffff0LL && x.numel() * 4 < 0x7ffffff0LL, "wgrad_f32: tensor too large");
+  c10::hip::HIPGuard g(dy.device().index());
+  auto opts = dy.options();
+  if (R == 0) return {at::zeros({N, K}, opts), want_bias ? at::zeros({N}, opts) : at::Tensor()};
+  const int S = as::wgrad_f32_splits(R, static_cast<int>(N), static_cast<int>(K));
+  const int64_t NK = N * K, stride = NK + (want_bias ? N : 0);
+  auto part = at::empty({S, stride}, opts);
+  as::wgrad_f32(dy.data_ptr<float>(), x.data_ptr<float>(), part.data_ptr<float>(),
+                want_bias ? part.data_ptr<float>() + NK : nullptr, stride, R, static_cast<int>(N), static_cast<int>(K),
+                static_cast<int>(H), static_cast<int>(W), static_cast<int>(cin), S, stream());
+  at::Tensor flat;
+  if (S == 1) {
+    flat = part.view({stride});
+  } else {
+    flat = at::empty({stride}, opts);
+    as::column_reduce(part.data_ptr<float>(), flat.data_ptr<float>(), S, static_cast<int>(stride), stream());
+  }
+  return {flat.narrow(0, 0, NK).view({N, K}), want_bias ? flat.narrow(0, NK, N) : at::Tensor()};
+}
+
 std::vector<at::Tensor> wgrad(const at::Tensor& dy, const at::Tensor& x, int64_t cin, bool want_bias, bool bf16_out) {
   check_cuda(dy, "dy");
   check_cuda(x, "x");
@@ -1474,6 +1568,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("varlen_attn_fwd", &varlen_attn_fwd);
   m.def("varlen_attn_bwd", &varlen_attn_bwd);
   m.def("varlen_attn_fwd_f32", &varlen_attn_fwd_f32);
+  m.def("conv3x3_f32", &conv3x3_f32);
+  m.def("fused_clip_adam", &fused_clip_adam);
+  m.def("fused_adam_chunk", &as::fused_adam_chunk);
+  m.def("wgrad_f32", &wgrad_f32);
+  m.def("conv3x3_f32_supported", &as::conv3x3_f32_supported);
   m.def("varlen_attn_bwd_f32", &varlen_attn_bwd_f32);
   m.def("su_sample", &su_sample);
   m.def("segment_copy", &segment_copy);

@@ -217,6 +217,22 @@ bool conv3x3_supported(int Cin, int Cout);
 void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* res, void* out, int B, int H, int W,
                  int Cin, int Cout, int act, hipStream_t s);
 
+// ---- conv3x3_f32.hip / wgrad_f32.hip: the fp32 learner step's convolutions and weight gradients (f32 MFMA) --
+bool conv3x3_f32_supported(int Cin, int Cout);
+void conv3x3_f32_fwd(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H,
+                     int W, int Cin, int Cout, int act, hipStream_t s);
+int wgrad_f32_splits(long R, int N, int K);
+// slice s writes dW at part + s * part_stride ([N][K]) and db at db_part + s * part_stride ([N])
+void wgrad_f32(const float* dy, const float* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
+               int H, int W, int Cin, int S, hipStream_t st);
+
+// ---- optim.hip: fused pytorch_norm clip + Adam over a (tensor, offset) chunk table ----------------------
+int fused_adam_chunk();
+// table: per tensor {p, g, m, v, numel, 0} (int64 x 6); chunks: per chunk {tensor, offset} (int64 x 2)
+void fused_clip_adam(const void* table, const long* chunks, int nchunks, float* part, const float* gate, float* norm_out,
+                     float max_norm, float lr_bc1, float b1, float b2, float inv_sqrt_bc2, float eps, float wd,
+                     int decoupled, hipStream_t s);
+
 // ---- wgrad.hip ---------------------------------------------------------------------------------
 // dw_part [S, N, K] / db_part [S, N] fp32 partials of dW = dY^T X(r, k), db = sum_r dY; dy [R, N] bf16.
 // Cin == 0: x [R, K] bf16 (dense).  Cin > 0: x NHWC [R / (H W), H, W, Cin] bf16, K = 9 Cin (3x3 pad-1 conv).

@@ -1,0 +1,223 @@
+// 3x3 / stride 1 / pad 1 convolution in fp32 (the fp32 learner step, like-for-like with the reference's fp32
+// convolutions: spatial_encoder.py:74-86, res_block.py:50-65, action_arg_head.py:417-446), NHWC, on the
+// exact-f32 MFMA v_mfma_f32_32x32x2_f32 (gfx950 has no xf32/TF32 mode), with bias / residual / ReLU (and the
+// input-gradient form's ReLU mask) fused into the epilogue.
+//
+//   out[m, n] = act( bias[n] + res[m, n] + sum_{tap, c} x[shift_tap(m), c] * w[n, tap, c] )
+//
+// Implicit GEMM as the bf16 kernel (conv3x3.hip): M = B*H*W output pixels, N = Cout, K = 9*Cin tap-major
+// (the memory order of a channels_last [Cout, Cin, 3, 3] weight).  K-step = one tap x 16 input channels:
+// the A tile is 128 pixels x 16 channels gathered from the shifted pixels (one 16-B buffer load per 4
+// channels; taps outside the image read zeros through the buffer range check), the B tile BN x 16 weight
+// rows.  Register-staged double buffer, one barrier per K-step.
+//
+// 32x32x2 f32 MFMA: lane l holds A[row l&31][k l>>5] and B[k l>>5][col l&31] (one f32 each), C[row (r&3) +
+// 8(r>>2) + 4(l>>5)][col l&31] in 16 accumulators.  The k-slot assignment is free as long as A and B agree:
+// k-step kk of a 16-channel K-step gives lane half h channel 8h + kk, so a lane's 8 k-steps of a fragment are
+// 8 consecutive floats of one LDS row (two ds_read_b128).  LDS rows are 20 floats: 20 = 4 mod 16, the 16
+// rows read by a 16-lane group land on 16 distinct 4-bank groups.  The epilogue stores straight from the
+// accumulators: 32 lanes write 32 consecutive channels (128 B) of one pixel.
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f16v;
+
+constexpr int kOOB = 0x7ffffff0;
+
+template <int BN_>
+struct ConvF32Cfg {
+  static constexpr int BM = 128, BN = BN_, BK = 16, NT = 256;
+  static constexpr int WN = BN_ >= 128 ? 2 : 1;   // waves along N
+  static constexpr int WM = 4 / WN;                // waves along M
+  static constexpr int TM = BM / WM, TN = BN / WN; // wave tile
+  static constexpr int FM = TM / 32, FN = TN / 32; // 32x32 MFMA tiles per wave
+  static constexpr int P = BK + 4;                 // LDS row pitch (floats)
+  static constexpr int A_IT = BM * (BK / 4) / NT;  // 16-B pieces per thread
+  static constexpr int B_PIECES = BN * (BK / 4);
+  static constexpr int B_IT = (B_PIECES + NT - 1) / NT;
+  static constexpr int STAGE = (BM + BN) * P;      // floats
+  static_assert(A_IT * NT == BM * (BK / 4), "A tile pieces");
+};
+
+template <int BN>
+__global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ bias,
+                                                          const float* __restrict__ res, float* __restrict__ out,
+                                                          int B, int H, int W, int Cin, int Cout, int act) {
+  using C = ConvF32Cfg<BN>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * C::STAGE];
+
+  const int HW = H * W;
+  const long M = static_cast<long>(B) * HW;
+  const int K = 9 * Cin;
+  const int ntn = (Cout + BN - 1) / BN;
+  // XCD-aware bijective remap (8 XCDs, round-robin dispatch): consecutive M-tiles share input halo rows
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int tn = wg % ntn;
+  const long m0 = static_cast<long>(wg / ntn) * C::BM;
+  const int n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int l32 = lane & 31, h = lane >> 5;
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(x), 0, static_cast<int>(M * Cin * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(w), 0, static_cast<int>(static_cast<long>(Cout) * K * 4), 0x00020000);
+
+  // A pieces: row = pixel of the tile, ch4 = which 4-channel group of the 16-channel K-step
+  int a_pix[C::A_IT], a_row[C::A_IT], a_c4[C::A_IT], a_ok[C::A_IT];
+#pragma unroll
+  for (int i = 0; i < C::A_IT; ++i) {
+    const int idx = tid + i * C::NT;
+    a_row[i] = idx >> 2;
+    a_c4[i] = idx & 3;
+    const long m = m0 + a_row[i];
+    a_pix[i] = static_cast<int>(m);
+    a_ok[i] = 0;
+    if (m < M) {
+      const int rem = static_cast<int>(m % HW);
+      const int yy = rem / W, xx = rem - yy * W;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int y2 = yy + t / 3 - 1, x2 = xx + t % 3 - 1;
+        a_ok[i] |= (y2 >= 0 && y2 < H && x2 >= 0 && x2 < W) << t;
+      }
+    }
+  }
+  int b_off[C::B_IT];
+#pragma unroll
+  for (int i = 0; i < C::B_IT; ++i) {
+    const int idx = tid + i * C::NT;
+    const int n = idx >> 2, c4 = idx & 3;
+    b_off[i] = (idx < C::B_PIECES && n0 + n < Cout) ? ((n0 + n) * K + 4 * c4) * 4 : kOOB;
+  }
+
+  uint4 ra[C::A_IT], rb[C::B_IT];
+  auto load_regs = [&](int kt) {
+    const int k0 = kt * C::BK;
+    const int tap = k0 / Cin, c0 = k0 - tap * Cin;
+    const int shift = (tap / 3 - 1) * W + (tap % 3 - 1);
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) {
+      const int off = ((a_ok[i] >> tap) & 1) ? ((a_pix[i] + shift) * Cin + c0 + 4 * a_c4[i]) * 4 : kOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const int off = b_off[i] == kOOB ? kOOB : b_off[i] + k0 * 4;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0);
+      rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store_lds = [&](int s) {
+    float* A = smem + s * C::STAGE;
+    float* Bs = A + C::BM * C::P;
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) *reinterpret_cast<uint4*>(A + a_row[i] * C::P + 4 * a_c4[i]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const int idx = tid + i * C::NT;
+      if (C::B_PIECES % C::NT == 0 || idx < C::B_PIECES)
+        *reinterpret_cast<uint4*>(Bs + (idx >> 2) * C::P + 4 * (idx & 3)) = rb[i];
+    }
+  };
+
+  f16v acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int KT = K / C::BK;      // Cin % 16 == 0 (host check): every K-step lies inside one tap
+  load_regs(0);
+  store_lds(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) load_regs(kt + 1);
+    const float* A = smem + cur * C::STAGE;
+    const float* Bs = A + C::BM * C::P;
+    float af[C::FM][8], bfr[C::FN][8];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      const float* p = A + (wm * C::TM + 32 * i + l32) * C::P + 8 * h;
+      const float4 u0 = *reinterpret_cast<const float4*>(p), u1 = *reinterpret_cast<const float4*>(p + 4);
+      af[i][0] = u0.x; af[i][1] = u0.y; af[i][2] = u0.z; af[i][3] = u0.w;
+      af[i][4] = u1.x; af[i][5] = u1.y; af[i][6] = u1.z; af[i][7] = u1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+      const float* p = Bs + (wn * C::TN + 32 * j + l32) * C::P + 8 * h;
+      const float4 u0 = *reinterpret_cast<const float4*>(p), u1 = *reinterpret_cast<const float4*>(p + 4);
+      bfr[j][0] = u0.x; bfr[j][1] = u0.y; bfr[j][2] = u0.z; bfr[j][3] = u0.w;
+      bfr[j][4] = u1.x; bfr[j][5] = u1.y; bfr[j][6] = u1.z; bfr[j][7] = u1.w;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
+    if (kt + 1 < KT) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue straight from the accumulators: register e of tile (i, j) is pixel row (e&3) + 8(e>>2) + 4h,
+  // channel l32; lanes 0..31 / 32..63 each write 128 contiguous bytes
+#pragma unroll
+  for (int j = 0; j < C::FN; ++j) {
+    const int n = n0 + wn * C::TN + 32 * j + l32;
+    if (n >= Cout) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const long m = m0 + wm * C::TM + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (m >= M) continue;
+        float v = acc[i][j][e] + bv;
+        if (res) {
+          const float rv = res[m * Cout + n];
+          if (act == ACT_DRELU) v = rv > 0.f ? v : 0.f;
+          else v += rv;
+        }
+        if (act == ACT_RELU) v = fmaxf(v, 0.f);
+        out[m * Cout + n] = v;
+      }
+    }
+  }
+}
+
+template <int BN>
+void launch_f32(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
+                int Cin, int Cout, int act, hipStream_t s) {
+  const long M = static_cast<long>(B) * H * W;
+  const long nwg = (M + 127) / 128 * ((Cout + BN - 1) / BN);
+  if (nwg == 0) return;
+  hipLaunchKernelGGL((conv3x3_f32_kernel<BN>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias, res,
+                     out, B, H, W, Cin, Cout, act);
+}
+
+}  // namespace
+
+bool conv3x3_f32_supported(int Cin, int Cout) { return Cin % 16 == 0 && Cin > 0 && Cout > 0; }
+
+void conv3x3_f32_fwd(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H,
+                     int W, int Cin, int Cout, int act, hipStream_t s) {
+  if (Cout % 128 == 0) launch_f32<128>(x, w, bias, res, out, B, H, W, Cin, Cout, act, s);
+  else if (Cout > 32) launch_f32<64>(x, w, bias, res, out, B, H, W, Cin, Cout, act, s);
+  else launch_f32<32>(x, w, bias, res, out, B, H, W, Cin, Cout, act, s);
+}
+
+}  // namespace as

@@ -1,0 +1,229 @@
+// fp32 weight (and bias) gradients of the tall-skinny GEMMs and 3x3 convolutions of the fp32 learner step, on
+// the exact-f32 MFMA v_mfma_f32_32x32x2_f32.  Same decomposition as the bf16 kernel (wgrad.hip):
+//
+//   dW[n, k] = sum_r dY[r, n] * X(r, k)          db[n] = sum_r dY[r, n]
+//
+// with R = 10^4 .. 10^7 reduction rows split over S slices (grid = N-tiles x K-tiles x S), one fp32 partial
+// per slice, summed afterwards by one deterministic column reduction.  X(r, k) is either dense ([R, K]
+// row-major: nn.Linear, 1x1 conv on NHWC pixels) or the implicit im2col of a pad-1 3x3 conv on an NHWC image
+// (k = tap * Cin + c, zero outside the image): the [Cout, 3, 3, Cin] (channels_last) weight order.
+//
+// Both operands are reduction-major in memory (row r holds all n / all k) and are staged row-major in LDS as
+// loaded.  The 32x32x2 MFMA takes A[i][k] = dY[r][n0 + i] and B[k][j] = X(r, k0 + j) with lane l holding
+// row/column l&31 and reduction slot l>>5; k-step kk of a 32-row stage gives lane half h the row 16h + kk, so
+// each half-wave reads 32 consecutive floats of one LDS row (one conflict-free ds_read_b32 per operand).
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f16v;
+
+constexpr int kOOB = 0x7ffffff0;
+
+template <int BN_, int BK_>
+struct WgF32Cfg {
+  static constexpr int BN = BN_, BK = BK_, BR = 32, NT = 256;
+  static constexpr int TN = BN / 2, TK = BK / 2;     // 2 x 2 waves
+  static constexpr int FN = TN / 32, FK = TK / 32;   // 32x32 tiles per wave
+  static constexpr int PA = BN + 4, PB = BK + 4;     // LDS row pitch (floats)
+  static constexpr int CHA = BN / 4, CHB = BK / 4;   // 16-B pieces per row
+  static constexpr int A_IT = BR * CHA / NT, B_IT = BR * CHB / NT;
+  static constexpr int STAGE = BR * (PA + PB);       // floats
+  static_assert(A_IT * NT == BR * CHA && B_IT * NT == BR * CHB, "tile / thread mismatch");
+};
+
+template <int BN, int BK, bool CONV>
+__global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                        float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                        long part_stride, long R, int N, int K, int H, int W, int Cin,
+                                                        long rows_per_split, int tiles_n, int tiles_k) {
+  using C = WgF32Cfg<BN, BK>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * C::STAGE];
+
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tk = wg % tiles_k;
+  const int tn = (wg / tiles_k) % tiles_n;
+  const int s = wg / (tiles_k * tiles_n);
+  const int n0 = tn * BN, k0 = tk * BK;
+  const long r_begin = static_cast<long>(s) * rows_per_split;
+  const long r_end = r_begin + rows_per_split < R ? r_begin + rows_per_split : R;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wn = wid >> 1, wk = wid & 1;
+  const int l32 = lane & 31, h = lane >> 5;
+  const long HW = static_cast<long>(H) * W;
+
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dy), 0,
+                                                                      static_cast<int>(R * N * 4), 0x00020000);
+  const long xbytes = CONV ? R * Cin * 4 : R * K * 4;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0,
+                                                                      static_cast<int>(xbytes), 0x00020000);
+  // per-thread piece columns (fixed across stages): CHA and CHB divide NT
+  const int a_col = n0 + 4 * (tid % C::CHA);
+  const int b_col = k0 + 4 * (tid % C::CHB);
+  int b_c = b_col, b_dy = 0, b_dx = 0;
+  if (CONV) {
+    const int tap = b_col / Cin;
+    b_c = b_col - tap * Cin;
+    b_dy = tap / 3 - 1;
+    b_dx = tap % 3 - 1;
+  }
+  const bool a_ok = a_col < N, b_ok = b_col < K;
+
+  uint4 ra[C::A_IT], rb[C::B_IT];
+  auto load_regs = [&](long rs) {
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) {
+      const long r = rs + (tid + i * C::NT) / C::CHA;
+      const int off = (a_ok && r < r_end) ? static_cast<int>((r * N + a_col) * 4) : kOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0);
+      ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const long r = rs + (tid + i * C::NT) / C::CHB;
+      int off = kOOB;
+      if (b_ok && r < r_end) {
+        if (CONV) {
+          const int rem = static_cast<int>(r % HW);
+          const int yy = rem / W + b_dy, xx = rem % W + b_dx;
+          if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+            off = static_cast<int>(((r + b_dy * W + b_dx) * Cin + b_c) * 4);
+        } else {
+          off = static_cast<int>((r * K + b_col) * 4);
+        }
+      }
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store_lds = [&](int st) {
+    float* A = smem + st * C::STAGE;
+    float* Bt = A + C::BR * C::PA;
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) {
+      const int idx = tid + i * C::NT;
+      *reinterpret_cast<uint4*>(A + (idx / C::CHA) * C::PA + 4 * (idx % C::CHA)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const int idx = tid + i * C::NT;
+      *reinterpret_cast<uint4*>(Bt + (idx / C::CHB) * C::PB + 4 * (idx % C::CHB)) = rb[i];
+    }
+  };
+
+  f16v acc[C::FN][C::FK];
+#pragma unroll
+  for (int i = 0; i < C::FN; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FK; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const bool do_bias = db_part != nullptr && tk == 0 && wk == 0;
+  float bsum[C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FN; ++i) bsum[i] = 0.f;
+
+  const long nsteps = r_end > r_begin ? (r_end - r_begin + C::BR - 1) / C::BR : 0;
+  if (nsteps > 0) {
+    load_regs(r_begin);
+    store_lds(0);
+    __syncthreads();
+  }
+  for (long it = 0; it < nsteps; ++it) {
+    const int cur = static_cast<int>(it & 1);
+    if (it + 1 < nsteps) load_regs(r_begin + (it + 1) * C::BR);
+    const float* A = smem + cur * C::STAGE + (16 * h) * C::PA + wn * C::TN + l32;
+    const float* Bt = smem + cur * C::STAGE + C::BR * C::PA + (16 * h) * C::PB + wk * C::TK + l32;
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      float af[C::FN], bfr[C::FK];
+#pragma unroll
+      for (int i = 0; i < C::FN; ++i) af[i] = A[kk * C::PA + 32 * i];
+#pragma unroll
+      for (int j = 0; j < C::FK; ++j) bfr[j] = Bt[kk * C::PB + 32 * j];
+#pragma unroll
+      for (int i = 0; i < C::FN; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FK; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < C::FN; ++i) bsum[i] += af[i];
+      }
+    }
+    if (it + 1 < nsteps) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+
+  // accumulator (i, j) register e: n = n0 + wn TN + 32 i + (e&3) + 8 (e>>2) + 4 h, k = k0 + wk TK + 32 j + l32:
+  // 32 lanes store 128 contiguous bytes of one dW row
+  float* outp = dw_part + static_cast<long>(s) * part_stride;
+#pragma unroll
+  for (int i = 0; i < C::FN; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FK; ++j) {
+      const int k = k0 + wk * C::TK + 32 * j + l32;
+      if (k >= K) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int n = n0 + wn * C::TN + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (n < N) outp[static_cast<long>(n) * K + k] = acc[i][j][e];
+      }
+    }
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < C::FN; ++i) {
+      const float v = bsum[i] + __shfl_xor(bsum[i], 32, kWave);
+      const int n = n0 + wn * C::TN + 32 * i + l32;
+      if (h == 0 && n < N) db_part[static_cast<long>(s) * part_stride + n] = v;
+    }
+  }
+}
+
+template <int BN, int BK, bool CONV>
+void launch(const float* dy, const float* x, float* dwp, float* dbp, long ps, long R, int N, int K, int H, int W,
+            int Cin, int S, long rps, hipStream_t st) {
+  const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
+  const long nwg = static_cast<long>(tn) * tk * S;
+  hipLaunchKernelGGL((wgrad_f32_kernel<BN, BK, CONV>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x, dwp,
+                     dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
+}
+
+int pick(int n) { return n <= 64 ? 64 : 128; }
+
+}  // namespace
+
+int wgrad_f32_splits(long R, int N, int K) {
+  const long tiles = static_cast<long>((N + pick(N) - 1) / pick(N)) * ((K + pick(K) - 1) / pick(K));
+  long S = (1024 + tiles - 1) / tiles;                   // ~1024 workgroups
+  const long max_s = R < 2048 ? 1 : (R + 127) / 128;     // >= 4 stages per slice
+  if (S > max_s) S = max_s;
+  const long max_part = (16L << 20) / (static_cast<long>(N) * K);   // partials <= 64 MB
+  if (S > max_part) S = max_part;
+  if (S < 1) S = 1;
+  if (S > 4096) S = 4096;
+  return static_cast<int>(S);
+}
+
+void wgrad_f32(const float* dy, const float* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
+               int H, int W, int Cin, int S, hipStream_t st) {
+  long rps = (R + S - 1) / S;
+  rps = (rps + 31) / 32 * 32;
+  const bool conv = Cin > 0;
+  const int bn = pick(N), bk = pick(K);
+#define AS_WGF(BNv, BKv)                                                                   \
+  if (bn == BNv && bk == BKv) {                                                            \
+    if (conv) launch<BNv, BKv, true>(dy, x, dw_part, db_part, part_stride, R, N, K, H, W, Cin, S, rps, st); \
+    else launch<BNv, BKv, false>(dy, x, dw_part, db_part, part_stride, R, N, K, H, W, Cin, S, rps, st);     \
+    return;                                                                                \
+  }
+  AS_WGF(128, 128) AS_WGF(128, 64) AS_WGF(64, 128) AS_WGF(64, 64)
+#undef AS_WGF
+}
+
+}  // namespace as

@@ -207,7 +207,7 @@ def lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b
     x2 = x.reshape(T * B, -1)
     # bf16 input projection through linear(): its dW takes the split-R MFMA kernel, not a library GEMM that
     # tiles only the 4H x I output over T*B = 24576 rows (the selected-units head's LSTM)
-    xg = linear(x2, w_ih) if (x2.dtype == torch.bfloat16 and w_ih.dtype == torch.bfloat16) else \
+    xg = linear(x2, w_ih) if x2.dtype == w_ih.dtype and x2.dtype in (torch.bfloat16, torch.float32) else \
         torch.nn.functional.linear(x2, w_ih)
     xp = layer_norm(xg, lni_w, lni_b, out_dtype=torch.float32).view(T, B, 4 * H)
     w_dtype = torch.bfloat16 if torch.is_autocast_enabled() else torch.float32
@@ -583,6 +583,32 @@ def gather_rows(table, idx):
     return _GatherRows.apply(table, idx.long().contiguous())
 
 
+# ---------------------------------------------------------------------------- dtype-generic conv / GEMM pieces
+# Every conv / linear autograd node below runs on bf16 operands (the mixed-precision step: bf16 MFMA kernels) or
+# on fp32 operands (the fp32 step: f32-MFMA kernels conv3x3_f32.hip / wgrad_f32.hip); an fp32 operand is never
+# rounded to bf16.
+def _conv3(x, wk, bias, res, act_code):
+    """3x3 / pad 1 conv on NHWC x with a [Cout, 3, 3, Cin] weight, epilogue act code (_ACT / 4 = ReLU mask)."""
+    if x.dtype == torch.float32:
+        return _C.conv3x3_f32(x, wk, bias, res, act_code)
+    return _C.conv3x3_fwd(x, wk, bias, res, act_code)
+
+
+def _act_grad(dout, out, relu):
+    """dout * (out > 0) (relu) or dout, as a contiguous tensor of out's shape and dtype (one pass)."""
+    if out.dtype == torch.bfloat16:
+        return _C.act_grad_nhwc(dout, out, relu)
+    dout = dout.to(out.dtype).contiguous()
+    return torch.ops.aten.threshold_backward(dout, out, 0.0) if relu else dout
+
+
+def _wgrad(dy2d, x, cin, has_b, bf16_out):
+    """(dW, db) of a dense GEMM (cin == 0, x [R, K]) or a 3x3 conv (x NHWC image, Cin = cin) in dy's precision."""
+    if dy2d.dtype == torch.float32:
+        return _C.wgrad_f32(dy2d, x, cin, has_b)
+    return _C.wgrad(dy2d, x, cin, has_b, bf16_out)
+
+
 # ---------------------------------------------------------------------------- conv3x3 implicit GEMM
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
@@ -591,7 +617,7 @@ class _Conv3x3(torch.autograd.Function):
         if not wk.is_contiguous():
             wk = wk.contiguous()
         bias = _w32(b) if b is not None else None
-        out = _C.conv3x3_fwd(x_nhwc, wk, bias, res_nhwc, _ACT[act])
+        out = _conv3(x_nhwc, wk, bias, res_nhwc, _ACT[act])
         ctx.save_for_backward(x_nhwc, w_lp, out)
         ctx.act, ctx.has_res = act, res_nhwc is not None
         ctx.b_dtype = b.dtype if b is not None else None
@@ -600,12 +626,12 @@ class _Conv3x3(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         x, w, out = ctx.saved_tensors
-        dpre = _C.act_grad_nhwc(dout, out, ctx.act == 'relu')    # one pass: mask + cast + NHWC
-        dx = _C.conv3x3_fwd(dpre, _conv_wt(w), None, None, 0)
+        dpre = _act_grad(dout, out, ctx.act == 'relu')    # one pass: mask + cast + NHWC
+        dx = _conv3(dpre, _conv_wt(w), None, None, 0)
         has_b = ctx.b_dtype is not None
         cout, cin = w.shape[0], w.shape[1]
         bf = _bf16_grads(w.dtype, ctx.b_dtype)
-        dw, db = _C.wgrad(dpre.view(-1, cout), x, cin, has_b, bf)   # dW in [Cout,3,3,Cin] (channels_last) order
+        dw, db = _wgrad(dpre.view(-1, cout), x, cin, has_b, bf)   # dW in [Cout,3,3,Cin] (channels_last) order
         dw = dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype)
         return (dx, dw, db.to(ctx.b_dtype) if has_b else None, dpre if ctx.has_res else None, None)
 
@@ -617,11 +643,12 @@ def _conv_w(w):
 
 
 def _conv_wt(w):
-    """flipped, transposed weight [Cin,3,3,Cout] for the input gradient (a derived form: rebuilt once per
-    optimizer step for parameters).  Only bf16 weights reach the native conv (conv3x3_fwd rejects others),
-    so there is no fp32 branch to keep untested."""
+    """flipped, transposed weight [Cin,3,3,Cout] for the input gradient (bf16: a derived form rebuilt once per
+    optimizer step for parameters; fp32: built per call, a few hundred KB)."""
+    if w.dtype == torch.float32:
+        return w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()
     if w.dtype != torch.bfloat16:
-        raise TypeError(f'native conv3x3 backward needs bf16 weights, got {w.dtype}')
+        raise TypeError(f'native conv3x3 backward needs bf16 or fp32 weights, got {w.dtype}')
 
     def make():
         s0, s1, s2, s3 = w.stride()
@@ -724,15 +751,15 @@ def _conv_dx_drelu(dpre, w, y):
     """Input gradient of a 3x3 conv whose input y is a ReLU output, already gated by (y > 0): the gate
     is the dX conv's epilogue mode 4 (no separate read-modify-write pass over the activation)."""
     if FUSED_DRELU:
-        return _C.conv3x3_fwd(dpre, _conv_wt(w), None, y, 4)
-    return _C.act_grad_nhwc(_C.conv3x3_fwd(dpre, _conv_wt(w), None, None, 0), y, True)
+        return _conv3(dpre, _conv_wt(w), None, y, 4)
+    return _act_grad(_conv3(dpre, _conv_wt(w), None, None, 0), y, True)
 
 
 def _conv_dw(dpre, x, w, b_dtype):
     """dW (in w's dtype) and db of a 3x3 conv; callers cast db to b_dtype (a no-op when both are bf16:
     the cast is then fused into the split reduction)."""
     cout, cin = w.shape[0], w.shape[1]
-    dw, db = _C.wgrad(dpre.view(-1, cout), x, cin, b_dtype is not None, _bf16_grads(w.dtype, b_dtype))
+    dw, db = _wgrad(dpre.view(-1, cout), x, cin, b_dtype is not None, _bf16_grads(w.dtype, b_dtype))
     return dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype), db
 
 
@@ -743,8 +770,8 @@ class _ResBlock(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2):
-        y1 = _C.conv3x3_fwd(x, _conv_w(w1), _w32(b1), None, 1)
-        out = _C.conv3x3_fwd(y1, _conv_w(w2), _w32(b2), x, 1)
+        y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1)
+        out = _conv3(y1, _conv_w(w2), _w32(b2), x, 1)
         ctx.save_for_backward(x, w1, w2, y1, out)
         ctx.b_dtypes = (b1.dtype, b2.dtype)
         return out
@@ -752,20 +779,29 @@ class _ResBlock(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         x, w1, w2, y1, out = ctx.saved_tensors
-        dpre2 = _C.act_grad_nhwc(dout, out, True)
+        dpre2 = _act_grad(dout, out, True)
         dpre1 = _conv_dx_drelu(dpre2, w2, y1)
         dw2, db2 = _conv_dw(dpre2, y1, w2, ctx.b_dtypes[1])
-        dx = _C.conv3x3_fwd(dpre1, _conv_wt(w1), None, dpre2, 0)       # + skip gradient, fused
+        dx = _conv3(dpre1, _conv_wt(w1), None, dpre2, 0)       # + skip gradient, fused
         dw1, db1 = _conv_dw(dpre1, x, w1, ctx.b_dtypes[0])
         return dx, dw1, db1.to(ctx.b_dtypes[0]), dw2, db2.to(ctx.b_dtypes[1])
+
+
+def _f32_conv_ok(x, w, cin, cout):
+    """fp32 step (fp32 operands, no autocast) and a shape the f32-MFMA conv takes in both directions."""
+    return x.dtype == torch.float32 and w.dtype == torch.float32 and not torch.is_autocast_enabled() and \
+        _C.conv3x3_f32_supported(cin, cout) and _C.conv3x3_f32_supported(cout, cin)
 
 
 def resblock(x, w1, b1, w2, b2):
     """Native fused ResBlock; None when the shapes / dtypes are not covered (caller falls back)."""
     C = x.shape[1]
+    if x.dim() != 4 or b1 is None or b2 is None or tuple(w1.shape) != (C, C, 3, 3) or tuple(w2.shape) != (C, C, 3, 3):
+        return None
+    if _f32_conv_ok(x, w1, C, C):
+        return from_nhwc(_ResBlock.apply(nhwc(x), w1, b1, w2, b2))
     lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
-    if x.dim() != 4 or not lowp or b1 is None or b2 is None or not _C.conv3x3_supported(C, C) or \
-            tuple(w1.shape) != (C, C, 3, 3) or tuple(w2.shape) != (C, C, 3, 3):
+    if not lowp or not _C.conv3x3_supported(C, C):
         return None
     xl = nhwc(x.to(torch.bfloat16))
     w1l = w1 if w1.dtype == torch.bfloat16 else _CastWeight.apply(w1)
@@ -790,11 +826,11 @@ class _GatedResBlock(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, sp, w1, b1, w2, b2, *gate):
         B, H, W, C = x.shape
-        y1 = _C.conv3x3_fwd(x, _conv_w(w1), _w32(b1), None, 1)
-        y = _C.conv3x3_fwd(y1, _conv_w(w2), _w32(b2), None, 0)
+        y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1)
+        y = _conv3(y1, _conv_w(w2), _w32(b2), None, 0)
         h = x.view(-1, C)
         acts = [h]
-        if GATE_CHAIN and C == 128:
+        if GATE_CHAIN and C == 128 and x.dtype == torch.bfloat16:
             # the four gate layers in one launch, activation tile resident in LDS (gate_chain.hip)
             acts += _C.gate_chain(h, [gate[2 * i].detach().view(C, C) for i in range(4)],
                                   [_w32(gate[2 * i + 1]) for i in range(4)],
@@ -820,28 +856,28 @@ class _GatedResBlock(torch.autograd.Function):
         d = dg.view(-1, C)
         acts_in = [x.view(-1, C), a1, a2, a3]
         gws = [gw1, gw2, gw3, gw4]
-        if GATE_CHAIN and C == 128:
+        if GATE_CHAIN and C == 128 and x.dtype == torch.bfloat16:
             # d3, d2, d1 and the gate-path input gradient (+ the skip gradient) in one launch; the weight
             # gradients from the saved layer inputs and these
             d3, d2, d1, dx_gate = _C.gate_chain(d, [_wT(gws[i]) for i in (3, 2, 1, 0)],
                                                 [None] * 4, [a3, a2, a1, None], [None, None, None, dx_res.view(-1, C)],
                                                 0)
             for i, di in ((3, d), (2, d3), (1, d2), (0, d1)):
-                dw_i, db_i = _C.wgrad(di, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
+                dw_i, db_i = _wgrad(di, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
                 grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
         else:
             for i in (3, 2, 1, 0):
-                dw_i, db_i = _C.wgrad(d, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
+                dw_i, db_i = _wgrad(d, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
                 grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
                 if i > 0:
                     dh = torch.mm(d, gws[i].view(C, C))
                     P = dh.shape[0]
-                    d = _C.act_grad_nhwc(dh.view(1, 1, P, C), acts_in[i].view(1, 1, P, C), True).view(P, C)
+                    d = _act_grad(dh.view(1, 1, P, C), acts_in[i].view(1, 1, P, C), True).view(P, C)
             dx_gate = torch.addmm(dx_res.view(-1, C), d, gw1.view(C, C))      # skip + G1 input gradients
         # conv path
         dpre1 = _conv_dx_drelu(dy, w2, y1)
         dw2, db2 = _conv_dw(dy, y1, w2, ctx.dtypes[1])
-        dx = _C.conv3x3_fwd(dpre1, _conv_wt(w1), None, dx_gate.view(B, H, W, C).contiguous(), 0)
+        dx = _conv3(dpre1, _conv_wt(w1), None, dx_gate.view(B, H, W, C).contiguous(), 0)
         dw1, db1 = _conv_dw(dpre1, x, w1, ctx.dtypes[0])
         gate_grads = [None] * 8
         for i, dw_i, db_i in grads_g:
@@ -852,13 +888,15 @@ class _GatedResBlock(torch.autograd.Function):
 def gated_resblock(x, conv1, conv2, gates, sp):
     """Fused GatedResBlock (see _GatedResBlock); None when not covered (caller falls back)."""
     C = x.shape[1]
-    lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
-    if x.dim() != 4 or not lowp or not _C.conv3x3_supported(C, C) or C % 8:
-        return None
     ws = [conv1.weight, conv1.bias, conv2.weight, conv2.bias]
     for gc in gates:
         ws += [gc.weight, gc.bias]
-    if any(t is None for t in ws):
+    if x.dim() != 4 or any(t is None for t in ws) or C % 8:
+        return None
+    if _f32_conv_ok(x, conv1.weight, C, C) and all(t.dtype == torch.float32 for t in ws):
+        return from_nhwc(_GatedResBlock.apply(nhwc(x), sp.float(), *ws))
+    lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
+    if not lowp or not _C.conv3x3_supported(C, C):
         return None
     # conv / GEMM weights and the GEMM biases in bf16 (the per-op path's casts); the conv biases stay as
     # given: the conv epilogue adds them in fp32
@@ -891,6 +929,10 @@ def conv2d(x, w, b, stride, padding, act, residual):
     kh, kw = w.shape[2], w.shape[3]
     cout, cin = w.shape[0], w.shape[1]
     lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
+    if kh == 3 and kw == 3 and padding == 1 and _f32_conv_ok(x, w, cin, cout) and \
+            (residual is None or residual.dtype == torch.float32):
+        rl = nhwc(residual) if residual is not None else None
+        return from_nhwc(_Conv3x3.apply(nhwc(x), w, b, rl, act))
     if kh == 3 and kw == 3 and padding == 1 and lowp and _C.conv3x3_supported(cin, cout) \
             and _C.conv3x3_supported(cout, cin):
         xl = nhwc(x.to(torch.bfloat16))
@@ -1128,10 +1170,10 @@ class _Linear(torch.autograd.Function):
         x2, w, y = ctx.saved_tensors
         if ctx.relu:
             R, N = y.shape
-            dy = _C.act_grad_nhwc(dy.view(1, 1, R, N) if dy.is_contiguous() else dy.contiguous().view(1, 1, R, N),
-                                  y.view(1, 1, R, N), True).view(R, N)
+            dy = _act_grad(dy.view(1, 1, R, N) if dy.is_contiguous() else dy.contiguous().view(1, 1, R, N),
+                           y.view(1, 1, R, N), True).view(R, N)
         else:
-            dy = dy.to(torch.bfloat16).contiguous()
+            dy = dy.to(x2.dtype).contiguous()
         dx = None
         g = None
         if ctx.link is not None:
@@ -1145,7 +1187,7 @@ class _Linear(torch.autograd.Function):
             wt = _wT(w).t() if GEMM_REFORM and dy.shape[0] * w.shape[1] >= (1 << 22) else w
             dx = g.view(dy.shape[0], w.shape[1]).addmm_(dy, wt)
         elif ctx.needs_input_grad[0]:
-            if dy.shape[1] == 32 and x2.shape[1] % 16 == 0 and dy.is_contiguous():
+            if dy.shape[1] == 32 and x2.shape[1] % 16 == 0 and dy.is_contiguous() and dy.dtype == torch.bfloat16:
                 # thin-K product (the heads' 256 -> 32 key projections): one MFMA per output tile, a pure
                 # store stream (gemm_k32.hip); the library took 0.19 ms per 196k-row call
                 dx = _C.mm_k32(dy, _wT(w))
@@ -1157,7 +1199,7 @@ class _Linear(torch.autograd.Function):
             else:
                 dx = torch.mm(dy, w)
         has_b = ctx.b_dtype is not None
-        dw, db = _C.wgrad(dy, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
+        dw, db = _wgrad(dy, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
         return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None), None, None
 
 
@@ -1273,6 +1315,13 @@ def linear(x, w, b=None, act=None, grad_link=None):
             wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
             bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
             y = _SmallLinear.apply(xb, wb, bb, act == 'relu')
+        return y.view(*x.shape[:-1], N)
+    if not lowp and x.dtype == torch.float32 and w.dtype == torch.float32 and x.is_cuda and \
+            R >= _WGRAD_MIN_ROWS and N % 4 == 0 and K % 4 == 0 and R * max(N, K) * 4 < 0x7ffffff0 and \
+            act in (None, 'relu') and (b is None or b.dtype == torch.float32):
+        # fp32 step: library fp32 GEMMs forward / dX (exact f32 on gfx950), dW / db on the f32-MFMA split-R kernel
+        ensure_loaded()
+        y = _Linear.apply(x.reshape(R, K).contiguous(), w, b, act == 'relu', None)
         return y.view(*x.shape[:-1], N)
     if not lowp or R < _WGRAD_MIN_ROWS or N % 8 or K % 8 or R * max(N, K) * 2 >= 0x7ffffff0 or \
             act not in (None, 'relu'):

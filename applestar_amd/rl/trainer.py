@@ -9,6 +9,7 @@ over RCCL, sync-free logging.
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Dict, Optional
 
 import torch
@@ -51,6 +52,8 @@ def _amp(device: torch.device, dtype_name: Optional[str]):
     return torch.autocast('cuda', dtype=getattr(torch, dtype_name), cache_enabled=False)
 
 
+FUSED_CLIP_ADAM = os.environ.get('APPLESTAR_FUSED_ADAM', '1') != '0'     # A/B switch
+
 # grad-clip types whose state is all on the device (safe to replay from a graph)
 _GRAPH_SAFE_CLIPS = ('none', 'pytorch_norm', 'clip_norm', 'clip_const')
 
@@ -82,8 +85,8 @@ class RLTrainer:
         else:
             self.reducer = GradientReducer(self.params, bucket_mb=lc.bucket_mb, comm_dtype=comm)
             self.opt_params = self.params
-        self.reset_optimizer()
         self.grad_clip = build_grad_clip(lc.grad_clip)
+        self.reset_optimizer()
         self.loss = ReinforcementLoss(lc, lc.player_id)
         self.iter = 0
         self.remain_value_pretrain = int(lc.get('value_pretrain_iters', -1))
@@ -110,6 +113,14 @@ class RLTrainer:
         self.optimizer = build_optimizer(self.opt_params, lc, betas=(0.0, 0.99), eps=1e-5, device=self.device,
                                          capturable=capturable)
         self.lr_scheduler = None
+        # clip + Adam as two native launches (utils/fused_optim.py) on the eager GPU step; the graph-captured step
+        # keeps torch's capturable Adam (its bias corrections are host floats here)
+        from ..utils.fused_optim import FusedClipAdam
+        self.fused_opt = None
+        if self.device.type == 'cuda' and not capturable and FUSED_CLIP_ADAM and \
+                FusedClipAdam.supported(self.optimizer, self.grad_clip):
+            self.fused_opt = FusedClipAdam(self.optimizer, self.grad_clip.threshold
+                                           if self.grad_clip.clip_type != 'none' else None)
         if getattr(self, 'graph', None) is not None:
             self.graph.reset()
 
@@ -144,8 +155,12 @@ class RLTrainer:
 
     def _update(self) -> torch.Tensor:
         gate = self._lstm_gate()
-        norm = self.grad_clip.apply(self.opt_params, gate=gate)
-        self.optimizer.step()
+        if self.fused_opt is not None:
+            self.grad_clip.step += 1
+            norm = self.fused_opt.step(gate)
+        else:
+            norm = self.grad_clip.apply(self.opt_params, gate=gate)
+            self.optimizer.step()
         if self.master is not None:
             self.master.after_step()
         return norm

@@ -1080,3 +1080,126 @@ def test_value_spatial_proj_pool_matches_unfused(B, H, W):
     assert torch.equal(res[0][0], res[1][0])
     for a, r in zip(res[0][1:], res[1][1:]):
         assert _err(a, r) < 1e-2 * max(1, r.abs().max().item())
+
+
+# ------------------------------------------------------------------ fp32 step kernels (f32 MFMA), vs float64
+def _f64(t):
+    return t.detach().double().cpu().requires_grad_()
+
+
+@pytest.mark.parametrize('cin,cout,H,W,act,res', [(128, 128, 19, 20, 'relu', True), (32, 64, 21, 17, 'relu', False),
+                                                  (64, 128, 10, 12, None, False), (16, 16, 9, 11, 'relu', False),
+                                                  (16, 32, 8, 8, None, True), (128, 64, 5, 7, 'relu', False)])
+def test_conv3x3_f32_matches_fp64(cin, cout, H, W, act, res):
+    """fp32 operands take conv3x3_f32.hip (forward, dX with the flipped weight, split-R dW / db): within fp32
+    rounding of a float64 reference - no bf16 anywhere."""
+    from applestar_amd import ops
+    torch.manual_seed(21)
+    B, cl = 3, torch.channels_last
+    x = torch.randn(B, cin, H, W, device=DEV).contiguous(memory_format=cl).requires_grad_()
+    w = (torch.randn(cout, cin, 3, 3, device=DEV) / (3 * cin ** 0.5)).contiguous(memory_format=cl).requires_grad_()
+    b = (0.1 * torch.randn(cout, device=DEV)).requires_grad_()
+    r = torch.randn(B, cout, H, W, device=DEV).contiguous(memory_format=cl).requires_grad_() if res else None
+    y = ops.conv2d(x, w, b, 1, 1, act=act, residual=r)
+    assert y.dtype == torch.float32
+    xs, ws, bs = _f64(x), _f64(w), _f64(b)
+    rs = _f64(r) if res else None
+    yr = torch.nn.functional.conv2d(xs, ws, bs, 1, 1)
+    if res:
+        yr = yr + rs
+    if act == 'relu':
+        yr = torch.relu(yr)
+    assert _err(y.cpu(), yr) < 1e-5 * max(1.0, yr.abs().max().item())
+    g = torch.randn(yr.shape, dtype=torch.float64)
+    y.backward(g.float().to(DEV).contiguous(memory_format=cl))
+    yr.backward(g)
+    for name, a, ref in (('dx', x.grad, xs.grad), ('dw', w.grad, ws.grad), ('db', b.grad, bs.grad)) + \
+            ((('dres', r.grad, rs.grad),) if res else ()):
+        e = _err(a.cpu(), ref)
+        assert e < 2e-5 * max(1.0, ref.abs().max().item()), (name, e, ref.abs().max().item())
+
+
+@pytest.mark.parametrize('R,N,K', [(4096, 768, 256), (1000, 256, 1024), (390, 128, 48640 // 64), (100003, 32, 16)])
+def test_linear_f32_grads_match_fp64(R, N, K):
+    """The fp32 step's linear (library fp32 GEMMs forward / dX, wgrad_f32.hip dW / db) vs float64."""
+    from applestar_amd.ops import native as NN
+    torch.manual_seed(5)
+    x = torch.randn(R, K, device=DEV).requires_grad_()
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).requires_grad_()
+    b = (0.1 * torch.randn(N, device=DEV)).requires_grad_()
+    y = NN.linear(x, w, b, act='relu')
+    xs, ws, bs = _f64(x), _f64(w), _f64(b)
+    yr = torch.relu(xs @ ws.t() + bs)
+    assert _err(y.cpu(), yr) < 1e-5 * max(1.0, yr.abs().max().item())
+    g = torch.randn(yr.shape, dtype=torch.float64)
+    y.backward(g.float().to(DEV))
+    yr.backward(g)
+    for name, a, ref in (('dx', x.grad, xs.grad), ('dw', w.grad, ws.grad), ('db', b.grad, bs.grad)):
+        e = _err(a.cpu(), ref)
+        assert e < 2e-5 * max(1.0, ref.abs().max().item()), (name, e)
+
+
+@pytest.mark.parametrize('gated', [False, True])
+def test_fused_resblocks_f32_match_torch_fp64(gated):
+    """The one-node fp32 ResBlock / GatedResBlock (skip gradients fused into the dX conv epilogue) vs the same
+    module on float64 CPU weights (plain PyTorch path)."""
+    import copy
+    from applestar_amd.models.blocks import ResBlock, GatedResBlock
+    torch.manual_seed(8)
+    C, H, W = 128, 19, 20
+    blk = GatedResBlock(C) if gated else ResBlock(C)
+    ref = copy.deepcopy(blk).double()
+    blk = blk.to(DEV).to(memory_format=torch.channels_last)
+    x = torch.randn(2, C, H, W, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_()
+    xr = _f64(x)
+    y = blk(x)
+    yr = ref(xr)
+    assert _err(y.cpu(), yr) < 1e-5 * max(1.0, yr.abs().max().item())
+    g = torch.randn(yr.shape, dtype=torch.float64)
+    y.backward(g.float().to(DEV).contiguous(memory_format=torch.channels_last))
+    yr.backward(g)
+    assert _err(x.grad.cpu(), xr.grad) < 2e-5 * max(1.0, xr.grad.abs().max().item())
+    for (n, p), (_, pr) in zip(blk.named_parameters(), ref.named_parameters()):
+        e = _err(p.grad.cpu(), pr.grad)
+        assert e < 3e-5 * max(1.0, pr.grad.abs().max().item()), (n, e)
+
+
+@pytest.mark.parametrize('max_norm,wd', [(1.0, 0.0), (1e6, 0.0), (1.0, 1e-4)])
+def test_fused_clip_adam_matches_torch(max_norm, wd):
+    """optim.hip (two launches: chunked sum of squares, then clip-scaled Adam) == pytorch_norm clip + torch Adam
+    over 4 steps on tensors of mixed sizes / layouts, sharing the torch optimizer's state tensors."""
+    from applestar_amd.utils.fused_optim import FusedClipAdam
+    from applestar_amd.utils.grad_clip import GradClip
+    torch.manual_seed(3)
+    shapes = [(64, 32, 3, 3), (100003,), (256,), (7, 5), (40000, 33)]
+
+    def make():
+        ps = []
+        for i, s in enumerate(shapes):
+            p = torch.nn.Parameter(torch.randn(*s, device=DEV))
+            if len(s) == 4:
+                p.data = p.data.contiguous(memory_format=torch.channels_last)
+            p.grad = torch.zeros_like(p)
+            ps.append(p)
+        return ps
+    pa, pb = make(), make()
+    for a, b in zip(pa, pb):
+        b.data.copy_(a.data)
+    oa = torch.optim.Adam(pa, lr=1e-3, betas=(0.0, 0.99), eps=1e-5, weight_decay=wd)
+    ob = torch.optim.Adam(pb, lr=1e-3, betas=(0.0, 0.99), eps=1e-5, weight_decay=wd)
+    clip = GradClip('pytorch_norm', max_norm)
+    fused = FusedClipAdam(ob, max_norm)
+    for step in range(4):
+        for a, b in zip(pa, pb):
+            g = torch.randn_like(a) * (step + 1)
+            a.grad.copy_(g)
+            b.grad.copy_(g)
+        na = clip.apply(pa)
+        oa.step()
+        nb = fused.step()
+        assert abs(float(na) - float(nb)) <= 1e-5 * float(na)
+        for a, b in zip(pa, pb):
+            assert _err(a, b) < 1e-6 * max(1.0, a.abs().max().item()), step
+    for a, b in zip(pa, pb):
+        assert torch.allclose(oa.state[a]['exp_avg_sq'], ob.state[b]['exp_avg_sq'], rtol=1e-5, atol=1e-12)
+        assert float(oa.state[a]['step']) == float(ob.state[b]['step']) == 4.0

@@ -46,7 +46,8 @@ def main():
         print(f'  {d / K:8.2f} ms {100 * d / K / tot:5.1f}%  {n / K:6.0f} launches  {f}')
     print()
     for name, (d, n) in sorted(per.items(), key=lambda kv: -kv[1][0])[:top]:
-        print(f'{d / K:8.3f} ms/it {n / K:6.1f} calls/it  {re.sub(r"\s+", " ", name)[:160]}')
+        short = re.sub(r'\s+', ' ', name)[:160]
+        print(f'{d / K:8.3f} ms/it {n / K:6.1f} calls/it  {short}')
 
 
 if __name__ == '__main__':
