@@ -838,6 +838,32 @@ at::Tensor conv3x3_f32(const at::Tensor& x, const at::Tensor& wk, const c10::opt
   return out;
 }
 
+at::Tensor gemm_f32(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
+                    const c10::optional<at::Tensor>& res, int64_t act) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  TORCH_CHECK(a.scalar_type() == at::kFloat && b.scalar_type() == at::kFloat && a.dim() == 2 && b.dim() == 2 &&
+              a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1), "gemm_f32: fp32 contiguous A [M,K], B [N,K]");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(K % 4 == 0, "gemm_f32: K % 4");
+  TORCH_CHECK(M * K * 4 < 0x7ffffff0LL && N * K * 4 < 0x7ffffff0LL && M * N < (1LL << 40), "gemm_f32: too large");
+  const float* bp = nullptr;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous(), "gemm_f32: bias");
+    bp = bias->data_ptr<float>();
+  }
+  const float* rp = nullptr;
+  if (res && res->defined()) {
+    TORCH_CHECK(res->scalar_type() == at::kFloat && res->numel() == M * N && res->is_contiguous(), "gemm_f32: res");
+    rp = res->data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(a.device().index());
+  auto out = at::empty({M, N}, a.options());
+  as::gemm_f32(a.data_ptr<float>(), b.data_ptr<float>(), bp, rp, out.data_ptr<float>(), M, static_cast<int>(N),
+               static_cast<int>(K), static_cast<int>(act), stream());
+  return out;
+}
+
 std::vector<at::Tensor> wgrad_f32(const at::Tensor& dy, const at::Tensor& x, int64_t cin, bool want_bias) {
   check_cuda(dy, "dy");
   check_cuda(x, "x");
@@ -1572,6 +1598,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fused_clip_adam", &fused_clip_adam);
   m.def("fused_adam_chunk", &as::fused_adam_chunk);
   m.def("wgrad_f32", &wgrad_f32);
+  m.def("gemm_f32", &gemm_f32);
   m.def("conv3x3_f32_supported", &as::conv3x3_f32_supported);
   m.def("varlen_attn_bwd_f32", &varlen_attn_bwd_f32);
   m.def("su_sample", &su_sample);

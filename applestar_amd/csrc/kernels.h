@@ -222,6 +222,9 @@ bool conv3x3_f32_supported(int Cin, int Cout);
 void conv3x3_f32_fwd(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H,
                      int W, int Cin, int Cout, int act, hipStream_t s);
 int wgrad_f32_splits(long R, int N, int K);
+// out [M, N] = epi(A [M, K] . B [N, K]^T): + bias[n]; res added, or (act == ACT_DRELU) a mask res > 0; ReLU
+void gemm_f32(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
+              int act, hipStream_t s);
 // slice s writes dW at part + s * part_stride ([N][K]) and db at db_part + s * part_stride ([N])
 void wgrad_f32(const float* dy, const float* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
                int H, int W, int Cin, int S, hipStream_t st);

@@ -1,0 +1,195 @@
+// fp32 GEMM with a fused epilogue for the fp32 learner step's linears (SURVEY K3/K4 in fp32; the reference's
+// fc_block, distar/ctools/torch_utils/network/nn_module.py:231-270, and the post-LN transformer's projections,
+// distar/agent/default/model/module_utils.py:130-139), on the exact-f32 MFMA v_mfma_f32_32x32x2_f32:
+//
+//   Y[m, n] = epi( sum_k A[m, k] * B[n, k] )      A [M, K] row-major, B [N, K] row-major (nn.Linear weight)
+//   epi(v)  = act( v + bias[n] + res[m, n] )        act: none / ReLU
+//           | (v + bias[n]) * [res[m, n] > 0]       (ACT_DRELU: an input gradient masked by the ReLU output res)
+//
+// Forward Y = act(X W^T + b) takes B = W; the input gradient dX = dY W takes B = W^T (a [K, N] copy), and can
+// add the residual gradient handed over by a closing LayerNorm (GradLink) or apply the previous layer's ReLU
+// mask in the same epilogue - the separate [M, N] elementwise pass of a library GEMM disappears.
+//
+// Tiling as conv3x3_f32.hip (its implicit GEMM with one tap): 128 x BN tile per 256-thread workgroup, K-steps
+// of 16, register-staged LDS double buffer, 20-float LDS rows, k-slot kk of lane half h = column 8h + kk (two
+// ds_read_b128 per fragment and K-step), XCD-aware tile order.  K % 4 == 0; a K tail reads zeros through the
+// buffer range check.
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+typedef __attribute__((ext_vector_type(16))) float f16v;
+
+constexpr int kOOB = 0x7ffffff0;
+
+template <int BN_>
+struct GemmF32Cfg {
+  static constexpr int BM = 128, BN = BN_, BK = 16, NT = 256;
+  static constexpr int WN = BN_ >= 128 ? 2 : 1, WM = 4 / WN;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int FM = TM / 32, FN = TN / 32;
+  static constexpr int P = BK + 4;
+  static constexpr int A_IT = BM * (BK / 4) / NT;
+  static constexpr int B_PIECES = BN * (BK / 4);
+  static constexpr int B_IT = (B_PIECES + NT - 1) / NT;
+  static constexpr int STAGE = (BM + BN) * P;
+};
+
+template <int BN>
+__global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                       const float* __restrict__ bias, const float* __restrict__ res,
+                                                       float* __restrict__ out, long M, int N, int K, int act) {
+  using C = GemmF32Cfg<BN>;
+  __shared__ __attribute__((aligned(16))) float smem[2 * C::STAGE];
+  const int ntn = (N + BN - 1) / BN;
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+  const int tn = wg % ntn;
+  const long m0 = static_cast<long>(wg / ntn) * C::BM;
+  const int n0 = tn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int l32 = lane & 31, h = lane >> 5;
+
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a), 0, static_cast<int>(M * K * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(b), 0, static_cast<int>(static_cast<long>(N) * K * 4), 0x00020000);
+
+  int a_base[C::A_IT], a_row[C::A_IT], a_c4[C::A_IT];
+#pragma unroll
+  for (int i = 0; i < C::A_IT; ++i) {
+    const int idx = tid + i * C::NT;
+    a_row[i] = idx >> 2;
+    a_c4[i] = idx & 3;
+    const long m = m0 + a_row[i];
+    a_base[i] = m < M ? static_cast<int>(m * K) : -1;
+  }
+  int b_base[C::B_IT];
+#pragma unroll
+  for (int i = 0; i < C::B_IT; ++i) {
+    const int idx = tid + i * C::NT;
+    const int n = idx >> 2;
+    b_base[i] = (idx < C::B_PIECES && n0 + n < N) ? (n0 + n) * K : -1;
+  }
+
+  uint4 ra[C::A_IT], rb[C::B_IT];
+  auto load_regs = [&](int kt) {
+    const int k0 = kt * C::BK;
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) {
+      const int k = k0 + 4 * a_c4[i];
+      const int off = (a_base[i] >= 0 && k < K) ? (a_base[i] + k) * 4 : kOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(ar, off, 0, 0);
+      ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const int k = k0 + 4 * ((tid + i * C::NT) & 3);
+      const int off = (b_base[i] >= 0 && k < K) ? (b_base[i] + k) * 4 : kOOB;
+      const auto v = __builtin_amdgcn_raw_buffer_load_b128(br, off, 0, 0);
+      rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  auto store_lds = [&](int s) {
+    float* A = smem + s * C::STAGE;
+    float* Bs = A + C::BM * C::P;
+#pragma unroll
+    for (int i = 0; i < C::A_IT; ++i) *reinterpret_cast<uint4*>(A + a_row[i] * C::P + 4 * a_c4[i]) = ra[i];
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const int idx = tid + i * C::NT;
+      if (C::B_PIECES % C::NT == 0 || idx < C::B_PIECES)
+        *reinterpret_cast<uint4*>(Bs + (idx >> 2) * C::P + 4 * (idx & 3)) = rb[i];
+    }
+  };
+
+  f16v acc[C::FM][C::FN];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int KT = (K + C::BK - 1) / C::BK;
+  load_regs(0);
+  store_lds(0);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) load_regs(kt + 1);
+    const float* A = smem + cur * C::STAGE;
+    const float* Bs = A + C::BM * C::P;
+    float af[C::FM][8], bfr[C::FN][8];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      const float* p = A + (wm * C::TM + 32 * i + l32) * C::P + 8 * h;
+      const float4 u0 = *reinterpret_cast<const float4*>(p), u1 = *reinterpret_cast<const float4*>(p + 4);
+      af[i][0] = u0.x; af[i][1] = u0.y; af[i][2] = u0.z; af[i][3] = u0.w;
+      af[i][4] = u1.x; af[i][5] = u1.y; af[i][6] = u1.z; af[i][7] = u1.w;
+    }
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+      const float* p = Bs + (wn * C::TN + 32 * j + l32) * C::P + 8 * h;
+      const float4 u0 = *reinterpret_cast<const float4*>(p), u1 = *reinterpret_cast<const float4*>(p + 4);
+      bfr[j][0] = u0.x; bfr[j][1] = u0.y; bfr[j][2] = u0.z; bfr[j][3] = u0.w;
+      bfr[j][4] = u1.x; bfr[j][5] = u1.y; bfr[j][6] = u1.z; bfr[j][7] = u1.w;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
+    if (kt + 1 < KT) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+
+#pragma unroll
+  for (int j = 0; j < C::FN; ++j) {
+    const int n = n0 + wn * C::TN + 32 * j + l32;
+    if (n >= N) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const long m = m0 + wm * C::TM + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (m >= M) continue;
+        float v = acc[i][j][e] + bv;
+        if (res) {
+          const float rv = res[m * N + n];
+          if (act == ACT_DRELU) v = rv > 0.f ? v : 0.f;
+          else v += rv;
+        }
+        if (act == ACT_RELU) v = fmaxf(v, 0.f);
+        out[m * N + n] = v;
+      }
+    }
+  }
+}
+
+template <int BN>
+void launch_gemm(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
+                 int act, hipStream_t s) {
+  const long nwg = (M + 127) / 128 * ((N + BN - 1) / BN);
+  if (nwg == 0) return;
+  hipLaunchKernelGGL((gemm_f32_kernel<BN>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias, res, out, M,
+                     N, K, act);
+}
+
+}  // namespace
+
+void gemm_f32(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
+              int act, hipStream_t s) {
+  if (N % 128 == 0 && (M + 127) / 128 * (N / 128) >= 1024) launch_gemm<128>(a, b, bias, res, out, M, N, K, act, s);
+  else if (N > 32) launch_gemm<64>(a, b, bias, res, out, M, N, K, act, s);
+  else launch_gemm<32>(a, b, bias, res, out, M, N, K, act, s);
+}
+
+}  // namespace as

@@ -25,7 +25,8 @@ constexpr int kOOB = 0x7ffffff0;
 template <int BN_, int BK_>
 struct WgF32Cfg {
   static constexpr int BN = BN_, BK = BK_, BR = 32, NT = 256;
-  static constexpr int TN = BN / 2, TK = BK / 2;     // 2 x 2 waves
+  static constexpr int WN = BN_ >= 64 ? 2 : 1, WK = 4 / WN;   // waves: 2 x 2, or 1 x 4 for a 32-wide N tile
+  static constexpr int TN = BN / WN, TK = BK / WK;
   static constexpr int FN = TN / 32, FK = TK / 32;   // 32x32 tiles per wave
   static constexpr int PA = BN + 4, PB = BK + 4;     // LDS row pitch (floats)
   static constexpr int CHA = BN / 4, CHB = BK / 4;   // 16-B pieces per row
@@ -53,7 +54,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
   const long r_end = r_begin + rows_per_split < R ? r_begin + rows_per_split : R;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wn = wid >> 1, wk = wid & 1;
+  const int wn = wid / C::WK, wk = wid % C::WK;
   const int l32 = lane & 31, h = lane >> 5;
   const long HW = static_cast<long>(H) * W;
 
@@ -194,12 +195,15 @@ void launch(const float* dy, const float* x, float* dwp, float* dbp, long ps, lo
                      dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
 }
 
-int pick(int n) { return n <= 64 ? 64 : 128; }
+int pick(int n) { return n <= 32 ? 32 : (n <= 64 ? 64 : 128); }
+// the K tile: a wave covers >= 32 columns (2 waves along K for BN >= 64, 4 for the 32-wide N tile)
+int pick_k(int k, int bn) { return bn == 32 ? 128 : (k <= 64 ? 64 : 128); }
 
 }  // namespace
 
 int wgrad_f32_splits(long R, int N, int K) {
-  const long tiles = static_cast<long>((N + pick(N) - 1) / pick(N)) * ((K + pick(K) - 1) / pick(K));
+  const int bn = pick(N), bk = pick_k(K, bn);
+  const long tiles = static_cast<long>((N + bn - 1) / bn) * ((K + bk - 1) / bk);
   long S = (1024 + tiles - 1) / tiles;                   // ~1024 workgroups
   const long max_s = R < 2048 ? 1 : (R + 127) / 128;     // >= 4 stages per slice
   if (S > max_s) S = max_s;
@@ -215,14 +219,14 @@ void wgrad_f32(const float* dy, const float* x, float* dw_part, float* db_part, 
   long rps = (R + S - 1) / S;
   rps = (rps + 31) / 32 * 32;
   const bool conv = Cin > 0;
-  const int bn = pick(N), bk = pick(K);
+  const int bn = pick(N), bk = pick_k(K, bn);
 #define AS_WGF(BNv, BKv)                                                                   \
   if (bn == BNv && bk == BKv) {                                                            \
     if (conv) launch<BNv, BKv, true>(dy, x, dw_part, db_part, part_stride, R, N, K, H, W, Cin, S, rps, st); \
     else launch<BNv, BKv, false>(dy, x, dw_part, db_part, part_stride, R, N, K, H, W, Cin, S, rps, st);     \
     return;                                                                                \
   }
-  AS_WGF(128, 128) AS_WGF(128, 64) AS_WGF(64, 128) AS_WGF(64, 64)
+  AS_WGF(128, 128) AS_WGF(128, 64) AS_WGF(64, 128) AS_WGF(64, 64) AS_WGF(32, 128)
 #undef AS_WGF
 }
 

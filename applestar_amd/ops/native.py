@@ -1154,6 +1154,9 @@ class _Linear(torch.autograd.Function):
             if b is not None:
                 y = y + b.float()
             y = (torch.relu(y) if relu else y).to(x2.dtype)
+        elif x2.dtype == torch.float32 and _gemm_f32_ok(R, w.shape[0], K):
+            # fp32 step: f32-MFMA GEMM with the bias and ReLU in its epilogue (gemm_f32.hip)
+            y = _C.gemm_f32(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None, 1 if relu else 0)
         elif relu and b is not None:
             y = torch._addmm_activation(b, x2, w.t(), use_gelu=False)
         else:
@@ -1180,7 +1183,11 @@ class _Linear(torch.autograd.Function):
             g, ctx.link.g = ctx.link.g, None
             if _DEBUG_GRADLINK and g is not None and g._version != ctx.link.version:
                 raise RuntimeError('GradLink: the handed-over residual gradient was modified before the dX GEMM')
-        if g is not None:
+        if dy.dtype == torch.float32 and _gemm_f32_ok(dy.shape[0], w.shape[1], dy.shape[1]) and \
+                (g is not None or ctx.needs_input_grad[0]):
+            # fp32: dX = dY W (+ the handed-over residual gradient) on the f32-MFMA GEMM, out of place
+            dx = _C.gemm_f32(dy, _wT(w), None, None if g is None else g.view(dy.shape[0], w.shape[1]), 0)
+        elif g is not None:
             # + the residual gradient the closing LayerNorm handed over (GradLink), in the GEMM epilogue
             # in place: g is the LayerNorm's input gradient, which the branch's later layers (backward
             # runs earlier, same stream) have already consumed; out-of-place addmm copied g first
@@ -1204,6 +1211,13 @@ class _Linear(torch.autograd.Function):
 
 
 _WGRAD_MIN_ROWS = 256     # tools/ab_bench.py --variant wgrad_small: -0.7 ms/step vs 4096
+
+
+def _gemm_f32_ok(M, N, K):
+    """The f32-MFMA GEMM takes this [M, K] x [N, K]^T product: K % 4, 32-bit buffer offsets, and enough
+    128-row x 64-column tiles (>= 128) to fill the chip; smaller products stay on the library GEMM."""
+    return K % 4 == 0 and M * K * 4 < 0x7ffffff0 and N * K * 4 < 0x7ffffff0 and \
+        (M + 127) // 128 * ((N + 63) // 64) >= 128
 GEMM_REFORM = os.environ.get('APPLESTAR_GEMM_REFORM', '1') == '1'
 
 
@@ -1321,7 +1335,12 @@ def linear(x, w, b=None, act=None, grad_link=None):
             act in (None, 'relu') and (b is None or b.dtype == torch.float32):
         # fp32 step: library fp32 GEMMs forward / dX (exact f32 on gfx950), dW / db on the f32-MFMA split-R kernel
         ensure_loaded()
-        y = _Linear.apply(x.reshape(R, K).contiguous(), w, b, act == 'relu', None)
+        link = None
+        if grad_link is not None and RESID_LINK and x.dim() == 2 and x.is_contiguous() and x.requires_grad:
+            grad_link.armed, link, x2 = x, grad_link, x
+        else:
+            x2 = x.reshape(R, K).contiguous()
+        y = _Linear.apply(x2, w, b, act == 'relu', link)
         return y.view(*x.shape[:-1], N)
     if not lowp or R < _WGRAD_MIN_ROWS or N % 8 or K % 8 or R * max(N, K) * 2 >= 0x7ffffff0 or \
             act not in (None, 'relu'):

@@ -53,7 +53,8 @@ class FusedClipAdam:
                 s['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 s['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
             for name, x in (('param', p), ('grad', p.grad), ('exp_avg', s['exp_avg']), ('exp_avg_sq', s['exp_avg_sq'])):
-                if x.dtype != torch.float32 or not x.is_non_overlapping_and_dense() or x.stride() != p.stride():
+                dense = x.is_contiguous() or (x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last))
+                if x.dtype != torch.float32 or not dense or x.stride() != p.stride():
                     raise RuntimeError(f'FusedClipAdam: {name} of a {tuple(p.shape)} parameter is not an fp32 tensor '
                                        f'laid out like its parameter')
             rows += [p.data_ptr(), p.grad.data_ptr(), s['exp_avg'].data_ptr(), s['exp_avg_sq'].data_ptr(), p.numel(), 0]

@@ -1203,3 +1203,26 @@ def test_fused_clip_adam_matches_torch(max_norm, wd):
     for a, b in zip(pa, pb):
         assert torch.allclose(oa.state[a]['exp_avg_sq'], ob.state[b]['exp_avg_sq'], rtol=1e-5, atol=1e-12)
         assert float(oa.state[a]['step']) == float(ob.state[b]['step']) == 4.0
+
+
+@pytest.mark.parametrize('M,Nc,K', [(5000, 768, 256), (3001, 256, 1024), (20000, 32, 20), (2500, 96, 132)])
+@pytest.mark.parametrize('mode', ['bias_relu', 'res_add', 'drelu'])
+def test_gemm_f32_epilogues_match_fp64(M, Nc, K, mode):
+    """gemm_f32.hip: A [M,K] . B [Nc,K]^T with each epilogue (bias + ReLU; + residual; ReLU-output mask) vs float64."""
+    torch.manual_seed(M)
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(Nc, K, device=DEV) / K ** 0.5
+    bias = 0.1 * torch.randn(Nc, device=DEV)
+    res = torch.randn(M, Nc, device=DEV)
+    C = N.ensure_loaded()
+    ref = a.double().cpu() @ b.double().cpu().t() + bias.double().cpu()
+    if mode == 'bias_relu':
+        out = C.gemm_f32(a, b, bias, None, 1)
+        ref = ref.clamp_min(0)
+    elif mode == 'res_add':
+        out = C.gemm_f32(a, b, bias, res, 0)
+        ref = ref + res.double().cpu()
+    else:
+        out = C.gemm_f32(a, b, bias, res, 4)
+        ref = ref * (res.double().cpu() > 0)
+    assert _err(out.cpu(), ref) < 1e-5 * max(1.0, ref.abs().max().item())
