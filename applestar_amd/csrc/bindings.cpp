@@ -782,6 +782,73 @@ at::Tensor conv3x3_fwd(const at::Tensor& x, const at::Tensor& wk, const c10::opt
 // dy [R, N] bf16; x [R, K] bf16 (cin == 0) or NHWC [B, H, W, cin] bf16 (3x3 conv, K = 9 cin).
 // Returns (dW fp32 [N, K], db fp32 [N] or undefined); bf16_out: both in bf16, the cast fused into the
 // split reduction (the gradients of bf16 compute parameters under master weights).
+// ---------------------------------------------------------------- head sampling tails
+std::vector<at::Tensor> head_sample(const at::Tensor& logits, double temperature, const c10::optional<at::Tensor>& mask,
+                                    const c10::optional<at::Tensor>& lens, const at::Tensor& u,
+                                    const c10::optional<at::Tensor>& table, const c10::optional<at::Tensor>& tbias) {
+  check_cuda(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "head_sample: logits [B, C] with unit inner stride");
+  const int64_t B = logits.size(0), C = logits.size(1);
+  TORCH_CHECK(u.scalar_type() == at::kFloat && u.is_contiguous() && u.numel() == B, "head_sample: u fp32 [B]");
+  const uint8_t* mp = nullptr;
+  int64_t mld = 0;
+  if (mask && mask->defined()) {
+    TORCH_CHECK((mask->scalar_type() == at::kBool || mask->scalar_type() == at::kByte) && mask->is_contiguous() &&
+                (mask->numel() == C || mask->numel() == B * C), "head_sample: mask bool [C] or [B, C]");
+    mp = reinterpret_cast<const uint8_t*>(mask->data_ptr());
+    mld = mask->numel() == C ? 0 : C;
+  }
+  const int64_t* lp = nullptr;
+  if (lens && lens->defined()) {
+    TORCH_CHECK(lens->scalar_type() == at::kLong && lens->numel() == B && lens->is_contiguous(), "head_sample: lens");
+    lp = lens->data_ptr<int64_t>();
+  }
+  const void* tp = nullptr;
+  int tdt = 0, D = 0;
+  const float* bp = nullptr;
+  if (table && table->defined()) {
+    TORCH_CHECK(table->dim() == 2 && table->size(0) == C && table->is_contiguous(), "head_sample: table [C, D]");
+    TORCH_CHECK(tbias && tbias->defined() && tbias->scalar_type() == at::kFloat && tbias->numel() == table->size(1),
+                "head_sample: table bias fp32 [D]");
+    tp = table->data_ptr();
+    tdt = dt(*table);
+    D = static_cast<int>(table->size(1));
+    bp = tbias->data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(logits.device().index());
+  auto f = logits.options().dtype(at::kFloat);
+  auto out = at::empty({B, C}, f);
+  auto act = at::empty({B}, logits.options().dtype(at::kLong));
+  auto emb = at::empty({B, std::max<int64_t>(D, 1)}, f);
+  as::head_sample(logits.data_ptr(), dt(logits), logits.stride(0), static_cast<int>(B), static_cast<int>(C),
+                  static_cast<float>(1.0 / temperature), mp, mld, lp, u.data_ptr<float>(), tp, tdt, bp, D,
+                  out.data_ptr<float>(), act.data_ptr<int64_t>(), emb.data_ptr<float>(), stream());
+  return {out, act, emb};
+}
+
+std::vector<at::Tensor> target_unit_sample(const at::Tensor& e, const at::Tensor& w1, const at::Tensor& b1,
+                                           const at::Tensor& w2, const at::Tensor& b2, const at::Tensor& key,
+                                           const at::Tensor& lens, double temperature, const at::Tensor& u) {
+  check_cuda(e, "embedding");
+  TORCH_CHECK(e.dim() == 2 && e.size(1) == 1024 && e.is_contiguous(), "target_unit: embedding [B, 1024]");
+  const int64_t B = e.size(0);
+  TORCH_CHECK(key.dim() == 3 && key.size(0) == B && key.size(2) == 32 && key.is_contiguous(), "target_unit: key [B,N,32]");
+  for (auto* t : {&w1, &b1, &w2, &b2})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "target_unit: fp32 weights");
+  TORCH_CHECK(w1.numel() == 32 * 1024 && b1.numel() == 32 && w2.numel() == 32 * 32 && b2.numel() == 32, "target_unit: shapes");
+  TORCH_CHECK(lens.scalar_type() == at::kLong && lens.numel() == B && u.scalar_type() == at::kFloat && u.numel() == B,
+              "target_unit: lens int64 [B], u fp32 [B]");
+  const int64_t N = key.size(1);
+  c10::hip::HIPGuard g(e.device().index());
+  auto out = at::empty({B, N}, e.options().dtype(at::kFloat));
+  auto act = at::empty({B}, e.options().dtype(at::kLong));
+  as::target_unit_sample(e.data_ptr(), dt(e), w1.data_ptr<float>(), b1.data_ptr<float>(), w2.data_ptr<float>(),
+                         b2.data_ptr<float>(), key.data_ptr(), dt(key), static_cast<int>(B), static_cast<int>(N),
+                         lens.data_ptr<int64_t>(), static_cast<float>(1.0 / temperature), u.data_ptr<float>(),
+                         out.data_ptr<float>(), act.data_ptr<int64_t>(), stream());
+  return {out, act};
+}
+
 // ---------------------------------------------------------------- fused clip + Adam
 void fused_clip_adam(const at::Tensor& table, const at::Tensor& chunks, const at::Tensor& part,
                      const c10::optional<at::Tensor>& gate, const at::Tensor& norm_out, double max_norm, double lr_bc1,
@@ -1596,6 +1663,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("varlen_attn_fwd_f32", &varlen_attn_fwd_f32);
   m.def("conv3x3_f32", &conv3x3_f32);
   m.def("fused_clip_adam", &fused_clip_adam);
+  m.def("head_sample", &head_sample);
+  m.def("target_unit_sample", &target_unit_sample);
   m.def("fused_adam_chunk", &as::fused_adam_chunk);
   m.def("wgrad_f32", &wgrad_f32);
   m.def("gemm_f32", &gemm_f32);

@@ -229,6 +229,14 @@ void gemm_f32(const float* a, const float* b, const float* bias, const float* re
 void wgrad_f32(const float* dy, const float* x, float* dw_part, float* db_part, long part_stride, long R, int N, int K,
                int H, int W, int Cin, int S, hipStream_t st);
 
+// ---- heads.hip: fused sampling tails of the action heads (inference) -----------------------------------
+void head_sample(const void* logits, int logits_dt, long ld_logits, int B, int C, float inv_t, const uint8_t* mask,
+                 long mask_ld, const int64_t* lens, const float* u, const void* table, int table_dt,
+                 const float* tbias, int D, float* out_logits, int64_t* action, float* emb, hipStream_t s);
+void target_unit_sample(const void* e, int e_dt, const float* w1, const float* b1, const float* w2, const float* b2,
+                        const void* key, int key_dt, int B, int N, const int64_t* lens, float inv_t, const float* u,
+                        float* out_logits, int64_t* action, hipStream_t s);
+
 // ---- optim.hip: fused pytorch_norm clip + Adam over a (tensor, offset) chunk table ----------------------
 int fused_adam_chunk();
 // table: per tensor {p, g, m, v, numel, 0} (int64 x 6); chunks: per chunk {tensor, offset} (int64 x 2)

@@ -1,0 +1,188 @@
+// Fused sampling tails of the autoregressive action heads for actor inference:
+//
+//   head_sample : per row, scale the logits by 1/T, apply the head's mask (a shared [C] mask such as the
+//                 action-type race mask, or a per-row length such as entity_num), draw the action by inverse CDF
+//                 of softmax with the given uniform u, and gather its embedding relu(W^T[a] + b) (the
+//                 "one-hot @ fc1" of action_type_head.py:61-64 / action_arg_head.py:55-60, 84-86 as a row
+//                 gather).  Replaces softmax + cumsum + searchsorted + clamp + index_select + add + relu.
+//   target_unit : TargetUnitHead (action_arg_head.py:343-363) in one kernel per row: query MLP 1024 -> 32
+//                 (ReLU) -> 32, dot with the entity keys, length mask, 1/T, inverse-CDF sample.
+//
+// One 256-thread workgroup per batch row.  Sampling: m = max, p_i = exp(l_i - m), every thread sums a
+// contiguous segment of p, a block-wide exclusive scan of the segment sums locates the segment holding
+// u * sum p, and that thread walks its segment for the first index whose running sum exceeds the target
+// (torch.searchsorted(cumsum(softmax), u * total, right=True) up to summation order).  Fully masked rows
+// (impossible for valid observations) return the last index, like the clamped reference.
+#include "../common.h"
+#include "../kernels.h"
+
+namespace as {
+namespace {
+
+constexpr int kHT = 256;
+constexpr float kNeg = -1e9f;
+
+template <typename T>
+__device__ __forceinline__ float ld(const T* p, long i) { return Cvt<T>::load(p, i); }
+
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  return v;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return v;
+}
+
+// inverse-CDF draw over row[0..C) (already scaled / masked, fp32 in `row`): returns the index on every thread
+__device__ int sample_row(const float* __restrict__ row, int C, float u, float* red, float* scan) {
+  float mx = kNeg * 2.f;
+  for (int i = threadIdx.x; i < C; i += kHT) mx = fmaxf(mx, row[i]);
+  mx = block_max(mx, red);
+  const int seg = (C + kHT - 1) / kHT;
+  const int s0 = threadIdx.x * seg, s1 = min(C, s0 + seg);
+  float part = 0.f;
+  for (int i = s0; i < s1; ++i) part += __expf(row[i] - mx);
+  scan[threadIdx.x] = part;
+  __syncthreads();
+  // inclusive scan of the 256 segment sums (Hillis-Steele in LDS)
+  for (int off = 1; off < kHT; off <<= 1) {
+    const float add = threadIdx.x >= off ? scan[threadIdx.x - off] : 0.f;
+    __syncthreads();
+    scan[threadIdx.x] += add;
+    __syncthreads();
+  }
+  const float total = scan[kHT - 1];
+  const float target = u * total;
+  __shared__ int pick;
+  if (threadIdx.x == 0) pick = C - 1;
+  __syncthreads();
+  const float before = threadIdx.x ? scan[threadIdx.x - 1] : 0.f;
+  if (s0 < s1 && scan[threadIdx.x] > target && before <= target) {
+    float run = before;
+    int idx = s1 - 1;
+    for (int i = s0; i < s1; ++i) {
+      run += __expf(row[i] - mx);
+      if (run > target) { idx = i; break; }
+    }
+    atomicMin(&pick, idx);
+  }
+  __syncthreads();
+  const int r = pick;
+  __syncthreads();
+  return r;
+}
+
+template <typename TL, typename TW>
+__global__ __launch_bounds__(kHT) void head_sample_kernel(const TL* __restrict__ logits, long ld_logits, int C,
+                                                          float inv_t, const uint8_t* __restrict__ mask, long mask_ld,
+                                                          const int64_t* __restrict__ lens, const float* __restrict__ u,
+                                                          const TW* __restrict__ table, const float* __restrict__ tbias,
+                                                          int D, float* __restrict__ out_logits,
+                                                          int64_t* __restrict__ action, float* __restrict__ emb) {
+  __shared__ float red[4];
+  __shared__ float scan[kHT];
+  const int b = blockIdx.x;
+  const long len = lens ? lens[b] : C;
+  float* row = out_logits + static_cast<long>(b) * C;
+  for (int i = threadIdx.x; i < C; i += kHT) {
+    float v = ld(logits, static_cast<long>(b) * ld_logits + i) * inv_t;
+    if ((mask && !mask[static_cast<long>(b) * mask_ld + i]) || i >= len) v = kNeg;
+    row[i] = v;
+  }
+  __syncthreads();
+  const int a = sample_row(row, C, u[b], red, scan);
+  if (threadIdx.x == 0) action[b] = a;
+  if (table) {
+    for (int d = threadIdx.x; d < D; d += kHT)
+      emb[static_cast<long>(b) * D + d] = fmaxf(ld(table, static_cast<long>(a) * D + d) + tbias[d], 0.f);
+  }
+}
+
+template <typename TE, typename TK>
+__global__ __launch_bounds__(kHT) void target_unit_kernel(const TE* __restrict__ e, const float* __restrict__ w1,
+                                                          const float* __restrict__ b1, const float* __restrict__ w2,
+                                                          const float* __restrict__ b2, const TK* __restrict__ key,
+                                                          int N, const int64_t* __restrict__ lens, float inv_t,
+                                                          const float* __restrict__ u, float* __restrict__ out_logits,
+                                                          int64_t* __restrict__ action) {
+  constexpr int IN = 1024, KD = 32;
+  __shared__ float red[4];
+  __shared__ float scan[kHT];
+  __shared__ float q1[KD], q[KD];
+  const int b = blockIdx.x;
+  // q1 = relu(W1 e + b1): 8 threads per output, 128 inputs each
+  {
+    const int o = threadIdx.x >> 3, part = threadIdx.x & 7;
+    float s = 0.f;
+    const TE* er = e + static_cast<long>(b) * IN;
+    for (int i = part; i < IN; i += 8) s += w1[o * IN + i] * ld(er, i);
+    s += __shfl_xor(s, 1, kWave);
+    s += __shfl_xor(s, 2, kWave);
+    s += __shfl_xor(s, 4, kWave);
+    if (part == 0) q1[o] = fmaxf(s + b1[o], 0.f);
+  }
+  __syncthreads();
+  if (threadIdx.x < KD) {
+    float s = b2[threadIdx.x];
+    for (int i = 0; i < KD; ++i) s += w2[threadIdx.x * KD + i] * q1[i];
+    q[threadIdx.x] = s;
+  }
+  __syncthreads();
+  const long len = lens[b];
+  float* row = out_logits + static_cast<long>(b) * N;
+  for (int n = threadIdx.x; n < N; n += kHT) {
+    float s = 0.f;
+    const TK* kr = key + (static_cast<long>(b) * N + n) * KD;
+#pragma unroll
+    for (int c = 0; c < KD; ++c) s += q[c] * ld(kr, c);
+    row[n] = n < len ? s * inv_t : kNeg;
+  }
+  __syncthreads();
+  const int a = sample_row(row, N, u[b], red, scan);
+  if (threadIdx.x == 0) action[b] = a;
+}
+
+}  // namespace
+
+void head_sample(const void* logits, int logits_dt, long ld_logits, int B, int C, float inv_t, const uint8_t* mask,
+                 long mask_ld, const int64_t* lens, const float* u, const void* table, int table_dt,
+                 const float* tbias, int D, float* out_logits, int64_t* action, float* emb, hipStream_t s) {
+  if (B <= 0) return;
+#define AS_HS(TL, TW)                                                                                            \
+  hipLaunchKernelGGL((head_sample_kernel<TL, TW>), dim3(B), dim3(kHT), 0, s, static_cast<const TL*>(logits),      \
+                     ld_logits, C, inv_t, mask, mask_ld, lens, u, static_cast<const TW*>(table), tbias, D,        \
+                     out_logits, action, emb)
+  if (logits_dt == DT_BF16) {
+    if (table_dt == DT_BF16) AS_HS(bf16_t, bf16_t); else AS_HS(bf16_t, float);
+  } else {
+    if (table_dt == DT_BF16) AS_HS(float, bf16_t); else AS_HS(float, float);
+  }
+#undef AS_HS
+}
+
+void target_unit_sample(const void* e, int e_dt, const float* w1, const float* b1, const float* w2, const float* b2,
+                        const void* key, int key_dt, int B, int N, const int64_t* lens, float inv_t, const float* u,
+                        float* out_logits, int64_t* action, hipStream_t s) {
+  if (B <= 0) return;
+#define AS_TU(TE, TK)                                                                                             \
+  hipLaunchKernelGGL((target_unit_kernel<TE, TK>), dim3(B), dim3(kHT), 0, s, static_cast<const TE*>(e), w1, b1, w2, \
+                     b2, static_cast<const TK*>(key), N, lens, inv_t, u, out_logits, action)
+  if (e_dt == DT_BF16) {
+    if (key_dt == DT_BF16) AS_TU(bf16_t, bf16_t); else AS_TU(bf16_t, float);
+  } else {
+    if (key_dt == DT_BF16) AS_TU(float, bf16_t); else AS_TU(float, float);
+  }
+#undef AS_TU
+}
+
+}  // namespace as

@@ -41,6 +41,19 @@ def sample_from_logits(logits: torch.Tensor, u: Optional[torch.Tensor] = None, g
     return idx.clamp(max=p.shape[-1] - 1)
 
 
+def _embed_table(module, lin):
+    """lin.weight^T [n_in, n_out] contiguous (the one-hot -> fc row table of a head's embedding fc), cached per
+    weight version for the fused sampler."""
+    w = lin.weight
+    tag = (w.data_ptr(), w._version, w.dtype)
+    cache = module.__dict__.setdefault('_table_cache', {})
+    hit = cache.get(id(lin))
+    if hit is None or hit[0] != tag:
+        with torch.no_grad():
+            hit = cache[id(lin)] = (tag, w.detach().t().contiguous())
+    return hit[1]
+
+
 class ActionTypeHead(nn.Module):
     def __init__(self, input_dim=384, res_dim=256, action_num=gd.NUM_ACTIONS, context_dim=448, gate_dim=1024,
                  action_map_dim=256):
@@ -57,6 +70,16 @@ class ActionTypeHead(nn.Module):
     def forward(self, lstm_output, scalar_context, temperature: float = 1.0, action_type=None,
                 race_mask: Optional[torch.Tensor] = None, u=None):
         x = self.res(self.project(lstm_output))
+        w1 = self.action_map_fc1[0]
+        if action_type is None:
+            # actor inference: scale, race mask, sample and the action-map row gather in one kernel (heads.hip)
+            fused = ops.head_sample(self.action_fc(x, scalar_context), temperature, mask=race_mask, u=u,
+                                    table=_embed_table(self, w1), bias=w1.bias)
+            if fused is not None:
+                logits, action_type, e1 = fused
+                e1 = self.action_map_fc2(e1)
+                embedding = self.glu1(e1, scalar_context) + self.glu2(lstm_output, scalar_context)
+                return logits, action_type, embedding
         logits = self.action_fc(x, scalar_context) / temperature
         if race_mask is not None:
             logits = logits.masked_fill(~race_mask.to(logits.device).unsqueeze(0), NEG)
@@ -87,6 +110,13 @@ class _ArgMLPHead(nn.Module):
 
     def forward(self, embedding, temperature: float = 1.0, action=None, u=None):
         logits = self.fc3(self.fc2(self.fc1(embedding)))
+        w = self.embed_fc1[0]
+        if action is None:
+            fused = ops.head_sample(logits, temperature if self.use_temperature else 1.0, u=u,
+                                    table=_embed_table(self, w), bias=w.bias)
+            if fused is not None:     # actor inference: sample + row-gather embedding in one kernel (heads.hip)
+                logits, action, e = fused
+                return logits, action, embedding + self.embed_fc2(e)
         if self.use_temperature:
             logits = logits / temperature
         if action is None:
@@ -303,6 +333,11 @@ class TargetUnitHead(nn.Module):
                 key=None):
         if key is None:
             key = self.key_fc(entity_embedding)
+        if target_unit is None:
+            fused = ops.target_unit_sample(embedding, self.query_fc1[0], self.query_fc2[0], key, entity_num,
+                                           temperature, u)
+            if fused is not None:     # actor inference: query MLP + key dot + mask + sample in one kernel
+                return fused
         q = self.query_fc2(self.query_fc1(embedding))
         logits = torch.einsum('bc,bnc->bn', q.float(), key.float())
         mask = ops.sequence_mask(entity_num, key.shape[1])
@@ -348,5 +383,6 @@ class LocationHead(nn.Module):
         last = self.upsample[-1][0]  # 32 -> 1: fused upsample + conv, the 32-ch map never hits HBM
         logits = ops.upsample_conv_out(x, last.weight, last.bias) / temperature
         if location is None:
-            location = sample_from_logits(logits, u)
+            fused = ops.head_sample(logits, 1.0, u=u)
+            location = fused[1] if fused is not None else sample_from_logits(logits, u)
         return logits, location

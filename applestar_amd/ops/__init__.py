@@ -18,7 +18,7 @@ from . import _ext
 
 __all__ = ['linear', 'layer_norm', 'conv2d', 'max_pool2x2', 'segment_sum', 'gather_rows', 'gated_residual', 'lnlstm_layer', 'varlen_attention',
            'masked_attention', 'scatter_connection', 'sequence_mask', 'native_enabled', 'set_native', 'upsample2x',
-           'upsample_conv_out']
+           'upsample_conv_out', 'head_sample', 'target_unit_sample']
 
 _NATIVE_ENABLED = True
 
@@ -183,6 +183,45 @@ def upsample_conv_out(x, w, b):
         return n.upsample_conv_out(x, w, b)
     y = ref.conv2d(upsample2x(x), w, b, 1, 1)
     return y.reshape(x.shape[0], -1).float()
+
+
+def head_sample(logits, temperature: float = 1.0, mask=None, lens=None, u=None, table=None, bias=None):
+    """Inference sampling tail of an action head (csrc/kernels/heads.hip) on the GPU:
+    (logits / T with the head's mask as fp32 [B, C], inverse-CDF sample [B] int64, relu(table[a] + bias) [B, D]
+    or None).  ``mask``: bool [C] (shared) or [B, C]; ``lens``: [B] valid prefix length; ``u``: [B] uniforms
+    (drawn when None).  None off the GPU / with the native kernels off (callers keep the torch path)."""
+    n = _native(logits)
+    if n is None or torch.is_grad_enabled():
+        return None
+    C = n.ensure_loaded()
+    B = logits.shape[0]
+    if u is None:
+        u = torch.rand(B, device=logits.device)
+    lg = logits if logits.dtype in (torch.float32, torch.bfloat16) else logits.float()
+    if lg.stride(-1) != 1:
+        lg = lg.contiguous()
+    out, act, emb = C.head_sample(lg, float(temperature), None if mask is None else mask.to(logits.device).contiguous(),
+                                  None if lens is None else lens.long().contiguous(), u.float().contiguous(),
+                                  table, None if bias is None else bias.float().contiguous())
+    return out, act, (emb if table is not None else None)
+
+
+def target_unit_sample(embedding, q1, q2, key, entity_num, temperature: float = 1.0, u=None):
+    """TargetUnitHead inference in one kernel (query MLP, key dot, length mask, 1/T, sample); None when it does not
+    apply (CPU, grad mode, native off, non-reference widths)."""
+    n = _native(embedding)
+    if n is None or torch.is_grad_enabled() or embedding.shape[-1] != 1024 or key.shape[-1] != 32 or \
+            q1.weight.shape != (32, 1024) or q2.weight.shape != (32, 32):
+        return None
+    C = n.ensure_loaded()
+    B = embedding.shape[0]
+    if u is None:
+        u = torch.rand(B, device=embedding.device)
+    f = lambda t: t.detach().float().contiguous()  # noqa: E731
+    e = embedding if embedding.dtype in (torch.float32, torch.bfloat16) else embedding.float()
+    k = key if key.dtype in (torch.float32, torch.bfloat16) else key.float()
+    return tuple(C.target_unit_sample(e.contiguous(), f(q1.weight), f(q1.bias), f(q2.weight), f(q2.bias), k.contiguous(),
+                                      entity_num.long().contiguous(), float(temperature), u.float().contiguous()))
 
 
 def grad_link(x):

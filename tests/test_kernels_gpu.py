@@ -1226,3 +1226,71 @@ def test_gemm_f32_epilogues_match_fp64(M, Nc, K, mode):
         out = C.gemm_f32(a, b, bias, res, 4)
         ref = ref * (res.double().cpu() > 0)
     assert _err(out.cpu(), ref) < 1e-5 * max(1.0, ref.abs().max().item())
+
+
+def _same_or_boundary(a, b, logits, u):
+    """Sampled indices agree, except where u sits within float rounding of a CDF boundary."""
+    p = torch.softmax(logits.double(), -1)
+    cdf = torch.cumsum(p, -1)
+    for i in torch.nonzero(a != b).flatten().tolist():
+        lo = min(int(a[i]), int(b[i]))
+        assert abs(float(cdf[i, lo]) - float(u[i])) < 1e-5, (i, int(a[i]), int(b[i]))
+
+
+@pytest.mark.parametrize('B,C,dtype,masked', [(16, 327, torch.bfloat16, 'shared'), (3, 128, torch.float32, None),
+                                              (64, 2, torch.bfloat16, None), (2, 24320, torch.float32, None),
+                                              (5, 513, torch.float32, 'lens')])
+def test_head_sample_matches_reference_sampler(B, C, dtype, masked):
+    """heads.hip head_sample: same scaled / masked logits, same inverse-CDF draw as sample_from_logits for the same
+    uniforms, and the row-gathered embedding relu(W^T[a] + b)."""
+    from applestar_amd import ops
+    from applestar_amd.models.heads import sample_from_logits, NEG
+    torch.manual_seed(B * C)
+    logits = (torch.randn(B, C, device=DEV) * 3).to(dtype)
+    u = torch.rand(B, device=DEV)
+    mask = lens = None
+    ref = logits.float() / 0.8
+    if masked == 'shared':
+        mask = torch.rand(C, device=DEV) > 0.3
+        ref = ref.masked_fill(~mask, NEG)
+    elif masked == 'lens':
+        lens = torch.randint(1, C + 1, (B,), device=DEV)
+        ref = ref.masked_fill(torch.arange(C, device=DEV)[None] >= lens[:, None], NEG)
+    table = torch.randn(C, 256, device=DEV).to(dtype)
+    bias = torch.randn(256, device=DEV)
+    with torch.no_grad():
+        out, act, emb = ops.head_sample(logits, 0.8, mask=mask, lens=lens, u=u, table=table, bias=bias)
+    assert _err(out, ref) < 1e-5 * ref.abs().clamp(max=1e3).max().item() + 1e-6
+    ra = sample_from_logits(ref, u)
+    _same_or_boundary(act.cpu(), ra.cpu(), ref.cpu(), u.cpu())
+    assert torch.equal(emb, torch.relu(table.float()[act] + bias))
+    if mask is not None:
+        assert bool(mask[act].all())
+    if lens is not None:
+        assert bool((act < lens).all())
+
+
+@pytest.mark.parametrize('edtype', [torch.float32, torch.bfloat16])
+def test_target_unit_fused_matches_torch(edtype):
+    """heads.hip target_unit_sample == TargetUnitHead's torch path (query MLP, key dot, mask, 1/T, sample)."""
+    from applestar_amd import ops
+    from applestar_amd.models.heads import TargetUnitHead
+    torch.manual_seed(9)
+    B, N = 6, 300
+    head = TargetUnitHead().to(DEV)
+    emb = torch.randn(B, 1024, device=DEV).to(edtype)
+    ent = torch.randn(B, N, 256, device=DEV).to(edtype)
+    en = torch.randint(1, N + 1, (B,), device=DEV)
+    u = torch.rand(B, device=DEV)
+    with torch.no_grad():
+        key = head.key_fc(ent.float()).to(edtype)
+        lf, af = head(emb, ent, en, 0.7, u=u, key=key)
+        ops.set_native(False)
+        try:
+            lr_, ar_ = head(emb.float(), ent.float(), en, 0.7, u=u, key=key.float())
+        finally:
+            ops.set_native(True)
+    valid = lr_ > -1e8
+    assert torch.equal(valid, lf > -1e8)
+    assert _err(lf[valid], lr_[valid]) < 2e-4 * max(1.0, lr_[valid].abs().max().item())
+    _same_or_boundary(af.cpu(), ar_.cpu(), lr_.cpu(), u.cpu())

@@ -22,9 +22,14 @@ def run():
     H, Dh = 2, 128
     T = int(lens.sum())
     cu = torch.cat([torch.zeros(1, dtype=torch.int64), lens.cumsum(0)]).to(torch.int32).cuda()
-    qkv = (torch.randn(T, 3 * H * Dh, device='cuda') * 0.5).to(torch.bfloat16)
+    prec = os.environ.get('PREC', 'bf16')          # bf16: attention.hip, fp32: attention_f32.hip
+    qkv = torch.randn(T, 3 * H * Dh, device='cuda') * 0.5
+    if prec == 'bf16':
+        qkv = qkv.to(torch.bfloat16)
+    fwd = C.varlen_attn_fwd if prec == 'bf16' else C.varlen_attn_fwd_f32
+    bwd = C.varlen_attn_bwd if prec == 'bf16' else C.varlen_attn_bwd_f32
     mx = int(lens.max())
-    out, lse = C.varlen_attn_fwd(qkv, cu, mx, H)
+    out, lse = fwd(qkv, cu, mx, H)
     dout = torch.randn_like(out)
 
     def timed(fn, n=20):
@@ -39,10 +44,10 @@ def run():
         torch.cuda.synchronize()
         return s.elapsed_time(e) / n * 1e3
 
-    f = timed(lambda: C.varlen_attn_fwd(qkv, cu, mx, H))
-    b = timed(lambda: C.varlen_attn_bwd(qkv, out, dout, lse, cu, mx, H))
+    f = timed(lambda: fwd(qkv, cu, mx, H))
+    b = timed(lambda: bwd(qkv, out, dout, lse, cu, mx, H))
     flop = float((lens.double() ** 2).sum()) * H * Dh * 4        # QK^T + PV
-    print(json.dumps({'lens': dist, 'fwd_us': round(f, 1),
+    print(json.dumps({'prec': prec, 'lens': dist, 'fwd_us': round(f, 1),
                       'bwd_us': round(b, 1), 'fwd_tflops': round(flop / f / 1e6, 1),
                       'bwd_tflops': round(2.5 * flop / b / 1e6, 1)}), flush=True)
 

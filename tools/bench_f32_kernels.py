@@ -1,0 +1,68 @@
+"""Microbenchmarks of the fp32 learner step's f32-MFMA kernels on the learner's shapes: conv3x3_f32 (forward /
+dX), wgrad_f32 (conv + dense dW), gemm_f32, against the exact-f32 MFMA peak (157.3 TFLOP/s, MI355X).  One JSON
+line per (kernel, shape) with us / call and TFLOP/s.  Also the child process of PMC passes (tools/gpu_pmc.sh).
+
+    python tools/bench_f32_kernels.py [conv|wgrad|gemm|all]
+"""
+import json
+import os
+import sys
+
+import torch
+
+CONV = [(390, 19, 20, 128, 128), (390, 38, 40, 64, 128), (384, 38, 40, 128, 64), (384, 76, 80, 64, 32),
+        (390, 76, 80, 16, 16), (390, 19, 20, 32, 32)]
+GEMM = [(100000, 768, 256), (100000, 256, 256), (100000, 1024, 256), (100000, 256, 1024), (24576, 1536, 384)]
+
+
+def timed(fn, n=10):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n * 1e3
+
+
+def emit(kind, shape, us, flop):
+    print(json.dumps({'kernel': kind, 'shape': shape, 'us': round(us, 1), 'tflops': round(flop / us / 1e6, 1),
+                      'pct_f32_peak': round(100 * flop / us / 1e6 / 157.3, 1)}), flush=True)
+
+
+def main():
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from applestar_amd.ops import native
+    C = native.ensure_loaded()
+    which = sys.argv[1] if len(sys.argv) > 1 else 'all'
+    if which in ('conv', 'all'):
+        for B, H, W, cin, cout in CONV:
+            x = torch.randn(B, H, W, cin, device='cuda')
+            w = torch.randn(cout, 3, 3, cin, device='cuda') / 30
+            b = torch.randn(cout, device='cuda')
+            flop = 2.0 * B * H * W * cout * 9 * cin
+            emit('conv3x3_f32', [B, H, W, cin, cout], timed(lambda: C.conv3x3_f32(x, w, b, None, 1)), flop)
+    if which in ('wgrad', 'all'):
+        for B, H, W, cin, cout in CONV:
+            x = torch.randn(B, H, W, cin, device='cuda')
+            dy = torch.randn(B * H * W, cout, device='cuda')
+            flop = 2.0 * B * H * W * cout * 9 * cin
+            emit('wgrad_f32_conv', [B, H, W, cin, cout], timed(lambda: C.wgrad_f32(dy, x, cin, True)), flop)
+        for M, N, K in GEMM:
+            x = torch.randn(M, K, device='cuda')
+            dy = torch.randn(M, N, device='cuda')
+            emit('wgrad_f32_dense', [M, N, K], timed(lambda: C.wgrad_f32(dy, x, 0, True)), 2.0 * M * N * K)
+    if which in ('gemm', 'all'):
+        for M, N, K in GEMM:
+            a = torch.randn(M, K, device='cuda')
+            b = torch.randn(N, K, device='cuda')
+            bias = torch.randn(N, device='cuda')
+            emit('gemm_f32', [M, N, K], timed(lambda: C.gemm_f32(a, b, bias, None, 1)), 2.0 * M * N * K)
+            emit('torch_fp32_linear', [M, N, K], timed(lambda: torch.nn.functional.linear(a, b, bias)), 2.0 * M * N * K)
+
+
+if __name__ == '__main__':
+    main()

@@ -26,7 +26,9 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     ngap = int(sys.argv[2]) if len(sys.argv) > 2 else 25
     rows.sort(key=lambda r: int(r['Start_Timestamp']))
-    opt = [i for i, r in enumerate(rows) if 'fused_adam' in r['Kernel_Name'].lower() or 'FusedOpti' in r['Kernel_Name']]
+    # optimizer bursts: torch's fused Adam, or the native fused clip + Adam (optim.hip mt_adam_kernel)
+    opt = [i for i, r in enumerate(rows) if 'fused_adam' in r['Kernel_Name'].lower() or 'FusedOpti' in r['Kernel_Name']
+           or 'mt_adam_kernel' in r['Kernel_Name']]
     ends = []
     for i in opt:
         if not ends or i > ends[-1] + 5:
