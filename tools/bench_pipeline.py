@@ -36,6 +36,29 @@ def _free_port():
     return p
 
 
+def _learner_main(comm, B, T, gpu, precision, iq):
+    import torch
+    if not gpu:
+        torch.set_num_threads(2)      # CPU rehearsal: leave cores to the env workers and the inference server
+    from applestar_amd.learner.rl_learner import RLLearner
+    lrn = RLLearner({'common': {'experiment_name': 'pipeline'},
+                     'learner': {'use_cuda': gpu, 'player_id': 'MP0', 'use_value_feature': False,
+                                 'amp_dtype': 'bfloat16' if precision == 'bf16' else None,
+                                 'data': {'batch_size': B, 'trajectory_length': T, 'buffer_size': 2 * B},
+                                 'log_to_stdout': False},
+                     'communication': comm})
+    orig = lrn._train
+
+    def timed(data):
+        out = orig(data)
+        if gpu:
+            torch.cuda.synchronize()
+        iq.put((time.time(), lrn.last_iter.val + 1))
+        return out
+    lrn._train = timed
+    lrn.run(max_iterations=1000000)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--envs', type=int, default=8)
@@ -53,7 +76,6 @@ def main():
     from applestar_amd.league.league import League
     from applestar_amd.league.api import create_league_app
     from applestar_amd.actor.actor import Actor
-    from applestar_amd.learner.rl_learner import RLLearner
 
     gpu = torch.cuda.is_available()
     coord = serve_coordinator(Coordinator(), '127.0.0.1', 0)
@@ -72,30 +94,19 @@ def main():
             'league_port': lport, 'learner_send_model_freq': 50, 'learner_send_train_info_freq': 50,
             'actor_ask_for_job_interval': 3600, 'actor_model_update_interval': 30}
     T, B = args.traj_len, args.batch
+    # the learner runs in its own process, as in a deployment: in a thread of the actor process its ~25 ms of
+    # Python per step would hold the GIL the inference server's batching loop needs
+    import multiprocessing as mp
+    ctx = mp.get_context('spawn')
+    iq = ctx.Queue()
+    lp = ctx.Process(target=_learner_main, args=(comm, B, T, gpu, args.precision, iq), daemon=True)
+    lp.start()
     iters = []          # (wall time, iteration) after each learner iteration
-    holder = {}
-    stop = threading.Event()
 
-    def run_learner():
-        lrn = RLLearner({'common': {'experiment_name': 'pipeline'},
-                         'learner': {'use_cuda': gpu, 'player_id': 'MP0', 'use_value_feature': False,
-                                     'amp_dtype': 'bfloat16' if args.precision == 'bf16' else None,
-                                     'data': {'batch_size': B, 'trajectory_length': T, 'buffer_size': 2 * B},
-                                     'log_to_stdout': False},
-                         'communication': comm})
-        holder['l'] = lrn
-        orig = lrn._train
-
-        def timed(data):
-            out = orig(data)
-            if gpu:
-                torch.cuda.synchronize()
-            iters.append((time.time(), lrn.last_iter.val + 1))
-            return out
-        lrn._train = timed
-        lrn.run(max_iterations=1000000)
-    lt = threading.Thread(target=run_learner, daemon=True)
-    lt.start()
+    def drain():
+        while True:
+            iters.append(iq.get())
+    threading.Thread(target=drain, daemon=True).start()
     actor = Actor({'common': {'experiment_name': 'pipeline'},
                    'actor': {'job_type': 'train', 'env_num': args.envs, 'gpu_batch_inference': True, 'traj_len': T,
                              'episode_num': 100000, 'print_freq': 1000000},
@@ -129,7 +140,7 @@ def main():
            'startup_s': round(t0 - t_start, 1),
            'data': 'FakeSC2Env observations, random-init policy; learner reuses each trajectory 2x (reference)'}
     print(json.dumps(out), flush=True)
-    stop.set()
+    lp.terminate()
     try:
         actor.close()
     except Exception:   # noqa: BLE001 - best-effort teardown of the worker processes
