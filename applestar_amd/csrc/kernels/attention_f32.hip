@@ -12,8 +12,12 @@
 // keys {16 n + 4 lg + i} and P^T / dS^T feed the B operand from the lane's own registers.  For the
 // products that reduce over the head dim, lane group lg owns dims 32 lg .. 32 lg + 31 (k-step j = dim
 // 32 lg + j): the query / dO fragments are 32 registers loaded once, the K / V / Q / dO row fragments
-// are contiguous float4 LDS reads.  LDS rows are padded to 132 floats: 132 = 4 mod 8 makes the
-// transposed (one float per lane, rows 4 lg apart) reads conflict-free.
+// are contiguous float4 LDS reads.  LDS rows are padded to 132 floats and the two 32-float halves of
+// every row with bit 3 set are swapped (dim d of row r at r * 132 + (d ^ 32 ((r >> 3) & 1))): with the pitch
+// alone the float4 row reads of lane groups lg and lg ^ 1 collide 2-way (rows lr and lr + 8 land 32 banks
+// apart), with the swap both the float4 row reads and the transposed one-float-per-lane reads are
+// conflict-free (exhaustive check over the ds_read_b128 / b32 lane groups).  (A register prefetch of the next
+// key block measured slower in the learner step: 64 more live VGPRs for sequences of 1-8 blocks, r3i.)
 #include "../common.h"
 #include "../kernels.h"
 
@@ -41,7 +45,11 @@ __device__ __forceinline__ float xor_sum(float v) {
   return v + __shfl_xor(v, 32, 64);
 }
 
+// swizzled LDS float offset of (row r, dim d); d a multiple of 4 keeps float4 groups intact
+__device__ __forceinline__ int swz(int r, int d) { return r * P + (d ^ (((r >> 3) & 1) << 5)); }
+
 // [64 x 128] fp32 tile rows r0.. (rows >= nvalid zero) from a row-strided global matrix into LDS T[64][P]
+// (swizzled)
 __device__ __forceinline__ void stage_tile(float* T, const float* __restrict__ base, long ld, int r0, int nvalid) {
   const int t = threadIdx.x, r = t >> 2, c = t & 3;
   const bool ok = r0 + r < nvalid;
@@ -49,8 +57,9 @@ __device__ __forceinline__ void stage_tile(float* T, const float* __restrict__ b
   float4 v[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) v[q] = ok ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+  float* row = T + swz(r, 32 * c);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) *reinterpret_cast<float4*>(T + r * P + 32 * c + 4 * q) = v[q];
+  for (int q = 0; q < 8; ++q) *reinterpret_cast<float4*>(row + 4 * q) = v[q];
 }
 
 // 32 consecutive floats of one row (this lane group's dims) -> registers
@@ -65,7 +74,7 @@ __device__ __forceinline__ void load_row32(float (&f)[32], const float* __restri
 // acc += (rows 16 n + lr of LDS tile T) . frag over the head dim (lane group lg: dims 32 lg + j)
 __device__ __forceinline__ f4 row_dot(const float* T, int n, const float (&frag)[32], f4 acc) {
   const int l = threadIdx.x & 63;
-  const float* row = T + (16 * n + (l & 15)) * P + 32 * (l >> 4);
+  const float* row = T + swz(16 * n + (l & 15), 32 * (l >> 4));
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const float4 a = *reinterpret_cast<const float4*>(row + 4 * q);
@@ -81,11 +90,16 @@ __device__ __forceinline__ f4 row_dot(const float* T, int n, const float (&frag)
 // registers of tile n)
 __device__ __forceinline__ void tr_accumulate(const float* T, int n, const f4& b, f4 (&acc)[8]) {
   const int l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
-  const float* base = T + (16 * n + 4 * lg) * P + lr;
+  // rows 16 n + 4 lg + i have bit 3 = lg >> 1: dim 16 nd + lr sits at 16 nd + lr +- 32 (swapped halves),
+  // i.e. +32 for nd in {0, 1, 4, 5} and -32 for {2, 3, 6, 7}: two bases with compile-time offsets
+  const int sw = (lg >> 1) << 5;
+  const float* lo = T + (16 * n + 4 * lg) * P + lr + sw;
+  const float* hi = T + (16 * n + 4 * lg) * P + lr - sw;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int nd = 0; nd < 8; ++nd) acc[nd] = mfma4(base[i * P + 16 * nd], b[i], acc[nd]);
+    for (int nd = 0; nd < 8; ++nd)
+      acc[nd] = mfma4((nd & 2) ? hi[i * P + 16 * nd] : lo[i * P + 16 * nd], b[i], acc[nd]);
 }
 
 __device__ __forceinline__ bool attn_item(int QB, int S, int H, int& blk, int& s, int& h) {

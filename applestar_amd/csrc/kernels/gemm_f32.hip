@@ -11,9 +11,14 @@
 // mask in the same epilogue - the separate [M, N] elementwise pass of a library GEMM disappears.
 //
 // Tiling as conv3x3_f32.hip (its implicit GEMM with one tap): 128 x BN tile per 256-thread workgroup, K-steps
-// of 16, register-staged LDS double buffer, 20-float LDS rows, k-slot kk of lane half h = column 8h + kk (two
-// ds_read_b128 per fragment and K-step), XCD-aware tile order.  K % 4 == 0; a K tail reads zeros through the
-// buffer range check.
+// of BK = 16 (APPLESTAR_GEMM_F32_BK=32 selects 32-deep stages: half the barriers, but 74 KB of LDS leaves 2
+// workgroups per CU and measured 2-8 % slower on the learner's shapes, r3i),
+// register-staged LDS double buffer, BK + 4-float LDS rows (conflict-free float4 fragment reads: rows r * 36
+// and r * 20 fall in distinct 4-bank groups over each ds_read_b128 lane group), k-slot kk of lane half h =
+// column (BK / 2) h + kk, XCD-aware tile order.  K % 4 == 0; a K tail reads zeros through the buffer range
+// check.
+#include <cstdlib>
+
 #include "../common.h"
 #include "../kernels.h"
 
@@ -24,24 +29,26 @@ typedef __attribute__((ext_vector_type(16))) float f16v;
 
 constexpr int kOOB = 0x7ffffff0;
 
-template <int BN_>
+template <int BN_, int BK_>
 struct GemmF32Cfg {
-  static constexpr int BM = 128, BN = BN_, BK = 16, NT = 256;
+  static constexpr int BM = 128, BN = BN_, BK = BK_, NT = 256;
+  static constexpr int CH = BK / 4;            // 16-B pieces per tile row
+  static constexpr int KH = BK / 2;            // floats per lane half per stage (= MFMA k-steps)
   static constexpr int WN = BN_ >= 128 ? 2 : 1, WM = 4 / WN;
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 32, FN = TN / 32;
   static constexpr int P = BK + 4;
-  static constexpr int A_IT = BM * (BK / 4) / NT;
-  static constexpr int B_PIECES = BN * (BK / 4);
+  static constexpr int A_IT = BM * CH / NT;
+  static constexpr int B_PIECES = BN * CH;
   static constexpr int B_IT = (B_PIECES + NT - 1) / NT;
   static constexpr int STAGE = (BM + BN) * P;
 };
 
-template <int BN>
+template <int BN, int BK>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                        const float* __restrict__ bias, const float* __restrict__ res,
                                                        float* __restrict__ out, long M, int N, int K, int act) {
-  using C = GemmF32Cfg<BN>;
+  using C = GemmF32Cfg<BN, BK>;
   __shared__ __attribute__((aligned(16))) float smem[2 * C::STAGE];
   const int ntn = (N + BN - 1) / BN;
   const int nwg = gridDim.x, orig = blockIdx.x;
@@ -63,8 +70,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 #pragma unroll
   for (int i = 0; i < C::A_IT; ++i) {
     const int idx = tid + i * C::NT;
-    a_row[i] = idx >> 2;
-    a_c4[i] = idx & 3;
+    a_row[i] = idx / C::CH;
+    a_c4[i] = idx % C::CH;
     const long m = m0 + a_row[i];
     a_base[i] = m < M ? static_cast<int>(m * K) : -1;
   }
@@ -72,7 +79,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 #pragma unroll
   for (int i = 0; i < C::B_IT; ++i) {
     const int idx = tid + i * C::NT;
-    const int n = idx >> 2;
+    const int n = idx / C::CH;
     b_base[i] = (idx < C::B_PIECES && n0 + n < N) ? (n0 + n) * K : -1;
   }
 
@@ -88,7 +95,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     }
 #pragma unroll
     for (int i = 0; i < C::B_IT; ++i) {
-      const int k = k0 + 4 * ((tid + i * C::NT) & 3);
+      const int k = k0 + 4 * ((tid + i * C::NT) % C::CH);
       const int off = (b_base[i] >= 0 && k < K) ? (b_base[i] + k) * 4 : kOOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(br, off, 0, 0);
       rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
@@ -103,7 +110,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     for (int i = 0; i < C::B_IT; ++i) {
       const int idx = tid + i * C::NT;
       if (C::B_PIECES % C::NT == 0 || idx < C::B_PIECES)
-        *reinterpret_cast<uint4*>(Bs + (idx >> 2) * C::P + 4 * (idx & 3)) = rb[i];
+        *reinterpret_cast<uint4*>(Bs + (idx / C::CH) * C::P + 4 * (idx % C::CH)) = rb[i];
     }
   };
 
@@ -124,23 +131,27 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     if (kt + 1 < KT) load_regs(kt + 1);
     const float* A = smem + cur * C::STAGE;
     const float* Bs = A + C::BM * C::P;
-    float af[C::FM][8], bfr[C::FN][8];
+    float af[C::FM][C::KH], bfr[C::FN][C::KH];
 #pragma unroll
     for (int i = 0; i < C::FM; ++i) {
-      const float* p = A + (wm * C::TM + 32 * i + l32) * C::P + 8 * h;
-      const float4 u0 = *reinterpret_cast<const float4*>(p), u1 = *reinterpret_cast<const float4*>(p + 4);
-      af[i][0] = u0.x; af[i][1] = u0.y; af[i][2] = u0.z; af[i][3] = u0.w;
-      af[i][4] = u1.x; af[i][5] = u1.y; af[i][6] = u1.z; af[i][7] = u1.w;
+      const float* p = A + (wm * C::TM + 32 * i + l32) * C::P + C::KH * h;
+#pragma unroll
+      for (int q = 0; q < C::KH / 4; ++q) {
+        const float4 u = *reinterpret_cast<const float4*>(p + 4 * q);
+        af[i][4 * q] = u.x; af[i][4 * q + 1] = u.y; af[i][4 * q + 2] = u.z; af[i][4 * q + 3] = u.w;
+      }
     }
 #pragma unroll
     for (int j = 0; j < C::FN; ++j) {
-      const float* p = Bs + (wn * C::TN + 32 * j + l32) * C::P + 8 * h;
-      const float4 u0 = *reinterpret_cast<const float4*>(p), u1 = *reinterpret_cast<const float4*>(p + 4);
-      bfr[j][0] = u0.x; bfr[j][1] = u0.y; bfr[j][2] = u0.z; bfr[j][3] = u0.w;
-      bfr[j][4] = u1.x; bfr[j][5] = u1.y; bfr[j][6] = u1.z; bfr[j][7] = u1.w;
+      const float* p = Bs + (wn * C::TN + 32 * j + l32) * C::P + C::KH * h;
+#pragma unroll
+      for (int q = 0; q < C::KH / 4; ++q) {
+        const float4 u = *reinterpret_cast<const float4*>(p + 4 * q);
+        bfr[j][4 * q] = u.x; bfr[j][4 * q + 1] = u.y; bfr[j][4 * q + 2] = u.z; bfr[j][4 * q + 3] = u.w;
+      }
     }
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk)
+    for (int kk = 0; kk < C::KH; ++kk)
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
@@ -174,22 +185,37 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   }
 }
 
-template <int BN>
+template <int BN, int BK>
 void launch_gemm(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
                  int act, hipStream_t s) {
   const long nwg = (M + 127) / 128 * ((N + BN - 1) / BN);
   if (nwg == 0) return;
-  hipLaunchKernelGGL((gemm_f32_kernel<BN>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias, res, out, M,
-                     N, K, act);
+  hipLaunchKernelGGL((gemm_f32_kernel<BN, BK>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias, res, out,
+                     M, N, K, act);
+}
+
+int gemm_bk() {
+  static const int bk = [] {
+    const char* e = std::getenv("APPLESTAR_GEMM_F32_BK");
+    return e && std::atoi(e) == 32 ? 32 : 16;
+  }();
+  return bk;
 }
 
 }  // namespace
 
 void gemm_f32(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
               int act, hipStream_t s) {
-  if (N % 128 == 0 && (M + 127) / 128 * (N / 128) >= 1024) launch_gemm<128>(a, b, bias, res, out, M, N, K, act, s);
-  else if (N > 32) launch_gemm<64>(a, b, bias, res, out, M, N, K, act, s);
-  else launch_gemm<32>(a, b, bias, res, out, M, N, K, act, s);
+  const bool deep = gemm_bk() == 32 && K >= 64;
+  if (N % 128 == 0 && (M + 127) / 128 * (N / 128) >= 1024) {
+    if (deep) launch_gemm<128, 32>(a, b, bias, res, out, M, N, K, act, s);
+    else launch_gemm<128, 16>(a, b, bias, res, out, M, N, K, act, s);
+  } else if (N > 32) {
+    if (deep) launch_gemm<64, 32>(a, b, bias, res, out, M, N, K, act, s);
+    else launch_gemm<64, 16>(a, b, bias, res, out, M, N, K, act, s);
+  } else {
+    launch_gemm<32, 16>(a, b, bias, res, out, M, N, K, act, s);
+  }
 }
 
 }  // namespace as

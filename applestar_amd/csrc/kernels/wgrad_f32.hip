@@ -74,13 +74,27 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
     b_dx = tap % 3 - 1;
   }
   const bool a_ok = a_col < N, b_ok = b_col < K;
+  // conv pieces: image coordinates of each piece's row, advanced by BR rows per stage (32-bit offsets: the
+  // host keeps every operand below 2^31 bytes).  Replaces a 64-bit modulo and two divisions per piece and
+  // stage, which were the bulk of the loop's VALU work on the narrow (Cout 32 / 64) tiles.
+  int py[C::B_IT], px[C::B_IT];
+  const int adv_y = C::BR / W, adv_x = C::BR % W;
+  if (CONV) {
+#pragma unroll
+    for (int i = 0; i < C::B_IT; ++i) {
+      const long r = r_begin + (tid + i * C::NT) / C::CHB;
+      const int rem = static_cast<int>(r % HW);
+      py[i] = rem / W;
+      px[i] = rem - py[i] * W;
+    }
+  }
 
   uint4 ra[C::A_IT], rb[C::B_IT];
   auto load_regs = [&](long rs) {
 #pragma unroll
     for (int i = 0; i < C::A_IT; ++i) {
       const long r = rs + (tid + i * C::NT) / C::CHA;
-      const int off = (a_ok && r < r_end) ? static_cast<int>((r * N + a_col) * 4) : kOOB;
+      const int off = (a_ok && r < r_end) ? (static_cast<int>(r) * N + a_col) * 4 : kOOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(yr, off, 0, 0);
       ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
     }
@@ -88,15 +102,16 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
     for (int i = 0; i < C::B_IT; ++i) {
       const long r = rs + (tid + i * C::NT) / C::CHB;
       int off = kOOB;
-      if (b_ok && r < r_end) {
-        if (CONV) {
-          const int rem = static_cast<int>(r % HW);
-          const int yy = rem / W + b_dy, xx = rem % W + b_dx;
-          if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-            off = static_cast<int>(((r + b_dy * W + b_dx) * Cin + b_c) * 4);
-        } else {
-          off = static_cast<int>((r * K + b_col) * 4);
-        }
+      if (CONV) {
+        const int yy = py[i] + b_dy, xx = px[i] + b_dx;
+        if (b_ok && r < r_end && yy >= 0 && yy < H && xx >= 0 && xx < W)
+          off = ((static_cast<int>(r) + b_dy * W + b_dx) * Cin + b_c) * 4;
+        px[i] += adv_x;
+        py[i] += adv_y;
+        if (px[i] >= W) { px[i] -= W; ++py[i]; }
+        while (py[i] >= H) py[i] -= H;
+      } else if (b_ok && r < r_end) {
+        off = (static_cast<int>(r) * K + b_col) * 4;
       }
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
       rb[i] = make_uint4(v[0], v[1], v[2], v[3]);

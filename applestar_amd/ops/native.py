@@ -6,6 +6,7 @@ Shapes/dtypes the kernels do not cover raise instead of silently using torch.
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -609,6 +610,63 @@ def _wgrad(dy2d, x, cin, has_b, bf16_out):
     return _C.wgrad(dy2d, x, cin, has_b, bf16_out)
 
 
+# ---------------------------------------------------------------------------- weight gradients on a side stream
+SIDE_WGRAD = os.environ.get('APPLESTAR_SIDE_WGRAD', '0') == '1'     # A/B switch (off: measured slower, r3j)
+_SIDE_MIN_ROWS = 1 << 15
+_SIDE_STREAMS = {}
+
+
+class _NullCtx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+_NULL_CTX = _NullCtx()
+
+
+class _SideWork:
+    """Runs a backward node's weight-gradient kernels on a second HIP stream, concurrently with the input-
+    gradient kernels that stay on the main stream: the dW (split-R) and dX (implicit GEMM) kernels of a layer
+    are independent, and either alone leaves the chip partly idle in its last round of workgroups (a 19x20
+    ResBlock conv is 1158 tiles = 1.5 rounds of the ~768 resident workgroups).  ``fork()`` makes the side
+    stream wait for the main stream's work so far (the side kernels read tensors the main stream produced);
+    ``join(*outs)`` makes the main stream wait for the side kernels and marks their outputs (allocated from
+    the side stream's pool) as used on the main stream.  The caller keeps the inputs referenced until the
+    join, so the main stream cannot recycle them while the side stream reads.  Only for large products (the
+    event hops cost more than the overlap buys on small ones).  Off by default (APPLESTAR_SIDE_WGRAD=1 turns
+    it on): measured 87.5 -> 88.7 ms (fp32) and 27.3 -> 29.8 ms (bf16) per learner step on one MI355X
+    (profiles/r3j_side_stream_ab.txt) - the two streams contend for the same CUs and the dX chain, which is
+    the critical path, slows down more than the tails it fills."""
+    __slots__ = ('on', 'main', 'side')
+
+    def __init__(self, ref, rows):
+        self.on = SIDE_WGRAD and ref.is_cuda and rows >= _SIDE_MIN_ROWS
+        if self.on:
+            self.main = torch.cuda.current_stream(ref.device)
+            s = _SIDE_STREAMS.get(ref.device)
+            if s is None:
+                s = _SIDE_STREAMS[ref.device] = torch.cuda.Stream(device=ref.device)
+            self.side = s
+
+    def fork(self):
+        """Context manager: the enclosed launches go to the side stream, ordered after the main stream's work."""
+        if not self.on:
+            return _NULL_CTX
+        self.side.wait_stream(self.main)
+        return torch.cuda.stream(self.side)
+
+    def join(self, *outs):
+        if self.on:
+            self.main.wait_stream(self.side)
+            for t in outs:
+                if t is not None:
+                    t.record_stream(self.main)
+        return outs
+
+
 # ---------------------------------------------------------------------------- conv3x3 implicit GEMM
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
@@ -627,13 +685,17 @@ class _Conv3x3(torch.autograd.Function):
     def backward(ctx, dout):
         x, w, out = ctx.saved_tensors
         dpre = _act_grad(dout, out, ctx.act == 'relu')    # one pass: mask + cast + NHWC
-        dx = _conv3(dpre, _conv_wt(w), None, None, 0)
         has_b = ctx.b_dtype is not None
         cout, cin = w.shape[0], w.shape[1]
         bf = _bf16_grads(w.dtype, ctx.b_dtype)
-        dw, db = _wgrad(dpre.view(-1, cout), x, cin, has_b, bf)   # dW in [Cout,3,3,Cin] (channels_last) order
-        dw = dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype)
-        return (dx, dw, db.to(ctx.b_dtype) if has_b else None, dpre if ctx.has_res else None, None)
+        side = _SideWork(dpre, dpre.numel() // cout)
+        with side.fork():
+            dw, db = _wgrad(dpre.view(-1, cout), x, cin, has_b, bf)   # dW in [Cout,3,3,Cin] (channels_last) order
+            dw = dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype)
+            db = db.to(ctx.b_dtype) if has_b else None
+        dx = _conv3(dpre, _conv_wt(w), None, None, 0)
+        side.join(dw, db)
+        return (dx, dw, db, dpre if ctx.has_res else None, None)
 
 
 def _conv_w(w):
@@ -780,11 +842,17 @@ class _ResBlock(torch.autograd.Function):
     def backward(ctx, dout):
         x, w1, w2, y1, out = ctx.saved_tensors
         dpre2 = _act_grad(dout, out, True)
+        side = _SideWork(dpre2, dpre2.numel() // dpre2.shape[-1])
+        with side.fork():       # weight gradients concurrent with the dX convs
+            dw2, db2 = _conv_dw(dpre2, y1, w2, ctx.b_dtypes[1])
+            db2 = db2.to(ctx.b_dtypes[1])
         dpre1 = _conv_dx_drelu(dpre2, w2, y1)
-        dw2, db2 = _conv_dw(dpre2, y1, w2, ctx.b_dtypes[1])
+        with side.fork():
+            dw1, db1 = _conv_dw(dpre1, x, w1, ctx.b_dtypes[0])
+            db1 = db1.to(ctx.b_dtypes[0])
         dx = _conv3(dpre1, _conv_wt(w1), None, dpre2, 0)       # + skip gradient, fused
-        dw1, db1 = _conv_dw(dpre1, x, w1, ctx.b_dtypes[0])
-        return dx, dw1, db1.to(ctx.b_dtypes[0]), dw2, db2.to(ctx.b_dtypes[1])
+        side.join(dw1, db1, dw2, db2)
+        return dx, dw1, db1, dw2, db2
 
 
 def _f32_conv_ok(x, w, cin, cout):
@@ -874,15 +942,21 @@ class _GatedResBlock(torch.autograd.Function):
                     P = dh.shape[0]
                     d = _act_grad(dh.view(1, 1, P, C), acts_in[i].view(1, 1, P, C), True).view(P, C)
             dx_gate = torch.addmm(dx_res.view(-1, C), d, gw1.view(C, C))      # skip + G1 input gradients
-        # conv path
+        # conv path: its weight gradients on the side stream, concurrent with the dX convs
+        side = _SideWork(dy, B * H * W)
+        with side.fork():
+            dw2, db2 = _conv_dw(dy, y1, w2, ctx.dtypes[1])
+            db2 = db2.to(ctx.dtypes[1])
         dpre1 = _conv_dx_drelu(dy, w2, y1)
-        dw2, db2 = _conv_dw(dy, y1, w2, ctx.dtypes[1])
+        with side.fork():
+            dw1, db1 = _conv_dw(dpre1, x, w1, ctx.dtypes[0])
+            db1 = db1.to(ctx.dtypes[0])
         dx = _conv3(dpre1, _conv_wt(w1), None, dx_gate.view(B, H, W, C).contiguous(), 0)
-        dw1, db1 = _conv_dw(dpre1, x, w1, ctx.dtypes[0])
+        side.join(dw1, db1, dw2, db2)
         gate_grads = [None] * 8
         for i, dw_i, db_i in grads_g:
             gate_grads[2 * i], gate_grads[2 * i + 1] = dw_i, db_i
-        return (dx, dsp.to(sp.dtype), dw1, db1.to(ctx.dtypes[0]), dw2, db2.to(ctx.dtypes[1]), *gate_grads)
+        return (dx, dsp.to(sp.dtype), dw1, db1, dw2, db2, *gate_grads)
 
 
 def gated_resblock(x, conv1, conv2, gates, sp):
@@ -1157,6 +1231,8 @@ class _Linear(torch.autograd.Function):
         elif x2.dtype == torch.float32 and _gemm_f32_ok(R, w.shape[0], K):
             # fp32 step: f32-MFMA GEMM with the bias and ReLU in its epilogue (gemm_f32.hip)
             y = _C.gemm_f32(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None, 1 if relu else 0)
+            if relu and RELU_LINK:
+                _note_relu_out(y)
         elif relu and b is not None:
             y = torch._addmm_activation(b, x2, w.t(), use_gelu=False)
         else:
@@ -1166,17 +1242,26 @@ class _Linear(torch.autograd.Function):
         ctx.save_for_backward(x2, w, y if relu else None)
         ctx.relu = relu
         ctx.b_dtype = b.dtype if b is not None else None
+        ctx.mask_in = x2.dtype == torch.float32 and link is None and _relu_src(x2)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x2, w, y = ctx.saved_tensors
-        if ctx.relu:
+        if ctx.relu and y.dtype == torch.float32 and _premasked(y, dy):
+            dy = dy.contiguous().view(y.shape)      # the consumer's dX epilogue applied this ReLU's mask
+        elif ctx.relu:
             R, N = y.shape
             dy = _act_grad(dy.view(1, 1, R, N) if dy.is_contiguous() else dy.contiguous().view(1, 1, R, N),
                            y.view(1, 1, R, N), True).view(R, N)
         else:
             dy = dy.to(x2.dtype).contiguous()
+        has_b = ctx.b_dtype is not None
+        side = _SideWork(dy, dy.shape[0])
+        with side.fork():       # dW / db concurrent with the dX GEMM below
+            dw, db = _wgrad(dy, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
+            dw = dw.to(w.dtype)
+            db = db.to(ctx.b_dtype) if has_b else None
         dx = None
         g = None
         if ctx.link is not None:
@@ -1185,8 +1270,14 @@ class _Linear(torch.autograd.Function):
                 raise RuntimeError('GradLink: the handed-over residual gradient was modified before the dX GEMM')
         if dy.dtype == torch.float32 and _gemm_f32_ok(dy.shape[0], w.shape[1], dy.shape[1]) and \
                 (g is not None or ctx.needs_input_grad[0]):
-            # fp32: dX = dY W (+ the handed-over residual gradient) on the f32-MFMA GEMM, out of place
-            dx = _C.gemm_f32(dy, _wT(w), None, None if g is None else g.view(dy.shape[0], w.shape[1]), 0)
+            # fp32: dX = dY W (+ the handed-over residual gradient) on the f32-MFMA GEMM, out of place; when x is
+            # the ReLU output of another fp32 linear, that ReLU's mask is applied here (epilogue mode 4) and
+            # the producer's backward skips its own threshold pass (_premasked)
+            if g is None and ctx.mask_in:
+                dx = _C.gemm_f32(dy, _wT(w), None, x2, 4)
+                _MASKED_DX[x2.data_ptr()] = (dx, dx._version)
+            else:
+                dx = _C.gemm_f32(dy, _wT(w), None, None if g is None else g.view(dy.shape[0], w.shape[1]), 0)
         elif g is not None:
             # + the residual gradient the closing LayerNorm handed over (GradLink), in the GEMM epilogue
             # in place: g is the LayerNorm's input gradient, which the branch's later layers (backward
@@ -1205,9 +1296,44 @@ class _Linear(torch.autograd.Function):
                 dx = torch.nn.functional.linear(dy, _wT(w))
             else:
                 dx = torch.mm(dy, w)
-        has_b = ctx.b_dtype is not None
-        dw, db = _wgrad(dy, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
-        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if has_b else None), None, None
+        side.join(dw, db)
+        return dx, dw, db, None, None
+
+
+# ---------------------------------------------------------------------------- ReLU-mask hand-off (fp32 linears)
+RELU_LINK = os.environ.get('APPLESTAR_RELU_LINK', '1') == '1'   # A/B switch
+_RELU_OUTS = {}      # data_ptr -> weakref of an fp32 _Linear ReLU output (recorded in forward)
+_MASKED_DX = {}      # data_ptr of such an output -> (dX of its consumer, version): already ReLU-masked
+
+
+def _relu_src(x2):
+    """x2 is (the storage of, same size) the ReLU output of an fp32 ``_Linear``: its consumer's dX may apply
+    that ReLU's mask in the GEMM epilogue (mask(x2 > 0) = relu'(pre) exactly, since x2 = relu(pre))."""
+    if not RELU_LINK:
+        return False
+    r = _RELU_OUTS.get(x2.data_ptr())
+    t = r() if r is not None else None
+    return t is not None and t.data_ptr() == x2.data_ptr() and t.numel() == x2.numel() and t.dtype == x2.dtype
+
+
+def _note_relu_out(y):
+    if len(_RELU_OUTS) > 4096:
+        for k in [k for k, r in _RELU_OUTS.items() if r() is None]:
+            del _RELU_OUTS[k]
+    _RELU_OUTS[y.data_ptr()] = weakref.ref(y)
+
+
+def _premasked(y, dy):
+    """The incoming gradient dy of ReLU output y is exactly the dX its sole consumer already masked by
+    (y > 0) (same storage, unmodified): the separate threshold_backward pass is skipped.  Any other
+    gradient (a sum over several consumers is a new tensor) takes the mask as usual; masking is idempotent,
+    so a missed hand-off costs one pass, never correctness.  As with GradLink, a ``retain_grad`` / hook on
+    such an intermediate ReLU output would observe the masked gradient."""
+    if len(_MASKED_DX) > 256:
+        _MASKED_DX.clear()
+    rec = _MASKED_DX.pop(y.data_ptr(), None)
+    return rec is not None and rec[0].data_ptr() == dy.data_ptr() and rec[0]._version == rec[1] and \
+        rec[0].numel() == dy.numel()
 
 
 _WGRAD_MIN_ROWS = 256     # tools/ab_bench.py --variant wgrad_small: -0.7 ms/step vs 4096

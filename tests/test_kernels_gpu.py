@@ -1139,6 +1139,39 @@ def test_linear_f32_grads_match_fp64(R, N, K):
         assert e < 2e-5 * max(1.0, ref.abs().max().item()), (name, e)
 
 
+@pytest.mark.parametrize('extra_consumer', [False, True])
+def test_linear_f32_relu_handoff_matches_fp64(extra_consumer):
+    """Chained fp32 linears: the second layer's dX epilogue applies the first layer's ReLU mask and the first
+    layer's backward skips its threshold pass (native._premasked); with a second consumer of the hidden
+    activation the summed gradient must take the mask as usual.  Both vs float64."""
+    from applestar_amd.ops import native as NN
+    torch.manual_seed(6)
+    R, K, H, O = 6000, 256, 512, 256
+    x = torch.randn(R, K, device=DEV).requires_grad_()
+    w1 = (torch.randn(H, K, device=DEV) / K ** 0.5).requires_grad_()
+    b1 = (0.1 * torch.randn(H, device=DEV)).requires_grad_()
+    w2 = (torch.randn(O, H, device=DEV) / H ** 0.5).requires_grad_()
+    b2 = (0.1 * torch.randn(O, device=DEV)).requires_grad_()
+    h = NN.linear(x, w1, b1, act='relu')
+    assert NN._relu_src(h)
+    y = NN.linear(h, w2, b2, act='relu')
+    if extra_consumer:
+        y = y.sum(1, keepdim=True) + (h * h).sum(1, keepdim=True)
+    xs, w1s, b1s, w2s, b2s = (_f64(t) for t in (x, w1, b1, w2, b2))
+    hs = torch.relu(xs @ w1s.t() + b1s)
+    ys = torch.relu(hs @ w2s.t() + b2s)
+    if extra_consumer:
+        ys = ys.sum(1, keepdim=True) + (hs * hs).sum(1, keepdim=True)
+    g = torch.randn(ys.shape, dtype=torch.float64)
+    y.backward(g.float().to(DEV))
+    ys.backward(g)
+    assert not NN._MASKED_DX, 'the producer did not consume the hand-off'
+    for name, a, ref in (('dx', x.grad, xs.grad), ('dw1', w1.grad, w1s.grad), ('db1', b1.grad, b1s.grad),
+                         ('dw2', w2.grad, w2s.grad), ('db2', b2.grad, b2s.grad)):
+        e = _err(a.cpu(), ref)
+        assert e < 2e-5 * max(1.0, ref.abs().max().item()), (name, e)
+
+
 @pytest.mark.parametrize('gated', [False, True])
 def test_fused_resblocks_f32_match_torch_fp64(gated):
     """The one-node fp32 ResBlock / GatedResBlock (skip gradients fused into the dX conv epilogue) vs the same
