@@ -22,6 +22,7 @@ ROOT = os.path.dirname(PKG)
 # Build variants: APPLESTAR_BUILD=debug adds -g and device-side bounds asserts (AS_DEBUG);
 # APPLESTAR_HOST_SANITIZE=address|undefined|thread instruments the HOST code only (bindings + the host
 # halves of the .hip launchers, via -Xarch_host); GPU sanitizers / xnack are not used on this pool.
+# APPLESTAR_BUILD=shortpoll: the split-LSTM exchange with the round-2 poll budget of 2^16 passes (diagnostics).
 VARIANT = os.environ.get('APPLESTAR_BUILD', 'release')
 SANITIZE = os.environ.get('APPLESTAR_HOST_SANITIZE', '')
 BUILD = os.path.join(ROOT, 'build', 'csrc' + ('' if VARIANT == 'release' and not SANITIZE else
@@ -57,6 +58,8 @@ def write_ninja() -> str:
                  f'-D__HIP_PLATFORM_AMD__ -Wno-unused-result')
     if VARIANT == 'debug':
         hip_flags += ' -g -DAS_DEBUG'
+    if VARIANT == 'shortpoll':      # diagnostics: the round-2 split-LSTM poll budget (tools/diag/graph_sync_diag.py)
+        hip_flags += ' -DAS_SPLIT_POLL_LIMIT=65536u'
     if SANITIZE:
         hip_flags += f' -Xarch_host -fsanitize={SANITIZE}'
     cxx_flags = ' '.join([

@@ -461,7 +461,7 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
 // by step parity - a producer can run at most one step ahead).  No counter, no fences, no workgroup
 // barrier: the previous counter form (stores -> release -> fetch_add; poll -> acquire -> loads) cost
 // several dependent L2 round trips per step.
-// The poll is bounded: after 2^16 passes (tens of ms) it sets *err and continues (garbage, but the grid drains).
+// The poll is bounded: after kSplitPollLimit passes it sets *err and continues (garbage, but the grid drains).
 constexpr int kSplitKS = 8;
 
 // poll budget of the cross-workgroup exchange (each pass sleeps ~64 clocks plus one L2 round trip: ~2^20
@@ -469,7 +469,10 @@ constexpr int kSplitKS = 8;
 // read with the step's logged scalars: the optimizer update of that step is gated to zero and the learner
 // raises.  The budget is generous on purpose: side-stream kernels can delay the residency of a row's 8
 // workgroups for milliseconds, and a false timeout costs a whole run.
-constexpr unsigned kSplitPollLimit = 1u << 20;
+#ifndef AS_SPLIT_POLL_LIMIT
+#define AS_SPLIT_POLL_LIMIT (1u << 20)     // the 'shortpoll' build variant (csrc/build.py) restores 2^16
+#endif
+constexpr unsigned kSplitPollLimit = AS_SPLIT_POLL_LIMIT;
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;

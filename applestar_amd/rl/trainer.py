@@ -34,10 +34,9 @@ DEFAULT_LEARNER_CONFIG = AttrDict({
         'bucket_mb': 32,
         'comm_dtype': None,
         'amp_dtype': 'bfloat16',
-        # HIP-graph capture of the whole step (runtime/step_graph.py); GPU only.  Off by default: on ROCm 7
-        # a replay of the ~2,400-node step graph costs ~23 ms of host time (~9.5 us per node, vs ~16 us
-        # per eager launch) and the replayed step ran 2.6 ms slower on the GPU (bench r2d/r2e:
-        # 45.8 vs 43.2 ms/step), so the eager step wins until the launch count is much lower
+        # HIP-graph capture of the whole step (runtime/step_graph.py); GPU only.  Off by default: a replay
+        # issues in ~1.5 ms of host time, but the captured step runs 29.8 vs 27.3 ms on the GPU (bf16,
+        # profiles/r3l_graph_sync_probe.txt) - it pays only when the host, not the GPU, is the bottleneck
         'graph_step': False,
     },
     'model': {'enable_baselines': ['winloss']},

@@ -1,12 +1,22 @@
 """Whole learner step as HIP graphs: forward + loss + backward in one graph, clip + Adam + weight
 publish in a second; the data-parallel gradient all-reduce (RCCL) runs eagerly between the two.
 
-An RL learner step is ~2,400 kernel launches; eagerly each costs ~16 us of host time (PyTorch
-dispatch + autograd).  Measured on MI355X / ROCm 7 (profiles/r2e_*): replaying the step graph costs
-~23 ms of host time (~9.5 us per node: the HIP runtime still submits node by node) and the replayed
-step ran 2.6 ms slower on the GPU than the eager one, so RLTrainer keeps this opt-in
-(``learner.graph_step``) until fusion has cut the node count; the machinery (static shapes, eager
+An RL learner step is ~1,250 kernel launches (bf16); eagerly each costs ~16 us of host time (PyTorch
+dispatch + autograd).  Measured on MI355X / ROCm 7 (profiles/r3l_graph_sync_probe.txt): a replay issues in
+~1.5 ms of host time and the step is then GPU-bound at 29.8 ms, vs 27.3 ms for the eager step (the captured
+step keeps torch's capturable Adam and per-call weight forms instead of the fused clip+Adam and the cached
+derived weights), so RLTrainer keeps this opt-in (``learner.graph_step``): it pays where the host is the
+bottleneck (many ranks per node contending for CPU), not on an idle host.  The machinery (static shapes, eager
 warm-up, shared pool, the DP all-reduce between the two graphs) is tested for equivalence.
+
+Host waits: round 2 needed a host synchronize after each replay (without it, eager work behind a replay read
+an inf gradient norm).  The probe (tools/diag/graph_sync_diag.py) snapshots the graph's outputs from the
+stream right behind the replay and compares them with the settled values: with the current code every
+snapshot matches and nothing is non-finite over 12 replays - alone, interleaved with an eager trainer, with
+private pools, and even with the round-2 split-LSTM poll budget rebuilt in (the 'shortpoll' variant).  The
+failure went away with the removal of the per-parameter gradient hooks (parallel/dp.py, round 3), whose
+AccumulateGrad work was bound to the stream of an earlier step; so the waits are gone (opt back in with
+APPLESTAR_GRAPH_HOST_SYNC=1 when debugging).
 
 Shapes must be static per graph.  The one data-dependent shape of the learner step, the packed entity
 count, is fixed by packing to ``encoders.entity_pad_for(total, N)`` rows (``EntityEncoder._forward_padded``:
@@ -96,6 +106,11 @@ class GraphedTrainStep:
         self.single_graph = not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
         # forked side streams (value / scalar encoders) inside the capture; off: captured on one stream
         self.side_streams = os.environ.get('APPLESTAR_GRAPH_SIDE_STREAMS', '0') == '1'
+        # host waits after the replays (module docstring: no longer needed); APPLESTAR_GRAPH_HOST_SYNC=1 for debugging
+        self.host_sync = os.environ.get('APPLESTAR_GRAPH_HOST_SYNC', '0') == '1'
+        # one private memory pool per graph instead of one shared pool (diagnostics)
+        self.private_pools = os.environ.get('APPLESTAR_GRAPH_PRIVATE_POOLS', '0') == '1'
+        self.after_replay: Optional[Callable[[_Entry], None]] = None    # diagnostics hook, before any host wait
 
     def _eager(self, batch):
         info = self.fwd_bwd(batch)
@@ -107,7 +122,7 @@ class GraphedTrainStep:
     def _capture(self, key, batch) -> _Entry:
         if len(self._graphs) >= self.max_graphs:
             self._graphs.popitem(last=False)
-        if self._pool is None:
+        if self._pool is None or self.private_pools:
             self._pool = torch.cuda.graph_pool_handle()
         e = _Entry()
         e.static_in = _tree_clone(batch)
@@ -150,22 +165,20 @@ class GraphedTrainStep:
         _tree_copy_(e.static_in, batch)
         t1 = time.perf_counter()
         e.fb.replay()
+        if self.after_replay is not None:
+            self.after_replay(e)
         if self.check_fn is not None:      # debugging hook between the two graphs
             self.check_fn()
         t2 = time.perf_counter()
         if e.upd is not None:
-            # ROCm 7: a graph launched right behind another on the same stream was seen reading the first
-            # graph's outputs before they landed (test_graphed_train_step_matches_eager: inf gradient norm
-            # unless the host waited in between), so the multi-rank path waits for the stream here
-            torch.cuda.current_stream(self.device).synchronize()
+            if self.host_sync:
+                torch.cuda.current_stream(self.device).synchronize()
             self.reduce()
         t3 = time.perf_counter()
         if e.upd is not None:
             e.upd.replay()
-        # ROCm 7 workaround: without a host wait here, eager work queued behind the replay (the output
-        # copy below) read an inf gradient norm on the second replay of a graph
-        # (test_graphed_train_step_matches_eager fails 6/6 without it, passes with it)
-        torch.cuda.current_stream(self.device).synchronize()
+        if self.host_sync:
+            torch.cuda.current_stream(self.device).synchronize()
         t4 = time.perf_counter()
         for k, dt in (('copy_in', t1 - t0), ('replay_fwd_bwd', t2 - t1), ('reduce', t3 - t2), ('replay_update', t4 - t3)):
             t[k] = t.get(k, 0.0) + dt
