@@ -13,10 +13,11 @@ Host waits: round 2 needed a host synchronize after each replay (without it, eag
 an inf gradient norm).  The probe (tools/diag/graph_sync_diag.py) snapshots the graph's outputs from the
 stream right behind the replay and compares them with the settled values: with the current code every
 snapshot matches and nothing is non-finite over 12 replays - alone, interleaved with an eager trainer, with
-private pools, and even with the round-2 split-LSTM poll budget rebuilt in (the 'shortpoll' variant).  The
-failure went away with the removal of the per-parameter gradient hooks (parallel/dp.py, round 3), whose
-AccumulateGrad work was bound to the stream of an earlier step; so the waits are gone (opt back in with
-APPLESTAR_GRAPH_HOST_SYNC=1 when debugging).
+private pools, and even with the round-2 split-LSTM poll budget rebuilt in (the 'shortpoll' variant), which
+rules the LSTM exchange out.  The change on this path since round 2 is the removal of the per-parameter
+gradient hooks (parallel/dp.py, round 3), whose AccumulateGrad work was bound to the stream of an earlier
+step - the likely cause, not reproduced in isolation.  The waits are gone (APPLESTAR_GRAPH_HOST_SYNC=1 puts
+them back when debugging).
 
 Shapes must be static per graph.  The one data-dependent shape of the learner step, the packed entity
 count, is fixed by packing to ``encoders.entity_pad_for(total, N)`` rows (``EntityEncoder._forward_padded``:
