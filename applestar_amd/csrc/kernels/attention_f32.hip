@@ -51,7 +51,9 @@ __device__ __forceinline__ int swz(int r, int d) { return r * P + (d ^ (((r >> 3
 // [64 x 128] fp32 tile rows r0.. (rows >= nvalid zero) from a row-strided global matrix into LDS T[64][P]
 // (swizzled)
 __device__ __forceinline__ void stage_tile(float* T, const float* __restrict__ base, long ld, int r0, int nvalid) {
-  const int t = threadIdx.x, r = t >> 2, c = t & 3;
+  // the 8 contiguous lanes of a ds_write_b128 bank group take 8 rows of one 32-float column (row r at
+  // 4 r mod 32: disjoint windows); four columns of two rows per group were 4-way conflicts
+  const int t = threadIdx.x, r = (t & 7) + 8 * (t >> 5), c = (t >> 3) & 3;
   const bool ok = r0 + r < nvalid;
   const float4* src = reinterpret_cast<const float4*>(base + static_cast<long>(ok ? r0 + r : 0) * ld + 32 * c);
   float4 v[8];

@@ -15,7 +15,10 @@
 // 8(r>>2) + 4(l>>5)][col l&31] in 16 accumulators.  The k-slot assignment is free as long as A and B agree:
 // k-step kk of a 16-channel K-step gives lane half h channel 8h + kk, so a lane's 8 k-steps of a fragment are
 // 8 consecutive floats of one LDS row (two ds_read_b128).  LDS rows are 20 floats: 20 = 4 mod 16, the 16
-// rows read by a 16-lane group land on 16 distinct 4-bank groups.  The epilogue stores straight from the
+// rows read by a 16-lane group land on 16 distinct 4-bank groups.  Staging pieces (16 B) are dealt so that
+// the 8 contiguous lanes of a ds_write_b128 bank group write 8 different rows of one 4-float column (row
+// pitches 20 r mod 32 for r = 0..7 are disjoint 4-bank windows; row-major dealing put two rows' 16 floats
+// on overlapping banks: 2-way on every staging write).  The epilogue stores straight from the
 // accumulators: 32 lanes write 32 consecutive channels (128 B) of one pixel.
 #include "../common.h"
 #include "../kernels.h"
@@ -29,6 +32,9 @@ constexpr int kOOB = 0x7ffffff0;
 
 template <int BN_>
 struct ConvF32Cfg {
+  // 16-B piece idx -> (tile row, 4-float column): 8 consecutive pieces = 8 rows of one column
+  static __device__ __forceinline__ int prow(int idx) { return (idx & 7) + 8 * (idx >> 5); }
+  static __device__ __forceinline__ int pcol(int idx) { return (idx >> 3) & 3; }
   static constexpr int BM = 128, BN = BN_, BK = 16, NT = 256;
   static constexpr int WN = BN_ >= 128 ? 2 : 1;   // waves along N
   static constexpr int WM = 4 / WN;                // waves along M
@@ -76,8 +82,8 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
 #pragma unroll
   for (int i = 0; i < C::A_IT; ++i) {
     const int idx = tid + i * C::NT;
-    a_row[i] = idx >> 2;
-    a_c4[i] = idx & 3;
+    a_row[i] = C::prow(idx);
+    a_c4[i] = C::pcol(idx);
     const long m = m0 + a_row[i];
     a_pix[i] = static_cast<int>(m);
     a_ok[i] = 0;
@@ -95,7 +101,7 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
 #pragma unroll
   for (int i = 0; i < C::B_IT; ++i) {
     const int idx = tid + i * C::NT;
-    const int n = idx >> 2, c4 = idx & 3;
+    const int n = C::prow(idx), c4 = C::pcol(idx);
     b_off[i] = (idx < C::B_PIECES && n0 + n < Cout) ? ((n0 + n) * K + 4 * c4) * 4 : kOOB;
   }
 
@@ -126,7 +132,7 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
     for (int i = 0; i < C::B_IT; ++i) {
       const int idx = tid + i * C::NT;
       if (C::B_PIECES % C::NT == 0 || idx < C::B_PIECES)
-        *reinterpret_cast<uint4*>(Bs + (idx >> 2) * C::P + 4 * (idx & 3)) = rb[i];
+        *reinterpret_cast<uint4*>(Bs + C::prow(idx) * C::P + 4 * C::pcol(idx)) = rb[i];
     }
   };
 

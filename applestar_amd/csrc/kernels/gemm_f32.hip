@@ -34,6 +34,10 @@ struct GemmF32Cfg {
   static constexpr int BM = 128, BN = BN_, BK = BK_, NT = 256;
   static constexpr int CH = BK / 4;            // 16-B pieces per tile row
   static constexpr int KH = BK / 2;            // floats per lane half per stage (= MFMA k-steps)
+  // 16-B piece idx -> (tile row, column piece): 8 consecutive pieces = 8 rows of one column piece, so the 8
+  // contiguous lanes of a ds_write_b128 bank group hit disjoint banks (as conv3x3_f32.hip)
+  static __device__ __forceinline__ int prow(int idx) { return (idx & 7) + 8 * (idx / (8 * CH)); }
+  static __device__ __forceinline__ int pcol(int idx) { return (idx >> 3) % CH; }
   static constexpr int WN = BN_ >= 128 ? 2 : 1, WM = 4 / WN;
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 32, FN = TN / 32;
@@ -70,8 +74,8 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 #pragma unroll
   for (int i = 0; i < C::A_IT; ++i) {
     const int idx = tid + i * C::NT;
-    a_row[i] = idx / C::CH;
-    a_c4[i] = idx % C::CH;
+    a_row[i] = C::prow(idx);
+    a_c4[i] = C::pcol(idx);
     const long m = m0 + a_row[i];
     a_base[i] = m < M ? static_cast<int>(m * K) : -1;
   }
@@ -79,7 +83,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 #pragma unroll
   for (int i = 0; i < C::B_IT; ++i) {
     const int idx = tid + i * C::NT;
-    const int n = idx / C::CH;
+    const int n = C::prow(idx);
     b_base[i] = (idx < C::B_PIECES && n0 + n < N) ? (n0 + n) * K : -1;
   }
 
@@ -95,7 +99,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     }
 #pragma unroll
     for (int i = 0; i < C::B_IT; ++i) {
-      const int k = k0 + 4 * ((tid + i * C::NT) % C::CH);
+      const int k = k0 + 4 * C::pcol(tid + i * C::NT);
       const int off = (b_base[i] >= 0 && k < K) ? (b_base[i] + k) * 4 : kOOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(br, off, 0, 0);
       rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
@@ -110,7 +114,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     for (int i = 0; i < C::B_IT; ++i) {
       const int idx = tid + i * C::NT;
       if (C::B_PIECES % C::NT == 0 || idx < C::B_PIECES)
-        *reinterpret_cast<uint4*>(Bs + (idx / C::CH) * C::P + 4 * (idx % C::CH)) = rb[i];
+        *reinterpret_cast<uint4*>(Bs + C::prow(idx) * C::P + 4 * C::pcol(idx)) = rb[i];
     }
   };
 

@@ -55,6 +55,18 @@ def main():
             x = torch.randn(M, K, device='cuda')
             dy = torch.randn(M, N, device='cuda')
             emit('wgrad_f32_dense', [M, N, K], timed(lambda: C.wgrad_f32(dy, x, 0, True)), 2.0 * M * N * K)
+    if which == 'tail':
+        # wave quantization probe: 768 resident 128x128 tiles (3 per CU); time should step at whole rounds
+        for M in (49000, 50000, 98000, 99000, 100000, 147000, 148000):
+            a = torch.randn(M, 256, device='cuda')
+            b = torch.randn(256, 256, device='cuda')
+            emit('gemm_f32_tail', [M, 256, 256, (M + 127) // 128 * 2], timed(lambda: C.gemm_f32(a, b, None, None, 0)),
+                 2.0 * M * 256 * 256)
+        for B in (130, 200, 259, 260, 390):
+            x = torch.randn(B, 19, 20, 128, device='cuda')
+            w = torch.randn(128, 3, 3, 128, device='cuda') / 30
+            emit('conv3x3_f32_tail', [B, 19, 20, 128, 128, (B * 380 + 127) // 128],
+                 timed(lambda: C.conv3x3_f32(x, w, None, None, 0)), 2.0 * B * 380 * 128 * 9 * 128)
     if which in ('gemm', 'all'):
         for M, N, K in GEMM:
             a = torch.randn(M, K, device='cuda')
