@@ -108,7 +108,10 @@ def test_metrics_match_reference():
     assert torch.equal(hamming_distance(x, y), m.hamming_distance(x, y))
 
 
-def _run_episode(job_type, steps=900, traj_len=3, value_feature=False):
+def _run_episode(job_type, steps=900, traj_len=3, value_feature=False, until_full=None):
+    """Play one fake-env episode with two agents; train jobs collect trajectories.  ``until_full``: stop once
+    that many full (traj_len + 1 step) trajectories exist - the trajectory tests need a handful, not the
+    whole 900-step episode (~10 min of CPU forwards)."""
     torch.manual_seed(0)
     random.seed(0)
     cfg = {'actor': {'job_type': job_type, 'traj_len': traj_len}, 'common': {'type': 'rl'},
@@ -131,6 +134,8 @@ def _run_episode(job_type, steps=900, traj_len=3, value_feature=False):
                 if t:
                     trajs.append(t)
         obs = nobs
+        if until_full is not None and sum(len(t) == traj_len + 1 for t in trajs) >= until_full:
+            break
     return agents, trajs, acts_seen, rew
 
 
@@ -146,7 +151,7 @@ def test_agent_eval_episode_actions_valid():
 
 def test_agent_train_trajectories_collate_and_learn():
     from applestar_amd.rl.trainer import RLTrainer
-    _, trajs, _, _ = _run_episode('train_test', traj_len=3, value_feature=True)
+    _, trajs, _, _ = _run_episode('train_test', traj_len=3, value_feature=True, until_full=6)
     full = [t for t in trajs if len(t) == 4]
     assert len(full) >= 2
     step = full[0][0]
@@ -181,7 +186,7 @@ def test_trajectory_ring_matches_host_collate():
     """The HBM ring's on-device batch assembly reproduces collate_trajectories exactly (host path)."""
     from applestar_amd.runtime.traj_ring import TrajectoryRing
     from applestar_amd.utils import serialize
-    _, trajs, _, _ = _run_episode('train_test', traj_len=3, value_feature=True)
+    _, trajs, _, _ = _run_episode('train_test', traj_len=3, value_feature=True, until_full=6)
     full = [t for t in trajs if len(t) == 4][:3]
     ref = collate_trajectories(full)
     ring = TrajectoryRing(64 << 20, device='cpu')

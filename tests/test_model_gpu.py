@@ -50,7 +50,7 @@ def test_trajectory_ring_on_gpu_matches_host_collate():
     from applestar_amd.agent.collate import collate_trajectories
     from applestar_amd.runtime.traj_ring import TrajectoryRing
     from applestar_amd.utils import serialize
-    _, trajs, _, _ = _run_episode('train_test', traj_len=3, value_feature=True)
+    _, trajs, _, _ = _run_episode('train_test', traj_len=3, value_feature=True, until_full=6)
     full = [t for t in trajs if len(t) == 4][:3]
     ref = collate_trajectories(full)
     ring = TrajectoryRing(256 << 20, device='cuda')

@@ -87,7 +87,7 @@ def test_rl_dataloader_ring_mode_cpu():
     from applestar_amd.comm.adapter import Coordinator, serve_coordinator, Adapter
     from applestar_amd.learner.dataloader import RLDataLoader
     from test_agent import _run_episode
-    _, trajs, _, _ = _run_episode('train_test', traj_len=3)
+    _, trajs, _, _ = _run_episode('train_test', traj_len=3, until_full=6)
     full = [t for t in trajs if len(t) == 4][:4]
     srv = serve_coordinator(Coordinator(), '127.0.0.1', 0)
     port = srv.server_address[1]
