@@ -9,7 +9,10 @@
   token ``sl_traj`` and the loader pulls them instead;
 * batching: ``batch_size`` slots, each consuming consecutive ``trajectory_length`` chunks of ONE
   replay so the learner can carry the LSTM state (``new_episodes`` marks a slot's first chunk); a
-  short final chunk is padded by repeating its last step with every action mask off.
+  short final chunk is padded by repeating its last step with every action mask off;
+* the shared batch (``sl_dataloader.py:19-94``): on a GPU a collator process packs every batch into one of
+  three pinned shared-memory slabs and the learner copies it to HBM with one async DMA on a side stream
+  (``runtime/shared_batch.py``), so collation and the H2D copy overlap the previous step.
 """
 from __future__ import annotations
 
@@ -61,47 +64,14 @@ def _decode_worker(cfg_dict, jobs, out_q):
     out_q.put(None)
 
 
-class ReplayDataLoader:
-    def __init__(self, cfg, device='cpu', rank: int = 0, world_size: int = 1, source: Optional[Iterator] = None):
-        d = cfg.learner.data
-        self.B, self.T = int(d.batch_size), int(d.trajectory_length)
-        self.device = torch.device(device)
-        self._procs = []
-        if source is not None:                    # injected trajectory iterator (tests / custom sources)
-            self._source = source
-        elif d.get('remote', False):              # replay actors push to the coordinator
-            from ..comm.adapter import Adapter
-            ad = Adapter(cfg.communication.coordinator_ip, cfg.communication.coordinator_port)
-            self._source = self._pull_remote(ad)
-        else:
-            ctx = mp.get_context('spawn')
-            self._jobs, self._out = ctx.Queue(), ctx.Queue(maxsize=4 * self.B)
-            for p in replay_paths(d.train_data_file, d.get('epochs', 1), rank, world_size):
-                for player in (0, 1):
-                    self._jobs.put((p, player))
-            n = int(d.get('num_workers', 1))
-            for _ in range(n):
-                self._jobs.put(None)
-                pr = ctx.Process(target=_decode_worker, args=(dict(cfg), self._jobs, self._out), daemon=True)
-                pr.start()
-                self._procs.append(pr)
-            self._source = self._pull_local(n)
-        self._slots = [None] * self.B            # (trajectory, cursor)
+class _SlotAssembler:
+    """``batch_size`` slots, each consuming consecutive ``trajectory_length`` chunks of ONE trajectory (the
+    learner carries the LSTM state per slot; ``new_episodes`` marks a slot's first chunk); a short final chunk
+    is padded by repeating its last step with every action mask off.  Yields collated host batches."""
 
-    def _pull_local(self, n_workers: int):
-        done = 0
-        while done < n_workers:
-            item = self._out.get()
-            if item is None:
-                done += 1
-                continue
-            yield serialize.loads(item)
-
-    @staticmethod
-    def _pull_remote(adapter):
-        while True:
-            for t in adapter.pull('sl_traj', size=1, block=True):
-                yield t
+    def __init__(self, source: Iterator, B: int, T: int):
+        self._source, self.B, self.T = source, B, T
+        self._slots = [None] * B            # (trajectory, cursor)
 
     def _chunk(self, b: int):
         new = False
@@ -129,14 +99,107 @@ class ReplayDataLoader:
             lens.append(n)
             news.append(new)
         batch = collate_obs(steps)                 # batch-major [B*T], entities padded to the max
-        batch['traj_lens'] = lens
+        batch['traj_lens'] = lens                  # host lists: ride in the slab layout, never on the device
         batch['new_episodes'] = news
-        if self.device.type != 'cpu':
-            from ..rl.synthetic import to_device
-            batch = to_device(batch, self.device)
         return batch
 
+
+def _pull_local(out_q, n_workers: int):
+    done = 0
+    while done < n_workers:
+        item = out_q.get()
+        if item is None:
+            done += 1
+            continue
+        yield serialize.loads(item)
+
+
+def _pull_remote(ip, port):
+    from ..comm.adapter import Adapter
+    adapter = Adapter(ip, port)
+    while True:
+        for t in adapter.pull('sl_traj', size=1, block=True):
+            yield t
+
+
+class _CollatorBatches:
+    """Picklable batch factory run inside the shared-batch collator process: builds the trajectory source
+    there (decode-worker queue, remote coordinator, or a user factory) and assembles batches from it."""
+
+    def __init__(self, B, T, kind, *args):
+        self.B, self.T, self.kind, self.args = B, T, kind, args
+
+    def __call__(self):
+        if self.kind == 'local':
+            src = _pull_local(*self.args)
+        elif self.kind == 'remote':
+            src = _pull_remote(*self.args)
+        else:
+            src = iter(self.args[0]())
+        return _SlotAssembler(src, self.B, self.T)
+
+
+class ReplayDataLoader:
+    """SL batches from replay trajectories.  On a GPU (or with ``learner.data.shared_batch``) a collator process
+    packs each batch into a pinned shared-memory slab and the learner issues one async H2D copy of it
+    (runtime/shared_batch.py); otherwise batches are collated in-process.  ``source``: an injected trajectory
+    iterator (in-process); ``source_factory``: a picklable callable returning one (usable by the collator)."""
+
+    def __init__(self, cfg, device='cpu', rank: int = 0, world_size: int = 1, source: Optional[Iterator] = None,
+                 source_factory=None):
+        d = cfg.learner.data
+        self.B, self.T = int(d.batch_size), int(d.trajectory_length)
+        self.device = torch.device(device)
+        self._procs = []
+        self._shared = None
+        if source is not None:                    # injected trajectory iterator (tests / custom sources)
+            spec = None
+            src = source
+        elif source_factory is not None:
+            spec = ('factory', source_factory)
+        elif d.get('remote', False):              # replay actors push to the coordinator
+            spec = ('remote', cfg.communication.coordinator_ip, cfg.communication.coordinator_port)
+        else:
+            ctx = mp.get_context('spawn')
+            jobs, out = ctx.Queue(), ctx.Queue(maxsize=4 * self.B)
+            for p in replay_paths(d.train_data_file, d.get('epochs', 1), rank, world_size):
+                for player in (0, 1):
+                    jobs.put((p, player))
+            n = int(d.get('num_workers', 1))
+            for _ in range(n):
+                jobs.put(None)
+                pr = ctx.Process(target=_decode_worker, args=(dict(cfg), jobs, out), daemon=True)
+                pr.start()
+                self._procs.append(pr)
+            spec = ('local', out, n)
+        use_shared = bool(d.get('shared_batch', self.device.type == 'cuda')) and spec is not None
+        if use_shared:
+            from ..runtime.shared_batch import SharedBatchLoader
+            self._shared = SharedBatchLoader(_CollatorBatches(self.B, self.T, *spec), self.device,
+                                             n_slabs=int(d.get('shared_slabs', 3)),
+                                             slab_bytes=int(d.get('slab_mb', 512)) << 20)
+            self._iter = self._shared
+        else:
+            if spec is not None:
+                src = _CollatorBatches(1, 1, *spec)()._source
+            self._iter = self._in_process(_SlotAssembler(src, self.B, self.T))
+
+    def _in_process(self, assembler):
+        for batch in assembler:
+            if self.device.type != 'cpu':
+                from ..rl.synthetic import to_device
+                batch = to_device(batch, self.device)
+            yield batch
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        return next(self._iter)
+
     def close(self):
+        if self._shared is not None:
+            self._shared.close()
         for p in self._procs:
             p.terminate()
 

@@ -122,3 +122,29 @@ def sl_batch(batch_size: int, traj_len: int, max_entities: int = MAX_ENTITY_NUM,
 
 
 to_device = _tree_to
+
+
+def sl_trajectory(length: int, seed: int = 0, max_entities: int = 12):
+    """A decoded-replay-shaped trajectory (list of per-step dicts with the ReplayDecoder's keys, entities and
+    selected units trimmed to their counts) of random observations / actions, for SL data-path tests."""
+    g = torch.Generator().manual_seed(seed)
+    steps = []
+    for _ in range(length):
+        o = random_obs(1, max_entities=max_entities, generator=g)
+        a, su = random_actions(1, o['entity_num'], generator=g)
+        n = int(o['entity_num'][0])
+        steps.append({
+            'spatial_info': {k: v[0] for k, v in o['spatial_info'].items()},
+            'entity_info': {k: v[0][:n] for k, v in o['entity_info'].items()},
+            'scalar_info': {k: v[0] for k, v in o['scalar_info'].items()},
+            'entity_num': o['entity_num'][0], 'selected_units_num': su[0],
+            'action_info': {k: v[0][:max(int(su[0]), 1)] if k == 'selected_units' else v[0] for k, v in a.items()},
+            'action_mask': {'action_type': torch.tensor(True), 'delay': torch.tensor(True),
+                            **{k: v[0].bool() for k, v in actions_mask(a['action_type']).items()}}})
+    return steps
+
+
+def sl_trajectories(lengths, seed: int = 0, max_entities: int = 12):
+    """Iterator of :func:`sl_trajectory` (picklable through functools.partial: a collator-process source)."""
+    for i, L in enumerate(lengths):
+        yield sl_trajectory(L, seed + i, max_entities)

@@ -353,3 +353,34 @@ def test_fused_rl_loss_matches_torch_loss(only_value, bo_pg_weight):
             continue
         a = torch.zeros_like(r) if a is None else a
         assert float((a - r).abs().max()) <= 1e-5 + 1e-4 * float(r.abs().max())
+
+
+def test_replay_dataloader_shared_batch_gpu():
+    """SL shared batch on the GPU: collator process -> hipHostRegister'ed shared slab -> one async H2D per
+    batch on a side stream; the device batches equal the in-process host collation of the same data."""
+    import functools
+    from applestar_amd.learner.replay_dataloader import ReplayDataLoader
+    from applestar_amd.rl.synthetic import sl_trajectories
+    from applestar_amd.utils.config import AttrDict
+    lengths = [9, 3, 4, 6, 4, 7, 2, 8, 5]
+    cfg = AttrDict({'learner': {'data': {'batch_size': 3, 'trajectory_length': 4, 'slab_mb': 32}}})
+    shared = ReplayDataLoader(cfg, device='cuda', source_factory=functools.partial(sl_trajectories, lengths, 5))
+    plain = ReplayDataLoader(cfg, source=sl_trajectories(lengths, 5))
+    assert shared._shared is not None and len(shared._shared._registered) == 3   # pinned slabs
+
+    def cmp(a, b, path=''):
+        if isinstance(a, dict):
+            for k in b:
+                cmp(a[k], b[k], f'{path}/{k}')
+        elif isinstance(a, (list, tuple)):
+            for x, y in zip(a, b):
+                cmp(x, y, path)
+        elif torch.is_tensor(a):
+            assert a.is_cuda and torch.equal(a.cpu(), b), path
+        else:
+            assert a == b, path
+    try:
+        for _ in range(5):
+            cmp(next(shared), next(plain))
+    finally:
+        shared.close()

@@ -42,26 +42,9 @@ def test_replay_dataloader_slots_carry_and_pad():
     padded with masked steps, and the batch trains."""
     import torch
     from applestar_amd.learner.replay_dataloader import ReplayDataLoader
-    from applestar_amd.lib.features import random_obs, random_actions, actions_mask
     from applestar_amd.utils.config import AttrDict
 
-    def traj(L, seed):
-        g = torch.Generator().manual_seed(seed)
-        steps = []
-        for i in range(L):
-            o = random_obs(1, max_entities=12, generator=g)
-            a, su = random_actions(1, o['entity_num'], generator=g)
-            one = lambda t: t[0]
-            s = {'spatial_info': {k: one(v) for k, v in o['spatial_info'].items()},
-                 'entity_info': {k: one(v)[:int(o['entity_num'][0])] for k, v in o['entity_info'].items()},
-                 'scalar_info': {k: one(v) for k, v in o['scalar_info'].items()},
-                 'entity_num': o['entity_num'][0], 'selected_units_num': su[0],
-                 'action_info': {k: one(v)[:max(int(su[0]), 1)] if k == 'selected_units' else one(v)
-                                 for k, v in a.items()},
-                 'action_mask': {'action_type': torch.tensor(True), 'delay': torch.tensor(True),
-                                 **{k: one(v).bool() for k, v in actions_mask(a['action_type']).items()}}}
-            steps.append(s)
-        return steps
+    from applestar_amd.rl.synthetic import sl_trajectory as traj
     src = iter([traj(5, 0), traj(3, 1), traj(4, 2), traj(6, 3), traj(4, 4)])
     cfg = AttrDict({'learner': {'data': {'batch_size': 2, 'trajectory_length': 4}}})
     dl = ReplayDataLoader(cfg, source=src)
@@ -75,3 +58,39 @@ def test_replay_dataloader_slots_carry_and_pad():
     tr = SLTrainer({'learner': {'data': {'batch_size': 2, 'trajectory_length': 4}, 'ignore_steps': 0}}, device='cpu')
     info = tr.step(b1)
     assert torch.isfinite(info['total_loss'])
+
+
+def test_replay_dataloader_shared_batch_process_matches_in_process():
+    """The shared-batch path (collator process -> shared slab -> views) yields exactly the batches of the
+    in-process path for the same trajectories, slot bookkeeping included."""
+    import functools
+    import torch
+    from applestar_amd.learner.replay_dataloader import ReplayDataLoader
+    from applestar_amd.rl.synthetic import sl_trajectories
+    from applestar_amd.utils.config import AttrDict
+    lengths = [5, 3, 4, 6, 4, 7, 2]
+    cfg = AttrDict({'learner': {'data': {'batch_size': 2, 'trajectory_length': 4, 'shared_batch': True,
+                                         'slab_mb': 16}}})
+    shared = ReplayDataLoader(cfg, source_factory=functools.partial(sl_trajectories, lengths, 3))
+    plain = ReplayDataLoader(AttrDict({'learner': {'data': {'batch_size': 2, 'trajectory_length': 4}}}),
+                             source=sl_trajectories(lengths, 3))
+    assert shared._shared is not None and plain._shared is None
+
+    def cmp(a, b, path=''):
+        if isinstance(a, dict):
+            assert set(a) == set(b), path
+            for k in a:
+                cmp(a[k], b[k], f'{path}/{k}')
+        elif isinstance(a, (list, tuple)):
+            assert len(a) == len(b), path
+            for x, y in zip(a, b):
+                cmp(x, y, path)
+        elif torch.is_tensor(a):
+            assert a.dtype == b.dtype and torch.equal(a, b), path
+        else:
+            assert a == b, path
+    try:
+        for _ in range(4):
+            cmp(next(shared), next(plain))
+    finally:
+        shared.close()
