@@ -11,8 +11,9 @@ MI355X design:
 * dynamic batching: the server waits on all pipes (``connection.wait``), then keeps collecting until
   either every live worker has a request queued or ``max_wait_ms`` passed, and runs ONE forward per
   (player, kind) group over only the rows that asked — padded to the group's max entity count;
-* the batched input is assembled in pinned host memory and copied with ``non_blocking``;
-  outputs come back with one D2H copy per group;
+* the batched input is packed into ONE pinned host buffer and copied with one ``non_blocking`` DMA
+  (``runtime.prefetch.pack_tree``); the outputs come back with non-blocking D2H copies and a single stream
+  synchronize per group (per-tensor blocking copies cost a host round trip each);
 * on the GPU each (player, kind, power-of-two batch bucket) is a HIP graph (``runtime.graphs.GraphedPolicy``,
   entities padded to MAX_ENTITY_NUM): B = 1 agent step 8.7 ms eager -> 3.1 ms replayed.
 """
@@ -107,20 +108,28 @@ class InferenceServer:
             from ..runtime.graphs import GraphedPolicy
             bp = 1 << (len(inputs) - 1).bit_length()                   # batch bucket (power of two)
             rows = list(inputs) + [inputs[0]] * (bp - len(inputs))      # dummy rows, never returned
-            batch = _to(collate_obs(rows, pad_entities=MAX_ENTITY_NUM), self.device)
+            t0 = time.perf_counter()
+            batch = _packed_to(collate_obs(rows, pad_entities=MAX_ENTITY_NUM), self.device)
+            self.stats['collate_h2d_s'] += time.perf_counter() - t0
             key = (player_id, kind, bp)
             gp = self._graphed.get(key)
             if gp is None:
                 gp = self._graphed[key] = GraphedPolicy(
                     model, 'compute_logp_action' if kind == 'policy' else 'compute_teacher_logit')
+            t0 = time.perf_counter()
             out = gp(**batch)
+            self.stats['launch_s'] += time.perf_counter() - t0
         else:
             batch = _to(collate_obs(inputs), self.device)
             ctx = torch.autocast('cuda', dtype=self.amp_dtype) if self.amp_dtype else _null()
             with torch.no_grad(), ctx:
                 out = model.compute_logp_action(**batch) if kind == 'policy' else model.compute_teacher_logit(**batch)
-        out = _to_cpu(out)                       # copies the (graph-static) outputs before the next replay
+        t0 = time.perf_counter()
+        out = _to_cpu(out, self.device)          # copies the (graph-static) outputs before the next replay
+        self.stats['d2h_wait_s'] += time.perf_counter() - t0
+        t0 = time.perf_counter()
         res = [decollate_output(out, i) for i in range(len(inputs))]
+        self.stats['decollate_s'] += time.perf_counter() - t0
         if kind == 'policy':
             for r in res:
                 r['model_last_iter'] = self.model_iter[player_id]
@@ -187,11 +196,25 @@ class _null:
         return False
 
 
-def _to_cpu(tree):
-    if isinstance(tree, torch.Tensor):
-        return tree.detach().to('cpu', non_blocking=False)
-    if isinstance(tree, dict):
-        return {k: _to_cpu(v) for k, v in tree.items()}
-    if isinstance(tree, (list, tuple)):
-        return type(tree)(_to_cpu(v) for v in tree)
-    return tree
+def _packed_to(batch, device):
+    """Host batch -> device: one pinned buffer, one async copy (CPU: unchanged)."""
+    if device.type != 'cuda':
+        return batch
+    from ..runtime.prefetch import pack_tree
+    return pack_tree(batch, pin=True).to_device(device)
+
+
+def _to_cpu(tree, device=None):
+    """Device outputs -> host: every copy non-blocking into pinned memory, then ONE stream synchronize."""
+    def issue(x):
+        if isinstance(x, torch.Tensor):
+            return x.detach().to('cpu', non_blocking=x.is_cuda)
+        if isinstance(x, dict):
+            return {k: issue(v) for k, v in x.items()}
+        if isinstance(x, (list, tuple)):
+            return type(x)(issue(v) for v in x)
+        return x
+    out = issue(tree)
+    if device is not None and device.type == 'cuda':
+        torch.cuda.current_stream(device).synchronize()
+    return out

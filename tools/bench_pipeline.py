@@ -122,10 +122,14 @@ def main():
     t0 = time.time()
     st0 = probe.stats()
     it0 = iters[-1][1] if iters else 0
+    srv_stats = lambda: dict(actor._server.stats) if getattr(actor, '_server', None) is not None else {}
+    ss0 = srv_stats()
     time.sleep(args.seconds)
     t1 = time.time()
     st1 = probe.stats()
     it1 = iters[-1][1] if iters else 0
+    ss1 = srv_stats()
+    sd = {k: ss1.get(k, 0.0) - ss0.get(k, 0.0) for k in ss1}
     pushed = st1.get('push', {}).get('MP0traj', 0) - st0.get('push', {}).get('MP0traj', 0)
     dt = t1 - t0
     n_it = it1 - it0
@@ -138,6 +142,12 @@ def main():
            'learner_samples_per_s_fed': round(n_it * B * T / dt, 1),
            'fresh_samples_per_s': round(pushed * T / dt, 1),
            'startup_s': round(t0 - t_start, 1),
+           'inference_server': {
+               'groups_per_s': round(sd.get('batches', 0) / dt, 1),
+               'mean_group_rows': round(sd.get('requests', 0) / max(sd.get('batches', 0), 1), 2),
+               'ms_per_group': {k[:-2]: round(1e3 * sd.get(k, 0) / max(sd.get('batches', 0), 1), 3)
+                                for k in ('forward_s', 'collate_h2d_s', 'launch_s', 'd2h_wait_s', 'decollate_s')},
+               'busy_fraction': round(sd.get('forward_s', 0) / dt, 3)},
            'data': 'FakeSC2Env observations, random-init policy; learner reuses each trajectory 2x (reference)'}
     print(json.dumps(out), flush=True)
     lp.terminate()
