@@ -26,9 +26,12 @@ def main():
     ap.add_argument('--max-entities', type=int, default=16)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--no-sync', action='store_true', help='pipelined steps (no device sync between them): shows where the host blocks')
+    ap.add_argument('--fp32', action='store_true', help='the fp32 step (no autocast, fp32 weights)')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
-    tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}, device=dev)
+    amp = None if args.fp32 else 'bfloat16'
+    tr = RLTrainer({'learner': {'use_value_feature': True, 'amp_dtype': amp}, 'model': {'enable_baselines': ['winloss']}},
+                   device=dev)
     h = rl_batch(args.batch, args.unroll, max_entities=args.max_entities, seed=0)
     b = to_device(h, dev)
     b['entity_total'] = entity_total_hint(h)
@@ -39,13 +42,16 @@ def main():
         t = [time.perf_counter()]
         if not tr.model.training:
             tr.model.train()
-        with _amp(dev, 'bfloat16'):
+        with _amp(dev, amp):
             out = tr.model.rl_learner_forward(**b)
         t.append(time.perf_counter())
         info = tr.loss.compute_loss(out)
         t.append(time.perf_counter())
-        tr.reducer.zero_grad()
-        tr.master.backward(info['total_loss'])
+        tr.reducer.zero_grad(buffers=False)
+        if tr.master is not None:
+            tr.master.backward(info['total_loss'])
+        else:
+            tr.reducer.backward(info['total_loss'])
         t.append(time.perf_counter())
         tr._reduce()
         tr._update()

@@ -1,5 +1,5 @@
 """List the host<->device synchronisations of one RL learner step (torch.cuda.set_sync_debug_mode),
-with the applestar_amd source line that triggered each.  Usage: python tools/sync_points.py"""
+with the applestar_amd source line that triggered each.  Usage: python tools/sync_points.py [--fp32 | --infer]"""
 import collections
 import os
 import sys
@@ -34,7 +34,8 @@ def main():
         tr = _T()
         b = {}
     else:
-        tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}},
+        amp = None if '--fp32' in sys.argv else 'bfloat16'
+        tr = RLTrainer({'learner': {'use_value_feature': True, 'amp_dtype': amp}, 'model': {'enable_baselines': ['winloss']}},
                        device=dev)
         from applestar_amd.runtime.prefetch import entity_total_hint
         h = rl_batch(6, 64, seed=0)
