@@ -1668,6 +1668,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fused_adam_chunk", &as::fused_adam_chunk);
   m.def("wgrad_f32", &wgrad_f32);
   m.def("gemm_f32", &gemm_f32);
+  m.def("f32_mfma_mode", &as::f32_mfma_mode);
+  m.def("set_f32_mfma_mode", &as::set_f32_mfma_mode);
   m.def("conv3x3_f32_supported", &as::conv3x3_f32_supported);
   m.def("varlen_attn_bwd_f32", &varlen_attn_bwd_f32);
   m.def("su_sample", &su_sample);

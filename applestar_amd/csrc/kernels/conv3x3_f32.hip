@@ -22,6 +22,7 @@
 // accumulators: 32 lanes write 32 consecutive channels (128 B) of one pixel.
 #include "../common.h"
 #include "../kernels.h"
+#include "../split_mfma.h"
 
 namespace as {
 namespace {
@@ -48,7 +49,7 @@ struct ConvF32Cfg {
   static_assert(A_IT * NT == BM * (BK / 4), "A tile pieces");
 };
 
-template <int BN>
+template <int BN, bool SPLIT>
 __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ res, float* __restrict__ out,
@@ -168,13 +169,26 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
       bfr[j][0] = u0.x; bfr[j][1] = u0.y; bfr[j][2] = u0.z; bfr[j][3] = u0.w;
       bfr[j][4] = u1.x; bfr[j][5] = u1.y; bfr[j][6] = u1.z; bfr[j][7] = u1.w;
     }
+    if constexpr (SPLIT) {
+      // bf16x6 (split_mfma.h): lane half h's 8 channels are the MFMA's k-slots 8h..8h+7
+      Split3 sa[C::FM], sb[C::FN];
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk)
+      for (int i = 0; i < C::FM; ++i) sa[i] = split8(af[i]);
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) sb[j] = split8(bfr[j]);
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-        for (int j = 0; j < C::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
+    }
     if (kt + 1 < KT) store_lds(cur ^ 1);
     __syncthreads();
   }
@@ -211,8 +225,12 @@ void launch_f32(const float* x, const float* w, const float* bias, const float* 
   const long M = static_cast<long>(B) * H * W;
   const long nwg = (M + 127) / 128 * ((Cout + BN - 1) / BN);
   if (nwg == 0) return;
-  hipLaunchKernelGGL((conv3x3_f32_kernel<BN>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias, res,
-                     out, B, H, W, Cin, Cout, act);
+  if (f32_mfma_mode())
+    hipLaunchKernelGGL((conv3x3_f32_kernel<BN, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias,
+                       res, out, B, H, W, Cin, Cout, act);
+  else
+    hipLaunchKernelGGL((conv3x3_f32_kernel<BN, false>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias,
+                       res, out, B, H, W, Cin, Cout, act);
 }
 
 }  // namespace

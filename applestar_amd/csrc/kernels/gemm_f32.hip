@@ -18,9 +18,11 @@
 // column (BK / 2) h + kk, XCD-aware tile order.  K % 4 == 0; a K tail reads zeros through the buffer range
 // check.
 #include <cstdlib>
+#include <string>
 
 #include "../common.h"
 #include "../kernels.h"
+#include "../split_mfma.h"
 
 namespace as {
 namespace {
@@ -48,7 +50,7 @@ struct GemmF32Cfg {
   static constexpr int STAGE = (BM + BN) * P;
 };
 
-template <int BN, int BK>
+template <int BN, int BK, bool SPLIT>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                        const float* __restrict__ bias, const float* __restrict__ res,
                                                        float* __restrict__ out, long M, int N, int K, int act) {
@@ -154,13 +156,29 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
         bfr[j][4 * q] = u.x; bfr[j][4 * q + 1] = u.y; bfr[j][4 * q + 2] = u.z; bfr[j][4 * q + 3] = u.w;
       }
     }
+    if constexpr (SPLIT) {
+      // bf16x6 (split_mfma.h): lane half h's 8-float run of a fragment is the MFMA's k-slots 8h..8h+7
 #pragma unroll
-    for (int kk = 0; kk < C::KH; ++kk)
+      for (int c = 0; c < C::KH / 8; ++c) {
+        Split3 sa[C::FM], sb[C::FN];
 #pragma unroll
-      for (int i = 0; i < C::FM; ++i)
+        for (int i = 0; i < C::FM; ++i) sa[i] = split8(*reinterpret_cast<const float(*)[8]>(&af[i][8 * c]));
 #pragma unroll
-        for (int j = 0; j < C::FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < C::FN; ++j) sb[j] = split8(*reinterpret_cast<const float(*)[8]>(&bfr[j][8 * c]));
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < C::KH; ++kk)
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
+    }
     if (kt + 1 < KT) store_lds(cur ^ 1);
     __syncthreads();
   }
@@ -194,8 +212,12 @@ void launch_gemm(const float* a, const float* b, const float* bias, const float*
                  int act, hipStream_t s) {
   const long nwg = (M + 127) / 128 * ((N + BN - 1) / BN);
   if (nwg == 0) return;
-  hipLaunchKernelGGL((gemm_f32_kernel<BN, BK>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias, res, out,
-                     M, N, K, act);
+  if (f32_mfma_mode())
+    hipLaunchKernelGGL((gemm_f32_kernel<BN, BK, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias,
+                       res, out, M, N, K, act);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<BN, BK, false>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias,
+                       res, out, M, N, K, act);
 }
 
 int gemm_bk() {
@@ -206,7 +228,18 @@ int gemm_bk() {
   return bk;
 }
 
+int& mode_ref() {
+  static int mode = [] {
+    const char* e = std::getenv("APPLESTAR_F32_MFMA");
+    return e && std::string(e) == "exact" ? 0 : 1;
+  }();
+  return mode;
+}
+
 }  // namespace
+
+int f32_mfma_mode() { return mode_ref(); }
+void set_f32_mfma_mode(int mode) { mode_ref() = mode ? 1 : 0; }
 
 void gemm_f32(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
               int act, hipStream_t s) {

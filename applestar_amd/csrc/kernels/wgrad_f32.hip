@@ -14,6 +14,7 @@
 // each half-wave reads 32 consecutive floats of one LDS row (one conflict-free ds_read_b32 per operand).
 #include "../common.h"
 #include "../kernels.h"
+#include "../split_mfma.h"
 
 namespace as {
 namespace {
@@ -35,7 +36,7 @@ struct WgF32Cfg {
   static_assert(A_IT * NT == BR * CHA && B_IT * NT == BR * CHB, "tile / thread mismatch");
 };
 
-template <int BN, int BK, bool CONV>
+template <int BN, int BK, bool CONV, bool SPLIT>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                         float* __restrict__ dw_part, float* __restrict__ db_part,
                                                         long part_stride, long R, int N, int K, int H, int W, int Cin,
@@ -155,6 +156,35 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
     if (it + 1 < nsteps) load_regs(r_begin + (it + 1) * C::BR);
     const float* A = smem + cur * C::STAGE + (16 * h) * C::PA + wn * C::TN + l32;
     const float* Bt = smem + cur * C::STAGE + C::BR * C::PA + (16 * h) * C::PB + wk * C::TK + l32;
+    if constexpr (SPLIT) {
+      // bf16x6 (split_mfma.h): 16-row chunk c of lane half h = the MFMA's k-slots 8h..8h+7
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        float av[C::FN][8], bv[C::FK][8];
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+#pragma unroll
+          for (int i = 0; i < C::FN; ++i) av[i][t] = A[(8 * c + t) * C::PA + 32 * i];
+#pragma unroll
+          for (int j = 0; j < C::FK; ++j) bv[j][t] = Bt[(8 * c + t) * C::PB + 32 * j];
+        }
+        Split3 sa[C::FN], sb[C::FK];
+#pragma unroll
+        for (int i = 0; i < C::FN; ++i) sa[i] = split8(av[i]);
+#pragma unroll
+        for (int j = 0; j < C::FK; ++j) sb[j] = split8(bv[j]);
+#pragma unroll
+        for (int i = 0; i < C::FN; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FK; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+        if (do_bias) {
+#pragma unroll
+          for (int i = 0; i < C::FN; ++i)
+#pragma unroll
+            for (int t = 0; t < 8; ++t) bsum[i] += av[i][t];
+        }
+      }
+    } else {
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       float af[C::FN], bfr[C::FK];
@@ -171,6 +201,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
 #pragma unroll
         for (int i = 0; i < C::FN; ++i) bsum[i] += af[i];
       }
+    }
     }
     if (it + 1 < nsteps) store_lds(cur ^ 1);
     __syncthreads();
@@ -206,8 +237,12 @@ void launch(const float* dy, const float* x, float* dwp, float* dbp, long ps, lo
             int Cin, int S, long rps, hipStream_t st) {
   const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
   const long nwg = static_cast<long>(tn) * tk * S;
-  hipLaunchKernelGGL((wgrad_f32_kernel<BN, BK, CONV>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x, dwp,
-                     dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
+  if (f32_mfma_mode())
+    hipLaunchKernelGGL((wgrad_f32_kernel<BN, BK, CONV, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x,
+                       dwp, dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
+  else
+    hipLaunchKernelGGL((wgrad_f32_kernel<BN, BK, CONV, false>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy,
+                       x, dwp, dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
 }
 
 int pick(int n) { return n <= 32 ? 32 : (n <= 64 ? 64 : 128); }

@@ -1083,6 +1083,17 @@ def test_value_spatial_proj_pool_matches_unfused(B, H, W):
 
 
 # ------------------------------------------------------------------ fp32 step kernels (f32 MFMA), vs float64
+@pytest.fixture(params=['split', 'exact'])
+def f32_mfma(request):
+    """Both product modes of the fp32 kernels (csrc/split_mfma.h): the bf16x6 split (default) and the exact-f32
+    MFMA; every fp32 kernel test holds both to the same float64 bound."""
+    C = N.ensure_loaded()
+    old = C.f32_mfma_mode()
+    C.set_f32_mfma_mode(1 if request.param == 'split' else 0)
+    yield request.param
+    C.set_f32_mfma_mode(old)
+
+
 def _f64(t):
     return t.detach().double().cpu().requires_grad_()
 
@@ -1090,7 +1101,7 @@ def _f64(t):
 @pytest.mark.parametrize('cin,cout,H,W,act,res', [(128, 128, 19, 20, 'relu', True), (32, 64, 21, 17, 'relu', False),
                                                   (64, 128, 10, 12, None, False), (16, 16, 9, 11, 'relu', False),
                                                   (16, 32, 8, 8, None, True), (128, 64, 5, 7, 'relu', False)])
-def test_conv3x3_f32_matches_fp64(cin, cout, H, W, act, res):
+def test_conv3x3_f32_matches_fp64(cin, cout, H, W, act, res, f32_mfma):
     """fp32 operands take conv3x3_f32.hip (forward, dX with the flipped weight, split-R dW / db): within fp32
     rounding of a float64 reference - no bf16 anywhere."""
     from applestar_amd import ops
@@ -1120,8 +1131,8 @@ def test_conv3x3_f32_matches_fp64(cin, cout, H, W, act, res):
 
 
 @pytest.mark.parametrize('R,N,K', [(4096, 768, 256), (1000, 256, 1024), (390, 128, 48640 // 64), (100003, 32, 16)])
-def test_linear_f32_grads_match_fp64(R, N, K):
-    """The fp32 step's linear (library fp32 GEMMs forward / dX, wgrad_f32.hip dW / db) vs float64."""
+def test_linear_f32_grads_match_fp64(R, N, K, f32_mfma):
+    """The fp32 step's linear (gemm_f32.hip forward / dX, wgrad_f32.hip dW / db) vs float64."""
     from applestar_amd.ops import native as NN
     torch.manual_seed(5)
     x = torch.randn(R, K, device=DEV).requires_grad_()
@@ -1140,7 +1151,7 @@ def test_linear_f32_grads_match_fp64(R, N, K):
 
 
 @pytest.mark.parametrize('extra_consumer', [False, True])
-def test_linear_f32_relu_handoff_matches_fp64(extra_consumer):
+def test_linear_f32_relu_handoff_matches_fp64(extra_consumer, f32_mfma):
     """Chained fp32 linears: the second layer's dX epilogue applies the first layer's ReLU mask and the first
     layer's backward skips its threshold pass (native._premasked); with a second consumer of the hidden
     activation the summed gradient must take the mask as usual.  Both vs float64."""
@@ -1173,7 +1184,7 @@ def test_linear_f32_relu_handoff_matches_fp64(extra_consumer):
 
 
 @pytest.mark.parametrize('gated', [False, True])
-def test_fused_resblocks_f32_match_torch_fp64(gated):
+def test_fused_resblocks_f32_match_torch_fp64(gated, f32_mfma):
     """The one-node fp32 ResBlock / GatedResBlock (skip gradients fused into the dX conv epilogue) vs the same
     module on float64 CPU weights (plain PyTorch path)."""
     import copy
@@ -1240,7 +1251,7 @@ def test_fused_clip_adam_matches_torch(max_norm, wd):
 
 @pytest.mark.parametrize('M,Nc,K', [(5000, 768, 256), (3001, 256, 1024), (20000, 32, 20), (2500, 96, 132)])
 @pytest.mark.parametrize('mode', ['bias_relu', 'res_add', 'drelu'])
-def test_gemm_f32_epilogues_match_fp64(M, Nc, K, mode):
+def test_gemm_f32_epilogues_match_fp64(M, Nc, K, mode, f32_mfma):
     """gemm_f32.hip: A [M,K] . B [Nc,K]^T with each epilogue (bias + ReLU; + residual; ReLU-output mask) vs float64."""
     torch.manual_seed(M)
     a = torch.randn(M, K, device=DEV)
