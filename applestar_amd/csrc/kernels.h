@@ -223,8 +223,9 @@ void conv3x3_f32_fwd(const float* x, const float* w, const float* bias, const fl
                      int W, int Cin, int Cout, int act, hipStream_t s);
 int wgrad_f32_splits(long R, int N, int K);
 // out [M, N] = epi(A [M, K] . B [N, K]^T): + bias[n]; res added, or (act == ACT_DRELU) a mask res > 0; ReLU
-// fp32 product mode of the f32 kernels: 0 = exact-f32 MFMA, 1 = bf16x6 split MFMA (split_mfma.h; default,
-// APPLESTAR_F32_MFMA=exact selects 0)
+// fp32 product mode of the f32 kernels: 0 = exact-f32 MFMA, 1 = bf16x6 split MFMA (split_mfma.h), split once at
+// LDS staging (default), 2 = the same split done per wave after an fp32 LDS read (A/B reference);
+// APPLESTAR_F32_MFMA=exact / regsplit select 0 / 2
 int f32_mfma_mode();
 void set_f32_mfma_mode(int mode);
 void gemm_f32(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,

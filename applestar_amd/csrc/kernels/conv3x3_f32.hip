@@ -46,16 +46,22 @@ struct ConvF32Cfg {
   static constexpr int B_PIECES = BN * (BK / 4);
   static constexpr int B_IT = (B_PIECES + NT - 1) / NT;
   static constexpr int STAGE = (BM + BN) * P;      // floats
+  // split staging (SPLIT == 2, split_mfma.h): row = three bf16 planes of 16 channels + 16 B pad = 28 dwords
+  // (the 16 rows of a ds_read_b128 lane group start on 16 distinct 4-bank groups)
+  static constexpr int PS = 28;
+  static constexpr int STAGE_S = (BM + BN) * PS;
+  static constexpr int SMEM = STAGE > STAGE_S ? STAGE : STAGE_S;
   static_assert(A_IT * NT == BM * (BK / 4), "A tile pieces");
 };
 
-template <int BN, bool SPLIT>
+// SPLIT: 0 exact-f32 MFMA; 1 bf16x6 split in registers after the fp32 LDS read; 2 bf16x6 split once at staging
+template <int BN, int SPLIT>
 __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ res, float* __restrict__ out,
                                                           int B, int H, int W, int Cin, int Cout, int act) {
   using C = ConvF32Cfg<BN>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * C::STAGE];
+  __shared__ __attribute__((aligned(16))) float smem[2 * (SPLIT == 2 ? C::STAGE_S : C::STAGE)];
 
   const int HW = H * W;
   const long M = static_cast<long>(B) * HW;
@@ -125,6 +131,25 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
     }
   };
   auto store_lds = [&](int s) {
+    if constexpr (SPLIT == 2) {
+      unsigned* A = reinterpret_cast<unsigned*>(smem) + s * C::STAGE_S;
+      unsigned* Bs = A + C::BM * C::PS;
+      auto put = [](unsigned* d, const uint4& v) {
+        uint2 s0, s1, s2;
+        split4(v, s0, s1, s2);
+        *reinterpret_cast<uint2*>(d) = s0;
+        *reinterpret_cast<uint2*>(d + 8) = s1;
+        *reinterpret_cast<uint2*>(d + 16) = s2;
+      };
+#pragma unroll
+      for (int i = 0; i < C::A_IT; ++i) put(A + a_row[i] * C::PS + 2 * a_c4[i], ra[i]);
+#pragma unroll
+      for (int i = 0; i < C::B_IT; ++i) {
+        const int idx = tid + i * C::NT;
+        if (C::B_PIECES % C::NT == 0 || idx < C::B_PIECES) put(Bs + C::prow(idx) * C::PS + 2 * C::pcol(idx), rb[i]);
+      }
+      return;
+    }
     float* A = smem + s * C::STAGE;
     float* Bs = A + C::BM * C::P;
 #pragma unroll
@@ -152,6 +177,31 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < KT) load_regs(kt + 1);
+    if constexpr (SPLIT == 2) {
+      // lane half h: channels 8 h .. 8 h + 7 of the K-step = the MFMA's k-slots 8 h .. 8 h + 7
+      const unsigned* A = reinterpret_cast<const unsigned*>(smem) + cur * C::STAGE_S;
+      const unsigned* Bs = A + C::BM * C::PS;
+      Split3 sa[C::FM], sb[C::FN];
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const unsigned* p = A + (wm * C::TM + 32 * i + l32) * C::PS + 4 * h;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) sa[i].p[q] = *reinterpret_cast<const u32v4*>(p + 8 * q);
+      }
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j) {
+        const unsigned* p = Bs + (wn * C::TN + 32 * j + l32) * C::PS + 4 * h;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) sb[j].p[q] = *reinterpret_cast<const u32v4*>(p + 8 * q);
+      }
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+      if (kt + 1 < KT) store_lds(cur ^ 1);
+      __syncthreads();
+      continue;
+    }
     const float* A = smem + cur * C::STAGE;
     const float* Bs = A + C::BM * C::P;
     float af[C::FM][8], bfr[C::FN][8];
@@ -169,7 +219,7 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
       bfr[j][0] = u0.x; bfr[j][1] = u0.y; bfr[j][2] = u0.z; bfr[j][3] = u0.w;
       bfr[j][4] = u1.x; bfr[j][5] = u1.y; bfr[j][6] = u1.z; bfr[j][7] = u1.w;
     }
-    if constexpr (SPLIT) {
+    if constexpr (SPLIT == 1) {
       // bf16x6 (split_mfma.h): lane half h's 8 channels are the MFMA's k-slots 8h..8h+7
       Split3 sa[C::FM], sb[C::FN];
 #pragma unroll
@@ -225,12 +275,16 @@ void launch_f32(const float* x, const float* w, const float* bias, const float* 
   const long M = static_cast<long>(B) * H * W;
   const long nwg = (M + 127) / 128 * ((Cout + BN - 1) / BN);
   if (nwg == 0) return;
-  if (f32_mfma_mode())
-    hipLaunchKernelGGL((conv3x3_f32_kernel<BN, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias,
-                       res, out, B, H, W, Cin, Cout, act);
+  const int mode = f32_mfma_mode();
+  if (mode == 1)
+    hipLaunchKernelGGL((conv3x3_f32_kernel<BN, 2>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias, res,
+                       out, B, H, W, Cin, Cout, act);
+  else if (mode == 2)
+    hipLaunchKernelGGL((conv3x3_f32_kernel<BN, 1>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias, res,
+                       out, B, H, W, Cin, Cout, act);
   else
-    hipLaunchKernelGGL((conv3x3_f32_kernel<BN, false>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias,
-                       res, out, B, H, W, Cin, Cout, act);
+    hipLaunchKernelGGL((conv3x3_f32_kernel<BN, 0>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias, res,
+                       out, B, H, W, Cin, Cout, act);
 }
 
 }  // namespace

@@ -48,14 +48,21 @@ struct GemmF32Cfg {
   static constexpr int B_PIECES = BN * CH;
   static constexpr int B_IT = (B_PIECES + NT - 1) / NT;
   static constexpr int STAGE = (BM + BN) * P;
+  // split staging (SPLIT == 2): row = three bf16 planes of BK values + 16 B pad, 3 BK / 2 + 4 dwords (28 / 52:
+  // the 16 rows of a ds_read_b128 lane group start on 16 distinct 4-bank groups)
+  static constexpr int PS = 3 * BK / 2 + 4;
+  static constexpr int STAGE_S = (BM + BN) * PS;
+  static constexpr int SMEM = STAGE > STAGE_S ? STAGE : STAGE_S;
 };
 
-template <int BN, int BK, bool SPLIT>
+// SPLIT: 0 exact-f32 MFMA; 1 bf16x6 split in registers after the fp32 LDS read; 2 bf16x6 split once at staging
+// (three bf16 planes per LDS row, fragments read as bf16x8)
+template <int BN, int BK, int SPLIT>
 __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                        const float* __restrict__ bias, const float* __restrict__ res,
                                                        float* __restrict__ out, long M, int N, int K, int act) {
   using C = GemmF32Cfg<BN, BK>;
-  __shared__ __attribute__((aligned(16))) float smem[2 * C::STAGE];
+  __shared__ __attribute__((aligned(16))) float smem[2 * (SPLIT == 2 ? C::STAGE_S : C::STAGE)];
   const int ntn = (N + BN - 1) / BN;
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
@@ -89,34 +96,53 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
     b_base[i] = (idx < C::B_PIECES && n0 + n < N) ? (n0 + n) * K : -1;
   }
 
-  uint4 ra[C::A_IT], rb[C::B_IT];
-  auto load_regs = [&](int kt) {
+  uint4 ra[1][C::A_IT], rb[1][C::B_IT];
+  auto load_regs = [&](int kt, uint4 (&xa)[C::A_IT], uint4 (&xb)[C::B_IT]) {
     const int k0 = kt * C::BK;
 #pragma unroll
     for (int i = 0; i < C::A_IT; ++i) {
       const int k = k0 + 4 * a_c4[i];
       const int off = (a_base[i] >= 0 && k < K) ? (a_base[i] + k) * 4 : kOOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(ar, off, 0, 0);
-      ra[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      xa[i] = make_uint4(v[0], v[1], v[2], v[3]);
     }
 #pragma unroll
     for (int i = 0; i < C::B_IT; ++i) {
       const int k = k0 + 4 * C::pcol(tid + i * C::NT);
       const int off = (b_base[i] >= 0 && k < K) ? (b_base[i] + k) * 4 : kOOB;
       const auto v = __builtin_amdgcn_raw_buffer_load_b128(br, off, 0, 0);
-      rb[i] = make_uint4(v[0], v[1], v[2], v[3]);
+      xb[i] = make_uint4(v[0], v[1], v[2], v[3]);
     }
   };
-  auto store_lds = [&](int s) {
-    float* A = smem + s * C::STAGE;
-    float* Bs = A + C::BM * C::P;
+  auto store_lds = [&](int s, const uint4 (&xa)[C::A_IT], const uint4 (&xb)[C::B_IT]) {
+    if constexpr (SPLIT == 2) {
+      unsigned* A = reinterpret_cast<unsigned*>(smem) + s * C::STAGE_S;
+      unsigned* Bs = A + C::BM * C::PS;
+      auto put = [](unsigned* d, const uint4& v) {
+        uint2 s0, s1, s2;
+        split4(v, s0, s1, s2);
+        *reinterpret_cast<uint2*>(d) = s0;
+        *reinterpret_cast<uint2*>(d + C::BK / 2) = s1;
+        *reinterpret_cast<uint2*>(d + C::BK) = s2;
+      };
 #pragma unroll
-    for (int i = 0; i < C::A_IT; ++i) *reinterpret_cast<uint4*>(A + a_row[i] * C::P + 4 * a_c4[i]) = ra[i];
+      for (int i = 0; i < C::A_IT; ++i) put(A + a_row[i] * C::PS + 2 * a_c4[i], xa[i]);
 #pragma unroll
-    for (int i = 0; i < C::B_IT; ++i) {
-      const int idx = tid + i * C::NT;
-      if (C::B_PIECES % C::NT == 0 || idx < C::B_PIECES)
-        *reinterpret_cast<uint4*>(Bs + C::prow(idx) * C::P + 4 * C::pcol(idx)) = rb[i];
+      for (int i = 0; i < C::B_IT; ++i) {
+        const int idx = tid + i * C::NT;
+        if (C::B_PIECES % C::NT == 0 || idx < C::B_PIECES) put(Bs + C::prow(idx) * C::PS + 2 * C::pcol(idx), xb[i]);
+      }
+    } else {
+      float* A = smem + s * C::STAGE;
+      float* Bs = A + C::BM * C::P;
+#pragma unroll
+      for (int i = 0; i < C::A_IT; ++i) *reinterpret_cast<uint4*>(A + a_row[i] * C::P + 4 * a_c4[i]) = xa[i];
+#pragma unroll
+      for (int i = 0; i < C::B_IT; ++i) {
+        const int idx = tid + i * C::NT;
+        if (C::B_PIECES % C::NT == 0 || idx < C::B_PIECES)
+          *reinterpret_cast<uint4*>(Bs + C::prow(idx) * C::P + 4 * C::pcol(idx)) = xb[i];
+      }
     }
   };
 
@@ -128,13 +154,33 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  const int KT = (K + C::BK - 1) / C::BK;
-  load_regs(0);
-  store_lds(0);
-  __syncthreads();
-  for (int kt = 0; kt < KT; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < KT) load_regs(kt + 1);
+  auto compute = [&](int cur) {
+    if constexpr (SPLIT == 2) {
+      // chunk c of lane half h: columns 16 c + 8 h .. + 7 = the MFMA's k-slots 8 h .. 8 h + 7
+      const unsigned* A = reinterpret_cast<const unsigned*>(smem) + cur * C::STAGE_S;
+      const unsigned* Bs = A + C::BM * C::PS;
+#pragma unroll
+      for (int c = 0; c < C::BK / 16; ++c) {
+        Split3 sa[C::FM], sb[C::FN];
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) {
+          const unsigned* p = A + (wm * C::TM + 32 * i + l32) * C::PS + 8 * c + 4 * h;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) sa[i].p[q] = *reinterpret_cast<const u32v4*>(p + q * (C::BK / 2));
+        }
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          const unsigned* p = Bs + (wn * C::TN + 32 * j + l32) * C::PS + 8 * c + 4 * h;
+#pragma unroll
+          for (int q = 0; q < 3; ++q) sb[j].p[q] = *reinterpret_cast<const u32v4*>(p + q * (C::BK / 2));
+        }
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+      }
+      return;
+    }
     const float* A = smem + cur * C::STAGE;
     const float* Bs = A + C::BM * C::P;
     float af[C::FM][C::KH], bfr[C::FN][C::KH];
@@ -156,7 +202,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
         bfr[j][4 * q] = u.x; bfr[j][4 * q + 1] = u.y; bfr[j][4 * q + 2] = u.z; bfr[j][4 * q + 3] = u.w;
       }
     }
-    if constexpr (SPLIT) {
+    if constexpr (SPLIT == 1) {
       // bf16x6 (split_mfma.h): lane half h's 8-float run of a fragment is the MFMA's k-slots 8h..8h+7
 #pragma unroll
       for (int c = 0; c < C::KH / 8; ++c) {
@@ -179,7 +225,19 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
           for (int j = 0; j < C::FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < KT) store_lds(cur ^ 1);
+  };
+
+  // LDS buffer kt & 1 holds K-step kt, the registers kt + 1 (a second register set two K-steps ahead
+  // measured no faster and made the unrolled loop copy the accumulators)
+  const int KT = (K + C::BK - 1) / C::BK;
+  load_regs(0, ra[0], rb[0]);
+  store_lds(0, ra[0], rb[0]);
+  __syncthreads();
+  for (int kt = 0; kt < KT; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < KT) load_regs(kt + 1, ra[0], rb[0]);
+    compute(cur);
+    if (kt + 1 < KT) store_lds(cur ^ 1, ra[0], rb[0]);
     __syncthreads();
   }
 
@@ -212,12 +270,16 @@ void launch_gemm(const float* a, const float* b, const float* bias, const float*
                  int act, hipStream_t s) {
   const long nwg = (M + 127) / 128 * ((N + BN - 1) / BN);
   if (nwg == 0) return;
-  if (f32_mfma_mode())
-    hipLaunchKernelGGL((gemm_f32_kernel<BN, BK, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias,
-                       res, out, M, N, K, act);
+  const int mode = f32_mfma_mode();
+  if (mode == 1)
+    hipLaunchKernelGGL((gemm_f32_kernel<BN, BK, 2>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias, res,
+                       out, M, N, K, act);
+  else if (mode == 2)
+    hipLaunchKernelGGL((gemm_f32_kernel<BN, BK, 1>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias, res,
+                       out, M, N, K, act);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<BN, BK, false>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias,
-                       res, out, M, N, K, act);
+    hipLaunchKernelGGL((gemm_f32_kernel<BN, BK, 0>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias, res,
+                       out, M, N, K, act);
 }
 
 int gemm_bk() {
@@ -231,7 +293,8 @@ int gemm_bk() {
 int& mode_ref() {
   static int mode = [] {
     const char* e = std::getenv("APPLESTAR_F32_MFMA");
-    return e && std::string(e) == "exact" ? 0 : 1;
+    const std::string v = e ? e : "";
+    return v == "exact" ? 0 : (v == "regsplit" ? 2 : 1);
   }();
   return mode;
 }
@@ -239,7 +302,7 @@ int& mode_ref() {
 }  // namespace
 
 int f32_mfma_mode() { return mode_ref(); }
-void set_f32_mfma_mode(int mode) { mode_ref() = mode ? 1 : 0; }
+void set_f32_mfma_mode(int mode) { mode_ref() = mode >= 0 && mode <= 2 ? mode : 1; }
 
 void gemm_f32(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
               int act, hipStream_t s) {

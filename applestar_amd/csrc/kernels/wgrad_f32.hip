@@ -36,7 +36,7 @@ struct WgF32Cfg {
   static_assert(A_IT * NT == BR * CHA && B_IT * NT == BR * CHB, "tile / thread mismatch");
 };
 
-template <int BN, int BK, bool CONV, bool SPLIT>
+template <int BN, int BK, bool CONV, int SPLIT>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                         float* __restrict__ dw_part, float* __restrict__ db_part,
                                                         long part_stride, long R, int N, int K, int H, int W, int Cin,
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
     if (it + 1 < nsteps) load_regs(r_begin + (it + 1) * C::BR);
     const float* A = smem + cur * C::STAGE + (16 * h) * C::PA + wn * C::TN + l32;
     const float* Bt = smem + cur * C::STAGE + C::BR * C::PA + (16 * h) * C::PB + wk * C::TK + l32;
-    if constexpr (SPLIT) {
+    if constexpr (SPLIT == 1) {
       // bf16x6 (split_mfma.h): 16-row chunk c of lane half h = the MFMA's k-slots 8h..8h+7
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
@@ -238,10 +238,10 @@ void launch(const float* dy, const float* x, float* dwp, float* dbp, long ps, lo
   const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
   const long nwg = static_cast<long>(tn) * tk * S;
   if (f32_mfma_mode())
-    hipLaunchKernelGGL((wgrad_f32_kernel<BN, BK, CONV, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x,
+    hipLaunchKernelGGL((wgrad_f32_kernel<BN, BK, CONV, 1>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x,
                        dwp, dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
   else
-    hipLaunchKernelGGL((wgrad_f32_kernel<BN, BK, CONV, false>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy,
+    hipLaunchKernelGGL((wgrad_f32_kernel<BN, BK, CONV, 0>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy,
                        x, dwp, dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
 }
 

@@ -23,7 +23,7 @@ def run(C, kind, shape, flop, fn, ref_fn, acc_fn=None):
     row = {'kernel': kind, 'shape': shape}
     ref = ref_fn()
     acc_fn = acc_fn or fn
-    for mode, tag in ((0, 'exact'), (1, 'split')):
+    for mode, tag in ((0, 'exact'), (1, 'split'), (2, 'regsplit')):
         C.set_f32_mfma_mode(mode)
         us = timed(fn)
         out = acc_fn()
