@@ -197,7 +197,7 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sb[j], sa[i], acc[i][j]);
       if (kt + 1 < KT) store_lds(cur ^ 1);
       __syncthreads();
       continue;
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sb[j], sa[i], acc[i][j]);
     } else {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
@@ -237,33 +237,53 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
         for (int i = 0; i < C::FM; ++i)
 #pragma unroll
           for (int j = 0; j < C::FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(bfr[j][kk], af[i][kk], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < KT) store_lds(cur ^ 1);
     __syncthreads();
   }
 
-  // epilogue straight from the accumulators: register e of tile (i, j) is pixel row (e&3) + 8(e>>2) + 4h,
-  // channel l32; lanes 0..31 / 32..63 each write 128 contiguous bytes
+  // operands enter the MFMA swapped (B fragment first), so the accumulator is the transposed tile: lane l32 is
+  // output row m, registers 4 g .. 4 g + 3 are four consecutive columns n - one 16-B load / store per group
+  // (the untransposed tile stored one float per lane and register: 64 stores per tile, 35 % of a K = 256 GEMM)
+  const bool vec = (Cout & 3) == 0;
 #pragma unroll
-  for (int j = 0; j < C::FN; ++j) {
-    const int n = n0 + wn * C::TN + 32 * j + l32;
-    if (n >= Cout) continue;
-    const float bv = bias ? bias[n] : 0.f;
+  for (int i = 0; i < C::FM; ++i) {
+    const long m = m0 + wm * C::TM + 32 * i + l32;
+    if (m >= M) continue;
+    float* orow = out + m * Cout;
+    const float* rrow = res ? res + m * Cout : nullptr;
 #pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
+    for (int j = 0; j < C::FN; ++j) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const long m = m0 + wm * C::TM + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (m >= M) continue;
-        float v = acc[i][j][e] + bv;
-        if (res) {
-          const float rv = res[m * Cout + n];
-          if (act == ACT_DRELU) v = rv > 0.f ? v : 0.f;
-          else v += rv;
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * C::TN + 32 * j + 8 * g + 4 * h;
+        float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        if (vec && n + 3 < Cout) {
+          if (bias) {
+            const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+          }
+          if (rrow) {
+            const float4 rv = *reinterpret_cast<const float4*>(rrow + n);
+            const float r[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = act == ACT_DRELU ? (r[q] > 0.f ? v[q] : 0.f) : v[q] + r[q];
+          }
+          if (act == ACT_RELU)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+          *reinterpret_cast<float4*>(orow + n) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (n + q >= Cout) continue;
+            float x = v[q] + (bias ? bias[n + q] : 0.f);
+            if (rrow) x = act == ACT_DRELU ? (rrow[n + q] > 0.f ? x : 0.f) : x + rrow[n + q];
+            if (act == ACT_RELU) x = fmaxf(x, 0.f);
+            orow[n + q] = x;
+          }
         }
-        if (act == ACT_RELU) v = fmaxf(v, 0.f);
-        out[m * Cout + n] = v;
       }
     }
   }

@@ -31,6 +31,12 @@ typedef __attribute__((ext_vector_type(16))) float f16v;
 
 constexpr int kOOB = 0x7ffffff0;
 
+// GF_ABL: timing-ablation bits for tools/native/gemm_f32_ablation.cpp only (1: no K-step loads after the first,
+// 2: no MFMAs (fragments kept live), 4: no epilogue stores); 0 in every library build
+#ifndef GF_ABL
+#define GF_ABL 0
+#endif
+
 template <int BN_, int BK_>
 struct GemmF32Cfg {
   static constexpr int BM = 128, BN = BN_, BK = BK_, NT = 256;
@@ -174,10 +180,21 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 #pragma unroll
           for (int q = 0; q < 3; ++q) sb[j].p[q] = *reinterpret_cast<const u32v4*>(p + q * (C::BK / 2));
         }
+        if constexpr ((GF_ABL & 2) != 0) {
 #pragma unroll
-        for (int i = 0; i < C::FM; ++i)
+          for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-          for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+            for (int q = 0; q < 3; ++q) asm volatile("" ::"v"(sa[i].p[q]));
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+            for (int q = 0; q < 3; ++q) asm volatile("" ::"v"(sb[j].p[q]));
+        } else {
+#pragma unroll
+          for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+            for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sb[j], sa[i], acc[i][j]);
+        }
       }
       return;
     }
@@ -214,7 +231,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 #pragma unroll
         for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-          for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+          for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sb[j], sa[i], acc[i][j]);
       }
     } else {
 #pragma unroll
@@ -223,7 +240,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
         for (int i = 0; i < C::FM; ++i)
 #pragma unroll
           for (int j = 0; j < C::FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][kk], bfr[j][kk], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(bfr[j][kk], af[i][kk], acc[i][j], 0, 0, 0);
     }
   };
 
@@ -235,31 +252,63 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   __syncthreads();
   for (int kt = 0; kt < KT; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < KT) load_regs(kt + 1, ra[0], rb[0]);
+    if (kt + 1 < KT && ((GF_ABL & 1) == 0 || kt == 0)) load_regs(kt + 1, ra[0], rb[0]);
     compute(cur);
     if (kt + 1 < KT) store_lds(cur ^ 1, ra[0], rb[0]);
     __syncthreads();
   }
 
+  if constexpr ((GF_ABL & 4) != 0) {
+    float t = 0.f;
 #pragma unroll
-  for (int j = 0; j < C::FN; ++j) {
-    const int n = n0 + wn * C::TN + 32 * j + l32;
-    if (n >= N) continue;
-    const float bv = bias ? bias[n] : 0.f;
+    for (int i = 0; i < C::FM; ++i)
 #pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
+      for (int j = 0; j < C::FN; ++j)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const long m = m0 + wm * C::TM + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (m >= M) continue;
-        float v = acc[i][j][e] + bv;
-        if (res) {
-          const float rv = res[m * N + n];
-          if (act == ACT_DRELU) v = rv > 0.f ? v : 0.f;
-          else v += rv;
+        for (int e = 0; e < 16; ++e) t += acc[i][j][e];
+    if (t != 12345.678f) return;
+  }
+  // operands enter the MFMA swapped (B fragment first), so the accumulator is the transposed tile: lane l32 is
+  // output row m, registers 4 g .. 4 g + 3 are four consecutive columns n - one 16-B load / store per group
+  // (the untransposed tile stored one float per lane and register: 64 stores per tile, 35 % of a K = 256 GEMM)
+  const bool vec = (N & 3) == 0;
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i) {
+    const long m = m0 + wm * C::TM + 32 * i + l32;
+    if (m >= M) continue;
+    float* orow = out + m * N;
+    const float* rrow = res ? res + m * N : nullptr;
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * C::TN + 32 * j + 8 * g + 4 * h;
+        float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        if (vec && n + 3 < N) {
+          if (bias) {
+            const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+          }
+          if (rrow) {
+            const float4 rv = *reinterpret_cast<const float4*>(rrow + n);
+            const float r[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = act == ACT_DRELU ? (r[q] > 0.f ? v[q] : 0.f) : v[q] + r[q];
+          }
+          if (act == ACT_RELU)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+          *reinterpret_cast<float4*>(orow + n) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (n + q >= N) continue;
+            float x = v[q] + (bias ? bias[n + q] : 0.f);
+            if (rrow) x = act == ACT_DRELU ? (rrow[n + q] > 0.f ? x : 0.f) : x + rrow[n + q];
+            if (act == ACT_RELU) x = fmaxf(x, 0.f);
+            orow[n + q] = x;
+          }
         }
-        if (act == ACT_RELU) v = fmaxf(v, 0.f);
-        out[m * N + n] = v;
       }
     }
   }
