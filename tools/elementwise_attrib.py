@@ -18,9 +18,12 @@ def main():
     ap.add_argument('--steps', type=int, default=2)
     ap.add_argument('--top', type=int, default=70)
     ap.add_argument('--out', default='gpurun_out/elementwise_attrib.txt')
+    ap.add_argument('--precision', choices=['fp32', 'bf16'], default='bf16')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
-    tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}, device=dev)
+    amp = 'bfloat16' if args.precision == 'bf16' else None
+    tr = RLTrainer({'learner': {'use_value_feature': True, 'amp_dtype': amp}, 'model': {'enable_baselines': ['winloss']}},
+                   device=dev)
     b = to_device(rl_batch(6, 64, seed=0), dev)
     for _ in range(2):
         tr.step(dict(b))
