@@ -1,0 +1,239 @@
+// The fp32 GEMM main loop shared by gemm_f32.hip and conv3x3_f32.hip (split-MFMA mode): a 128 x BN output tile per
+// 256-thread workgroup, K-steps of BK (16 / 32) floats, tiles streamed global -> LDS by LDS-DMA (buffer_load_dwordx4 ... lds)
+// through an NS-deep ring, products as bf16x6 split MFMAs (split_mfma.h) on fragments split in registers.
+//
+// Why this shape (measured, profiles/r3u_gemm_f32_ablation_*): the register-staged double buffer kept one 16 KB
+// K-step in flight per workgroup and its memory side alone ran at 1.7 TB/s (the ablation without MFMAs took as
+// long as the one without loads, and the two barely overlapped).  LDS-DMA needs no staging registers, so NS - 1
+// K-steps stay in flight; the waits are counted (s_waitcnt vmcnt(N), never 0 in the loop) and the barrier is the
+// raw s_barrier (a __syncthreads() would drain the DMA queue).
+//
+// LDS image (lane-linear, as the DMA writes it): a stage holds the A rows then the B rows, BK floats per row
+// (BK / 4 16-B slots); one wave-instruction fills 1 KB of rows.  Slot s of row r holds column piece s ^ swz(r) -
+// the swizzle rides on the per-lane SOURCE address - so the 16 rows read by a ds_read_b128 lane group land on 16
+// distinct 4-bank groups.
+//
+// Loop (one barrier per K-step):  wait until this wave's loads of step kt landed (vmcnt((NS-2) * loads per
+// step)) -> s_barrier (every wave's step kt landed; every wave finished reading step kt - 1) -> issue step
+// kt + NS - 1 into the slot of step kt - 1 -> compute step kt.  Loads past the last step use an out-of-range
+// offset (zeros into a slot nobody reads) so the counts stay uniform.
+#pragma once
+#include "common.h"
+#include "split_mfma.h"
+
+namespace as {
+namespace pipe {
+
+typedef __attribute__((ext_vector_type(16))) float f16v;
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+
+constexpr int kOOB = 0x7ffffff0;
+
+// PIPE_ABL: timing-ablation bits for tools/native/gemm_f32_ablation.cpp only (1: fragments bit-cast instead of
+// split (wrong values, no split VALU), 2: no MFMAs); 0 in every library build
+#ifndef PIPE_ABL
+#define PIPE_ABL 0
+#endif
+
+template <int BN_, int NS_, int BK_ = 16>
+struct Cfg {
+  static constexpr int BM = 128, BN = BN_, NS = NS_, BK = BK_, NT = 256;
+  static constexpr int WN = BN_ >= 128 ? 2 : 1, WM = 4 / WN;
+  static constexpr int TM = BM / WM, TN = BN / WN;
+  static constexpr int FM = TM / 32, FN = TN / 32;
+  static constexpr int RB = BK * 4, SL = BK / 4;              // bytes / 16-B slots per LDS row
+  static constexpr int RPI = 1024 / RB;                       // rows per DMA wave-instruction (1 KB)
+  static constexpr int A_CH = BM / RPI, B_CH = BN / RPI;      // DMA chunks per stage
+  static constexpr int A_PW = A_CH / 4;                       // A chunks per wave
+  static constexpr int B_PW = B_CH >= 4 ? B_CH / 4 : 1;       // B chunks per wave (waves >= B_CH issue none)
+  static constexpr int STAGE = (BM + BN) * RB;                // bytes per stage array
+  // slot swizzle: the 16 rows of a ds_read_b128 lane group on 16 distinct 4-bank groups (64-B rows: XOR with
+  // bits 2-3 of the row; 128-B rows: bits 1-3)
+  static __device__ __forceinline__ int swz(int r) { return BK == 16 ? (r >> 2) & 3 : (r >> 1) & 7; }
+  static __device__ __forceinline__ int slot_of(int r, int p) { return p ^ swz(r); }
+  // the DMA piece of `lane` in chunk `ch` (global chunk index within the A or B rows): row and column piece
+  static __device__ __forceinline__ int dma_row(int ch, int lane) { return RPI * ch + lane / SL; }
+  static __device__ __forceinline__ int dma_piece(int row, int lane) { return slot_of(row, lane % SL); }
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// raw buffer resource (base, size in bytes; out-of-range offsets read zeros) as an SGPR quad for the asm DMA
+__device__ __forceinline__ i32x4 rsrc(const void* base, long bytes) {
+  const unsigned long a = reinterpret_cast<unsigned long>(base);
+  i32x4 r;
+  r[0] = __builtin_amdgcn_readfirstlane(static_cast<int>(a & 0xffffffffu));
+  r[1] = __builtin_amdgcn_readfirstlane(static_cast<int>((a >> 32) & 0xffff));
+  r[2] = static_cast<int>(bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+
+// one LDS-DMA piece: 16 B from the buffer at byte offset voff (kOOB: zeros) to dst + 16 * lane.  Inline asm, so
+// the compiler's waitcnt pass does not see the DMA: through the builtin it could not tell the stage being
+// written from the stage being read and put an s_waitcnt vmcnt(0) before the fragment reads of every K-step
+// (the loop's own counted waits order the DMA; M0 is set here and needs one wait state before the load)
+__device__ __forceinline__ void dma16(i32x4 r, char* dst, int voff) {
+  const unsigned lds = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void*)dst));
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds"
+               :
+               : "s"(__builtin_amdgcn_readfirstlane(lds)), "v"(voff), "s"(r)
+               : "memory", "m0");
+}
+
+// fragment of 8 consecutive floats (pieces p0, p0 + 1) of LDS row r
+template <class C>
+__device__ __forceinline__ Split3 frag(const char* stage, int r, int p0) {
+  const float4 u0 = *reinterpret_cast<const float4*>(stage + r * C::RB + 16 * C::slot_of(r, p0));
+  const float4 u1 = *reinterpret_cast<const float4*>(stage + r * C::RB + 16 * C::slot_of(r, p0 + 1));
+  if constexpr ((PIPE_ABL & 1) != 0) {
+    Split3 x;
+    x.p[0] = u32v4{__float_as_uint(u0.x), __float_as_uint(u0.y), __float_as_uint(u0.z), __float_as_uint(u0.w)};
+    x.p[1] = u32v4{__float_as_uint(u1.x), __float_as_uint(u1.y), __float_as_uint(u1.z), __float_as_uint(u1.w)};
+    x.p[2] = x.p[0] ^ x.p[1];
+    return x;
+  }
+  const float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+  return split8(v);
+}
+
+// The main loop.  ASrc / BSrc: (chunk index within the wave's share, K-step) -> byte offset of this lane's 16-B
+// piece (the piece is column slot_of(row, lane & 3) of row 16 chunk + lane / 4), or kOOB.  smem: NS stage arrays
+// (separate __shared__ objects) and the loop unrolled by NS, so every DMA target and every fragment read names a
+// compile-time stage: with one array and a runtime stage index the compiler cannot tell the DMA just issued from
+// the stage being read and drains the DMA queue (s_waitcnt vmcnt(0)) before every K-step's first ds_read.
+template <class C, class ASrc, class BSrc>
+__device__ __forceinline__ void mainloop(char* const (&smem)[C::NS], i32x4 ar, i32x4 br, int KT, const ASrc& asrc,
+                                         const BSrc& bsrc, f16v (&acc)[C::FM][C::FN]) {
+  constexpr int NS = C::NS;
+  // the wave id in a scalar register: the per-wave branches below are uniform (s_cbranch, and only the taken
+  // side's s_waitcnt executes)
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int l32 = lane & 31, h = lane >> 5;
+  const bool b_wave = C::B_CH >= 4 || wid < C::B_CH;
+  auto issue = [&](char* st, int kt) {
+#pragma unroll
+    for (int c = 0; c < C::A_PW; ++c) dma16(ar, st + (wid + 4 * c) * 1024, asrc(c, kt));
+    if (b_wave) {
+#pragma unroll
+      for (int c = 0; c < C::B_PW; ++c) dma16(br, st + C::BM * C::RB + (wid + 4 * c) * 1024, bsrc(c, kt));
+    }
+  };
+  auto step = [&](const char* st, char* next, int kt) {
+    // this wave's loads of step kt: NS - 2 later steps may stay in flight
+    if (b_wave) wait_vm<(NS - 2) * (C::A_PW + C::B_PW)>();
+    else wait_vm<(NS - 2) * C::A_PW>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(next, kt + NS - 1);
+#pragma unroll
+    for (int c = 0; c < C::BK / 16; ++c) {
+    // chunk c of lane half h: columns 16 c + 8 h .. + 7 = the MFMA's k-slots 8 h .. 8 h + 7
+    Split3 sa[C::FM], sb[C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) sa[i] = frag<C>(st, wm * C::TM + 32 * i + l32, 4 * c + 2 * h);
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j) sb[j] = frag<C>(st + C::BM * C::RB, wn * C::TN + 32 * j + l32, 4 * c + 2 * h);
+    // swapped operands: the accumulator is the transposed tile (lane = output row, registers = columns)
+    if constexpr ((PIPE_ABL & 2) != 0) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) asm volatile("" ::"v"(sa[i].p[q]));
+#pragma unroll
+      for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) asm volatile("" ::"v"(sb[j].p[q]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_x6(sb[j], sa[i], acc[i][j]);
+    }
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue(smem[s], s);
+  for (int kt = 0; kt < KT; kt += NS) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (kt + s >= KT) break;
+      step(smem[s], smem[(s + NS - 1) % NS], kt + s);
+    }
+  }
+  wait_vm<0>();
+}
+
+// Epilogue of a wave's transposed accumulator tiles: lane l32 of tile (i, j) is output row mw + 32 i + l32,
+// registers 4 g .. 4 g + 3 are columns nw + 32 j + 8 g + 4 h + 0..3.  out / res rows have N floats.
+//   v = acc + bias[n] (+ res[m, n] | masked by res[m, n] > 0 for ACT_DRELU), then ReLU for ACT_RELU
+template <int FM, int FN>
+__device__ __forceinline__ void store_tile(const f16v (&acc)[FM][FN], float* __restrict__ out,
+                                           const float* __restrict__ bias, const float* __restrict__ res, long M,
+                                           int N, long mw, int nw, int act) {
+  const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+  const bool vec = (N & 3) == 0;
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const long m = mw + 32 * i + l32;
+    if (m >= M) continue;
+    float* orow = out + m * N;
+    const float* rrow = res ? res + m * N : nullptr;
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = nw + 32 * j + 8 * g + 4 * h;
+        float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        if (vec && n + 3 < N) {
+          if (bias) {
+            const float4 bv = *reinterpret_cast<const float4*>(bias + n);
+            v[0] += bv.x; v[1] += bv.y; v[2] += bv.z; v[3] += bv.w;
+          }
+          if (rrow) {
+            const float4 rv = *reinterpret_cast<const float4*>(rrow + n);
+            const float r[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = act == ACT_DRELU ? (r[q] > 0.f ? v[q] : 0.f) : v[q] + r[q];
+          }
+          if (act == ACT_RELU)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
+          *reinterpret_cast<float4*>(orow + n) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (n + q >= N) continue;
+            float x = v[q] + (bias ? bias[n + q] : 0.f);
+            if (rrow) x = act == ACT_DRELU ? (rrow[n + q] > 0.f ? x : 0.f) : x + rrow[n + q];
+            if (act == ACT_RELU) x = fmaxf(x, 0.f);
+            orow[n + q] = x;
+          }
+        }
+      }
+    }
+  }
+}
+
+// XCD-aware bijective remap of the workgroup id (8 XCDs, round-robin dispatch): consecutive logical ids share an
+// XCD's L2
+__device__ __forceinline__ int xcd_remap() {
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, r8 = nwg & 7;
+  return (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (orig >> 3);
+}
+
+}  // namespace pipe
+}  // namespace as

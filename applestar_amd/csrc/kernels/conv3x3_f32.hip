@@ -23,6 +23,7 @@
 #include "../common.h"
 #include "../kernels.h"
 #include "../split_mfma.h"
+#include "../f32_pipe.h"
 
 namespace as {
 namespace {
@@ -289,6 +290,65 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
   }
 }
 
+// split-MFMA mode: the LDS-DMA ring of f32_pipe.h with the A rows gathered per tap (a lane's DMA piece is 4
+// channels of its row's shifted pixel; taps outside the image read zeros through the buffer range check)
+template <int BN, int NS>
+__global__ __launch_bounds__(256, 3) void conv3x3_f32_pipe_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                               const float* __restrict__ bias,
+                                                               const float* __restrict__ res, float* __restrict__ out,
+                                                               int B, int H, int W, int Cin, int Cout, int act) {
+  using C = pipe::Cfg<BN, NS, 16>;
+  __shared__ __attribute__((aligned(16))) char s0[C::STAGE], s1[C::STAGE], s2[NS > 2 ? C::STAGE : 16],
+      s3[NS > 3 ? C::STAGE : 16];
+  char* const all[4] = {s0, s1, s2, s3};
+  char* smem[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) smem[i] = all[i];
+  const int HW = H * W;
+  const long M = static_cast<long>(B) * HW;
+  const int K = 9 * Cin;
+  const int ntn = (Cout + BN - 1) / BN;
+  const int wg = pipe::xcd_remap();
+  const long m0 = static_cast<long>(wg / ntn) * C::BM;
+  const int n0 = (wg % ntn) * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const pipe::i32x4 xr = pipe::rsrc(x, M * Cin * 4), wr = pipe::rsrc(w, static_cast<long>(Cout) * K * 4);
+  int a_pix[C::A_PW], a_ok[C::A_PW], a_c[C::A_PW], b_off[C::B_PW];
+#pragma unroll
+  for (int c = 0; c < C::A_PW; ++c) {
+    const int row = C::dma_row(wid + 4 * c, lane);
+    const long m = m0 + row;
+    a_c[c] = 4 * C::dma_piece(row, lane);
+    a_pix[c] = static_cast<int>(m);
+    a_ok[c] = 0;
+    if (m < M) {
+      const int rem = static_cast<int>(m % HW);
+      const int yy = rem / W, xx = rem - yy * W;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int y2 = yy + t / 3 - 1, x2 = xx + t % 3 - 1;
+        a_ok[c] |= (y2 >= 0 && y2 < H && x2 >= 0 && x2 < W) << t;
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < C::B_PW; ++c) {
+    const int row = C::dma_row(wid + 4 * c, lane);
+    b_off[c] = n0 + row < Cout ? ((n0 + row) * K + 4 * C::dma_piece(row, lane)) * 4 : -1;
+  }
+  const int KT = K / 16;      // Cin % 16 == 0 (host check): every K-step lies inside one tap
+  auto asrc = [&](int c, int kt) {
+    const int k0 = kt * 16, tap = k0 / Cin, c0 = k0 - tap * Cin;
+    const int shift = (tap / 3 - 1) * W + (tap % 3 - 1);
+    return kt < KT && ((a_ok[c] >> tap) & 1) ? ((a_pix[c] + shift) * Cin + c0 + a_c[c]) * 4 : pipe::kOOB;
+  };
+  auto bsrc = [&](int c, int kt) { return b_off[c] >= 0 && kt < KT ? b_off[c] + kt * 64 : pipe::kOOB; };
+  f16v acc[C::FM][C::FN];
+  pipe::mainloop<C>(smem, xr, wr, KT, asrc, bsrc, acc);
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  pipe::store_tile<C::FM, C::FN>(acc, out, bias, res, M, Cout, m0 + wm * C::TM, n0 + wn * C::TN, act);
+}
+
 template <int BN>
 void launch_f32(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
                 int Cin, int Cout, int act, hipStream_t s) {
@@ -297,6 +357,9 @@ void launch_f32(const float* x, const float* w, const float* bias, const float* 
   if (nwg == 0) return;
   const int mode = f32_mfma_mode();
   if (mode == 1)
+    hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<BN, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias,
+                       res, out, B, H, W, Cin, Cout, act);
+  else if (mode == 3)
     hipLaunchKernelGGL((conv3x3_f32_kernel<BN, 2>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias, res,
                        out, B, H, W, Cin, Cout, act);
   else if (mode == 2)

@@ -23,6 +23,7 @@
 #include "../common.h"
 #include "../kernels.h"
 #include "../split_mfma.h"
+#include "../f32_pipe.h"
 
 namespace as {
 namespace {
@@ -314,6 +315,74 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
   }
 }
 
+// split-MFMA mode: LDS-DMA ring + register split (f32_pipe.h)
+template <int BN, int NS, int BK>
+__global__ __launch_bounds__(256, 3) void gemm_f32_pipe_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                            const float* __restrict__ bias,
+                                                            const float* __restrict__ res, float* __restrict__ out,
+                                                            long M, int N, int K, int act) {
+  using C = pipe::Cfg<BN, NS, BK>;
+  __shared__ __attribute__((aligned(16))) char s0[C::STAGE], s1[C::STAGE], s2[NS > 2 ? C::STAGE : 16],
+      s3[NS > 3 ? C::STAGE : 16];
+  char* const all[4] = {s0, s1, s2, s3};
+  char* smem[NS];
+#pragma unroll
+  for (int i = 0; i < NS; ++i) smem[i] = all[i];
+  const int ntn = (N + BN - 1) / BN;
+  const int wg = pipe::xcd_remap();
+  const long m0 = static_cast<long>(wg / ntn) * C::BM;
+  const int n0 = (wg % ntn) * BN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const pipe::i32x4 ar = pipe::rsrc(a, M * K * 4), br = pipe::rsrc(b, static_cast<long>(N) * K * 4);
+  // this lane's DMA piece per chunk (column piece p of its row, swizzled)
+  int a_off[C::A_PW], a_k[C::A_PW], b_off[C::B_PW], b_k[C::B_PW];
+#pragma unroll
+  for (int c = 0; c < C::A_PW; ++c) {
+    const int row = C::dma_row(wid + 4 * c, lane), p = C::dma_piece(row, lane);
+    const long m = m0 + row;
+    a_k[c] = 4 * p;
+    a_off[c] = m < M ? static_cast<int>((m * K + 4 * p) * 4) : -1;
+  }
+#pragma unroll
+  for (int c = 0; c < C::B_PW; ++c) {
+    const int row = C::dma_row(wid + 4 * c, lane), p = C::dma_piece(row, lane);
+    b_k[c] = 4 * p;
+    b_off[c] = n0 + row < N ? ((n0 + row) * K + 4 * p) * 4 : -1;
+  }
+  auto asrc = [&](int c, int kt) {
+    return a_off[c] >= 0 && kt * BK + a_k[c] < K ? a_off[c] + kt * BK * 4 : pipe::kOOB;
+  };
+  auto bsrc = [&](int c, int kt) {
+    return b_off[c] >= 0 && kt * BK + b_k[c] < K ? b_off[c] + kt * BK * 4 : pipe::kOOB;
+  };
+  f16v acc[C::FM][C::FN];
+  pipe::mainloop<C>(smem, ar, br, (K + BK - 1) / BK, asrc, bsrc, acc);
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  pipe::store_tile<C::FM, C::FN>(acc, out, bias, res, M, N, m0 + wm * C::TM, n0 + wn * C::TN, act);
+}
+
+int pipe_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("APPLESTAR_F32_PIPE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <int BN>
+void launch_pipe(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
+                 int act, hipStream_t s, long nwg) {
+  const dim3 g(static_cast<unsigned>(nwg)), blk(256);
+  // ring depth / K-step measured on the entity-transformer shapes (profiles/r3x_pipe_variants.txt): 3 stages of 16
+  // (48 KB: 3 workgroups per CU) beat 4 x 16 by 4-7 %, 2 x 32 by 7-10 %, 3 x 32 and 6 x 16 (1 workgroup per CU)
+  // by 25-40 % - occupancy, not ring depth, hides the DMA latency
+  switch (pipe_variant()) {
+    case 1: hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 4, 16>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act); break;
+    case 2: hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 2, 32>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act); break;
+    default: hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 3, 16>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act);
+  }
+}
+
 template <int BN, int BK>
 void launch_gemm(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
                  int act, hipStream_t s) {
@@ -321,6 +390,8 @@ void launch_gemm(const float* a, const float* b, const float* bias, const float*
   if (nwg == 0) return;
   const int mode = f32_mfma_mode();
   if (mode == 1)
+    launch_pipe<BN>(a, b, bias, res, out, M, N, K, act, s, nwg);
+  else if (mode == 3)
     hipLaunchKernelGGL((gemm_f32_kernel<BN, BK, 2>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, b, bias, res,
                        out, M, N, K, act);
   else if (mode == 2)
@@ -343,7 +414,7 @@ int& mode_ref() {
   static int mode = [] {
     const char* e = std::getenv("APPLESTAR_F32_MFMA");
     const std::string v = e ? e : "";
-    return v == "exact" ? 0 : (v == "regsplit" ? 2 : 1);
+    return v == "exact" ? 0 : (v == "regsplit" ? 2 : (v == "stagesplit" ? 3 : 1));
   }();
   return mode;
 }
@@ -351,7 +422,7 @@ int& mode_ref() {
 }  // namespace
 
 int f32_mfma_mode() { return mode_ref(); }
-void set_f32_mfma_mode(int mode) { mode_ref() = mode >= 0 && mode <= 2 ? mode : 1; }
+void set_f32_mfma_mode(int mode) { mode_ref() = mode >= 0 && mode <= 3 ? mode : 1; }
 
 void gemm_f32(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
               int act, hipStream_t s) {
