@@ -259,6 +259,12 @@ class _EntityEmbed(torch.autograd.Function):
                                            dout.to(out.dtype).contiguous(), out, k_in)
             return (dw, db, None, None) + (None,) * len(fields)
         dpre = (dout * (out > 0)).to(out_dtype)
+        if out_dtype == torch.float32 and dpre.shape[1] % 4 == 0:
+            # fp32 step: the split-R f32 weight gradient over the one-hot input padded to a multiple of 4 columns
+            kp = (k_in + 3) // 4 * 4
+            X = _C.entity_onehot(list(fields), kind, offset, width, index, kp, _dt_code(out_dtype))
+            dw, db = _C.wgrad_f32(dpre.contiguous(), X, 0, True)
+            return (dw[:, :k_in], db, None, None) + (None,) * len(fields)
         X = _C.entity_onehot(list(fields), kind, offset, width, index, k_in, _dt_code(out_dtype))
         dw = (dpre.t() @ X).float()
         db = dpre.float().sum(0)
@@ -904,6 +910,11 @@ class _GatedResBlock(torch.autograd.Function):
                                   [_w32(gate[2 * i + 1]) for i in range(4)],
                                   [None] * 4, [None] * 4, 0b0111)
             h = acts[-1]
+        elif x.dtype == torch.float32 and _gemm_f32_ok(h.shape[0], C, C):
+            # fp32 step: the four gate layers on the f32 GEMM with bias (+ ReLU) in the epilogue
+            for i in range(4):
+                h = _C.gemm_f32(h, gate[2 * i].detach().view(C, C), _w32(gate[2 * i + 1]), None, 1 if i < 3 else 0)
+                acts.append(h)
         else:
             for i in range(4):
                 gw, gb = gate[2 * i].detach().view(C, C), gate[2 * i + 1].detach()
@@ -933,6 +944,15 @@ class _GatedResBlock(torch.autograd.Function):
             for i, di in ((3, d), (2, d3), (1, d2), (0, d1)):
                 dw_i, db_i = _wgrad(di, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
                 grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
+        elif x.dtype == torch.float32 and _gemm_f32_ok(d.shape[0], C, C):
+            # fp32 step: each input gradient on the f32 GEMM with the previous layer's ReLU mask (ACT_DRELU on its
+            # saved output) or the skip gradient in the epilogue - no threshold_backward / addmm passes
+            for i in (3, 2, 1, 0):
+                dw_i, db_i = _wgrad(d, acts_in[i], 0, True, False)
+                grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
+                if i > 0:
+                    d = _C.gemm_f32(d, _wT(gws[i]), None, acts_in[i], 4)
+            dx_gate = _C.gemm_f32(d, _wT(gws[0]), None, dx_res.view(-1, C).contiguous(), 0)
         else:
             for i in (3, 2, 1, 0):
                 dw_i, db_i = _wgrad(d, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))

@@ -1208,6 +1208,38 @@ def test_fused_resblocks_f32_match_torch_fp64(gated, f32_mfma):
         assert e < 3e-5 * max(1.0, pr.grad.abs().max().item()), (n, e)
 
 
+def test_gated_resblock_f32_gemm_gate_path(f32_mfma, monkeypatch):
+    """At 12 x 38 x 40 pixels the fp32 GatedResBlock's four gate layers take the f32 GEMM (bias + ReLU forward,
+    the ReLU masks and the skip gradient in the dX epilogues).  Against the same block with the gate layers on the
+    library fp32 GEMM, same inputs: every gradient within 1e-5 (relative Frobenius).  The gate layers get small
+    weights and +-1 biases (half the channels on, half off, none near zero): with random ones a few of the 7 M ReLU
+    decisions sit within fp32 rounding of zero and flip between any two fp32 implementations (and against
+    float64), moving the first gate layer's weight gradient by ~1e-3 - tools/diag/gated_block_f32.py,
+    profiles/r3y_gated_block_diag.txt."""
+    import copy
+    from applestar_amd.models.blocks import GatedResBlock
+    torch.manual_seed(9)
+    blk0 = GatedResBlock(128)
+    with torch.no_grad():
+        for m in blk0.GateWeightG:
+            m[0].weight.mul_(0.01)
+            m[0].bias.copy_(torch.where(torch.arange(128) % 2 == 0, 1.0, -1.0))
+    x = torch.randn(12, 128, 38, 40, device=DEV).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(12, 128, 38, 40, device=DEV).contiguous(memory_format=torch.channels_last)
+    assert N._gemm_f32_ok(12 * 38 * 40, 128, 128)
+    grads = []
+    for lib in (False, True):
+        if lib:
+            monkeypatch.setattr(N, '_gemm_f32_ok', lambda *a: False)
+        blk = copy.deepcopy(blk0).to(DEV).to(memory_format=torch.channels_last)
+        xg = x.clone().requires_grad_()
+        blk(xg).backward(g)
+        grads.append([xg.grad] + [p.grad for p in blk.parameters()])
+    for i, (a, r) in enumerate(zip(*grads)):
+        fro = ((a - r).norm() / r.norm()).item()
+        assert fro < 1e-5, (i, fro)
+
+
 @pytest.mark.parametrize('max_norm,wd', [(1.0, 0.0), (1e6, 0.0), (1.0, 1e-4)])
 def test_fused_clip_adam_matches_torch(max_norm, wd):
     """optim.hip (two launches: chunked sum of squares, then clip-scaled Adam) == pytorch_norm clip + torch Adam
