@@ -10,8 +10,11 @@ all-reduce, grad clip, Adam.  Synthetic observations with the reference fake-dat
 
 Precision.  The reference learner is fp32 end to end (``distar/agent/default/rl_learner.py:82-145``:
 no autocast / AMP anywhere in ``distar/``).  ``--precision fp32`` runs the like-for-like step: fp32
-weights, fp32 activations, every GEMM / conv / attention on fp32 operands (gfx950 has no TF32/xf32
-mode, so library GEMMs are exact fp32).  ``--precision bf16`` is the mixed-precision step: bf16
+weights, fp32 activations, every GEMM / conv / attention on fp32 operands.  gfx950 has no TF32/xf32 mode;
+the native conv / GEMM / weight-gradient products run as fp32-accurate bf16x6 split MFMAs
+(``applestar_amd/csrc/split_mfma.h``: exact three-way bf16 split of each fp32 operand, six partial products,
+fp32 accumulation; error vs float64 equal to or below the exact-f32 MFMA's), ``APPLESTAR_F32_MFMA=exact``
+runs them on the exact-f32 MFMA instead; the JSON's ``config.fp32_products`` names the mode.  ``--precision bf16`` is the mixed-precision step: bf16
 compute weights over fp32 master weights, fp32 LayerNorm statistics / softmax / losses / optimizer;
 its training parity against fp32 is pinned by ``tests/test_precision_parity_gpu.py``.
 ``--precision both`` (default) measures both, fp32 first; the headline ``value`` / ``dtype`` are the
@@ -43,6 +46,13 @@ INFERENCE_BASELINE_16ENV_MS = 160.0  # batched GPU inference, 16 envs (guidance_
 
 def _log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def _fp32_products():
+    from applestar_amd.ops import native
+    mode = native.ensure_loaded().f32_mfma_mode()
+    return ('exact-f32 MFMA (v_mfma_f32_32x32x2_f32)' if mode == 0 else
+            'fp32-accurate bf16x6 split MFMA (exact 3-way bf16 split, 6 partial products, fp32 accumulation)')
 
 
 def _make_trainer(args, precision, device):
@@ -262,6 +272,7 @@ def main():
                 'precision': ('fp32 weights / activations / GEMM operands (like-for-like with the reference)'
                               if head == 'fp32' else 'bf16 compute over fp32 master weights'),
                 'native_kernels': (not args.no_native) and gpu,
+                'fp32_products': (_fp32_products() if head == 'fp32' and gpu and not args.no_native else None),
                 **{k: v for k, v in hs.items() if k not in ('value', 'ms_per_step', 'vs_baseline')},
                 'graph_step': results[head]['graph_step'],
             },
