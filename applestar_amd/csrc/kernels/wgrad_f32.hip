@@ -15,6 +15,7 @@
 #include "../common.h"
 #include "../kernels.h"
 #include "../split_mfma.h"
+#include "../f32_pipe.h"
 
 namespace as {
 namespace {
@@ -232,11 +233,186 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
   }
 }
 
+// split-MFMA mode on the LDS-DMA ring of f32_pipe.h: K-steps of RS = 16 reduction rows, stage = the dY rows
+// [16][BN] then the X rows [16][BK] as loaded (lane-linear, 1 KB per DMA wave-instruction = 1024 / (4 BN) rows).
+// Fragments: lane (l32, h) takes rows 8 h .. 8 h + 7 of its column (eight ds_read_b32; the 32 lanes of a b32 group
+// read 32 consecutive floats of one row).  The conv form's X piece of a lane is a fixed 4-channel group of one tap
+// (the lane's column is the same in every stage); its row's image coordinates advance by 16 rows per issued step.
+template <int BN, int BK, bool CONV, int NS>
+__global__ __launch_bounds__(256, (BN == 128 && BK == 128) ? 2 : 3) void wgrad_f32_pipe_kernel(const float* __restrict__ dy,
+                                                                const float* __restrict__ x,
+                                                                float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                                long part_stride, long R, int N, int K, int H, int W,
+                                                                int Cin, long rows_per_split, int tiles_n, int tiles_k) {
+  constexpr int RS = 16;
+  constexpr int A_BYTES = RS * BN * 4, B_BYTES = RS * BK * 4, STAGE = A_BYTES + B_BYTES;
+  constexpr int A_PW = A_BYTES / 4096, B_PW = B_BYTES / 4096;          // DMA wave-instructions per wave
+  constexpr int A_CPR = BN / 4, B_CPR = BK / 4;                       // 16-B pieces per row
+  constexpr int A_RPI = 64 / A_CPR, B_RPI = 64 / B_CPR;               // rows per wave-instruction
+  static_assert(A_PW >= 1 && B_PW >= 1 && A_PW * 4096 == A_BYTES && B_PW * 4096 == B_BYTES, "tile / DMA mismatch");
+  constexpr int WN = BN >= 64 ? 2 : 1, WK = 4 / WN;
+  constexpr int TN = BN / WN, TK = BK / WK, FN = TN / 32, FK = TK / 32;
+  static_assert(NS == 3, "three stage arrays");
+  __shared__ __attribute__((aligned(16))) char s0[STAGE], s1[STAGE], s2[STAGE];
+  char* const smem[3] = {s0, s1, s2};
+
+  const int wg = pipe::xcd_remap();
+  const int tk = wg % tiles_k;
+  const int tn = (wg / tiles_k) % tiles_n;
+  const int s = wg / (tiles_k * tiles_n);
+  const int n0 = tn * BN, k0 = tk * BK;
+  const long r_begin = static_cast<long>(s) * rows_per_split;
+  const long r_end = r_begin + rows_per_split < R ? r_begin + rows_per_split : R;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wid / WK, wk = wid % WK;
+  const int l32 = lane & 31, h = lane >> 5;
+  const long HW = static_cast<long>(H) * W;
+  const pipe::i32x4 yr = pipe::rsrc(dy, R * N * 4), xr = pipe::rsrc(x, CONV ? R * Cin * 4 : R * K * 4);
+
+  // DMA pieces: fixed column per lane, row (within a step) per chunk
+  const int a_col = n0 + 4 * (lane % A_CPR), b_col = k0 + 4 * (lane % B_CPR);
+  int a_row[A_PW], b_row[B_PW];
+#pragma unroll
+  for (int c = 0; c < A_PW; ++c) a_row[c] = (wid + 4 * c) * A_RPI + lane / A_CPR;
+#pragma unroll
+  for (int c = 0; c < B_PW; ++c) b_row[c] = (wid + 4 * c) * B_RPI + lane / B_CPR;
+  int b_c = b_col, b_dy = 0, b_dx = 0;
+  if (CONV) {
+    const int tap = b_col / Cin;
+    b_c = b_col - tap * Cin;
+    b_dy = tap / 3 - 1;
+    b_dx = tap % 3 - 1;
+  }
+  const bool a_ok = a_col < N, b_ok = b_col < K;
+  // conv: image coordinates of each chunk's row for the next step to issue (advanced by RS rows per issue)
+  int py[B_PW], px[B_PW];
+  const int adv_y = RS / W, adv_x = RS % W;
+  if (CONV) {
+#pragma unroll
+    for (int c = 0; c < B_PW; ++c) {
+      const int rem = static_cast<int>((r_begin + b_row[c]) % HW);
+      py[c] = rem / W;
+      px[c] = rem - py[c] * W;
+    }
+  }
+  const long nsteps = r_end > r_begin ? (r_end - r_begin + RS - 1) / RS : 0;
+  auto issue = [&](char* st, long kt) {
+    const long r0 = r_begin + kt * RS;
+#pragma unroll
+    for (int c = 0; c < A_PW; ++c) {
+      const long r = r0 + a_row[c];
+      pipe::dma16(yr, st + (wid + 4 * c) * 1024,
+                  (kt < nsteps && a_ok && r < r_end) ? (static_cast<int>(r) * N + a_col) * 4 : pipe::kOOB);
+    }
+#pragma unroll
+    for (int c = 0; c < B_PW; ++c) {
+      const long r = r0 + b_row[c];
+      int off = pipe::kOOB;
+      if (CONV) {
+        const int yy = py[c] + b_dy, xx = px[c] + b_dx;
+        if (kt < nsteps && b_ok && r < r_end && yy >= 0 && yy < H && xx >= 0 && xx < W)
+          off = ((static_cast<int>(r) + b_dy * W + b_dx) * Cin + b_c) * 4;
+        px[c] += adv_x;
+        py[c] += adv_y;
+        if (px[c] >= W) { px[c] -= W; ++py[c]; }
+        while (py[c] >= H) py[c] -= H;
+      } else if (kt < nsteps && b_ok && r < r_end) {
+        off = (static_cast<int>(r) * K + b_col) * 4;
+      }
+      pipe::dma16(xr, st + A_BYTES + (wid + 4 * c) * 1024, off);
+    }
+  };
+
+  f16v acc[FN][FK];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const bool do_bias = db_part != nullptr && tk == 0 && wk == 0;
+  float bsum[FN];
+#pragma unroll
+  for (int i = 0; i < FN; ++i) bsum[i] = 0.f;
+
+  auto step = [&](const char* st, char* next, long kt) {
+    pipe::wait_vm<(NS - 2) * (A_PW + B_PW)>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(next, kt + NS - 1);
+    const float* A = reinterpret_cast<const float*>(st) + (8 * h) * BN + wn * TN + l32;
+    const float* Bt = reinterpret_cast<const float*>(st + A_BYTES) + (8 * h) * BK + wk * TK + l32;
+    float av[FN][8], bv[FK][8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i) av[i][t] = A[t * BN + 32 * i];
+#pragma unroll
+      for (int j = 0; j < FK; ++j) bv[j][t] = Bt[t * BK + 32 * j];
+    }
+    Split3 sa[FN], sb[FK];
+#pragma unroll
+    for (int i = 0; i < FN; ++i) sa[i] = split8(av[i]);
+#pragma unroll
+    for (int j = 0; j < FK; ++j) sb[j] = split8(bv[j]);
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FK; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+    if (do_bias) {
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) bsum[i] += av[i][t];
+    }
+  };
+  issue(smem[0], 0);
+  issue(smem[1], 1);
+  for (long kt = 0; kt < nsteps; kt += NS) {
+    step(smem[0], smem[2], kt);
+    if (kt + 1 >= nsteps) break;
+    step(smem[1], smem[0], kt + 1);
+    if (kt + 2 >= nsteps) break;
+    step(smem[2], smem[1], kt + 2);
+  }
+  pipe::wait_vm<0>();
+
+  // accumulator (i, j) register e: n = n0 + wn TN + 32 i + (e&3) + 8 (e>>2) + 4 h, k = k0 + wk TK + 32 j + l32
+  float* outp = dw_part + static_cast<long>(s) * part_stride;
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FK; ++j) {
+      const int k = k0 + wk * TK + 32 * j + l32;
+      if (k >= K) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int n = n0 + wn * TN + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (n < N) outp[static_cast<long>(n) * K + k] = acc[i][j][e];
+      }
+    }
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const float v = bsum[i] + __shfl_xor(bsum[i], 32, kWave);
+      const int n = n0 + wn * TN + 32 * i + l32;
+      if (h == 0 && n < N) db_part[static_cast<long>(s) * part_stride + n] = v;
+    }
+  }
+}
+
 template <int BN, int BK, bool CONV>
 void launch(const float* dy, const float* x, float* dwp, float* dbp, long ps, long R, int N, int K, int H, int W,
             int Cin, int S, long rps, hipStream_t st) {
   const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
   const long nwg = static_cast<long>(tn) * tk * S;
+  if constexpr (BN >= 64) {
+    if (f32_mfma_mode() == 1) {
+      hipLaunchKernelGGL((wgrad_f32_pipe_kernel<BN, BK, CONV, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st,
+                         dy, x, dwp, dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
+      return;
+    }
+  }
   if (f32_mfma_mode())
     hipLaunchKernelGGL((wgrad_f32_kernel<BN, BK, CONV, 1>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x,
                        dwp, dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
