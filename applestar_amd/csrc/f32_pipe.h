@@ -36,9 +36,9 @@ constexpr int kOOB = 0x7ffffff0;
 #define PIPE_ABL 0
 #endif
 
-template <int BN_, int NS_, int BK_ = 16>
+template <int BN_, int NS_, int BK_ = 16, int BM_ = 128>
 struct Cfg {
-  static constexpr int BM = 128, BN = BN_, NS = NS_, BK = BK_, NT = 256;
+  static constexpr int BM = BM_, BN = BN_, NS = NS_, BK = BK_, NT = 256;
   static constexpr int WN = BN_ >= 128 ? 2 : 1, WM = 4 / WN;
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 32, FN = TN / 32;

@@ -20,6 +20,8 @@
 // pitches 20 r mod 32 for r = 0..7 are disjoint 4-bank windows; row-major dealing put two rows' 16 floats
 // on overlapping banks: 2-way on every staging write).  The epilogue stores straight from the
 // accumulators: 32 lanes write 32 consecutive channels (128 B) of one pixel.
+#include <cstdlib>
+
 #include "../common.h"
 #include "../kernels.h"
 #include "../split_mfma.h"
@@ -292,12 +294,12 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
 
 // split-MFMA mode: the LDS-DMA ring of f32_pipe.h with the A rows gathered per tap (a lane's DMA piece is 4
 // channels of its row's shifted pixel; taps outside the image read zeros through the buffer range check)
-template <int BN, int NS>
-__global__ __launch_bounds__(256, 3) void conv3x3_f32_pipe_kernel(const float* __restrict__ x, const float* __restrict__ w,
+template <int BN, int NS, int BM = 128>
+__global__ __launch_bounds__(256, BM == 128 ? 3 : 2) void conv3x3_f32_pipe_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                                const float* __restrict__ bias,
                                                                const float* __restrict__ res, float* __restrict__ out,
                                                                int B, int H, int W, int Cin, int Cout, int act) {
-  using C = pipe::Cfg<BN, NS, 16>;
+  using C = pipe::Cfg<BN, NS, 16, BM>;
   __shared__ __attribute__((aligned(16))) char s0[C::STAGE], s1[C::STAGE], s2[NS > 2 ? C::STAGE : 16],
       s3[NS > 3 ? C::STAGE : 16];
   char* const all[4] = {s0, s1, s2, s3};
