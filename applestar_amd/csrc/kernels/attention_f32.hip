@@ -18,8 +18,11 @@
 // apart), with the swap both the float4 row reads and the transposed one-float-per-lane reads are
 // conflict-free (exhaustive check over the ds_read_b128 / b32 lane groups).  (A register prefetch of the next
 // key block measured slower in the learner step: 64 more live VGPRs for sequences of 1-8 blocks, r3i.)
+#include <cstdlib>
+
 #include "../common.h"
 #include "../kernels.h"
+#include "../split_mfma.h"
 
 namespace as {
 namespace {
@@ -104,6 +107,61 @@ __device__ __forceinline__ void tr_accumulate(const float* T, int n, const f4& b
       acc[nd] = mfma4((nd & 2) ? hi[i * P + 16 * nd] : lo[i * P + 16 * nd], b[i], acc[nd]);
 }
 
+// ---- bf16x6 split-MFMA forms (split_mfma.h) on v_mfma_f32_16x16x32_bf16: A[l&15][k = 8 (l>>4) + t],
+// B[k][l&15], the same C layout as the 16x16x4 f32 MFMA.  Fragments are split in registers.
+__device__ __forceinline__ f4 mfma16_bf16(u32v4 a, u32v4 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(a), as_bf(b), c, 0, 0, 0);
+}
+__device__ __forceinline__ f4 mfma16_x6(const Split3& a, const Split3& b, f4 c) {
+  c = mfma16_bf16(a.p[1], b.p[1], c);
+  c = mfma16_bf16(a.p[0], b.p[2], c);
+  c = mfma16_bf16(a.p[2], b.p[0], c);
+  c = mfma16_bf16(a.p[0], b.p[1], c);
+  c = mfma16_bf16(a.p[1], b.p[0], c);
+  return mfma16_bf16(a.p[0], b.p[0], c);
+}
+
+// the 32-float register fragment (dims 32 lg + j) as four split 8-float groups: group c = dims 32 lg + 8 c + t
+__device__ __forceinline__ void split_frag(const float (&f)[32], Split3 (&fs)[4]) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) fs[c] = split8(*reinterpret_cast<const float(*)[8]>(&f[8 * c]));
+}
+
+// row_dot with split products: instruction c takes dims 32 lg + 8 c + t (k-slot t of lane group lg)
+__device__ __forceinline__ f4 row_dot_x6(const float* T, int n, const Split3 (&fs)[4], f4 acc) {
+  const int l = threadIdx.x & 63;
+  const float* row = T + swz(16 * n + (l & 15), 32 * (l >> 4));
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float4 a0 = *reinterpret_cast<const float4*>(row + 8 * c);
+    const float4 a1 = *reinterpret_cast<const float4*>(row + 8 * c + 4);
+    const float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    acc = mfma16_x6(split8(v), fs[c], acc);
+  }
+  return acc;
+}
+
+// tr_accumulate over the key tile pair (2 p, 2 p + 1) with split products: k-slot t of lane group lg is key
+// 16 (2 p + (t >> 2)) + 4 lg + (t & 3); B = this lane's C registers of the two tiles
+__device__ __forceinline__ void tr_accumulate_x6(const float* T, int p, const f4& b0, const f4& b1, f4 (&acc)[8]) {
+  const int l = threadIdx.x & 63, lr = l & 15, lg = l >> 4;
+  const int sw = (lg >> 1) << 5;
+  const float bv[8] = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+  const Split3 sb = split8(bv);
+#pragma unroll
+  for (int nd = 0; nd < 8; ++nd) {
+    float av[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int n = 2 * p + (t >> 2), i = t & 3;
+      const float* lo = T + (16 * n + 4 * lg) * P + lr + sw;
+      const float* hi = T + (16 * n + 4 * lg) * P + lr - sw;
+      av[t] = (nd & 2) ? hi[i * P + 16 * nd] : lo[i * P + 16 * nd];
+    }
+    acc[nd] = mfma16_x6(split8(av), sb, acc[nd]);
+  }
+}
+
 __device__ __forceinline__ bool attn_item(int QB, int S, int H, int& blk, int& s, int& h) {
   const int per = gridDim.x >> 3;
   const int u = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
@@ -115,6 +173,7 @@ __device__ __forceinline__ bool attn_item(int QB, int S, int H, int& blk, int& s
   return true;
 }
 
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void attn_f32_fwd_kernel(const float* __restrict__ qkv, const int* __restrict__ cu,
                                                             float* __restrict__ out, float* __restrict__ lse2, int H,
                                                             long Ttot, float scale_log2, int QB, int S) {
@@ -132,6 +191,8 @@ __global__ __launch_bounds__(256) void attn_f32_fwd_kernel(const float* __restri
   const int qrow = qb * BR + w * 16 + lr;
   float qf[32];
   load_row32(qf, seq + static_cast<long>(qrow < len ? qrow : 0) * ROW + h * D + 32 * lg, qrow < len);
+  Split3 qs[4];
+  if constexpr (SPLIT) split_frag(qf, qs);
   f4 o[8];   // O^T: o[nd][i] = O[qrow][16 nd + 4 lg + i]
 #pragma unroll
   for (int n = 0; n < 8; ++n) o[n] = f4{0.f, 0.f, 0.f, 0.f};
@@ -144,7 +205,8 @@ __global__ __launch_bounds__(256) void attn_f32_fwd_kernel(const float* __restri
     __syncthreads();
     f4 st[4];   // S^T: st[n][i] = S[qrow][key kb*64 + 16 n + 4 lg + i]
 #pragma unroll
-    for (int n = 0; n < 4; ++n) st[n] = row_dot(K_s, n, qf, f4{0.f, 0.f, 0.f, 0.f});
+    for (int n = 0; n < 4; ++n)
+      st[n] = SPLIT ? row_dot_x6(K_s, n, qs, f4{0.f, 0.f, 0.f, 0.f}) : row_dot(K_s, n, qf, f4{0.f, 0.f, 0.f, 0.f});
     float mx = -1e30f;
 #pragma unroll
     for (int n = 0; n < 4; ++n)
@@ -171,8 +233,13 @@ __global__ __launch_bounds__(256) void attn_f32_fwd_kernel(const float* __restri
     for (int n = 0; n < 8; ++n)
 #pragma unroll
       for (int i = 0; i < 4; ++i) o[n][i] *= alpha;
+    if constexpr (SPLIT) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) tr_accumulate(V_s, n, st[n], o);
+      for (int p2 = 0; p2 < 2; ++p2) tr_accumulate_x6(V_s, p2, st[2 * p2], st[2 * p2 + 1], o);
+    } else {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) tr_accumulate(V_s, n, st[n], o);
+    }
   }
   if (qrow < len) {
     const float inv = 1.f / lsum;
@@ -186,6 +253,7 @@ __global__ __launch_bounds__(256) void attn_f32_fwd_kernel(const float* __restri
 }
 
 // dQ (and delta = rowsum(dO * O)) for 64 rows; loops key blocks: S^T, dP^T, dS^T, dQ^T += K^T dS^T
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void attn_f32_bwd_dq_kernel(const float* __restrict__ qkv, const float* __restrict__ o,
                                                                const float* __restrict__ dout,
                                                                const float* __restrict__ lse2, float* __restrict__ delta,
@@ -210,6 +278,11 @@ __global__ __launch_bounds__(256) void attn_f32_bwd_dq_kernel(const float* __res
   float qf[32], df[32];
   load_row32(qf, seq + static_cast<long>(qr) * ROW + h * D + 32 * lg, rval);
   load_row32(df, dseq + static_cast<long>(qr) * HD + h * D + 32 * lg, rval);
+  Split3 qs[4], ds[4];
+  if constexpr (SPLIT) {
+    split_frag(qf, qs);
+    split_frag(df, ds);
+  }
   const float ls = rval ? lse2[static_cast<long>(h) * Ttot + start + qrow] : 1e30f;
   float dl = 0.f;
   {
@@ -231,17 +304,38 @@ __global__ __launch_bounds__(256) void attn_f32_bwd_dq_kernel(const float* __res
     stage_tile(K_s, seq + HD + h * D, ROW, kb * BR, len);
     stage_tile(V_s, seq + 2 * HD + h * D, ROW, kb * BR, len);
     __syncthreads();
+    if constexpr (SPLIT) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const f4 st = row_dot(K_s, n, qf, f4{0.f, 0.f, 0.f, 0.f});
-      f4 dpt = row_dot(V_s, n, df, f4{0.f, 0.f, 0.f, 0.f});
+      for (int p2 = 0; p2 < 2; ++p2) {
+        f4 dpp[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const bool kv = kb * BR + 16 * n + 4 * lg + i < len;
-        const float p = kv ? ex2(st[i] * scale_log2 - ls) : 0.f;
-        dpt[i] = p * (dpt[i] - dl);
+        for (int u = 0; u < 2; ++u) {
+          const int n = 2 * p2 + u;
+          const f4 st = row_dot_x6(K_s, n, qs, f4{0.f, 0.f, 0.f, 0.f});
+          f4 dpt = row_dot_x6(V_s, n, ds, f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const bool kv = kb * BR + 16 * n + 4 * lg + i < len;
+            const float p = kv ? ex2(st[i] * scale_log2 - ls) : 0.f;
+            dpt[i] = p * (dpt[i] - dl);
+          }
+          dpp[u] = dpt;
+        }
+        tr_accumulate_x6(K_s, p2, dpp[0], dpp[1], dq);
       }
-      tr_accumulate(K_s, n, dpt, dq);
+    } else {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const f4 st = row_dot(K_s, n, qf, f4{0.f, 0.f, 0.f, 0.f});
+        f4 dpt = row_dot(V_s, n, df, f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool kv = kb * BR + 16 * n + 4 * lg + i < len;
+          const float p = kv ? ex2(st[i] * scale_log2 - ls) : 0.f;
+          dpt[i] = p * (dpt[i] - dl);
+        }
+        tr_accumulate(K_s, n, dpt, dq);
+      }
     }
   }
   if (rval) {
@@ -255,6 +349,7 @@ __global__ __launch_bounds__(256) void attn_f32_bwd_dq_kernel(const float* __res
 
 // dK, dV for 64 keys; loops row blocks: S = Q K^T and dP = dO V^T leave lane (lg, lr) holding key lr and
 // rows 16 n + 4 lg + i; dV^T += dO^T P, dK^T += Q^T dS take P / dS from registers
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void attn_f32_bwd_dkdv_kernel(const float* __restrict__ qkv,
                                                                  const float* __restrict__ dout,
                                                                  const float* __restrict__ lse2,
@@ -281,6 +376,11 @@ __global__ __launch_bounds__(256) void attn_f32_bwd_dkdv_kernel(const float* __r
   float kf[32], vf[32];
   load_row32(kf, seq + static_cast<long>(kr) * ROW + HD + h * D + 32 * lg, kval);
   load_row32(vf, seq + static_cast<long>(kr) * ROW + 2 * HD + h * D + 32 * lg, kval);
+  Split3 ks[4], vs[4];
+  if constexpr (SPLIT) {
+    split_frag(kf, ks);
+    split_frag(vf, vs);
+  }
   f4 dk[8], dv[8];   // dK^T / dV^T: [nd][i] = d(key)[16 nd + 4 lg + i]
 #pragma unroll
   for (int n = 0; n < 8; ++n) { dk[n] = f4{0.f, 0.f, 0.f, 0.f}; dv[n] = f4{0.f, 0.f, 0.f, 0.f}; }
@@ -295,19 +395,43 @@ __global__ __launch_bounds__(256) void attn_f32_bwd_dkdv_kernel(const float* __r
       del_s[tid] = r < len ? delta[static_cast<long>(h) * Ttot + start + r] : 0.f;
     }
     __syncthreads();
+    if constexpr (SPLIT) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      f4 sc = row_dot(Q_s, n, kf, f4{0.f, 0.f, 0.f, 0.f});     // [i]: row 16 n + 4 lg + i, key lr
-      f4 dp = row_dot(dO_s, n, vf, f4{0.f, 0.f, 0.f, 0.f});
+      for (int p2 = 0; p2 < 2; ++p2) {
+        f4 scp[2], dpp[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rl = 16 * n + 4 * lg + i;
-        const float p = kval ? ex2(sc[i] * scale_log2 - lse_s[rl]) : 0.f;   // padded rows: lse = +inf
-        sc[i] = p;
-        dp[i] = p * (dp[i] - del_s[rl]);
+        for (int u = 0; u < 2; ++u) {
+          const int n = 2 * p2 + u;
+          f4 sc = row_dot_x6(Q_s, n, ks, f4{0.f, 0.f, 0.f, 0.f});
+          f4 dp = row_dot_x6(dO_s, n, vs, f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int rl = 16 * n + 4 * lg + i;
+            const float p = kval ? ex2(sc[i] * scale_log2 - lse_s[rl]) : 0.f;
+            sc[i] = p;
+            dp[i] = p * (dp[i] - del_s[rl]);
+          }
+          scp[u] = sc;
+          dpp[u] = dp;
+        }
+        tr_accumulate_x6(dO_s, p2, scp[0], scp[1], dv);
+        tr_accumulate_x6(Q_s, p2, dpp[0], dpp[1], dk);
       }
-      tr_accumulate(dO_s, n, sc, dv);
-      tr_accumulate(Q_s, n, dp, dk);
+    } else {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        f4 sc = row_dot(Q_s, n, kf, f4{0.f, 0.f, 0.f, 0.f});     // [i]: row 16 n + 4 lg + i, key lr
+        f4 dp = row_dot(dO_s, n, vf, f4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rl = 16 * n + 4 * lg + i;
+          const float p = kval ? ex2(sc[i] * scale_log2 - lse_s[rl]) : 0.f;   // padded rows: lse = +inf
+          sc[i] = p;
+          dp[i] = p * (dp[i] - del_s[rl]);
+        }
+        tr_accumulate(dO_s, n, sc, dv);
+        tr_accumulate(Q_s, n, dp, dk);
+      }
     }
   }
   if (kval) {
@@ -330,7 +454,10 @@ void varlen_attn_fwd_f32(const float* qkv, const int* cu, float* out, float* lse
   const float scale_log2 = scale * 1.4426950408889634f;
   const int QB = (max_len + BR - 1) / BR;
   const dim3 grid(static_cast<unsigned>((static_cast<long>(QB) * S * H + 7) / 8 * 8));
-  hipLaunchKernelGGL(attn_f32_fwd_kernel, grid, dim3(256), 0, s, qkv, cu, out, lse2, H, Ttot, scale_log2, QB, S);
+  if (f32_mfma_mode())
+    hipLaunchKernelGGL(attn_f32_fwd_kernel<true>, grid, dim3(256), 0, s, qkv, cu, out, lse2, H, Ttot, scale_log2, QB, S);
+  else
+    hipLaunchKernelGGL(attn_f32_fwd_kernel<false>, grid, dim3(256), 0, s, qkv, cu, out, lse2, H, Ttot, scale_log2, QB, S);
 }
 
 void varlen_attn_bwd_f32(const float* qkv, const float* out, const float* dout, const float* lse2, const int* cu,
@@ -338,10 +465,23 @@ void varlen_attn_bwd_f32(const float* qkv, const float* out, const float* dout, 
   const float scale_log2 = scale * 1.4426950408889634f;
   const int QB = (max_len + BR - 1) / BR;
   const dim3 grid(static_cast<unsigned>((static_cast<long>(QB) * S * H + 7) / 8 * 8));
-  hipLaunchKernelGGL(attn_f32_bwd_dq_kernel, grid, dim3(256), 0, s, qkv, out, dout, lse2, delta, cu, dqkv, H, Ttot,
-                     scale_log2, scale, QB, S);
-  hipLaunchKernelGGL(attn_f32_bwd_dkdv_kernel, grid, dim3(256), 0, s, qkv, dout, lse2, delta, cu, dqkv, H, Ttot,
-                     scale_log2, scale, QB, S);
+  // the split backward kernels hold 228 / 276 VGPRs (one workgroup per CU for dK/dV) and measured 17 % slower
+  // than the exact-f32 ones (r3z_attn_micro.txt): the backward stays on the exact-f32 MFMA unless asked for
+  static const bool bwd_split = [] {
+    const char* e = std::getenv("APPLESTAR_F32_ATTN_BWD_SPLIT");
+    return e && e[0] == '1';
+  }();
+  if (f32_mfma_mode() && bwd_split) {
+    hipLaunchKernelGGL(attn_f32_bwd_dq_kernel<true>, grid, dim3(256), 0, s, qkv, out, dout, lse2, delta, cu, dqkv, H,
+                       Ttot, scale_log2, scale, QB, S);
+    hipLaunchKernelGGL(attn_f32_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, qkv, dout, lse2, delta, cu, dqkv, H, Ttot,
+                       scale_log2, scale, QB, S);
+  } else {
+    hipLaunchKernelGGL(attn_f32_bwd_dq_kernel<false>, grid, dim3(256), 0, s, qkv, out, dout, lse2, delta, cu, dqkv, H,
+                       Ttot, scale_log2, scale, QB, S);
+    hipLaunchKernelGGL(attn_f32_bwd_dkdv_kernel<false>, grid, dim3(256), 0, s, qkv, dout, lse2, delta, cu, dqkv, H,
+                       Ttot, scale_log2, scale, QB, S);
+  }
 }
 
 }  // namespace as

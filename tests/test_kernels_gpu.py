@@ -266,7 +266,7 @@ def test_varlen_attention_matches_reference(lens):
 
 @pytest.mark.parametrize('lens', [[1, 64, 65, 200, 511], [37], [128, 3, 300]])
 @pytest.mark.parametrize('score_scale', [0.5, 2.0])
-def test_varlen_attention_fp32_matches_fp64(lens, score_scale):
+def test_varlen_attention_fp32_matches_fp64(lens, score_scale, f32_mfma):
     """fp32 operands take the f32-MFMA kernel (attention_f32.hip), never a bf16 copy: forward and all three
     input gradients within fp32 rounding of a float64 reference."""
     torch.manual_seed(11)
