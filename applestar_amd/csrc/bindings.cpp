@@ -362,12 +362,20 @@ at::Tensor upsample2x_fwd(const at::Tensor& x) {  // x [B,H,W,C]
   return y;
 }
 
-at::Tensor upsample2x_bwd(const at::Tensor& dy) {  // dy [B,2H,2W,C]
+// mask (optional): the forward input x (NHWC, a ReLU output): dx *= [x > 0]
+at::Tensor upsample2x_bwd(const at::Tensor& dy, const c10::optional<at::Tensor>& mask) {  // dy [B,2H,2W,C]
   check_cuda(dy, "dy");
   TORCH_CHECK(dy.dim() == 4 && dy.size(3) % 4 == 0 && dy.size(1) % 2 == 0 && dy.size(2) % 2 == 0, "upsample2x_bwd");
   c10::hip::HIPGuard g(dy.device().index());
   auto dx = at::empty({dy.size(0), dy.size(1) / 2, dy.size(2) / 2, dy.size(3)}, dy.options());
-  as::upsample2x_bwd(dy.data_ptr(), dx.data_ptr(), dt(dy), dx.size(0), dx.size(1), dx.size(2), dx.size(3), stream());
+  const void* mp = nullptr;
+  if (mask && mask->defined()) {
+    TORCH_CHECK(mask->sizes() == dx.sizes() && mask->scalar_type() == dy.scalar_type() && mask->is_contiguous(),
+                "upsample2x_bwd: mask");
+    mp = mask->data_ptr();
+  }
+  as::upsample2x_bwd(dy.data_ptr(), dx.data_ptr(), dt(dy), dx.size(0), dx.size(1), dx.size(2), dx.size(3), stream(),
+                     mp);
   return dx;
 }
 
@@ -689,15 +697,23 @@ std::vector<at::Tensor> maxpool2_fwd(const at::Tensor& x) {  // x [B,H,W,C]
   return {y, pos};
 }
 
-at::Tensor maxpool2_bwd(const at::Tensor& dy, const at::Tensor& pos, int64_t H, int64_t W) {
+// mask (optional): the forward input x (NHWC, a ReLU output): dx *= [x > 0]
+at::Tensor maxpool2_bwd(const at::Tensor& dy, const at::Tensor& pos, int64_t H, int64_t W,
+                        const c10::optional<at::Tensor>& mask) {
   check_cuda(dy, "dy");
   check_cuda(pos, "pos");
   TORCH_CHECK(dy.dim() == 4 && dy.sizes() == pos.sizes() && dy.size(1) == H / 2 && dy.size(2) == W / 2,
               "maxpool2_bwd: shapes");
   c10::hip::HIPGuard g(dy.device().index());
   auto dx = at::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
+  const void* mp = nullptr;
+  if (mask && mask->defined()) {
+    TORCH_CHECK(mask->sizes() == dx.sizes() && mask->scalar_type() == dy.scalar_type() && mask->is_contiguous(),
+                "maxpool2_bwd: mask");
+    mp = mask->data_ptr();
+  }
   as::maxpool2_bwd(dy.data_ptr(), pos.data_ptr<uint8_t>(), dx.data_ptr(), dt(dy), dy.size(0), H, W, dy.size(3),
-                   stream());
+                   stream(), mp);
   return dx;
 }
 
@@ -1649,7 +1665,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("entity_embed_fwd", &entity_embed_fwd);
   m.def("entity_onehot", &entity_onehot);
   m.def("upsample2x_fwd", &upsample2x_fwd);
-  m.def("upsample2x_bwd", &upsample2x_bwd);
+  m.def("upsample2x_bwd", &upsample2x_bwd, py::arg("dy"), py::arg("mask") = py::none());
   m.def("entity_embed_wgrad", &entity_embed_wgrad);
   m.def("mm_k32", &mm_k32);
   m.def("spatial_embed_fwd", &spatial_embed_fwd);
@@ -1678,7 +1694,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("upconv1_fwd", &upconv1_fwd);
   m.def("upconv1_bwd", &upconv1_bwd);
   m.def("maxpool2_fwd", &maxpool2_fwd);
-  m.def("maxpool2_bwd", &maxpool2_bwd);
+  m.def("maxpool2_bwd", &maxpool2_bwd, py::arg("dy"), py::arg("pos"), py::arg("H"), py::arg("W"),
+        py::arg("mask") = py::none());
   m.def("maxpool2_bwd_relu", &maxpool2_bwd_relu);
   m.def("spatial_embed_pool_fwd", &spatial_embed_pool_fwd);
   m.def("spatial_pool_supported", [](int64_t h, int64_t w) { return as::spatial_pool_supported(static_cast<int>(h), static_cast<int>(w)); });

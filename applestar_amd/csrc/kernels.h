@@ -115,7 +115,8 @@ struct SpatialPlanes {
 };
 // NHWC bilinear x2 (align_corners=False); C % 4 == 0
 void upsample2x_fwd(const void* x, void* y, int dt, int B, int H, int W, int C, hipStream_t s);
-void upsample2x_bwd(const void* dy, void* dx, int dt, int B, int H, int W, int C, hipStream_t s);
+void upsample2x_bwd(const void* dy, void* dx, int dt, int B, int H, int W, int C, hipStream_t s,
+                    const void* mask = nullptr);
 // bits [B*H*W] (zeroed, size % 4 == 0): bit e set where effect e has a point
 void spatial_effect_bits(const SpatialPlanes& sp, uint8_t* bits, int B, int L, int HW, hipStream_t s);
 // pre [npix][32] = bias + Wd . dense(pixel);  Wd [32][24]
@@ -198,7 +199,8 @@ namespace as {
 // ---- pool_reduce.hip ---------------------------------------------------------------------------
 // NHWC 2x2/stride-2 max-pool; pos [B,H/2,W/2,C] uint8 window position; C % 8 == 0
 void maxpool2_fwd(const void* x, void* y, uint8_t* pos, int dt, int B, int H, int W, int C, hipStream_t s);
-void maxpool2_bwd(const void* dy, const uint8_t* pos, void* dx, int dt, int B, int H, int W, int C, hipStream_t s);
+void maxpool2_bwd(const void* dy, const uint8_t* pos, void* dx, int dt, int B, int H, int W, int C, hipStream_t s,
+                  const void* mask = nullptr);
 // bf16, even H / W: dx = dy at the argmax where the pooled ReLU output y > 0, else 0 (relu -> maxpool2 backward)
 void maxpool2_bwd_relu(const void* dy, const uint8_t* pos, const void* y, void* dx, int B, int H, int W, int C,
                        hipStream_t s);

@@ -104,9 +104,12 @@ __global__ __launch_bounds__(256) void maxpool2_fwd_kernel(const T* __restrict__
 }
 
 // dy [B][Ho][Wo][C], pos -> dx [B][H][W][C] (every element written; an odd trailing row/col gets 0)
+// mask (optional): the pool's input x when it is a ReLU output - dx is also multiplied by [x > 0] (the
+// producer's ReLU backward folded in; its separate threshold pass is then skipped, ops/native.py _premasked)
 template <typename T>
 __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const T* __restrict__ dy, const uint8_t* __restrict__ pos,
-                                                           T* __restrict__ dx, int B, int H, int W, int C) {
+                                                           T* __restrict__ dx, int B, int H, int W, int C,
+                                                           const T* __restrict__ mask) {
   const int Ho = H >> 1, Wo = W >> 1, C8 = C >> 3;
   const long total = static_cast<long>(B) * H * W * C8;
   for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
@@ -128,6 +131,11 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_kernel(const T* __restrict__
       for (int k = 0; k < 8; ++k) {
         const uint32_t p = ((k < 4 ? pp.x : pp.y) >> (8 * (k & 3))) & 0xffu;
         o.v[k] = p == me ? g.v[k] : 0.f;
+      }
+      if (mask) {
+        const V8 xm = load8<T>(mask + i * 8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o.v[k] = xm.v[k] > 0.f ? o.v[k] : 0.f;
       }
     } else {
 #pragma unroll
@@ -335,15 +343,16 @@ void maxpool2_fwd(const void* x, void* y, uint8_t* pos, int dt, int B, int H, in
                        static_cast<float*>(y), pos, B, H, W, C);
 }
 
-void maxpool2_bwd(const void* dy, const uint8_t* pos, void* dx, int dt, int B, int H, int W, int C, hipStream_t s) {
+void maxpool2_bwd(const void* dy, const uint8_t* pos, void* dx, int dt, int B, int H, int W, int C, hipStream_t s,
+                  const void* mask) {
   const long n = static_cast<long>(B) * H * W * (C / 8);
   if (n == 0) return;
   if (dt == DT_BF16)
     hipLaunchKernelGGL(maxpool2_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const bf16_t*>(dy),
-                       pos, static_cast<bf16_t*>(dx), B, H, W, C);
+                       pos, static_cast<bf16_t*>(dx), B, H, W, C, static_cast<const bf16_t*>(mask));
   else
     hipLaunchKernelGGL(maxpool2_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const float*>(dy),
-                       pos, static_cast<float*>(dx), B, H, W, C);
+                       pos, static_cast<float*>(dx), B, H, W, C, static_cast<const float*>(mask));
 }
 
 void segment_sum(const void* x, int dt, const int* cu, float* out, int S, int C, hipStream_t s) {

@@ -69,9 +69,11 @@ __global__ __launch_bounds__(256) void upsample2x_fwd_kernel(const T* __restrict
 }
 
 // dy [B][2H][2W][C] -> dx [B][H][W][C]
+// mask (optional): the upsample's input x when it is a ReLU output - dx is also multiplied by [x > 0] (the
+// producer's ReLU backward folded in, ops/native.py _premasked); the bf16 vector path below takes none
 template <typename T>
 __global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx, int B, int H,
-                                                             int W, int C) {
+                                                             int W, int C, const T* __restrict__ mask) {
   const int C4 = C / 4;
   const long total = static_cast<long>(B) * H * W * C4;
   for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
@@ -98,7 +100,10 @@ __global__ __launch_bounds__(256) void upsample2x_bwd_kernel(const T* __restrict
     }
     const long d = ((static_cast<long>(b) * H + ky) * W + kx) * C + c4 * 4;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) Cvt<T>::store(dx, d + k, acc[k]);
+    for (int k = 0; k < 4; ++k) {
+      const float v = mask && !(Cvt<T>::load(mask, d + k) > 0.f) ? 0.f : acc[k];
+      Cvt<T>::store(dx, d + k, v);
+    }
   }
 }
 
@@ -954,9 +959,9 @@ void upsample2x_fwd(const void* x, void* y, int dt, int B, int H, int W, int C, 
                        static_cast<float*>(y), B, H, W, C);
 }
 
-void upsample2x_bwd(const void* dy, void* dx, int dt, int B, int H, int W, int C, hipStream_t s) {
+void upsample2x_bwd(const void* dy, void* dx, int dt, int B, int H, int W, int C, hipStream_t s, const void* mask) {
   const long n8 = static_cast<long>(B) * H * W * (C / 8);
-  if (dt == DT_BF16 && C % 8 == 0 && n8 < (1L << 31) - (1L << 24)) {
+  if (dt == DT_BF16 && C % 8 == 0 && n8 < (1L << 31) - (1L << 24) && mask == nullptr) {
     hipLaunchKernelGGL(upsample2x_bwd_v8_kernel, dim3(grid_for(n8)), dim3(256), 0, s, static_cast<const bf16_t*>(dy),
                        static_cast<bf16_t*>(dx), B, H, W, C);
     return;
@@ -964,10 +969,11 @@ void upsample2x_bwd(const void* dy, void* dx, int dt, int B, int H, int W, int C
   const long n = static_cast<long>(B) * H * W * (C / 4);
   if (dt == DT_BF16)
     hipLaunchKernelGGL(upsample2x_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s,
-                       static_cast<const bf16_t*>(dy), static_cast<bf16_t*>(dx), B, H, W, C);
+                       static_cast<const bf16_t*>(dy), static_cast<bf16_t*>(dx), B, H, W, C,
+                       static_cast<const bf16_t*>(mask));
   else
     hipLaunchKernelGGL(upsample2x_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const float*>(dy),
-                       static_cast<float*>(dx), B, H, W, C);
+                       static_cast<float*>(dx), B, H, W, C, static_cast<const float*>(mask));
 }
 
 bool spatial_pool_supported(int H, int W) { return H % 2 == 0 && W % 2 == 0 && 2 * W <= kPoolTile && W >= 2; }

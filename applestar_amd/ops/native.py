@@ -283,11 +283,18 @@ def entity_embed(entity_info, flat_index, w, b):
 class _Upsample2x(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_nhwc):
+        # an fp32 ReLU output as input: the backward applies its mask (the producer conv skips its threshold)
+        relu_in = x_nhwc.dtype == torch.float32 and x_nhwc.is_contiguous() and _relu_src(x_nhwc)
+        ctx.save_for_backward(x_nhwc if relu_in else None)
         return _C.upsample2x_fwd(x_nhwc)
 
     @staticmethod
     def backward(ctx, dy):
-        return _C.upsample2x_bwd(dy.contiguous())
+        x, = ctx.saved_tensors
+        dx = _C.upsample2x_bwd(dy.contiguous(), x)
+        if x is not None:
+            _MASKED_DX[x.data_ptr()] = (dx, dx._version)
+        return dx
 
 
 def upsample2x(x):
@@ -528,14 +535,19 @@ class _MaxPool2(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_nhwc):
         y, pos = _C.maxpool2_fwd(x_nhwc)
-        ctx.save_for_backward(pos)
+        # an fp32 ReLU output as input: the backward applies its mask (the producer conv skips its threshold)
+        relu_in = x_nhwc.dtype == torch.float32 and x_nhwc.is_contiguous() and _relu_src(x_nhwc)
+        ctx.save_for_backward(pos, x_nhwc if relu_in else None)
         ctx.hw = (x_nhwc.shape[1], x_nhwc.shape[2])
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        pos, = ctx.saved_tensors
-        return _C.maxpool2_bwd(dy.contiguous(), pos, *ctx.hw)
+        pos, x = ctx.saved_tensors
+        dx = _C.maxpool2_bwd(dy.contiguous(), pos, *ctx.hw, x)
+        if x is not None:
+            _MASKED_DX[x.data_ptr()] = (dx, dx._version)
+        return dx
 
 
 def maxpool2x2(x):
@@ -682,6 +694,8 @@ class _Conv3x3(torch.autograd.Function):
             wk = wk.contiguous()
         bias = _w32(b) if b is not None else None
         out = _conv3(x_nhwc, wk, bias, res_nhwc, _ACT[act])
+        if act == 'relu' and out.dtype == torch.float32:
+            _note_relu_out(out)
         ctx.save_for_backward(x_nhwc, w_lp, out)
         ctx.act, ctx.has_res = act, res_nhwc is not None
         ctx.b_dtype = b.dtype if b is not None else None
@@ -690,7 +704,10 @@ class _Conv3x3(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         x, w, out = ctx.saved_tensors
-        dpre = _act_grad(dout, out, ctx.act == 'relu')    # one pass: mask + cast + NHWC
+        if ctx.act == 'relu' and _premasked(out, dout):
+            dpre = dout.contiguous()                       # the consumer's backward applied the mask
+        else:
+            dpre = _act_grad(dout, out, ctx.act == 'relu')    # one pass: mask + cast + NHWC
         has_b = ctx.b_dtype is not None
         cout, cin = w.shape[0], w.shape[1]
         bf = _bf16_grads(w.dtype, ctx.b_dtype)

@@ -1208,6 +1208,38 @@ def test_fused_resblocks_f32_match_torch_fp64(gated, f32_mfma):
         assert e < 3e-5 * max(1.0, pr.grad.abs().max().item()), (n, e)
 
 
+@pytest.mark.parametrize('between', ['maxpool', 'upsample'])
+@pytest.mark.parametrize('extra_consumer', [False, True])
+def test_conv_relu_mask_handoff_f32(between, extra_consumer):
+    """fp32 conv(ReLU) -> maxpool / bilinear x2 -> conv: the pool / upsample backward applies the first conv's ReLU
+    mask and the conv backward skips its threshold pass (ops/native.py _premasked); with a second consumer of the
+    ReLU output the summed gradient takes the mask as usual.  Both vs float64."""
+    from applestar_amd import ops
+    torch.manual_seed(12)
+    cl = torch.channels_last
+    x = torch.randn(3, 16, 20, 24, device=DEV).contiguous(memory_format=cl).requires_grad_()
+    w1 = (torch.randn(32, 16, 3, 3, device=DEV) / 12).contiguous(memory_format=cl).requires_grad_()
+    b1 = (0.1 * torch.randn(32, device=DEV)).requires_grad_()
+    w2 = (torch.randn(32, 32, 3, 3, device=DEV) / 17).contiguous(memory_format=cl).requires_grad_()
+    ts = [_f64(t) for t in (x, w1, b1, w2)]
+
+    def net(x, w1, b1, w2, ref):
+        h = ops.conv2d(x, w1, b1, 1, 1, act='relu') if not ref else torch.relu(torch.nn.functional.conv2d(x, w1, b1, 1, 1))
+        if between == 'maxpool':
+            m = N.maxpool2x2(h) if not ref else torch.nn.functional.max_pool2d(h, 2, 2)
+        else:
+            m = N.upsample2x(h) if not ref else torch.nn.functional.interpolate(h, scale_factor=2.0, mode='bilinear',
+                                                                                align_corners=False)
+        y = ops.conv2d(m, w2, None, 1, 1) if not ref else torch.nn.functional.conv2d(m, w2, None, 1, 1)
+        out = (y * y).sum()
+        return out + (h * h).sum() if extra_consumer else out
+    net(x, w1, b1, w2, False).backward()
+    net(*ts, True).backward()
+    for name, a, r in zip(('dx', 'dw1', 'db1', 'dw2'), (x, w1, b1, w2), ts):
+        e = _err(a.grad.cpu(), r.grad)
+        assert e < 3e-5 * max(1.0, r.grad.abs().max().item()), (name, e)
+
+
 def test_gated_resblock_f32_gemm_gate_path(f32_mfma, monkeypatch):
     """At 12 x 38 x 40 pixels the fp32 GatedResBlock's four gate layers take the f32 GEMM (bias + ReLU forward,
     the ReLU masks and the skip gradient in the dX epilogues).  Against the same block with the gate layers on the
