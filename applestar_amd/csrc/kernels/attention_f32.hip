@@ -19,6 +19,7 @@
 // conflict-free (exhaustive check over the ds_read_b128 / b32 lane groups).  (A register prefetch of the next
 // key block measured slower in the learner step: 64 more live VGPRs for sequences of 1-8 blocks, r3i.)
 #include <cstdlib>
+#include <string>
 
 #include "../common.h"
 #include "../kernels.h"
@@ -137,6 +138,20 @@ __device__ __forceinline__ f4 row_dot_x6(const float* T, int n, const Split3 (&f
     const float4 a1 = *reinterpret_cast<const float4*>(row + 8 * c + 4);
     const float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     acc = mfma16_x6(split8(v), fs[c], acc);
+  }
+  return acc;
+}
+
+// row_dot_x6 with the register fragment split on the fly (fewer live VGPRs than a pre-split fragment)
+__device__ __forceinline__ f4 row_dot_x6_raw(const float* T, int n, const float (&f)[32], f4 acc) {
+  const int l = threadIdx.x & 63;
+  const float* row = T + swz(16 * n + (l & 15), 32 * (l >> 4));
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float4 a0 = *reinterpret_cast<const float4*>(row + 8 * c);
+    const float4 a1 = *reinterpret_cast<const float4*>(row + 8 * c + 4);
+    const float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    acc = mfma16_x6(split8(v), split8(*reinterpret_cast<const float(*)[8]>(&f[8 * c])), acc);
   }
   return acc;
 }
@@ -350,7 +365,7 @@ __global__ __launch_bounds__(256) void attn_f32_bwd_dq_kernel(const float* __res
 // dK, dV for 64 keys; loops row blocks: S = Q K^T and dP = dO V^T leave lane (lg, lr) holding key lr and
 // rows 16 n + 4 lg + i; dV^T += dO^T P, dK^T += Q^T dS take P / dS from registers
 template <bool SPLIT>
-__global__ __launch_bounds__(256) void attn_f32_bwd_dkdv_kernel(const float* __restrict__ qkv,
+__global__ __launch_bounds__(256, 2) void attn_f32_bwd_dkdv_kernel(const float* __restrict__ qkv,
                                                                  const float* __restrict__ dout,
                                                                  const float* __restrict__ lse2,
                                                                  const float* __restrict__ delta,
@@ -376,11 +391,6 @@ __global__ __launch_bounds__(256) void attn_f32_bwd_dkdv_kernel(const float* __r
   float kf[32], vf[32];
   load_row32(kf, seq + static_cast<long>(kr) * ROW + HD + h * D + 32 * lg, kval);
   load_row32(vf, seq + static_cast<long>(kr) * ROW + 2 * HD + h * D + 32 * lg, kval);
-  Split3 ks[4], vs[4];
-  if constexpr (SPLIT) {
-    split_frag(kf, ks);
-    split_frag(vf, vs);
-  }
   f4 dk[8], dv[8];   // dK^T / dV^T: [nd][i] = d(key)[16 nd + 4 lg + i]
 #pragma unroll
   for (int n = 0; n < 8; ++n) { dk[n] = f4{0.f, 0.f, 0.f, 0.f}; dv[n] = f4{0.f, 0.f, 0.f, 0.f}; }
@@ -402,8 +412,8 @@ __global__ __launch_bounds__(256) void attn_f32_bwd_dkdv_kernel(const float* __r
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int n = 2 * p2 + u;
-          f4 sc = row_dot_x6(Q_s, n, ks, f4{0.f, 0.f, 0.f, 0.f});
-          f4 dp = row_dot_x6(dO_s, n, vs, f4{0.f, 0.f, 0.f, 0.f});
+          f4 sc = row_dot_x6_raw(Q_s, n, kf, f4{0.f, 0.f, 0.f, 0.f});
+          f4 dp = row_dot_x6_raw(dO_s, n, vf, f4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int rl = 16 * n + 4 * lg + i;
@@ -465,23 +475,27 @@ void varlen_attn_bwd_f32(const float* qkv, const float* out, const float* dout, 
   const float scale_log2 = scale * 1.4426950408889634f;
   const int QB = (max_len + BR - 1) / BR;
   const dim3 grid(static_cast<unsigned>((static_cast<long>(QB) * S * H + 7) / 8 * 8));
-  // the split backward kernels hold 228 / 276 VGPRs (one workgroup per CU for dK/dV) and measured 17 % slower
-  // than the exact-f32 ones (r3z_attn_micro.txt): the backward stays on the exact-f32 MFMA unless asked for
-  static const bool bwd_split = [] {
+  // split backward (profiles/r3z_attn_bwd_variants.txt): exact 1933 us, dQ split 1809, both split 1636 with dK/dV
+  // held to two waves per SIMD (its K / V fragments split on the fly; at 276 VGPRs, one workgroup per CU, it was
+  // slower than exact).  APPLESTAR_F32_ATTN_BWD_SPLIT = both (default) | dq | none
+  static const int bwd_split = [] {
     const char* e = std::getenv("APPLESTAR_F32_ATTN_BWD_SPLIT");
-    return e && e[0] == '1';
+    const std::string v = e ? e : "both";
+    return v == "both" ? 3 : (v == "none" ? 0 : 1);
   }();
-  if (f32_mfma_mode() && bwd_split) {
+  const bool sq = f32_mfma_mode() && (bwd_split & 1), skv = f32_mfma_mode() && (bwd_split & 2);
+  if (sq)
     hipLaunchKernelGGL(attn_f32_bwd_dq_kernel<true>, grid, dim3(256), 0, s, qkv, out, dout, lse2, delta, cu, dqkv, H,
                        Ttot, scale_log2, scale, QB, S);
-    hipLaunchKernelGGL(attn_f32_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, qkv, dout, lse2, delta, cu, dqkv, H, Ttot,
-                       scale_log2, scale, QB, S);
-  } else {
+  else
     hipLaunchKernelGGL(attn_f32_bwd_dq_kernel<false>, grid, dim3(256), 0, s, qkv, out, dout, lse2, delta, cu, dqkv, H,
                        Ttot, scale_log2, scale, QB, S);
+  if (skv)
+    hipLaunchKernelGGL(attn_f32_bwd_dkdv_kernel<true>, grid, dim3(256), 0, s, qkv, dout, lse2, delta, cu, dqkv, H, Ttot,
+                       scale_log2, scale, QB, S);
+  else
     hipLaunchKernelGGL(attn_f32_bwd_dkdv_kernel<false>, grid, dim3(256), 0, s, qkv, dout, lse2, delta, cu, dqkv, H,
                        Ttot, scale_log2, scale, QB, S);
-  }
 }
 
 }  // namespace as
