@@ -1323,8 +1323,8 @@ at::Tensor vsp_fwd(const at::Tensor& sc, const at::Tensor& own, const at::Tensor
   check_cuda(w, "w");
   check_cuda(b, "b");
   const int64_t P = sc.size(0);
-  TORCH_CHECK(sc.scalar_type() == at::kBFloat16 && sc.dim() == 2 && sc.size(1) == as::vsp_in_channels() - 2,
-              "vsp: sc [P, 8] bf16");
+  TORCH_CHECK((sc.scalar_type() == at::kBFloat16 || sc.scalar_type() == at::kFloat) && sc.dim() == 2 &&
+              sc.size(1) == as::vsp_in_channels() - 2 && sc.is_contiguous(), "vsp: sc [P, 8] bf16 / fp32");
   TORCH_CHECK(own.element_size() == 1 && enemy.element_size() == 1 && own.numel() == P && enemy.numel() == P,
               "vsp: own / enemy [P] bool");
   TORCH_CHECK(w.scalar_type() == at::kFloat && w.size(0) == as::vsp_out_channels() && w.size(1) == as::vsp_in_channels()
@@ -1332,7 +1332,7 @@ at::Tensor vsp_fwd(const at::Tensor& sc, const at::Tensor& own, const at::Tensor
   c10::hip::HIPGuard g(sc.device().index());
   auto out = at::empty({P, as::vsp_out_channels()}, sc.options());
   as::vsp_fwd(sc.data_ptr(), own.data_ptr(), enemy.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(),
-              out.data_ptr(), P, stream());
+              out.data_ptr(), P, stream(), dt(sc));
   return out;
 }
 
@@ -1346,9 +1346,11 @@ std::vector<at::Tensor> vsp_bwd(const at::Tensor& dout, const at::Tensor& out, c
   check_cuda(enemy, "enemy");
   check_cuda(w, "w");
   const int64_t P = sc.size(0);
-  TORCH_CHECK(dout.scalar_type() == at::kBFloat16 && out.scalar_type() == at::kBFloat16 && dout.sizes() == out.sizes()
-              && out.size(0) == P && out.size(1) == as::vsp_out_channels(), "vsp_bwd: dout / out [P, 16] bf16");
-  TORCH_CHECK(sc.scalar_type() == at::kBFloat16 && sc.size(1) == as::vsp_in_channels() - 2, "vsp_bwd: sc [P, 8] bf16");
+  TORCH_CHECK(dout.scalar_type() == sc.scalar_type() && out.scalar_type() == sc.scalar_type() &&
+              dout.sizes() == out.sizes() && out.size(0) == P && out.size(1) == as::vsp_out_channels() &&
+              dout.is_contiguous() && out.is_contiguous(), "vsp_bwd: dout / out [P, 16] of sc's dtype");
+  TORCH_CHECK((sc.scalar_type() == at::kBFloat16 || sc.scalar_type() == at::kFloat) &&
+              sc.size(1) == as::vsp_in_channels() - 2 && sc.is_contiguous(), "vsp_bwd: sc [P, 8] bf16 / fp32");
   TORCH_CHECK(own.element_size() == 1 && enemy.element_size() == 1 && own.numel() == P && enemy.numel() == P,
               "vsp_bwd: own / enemy [P] bool");
   TORCH_CHECK(w.scalar_type() == at::kFloat && w.size(0) == as::vsp_out_channels() && w.size(1) == as::vsp_in_channels(),
@@ -1358,7 +1360,7 @@ std::vector<at::Tensor> vsp_bwd(const at::Tensor& dout, const at::Tensor& out, c
   auto dsc = at::empty_like(sc);
   auto part = at::empty({nblk, as::vsp_out_channels() * (as::vsp_in_channels() + 1)}, sc.options().dtype(at::kFloat));
   as::vsp_bwd(dout.data_ptr(), out.data_ptr(), sc.data_ptr(), own.data_ptr(), enemy.data_ptr(), w.data_ptr<float>(),
-              dsc.data_ptr(), part.data_ptr<float>(), P, nblk, stream());
+              dsc.data_ptr(), part.data_ptr<float>(), P, nblk, stream(), dt(sc));
   return {dsc, part.sum(0).view({as::vsp_out_channels(), as::vsp_in_channels() + 1})};
 }
 
@@ -1372,7 +1374,8 @@ std::vector<at::Tensor> vsp_pool_fwd(const at::Tensor& sc, const at::Tensor& own
   check_cuda(b, "b");
   const int64_t P = B * H * W;
   TORCH_CHECK(H % 2 == 0 && W % 2 == 0 && sc.dim() == 2 && sc.size(0) == P && sc.size(1) == as::vsp_in_channels() - 2 &&
-              sc.scalar_type() == at::kBFloat16, "vsp_pool: sc [B*H*W, 8] bf16, even H / W");
+              (sc.scalar_type() == at::kBFloat16 || sc.scalar_type() == at::kFloat) && sc.is_contiguous(),
+              "vsp_pool: sc [B*H*W, 8] bf16 / fp32, even H / W");
   TORCH_CHECK(own.element_size() == 1 && enemy.element_size() == 1 && own.numel() == P && enemy.numel() == P,
               "vsp_pool: own / enemy [B*H*W] bool");
   TORCH_CHECK(w.scalar_type() == at::kFloat && w.size(0) == as::vsp_out_channels() && w.size(1) == as::vsp_in_channels()
@@ -1383,7 +1386,7 @@ std::vector<at::Tensor> vsp_pool_fwd(const at::Tensor& sc, const at::Tensor& own
   auto pos = at::empty({Po, as::vsp_out_channels()}, sc.options().dtype(at::kByte));
   as::vsp_pool_fwd(sc.data_ptr(), own.data_ptr(), enemy.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(),
                    pooled.data_ptr(), pos.data_ptr<uint8_t>(), static_cast<int>(B), static_cast<int>(H),
-                   static_cast<int>(W), stream());
+                   static_cast<int>(W), stream(), dt(sc));
   return {pooled, pos};
 }
 
@@ -1397,8 +1400,8 @@ std::vector<at::Tensor> vsp_pool_bwd(const at::Tensor& dpooled, const at::Tensor
   check_cuda(sc, "sc");
   check_cuda(w, "w");
   const int64_t P = B * H * W, Po = B * (H / 2) * (W / 2);
-  TORCH_CHECK(dpooled.scalar_type() == at::kBFloat16 && pooled.scalar_type() == at::kBFloat16 &&
-              dpooled.sizes() == pooled.sizes() && pos.sizes() == pooled.sizes() && pooled.size(0) == Po &&
+  TORCH_CHECK(dpooled.scalar_type() == sc.scalar_type() && pooled.scalar_type() == sc.scalar_type() &&
+              dpooled.is_contiguous() && sc.is_contiguous() && dpooled.sizes() == pooled.sizes() && pos.sizes() == pooled.sizes() && pooled.size(0) == Po &&
               pooled.size(1) == as::vsp_out_channels(), "vsp_pool_bwd: dpooled / pooled / pos [Po, 16]");
   TORCH_CHECK(sc.size(0) == P && sc.size(1) == as::vsp_in_channels() - 2 && own.numel() == P && enemy.numel() == P &&
               own.element_size() == 1 && enemy.element_size() == 1 && own.is_contiguous() && enemy.is_contiguous(),
@@ -1411,7 +1414,7 @@ std::vector<at::Tensor> vsp_pool_bwd(const at::Tensor& dpooled, const at::Tensor
   auto part = at::empty({nblk, as::vsp_out_channels() * (as::vsp_in_channels() + 1)}, sc.options().dtype(at::kFloat));
   as::vsp_pool_bwd(dpooled.data_ptr(), pos.data_ptr<uint8_t>(), pooled.data_ptr(), sc.data_ptr(), own.data_ptr(),
                    enemy.data_ptr(), w.data_ptr<float>(), dsc.data_ptr(), part.data_ptr<float>(), static_cast<int>(B),
-                   static_cast<int>(H), static_cast<int>(W), nblk, stream());
+                   static_cast<int>(H), static_cast<int>(W), nblk, stream(), dt(sc));
   return {dsc, part.sum(0).view({as::vsp_out_channels(), as::vsp_in_channels() + 1})};
 }
 

@@ -51,17 +51,17 @@ void gated_residual_fwd(const void* y, const void* g, const float* sp, const voi
 int vsp_in_channels();
 int vsp_out_channels();
 void vsp_fwd(const void* sc, const void* own, const void* enemy, const float* w, const float* b, void* out, long P,
-             hipStream_t s);
+             hipStream_t s, int dt = DT_BF16);
 int vsp_bwd_blocks(long P);
 // pooled (even H, W): relu(projection) -> max_pool2x2; pooled [B*H/2*W/2, 16] bf16 + argmax bytes (maxpool2
 // format); backward from the pooled gradient: dSc [P, 8] (zero off the argmax pixels) and partial dW / db rows
 void vsp_pool_fwd(const void* sc, const void* own, const void* enemy, const float* w, const float* b, void* pooled,
-                  uint8_t* pos, int B, int H, int W, hipStream_t s);
+                  uint8_t* pos, int B, int H, int W, hipStream_t s, int dt = DT_BF16);
 void vsp_pool_bwd(const void* dpooled, const uint8_t* pos, const void* pooled, const void* sc, const void* own,
                   const void* enemy, const float* w, void* dsc, float* part, int B, int H, int W, int nblk,
-                  hipStream_t s);
+                  hipStream_t s, int dt = DT_BF16);
 void vsp_bwd(const void* dout, const void* out, const void* sc, const void* own, const void* enemy, const float* w,
-             void* dsc, float* part, long P, int nblk, hipStream_t s);
+             void* dsc, float* part, long P, int nblk, hipStream_t s, int dt = DT_BF16);
 // location-head input: relu(y0 + W_p relu(p)) per NHWC pixel and its one-pass backward (locin.hip)
 bool loc_in_supported(int C, int P);
 void loc_in_fwd(const void* y0, const void* p, const float* wp, void* out, long npix, int HW, hipStream_t s);

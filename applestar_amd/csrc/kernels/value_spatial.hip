@@ -41,9 +41,32 @@ __device__ __forceinline__ uint4 vs_pack8(const float* f) {
   return v;
 }
 
-__global__ __launch_bounds__(256) void vsp_fwd_kernel(const bf16_t* __restrict__ sc, const uint8_t* __restrict__ own,
+// 8 consecutive elements <-> fp32 registers for both I/O types (the fp32 learner step: fp32 maps end to end,
+// the same fp32 FMA math as the bf16 form)
+template <typename T> __device__ __forceinline__ void vs_load8(const T* p, float* f);
+template <> __device__ __forceinline__ void vs_load8<bf16_t>(const bf16_t* p, float* f) {
+  vs_unpack8(*reinterpret_cast<const uint4*>(p), f);
+}
+template <> __device__ __forceinline__ void vs_load8<float>(const float* p, float* f) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+template <typename T> __device__ __forceinline__ void vs_store8(T* p, const float* f);
+template <> __device__ __forceinline__ void vs_store8<bf16_t>(bf16_t* p, const float* f) {
+  *reinterpret_cast<uint4*>(p) = vs_pack8(f);
+}
+template <> __device__ __forceinline__ void vs_store8<float>(float* p, const float* f) {
+  reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+  reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+}
+// the value the materialised map of type T would hold
+template <typename T> __device__ __forceinline__ float vs_round(float v) { return v; }
+template <> __device__ __forceinline__ float vs_round<bf16_t>(float v) { return bf2f(f2bf(v)); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void vsp_fwd_kernel(const T* __restrict__ sc, const uint8_t* __restrict__ own,
                                                       const uint8_t* __restrict__ enemy, const float* __restrict__ w,
-                                                      const float* __restrict__ b, bf16_t* __restrict__ out, long P) {
+                                                      const float* __restrict__ b, T* __restrict__ out, long P) {
   const int h = threadIdx.x & 1;
   float wr[8][kVsIn], br[8];
 #pragma unroll
@@ -55,7 +78,7 @@ __global__ __launch_bounds__(256) void vsp_fwd_kernel(const bf16_t* __restrict__
   const long step = static_cast<long>(gridDim.x) * (blockDim.x >> 1);
   for (long pix = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) >> 1; pix < P; pix += step) {
     float s[kVsSc];
-    vs_unpack8(*reinterpret_cast<const uint4*>(sc + pix * kVsSc), s);
+    vs_load8<T>(sc + pix * kVsSc, s);
     const float fo = own[pix] ? 1.f : 0.f, fe = enemy[pix] ? 1.f : 0.f;
     float v[8];
 #pragma unroll
@@ -65,14 +88,15 @@ __global__ __launch_bounds__(256) void vsp_fwd_kernel(const bf16_t* __restrict__
       for (int k = 0; k < kVsSc; ++k) a = fmaf(wr[c][k], s[k], a);
       v[c] = fmaxf(a, 0.f);
     }
-    *reinterpret_cast<uint4*>(out + pix * kVsOut + 8 * h) = vs_pack8(v);
+    vs_store8<T>(out + pix * kVsOut + 8 * h, v);
   }
 }
 
-__global__ __launch_bounds__(256) void vsp_bwd_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ out,
-                                                      const bf16_t* __restrict__ sc, const uint8_t* __restrict__ own,
+template <typename T>
+__global__ __launch_bounds__(256) void vsp_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ out,
+                                                      const T* __restrict__ sc, const uint8_t* __restrict__ own,
                                                       const uint8_t* __restrict__ enemy, const float* __restrict__ w,
-                                                      bf16_t* __restrict__ dsc, float* __restrict__ part, long P) {
+                                                      T* __restrict__ dsc, float* __restrict__ part, long P) {
   __shared__ float red[4][2][kVsAcc];
   const int h = threadIdx.x & 1;
   float wr[8][kVsSc], acc[8][kVsIn + 1];
@@ -87,9 +111,9 @@ __global__ __launch_bounds__(256) void vsp_bwd_kernel(const bf16_t* __restrict__
   // both lanes of a pixel pair run the same trip count, so the pair shuffle always sees its partner
   for (long pix = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) >> 1; pix < P; pix += step) {
     float d[8], o[8], s[kVsSc];
-    vs_unpack8(*reinterpret_cast<const uint4*>(dout + pix * kVsOut + 8 * h), d);
-    vs_unpack8(*reinterpret_cast<const uint4*>(out + pix * kVsOut + 8 * h), o);
-    vs_unpack8(*reinterpret_cast<const uint4*>(sc + pix * kVsSc), s);
+    vs_load8<T>(dout + pix * kVsOut + 8 * h, d);
+    vs_load8<T>(out + pix * kVsOut + 8 * h, o);
+    vs_load8<T>(sc + pix * kVsSc, s);
     const float fo = own[pix] ? 1.f : 0.f, fe = enemy[pix] ? 1.f : 0.f;
     float ds[kVsSc];
 #pragma unroll
@@ -108,7 +132,7 @@ __global__ __launch_bounds__(256) void vsp_bwd_kernel(const bf16_t* __restrict__
     }
 #pragma unroll
     for (int k = 0; k < kVsSc; ++k) ds[k] += __shfl_xor(ds[k], 1, 64);
-    if (h == 0) *reinterpret_cast<uint4*>(dsc + pix * kVsSc) = vs_pack8(ds);
+    if (h == 0) vs_store8<T>(dsc + pix * kVsSc, ds);
   }
   // lanes of equal parity hold partial sums of the same 88 entries: fold the 32 of each wave
 #pragma unroll
@@ -139,9 +163,10 @@ __global__ __launch_bounds__(256) void vsp_bwd_kernel(const bf16_t* __restrict__
 // per POOLED pixel evaluates its 2x2 window and writes the pooled map + maxpool2's argmax bytes; the 303 MB
 // full-resolution map is never written or re-read.  Backward: the gradient reaches only the argmax pixel of
 // each channel, and only where the pooled (ReLU) value is positive.
-__global__ __launch_bounds__(256) void vsp_pool_fwd_kernel(const bf16_t* __restrict__ sc, const uint8_t* __restrict__ own,
+template <typename T>
+__global__ __launch_bounds__(256) void vsp_pool_fwd_kernel(const T* __restrict__ sc, const uint8_t* __restrict__ own,
                                                            const uint8_t* __restrict__ enemy, const float* __restrict__ w,
-                                                           const float* __restrict__ b, bf16_t* __restrict__ pooled,
+                                                           const float* __restrict__ b, T* __restrict__ pooled,
                                                            uint8_t* __restrict__ pos, int B, int H, int W) {
   const int h = threadIdx.x & 1;
   float wr[8][kVsIn], br[8];
@@ -166,14 +191,14 @@ __global__ __launch_bounds__(256) void vsp_pool_fwd_kernel(const bf16_t* __restr
 #pragma unroll
     for (int t4 = 0; t4 < 4; ++t4) {
       float s[kVsSc];
-      vs_unpack8(*reinterpret_cast<const uint4*>(sc + pix[t4] * kVsSc), s);
+      vs_load8<T>(sc + pix[t4] * kVsSc, s);
       const float fo = own[pix[t4]] ? 1.f : 0.f, fe = enemy[pix[t4]] ? 1.f : 0.f;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
         float a = fmaf(wr[c][kVsSc], fo, fmaf(wr[c][kVsSc + 1], fe, br[c]));
 #pragma unroll
         for (int k = 0; k < kVsSc; ++k) a = fmaf(wr[c][k], s[k], a);
-        const float v = bf2f(f2bf(fmaxf(a, 0.f)));     // the value the unfused bf16 map would hold
+        const float v = vs_round<T>(fmaxf(a, 0.f));     // the value the unfused map would hold
         if (t4 == 0) {
           m[c] = v;
         } else if (v > m[c]) {
@@ -183,17 +208,18 @@ __global__ __launch_bounds__(256) void vsp_pool_fwd_kernel(const bf16_t* __restr
         }
       }
     }
-    *reinterpret_cast<uint4*>(pooled + q * kVsOut + 8 * h) = vs_pack8(m);
+    vs_store8<T>(pooled + q * kVsOut + 8 * h, m);
     *reinterpret_cast<uint2*>(pos + q * kVsOut + 8 * h) = make_uint2(lo, hi);
   }
 }
 
-__global__ __launch_bounds__(256) void vsp_pool_bwd_kernel(const bf16_t* __restrict__ dpooled,
+template <typename T>
+__global__ __launch_bounds__(256) void vsp_pool_bwd_kernel(const T* __restrict__ dpooled,
                                                            const uint8_t* __restrict__ pos,
-                                                           const bf16_t* __restrict__ pooled,
-                                                           const bf16_t* __restrict__ sc, const uint8_t* __restrict__ own,
+                                                           const T* __restrict__ pooled,
+                                                           const T* __restrict__ sc, const uint8_t* __restrict__ own,
                                                            const uint8_t* __restrict__ enemy, const float* __restrict__ w,
-                                                           bf16_t* __restrict__ dsc, float* __restrict__ part, int B,
+                                                           T* __restrict__ dsc, float* __restrict__ part, int B,
                                                            int H, int W) {
   __shared__ float red[4][2][kVsAcc];
   const int h = threadIdx.x & 1;
@@ -215,8 +241,8 @@ __global__ __launch_bounds__(256) void vsp_pool_bwd_kernel(const bf16_t* __restr
     const long bb = t / Ho;
     const long p00 = (bb * H + 2 * oy) * W + 2 * ox;
     float d[8], y[8];
-    vs_unpack8(*reinterpret_cast<const uint4*>(dpooled + q * kVsOut + 8 * h), d);
-    vs_unpack8(*reinterpret_cast<const uint4*>(pooled + q * kVsOut + 8 * h), y);
+    vs_load8<T>(dpooled + q * kVsOut + 8 * h, d);
+    vs_load8<T>(pooled + q * kVsOut + 8 * h, y);
     const uint2 pp = *reinterpret_cast<const uint2*>(pos + q * kVsOut + 8 * h);
 #pragma unroll 1
     for (int t4 = 0; t4 < 4; ++t4) {
@@ -231,7 +257,7 @@ __global__ __launch_bounds__(256) void vsp_pool_bwd_kernel(const bf16_t* __restr
       for (int k = 0; k < kVsSc; ++k) ds[k] = 0.f;
       float s[kVsSc];
       const long px = p00 + (t4 >> 1) * W + (t4 & 1);
-      vs_unpack8(*reinterpret_cast<const uint4*>(sc + px * kVsSc), s);
+      vs_load8<T>(sc + px * kVsSc, s);
       const float fo = own[px] ? 1.f : 0.f, fe = enemy[px] ? 1.f : 0.f;
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -246,7 +272,7 @@ __global__ __launch_bounds__(256) void vsp_pool_bwd_kernel(const bf16_t* __restr
       }
 #pragma unroll
       for (int k = 0; k < kVsSc; ++k) ds[k] += __shfl_xor(ds[k], 1, 64);
-      if (h == 0) *reinterpret_cast<uint4*>(dsc + px * kVsSc) = vs_pack8(ds);
+      if (h == 0) vs_store8<T>(dsc + px * kVsSc, ds);
     }
   }
 #pragma unroll
@@ -277,14 +303,17 @@ __global__ __launch_bounds__(256) void vsp_pool_bwd_kernel(const bf16_t* __restr
 int vsp_in_channels() { return kVsIn; }
 int vsp_out_channels() { return kVsOut; }
 
+#define AS_VSP_T(dt, ...) \
+  if (dt == DT_BF16) { using T = bf16_t; __VA_ARGS__; } else { using T = float; __VA_ARGS__; }
+
 void vsp_fwd(const void* sc, const void* own, const void* enemy, const float* w, const float* b, void* out, long P,
-             hipStream_t s) {
+             hipStream_t s, int dt) {
   long blocks = (P * 2 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(vsp_fwd_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
-                     static_cast<const bf16_t*>(sc), static_cast<const uint8_t*>(own),
-                     static_cast<const uint8_t*>(enemy), w, b, static_cast<bf16_t*>(out), P);
+  AS_VSP_T(dt, hipLaunchKernelGGL(vsp_fwd_kernel<T>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
+                                  static_cast<const T*>(sc), static_cast<const uint8_t*>(own),
+                                  static_cast<const uint8_t*>(enemy), w, b, static_cast<T*>(out), P))
 }
 
 int vsp_bwd_blocks(long P) {
@@ -294,31 +323,33 @@ int vsp_bwd_blocks(long P) {
 }
 
 void vsp_pool_fwd(const void* sc, const void* own, const void* enemy, const float* w, const float* b, void* pooled,
-                  uint8_t* pos, int B, int H, int W, hipStream_t s) {
+                  uint8_t* pos, int B, int H, int W, hipStream_t s, int dt) {
   const long Po = static_cast<long>(B) * (H / 2) * (W / 2);
   long blocks = (Po * 2 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(vsp_pool_fwd_kernel, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
-                     static_cast<const bf16_t*>(sc), static_cast<const uint8_t*>(own),
-                     static_cast<const uint8_t*>(enemy), w, b, static_cast<bf16_t*>(pooled), pos, B, H, W);
+  AS_VSP_T(dt, hipLaunchKernelGGL(vsp_pool_fwd_kernel<T>, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, s,
+                                  static_cast<const T*>(sc), static_cast<const uint8_t*>(own),
+                                  static_cast<const uint8_t*>(enemy), w, b, static_cast<T*>(pooled), pos, B, H, W))
 }
 
 void vsp_pool_bwd(const void* dpooled, const uint8_t* pos, const void* pooled, const void* sc, const void* own,
                   const void* enemy, const float* w, void* dsc, float* part, int B, int H, int W, int nblk,
-                  hipStream_t s) {
-  hipLaunchKernelGGL(vsp_pool_bwd_kernel, dim3(nblk), dim3(256), 0, s, static_cast<const bf16_t*>(dpooled), pos,
-                     static_cast<const bf16_t*>(pooled), static_cast<const bf16_t*>(sc),
-                     static_cast<const uint8_t*>(own), static_cast<const uint8_t*>(enemy), w,
-                     static_cast<bf16_t*>(dsc), part, B, H, W);
+                  hipStream_t s, int dt) {
+  AS_VSP_T(dt, hipLaunchKernelGGL(vsp_pool_bwd_kernel<T>, dim3(nblk), dim3(256), 0, s, static_cast<const T*>(dpooled),
+                                  pos, static_cast<const T*>(pooled), static_cast<const T*>(sc),
+                                  static_cast<const uint8_t*>(own), static_cast<const uint8_t*>(enemy), w,
+                                  static_cast<T*>(dsc), part, B, H, W))
 }
 
 void vsp_bwd(const void* dout, const void* out, const void* sc, const void* own, const void* enemy, const float* w,
-             void* dsc, float* part, long P, int nblk, hipStream_t s) {
-  hipLaunchKernelGGL(vsp_bwd_kernel, dim3(nblk), dim3(256), 0, s, static_cast<const bf16_t*>(dout),
-                     static_cast<const bf16_t*>(out), static_cast<const bf16_t*>(sc),
-                     static_cast<const uint8_t*>(own), static_cast<const uint8_t*>(enemy), w,
-                     static_cast<bf16_t*>(dsc), part, P);
+             void* dsc, float* part, long P, int nblk, hipStream_t s, int dt) {
+  AS_VSP_T(dt, hipLaunchKernelGGL(vsp_bwd_kernel<T>, dim3(nblk), dim3(256), 0, s, static_cast<const T*>(dout),
+                                  static_cast<const T*>(out), static_cast<const T*>(sc),
+                                  static_cast<const uint8_t*>(own), static_cast<const uint8_t*>(enemy), w,
+                                  static_cast<T*>(dsc), part, P))
 }
+
+#undef AS_VSP_T
 
 }  // namespace as

@@ -1090,7 +1090,7 @@ class _ValueSpatialProj(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         sc2d, own, enemy, wf, out = ctx.saved_tensors
-        dsc, dwb = _C.vsp_bwd(dout.to(torch.bfloat16).contiguous(), out, sc2d, own, enemy, wf)
+        dsc, dwb = _C.vsp_bwd(dout.to(sc2d.dtype).contiguous(), out, sc2d, own, enemy, wf)
         w_dtype, b_dtype = ctx.dtypes
         return dsc, None, None, dwb[:, :-1].to(w_dtype), dwb[:, -1].to(b_dtype)
 
@@ -1111,7 +1111,7 @@ class _ValueSpatialProjPool(torch.autograd.Function):
     def backward(ctx, dpooled):
         sc2d, own, enemy, wf, pooled, pos = ctx.saved_tensors
         w_dtype, b_dtype, B, H, W = ctx.meta
-        dsc, dwb = _C.vsp_pool_bwd(dpooled.to(torch.bfloat16).contiguous(), pos, pooled, sc2d, own, enemy, wf, B, H, W)
+        dsc, dwb = _C.vsp_pool_bwd(dpooled.to(sc2d.dtype).contiguous(), pos, pooled, sc2d, own, enemy, wf, B, H, W)
         return dsc, None, None, dwb[:, :-1].to(w_dtype), dwb[:, -1].to(b_dtype), None, None, None
 
 
@@ -1120,15 +1120,14 @@ def value_spatial_proj_pool(sc, own, enemy, w, b):
     None when it does not apply."""
     if not (VSP_FUSED and VSP_POOL_FUSED):
         return None
-    if not _lowp(sc):      # bf16 kernel: an fp32 step takes the fp32 conv path, never a rounded copy
-        return None
     B, C, H, W = sc.shape
     cout, cin = w.shape[0], w.shape[1]
     if H % 2 or W % 2 or cout != _C.vsp_out_channels() or cin != _C.vsp_in_channels() or C != cin - 2 or b is None \
             or own.dtype != torch.bool or enemy.dtype != torch.bool or own.numel() != B * H * W \
             or enemy.numel() != B * H * W:
         return None
-    sc2d = nhwc(sc.to(torch.bfloat16)).view(-1, C)
+    # bf16 maps under autocast; the fp32 step keeps fp32 maps (the kernel's math is fp32 FMA either way)
+    sc2d = nhwc(sc.to(torch.bfloat16) if _lowp(sc) else sc.float()).view(-1, C)
     with torch.autocast('cuda', enabled=False):
         y = _ValueSpatialProjPool.apply(sc2d, own.reshape(-1).view(torch.uint8), enemy.reshape(-1).view(torch.uint8),
                                         w.view(cout, cin), b, B, H, W)
@@ -1141,15 +1140,13 @@ def value_spatial_proj(sc, own, enemy, w, b):
     None when the shapes are not the kernel's."""
     if not VSP_FUSED:
         return None
-    if not _lowp(sc):      # bf16 kernel: an fp32 step takes the fp32 conv path, never a rounded copy
-        return None
     B, C, H, W = sc.shape
     cout, cin = w.shape[0], w.shape[1]
     if cout != _C.vsp_out_channels() or cin != _C.vsp_in_channels() or C != cin - 2 or b is None \
             or own.dtype != torch.bool or enemy.dtype != torch.bool or own.numel() != B * H * W \
             or enemy.numel() != B * H * W:
         return None
-    sc2d = nhwc(sc.to(torch.bfloat16)).view(-1, C)
+    sc2d = nhwc(sc.to(torch.bfloat16) if _lowp(sc) else sc.float()).view(-1, C)
     with torch.autocast('cuda', enabled=False):
         y = _ValueSpatialProj.apply(sc2d, own.reshape(-1).view(torch.uint8), enemy.reshape(-1).view(torch.uint8),
                                     w.view(cout, cin), b)

@@ -989,6 +989,35 @@ def test_value_spatial_proj_matches_cat_path(B, H, W):
     assert rel(b.grad, br.grad) < 2e-2
 
 
+@pytest.mark.parametrize('pooled', [True, False])
+def test_value_spatial_proj_fp32_matches_fp64(pooled):
+    """fp32 step: the value-encoder projection (pooled and plain) keeps fp32 maps (no bf16 copy) - forward and the
+    scatter-map / weight / bias gradients vs float64 torch (cat + 1x1 conv + ReLU (+ max_pool2x2))."""
+    import torch.nn.functional as F
+    torch.manual_seed(43)
+    B, H, W = 3, 38, 40
+    sc0 = torch.zeros(B * H * W, 8, device=DEV)
+    hot = torch.rand(B * H * W, device=DEV) < 0.2
+    sc0[hot] = torch.randn(int(hot.sum()), 8, device=DEV)
+    own = torch.rand(B, 1, H, W, device=DEV) < 0.1
+    enemy = torch.rand(B, 1, H, W, device=DEV) < 0.1
+    sc = sc0.view(B, H, W, 8).permute(0, 3, 1, 2).requires_grad_()
+    w = (0.3 * torch.randn(16, 10, 1, 1, device=DEV)).requires_grad_()
+    b = (0.1 * torch.randn(16, device=DEV)).requires_grad_()
+    y = N.value_spatial_proj_pool(sc, own, enemy, w, b) if pooled else N.value_spatial_proj(sc, own, enemy, w, b)
+    assert y is not None and y.dtype == torch.float32
+    g = torch.randn(y.shape, dtype=torch.float64)
+    y.backward(g.float().to(DEV).contiguous(memory_format=torch.channels_last))
+    sr, wr, br = (_f64(t) for t in (sc, w, b))
+    z = torch.relu(F.conv2d(torch.cat([sr, own.double().cpu(), enemy.double().cpu()], 1), wr, br))
+    if pooled:
+        z = F.max_pool2d(z, 2, 2)
+    z.backward(g)
+    assert _err(y.cpu(), z) < 1e-5 * max(1.0, z.abs().max().item())
+    for name, a, r in (('dsc', sc.grad, sr.grad), ('dw', w.grad, wr.grad), ('db', b.grad, br.grad)):
+        assert _err(a.cpu(), r) < 2e-5 * max(1.0, r.abs().max().item()), name
+
+
 @pytest.mark.parametrize('R,K,N,relu', [(390, 48640, 256, True), (5000, 256, 1024, False)])
 def test_native_linear_reformulated_gemms(R, K, N, relu):
     """The library-GEMM reformulations in _Linear: a few rows over a huge K run as a 32-chunk split-K batched

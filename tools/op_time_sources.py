@@ -56,9 +56,12 @@ class Timer(TorchDispatchMode):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--out', default='gpurun_out/op_time_sources.txt')
+    ap.add_argument('--precision', choices=['fp32', 'bf16'], default='bf16')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
-    tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}, device=dev)
+    amp = 'bfloat16' if args.precision == 'bf16' else None
+    tr = RLTrainer({'learner': {'use_value_feature': True, 'amp_dtype': amp},
+                    'model': {'enable_baselines': ['winloss']}}, device=dev)
     h = rl_batch(6, 64, seed=0)
     b = to_device(h, dev)
     b['entity_total'] = entity_total_hint(h)
@@ -67,7 +70,7 @@ def main():
     torch.cuda.synchronize()
     mode = Timer()
     with mode:
-        with _amp(dev, 'bfloat16'):
+        with _amp(dev, amp):
             out = tr.model.rl_learner_forward(**b)
         info = tr.loss.compute_loss(out)
         loss = info['total_loss']
