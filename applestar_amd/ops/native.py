@@ -730,14 +730,15 @@ def _conv_w(w):
 def _conv_wt(w):
     """flipped, transposed weight [Cin,3,3,Cout] for the input gradient (bf16: a derived form rebuilt once per
     optimizer step for parameters; fp32: built per call, a few hundred KB)."""
-    if w.dtype == torch.float32:
-        return w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()
-    if w.dtype != torch.bfloat16:
+    if w.dtype not in (torch.float32, torch.bfloat16):
         raise TypeError(f'native conv3x3 backward needs bf16 or fp32 weights, got {w.dtype}')
 
     def make():
         s0, s1, s2, s3 = w.stride()
-        return _C.conv_wt(w.detach()), [w.shape[1], 3, 3, w.shape[0], s1, -s2, -s3, s0, 2 * s2 + 2 * s3]
+        spec = [w.shape[1], 3, 3, w.shape[0], s1, -s2, -s3, s0, 2 * s2 + 2 * s3]
+        if w.dtype == torch.float32:
+            return w.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous(), spec
+        return _C.conv_wt(w.detach()), spec
     return _derived(w, 'convwt', make)
 
 
@@ -1502,6 +1503,14 @@ def linear(x, w, b=None, act=None, grad_link=None):
             x2 = x.reshape(R, K).contiguous()
         y = _Linear.apply(x2, w, b, act == 'relu', link)
         return y.view(*x.shape[:-1], N)
+    if not lowp and x.is_cuda and K % 4 and R < _SMALL_LINEAR_ROWS and act in (None, 'relu') and \
+            x.dtype == torch.float32 and w.dtype == torch.float32:
+        # fp32, a few rows, K not a multiple of 4 (the scalar encoder's 167- / 269-wide inputs): the library's
+        # weight-gradient GEMM on the odd K ran 0.33 ms for a 390 x 167 x 128 product; zero-padded to K % 4 == 0
+        # (two copies of a few hundred KB) it takes the aligned kernels
+        pad = 4 - K % 4
+        y = torch.nn.functional.linear(torch.nn.functional.pad(x, (0, pad)), torch.nn.functional.pad(w, (0, pad)), b)
+        return torch.relu(y) if act == 'relu' else y
     if not lowp or R < _WGRAD_MIN_ROWS or N % 8 or K % 8 or R * max(N, K) * 2 >= 0x7ffffff0 or \
             act not in (None, 'relu'):
         y = torch.nn.functional.linear(x, w, b)

@@ -84,6 +84,14 @@ class RLTrainer:
         else:
             self.reducer = GradientReducer(self.params, bucket_mb=lc.bucket_mb, comm_dtype=comm)
             self.opt_params = self.params
+        # fp32 step: the weights' derived forms (transposed GEMM weights, flipped conv weights) rebuilt once per
+        # optimizer step in a few multi-tensor launches instead of one transpose / flip copy per layer and call
+        self.derived = None
+        if self.master is None and self.device.type == 'cuda' and not lc.get('graph_step', False):
+            from ..ops.native import DerivedWeights
+            self.derived = DerivedWeights()
+            for p in self.params:
+                p._derived_forms = self.derived
         self.grad_clip = build_grad_clip(lc.grad_clip)
         self.reset_optimizer()
         self.loss = ReinforcementLoss(lc, lc.player_id)
@@ -162,6 +170,8 @@ class RLTrainer:
             self.optimizer.step()
         if self.master is not None:
             self.master.after_step()
+        elif self.derived is not None:
+            self.derived.refresh()
         return norm
 
     def _lstm_gate(self):

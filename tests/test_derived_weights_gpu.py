@@ -85,3 +85,30 @@ def test_cached_forms_match_per_call_forms_over_steps():
             moved += int(fk in before and not torch.equal(before[fk], out))
     assert len(reg.forms) > 50 and len(b.master.derived.forms) == 0
     assert moved > 50          # the refreshed forms did change between steps
+
+
+def test_fp32_trainer_cached_forms_match_per_call_forms():
+    """The fp32 learner (no master weights) caches the same derived forms (transposed GEMM weights, flipped conv
+    weights), rebuilt after every optimizer step: each cached form equals a fresh rebuild from the current fp32
+    parameter, and loss / gradient norm equal those of a learner that rebuilds every form per call."""
+    cfg = {'learner': dict(CFG['learner'], learning_rate=1e-2, amp_dtype=None), 'model': CFG['model']}
+    torch.manual_seed(0)
+    a = RLTrainer(cfg, device='cuda')
+    torch.manual_seed(0)
+    b = RLTrainer(cfg, device='cuda')
+    assert a.master is None and a.derived is not None
+    b.derived.enabled = False
+    batches = [to_device(rl_batch(2, 4, max_entities=64, seed=s), 'cuda') for s in (1, 2, 3)]
+    reg = a.derived
+    for i, batch in enumerate(batches):
+        ia, ib = a.step(dict(batch)), b.step(dict(batch))
+        torch.cuda.synchronize()
+        la, lb = float(ia['total_loss']), float(ib['total_loss'])
+        assert abs(la - lb) <= 1e-4 * max(1.0, abs(lb)), (i, la, lb)
+        for fk, (p, out, spec, epoch, version) in reg.forms.items():
+            if fk[1] == 'convwt':
+                ref = p.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous()
+            else:
+                ref = p.detach().reshape(p.shape[0], -1).t().contiguous()
+            assert torch.equal(out, ref), (i, fk[1], tuple(p.shape))
+    assert len(reg.forms) > 20 and len(b.derived.forms) == 0
