@@ -1375,10 +1375,16 @@ _WGRAD_MIN_ROWS = 256     # tools/ab_bench.py --variant wgrad_small: -0.7 ms/ste
 
 
 def _gemm_f32_ok(M, N, K):
-    """The f32-MFMA GEMM takes this [M, K] x [N, K]^T product: K % 4, 32-bit buffer offsets, and enough
-    128-row x 64-column tiles (>= 128) to fill the chip; smaller products stay on the library GEMM."""
+    """The f32-MFMA GEMM takes this [M, K] x [N, K]^T product: K % 4, 32-bit buffer offsets, and either enough
+    128-row x 64-column tiles (>= 128) to fill the chip or a short reduction: a few-hundred-row product with
+    K <= 384 runs 5-16 us against the library's ~19 us floor; with K >= 1024 its few tiles each walk the whole K
+    (34 us) and the library stays (tools/bench_small_f32.py, profiles/r3z3_small_f32.jsonl)."""
     return K % 4 == 0 and M * K * 4 < 0x7ffffff0 and N * K * 4 < 0x7ffffff0 and \
-        (M + 127) // 128 * ((N + 63) // 64) >= 128
+        ((M + 127) // 128 * ((N + 63) // 64) >= 128 or K <= F32_SMALL_K)
+
+
+F32_SMALL_K = 0          # tools/ab_bench.py --variant f32_small_gemm: 384 measured +0.38 ms/step (r3z4), off
+F32_KPAD = False         # tools/ab_bench.py --variant f32_kpad: neutral (64.06 vs 64.14 ms, r3z4), off
 GEMM_REFORM = os.environ.get('APPLESTAR_GEMM_REFORM', '1') == '1'
 
 
@@ -1503,7 +1509,7 @@ def linear(x, w, b=None, act=None, grad_link=None):
             x2 = x.reshape(R, K).contiguous()
         y = _Linear.apply(x2, w, b, act == 'relu', link)
         return y.view(*x.shape[:-1], N)
-    if not lowp and x.is_cuda and K % 4 and R < _SMALL_LINEAR_ROWS and act in (None, 'relu') and \
+    if F32_KPAD and not lowp and x.is_cuda and K % 4 and R < _SMALL_LINEAR_ROWS and act in (None, 'relu') and \
             x.dtype == torch.float32 and w.dtype == torch.float32:
         # fp32, a few rows, K not a multiple of 4 (the scalar encoder's 167- / 269-wide inputs): the library's
         # weight-gradient GEMM on the odd K ran 0.33 ms for a 390 x 167 x 128 product; zero-padded to K % 4 == 0

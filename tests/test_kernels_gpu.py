@@ -1159,7 +1159,8 @@ def test_conv3x3_f32_matches_fp64(cin, cout, H, W, act, res, f32_mfma):
         assert e < 2e-5 * max(1.0, ref.abs().max().item()), (name, e, ref.abs().max().item())
 
 
-@pytest.mark.parametrize('R,N,K', [(4096, 768, 256), (1000, 256, 1024), (390, 128, 48640 // 64), (100003, 32, 16)])
+@pytest.mark.parametrize('R,N,K', [(4096, 768, 256), (1000, 256, 1024), (390, 128, 48640 // 64), (100003, 32, 16),
+                                   (390, 256, 256), (384, 1024, 384), (7800, 64, 128)])
 def test_linear_f32_grads_match_fp64(R, N, K, f32_mfma):
     """The fp32 step's linear (gemm_f32.hip forward / dX, wgrad_f32.hip dW / db) vs float64."""
     from applestar_amd.ops import native as NN
@@ -1179,14 +1180,15 @@ def test_linear_f32_grads_match_fp64(R, N, K, f32_mfma):
         assert e < 2e-5 * max(1.0, ref.abs().max().item()), (name, e)
 
 
+@pytest.mark.parametrize('R,H', [(6000, 512), (390, 256)])
 @pytest.mark.parametrize('extra_consumer', [False, True])
-def test_linear_f32_relu_handoff_matches_fp64(extra_consumer, f32_mfma):
+def test_linear_f32_relu_handoff_matches_fp64(extra_consumer, R, H, f32_mfma):
     """Chained fp32 linears: the second layer's dX epilogue applies the first layer's ReLU mask and the first
     layer's backward skips its threshold pass (native._premasked); with a second consumer of the hidden
     activation the summed gradient must take the mask as usual.  Both vs float64."""
     from applestar_amd.ops import native as NN
     torch.manual_seed(6)
-    R, K, H, O = 6000, 256, 512, 256
+    K, O = 256, 256
     x = torch.randn(R, K, device=DEV).requires_grad_()
     w1 = (torch.randn(H, K, device=DEV) / K ** 0.5).requires_grad_()
     b1 = (0.1 * torch.randn(H, device=DEV)).requires_grad_()

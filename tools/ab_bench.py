@@ -35,6 +35,10 @@ def set_variant(name, on):
     elif name == 'side_stream':
         from applestar_amd.models import model
         model.SIDE_STREAMS_ENABLED = on
+    elif name == 'f32_small_gemm':
+        native.F32_SMALL_K = 384 if on else 0
+    elif name == 'f32_kpad':
+        native.F32_KPAD = on
     else:
         raise ValueError(name)
 
@@ -44,9 +48,11 @@ def main():
     ap.add_argument('--variant', required=True)
     ap.add_argument('--rounds', type=int, default=4)
     ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--precision', choices=['bf16', 'fp32'], default='bf16')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
-    tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}, device=dev)
+    tr = RLTrainer({'learner': {'use_value_feature': True,
+                                'amp_dtype': 'bfloat16' if args.precision == 'bf16' else None}, 'model': {'enable_baselines': ['winloss']}}, device=dev)
     hb = [pin_tree(rl_batch(6, 64, max_entities=512, seed=i)) for i in range(2)]
 
     def src():
@@ -71,7 +77,7 @@ def main():
                 tr.step(next(it))
             torch.cuda.synchronize()
             res[on].append(1000 * (time.perf_counter() - t0) / args.steps)
-    out = {'variant': args.variant, 'off_ms': [round(x, 2) for x in res[False]],
+    out = {'variant': args.variant, 'precision': args.precision, 'off_ms': [round(x, 2) for x in res[False]],
            'on_ms': [round(x, 2) for x in res[True]],
            'off_mean': round(sum(res[False]) / len(res[False]), 2), 'on_mean': round(sum(res[True]) / len(res[True]), 2)}
     print(json.dumps(out), flush=True)
