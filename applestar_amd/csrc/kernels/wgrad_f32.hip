@@ -239,12 +239,14 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
 // read 32 consecutive floats of one row).  The conv form's X piece of a lane is a fixed 4-channel group of one tap
 // (the lane's column is the same in every stage); its row's image coordinates advance by 16 rows per issued step.
 template <int BN, int BK, bool CONV, int NS>
-__global__ __launch_bounds__(256, (BN == 128 && BK == 128) ? 2 : 3) void wgrad_f32_pipe_kernel(const float* __restrict__ dy,
+__global__ __launch_bounds__(256, ((BN == 128 && BK == 128) || BN == 32) ? 2 : 3) void wgrad_f32_pipe_kernel(const float* __restrict__ dy,
                                                                 const float* __restrict__ x,
                                                                 float* __restrict__ dw_part, float* __restrict__ db_part,
                                                                 long part_stride, long R, int N, int K, int H, int W,
                                                                 int Cin, long rows_per_split, int tiles_n, int tiles_k) {
-  constexpr int RS = 16;
+  // a 32-wide N tile takes 32 reduction rows per stage (two MFMA K-steps) so its dY rows still fill one 4-KB
+  // DMA wave-instruction per wave
+  constexpr int RS = BN == 32 ? 32 : 16, SUB = RS / 16;
   constexpr int A_BYTES = RS * BN * 4, B_BYTES = RS * BK * 4, STAGE = A_BYTES + B_BYTES;
   constexpr int A_PW = A_BYTES / 4096, B_PW = B_BYTES / 4096;          // DMA wave-instructions per wave
   constexpr int A_CPR = BN / 4, B_CPR = BK / 4;                       // 16-B pieces per row
@@ -340,30 +342,33 @@ __global__ __launch_bounds__(256, (BN == 128 && BK == 128) ? 2 : 3) void wgrad_f
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     issue(next, kt + NS - 1);
-    const float* A = reinterpret_cast<const float*>(st) + (8 * h) * BN + wn * TN + l32;
-    const float* Bt = reinterpret_cast<const float*>(st + A_BYTES) + (8 * h) * BK + wk * TK + l32;
-    float av[FN][8], bv[FK][8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
+    for (int sub = 0; sub < SUB; ++sub) {
+      const float* A = reinterpret_cast<const float*>(st) + (16 * sub + 8 * h) * BN + wn * TN + l32;
+      const float* Bt = reinterpret_cast<const float*>(st + A_BYTES) + (16 * sub + 8 * h) * BK + wk * TK + l32;
+      float av[FN][8], bv[FK][8];
 #pragma unroll
-      for (int i = 0; i < FN; ++i) av[i][t] = A[t * BN + 32 * i];
+      for (int t = 0; t < 8; ++t) {
 #pragma unroll
-      for (int j = 0; j < FK; ++j) bv[j][t] = Bt[t * BK + 32 * j];
-    }
-    Split3 sa[FN], sb[FK];
+        for (int i = 0; i < FN; ++i) av[i][t] = A[t * BN + 32 * i];
 #pragma unroll
-    for (int i = 0; i < FN; ++i) sa[i] = split8(av[i]);
+        for (int j = 0; j < FK; ++j) bv[j][t] = Bt[t * BK + 32 * j];
+      }
+      Split3 sa[FN], sb[FK];
 #pragma unroll
-    for (int j = 0; j < FK; ++j) sb[j] = split8(bv[j]);
+      for (int i = 0; i < FN; ++i) sa[i] = split8(av[i]);
 #pragma unroll
-    for (int i = 0; i < FN; ++i)
-#pragma unroll
-      for (int j = 0; j < FK; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
-    if (do_bias) {
+      for (int j = 0; j < FK; ++j) sb[j] = split8(bv[j]);
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int t = 0; t < 8; ++t) bsum[i] += av[i][t];
+        for (int j = 0; j < FK; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int t = 0; t < 8; ++t) bsum[i] += av[i][t];
+      }
     }
   };
   issue(smem[0], 0);
@@ -401,13 +406,22 @@ __global__ __launch_bounds__(256, (BN == 128 && BK == 128) ? 2 : 3) void wgrad_f
   }
 }
 
+// A/B switch for the 32-wide ring kernel (APPLESTAR_WGRAD32_PIPE=0: the register-staged kernel)
+bool wgrad_f32_pipe32_off() {
+  static const bool off = [] {
+    const char* e = std::getenv("APPLESTAR_WGRAD32_PIPE");
+    return e != nullptr && e[0] == '0';
+  }();
+  return off;
+}
+
 template <int BN, int BK, bool CONV>
 void launch(const float* dy, const float* x, float* dwp, float* dbp, long ps, long R, int N, int K, int H, int W,
             int Cin, int S, long rps, hipStream_t st) {
   const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
   const long nwg = static_cast<long>(tn) * tk * S;
-  if constexpr (BN >= 64) {
-    if (f32_mfma_mode() == 1) {
+  if constexpr (BN >= 32) {
+    if (f32_mfma_mode() == 1 && !(BN == 32 && wgrad_f32_pipe32_off())) {
       hipLaunchKernelGGL((wgrad_f32_pipe_kernel<BN, BK, CONV, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st,
                          dy, x, dwp, dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
       return;
