@@ -406,11 +406,13 @@ __global__ __launch_bounds__(256, ((BN == 128 && BK == 128) || BN == 32) ? 2 : 3
   }
 }
 
-// A/B switch for the 32-wide ring kernel (APPLESTAR_WGRAD32_PIPE=0: the register-staged kernel)
+// The 32-wide ring kernel is opt-in (APPLESTAR_WGRAD32_PIPE=1): on the learner's narrow convs it measured
+// 5-13 % slower than the register-staged kernel (76x80 64->32: 1358 vs 1283 us; 19x20 32->32: 66.7 vs
+// 59.2 us; profiles/r3v2_wgrad32_ab.jsonl) - 60 KB of stages hold it at 2 workgroups per CU.
 bool wgrad_f32_pipe32_off() {
   static const bool off = [] {
     const char* e = std::getenv("APPLESTAR_WGRAD32_PIPE");
-    return e != nullptr && e[0] == '0';
+    return e == nullptr || e[0] != '1';
   }();
   return off;
 }

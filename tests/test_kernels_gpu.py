@@ -1182,11 +1182,15 @@ def test_linear_f32_grads_match_fp64(R, N, K, f32_mfma):
 
 @pytest.mark.parametrize('R,H', [(6000, 512), (390, 256)])
 @pytest.mark.parametrize('extra_consumer', [False, True])
-def test_linear_f32_relu_handoff_matches_fp64(extra_consumer, R, H, f32_mfma):
+def test_linear_f32_relu_handoff_matches_fp64(extra_consumer, R, H, f32_mfma, monkeypatch):
     """Chained fp32 linears: the second layer's dX epilogue applies the first layer's ReLU mask and the first
     layer's backward skips its threshold pass (native._premasked); with a second consumer of the hidden
-    activation the summed gradient must take the mask as usual.  Both vs float64."""
+    activation the summed gradient must take the mask as usual.  Both vs float64.  The few-row case routes its
+    products to gemm_f32 through the small-product switch (off by default: the library wins there in the step,
+    profiles/r3z4_ab_small.jsonl), so the hand-off is exercised on few-row tiles too."""
     from applestar_amd.ops import native as NN
+    if R < 1000:
+        monkeypatch.setattr(NN, 'F32_SMALL_K', 384)
     torch.manual_seed(6)
     K, O = 256, 256
     x = torch.randn(R, K, device=DEV).requires_grad_()

@@ -1,6 +1,6 @@
 """fp32 weight gradients with a <= 32-wide output (N tile 32): time per call and error vs float64 on a row
 subsample, for the A/B of the 32-wide LDS-DMA ring kernel (run once with APPLESTAR_WGRAD32_PIPE=0 for the
-register-staged kernel; the switch is read once per process).
+register-staged kernel, APPLESTAR_WGRAD32_PIPE=1 for the ring; the switch is read once per process).
 
     python tools/bench_wgrad32.py > out.jsonl
 """
@@ -28,7 +28,7 @@ def main():
     from applestar_amd.ops import native
     C = native.ensure_loaded()
     C.set_f32_mfma_mode(1)
-    mode = 'regstaged' if os.environ.get('APPLESTAR_WGRAD32_PIPE', '1') == '0' else 'ring'
+    mode = 'ring' if os.environ.get('APPLESTAR_WGRAD32_PIPE', '0') == '1' else 'regstaged'
     torch.manual_seed(0)
     for B, H, W, cin, cout in CONV:
         x = torch.randn(B, H, W, cin, device='cuda')

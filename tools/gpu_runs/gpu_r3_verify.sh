@@ -3,15 +3,15 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" 2>/dev/null || cd /root/repo
 mkdir -p gpurun_out
-timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/v_bench.json 2> gpurun_out/v_bench.err || { echo bench failed; tail -20 gpurun_out/v_bench.err; exit 1; }
-cat gpurun_out/v_bench.json
+[ -n "$NOBENCH" ] || timeout -k 10 400 python -u bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/v_bench.json 2> gpurun_out/v_bench.err || { echo bench failed; tail -20 gpurun_out/v_bench.err; exit 1; }
+[ -n "$NOBENCH" ] || cat gpurun_out/v_bench.json
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/v_smoke.log 2>&1 || { echo smoke failed; tail -20 gpurun_out/v_smoke.log; exit 1; }
 tail -1 gpurun_out/v_smoke.log
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/v_pytest.txt 2>&1; rc=$?
 tail -3 gpurun_out/v_pytest.txt; [ $rc -eq 0 ] || exit $rc
 if [ -n "$WGRAD32_AB" ]; then
   APPLESTAR_WGRAD32_PIPE=0 timeout -k 10 120 python -u tools/bench_wgrad32.py > gpurun_out/v_wgrad32_ab.jsonl 2>/dev/null &&
-  timeout -k 10 120 python -u tools/bench_wgrad32.py >> gpurun_out/v_wgrad32_ab.jsonl 2>/dev/null; rc=$?
+  APPLESTAR_WGRAD32_PIPE=1 timeout -k 10 120 python -u tools/bench_wgrad32.py >> gpurun_out/v_wgrad32_ab.jsonl 2>/dev/null; rc=$?
   cat gpurun_out/v_wgrad32_ab.jsonl
 fi
 [ $rc -eq 0 ] || exit $rc
