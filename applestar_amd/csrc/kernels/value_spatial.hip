@@ -213,6 +213,8 @@ __global__ __launch_bounds__(256) void vsp_pool_fwd_kernel(const T* __restrict__
   }
 }
 
+// four lanes per pooled pixel, four output channels each (acc 4 x 11 + weights 4 x 8 per lane: < 128 VGPRs, so
+// the window's inputs can all be loaded before the first update without dropping below 4 waves per SIMD)
 template <typename T>
 __global__ __launch_bounds__(256) void vsp_pool_bwd_kernel(const T* __restrict__ dpooled,
                                                            const uint8_t* __restrict__ pos,
@@ -221,80 +223,106 @@ __global__ __launch_bounds__(256) void vsp_pool_bwd_kernel(const T* __restrict__
                                                            const uint8_t* __restrict__ enemy, const float* __restrict__ w,
                                                            T* __restrict__ dsc, float* __restrict__ part, int B,
                                                            int H, int W) {
-  __shared__ float red[4][2][kVsAcc];
-  const int h = threadIdx.x & 1;
-  float wr[8][kVsSc], acc[8][kVsIn + 1];
+  constexpr int CL = 4;                        // channels per lane
+  constexpr int NA = CL * (kVsIn + 1);         // accumulators per lane
+  __shared__ float red[4][4][NA];
+  const int h = threadIdx.x & 3;
+  float wr[CL][kVsSc], acc[CL][kVsIn + 1];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
+  for (int c = 0; c < CL; ++c) {
 #pragma unroll
-    for (int k = 0; k < kVsSc; ++k) wr[c][k] = w[(8 * h + c) * kVsIn + k];
+    for (int k = 0; k < kVsSc; ++k) wr[c][k] = w[(CL * h + c) * kVsIn + k];
 #pragma unroll
     for (int k = 0; k <= kVsIn; ++k) acc[c][k] = 0.f;
   }
   const int Ho = H >> 1, Wo = W >> 1;
   const long Po = static_cast<long>(B) * Ho * Wo;
-  const long step = static_cast<long>(gridDim.x) * (blockDim.x >> 1);
-  for (long q = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) >> 1; q < Po; q += step) {
+  const long step = static_cast<long>(gridDim.x) * (blockDim.x >> 2);
+  for (long q = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) >> 2; q < Po; q += step) {
     const int ox = static_cast<int>(q % Wo);
     const long t = q / Wo;
     const int oy = static_cast<int>(t % Ho);
     const long bb = t / Ho;
     const long p00 = (bb * H + 2 * oy) * W + 2 * ox;
-    float d[8], y[8];
-    vs_load8<T>(dpooled + q * kVsOut + 8 * h, d);
-    vs_load8<T>(pooled + q * kVsOut + 8 * h, y);
-    const uint2 pp = *reinterpret_cast<const uint2*>(pos + q * kVsOut + 8 * h);
-#pragma unroll 1
-    for (int t4 = 0; t4 < 4; ++t4) {
-      float g[8];
+    // every load of the pooled pixel and its 2x2 window is issued before the first update
+    float d[CL], y[CL];
+    if constexpr (sizeof(T) == 4) {
+      const float4 dv = *reinterpret_cast<const float4*>(dpooled + q * kVsOut + CL * h);
+      const float4 yv = *reinterpret_cast<const float4*>(pooled + q * kVsOut + CL * h);
+      d[0] = dv.x; d[1] = dv.y; d[2] = dv.z; d[3] = dv.w;
+      y[0] = yv.x; y[1] = yv.y; y[2] = yv.z; y[3] = yv.w;
+    } else {
+      const uint2 dv = *reinterpret_cast<const uint2*>(dpooled + q * kVsOut + CL * h);
+      const uint2 yv = *reinterpret_cast<const uint2*>(pooled + q * kVsOut + CL * h);
+      const uint32_t dw[2] = {dv.x, dv.y}, yw[2] = {yv.x, yv.y};
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const uint32_t pc = ((c < 4 ? pp.x : pp.y) >> (8 * (c & 3))) & 0xffu;
+      for (int i = 0; i < 2; ++i) {
+        d[2 * i] = bf2f(static_cast<bf16_t>(dw[i] & 0xffffu));
+        d[2 * i + 1] = bf2f(static_cast<bf16_t>(dw[i] >> 16));
+        y[2 * i] = bf2f(static_cast<bf16_t>(yw[i] & 0xffffu));
+        y[2 * i + 1] = bf2f(static_cast<bf16_t>(yw[i] >> 16));
+      }
+    }
+    const uint32_t pp = *reinterpret_cast<const uint32_t*>(pos + q * kVsOut + CL * h);
+    float s4[4][kVsSc], fo4[4], fe4[4];
+#pragma unroll
+    for (int t4 = 0; t4 < 4; ++t4) {
+      const long px = p00 + (t4 >> 1) * W + (t4 & 1);
+      vs_load8<T>(sc + px * kVsSc, s4[t4]);
+      fo4[t4] = own[px] ? 1.f : 0.f;
+      fe4[t4] = enemy[px] ? 1.f : 0.f;
+    }
+#pragma unroll
+    for (int t4 = 0; t4 < 4; ++t4) {
+      float g[CL];
+#pragma unroll
+      for (int c = 0; c < CL; ++c) {
+        const uint32_t pc = (pp >> (8 * c)) & 0xffu;
         g[c] = (pc == static_cast<uint32_t>(t4) && y[c] > 0.f) ? d[c] : 0.f;
       }
       float ds[kVsSc];
 #pragma unroll
       for (int k = 0; k < kVsSc; ++k) ds[k] = 0.f;
-      float s[kVsSc];
-      const long px = p00 + (t4 >> 1) * W + (t4 & 1);
-      vs_load8<T>(sc + px * kVsSc, s);
-      const float fo = own[px] ? 1.f : 0.f, fe = enemy[px] ? 1.f : 0.f;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
+      for (int c = 0; c < CL; ++c) {
 #pragma unroll
         for (int k = 0; k < kVsSc; ++k) {
-          acc[c][k] = fmaf(g[c], s[k], acc[c][k]);
+          acc[c][k] = fmaf(g[c], s4[t4][k], acc[c][k]);
           ds[k] = fmaf(wr[c][k], g[c], ds[k]);
         }
-        acc[c][kVsSc] = fmaf(g[c], fo, acc[c][kVsSc]);
-        acc[c][kVsSc + 1] = fmaf(g[c], fe, acc[c][kVsSc + 1]);
+        acc[c][kVsSc] = fmaf(g[c], fo4[t4], acc[c][kVsSc]);
+        acc[c][kVsSc + 1] = fmaf(g[c], fe4[t4], acc[c][kVsSc + 1]);
         acc[c][kVsIn] += g[c];
       }
 #pragma unroll
-      for (int k = 0; k < kVsSc; ++k) ds[k] += __shfl_xor(ds[k], 1, 64);
-      if (h == 0) vs_store8<T>(dsc + px * kVsSc, ds);
+      for (int k = 0; k < kVsSc; ++k) {
+        ds[k] += __shfl_xor(ds[k], 1, 64);
+        ds[k] += __shfl_xor(ds[k], 2, 64);
+      }
+      if (h == 0) vs_store8<T>(dsc + (p00 + (t4 >> 1) * W + (t4 & 1)) * kVsSc, ds);
     }
   }
 #pragma unroll
-  for (int c = 0; c < 8; ++c)
+  for (int c = 0; c < CL; ++c)
 #pragma unroll
     for (int k = 0; k <= kVsIn; ++k) {
       float v = acc[c][k];
 #pragma unroll
-      for (int off = 2; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+      for (int off = 4; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
       acc[c][k] = v;
     }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane < 2) {
+  if (lane < 4) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
+    for (int c = 0; c < CL; ++c)
 #pragma unroll
       for (int k = 0; k <= kVsIn; ++k) red[wv][lane][c * (kVsIn + 1) + k] = acc[c][k];
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < 2 * kVsAcc; e += blockDim.x) {
-    const int hh = e / kVsAcc, j = e % kVsAcc;
-    part[static_cast<long>(blockIdx.x) * 2 * kVsAcc + e] = red[0][hh][j] + red[1][hh][j] + red[2][hh][j] + red[3][hh][j];
+  // part[block][ch * 11 + j] with ch = 4 * h + c  (== h * 44 + c * 11 + k): the layout of the other backward
+  for (int e = threadIdx.x; e < 4 * NA; e += blockDim.x) {
+    const int hh = e / NA, j = e % NA;
+    part[static_cast<long>(blockIdx.x) * 4 * NA + e] = red[0][hh][j] + red[1][hh][j] + red[2][hh][j] + red[3][hh][j];
   }
 }
 
