@@ -46,32 +46,116 @@ template <> struct Row4<bf16_t> {
   }
 };
 
-// wT [K_in][256]; out [T][256]
+// wT [K_in][256]; out [T][256].  Per entity, lane k < f.n loads field k's value (one memory latency for all
+// fields), expands it into its (W^T row, scale) entries - 1 for one-hot / scalar fields, one per set bit of a
+// binary field - and writes them at its exclusive prefix offset into the wave's LDS list; the wave then
+// gathers the rows four at a time (four row loads in flight) and accumulates them in list order, i.e. the same
+// order (and so the same bits) as a field-by-field loop.  Lists longer than kEeList entries fall back to that
+// loop.
+constexpr int kEeList = 128;
+
+template <typename TW>
+__device__ __forceinline__ void ee_fields_serial(const EntityFields& f, long src, const TW* __restrict__ wT, int lane,
+                                                 float* acc) {
+  constexpr int C = 256;
+  for (int k = 0; k < f.n; ++k) {
+    const float v = load_field(f.ptr[k], f.dtype[k], src);
+    const int off = f.offset[k], width = f.width[k];
+    if (f.kind[k] == FIELD_ONE_HOT) {
+      const int col = off + clampi(static_cast<int>(v), 0, width - 1);
+      Row4<TW>::add(wT + static_cast<long>(col) * C + lane * 4, 1.f, acc);
+    } else if (f.kind[k] == FIELD_BINARY) {
+      const int iv = clampi(static_cast<int>(v), 0, (1 << width) - 1);
+      for (int bit = 0; bit < width; ++bit)
+        if ((iv >> (width - 1 - bit)) & 1) Row4<TW>::add(wT + static_cast<long>(off + bit) * C + lane * 4, 1.f, acc);
+    } else {
+      Row4<TW>::add(wT + static_cast<long>(off) * C + lane * 4, v, acc);
+    }
+  }
+}
+
 template <typename TW, typename TO>
 __global__ __launch_bounds__(256) void entity_embed_fwd_kernel(EntityFields f, const int64_t* __restrict__ index,
                                                                const TW* __restrict__ wT, const float* __restrict__ bias,
                                                                TO* __restrict__ out, long T) {
   constexpr int C = 256;
-  const int lane = threadIdx.x & 63;
+  __shared__ int s_col[4][kEeList];
+  __shared__ float s_scale[4][kEeList];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const long wave = (static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const long nwave = (static_cast<long>(gridDim.x) * blockDim.x) >> 6;
   const float4 bv = *reinterpret_cast<const float4*>(bias + lane * 4);
+  const int nf = f.n;
+  // this lane's field (lane < nf): kind / offset / width / source, fixed for the whole kernel
+  const int kk = lane < nf ? lane : 0;
+  int kind = 0, off = 0, width = 1, fdt = 0;
+  const void* fptr = nullptr;
+  for (int k = 0; k < nf; ++k)      // uniform loop: picks the lane's entry without dynamic kernarg indexing
+    if (k == kk) { kind = f.kind[k]; off = f.offset[k]; width = f.width[k]; fdt = f.dtype[k]; fptr = f.ptr[k]; }
   for (long t = wave; t < T; t += nwave) {
     const long src = index[t];
     float acc[4] = {bv.x, bv.y, bv.z, bv.w};
-    for (int k = 0; k < f.n; ++k) {
-      const float v = load_field(f.ptr[k], f.dtype[k], src);
-      const int off = f.offset[k], width = f.width[k];
-      if (f.kind[k] == FIELD_ONE_HOT) {
-        const int col = off + clampi(static_cast<int>(v), 0, width - 1);
-        Row4<TW>::add(wT + static_cast<long>(col) * C + lane * 4, 1.f, acc);
-      } else if (f.kind[k] == FIELD_BINARY) {
-        const int iv = clampi(static_cast<int>(v), 0, (1 << width) - 1);
-        for (int bit = 0; bit < width; ++bit)
-          if ((iv >> (width - 1 - bit)) & 1) Row4<TW>::add(wT + static_cast<long>(off + bit) * C + lane * 4, 1.f, acc);
+    int cnt = 0, iv = 0;
+    float v = 0.f;
+    if (lane < nf) {
+      v = load_field(fptr, fdt, src);
+      if (kind == FIELD_BINARY) {
+        iv = clampi(static_cast<int>(v), 0, (1 << width) - 1);
+        cnt = __popc(iv);
       } else {
-        Row4<TW>::add(wT + static_cast<long>(off) * C + lane * 4, v, acc);
+        cnt = 1;
       }
+    }
+    // exclusive prefix sum of cnt over the wave
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    const int total = __shfl(incl, 63, 64);
+    if (total > kEeList) {
+      ee_fields_serial<TW>(f, src, wT, lane, acc);
+    } else {
+      int pos = incl - cnt;
+      if (lane < nf) {
+        if (kind == FIELD_ONE_HOT) {
+          s_col[wv][pos] = off + clampi(static_cast<int>(v), 0, width - 1);
+          s_scale[wv][pos] = 1.f;
+        } else if (kind == FIELD_BINARY) {
+          for (int bit = 0; bit < width; ++bit)
+            if ((iv >> (width - 1 - bit)) & 1) {
+              s_col[wv][pos] = off + bit;
+              s_scale[wv][pos] = 1.f;
+              ++pos;
+            }
+        } else {
+          s_col[wv][pos] = off;
+          s_scale[wv][pos] = v;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      int e = 0;
+      for (; e + 4 <= total; e += 4) {
+        int col[4];
+        float sc[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { col[u] = s_col[wv][e + u]; sc[u] = s_scale[wv][e + u]; }
+        float r[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          r[u][0] = r[u][1] = r[u][2] = r[u][3] = 0.f;
+          Row4<TW>::add(wT + static_cast<long>(col[u]) * C + lane * 4, 1.f, r[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[i] = fmaf(sc[u], r[u][i], acc[i]);
+      }
+      for (; e < total; ++e) Row4<TW>::add(wT + static_cast<long>(s_col[wv][e]) * C + lane * 4, s_scale[wv][e], acc);
+      __builtin_amdgcn_wave_barrier();     // the list is rewritten for the next entity
     }
     float o[4] = {fmaxf(acc[0], 0.f), fmaxf(acc[1], 0.f), fmaxf(acc[2], 0.f), fmaxf(acc[3], 0.f)};
 #pragma unroll
