@@ -1069,21 +1069,24 @@ void spatial_embed_fused(const SpatialPlanes& sp, const float* wd, const float* 
 #undef AS_SP
 }
 
-int spatial_wgrad_blocks(int B) { return B * 4; }
+// workgroups per observation of the spatial dense wgrad: 16 (was 4: 6 waves per SIMD in one round, too few
+// loads in flight for the 2.4 GB of dpre / gate the fp32 step streams)
+constexpr int kSpWgPerObs = 16;
+int spatial_wgrad_blocks(int B) { return B * kSpWgPerObs; }
 
 void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, const void* gate, int dt, float* part, int B, int H,
                          int W, int L, hipStream_t s) {
   const int tiles = (H * W + kSpTile - 1) / kSpTile;
   if (B == 0) return;
   if (dt == DT_BF16 && spatial_mfma())
-    hipLaunchKernelGGL(spatial_dense_wgrad_mfma_kernel, dim3(static_cast<unsigned>(B) * 4), dim3(256), 0, s, sp,
-                       static_cast<const bf16_t*>(dpre), static_cast<const bf16_t*>(gate), part, H, W, L, tiles, 4);
+    hipLaunchKernelGGL(spatial_dense_wgrad_mfma_kernel, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256), 0, s, sp,
+                       static_cast<const bf16_t*>(dpre), static_cast<const bf16_t*>(gate), part, H, W, L, tiles, kSpWgPerObs);
   else if (dt == DT_BF16)
-    hipLaunchKernelGGL(spatial_dense_wgrad_kernel<bf16_t>, dim3(static_cast<unsigned>(B) * 4), dim3(256), 0, s, sp,
-                       static_cast<const bf16_t*>(dpre), static_cast<const bf16_t*>(gate), part, H, W, L, tiles, 4);
+    hipLaunchKernelGGL(spatial_dense_wgrad_kernel<bf16_t>, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256), 0, s, sp,
+                       static_cast<const bf16_t*>(dpre), static_cast<const bf16_t*>(gate), part, H, W, L, tiles, kSpWgPerObs);
   else
-    hipLaunchKernelGGL(spatial_dense_wgrad_kernel<float>, dim3(static_cast<unsigned>(B) * 4), dim3(256), 0, s, sp,
-                       static_cast<const float*>(dpre), static_cast<const float*>(gate), part, H, W, L, tiles, 4);
+    hipLaunchKernelGGL(spatial_dense_wgrad_kernel<float>, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256), 0, s, sp,
+                       static_cast<const float*>(dpre), static_cast<const float*>(gate), part, H, W, L, tiles, kSpWgPerObs);
 }
 
 void relu_cast(const float* x, void* y, int dt, long n, hipStream_t s) {
