@@ -422,7 +422,7 @@ void launch(const float* dy, const float* x, float* dwp, float* dbp, long ps, lo
             int Cin, int S, long rps, hipStream_t st) {
   const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
   const long nwg = static_cast<long>(tn) * tk * S;
-  if constexpr (BN >= 32) {
+  if constexpr (BN >= 32 && BK <= 128) {
     if (f32_mfma_mode() == 1 && !(BN == 32 && wgrad_f32_pipe32_off())) {
       hipLaunchKernelGGL((wgrad_f32_pipe_kernel<BN, BK, CONV, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st,
                          dy, x, dwp, dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
@@ -438,8 +438,21 @@ void launch(const float* dy, const float* x, float* dwp, float* dbp, long ps, lo
 }
 
 int pick(int n) { return n <= 32 ? 32 : (n <= 64 ? 64 : 128); }
+// A/B switch: the 32-wide N tile with a 256-wide K tile (each wave 32 x 64: the dY fragment feeds two MFMA
+// blocks) for K >= 256 (APPLESTAR_WGRAD32_BK=256).  Measured 20 % slower on the learner's narrow convs
+// (profiles/r3v6_wgrad32_bk256_ab.jsonl: 75 KB of stages, 2 workgroups per CU), so off by default.
+bool wgrad32_bk256() {
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_WGRAD32_BK");
+    return e != nullptr && e[0] == '2';
+  }();
+  return on;
+}
 // the K tile: a wave covers >= 32 columns (2 waves along K for BN >= 64, 4 for the 32-wide N tile)
-int pick_k(int k, int bn) { return bn == 32 ? 128 : (k <= 64 ? 64 : 128); }
+int pick_k(int k, int bn) {
+  if (bn == 32) return (k >= 256 && wgrad32_bk256()) ? 256 : 128;
+  return k <= 64 ? 64 : 128;
+}
 
 }  // namespace
 
@@ -468,7 +481,7 @@ void wgrad_f32(const float* dy, const float* x, float* dw_part, float* db_part, 
     else launch<BNv, BKv, false>(dy, x, dw_part, db_part, part_stride, R, N, K, H, W, Cin, S, rps, st);     \
     return;                                                                                \
   }
-  AS_WGF(128, 128) AS_WGF(128, 64) AS_WGF(64, 128) AS_WGF(64, 64) AS_WGF(32, 128)
+  AS_WGF(128, 128) AS_WGF(128, 64) AS_WGF(64, 128) AS_WGF(64, 64) AS_WGF(32, 128) AS_WGF(32, 256)
 #undef AS_WGF
 }
 

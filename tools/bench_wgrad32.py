@@ -29,6 +29,8 @@ def main():
     C = native.ensure_loaded()
     C.set_f32_mfma_mode(1)
     mode = 'ring' if os.environ.get('APPLESTAR_WGRAD32_PIPE', '0') == '1' else 'regstaged'
+    if os.environ.get('APPLESTAR_WGRAD32_BK', '128') == '256':
+        mode += '_bk256'
     torch.manual_seed(0)
     for B, H, W, cin, cout in CONV:
         x = torch.randn(B, H, W, cin, device='cuda')

@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -3 gpurun_out/v_pytest.txt; [ $rc -eq 0 ] || exit $rc
 if [ -n "$WGRAD32_AB" ]; then
   APPLESTAR_WGRAD32_PIPE=0 timeout -k 10 120 python -u tools/bench_wgrad32.py > gpurun_out/v_wgrad32_ab.jsonl 2>/dev/null &&
-  APPLESTAR_WGRAD32_PIPE=1 timeout -k 10 120 python -u tools/bench_wgrad32.py >> gpurun_out/v_wgrad32_ab.jsonl 2>/dev/null; rc=$?
+  APPLESTAR_WGRAD32_BK=256 timeout -k 10 120 python -u tools/bench_wgrad32.py >> gpurun_out/v_wgrad32_ab.jsonl 2>/dev/null; rc=$?
   cat gpurun_out/v_wgrad32_ab.jsonl
 fi
 [ $rc -eq 0 ] || exit $rc
