@@ -867,12 +867,14 @@ std::vector<at::Tensor> target_unit_sample(const at::Tensor& e, const at::Tensor
 
 // ---------------------------------------------------------------- fused clip + Adam
 void fused_clip_adam(const at::Tensor& table, const at::Tensor& chunks, const at::Tensor& part,
-                     const c10::optional<at::Tensor>& gate, const at::Tensor& norm_out, double max_norm, double lr_bc1,
-                     double b1, double b2, double inv_sqrt_bc2, double eps, double wd, bool decoupled) {
+                     const c10::optional<at::Tensor>& gate, const at::Tensor& norm_out, double max_norm,
+                     const c10::optional<at::Tensor>& mom, const c10::optional<at::Tensor>& scale, bool mom_init,
+                     const c10::optional<at::Tensor>& hp, double lr_bc1, double b1, double b2, double inv_sqrt_bc2,
+                     double eps, double wd, bool decoupled) {
   check_cuda(table, "table");
   TORCH_CHECK(table.scalar_type() == at::kLong && chunks.scalar_type() == at::kLong && table.is_contiguous() &&
               chunks.is_contiguous() && table.numel() % 6 == 0 && chunks.numel() % 2 == 0, "fused_clip_adam: tables");
-  const int64_t nch = chunks.numel() / 2;
+  const int64_t nch = chunks.numel() / 2, nt = table.numel() / 6;
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.numel() >= nch, "fused_clip_adam: part");
   TORCH_CHECK(norm_out.scalar_type() == at::kFloat && norm_out.numel() >= 1, "fused_clip_adam: norm_out");
   const float* gp = nullptr;
@@ -880,12 +882,28 @@ void fused_clip_adam(const at::Tensor& table, const at::Tensor& chunks, const at
     TORCH_CHECK(gate->scalar_type() == at::kFloat && gate->numel() == 1, "fused_clip_adam: gate fp32 scalar");
     gp = gate->data_ptr<float>();
   }
+  float* mp = nullptr;
+  float* sp = nullptr;
+  if (mom && mom->defined()) {
+    TORCH_CHECK(scale && scale->defined(), "fused_clip_adam: momentum_norm needs mom and scale");
+    TORCH_CHECK(mom->scalar_type() == at::kFloat && mom->numel() == nt && mom->is_contiguous() &&
+                scale->scalar_type() == at::kFloat && scale->numel() == nt && scale->is_contiguous(),
+                "fused_clip_adam: mom / scale fp32 [ntensors]");
+    mp = mom->data_ptr<float>();
+    sp = scale->data_ptr<float>();
+  }
+  const float* hpp = nullptr;
+  if (hp && hp->defined()) {
+    TORCH_CHECK(hp->scalar_type() == at::kFloat && hp->numel() == 3 && hp->is_cuda(), "fused_clip_adam: hp fp32 [3]");
+    hpp = hp->data_ptr<float>();
+  }
   c10::hip::HIPGuard g(table.device().index());
   as::fused_clip_adam(table.data_ptr(), reinterpret_cast<const long*>(chunks.data_ptr<int64_t>()),
-                      static_cast<int>(nch), part.data_ptr<float>(), gp, norm_out.data_ptr<float>(),
-                      static_cast<float>(max_norm), static_cast<float>(lr_bc1), static_cast<float>(b1),
-                      static_cast<float>(b2), static_cast<float>(inv_sqrt_bc2), static_cast<float>(eps),
-                      static_cast<float>(wd), decoupled ? 1 : 0, stream());
+                      static_cast<int>(nch), static_cast<int>(nt), part.data_ptr<float>(), gp,
+                      norm_out.data_ptr<float>(), static_cast<float>(max_norm), mp, sp, mom_init ? 1 : 0, hpp,
+                      static_cast<float>(lr_bc1), static_cast<float>(b1), static_cast<float>(b2),
+                      static_cast<float>(inv_sqrt_bc2), static_cast<float>(eps), static_cast<float>(wd),
+                      decoupled ? 1 : 0, stream());
 }
 
 // ---------------------------------------------------------------- fp32 conv3x3 / weight gradients
@@ -1656,8 +1674,11 @@ at::Tensor pointwise_conv(const at::Tensor& x, const at::Tensor& w, const c10::o
   return y;
 }
 
+void register_codec(pybind11::module& m);   // codec.cpp: native tensor-tree frames (utils/serialize.py)
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "applestar_amd HIP kernels for gfx950 (MI355X)";
+  register_codec(m);
   m.def("layer_norm_fwd", &layer_norm_fwd);
   m.def("layer_norm_bwd", &layer_norm_bwd);
   m.def("reverse_scan", &reverse_scan);

@@ -96,9 +96,10 @@ def write_ninja() -> str:
         o = os.path.join(BUILD, os.path.basename(k) + '.o')
         lines.append(f'build {o}: hip {k}')
         objs.append(o)
-    b_o = os.path.join(BUILD, 'bindings.o')
-    lines.append(f'build {b_o}: cxx {os.path.join(HERE, "bindings.cpp")}')
-    objs.append(b_o)
+    for cpp in ('bindings.cpp', 'codec.cpp'):
+        b_o = os.path.join(BUILD, cpp.replace('.cpp', '.o'))
+        lines.append(f'build {b_o}: cxx {os.path.join(HERE, cpp)}')
+        objs.append(b_o)
     lines.append(f'build {ext_filename()}: link {" ".join(objs)}')
     lines.append(f'default {ext_filename()}')
     os.makedirs(BUILD, exist_ok=True)

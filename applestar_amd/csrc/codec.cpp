@@ -1,0 +1,463 @@
+// Native tensor-tree codec for the actor <-> inference-server <-> learner data plane (utils/serialize.py).
+//
+// The frame format is the Python codec's, unchanged (so frames from either side interoperate and the learner's
+// trajectory ring keeps parsing headers with json):
+//     "ASTR1" | u64 header_len | u8 compressed | JSON header | zero pad to 64 | body (tensor bytes, 64-B aligned)
+// with header nodes {"__d__": [[key, node], ...]}, {"__l__": [...]}, {"__tu__": [...]},
+// {"__t__": [dtype, shape, body_offset, nbytes]}, {"__v__": scalar}.
+//
+// Why native: an agent step's request is a tree of ~120 small tensors and a trajectory ~64 x 150.  The Python
+// encoder spends ~10 us per tensor leaf in attribute calls (detach / contiguous / view / numpy / slice
+// assignment) - 3 ms per request and ~380 ms per trajectory (tools/actor_step_profile.py), which made the env
+// workers, and on the server side the request decode, the pipeline's bottleneck.  Here a leaf is a type check,
+// a pointer read and one memcpy; the header is emitted and parsed without building intermediate JSON objects.
+// Reference counterpart: the reference pickles + lz4-compresses every trajectory (file_helper.py:255-302).
+#include <torch/extension.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace {
+
+constexpr char kMagic[] = "ASTR1";
+constexpr size_t kMagicLen = 5;
+constexpr int64_t kAlign = 64;
+
+const char* dtype_code(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return "f32";
+    case at::kHalf: return "f16";
+    case at::kBFloat16: return "bf16";
+    case at::kDouble: return "f64";
+    case at::kLong: return "i64";
+    case at::kInt: return "i32";
+    case at::kShort: return "i16";
+    case at::kChar: return "i8";
+    case at::kByte: return "u8";
+    case at::kBool: return "b";
+    default: return nullptr;
+  }
+}
+
+bool dtype_from_code(const std::string& s, at::ScalarType* t) {
+  static const std::pair<const char*, at::ScalarType> tab[] = {
+      {"f32", at::kFloat}, {"f16", at::kHalf}, {"bf16", at::kBFloat16}, {"f64", at::kDouble}, {"i64", at::kLong},
+      {"i32", at::kInt},   {"i16", at::kShort}, {"i8", at::kChar},       {"u8", at::kByte},    {"b", at::kBool}};
+  for (const auto& e : tab)
+    if (s == e.first) {
+      *t = e.second;
+      return true;
+    }
+  return false;
+}
+
+void json_string(std::string& out, const char* s, size_t n) {
+  out.push_back('"');
+  for (size_t i = 0; i < n; ++i) {
+    const unsigned char c = static_cast<unsigned char>(s[i]);
+    switch (c) {
+      case '"': out += "\\\""; break;
+      case '\\': out += "\\\\"; break;
+      case '\n': out += "\\n"; break;
+      case '\r': out += "\\r"; break;
+      case '\t': out += "\\t"; break;
+      default:
+        if (c < 0x20) {
+          char buf[8];
+          snprintf(buf, sizeof(buf), "\\u%04x", c);
+          out += buf;
+        } else if (c < 0x80) {
+          out.push_back(static_cast<char>(c));
+        } else {   // non-ASCII: \uXXXX (surrogate pairs above the BMP), as json.dumps(ensure_ascii=True)
+          unsigned cp = 0;
+          int extra = c >= 0xF0 ? 3 : c >= 0xE0 ? 2 : 1;
+          cp = c & (0x3F >> extra);
+          for (int k = 0; k < extra && i + 1 < n; ++k) cp = (cp << 6) | (static_cast<unsigned char>(s[++i]) & 0x3F);
+          char buf[16];
+          if (cp >= 0x10000) {
+            cp -= 0x10000;
+            snprintf(buf, sizeof(buf), "\\u%04x\\u%04x", 0xD800 + (cp >> 10), 0xDC00 + (cp & 0x3FF));
+          } else {
+            snprintf(buf, sizeof(buf), "\\u%04x", cp);
+          }
+          out += buf;
+        }
+    }
+  }
+  out.push_back('"');
+}
+
+void json_double(std::string& out, double v) {
+  if (std::isnan(v)) { out += "NaN"; return; }
+  if (std::isinf(v)) { out += v > 0 ? "Infinity" : "-Infinity"; return; }
+  char buf[40];
+  snprintf(buf, sizeof(buf), "%.17g", v);
+  out += buf;
+  // keep it a float on the way back ("1" would decode as an int)
+  if (!strpbrk(buf, ".eEn")) out += ".0";
+}
+
+struct Encoder {
+  std::string header;
+  std::vector<std::pair<int64_t, at::Tensor>> blobs;
+  int64_t offset = 0;
+
+  void scalar(py::handle o) {
+    header += "{\"__v__\": ";
+    if (o.is_none()) {
+      header += "null";
+    } else if (PyBool_Check(o.ptr())) {
+      header += o.ptr() == Py_True ? "true" : "false";
+    } else if (PyLong_Check(o.ptr())) {
+      int overflow = 0;
+      const long long v = PyLong_AsLongLongAndOverflow(o.ptr(), &overflow);
+      if (overflow) {
+        header += py::str(o).cast<std::string>();
+      } else {
+        header += std::to_string(v);
+      }
+    } else if (PyFloat_Check(o.ptr())) {
+      const double v = PyFloat_AsDouble(o.ptr());
+      if (std::isfinite(v)) {
+        header += py::repr(o).cast<std::string>();   // shortest round-trip form, as json.dumps
+      } else {
+        json_double(header, v);
+      }
+    } else {   // str
+      Py_ssize_t n = 0;
+      const char* s = PyUnicode_AsUTF8AndSize(o.ptr(), &n);
+      if (!s) throw py::error_already_set();
+      json_string(header, s, static_cast<size_t>(n));
+    }
+    header += "}";
+  }
+
+  void tensor(const at::Tensor& t0) {
+    at::Tensor t = t0.is_cpu() ? t0 : t0.cpu();
+    t = t.contiguous();
+    const char* code = dtype_code(t.scalar_type());
+    if (!code) throw py::type_error("tree_dumps: unsupported tensor dtype");
+    const int64_t off = (offset + kAlign - 1) / kAlign * kAlign;
+    const int64_t nbytes = t.numel() * static_cast<int64_t>(t.element_size());
+    blobs.emplace_back(off, t);
+    offset = off + nbytes;
+    header += "{\"__t__\": [\"";
+    header += code;
+    header += "\", [";
+    for (int64_t d = 0; d < t.dim(); ++d) {
+      if (d) header += ", ";
+      header += std::to_string(t.size(d));
+    }
+    header += "], ";
+    header += std::to_string(off);
+    header += ", ";
+    header += std::to_string(nbytes);
+    header += "]}";
+  }
+
+  void node(py::handle o) {
+    PyObject* p = o.ptr();
+    if (THPVariable_Check(p)) {
+      tensor(THPVariable_Unpack(p));
+    } else if (PyDict_Check(p)) {
+      header += "{\"__d__\": [";
+      PyObject *k, *v;
+      Py_ssize_t pos = 0;
+      bool first = true;
+      while (PyDict_Next(p, &pos, &k, &v)) {
+        if (!first) header += ", ";
+        first = false;
+        header += "[";
+        if (PyUnicode_Check(k)) {
+          Py_ssize_t n = 0;
+          const char* s = PyUnicode_AsUTF8AndSize(k, &n);
+          if (!s) throw py::error_already_set();
+          json_string(header, s, static_cast<size_t>(n));
+        } else if (PyLong_Check(k) && !PyBool_Check(k)) {
+          header += py::str(k).cast<std::string>();   // [key, node] pairs keep int keys ints
+        } else {
+          throw py::type_error("tree_dumps: dict keys must be str or int");
+        }
+        header += ", ";
+        node(v);
+        header += "]";
+      }
+      header += "]}";
+    } else if (PyList_Check(p) || PyTuple_Check(p)) {
+      const bool is_list = PyList_Check(p);
+      header += is_list ? "{\"__l__\": [" : "{\"__tu__\": [";
+      const Py_ssize_t n = is_list ? PyList_GET_SIZE(p) : PyTuple_GET_SIZE(p);
+      for (Py_ssize_t i = 0; i < n; ++i) {
+        if (i) header += ", ";
+        node(is_list ? PyList_GET_ITEM(p, i) : PyTuple_GET_ITEM(p, i));
+      }
+      header += "]}";
+    } else if (p == Py_None || PyBool_Check(p) || PyLong_Check(p) || PyFloat_Check(p) || PyUnicode_Check(p)) {
+      scalar(o);
+    } else {
+      // numpy arrays / numpy scalars and anything else: the Python codec handles them
+      throw py::type_error("tree_dumps: unsupported leaf type");
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------------------- decode
+struct Decoder {
+  const char* s;
+  const char* end;
+  const uint8_t* body;
+  int64_t body_len;
+  bool copy;
+  py::object owner;    // keeps the source buffer alive for aliasing (copy=False) tensors
+
+  [[noreturn]] void fail(const char* what) const { throw py::value_error(std::string("tree_loads: ") + what); }
+
+  void ws() {
+    while (s < end && (*s == ' ' || *s == '\n' || *s == '\r' || *s == '\t')) ++s;
+  }
+  void expect(char c) {
+    ws();
+    if (s >= end || *s != c) fail("malformed header");
+    ++s;
+  }
+  bool peek(char c) {
+    ws();
+    return s < end && *s == c;
+  }
+
+  std::string str() {
+    expect('"');
+    std::string out;
+    while (s < end && *s != '"') {
+      char c = *s++;
+      if (c != '\\') {
+        out.push_back(c);
+        continue;
+      }
+      if (s >= end) fail("bad escape");
+      c = *s++;
+      switch (c) {
+        case '"': out.push_back('"'); break;
+        case '\\': out.push_back('\\'); break;
+        case '/': out.push_back('/'); break;
+        case 'b': out.push_back('\b'); break;
+        case 'f': out.push_back('\f'); break;
+        case 'n': out.push_back('\n'); break;
+        case 'r': out.push_back('\r'); break;
+        case 't': out.push_back('\t'); break;
+        case 'u': {
+          if (end - s < 4) fail("bad \\u escape");
+          unsigned cp = static_cast<unsigned>(std::stoul(std::string(s, 4), nullptr, 16));
+          s += 4;
+          if (cp >= 0xD800 && cp < 0xDC00 && end - s >= 6 && s[0] == '\\' && s[1] == 'u') {
+            const unsigned lo = static_cast<unsigned>(std::stoul(std::string(s + 2, 4), nullptr, 16));
+            s += 6;
+            cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+          }
+          if (cp < 0x80) {
+            out.push_back(static_cast<char>(cp));
+          } else if (cp < 0x800) {
+            out.push_back(static_cast<char>(0xC0 | (cp >> 6)));
+            out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+          } else if (cp < 0x10000) {
+            out.push_back(static_cast<char>(0xE0 | (cp >> 12)));
+            out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+            out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+          } else {
+            out.push_back(static_cast<char>(0xF0 | (cp >> 18)));
+            out.push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3F)));
+            out.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3F)));
+            out.push_back(static_cast<char>(0x80 | (cp & 0x3F)));
+          }
+          break;
+        }
+        default: fail("bad escape");
+      }
+    }
+    if (s >= end) fail("unterminated string");
+    ++s;
+    return out;
+  }
+
+  int64_t integer() {
+    ws();
+    char* e = nullptr;
+    const long long v = strtoll(s, &e, 10);
+    if (e == s) fail("expected an integer");
+    s = e;
+    return v;
+  }
+
+  py::object value() {   // JSON scalar -> Python object
+    ws();
+    if (s >= end) fail("truncated header");
+    if (*s == '"') return py::str(str());
+    if (!strncmp(s, "null", 4)) { s += 4; return py::none(); }
+    if (!strncmp(s, "true", 4)) { s += 4; return py::bool_(true); }
+    if (!strncmp(s, "false", 5)) { s += 5; return py::bool_(false); }
+    if (!strncmp(s, "NaN", 3)) { s += 3; return py::float_(std::nan("")); }
+    if (!strncmp(s, "Infinity", 8)) { s += 8; return py::float_(INFINITY); }
+    if (!strncmp(s, "-Infinity", 9)) { s += 9; return py::float_(-INFINITY); }
+    const char* st = s;
+    bool is_float = false;
+    if (*s == '-' || *s == '+') ++s;
+    while (s < end && ((*s >= '0' && *s <= '9') || *s == '.' || *s == 'e' || *s == 'E' || *s == '-' || *s == '+')) {
+      if (*s == '.' || *s == 'e' || *s == 'E') is_float = true;
+      ++s;
+    }
+    std::string num(st, s);
+    if (num.empty()) fail("bad value");
+    if (is_float) return py::float_(std::stod(num));
+    // arbitrary-size ints through Python
+    return py::reinterpret_steal<py::object>(PyLong_FromString(num.c_str(), nullptr, 10));
+  }
+
+  py::object tensor_node() {   // after "__t__":
+    expect('[');
+    at::ScalarType dt;
+    if (!dtype_from_code(str(), &dt)) fail("unknown dtype");
+    expect(',');
+    expect('[');
+    std::vector<int64_t> shape;
+    if (!peek(']')) {
+      shape.push_back(integer());
+      while (peek(',')) {
+        ++s;
+        shape.push_back(integer());
+      }
+    }
+    expect(']');
+    expect(',');
+    const int64_t off = integer();
+    expect(',');
+    const int64_t nbytes = integer();
+    expect(']');
+    const auto opts = at::TensorOptions().dtype(dt);
+    if (nbytes == 0) return py::reinterpret_steal<py::object>(THPVariable_Wrap(at::empty(shape, opts)));
+    if (off < 0 || off + nbytes > body_len) fail("tensor outside the body");
+    at::Tensor t;
+    if (copy) {
+      t = at::empty(shape, opts);
+      if (t.numel() * static_cast<int64_t>(t.element_size()) != nbytes) fail("tensor size mismatch");
+      std::memcpy(t.data_ptr(), body + off, static_cast<size_t>(nbytes));
+    } else {
+      py::object keep = owner;
+      auto* holder = new py::object(keep);
+      t = at::from_blob(const_cast<uint8_t*>(body + off), shape, [holder](void*) {
+            py::gil_scoped_acquire g;
+            delete holder;
+          }, opts);
+      if (t.numel() * static_cast<int64_t>(t.element_size()) != nbytes) fail("tensor size mismatch");
+    }
+    return py::reinterpret_steal<py::object>(THPVariable_Wrap(t));
+  }
+
+  py::object node() {
+    expect('{');
+    const std::string tag = str();
+    expect(':');
+    py::object out;
+    if (tag == "__t__") {
+      out = tensor_node();
+    } else if (tag == "__d__") {
+      py::dict d;
+      expect('[');
+      bool first = true;
+      while (!peek(']')) {
+        if (!first) expect(',');
+        first = false;
+        expect('[');
+        py::object k = peek('"') ? py::object(py::str(str())) : value();
+        expect(',');
+        d[k] = node();
+        expect(']');
+      }
+      expect(']');
+      out = d;
+    } else if (tag == "__l__" || tag == "__tu__") {
+      py::list l;
+      expect('[');
+      bool first = true;
+      while (!peek(']')) {
+        if (!first) expect(',');
+        first = false;
+        l.append(node());
+      }
+      expect(']');
+      out = tag == "__l__" ? py::object(l) : py::object(py::tuple(l));
+    } else if (tag == "__v__") {
+      out = value();
+    } else {
+      fail("unknown node tag");
+    }
+    expect('}');
+    return out;
+  }
+};
+
+py::bytes tree_dumps(py::handle tree) {
+  Encoder enc;
+  enc.header.reserve(8192);
+  enc.node(tree);
+  const int64_t hlen = static_cast<int64_t>(enc.header.size());
+  const int64_t pre = static_cast<int64_t>(kMagicLen) + 9;
+  const int64_t pad = (kAlign - (pre + hlen) % kAlign) % kAlign;
+  const int64_t total = pre + hlen + pad + enc.offset;
+  PyObject* out = PyBytes_FromStringAndSize(nullptr, static_cast<Py_ssize_t>(total));
+  if (!out) throw py::error_already_set();
+  char* dst = PyBytes_AS_STRING(out);
+  std::memcpy(dst, kMagic, kMagicLen);
+  const uint64_t hl = static_cast<uint64_t>(hlen);
+  std::memcpy(dst + kMagicLen, &hl, 8);   // little endian (x86 / the '<Q' of the Python codec)
+  dst[kMagicLen + 8] = 0;
+  std::memcpy(dst + pre, enc.header.data(), static_cast<size_t>(hlen));
+  char* body = dst + pre + hlen + pad;
+  std::memset(dst + pre + hlen, 0, static_cast<size_t>(pad));
+  {
+    py::gil_scoped_release nogil;   // the copies touch no Python object
+    int64_t cur = 0;
+    for (const auto& b : enc.blobs) {
+      if (b.first > cur) std::memset(body + cur, 0, static_cast<size_t>(b.first - cur));
+      const int64_t n = b.second.numel() * static_cast<int64_t>(b.second.element_size());
+      if (n) std::memcpy(body + b.first, b.second.data_ptr(), static_cast<size_t>(n));
+      cur = b.first + n;
+    }
+  }
+  return py::reinterpret_steal<py::bytes>(out);
+}
+
+py::object tree_loads(py::object data, bool copy) {
+  py::buffer buf = py::reinterpret_borrow<py::buffer>(data);
+  py::buffer_info info = buf.request();
+  const auto* p = static_cast<const uint8_t*>(info.ptr);
+  const int64_t n = static_cast<int64_t>(info.size * info.itemsize);
+  const int64_t pre = static_cast<int64_t>(kMagicLen) + 9;
+  if (n < pre || std::memcmp(p, kMagic, kMagicLen) != 0) throw py::value_error("not an applestar frame");
+  uint64_t hlen = 0;
+  std::memcpy(&hlen, p + kMagicLen, 8);
+  if (p[kMagicLen + 8] != 0) throw py::value_error("tree_loads: compressed frame (use the Python codec)");
+  if (pre + static_cast<int64_t>(hlen) > n) throw py::value_error("tree_loads: truncated frame");
+  const int64_t pad = (kAlign - (pre + static_cast<int64_t>(hlen)) % kAlign) % kAlign;
+  const int64_t body_start = pre + static_cast<int64_t>(hlen) + pad;
+  Decoder d;
+  d.s = reinterpret_cast<const char*>(p + pre);
+  d.end = d.s + hlen;
+  d.body = p + body_start;
+  d.body_len = n - body_start;
+  d.copy = copy;
+  d.owner = data;
+  return d.node();
+}
+
+}  // namespace
+
+void register_codec(py::module& m) {
+  m.def("tree_dumps", &tree_dumps, "tensor tree -> applestar frame (uncompressed)");
+  m.def("tree_loads", &tree_loads, py::arg("data"), py::arg("copy") = true,
+        "applestar frame -> tensor tree (copy=False: tensors alias the buffer)");
+}

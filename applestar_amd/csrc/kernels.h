@@ -244,11 +244,14 @@ void target_unit_sample(const void* e, int e_dt, const float* w1, const float* b
                         const void* key, int key_dt, int B, int N, const int64_t* lens, float inv_t, const float* u,
                         float* out_logits, int64_t* action, hipStream_t s);
 
-// ---- optim.hip: fused pytorch_norm clip + Adam over a (tensor, offset) chunk table ----------------------
+// ---- optim.hip: fused pytorch_norm / momentum_norm clip + Adam over a (tensor, offset) chunk table -------
 int fused_adam_chunk();
-// table: per tensor {p, g, m, v, numel, 0} (int64 x 6); chunks: per chunk {tensor, offset} (int64 x 2)
-void fused_clip_adam(const void* table, const long* chunks, int nchunks, float* part, const float* gate, float* norm_out,
-                     float max_norm, float lr_bc1, float b1, float b2, float inv_sqrt_bc2, float eps, float wd,
+// table: per tensor {p, g, m, v, numel, first chunk} (int64 x 6); chunks: per chunk {tensor, offset} (int64 x 2).
+// mom / scale (fp32 [ntensors]) non-null: momentum_norm clip with threshold max_norm; else pytorch_norm at
+// max_norm (0 = no clip).  hp (fp32 [3] = lr / bc1, 1 / sqrt(bc2), wd) non-null overrides those arguments.
+void fused_clip_adam(const void* table, const long* chunks, int nchunks, int ntensors, float* part,
+                     const float* gate, float* norm_out, float max_norm, float* mom, float* scale, int mom_init,
+                     const float* hp, float lr_bc1, float b1, float b2, float inv_sqrt_bc2, float eps, float wd,
                      int decoupled, hipStream_t s);
 
 // ---- wgrad.hip ---------------------------------------------------------------------------------

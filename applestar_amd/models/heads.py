@@ -41,10 +41,17 @@ def sample_from_logits(logits: torch.Tensor, u: Optional[torch.Tensor] = None, g
     return idx.clamp(max=p.shape[-1] - 1)
 
 
+def _capturing() -> bool:
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
 def _embed_table(module, lin):
     """lin.weight^T [n_in, n_out] contiguous (the one-hot -> fc row table of a head's embedding fc), cached per
-    weight version for the fused sampler."""
+    weight version for the fused sampler.  While a HIP graph is being captured the transpose is recorded in
+    the graph instead (a cached copy's address would be baked in and go stale after an in-place weight load)."""
     w = lin.weight
+    if _capturing():
+        return w.detach().t().contiguous()
     tag = (w.data_ptr(), w._version, w.dtype)
     cache = module.__dict__.setdefault('_table_cache', {})
     hit = cache.get(id(lin))
@@ -240,6 +247,9 @@ class SelectedUnitsHead(nn.Module):
     def _folded_query(self):
         """(Wq1 We2 [256,256] bf16, Wq1 be2 [256]) cached per weight version (pointer.hip fold)."""
         q1, e2 = self.query_fc1[0], self.embed_fc2[0]
+        if _capturing():      # recorded in the graph: replays see weights loaded in place later
+            wq1 = q1.weight.float()
+            return (wq1 @ e2.weight.float()).to(torch.bfloat16).contiguous(), wq1 @ e2.bias.float()
         tag = (q1.weight.data_ptr(), q1.weight._version, e2.weight.data_ptr(), e2.weight._version, e2.bias._version)
         if getattr(self, '_fold_tag', None) != tag:
             with torch.no_grad():

@@ -126,6 +126,17 @@ class MasterWeights:
             if not avg:
                 buf.div_(self.reducer.world)
 
+    def segments(self):
+        """(offset, numel) of every bf16 parameter inside the flat master, in master order (per-layer pieces
+        for per-tensor gradient clips such as momentum_norm)."""
+        out = []
+        for b, off, _ in self._slices:
+            o2 = off
+            for p in b.params:
+                out.append((o2, p.numel()))
+                o2 += p.numel()
+        return out
+
     def _master_grad_views(self):
         views = getattr(self, '_mg_views', None)
         if views is None:

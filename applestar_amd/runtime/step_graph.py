@@ -86,7 +86,8 @@ class GraphedTrainStep:
 
     * ``fwd_bwd(batch) -> Dict[str, 0-d tensor]``: forward, loss and backward into the gradient buffers;
     * ``reduce()``: the cross-rank gradient reduction (eager, between the graphs; no-op on one rank);
-    * ``update() -> 0-d tensor``: clip + optimizer + weight publish, returns the pre-clip gradient norm.
+    * ``update() -> 0-d tensor``: clip + optimizer + weight publish, returns the pre-clip gradient norm;
+    * ``pre_replay()`` (attribute, optional): the update's host work, run before every replay.
     """
 
     def __init__(self, fwd_bwd: Callable[[Dict], Dict[str, torch.Tensor]], reduce: Callable[[], None],
@@ -112,6 +113,9 @@ class GraphedTrainStep:
         # one private memory pool per graph instead of one shared pool (diagnostics)
         self.private_pools = os.environ.get('APPLESTAR_GRAPH_PRIVATE_POOLS', '0') == '1'
         self.after_replay: Optional[Callable[[_Entry], None]] = None    # diagnostics hook, before any host wait
+        # host work of the update that cannot live in a graph (optimizer step count, bias corrections uploaded
+        # to the device buffer the captured update reads): run before every replay
+        self.pre_replay: Optional[Callable[[], None]] = None
 
     def _eager(self, batch):
         info = self.fwd_bwd(batch)
@@ -139,6 +143,7 @@ class GraphedTrainStep:
                 e.keys = sorted(k for k, v in info.items() if torch.is_tensor(v) and v.numel() == 1)
                 e.packed = torch.stack([info[k].detach().float().reshape(()) for k in e.keys]) if e.keys else None
                 if self.single_graph:
+                    self.reduce()          # one rank: no collective, only the step's health gate
                     e.grad_norm = self.update().detach().float().reshape(())
         finally:
             encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED = flags
@@ -163,6 +168,8 @@ class GraphedTrainStep:
             self._graphs.move_to_end(key)
         t = self.host_time
         t0 = time.perf_counter()
+        if self.pre_replay is not None:
+            self.pre_replay()
         _tree_copy_(e.static_in, batch)
         t1 = time.perf_counter()
         e.fb.replay()

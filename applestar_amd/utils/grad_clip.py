@@ -65,8 +65,11 @@ class GradClip:
     @torch.no_grad()
     def apply(self, parameters: Iterable[torch.nn.Parameter], gate: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Clip in place and return the global norm.  ``gate``: an optional device scalar (1 = keep, 0 = drop
-        the whole step's gradient, e.g. a timed-out LSTM exchange), folded into the clip coefficient where
-        there is one; no host sync either way."""
+        the whole step's gradient, e.g. a timed-out LSTM exchange); no host sync either way.  A dropped step's
+        gradients are SELECTED away (``torch.where``), not multiplied by 0 - the gradients of a timed-out step
+        can be NaN - and the momentum EMA keeps its value.  (The optimizer step that follows still runs on zero
+        gradients: with the learners' default beta1 = 0 and no weight decay that leaves the weights unchanged;
+        the fused path, utils/fused_optim.py, skips the update altogether.)"""
         self.step += 1
         grads = _grads(list(parameters))
         if not grads:
@@ -76,9 +79,6 @@ class GradClip:
         t = self.clip_type
         if t in ('pytorch_norm', 'clip_norm'):
             coef = (self.threshold / (total + 1e-6)).clamp(max=1.0)
-            if gate is not None:
-                coef = coef * gate
-                gate = None
             torch._foreach_mul_(grads, coef)
         elif t == 'max_norm':
             bc1 = 1 - self.beta1 ** self.step
@@ -97,7 +97,10 @@ class GradClip:
                                     self.threshold * self.norm_mom / (g + 1e-6))
             torch._foreach_mul_(grads, list(scale.unbind()))
             new = g * scale
-            self.norm_mom = new.clone() if self.norm_mom is None else self.norm_mom * 0.99 + new * 0.01
+            mom = new.clone() if self.norm_mom is None else self.norm_mom * 0.99 + new * 0.01
+            if gate is not None and self.norm_mom is not None:
+                mom = torch.where(gate > 0, mom, self.norm_mom)
+            self.norm_mom = mom
             total = _global_norm(list(new.unbind()), self.norm_type)
         elif t == 'clip_value':
             bc2 = 1 - self.beta2 ** self.step
@@ -113,5 +116,7 @@ class GradClip:
             for g in grads:
                 g.clamp_(-self.threshold, self.threshold)
         if gate is not None:
-            torch._foreach_mul_(grads, gate)
+            keep = gate.reshape(()) > 0
+            for g in grads:
+                torch.where(keep, g, torch.zeros((), dtype=g.dtype, device=g.device), out=g)
         return total

@@ -10,7 +10,7 @@ from applestar_amd.rl.trainer import RLTrainer
 
 pytestmark = pytest.mark.gpu
 
-CFG = {'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}
+CFG = {'learner': {'use_value_feature': True, 'amp_dtype': 'bfloat16'}, 'model': {'enable_baselines': ['winloss']}}
 
 
 def test_multi_strided_copy_forms_match_torch():

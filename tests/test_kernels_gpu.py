@@ -1348,6 +1348,119 @@ def test_fused_clip_adam_matches_torch(max_norm, wd):
         assert float(oa.state[a]['step']) == float(ob.state[b]['step']) == 4.0
 
 
+@pytest.mark.parametrize('segmented', [False, True])
+def test_fused_momentum_norm_adam_matches_torch(segmented):
+    """optim.hip momentum_norm (per-tensor norm vs the EMA of past clipped norms, three launches) + Adam(0.9,
+    0.999, L2 decay) == GradClip('momentum_norm') + torch Adam over 5 steps.  ``segmented``: the same tensors as
+    pieces of ONE flat parameter (the bf16 learner's fp32 master), split back by the chunk table."""
+    from applestar_amd.utils.fused_optim import FusedClipAdam
+    from applestar_amd.utils.grad_clip import GradClip
+    torch.manual_seed(5)
+    shapes = [(64, 32, 3, 3), (100003,), (256,), (7, 5), (40000, 33)]
+    pa = [torch.nn.Parameter(torch.randn(*s, device=DEV)) for s in shapes]
+    for p in pa:
+        p.grad = torch.zeros_like(p)
+    n = [p.numel() for p in pa]
+    if segmented:
+        flat = torch.nn.Parameter(torch.cat([p.detach().reshape(-1) for p in pa]))
+        flat.grad = torch.zeros_like(flat)
+        pb = [flat]
+        offs = [sum(n[:i]) for i in range(len(n))]
+        segments = {flat: list(zip(offs, n))}
+    else:
+        pb = [torch.nn.Parameter(p.detach().clone()) for p in pa]
+        for p in pb:
+            p.grad = torch.zeros_like(p)
+        segments = None
+    oa = torch.optim.Adam(pa, lr=1e-3, weight_decay=1e-5)
+    ob = torch.optim.Adam(pb, lr=1e-3, weight_decay=1e-5)
+    ca, cb = GradClip('momentum_norm', 1.0), GradClip('momentum_norm', 1.0)
+    fused = FusedClipAdam(ob, None, clip=cb, segments=segments)
+    for step in range(5):
+        gs = [torch.randn_like(a) * (1 + 3 * (step % 2)) for a in pa]     # alternating scale: the clip engages
+        for a, g in zip(pa, gs):
+            a.grad.copy_(g)
+        if segmented:
+            pb[0].grad.copy_(torch.cat([g.reshape(-1) for g in gs]))
+        else:
+            for b, g in zip(pb, gs):
+                b.grad.copy_(g)
+        na = ca.apply(pa)
+        oa.step()
+        nb = fused.step()
+        assert abs(float(na) - float(nb)) <= 1e-5 * float(na), step
+        assert torch.allclose(ca.norm_mom, cb.norm_mom, rtol=1e-5), step
+        got = pb[0].detach().split(n) if segmented else [b.detach().reshape(-1) for b in pb]
+        for a, b in zip(pa, got):
+            assert _err(a.detach().reshape(-1), b) < 1e-6 * max(1.0, a.abs().max().item()), step
+
+
+@pytest.mark.parametrize('clip_type', ['pytorch_norm', 'momentum_norm'])
+def test_fused_adam_gate_skips_update(clip_type):
+    """A zero health gate (timed-out LSTM exchange) with NaN gradients leaves the parameters, both Adam moments
+    and the momentum EMA bit-identical; the next step with the gate open updates normally."""
+    from applestar_amd.utils.fused_optim import FusedClipAdam
+    from applestar_amd.utils.grad_clip import GradClip
+    torch.manual_seed(6)
+    ps = [torch.nn.Parameter(torch.randn(*s, device=DEV)) for s in [(300, 17), (70001,)]]
+    for p in ps:
+        p.grad = torch.randn_like(p)
+    opt = torch.optim.Adam(ps, lr=1e-3, betas=(0.5, 0.99), weight_decay=1e-4)
+    clip = GradClip(clip_type, 1.0)
+    fused = FusedClipAdam(opt, 1.0 if clip_type == 'pytorch_norm' else None, clip=clip)
+    fused.step(torch.ones((), device=DEV))                                # state exists, EMA initialised
+    snap = [t.clone() for p in ps for t in (p.detach(), opt.state[p]['exp_avg'], opt.state[p]['exp_avg_sq'])]
+    mom = clip.norm_mom.clone() if clip.norm_mom is not None else None
+    for p in ps:
+        p.grad.fill_(float('nan'))
+    fused.step(torch.zeros((), device=DEV))
+    torch.cuda.synchronize()
+    now = [t for p in ps for t in (p.detach(), opt.state[p]['exp_avg'], opt.state[p]['exp_avg_sq'])]
+    assert all(torch.equal(a, b) for a, b in zip(snap, now))
+    if mom is not None:
+        assert torch.equal(mom, clip.norm_mom)
+    for p in ps:
+        p.grad.copy_(torch.randn_like(p))
+    fused.step(torch.ones((), device=DEV))
+    assert all(torch.isfinite(p).all() and not torch.equal(p.detach(), s) for p, s in zip(ps, snap[::3]))
+
+
+def test_fused_adam_device_hparams_in_graph():
+    """The update captured in a HIP graph reads lr / bias corrections from the device buffer that prepare()
+    refreshes before each replay: 4 replays == 4 eager fused steps."""
+    from applestar_amd.utils.fused_optim import FusedClipAdam
+    torch.manual_seed(8)
+    shapes = [(513, 9), (4096,)]
+    pa = [torch.nn.Parameter(torch.randn(*s, device=DEV)) for s in shapes]
+    pb = [torch.nn.Parameter(p.detach().clone()) for p in pa]
+    for p in pa + pb:
+        p.grad = torch.zeros_like(p)
+    oa = torch.optim.Adam(pa, lr=1e-2, betas=(0.0, 0.99), eps=1e-5)
+    ob = torch.optim.Adam(pb, lr=1e-2, betas=(0.0, 0.99), eps=1e-5)
+    fa, fb = FusedClipAdam(oa, 1.0), FusedClipAdam(ob, 1.0, device_hparams=True)
+    grads = [[torch.randn_like(p) for p in pa] for _ in range(5)]
+
+    def load(ps, i):
+        for p, g in zip(ps, grads[i]):
+            p.grad.copy_(g)
+    load(pa, 0); fa.step()
+    load(pb, 0); fb.step()                 # eager first step (creates the state)
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            fb.step()
+    torch.cuda.current_stream().wait_stream(s)
+    for i in range(1, 5):
+        load(pa, i); fa.step()
+        load(pb, i); fb.prepare(); g.replay()
+    torch.cuda.synchronize()
+    for a, b in zip(pa, pb):
+        assert torch.equal(a.detach(), b.detach())
+    assert float(ob.state[pb[0]]['step']) == 5.0
+
+
 @pytest.mark.parametrize('M,Nc,K', [(5000, 768, 256), (3001, 256, 1024), (20000, 32, 20), (2500, 96, 132)])
 @pytest.mark.parametrize('mode', ['bias_relu', 'res_add', 'drelu'])
 def test_gemm_f32_epilogues_match_fp64(M, Nc, K, mode, f32_mfma):

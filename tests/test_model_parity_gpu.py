@@ -23,7 +23,7 @@ from applestar_amd.rl.synthetic import rl_batch, to_device
 from applestar_amd.rl.trainer import RLTrainer
 
 pytestmark = pytest.mark.gpu
-CFG = {'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}
+CFG = {'learner': {'use_value_feature': True, 'amp_dtype': 'bfloat16'}, 'model': {'enable_baselines': ['winloss']}}
 HEADS = ['action_type', 'delay', 'queued', 'selected_units', 'target_unit', 'target_location']
 OUT_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'gpurun_out')
 

@@ -1,0 +1,80 @@
+"""utils/serialize.py frames: the native codec (csrc/codec.cpp) and the Python codec produce and read the same
+frames (byte-identical encodes, cross-decodes), for every supported dtype and leaf kind."""
+import math
+
+import pytest
+import torch
+
+from applestar_amd.utils import serialize
+
+NATIVE = serialize._native()
+needs_native = pytest.mark.skipif(not NATIVE, reason='native extension not built')
+
+
+def _tree():
+    g = torch.Generator().manual_seed(0)
+    t = {
+        'f32': torch.randn(3, 5, generator=g), 'f16': torch.randn(7, generator=g).half(),
+        'bf16': torch.randn(2, 2, generator=g).bfloat16(), 'f64': torch.randn(4, generator=g).double(),
+        'i64': torch.arange(9).view(3, 3), 'i32': torch.arange(5, dtype=torch.int32),
+        'i16': torch.tensor([-3, 7], dtype=torch.int16), 'i8': torch.tensor([-1, 2], dtype=torch.int8),
+        'u8': torch.tensor([0, 255], dtype=torch.uint8), 'b': torch.tensor([True, False, True]),
+        'empty': torch.zeros(0, 4), 'scalar_t': torch.tensor(3.5), 'noncontig': torch.randn(4, 6, generator=g).t(),
+        'nested': {'l': [torch.ones(2), 1, 2.5, None, True, 'x"y\\z\né\U0001F600'],
+                   'tu': (torch.zeros(1, dtype=torch.long), -7, 2 ** 70, float('inf'), -float('inf'), 1.0, 1e-300)},
+        7: 'int key', 'nan': float('nan'),
+    }
+    return t
+
+
+def _eq(a, b):
+    if torch.is_tensor(a):
+        assert torch.is_tensor(b) and a.dtype == b.dtype and a.shape == b.shape
+        assert torch.equal(a.contiguous().view(-1).view(torch.uint8) if a.dtype != torch.bool else a,
+                           b.contiguous().view(-1).view(torch.uint8) if b.dtype != torch.bool else b)
+    elif isinstance(a, dict):
+        assert sorted(map(str, a)) == sorted(map(str, b))
+        for k in a:
+            _eq(a[k], b[str(k)] if str(k) in b else b[k])
+    elif isinstance(a, (list, tuple)):
+        assert type(a) == type(b) and len(a) == len(b)
+        for x, y in zip(a, b):
+            _eq(x, y)
+    elif isinstance(a, float) and math.isnan(a):
+        assert isinstance(b, float) and math.isnan(b)
+    else:
+        assert a == b and type(a) == type(b), (a, b)
+
+
+def test_python_codec_roundtrip():
+    t = _tree()
+    _eq(t, serialize.loads_py(serialize.dumps_py(t)))
+
+
+@needs_native
+def test_native_matches_python_codec():
+    t = _tree()
+    nat = NATIVE.tree_dumps(t)
+    py = serialize.dumps_py(t)
+    assert nat == py                                    # same header text and body layout
+    _eq(t, NATIVE.tree_loads(py, True))
+    _eq(t, serialize.loads_py(nat))
+    _eq(t, serialize.loads(nat))
+
+
+@needs_native
+def test_native_alias_mode_and_fallback():
+    t = {'a': torch.arange(10, dtype=torch.float32), 'b': [torch.ones(3, dtype=torch.int16)]}
+    buf = bytearray(serialize.dumps(t))
+    out = serialize.loads(buf, copy=False)
+    _eq(t, out)
+    del buf
+    assert out['a'].sum().item() == 45.0               # the aliased tensors keep the buffer alive
+    import numpy as np
+    mixed = {'np': np.arange(4), 'npf': np.float32(2.5)}   # numpy leaves: the Python encoder takes over
+    back = serialize.loads(serialize.dumps(mixed))
+    assert torch.equal(back['np'], torch.arange(4)) and back['npf'] == 2.5
+    with pytest.raises(ValueError):
+        serialize.loads(b'NOTAFRAME' + bytes(20))
+    z = serialize.dumps(t, compress=True)               # compressed frames stay on the Python codec
+    _eq(t, serialize.loads(z))
