@@ -226,8 +226,8 @@ def _worker_main(cfg_dict, job, env_id, req_conns, ctrl, result_q, coord):
     clients = None
     if req_conns is not None:
         clients = {}
-        for (pid, kind), conn in req_conns.items():
-            clients[(pid, kind)] = InferenceClient(conn, pid, kind)
+        for (pid, key_kind), (conn, kind, tkey) in req_conns.items():
+            clients[(pid, key_kind)] = InferenceClient(conn, pid, kind, teacher_id=tkey)
     adapter = None
     if coord is not None and cfg.actor.job_type == 'train':
         from ..comm.adapter import Adapter
@@ -304,17 +304,20 @@ class Actor:
         for env_id in range(self._cfg.env_num):
             req = None
             if gpu:
+                # one pipe per (player, kind): a training agent's policy sample and its teacher's logits for that
+                # action are ONE request ('policy+teacher', served by one graph); eval agents ask the policy only
                 req = {}
                 for idx, pid in enumerate(job['player_ids']):
                     if 'bot' in job['pipelines'][idx]:
                         continue
                     tid = job['teacher_player_ids'][idx]
-                    for key in ((pid, 'policy'), (tid if tid != 'none' else pid, 'teacher')):
-                        if key in req or (key[1] == 'teacher' and 'train' not in self._job_type):
-                            continue
-                        parent, child = ctx.Pipe()
-                        self._server.add_connection(parent)
-                        req[key] = child
+                    tkey = tid if tid != 'none' else pid
+                    kind = 'policy+teacher' if 'train' in self._job_type else 'policy'
+                    if (pid, 'policy') in req:
+                        continue
+                    parent, child = ctx.Pipe()
+                    self._server.add_connection(parent, route=(pid, kind, tkey if kind != 'policy' else None))
+                    req[(pid, 'policy')] = (child, kind, tkey)
             p_ctrl, c_ctrl = ctx.Pipe()
             p = ctx.Process(target=_worker_main, daemon=True,
                             args=(dict(self._whole_cfg), job, env_id, req, c_ctrl, self._result_q, coord))

@@ -2,33 +2,40 @@
 
 Reference (``agent.py:145-158,364-385,781-805``, ``actor.py:268-299``): every env process writes its
 observation into a shared-memory slot and bumps a signal; a GPU loop runs ``compute_logp_action`` on
-*all* slots (active or not) and copies flagged rows back; env processes poll with ``sleep(0.01)``.
+*all* slots (active or not) and copies flagged rows back; env processes poll with ``sleep(0.01)``; the teacher
+forward of ``collect_data`` is a second, separate model call per agent step.
 
 MI355X design:
 * one server per GPU owns every model (policy per player, teacher per player) on the device;
-* env workers send one serialized request (``utils.serialize``: one buffer, no pickling) over a
-  pipe and block on the reply — no polling;
-* dynamic batching: the server waits on all pipes (``connection.wait``), then keeps collecting until
-  either every live worker has a request queued or ``max_wait_ms`` passed, and runs ONE forward per
-  (player, kind) group over only the rows that asked — padded to the group's max entity count;
-* the batched input is packed into ONE pinned host buffer and copied with one ``non_blocking`` DMA
-  (``runtime.prefetch.pack_tree``); the outputs come back with non-blocking D2H copies and a single stream
-  synchronize per group (per-tensor blocking copies cost a host round trip each);
-* on the GPU each (player, kind, power-of-two batch bucket) is a HIP graph (``runtime.graphs.GraphedPolicy``,
-  entities padded to MAX_ENTITY_NUM): B = 1 agent step 8.7 ms eager -> 3.1 ms replayed.
+* env workers send one request frame (``utils.serialize``, native codec) over a pipe and block on the reply -
+  no polling.  Each pipe is bound to a ROUTE ``(player, kind, teacher)`` when it is registered, so the server
+  never decodes a request on its own: B frames go straight into ``collate_frames`` (csrc/codec.cpp), which
+  lays the collated batch out in ONE pinned staging buffer (entities padded to the batch's entity BUCKET,
+  128 / 256 / 512) that is copied with one H2D DMA;
+* ``kind='policy+teacher'`` serves a training agent's step in ONE request: the policy samples the action and
+  the teacher's teacher-forced logits for that very action are computed in the same HIP graph (the
+  reference's two round trips per agent step become one; ``agent.py`` caches the teacher half for
+  ``collect_data``);
+* every (route, batch bucket, entity bucket) is a captured HIP graph (``runtime.graphs.GraphedPolicy``);
+* two-stage pipeline: a batch is LAUNCHED (H2D, replay, async D2H into pinned memory, event) and FINISHED
+  (event wait, per-row replies) on the next loop turn, after the next batch was collected and launched -
+  the host work of batch k+1 overlaps the GPU work of batch k, and replies go out as soon as the event fired.
 """
 from __future__ import annotations
 
 import threading
 import time
-from collections import defaultdict
+from collections import defaultdict, deque
 from multiprocessing.connection import Connection, wait
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
 from ..agent.collate import collate_obs, decollate_output
 from ..utils import serialize
+
+ENTITY_BUCKETS = (128, 256, 512)
+POLICY_TEACHER = 'policy+teacher'
 
 
 def _to(tree, device, non_blocking=True):
@@ -44,35 +51,70 @@ def _to(tree, device, non_blocking=True):
 
 
 class InferenceClient:
-    """Worker-side handle: ``infer(model_input) -> per-sample output`` (blocking)."""
+    """Worker-side handle: ``infer(model_input) -> per-sample output`` (blocking).  The connection is bound to
+    its route on the server side (``InferenceServer.add_connection(conn, route)``), so a request is the bare
+    model input; routes registered without a key get the self-describing envelope."""
 
-    def __init__(self, conn: Connection, player_id: str, kind: str = 'policy'):
+    def __init__(self, conn: Connection, player_id: str, kind: str = 'policy', teacher_id: Optional[str] = None,
+                 routed: bool = True):
         self._conn = conn
         self.player_id = player_id
         self.kind = kind
+        self.teacher_id = teacher_id
+        self.routed = routed
 
     def infer(self, model_input: Dict) -> Dict:
-        self._conn.send_bytes(serialize.dumps({'player_id': self.player_id, 'kind': self.kind, 'input': model_input}))
+        if self.routed:
+            self._conn.send_bytes(serialize.dumps(model_input))
+        else:
+            self._conn.send_bytes(serialize.dumps({'player_id': self.player_id, 'kind': self.kind,
+                                                   'teacher_id': self.teacher_id, 'input': model_input}))
         return serialize.loads(self._conn.recv_bytes())
+
+
+class _PolicyTeacher(torch.nn.Module):
+    """One agent step of a training actor: policy sample + the teacher's logits for the sampled action
+    (``compute_logp_action`` then ``compute_teacher_logit`` with the teacher's own LSTM state)."""
+
+    def __init__(self, policy, teacher):
+        super().__init__()
+        self.policy, self.teacher = policy, teacher
+
+    def step(self, spatial_info, entity_info, scalar_info, entity_num, hidden_state, teacher_hidden_state,
+             noise=None, **kwargs):
+        out = self.policy.compute_logp_action(spatial_info, entity_info, scalar_info, entity_num, hidden_state,
+                                              noise=noise)
+        t = self.teacher.compute_teacher_logit(spatial_info, entity_info, scalar_info, entity_num,
+                                               teacher_hidden_state, out['selected_units_num'], out['action_info'])
+        out['teacher'] = {'logit': t['logit'], 'hidden_state': t['hidden_state']}
+        return out
+
+
+class _Launched:
+    __slots__ = ('conns', 'n', 'out', 'event', 'route', 'keep_logits', 't0')
 
 
 class InferenceServer:
     def __init__(self, device='cuda', max_wait_ms: float = 2.0, amp_dtype: Optional[torch.dtype] = torch.bfloat16,
-                 use_graphs: Optional[bool] = None):
+                 use_graphs: Optional[bool] = None, entity_buckets=ENTITY_BUCKETS, max_batch: int = 64):
         self.device = torch.device(device)
-        # HIP-graph replay per (player, kind, batch bucket): entities padded to MAX_ENTITY_NUM and the batch
-        # to the next power of two, so a handful of captured graphs serve every request
+        # HIP-graph replay per (route, batch bucket, entity bucket); a handful of captured graphs serve every request
         self.use_graphs = (self.device.type == 'cuda' and amp_dtype == torch.bfloat16) if use_graphs is None \
             else bool(use_graphs)
+        self.entity_buckets = tuple(sorted(entity_buckets))
+        self.max_batch = int(max_batch)
         self._graphed: Dict[tuple, object] = {}
+        self._runners: Dict[tuple, torch.nn.Module] = {}
         self.max_wait = max_wait_ms / 1000.0
         self.amp_dtype = amp_dtype if self.device.type == 'cuda' else None
         self.models: Dict[str, torch.nn.Module] = {}
         self.teachers: Dict[str, torch.nn.Module] = {}
         self.model_iter: Dict[str, int] = defaultdict(int)
         self._conns: List[Connection] = []
+        self._routes: Dict[Connection, Optional[tuple]] = {}
         self._lock = threading.Lock()
         self._stop = False
+        self._inflight: deque = deque()
         self.stats = defaultdict(float)
 
     # ------------------------------------------------------------------ models
@@ -80,11 +122,13 @@ class InferenceServer:
         model = model.to(self.device).eval()
         with self._lock:
             (self.teachers if teacher else self.models)[player_id] = model
-            kind = 'teacher' if teacher else 'policy'
-            self._graphed = {k: v for k, v in self._graphed.items() if k[:2] != (player_id, kind)}
+            self._graphed = {k: v for k, v in self._graphed.items() if player_id not in k[0][::2]}
+            self._runners = {k: v for k, v in self._runners.items() if player_id not in k[::2]}
 
     def load_state_dict(self, player_id: str, state_dict: Dict, teacher: bool = False, last_iter: int = 0):
-        """Hot model update (weights pulled from the learner) without rebuilding the module."""
+        """Hot model update (weights pulled from the learner) without rebuilding the module.  Captured graphs
+        stay valid: they read the parameters in place and recompute every weight-derived table inside the graph
+        (models/heads.py ``_capturing``)."""
         with self._lock:
             m = (self.teachers if teacher else self.models)[player_id]
             own = m.state_dict()
@@ -95,68 +139,141 @@ class InferenceServer:
             if not teacher:
                 self.model_iter[player_id] = int(last_iter)
 
-    def add_connection(self, conn: Connection):
+    def add_connection(self, conn: Connection, route: Optional[Tuple[str, str, Optional[str]]] = None):
+        """``route`` = (player_id, kind, teacher_id): requests on ``conn`` are bare model inputs for that route
+        (kind 'policy', 'teacher' or 'policy+teacher'); None: self-describing envelopes."""
         with self._lock:
             self._conns.append(conn)
+            self._routes[conn] = tuple(route) if route is not None else None
 
-    # ------------------------------------------------------------------ serving
-    def _forward(self, player_id: str, kind: str, inputs: List[Dict]) -> List[Dict]:
+    # ------------------------------------------------------------------ execution
+    def _runner(self, route) -> Tuple[torch.nn.Module, str]:
+        pid, kind, tid = route
         with self._lock:
-            model = self.models[player_id] if kind == 'policy' else self.teachers[player_id]
-        if self.use_graphs:
-            from ..lib.features import MAX_ENTITY_NUM
+            if kind == 'policy':
+                return self.models[pid], 'compute_logp_action'
+            if kind == 'teacher':
+                return self.teachers[pid], 'compute_teacher_logit'
+            r = self._runners.get(route)
+            if r is None:
+                r = self._runners[route] = _PolicyTeacher(self.models[pid], self.teachers[tid or pid])
+            return r, 'step'
+
+    def _bucket(self, n: int) -> int:
+        for b in self.entity_buckets:
+            if b >= n:
+                return b
+        return n
+
+    def _collate(self, frames: List[bytes], inputs: Optional[List[Dict]], rows: int, graphs: bool):
+        """Device batch of ``rows`` samples (dummy copies of sample 0 pad a graph's batch bucket)."""
+        from ..ops import _ext
+        nat = _ext._load()
+        if frames is not None and nat is not None and hasattr(nat, 'collate_frames'):
+            fr = list(frames) + [frames[0]] * (rows - len(frames))
+            dev = self.device if self.device.type == 'cuda' else None
+            return nat.collate_frames(fr, 0, None if dev is None else str(dev),
+                                      list(self.entity_buckets) if graphs else [])
+        if inputs is None:
+            inputs = [serialize.loads(f) for f in frames]
+        inputs = list(inputs) + [inputs[0]] * (rows - len(inputs))
+        pad = self._bucket(max(int(o['entity_num']) for o in inputs)) if graphs else 0
+        batch = collate_obs(inputs, pad_entities=pad)
+        return _packed_to(batch, self.device)
+
+    def _launch(self, route, frames=None, inputs=None, keep_logits: bool = False) -> _Launched:
+        t0 = time.perf_counter()
+        model, method = self._runner(route)
+        n = len(frames) if frames is not None else len(inputs)
+        graphs = self.use_graphs
+        rows = 1 << (n - 1).bit_length() if graphs else n            # batch bucket (power of two)
+        batch = self._collate(frames, inputs, rows, graphs)
+        t1 = time.perf_counter()
+        self.stats['collate_h2d_s'] += t1 - t0
+        if graphs:
             from ..runtime.graphs import GraphedPolicy
-            bp = 1 << (len(inputs) - 1).bit_length()                   # batch bucket (power of two)
-            rows = list(inputs) + [inputs[0]] * (bp - len(inputs))      # dummy rows, never returned
-            t0 = time.perf_counter()
-            batch = _packed_to(collate_obs(rows, pad_entities=MAX_ENTITY_NUM), self.device)
-            self.stats['collate_h2d_s'] += time.perf_counter() - t0
-            key = (player_id, kind, bp)
+            key = (route, rows, batch['entity_info']['unit_type'].shape[-1])
             gp = self._graphed.get(key)
             if gp is None:
-                gp = self._graphed[key] = GraphedPolicy(
-                    model, 'compute_logp_action' if kind == 'policy' else 'compute_teacher_logit')
-            t0 = time.perf_counter()
+                gp = self._graphed[key] = GraphedPolicy(model, method, max_graphs=1)
             out = gp(**batch)
-            self.stats['launch_s'] += time.perf_counter() - t0
         else:
-            batch = _to(collate_obs(inputs), self.device)
             ctx = torch.autocast('cuda', dtype=self.amp_dtype) if self.amp_dtype else _null()
             with torch.no_grad(), ctx:
-                out = model.compute_logp_action(**batch) if kind == 'policy' else model.compute_teacher_logit(**batch)
+                out = getattr(model, method)(**batch)
+        self.stats['launch_s'] += time.perf_counter() - t1
+        if not keep_logits and route[1] != 'teacher':
+            out = {k: v for k, v in out.items() if k != 'logit'}     # the agent keeps only the taken action's logp
+        L = _Launched()
+        L.n, L.route, L.keep_logits, L.t0 = n, route, keep_logits, t0
+        L.out = _to_cpu_async(out)        # pinned, non_blocking: copied before the next replay overwrites them
+        L.event = None
+        if self.device.type == 'cuda':
+            L.event = torch.cuda.Event()
+            L.event.record()
+        return L
+
+    def _results(self, L: _Launched) -> List[Dict]:
         t0 = time.perf_counter()
-        out = _to_cpu(out, self.device)          # copies the (graph-static) outputs before the next replay
-        self.stats['d2h_wait_s'] += time.perf_counter() - t0
-        t0 = time.perf_counter()
-        res = [decollate_output(out, i) for i in range(len(inputs))]
-        self.stats['decollate_s'] += time.perf_counter() - t0
-        if kind == 'policy':
+        if L.event is not None:
+            L.event.synchronize()
+        t1 = time.perf_counter()
+        self.stats['d2h_wait_s'] += t1 - t0
+        out = L.out
+        teacher = out.pop('teacher', None)
+        res = [decollate_output(out, i) for i in range(L.n)]
+        if teacher is not None:
+            t = dict(teacher, entity_num=out['entity_num'], selected_units_num=out['selected_units_num'])
+            for i, r in enumerate(res):
+                td = decollate_output(t, i)
+                r['teacher'] = {'logit': td['logit'], 'hidden_state': td['hidden_state']}
+        pid, kind, _ = L.route
+        if kind != 'teacher':
             for r in res:
-                r['model_last_iter'] = self.model_iter[player_id]
+                r['model_last_iter'] = self.model_iter[pid]
+        self.stats['decollate_s'] += time.perf_counter() - t1
         return res
 
-    def serve_once(self, timeout: float = 0.1) -> int:
-        """Collect one dynamic batch and answer it; returns the number of requests served."""
+    def _forward(self, player_id: str, kind: str, inputs: List[Dict], teacher_id: Optional[str] = None) -> List[Dict]:
+        """Synchronous batch of decoded inputs (tests / in-process callers); replies keep the policy logits."""
+        return self._results(self._launch((player_id, kind, teacher_id), inputs=inputs, keep_logits=True))
+
+    # ------------------------------------------------------------------ serving
+    def _finish(self, L: _Launched):
+        res = self._results(L)
+        t0 = time.perf_counter()
+        for c, o in zip(L.conns, res):
+            try:
+                c.send_bytes(serialize.dumps(o))
+            except (BrokenPipeError, OSError):
+                pass
+        self.stats['reply_s'] += time.perf_counter() - t0
+        self.stats['served_s'] += time.perf_counter() - L.t0
+
+    def _collect(self, timeout: float) -> Dict[tuple, List[Tuple[Connection, bytes]]]:
         with self._lock:
             conns = list(self._conns)
+        groups: Dict[tuple, List] = defaultdict(list)
         if not conns:
-            time.sleep(timeout)
-            return 0
+            if timeout > 0:
+                time.sleep(timeout)
+            return groups
         ready = wait(conns, timeout=timeout)
         if not ready:
-            return 0
-        pending: Dict[Connection, Dict] = {}
-        deadline = time.time() + self.max_wait
+            return groups
+        pending: Dict[Connection, bytes] = {}
+        deadline = time.time() + (self.max_wait if timeout > 0 else 0.0)
         while True:
             for c in ready:
                 if c in pending:
                     continue
                 try:
-                    pending[c] = serialize.loads(c.recv_bytes())
+                    pending[c] = c.recv_bytes()
                 except (EOFError, OSError):
                     with self._lock:
                         if c in self._conns:
                             self._conns.remove(c)
+                            self._routes.pop(c, None)
             live = len(self._conns)
             left = deadline - time.time()
             if len(pending) >= live or left <= 0:
@@ -164,25 +281,43 @@ class InferenceServer:
             ready = [c for c in wait([c for c in conns if c not in pending and c in self._conns], timeout=left)]
             if not ready:
                 break
-        groups = defaultdict(list)
-        for c, req in pending.items():
-            groups[(req['player_id'], req['kind'])].append((c, req['input']))
-        t0 = time.time()
-        for (pid, kind), items in groups.items():
-            outs = self._forward(pid, kind, [x for _, x in items])
-            for (c, _), o in zip(items, outs):
-                try:
-                    c.send_bytes(serialize.dumps(o))
-                except (BrokenPipeError, OSError):
-                    pass
-        self.stats['batches'] += len(groups)
-        self.stats['requests'] += len(pending)
-        self.stats['forward_s'] += time.time() - t0
-        return len(pending)
+        for c, frame in pending.items():
+            route = self._routes.get(c)
+            if route is None:                       # envelope: decode to find the route
+                req = serialize.loads(frame)
+                route = (req['player_id'], req['kind'], req.get('teacher_id'))
+                frame = serialize.dumps(req['input'])
+            groups[route].append((c, frame))
+        return groups
+
+    def serve_once(self, timeout: float = 0.1) -> int:
+        """Collect one dynamic batch per route and launch it; finish (reply to) the batches launched on the
+        previous call.  Returns the number of requests launched."""
+        groups = self._collect(0.0 if self._inflight else timeout)
+        prev = list(self._inflight)
+        self._inflight.clear()
+        served = 0
+        for route, items in groups.items():
+            for s in range(0, len(items), self.max_batch):
+                chunk = items[s:s + self.max_batch]
+                L = self._launch(route, frames=[f for _, f in chunk])
+                L.conns = [c for c, _ in chunk]
+                self._inflight.append(L)
+                self.stats['batches'] += 1
+                served += len(chunk)
+        for L in prev:
+            self._finish(L)
+        self.stats['requests'] += served
+        return served
+
+    def drain(self):
+        while self._inflight:
+            self._finish(self._inflight.popleft())
 
     def serve_forever(self, stop_event: Optional[threading.Event] = None):
         while not self._stop and not (stop_event is not None and stop_event.is_set()):
             self.serve_once()
+        self.drain()
 
     def stop(self):
         self._stop = True
@@ -204,17 +339,20 @@ def _packed_to(batch, device):
     return pack_tree(batch, pin=True).to_device(device)
 
 
+def _to_cpu_async(tree):
+    """Device outputs -> pinned host tensors with non_blocking copies (the caller waits on an event)."""
+    if isinstance(tree, torch.Tensor):
+        return tree.detach().to('cpu', non_blocking=tree.is_cuda)
+    if isinstance(tree, dict):
+        return {k: _to_cpu_async(v) for k, v in tree.items()}
+    if isinstance(tree, (list, tuple)):
+        return type(tree)(_to_cpu_async(v) for v in tree)
+    return tree
+
+
 def _to_cpu(tree, device=None):
     """Device outputs -> host: every copy non-blocking into pinned memory, then ONE stream synchronize."""
-    def issue(x):
-        if isinstance(x, torch.Tensor):
-            return x.detach().to('cpu', non_blocking=x.is_cuda)
-        if isinstance(x, dict):
-            return {k: issue(v) for k, v in x.items()}
-        if isinstance(x, (list, tuple)):
-            return type(x)(issue(v) for v in x)
-        return x
-    out = issue(tree)
+    out = _to_cpu_async(tree)
     if device is not None and device.type == 'cuda':
         torch.cuda.current_stream(device).synchronize()
     return out

@@ -81,6 +81,10 @@ class Agent:
         self._player_id = None
         self._client = inference_client
         self._teacher_client = teacher_client
+        # 'policy+teacher' client: the server returns the teacher's logits for the sampled action with the policy
+        # reply (one round trip per agent step); collect_data then uses the cached half
+        self._merged = inference_client is not None and getattr(inference_client, 'kind', '') == 'policy+teacher'
+        self._teacher_out = None
         self.z_idx = None
         if model is None and inference_client is None:
             from ..models.model import Model
@@ -91,7 +95,7 @@ class Agent:
             if self._use_cuda:
                 self.model.cuda()
         self.teacher_model = teacher_model
-        if 'train' in self._job_type and teacher_model is None and teacher_client is None:
+        if 'train' in self._job_type and teacher_model is None and teacher_client is None and not self._merged:
             from ..models.model import Model
             self.teacher_model = Model(c).eval()
         self.successive_model = None
@@ -278,7 +282,11 @@ class Agent:
         self._stat_api.update(int(self._last_action_type), observation['action_result'][0], self._observation,
                               self._game_step)
         if self._client is not None:
-            out = self._client.infer(self._model_input(agent_obs))
+            req = self._model_input(agent_obs)
+            if self._merged:
+                req['teacher_hidden_state'] = self._teacher_hidden_state
+            out = self._client.infer(req)
+            self._teacher_out = out.pop('teacher', None)
             self._model_last_iter = int(out.pop('model_last_iter', self._model_last_iter))
         else:
             batch = collate_obs([self._model_input(agent_obs)])
@@ -375,7 +383,9 @@ class Agent:
                       'hidden_state': self._teacher_hidden_state,
                       'selected_units_num': self._output['selected_units_num'],
                       'action_info': self._output['action_info']}
-        if self._teacher_client is not None:
+        if self._teacher_out is not None:        # computed with the policy step (merged request)
+            t_out, self._teacher_out = self._teacher_out, None
+        elif self._teacher_client is not None:
             t_out = self._teacher_client.infer(teacher_in)
         else:
             batch = collate_obs([teacher_in])

@@ -13,7 +13,9 @@
 // a pointer read and one memcpy; the header is emitted and parsed without building intermediate JSON objects.
 // Reference counterpart: the reference pickles + lz4-compresses every trajectory (file_helper.py:255-302).
 #include <torch/extension.h>
+#include <pybind11/stl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -454,10 +456,276 @@ py::object tree_loads(py::object data, bool copy) {
   return d.node();
 }
 
+// ------------------------------------------------------------------------------------------------- batch collate
+// The inference server's per-batch host path: B request frames -> one pinned staging buffer laid out as the
+// collated batch (agent/collate.py collate_obs: every leaf stacked on a new dim 0; entity_info leaves padded on
+// their last dim to the batch's entity bucket; action_info/selected_units padded to 64) -> one H2D copy ->
+// device views.  Replaces B frame decodes + ~110 torch.stack / pad calls + the pack-into-pinned copy.
+struct Node {
+  enum Kind { DICT, LIST, TUPLE, TENSOR, VALUE } kind = VALUE;
+  std::vector<py::object> keys;
+  std::vector<Node> kids;
+  at::ScalarType dt = at::kByte;
+  std::vector<int64_t> shape;
+  int64_t off = 0, nbytes = 0;
+  py::object value;
+};
+
+struct StructParser : Decoder {
+  Node parse() {
+    Node n;
+    expect('{');
+    const std::string tag = str();
+    expect(':');
+    if (tag == "__t__") {
+      n.kind = Node::TENSOR;
+      expect('[');
+      if (!dtype_from_code(str(), &n.dt)) fail("unknown dtype");
+      expect(',');
+      expect('[');
+      if (!peek(']')) {
+        n.shape.push_back(integer());
+        while (peek(',')) {
+          ++s;
+          n.shape.push_back(integer());
+        }
+      }
+      expect(']');
+      expect(',');
+      n.off = integer();
+      expect(',');
+      n.nbytes = integer();
+      expect(']');
+      if (n.off < 0 || n.off + n.nbytes > body_len) fail("tensor outside the body");
+    } else if (tag == "__d__") {
+      n.kind = Node::DICT;
+      expect('[');
+      bool first = true;
+      while (!peek(']')) {
+        if (!first) expect(',');
+        first = false;
+        expect('[');
+        n.keys.push_back(peek('"') ? py::object(py::str(str())) : value());
+        expect(',');
+        n.kids.push_back(parse());
+        expect(']');
+      }
+      expect(']');
+    } else if (tag == "__l__" || tag == "__tu__") {
+      n.kind = tag == "__l__" ? Node::LIST : Node::TUPLE;
+      expect('[');
+      bool first = true;
+      while (!peek(']')) {
+        if (!first) expect(',');
+        first = false;
+        n.kids.push_back(parse());
+      }
+      expect(']');
+    } else if (tag == "__v__") {
+      n.kind = Node::VALUE;
+      n.value = value();
+    } else {
+      fail("unknown node tag");
+    }
+    expect('}');
+    return n;
+  }
+};
+
+struct Leaf {            // one collated tensor: B source slices -> one slot of the staging buffer
+  at::ScalarType dt;
+  std::vector<int64_t> shape;      // [B, ...] output shape
+  int64_t off = 0;                 // byte offset in the staging buffer
+  std::vector<const uint8_t*> src; // per-sample source bytes
+  std::vector<int64_t> src_last;   // per-sample size of the (padded) last dim; -1: no padding
+};
+
+struct Collator {
+  int64_t B = 0, pad_entities = 0, su_len = 64;
+  std::vector<int64_t> buckets;    // entity-count buckets (ascending): the padded size is the first >= the max
+  std::vector<const uint8_t*> bodies;
+  std::vector<Leaf> leaves;
+  int64_t total = 0;
+
+  // returns the output-tree template: TENSOR nodes carry the leaf index in `off`
+  Node plan(const std::vector<const Node*>& ns, const std::string& path, bool entity) {
+    const Node& n0 = *ns[0];
+    for (const Node* n : ns)
+      if (n->kind != n0.kind || n->kids.size() != n0.kids.size())
+        throw py::value_error("collate_frames: requests differ in structure at '" + path + "'");
+    Node out;
+    out.kind = n0.kind;
+    if (n0.kind == Node::DICT || n0.kind == Node::LIST || n0.kind == Node::TUPLE) {
+      out.keys = n0.keys;
+      for (size_t i = 0; i < n0.kids.size(); ++i) {
+        std::vector<const Node*> kids;
+        for (const Node* n : ns) kids.push_back(&n->kids[i]);
+        std::string key = n0.kind == Node::DICT ? py::str(n0.keys[i]).cast<std::string>() : std::to_string(i);
+        const bool ent = entity || (path.empty() && n0.kind == Node::DICT && key == "entity_info");
+        out.kids.push_back(plan(kids, path.empty() ? key : path + "/" + key, ent));
+      }
+      return out;
+    }
+    if (n0.kind == Node::VALUE) {
+      py::list vals;
+      for (const Node* n : ns) vals.append(n->value);
+      out.value = vals;
+      return out;
+    }
+    Leaf L;
+    L.dt = n0.dt;
+    const size_t rank = n0.shape.size();
+    const bool su = path == "action_info/selected_units";
+    const bool pad_last = rank >= 1 && (entity || su);
+    int64_t last = rank ? n0.shape[rank - 1] : 0;
+    for (const Node* n : ns) {
+      if (n->dt != n0.dt || n->shape.size() != rank) throw py::value_error("collate_frames: dtype / rank differ at " + path);
+      for (size_t d = 0; d + (pad_last ? 1 : 0) < rank; ++d)
+        if (n->shape[d] != n0.shape[d]) throw py::value_error("collate_frames: shapes differ at " + path);
+      if (pad_last) last = std::max(last, n->shape[rank - 1]);
+    }
+    if (pad_last) {
+      if (su) {
+        last = std::max(last, su_len);
+      } else {
+        last = std::max(last, pad_entities);
+        for (int64_t b : buckets)
+          if (b >= last) {
+            last = b;
+            break;
+          }
+      }
+    }
+    L.shape.push_back(B);
+    for (size_t d = 0; d < rank; ++d) L.shape.push_back(pad_last && d == rank - 1 ? last : n0.shape[d]);
+    for (size_t b = 0; b < ns.size(); ++b) {
+      L.src.push_back(bodies[b] + ns[b]->off);
+      L.src_last.push_back(pad_last ? ns[b]->shape[rank - 1] : -1);
+    }
+    int64_t bytes = at::elementSize(L.dt);
+    for (int64_t d : L.shape) bytes *= d;
+    L.off = (total + kAlign - 1) / kAlign * kAlign;
+    total = L.off + bytes;
+    out.off = static_cast<int64_t>(leaves.size());
+    leaves.push_back(std::move(L));
+    return out;
+  }
+
+  void copy_into(uint8_t* dst) const {
+    for (const Leaf& L : leaves) {
+      const int64_t es = at::elementSize(L.dt);
+      int64_t per = es;      // bytes per sample
+      for (size_t d = 1; d < L.shape.size(); ++d) per *= L.shape[d];
+      for (int64_t b = 0; b < B; ++b) {
+        uint8_t* o = dst + L.off + b * per;
+        if (L.src_last[b] < 0) {
+          std::memcpy(o, L.src[b], static_cast<size_t>(per));
+          continue;
+        }
+        const int64_t out_last = L.shape.back();
+        const int64_t rows = out_last ? per / (out_last * es) : 0;
+        const int64_t in_row = L.src_last[b] * es, out_row = out_last * es;
+        for (int64_t r = 0; r < rows; ++r) {
+          std::memcpy(o + r * out_row, L.src[b] + r * in_row, static_cast<size_t>(in_row));
+          std::memset(o + r * out_row + in_row, 0, static_cast<size_t>(out_row - in_row));
+        }
+      }
+    }
+  }
+
+  py::object build(const Node& t, const at::Tensor& buf) const {
+    switch (t.kind) {
+      case Node::DICT: {
+        py::dict d;
+        for (size_t i = 0; i < t.kids.size(); ++i) d[t.keys[i]] = build(t.kids[i], buf);
+        return d;
+      }
+      case Node::LIST:
+      case Node::TUPLE: {
+        py::list l;
+        for (const Node& k : t.kids) l.append(build(k, buf));
+        return t.kind == Node::LIST ? py::object(l) : py::object(py::tuple(l));
+      }
+      case Node::VALUE: {
+        py::list vals = t.value;
+        bool numeric = true;
+        for (auto v : vals)
+          if (!(PyLong_Check(v.ptr()) || PyFloat_Check(v.ptr()))) numeric = false;
+        if (numeric && py::len(vals)) {
+          py::object torch = py::module_::import("torch");
+          return torch.attr("tensor")(vals);
+        }
+        return vals;
+      }
+      case Node::TENSOR: {
+        const Leaf& L = leaves[static_cast<size_t>(t.off)];
+        int64_t bytes = at::elementSize(L.dt);
+        for (int64_t d : L.shape) bytes *= d;
+        at::Tensor v = buf.narrow(0, L.off, bytes).view(L.dt).view(L.shape);
+        return py::reinterpret_steal<py::object>(THPVariable_Wrap(v));
+      }
+    }
+    return py::none();
+  }
+};
+
+// frames: list of uncompressed frames of the same structure.  device: None -> host tensors; else the batch is
+// staged in pinned memory and copied with ONE non_blocking H2D on the current stream.
+py::object collate_frames(py::list frames, int64_t pad_entities, py::object device, std::vector<int64_t> buckets) {
+  const int64_t B = static_cast<int64_t>(py::len(frames));
+  if (B == 0) throw py::value_error("collate_frames: no frames");
+  std::vector<Node> roots;
+  Collator c;
+  c.B = B;
+  c.pad_entities = pad_entities;
+  c.buckets = buckets;
+  std::sort(c.buckets.begin(), c.buckets.end());
+  std::vector<py::buffer_info> infos;
+  for (auto f : frames) {
+    py::buffer buf = py::reinterpret_borrow<py::buffer>(f);
+    infos.push_back(buf.request());
+    const auto* p = static_cast<const uint8_t*>(infos.back().ptr);
+    const int64_t n = static_cast<int64_t>(infos.back().size * infos.back().itemsize);
+    const int64_t pre = static_cast<int64_t>(kMagicLen) + 9;
+    if (n < pre || std::memcmp(p, kMagic, kMagicLen) != 0 || p[kMagicLen + 8] != 0)
+      throw py::value_error("collate_frames: not an uncompressed applestar frame");
+    uint64_t hlen = 0;
+    std::memcpy(&hlen, p + kMagicLen, 8);
+    const int64_t pad = (kAlign - (pre + static_cast<int64_t>(hlen)) % kAlign) % kAlign;
+    StructParser sp;
+    sp.s = reinterpret_cast<const char*>(p + pre);
+    sp.end = sp.s + hlen;
+    sp.body = p + pre + static_cast<int64_t>(hlen) + pad;
+    sp.body_len = n - (pre + static_cast<int64_t>(hlen) + pad);
+    sp.copy = true;
+    roots.push_back(sp.parse());
+    c.bodies.push_back(sp.body);
+  }
+  std::vector<const Node*> rs;
+  for (const Node& r : roots) rs.push_back(&r);
+  const Node tmpl = c.plan(rs, "", false);
+  const bool to_dev = !device.is_none();
+  auto opts = at::TensorOptions().dtype(at::kByte);
+  if (to_dev) opts = opts.pinned_memory(true);
+  at::Tensor host = at::empty({std::max<int64_t>(c.total, 1)}, opts);
+  {
+    py::gil_scoped_release nogil;
+    c.copy_into(host.data_ptr<uint8_t>());
+  }
+  at::Tensor buf = host;
+  if (to_dev) {
+    const at::Device dev(py::str(device).cast<std::string>());
+    buf = host.to(dev, /*non_blocking=*/true);
+  }
+  return c.build(tmpl, buf);
+}
+
 }  // namespace
 
 void register_codec(py::module& m) {
   m.def("tree_dumps", &tree_dumps, "tensor tree -> applestar frame (uncompressed)");
   m.def("tree_loads", &tree_loads, py::arg("data"), py::arg("copy") = true,
         "applestar frame -> tensor tree (copy=False: tensors alias the buffer)");
+  m.def("collate_frames", &collate_frames, py::arg("frames"), py::arg("pad_entities") = 0,
+        py::arg("device") = py::none(), py::arg("buckets") = std::vector<int64_t>{}, "B request frames -> collated batch (one pinned staging buffer, one H2D)");
 }

@@ -238,6 +238,39 @@ def test_inference_server_graphed_sees_hot_weight_load():
             assert (la - lb).abs().max().item() < 1e-3 * max(1.0, lb.abs().max().item()), k
 
 
+def test_inference_server_policy_teacher_graphed_matches_eager():
+    """The training actor's merged request ('policy+teacher': policy sample + the teacher's logits for it, one
+    HIP graph per (batch bucket, entity bucket)) agrees with the eager merged path; the routed-frame path
+    (native collate_frames into one pinned buffer) gives the same replies as in-process inputs."""
+    from applestar_amd.actor.inference import InferenceServer
+    from applestar_amd.utils import serialize
+    import sys, os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_inference_server import _requests
+    torch.manual_seed(0)
+    pol, tea = Model().eval(), Model().eval()
+    reqs = _requests(3, 5, entity=(12, 200, 77))
+    for r in reqs:
+        r['teacher_hidden_state'] = [(torch.randn(384) * 0.1, torch.randn(384) * 0.1) for _ in range(3)]
+    outs = {}
+    for graphs in (False, True):
+        srv = InferenceServer('cuda', use_graphs=graphs)
+        srv.set_model('p', copy.deepcopy(pol))
+        srv.set_model('t', copy.deepcopy(tea), teacher=True)
+        outs[graphs] = srv._forward('p', 'policy+teacher', reqs, teacher_id='t')
+        if graphs:
+            L = srv._launch(('p', 'policy+teacher', 't'), frames=[serialize.dumps(r) for r in reqs], keep_logits=True)
+            outs['frames'] = srv._results(L)
+            assert {k[2] for k in srv._graphed} == {256}          # entity bucket of max(12, 200, 77)
+    for a, b, c in zip(outs[True], outs[False], outs['frames']):
+        # the teacher's action-type logits do not depend on the sampled action: graphed == eager up to bf16
+        ta, tb = a['teacher']['logit']['action_type'].float(), b['teacher']['logit']['action_type'].float()
+        assert (ta - tb).abs().max().item() < 0.05 * max(1.0, tb.abs().max().item())
+        for k in ('action_type', 'delay', 'queued', 'target_unit', 'target_location'):   # same graph, same bits
+            assert torch.equal(a['action_info'][k], c['action_info'][k]), k
+            assert torch.equal(a['teacher']['logit'][k], c['teacher']['logit'][k]), k
+
+
 @pytest.mark.parametrize('amp', ['bfloat16', None])
 def test_graphed_train_step_matches_eager(amp):
     """Whole-step HIP graphs (runtime/step_graph.py: fwd+loss+bwd+clip+Adam in one graph on one rank, fixed

@@ -78,3 +78,30 @@ def test_native_alias_mode_and_fallback():
         serialize.loads(b'NOTAFRAME' + bytes(20))
     z = serialize.dumps(t, compress=True)               # compressed frames stay on the Python codec
     _eq(t, serialize.loads(z))
+
+
+@needs_native
+def test_native_collate_frames_matches_collate_obs():
+    """collate_frames (native: B request frames -> one staged batch) == collate_obs over the decoded requests:
+    entity leaves padded to the entity bucket, action_info selected_units to 64, hidden states stacked."""
+    from applestar_amd.agent.collate import collate_obs
+    from applestar_amd.lib.features import random_obs
+    g = torch.Generator().manual_seed(3)
+    obs = random_obs(3, entity_num=torch.tensor([12, 200, 77]), generator=g)
+    reqs = []
+    for i in range(3):
+        n = int(obs['entity_num'][i])
+        r = {k: ({kk: (vv[i, :n] if k == 'entity_info' else vv[i]) for kk, vv in v.items()} if isinstance(v, dict)
+                 else v[i]) for k, v in obs.items()}
+        r['hidden_state'] = [(torch.randn(384, generator=g), torch.randn(384, generator=g)) for _ in range(3)]
+        r['action_info'] = {'action_type': torch.tensor(i), 'selected_units': torch.arange(i + 2)}
+        r['flag'] = i
+        reqs.append(r)
+    for pad in (0, 256):
+        ref = collate_obs(reqs, pad_entities=pad)
+        got = NATIVE.collate_frames([serialize.dumps(r) for r in reqs], pad)
+        _eq(ref, got)
+    with pytest.raises(ValueError):
+        bad = dict(reqs[1])
+        bad.pop('flag')
+        NATIVE.collate_frames([serialize.dumps(reqs[0]), serialize.dumps(bad)], 0)
