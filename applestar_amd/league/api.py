@@ -72,7 +72,11 @@ def create_league_app(league: League):
 
     @app.route('/league/load_resume', methods=['POST'])
     def load_resume():
-        league.load_resume(request.json['resume_path'])
+        d = request.json or {}
+        path = d.get('resume_path') or d.get('path')
+        if not path or not os.path.exists(path):
+            return bad(f'resume file {path} not found')
+        league.load_resume(path)
         return ok(True)
 
     @app.route('/league/show_elo', methods=['GET'])
@@ -110,9 +114,85 @@ def create_league_app(league: League):
 
     @app.route('/league/reset_player_stat', methods=['POST'])
     def reset_player_stat():
-        pid = request.json['player_id']
-        league.all_players[pid].reset_stats()
-        return ok(True)
+        d = request.json or {}
+        return ok(True) if league.reset_player_stat(d) else bad(f"unknown player {d.get('player_id')}")
+
+    # ---- statistics views (league_api.py:56-138): active and historical players
+    def stat_route(stat, hist):
+        def view():
+            return ok(league.show_stat(stat, historical=hist))
+        view.__name__ = f'show_{"hist_" if hist else ""}{stat}'
+        return view
+
+    for stat, name in (('dist_stat', 'dist_stat'), ('cum_stat', 'cum_stat'), ('unit_num_stat', 'unit_num_stat'),
+                       ('opponent_payoff', 'opponent_payoff'), ('teammate_payoff', 'teammate_payoff'),
+                       ('payoff', 'payoff')):
+        if name != 'payoff':
+            app.add_url_rule(f'/league/show_{name}', view_func=stat_route(stat, False), methods=['GET'])
+        app.add_url_rule(f'/league/show_hist_{name}', view_func=stat_route(stat, True), methods=['GET'])
+
+    # ---- ratings (league_api.py:205-247)
+    @app.route('/league/save_elo', methods=['GET'])
+    def save_elo():
+        return ok(league.save_elo_ratings(zero_min=False))
+
+    @app.route('/league/save_zero_elo', methods=['GET'])
+    def save_zero_elo():
+        return ok(league.save_elo_ratings(zero_min=True))
+
+    @app.route('/league/update_elo', methods=['POST'])
+    def update_elo():
+        return ok(league.update_elo(request.json or {}))
+
+    @app.route('/league/show_trueskill', methods=['GET'])
+    def show_trueskill():
+        return ok(league.trueskill.ratings())
+
+    @app.route('/league/save_trueskill', methods=['GET'])
+    def save_trueskill():
+        return ok(league.save_trueskill_ratings())
+
+    @app.route('/league/update_trueskill', methods=['POST'])
+    def update_trueskill():
+        return ok(league.update_trueskill(request.json or {}))
+
+    # ---- player management (league_api.py:188-199,257-313)
+    @app.route('/league/add_hist_player', methods=['POST'])
+    def add_hist_player():
+        return ok(True) if league.add_hist_player(request.json or {}) else bad('checkpoint not found')
+
+    @app.route('/league/remove_hist_player', methods=['POST'])
+    def remove_hist_player():
+        return ok(True) if league.remove_hist_player(request.json or {}) else bad('no such historical player')
+
+    @app.route('/league/update_player', methods=['POST'])
+    def update_player():
+        d = request.json or {}
+        return ok(True) if league.update_player(d) else bad(f"unknown player {d.get('player_id')}")
+
+    @app.route('/league/display_player', methods=['POST'])
+    def display_player():
+        return ok(league.display_player(request.json or {}))
+
+    @app.route('/league/refresh_active_player', methods=['GET'])
+    def refresh_active_player():
+        return ok(league.refresh_active_player())
+
+    @app.route('/league/refresh_hist_player', methods=['GET'])
+    def refresh_hist_player():
+        return ok(league.refresh_hist_player())
+
+    @app.route('/league/refresh_all_player', methods=['GET'])
+    def refresh_all_player():
+        return ok(league.refresh_active_player() and league.refresh_hist_player())
+
+    @app.route('/league/backup_models', methods=['POST'])
+    def backup_models():
+        return ok(league.backup_models(request.json or {}))
+
+    @app.route('/league/show_config', methods=['GET'])
+    def show_config():
+        return ok(json.loads(json.dumps(league.cfg, default=str)))
 
     return app
 

@@ -26,7 +26,7 @@ from typing import Dict, Optional
 from ..utils.config import AttrDict, deep_merge_dicts
 from ..utils.log import TextLogger
 from .players import (ActivePlayer, HistoricalPlayer, MainPlayer, active_player_type, player_from_dict)
-from .stats import ELORating
+from .stats import ELORating, TrueSkillRating
 
 DEFAULT_LEAGUE_CONFIG = AttrDict({
     'common': {'experiment_name': 'rl_train'},
@@ -73,6 +73,7 @@ class League:
         from ..runtime.health import HeartbeatRegistry
         self.health = HeartbeatRegistry(float(self.cfg.get('heartbeat_timeout', 120.0)))
         self.elo = ELORating()
+        self.trueskill = TrueSkillRating()
         self.active_players: Dict[str, ActivePlayer] = {}
         self.historical_players: Dict[str, HistoricalPlayer] = {}
         self.learner_info = {}
@@ -283,6 +284,7 @@ class League:
                     self._log_player(p, opp)
             first = info.get('0') or next(iter(info.values()))
             self.elo.update(first['player_id'], first['opponent_id'], int(first['winloss']))
+            self.trueskill.update(first['player_id'], first['opponent_id'], int(first['winloss']))
             if self.elo.game_count % max(int(self.cfg.print_freq), 1) == 0:
                 self.logger.info('ELO\n' + self.elo.text())
 
@@ -320,7 +322,7 @@ class League:
         with self.lock:
             return {'active': {k: v.to_dict() for k, v in self.active_players.items()},
                     'historical': {k: v.to_dict() for k, v in self.historical_players.items()},
-                    'elo': self.elo.to_dict()}
+                    'elo': self.elo.to_dict(), 'trueskill': self.trueskill.to_dict()}
 
     def save_resume(self, path: Optional[str] = None) -> str:
         path = path or os.path.join(self.resume_dir, f'league.resume.{int(time.time())}.json')
@@ -337,6 +339,161 @@ class League:
             self.active_players = {k: player_from_dict(v) for k, v in d['active'].items()}
             self.historical_players = {k: player_from_dict(v) for k, v in d['historical'].items()}
             self.elo = ELORating.from_dict(d['elo'])
+            if 'trueskill' in d:
+                self.trueskill = TrueSkillRating.from_dict(d['trueskill'])
+
+    # ------------------------------------------------------------------ admin (league_api.py:56-305)
+    def correspondent_player_ids(self, player_id):
+        """'all' / 'active' / 'hist' / a list / one id -> the matching player ids (league.py:847-862)."""
+        if player_id == 'all':
+            return list(self.all_players)
+        if player_id == 'active':
+            return list(self.active_players)
+        if player_id == 'hist':
+            return list(self.historical_players)
+        if isinstance(player_id, (list, tuple)):
+            return [p for p in player_id if p in self.all_players]
+        return [player_id] if player_id in self.all_players else []
+
+    def show_stat(self, stat_type: str, historical: bool = False) -> Dict:
+        """One statistic of every active (or historical) player, as a dict; also written to the league log."""
+        players = self.historical_players if historical else self.active_players
+        out = {}
+        with self.lock:
+            for pid, p in players.items():
+                st = getattr(p, stat_type, None)
+                if st is None:
+                    continue
+                out[pid] = st.stat_info_dict()
+                self.logger.info('=' * 20 + pid + '=' * 20 + f'\n{stat_type}: {json.dumps(out[pid], default=str)}')
+        return out
+
+    def save_elo_ratings(self, zero_min: bool = False) -> str:
+        path = os.path.join(self.root, 'elo_ratings' + ('_zero' if zero_min else '') + '.json')
+        with open(path, 'w') as f:
+            json.dump(self.elo.ratings(start_from_zero=zero_min), f, indent=1)
+        return path
+
+    def update_elo(self, info: Dict) -> bool:
+        """{player_id: elo} (absolute ratings; the stored value is relative to init_elo)."""
+        with self.lock:
+            for pid, v in (info or {}).items():
+                self.elo.elos[pid] = float(v) - self.elo.init_elo
+        return True
+
+    def save_trueskill_ratings(self) -> str:
+        path = os.path.join(self.root, 'trueskill_ratings.json')
+        with open(path, 'w') as f:
+            json.dump(self.trueskill.ratings(), f, indent=1)
+        return path
+
+    def update_trueskill(self, info: Dict) -> bool:
+        """{player_id: {'mu': .., 'sigma': ..}}."""
+        with self.lock:
+            for pid, v in (info or {}).items():
+                self.trueskill.set(pid, v.get('mu'), v.get('sigma'))
+        return True
+
+    def add_hist_player(self, info: Dict) -> bool:
+        """Copy a checkpoint into the league and add it as a historical player (league.py:558-588)."""
+        ckpt = info.get('checkpoint_path', 'none')
+        if ckpt == 'none' or not os.path.exists(ckpt):
+            return False
+        pid = info.get('player_id') or 'none'
+        if pid == 'none':
+            self._added = getattr(self, '_added', 0) + 1
+            pid = f'HP_ADD{self._added}'
+        dst = os.path.join(self.model_dir, pid + '_' + os.path.basename(ckpt))
+        shutil.copyfile(ckpt, dst)
+        hp = HistoricalPlayer(dst, pid, info.get('pipeline', 'default'), info.get('frac_id', 1),
+                              info.get('z_path', '3map.json'), info.get('z_prob', 0.0), **self._player_kw())
+        with self.lock:
+            self.historical_players[pid] = hp
+        self.logger.info(f'added historical player {pid}')
+        return True
+
+    def remove_hist_player(self, info: Dict) -> bool:
+        """Drop historical players and every payoff record against them (league.py:739-758)."""
+        ids = [p for p in self.correspondent_player_ids(info['player_id']) if p in self.historical_players]
+        with self.lock:
+            for pid in ids:
+                self.historical_players.pop(pid, None)
+                for p in self.all_players.values():
+                    for k in ('payoff', 'teammate_payoff', 'opponent_payoff'):
+                        getattr(p, k).record.pop(pid, None)
+                self.logger.info(f'removed historical player {pid}')
+        return bool(ids)
+
+    _UPDATABLE = ('checkpoint_path', 'pipeline', 'frac_id', 'z_path', 'teacher_id', 'teacher_checkpoint_path',
+                  'chosen_weight', 'total_agent_step', 'decay', 'warm_up_size', 'total_game_count', 'parent_id',
+                  'one_phase_step', 'last_enough_step', 'snapshot_times', 'strong_win_rate', 'snapshot_flag',
+                  'reset_flag', 'z_prob')
+
+    def update_player(self, info: Dict) -> bool:
+        """Set attributes of one player (league.py:617-635)."""
+        p = self.all_players.get(info.get('player_id'))
+        if p is None:
+            return False
+        with self.lock:
+            for k in self._UPDATABLE:
+                if k in info and hasattr(p, k):
+                    v = info[k]
+                    if k == 'one_phase_step':
+                        v = int(float(v))
+                    setattr(p, k, v)
+        return True
+
+    def display_player(self, info: Dict) -> Dict:
+        out = {}
+        for pid in self.correspondent_player_ids(info['player_id']):
+            p = self.all_players[pid]
+            d = {'repr': repr(p)}
+            for st in info.get('stat_types', []):
+                if hasattr(p, st):
+                    d[st] = getattr(p, st).stat_info_dict()
+            out[pid] = d
+            self.logger.info(f'{pid}: {json.dumps(d, default=str)}')
+        return out
+
+    def reset_player_stat(self, info: Dict) -> bool:
+        ids = self.correspondent_player_ids(info['player_id'])
+        with self.lock:
+            for pid in ids:
+                self.all_players[pid].reset_stats(info.get('stat_types'))
+        return bool(ids)
+
+    def _refresh(self, players: Dict) -> None:
+        """Rebuild player objects from their persisted state with the current league settings (new code or
+        config takes effect without a restart; league.py:637-705)."""
+        with self.lock:
+            for pid, old in list(players.items()):
+                d = old.to_dict()
+                d['min_win_rate_games'] = self.cfg.payoff_min_win_rate_games
+                players[pid] = player_from_dict(d)
+                self.logger.info(f'refreshed player {pid}')
+
+    def refresh_active_player(self) -> bool:
+        self._refresh(self.active_players)
+        return True
+
+    def refresh_hist_player(self) -> bool:
+        self._refresh(self.historical_players)
+        return True
+
+    def backup_models(self, info: Optional[Dict] = None) -> str:
+        """Copy the checkpoints of the selected players (default all) into ``league_models_backup/<time>``."""
+        info = info or {}
+        dst = info.get('backup_dir') or os.path.join(self.root, 'league_models_backup',
+                                                     time.strftime('%Y-%m-%d-%H-%M-%S'))
+        os.makedirs(dst, exist_ok=True)
+        n = 0
+        for pid in self.correspondent_player_ids(info.get('player_id', 'all')):
+            src = self.all_players[pid].checkpoint_path
+            if src and os.path.isfile(src):
+                shutil.copyfile(src, os.path.join(dst, os.path.basename(src)))
+                n += 1
+        self.logger.info(f'backed up {n} checkpoints to {dst}')
+        return dst
 
     def _resume_loop(self):
         freq = float(self.cfg.save_resume_freq)

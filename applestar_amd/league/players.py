@@ -51,17 +51,25 @@ class Player:
         self.min_win_rate_games = min_win_rate_games
         self.total_game_count = total_game_count
         self.payoff = Payoff(decay, warm_up_size, min_win_rate_games)
+        # team-game payoffs of the reference's Player (kept and persisted; 1v1 results only feed ``payoff``)
+        self.teammate_payoff = Payoff(decay, warm_up_size, min_win_rate_games)
+        self.opponent_payoff = Payoff(decay, warm_up_size, min_win_rate_games)
 
     def get_race(self) -> str:
         return random.choice(FRAC_ID[self.frac_id])
 
-    def reset_stats(self):
-        self.payoff = Payoff(self.decay, self.warm_up_size, self.min_win_rate_games)
+    STAT_TYPES = ('payoff', 'teammate_payoff', 'opponent_payoff')
+
+    def reset_stats(self, stat_types=None):
+        for k in (Player.STAT_TYPES if stat_types is None else stat_types):
+            if k in Player.STAT_TYPES:
+                setattr(self, k, Payoff(self.decay, self.warm_up_size, self.min_win_rate_games))
 
     def to_dict(self) -> Dict:
         d = {k: getattr(self, k) for k in self.persist}
         d['kind'] = self.kind
-        d['payoff'] = self.payoff.to_dict()
+        for k in self.STAT_TYPES:
+            d[k] = getattr(self, k).to_dict()
         return d
 
     def __repr__(self):
@@ -174,11 +182,14 @@ class ActivePlayer(Player):
                                 warm_up_size=self.warm_up_size, min_win_rate_games=self.min_win_rate_games,
                                 parent_id=self.player_id)
 
-    def reset_stats(self):
-        super().reset_stats()
-        self.dist_stat = RaceStat(self.decay, self.warm_up_size)
-        self.cum_stat = RaceStat(self.decay, self.warm_up_size)
-        self.unit_num_stat = RaceStat(self.decay, self.warm_up_size)
+    STAT_TYPES = Player.STAT_TYPES + ('dist_stat', 'cum_stat', 'unit_num_stat')
+
+    def reset_stats(self, stat_types=None):
+        types = stat_types or self.STAT_TYPES
+        super().reset_stats([k for k in types if k in Player.STAT_TYPES])
+        for k in ('dist_stat', 'cum_stat', 'unit_num_stat'):
+            if k in types:
+                setattr(self, k, RaceStat(self.decay, self.warm_up_size))
 
     def to_dict(self):
         d = super().to_dict()
@@ -386,7 +397,7 @@ def active_player_type(player_id: str):
 def player_from_dict(d: Dict) -> Player:
     d = dict(d)
     kind = d.pop('kind')
-    payoff = d.pop('payoff', None)
+    payoffs = {k: d.pop(k, None) for k in Player.STAT_TYPES}
     stats = {k: d.pop(k, None) for k in ('dist_stat', 'cum_stat', 'unit_num_stat')}
     if kind == 'historical':
         p = HistoricalPlayer(**d)
@@ -395,6 +406,7 @@ def player_from_dict(d: Dict) -> Player:
         for k, v in stats.items():
             if v is not None:
                 setattr(p, k, RaceStat.from_dict(v))
-    if payoff is not None:
-        p.payoff = Payoff.from_dict(payoff)
+    for k, v in payoffs.items():
+        if v is not None:
+            setattr(p, k, Payoff.from_dict(v))
     return p

@@ -13,7 +13,7 @@ from __future__ import annotations
 
 import math
 from collections import defaultdict, deque
-from typing import Dict, Iterable, List
+from typing import Optional, Dict, Iterable, List
 
 import numpy as np
 
@@ -181,6 +181,93 @@ def trueskill_win_probability(mu1: float, sigma1: float, mu2: float, sigma2: flo
     delta = mu1 - mu2
     denom = math.sqrt(2 * beta * beta + sigma1 * sigma1 + sigma2 * sigma2)
     return 0.5 * (1 + math.erf(delta / (denom * math.sqrt(2))))
+
+
+def _norm_pdf(x: float) -> float:
+    return math.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+
+
+def _norm_cdf(x: float) -> float:
+    return 0.5 * (1 + math.erf(x / math.sqrt(2)))
+
+
+def _norm_ppf(p: float) -> float:
+    lo, hi = -10.0, 10.0
+    for _ in range(100):
+        mid = 0.5 * (lo + hi)
+        lo, hi = (mid, hi) if _norm_cdf(mid) < p else (lo, mid)
+    return 0.5 * (lo + hi)
+
+
+class TrueSkillRating:
+    """1v1 TrueSkill (Herbrich et al. 2006) for the league's players: Gaussian skill N(mu, sigma^2), dynamics
+    noise tau, performance noise beta, draw margin from ``draw_probability``.  The reference's league API exposes
+    show / save / update_trueskill routes (``league_api.py:230-247``) whose league methods it never defines;
+    this is the working version (win probability: :func:`trueskill_win_probability`)."""
+
+    def __init__(self, mu: float = 25.0, sigma: float = 25 / 3, beta: float = 25 / 6, tau: float = 25 / 300,
+                 draw_probability: float = 0.1):
+        self.mu0, self.sigma0, self.beta, self.tau, self.draw_probability = mu, sigma, beta, tau, draw_probability
+        self.eps = _norm_ppf((draw_probability + 1) / 2) * math.sqrt(2) * beta
+        self.mu: Dict[str, float] = {}
+        self.sigma: Dict[str, float] = {}
+        self.game_count = 0
+
+    def get(self, pid: str):
+        return self.mu.get(pid, self.mu0), self.sigma.get(pid, self.sigma0)
+
+    def update(self, p1: str, p2: str, result: int) -> None:
+        """result: 1 = p1 won, -1 = p2 won, 0 = draw."""
+        if result < 0:
+            p1, p2 = p2, p1
+        (m1, s1), (m2, s2) = self.get(p1), self.get(p2)
+        s1, s2 = math.sqrt(s1 * s1 + self.tau ** 2), math.sqrt(s2 * s2 + self.tau ** 2)
+        c = math.sqrt(2 * self.beta ** 2 + s1 * s1 + s2 * s2)
+        t, e = (m1 - m2) / c, self.eps / c
+        if result == 0:
+            den = max(_norm_cdf(e - t) - _norm_cdf(-e - t), 1e-12)
+            v = (_norm_pdf(-e - t) - _norm_pdf(e - t)) / den
+            w = v * v + ((e - t) * _norm_pdf(e - t) + (e + t) * _norm_pdf(e + t)) / den
+        else:
+            den = max(_norm_cdf(t - e), 1e-12)
+            v = _norm_pdf(t - e) / den
+            w = v * (v + t - e)
+        self.mu[p1] = m1 + s1 * s1 / c * v
+        self.mu[p2] = m2 - s2 * s2 / c * v
+        self.sigma[p1] = s1 * math.sqrt(max(1 - s1 * s1 / (c * c) * w, 1e-6))
+        self.sigma[p2] = s2 * math.sqrt(max(1 - s2 * s2 / (c * c) * w, 1e-6))
+        self.game_count += 1
+
+    def set(self, pid: str, mu: Optional[float] = None, sigma: Optional[float] = None) -> None:
+        if mu is not None:
+            self.mu[pid] = float(mu)
+        if sigma is not None:
+            self.sigma[pid] = float(sigma)
+
+    def win_probability(self, p1: str, p2: str) -> float:
+        (m1, s1), (m2, s2) = self.get(p1), self.get(p2)
+        return trueskill_win_probability(m1, s1, m2, s2, self.beta)
+
+    def ratings(self) -> Dict[str, Dict[str, float]]:
+        """Sorted by the conservative skill mu - 3 sigma."""
+        ids = sorted(set(self.mu) | set(self.sigma), key=lambda k: self.get(k)[0] - 3 * self.get(k)[1])
+        return {k: {'mu': self.get(k)[0], 'sigma': self.get(k)[1], 'skill': self.get(k)[0] - 3 * self.get(k)[1]}
+                for k in ids}
+
+    def text(self) -> str:
+        return '\n'.join(f'{k:24s} mu {v["mu"]:7.2f} sigma {v["sigma"]:6.2f} skill {v["skill"]:7.2f}'
+                         for k, v in self.ratings().items())
+
+    def to_dict(self):
+        return {'mu0': self.mu0, 'sigma0': self.sigma0, 'beta': self.beta, 'tau': self.tau,
+                'draw_probability': self.draw_probability, 'mu': self.mu, 'sigma': self.sigma,
+                'game_count': self.game_count}
+
+    @classmethod
+    def from_dict(cls, d):
+        t = cls(d['mu0'], d['sigma0'], d['beta'], d['tau'], d['draw_probability'])
+        t.mu, t.sigma, t.game_count = dict(d['mu']), dict(d['sigma']), d['game_count']
+        return t
 
 
 class RaceStat:

@@ -222,11 +222,30 @@ class RLLearner(BaseLearner):
         """Thread-safe: applied between iterations (admin HTTP routes call this)."""
         self._admin_flags[kind] = payload
 
+    def reset_comm_setting(self) -> None:
+        """Re-create the league / data-plane links from the (possibly hot-updated) communication config
+        (``rl_learner.py:244-261``): close the old LearnerComm and dataloader, register again, rebuild the
+        dataloader (its HBM trajectory ring is re-allocated on the new coordinator)."""
+        self.comm.close()
+        if hasattr(self.dataloader, 'close'):
+            self.dataloader.close()
+        self.comm = LearnerComm(self.cfg, self)
+        if self.cfg.learner.job_type == 'train':
+            self.comm.register(self)
+        self.dataloader = self._setup_dataloader()
+        self.info(f'{self.comm.player_id} communication reset')
+
     def _apply_admin(self, kind: str, payload):
-        if kind == 'update_config':
+        if kind == 'reset_comm_setting':
+            deep_update(self.cfg, payload or {})
+            self.reset_comm_setting()
+        elif kind == 'update_config':
             deep_update(self.cfg, payload or {})
             for g in self.optimizer.param_groups:
                 g['lr'] = self.cfg.learner.learning_rate
+            sched = getattr(self.trainer, 'lr_scheduler', None)
+            if sched is not None and hasattr(sched, 'base_lrs'):
+                sched.base_lrs = [self.cfg.learner.learning_rate for _ in sched.base_lrs]
         elif kind == 'reset_value':
             self.reset_value()
             self.trainer.remain_value_pretrain = int((payload or {}).get(
@@ -239,7 +258,7 @@ class RLLearner(BaseLearner):
 
 
 def create_learner_app(learner: RLLearner):
-    """Flask admin routes ``/rl_learner/{update_config,reset_value}`` (``rl_learner.py:203-287``)."""
+    """Flask admin routes ``/rl_learner/{update_config,reset_value,reset_comm_setting}`` (``rl_learner.py:263-287``)."""
     from flask import Flask, jsonify, request
     app = Flask('applestar_learner')
 
@@ -251,6 +270,11 @@ def create_learner_app(learner: RLLearner):
     @app.route('/rl_learner/reset_value', methods=['POST'])
     def reset_value():
         learner.request_admin('reset_value', request.json or {})
+        return jsonify({'code': 0, 'info': True})
+
+    @app.route('/rl_learner/reset_comm_setting', methods=['GET', 'POST'])
+    def reset_comm_setting():
+        learner.request_admin('reset_comm_setting', request.get_json(silent=True) or {})
         return jsonify({'code': 0, 'info': True})
 
     @app.route('/rl_learner/status', methods=['GET'])

@@ -105,8 +105,10 @@ class TrainEngine:
         lc = self.cfg.learner
         self.optimizer = build_optimizer(self.opt_params, lc, betas=self.ADAM_BETAS, eps=self.ADAM_EPS,
                                          device=self.device)
-        from ..utils.lr_scheduler import build_lr_scheduler
-        self.lr_scheduler = build_lr_scheduler(self.optimizer, lc.get('lr_scheduler', {'type': 'none'}))
+        self.lr_scheduler = None            # the RL learner's LR is constant (rl_learner.py: MultiStepLR, no milestones)
+        if lc.get('lr_scheduler') is not None:
+            from ..utils.lr_scheduler import build_lr_scheduler
+            self.lr_scheduler = build_lr_scheduler(self.optimizer, lc.lr_scheduler)
         # clip + Adam as two / three native launches (utils/fused_optim.py) on the GPU
         from ..utils.fused_optim import FusedClipAdam
         self.fused_opt = None

@@ -95,3 +95,58 @@ def test_http_api(tmp_path):
     lg.drain_results()
     assert c.get('/league/show_elo').json['code'] == 0
     lg.close()
+
+
+def test_http_admin_routes(tmp_path):
+    """The league admin surface of league_api.py:56-313: statistics views (active + historical), ELO /
+    TrueSkill show-save-update, historical player add / remove, player update / display / stat reset,
+    refresh, model backup, config view, resume load - each answers code 0 and has its effect."""
+    pytest.importorskip('flask')
+    from applestar_amd.league.api import create_league_app
+    lg = League(_cfg(tmp_path, players=('MP0',)), root=str(tmp_path), start_threads=True)
+    c = create_league_app(lg).test_client()
+    for i in range(6):
+        job = c.post('/league/actor_ask_for_job', json={'job_type': 'train'}).json['info']
+        res = {'0': {'player_id': job['player_ids'][0], 'opponent_id': job['player_ids'][1], 'winloss': 1 - i % 3,
+                     'race_id': 'zerg', 'dist/bo': 3.0},
+               'game_steps': 10, 'game_iters': 5, 'game_duration': 1.0}
+        c.post('/league/actor_send_result', json=res)
+    lg.drain_results()
+    for route in ('show_dist_stat', 'show_cum_stat', 'show_unit_num_stat', 'show_opponent_payoff',
+                  'show_teammate_payoff', 'show_hist_payoff', 'show_hist_dist_stat', 'show_hist_cum_stat',
+                  'show_hist_unit_num_stat', 'show_hist_opponent_payoff', 'show_hist_teammate_payoff', 'show_payoff',
+                  'show_elo', 'show_trueskill', 'show_config', 'refresh_active_player', 'refresh_hist_player',
+                  'refresh_all_player'):
+        assert c.get(f'/league/{route}').json['code'] == 0, route
+    assert 'zerg' in c.get('/league/show_dist_stat').json['info']['MP0']
+    ts = c.get('/league/show_trueskill').json['info']
+    assert len(ts) >= 2 and all(v['sigma'] < 25 / 3 for v in ts.values())
+    assert c.post('/league/update_trueskill', json={'MP0': {'mu': 30.0}}).json['code'] == 0
+    assert lg.trueskill.get('MP0')[0] == 30.0
+    assert c.post('/league/update_elo', json={'MP0': 1500}).json['code'] == 0
+    assert abs(lg.elo.ratings(start_from_zero=False)['MP0'] - 1500) < 1e-6
+    for route in ('save_elo', 'save_zero_elo', 'save_trueskill'):
+        path = c.get(f'/league/{route}').json['info']
+        assert os.path.exists(path), route
+    ckpt = tmp_path / 'extra.pth'
+    ckpt.write_bytes(b'weights')
+    assert c.post('/league/add_hist_player', json={'player_id': 'HPX', 'checkpoint_path': str(ckpt)}).json['code'] == 0
+    assert 'HPX' in lg.historical_players
+    assert c.post('/league/add_hist_player', json={'checkpoint_path': '/nonexistent'}).json['code'] == 1
+    assert c.post('/league/update_player', json={'player_id': 'MP0', 'chosen_weight': 3.0,
+                                                 'one_phase_step': '1e6'}).json['code'] == 0
+    assert lg.active_players['MP0'].chosen_weight == 3.0 and lg.active_players['MP0'].one_phase_step == 1000000
+    shown = c.post('/league/display_player', json={'player_id': 'active', 'stat_types': ['payoff']}).json['info']
+    assert 'MP0' in shown and 'payoff' in shown['MP0']
+    assert c.post('/league/reset_player_stat', json={'player_id': 'MP0', 'stat_types': ['dist_stat']}).json['code'] == 0
+    assert lg.active_players['MP0'].dist_stat.stat_info_dict() == {}
+    assert sum(len(p.payoff.record) for p in lg.all_players.values()) > 0     # payoffs kept
+    lg.active_players['MP0'].checkpoint_path = str(ckpt)
+    bdir = c.post('/league/backup_models', json={'player_id': 'all'}).json['info']
+    assert os.path.exists(os.path.join(bdir, 'extra.pth'))
+    assert c.post('/league/remove_hist_player', json={'player_id': 'HPX'}).json['code'] == 0
+    assert 'HPX' not in lg.historical_players
+    path = c.get('/league/save_resume').json['info']
+    assert c.post('/league/load_resume', json={'path': path}).json['code'] == 0
+    assert lg.trueskill.get('MP0')[0] == 30.0                                   # TrueSkill persisted in the resume
+    lg.close()

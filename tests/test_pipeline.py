@@ -105,3 +105,25 @@ def test_rl_dataloader_ring_mode_cpu():
     dl.close()
     prod.close()
     srv.shutdown()
+
+
+def test_learner_admin_routes(tmp_path, monkeypatch):
+    """/rl_learner/{update_config, reset_value, reset_comm_setting} (rl_learner.py:263-287): requests are
+    applied between iterations - the learning rate changes, and the comm link and dataloader are rebuilt."""
+    pytest.importorskip('flask')
+    monkeypatch.chdir(tmp_path)
+    from applestar_amd.learner.rl_learner import RLLearner, create_learner_app
+    lrn = RLLearner({'common': {'experiment_name': 'adm'},
+                     'learner': {'use_cuda': False, 'player_id': 'MP0', 'use_value_feature': False,
+                                 'data': {'batch_size': 1, 'trajectory_length': 2, 'synthetic': True},
+                                 'log_to_stdout': False}})
+    c = create_learner_app(lrn).test_client()
+    old_comm, old_loader = lrn.comm, lrn.dataloader
+    assert c.post('/rl_learner/update_config', json={'learner': {'learning_rate': 3e-4}}).json['code'] == 0
+    assert c.get('/rl_learner/reset_comm_setting').json['code'] == 0
+    assert c.post('/rl_learner/reset_value', json={}).json['code'] == 0
+    lrn.run(max_iterations=1)
+    assert lrn.trainer.optimizer.param_groups[0]['lr'] == 3e-4
+    assert lrn.comm is not old_comm and lrn.dataloader is not old_loader
+    assert c.get('/rl_learner/status').json['info']['iter'] == 1
+    lrn.close()
