@@ -30,7 +30,7 @@ class RLDataLoader:
 
     def __init__(self, adapter, player_id: str, batch_size: int, buffer_size: Optional[int] = None,
                  device='cpu', queue_size: int = 2, pull_timeout: Optional[float] = None, seed: int = 0,
-                 ring_bytes: int = 16 << 30, max_reuse: int = 2, device_collate: Optional[bool] = None):
+                 ring_bytes: Optional[int] = None, max_reuse: int = 2, device_collate: Optional[bool] = None):
         self._adapter = adapter
         self._token = player_id + 'traj'
         self.batch_size = int(batch_size)
@@ -43,8 +43,8 @@ class RLDataLoader:
         self.device = torch.device(device)
         self.device_collate = (self.device.type == 'cuda') if device_collate is None else device_collate
         if self.device_collate:
-            from ..runtime.traj_ring import TrajectoryRing
-            self._ring = TrajectoryRing(ring_bytes, self.device)
+            from ..runtime.traj_ring import TrajectoryRing, auto_ring_bytes
+            self._ring = TrajectoryRing(ring_bytes or auto_ring_bytes(self.device), self.device)
             self._avail = threading.Condition()
             self._thread = threading.Thread(target=self._ring_loop, daemon=True, name='rl-ring-ingest')
             self._thread.start()

@@ -183,8 +183,19 @@ class RLLearner(BaseLearner):
                                          use_value_feature=lc.use_value_feature)
         return RLDataLoader(Adapter(c.coordinator_ip, c.coordinator_port), lc.player_id, lc.data.batch_size,
                             lc.data.get('buffer_size'), self.device,
-                            ring_bytes=int(float(lc.data.get('ring_gb', 16)) * (1 << 30)),
+                            ring_bytes=self._ring_bytes(),
                             max_reuse=int(lc.data.get('max_reuse', 2)))
+
+    def _ring_bytes(self) -> int:
+        """``learner.data.ring_gb``: a number of GB, or 'auto' (default) = sized from the free HBM minus the
+        step's peak (runtime/traj_ring.py auto_ring_bytes; ``ring_fraction`` of it, default 0.75)."""
+        d = self.cfg.learner.data
+        gb = d.get('ring_gb', 'auto')
+        if gb in (None, 'auto'):
+            from ..runtime.traj_ring import auto_ring_bytes
+            return auto_ring_bytes(self.device, step_peak_gb=float(d.get('step_peak_gb', 20.0)),
+                                   fraction=float(d.get('ring_fraction', 0.75)))
+        return int(float(gb) * (1 << 30))
 
     def _train(self, data: Dict) -> Dict:
         mli = data.pop('model_last_iter', None)

@@ -66,6 +66,26 @@ class _Traj:
         self.uses = 0
 
 
+def auto_ring_bytes(device, step_peak_gb: float = 20.0, headroom_gb: float = 8.0, fraction: float = 0.75,
+                    min_gb: float = 1.0, max_gb: Optional[float] = None) -> int:
+    """HBM ring size from what the device has free: ``fraction`` x (free - learner step peak - headroom).
+
+    The fp32 learner step peaks at 15.1 GB of HBM (B = 6, T = 64; bench.py's ``peak_mem_gb``), the bf16 step
+    lower, so the default ``step_peak_gb`` of 20 GB leaves a margin; on an MI355X (288 GB) with the learner
+    alone that is ~195 GB of trajectories - ~6,000 T = 64 trajectories of ~30 MB at 512 entities - instead of a
+    fixed 16 GB.  ``fraction`` < 1 leaves room for an inference server sharing the GPU.  Call before the model's
+    first step (the free memory then does not include the step's activations yet)."""
+    dev = torch.device(device)
+    if dev.type != 'cuda':
+        return int(min_gb * (1 << 30))
+    free, _ = torch.cuda.mem_get_info(dev)
+    avail = free - (step_peak_gb + headroom_gb) * (1 << 30)
+    n = max(avail * fraction, min_gb * (1 << 30))
+    if max_gb is not None:
+        n = min(n, max_gb * (1 << 30))
+    return int(n) // (1 << 20) * (1 << 20)
+
+
 class TrajectoryRing:
     def __init__(self, capacity_bytes: int, device='cuda', staging_buffers: int = 4):
         self.device = torch.device(device)

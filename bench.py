@@ -16,7 +16,8 @@ the native conv / GEMM / weight-gradient products run as fp32-accurate bf16x6 sp
 fp32 accumulation; error vs float64 equal to or below the exact-f32 MFMA's), ``APPLESTAR_F32_MFMA=exact``
 runs them on the exact-f32 MFMA instead; the JSON's ``config.fp32_products`` names the mode.  ``--precision bf16`` is the mixed-precision step: bf16
 compute weights over fp32 master weights, fp32 LayerNorm statistics / softmax / losses / optimizer;
-its training parity against fp32 is pinned by ``tests/test_precision_parity_gpu.py``.
+its training parity against fp32 is pinned by
+``tests/test_model_parity_gpu.py::test_bf16_training_tracks_fp32``.
 ``--precision both`` (default) measures both, fp32 first; the headline ``value`` / ``dtype`` are the
 fp32 run, the bf16 run is reported under ``"mixed_bf16"``.
 

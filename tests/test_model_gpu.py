@@ -355,11 +355,12 @@ def test_stacked_lstm_pipelined_matches_layer_by_layer():
 
 
 @pytest.mark.gpu
-def test_data_parallel_two_ranks_finite_and_identical(tmp_path):
-    """Two ranks (gloo, sharing the one GPU) run the bf16 master-weight learner with backward-overlapped
-    bucket all-reduces: every step's gradient norm is finite and identical on both ranks (the reduced
-    gradient), and the loss stays finite.  Regression test for bucket copies issued from a side-stream
-    gradient hook (parallel/dp.py ``join_hook_stream``)."""
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_data_parallel_two_ranks_finite_and_identical(tmp_path, precision):
+    """Two ranks (gloo, sharing the one GPU) run the learner step of each precision - fp32: GradientReducer
+    buckets + derived weight forms + fused clip/Adam; bf16: master weights - on different data: every step's
+    gradient norm is finite and bit-identical on both ranks (the reduced gradient), the loss stays finite, and
+    the updated weights are bit-identical (same replica after every step)."""
     import json
     import os
     import subprocess
@@ -367,8 +368,8 @@ def test_data_parallel_two_ranks_finite_and_identical(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, APPLESTAR_DIST_BACKEND='gloo')
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
-           '--master-addr', '127.0.0.1', '--master-port', '29631', os.path.join(root, 'tools', 'loss_probe.py'),
-           '--steps', '3', '--batch', '2', '--unroll', '8']
+           '--master-addr', '127.0.0.1', '--master-port', str(29631 + (precision == 'bf16')), os.path.join(root, 'tools', 'loss_probe.py'),
+           '--steps', '3', '--batch', '2', '--unroll', '8', '--precision', precision]
     res = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=400)
     assert res.returncode == 0, res.stderr[-3000:]
     recs = [json.loads(l) for l in res.stdout.splitlines() if l.startswith('{')]
@@ -377,8 +378,9 @@ def test_data_parallel_two_ranks_finite_and_identical(tmp_path):
         assert math.isfinite(r['loss']) and math.isfinite(r['grad_norm']), r
         assert 'nonfinite_grads' not in r, r
     for s in range(3):
-        a, b = [r['grad_norm'] for r in recs if r['step'] == s]
-        assert a == b
+        a, b = [r for r in recs if r['step'] == s]
+        assert a['grad_norm'] == b['grad_norm'] and a['weight_hash'] == b['weight_hash'], (a, b)
+        assert a['loss'] != b['loss']          # different data per rank: the equality above is the reduction
 
 
 @pytest.mark.parametrize('only_value', [False, True])

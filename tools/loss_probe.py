@@ -26,6 +26,7 @@ def main():
     ap.add_argument('--seed-base', type=int, default=-1, help='batch seed base (default: 1000 * rank, as bench.py)')
     ap.add_argument('--n-batches', type=int, default=2)
     ap.add_argument('--loss-parts', action='store_true')
+    ap.add_argument('--precision', choices=['fp32', 'bf16'], default='fp32')
     args = ap.parse_args()
 
     from applestar_amd.parallel import dist as pdist
@@ -37,8 +38,9 @@ def main():
     gpu = torch.cuda.is_available()
     device = torch.device('cuda', torch.cuda.current_device()) if gpu else torch.device('cpu')
     torch.manual_seed(1234 + rank)
-    trainer = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}},
-                        device=device)
+    trainer = RLTrainer({'learner': {'use_value_feature': True,
+                                     'amp_dtype': 'bfloat16' if args.precision == 'bf16' else None},
+                         'model': {'enable_baselines': ['winloss']}}, device=device)
     base = 1000 * rank if args.seed_base < 0 else args.seed_base
     batches = [rl_batch(args.batch, args.unroll, seed=base + i) for i in range(args.n_batches)]
 
@@ -54,6 +56,13 @@ def main():
         info = trainer.step(next(it))
         rec = {'rank': rank, 'world': world, 'step': s, 'loss': float(info['total_loss']),
                'grad_norm': float(info['gradient'])}
+        # bit-level fingerprint of the weights after the update: identical on every rank iff the ranks hold
+        # the same replica (the fp32 masters in the bf16 step)
+        with torch.no_grad():
+            flat = trainer.master.master.detach() if trainer.master is not None else \
+                torch.cat([p.detach().reshape(-1) for p in trainer.params])
+            rec['weight_sum'] = float(flat.double().sum())
+            rec['weight_hash'] = int((flat.view(torch.int32).long() * 2654435761 % (1 << 31)).sum().item())
         if args.loss_parts:
             rec['parts'] = {k: float(v) for k, v in info.items()
                             if torch.is_tensor(v) and v.numel() == 1 and k not in ('total_loss', 'gradient')}
