@@ -213,12 +213,40 @@ class InferenceServer:
             L.event.record()
         return L
 
-    def _results(self, L: _Launched) -> List[Dict]:
+    def _wait(self, L: _Launched) -> float:
         t0 = time.perf_counter()
         if L.event is not None:
             L.event.synchronize()
         t1 = time.perf_counter()
         self.stats['d2h_wait_s'] += t1 - t0
+        return t1
+
+    def _reply_frames(self, L: _Launched) -> Optional[List[bytes]]:
+        """Per-row reply frames straight from the host batch (csrc/codec.cpp rows_dumps: decollate_output's
+        trimming and the encode in one native pass); None without the extension."""
+        from ..ops import _ext
+        nat = _ext._load()
+        if nat is None or not hasattr(nat, 'rows_dumps'):
+            return None
+        t1 = self._wait(L)
+        out = dict(L.out)
+        n = L.n
+        s = [int(v) for v in out['selected_units_num'][:n].tolist()]
+        e = [int(v) for v in out['entity_num'][:n].tolist()]
+        e1 = [v + 1 for v in e]
+        trims = {'logit/selected_units': [(0, s), (1, e1)], 'logit/target_unit': [(0, e)],
+                 'action_info/selected_units': [(0, s)], 'action_logp/selected_units': [(0, s)],
+                 'extra_units': [(0, e)],
+                 'teacher/logit/selected_units': [(0, s), (1, e1)], 'teacher/logit/target_unit': [(0, e)]}
+        pid, kind, _ = L.route
+        if kind != 'teacher':
+            out['model_last_iter'] = self.model_iter[pid]
+        frames = nat.rows_dumps(out, n, trims)
+        self.stats['decollate_s'] += time.perf_counter() - t1
+        return frames
+
+    def _results(self, L: _Launched) -> List[Dict]:
+        t1 = self._wait(L)
         out = L.out
         teacher = out.pop('teacher', None)
         res = [decollate_output(out, i) for i in range(L.n)]
@@ -240,11 +268,13 @@ class InferenceServer:
 
     # ------------------------------------------------------------------ serving
     def _finish(self, L: _Launched):
-        res = self._results(L)
+        frames = self._reply_frames(L)
+        if frames is None:
+            frames = [serialize.dumps(o) for o in self._results(L)]
         t0 = time.perf_counter()
-        for c, o in zip(L.conns, res):
+        for c, f in zip(L.conns, frames):
             try:
-                c.send_bytes(serialize.dumps(o))
+                c.send_bytes(f)
             except (BrokenPipeError, OSError):
                 pass
         self.stats['reply_s'] += time.perf_counter() - t0

@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -104,10 +105,16 @@ void json_double(std::string& out, double v) {
   if (!strpbrk(buf, ".eEn")) out += ".0";
 }
 
+using Trims = std::map<std::string, std::vector<std::pair<int64_t, std::vector<int64_t>>>>;
+
 struct Encoder {
   std::string header;
   std::vector<std::pair<int64_t, at::Tensor>> blobs;
   int64_t offset = 0;
+  // row mode (rows_dumps): every tensor leaf with a batch dim becomes leaf[row], narrowed per `trims`
+  int64_t row = -1;
+  const Trims* trims = nullptr;
+  std::string path;
 
   void scalar(py::handle o) {
     header += "{\"__v__\": ";
@@ -162,10 +169,24 @@ struct Encoder {
     header += "]}";
   }
 
+  at::Tensor row_view(const at::Tensor& t0) const {
+    if (t0.dim() == 0) return t0;
+    at::Tensor t = t0.select(0, row);
+    if (trims) {
+      auto it = trims->find(path);
+      if (it != trims->end())
+        for (const auto& dl : it->second) {
+          const int64_t d = dl.first, len = dl.second[static_cast<size_t>(row)];
+          if (d < t.dim()) t = t.narrow(d, 0, std::max<int64_t>(0, std::min(len, t.size(d))));
+        }
+    }
+    return t;
+  }
+
   void node(py::handle o) {
     PyObject* p = o.ptr();
     if (THPVariable_Check(p)) {
-      tensor(THPVariable_Unpack(p));
+      tensor(row >= 0 ? row_view(THPVariable_Unpack(p)) : THPVariable_Unpack(p));
     } else if (PyDict_Check(p)) {
       header += "{\"__d__\": [";
       PyObject *k, *v;
@@ -186,7 +207,15 @@ struct Encoder {
           throw py::type_error("tree_dumps: dict keys must be str or int");
         }
         header += ", ";
-        node(v);
+        if (row >= 0) {
+          const size_t keep = path.size();
+          if (!path.empty()) path += '/';
+          path += py::str(k).cast<std::string>();
+          node(v);
+          path.resize(keep);
+        } else {
+          node(v);
+        }
         header += "]";
       }
       header += "]}";
@@ -402,10 +431,32 @@ struct Decoder {
   }
 };
 
+py::bytes frame_of(Encoder& enc);
+
 py::bytes tree_dumps(py::handle tree) {
   Encoder enc;
   enc.header.reserve(8192);
   enc.node(tree);
+  return frame_of(enc);
+}
+
+// one reply frame per batch row: row i of every batched tensor leaf (0-d leaves and non-tensor leaves as they
+// are), leaf paths in `trims` narrowed to per-row lengths - the inference server's decollate + encode in one pass
+std::vector<py::bytes> rows_dumps(py::handle tree, int64_t n, const Trims& trims) {
+  std::vector<py::bytes> out;
+  out.reserve(static_cast<size_t>(n));
+  for (int64_t i = 0; i < n; ++i) {
+    Encoder enc;
+    enc.header.reserve(4096);
+    enc.row = i;
+    enc.trims = &trims;
+    enc.node(tree);
+    out.push_back(frame_of(enc));
+  }
+  return out;
+}
+
+py::bytes frame_of(Encoder& enc) {
   const int64_t hlen = static_cast<int64_t>(enc.header.size());
   const int64_t pre = static_cast<int64_t>(kMagicLen) + 9;
   const int64_t pad = (kAlign - (pre + hlen) % kAlign) % kAlign;
@@ -726,6 +777,8 @@ void register_codec(py::module& m) {
   m.def("tree_dumps", &tree_dumps, "tensor tree -> applestar frame (uncompressed)");
   m.def("tree_loads", &tree_loads, py::arg("data"), py::arg("copy") = true,
         "applestar frame -> tensor tree (copy=False: tensors alias the buffer)");
+  m.def("rows_dumps", &rows_dumps, py::arg("tree"), py::arg("n"), py::arg("trims"),
+        "one frame per batch row (row i of every batched leaf, per-path per-row narrowing)");
   m.def("collate_frames", &collate_frames, py::arg("frames"), py::arg("pad_entities") = 0,
         py::arg("device") = py::none(), py::arg("buckets") = std::vector<int64_t>{}, "B request frames -> collated batch (one pinned staging buffer, one H2D)");
 }

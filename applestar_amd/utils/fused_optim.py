@@ -139,8 +139,19 @@ class FusedClipAdam:
         if self.device_hparams:
             if self._hp is None:
                 self._hp = torch.zeros(3, dtype=torch.float32, device=self._part.device)
-            # pageable source: the runtime stages it before returning, so the host value can change next step
-            self._hp.copy_(torch.tensor(self._host_hp[:3], dtype=torch.float32), non_blocking=False)
+                # a ring of pinned host slots: the upload is an async DMA on the step's stream (a pageable copy
+                # would block the host until the previous step finished - no host / GPU overlap at all)
+                self._hp_host = torch.empty(8, 3, dtype=torch.float32, pin_memory=True)
+                self._hp_events = [None] * 8
+                self._hp_slot = 0
+            i = self._hp_slot
+            self._hp_slot = (i + 1) % 8
+            if self._hp_events[i] is not None:
+                self._hp_events[i].synchronize()       # the DMA that last read this slot (8 steps ago) is done
+            self._hp_host[i, 0], self._hp_host[i, 1], self._hp_host[i, 2] = self._host_hp[:3]
+            self._hp.copy_(self._hp_host[i], non_blocking=True)
+            ev = self._hp_events[i] = self._hp_events[i] or torch.cuda.Event()
+            ev.record()
         self._prepared = True
 
     @torch.no_grad()
