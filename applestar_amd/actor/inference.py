@@ -106,6 +106,7 @@ class InferenceServer:
         self._graphed: Dict[tuple, object] = {}
         self._runners: Dict[tuple, torch.nn.Module] = {}
         self.max_wait = max_wait_ms / 1000.0
+        self.max_busy_wait = 0.05       # cap on collecting behind an in-flight batch (seconds)
         self.amp_dtype = amp_dtype if self.device.type == 'cuda' else None
         self.models: Dict[str, torch.nn.Module] = {}
         self.teachers: Dict[str, torch.nn.Module] = {}
@@ -280,7 +281,10 @@ class InferenceServer:
         self.stats['reply_s'] += time.perf_counter() - t0
         self.stats['served_s'] += time.perf_counter() - L.t0
 
-    def _collect(self, timeout: float) -> Dict[tuple, List[Tuple[Connection, bytes]]]:
+    def _collect(self, timeout: float, busy=None) -> Dict[tuple, List[Tuple[Connection, bytes]]]:
+        """Requests that arrived.  ``busy``: the GPU is still running the in-flight batch - keep collecting
+        (the next batch could not start earlier anyway) until it finishes, every live pipe has asked, or
+        ``max_busy_wait`` passed: under load the batches grow by themselves, which makes every row cheaper."""
         with self._lock:
             conns = list(self._conns)
         groups: Dict[tuple, List] = defaultdict(list)
@@ -288,10 +292,23 @@ class InferenceServer:
             if timeout > 0:
                 time.sleep(timeout)
             return groups
-        ready = wait(conns, timeout=timeout)
-        if not ready:
-            return groups
         pending: Dict[Connection, bytes] = {}
+        if busy is not None:
+            t_end = time.time() + self.max_busy_wait
+            while busy() and len(pending) < len(self._conns) and time.time() < t_end:
+                for c in wait([c for c in conns if c not in pending and c in self._conns], timeout=0.0005):
+                    try:
+                        pending[c] = c.recv_bytes()
+                    except (EOFError, OSError):
+                        with self._lock:
+                            if c in self._conns:
+                                self._conns.remove(c)
+                                self._routes.pop(c, None)
+            ready = [c for c in wait([c for c in conns if c not in pending], timeout=0.0)]
+        else:
+            ready = wait(conns, timeout=timeout)
+        if not ready and not pending:
+            return groups
         deadline = time.time() + (self.max_wait if timeout > 0 else 0.0)
         while True:
             for c in ready:
@@ -323,7 +340,11 @@ class InferenceServer:
     def serve_once(self, timeout: float = 0.1) -> int:
         """Collect one dynamic batch per route and launch it; finish (reply to) the batches launched on the
         previous call.  Returns the number of requests launched."""
-        groups = self._collect(0.0 if self._inflight else timeout)
+        busy = None
+        if self._inflight and self._inflight[-1].event is not None:
+            ev = self._inflight[-1].event
+            busy = lambda: not ev.query()
+        groups = self._collect(0.0 if self._inflight else timeout, busy)
         prev = list(self._inflight)
         self._inflight.clear()
         served = 0

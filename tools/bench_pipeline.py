@@ -146,8 +146,11 @@ def main():
                'groups_per_s': round(sd.get('batches', 0) / dt, 1),
                'mean_group_rows': round(sd.get('requests', 0) / max(sd.get('batches', 0), 1), 2),
                'ms_per_group': {k[:-2]: round(1e3 * sd.get(k, 0) / max(sd.get('batches', 0), 1), 3)
-                                for k in ('forward_s', 'collate_h2d_s', 'launch_s', 'd2h_wait_s', 'decollate_s')},
-               'busy_fraction': round(sd.get('forward_s', 0) / dt, 3)},
+                                for k in ('collate_h2d_s', 'launch_s', 'd2h_wait_s', 'decollate_s', 'reply_s',
+                                          'served_s')},
+               'host_busy_fraction': round(sum(sd.get(k, 0) for k in ('collate_h2d_s', 'launch_s', 'decollate_s',
+                                                                       'reply_s')) / dt, 3)},
+           'cpus': os.cpu_count(),
            'data': 'FakeSC2Env observations, random-init policy; learner reuses each trajectory 2x (reference)'}
     print(json.dumps(out), flush=True)
     lp.terminate()
