@@ -120,6 +120,18 @@ def run_learner(args, precision, rank, world, device, host_batches):
     if world > 1:
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     elapsed = float(t.item())
+    replicas = None
+    if world > 1:
+        # after the timed region: every rank's weights (fp32 masters in the bf16 step) and last gradient norm
+        # must be bit-identical - the data-parallel invariant - checked with one small all-gather
+        with torch.no_grad():
+            flat = trainer.master.master.detach() if trainer.master is not None else \
+                torch.cat([p.detach().reshape(-1) for p in trainer.params])
+            fp = torch.stack([(flat.view(torch.int32).long() * 2654435761 % (1 << 31)).sum(),
+                              info['gradient'].detach().reshape(()).double().view(torch.int64)]).to(device)
+        allfp = [torch.zeros_like(fp) for _ in range(world)]
+        torch.distributed.all_gather(allfp, fp)
+        replicas = all(torch.equal(allfp[0], f) for f in allfp[1:])
     gpu_ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(args.steps)] if gpu else []
     host_ms = [1000.0 * h for h in host_t]
     if rank == 0:
@@ -133,6 +145,7 @@ def run_learner(args, precision, rank, world, device, host_batches):
         'step_ms_max': max(gpu_ms) if gpu_ms else None,
         'step_ms_median': sorted(gpu_ms)[len(gpu_ms) // 2] if gpu_ms else None,
         'final_loss': loss,
+        'replicas_identical': replicas,
         'peak_mem_gb': (torch.cuda.max_memory_allocated(device) / 2 ** 30) if gpu else None,
         'graph_step': ({'captures': trainer.graph.captures, 'replays': trainer.graph.replays,
                         'eager_steps': trainer.graph.eager_steps}
@@ -241,7 +254,7 @@ def main():
                        'step_ms_min': r['step_ms_min'] and round(r['step_ms_min'], 3),
                        'step_ms_median': r['step_ms_median'] and round(r['step_ms_median'], 3),
                        'step_ms_max': r['step_ms_max'] and round(r['step_ms_max'], 3),
-                       'final_loss': r['final_loss'],
+                       'final_loss': r['final_loss'], 'replicas_identical': r['replicas_identical'],
                        'peak_mem_gb': r['peak_mem_gb'] and round(r['peak_mem_gb'], 2)}
 
         head = precisions[0]
