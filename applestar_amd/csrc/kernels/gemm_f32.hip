@@ -361,6 +361,89 @@ __global__ __launch_bounds__(256, 3) void gemm_f32_pipe_kernel(const float* __re
   pipe::store_tile<C::FM, C::FN>(acc, out, bias, res, M, N, m0 + wm * C::TM, n0 + wn * C::TN, act);
 }
 
+// Few-row products: fewer than 128 of the pipe kernel's 128 x 64 tiles (the heads, the scalar encoder and the
+// value projections on ~400 rows; the location head's 1-row-per-sample GEMVs).  There the 128-row tile leaves
+// most of the chip idle and the library's smallest kernels floor at ~19 us per call.  Here a 256-thread
+// workgroup owns one 32 x 32 output tile and its four waves split the reduction (wave w takes K-steps w, w + 4,
+// ...): operands stream from global memory (L2-resident at these sizes) straight into registers, KU K-steps of
+// loads in flight per wave, no LDS staging; the four partial tiles meet once in LDS and wave 0 applies the same
+// fused epilogue (bias, ReLU, residual, ReLU-mask) - so a linear's bias / ReLU / ReLU-mask hand-off work here too.
+//   lane (l32, h): A row m0 + l32 and B row n0 + l32, the 8 floats at k = 16 kt + 8 h .. + 7 of K-step kt;
+//   split mode: one bf16x6 product per K-step (k-slots 8 h .. 8 h + 7 of lane half h);
+//   exact mode: eight v_mfma_f32_32x32x2_f32, instruction t pairing k = 16 kt + 8 h + t on both operands.
+// The accumulator is the transposed tile (lane = output row), stored by pipe::store_tile.
+template <int KU, int SPLIT>
+__global__ __launch_bounds__(256) void gemm_f32_small_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                                                             const float* __restrict__ bias,
+                                                             const float* __restrict__ res, float* __restrict__ out,
+                                                             long M, int N, int K, int act, int tiles_n) {
+  __shared__ float red[3][16][64];
+  const int tn = blockIdx.x % tiles_n;
+  const long tm = blockIdx.x / tiles_n;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+  const long m = tm * 32 + l32;
+  const int n = tn * 32 + l32;
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a), 0,
+                                                                      static_cast<int>(M * K * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), 0,
+                                                                      static_cast<int>(static_cast<long>(N) * K * 4),
+                                                                      0x00020000);
+  const int a_row = m < M ? static_cast<int>(m * K) * 4 : -1;
+  const int b_row = n < N ? n * K * 4 : -1;
+  const int KT = (K + 15) / 16;
+  // pieces past K (K % 4 == 0) or of rows past M / N read zeros (out-of-range buffer offset)
+  auto off = [&](int row, int kt, int q) {
+    const int k = 16 * kt + 8 * h + 4 * q;
+    return row >= 0 && k < K ? row + 4 * k : kOOB;
+  };
+  float4 ra[KU][2], rb[KU][2];
+  auto load = [&](int u, int kt) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const auto va = __builtin_amdgcn_raw_buffer_load_b128(ar, off(a_row, kt, q), 0, 0);
+      const auto vb = __builtin_amdgcn_raw_buffer_load_b128(br, off(b_row, kt, q), 0, 0);
+      ra[u][q] = make_float4(__uint_as_float(va[0]), __uint_as_float(va[1]), __uint_as_float(va[2]),
+                             __uint_as_float(va[3]));
+      rb[u][q] = make_float4(__uint_as_float(vb[0]), __uint_as_float(vb[1]), __uint_as_float(vb[2]),
+                             __uint_as_float(vb[3]));
+    }
+  };
+  // this wave's K-steps: w, w + 4, w + 8, ...
+  const int nk = KT > w ? (KT - w + 3) / 4 : 0;
+#pragma unroll
+  for (int u = 0; u < KU; ++u) load(u, w + 4 * u);
+  f16v acc[1][1];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[0][0][e] = 0.f;
+  for (int i0 = 0; i0 < nk; i0 += KU) {
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      if (i0 + u >= nk) break;
+      const float va[8] = {ra[u][0].x, ra[u][0].y, ra[u][0].z, ra[u][0].w,
+                           ra[u][1].x, ra[u][1].y, ra[u][1].z, ra[u][1].w};
+      const float vb[8] = {rb[u][0].x, rb[u][0].y, rb[u][0].z, rb[u][0].w,
+                           rb[u][1].x, rb[u][1].y, rb[u][1].z, rb[u][1].w};
+      load(u, w + 4 * (i0 + u + KU));     // refill the slot just read (zeros past the last K-step)
+      if constexpr (SPLIT) {
+        acc[0][0] = mfma_x6(split8(vb), split8(va), acc[0][0]);
+      } else {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(vb[t], va[t], acc[0][0], 0, 0, 0);
+      }
+    }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[w - 1][e][lane] = acc[0][0][e];
+  }
+  __syncthreads();
+  if (w == 0) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[0][0][e] += red[0][e][lane] + red[1][e][lane] + red[2][e][lane];
+    pipe::store_tile<1, 1>(acc, out, bias, res, M, N, tm * 32, tn * 32, act);
+  }
+}
+
 int pipe_variant() {
   static const int v = [] {
     const char* e = std::getenv("APPLESTAR_F32_PIPE");
@@ -424,8 +507,19 @@ int& mode_ref() {
 int f32_mfma_mode() { return mode_ref(); }
 void set_f32_mfma_mode(int mode) { mode_ref() = mode >= 0 && mode <= 3 ? mode : 1; }
 
+bool gemm_f32_is_small(long M, int N) { return (M + 127) / 128 * ((N + 63) / 64) < 128; }
+
 void gemm_f32(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
               int act, hipStream_t s) {
+  if (gemm_f32_is_small(M, N)) {
+    const int tn = (N + 31) / 32;
+    const dim3 g(static_cast<unsigned>((M + 31) / 32 * tn)), blk(256);
+    if (f32_mfma_mode() == 0)
+      hipLaunchKernelGGL((gemm_f32_small_kernel<4, 0>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act, tn);
+    else
+      hipLaunchKernelGGL((gemm_f32_small_kernel<4, 1>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act, tn);
+    return;
+  }
   const bool deep = gemm_bk() == 32 && K >= 64;
   if (N % 128 == 0 && (M + 127) / 128 * (N / 128) >= 1024) {
     if (deep) launch_gemm<128, 32>(a, b, bias, res, out, M, N, K, act, s);

@@ -1375,15 +1375,17 @@ _WGRAD_MIN_ROWS = 256     # tools/ab_bench.py --variant wgrad_small: -0.7 ms/ste
 
 
 def _gemm_f32_ok(M, N, K):
-    """The f32-MFMA GEMM takes this [M, K] x [N, K]^T product: K % 4, 32-bit buffer offsets, and either enough
-    128-row x 64-column tiles (>= 128) to fill the chip or a short reduction: a few-hundred-row product with
-    K <= 384 runs 5-16 us against the library's ~19 us floor; with K >= 1024 its few tiles each walk the whole K
-    (34 us) and the library stays (tools/bench_small_f32.py, profiles/r3z3_small_f32.jsonl)."""
+    """The native f32 GEMM takes this [M, K] x [N, K]^T product: K % 4 and 32-bit buffer offsets.  Products with
+    >= 128 of its 128 x 64 tiles run the LDS-DMA pipe kernel; fewer (the few-row linears: heads, scalar encoder,
+    value projections) run one wave per 32 x 32 tile straight from L2 (``gemm_f32_small_kernel``), which replaced
+    ~170 library calls per fp32 step (r4) - up to a reduction of ``F32_SMALL_K_MAX`` (the spatial encoder's
+    48,640-wide fc keeps its batched split-K form)."""
     return K % 4 == 0 and M * K * 4 < 0x7ffffff0 and N * K * 4 < 0x7ffffff0 and \
-        ((M + 127) // 128 * ((N + 63) // 64) >= 128 or K <= F32_SMALL_K)
+        ((M + 127) // 128 * ((N + 63) // 64) >= 128 or (F32_SMALL and K <= F32_SMALL_K_MAX))
 
 
-F32_SMALL_K = 0          # tools/ab_bench.py --variant f32_small_gemm: 384 measured +0.38 ms/step (r3z4), off
+F32_SMALL = os.environ.get('APPLESTAR_F32_SMALL_GEMM', '1') == '1'     # A/B switch
+F32_SMALL_K_MAX = 4096
 F32_KPAD = False         # tools/ab_bench.py --variant f32_kpad: neutral (64.06 vs 64.14 ms, r3z4), off
 GEMM_REFORM = os.environ.get('APPLESTAR_GEMM_REFORM', '1') == '1'
 

@@ -1185,12 +1185,10 @@ def test_linear_f32_grads_match_fp64(R, N, K, f32_mfma):
 def test_linear_f32_relu_handoff_matches_fp64(extra_consumer, R, H, f32_mfma, monkeypatch):
     """Chained fp32 linears: the second layer's dX epilogue applies the first layer's ReLU mask and the first
     layer's backward skips its threshold pass (native._premasked); with a second consumer of the hidden
-    activation the summed gradient must take the mask as usual.  Both vs float64.  The few-row case routes its
-    products to gemm_f32 through the small-product switch (off by default: the library wins there in the step,
-    profiles/r3z4_ab_small.jsonl), so the hand-off is exercised on few-row tiles too."""
+    activation the summed gradient must take the mask as usual.  Both vs float64.  The few-row case runs its
+    products on the small-product kernel (gemm_f32_small_kernel), so the hand-off is exercised there too."""
     from applestar_amd.ops import native as NN
-    if R < 1000:
-        monkeypatch.setattr(NN, 'F32_SMALL_K', 384)
+    monkeypatch.setattr(NN, 'F32_SMALL', True)
     torch.manual_seed(6)
     K, O = 256, 256
     x = torch.randn(R, K, device=DEV).requires_grad_()
@@ -1459,6 +1457,27 @@ def test_fused_adam_device_hparams_in_graph():
     for a, b in zip(pa, pb):
         assert torch.equal(a.detach(), b.detach())
     assert float(ob.state[pb[0]]['step']) == 5.0
+
+
+@pytest.mark.parametrize('M,Nc,K', [(390, 256, 256), (384, 1024, 448), (33, 70, 1020), (2047, 130, 4096), (1, 327, 64)])
+@pytest.mark.parametrize('mode', ['bias_relu', 'res_add', 'drelu'])
+def test_gemm_f32_small_epilogues_match_fp64(M, Nc, K, mode, f32_mfma):
+    """gemm_f32 on few-row products (< 128 pipe tiles: one wave per 32 x 32 tile, operands from L2, K tails,
+    ragged M / N edges, K up to 4096) with each epilogue vs float64, in both f32 MFMA modes."""
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(Nc, K, device=DEV) / K ** 0.5
+    bias = 0.1 * torch.randn(Nc, device=DEV)
+    res = torch.randn(M, Nc, device=DEV)
+    C = N.ensure_loaded()
+    ref = a.double() @ b.double().t() + bias.double()
+    if mode == 'bias_relu':
+        got, ref = C.gemm_f32(a, b, bias, None, 1), torch.relu(ref)
+    elif mode == 'res_add':
+        got, ref = C.gemm_f32(a, b, bias, res, 0), ref + res.double()
+    else:
+        got, ref = C.gemm_f32(a, b, bias, res, 4), ref * (res.double() > 0)
+    assert (got.double() - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
 
 
 @pytest.mark.parametrize('M,Nc,K', [(5000, 768, 256), (3001, 256, 1024), (20000, 32, 20), (2500, 96, 132)])

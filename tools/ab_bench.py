@@ -36,7 +36,7 @@ def set_variant(name, on):
         from applestar_amd.models import model
         model.SIDE_STREAMS_ENABLED = on
     elif name == 'f32_small_gemm':
-        native.F32_SMALL_K = 384 if on else 0
+        native.F32_SMALL = on
     elif name == 'f32_kpad':
         native.F32_KPAD = on
     else:

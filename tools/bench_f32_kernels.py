@@ -67,6 +67,17 @@ def main():
             w = torch.randn(128, 3, 3, 128, device='cuda') / 30
             emit('conv3x3_f32_tail', [B, 19, 20, 128, 128, (B * 380 + 127) // 128],
                  timed(lambda: C.conv3x3_f32(x, w, None, None, 0)), 2.0 * B * 380 * 128 * 9 * 128)
+    if which in ('small', 'all'):
+        # few-row products of the fp32 step (heads / scalar encoder / value projections): native small-tile
+        # kernel vs the library
+        for M, N, K in [(384, 256, 384), (384, 1024, 448), (390, 256, 256), (384, 256, 1024), (390, 1024, 64),
+                        (384, 128, 256), (390, 64, 320)]:
+            a = torch.randn(M, K, device='cuda')
+            b = torch.randn(N, K, device='cuda')
+            bias = torch.randn(N, device='cuda')
+            emit('gemm_f32_small', [M, N, K], timed(lambda: C.gemm_f32(a, b, bias, None, 1), 50), 2.0 * M * N * K)
+            emit('torch_fp32_addmm_relu', [M, N, K],
+                 timed(lambda: torch._addmm_activation(bias, a, b.t(), use_gelu=False), 50), 2.0 * M * N * K)
     if which in ('gemm', 'all'):
         for M, N, K in GEMM:
             a = torch.randn(M, K, device='cuda')
