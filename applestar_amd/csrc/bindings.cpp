@@ -965,6 +965,34 @@ at::Tensor gemm_f32(const at::Tensor& a, const at::Tensor& b, const c10::optiona
   return out;
 }
 
+at::Tensor gemm_bf16_small(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
+                           const c10::optional<at::Tensor>& res, int64_t act) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 && b.dim() == 2 &&
+              a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
+              "gemm_bf16_small: bf16 contiguous A [M,K], B [N,K]");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(K % 8 == 0, "gemm_bf16_small: K % 8");
+  TORCH_CHECK(M * K * 2 < 0x7ffffff0LL && N * K * 2 < 0x7ffffff0LL && M * N < (1LL << 31), "gemm_bf16_small: too large");
+  const float* bp = nullptr;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous(), "gemm_bf16_small: fp32 bias");
+    bp = bias->data_ptr<float>();
+  }
+  const void* rp = nullptr;
+  if (res && res->defined()) {
+    TORCH_CHECK(res->scalar_type() == at::kBFloat16 && res->numel() == M * N && res->is_contiguous(),
+                "gemm_bf16_small: bf16 res");
+    rp = res->data_ptr();
+  }
+  c10::hip::HIPGuard g(a.device().index());
+  auto out = at::empty({M, N}, a.options());
+  as::gemm_bf16_small(a.data_ptr(), b.data_ptr(), bp, rp, out.data_ptr(), M, static_cast<int>(N), static_cast<int>(K),
+                      static_cast<int>(act), stream());
+  return out;
+}
+
 std::vector<at::Tensor> wgrad_f32(const at::Tensor& dy, const at::Tensor& x, int64_t cin, bool want_bias) {
   check_cuda(dy, "dy");
   check_cuda(x, "x");
@@ -1708,6 +1736,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fused_adam_chunk", &as::fused_adam_chunk);
   m.def("wgrad_f32", &wgrad_f32);
   m.def("gemm_f32", &gemm_f32);
+  m.def("gemm_bf16_small", &gemm_bf16_small);
   m.def("f32_mfma_mode", &as::f32_mfma_mode);
   m.def("set_f32_mfma_mode", &as::set_f32_mfma_mode);
   m.def("conv3x3_f32_supported", &as::conv3x3_f32_supported);

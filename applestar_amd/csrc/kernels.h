@@ -230,6 +230,9 @@ int wgrad_f32_splits(long R, int N, int K);
 // APPLESTAR_F32_MFMA=exact / regsplit select 0 / 2
 int f32_mfma_mode();
 void set_f32_mfma_mode(int mode);
+// few-row bf16 GEMM (gemm_f32.hip): out [M, N] bf16 = epi(A [M, K] . B [N, K]^T), bf16 A / B / res, fp32 bias; K % 8 == 0
+void gemm_bf16_small(const void* a, const void* b, const float* bias, const void* res, void* out, long M, int N, int K,
+                     int act, hipStream_t s);
 void gemm_f32(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
               int act, hipStream_t s);
 // slice s writes dW at part + s * part_stride ([N][K]) and db at db_part + s * part_stride ([N])

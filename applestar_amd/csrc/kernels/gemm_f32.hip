@@ -444,6 +444,87 @@ __global__ __launch_bounds__(256) void gemm_f32_small_kernel(const float* __rest
   }
 }
 
+// bf16 form of the few-row kernel (the mixed-precision step's heads / scalar encoder / value projections):
+// bf16 operands, one v_mfma_f32_32x32x16_bf16 per K-step, fp32 accumulation and epilogue, bf16 output.
+//   out[m, n] = bf16( act( sum_k A[m, k] B[n, k] + bias[n] (+ res[m, n] | * [res[m, n] > 0]) ) )
+// lane (l32, h): A row m0 + l32 / B row n0 + l32, the 8 bf16 at k = 16 kt + 8 h (one 16-B load each).
+template <int KU>
+__global__ __launch_bounds__(256) void gemm_bf16_small_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                                                              const float* __restrict__ bias,
+                                                              const bf16_t* __restrict__ res, bf16_t* __restrict__ out,
+                                                              long M, int N, int K, int act, int tiles_n) {
+  __shared__ float red[3][16][64];
+  const int tn = blockIdx.x % tiles_n;
+  const long tm = blockIdx.x / tiles_n;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
+  const long m = tm * 32 + l32;
+  const int n = tn * 32 + l32;
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a), 0,
+                                                                      static_cast<int>(M * K * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(b), 0,
+                                                                      static_cast<int>(static_cast<long>(N) * K * 2),
+                                                                      0x00020000);
+  const int a_row = m < M ? static_cast<int>(m * K) * 2 : -1;
+  const int b_row = n < N ? n * K * 2 : -1;
+  const int KT = (K + 15) / 16;
+  auto off = [&](int row, int kt) {
+    const int k = 16 * kt + 8 * h;
+    return row >= 0 && k < K ? row + 2 * k : kOOB;      // K % 8 == 0: a piece never straddles K
+  };
+  u32v4 ra[KU], rb[KU];
+  auto load = [&](int u, int kt) {
+    const auto va = __builtin_amdgcn_raw_buffer_load_b128(ar, off(a_row, kt), 0, 0);
+    const auto vb = __builtin_amdgcn_raw_buffer_load_b128(br, off(b_row, kt), 0, 0);
+    ra[u] = u32v4{va[0], va[1], va[2], va[3]};
+    rb[u] = u32v4{vb[0], vb[1], vb[2], vb[3]};
+  };
+  const int nk = KT > w ? (KT - w + 3) / 4 : 0;
+#pragma unroll
+  for (int u = 0; u < KU; ++u) load(u, w + 4 * u);
+  f16v acc[1][1];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) acc[0][0][e] = 0.f;
+  for (int i0 = 0; i0 < nk; i0 += KU) {
+#pragma unroll
+    for (int u = 0; u < KU; ++u) {
+      if (i0 + u >= nk) break;
+      const u32v4 va = ra[u], vb = rb[u];
+      load(u, w + 4 * (i0 + u + KU));
+      acc[0][0] = mfma_bf16(vb, va, acc[0][0]);
+    }
+  }
+  if (w > 0) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[w - 1][e][lane] = acc[0][0][e];
+  }
+  __syncthreads();
+  if (w != 0) return;
+  // transposed tile: lane = output row m0 + l32, register 4 g + q = column n0 + 8 g + 4 h + q
+  if (m >= M) return;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int n0 = tn * 32 + 8 * g + 4 * h;
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = 4 * g + q;
+      v[q] = acc[0][0][e] + red[0][e][lane] + red[1][e][lane] + red[2][e][lane];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int nn = n0 + q;
+      if (nn >= N) continue;
+      float x = v[q] + (bias ? bias[nn] : 0.f);
+      if (res) {
+        const float r = bf2f(res[m * N + nn]);
+        x = act == ACT_DRELU ? (r > 0.f ? x : 0.f) : x + r;
+      }
+      if (act == ACT_RELU) x = fmaxf(x, 0.f);
+      out[m * N + nn] = f2bf(x);
+    }
+  }
+}
+
 int pipe_variant() {
   static const int v = [] {
     const char* e = std::getenv("APPLESTAR_F32_PIPE");
@@ -506,6 +587,14 @@ int& mode_ref() {
 
 int f32_mfma_mode() { return mode_ref(); }
 void set_f32_mfma_mode(int mode) { mode_ref() = mode >= 0 && mode <= 3 ? mode : 1; }
+
+void gemm_bf16_small(const void* a, const void* b, const float* bias, const void* res, void* out, long M, int N, int K,
+                     int act, hipStream_t s) {
+  const int tn = (N + 31) / 32;
+  hipLaunchKernelGGL((gemm_bf16_small_kernel<4>), dim3(static_cast<unsigned>((M + 31) / 32 * tn)), dim3(256), 0, s,
+                     static_cast<const bf16_t*>(a), static_cast<const bf16_t*>(b), bias,
+                     static_cast<const bf16_t*>(res), static_cast<bf16_t*>(out), M, N, K, act, tn);
+}
 
 bool gemm_f32_is_small(long M, int N) { return (M + 127) / 128 * ((N + 63) / 64) < 128; }
 

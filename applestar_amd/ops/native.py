@@ -1268,6 +1268,10 @@ class _Linear(torch.autograd.Function):
             y = _C.gemm_f32(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None, 1 if relu else 0)
             if relu and RELU_LINK:
                 _note_relu_out(y)
+        elif _bf16_small_ok(x2, R, w.shape[0], K):
+            # bf16 step, few rows: one workgroup per 32 x 32 tile (gemm_bf16_small_kernel), bias + ReLU fused
+            y = _C.gemm_bf16_small(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None,
+                                   1 if relu else 0)
         elif relu and b is not None:
             y = torch._addmm_activation(b, x2, w.t(), use_gelu=False)
         else:
@@ -1313,6 +1317,11 @@ class _Linear(torch.autograd.Function):
                 _MASKED_DX[x2.data_ptr()] = (dx, dx._version)
             else:
                 dx = _C.gemm_f32(dy, _wT(w), None, None if g is None else g.view(dy.shape[0], w.shape[1]), 0)
+        elif (g is not None or ctx.needs_input_grad[0]) and _bf16_small_ok(dy, dy.shape[0], w.shape[1], dy.shape[1]) \
+                and (g is None or g.dtype == torch.bfloat16):
+            # bf16 step, few rows: dX = dY W (+ the handed-over residual gradient) on the small-tile kernel
+            dx = _C.gemm_bf16_small(dy.contiguous(), _wT(w), None,
+                                    None if g is None else g.view(dy.shape[0], w.shape[1]).contiguous(), 0)
         elif g is not None:
             # + the residual gradient the closing LayerNorm handed over (GradLink), in the GEMM epilogue
             # in place: g is the LayerNorm's input gradient, which the branch's later layers (backward
@@ -1385,6 +1394,13 @@ def _gemm_f32_ok(M, N, K):
 
 
 F32_SMALL = os.environ.get('APPLESTAR_F32_SMALL_GEMM', '1') == '1'     # A/B switch
+BF16_SMALL = os.environ.get('APPLESTAR_BF16_SMALL_GEMM', '1') == '1'   # A/B switch
+
+
+def _bf16_small_ok(a, M, N, K):
+    """A bf16 [M, K] x [N, K]^T product for gemm_bf16_small_kernel: few tiles (as the fp32 small path), K % 8."""
+    return BF16_SMALL and a.dtype == torch.bfloat16 and a.is_cuda and K % 8 == 0 and K <= F32_SMALL_K_MAX and \
+        (M + 127) // 128 * ((N + 63) // 64) < 128 and M * K * 2 < 0x7ffffff0 and N * K * 2 < 0x7ffffff0
 F32_SMALL_K_MAX = 4096
 F32_KPAD = False         # tools/ab_bench.py --variant f32_kpad: neutral (64.06 vs 64.14 ms, r3z4), off
 GEMM_REFORM = os.environ.get('APPLESTAR_GEMM_REFORM', '1') == '1'

@@ -1480,6 +1480,49 @@ def test_gemm_f32_small_epilogues_match_fp64(M, Nc, K, mode, f32_mfma):
     assert (got.double() - ref).abs().max().item() < 2e-5 * max(1.0, ref.abs().max().item())
 
 
+@pytest.mark.parametrize('M,Nc,K', [(390, 256, 256), (384, 1024, 448), (33, 72, 1024), (1, 328, 64)])
+@pytest.mark.parametrize('mode', ['bias_relu', 'res_add', 'drelu'])
+def test_gemm_bf16_small_epilogues(M, Nc, K, mode):
+    """gemm_bf16_small (the bf16 step's few-row products): bf16 operands, fp32 accumulation + epilogue, bf16 out,
+    vs float64 of the same bf16 inputs within one bf16 rounding of the result."""
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(Nc, K, device=DEV) / K ** 0.5).bfloat16()
+    bias = 0.1 * torch.randn(Nc, device=DEV)
+    res = torch.randn(M, Nc, device=DEV).bfloat16()
+    C = N.ensure_loaded()
+    ref = a.double() @ b.double().t() + bias.double()
+    if mode == 'bias_relu':
+        got, ref = C.gemm_bf16_small(a, b, bias, None, 1), torch.relu(ref)
+    elif mode == 'res_add':
+        got, ref = C.gemm_bf16_small(a, b, bias, res, 0), ref + res.double()
+    else:
+        got, ref = C.gemm_bf16_small(a, b, bias, res, 4), ref * (res.double() > 0)
+    assert got.dtype == torch.bfloat16
+    err = (got.double() - ref).abs()
+    assert (err <= 2 ** -7 * ref.abs() + 1e-3 * max(1.0, ref.abs().max().item())).all(), err.max().item()
+
+
+def test_bf16_linear_small_path_matches_library(monkeypatch):
+    """A few-row bf16 linear (+ ReLU) through _Linear on the small-tile kernels vs the library path (switch off):
+    forward and all three gradients within bf16 rounding."""
+    from applestar_amd.ops import native as NN
+    torch.manual_seed(7)
+    x0 = torch.randn(384, 448, device=DEV).bfloat16()
+    w0 = (torch.randn(256, 448, device=DEV) / 448 ** 0.5).bfloat16()
+    b0 = (0.1 * torch.randn(256, device=DEV)).bfloat16()
+    g = torch.randn(384, 256, device=DEV).bfloat16()
+    outs = {}
+    for on in (True, False):
+        monkeypatch.setattr(NN, 'BF16_SMALL', on)
+        x, w, b = (t.clone().requires_grad_() for t in (x0, w0, b0))
+        y = NN.linear(x, w, b, act='relu')
+        y.backward(g)
+        outs[on] = [t.float() for t in (y, x.grad, w.grad, b.grad)]
+    for name, a, r in zip(('y', 'dx', 'dw', 'db'), outs[True], outs[False]):
+        assert (a - r).norm() <= 1e-2 * r.norm(), (name, float((a - r).norm() / r.norm()))
+
+
 @pytest.mark.parametrize('M,Nc,K', [(5000, 768, 256), (3001, 256, 1024), (20000, 32, 20), (2500, 96, 132)])
 @pytest.mark.parametrize('mode', ['bias_relu', 'res_add', 'drelu'])
 def test_gemm_f32_epilogues_match_fp64(M, Nc, K, mode, f32_mfma):
