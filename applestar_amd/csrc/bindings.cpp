@@ -1602,9 +1602,10 @@ void multi_copy(const std::vector<at::Tensor>& dsts, const std::vector<at::Tenso
     const at::Tensor& d = dsts[i];
     const at::Tensor& s = srcs[i];
     TORCH_CHECK(d.is_cuda() && s.is_cuda() && d.sizes() == s.sizes(), "multi_copy: GPU tensors of equal shape");
+    const bool same = d.scalar_type() == s.scalar_type();
     const bool ok = d.strides() == s.strides() && d.is_non_overlapping_and_dense() &&
-                    (d.scalar_type() == at::kFloat || d.scalar_type() == at::kBFloat16) &&
-                    (s.scalar_type() == at::kFloat || s.scalar_type() == at::kBFloat16);
+                    (same || ((d.scalar_type() == at::kFloat || d.scalar_type() == at::kBFloat16) &&
+                              (s.scalar_type() == at::kFloat || s.scalar_type() == at::kBFloat16)));
     if (!ok) {
       at::Tensor dd = d;
       dd.copy_(s);
@@ -1612,13 +1613,20 @@ void multi_copy(const std::vector<at::Tensor>& dsts, const std::vector<at::Tenso
     }
     const long n = d.numel();
     if (n == 0) continue;
-    // storage-order copy: the lowest address of a non-overlapping dense tensor is its data_ptr
+    // storage-order copy: the lowest address of a non-overlapping dense tensor is its data_ptr; equal dtypes
+    // (any dtype) travel as raw bytes
     const int t = a.ntensors++;
     a.src[t] = s.data_ptr();
     a.dst[t] = d.data_ptr();
-    a.n[t] = n;
-    a.dts[t] = static_cast<unsigned char>((s.scalar_type() == at::kFloat ? 1 : 0) | (d.scalar_type() == at::kFloat ? 2 : 0));
-    a.chunk_start[t + 1] = a.chunk_start[t] + static_cast<int>((n + as::kCopyChunk - 1) / as::kCopyChunk);
+    if (same) {
+      a.n[t] = n * static_cast<long>(d.element_size());
+      a.dts[t] = 4;
+      a.chunk_start[t + 1] = a.chunk_start[t] + static_cast<int>((a.n[t] + as::kCopyRawChunk - 1) / as::kCopyRawChunk);
+    } else {
+      a.n[t] = n;
+      a.dts[t] = static_cast<unsigned char>((s.scalar_type() == at::kFloat ? 1 : 0) | (d.scalar_type() == at::kFloat ? 2 : 0));
+      a.chunk_start[t + 1] = a.chunk_start[t] + static_cast<int>((n + as::kCopyChunk - 1) / as::kCopyChunk);
+    }
     if (a.ntensors == as::kCopyMaxT) flush();
   }
   flush();

@@ -266,13 +266,14 @@ int wgrad_splits(long R, int N, int K);
 // ---- multi_copy.hip ----------------------------------------------------------------------------
 constexpr int kCopyMaxT = 64;
 constexpr long kCopyChunk = 8192;
+constexpr long kCopyRawChunk = 65536;  // bytes per workgroup in raw mode (a multiple of 16)
 struct CopyArgs {                     // passed by value (< 2 KB of kernel arguments)
   int ntensors;
-  int chunk_start[kCopyMaxT + 1];     // prefix sums of ceil(n / kCopyChunk)
+  int chunk_start[kCopyMaxT + 1];     // prefix sums of ceil(n / kCopyChunk) (raw: ceil(n / kCopyRawChunk))
   const void* src[kCopyMaxT];
   void* dst[kCopyMaxT];
-  long n[kCopyMaxT];
-  unsigned char dts[kCopyMaxT];       // bit 0: src fp32, bit 1: dst fp32 (else bf16)
+  long n[kCopyMaxT];                  // elements (raw: bytes)
+  unsigned char dts[kCopyMaxT];       // bit 0: src fp32, bit 1: dst fp32 (else bf16), bit 2: raw bytes, same dtype
 };
 void multi_copy(const CopyArgs& a, hipStream_t s);
 

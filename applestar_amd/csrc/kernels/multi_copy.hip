@@ -14,11 +14,25 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyArgs a) {
   const int b = blockIdx.x;
   int t = 0;
   while (t + 1 < a.ntensors && a.chunk_start[t + 1] <= b) ++t;
+  const void* src = a.src[t];
+  void* dst = a.dst[t];
+  if (a.dts[t] & 4) {
+    // raw bytes (any dtype, n in bytes): 16-byte words when both ends and the length are 16-aligned
+    const long i0 = static_cast<long>(b - a.chunk_start[t]) * kCopyRawChunk;
+    const long i1 = i0 + kCopyRawChunk < a.n[t] ? i0 + kCopyRawChunk : a.n[t];
+    const auto* s8 = static_cast<const unsigned char*>(src);
+    auto* d8 = static_cast<unsigned char*>(dst);
+    if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | a.n[t]) & 15) == 0) {
+      for (long i = i0 + 16 * threadIdx.x; i < i1; i += 16 * 256)
+        *reinterpret_cast<uint4*>(d8 + i) = *reinterpret_cast<const uint4*>(s8 + i);
+    } else {
+      for (long i = i0 + threadIdx.x; i < i1; i += 256) d8[i] = s8[i];
+    }
+    return;
+  }
   const long i0 = static_cast<long>(b - a.chunk_start[t]) * kCopyChunk;
   const long i1 = i0 + kCopyChunk < a.n[t] ? i0 + kCopyChunk : a.n[t];
   const bool sf = (a.dts[t] & 1) != 0, df = (a.dts[t] & 2) != 0;
-  const void* src = a.src[t];
-  void* dst = a.dst[t];
   for (long i = i0 + threadIdx.x; i < i1; i += 256) {
     const float v = sf ? static_cast<const float*>(src)[i] : bf2f(static_cast<const bf16_t*>(src)[i]);
     if (df) static_cast<float*>(dst)[i] = v;

@@ -52,17 +52,32 @@ def _tree_clone(x):
     return x
 
 
-def _tree_copy_(dst, src, path='batch'):
+def _tree_pairs(dst, src, out, path='batch'):
     if torch.is_tensor(dst):
         if dst.shape != src.shape or dst.dtype != src.dtype:
             raise ValueError(f'{path}: {tuple(src.shape)}/{src.dtype} != captured {tuple(dst.shape)}/{dst.dtype}')
-        dst.copy_(src, non_blocking=True)
+        out.append((dst, src))
     elif isinstance(dst, dict):
         for k in dst:
-            _tree_copy_(dst[k], src[k], f'{path}.{k}')
+            _tree_pairs(dst[k], src[k], out, f'{path}.{k}')
     elif isinstance(dst, (list, tuple)):
         for i, (a, b) in enumerate(zip(dst, src)):
-            _tree_copy_(a, b, f'{path}[{i}]')
+            _tree_pairs(a, b, out, f'{path}[{i}]')
+    return out
+
+
+def _tree_copy_(dst, src):
+    """Refresh the captured input tensors from a new batch.  A learner batch has ~130 leaves: copied one by
+    one that is ~130 blit launches per replay (rocprof r4n: 1.1 ms of copyBuffer per bf16 step), so device
+    leaves go through the native multi-tensor copy (raw bytes, 64 leaves per launch)."""
+    dev, rest = [], []
+    for d, s in _tree_pairs(dst, src, []):
+        (dev if d.is_cuda and s.is_cuda and d.device == s.device else rest).append((d, s))
+    if dev:
+        from ..ops import native
+        native.ensure_loaded().multi_copy([d for d, _ in dev], [s for _, s in dev])
+    for d, s in rest:
+        d.copy_(s, non_blocking=True)
 
 
 def batch_signature(x):

@@ -40,6 +40,8 @@ class FusedClipAdam:
     the hyperparameter upload); :meth:`step` calls it unless a HIP graph is being captured, in which case the
     owner calls it before every replay."""
 
+    HP_RING = 32       # pinned host slots of the device-hyperparameter upload (see prepare)
+
     def __init__(self, optimizer: torch.optim.Optimizer, max_norm: Optional[float], clip=None,
                  device_hparams: bool = False, segments: Optional[Dict] = None):
         self.opt = optimizer
@@ -51,7 +53,14 @@ class FusedClipAdam:
         self._host_hp = None
         self._table = None
         self._sig = None
+        self._steps = None
+        self._pending = 0          # steps not yet added to the per-parameter ``step`` tensors (see hparams)
         self._prepared = False
+        # the per-parameter counters are written lazily: before anyone reads the optimizer's state dict, and
+        # dropped when a state dict is loaded over them
+        if hasattr(optimizer, 'register_state_dict_pre_hook'):
+            optimizer.register_state_dict_pre_hook(lambda opt: self.sync_steps())
+            optimizer.register_load_state_dict_pre_hook(lambda opt, sd: self._drop_pending())
 
     @staticmethod
     def supported(optimizer, clip) -> bool:
@@ -69,7 +78,18 @@ class FusedClipAdam:
     def _params(self):
         return [p for p in self.opt.param_groups[0]['params'] if p.requires_grad]
 
+    def sync_steps(self):
+        """Write the pending step increments into the optimizer's per-parameter ``step`` tensors."""
+        if self._pending and self._steps is not None:
+            for t in self._steps:
+                t += float(self._pending)
+        self._pending = 0
+
+    def _drop_pending(self):
+        self._pending = 0
+
     def _build(self, params):
+        self.sync_steps()
         from ..ops import native
         C = native.ensure_loaded()
         chunk = C.fused_adam_chunk()
@@ -98,6 +118,7 @@ class FusedClipAdam:
         self._chunks = torch.tensor(chunks, dtype=torch.int64, device=dev)
         self._part = torch.empty(len(chunks) // 2, dtype=torch.float32, device=dev)
         self._scale = torch.ones(self.ntensors, dtype=torch.float32, device=dev)
+        self._steps = [st[p]['step'] for p in params]
         self._C = C
 
     def _signature(self, params):
@@ -119,10 +140,17 @@ class FusedClipAdam:
         g = self.opt.param_groups[0]
         params = self._params()
         st = self.opt.state
-        step = float(st[params[0]]['step']) + 1.0 if 'step' in st[params[0]] else 1.0
-        for p in params:
-            if 'step' in st[p]:
-                st[p]['step'] += 1.0
+        # the per-parameter step counters (torch.optim.Adam's state layout, kept for checkpoints) advance lazily:
+        # ~470 scalar CPU tensor adds per step were ~2-4 ms of host time (a foreach add is no faster on the CPU)
+        if self._steps is not None and len(self._steps) == len(params) and hasattr(self.opt, 'register_state_dict_pre_hook'):
+            step = float(self._steps[0]) + self._pending + 1.0
+            self._pending += 1
+        else:
+            self.sync_steps()
+            step = float(st[params[0]]['step']) + 1.0 if 'step' in st[params[0]] else 1.0
+            for p in params:
+                if 'step' in st[p]:
+                    st[p]['step'] += 1.0
         b1, b2 = g['betas']
         lr, wd = float(g['lr']), float(g['weight_decay'])
         decoupled = bool(getattr(self.opt, '_decoupled_wd', 0.0)) or isinstance(self.opt, torch.optim.AdamW)
@@ -140,14 +168,16 @@ class FusedClipAdam:
             if self._hp is None:
                 self._hp = torch.zeros(3, dtype=torch.float32, device=self._part.device)
                 # a ring of pinned host slots: the upload is an async DMA on the step's stream (a pageable copy
-                # would block the host until the previous step finished - no host / GPU overlap at all)
-                self._hp_host = torch.empty(8, 3, dtype=torch.float32, pin_memory=True)
-                self._hp_events = [None] * 8
+                # would block the host until the previous step finished - no host / GPU overlap at all).  The ring
+                # bounds how far the host may run ahead of the GPU: 32 steps (with 8, a graphed step's host
+                # blocked here after 8 replays and its issue time read as ~0.55 of the GPU step instead of ~0.1)
+                self._hp_host = torch.empty(self.HP_RING, 3, dtype=torch.float32, pin_memory=True)
+                self._hp_events = [None] * self.HP_RING
                 self._hp_slot = 0
             i = self._hp_slot
-            self._hp_slot = (i + 1) % 8
+            self._hp_slot = (i + 1) % self.HP_RING
             if self._hp_events[i] is not None:
-                self._hp_events[i].synchronize()       # the DMA that last read this slot (8 steps ago) is done
+                self._hp_events[i].synchronize()       # the DMA that last read this slot (HP_RING steps ago) is done
             self._hp_host[i, 0], self._hp_host[i, 1], self._hp_host[i, 2] = self._host_hp[:3]
             self._hp.copy_(self._hp_host[i], non_blocking=True)
             ev = self._hp_events[i] = self._hp_events[i] or torch.cuda.Event()

@@ -672,6 +672,56 @@ def test_multi_copy_converts_and_handles_many_tensors():
         assert torch.equal(d, s.to(d.dtype)), (d.shape, d.dtype, s.dtype)
 
 
+def test_multi_copy_raw_bytes_any_dtype():
+    """Equal-dtype pairs travel as raw bytes (the graph step's batch refresh): int64 / int32 / bool / uint8 /
+    fp16 / fp32 leaves, odd byte counts and views at unaligned offsets (byte path), > 64 MB leaves (many
+    chunks), one launch per 64 leaves."""
+    from applestar_amd.ops import native
+    from applestar_amd.runtime.step_graph import _tree_copy_
+    C = native.ensure_loaded()
+    torch.manual_seed(18)
+    srcs, dsts = [], []
+    big = torch.randint(-2 ** 40, 2 ** 40, (9 * 10 ** 6,), device=DEV)      # 72 MB
+    srcs.append(big)
+    dsts.append(torch.empty_like(big))
+    base_u8 = torch.randint(0, 255, (10 ** 5,), device=DEV, dtype=torch.uint8)
+    dst_u8 = torch.zeros(10 ** 5 + 64, device=DEV, dtype=torch.uint8)
+    for i in range(140):
+        kind = i % 6
+        n = int(torch.randint(1, 3000, ()).item())
+        if kind == 0:
+            s = torch.randint(-10 ** 9, 10 ** 9, (n,), device=DEV)
+        elif kind == 1:
+            s = torch.randint(-10 ** 6, 10 ** 6, (n, 3), device=DEV, dtype=torch.int32)
+        elif kind == 2:
+            s = torch.rand(n, device=DEV) > 0.5
+        elif kind == 3:                                  # unaligned source and destination views
+            o = int(torch.randint(1, 15, ()).item())
+            s = base_u8[o:o + n]
+            dsts.append(dst_u8[o + 3:o + 3 + n])
+            srcs.append(s)
+            continue
+        elif kind == 4:
+            s = torch.randn(n, device=DEV).half()
+        else:
+            s = torch.randn(n, 2, device=DEV)
+        srcs.append(s)
+        dsts.append(torch.empty_like(s))
+    C.multi_copy(dsts, srcs)
+    torch.cuda.synchronize()
+    for d, s in zip(dsts, srcs):
+        assert torch.equal(d, s), (d.shape, d.dtype)
+    # the graph step's tree refresh: nested dict/list of device leaves + a host leaf
+    src = {'a': [torch.arange(7, device=DEV), torch.ones(3, 4, device=DEV, dtype=torch.bool)],
+           'b': {'c': torch.randn(5, device=DEV)}, 'h': torch.arange(3)}
+    dst = {'a': [torch.zeros(7, device=DEV, dtype=torch.long), torch.zeros(3, 4, device=DEV, dtype=torch.bool)],
+           'b': {'c': torch.zeros(5, device=DEV)}, 'h': torch.zeros(3, dtype=torch.long)}
+    _tree_copy_(dst, src)
+    torch.cuda.synchronize()
+    assert torch.equal(dst['a'][0], src['a'][0]) and torch.equal(dst['a'][1], src['a'][1])
+    assert torch.equal(dst['b']['c'], src['b']['c']) and torch.equal(dst['h'], src['h'])
+
+
 @pytest.mark.parametrize('cin,cout,act', [(16, 16, 'relu'), (32, 8, None), (8, 32, 'relu')])
 def test_pointwise_conv1x1_matches_fp32(cin, cout, act):
     from applestar_amd import ops
@@ -1341,6 +1391,7 @@ def test_fused_clip_adam_matches_torch(max_norm, wd):
         assert abs(float(na) - float(nb)) <= 1e-5 * float(na)
         for a, b in zip(pa, pb):
             assert _err(a, b) < 1e-6 * max(1.0, a.abs().max().item()), step
+    ob.state_dict()                  # the fused step's per-parameter counters are written lazily, before a state read
     for a, b in zip(pa, pb):
         assert torch.allclose(oa.state[a]['exp_avg_sq'], ob.state[b]['exp_avg_sq'], rtol=1e-5, atol=1e-12)
         assert float(oa.state[a]['step']) == float(ob.state[b]['step']) == 4.0
@@ -1456,6 +1507,7 @@ def test_fused_adam_device_hparams_in_graph():
     torch.cuda.synchronize()
     for a, b in zip(pa, pb):
         assert torch.equal(a.detach(), b.detach())
+    ob.state_dict()
     assert float(ob.state[pb[0]]['step']) == 5.0
 
 

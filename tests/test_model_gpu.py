@@ -312,6 +312,7 @@ def test_graphed_train_step_matches_eager(amp):
                                       'lstm split timeout flag', lstm_err))
     torch.cuda.synchronize()
     assert graphed.graph.captures == 2 and graphed.graph.replays == 3 and graphed.graph.eager_steps == 2
+    eager.optimizer.state_dict(), graphed.optimizer.state_dict()   # lazy per-parameter step counters written
     st_e = eager.optimizer.state[eager.opt_params[0]]['step']
     st_g = graphed.optimizer.state[graphed.opt_params[0]]['step']
     assert float(st_e) == float(st_g) == 5.0

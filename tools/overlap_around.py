@@ -13,7 +13,8 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 pat = re.compile(sys.argv[2])
 top = int(sys.argv[3]) if len(sys.argv) > 3 else 8
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-opt = [i for i, r in enumerate(rows) if 'FusedOpti' in r['Kernel_Name'] or 'fused_adam' in r['Kernel_Name'].lower()]
+opt = [i for i, r in enumerate(rows) if 'FusedOpti' in r['Kernel_Name'] or 'fused_adam' in r['Kernel_Name'].lower()
+       or 'mt_adam_kernel' in r['Kernel_Name']]
 ends = []
 for i in opt:
     if not ends or i > ends[-1] + 5:

@@ -6,7 +6,8 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-opt_idx = [i for i, r in enumerate(rows) if 'FusedOpti' in r['Kernel_Name'] or 'fused_adam' in r['Kernel_Name'].lower()]
+opt_idx = [i for i, r in enumerate(rows) if 'FusedOpti' in r['Kernel_Name'] or 'fused_adam' in r['Kernel_Name'].lower()
+           or 'mt_adam_kernel' in r['Kernel_Name']]
 # iteration = kernels after the second-to-last optimizer burst up to the last one
 ends = []
 for i in opt_idx:
