@@ -965,8 +965,8 @@ at::Tensor gemm_f32(const at::Tensor& a, const at::Tensor& b, const c10::optiona
   return out;
 }
 
-at::Tensor gemm_bf16_small(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
-                           const c10::optional<at::Tensor>& res, int64_t act) {
+at::Tensor gemm_bf16_impl(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
+                          const c10::optional<at::Tensor>& res, int64_t act, bool small_only) {
   check_cuda(a, "a");
   check_cuda(b, "b");
   TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && a.dim() == 2 && b.dim() == 2 &&
@@ -988,9 +988,131 @@ at::Tensor gemm_bf16_small(const at::Tensor& a, const at::Tensor& b, const c10::
   }
   c10::hip::HIPGuard g(a.device().index());
   auto out = at::empty({M, N}, a.options());
-  as::gemm_bf16_small(a.data_ptr(), b.data_ptr(), bp, rp, out.data_ptr(), M, static_cast<int>(N), static_cast<int>(K),
-                      static_cast<int>(act), stream());
+  if (small_only)
+    as::gemm_bf16_small(a.data_ptr(), b.data_ptr(), bp, rp, out.data_ptr(), M, static_cast<int>(N),
+                        static_cast<int>(K), static_cast<int>(act), stream());
+  else
+    as::gemm_bf16(a.data_ptr(), b.data_ptr(), bp, rp, out.data_ptr(), M, static_cast<int>(N), static_cast<int>(K),
+                  static_cast<int>(act), stream());
   return out;
+}
+
+// few-row kernel only / size-dispatched (LDS-DMA ring for >= 128 tiles)
+at::Tensor gemm_bf16_small(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
+                           const c10::optional<at::Tensor>& res, int64_t act) {
+  return gemm_bf16_impl(a, b, bias, res, act, true);
+}
+at::Tensor gemm_bf16(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
+                     const c10::optional<at::Tensor>& res, int64_t act) {
+  return gemm_bf16_impl(a, b, bias, res, act, false);
+}
+
+// ---------------------------------------------------------------- few-row products of any shape (gemm_small.hip)
+// out [M, N] = epi(mask(a) . b^T): a [M, K], b [N, K] (fp32 or bf16, same dtype), fp32 bias [N], res [M, N] and
+// amask [M, K] in a's dtype; mask_mode / act: as::Act codes (mask: 0 none, 1 ReLU, 2 sigmoid of the saved output)
+at::Tensor small_gemm(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
+                      const c10::optional<at::Tensor>& res, const c10::optional<at::Tensor>& amask, int64_t mask_mode,
+                      int64_t act) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  const bool bf = a.scalar_type() == at::kBFloat16;
+  TORCH_CHECK((bf || a.scalar_type() == at::kFloat) && b.scalar_type() == a.scalar_type() && a.dim() == 2 &&
+                  b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
+              "small_gemm: contiguous A [M,K], B [N,K] of one dtype (fp32 / bf16)");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(M * K < (1LL << 31) && N * K < (1LL << 31) && M * N < (1LL << 31), "small_gemm: too large");
+  TORCH_CHECK(mask_mode >= 0 && mask_mode <= 2 && (act == 0 || act == 1 || act == 2 || act == 4), "small_gemm: codes");
+  const float* bp = nullptr;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous() && bias->is_cuda(),
+                "small_gemm: fp32 bias [N]");
+    bp = bias->data_ptr<float>();
+  }
+  const void* rp = nullptr;
+  if (res && res->defined()) {
+    TORCH_CHECK(res->scalar_type() == a.scalar_type() && res->numel() == M * N && res->is_contiguous() && res->is_cuda(),
+                "small_gemm: res [M, N] in A's dtype");
+    rp = res->data_ptr();
+  }
+  TORCH_CHECK(act != 4 || rp != nullptr, "small_gemm: the DRELU epilogue masks by res");
+  const void* mp = nullptr;
+  if (amask && amask->defined() && mask_mode > 0) {
+    TORCH_CHECK(amask->scalar_type() == a.scalar_type() && amask->numel() == M * K && amask->is_contiguous() &&
+                    amask->is_cuda(), "small_gemm: amask [M, K] in A's dtype");
+    mp = amask->data_ptr();
+  }
+  c10::hip::HIPGuard g(a.device().index());
+  auto out = at::empty({M, N}, a.options());
+  as::small_nt(a.data_ptr(), b.data_ptr(), bp, rp, mp, static_cast<int>(mask_mode), out.data_ptr(), M,
+               static_cast<int>(N), static_cast<int>(K), static_cast<int>(act), bf, stream());
+  return out;
+}
+
+// few rows, long K (the spatial encoder's 48,640-wide fc): split-K over S workgroup slices + an ordered sum with
+// the bias / act epilogue (deterministic); S == 1 -> the one-pass kernel
+at::Tensor small_gemm_splitk(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
+                             int64_t act) {
+  check_cuda(a, "a");
+  check_cuda(b, "b");
+  const bool bf = a.scalar_type() == at::kBFloat16;
+  TORCH_CHECK((bf || a.scalar_type() == at::kFloat) && b.scalar_type() == a.scalar_type() && a.dim() == 2 &&
+                  b.dim() == 2 && a.is_contiguous() && b.is_contiguous() && a.size(1) == b.size(1),
+              "small_gemm_splitk: contiguous A [M,K], B [N,K] of one dtype (fp32 / bf16)");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(M * K < (1LL << 31) && N * K < (1LL << 31) && M * N < (1LL << 28), "small_gemm_splitk: too large");
+  TORCH_CHECK(act == 0 || act == 1 || act == 2, "small_gemm_splitk: act code");
+  const float* bp = nullptr;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous() && bias->is_cuda(),
+                "small_gemm_splitk: fp32 bias [N]");
+    bp = bias->data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(a.device().index());
+  auto out = at::empty({M, N}, a.options());
+  const int S = as::small_nt_splits(M, static_cast<int>(N), static_cast<int>(K));
+  if (S <= 1) {
+    as::small_nt(a.data_ptr(), b.data_ptr(), bp, nullptr, nullptr, 0, out.data_ptr(), M, static_cast<int>(N),
+                 static_cast<int>(K), static_cast<int>(act), bf, stream());
+    return out;
+  }
+  auto part = at::empty({S, M, N}, a.options().dtype(at::kFloat));
+  as::small_nt_splitk(a.data_ptr(), b.data_ptr(), bp, part.data_ptr<float>(), S, out.data_ptr(), M,
+                      static_cast<int>(N), static_cast<int>(K), static_cast<int>(act), bf, stream());
+  return out;
+}
+
+// dW [N, K] = mask(dy)^T . x and db [N] = column sums of mask(dy) over R rows (dy [R, N], x [R, K], ymask [R, N]:
+// the layer output whose activation gradient masks dy); dW / db in bf16 when out_bf16 (bf16 inputs only)
+std::vector<at::Tensor> small_wgrad(const at::Tensor& dy, const at::Tensor& x, const c10::optional<at::Tensor>& ymask,
+                                    int64_t mask_mode, bool want_bias, bool out_bf16) {
+  check_cuda(dy, "dy");
+  check_cuda(x, "x");
+  const bool bf = dy.scalar_type() == at::kBFloat16;
+  TORCH_CHECK((bf || dy.scalar_type() == at::kFloat) && x.scalar_type() == dy.scalar_type() && dy.dim() == 2 &&
+                  x.dim() == 2 && dy.is_contiguous() && x.is_contiguous() && dy.size(0) == x.size(0),
+              "small_wgrad: contiguous dy [R, N], x [R, K] of one dtype");
+  TORCH_CHECK(!out_bf16 || bf, "small_wgrad: bf16 output needs bf16 inputs");
+  TORCH_CHECK(mask_mode >= 0 && mask_mode <= 2, "small_wgrad: mask code");
+  const int64_t R = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(R * N < (1LL << 31) && R * K < (1LL << 31) && N * K < (1LL << 31), "small_wgrad: too large");
+  const void* mp = nullptr;
+  if (ymask && ymask->defined() && mask_mode > 0) {
+    TORCH_CHECK(ymask->scalar_type() == dy.scalar_type() && ymask->numel() == R * N && ymask->is_contiguous() &&
+                    ymask->is_cuda(), "small_wgrad: ymask [R, N] in dy's dtype");
+    mp = ymask->data_ptr();
+  }
+  c10::hip::HIPGuard g(dy.device().index());
+  auto opts = out_bf16 ? dy.options() : dy.options().dtype(at::kFloat);
+  auto dw = at::empty({N, K}, opts);
+  at::Tensor db = want_bias ? at::empty({N}, opts) : at::Tensor();
+  if (R == 0) {
+    dw.zero_();
+    if (want_bias) db.zero_();
+    return {dw, db};
+  }
+  as::small_tn(dy.data_ptr(), x.data_ptr(), mp, static_cast<int>(mask_mode), dw.data_ptr(),
+               want_bias ? db.data_ptr() : nullptr, R, static_cast<int>(N), static_cast<int>(K), bf, out_bf16, stream());
+  return {dw, db};
 }
 
 std::vector<at::Tensor> wgrad_f32(const at::Tensor& dy, const at::Tensor& x, int64_t cin, bool want_bias) {
@@ -1745,6 +1867,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_f32", &wgrad_f32);
   m.def("gemm_f32", &gemm_f32);
   m.def("gemm_bf16_small", &gemm_bf16_small);
+  m.def("gemm_bf16", &gemm_bf16);
+  m.def("small_gemm", &small_gemm);
+  m.def("small_wgrad", &small_wgrad);
+  m.def("small_gemm_splitk", &small_gemm_splitk);
   m.def("f32_mfma_mode", &as::f32_mfma_mode);
   m.def("set_f32_mfma_mode", &as::set_f32_mfma_mode);
   m.def("conv3x3_f32_supported", &as::conv3x3_f32_supported);

@@ -101,12 +101,22 @@ __device__ __forceinline__ Split3 frag(const char* stage, int r, int p0) {
   return split8(v);
 }
 
+// bf16 fragment: the 8 bf16 (one 16-B slot, piece p) of LDS row r (the bf16 form of the ring: a stage row holds
+// 2 BK bf16, piece p = k 8 p .. 8 p + 7)
+template <class C>
+__device__ __forceinline__ u32v4 frag_bf16(const char* stage, int r, int p) {
+  const uint4 u = *reinterpret_cast<const uint4*>(stage + r * C::RB + 16 * C::slot_of(r, p));
+  return u32v4{u.x, u.y, u.z, u.w};
+}
+
 // The main loop.  ASrc / BSrc: (chunk index within the wave's share, K-step) -> byte offset of this lane's 16-B
 // piece (the piece is column slot_of(row, lane & 3) of row 16 chunk + lane / 4), or kOOB.  smem: NS stage arrays
 // (separate __shared__ objects) and the loop unrolled by NS, so every DMA target and every fragment read names a
 // compile-time stage: with one array and a runtime stage index the compiler cannot tell the DMA just issued from
 // the stage being read and drains the DMA queue (s_waitcnt vmcnt(0)) before every K-step's first ds_read.
-template <class C, class ASrc, class BSrc>
+// BF16: the ring carries bf16 operands (a stage row = 2 BK bf16 = BK / 8 chunks of 16): plain bf16 MFMAs on
+// one fragment read per operand and chunk, no split (gemm_bf16.hip).
+template <class C, class ASrc, class BSrc, bool BF16 = false>
 __device__ __forceinline__ void mainloop(char* const (&smem)[C::NS], i32x4 ar, i32x4 br, int KT, const ASrc& asrc,
                                          const BSrc& bsrc, f16v (&acc)[C::FM][C::FN]) {
   constexpr int NS = C::NS;
@@ -131,6 +141,21 @@ __device__ __forceinline__ void mainloop(char* const (&smem)[C::NS], i32x4 ar, i
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     issue(next, kt + NS - 1);
+    if constexpr (BF16) {
+#pragma unroll
+      for (int c = 0; c < C::BK / 8; ++c) {
+        u32v4 fa[C::FM], fb[C::FN];
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i) fa[i] = frag_bf16<C>(st, wm * C::TM + 32 * i + l32, 2 * c + h);
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) fb[j] = frag_bf16<C>(st + C::BM * C::RB, wn * C::TN + 32 * j + l32, 2 * c + h);
+#pragma unroll
+        for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::FN; ++j) acc[i][j] = mfma_bf16(fb[j], fa[i], acc[i][j]);
+      }
+      return;
+    }
 #pragma unroll
     for (int c = 0; c < C::BK / 16; ++c) {
     // chunk c of lane half h: columns 16 c + 8 h .. + 7 = the MFMA's k-slots 8 h .. 8 h + 7
@@ -221,6 +246,100 @@ __device__ __forceinline__ void store_tile(const f16v (&acc)[FM][FN], float* __r
             if (act == ACT_RELU) x = fmaxf(x, 0.f);
             orow[n + q] = x;
           }
+        }
+      }
+    }
+  }
+}
+
+// Epilogue through LDS (after the main loop; `lds` >= 32 x BN floats, e.g. one ring stage): the tile is written
+// 32 rows at a time into LDS (float4 granules XOR-swizzled by row: the 32 lanes of a fragment column hit 16
+// distinct 4-bank groups) and read back row-major, so each thread finishes 8 consecutive columns of one row
+// and 16 / 32 lanes store one contiguous row segment (the register layout stores one 8- / 16-B piece per row
+// and lane: every store instruction touched 64 rows).  Bias / residual / ReLU / ReLU-mask as store_tile.
+template <class C, typename TO>
+__device__ __forceinline__ void store_tile_staged(const f16v (&acc)[C::FM][C::FN], char* lds, TO* __restrict__ out,
+                                                  const float* __restrict__ bias, const TO* __restrict__ res, long M,
+                                                  int N, long m0, int n0, int act) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int l32 = lane & 31, h = lane >> 5;
+  constexpr int G = C::BN / 4;            // float4 granules per staged row
+  constexpr int CPR = C::BN / 8;          // 8-column pieces per row
+  float* t = reinterpret_cast<float*>(lds);
+  const bool vec = (N & 7) == 0;
+#pragma unroll 1
+  for (int pass = 0; pass < C::WM * C::FM; ++pass) {
+    const int pw = pass / C::FM, pi = pass % C::FM;     // tile rows pw TM + 32 pi .. + 31
+    __syncthreads();                                     // the ring / the previous pass is no longer read
+    if (wm == pw) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        if (i != pi) continue;
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int gr = (wn * C::TN + 32 * j + 8 * g + 4 * h) / 4;
+            *reinterpret_cast<float4*>(t + (l32 * G + (gr ^ (l32 % G))) * 4) =
+                make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+          }
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < 32 * CPR; c += 256) {
+      const int r = c / CPR, cc = c % CPR;
+      const long m = m0 + pw * C::TM + 32 * pi + r;
+      const int n = n0 + 8 * cc;
+      if (m >= M || n >= N) continue;
+      const float4 u0 = *reinterpret_cast<const float4*>(t + (r * G + ((2 * cc) ^ (r % G))) * 4);
+      const float4 u1 = *reinterpret_cast<const float4*>(t + (r * G + ((2 * cc + 1) ^ (r % G))) * 4);
+      float v[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      TO* orow = out + m * N;
+      const TO* rrow = res ? res + m * N : nullptr;
+      if (vec) {
+        if (bias) {
+          const float4 b0 = *reinterpret_cast<const float4*>(bias + n), b1 = *reinterpret_cast<const float4*>(bias + n + 4);
+          v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+        }
+        if (rrow) {
+          float r8[8];
+          if constexpr (sizeof(TO) == 2) {
+            const uint4 rv = *reinterpret_cast<const uint4*>(rrow + n);
+            const unsigned rw[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              r8[2 * q] = __uint_as_float(rw[q] << 16);
+              r8[2 * q + 1] = __uint_as_float(rw[q] & 0xffff0000u);
+            }
+          } else {
+            const float4 r0 = *reinterpret_cast<const float4*>(rrow + n), r1 = *reinterpret_cast<const float4*>(rrow + n + 4);
+            r8[0] = r0.x; r8[1] = r0.y; r8[2] = r0.z; r8[3] = r0.w; r8[4] = r1.x; r8[5] = r1.y; r8[6] = r1.z; r8[7] = r1.w;
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = act == ACT_DRELU ? (r8[q] > 0.f ? v[q] : 0.f) : v[q] + r8[q];
+        }
+        if (act == ACT_RELU)
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q], 0.f);
+        if constexpr (sizeof(TO) == 2) {
+          *reinterpret_cast<uint4*>(orow + n) =
+              make_uint4(f2bf2(v[0], v[1]), f2bf2(v[2], v[3]), f2bf2(v[4], v[5]), f2bf2(v[6], v[7]));
+        } else {
+          *reinterpret_cast<float4*>(orow + n) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(orow + n + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          if (n + q >= N) continue;
+          float x = v[q] + (bias ? bias[n + q] : 0.f);
+          if (rrow) {
+            const float r = Cvt<TO>::load(rrow, n + q);
+            x = act == ACT_DRELU ? (r > 0.f ? x : 0.f) : x + r;
+          }
+          if (act == ACT_RELU) x = fmaxf(x, 0.f);
+          Cvt<TO>::store(orow, n + q, x);
         }
       }
     }

@@ -230,9 +230,28 @@ int wgrad_f32_splits(long R, int N, int K);
 // APPLESTAR_F32_MFMA=exact / regsplit select 0 / 2
 int f32_mfma_mode();
 void set_f32_mfma_mode(int mode);
+// few-row products of any shape (gemm_small.hip), fp32 (split / exact per f32_mfma_mode) or bf16:
+//   small_nt: out [M, N] = epi(mask(A) [M, K] . B [N, K]^T); epi: + bias (fp32) (+ res | DRELU mask by res), act
+//             RELU / SIGMOID; mask(A) = A * act'(amask) for mask_mode RELU / SIGMOID (amask: the layer output y)
+//   small_tn: dW [N, K] = mask(dY)^T . X over R rows (dY [R, N], X [R, K]), db [N] = column sums of mask(dY)
+void small_nt(const void* a, const void* b, const float* bias, const void* res, const void* amask, int mask_mode,
+              void* out, long M, int N, int K, int act, bool bf16, hipStream_t s);
+// split-K form for few tiles and a long K (> 4096): S slices write fp32 partial tiles part [S, M, N], then one
+// pass sums them in slice order with the bias / act epilogue; small_nt_splits: S (1 = use small_nt)
+int small_nt_splits(long M, int N, int K);
+void small_nt_splitk(const void* a, const void* b, const float* bias, float* part, int S, void* out, long M, int N,
+                     int K, int act, bool bf16, hipStream_t s);
+void small_tn(const void* dy, const void* x, const void* ymask, int mask_mode, void* dw, void* db, long R, int N,
+              int K, bool bf16_in, bool bf16_out, hipStream_t s);
 // few-row bf16 GEMM (gemm_f32.hip): out [M, N] bf16 = epi(A [M, K] . B [N, K]^T), bf16 A / B / res, fp32 bias; K % 8 == 0
 void gemm_bf16_small(const void* a, const void* b, const float* bias, const void* res, void* out, long M, int N, int K,
                      int act, hipStream_t s);
+// fewer than 128 tiles of 128 x 64: the few-row kernels (gemm_f32_small / gemm_bf16_small) take the product
+bool gemm_f32_is_small(long M, int N);
+// bf16 GEMM (gemm_bf16.hip): out [M, N] bf16 = epi(A [M, K] . B [N, K]^T), bf16 A / B / res, fp32 bias; K % 8 == 0;
+// LDS-DMA ring (f32_pipe.h, bf16 form), or gemm_bf16_small for few tiles
+void gemm_bf16(const void* a, const void* b, const float* bias, const void* res, void* out, long M, int N, int K,
+               int act, hipStream_t s);
 void gemm_f32(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
               int act, hipStream_t s);
 // slice s writes dW at part + s * part_stride ([N][K]) and db at db_part + s * part_stride ([N])

@@ -294,7 +294,7 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
 
 // split-MFMA mode: the LDS-DMA ring of f32_pipe.h with the A rows gathered per tap (a lane's DMA piece is 4
 // channels of its row's shifted pixel; taps outside the image read zeros through the buffer range check)
-template <int BN, int NS, int BM = 128>
+template <int BN, int NS, int BM = 128, bool STAGED = false>
 __global__ __launch_bounds__(256, BM == 128 ? 3 : 2) void conv3x3_f32_pipe_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                                const float* __restrict__ bias,
                                                                const float* __restrict__ res, float* __restrict__ out,
@@ -347,8 +347,20 @@ __global__ __launch_bounds__(256, BM == 128 ? 3 : 2) void conv3x3_f32_pipe_kerne
   auto bsrc = [&](int c, int kt) { return b_off[c] >= 0 && kt < KT ? b_off[c] + kt * 64 : pipe::kOOB; };
   f16v acc[C::FM][C::FN];
   pipe::mainloop<C>(smem, xr, wr, KT, asrc, bsrc, acc);
-  const int wm = wid / C::WN, wn = wid % C::WN;
-  pipe::store_tile<C::FM, C::FN>(acc, out, bias, res, M, Cout, m0 + wm * C::TM, n0 + wn * C::TN, act);
+  if constexpr (STAGED) {
+    pipe::store_tile_staged<C, float>(acc, smem[0], out, bias, res, M, Cout, m0, n0, act);
+  } else {
+    const int wm = wid / C::WN, wn = wid % C::WN;
+    pipe::store_tile<C::FM, C::FN>(acc, out, bias, res, M, Cout, m0 + wm * C::TM, n0 + wn * C::TN, act);
+  }
+}
+
+bool conv_f32_staged() {
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_F32_STAGED");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
 }
 
 template <int BN>
@@ -358,7 +370,10 @@ void launch_f32(const float* x, const float* w, const float* bias, const float* 
   const long nwg = (M + 127) / 128 * ((Cout + BN - 1) / BN);
   if (nwg == 0) return;
   const int mode = f32_mfma_mode();
-  if (mode == 1)
+  if (mode == 1 && conv_f32_staged())
+    hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<BN, 3, 128, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x,
+                       w, bias, res, out, B, H, W, Cin, Cout, act);
+  else if (mode == 1)
     hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<BN, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias,
                        res, out, B, H, W, Cin, Cout, act);
   else if (mode == 3)

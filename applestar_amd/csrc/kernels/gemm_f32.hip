@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 }
 
 // split-MFMA mode: LDS-DMA ring + register split (f32_pipe.h)
-template <int BN, int NS, int BK>
+template <int BN, int NS, int BK, bool STAGED = false>
 __global__ __launch_bounds__(256, 3) void gemm_f32_pipe_kernel(const float* __restrict__ a, const float* __restrict__ b,
                                                             const float* __restrict__ bias,
                                                             const float* __restrict__ res, float* __restrict__ out,
@@ -357,8 +357,20 @@ __global__ __launch_bounds__(256, 3) void gemm_f32_pipe_kernel(const float* __re
   };
   f16v acc[C::FM][C::FN];
   pipe::mainloop<C>(smem, ar, br, (K + BK - 1) / BK, asrc, bsrc, acc);
-  const int wm = wid / C::WN, wn = wid % C::WN;
-  pipe::store_tile<C::FM, C::FN>(acc, out, bias, res, M, N, m0 + wm * C::TM, n0 + wn * C::TN, act);
+  if constexpr (STAGED) {
+    pipe::store_tile_staged<C, float>(acc, smem[0], out, bias, res, M, N, m0, n0, act);
+  } else {
+    const int wm = wid / C::WN, wn = wid % C::WN;
+    pipe::store_tile<C::FM, C::FN>(acc, out, bias, res, M, N, m0 + wm * C::TM, n0 + wn * C::TN, act);
+  }
+}
+
+bool f32_staged() {
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_F32_STAGED");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
 }
 
 // Few-row products: fewer than 128 of the pipe kernel's 128 x 64 tiles (the heads, the scalar encoder and the
@@ -543,7 +555,11 @@ void launch_pipe(const float* a, const float* b, const float* bias, const float*
   switch (pipe_variant()) {
     case 1: hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 4, 16>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act); break;
     case 2: hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 2, 32>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act); break;
-    default: hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 3, 16>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act);
+    default:
+      if (f32_staged())
+        hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 3, 16, true>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act);
+      else
+        hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 3, 16>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act);
   }
 }
 

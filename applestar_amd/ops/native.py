@@ -1253,7 +1253,15 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x2, w, b, relu, link=None):
         ctx.link = link
         R, K = x2.shape
-        if GEMM_REFORM and R <= 2048 and K >= 16384 and K % (32 * 8) == 0:
+        if SMALL_NATIVE and x2.is_cuda and R <= 2048 and K > F32_SMALL_K_MAX and \
+                (R + 127) // 128 * ((w.shape[0] + 63) // 64) < 128 and R * K < (1 << 31) and w.shape[0] * K < (1 << 31):
+            # few rows, long reduction (the spatial encoder's 48,640 -> 256 fc, the location head's 12,160 -> 128):
+            # split-K over workgroup slices + one ordered sum with the bias / ReLU epilogue (gemm_small.hip),
+            # in the operands' precision
+            y = _C.small_gemm_splitk(x2, w.detach().contiguous(), _w32(b) if b is not None else None, 1 if relu else 0)
+            if relu and y.dtype == torch.float32 and RELU_LINK:
+                _note_relu_out(y)
+        elif GEMM_REFORM and R <= 2048 and K >= 16384 and K % (32 * 8) == 0:
             # few rows, huge reduction (the spatial encoder's 48640 -> 256 fc): the library ran a 256x16 tile
             # over the whole K (0.14-0.30 ms); 32 K-chunks as one batched GEMM + an fp32 sum: 48 us
             S = 32
@@ -1272,6 +1280,10 @@ class _Linear(torch.autograd.Function):
             # bf16 step, few rows: one workgroup per 32 x 32 tile (gemm_bf16_small_kernel), bias + ReLU fused
             y = _C.gemm_bf16_small(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None,
                                    1 if relu else 0)
+        elif _bf16_pipe_ok(x2, R, w.shape[0], K):
+            # bf16 step, many rows (the entity transformer, the pointer heads' key MLPs): the LDS-DMA ring kernel
+            # (gemm_bf16.hip), bias + ReLU in its epilogue
+            y = _C.gemm_bf16(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None, 1 if relu else 0)
         elif relu and b is not None:
             y = torch._addmm_activation(b, x2, w.t(), use_gelu=False)
         else:
@@ -1322,6 +1334,11 @@ class _Linear(torch.autograd.Function):
             # bf16 step, few rows: dX = dY W (+ the handed-over residual gradient) on the small-tile kernel
             dx = _C.gemm_bf16_small(dy.contiguous(), _wT(w), None,
                                     None if g is None else g.view(dy.shape[0], w.shape[1]).contiguous(), 0)
+        elif (g is not None or ctx.needs_input_grad[0]) and _bf16_pipe_ok(dy, dy.shape[0], w.shape[1], dy.shape[1]) \
+                and (g is None or g.dtype == torch.bfloat16) and not (g is None and dy.shape[1] == 32):
+            # bf16 step, many rows: dX = dY W (+ the handed-over residual gradient) on the LDS-DMA ring kernel
+            dx = _C.gemm_bf16(dy.contiguous(), _wT(w), None,
+                              None if g is None else g.view(dy.shape[0], w.shape[1]).contiguous(), 0)
         elif g is not None:
             # + the residual gradient the closing LayerNorm handed over (GradLink), in the GEMM epilogue
             # in place: g is the LayerNorm's input gradient, which the branch's later layers (backward
@@ -1402,6 +1419,18 @@ def _bf16_small_ok(a, M, N, K):
     return BF16_SMALL and a.dtype == torch.bfloat16 and a.is_cuda and K % 8 == 0 and K <= F32_SMALL_K_MAX and \
         (M + 127) // 128 * ((N + 63) // 64) < 128 and M * K * 2 < 0x7ffffff0 and N * K * 2 < 0x7ffffff0
 F32_SMALL_K_MAX = 4096
+BF16_PIPE = os.environ.get('APPLESTAR_BF16_GEMM', '1') != '0'          # A/B switch ('all': every shape)
+BF16_PIPE_ALL = os.environ.get('APPLESTAR_BF16_GEMM', '1') == 'all'
+
+
+def _bf16_pipe_ok(a, M, N, K):
+    """A bf16 [M, K] x [N, K]^T product of >= 128 tiles for gemm_bf16.hip: K % 8, 32-bit byte offsets.  Shapes with
+    K >= 256 and N >= 256 over many rows (the entity transformer's projections / FFN, both directions) stay on
+    hipBLASLt, which measured 1.0-1.5x faster there (profiles/r4o_gemm_bf16_vs_hipblaslt.jsonl); the native kernel
+    wins the thin-output and few-row products (N or K <= 128: 0.5-0.93x the library's time)."""
+    return BF16_PIPE and a.dtype == torch.bfloat16 and a.is_cuda and K % 8 == 0 and K < 16384 and \
+        M * K * 2 < 0x7ffffff0 and N * K * 2 < 0x7ffffff0 and M * N < (1 << 31) and \
+        (M + 127) // 128 * ((N + 63) // 64) >= 128 and (BF16_PIPE_ALL or not (K >= 256 and N >= 256 and M > 2048))
 F32_KPAD = False         # tools/ab_bench.py --variant f32_kpad: neutral (64.06 vs 64.14 ms, r3z4), off
 GEMM_REFORM = os.environ.get('APPLESTAR_GEMM_REFORM', '1') == '1'
 
@@ -1489,6 +1518,41 @@ class _SmallLinear(torch.autograd.Function):
         return dx, dw, db, None
 
 
+SMALL_NATIVE = os.environ.get('APPLESTAR_SMALL_NATIVE', '1') == '1'     # A/B switch
+_MASK = {None: 0, 'relu': 1, 'sigmoid': 2}
+
+
+class _SmallLinearNative(torch.autograd.Function):
+    """act(x W^T + b) over a few rows for ANY K / N (gemm_small.hip), fp32 or bf16: forward one launch with the
+    bias and ReLU / sigmoid in the epilogue; backward two launches - dX = mask(dY) W against the transposed
+    weight form, dW and db in one TN kernel - where mask(dY) = dY * act'(y) is applied as dY is loaded (no
+    threshold pass, no ones-row GEMV).  Replaces the library path of the odd-width scalar-encoder / head /
+    value layers and the GLU gates (three library GEMMs + one or two elementwise passes per layer)."""
+
+    @staticmethod
+    def forward(ctx, x2, w, b, act):
+        y = _C.small_gemm(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None, None, 0, _ACT[act])
+        ctx.save_for_backward(x2, w, y if act else None)
+        ctx.act, ctx.has_b = act, b is not None
+        ctx.b_dtype = b.dtype if b is not None else None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, y = ctx.saved_tensors
+        dy = dy.to(x2.dtype).contiguous()
+        mode = _MASK[ctx.act]
+        dx = _C.small_gemm(dy, _wT(w), None, None, y, mode, 0) if ctx.needs_input_grad[0] else None
+        bf = x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+        dw, db = _C.small_wgrad(dy, x2, y, mode, ctx.has_b, bf)
+        return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if ctx.has_b else None), None
+
+
+def _small_native_ok(x, R, N, K, act):
+    return SMALL_NATIVE and x.is_cuda and act in _MASK and 0 < R < _SMALL_LINEAR_ROWS and N > 0 and K > 0 and \
+        R * K < (1 << 31) and R * N < (1 << 31)
+
+
 def linear(x, w, b=None, act=None, grad_link=None):
     """bf16 act(x W^T + b) over the last dim of x with the native weight gradient when the row count is
     large; other shapes take F.linear (+ the activation).  ``grad_link``: a :class:`GradLink` the residual
@@ -1506,6 +1570,14 @@ def linear(x, w, b=None, act=None, grad_link=None):
             wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
             bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
             y = _LinearSplitK.apply(xb, wb, bb, act == 'relu')
+        return y.view(*x.shape[:-1], N)
+    if lowp and _small_native_ok(x, R, N, K, act) and (R < _WGRAD_MIN_ROWS or N % 8 or K % 8 or act == 'sigmoid'):
+        # few rows, odd widths or a sigmoid gate: the native any-shape kernels both ways (gemm_small.hip)
+        ensure_loaded()
+        with torch.autocast('cuda', enabled=False):
+            xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
+            wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
+            y = _SmallLinearNative.apply(xb, wb, b, act)
         return y.view(*x.shape[:-1], N)
     if lowp and x.is_cuda and act in (None, 'relu') and R < _SMALL_LINEAR_ROWS and \
             (R < _WGRAD_MIN_ROWS or N % 8 or K % 8):
@@ -1526,6 +1598,12 @@ def linear(x, w, b=None, act=None, grad_link=None):
         else:
             x2 = x.reshape(R, K).contiguous()
         y = _Linear.apply(x2, w, b, act == 'relu', link)
+        return y.view(*x.shape[:-1], N)
+    if not lowp and x.dtype == torch.float32 and w.dtype == torch.float32 and (b is None or b.dtype == torch.float32) \
+            and _small_native_ok(x, R, N, K, act):
+        # fp32, few rows with odd widths / under the split-R threshold, or a sigmoid gate (gemm_small.hip)
+        ensure_loaded()
+        y = _SmallLinearNative.apply(x.reshape(R, K).contiguous(), w, b, act)
         return y.view(*x.shape[:-1], N)
     if F32_KPAD and not lowp and x.is_cuda and K % 4 and R < _SMALL_LINEAR_ROWS and act in (None, 'relu') and \
             x.dtype == torch.float32 and w.dtype == torch.float32:

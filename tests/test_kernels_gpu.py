@@ -1575,6 +1575,178 @@ def test_bf16_linear_small_path_matches_library(monkeypatch):
         assert (a - r).norm() <= 1e-2 * r.norm(), (name, float((a - r).norm() / r.norm()))
 
 
+_SMALL_SHAPES = [(390, 128, 167, 'relu'), (390, 64, 10, 'relu'), (384, 327, 256, None), (384, 2, 256, None),
+                 (390, 1, 256, None), (384, 256, 448, 'sigmoid'), (100, 77, 33, 'relu'), (1, 5, 7, None),
+                 (3000, 129, 131, 'sigmoid'), (390, 64, 269, 'relu')]
+
+
+def _count_small(monkeypatch):
+    from applestar_amd.ops import native as NN
+    C = NN.ensure_loaded()
+    calls = {'nt': 0, 'tn': 0}
+
+    class _Wrap:
+        def __getattr__(self, k):
+            return getattr(C, k)
+
+        def small_gemm(self, *a):
+            calls['nt'] += 1
+            return C.small_gemm(*a)
+
+        def small_wgrad(self, *a):
+            calls['tn'] += 1
+            return C.small_wgrad(*a)
+    monkeypatch.setattr(NN, '_C', _Wrap())
+    return calls
+
+
+@pytest.mark.parametrize('R,Nc,K,act', _SMALL_SHAPES)
+def test_small_linear_native_fp32_matches_fp64(R, Nc, K, act, f32_mfma, monkeypatch):
+    """Few-row fp32 linears of any shape (odd K / N, sigmoid gates) on gemm_small.hip: forward (bias + act in the
+    epilogue), dX (activation gradient applied as dY is loaded) and the TN dW + db kernel, vs float64."""
+    from applestar_amd.ops import native as NN
+    calls = _count_small(monkeypatch)
+    torch.manual_seed(R + K)
+    x = torch.randn(R, K, device=DEV).requires_grad_()
+    w = (torch.randn(Nc, K, device=DEV) / K ** 0.5).requires_grad_()
+    b = (0.1 * torch.randn(Nc, device=DEV)).requires_grad_()
+    y = NN.linear(x, w, b, act=act)
+    xs, ws, bs = _f64(x), _f64(w), _f64(b)
+    yr = xs @ ws.t() + bs
+    yr = torch.relu(yr) if act == 'relu' else (torch.sigmoid(yr) if act == 'sigmoid' else yr)
+    assert _err(y.cpu(), yr) < 1e-5 * max(1.0, yr.abs().max().item())
+    g = torch.randn(yr.shape, dtype=torch.float64)
+    y.backward(g.float().to(DEV))
+    yr.backward(g)
+    for name, a, ref in (('dx', x.grad, xs.grad), ('dw', w.grad, ws.grad), ('db', b.grad, bs.grad)):
+        e = _err(a.cpu(), ref)
+        assert e < 2e-5 * max(1.0, ref.abs().max().item()), (name, e)
+    assert calls == {'nt': 2, 'tn': 1}, calls
+
+
+@pytest.mark.parametrize('R,Nc,K,act', _SMALL_SHAPES)
+def test_small_linear_native_bf16_matches_fp64(R, Nc, K, act, monkeypatch):
+    """The bf16 step's form of the same layers: bf16 operands / outputs / gradients, fp32 accumulation, vs float64
+    of the same bf16 inputs within bf16 rounding (relative Frobenius error)."""
+    from applestar_amd.ops import native as NN
+    calls = _count_small(monkeypatch)
+    torch.manual_seed(R + K + 1)
+    x = torch.randn(R, K, device=DEV).bfloat16().requires_grad_()
+    w = (torch.randn(Nc, K, device=DEV) / K ** 0.5).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(Nc, device=DEV)).bfloat16().requires_grad_()
+    y = NN.linear(x, w, b, act=act)
+    assert y.dtype == torch.bfloat16
+    xs, ws, bs = _f64(x), _f64(w), _f64(b)
+    yr = xs @ ws.t() + bs
+    yr = torch.relu(yr) if act == 'relu' else (torch.sigmoid(yr) if act == 'sigmoid' else yr)
+    g = torch.randn(yr.shape, dtype=torch.float64).bfloat16().double()
+    y.backward(g.to(DEV).bfloat16())
+    yr.backward(g)
+    for name, a, ref in (('y', y, yr), ('dx', x.grad, xs.grad), ('dw', w.grad, ws.grad), ('db', b.grad, bs.grad)):
+        assert a.dtype == torch.bfloat16, name
+        e = float((a.double().cpu() - ref.detach()).norm() / max(ref.detach().norm().item(), 1e-30))
+        assert e < 1e-2, (name, e)
+    assert calls == {'nt': 2, 'tn': 1}, calls
+
+
+@pytest.mark.parametrize('M,Nc,K,act', [(390, 256, 48640, 1), (390, 128, 12160, 0), (17, 40, 9001, 2)])
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+def test_small_gemm_splitk_matches_fp64(M, Nc, K, act, dt, f32_mfma):
+    """Split-K few-row product (the spatial encoder's 48,640-wide fc): slices + ordered sum + epilogue vs float64."""
+    C = N.ensure_loaded()
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K, device=DEV).to(dt)
+    b = (torch.randn(Nc, K, device=DEV) / K ** 0.5).to(dt)
+    bias = 0.1 * torch.randn(Nc, device=DEV)
+    ref = a.double() @ b.double().t() + bias.double()
+    ref = torch.relu(ref) if act == 1 else (torch.sigmoid(ref) if act == 2 else ref)
+    got = C.small_gemm_splitk(a, b, bias, act)
+    assert got.dtype == dt
+    err = (got.double() - ref).abs().max().item()
+    tol = (2e-5 if dt == torch.float32 else 1e-2) * max(1.0, ref.abs().max().item())
+    assert err < tol, err
+
+
+def test_linear_f32_long_k_grads_match_fp64(f32_mfma):
+    """A few-row fp32 linear with K > 4096 (split-K forward, native dX / dW) vs float64."""
+    from applestar_amd.ops import native as NN
+    torch.manual_seed(41)
+    R, Nc, K = 390, 256, 16640
+    x = torch.randn(R, K, device=DEV).requires_grad_()
+    w = (torch.randn(Nc, K, device=DEV) / K ** 0.5).requires_grad_()
+    b = (0.1 * torch.randn(Nc, device=DEV)).requires_grad_()
+    y = NN.linear(x, w, b, act='relu')
+    xs, ws, bs = _f64(x), _f64(w), _f64(b)
+    yr = torch.relu(xs @ ws.t() + bs)
+    assert _err(y.cpu(), yr) < 1e-5 * max(1.0, yr.abs().max().item())
+    g = torch.randn(yr.shape, dtype=torch.float64)
+    y.backward(g.float().to(DEV))
+    yr.backward(g)
+    for name, a, ref in (('dx', x.grad, xs.grad), ('dw', w.grad, ws.grad), ('db', b.grad, bs.grad)):
+        e = _err(a.cpu(), ref)
+        assert e < 2e-5 * max(1.0, ref.abs().max().item()), (name, e)
+
+
+@pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
+def test_small_gemm_residual_epilogues(dt, f32_mfma):
+    """small_gemm's residual add and residual ReLU-mask epilogues (odd K / N) vs float64."""
+    C = N.ensure_loaded()
+    torch.manual_seed(31)
+    a = torch.randn(77, 45, device=DEV).to(dt)
+    b = (torch.randn(39, 45, device=DEV) / 7).to(dt)
+    res = torch.randn(77, 39, device=DEV).to(dt)
+    ref = a.double() @ b.double().t()
+    tol = 2e-5 if dt == torch.float32 else 1e-2
+    got = C.small_gemm(a, b, None, res, None, 0, 0)
+    assert (got.double() - (ref + res.double())).abs().max().item() < tol * 4
+    got = C.small_gemm(a, b, None, res, None, 0, 4)
+    assert (got.double() - ref * (res.double() > 0)).abs().max().item() < tol * 4
+
+
+@pytest.mark.parametrize('M,Nc,K', [(5000, 768, 256), (3001, 256, 1024), (20000, 32, 24), (2500, 96, 136),
+                                    (9000, 1024, 256), (390, 12160, 128)])
+@pytest.mark.parametrize('mode', ['bias_relu', 'res_add', 'drelu'])
+def test_gemm_bf16_pipe_epilogues(M, Nc, K, mode):
+    """gemm_bf16 (the bf16 step's large products on the LDS-DMA ring): bf16 operands, fp32 accumulation and
+    epilogue, bf16 out, vs float64 of the same bf16 inputs within one bf16 rounding of the result."""
+    torch.manual_seed(M + K + 3)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(Nc, K, device=DEV) / K ** 0.5).bfloat16()
+    bias = 0.1 * torch.randn(Nc, device=DEV)
+    res = torch.randn(M, Nc, device=DEV).bfloat16()
+    C = N.ensure_loaded()
+    ref = a.double() @ b.double().t() + bias.double()
+    if mode == 'bias_relu':
+        got, ref = C.gemm_bf16(a, b, bias, None, 1), torch.relu(ref)
+    elif mode == 'res_add':
+        got, ref = C.gemm_bf16(a, b, bias, res, 0), ref + res.double()
+    else:
+        got, ref = C.gemm_bf16(a, b, bias, res, 4), ref * (res.double() > 0)
+    assert got.dtype == torch.bfloat16
+    err = (got.double() - ref).abs()
+    assert (err <= 2 ** -7 * ref.abs() + 1e-3 * max(1.0, ref.abs().max().item())).all(), err.max().item()
+
+
+def test_bf16_linear_pipe_path_matches_library(monkeypatch):
+    """A many-row bf16 linear (+ ReLU) through _Linear on gemm_bf16 (forward and dX) vs the library path (switch
+    off): forward and all three gradients within bf16 rounding."""
+    from applestar_amd.ops import native as NN
+    torch.manual_seed(8)
+    x0 = torch.randn(6000, 256, device=DEV).bfloat16()
+    w0 = (torch.randn(1024, 256, device=DEV) / 16).bfloat16()
+    b0 = (0.1 * torch.randn(1024, device=DEV)).bfloat16()
+    g = torch.randn(6000, 1024, device=DEV).bfloat16()
+    outs = {}
+    for on in (True, False):
+        monkeypatch.setattr(NN, 'BF16_PIPE', on)
+        x, w, b = (t.clone().requires_grad_() for t in (x0, w0, b0))
+        y = NN.linear(x, w, b, act='relu')
+        y.backward(g)
+        outs[on] = [t.float() for t in (y, x.grad, w.grad, b.grad)]
+    for name, a, r in zip(('y', 'dx', 'dw', 'db'), outs[True], outs[False]):
+        assert (a - r).norm() <= 1e-2 * r.norm(), (name, float((a - r).norm() / r.norm()))
+
+
 @pytest.mark.parametrize('M,Nc,K', [(5000, 768, 256), (3001, 256, 1024), (20000, 32, 20), (2500, 96, 132)])
 @pytest.mark.parametrize('mode', ['bias_relu', 'res_add', 'drelu'])
 def test_gemm_f32_epilogues_match_fp64(M, Nc, K, mode, f32_mfma):

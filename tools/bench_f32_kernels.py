@@ -78,6 +78,18 @@ def main():
             emit('gemm_f32_small', [M, N, K], timed(lambda: C.gemm_f32(a, b, bias, None, 1), 50), 2.0 * M * N * K)
             emit('torch_fp32_addmm_relu', [M, N, K],
                  timed(lambda: torch._addmm_activation(bias, a, b.t(), use_gelu=False), 50), 2.0 * M * N * K)
+    if which in ('bf16', 'all'):
+        # the bf16 step's large products (tools/gemm_census.py): native LDS-DMA ring kernel vs hipBLASLt
+        for M, N, K in [(99526, 768, 256), (99526, 256, 256), (99526, 1024, 256), (99526, 256, 1024),
+                        (99526, 256, 768), (199290, 64, 256), (24576, 1024, 256), (145920, 128, 128),
+                        (390, 12160, 128), (199290, 256, 64)]:
+            a = torch.randn(M, K, device='cuda').bfloat16()
+            b = (torch.randn(N, K, device='cuda') / K ** 0.5).bfloat16()
+            bias = torch.randn(N, device='cuda')
+            bb = bias.bfloat16()
+            emit('gemm_bf16', [M, N, K], timed(lambda: C.gemm_bf16(a, b, bias, None, 1), 20), 2.0 * M * N * K)
+            emit('torch_bf16_addmm_relu', [M, N, K],
+                 timed(lambda: torch._addmm_activation(bb, a, b.t(), use_gelu=False), 20), 2.0 * M * N * K)
     if which in ('gemm', 'all'):
         for M, N, K in GEMM:
             a = torch.randn(M, K, device='cuda')
