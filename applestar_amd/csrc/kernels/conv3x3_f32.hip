@@ -355,9 +355,11 @@ __global__ __launch_bounds__(256, BM == 128 ? 3 : 2) void conv3x3_f32_pipe_kerne
   }
 }
 
+// the LDS-staged epilogue measured -3 ... +6 % on the conv shapes (profiles/r4p_conv_f32_staged_epilogue.txt):
+// opt-in (APPLESTAR_CONV_F32_STAGED=1)
 bool conv_f32_staged() {
   static const bool on = [] {
-    const char* e = std::getenv("APPLESTAR_F32_STAGED");
+    const char* e = std::getenv("APPLESTAR_CONV_F32_STAGED");
     return e != nullptr && e[0] == '1';
   }();
   return on;

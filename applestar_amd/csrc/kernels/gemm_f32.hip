@@ -365,10 +365,12 @@ __global__ __launch_bounds__(256, 3) void gemm_f32_pipe_kernel(const float* __re
   }
 }
 
+// row-coalesced LDS-staged epilogue (pipe::store_tile_staged): 1-4 % faster on the learner's GEMM shapes
+// (profiles/r4p_gemm_f32_staged_epilogue.txt); APPLESTAR_GEMM_F32_STAGED=0 restores the register stores
 bool f32_staged() {
   static const bool on = [] {
-    const char* e = std::getenv("APPLESTAR_F32_STAGED");
-    return e != nullptr && e[0] == '1';
+    const char* e = std::getenv("APPLESTAR_GEMM_F32_STAGED");
+    return e == nullptr || e[0] != '0';
   }();
   return on;
 }

@@ -1253,7 +1253,7 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x2, w, b, relu, link=None):
         ctx.link = link
         R, K = x2.shape
-        if SMALL_NATIVE and x2.is_cuda and R <= 2048 and K > F32_SMALL_K_MAX and \
+        if SMALL_NATIVE and SPLITK_NATIVE and x2.is_cuda and R <= 2048 and K > F32_SMALL_K_MAX and \
                 (R + 127) // 128 * ((w.shape[0] + 63) // 64) < 128 and R * K < (1 << 31) and w.shape[0] * K < (1 << 31):
             # few rows, long reduction (the spatial encoder's 48,640 -> 256 fc, the location head's 12,160 -> 128):
             # split-K over workgroup slices + one ordered sum with the bias / ReLU epilogue (gemm_small.hip),
@@ -1548,7 +1548,16 @@ class _SmallLinearNative(torch.autograd.Function):
         return dx, dw.to(w.dtype), (db.to(ctx.b_dtype) if ctx.has_b else None), None
 
 
+_SMALL_SIGMOID = os.environ.get('APPLESTAR_SMALL_SIGMOID', '1') == '1'    # bisection switches
+_SMALL_ODD = os.environ.get('APPLESTAR_SMALL_ODD', '1') == '1'
+SPLITK_NATIVE = os.environ.get('APPLESTAR_SPLITK_NATIVE', '1') == '1'
+
+
 def _small_native_ok(x, R, N, K, act):
+    if act == 'sigmoid' and not _SMALL_SIGMOID:
+        return False
+    if act != 'sigmoid' and not _SMALL_ODD:
+        return False
     return SMALL_NATIVE and x.is_cuda and act in _MASK and 0 < R < _SMALL_LINEAR_ROWS and N > 0 and K > 0 and \
         R * K < (1 << 31) and R * N < (1 << 31)
 
