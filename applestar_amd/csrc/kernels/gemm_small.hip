@@ -38,7 +38,31 @@ __device__ __forceinline__ void step_mfma(const float (&va)[8], const float (&vb
   }
 }
 
-template <typename T, int SPLIT>
+// 8 values of row `row` (element offset, < 0: none) at k0 .. k0 + 7 through 16-B buffer loads (rows 16-B aligned:
+// K % 4 fp32 / K % 8 bf16); a piece at or past K, or of a missing row, reads zeros (out-of-range offset)
+template <typename T>
+__device__ __forceinline__ void load8_vec(__amdgpu_buffer_rsrc_t r, long row, int k0, int K, float (&v)[8]) {
+  constexpr int kOOBv = 0x7ffffff0;
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int off = row >= 0 && k0 + 4 * q < K ? static_cast<int>((row + k0 + 4 * q) * 4) : kOOBv;
+      const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * q + j] = __uint_as_float(x[j]);
+    }
+  } else {
+    const int off = row >= 0 && k0 < K ? static_cast<int>((row + k0) * 2) : kOOBv;
+    const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(x[j] << 16);
+      v[2 * j + 1] = __uint_as_float(x[j] & 0xffff0000u);
+    }
+  }
+}
+
+template <typename T, int SPLIT, bool VEC = false>
 __global__ __launch_bounds__(256) void small_nt_kernel(const T* __restrict__ a, const T* __restrict__ b,
                                                        const float* __restrict__ bias, const T* __restrict__ res,
                                                        const T* __restrict__ amask, int mask_mode,
@@ -61,17 +85,49 @@ __global__ __launch_bounds__(256) void small_nt_kernel(const T* __restrict__ a, 
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] = 0.f;
 
-  for (int kt = kt0 + w; kt < kt1; kt += 4) {
-    const int k0 = 16 * kt + 8 * h;
-    float va[8], vb[8];
+  if constexpr (VEC) {
+    // aligned rows: 16-B buffer loads, KU K-steps of both operands in flight per wave (the long-K split-K slices
+    // and the aligned few-row products); the activation-gradient mask is not used on this path
+    constexpr int KU = 4;
+    const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(a), 0,
+                                                                        static_cast<int>(M * K * sizeof(T)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<T*>(b), 0, static_cast<int>(static_cast<long>(N) * K * sizeof(T)), 0x00020000);
+    const long ra0 = mok ? arow : -1, rb0 = nok ? brow : -1;
+    float va[KU][8], vb[KU][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bool kok = k0 + j < K;
-      va[j] = mok && kok ? Cvt<T>::load(a, arow + k0 + j) : 0.f;
-      vb[j] = nok && kok ? Cvt<T>::load(b, brow + k0 + j) : 0.f;
-      if (amask != nullptr && mok && kok) va[j] *= grad_mask(Cvt<T>::load(amask, arow + k0 + j), mask_mode);
+    for (int u = 0; u < KU; ++u) {
+      const int kt = kt0 + w + 4 * u;
+      load8_vec<T>(ar, kt < kt1 ? ra0 : -1, 16 * kt + 8 * h, K, va[u]);
+      load8_vec<T>(br, kt < kt1 ? rb0 : -1, 16 * kt + 8 * h, K, vb[u]);
     }
-    step_mfma<T, SPLIT>(va, vb, acc);
+    for (int kt = kt0 + w; kt < kt1; kt += 4 * KU) {
+#pragma unroll
+      for (int u = 0; u < KU; ++u) {
+        const int kc = kt + 4 * u;
+        if (kc >= kt1) break;
+        float xa[8], xb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { xa[j] = va[u][j]; xb[j] = vb[u][j]; }
+        const int kn = kc + 4 * KU;          // refill the slot just read (zeros past the slice)
+        load8_vec<T>(ar, kn < kt1 ? ra0 : -1, 16 * kn + 8 * h, K, va[u]);
+        load8_vec<T>(br, kn < kt1 ? rb0 : -1, 16 * kn + 8 * h, K, vb[u]);
+        step_mfma<T, SPLIT>(xa, xb, acc);
+      }
+    }
+  } else {
+    for (int kt = kt0 + w; kt < kt1; kt += 4) {
+      const int k0 = 16 * kt + 8 * h;
+      float va[8], vb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bool kok = k0 + j < K;
+        va[j] = mok && kok ? Cvt<T>::load(a, arow + k0 + j) : 0.f;
+        vb[j] = nok && kok ? Cvt<T>::load(b, brow + k0 + j) : 0.f;
+        if (amask != nullptr && mok && kok) va[j] *= grad_mask(Cvt<T>::load(amask, arow + k0 + j), mask_mode);
+      }
+      step_mfma<T, SPLIT>(va, vb, acc);
+    }
   }
   if (w > 0) {
 #pragma unroll
@@ -130,19 +186,28 @@ __global__ __launch_bounds__(256) void small_tn_kernel(const T* __restrict__ dy,
 #pragma unroll
   for (int e = 0; e < 16; ++e) acc[e] = 0.f;
   float dsum = 0.f;
-
-  for (long s = w; s < RT; s += 4) {
+  // one reduction step's operands: 8 rows of the lane's dY column (masked) and X column; the next step's are
+  // loaded before this one's MFMAs (the loop is latency-bound: a handful of steps per wave)
+  auto load = [&](long s, float (&va)[8], float (&vb)[8]) {
     const long r0 = 16 * s + 8 * h;
-    float va[8], vb[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const bool rok = r0 + j < R;
+      const bool rok = s < RT && r0 + j < R;
       va[j] = rok && nok ? Cvt<T>::load(dy, (r0 + j) * N + n) : 0.f;
       if (ymask != nullptr && rok && nok) va[j] *= grad_mask(Cvt<T>::load(ymask, (r0 + j) * N + n), mask_mode);
       vb[j] = rok && kok ? Cvt<T>::load(x, (r0 + j) * K + k) : 0.f;
-      dsum += va[j];
     }
-    step_mfma<T, SPLIT>(va, vb, acc);
+  };
+  float ca[8], cb[8];
+  load(w, ca, cb);
+  for (long s = w; s < RT; s += 4) {
+    float na[8], nb[8];
+    load(s + 4, na, nb);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dsum += ca[j];
+    step_mfma<T, SPLIT>(ca, cb, acc);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { ca[j] = na[j]; cb[j] = nb[j]; }
   }
   if (w > 0) {
 #pragma unroll
@@ -186,14 +251,21 @@ __global__ __launch_bounds__(256) void small_nt_finish_kernel(const float* __res
 
 }  // namespace
 
+// the 16-B-load path: rows 16-B aligned (K % 4 fp32 / K % 8 bf16), 16-B aligned bases, byte sizes < 2^31
+bool small_vec_ok(const void* a, const void* b, long M, int N, int K, bool bf16) {
+  const long es = bf16 ? 2 : 4;
+  return K % (16 / es) == 0 && (reinterpret_cast<uintptr_t>(a) & 15) == 0 && (reinterpret_cast<uintptr_t>(b) & 15) == 0 &&
+         M * K * es < 0x7ffffff0L && static_cast<long>(N) * K * es < 0x7ffffff0L;
+}
+
 int small_nt_splits(long M, int N, int K) {
   // few tiles and a long reduction (the spatial encoder's 48,640-wide fc over ~400 rows): slice K so that the
   // grid reaches ~2 workgroups per CU, each slice >= 64 K-steps of 16
   const long tiles = (M + 31) / 32 * ((N + 31) / 32);
   const int kt = (K + 15) / 16;
   if (tiles >= 256 || kt < 256) return 1;
-  int s = static_cast<int>((512 + tiles - 1) / tiles);
-  s = min(s, kt / 64);
+  int s = static_cast<int>((2048 + tiles - 1) / tiles);   // ~2048 workgroups, slices of >= 32 K-steps
+  s = min(s, kt / 32);
   return max(1, min(s, 64));
 }
 
@@ -206,15 +278,25 @@ void small_nt_splitk(const void* a, const void* b, const float* bias, float* par
   const dim3 g(static_cast<unsigned>(nwg), static_cast<unsigned>(S)), blk(256);
   const long MN = M * N;
   const dim3 gf(static_cast<unsigned>((MN + 255) / 256));
+  const bool vec = small_vec_ok(a, b, M, N, K, bf16);
   if (bf16) {
-    hipLaunchKernelGGL((small_nt_kernel<bf16_t, 0>), g, blk, 0, s, static_cast<const bf16_t*>(a),
-                       static_cast<const bf16_t*>(b), nullptr, nullptr, nullptr, 0, nullptr, M, N, K, 0, tn, kspan,
-                       part);
+    if (vec)
+      hipLaunchKernelGGL((small_nt_kernel<bf16_t, 0, true>), g, blk, 0, s, static_cast<const bf16_t*>(a),
+                         static_cast<const bf16_t*>(b), nullptr, nullptr, nullptr, 0, nullptr, M, N, K, 0, tn, kspan,
+                         part);
+    else
+      hipLaunchKernelGGL((small_nt_kernel<bf16_t, 0>), g, blk, 0, s, static_cast<const bf16_t*>(a),
+                         static_cast<const bf16_t*>(b), nullptr, nullptr, nullptr, 0, nullptr, M, N, K, 0, tn, kspan,
+                         part);
     hipLaunchKernelGGL(small_nt_finish_kernel<bf16_t>, gf, blk, 0, s, part, S, bias, static_cast<bf16_t*>(out), MN,
                        N, act);
   } else {
     if (f32_mfma_mode() == 0)
       hipLaunchKernelGGL((small_nt_kernel<float, 0>), g, blk, 0, s, static_cast<const float*>(a),
+                         static_cast<const float*>(b), nullptr, nullptr, nullptr, 0, nullptr, M, N, K, 0, tn, kspan,
+                         part);
+    else if (vec)
+      hipLaunchKernelGGL((small_nt_kernel<float, 1, true>), g, blk, 0, s, static_cast<const float*>(a),
                          static_cast<const float*>(b), nullptr, nullptr, nullptr, 0, nullptr, M, N, K, 0, tn, kspan,
                          part);
     else
@@ -232,6 +314,17 @@ void small_nt(const void* a, const void* b, const float* bias, const void* res, 
   const long nwg = (M + 31) / 32 * tn;
   if (nwg == 0) return;
   const dim3 g(static_cast<unsigned>(nwg)), blk(256);
+  if ((amask == nullptr || mask_mode == 0) && small_vec_ok(a, b, M, N, K, bf16) && (bf16 || f32_mfma_mode() != 0)) {
+    if (bf16)
+      hipLaunchKernelGGL((small_nt_kernel<bf16_t, 0, true>), g, blk, 0, s, static_cast<const bf16_t*>(a),
+                         static_cast<const bf16_t*>(b), bias, static_cast<const bf16_t*>(res), nullptr, 0,
+                         static_cast<bf16_t*>(out), M, N, K, act, tn, 0, nullptr);
+    else
+      hipLaunchKernelGGL((small_nt_kernel<float, 1, true>), g, blk, 0, s, static_cast<const float*>(a),
+                         static_cast<const float*>(b), bias, static_cast<const float*>(res), nullptr, 0,
+                         static_cast<float*>(out), M, N, K, act, tn, 0, nullptr);
+    return;
+  }
   if (bf16) {
     hipLaunchKernelGGL((small_nt_kernel<bf16_t, 0>), g, blk, 0, s, static_cast<const bf16_t*>(a),
                        static_cast<const bf16_t*>(b), bias, static_cast<const bf16_t*>(res),

@@ -78,6 +78,22 @@ def main():
             emit('gemm_f32_small', [M, N, K], timed(lambda: C.gemm_f32(a, b, bias, None, 1), 50), 2.0 * M * N * K)
             emit('torch_fp32_addmm_relu', [M, N, K],
                  timed(lambda: torch._addmm_activation(bias, a, b.t(), use_gelu=False), 50), 2.0 * M * N * K)
+    if which in ('smallnative', 'all'):
+        # the any-shape few-row kernels (gemm_small.hip) on the step's shapes vs the library
+        for R, N, K in [(390, 64, 10), (390, 128, 167), (384, 256, 448), (390, 64, 269), (390, 1, 256),
+                        (384, 327, 256), (390, 32, 90)]:
+            for dt in (torch.float32, torch.bfloat16):
+                x = torch.randn(R, K, device='cuda').to(dt)
+                w = torch.randn(N, K, device='cuda').to(dt)
+                dy = torch.randn(R, N, device='cuda').to(dt)
+                y = torch.randn(R, N, device='cuda').to(dt)
+                bias = torch.randn(N, device='cuda')
+                tag = 'f32' if dt == torch.float32 else 'bf16'
+                emit(f'small_nt_{tag}', [R, N, K], timed(lambda: C.small_gemm(x, w, bias, None, None, 0, 1), 50),
+                     2.0 * R * N * K)
+                emit(f'small_tn_{tag}', [R, N, K], timed(lambda: C.small_wgrad(dy, x, y, 1, True, dt == torch.bfloat16), 50),
+                     2.0 * R * N * K)
+                emit(f'torch_dw_{tag}', [R, N, K], timed(lambda: dy.t() @ x, 50), 2.0 * R * N * K)
     if which in ('bf16', 'all'):
         # the bf16 step's large products (tools/gemm_census.py): native LDS-DMA ring kernel vs hipBLASLt
         for M, N, K in [(99526, 768, 256), (99526, 256, 256), (99526, 1024, 256), (99526, 256, 1024),

@@ -82,9 +82,32 @@ def main():
     torch.cuda.synchronize()
     b = next(it)
     census = Census(args.all)
-    with census:
-        trainer.step(b)
-    torch.cuda.synchronize()
+    # native few-row / split-K products too: wrap the extension's entry points for this step
+    from applestar_amd.ops import native as NN
+    C = NN.ensure_loaded()
+    native_calls = collections.Counter()
+
+    class _Wrap:
+        def __getattr__(self, k):
+            f = getattr(C, k)
+            if k not in ('small_gemm', 'small_wgrad', 'small_gemm_splitk', 'gemm_f32', 'gemm_bf16', 'gemm_bf16_small',
+                         'wgrad_f32', 'wgrad', 'mm_k32'):
+                return f
+
+            def g(*a):
+                native_calls[(k, tuple(tuple(t.shape) for t in a if torch.is_tensor(t)))] += 1
+                return f(*a)
+            return g
+    NN._C = _Wrap()
+    try:
+        with census:
+            trainer.step(b)
+        torch.cuda.synchronize()
+    finally:
+        NN._C = C
+    print(f'{sum(native_calls.values())} native GEMM-family calls')
+    for (k, shapes), n in sorted(native_calls.items(), key=lambda kv: -kv[1]):
+        print(f'  native {n:3d} {k:18s} {shapes}')
     print(f'{sum(census.calls.values())} library GEMM calls in one {args.mode} {args.precision} step')
     key = (lambda kv: -kv[1] * (kv[0][1] if isinstance(kv[0][1], int) else 1)) if args.all else (lambda kv: -kv[1])
     for (name, shapes, dt, site), n in sorted(census.calls.items(), key=key):
