@@ -456,10 +456,22 @@ int pick_k(int k, int bn) {
 
 }  // namespace
 
+// target workgroup count of the split-R decomposition (APPLESTAR_WGRAD_F32_WG): fp32 step 62.4 / 62.5 ms at
+// 1024, 61.6 / 62.0 at 3072, flat to 8192, 64.5 at 512, 68.5 at 256 (profiles/r4t_wgrad_f32_wg_sweep.txt)
+long wgrad_f32_target_wg() {
+  static const long v = [] {
+    const char* e = std::getenv("APPLESTAR_WGRAD_F32_WG");
+    const long x = e ? std::atol(e) : 3072;
+    return x >= 64 ? x : 3072;
+  }();
+  return v;
+}
+
 int wgrad_f32_splits(long R, int N, int K) {
   const int bn = pick(N), bk = pick_k(K, bn);
   const long tiles = static_cast<long>((N + bn - 1) / bn) * ((K + bk - 1) / bk);
-  long S = (1024 + tiles - 1) / tiles;                   // ~1024 workgroups
+  const long target = wgrad_f32_target_wg();
+  long S = (target + tiles - 1) / tiles;                 // ~target workgroups
   const long max_s = R < 2048 ? 1 : (R + 127) / 128;     // >= 4 stages per slice
   if (S > max_s) S = max_s;
   const long max_part = (16L << 20) / (static_cast<long>(N) * K);   // partials <= 64 MB
