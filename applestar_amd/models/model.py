@@ -48,6 +48,7 @@ DEFAULT_MODEL_CONFIG = AttrDict({
 _SIDE_STREAMS: Dict[tuple, 'torch.cuda.Stream'] = {}
 SIDE_STREAMS_ENABLED = True
 CRITIC_SIDE_STREAM = False   # tools/ab_bench.py --variant critic_side: no gain (+1.9 ms, noisy)
+VE_AFTER_CORE = os.environ.get('APPLESTAR_VE_AFTER_CORE', '1') == '1'   # A/B r4: fp32 61.3 / 60.8 vs 61.8 / 61.6 ms
 # selected-units + target-unit key projections as one product before the row slice (APPLESTAR_JOINT_KEYS=0: per head)
 JOINT_KEYS = os.environ.get('APPLESTAR_JOINT_KEYS', '1') != '0'
 # value baselines' ResFCBlock2 stack as the fused resmlp kernels on the GPU (APPLESTAR_FUSED_RESMLP=0: op by op)
@@ -303,13 +304,19 @@ class Model(nn.Module):
         # stream, overlapping the policy encoders and the latency-bound core LSTM (which occupies a handful
         # of CUs); autograd replays its backward on the same side stream, so that overlaps as well.
         vf = None
-        if self._use_value_feature:
+        if self._use_value_feature and not VE_AFTER_CORE:
             vf = _side_stream_call(self.value_encoder, value_feature)
         lstm_input, scalar_context, baseline_feature, entity_embeddings, map_skip = self._encode(
             spatial_info, entity_info, scalar_info, entity_num, kwargs.get('entity_total'), kwargs.get('entity_pad'))
         H = hidden_state[0][0].shape[-1]
         h0 = [(h.view(-1, B, H)[0], c.view(-1, B, H)[0]) for h, c in hidden_state]
+        if self._use_value_feature and VE_AFTER_CORE and lstm_input.is_cuda:
+            # issued right behind the core LSTM's inputs: the value encoder's forward runs on its side stream
+            # while the latency-bound recurrence occupies a few dozen CUs (A/B switch)
+            vf = _side_stream_call(self.value_encoder, value_feature)
         out, _ = self._core(lstm_input.view(T + 1, B, -1), h0)
+        if self._use_value_feature and vf is None:
+            vf = _side_stream_call(self.value_encoder, value_feature)
         lstm_output = out.reshape((T + 1) * B, -1)
         n = T * B
         critic_input = lstm_output
