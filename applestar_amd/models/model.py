@@ -48,6 +48,7 @@ DEFAULT_MODEL_CONFIG = AttrDict({
 _SIDE_STREAMS: Dict[tuple, 'torch.cuda.Stream'] = {}
 SIDE_STREAMS_ENABLED = True
 CRITIC_SIDE_STREAM = False   # tools/ab_bench.py --variant critic_side: no gain (+1.9 ms, noisy)
+VE_BWD_OVERLAP = os.environ.get('APPLESTAR_VE_BWD_OVERLAP', '0') == '1'   # A/B r4: 61.6 / 61.7 vs 61.3 / 61.6 ms, off
 VE_AFTER_CORE = os.environ.get('APPLESTAR_VE_AFTER_CORE', '1') == '1'   # A/B r4: fp32 61.3 / 60.8 vs 61.8 / 61.6 ms
 # selected-units + target-unit key projections as one product before the row slice (APPLESTAR_JOINT_KEYS=0: per head)
 JOINT_KEYS = os.environ.get('APPLESTAR_JOINT_KEYS', '1') != '0'
@@ -67,9 +68,10 @@ def _device_table(name: str, t: torch.Tensor, device) -> torch.Tensor:
     return _DEVICE_TABLES[key]
 
 
-def _side_stream_call(fn, inputs, slot: int = 0):
+def _side_stream_call(fn, inputs, slot: int = 0, after=None):
     """Run ``fn(inputs)`` on side stream ``slot`` of the device (GPU) and return a handle for
-    :func:`_side_stream_join`."""
+    :func:`_side_stream_join`.  ``after``: an event recorded on the main stream earlier; the side stream waits for
+    it instead of for everything issued so far (the inputs were ready at that point)."""
     dev = next((v.device for v in inputs.values() if torch.is_tensor(v)), None) if isinstance(inputs, dict) else None
     if dev is None or dev.type != 'cuda' or not SIDE_STREAMS_ENABLED:
         return fn(inputs), None
@@ -77,7 +79,10 @@ def _side_stream_call(fn, inputs, slot: int = 0):
     side = _SIDE_STREAMS.get((dev.index, slot))
     if side is None:
         side = _SIDE_STREAMS[(dev.index, slot)] = torch.cuda.Stream(dev)
-    side.wait_stream(main)                 # inputs were produced on the main stream
+    if after is not None:
+        side.wait_event(after)
+    else:
+        side.wait_stream(main)             # inputs were produced on the main stream
     for t in inputs.values():              # ... and are read on the side stream
         if torch.is_tensor(t) and t.is_cuda:
             t.record_stream(side)
@@ -310,13 +315,21 @@ class Model(nn.Module):
             spatial_info, entity_info, scalar_info, entity_num, kwargs.get('entity_total'), kwargs.get('entity_pad'))
         H = hidden_state[0][0].shape[-1]
         h0 = [(h.view(-1, B, H)[0], c.view(-1, B, H)[0]) for h, c in hidden_state]
-        if self._use_value_feature and VE_AFTER_CORE and lstm_input.is_cuda:
+        ev = None
+        if self._use_value_feature and VE_AFTER_CORE and lstm_input.is_cuda and VE_BWD_OVERLAP and \
+                SIDE_STREAMS_ENABLED and not torch.cuda.is_current_stream_capturing():
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(lstm_input.device))
+        elif self._use_value_feature and VE_AFTER_CORE and lstm_input.is_cuda:
             # issued right behind the core LSTM's inputs: the value encoder's forward runs on its side stream
             # while the latency-bound recurrence occupies a few dozen CUs (A/B switch)
             vf = _side_stream_call(self.value_encoder, value_feature)
         out, _ = self._core(lstm_input.view(T + 1, B, -1), h0)
         if self._use_value_feature and vf is None:
-            vf = _side_stream_call(self.value_encoder, value_feature)
+            # VE_BWD_OVERLAP: created AFTER the core LSTM (so autograd issues its backward before the LSTM's: the
+            # side-stream backward then runs beside the recurrence's backward), but ordered on the GPU only
+            # behind the event recorded before the LSTM (its forward still overlaps the recurrence)
+            vf = _side_stream_call(self.value_encoder, value_feature, after=ev)
         lstm_output = out.reshape((T + 1) * B, -1)
         n = T * B
         critic_input = lstm_output
