@@ -25,6 +25,8 @@
 // Loads go through buffer descriptors: rows past the slice end, columns past N/K and taps outside the
 // image get an out-of-range offset and read as zeros (no branches around loads).  The bias gradient is
 // accumulated from the A fragments by the waves that own K-column 0 of K-tile 0.
+#include <cstdlib>
+
 #include "../common.h"
 #include "../kernels.h"
 
@@ -324,10 +326,21 @@ int pick_bk(int K) {
 }
 }  // namespace
 
+// target workgroup count (APPLESTAR_WGRAD_WG, default 1024)
+long wgrad_target_wg() {
+  static const long v = [] {
+    const char* e = std::getenv("APPLESTAR_WGRAD_WG");
+    const long x = e ? std::atol(e) : 1024;
+    return x >= 64 ? x : 1024;
+  }();
+  return v;
+}
+
 int wgrad_splits(long R, int N, int K) {
   const int BN = pick_bn(N), BK = pick_bk(K);
   const long tiles = static_cast<long>((N + BN - 1) / BN) * ((K + BK - 1) / BK);
-  long S = (1024 + tiles - 1) / tiles;                 // ~1024 workgroups: 2 resident per CU, 2 rounds
+  const long target = wgrad_target_wg();
+  long S = (target + tiles - 1) / tiles;               // ~target workgroups: 2 resident per CU
   // at least 256 rows (4 stages) per slice; short reductions (R < 2048, e.g. the 390-row policy / value
   // MLP gradients) take one slice so no partial-sum pass is launched at all
   const long max_s = R < 2048 ? 1 : (R + 255) / 256;
