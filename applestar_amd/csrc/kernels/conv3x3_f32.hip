@@ -365,6 +365,16 @@ bool conv_f32_staged() {
   return on;
 }
 
+// 256-row tiles for the narrow (32-channel) outputs: each wave then owns 64 x 32 (two A fragments per B
+// fragment instead of one) - APPLESTAR_CONV_F32_N32_BM256=1 (A/B switch)
+bool conv_n32_bm256() {
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_CONV_F32_N32_BM256");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 template <int BN>
 void launch_f32(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
                 int Cin, int Cout, int act, hipStream_t s) {
@@ -372,6 +382,14 @@ void launch_f32(const float* x, const float* w, const float* bias, const float* 
   const long nwg = (M + 127) / 128 * ((Cout + BN - 1) / BN);
   if (nwg == 0) return;
   const int mode = f32_mfma_mode();
+  if constexpr (BN == 32) {
+    if (mode == 1 && conv_n32_bm256()) {
+      const long nwg2 = (M + 255) / 256 * ((Cout + BN - 1) / BN);
+      hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<32, 3, 256>), dim3(static_cast<unsigned>(nwg2)), dim3(256), 0, s, x,
+                         w, bias, res, out, B, H, W, Cin, Cout, act);
+      return;
+    }
+  }
   if (mode == 1 && conv_f32_staged())
     hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<BN, 3, 128, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x,
                        w, bias, res, out, B, H, W, Cin, Cout, act);
