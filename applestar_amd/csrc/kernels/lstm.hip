@@ -253,20 +253,33 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_kernel(
   float lw[COLS], lb[COLS];
 #pragma unroll
   for (int k = 0; k < COLS; ++k) { lw[k] = lnh_w[tid * COLS + k]; lb[k] = lnh_b[tid * COLS + k]; }
+  // the whole W^T column slice of this thread in registers (H x COLS: 64 values at H = 32), loaded once - the
+  // per-step L2 stream of W was the recurrence's critical path (one dependent load round trip per step)
+  RegW<TW, H * COLS> wreg;
+#pragma unroll
+  for (int i = 0; i < H; ++i)
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) wreg.load(i * COLS + k, wT, static_cast<long>(i) * G + tid * COLS + k);
+  // the input projection of the next step is fetched during this one
+  float xpc[COLS];
+#pragma unroll
+  for (int k = 0; k < COLS; ++k) xpc[k] = T > 0 ? xp[static_cast<long>(b) * G + tid * COLS + k] : 0.f;
   __syncthreads();
   for (int t = 0; t < T; ++t) {
+    float xpn[COLS];
+    {
+      const long nrow = static_cast<long>(t + 1 < T ? t + 1 : t) * B + b;
+#pragma unroll
+      for (int k = 0; k < COLS; ++k) xpn[k] = xp[nrow * G + tid * COLS + k];
+    }
     float acc[COLS];
 #pragma unroll
     for (int k = 0; k < COLS; ++k) acc[k] = 0.f;
-    const TW* wp = wT + tid * COLS;
-    // deep unroll: the W^T stream is L2-latency bound at B=6, keep many 8-16 B loads in flight
-#pragma unroll 32
+#pragma unroll
     for (int i = 0; i < H; ++i) {
-      float wv[COLS];
-      WLoad<TW, COLS>::load(wp + static_cast<long>(i) * G, wv);
       const float hv = h_s[i];
 #pragma unroll
-      for (int k = 0; k < COLS; ++k) acc[k] = fmaf(hv, wv[k], acc[k]);
+      for (int k = 0; k < COLS; ++k) acc[k] = fmaf(hv, wreg.get(i * COLS + k), acc[k]);
     }
     float s = 0.f;
 #pragma unroll
@@ -282,12 +295,14 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_kernel(
     for (int k = 0; k < COLS; ++k) {
       const int j = tid * COLS + k;
       const float xh = (acc[k] - mu) * rs;
-      const float gv = xp[row * G + j] + xh * lw[k] + lb[k];
+      const float gv = xpc[k] + xh * lw[k] + lb[k];
       xhat_h[row * G + j] = xh;
       gates_out[row * G + j] = gv;
       g_s[j] = gv;
     }
     if (tid == 0) rstd_h[row] = rs;
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) xpc[k] = xpn[k];
     __syncthreads();
     float cpre = 0.f, og = 0.f;
     if (unit) {
@@ -328,12 +343,31 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
     float* __restrict__ dgates, float* __restrict__ dhg, float* __restrict__ dc_ln, float* __restrict__ dh0,
     float* __restrict__ dc0) {
   constexpr int G = 4 * H;
+  // dh_{t-1} = dhg @ W  (W [G][H]): 2-D split, each thread owns KV consecutive outputs and 1/JG of the
+  // reduction (partials combined through LDS); its (G / JG) x KV weight block lives in registers for the
+  // whole sequence (64 values at H = 32)
+  constexpr int KV = sizeof(TW) == 2 ? 8 : 4;
+  constexpr int KT = H / KV;              // threads along k
+  constexpr int JG = NT / KT;             // reduction groups
+  constexpr int JR = G / JG;              // rows per group
+  static_assert(H % KV == 0 && JG >= 1 && G % JG == 0 && KT * JG == NT, "dh tiling");
   __shared__ float dh_s[H];
   __shared__ float dg_s[G];
+  __shared__ float part[JG][H];
   __shared__ float red[2 * (NT / kWave)];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const bool unit = tid < H;
+  const int kq = tid % KT, jg = tid / KT;
+  // register-resident weight block when it is small (H = 32); the wide fallback (H = 384 unsplit) streams W
+  constexpr bool kRegW = JR * KV <= 128;
+  RegW<TW, kRegW ? JR * KV : 2> wreg;
+  if constexpr (kRegW) {
+#pragma unroll
+    for (int m = 0; m < JR; ++m)
+#pragma unroll
+      for (int v = 0; v < KV; ++v) wreg.load(m * KV + v, w, static_cast<long>(jg * JR + m) * H + kq * KV + v);
+  }
   float dc = 0.f, lcw = 0.f;
   if (unit) {
     dh_s[tid] = dhT[static_cast<long>(b) * H + tid];
@@ -343,31 +377,53 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
   float lw[COLS];
 #pragma unroll
   for (int k = 0; k < COLS; ++k) lw[k] = lnh_w[tid * COLS + k];
+  // the step's saved activations, fetched one step ahead (their latency hides under the previous step)
+  struct StepIn { float dout, cc, go, xc, gi, gf, gg, cprev, rc, xh[COLS], rh; };
+  const int ut = unit ? tid : 0;
+  auto load_in = [&](int t, StepIn& v) {
+    const long row = static_cast<long>(t) * B + b;
+    v.dout = dout[row * H + ut];
+    v.cc = c_all[(row + B) * H + ut];
+    v.go = gates[row * G + 3 * H + ut];
+    v.xc = xhat_c[row * H + ut];
+    v.gi = gates[row * G + ut];
+    v.gf = gates[row * G + H + ut];
+    v.gg = gates[row * G + 2 * H + ut];
+    v.cprev = c_all[row * H + ut];
+    v.rc = rstd_c[row];
+#pragma unroll
+    for (int k = 0; k < COLS; ++k) v.xh[k] = xhat_h[row * G + tid * COLS + k];
+    v.rh = rstd_h[row];
+  };
+  StepIn cur;
+  if (T > 0) load_in(T - 1, cur);
   __syncthreads();
   for (int t = T - 1; t >= 0; --t) {
     const long row = static_cast<long>(t) * B + b;
+    StepIn nxt;
+    load_in(t > 0 ? t - 1 : 0, nxt);
     // ---- cell: h = o tanh(c), c = LN_c(cpre)
     float dxh = 0.f, xc = 0.f, ig = 0.f, fg = 0.f, gg = 0.f, cprev = 0.f;
     if (unit) {
-      const float dh = dout[row * H + tid] + dh_s[tid];
-      const float cc = c_all[(row + B) * H + tid];
+      const float dh = cur.dout + dh_s[tid];
+      const float cc = cur.cc;
       const float tc = tanhf(cc);
-      const float og = sigmoidf_(gates[row * G + 3 * H + tid]);
+      const float og = sigmoidf_(cur.go);
       const float do_pre = dh * tc * og * (1.f - og);
       const float dct = dc + dh * og * (1.f - tc * tc);
       dc_ln[row * H + tid] = dct;
       dxh = dct * lcw;
-      xc = xhat_c[row * H + tid];
-      ig = sigmoidf_(gates[row * G + tid]);
-      fg = sigmoidf_(gates[row * G + H + tid]);
-      gg = tanhf(gates[row * G + 2 * H + tid]);
-      cprev = c_all[row * H + tid];
+      xc = cur.xc;
+      ig = sigmoidf_(cur.gi);
+      fg = sigmoidf_(cur.gf);
+      gg = tanhf(cur.gg);
+      cprev = cur.cprev;
       dg_s[3 * H + tid] = do_pre;
     }
     const float2 mm = block_sum2<NT>(dxh, dxh * xc, red);
     const float m1 = mm.x * (1.f / H), m2 = mm.y * (1.f / H);
     if (unit) {
-      const float dcpre = rstd_c[row] * (dxh - m1 - xc * m2);
+      const float dcpre = cur.rc * (dxh - m1 - xc * m2);
       dg_s[tid] = dcpre * gg * ig * (1.f - ig);
       dg_s[H + tid] = dcpre * cprev * fg * (1.f - fg);
       dg_s[2 * H + tid] = dcpre * ig * (1.f - gg * gg);
@@ -382,7 +438,7 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
       const int j = tid * COLS + k;
       const float dgv = dg_s[j];
       dgates[row * G + j] = dgv;
-      xh[k] = xhat_h[row * G + j];
+      xh[k] = cur.xh[k];
       dx[k] = dgv * lw[k];
       s1 += dx[k];
       s2 += dx[k] * xh[k];
@@ -392,7 +448,7 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
       s1 = ss.x * (1.f / G);
       s2 = ss.y * (1.f / G);
     }
-    const float rs = rstd_h[row];
+    const float rs = cur.rh;
 #pragma unroll
     for (int k = 0; k < COLS; ++k) {
       const int j = tid * COLS + k;
@@ -401,21 +457,21 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
       dg_s[j] = v;  // each thread overwrites only its own columns
     }
     __syncthreads();
-    // ---- dh_{t-1} = dhg @ W  (W [G][H]): 2-D split, each thread owns KV consecutive outputs (one
-    // 16-byte load per j) and 1/JG of the reduction; partials combined through LDS
     {
-      constexpr int KV = sizeof(TW) == 2 ? 8 : 4;
-      constexpr int KT = H / KV;              // threads along k
-      constexpr int JG = NT / KT;             // reduction groups
-      static_assert(H % KV == 0 && JG >= 1 && G % JG == 0, "dh tiling");
-      const int kq = tid % KT, jg = tid / KT;
       float acc[KV];
 #pragma unroll
       for (int v = 0; v < KV; ++v) acc[v] = 0.f;
-      if (jg < JG) {
-        const int j0 = jg * (G / JG), j1 = j0 + G / JG;
+      if constexpr (kRegW) {
+#pragma unroll
+        for (int m = 0; m < JR; ++m) {
+          const float d = dg_s[jg * JR + m];
+#pragma unroll
+          for (int v = 0; v < KV; ++v) acc[v] = fmaf(d, wreg.get(m * KV + v), acc[v]);
+        }
+      } else {
 #pragma unroll 16
-        for (int j = j0; j < j1; ++j) {
+        for (int m = 0; m < JR; ++m) {
+          const int j = jg * JR + m;
           const float d = dg_s[j];
           float wv[KV];
           WLoad16<TW>::load(w + static_cast<long>(j) * H + kq * KV, wv);
@@ -423,11 +479,8 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
           for (int v = 0; v < KV; ++v) acc[v] = fmaf(d, wv[v], acc[v]);
         }
       }
-      __shared__ float part[JG][H];
-      if (jg < JG) {
 #pragma unroll
-        for (int v = 0; v < KV; ++v) part[jg][kq * KV + v] = acc[v];
-      }
+      for (int v = 0; v < KV; ++v) part[jg][kq * KV + v] = acc[v];
       __syncthreads();
       if (unit) {
         float sacc = 0.f;
@@ -436,6 +489,7 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
         dh_s[tid] = sacc;
       }
     }
+    cur = nxt;
     __syncthreads();
   }
   if (unit) {
