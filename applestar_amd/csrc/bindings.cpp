@@ -1875,6 +1875,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_f32_mfma_mode", &as::set_f32_mfma_mode);
   m.def("conv3x3_f32_supported", &as::conv3x3_f32_supported);
   m.def("varlen_attn_bwd_f32", &varlen_attn_bwd_f32);
+  m.def("attn_f32_variant", [](int64_t v) { return static_cast<int64_t>(as::attn_f32_variant(static_cast<int>(v))); });
   m.def("su_sample", &su_sample);
   m.def("segment_copy", &segment_copy);
   m.def("conv_wt", &conv_wt);

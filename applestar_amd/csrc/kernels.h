@@ -155,6 +155,8 @@ void varlen_attn_bwd(const void* qkv, const void* out, const void* dout, const f
 // The same in fp32 (f32-input MFMA): qkv / out / dout / dqkv fp32 - the fp32 learner step's attention.
 void varlen_attn_fwd_f32(const float* qkv, const int* cu, float* out, float* lse2, int S, int max_len, int H, long Ttot,
                          float scale, hipStream_t s);
+// fp32 attention split-path variant (attention_f32.hip); v < 0 only reads it.  Returns the previous value.
+int attn_f32_variant(int v);
 void varlen_attn_bwd_f32(const float* qkv, const float* out, const float* dout, const float* lse2, const int* cu,
                          float* dqkv, float* delta, int S, int max_len, int H, long Ttot, float scale, hipStream_t s);
 

@@ -264,9 +264,19 @@ def test_varlen_attention_matches_reference(lens):
     assert _err(qkv.grad, ref_in.grad) < 3e-2 * max(1.0, scale)
 
 
+@pytest.fixture(params=[23, 0, 1, 9], ids=['img_default', 'perwave', 'img_pf_rawv', 'img_dq_nopf'])
+def attn_variant(request):
+    """fp32 attention split-path variant (attention_f32.hip attn_f32_variant): pre-split LDS images (default) and
+    its forward / dQ forms, or the per-wave split kernels"""
+    C = N.ensure_loaded()
+    old = C.attn_f32_variant(request.param)
+    yield request.param
+    C.attn_f32_variant(old)
+
+
 @pytest.mark.parametrize('lens', [[1, 64, 65, 200, 511], [37], [128, 3, 300]])
 @pytest.mark.parametrize('score_scale', [0.5, 2.0])
-def test_varlen_attention_fp32_matches_fp64(lens, score_scale, f32_mfma):
+def test_varlen_attention_fp32_matches_fp64(lens, score_scale, f32_mfma, attn_variant):
     """fp32 operands take the f32-MFMA kernel (attention_f32.hip), never a bf16 copy: forward and all three
     input gradients within fp32 rounding of a float64 reference."""
     torch.manual_seed(11)

@@ -2,7 +2,7 @@
 dX), wgrad_f32 (conv + dense dW), gemm_f32, against the exact-f32 MFMA peak (157.3 TFLOP/s, MI355X).  One JSON
 line per (kernel, shape) with us / call and TFLOP/s.  Also the child process of PMC passes (tools/gpu_pmc.sh).
 
-    python tools/bench_f32_kernels.py [conv|wgrad|gemm|all]
+    python tools/bench_f32_kernels.py [conv|wgrad|gemm|small|smallnative|bf16|attn|all]
 """
 import json
 import os
@@ -106,6 +106,31 @@ def main():
             emit('gemm_bf16', [M, N, K], timed(lambda: C.gemm_bf16(a, b, bias, None, 1), 20), 2.0 * M * N * K)
             emit('torch_bf16_addmm_relu', [M, N, K],
                  timed(lambda: torch._addmm_activation(bb, a, b.t(), use_gelu=False), 20), 2.0 * M * N * K)
+    if which in ('attn', 'all'):
+        # the entity transformer's fp32 attention at the learner's shape (384 observations, 2 heads x 128, lengths
+        # up to 512, mean ~260): forward and backward per split-path variant (attention_f32.hip)
+        g = torch.Generator().manual_seed(0)
+        lens = torch.randint(1, 513, (384,), generator=g)
+        cu = torch.zeros(385, dtype=torch.int32)
+        cu[1:] = lens.cumsum(0)
+        cu = cu.cuda()
+        T, H = int(lens.sum()), 2
+        qkv = torch.randn(T, 3 * H * 128, device='cuda')
+        flop_f = 4.0 * H * 128 * float((lens.double() ** 2).sum())
+        ref = None
+        for v in (0, 1, 7, 17, 23):
+            old = C.attn_f32_variant(v)
+            out, lse = C.varlen_attn_fwd_f32(qkv, cu, 512, H)
+            dout = torch.randn(out.shape, device='cuda') if ref is None else ref[2]
+            dq = C.varlen_attn_bwd_f32(qkv, out, dout, lse, cu, 512, H)
+            if ref is None:
+                ref = (out, dq, dout)
+            err_f = float((out - ref[0]).abs().max())
+            err_b = float((dq - ref[1]).abs().max() / ref[1].abs().max())
+            emit(f'attn_f32_fwd_v{v}', [T, H, err_f], timed(lambda: C.varlen_attn_fwd_f32(qkv, cu, 512, H)), flop_f)
+            emit(f'attn_f32_bwd_v{v}', [T, H, err_b],
+                 timed(lambda: C.varlen_attn_bwd_f32(qkv, out, dout, lse, cu, 512, H)), 2.5 * flop_f)
+            C.attn_f32_variant(old)
     if which in ('gemm', 'all'):
         for M, N, K in GEMM:
             a = torch.randn(M, K, device='cuda')
