@@ -1635,6 +1635,45 @@ std::vector<at::Tensor> gate_chain(const at::Tensor& x, const std::vector<at::Te
   return outs;
 }
 
+// fp32 chain: x [P,128] fp32; m: 4 x [128,128] fp32 (row n = output channel); bias: 4 x fp32 [128] or None;
+// mask / res: 4 x fp32 [P,128] or None -> 4 outputs [P,128] fp32
+std::vector<at::Tensor> gate_chain_f32(const at::Tensor& x, const std::vector<at::Tensor>& m,
+                                       const std::vector<c10::optional<at::Tensor>>& bias,
+                                       const std::vector<c10::optional<at::Tensor>>& mask,
+                                       const std::vector<c10::optional<at::Tensor>>& res, int64_t relu_mask) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.dim() == 2 && x.size(1) == 128 && x.is_contiguous(),
+              "gate_chain_f32: x [P,128] fp32 contiguous");
+  TORCH_CHECK(m.size() == 4 && bias.size() == 4 && mask.size() == 4 && res.size() == 4, "gate_chain_f32: 4 layers");
+  const int64_t P = x.size(0);
+  TORCH_CHECK(P * 128 < (1LL << 31), "gate_chain_f32: 32-bit element offsets");
+  as::GateChainF32Args a{};
+  a.x = x.data_ptr<float>();
+  a.relu_mask = static_cast<int>(relu_mask);
+  auto opt = [&](const c10::optional<at::Tensor>& t, bool rows, const char* what) -> const float* {
+    if (!t.has_value()) return nullptr;
+    check_cuda(*t, what);
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() &&
+                (rows ? t->sizes() == x.sizes() : t->numel() == 128), "gate_chain_f32: ", what, rows ? " like x" : " [128]");
+    return t->data_ptr<float>();
+  };
+  std::vector<at::Tensor> outs;
+  for (int L = 0; L < 4; ++L) {
+    check_cuda(m[L], "m");
+    TORCH_CHECK(m[L].scalar_type() == at::kFloat && m[L].size(0) == 128 && m[L].numel() == 128 * 128 &&
+                m[L].is_contiguous(), "gate_chain_f32: m [128,128] fp32 contiguous");
+    a.m[L] = m[L].data_ptr<float>();
+    a.bias[L] = opt(bias[L], false, "bias");
+    a.mask[L] = opt(mask[L], true, "mask");
+    a.res[L] = opt(res[L], true, "res");
+    outs.push_back(at::empty_like(x));
+    a.out[L] = outs.back().data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(x.device().index());
+  as::gate_chain_f32(a, P, stream());
+  return outs;
+}
+
 // ---------------------------------------------------------------- RL loss tail (rl_loss.hip)
 // -> {info [rl_loss_info_size(F)], dalp, dent, dkl [6,T,B], dv [F,T+1,B]}
 std::vector<at::Tensor> rl_loss(const at::Tensor& alp, const at::Tensor& blp, const at::Tensor& hm, const at::Tensor& ent,
@@ -1903,6 +1942,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("vsp_fwd", &vsp_fwd);
   m.def("rl_loss", &rl_loss);
   m.def("gate_chain", &gate_chain);
+  m.def("gate_chain_f32", &gate_chain_f32);
   m.def("vsp_pool_fwd", &vsp_pool_fwd);
   m.def("vsp_pool_bwd", &vsp_pool_bwd);
   m.def("vsp_in_channels", []() { return as::vsp_in_channels(); });

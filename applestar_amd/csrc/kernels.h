@@ -427,5 +427,17 @@ struct GateChainArgs {
   int relu_mask;
 };
 void gate_chain(const GateChainArgs& a, long P, hipStream_t s);
+// the fp32 chain (bf16x6 split products): out[L] = epilogue_L(in_L . m[L]^T), in_0 = x, in_{L+1} = out[L]; the
+// epilogue adds bias[L], applies ReLU (relu_mask bit L), zeroes where mask[L] <= 0, adds res[L] (each optional)
+struct GateChainF32Args {
+  const float* x;
+  const float* m[4];
+  const float* bias[4];
+  const float* mask[4];
+  const float* res[4];
+  float* out[4];
+  int relu_mask;
+};
+void gate_chain_f32(const GateChainF32Args& a, long P, hipStream_t s);
 
 }  // namespace as

@@ -13,6 +13,7 @@
 // input from HBM: ~25 us per layer per direction on the 145,920-row location-head map (r2cs).
 #include "../common.h"
 #include "../kernels.h"
+#include "../split_mfma.h"
 
 namespace as {
 namespace {
@@ -138,7 +139,139 @@ __global__ __launch_bounds__(256) void gate_chain_kernel(GateChainArgs a, long P
   }
 }
 
+// ---- fp32 chain (the fp32 learner step) on bf16x6 split products (split_mfma.h).  A 64-row tile lives in LDS
+// as a pre-split image (three bf16 planes of [64 rows][128 ch], 256-B rows, 16-B chunk index XORed by
+// 2 (row & 7) | ((row >> 3) & 1): conflict-free b128 row reads, the attention_f32.hip image).  The product is
+// computed transposed, C^T[n][r] = M[n][:] . X[r][:], so each lane ends a layer holding 4 consecutive channels of
+// one row: 16-B fp32 stores to HBM and 8-B plane writes of the next layer's image.  Wave w owns channels
+// 32 w .. 32 w + 31 (two 16-row A tiles of M, split once per layer into 96 VGPRs) over all 64 rows (four B tiles
+// read from the image per k-step).  Measured against four gemm_f32 launches on the 145,920-row location-head map
+// (profiles/r4z_gate_chain_f32.txt): forward 164 vs 183 us, backward 243 vs ~200 us, fp32 step unchanged
+// (58.2 / 58.2 vs 58.1 / 58.4 ms) - latency-bound at 3 workgroups per CU with a layer-serial chain, so it stays
+// behind APPLESTAR_GATE_CHAIN_F32=1 (default off).
+constexpr int kFR = 64;                      // rows per workgroup
+constexpr int kFPlane = kFR * 256;           // bytes per bf16 plane
+__device__ __forceinline__ int gcf_off(int r, int ch) { return 256 * r + 16 * (ch ^ ((2 * (r & 7)) | ((r >> 3) & 1))); }
+
+__device__ __forceinline__ gc_f4 gcf_x6(const Split3& a, const Split3& b, gc_f4 c) {
+  auto mm = [](u32v4 x, u32v4 y, gc_f4 acc) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(x), as_bf(y), acc, 0, 0, 0); };
+  c = mm(a.p[1], b.p[1], c);
+  c = mm(a.p[0], b.p[2], c);
+  c = mm(a.p[2], b.p[0], c);
+  c = mm(a.p[0], b.p[1], c);
+  c = mm(a.p[1], b.p[0], c);
+  return mm(a.p[0], b.p[0], c);
+}
+
+__global__ __launch_bounds__(256, 2) void gate_chain_f32_kernel(GateChainF32Args a, long P) {
+  __shared__ __attribute__((aligned(16))) char img[3 * kFPlane];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  const long m0 = static_cast<long>(blockIdx.x) * kFR;
+  // input tile -> image: thread t takes row t >> 2 (0..63), chunks 4 (t & 3) .. 4 (t & 3) + 3 (32 floats);
+  // rows past P are zero (clamped unconditional loads)
+  {
+    const int r = tid >> 2, c0 = 4 * (tid & 3);
+    const bool ok = m0 + r < P;
+    const float4* src = reinterpret_cast<const float4*>(a.x + (ok ? m0 + r : 0) * 128 + 8 * c0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float4 u = src[2 * c], v = src[2 * c + 1];
+      const float f[8] = {ok ? u.x : 0.f, ok ? u.y : 0.f, ok ? u.z : 0.f, ok ? u.w : 0.f,
+                          ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f};
+      const Split3 sp = split8(f);
+      const int o = gcf_off(r, c0 + c);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) *reinterpret_cast<u32v4*>(img + pl * kFPlane + o) = sp.p[pl];
+    }
+  }
+#pragma unroll 1
+  for (int L = 0; L < 4; ++L) {
+    // this wave's rows of M_L (channels 32 w + 16 j + lr), k = 32 ks + 8 lg + t, split once.  (Loading the next
+    // layer's rows during the epilogue: 192 VGPRs, 2 waves / SIMD, 189 us vs 164 - measured, reverted.)
+    Split3 mf[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float4* mrow = reinterpret_cast<const float4*>(a.m[L] + (32 * w + 16 * j + lr) * 128 + 8 * lg);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const float4 u = mrow[8 * ks], v = mrow[8 * ks + 1];
+        const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+        mf[j][ks] = split8(f);
+      }
+    }
+    __syncthreads();   // the image holds this layer's input
+    gc_f4 acc[2][4];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[j][m] = gc_f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int o = gcf_off(16 * m + lr, 4 * ks + lg);
+        Split3 xb;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) xb.p[pl] = *reinterpret_cast<const u32v4*>(img + pl * kFPlane + o);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[j][m] = gcf_x6(mf[j][ks], xb, acc[j][m]);
+      }
+    __syncthreads();   // every wave is done reading the image
+    const bool relu = (a.relu_mask >> L) & 1;
+    const float* bias = a.bias[L];
+    const float* msk = a.mask[L];
+    const float* res = a.res[L];
+    float* out = a.out[L];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = 32 * w + 16 * j + 4 * lg;   // channels n .. n + 3
+      const float4 bv = bias ? *reinterpret_cast<const float4*>(bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int r = 16 * m + lr;
+        const long row = m0 + r;
+        const bool ok = row < P;
+        const long ro = (ok ? row : 0) * 128 + n;
+        float v[4] = {acc[j][m][0] + bv.x, acc[j][m][1] + bv.y, acc[j][m][2] + bv.z, acc[j][m][3] + bv.w};
+        if (relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        if (msk) {
+          const float4 mk = *reinterpret_cast<const float4*>(msk + ro);
+          v[0] = mk.x > 0.f ? v[0] : 0.f;
+          v[1] = mk.y > 0.f ? v[1] : 0.f;
+          v[2] = mk.z > 0.f ? v[2] : 0.f;
+          v[3] = mk.w > 0.f ? v[3] : 0.f;
+        }
+        if (res) {
+          const float4 rr = *reinterpret_cast<const float4*>(res + ro);
+          v[0] += rr.x;
+          v[1] += rr.y;
+          v[2] += rr.z;
+          v[3] += rr.w;
+        }
+        if (ok) *reinterpret_cast<float4*>(out + ro) = make_float4(v[0], v[1], v[2], v[3]);
+        if (L < 3) {
+          uint2 s0, s1, s2;
+          split4(make_uint4(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])),
+                 s0, s1, s2);
+          const int o = gcf_off(r, n >> 3) + 8 * ((n >> 2) & 1);
+          *reinterpret_cast<uint2*>(img + o) = s0;
+          *reinterpret_cast<uint2*>(img + kFPlane + o) = s1;
+          *reinterpret_cast<uint2*>(img + 2 * kFPlane + o) = s2;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace
+
+void gate_chain_f32(const GateChainF32Args& a, long P, hipStream_t s) {
+  const long nwg = (P + kFR - 1) / kFR;
+  if (nwg > 0) hipLaunchKernelGGL(gate_chain_f32_kernel, dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a, P);
+}
 
 void gate_chain(const GateChainArgs& a, long P, hipStream_t s) {
   const long nwg = (P + kGRows - 1) / kGRows;

@@ -903,6 +903,9 @@ def resblock(x, w1, b1, w2, b2):
 
 
 GATE_CHAIN = os.environ.get('APPLESTAR_GATE_CHAIN', '1') == '1'
+# the fp32 step's gate chain in one launch per direction (gate_chain.hip gate_chain_f32_kernel): measured equal to the
+# four f32 GEMMs on the step (profiles/r4z_gate_chain_f32.txt), off by default
+GATE_CHAIN_F32 = os.environ.get('APPLESTAR_GATE_CHAIN_F32', '0') == '1'
 
 
 class _GatedResBlock(torch.autograd.Function):
@@ -927,6 +930,11 @@ class _GatedResBlock(torch.autograd.Function):
             acts += _C.gate_chain(h, [gate[2 * i].detach().view(C, C) for i in range(4)],
                                   [_w32(gate[2 * i + 1]) for i in range(4)],
                                   [None] * 4, [None] * 4, 0b0111)
+            h = acts[-1]
+        elif GATE_CHAIN_F32 and C == 128 and x.dtype == torch.float32 and h.shape[0] * C < 2 ** 31:
+            # fp32 step: the four gate layers in one launch, the split activation tile resident in LDS
+            acts += _C.gate_chain_f32(h, [gate[2 * i].detach().view(C, C) for i in range(4)],
+                                      [_w32(gate[2 * i + 1]) for i in range(4)], [None] * 4, [None] * 4, 0b0111)
             h = acts[-1]
         elif x.dtype == torch.float32 and _gemm_f32_ok(h.shape[0], C, C):
             # fp32 step: the four gate layers on the f32 GEMM with bias (+ ReLU) in the epilogue
@@ -961,6 +969,14 @@ class _GatedResBlock(torch.autograd.Function):
                                                 0)
             for i, di in ((3, d), (2, d3), (1, d2), (0, d1)):
                 dw_i, db_i = _wgrad(di, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
+                grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
+        elif GATE_CHAIN_F32 and C == 128 and x.dtype == torch.float32 and d.shape[0] * C < 2 ** 31:
+            # fp32 step: d3, d2, d1 and the gate-path input gradient (+ the skip gradient) in one launch
+            d3, d2, d1, dx_gate = _C.gate_chain_f32(d.contiguous(), [_wT(gws[i]) for i in (3, 2, 1, 0)], [None] * 4,
+                                                    [a3, a2, a1, None],
+                                                    [None, None, None, dx_res.view(-1, C).contiguous()], 0)
+            for i, di in ((3, d), (2, d3), (1, d2), (0, d1)):
+                dw_i, db_i = _wgrad(di, acts_in[i], 0, True, False)
                 grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
         elif x.dtype == torch.float32 and _gemm_f32_ok(d.shape[0], C, C):
             # fp32 step: each input gradient on the f32 GEMM with the previous layer's ReLU mask (ACT_DRELU on its

@@ -1333,9 +1333,11 @@ def test_conv_relu_mask_handoff_f32(between, extra_consumer):
         assert e < 3e-5 * max(1.0, r.grad.abs().max().item()), (name, e)
 
 
-def test_gated_resblock_f32_gemm_gate_path(f32_mfma, monkeypatch):
-    """At 12 x 38 x 40 pixels the fp32 GatedResBlock's four gate layers take the f32 GEMM (bias + ReLU forward,
-    the ReLU masks and the skip gradient in the dX epilogues).  Against the same block with the gate layers on the
+@pytest.mark.parametrize('chain', [True, False], ids=['chain_f32', 'gemm_f32'])
+def test_gated_resblock_f32_gemm_gate_path(f32_mfma, monkeypatch, chain):
+    """At 12 x 38 x 40 pixels the fp32 GatedResBlock's four gate layers take the one-launch fp32 chain
+    (gate_chain_f32: split activation tile resident in LDS) or four f32 GEMMs (bias + ReLU forward, the ReLU masks
+    and the skip gradient in the dX epilogues).  Against the same block with the gate layers on the
     library fp32 GEMM, same inputs: every gradient within 1e-5 (relative Frobenius).  The gate layers get small
     weights and +-1 biases (half the channels on, half off, none near zero): with random ones a few of the 7 M ReLU
     decisions sit within fp32 rounding of zero and flip between any two fp32 implementations (and against
@@ -1352,14 +1354,22 @@ def test_gated_resblock_f32_gemm_gate_path(f32_mfma, monkeypatch):
     x = torch.randn(12, 128, 38, 40, device=DEV).contiguous(memory_format=torch.channels_last)
     g = torch.randn(12, 128, 38, 40, device=DEV).contiguous(memory_format=torch.channels_last)
     assert N._gemm_f32_ok(12 * 38 * 40, 128, 128)
+    monkeypatch.setattr(N, 'GATE_CHAIN_F32', chain)
+    C = N.ensure_loaded()
+    calls = []
+    if chain:
+        real = C.gate_chain_f32
+        monkeypatch.setattr(C, 'gate_chain_f32', lambda *a: calls.append(1) or real(*a), raising=False)
     grads = []
     for lib in (False, True):
         if lib:
+            monkeypatch.setattr(N, 'GATE_CHAIN_F32', False)
             monkeypatch.setattr(N, '_gemm_f32_ok', lambda *a: False)
         blk = copy.deepcopy(blk0).to(DEV).to(memory_format=torch.channels_last)
         xg = x.clone().requires_grad_()
         blk(xg).backward(g)
         grads.append([xg.grad] + [p.grad for p in blk.parameters()])
+    assert len(calls) == (2 if chain else 0)   # one launch per direction
     for i, (a, r) in enumerate(zip(*grads)):
         fro = ((a - r).norm() / r.norm()).item()
         assert fro < 1e-5, (i, fro)

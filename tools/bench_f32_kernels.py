@@ -2,7 +2,7 @@
 dX), wgrad_f32 (conv + dense dW), gemm_f32, against the exact-f32 MFMA peak (157.3 TFLOP/s, MI355X).  One JSON
 line per (kernel, shape) with us / call and TFLOP/s.  Also the child process of PMC passes (tools/gpu_pmc.sh).
 
-    python tools/bench_f32_kernels.py [conv|wgrad|gemm|small|smallnative|bf16|attn|all]
+    python tools/bench_f32_kernels.py [conv|wgrad|gemm|small|smallnative|bf16|attn|gate|all]
 """
 import json
 import os
@@ -131,6 +131,26 @@ def main():
             emit(f'attn_f32_bwd_v{v}', [T, H, err_b],
                  timed(lambda: C.varlen_attn_bwd_f32(qkv, out, dout, lse, cu, 512, H)), 2.5 * flop_f)
             C.attn_f32_variant(old)
+    if which in ('gate', 'all'):
+        # the location head's gate chain (four 128 x 128 layers over 145,920 pixels): one launch vs four GEMMs
+        P = 145920
+        x = torch.randn(P, 128, device='cuda')
+        ms = [torch.randn(128, 128, device='cuda') / 11 for _ in range(4)]
+        bs = [torch.randn(128, device='cuda') for _ in range(4)]
+        flop = 4 * 2.0 * P * 128 * 128
+
+        def four():
+            h = x
+            for i in range(4):
+                h = C.gemm_f32(h, ms[i], bs[i], None, 1 if i < 3 else 0)
+            return h
+        emit('gate_chain_f32', [P, 128, 4], timed(lambda: C.gate_chain_f32(x, ms, bs, [None] * 4, [None] * 4, 7)), flop)
+        emit('gemm_f32_x4', [P, 128, 4], timed(four), flop)
+        d = torch.randn(P, 128, device='cuda')
+        acts = C.gate_chain_f32(x, ms, bs, [None] * 4, [None] * 4, 7)
+        emit('gate_chain_f32_bwd', [P, 128, 4],
+             timed(lambda: C.gate_chain_f32(d, [m.t().contiguous() for m in ms[::-1]], [None] * 4,
+                                            [acts[2], acts[1], acts[0], None], [None, None, None, x], 0)), flop)
     if which in ('gemm', 'all'):
         for M, N, K in GEMM:
             a = torch.randn(M, K, device='cuda')
