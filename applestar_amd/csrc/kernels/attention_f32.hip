@@ -487,7 +487,7 @@ __device__ __forceinline__ int img_off(int r, int ch) { return 256 * r + 16 * (c
 __device__ __forceinline__ void img_load(float4 (&v)[4], const float* __restrict__ base, long ld, int r0, int nvalid) {
   // unconditional loads from a clamped row, zeroed by select: a guarded load compiles to an exec-masked branch
   // around four dword loads per float4
-  const int t = threadIdx.x, row = t >> 3, j = t & 7;
+  const int t = threadIdx.x & 255, row = t >> 3, j = t & 7;
   const bool ok = r0 + row < nvalid;
   const float4* src = reinterpret_cast<const float4*>(base + static_cast<long>(ok ? r0 + row : 0) * ld + 8 * j);
   const int o[4] = {0, 1, 16, 17};
@@ -499,7 +499,7 @@ __device__ __forceinline__ void img_load(float4 (&v)[4], const float* __restrict
 }
 
 __device__ __forceinline__ void img_store(char* img, const float4 (&v)[4]) {
-  const int t = threadIdx.x, row = t >> 3, j = t & 7;
+  const int t = threadIdx.x & 255, row = t >> 3, j = t & 7;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const float4 a = v[2 * h], b = v[2 * h + 1];
@@ -837,7 +837,9 @@ __global__ __launch_bounds__(256, 2) void attn_f32_bwd_dkdv_img_kernel(
 // bit 0 = pre-split images (else
 // the per-wave split kernels above); bit 1 = forward at 3 waves / SIMD (168 VGPRs, spills); bit 2 = forward without
 // the register prefetch of the next block; bit 3 = dQ without it; bit 4 = dK/dV with the V fragment pre-split
-// (spills at 256 VGPRs; default: split on the fly)
+// (spills at 256 VGPRs; default: split on the fly).  Measured and removed: dK / dV with each 16-key slice on a
+// wave PAIR (8 waves: one holds the K fragment, computes P, accumulates dV; the other the V fragment, dP -> dS, dK;
+// P through LDS): 162 VGPRs, 1161 us backward (1378 us held to 128 VGPRs, 200 B spilled) vs 1001 us.
 static int g_attn_variant = [] {
   const char* e = std::getenv("APPLESTAR_F32_ATTN_IMG");
   return e ? std::atoi(e) : 23;
