@@ -27,12 +27,29 @@ from . import dist as pdist
 
 
 def copy_into(dst: List[torch.Tensor], src: List[torch.Tensor]):
-    """dst[i].copy_(src[i]) for all i: one native multi-tensor launch on the GPU (dtype-converting)."""
+    """dst[i].copy_(src[i]) for all i: one native multi-tensor launch on the GPU (dtype-converting).  Pairs whose
+    strides differ (a channels_last conv-weight gradient into its contiguous bucket view) go through one strided
+    multi-tensor launch instead of a ``copy_`` each (25 launches per fp32 step)."""
     if not dst:
         return
     if dst[0].is_cuda:
         from ..ops import native
-        native.ensure_loaded().multi_copy(dst, src)
+        C = native.ensure_loaded()
+        same, sd, ss, spec = ([], []), [], [], []
+        for d, s in zip(dst, src):
+            if d.stride() != s.stride() and d.is_contiguous() and 0 < s.dim() <= 4 and s.numel() > 0 and \
+                    d.dtype in (torch.float32, torch.bfloat16) and s.dtype in (torch.float32, torch.bfloat16) and \
+                    min(s.stride()) >= 0:
+                sd.append(d)
+                ss.append(s)
+                spec += native._view_spec(s, s)
+            else:
+                same[0].append(d)
+                same[1].append(s)
+        if same[0]:
+            C.multi_copy(*same)
+        if sd:
+            C.multi_strided_copy(sd, ss, spec)
     else:
         torch._foreach_copy_(dst, src)
 

@@ -682,6 +682,34 @@ def test_multi_copy_converts_and_handles_many_tensors():
         assert torch.equal(d, s.to(d.dtype)), (d.shape, d.dtype, s.dtype)
 
 
+def test_copy_into_strided_sources_without_copy_launches():
+    """parallel/dp.py copy_into (the gradient -> bucket copy): sources whose strides differ from the contiguous
+    destination (channels_last conv-weight gradients, transposed views) take ONE strided multi-tensor launch, equal
+    strides the raw / converting multi-copy - exact values, and no aten copy_ dispatched."""
+    from torch.utils._python_dispatch import TorchDispatchMode
+    from applestar_amd.parallel.dp import copy_into
+    torch.manual_seed(4)
+    srcs = [torch.randn(64, 32, 3, 3, device=DEV).contiguous(memory_format=torch.channels_last),
+            torch.randn(48, 80, device=DEV).t(),
+            torch.randn(7, 5, 3, device=DEV).permute(2, 0, 1),
+            torch.randn(1000, device=DEV),
+            torch.randn(33, 17, device=DEV).bfloat16().t(),
+            torch.randn(20, 30, device=DEV)]
+    dsts = [torch.empty(s.shape, device=DEV, dtype=torch.float32) for s in srcs]
+    seen = []
+
+    class Rec(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, a=(), kw=None):
+            seen.append(str(func.overloadpacket.__name__))
+            return func(*a, **(kw or {}))
+    with Rec():
+        copy_into(dsts, srcs)
+    torch.cuda.synchronize()
+    assert 'copy_' not in seen, seen
+    for d, s in zip(dsts, srcs):
+        assert torch.equal(d, s.float())
+
+
 def test_multi_copy_raw_bytes_any_dtype():
     """Equal-dtype pairs travel as raw bytes (the graph step's batch refresh): int64 / int32 / bool / uint8 /
     fp16 / fp32 leaves, odd byte counts and views at unaligned offsets (byte path), > 64 MB leaves (many
