@@ -123,8 +123,12 @@ class GraphedTrainStep:
         self.single_graph = not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
         # forked side streams (value / scalar encoders) inside the capture; off: captured on one stream
         self.side_streams = os.environ.get('APPLESTAR_GRAPH_SIDE_STREAMS', '0') == '1'
-        # host waits after the replays (module docstring: no longer needed); APPLESTAR_GRAPH_HOST_SYNC=1 for debugging
-        self.host_sync = os.environ.get('APPLESTAR_GRAPH_HOST_SYNC', '0') == '1'
+        # host waits after the replays (module docstring: no longer needed on one rank); APPLESTAR_GRAPH_HOST_SYNC=1
+        # for debugging.  Multi-rank keeps the wait between the two graphs (before the RCCL reduce) unless the
+        # variable is set to 0: the probe that retired it ran single-process only
+        env = os.environ.get('APPLESTAR_GRAPH_HOST_SYNC')
+        self.host_sync = env == '1'
+        self.host_sync_between = self.host_sync or (env is None and not self.single_graph)
         # one private memory pool per graph instead of one shared pool (diagnostics)
         self.private_pools = os.environ.get('APPLESTAR_GRAPH_PRIVATE_POOLS', '0') == '1'
         self.after_replay: Optional[Callable[[_Entry], None]] = None    # diagnostics hook, before any host wait
@@ -194,7 +198,7 @@ class GraphedTrainStep:
             self.check_fn()
         t2 = time.perf_counter()
         if e.upd is not None:
-            if self.host_sync:
+            if self.host_sync_between:
                 torch.cuda.current_stream(self.device).synchronize()
             self.reduce()
         t3 = time.perf_counter()
