@@ -1,5 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u tools/glue_sites.py --steps 1 --shapes > gpurun_out/glue_sites_fp32_shapes.txt 2> gpurun_out/glue_sites.err || { tail -20 gpurun_out/glue_sites.err; exit 1; }
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "copy" > gpurun_out/copy_pytest.txt 2>&1 || { tail -30 gpurun_out/copy_pytest.txt; exit 1; }
-tail -2 gpurun_out/copy_pytest.txt
+timeout -k 10 400 python bench.py --mode sl --steps 20 --warmup 5 --precision fp32 > gpurun_out/r4z_bench_sl.json 2> gpurun_out/r4z_bench_sl.err || { tail -20 gpurun_out/r4z_bench_sl.err; exit 1; }
+tail -1 gpurun_out/r4z_bench_sl.json
