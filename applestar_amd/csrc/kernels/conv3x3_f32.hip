@@ -20,6 +20,7 @@
 // pitches 20 r mod 32 for r = 0..7 are disjoint 4-bank windows; row-major dealing put two rows' 16 floats
 // on overlapping banks: 2-way on every staging write).  The epilogue stores straight from the
 // accumulators: 32 lanes write 32 consecutive channels (128 B) of one pixel.
+#include <algorithm>
 #include <cstdlib>
 
 #include "../common.h"
@@ -375,6 +376,141 @@ bool conv_n32_bm256() {
   return on;
 }
 
+// ---- narrow convolutions (Cin 16 / 32, Cout a multiple of 16: the value encoder's spatial tower) as direct
+// convolutions on 16x16x32 split MFMAs with no LDS.  The ring kernel's 128 x 32 tile wastes half of every MFMA at
+// Cout 16 and pads K = 144 to 256 (16 -> 16 at 76 x 80: 50 TF/s forward, 30 TF/s weight gradient).  Here a wave
+// owns 16 pixels x 16 NT output channels and computes C^T[cout][pixel] = W[cout][:] . im2col[pixel][:]: the
+// weight rows (A, cout = lr, k = 32 ks + 8 lg + t) are split once into registers and kept for the wave's whole
+// pixel range; the im2col operand (B, pixel = lr) is 8 consecutive channels of one tap - two 16-B loads per lane,
+// zero outside the image - split in registers; each lane ends with 4 consecutive channels of one pixel (16-B
+// NHWC stores).  K = 9 Cin is padded to whole 32-deep steps (144 -> 160 at Cin 16).
+typedef __attribute__((ext_vector_type(4))) float nf4;
+__device__ __forceinline__ nf4 nmfma_x6(const Split3& a, const Split3& b, nf4 c) {
+  auto mm = [](u32v4 x, u32v4 y, nf4 acc) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf(x), as_bf(y), acc, 0, 0, 0); };
+  c = mm(a.p[1], b.p[1], c);
+  c = mm(a.p[0], b.p[2], c);
+  c = mm(a.p[2], b.p[0], c);
+  c = mm(a.p[0], b.p[1], c);
+  c = mm(a.p[1], b.p[0], c);
+  return mm(a.p[0], b.p[0], c);
+}
+
+template <int CIN, int NT>
+__global__ __launch_bounds__(256) void conv3x3_f32_narrow_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                                const float* __restrict__ bias,
+                                                                const float* __restrict__ res, float* __restrict__ out,
+                                                                int B, int H, int W, int Cout, int act, long ntiles) {
+  constexpr int K = 9 * CIN, KS = (K + 31) / 32;
+  const int lane = threadIdx.x & 63, lg = lane >> 4, lr = lane & 15;
+  const int ncb = Cout / (16 * NT);                       // output-channel blocks
+  const long gw = static_cast<long>(blockIdx.x) * 4 + (threadIdx.x >> 6), nw = static_cast<long>(gridDim.x) * 4;
+  const int cb = static_cast<int>(gw % ncb);
+  const int n_base = cb * 16 * NT;
+  Split3 wf[NT][KS];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k0 = 32 * ks + 8 * lg;
+      float f[8];
+      if (k0 < K) {
+        const float4* src = reinterpret_cast<const float4*>(w + static_cast<long>(n_base + 16 * j + lr) * K + k0);
+        const float4 u = src[0], v = src[1];
+        f[0] = u.x; f[1] = u.y; f[2] = u.z; f[3] = u.w; f[4] = v.x; f[5] = v.y; f[6] = v.z; f[7] = v.w;
+      } else {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) f[t] = 0.f;
+      }
+      wf[j][ks] = split8(f);
+    }
+  float4 bv[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j)
+    bv[j] = bias ? *reinterpret_cast<const float4*>(bias + n_base + 16 * j + 4 * lg) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const int HW = H * W;
+  const long M = static_cast<long>(B) * HW;
+  for (long tile = gw / ncb; tile < ntiles; tile += nw / ncb) {
+    const long p = tile * 16 + lr;
+    const bool pv = p < M;
+    const long pc = pv ? p : 0;
+    const int rem = static_cast<int>(pc % HW), yy = rem / W, xx = rem - yy * W;
+    nf4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = nf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k0 = 32 * ks + 8 * lg, tap = k0 / CIN, c0 = k0 - tap * CIN;
+      const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+      const bool ok = pv && tap < 9 && yy + dy >= 0 && yy + dy < H && xx + dx >= 0 && xx + dx < W;
+      const long q = ok ? pc + dy * W + dx : pc;          // clamped, loaded unconditionally, zeroed by select
+      const float4* src = reinterpret_cast<const float4*>(x + q * CIN + (tap < 9 ? c0 : 0));
+      const float4 u = src[0], v = src[1];
+      const float f[8] = {ok ? u.x : 0.f, ok ? u.y : 0.f, ok ? u.z : 0.f, ok ? u.w : 0.f,
+                          ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f};
+      const Split3 xb = split8(f);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) acc[j] = nmfma_x6(wf[j][ks], xb, acc[j]);
+    }
+    if (pv) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = n_base + 16 * j + 4 * lg;
+        float v[4] = {acc[j][0] + bv[j].x, acc[j][1] + bv[j].y, acc[j][2] + bv[j].z, acc[j][3] + bv[j].w};
+        if (res) {
+          const float4 rv = *reinterpret_cast<const float4*>(res + p * Cout + n);
+          const float r[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = act == ACT_DRELU ? (r[e] > 0.f ? v[e] : 0.f) : v[e] + r[e];
+        }
+        if (act == ACT_RELU)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        *reinterpret_cast<float4*>(out + p * Cout + n) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
+// narrow direct conv in split mode (APPLESTAR_CONV_F32_NARROW = 1 (default) | 0 | all).  Measured against the ring
+// kernel (profiles/r4z_conv_f32_narrow.txt, 390 images): 16 -> 16 at 76 x 80 158 vs 227 us; 16 -> 32 at 38 x 40
+// 87 vs 77, 32 -> 16 118 vs 115, 32 -> 32 at 19 x 20 66 vs 37 - so by default only Cin = Cout = 16 takes it
+// ('all': every {16, 32} x {16, 32} shape).
+int conv_narrow_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("APPLESTAR_CONV_F32_NARROW");
+    if (e && e[0] == '0') return 0;
+    if (e && e[0] == 'a') return 2;
+    return 1;
+  }();
+  return m;
+}
+
+bool launch_narrow(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H,
+                   int W, int Cin, int Cout, int act, hipStream_t s) {
+  const int nm = conv_narrow_mode();
+  if (f32_mfma_mode() != 1 || nm == 0 || (Cin != 16 && Cin != 32) || (Cout != 16 && Cout != 32)) return false;
+  if (nm == 1 && (Cin != 16 || Cout != 16)) return false;
+  const long M = static_cast<long>(B) * H * W;
+  const long ntiles = (M + 15) / 16;
+  if (ntiles == 0) return true;
+  // ~8 workgroups per CU, each wave walking its tiles (the split weight rows amortised over them)
+  const int nt = (Cin == 16 && Cout == 32) ? 2 : 1;
+  const long ncb = Cout / (16 * nt);
+  long nwg = std::min<long>(2048, (ntiles * ncb + 3) / 4);
+  nwg = std::max<long>(nwg, 1);
+  // every wave's output-channel block is (wave id % ncb): keep the wave count a multiple of ncb
+  if (Cin == 16 && nt == 2)
+    hipLaunchKernelGGL((conv3x3_f32_narrow_kernel<16, 2>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias,
+                       res, out, B, H, W, Cout, act, ntiles);
+  else if (Cin == 16)
+    hipLaunchKernelGGL((conv3x3_f32_narrow_kernel<16, 1>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias,
+                       res, out, B, H, W, Cout, act, ntiles);
+  else
+    hipLaunchKernelGGL((conv3x3_f32_narrow_kernel<32, 1>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w, bias,
+                       res, out, B, H, W, Cout, act, ntiles);
+  return true;
+}
+
 template <int BN>
 void launch_f32(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H, int W,
                 int Cin, int Cout, int act, hipStream_t s) {
@@ -413,6 +549,7 @@ bool conv3x3_f32_supported(int Cin, int Cout) { return Cin % 16 == 0 && Cin > 0 
 
 void conv3x3_f32_fwd(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H,
                      int W, int Cin, int Cout, int act, hipStream_t s) {
+  if (launch_narrow(x, w, bias, res, out, B, H, W, Cin, Cout, act, s)) return;
   if (Cout % 128 == 0) launch_f32<128>(x, w, bias, res, out, B, H, W, Cin, Cout, act, s);
   else if (Cout > 32) launch_f32<64>(x, w, bias, res, out, B, H, W, Cin, Cout, act, s);
   else launch_f32<32>(x, w, bias, res, out, B, H, W, Cin, Cout, act, s);

@@ -1,4 +1,6 @@
 """Native HIP kernels vs plain-PyTorch fp32 references (run on an MI355X)."""
+import os
+
 import pytest
 import torch
 
@@ -1217,10 +1219,13 @@ def _f64(t):
 
 @pytest.mark.parametrize('cin,cout,H,W,act,res', [(128, 128, 19, 20, 'relu', True), (32, 64, 21, 17, 'relu', False),
                                                   (64, 128, 10, 12, None, False), (16, 16, 9, 11, 'relu', False),
-                                                  (16, 32, 8, 8, None, True), (128, 64, 5, 7, 'relu', False)])
+                                                  (16, 32, 8, 8, None, True), (128, 64, 5, 7, 'relu', False),
+                                                  (32, 32, 19, 20, 'relu', True), (32, 16, 7, 9, None, False)])
 def test_conv3x3_f32_matches_fp64(cin, cout, H, W, act, res, f32_mfma):
     """fp32 operands take conv3x3_f32.hip (forward, dX with the flipped weight, split-R dW / db): within fp32
-    rounding of a float64 reference - no bf16 anywhere."""
+    rounding of a float64 reference - no bf16 anywhere.  Cin = Cout = 16 takes the narrow direct-conv kernel in
+    split mode (forward and dX), the others the LDS-DMA ring (test_conv3x3_f32_narrow_all_shapes: every narrow
+    shape on the direct kernel)."""
     from applestar_amd import ops
     torch.manual_seed(21)
     B, cl = 3, torch.channels_last
@@ -1327,6 +1332,38 @@ def test_fused_resblocks_f32_match_torch_fp64(gated, f32_mfma):
     for (n, p), (_, pr) in zip(blk.named_parameters(), ref.named_parameters()):
         e = _err(p.grad.cpu(), pr.grad)
         assert e < 3e-5 * max(1.0, pr.grad.abs().max().item()), (n, e)
+
+
+@pytest.mark.parametrize('cin,cout', [(16, 16), (16, 32), (32, 16), (32, 32)])
+def test_conv3x3_f32_narrow_all_shapes(cin, cout):
+    """The narrow direct-conv kernel (conv3x3_f32.hip conv3x3_f32_narrow_kernel) on every shape it implements,
+    in a child process with APPLESTAR_CONV_F32_NARROW=all (the mode is read once per process): forward with bias +
+    residual + ReLU and the DReLU-masked form against float64."""
+    import subprocess
+    import sys
+    code = f'''
+import torch
+from applestar_amd.ops import native as N
+C = N.ensure_loaded()
+C.set_f32_mfma_mode(1)
+torch.manual_seed(5)
+B, H, W = 3, 13, 11
+x = torch.randn(B, H, W, {cin}, device="cuda")
+w = torch.randn({cout}, 3, 3, {cin}, device="cuda") / 12
+b = torch.randn({cout}, device="cuda")
+r = torch.randn(B, H, W, {cout}, device="cuda")
+ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2), b.double(), 1, 1)
+ref = ref.permute(0, 2, 3, 1)
+for act, res, want in ((1, r, torch.relu(ref + r.double())), (4, r, ref * (r.double() > 0)), (0, None, ref)):
+    y = C.conv3x3_f32(x, w, b, res, act)
+    err = (y.double() - want).abs().max().item()
+    assert err < 1e-5 * max(1.0, want.abs().max().item()), (act, err)
+print("ok")
+'''
+    env = dict(os.environ, APPLESTAR_CONV_F32_NARROW='all')
+    out = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True, timeout=120,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert out.returncode == 0 and out.stdout.strip().endswith('ok'), out.stderr[-2000:]
 
 
 @pytest.mark.parametrize('between', ['maxpool', 'upsample'])

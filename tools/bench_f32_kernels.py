@@ -2,7 +2,7 @@
 dX), wgrad_f32 (conv + dense dW), gemm_f32, against the exact-f32 MFMA peak (157.3 TFLOP/s, MI355X).  One JSON
 line per (kernel, shape) with us / call and TFLOP/s.  Also the child process of PMC passes (tools/gpu_pmc.sh).
 
-    python tools/bench_f32_kernels.py [conv|wgrad|gemm|small|smallnative|bf16|attn|gate|all]
+    python tools/bench_f32_kernels.py [conv|narrow|wgrad|gemm|small|smallnative|bf16|attn|gate|all]
 """
 import json
 import os
@@ -38,6 +38,15 @@ def main():
     from applestar_amd.ops import native
     C = native.ensure_loaded()
     which = sys.argv[1] if len(sys.argv) > 1 else 'all'
+    if which in ('narrow', 'all'):
+        # the value encoder's narrow convs: direct split-MFMA kernel vs the ring kernel (APPLESTAR_CONV_F32_NARROW)
+        for B, H, W, cin, cout in [(390, 76, 80, 16, 16), (390, 38, 40, 16, 32), (390, 38, 40, 32, 16),
+                                   (390, 19, 20, 32, 32)]:
+            x = torch.randn(B, H, W, cin, device='cuda')
+            w = torch.randn(cout, 3, 3, cin, device='cuda') / 30
+            b = torch.randn(cout, device='cuda')
+            flop = 2.0 * B * H * W * cout * 9 * cin
+            emit('conv3x3_f32', [B, H, W, cin, cout], timed(lambda: C.conv3x3_f32(x, w, b, None, 1)), flop)
     if which in ('conv', 'all'):
         for B, H, W, cin, cout in CONV:
             x = torch.randn(B, H, W, cin, device='cuda')
