@@ -11,6 +11,7 @@
 //   scatter columns of the 1x1 conv) are added by scatter_add_rows; relu_cast finishes.
 #include "../common.h"
 #include "../kernels.h"
+#include "../split_mfma.h"
 
 #include <cstdlib>
 
@@ -945,6 +946,128 @@ __global__ __launch_bounds__(256) void spatial_dense_wgrad_mfma_kernel(SpatialPl
   }
 }
 
+// fp32 form of the MFMA weight gradient (the fp32 step): the dense input X is exact in bf16, so splitting only the
+// fp32 dpre (gated by the projection's ReLU) exactly into three bf16 planes (split_mfma.h truncation split:
+// dpre = d0 + d1 + d2) makes dW = sum_p (d0 + d1 + d2)[p][n] X[p][c] three bf16 MFMAs per step, each product exact,
+// accumulated in fp32.  The scalar fp32 kernel above streams the same 2.4 GB of dpre / gate at ~1 ms per step with a
+// select-add per column; the planes are staged transposed (channel-major) in LDS like the bf16 image.
+__global__ __launch_bounds__(256) void spatial_dense_wgrad_mfma_f32_kernel(SpatialPlanes sp, const float* __restrict__ dpre,
+                                                                           const float* __restrict__ gate,
+                                                                           float* __restrict__ part, int H, int W, int L,
+                                                                           int tiles, int wg_per_obs) {
+  __shared__ __attribute__((aligned(16))) bf16_t dT[3][32 * kSpP];
+  __shared__ __attribute__((aligned(16))) uint32_t msk[kSpTile];
+  __shared__ __attribute__((aligned(16))) uint16_t hgt[kSpTile];
+  __shared__ uint32_t eb[kSpTile];
+  static_assert(sizeof(bf16_t) * 3 * 32 * kSpP >= sizeof(float) * 4 * 32 * 33, "reduction image aliases dT");
+  const int HW = H * W;
+  const int b = blockIdx.x / wg_per_obs, q = blockIdx.x % wg_per_obs;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, g = l >> 4, lr = l & 15;
+  f4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  eb[tid] = 0;
+  for (int tile = q; tile < tiles; tile += wg_per_obs) {
+    const int p0 = tile * kSpTile;
+    const int np = HW - p0 < kSpTile ? HW - p0 : kSpTile;
+    __syncthreads();  // previous tile consumed, eb zeroed
+    mark_effects(sp, eb, b, L, HW, p0, np);
+    __syncthreads();
+    const long base = static_cast<long>(b) * HW + p0;
+    if (tid < np) {
+      msk[tid] = pixel_mask(sp, base + tid, eb[tid]);
+      hgt[tid] = f2bf(static_cast<float>(sp.height[base + tid]) * (1.f / 256.f));
+    } else {
+      msk[tid] = 0;
+      hgt[tid] = 0;
+    }
+    {  // split dpre^T planes: thread = (pixel pair, 16-channel half); tail pixels are zero (clamped loads + select)
+      const int pp = 2 * (tid & 127), h16 = 16 * (tid >> 7);
+      const bool ok0 = pp < np, ok1 = pp + 1 < np;
+      const long r0 = (base + (ok0 ? pp : 0)) * 32 + h16, r1 = (base + (ok1 ? pp + 1 : 0)) * 32 + h16;
+      uint32_t* d0 = reinterpret_cast<uint32_t*>(dT[0]);
+      uint32_t* d1 = reinterpret_cast<uint32_t*>(dT[1]);
+      uint32_t* d2 = reinterpret_cast<uint32_t*>(dT[2]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float4 a = *reinterpret_cast<const float4*>(dpre + r0 + 4 * k);
+        float4 c = *reinterpret_cast<const float4*>(dpre + r1 + 4 * k);
+        float4 ga = make_float4(1.f, 1.f, 1.f, 1.f), gc = ga;
+        if (gate != nullptr) {
+          ga = *reinterpret_cast<const float4*>(gate + r0 + 4 * k);
+          gc = *reinterpret_cast<const float4*>(gate + r1 + 4 * k);
+        }
+        const float av[4] = {ok0 && ga.x > 0.f ? a.x : 0.f, ok0 && ga.y > 0.f ? a.y : 0.f,
+                             ok0 && ga.z > 0.f ? a.z : 0.f, ok0 && ga.w > 0.f ? a.w : 0.f};
+        const float cv[4] = {ok1 && gc.x > 0.f ? c.x : 0.f, ok1 && gc.y > 0.f ? c.y : 0.f,
+                             ok1 && gc.z > 0.f ? c.z : 0.f, ok1 && gc.w > 0.f ? c.w : 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = h16 + 4 * k + j;
+          unsigned s0, s1, s2;
+          split_pair(av[j], cv[j], s0, s1, s2);      // (pixel pp, pixel pp + 1) of channel n, per part
+          const int o = (n * kSpP + pp) >> 1;
+          d0[o] = s0;
+          d1[o] = s1;
+          d2[o] = s2;
+        }
+      }
+    }
+    __syncthreads();
+    eb[tid] = 0;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int p = 64 * w + 32 * ks + 8 * g;
+      bf8v a0[3], a1[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        a0[pl] = as_frag(*reinterpret_cast<const uint4*>(dT[pl] + lr * kSpP + p));
+        a1[pl] = as_frag(*reinterpret_cast<const uint4*>(dT[pl] + (16 + lr) * kSpP + p));
+      }
+      const uint4 m0 = *reinterpret_cast<const uint4*>(msk + p), m1 = *reinterpret_cast<const uint4*>(msk + p + 4);
+      const uint4 hh = *reinterpret_cast<const uint4*>(hgt + p);
+      const uint32_t mm[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+      const uint32_t hw[4] = {hh.x, hh.y, hh.z, hh.w};
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) {
+        const int c = 16 * ct + lr;
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          v[j] = (((mm[2 * j] >> c) & 1u) ? 0x3F80u : 0u) | (((mm[2 * j + 1] >> c) & 1u) ? 0x3F800000u : 0u);
+        if (c == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) v[j] = hw[j];
+        }
+        const bf8v bx = as_frag(make_uint4(v[0], v[1], v[2], v[3]));
+#pragma unroll
+        for (int pl = 2; pl >= 0; --pl) {   // smallest part first
+          acc[0][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[pl], bx, acc[0][ct], 0, 0, 0);
+          acc[1][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[pl], bx, acc[1][ct], 0, 0, 0);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(dT[0]);  // [4 waves][32 n][33]
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[(w * 32 + 16 * nt + 4 * g + i) * 33 + 16 * ct + lr] = acc[nt][ct][i];
+  __syncthreads();
+  float* row = part + static_cast<long>(blockIdx.x) * (32 * 24 + 32);
+  for (int i = tid; i < 32 * 25; i += 256) {
+    const int nn = i / 25, k = i % 25;
+    const float s = red[nn * 33 + k] + red[(32 + nn) * 33 + k] + red[(64 + nn) * 33 + k] + red[(96 + nn) * 33 + k];
+    if (k < 24) row[nn * 24 + k] = s;
+    else row[32 * 24 + nn] = s;
+  }
+}
+
 // APPLESTAR_SPATIAL_MFMA=0 selects the scalar fp32 kernels (A/B measurements)
 bool spatial_mfma() {
   static const bool on = [] {
@@ -1084,6 +1207,10 @@ void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, const void* 
   else if (dt == DT_BF16)
     hipLaunchKernelGGL(spatial_dense_wgrad_kernel<bf16_t>, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256), 0, s, sp,
                        static_cast<const bf16_t*>(dpre), static_cast<const bf16_t*>(gate), part, H, W, L, tiles, kSpWgPerObs);
+  else if (spatial_mfma())
+    hipLaunchKernelGGL(spatial_dense_wgrad_mfma_f32_kernel, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256), 0, s,
+                       sp, static_cast<const float*>(dpre), static_cast<const float*>(gate), part, H, W, L, tiles,
+                       kSpWgPerObs);
   else
     hipLaunchKernelGGL(spatial_dense_wgrad_kernel<float>, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256), 0, s, sp,
                        static_cast<const float*>(dpre), static_cast<const float*>(gate), part, H, W, L, tiles, kSpWgPerObs);

@@ -201,11 +201,13 @@ def test_spatial_embed_matches_reference_planes(autocast):
         assert _err(a, r) < tol * max(1, r.abs().max().item()) * 2
 
 
+@pytest.mark.parametrize('fp32', [False, True], ids=['bf16', 'fp32'])
 @pytest.mark.parametrize('crowded', [False, True])
-def test_spatial_embed_partial_tile(crowded):
+def test_spatial_embed_partial_tile(crowded, fp32):
     """Map sizes that are not a multiple of the kernels' 256-pixel tile (odd pixel count: the last
     tile is partial and its pixel pairs straddle the end) against an fp32 reference of the planes.
-    crowded: 300 entities inside the first tile (more than its 256-entry compacted list)."""
+    crowded: 300 entities inside the first tile (more than its 256-entry compacted list).  fp32: the fp32 step's
+    kernels (the weight gradient on three exact bf16 parts of dpre against the exact-in-bf16 planes), held to 1e-5."""
     from applestar_amd.lib.features import SPATIAL_ONE_HOT, EFFECT_KEYS
     torch.manual_seed(11)
     B, H, W, Nn, L = 3, 37, 45, (300 if crowded else 9), 5
@@ -220,8 +222,13 @@ def test_spatial_embed_partial_tile(crowded):
     rows = torch.randn(B, Nn, 32, device=DEV) * (torch.arange(Nn, device=DEV)[None] < en[:, None]).unsqueeze(2)
     w = (torch.randn(32, 24, device=DEV) * 0.3).requires_grad_()
     b = (torch.randn(32, device=DEV) * 0.1).requires_grad_()
-    with torch.autocast('cuda', dtype=torch.bfloat16):
-        out = N.spatial_embed(sp, rows.to(torch.bfloat16), ex, ey, en, w, b)
+    if fp32:
+        out = N.spatial_embed(sp, rows, ex, ey, en, w, b)
+    else:
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            out = N.spatial_embed(sp, rows.to(torch.bfloat16), ex, ey, en, w, b)
+    rows_ref = rows if fp32 else rows.to(torch.bfloat16).float()
+    tol = 1e-5 if fp32 else 2e-2
     planes = [sp['height_map'].float().unsqueeze(1) / 256]
     for k, n in SPATIAL_ONE_HOT:
         planes.append(torch.nn.functional.one_hot(sp[k].long().clamp(0, n - 1), n).permute(0, 3, 1, 2).float())
@@ -235,17 +242,17 @@ def test_spatial_embed_partial_tile(crowded):
     ent = torch.zeros(B, 32, H, W, device=DEV)
     for i in range(B):
         for j in range(int(en[i])):
-            ent[i, :, ey[i, j], ex[i, j]] += rows[i, j].to(torch.bfloat16).float()
+            ent[i, :, ey[i, j], ex[i, j]] += rows_ref[i, j]
     pre = pre + ent
     ref = torch.relu(pre)
-    assert _err(out, ref) < 2e-2 * max(1, ref.abs().max().item())
+    assert _err(out, ref) < tol * max(1, ref.abs().max().item())
     # channels_last gradient: the NHWC-contiguous dout takes the fused ReLU-gate path of the backward
     # (the NCHW gradient of test_spatial_embed_matches_reference_planes takes the act_grad path)
     g = torch.randn_like(ref).contiguous(memory_format=torch.channels_last)
     out.backward(g.to(out.dtype))
-    (pre * (out.detach().float() > 0)).backward(g.to(torch.bfloat16).float())
-    assert _err(w.grad, wr.grad) < 2e-2 * max(1, wr.grad.abs().max().item())
-    assert _err(b.grad, br.grad) < 2e-2 * max(1, br.grad.abs().max().item())
+    (pre * (out.detach().float() > 0)).backward(g if fp32 else g.to(torch.bfloat16).float())
+    assert _err(w.grad, wr.grad) < tol * max(1, wr.grad.abs().max().item())
+    assert _err(b.grad, br.grad) < tol * max(1, br.grad.abs().max().item())
 
 
 @pytest.mark.parametrize('lens', [[1, 64, 65, 200, 511], [37], [128, 3, 300]])
