@@ -434,8 +434,9 @@ std::vector<at::Tensor> spatial_embed_pool_fwd(const std::vector<at::Tensor>& pl
   TORCH_CHECK(w_dense.size(0) == 32 && w_dense.size(1) == 24 && w_dense.scalar_type() == at::kFloat &&
               bias.scalar_type() == at::kFloat && bias.numel() == 32, "spatial_embed_pool: w_dense [32,24], bias fp32");
   check_cuda(rows, "rows");
-  TORCH_CHECK(rows.dim() == 3 && rows.size(0) == B && rows.size(2) == 32 && rows.scalar_type() == at::kBFloat16,
-              "spatial_embed_pool: rows [B,N,32] bf16");
+  TORCH_CHECK(rows.dim() == 3 && rows.size(0) == B && rows.size(2) == 32 && rows.is_contiguous() &&
+              (rows.scalar_type() == at::kBFloat16 || rows.scalar_type() == at::kFloat),
+              "spatial_embed_pool: rows [B,N,32] bf16 / fp32 (the pooled map takes rows' dtype)");
   TORCH_CHECK(ex.scalar_type() == at::kByte && ey.scalar_type() == at::kByte && entity_num.scalar_type() == at::kLong &&
               ex.is_contiguous() && ey.is_contiguous() && entity_num.is_contiguous(),
               "spatial_embed_pool: entity x/y uint8, entity_num int64, contiguous");
@@ -445,7 +446,8 @@ std::vector<at::Tensor> spatial_embed_pool_fwd(const std::vector<at::Tensor>& pl
   as::spatial_embed_pool(sp, w_dense.data_ptr<float>(), bias.data_ptr<float>(), rows.data_ptr(), ex.data_ptr<uint8_t>(),
                          ey.data_ptr<uint8_t>(), entity_num.data_ptr<int64_t>(), pooled.data_ptr(),
                          pos.data_ptr<uint8_t>(), static_cast<int>(B), static_cast<int>(rows.size(1)),
-                         static_cast<int>(H), static_cast<int>(W), static_cast<int>(L), stream());
+                         static_cast<int>(H), static_cast<int>(W), static_cast<int>(L), stream(),
+                         rows.scalar_type() == at::kFloat);
   return {pooled, pos};
 }
 
@@ -721,14 +723,16 @@ at::Tensor maxpool2_bwd_relu(const at::Tensor& dy, const at::Tensor& pos, const 
   check_cuda(dy, "dy");
   check_cuda(pos, "pos");
   check_cuda(y, "y");
-  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 && dy.dim() == 4 &&
+  TORCH_CHECK(((dy.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16) ||
+               (dy.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat)) && dy.dim() == 4 &&
+              dy.is_contiguous() && y.is_contiguous() && pos.is_contiguous() &&
               dy.sizes() == pos.sizes() && dy.sizes() == y.sizes() && H % 2 == 0 && W % 2 == 0 &&
               dy.size(1) == H / 2 && dy.size(2) == W / 2 && dy.size(3) % 8 == 0, "maxpool2_bwd_relu: shapes");
   TORCH_CHECK(dy.numel() < (1L << 31) - (1L << 24), "maxpool2_bwd_relu: size");
   c10::hip::HIPGuard g(dy.device().index());
   auto dx = at::empty({dy.size(0), H, W, dy.size(3)}, dy.options());
   as::maxpool2_bwd_relu(dy.data_ptr(), pos.data_ptr<uint8_t>(), y.data_ptr(), dx.data_ptr(), dy.size(0), H, W,
-                        dy.size(3), stream());
+                        dy.size(3), stream(), dy.scalar_type() == at::kFloat);
   return dx;
 }
 

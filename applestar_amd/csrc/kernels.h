@@ -139,7 +139,7 @@ void spatial_embed_fused(const SpatialPlanes& sp, const float* wd, const float* 
 bool spatial_pool_supported(int H, int W);
 void spatial_embed_pool(const SpatialPlanes& sp, const float* wd, const float* bias, const void* rows, const uint8_t* ex,
                         const uint8_t* ey, const int64_t* entity_num, void* pooled, uint8_t* pos, int B, int N, int H,
-                        int W, int L, hipStream_t s);
+                        int W, int L, hipStream_t s, bool f32 = false);
 // per-workgroup partial rows [spatial_wgrad_blocks(B)][32*24 + 32] of dWd (n-major) and db from dpre [B*H*W, 32]
 int spatial_wgrad_blocks(int B);
 void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, const void* gate, int dt, float* part, int B, int H,
@@ -205,7 +205,7 @@ void maxpool2_bwd(const void* dy, const uint8_t* pos, void* dx, int dt, int B, i
                   const void* mask = nullptr);
 // bf16, even H / W: dx = dy at the argmax where the pooled ReLU output y > 0, else 0 (relu -> maxpool2 backward)
 void maxpool2_bwd_relu(const void* dy, const uint8_t* pos, const void* y, void* dx, int B, int H, int W, int C,
-                       hipStream_t s);
+                       hipStream_t s, bool f32 = false);
 // out [S, C] fp32 = per-segment row sums of x [T, C] (segments cu[s]..cu[s+1]); C <= 1024, C % 4 == 0
 void segment_sum(const void* x, int dt, const int* cu, float* out, int S, int C, hipStream_t s);
 // LayerNorm affine gradients: per row slice s of ln_affine_slices(R), part[s] = [sum dy*xh (C) | sum dy (C)]

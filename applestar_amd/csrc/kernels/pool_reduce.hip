@@ -322,14 +322,58 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_relu_kernel(const bf16_t* __
     *reinterpret_cast<uint4*>(dx + i00 + row + C) = make_uint4(outw[3][0], outw[3][1], outw[3][2], outw[3][3]);
   }
 }
+// fp32 form (the fp32 step's fused spatial embed + pool): 8 channels of one pooled pixel per thread, the gradient
+// written at the argmax when the pooled ReLU output there is positive, zeros elsewhere (two 16-B stores per window
+// position)
+__global__ __launch_bounds__(256) void maxpool2_bwd_relu_f32_kernel(const float* __restrict__ dy,
+                                                                    const uint8_t* __restrict__ pos,
+                                                                    const float* __restrict__ y, float* __restrict__ dx,
+                                                                    int B, int H, int W, int C) {
+  const int Ho = H >> 1, Wo = W >> 1, C8 = C >> 3;
+  const int total = B * Ho * Wo * C8;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c8 = i % C8;
+    int r = i / C8;
+    const int ox = r % Wo;
+    r /= Wo;
+    const int oy = r % Ho;
+    const int b = r / Ho;
+    const long oi = static_cast<long>(i) * 8;
+    const float4 g0 = *reinterpret_cast<const float4*>(dy + oi), g1 = *reinterpret_cast<const float4*>(dy + oi + 4);
+    const float4 y0 = *reinterpret_cast<const float4*>(y + oi), y1 = *reinterpret_cast<const float4*>(y + oi + 4);
+    const uint2 pp = *reinterpret_cast<const uint2*>(pos + oi);
+    const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float yv[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+    float o[4][8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t p = ((k < 4 ? pp.x : pp.y) >> (8 * (k & 3))) & 3u;
+      const float v = yv[k] > 0.f ? gv[k] : 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t][k] = p == static_cast<uint32_t>(t) ? v : 0.f;
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const long px = (static_cast<long>(b) * H + 2 * oy + (t >> 1)) * W + 2 * ox + (t & 1);
+      float* d = dx + px * C + 8 * c8;
+      *reinterpret_cast<float4*>(d) = make_float4(o[t][0], o[t][1], o[t][2], o[t][3]);
+      *reinterpret_cast<float4*>(d + 4) = make_float4(o[t][4], o[t][5], o[t][6], o[t][7]);
+    }
+  }
+}
+
 }  // namespace
 
 void maxpool2_bwd_relu(const void* dy, const uint8_t* pos, const void* y, void* dx, int B, int H, int W, int C,
-                       hipStream_t s) {
+                       hipStream_t s, bool f32) {
   const long n = static_cast<long>(B) * (H / 2) * (W / 2) * (C / 8);
   if (n == 0) return;
-  hipLaunchKernelGGL(maxpool2_bwd_relu_kernel, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const bf16_t*>(dy), pos,
-                     static_cast<const bf16_t*>(y), static_cast<bf16_t*>(dx), B, H, W, C);
+  if (f32)
+    hipLaunchKernelGGL(maxpool2_bwd_relu_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const float*>(dy),
+                       pos, static_cast<const float*>(y), static_cast<float*>(dx), B, H, W, C);
+  else
+    hipLaunchKernelGGL(maxpool2_bwd_relu_kernel, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const bf16_t*>(dy), pos,
+                       static_cast<const bf16_t*>(y), static_cast<bf16_t*>(dx), B, H, W, C);
 }
 
 void maxpool2_fwd(const void* x, void* y, uint8_t* pos, int dt, int B, int H, int W, int C, hipStream_t s) {

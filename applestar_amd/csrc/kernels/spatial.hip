@@ -697,14 +697,19 @@ __global__ __launch_bounds__(256) void spatial_embed_mfma_kernel(SpatialPlanes s
 constexpr int kPoolTile = 320;
 constexpr int kPoolMF = kPoolTile / 64;   // 16-pixel MFMA row fragments per wave
 
+// T = bf16_t: the mixed-precision step (W as hi + lo bf16, values compared as the bf16 map would hold them);
+// T = float: the fp32 step (W as three bf16 parts, ~fp32-exact products against the exact-in-bf16 planes; fp32
+// entity rows, fp32 pooled output)
+template <typename T>
 __global__ __launch_bounds__(256) void spatial_embed_pool_kernel(SpatialPlanes sp, const float* __restrict__ wd,
                                                                  const float* __restrict__ bias,
-                                                                 const bf16_t* __restrict__ rows,
+                                                                 const T* __restrict__ rows,
                                                                  const uint8_t* __restrict__ ex,
                                                                  const uint8_t* __restrict__ ey,
                                                                  const int64_t* __restrict__ entity_num,
-                                                                 bf16_t* __restrict__ pooled, uint8_t* __restrict__ pos,
+                                                                 T* __restrict__ pooled, uint8_t* __restrict__ pos,
                                                                  int N, int H, int W, int L) {
+  constexpr bool F32 = sizeof(T) == 4;
   __shared__ float acc_s[kPoolTile][33];
   __shared__ uint32_t eb[kPoolTile];
   __shared__ uint32_t msk[kPoolTile];
@@ -717,28 +722,33 @@ __global__ __launch_bounds__(256) void spatial_embed_pool_kernel(SpatialPlanes s
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6, g = l >> 4, lr = l & 15;
   for (int i = tid; i < kPoolTile; i += 256) eb[i] = 0;
   if (tid == 0) ent_cnt = 0;
-  bf8v bhi[2], blo[2];
+  bf8v bhi[2], blo[2], bl2[2];
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
     const int n = 16 * nt + lr;
-    uint32_t hw[4], lw[4];
+    uint32_t hw[4], lw[4], l2w[4];
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-      uint32_t h2 = 0, l2 = 0;
+      uint32_t h2 = 0, l2 = 0, m2 = 0;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int c = 8 * g + j + t;
         const float v = c < 24 ? wd[n * 24 + c] : (c == 24 ? bias[n] : 0.f);
         const bf16_t hi = f2bf(v);
-        const bf16_t lo = f2bf(v - bf2f(hi));
+        const float r1 = v - bf2f(hi);
+        const bf16_t lo = f2bf(r1);
+        const bf16_t lo2 = f2bf(r1 - bf2f(lo));
         h2 |= static_cast<uint32_t>(hi) << (16 * t);
         l2 |= static_cast<uint32_t>(lo) << (16 * t);
+        m2 |= static_cast<uint32_t>(lo2) << (16 * t);
       }
       hw[j / 2] = h2;
       lw[j / 2] = l2;
+      l2w[j / 2] = m2;
     }
     bhi[nt] = as_frag(make_uint4(hw[0], hw[1], hw[2], hw[3]));
     blo[nt] = as_frag(make_uint4(lw[0], lw[1], lw[2], lw[3]));
+    bl2[nt] = as_frag(make_uint4(l2w[0], l2w[1], l2w[2], l2w[3]));
   }
   __syncthreads();
   mark_effects(sp, eb, b, L, HW, p0, np);
@@ -763,8 +773,15 @@ __global__ __launch_bounds__(256) void spatial_embed_pool_kernel(SpatialPlanes s
     const bf8v a = as_frag(make_uint4(q0, bit_pair(mb, 2), bit_pair(mb, 4), bit_pair(mb, 6)));
 #pragma unroll
     for (int nt = 0; nt < 2; ++nt) {
-      f4 c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bhi[nt], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-      c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, blo[nt], c, 0, 0, 0);
+      f4 c = f4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (F32) {   // smallest part first
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bl2[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, blo[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bhi[nt], c, 0, 0, 0);
+      } else {
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bhi[nt], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, blo[nt], c, 0, 0, 0);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) acc_s[kPoolMF * 16 * w + 16 * m + 4 * g + i][16 * nt + lr] = c[i];
     }
@@ -782,7 +799,7 @@ __global__ __launch_bounds__(256) void spatial_embed_pool_kernel(SpatialPlanes s
       if (slot < kSpTile) {
         ent_list[slot] = make_int2(n, p);
       } else {
-        for (int c = 0; c < 32; ++c) atomicAdd(&acc_s[p][c], bf2f(rows[bn * 32 + c]));
+        for (int c = 0; c < 32; ++c) atomicAdd(&acc_s[p][c], Cvt<T>::load(rows, bn * 32 + c));
       }
     }
   }
@@ -792,7 +809,7 @@ __global__ __launch_bounds__(256) void spatial_embed_pool_kernel(SpatialPlanes s
     const int c = i & 31;
     const int2 e = ent_list[i >> 5];
     const long bn = static_cast<long>(b) * N + e.x;
-    atomicAdd(&acc_s[e.y][c], bf2f(rows[bn * 32 + c]));
+    atomicAdd(&acc_s[e.y][c], Cvt<T>::load(rows, bn * 32 + c));
   }
   __syncthreads();
   // relu + 2x2 max (first maximum in window order wins, NaN propagates: maxpool2_fwd's rule) -> 8 channels
@@ -803,25 +820,32 @@ __global__ __launch_bounds__(256) void spatial_embed_pool_kernel(SpatialPlanes s
     const int q[4] = {2 * ox, 2 * ox + 1, W + 2 * ox, W + 2 * ox + 1};
     float mv[8];
     uint32_t lo = 0, hi = 0;
+    // compared as the values the unfused map would hold (bf16-rounded in the bf16 step), so ties resolve as
+    // max_pool2x2 on that map
+    auto held = [](float v) { return F32 ? fmaxf(v, 0.f) : bf2f(f2bf(fmaxf(v, 0.f))); };
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      // compared as the bf16 values the unfused map would hold, so ties resolve as max_pool2x2 on that map
-      float m = bf2f(f2bf(fmaxf(acc_s[q[0]][c8 + k], 0.f)));
+      float m = held(acc_s[q[0]][c8 + k]);
       uint32_t pp = 0;
 #pragma unroll
       for (int t = 1; t < 4; ++t) {
-        const float v = bf2f(f2bf(fmaxf(acc_s[q[t]][c8 + k], 0.f)));
+        const float v = held(acc_s[q[t]][c8 + k]);
         if (v > m || isnan(v)) { m = v; pp = t; }
       }
       mv[k] = m;
       if (k < 4) lo |= pp << (8 * k);
       else hi |= pp << (8 * (k - 4));
     }
-    uint32_t o4[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) o4[j] = f2bf2(mv[2 * j], mv[2 * j + 1]);
     const long o = (obase + ox) * 32 + c8;
-    *reinterpret_cast<uint4*>(pooled + o) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+    if constexpr (F32) {
+      *reinterpret_cast<float4*>(pooled + o) = make_float4(mv[0], mv[1], mv[2], mv[3]);
+      *reinterpret_cast<float4*>(pooled + o + 4) = make_float4(mv[4], mv[5], mv[6], mv[7]);
+    } else {
+      uint32_t o4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o4[j] = f2bf2(mv[2 * j], mv[2 * j + 1]);
+      *reinterpret_cast<uint4*>(pooled + o) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
+    }
     *reinterpret_cast<uint2*>(pos + o) = make_uint2(lo, hi);
   }
 }
@@ -1121,10 +1145,14 @@ bool spatial_pool_supported(int H, int W) { return H % 2 == 0 && W % 2 == 0 && 2
 
 void spatial_embed_pool(const SpatialPlanes& sp, const float* wd, const float* bias, const void* rows, const uint8_t* ex,
                         const uint8_t* ey, const int64_t* entity_num, void* pooled, uint8_t* pos, int B, int N, int H,
-                        int W, int L, hipStream_t s) {
-  hipLaunchKernelGGL(spatial_embed_pool_kernel, dim3(B * (H / 2)), dim3(256), 0, s, sp, wd, bias,
-                     static_cast<const bf16_t*>(rows), ex, ey, entity_num, static_cast<bf16_t*>(pooled), pos, N, H, W,
-                     L);
+                        int W, int L, hipStream_t s, bool f32) {
+  if (f32)
+    hipLaunchKernelGGL(spatial_embed_pool_kernel<float>, dim3(B * (H / 2)), dim3(256), 0, s, sp, wd, bias,
+                       static_cast<const float*>(rows), ex, ey, entity_num, static_cast<float*>(pooled), pos, N, H, W, L);
+  else
+    hipLaunchKernelGGL(spatial_embed_pool_kernel<bf16_t>, dim3(B * (H / 2)), dim3(256), 0, s, sp, wd, bias,
+                       static_cast<const bf16_t*>(rows), ex, ey, entity_num, static_cast<bf16_t*>(pooled), pos, N, H, W,
+                       L);
 }
 
 void spatial_effect_bits(const SpatialPlanes& sp, uint8_t* bits, int B, int L, int HW, hipStream_t s) {

@@ -384,19 +384,24 @@ class _SpatialEmbedPool(torch.autograd.Function):
         pooled, pos, ex, ey, entity_num, *tensors = ctx.saved_tensors
         planes, effects = list(tensors[:ctx.n_planes]), list(tensors[ctx.n_planes:])
         H, W = ctx.HW
-        dpre = _C.maxpool2_bwd_relu(dpooled.to(torch.bfloat16).contiguous(), pos, pooled, H, W)
+        dpre = _C.maxpool2_bwd_relu(dpooled.to(pooled.dtype).contiguous(), pos, pooled, H, W)
         drows = _C.spatial_gather_rows(dpre, ex, ey, entity_num, ctx.N).to(ctx.rows_dtype)
         dw, db = _C.spatial_dense_wgrad(planes, effects, dpre)
         return (dw, db, drows) + (None,) * (4 + len(tensors))
 
 
+SPATIAL_POOL_FUSED_F32 = os.environ.get('APPLESTAR_SPATIAL_POOL_FUSED_F32', '1') == '1'
+
+
 def spatial_embed_pool(spatial_info, rows, entity_x, entity_y, entity_num, w_dense, bias):
-    """max_pool2x2(spatial_embed(...)) as [B,32,H/2,W/2] channels_last bf16, or None when the fused stage
-    does not apply (fp32 compute, odd or wide maps)."""
+    """max_pool2x2(spatial_embed(...)) as [B,32,H/2,W/2] channels_last (bf16 under autocast / bf16 rows; fp32 in
+    the fp32 step: the projection on three exact bf16 parts of W against the exact-in-bf16 planes), or None when
+    the fused stage does not apply (odd or wide maps)."""
     from ..lib.features import SPATIAL_ONE_HOT, EFFECT_KEYS
     H, W = spatial_info['height_map'].shape[-2:]
-    if not SPATIAL_POOL_FUSED or not torch.is_autocast_enabled() and rows.dtype != torch.bfloat16 or \
-            not _C.spatial_pool_supported(H, W):
+    lowp = torch.is_autocast_enabled() or rows.dtype == torch.bfloat16
+    f32 = not lowp and rows.dtype == torch.float32 and SPATIAL_POOL_FUSED_F32
+    if not SPATIAL_POOL_FUSED or not (lowp or f32) or not _C.spatial_pool_supported(H, W):
         return None
     planes = [spatial_info['height_map']] + [spatial_info[k] for k, _ in SPATIAL_ONE_HOT]
     planes = [p.to(torch.uint8).contiguous() for p in planes]
@@ -404,8 +409,8 @@ def spatial_embed_pool(spatial_info, rows, entity_x, entity_y, entity_num, w_den
     ex = entity_x.to(torch.uint8).contiguous()
     ey = entity_y.to(torch.uint8).contiguous()
     with torch.autocast('cuda', enabled=False):
-        out = _SpatialEmbedPool.apply(w_dense, bias, rows.to(torch.bfloat16), ex, ey, entity_num.long().contiguous(),
-                                      len(planes), *planes, *effects)
+        out = _SpatialEmbedPool.apply(w_dense, bias, rows.contiguous() if f32 else rows.to(torch.bfloat16), ex, ey,
+                                      entity_num.long().contiguous(), len(planes), *planes, *effects)
     return from_nhwc(out)
 
 

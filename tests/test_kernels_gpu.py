@@ -1139,12 +1139,15 @@ def test_native_linear_reformulated_gemms(R, K, N, relu):
         assert _err(a, r) < 2e-2 * max(1.0, r.abs().max().item())
 
 
+@pytest.mark.parametrize('fp32', [False, True], ids=['bf16', 'fp32'])
 @pytest.mark.parametrize('HW', [(38, 40), (152, 160)])
 @pytest.mark.parametrize('crowded', [False, True])
-def test_spatial_embed_pool_matches_unfused(HW, crowded):
+def test_spatial_embed_pool_matches_unfused(HW, crowded, fp32):
     """Fused relu(embed) -> max_pool2x2 (pixel-row-pair tiles) vs the unfused native embed + maxpool:
-    pooled output bit-equal (same arithmetic, same argmax rule) and the rows / dense-weight / bias
-    gradients equal up to summation order."""
+    bf16: pooled output bit-equal (same arithmetic, same argmax rule) and the rows / dense-weight / bias
+    gradients equal up to summation order.  fp32 (the fp32 step: the projection on three bf16 parts of W, fp32
+    entity rows; backward through the fp32 maxpool2_bwd_relu and the MFMA weight gradient without a gate): within
+    fp32 rounding of the unfused fp32 kernels."""
     from applestar_amd.lib.features import SPATIAL_ONE_HOT, EFFECT_KEYS
     from applestar_amd import ops
     torch.manual_seed(31)
@@ -1163,21 +1166,25 @@ def test_spatial_embed_pool_matches_unfused(HW, crowded):
     b0 = torch.randn(32, device=DEV) * 0.1
     outs, grads = [], []
     for fused in (True, False):
-        rows = rows0.to(torch.bfloat16).requires_grad_()
+        rows = (rows0.clone() if fp32 else rows0.to(torch.bfloat16)).requires_grad_()
         w, b = w0.clone().requires_grad_(), b0.clone().requires_grad_()
-        with torch.autocast('cuda', dtype=torch.bfloat16):
+        with torch.autocast('cuda', dtype=torch.bfloat16, enabled=not fp32):
             if fused:
                 y = N.spatial_embed_pool(sp, rows, ex, ey, en, w, b)
                 assert y is not None and y.shape == (B, 32, H // 2, W // 2)
+                assert y.dtype == (torch.float32 if fp32 else torch.bfloat16)
             else:
                 y = ops.max_pool2x2(N.spatial_embed(sp, rows, ex, ey, en, w, b))
         g = torch.randn(B, 32, H // 2, W // 2, device=DEV, generator=torch.Generator(DEV).manual_seed(5))
         y.backward(g.to(y.dtype).contiguous(memory_format=torch.channels_last))
         outs.append(y.detach().float())
         grads.append((rows.grad.float(), w.grad, b.grad))
-    assert torch.equal(outs[0], outs[1])
+    if fp32:
+        assert _err(outs[0], outs[1]) < 1e-5 * max(1, outs[1].abs().max().item())
+    else:
+        assert torch.equal(outs[0], outs[1])
     for a, r in zip(grads[0], grads[1]):
-        assert _err(a, r) < 1e-2 * max(1, r.abs().max().item())
+        assert _err(a, r) < (1e-5 if fp32 else 1e-2) * max(1, r.abs().max().item())
 
 
 @pytest.mark.parametrize('B,H,W', [(3, 152, 160), (2, 6, 10)])
