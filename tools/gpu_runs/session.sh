@@ -1,10 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py tests/test_model_parity_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread -k "spatial or parity" > gpurun_out/sp2_pytest.txt 2>&1 || { tail -40 gpurun_out/sp2_pytest.txt; exit 1; }
-tail -2 gpurun_out/sp2_pytest.txt
-for i in 1 2; do
-  timeout -k 10 200 python bench.py --steps 20 --warmup 5 --precision fp32 --inference 0 > gpurun_out/sp2_f32_$i.json 2>/dev/null || exit 1
-  python -c "import json;d=json.load(open('gpurun_out/sp2_f32_$i.json'));print('fp32 fused pool', $i, d['ms_per_step'])"
-  APPLESTAR_SPATIAL_POOL_FUSED_F32=0 timeout -k 10 200 python bench.py --steps 20 --warmup 5 --precision fp32 --inference 0 > gpurun_out/sp20_f32_$i.json 2>/dev/null || exit 1
-  python -c "import json;d=json.load(open('gpurun_out/sp20_f32_$i.json'));print('fp32 unfused', $i, d['ms_per_step'])"
-done
+timeout -k 10 200 python -u tools/probe_gemm_k128.py > gpurun_out/probe_k128_staged.jsonl 2>&1 || { tail -20 gpurun_out/probe_k128_staged.jsonl; exit 1; }
+APPLESTAR_GEMM_F32_STAGED=0 timeout -k 10 200 python -u tools/probe_gemm_k128.py > gpurun_out/probe_k128_direct.jsonl 2>&1 || { tail -20 gpurun_out/probe_k128_direct.jsonl; exit 1; }
+grep M gpurun_out/probe_k128_staged.jsonl gpurun_out/probe_k128_direct.jsonl
