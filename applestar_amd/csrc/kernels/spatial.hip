@@ -217,6 +217,94 @@ __global__ __launch_bounds__(256) void upsample2x_bwd_v8_kernel(const bf16_t* __
   }
 }
 
+// fp32, C % 4 == 0: the same per-input-pixel stencils with 16-B float4 vectors and 32-bit index math (the generic
+// per-output kernels above did 64-bit divisions and scalar loads: ~180 / 200 us per location-head upsample
+// forward / backward in the fp32 step).  mask (backward, optional): dx *= [mask > 0] (the producer's ReLU).
+__device__ __forceinline__ void f4a(const float4 v, float* f) { f[0] = v.x; f[1] = v.y; f[2] = v.z; f[3] = v.w; }
+
+__global__ __launch_bounds__(256) void upsample2x_fwd_v4f_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                                 int B, int H, int W, int C) {
+  const int C4 = C >> 2;
+  const int total = B * H * W * C4;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c4 = i % C4;
+    int p = i / C4;
+    const int xx = p % W;
+    p /= W;
+    const int yy = p % H;
+    const int b = p / H;
+    const int ys[3] = {yy > 0 ? yy - 1 : 0, yy, yy + 1 < H ? yy + 1 : H - 1};
+    const int xs[3] = {xx > 0 ? xx - 1 : 0, xx, xx + 1 < W ? xx + 1 : W - 1};
+    float r0[3][4], r1[3][4];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      float a[4], m[4], z[4];
+      const long col = static_cast<long>(xs[c]) * C + 4 * c4;
+      f4a(*reinterpret_cast<const float4*>(x + (static_cast<long>(b * H + ys[0]) * W) * C + col), a);
+      f4a(*reinterpret_cast<const float4*>(x + (static_cast<long>(b * H + ys[1]) * W) * C + col), m);
+      f4a(*reinterpret_cast<const float4*>(x + (static_cast<long>(b * H + ys[2]) * W) * C + col), z);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        r0[c][e] = 0.25f * a[e] + 0.75f * m[e];
+        r1[c][e] = 0.75f * m[e] + 0.25f * z[e];
+      }
+    }
+    const long W2 = 2L * W;
+    const long base = ((static_cast<long>(b) * 2 * H + 2 * yy) * W2 + 2 * xx) * C + 4 * c4;
+    auto st = [&](long off, const float (&r)[3][4], bool right) {
+      float o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = right ? 0.75f * r[1][e] + 0.25f * r[2][e] : 0.25f * r[0][e] + 0.75f * r[1][e];
+      *reinterpret_cast<float4*>(y + off) = make_float4(o[0], o[1], o[2], o[3]);
+    };
+    st(base, r0, false);
+    st(base + C, r0, true);
+    st(base + W2 * C, r1, false);
+    st(base + W2 * C + C, r1, true);
+  }
+}
+
+__global__ __launch_bounds__(256) void upsample2x_bwd_v4f_kernel(const float* __restrict__ dy, float* __restrict__ dx,
+                                                                 int B, int H, int W, int C, const float* __restrict__ mask) {
+  const int C4 = C >> 2;
+  const int total = B * H * W * C4;
+  const long W2 = 2L * W;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c4 = i % C4;
+    int p = i / C4;
+    const int xx = p % W;
+    p /= W;
+    const int yy = p % H;
+    const int b = p / H;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ty = 0; ty < 4; ++ty) {
+      const float wy = up_w(ty, yy, H);
+      if (wy == 0.f) continue;
+      const int oy = 2 * yy - 1 + ty;
+#pragma unroll
+      for (int tx = 0; tx < 4; ++tx) {
+        const float w = wy * up_w(tx, xx, W);
+        if (w == 0.f) continue;
+        const int ox = 2 * xx - 1 + tx;
+        float v[4];
+        f4a(*reinterpret_cast<const float4*>(dy + ((static_cast<long>(b) * 2 * H + oy) * W2 + ox) * C + 4 * c4), v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] = fmaf(w, v[e], acc[e]);
+      }
+    }
+    const long d = ((static_cast<long>(b) * H + yy) * W + xx) * C + 4 * c4;
+    if (mask) {
+      const float4 mk = *reinterpret_cast<const float4*>(mask + d);
+      acc[0] = mk.x > 0.f ? acc[0] : 0.f;
+      acc[1] = mk.y > 0.f ? acc[1] : 0.f;
+      acc[2] = mk.z > 0.f ? acc[2] : 0.f;
+      acc[3] = mk.w > 0.f ? acc[3] : 0.f;
+    }
+    *reinterpret_cast<float4*>(dx + d) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  }
+}
+
 // pre [B][H*W][32] fp32 = bias + W_dense . dense_input(pixel)
 // dense columns: 0 height/256 | 1..4 visibility | 5..6 creep | 7..11 player_relative | 12..13 alerts |
 //                14..15 pathable | 16..17 buildable | 18..23 effects
@@ -1108,11 +1196,26 @@ int grid_for(long n) {
 
 }  // namespace
 
+// APPLESTAR_UPSAMPLE_V4F=0: the generic per-output fp32 kernels (A/B switch)
+bool upsample_v4f() {
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_UPSAMPLE_V4F");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void upsample2x_fwd(const void* x, void* y, int dt, int B, int H, int W, int C, hipStream_t s) {
   const long n8 = static_cast<long>(B) * H * W * (C / 8);
   if (dt == DT_BF16 && C % 8 == 0 && n8 < (1L << 31) - (1L << 24)) {
     hipLaunchKernelGGL(upsample2x_fwd_v8_kernel, dim3(grid_for(n8)), dim3(256), 0, s, static_cast<const bf16_t*>(x),
                        static_cast<bf16_t*>(y), B, H, W, C);
+    return;
+  }
+  const long n4 = static_cast<long>(B) * H * W * (C / 4);
+  if (dt != DT_BF16 && C % 4 == 0 && n4 < (1L << 31) - (1L << 24) && upsample_v4f()) {
+    hipLaunchKernelGGL(upsample2x_fwd_v4f_kernel, dim3(grid_for(n4)), dim3(256), 0, s, static_cast<const float*>(x),
+                       static_cast<float*>(y), B, H, W, C);
     return;
   }
   const long n = static_cast<long>(B) * 4 * H * W * (C / 4);
@@ -1132,6 +1235,11 @@ void upsample2x_bwd(const void* dy, void* dx, int dt, int B, int H, int W, int C
     return;
   }
   const long n = static_cast<long>(B) * H * W * (C / 4);
+  if (dt != DT_BF16 && C % 4 == 0 && n < (1L << 31) - (1L << 24) && upsample_v4f()) {
+    hipLaunchKernelGGL(upsample2x_bwd_v4f_kernel, dim3(grid_for(n)), dim3(256), 0, s, static_cast<const float*>(dy),
+                       static_cast<float*>(dx), B, H, W, C, static_cast<const float*>(mask));
+    return;
+  }
   if (dt == DT_BF16)
     hipLaunchKernelGGL(upsample2x_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, s,
                        static_cast<const bf16_t*>(dy), static_cast<bf16_t*>(dx), B, H, W, C,
