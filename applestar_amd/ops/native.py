@@ -536,22 +536,33 @@ def upsample_conv_out(x, weight, bias):
 
 
 # ---------------------------------------------------------------------------- max-pool 2x2 (NHWC)
+POOL_BWD_RELU = os.environ.get('APPLESTAR_POOL_BWD_RELU', '1') == '1'
+
+
 class _MaxPool2(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_nhwc):
         y, pos = _C.maxpool2_fwd(x_nhwc)
-        # an fp32 ReLU output as input: the backward applies its mask (the producer conv skips its threshold)
+        # an fp32 ReLU output as input: the backward applies its mask (the producer conv skips its threshold).  The
+        # mask at the argmax is (pooled value > 0) - the pooled value IS the input there - so the backward reads the
+        # pooled output (maxpool2_bwd_relu: one thread per pooled pixel) instead of the full-resolution input
         relu_in = x_nhwc.dtype == torch.float32 and x_nhwc.is_contiguous() and _relu_src(x_nhwc)
-        ctx.save_for_backward(pos, x_nhwc if relu_in else None)
-        ctx.hw = (x_nhwc.shape[1], x_nhwc.shape[2])
+        H, W = x_nhwc.shape[1], x_nhwc.shape[2]
+        ctx.pooled_mask = relu_in and POOL_BWD_RELU and H % 2 == 0 and W % 2 == 0 and x_nhwc.shape[3] % 8 == 0
+        ctx.save_for_backward(pos, y if ctx.pooled_mask else (x_nhwc if relu_in else None))
+        ctx.x_ptr = x_nhwc.data_ptr() if relu_in else None
+        ctx.hw = (H, W)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        pos, x = ctx.saved_tensors
-        dx = _C.maxpool2_bwd(dy.contiguous(), pos, *ctx.hw, x)
-        if x is not None:
-            _MASKED_DX[x.data_ptr()] = (dx, dx._version)
+        pos, m = ctx.saved_tensors
+        if ctx.pooled_mask:
+            dx = _C.maxpool2_bwd_relu(dy.to(m.dtype).contiguous(), pos, m, *ctx.hw)
+        else:
+            dx = _C.maxpool2_bwd(dy.contiguous(), pos, *ctx.hw, m)
+        if ctx.x_ptr is not None:
+            _MASKED_DX[ctx.x_ptr] = (dx, dx._version)
         return dx
 
 
