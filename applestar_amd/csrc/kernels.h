@@ -287,7 +287,7 @@ int wgrad_splits(long R, int N, int K);
 // ---- multi_copy.hip ----------------------------------------------------------------------------
 constexpr int kCopyMaxT = 64;
 constexpr long kCopyChunk = 8192;
-constexpr long kCopyRawChunk = 65536;  // bytes per workgroup in raw mode (a multiple of 16)
+constexpr long kCopyRawChunk = 16384;  // bytes per workgroup in raw mode (a multiple of 16 x 256)
 struct CopyArgs {                     // passed by value (< 2 KB of kernel arguments)
   int ntensors;
   int chunk_start[kCopyMaxT + 1];     // prefix sums of ceil(n / kCopyChunk) (raw: ceil(n / kCopyRawChunk))
