@@ -373,7 +373,14 @@ def test_data_parallel_two_ranks_finite_and_identical(tmp_path, precision):
            '--steps', '3', '--batch', '2', '--unroll', '8', '--precision', precision]
     res = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=400)
     assert res.returncode == 0, res.stderr[-3000:]
-    recs = [json.loads(l) for l in res.stdout.splitlines() if l.startswith('{')]
+    # the two ranks share the launcher's stdout: a line may hold two records back to back
+    recs, dec = [], json.JSONDecoder()
+    for line in res.stdout.splitlines():
+        i = line.find('{')
+        while i >= 0:
+            obj, end = dec.raw_decode(line, i)
+            recs.append(obj)
+            i = line.find('{', end)
     assert len(recs) == 6, res.stdout[-2000:]
     for r in recs:
         assert math.isfinite(r['loss']) and math.isfinite(r['grad_norm']), r

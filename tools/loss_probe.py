@@ -71,7 +71,8 @@ def main():
             rec['nonfinite_grads'] = bad[:40]
             rec['n_nonfinite'] = len(bad)
             reported = True
-        print(json.dumps(rec), flush=True)
+        sys.stdout.write(json.dumps(rec) + '\n')   # one write per record: ranks share the launcher's stdout
+        sys.stdout.flush()
     pdist.finalize()
 
 
