@@ -44,6 +44,23 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyArgs a) {
   const long i0 = static_cast<long>(b - a.chunk_start[t]) * kCopyChunk;
   const long i1 = i0 + kCopyChunk < a.n[t] ? i0 + kCopyChunk : a.n[t];
   const bool sf = (a.dts[t] & 1) != 0, df = (a.dts[t] & 2) != 0;
+  if (i1 - i0 == kCopyChunk) {
+    // a full chunk: the thread's 32 elements loaded before any is stored (see the raw path)
+    constexpr int U = static_cast<int>(kCopyChunk / 256);
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + threadIdx.x + 256 * u;
+      v[u] = sf ? static_cast<const float*>(src)[i] : bf2f(static_cast<const bf16_t*>(src)[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + threadIdx.x + 256 * u;
+      if (df) static_cast<float*>(dst)[i] = v[u];
+      else static_cast<bf16_t*>(dst)[i] = f2bf(v[u]);
+    }
+    return;
+  }
   for (long i = i0 + threadIdx.x; i < i1; i += 256) {
     const float v = sf ? static_cast<const float*>(src)[i] : bf2f(static_cast<const bf16_t*>(src)[i]);
     if (df) static_cast<float*>(dst)[i] = v;
