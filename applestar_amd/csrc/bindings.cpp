@@ -872,8 +872,8 @@ std::vector<at::Tensor> target_unit_sample(const at::Tensor& e, const at::Tensor
 // ---------------------------------------------------------------- fused clip + Adam
 void fused_clip_adam(const at::Tensor& table, const at::Tensor& chunks, const at::Tensor& part,
                      const c10::optional<at::Tensor>& gate, const at::Tensor& norm_out, double max_norm,
-                     const c10::optional<at::Tensor>& mom, const c10::optional<at::Tensor>& scale, bool mom_init,
-                     const c10::optional<at::Tensor>& hp, double lr_bc1, double b1, double b2, double inv_sqrt_bc2,
+                     const c10::optional<at::Tensor>& mom, const c10::optional<at::Tensor>& scale,
+                     const c10::optional<at::Tensor>& mom_init, const c10::optional<at::Tensor>& hp, double lr_bc1, double b1, double b2, double inv_sqrt_bc2,
                      double eps, double wd, bool decoupled) {
   check_cuda(table, "table");
   TORCH_CHECK(table.scalar_type() == at::kLong && chunks.scalar_type() == at::kLong && table.is_contiguous() &&
@@ -888,8 +888,13 @@ void fused_clip_adam(const at::Tensor& table, const at::Tensor& chunks, const at
   }
   float* mp = nullptr;
   float* sp = nullptr;
+  float* ip = nullptr;
   if (mom && mom->defined()) {
-    TORCH_CHECK(scale && scale->defined(), "fused_clip_adam: momentum_norm needs mom and scale");
+    TORCH_CHECK(scale && scale->defined() && mom_init && mom_init->defined(),
+                "fused_clip_adam: momentum_norm needs mom, scale and the init flag");
+    TORCH_CHECK(mom_init->scalar_type() == at::kFloat && mom_init->numel() == 1 && mom_init->is_cuda() &&
+                mom->is_cuda() && mom->device() == table.device(), "fused_clip_adam: mom / init flag on the device");
+    ip = mom_init->data_ptr<float>();
     TORCH_CHECK(mom->scalar_type() == at::kFloat && mom->numel() == nt && mom->is_contiguous() &&
                 scale->scalar_type() == at::kFloat && scale->numel() == nt && scale->is_contiguous(),
                 "fused_clip_adam: mom / scale fp32 [ntensors]");
@@ -904,7 +909,7 @@ void fused_clip_adam(const at::Tensor& table, const at::Tensor& chunks, const at
   c10::hip::HIPGuard g(table.device().index());
   as::fused_clip_adam(table.data_ptr(), reinterpret_cast<const long*>(chunks.data_ptr<int64_t>()),
                       static_cast<int>(nch), static_cast<int>(nt), part.data_ptr<float>(), gp,
-                      norm_out.data_ptr<float>(), static_cast<float>(max_norm), mp, sp, mom_init ? 1 : 0, hpp,
+                      norm_out.data_ptr<float>(), static_cast<float>(max_norm), mp, sp, ip, hpp,
                       static_cast<float>(lr_bc1), static_cast<float>(b1), static_cast<float>(b2),
                       static_cast<float>(inv_sqrt_bc2), static_cast<float>(eps), static_cast<float>(wd),
                       decoupled ? 1 : 0, stream());

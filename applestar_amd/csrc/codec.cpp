@@ -261,6 +261,17 @@ struct Decoder {
     return s < end && *s == c;
   }
 
+  unsigned hex4(const char* p) const {
+    unsigned v = 0;
+    for (int i = 0; i < 4; ++i) {
+      const char c = p[i];
+      const int d = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+      if (d < 0) fail("bad \\u escape");
+      v = v * 16 + static_cast<unsigned>(d);
+    }
+    return v;
+  }
+
   std::string str() {
     expect('"');
     std::string out;
@@ -283,10 +294,11 @@ struct Decoder {
         case 't': out.push_back('\t'); break;
         case 'u': {
           if (end - s < 4) fail("bad \\u escape");
-          unsigned cp = static_cast<unsigned>(std::stoul(std::string(s, 4), nullptr, 16));
+          unsigned cp = hex4(s);
           s += 4;
           if (cp >= 0xD800 && cp < 0xDC00 && end - s >= 6 && s[0] == '\\' && s[1] == 'u') {
-            const unsigned lo = static_cast<unsigned>(std::stoul(std::string(s + 2, 4), nullptr, 16));
+            const unsigned lo = hex4(s + 2);
+            if (lo < 0xDC00 || lo >= 0xE000) fail("bad surrogate pair");
             s += 6;
             cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
           }
@@ -315,37 +327,75 @@ struct Decoder {
     return out;
   }
 
+  // a JSON integer, parsed inside [s, end) only (never past the header) and overflow-checked
   int64_t integer() {
     ws();
-    char* e = nullptr;
-    const long long v = strtoll(s, &e, 10);
-    if (e == s) fail("expected an integer");
-    s = e;
-    return v;
+    bool neg = false;
+    if (s < end && (*s == '-' || *s == '+')) neg = *s++ == '-';
+    if (s >= end || *s < '0' || *s > '9') fail("expected an integer");
+    uint64_t v = 0;
+    while (s < end && *s >= '0' && *s <= '9') {
+      const unsigned d = static_cast<unsigned>(*s++ - '0');
+      if (v > (static_cast<uint64_t>(INT64_MAX) - d) / 10) fail("integer out of range");
+      v = v * 10 + d;
+    }
+    return neg ? -static_cast<int64_t>(v) : static_cast<int64_t>(v);
+  }
+
+  // the literal `w` at s (bounded by end); consumes it when present
+  bool lit(const char* w) {
+    const size_t k = std::strlen(w);
+    if (static_cast<size_t>(end - s) < k || std::memcmp(s, w, k) != 0) return false;
+    s += k;
+    return true;
+  }
+
+  // a tensor descriptor must describe exactly its bytes: non-negative dims, nbytes = prod(shape) * element size
+  // (overflow-checked), and [off, off + nbytes) inside the body
+  void check_tensor(at::ScalarType dt, const std::vector<int64_t>& shape, int64_t off, int64_t nbytes) const {
+    if (nbytes < 0 || off < 0) fail("negative tensor offset / size");
+    uint64_t want = static_cast<uint64_t>(at::elementSize(dt));
+    for (int64_t d : shape) {
+      if (d < 0) fail("negative tensor dimension");
+      if (d && want > static_cast<uint64_t>(INT64_MAX) / static_cast<uint64_t>(d)) fail("tensor size overflows");
+      want *= static_cast<uint64_t>(d);
+    }
+    if (want != static_cast<uint64_t>(nbytes)) fail("tensor size mismatch");
+    if (nbytes > body_len || off > body_len - nbytes) fail("tensor outside the body");
   }
 
   py::object value() {   // JSON scalar -> Python object
     ws();
     if (s >= end) fail("truncated header");
     if (*s == '"') return py::str(str());
-    if (!strncmp(s, "null", 4)) { s += 4; return py::none(); }
-    if (!strncmp(s, "true", 4)) { s += 4; return py::bool_(true); }
-    if (!strncmp(s, "false", 5)) { s += 5; return py::bool_(false); }
-    if (!strncmp(s, "NaN", 3)) { s += 3; return py::float_(std::nan("")); }
-    if (!strncmp(s, "Infinity", 8)) { s += 8; return py::float_(INFINITY); }
-    if (!strncmp(s, "-Infinity", 9)) { s += 9; return py::float_(-INFINITY); }
+    if (lit("null")) return py::none();
+    if (lit("true")) return py::bool_(true);
+    if (lit("false")) return py::bool_(false);
+    if (lit("NaN")) return py::float_(std::nan(""));
+    if (lit("Infinity")) return py::float_(INFINITY);
+    if (lit("-Infinity")) return py::float_(-INFINITY);
     const char* st = s;
     bool is_float = false;
-    if (*s == '-' || *s == '+') ++s;
+    if (s < end && (*s == '-' || *s == '+')) ++s;
     while (s < end && ((*s >= '0' && *s <= '9') || *s == '.' || *s == 'e' || *s == 'E' || *s == '-' || *s == '+')) {
       if (*s == '.' || *s == 'e' || *s == 'E') is_float = true;
       ++s;
     }
     std::string num(st, s);
     if (num.empty()) fail("bad value");
-    if (is_float) return py::float_(std::stod(num));
+    if (is_float) {
+      char* e = nullptr;
+      const double v = std::strtod(num.c_str(), &e);
+      if (e != num.c_str() + num.size()) fail("bad number");
+      return py::float_(v);
+    }
     // arbitrary-size ints through Python
-    return py::reinterpret_steal<py::object>(PyLong_FromString(num.c_str(), nullptr, 10));
+    PyObject* v = PyLong_FromString(num.c_str(), nullptr, 10);
+    if (!v) {
+      PyErr_Clear();
+      fail("bad integer");
+    }
+    return py::reinterpret_steal<py::object>(v);
   }
 
   py::object tensor_node() {   // after "__t__":
@@ -369,8 +419,8 @@ struct Decoder {
     const int64_t nbytes = integer();
     expect(']');
     const auto opts = at::TensorOptions().dtype(dt);
+    check_tensor(dt, shape, off, nbytes);
     if (nbytes == 0) return py::reinterpret_steal<py::object>(THPVariable_Wrap(at::empty(shape, opts)));
-    if (off < 0 || off + nbytes > body_len) fail("tensor outside the body");
     at::Tensor t;
     if (copy) {
       t = at::empty(shape, opts);
@@ -494,7 +544,7 @@ py::object tree_loads(py::object data, bool copy) {
   uint64_t hlen = 0;
   std::memcpy(&hlen, p + kMagicLen, 8);
   if (p[kMagicLen + 8] != 0) throw py::value_error("tree_loads: compressed frame (use the Python codec)");
-  if (pre + static_cast<int64_t>(hlen) > n) throw py::value_error("tree_loads: truncated frame");
+  if (hlen > static_cast<uint64_t>(n - pre)) throw py::value_error("tree_loads: truncated frame");
   const int64_t pad = (kAlign - (pre + static_cast<int64_t>(hlen)) % kAlign) % kAlign;
   const int64_t body_start = pre + static_cast<int64_t>(hlen) + pad;
   Decoder d;
@@ -547,7 +597,7 @@ struct StructParser : Decoder {
       expect(',');
       n.nbytes = integer();
       expect(']');
-      if (n.off < 0 || n.off + n.nbytes > body_len) fail("tensor outside the body");
+      check_tensor(n.dt, n.shape, n.off, n.nbytes);
     } else if (tag == "__d__") {
       n.kind = Node::DICT;
       expect('[');
@@ -742,7 +792,9 @@ py::object collate_frames(py::list frames, int64_t pad_entities, py::object devi
       throw py::value_error("collate_frames: not an uncompressed applestar frame");
     uint64_t hlen = 0;
     std::memcpy(&hlen, p + kMagicLen, 8);
+    if (hlen > static_cast<uint64_t>(n - pre)) throw py::value_error("collate_frames: truncated frame");
     const int64_t pad = (kAlign - (pre + static_cast<int64_t>(hlen)) % kAlign) % kAlign;
+    if (pre + static_cast<int64_t>(hlen) + pad > n) throw py::value_error("collate_frames: truncated frame");
     StructParser sp;
     sp.s = reinterpret_cast<const char*>(p + pre);
     sp.end = sp.s + hlen;

@@ -274,7 +274,7 @@ int fused_adam_chunk();
 // mom / scale (fp32 [ntensors]) non-null: momentum_norm clip with threshold max_norm; else pytorch_norm at
 // max_norm (0 = no clip).  hp (fp32 [3] = lr / bc1, 1 / sqrt(bc2), wd) non-null overrides those arguments.
 void fused_clip_adam(const void* table, const long* chunks, int nchunks, int ntensors, float* part,
-                     const float* gate, float* norm_out, float max_norm, float* mom, float* scale, int mom_init,
+                     const float* gate, float* norm_out, float max_norm, float* mom, float* scale, float* mom_init,
                      const float* hp, float lr_bc1, float b1, float b2, float inv_sqrt_bc2, float eps, float wd,
                      int decoupled, hipStream_t s);
 

@@ -8,8 +8,10 @@
 //   1. mt_sumsq: one workgroup per 32K-element chunk of the (tensor, offset) chunk table writes the chunk's
 //      sum of squared gradients into part[chunk]  (fixed order: deterministic, identical on every rank);
 //   2. (momentum_norm only) mt_momentum_clip: one workgroup; per tensor t the norm g_t from its chunks'
-//      partials, scale_t = g_t < thr * mom_t ? 1 : thr * mom_t / (g_t + 1e-6) (1 on the first step),
-//      mom_t = 0.99 mom_t + 0.01 g_t scale_t, and the global norm of the clipped gradients;
+//      partials, scale_t = g_t < thr * mom_t ? 1 : thr * mom_t / (g_t + 1e-6) (1 until the EMA is initialised),
+//      mom_t = 0.99 mom_t + 0.01 g_t scale_t (mom_t = g_t on the initialising step), and the global norm of the
+//      clipped gradients.  "Initialised" is a device flag set by the first KEPT step: a gated first step leaves
+//      the EMA uninitialised (a host-side flag would mark it live at 0 and every later scale would be 0);
 //   3. mt_adam: coef = min(1, max_norm / (||g|| + 1e-6)) (every workgroup sums part[] in the same fixed
 //      order, a few KB from L2) or scale_t, then per element:
 //          g' = coef g (+ wd p),  m = b1 m + (1 - b1) g',  v = b2 v + (1 - b2) g'^2,
@@ -80,10 +82,11 @@ __global__ __launch_bounds__(kOptT) void mt_sumsq_kernel(const TensorRec* __rest
 __global__ __launch_bounds__(kOptT) void mt_momentum_clip_kernel(const TensorRec* __restrict__ tt, int ntensors,
                                                                  const float* __restrict__ part, float thr,
                                                                  float* __restrict__ mom, float* __restrict__ scale,
-                                                                 int init, const float* __restrict__ gate,
+                                                                 float* __restrict__ init_flag, const float* __restrict__ gate,
                                                                  float* __restrict__ norm_out) {
   __shared__ float red[kOptT / 64];
   const bool keep = !gated_off(gate);
+  const bool init = !(init_flag[0] > 0.f);    // read by every thread before thread 0 may set it (block_sum syncs)
   float acc = 0.f;
   for (int t = threadIdx.x; t < ntensors; t += kOptT) {
     const TensorRec r = tt[t];
@@ -102,7 +105,10 @@ __global__ __launch_bounds__(kOptT) void mt_momentum_clip_kernel(const TensorRec
     acc += nw * nw;
   }
   acc = block_sum(acc, red);
-  if (threadIdx.x == 0) norm_out[0] = sqrtf(acc);
+  if (threadIdx.x == 0) {
+    norm_out[0] = sqrtf(acc);
+    if (keep) init_flag[0] = 1.f;
+  }
 }
 
 __global__ __launch_bounds__(kOptT) void mt_adam_kernel(const TensorRec* __restrict__ tt, const long* __restrict__ chunks,
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(kOptT) void mt_adam_kernel(const TensorRec* __restr
 int fused_adam_chunk() { return kChunk; }
 
 void fused_clip_adam(const void* table, const long* chunks, int nchunks, int ntensors, float* part,
-                     const float* gate, float* norm_out, float max_norm, float* mom, float* scale, int mom_init,
+                     const float* gate, float* norm_out, float max_norm, float* mom, float* scale, float* mom_init,
                      const float* hp, float lr_bc1, float b1, float b2, float inv_sqrt_bc2, float eps, float wd,
                      int decoupled, hipStream_t s) {
   if (nchunks <= 0) return;

@@ -188,7 +188,10 @@ def create_league_app(league: League):
 
     @app.route('/league/backup_models', methods=['POST'])
     def backup_models():
-        return ok(league.backup_models(request.json or {}))
+        try:
+            return ok(league.backup_models(request.json or {}))
+        except ValueError as e:
+            return bad(str(e))
 
     @app.route('/league/show_config', methods=['GET'])
     def show_config():

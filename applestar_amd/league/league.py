@@ -16,6 +16,7 @@ from __future__ import annotations
 import itertools
 import json
 import os
+import re
 import queue
 import random
 import shutil
@@ -61,6 +62,10 @@ class League:
         self.cfg = self.whole_cfg.league
         exp = self.whole_cfg.common.experiment_name
         self.root = os.path.abspath(os.path.join(root, 'experiments', exp))
+        # admin routes may only read checkpoints / write backups under these directories (default: the directory
+        # the league runs in, which holds experiments/); extend with ``league.checkpoint_roots``
+        self.allowed_roots = [os.path.realpath(os.path.abspath(root))] + \
+            [os.path.realpath(os.path.abspath(r)) for r in (self.cfg.get('checkpoint_roots') or [])]
         self.model_dir = os.path.join(self.root, 'league_models')
         self.resume_dir = os.path.join(self.root, 'league_resume')
         os.makedirs(self.model_dir, exist_ok=True)
@@ -394,12 +399,23 @@ class League:
                 self.trueskill.set(pid, v.get('mu'), v.get('sigma'))
         return True
 
+    _SAFE_ID = re.compile(r'^[A-Za-z0-9_]+$')
+
+    def _allowed_path(self, path: str) -> bool:
+        """True when ``path`` resolves (symlinks too) inside one of the league's allowed roots."""
+        real = os.path.realpath(os.path.abspath(path))
+        return any(real == r or real.startswith(r + os.sep) for r in self.allowed_roots)
+
     def add_hist_player(self, info: Dict) -> bool:
-        """Copy a checkpoint into the league and add it as a historical player (league.py:558-588)."""
+        """Copy a checkpoint into the league and add it as a historical player (league.py:558-588).  The player id
+        must match ``[A-Za-z0-9_]+`` (it names a file under league_models/) and the checkpoint must lie under an
+        allowed root."""
         ckpt = info.get('checkpoint_path', 'none')
-        if ckpt == 'none' or not os.path.exists(ckpt):
+        if ckpt == 'none' or not os.path.isfile(ckpt) or not self._allowed_path(ckpt):
             return False
         pid = info.get('player_id') or 'none'
+        if pid != 'none' and not self._SAFE_ID.match(str(pid)):
+            return False
         if pid == 'none':
             self._added = getattr(self, '_added', 0) + 1
             pid = f'HP_ADD{self._added}'
@@ -485,6 +501,8 @@ class League:
         info = info or {}
         dst = info.get('backup_dir') or os.path.join(self.root, 'league_models_backup',
                                                      time.strftime('%Y-%m-%d-%H-%M-%S'))
+        if not self._allowed_path(dst):
+            raise ValueError(f'backup_dir {dst!r} is outside the league roots')
         os.makedirs(dst, exist_ok=True)
         n = 0
         for pid in self.correspondent_player_ids(info.get('player_id', 'all')):

@@ -123,8 +123,25 @@ class RLDataLoader:
     def __next__(self):
         return next(self._iter)
 
-    def close(self):
+    @property
+    def ring_bytes(self) -> Optional[int]:
+        """The HBM ring's capacity (None on the host path or after close): a rebuilt loader reuses it."""
+        ring = getattr(self, '_ring', None)
+        return ring.capacity if ring is not None else None
+
+    def close(self, timeout: float = 5.0):
+        """Stop the ingest thread, wait for it, and release the HBM ring (its arena goes back to the caching
+        allocator; the caller may ``torch.cuda.empty_cache()`` before sizing a new ring from free memory)."""
         self._stop.set()
+        if getattr(self, '_avail', None) is not None:
+            with self._avail:
+                self._avail.notify_all()
+        t = getattr(self, '_thread', None)
+        if t is not None and t.is_alive() and t is not threading.current_thread():
+            t.join(timeout)
+        self._iter = iter(())
+        if getattr(self, '_ring', None) is not None:
+            self._ring = None
 
 
 class SyntheticRLDataLoader:

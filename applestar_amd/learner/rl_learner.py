@@ -175,7 +175,7 @@ class RLLearner(BaseLearner):
     def _setup_trainer(self):
         return RLTrainer(self.cfg, device=self.device)
 
-    def _setup_dataloader(self):
+    def _setup_dataloader(self, ring_bytes: Optional[int] = None):
         lc = self.cfg.learner
         c = self.cfg.communication
         if lc.data.get('synthetic') or not c.coordinator_port:
@@ -183,7 +183,7 @@ class RLLearner(BaseLearner):
                                          use_value_feature=lc.use_value_feature)
         return RLDataLoader(Adapter(c.coordinator_ip, c.coordinator_port), lc.player_id, lc.data.batch_size,
                             lc.data.get('buffer_size'), self.device,
-                            ring_bytes=self._ring_bytes(),
+                            ring_bytes=ring_bytes or self._ring_bytes(),
                             max_reuse=int(lc.data.get('max_reuse', 2)))
 
     def _ring_bytes(self) -> int:
@@ -238,12 +238,20 @@ class RLLearner(BaseLearner):
         (``rl_learner.py:244-261``): close the old LearnerComm and dataloader, register again, rebuild the
         dataloader (its HBM trajectory ring is re-allocated on the new coordinator)."""
         self.comm.close()
+        # the old loader's ring is released (ingest thread joined, arena freed and returned to the driver) before
+        # the new one is sized, and the new ring keeps the old capacity: sizing it from mem_get_info while the old
+        # ~hundreds-of-GB arena is still allocated would shrink it to the floor
+        keep_bytes = getattr(self.dataloader, 'ring_bytes', None)
         if hasattr(self.dataloader, 'close'):
             self.dataloader.close()
+        self.dataloader = None
+        if self.device.type == 'cuda':
+            torch.cuda.synchronize(self.device)
+            torch.cuda.empty_cache()
         self.comm = LearnerComm(self.cfg, self)
         if self.cfg.learner.job_type == 'train':
             self.comm.register(self)
-        self.dataloader = self._setup_dataloader()
+        self.dataloader = self._setup_dataloader(ring_bytes=keep_bytes)
         self.info(f'{self.comm.player_id} communication reset')
 
     def _apply_admin(self, kind: str, payload):

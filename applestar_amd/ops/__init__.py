@@ -5,8 +5,11 @@ oracle in tests) and, for GPU tensors, a hand-written HIP/CDNA4 kernel in ``appl
 exposed through :mod:`.native`.  GPU tensors never silently take the reference path for an op that
 has a native kernel: if the extension is missing, :func:`._ext.require` raises.
 
-Ops without a bespoke kernel (plain GEMMs, convolutions) use the vendor libraries through PyTorch
-(hipBLASLt / MIOpen) by design.
+GEMMs and 3x3 convolutions are native too: in fp32 every linear / conv3x3 product (forward, dX, dW) runs on
+the bf16x6 split-MFMA kernels (``gemm_f32.hip``, ``conv3x3_f32.hip``, ``wgrad_f32.hip``) or the few-row kernels of
+``gemm_small.hip``; the library (hipBLASLt through ``torch.mm``) keeps only the handful of products listed by
+``tools/gemm_census.py`` (recurrent LSTM dW, batched pointer logits).  In the bf16 step the entity
+transformer's large products stay on hipBLASLt (faster there, docs/OPEN_ISSUES.md).
 """
 from __future__ import annotations
 
@@ -47,7 +50,8 @@ masked_attention = ref.masked_attention
 
 
 def linear(x, w, b=None, act=None, grad_link=None):
-    """act(x W^T + b).  GPU: hipBLASLt forward / dX, MFMA split-R kernel for dW / db of tall inputs.
+    """act(x W^T + b).  GPU: native split-MFMA GEMM (fp32) / ring or library GEMM (bf16) for the forward and dX
+    with fused bias / ReLU / residual epilogues, split-R MFMA kernel for dW / db of tall inputs.
     ``grad_link``: native GradLink (residual gradient added in the dX GEMM), ignored elsewhere."""
     n = _native(x)
     if n is not None:

@@ -82,6 +82,19 @@ def _collator_main(make_batches: Callable[[], Iterator[Any]], slabs, free_q, rea
         ready_q.put(('error', repr(e)))
 
 
+def check_shm_capacity(nbytes: int, path: str = '/dev/shm', margin: int = 64 << 20) -> None:
+    """Fail early, with the fix in the message, when the shared-memory filesystem cannot hold the slabs (torch's
+    ``share_memory_`` would otherwise die later with a bus error on first touch of an unbacked page)."""
+    import os
+    import shutil
+    if not os.path.isdir(path):
+        return
+    free = shutil.disk_usage(path).free
+    if free < nbytes + margin:
+        raise RuntimeError(f'shared batch slabs need {nbytes >> 20} MiB of {path} but only {free >> 20} MiB are '
+                           f'free: lower learner.data.slab_mb / n_slabs or enlarge {path}')
+
+
 class SharedBatchLoader:
     """Iterator of learner batches produced by a collator process through shared, pinned slabs.
 
@@ -94,6 +107,7 @@ class SharedBatchLoader:
         import torch.multiprocessing as tmp
         self.device = torch.device(device)
         self.gpu = self.device.type == 'cuda'
+        check_shm_capacity(int(n_slabs) * int(slab_bytes))
         ctx = tmp.get_context('spawn')
         self.slabs = [torch.empty(int(slab_bytes), dtype=torch.uint8).share_memory_() for _ in range(n_slabs)]
         self._registered = []
@@ -116,13 +130,23 @@ class SharedBatchLoader:
             self._next = self._stage()
 
     def _get(self):
+        # wait in short slices and keep returning slabs whose H2D copy has finished: with every slab in flight the
+        # collator can only produce once one comes back, so a wait that never releases would deadlock.  After
+        # ~50 ms with nothing ready, block on the oldest in-flight copy (it was enqueued, so it completes).
+        waited = 0.0
         while True:
+            self._release_done()
             try:
-                item = self._ready.get(timeout=5.0)
+                item = self._ready.get(timeout=0.05)
                 break
             except queue.Empty:
-                if not self._proc.is_alive():
-                    raise RuntimeError('shared-batch collator process died')
+                waited += 0.05
+                if self._inflight:
+                    self._release_done(block=True)
+                if waited >= 5.0:
+                    waited = 0.0
+                    if not self._proc.is_alive():
+                        raise RuntimeError('shared-batch collator process died')
         if item is None:
             return None
         if item[0] == 'error':
@@ -130,10 +154,12 @@ class SharedBatchLoader:
         return item
 
     def _release_done(self, block=False):
+        """Return finished slabs to the collator (``block``: also wait for the OLDEST in-flight copy)."""
         while self._inflight and (block or self._inflight[0][0].query()):
             ev, k = self._inflight.popleft()
             ev.synchronize()
             self._free.put(k)
+            block = False
 
     def _stage(self):
         item = self._get()

@@ -46,7 +46,9 @@ class FusedClipAdam:
                  device_hparams: bool = False, segments: Optional[Dict] = None):
         self.opt = optimizer
         self.max_norm = float(max_norm) if max_norm else 0.0
-        self.clip = clip if clip is not None and clip.clip_type == 'momentum_norm' else None
+        # only the 'ema' form of momentum_norm scales per tensor; its 'reference' form (the reference's effective
+        # behaviour, utils/grad_clip.py) is an unclipped step reporting the global norm
+        self.clip = clip if clip is not None and getattr(clip, 'ema', False) else None
         self.device_hparams = device_hparams
         self.segments = segments or {}
         self._hp = None
@@ -199,17 +201,18 @@ class FusedClipAdam:
         g = self.opt.param_groups[0]
         lr_bc1, inv_sqrt_bc2, wd, decoupled = self._host_hp
         b1, b2 = g['betas']
-        mom = scale = None
-        init = False
+        mom = scale = init = None
         if self.clip is not None:
             c = self.clip
             dev = self._part.device
-            if c.norm_mom is None or c.norm_mom.numel() != self.ntensors or c.norm_mom.device != dev:
-                if capturing:
-                    raise RuntimeError('FusedClipAdam: momentum state must exist before a capture')
-                c.norm_mom = torch.zeros(self.ntensors, dtype=torch.float32, device=dev)
-                init = True
-            mom, scale = c.norm_mom, self._scale
+            fresh = c.norm_mom is None or c.norm_mom.numel() != self.ntensors or c.norm_mom.device != dev or \
+                c.mom_init is None or c.mom_init.device != dev
+            if fresh and capturing:
+                raise RuntimeError('FusedClipAdam: momentum state must exist on the device before a capture')
+            # created as (0, not initialised) - the kernel initialises the EMA on the first KEPT step - or moved to
+            # the device when a checkpoint brought it in elsewhere (never re-zeroed)
+            mom, init = c.momentum_state(self.ntensors, dev)
+            scale = self._scale
         norm = torch.empty((), dtype=torch.float32, device=self._part.device)   # per step: callers may keep it
         self._C.fused_clip_adam(self._table, self._chunks, self._part,
                                 gate.reshape(1).float() if gate is not None else None, norm.view(1),

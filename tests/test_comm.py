@@ -65,12 +65,13 @@ def test_stream_channel_put_server_and_dead_server_removal():
         srv.shutdown()
 
 
-def test_protocol_codec_and_import_helper():
+def test_wire_codec_and_import_helper():
+    """The data plane's tensor wire codec (the reference's coordinator/protocol.py encode / decode) is
+    utils/serialize's frame format."""
     import torch
-    from applestar_amd.comm import protocol
-    from applestar_amd.utils import import_helper
+    from applestar_amd.utils import import_helper, serialize
     tree = {'a': torch.arange(10, dtype=torch.int16), 'b': [1.5, 'x', None, {'c': torch.ones(2, 3)}]}
-    out = protocol.decode(protocol.encode(tree, compress=True))
+    out = serialize.loads(serialize.dumps(tree, compress=True))
     assert torch.equal(out['a'], tree['a']) and out['b'][:3] == [1.5, 'x', None]
     assert torch.equal(out['b'][3]['c'], tree['b'][3]['c'])
     assert import_helper.try_import_link() is not None

@@ -1522,7 +1522,7 @@ def test_fused_momentum_norm_adam_matches_torch(segmented):
         segments = None
     oa = torch.optim.Adam(pa, lr=1e-3, weight_decay=1e-5)
     ob = torch.optim.Adam(pb, lr=1e-3, weight_decay=1e-5)
-    ca, cb = GradClip('momentum_norm', 1.0), GradClip('momentum_norm', 1.0)
+    ca, cb = GradClip('momentum_norm', 1.0, momentum_mode='ema'), GradClip('momentum_norm', 1.0, momentum_mode='ema')
     fused = FusedClipAdam(ob, None, clip=cb, segments=segments)
     for step in range(5):
         gs = [torch.randn_like(a) * (1 + 3 * (step % 2)) for a in pa]     # alternating scale: the clip engages
@@ -1543,6 +1543,56 @@ def test_fused_momentum_norm_adam_matches_torch(segmented):
             assert _err(a.detach().reshape(-1), b) < 1e-6 * max(1.0, a.abs().max().item()), step
 
 
+def test_fused_momentum_norm_gated_first_step_and_cpu_resume():
+    """(1) a gated-off FIRST fused momentum_norm step leaves the EMA uninitialised (the device flag),
+    so the next kept step initialises it and updates normally (a host flag would pin every scale to 0);
+    (2) a clip state loaded with map_location='cpu' is moved to the device, not re-zeroed: the fused step then
+    matches the torch GradClip continuing from the same state."""
+    from applestar_amd.utils.fused_optim import FusedClipAdam
+    from applestar_amd.utils.grad_clip import GradClip
+    torch.manual_seed(7)
+    ps = [torch.nn.Parameter(torch.randn(*s, device=DEV)) for s in [(300, 17), (4097,)]]
+    for p in ps:
+        p.grad = torch.full_like(p, float('nan'))
+    opt = torch.optim.Adam(ps, lr=1e-3)
+    clip = GradClip('momentum_norm', 1.0, momentum_mode='ema')
+    fused = FusedClipAdam(opt, None, clip=clip)
+    snap = [p.detach().clone() for p in ps]
+    fused.step(torch.zeros((), device=DEV))
+    torch.cuda.synchronize()
+    assert float(clip.mom_init) == 0.0 and all(torch.equal(p.detach(), s) for p, s in zip(ps, snap))
+    gs = [torch.randn_like(p) for p in ps]
+    for p, g in zip(ps, gs):
+        p.grad.copy_(g)
+    fused.step(torch.ones((), device=DEV))
+    torch.cuda.synchronize()
+    assert float(clip.mom_init) == 1.0
+    assert torch.allclose(clip.norm_mom, torch.stack([g.norm() for g in gs]), rtol=1e-5)
+    assert all(not torch.equal(p.detach(), s) for p, s in zip(ps, snap))
+    # resume from a CPU-mapped clip state
+    sd = {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in clip.state_dict().items()}
+    a = GradClip('momentum_norm', 1.0, momentum_mode='ema')
+    a.load_state_dict({k: (v.clone() if torch.is_tensor(v) else v) for k, v in sd.items()})
+    b = GradClip('momentum_norm', 1.0, momentum_mode='ema')
+    b.load_state_dict(sd)
+    assert b.norm_mom.device.type == 'cpu'
+    qa = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    qb = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    oa, ob = torch.optim.Adam(qa, lr=1e-3), torch.optim.Adam(qb, lr=1e-3)
+    fb = FusedClipAdam(ob, None, clip=b)
+    spike = [torch.randn_like(p) * 50 for p in ps]
+    for x, y, g in zip(qa, qb, spike):
+        x.grad, y.grad = g.clone(), g.clone()
+    a.norm_mom, a.mom_init = a.norm_mom.to(DEV), a.mom_init.to(DEV)
+    na = a.apply(qa)
+    oa.step()
+    nb = fb.step()
+    assert b.norm_mom.is_cuda and abs(float(na) - float(nb)) <= 1e-5 * float(na)
+    assert float(nb) < 0.1 * float(torch.stack([g.norm() for g in spike]).norm())    # the spike was clipped
+    for x, y in zip(qa, qb):
+        assert _err(x.detach().reshape(-1), y.detach().reshape(-1)) < 1e-6 * max(1.0, x.abs().max().item())
+
+
 @pytest.mark.parametrize('clip_type', ['pytorch_norm', 'momentum_norm'])
 def test_fused_adam_gate_skips_update(clip_type):
     """A zero health gate (timed-out LSTM exchange) with NaN gradients leaves the parameters, both Adam moments
@@ -1554,7 +1604,7 @@ def test_fused_adam_gate_skips_update(clip_type):
     for p in ps:
         p.grad = torch.randn_like(p)
     opt = torch.optim.Adam(ps, lr=1e-3, betas=(0.5, 0.99), weight_decay=1e-4)
-    clip = GradClip(clip_type, 1.0)
+    clip = GradClip(clip_type, 1.0, momentum_mode='ema')
     fused = FusedClipAdam(opt, 1.0 if clip_type == 'pytorch_norm' else None, clip=clip)
     fused.step(torch.ones((), device=DEV))                                # state exists, EMA initialised
     snap = [t.clone() for p in ps for t in (p.detach(), opt.state[p]['exp_avg'], opt.state[p]['exp_avg_sq'])]

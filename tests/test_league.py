@@ -133,6 +133,10 @@ def test_http_admin_routes(tmp_path):
     assert c.post('/league/add_hist_player', json={'player_id': 'HPX', 'checkpoint_path': str(ckpt)}).json['code'] == 0
     assert 'HPX' in lg.historical_players
     assert c.post('/league/add_hist_player', json={'checkpoint_path': '/nonexistent'}).json['code'] == 1
+    # no path traversal through the player id, no checkpoint / backup outside the league roots
+    assert c.post('/league/add_hist_player', json={'player_id': '../../evil', 'checkpoint_path': str(ckpt)}).json['code'] == 1
+    assert c.post('/league/add_hist_player', json={'player_id': 'HPY', 'checkpoint_path': '/etc/hostname'}).json['code'] == 1
+    assert c.post('/league/backup_models', json={'backup_dir': '/tmp/../etc/x'}).json['code'] == 1
     assert c.post('/league/update_player', json={'player_id': 'MP0', 'chosen_weight': 3.0,
                                                  'one_phase_step': '1e6'}).json['code'] == 0
     assert lg.active_players['MP0'].chosen_weight == 3.0 and lg.active_players['MP0'].one_phase_step == 1000000

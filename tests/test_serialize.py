@@ -105,3 +105,50 @@ def test_native_collate_frames_matches_collate_obs():
         bad = dict(reqs[1])
         bad.pop('flag')
         NATIVE.collate_frames([serialize.dumps(reqs[0]), serialize.dumps(bad)], 0)
+
+
+def _patched_header(frame: bytes, old: bytes, new: bytes) -> bytes:
+    """The frame with one header substring replaced (hlen re-stamped, body re-aligned as the encoder would)."""
+    import struct
+    pre = len(serialize.MAGIC) + 9
+    hlen = struct.unpack('<Q', frame[len(serialize.MAGIC):len(serialize.MAGIC) + 8])[0]
+    header = frame[pre:pre + hlen]
+    pad = (-(pre + hlen)) % 64
+    body = frame[pre + hlen + pad:]
+    assert old in header
+    header = header.replace(old, new, 1)
+    npad = (-(pre + len(header))) % 64
+    return serialize.MAGIC + struct.pack('<QB', len(header), 0) + header + b'\0' * npad + body
+
+
+@needs_native
+def test_native_decoders_reject_malformed_frames():
+    """a frame whose tensor descriptor disagrees with its bytes, a huge / truncated header
+    length, or a header cut mid-token must raise ValueError in BOTH native decoders (tree_loads and the inference
+    server's collate_frames) - never read outside the frame."""
+    import struct
+    t = {'a': torch.arange(12, dtype=torch.int32).reshape(3, 4), 'b': 1.5}
+    good = serialize.dumps(t)
+    assert serialize.loads(good)['a'].shape == (3, 4)
+    nb = str(12 * 4).encode()
+    bad_frames = [
+        _patched_header(good, b'[3, 4]', b'[300, 4]'),            # shape larger than nbytes
+        _patched_header(good, b'[3, 4]', b'[-3, -4]'),            # negative dims (product matches)
+        _patched_header(good, b', ' + nb + b']', b', -48]'),       # negative nbytes
+        _patched_header(good, b', ' + nb + b']', b', 0]'),         # zero nbytes for a non-empty shape
+        _patched_header(good, b'[3, 4]', b'[3, 99999999999999999999]'),   # overflowing dim
+        good[:len(serialize.MAGIC)] + struct.pack('<Q', 2 ** 63 + 5) + good[len(serialize.MAGIC) + 8:],  # huge hlen
+        good[:len(serialize.MAGIC)] + struct.pack('<Q', len(good)) + good[len(serialize.MAGIC) + 8:],    # hlen > frame
+        good[:len(serialize.MAGIC) + 9 + 20],                     # truncated mid-header
+    ]
+    for i, f in enumerate(bad_frames):
+        with pytest.raises(ValueError):
+            NATIVE.tree_loads(f, True)
+        with pytest.raises(ValueError):
+            NATIVE.collate_frames([f], 0)
+    # a descriptor pointing past the body
+    with pytest.raises(ValueError):
+        NATIVE.tree_loads(_patched_header(good, b'0, ' + nb, b'64, ' + nb) if b'0, ' + nb in good else good[:-8], True)
+    # literal scanning stops at the header end: a header ending in a bare 'tru' prefix
+    with pytest.raises(ValueError):
+        NATIVE.tree_loads(_patched_header(good, b'1.5', b'tru'), True)

@@ -94,3 +94,11 @@ def test_replay_dataloader_shared_batch_process_matches_in_process():
             cmp(next(shared), next(plain))
     finally:
         shared.close()
+
+
+def test_shared_batch_shm_capacity_check():
+    """the slabs are checked against /dev/shm's free space up front."""
+    from applestar_amd.runtime.shared_batch import check_shm_capacity
+    check_shm_capacity(1 << 20)
+    with pytest.raises(RuntimeError, match='slab'):
+        check_shm_capacity(1 << 62)

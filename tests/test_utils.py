@@ -87,7 +87,7 @@ def test_grad_clip_variants():
         p.grad = torch.randn(10) * 5
     c.apply(ps)
     assert max(float(p.grad.abs().max()) for p in ps) <= 0.5
-    m = build_grad_clip({'type': 'momentum_norm', 'threshold': 1.0})
+    m = build_grad_clip({'type': 'momentum_norm', 'threshold': 1.0, 'momentum_mode': 'ema'})
     for p in ps:
         p.grad = torch.ones(10)
     m.apply(ps)                      # first step initialises the per-parameter EMA
@@ -95,6 +95,82 @@ def test_grad_clip_variants():
         p.grad = torch.ones(10) * 100
     m.apply(ps)                      # a 100x spike is scaled back to the EMA norm
     assert all(abs(float(p.grad.norm()) - 10 ** 0.5) < 1e-3 for p in ps)
+
+
+def _reference_momentum_norm_apply(state, parameters, threshold=1.0, norm_type=2.0):
+    """A line-level port of the reference's momentum_norm branch (distar/ctools/torch_utils/grad_clip.py:73-106),
+    list bookkeeping included: the oracle for the 'reference' mode."""
+    parameters = list(parameters)
+    if state['flag'] == 0:
+        state['norm_mom'] = [None] * len(parameters)
+    total = 0.0
+    for idx, p in enumerate(parameters):
+        if p.grad is not None:
+            g = p.grad.data.norm(norm_type)
+            m = state['norm_mom'][idx]
+            s = 1.0 if m is None else (1.0 if g < threshold * m else threshold * m / (g + 1e-6))
+            p.grad.data.mul_(s)
+    for idx, p in enumerate(parameters):
+        if p.grad is not None:
+            g = p.grad.data.norm(norm_type)
+            if state['norm_mom'][idx] is None:
+                state['norm_mom'].append(float(g))
+            else:
+                state['norm_mom'][idx] = state['norm_mom'][idx] * 0.99 + float(g) * 0.01
+            total += g.item() ** norm_type
+    state['flag'] = 1
+    return total ** (1.0 / norm_type)
+
+
+def test_momentum_norm_reference_mode_matches_reference_apply():
+    """the reference's momentum_norm never scales a gradient (norm_mom[idx] stays None, the new norms
+    are appended past the end) and reports the unclipped global norm.  The default 'reference' mode reproduces
+    that over steps with 100x spikes; the 'ema' mode does clip them."""
+    torch.manual_seed(0)
+    shapes = [(10,), (4, 7), (3, 3, 3)]
+    ref_ps = [torch.nn.Parameter(torch.zeros(s)) for s in shapes]
+    ps = [torch.nn.Parameter(torch.zeros(s)) for s in shapes]
+    clip = build_grad_clip({'type': 'momentum_norm', 'threshold': 1.0})
+    assert clip.momentum_mode == 'reference'
+    ema = build_grad_clip({'type': 'momentum_norm', 'threshold': 1.0, 'momentum_mode': 'ema'})
+    ema_ps = [torch.nn.Parameter(torch.zeros(s)) for s in shapes]
+    state = {'flag': 0, 'norm_mom': None}
+    for step in range(6):
+        gs = [torch.randn(s) * (100.0 if step % 2 else 1.0) for s in shapes]
+        for a, b, c, g in zip(ref_ps, ps, ema_ps, gs):
+            a.grad, b.grad, c.grad = g.clone(), g.clone(), g.clone()
+        want = _reference_momentum_norm_apply(state, ref_ps)
+        got = clip.apply(ps)
+        ema.apply(ema_ps)
+        assert abs(float(got) - want) <= 1e-5 * want, step
+        for a, b in zip(ref_ps, ps):
+            assert torch.equal(a.grad, b.grad), step
+        if step % 2:
+            assert sum(float(c.grad.norm()) for c in ema_ps) < 0.1 * sum(float(b.grad.norm()) for b in ps)
+    assert len(state['norm_mom']) == len(shapes) * 7     # the reference's list growth, not reproduced here
+
+
+def test_momentum_norm_ema_gated_first_step_keeps_ema_uninitialised():
+    """a gated-off FIRST step must not mark the EMA initialised (with a host flag, every later scale
+    would be thr * 0 = 0 and all updates zero)."""
+    ps = [torch.nn.Parameter(torch.zeros(5)) for _ in range(2)]
+    clip = build_grad_clip({'type': 'momentum_norm', 'threshold': 1.0, 'momentum_mode': 'ema'})
+    for p in ps:
+        p.grad = torch.full((5,), float('nan'))
+    clip.apply(ps, gate=torch.zeros(()))
+    assert float(clip.mom_init) == 0.0
+    for p in ps:
+        p.grad = torch.ones(5)
+    clip.apply(ps, gate=torch.ones(()))
+    assert all(torch.equal(p.grad, torch.ones(5)) for p in ps)          # scale 1 on the initialising step
+    assert float(clip.mom_init) == 1.0 and torch.allclose(clip.norm_mom, torch.full((2,), 5 ** 0.5))
+    sd = clip.state_dict()
+    fresh = build_grad_clip({'type': 'momentum_norm', 'threshold': 1.0, 'momentum_mode': 'ema'})
+    fresh.load_state_dict(sd)
+    for p in ps:
+        p.grad = torch.ones(5) * 100
+    fresh.apply(ps)
+    assert all(abs(float(p.grad.norm()) - 5 ** 0.5) < 1e-3 for p in ps)
 
 
 def test_lr_warmup_schedule():
