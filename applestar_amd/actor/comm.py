@@ -55,15 +55,28 @@ class ActorComm:
             return
         self._last_update = now
         reset = False
+        server = getattr(actor, '_server', None)
         for pid in self.job['update_players']:
             t0 = time.time()
+            if server is not None and pid in server.models and self._colocated(server, pid):
+                # the learner shares this host: its /dev/shm snapshot slot, no network (runtime/flat_model.py)
+                if pid in server.poll_model_slots():
+                    self.update_times.append(time.time() - t0)
+                    flag = bool(server._subscribers[pid].reset_flag)
+                    if flag and not self._last_reset.get(pid, False):
+                        reset = True
+                    self._last_reset[pid] = flag
+                continue
             got = self._adapter.pull(pid + 'model', size=1, block=False)
             if not got:
                 continue
             sd = got[0]
-            server = getattr(actor, '_server', None)
             if server is not None and pid in server.models:
-                server.load_state_dict(pid, sd['model'], last_iter=sd.get('model_last_iter', 0))
+                if 'flat_model' in sd:        # the learner's flat snapshot (runtime/flat_model.py)
+                    server.load_flat(pid, sd['flat_model'], sd['names'], sd['shapes'],
+                                     last_iter=sd.get('model_last_iter', 0))
+                else:
+                    server.load_state_dict(pid, sd['model'], last_iter=sd.get('model_last_iter', 0))
             self.update_times.append(time.time() - t0)
             flag = bool(sd.get('reset_flag', False))
             if flag and not self._last_reset.get(pid, False):
@@ -71,6 +84,19 @@ class ActorComm:
             self._last_reset[pid] = flag
         if reset:
             actor.reset_env()
+
+    def _colocated(self, server, pid: str) -> bool:
+        """Attach (once) to the player's shared model slot when its learner runs on this host."""
+        att = self.__dict__.setdefault('_attached', {})
+        if pid not in att or (not att[pid] and time.time() - self.__dict__.get('_attach_t', 0.0) > 30.0):
+            from ..learner.rl_learner import model_slot_name
+            self._attach_t = time.time()
+            try:
+                att[pid] = bool(self._cfg.actor.get('shared_model_slot', True)) and \
+                    server.attach_model_slot(pid, model_slot_name(pid))
+            except (OSError, ValueError, RuntimeError):
+                att[pid] = False
+        return att[pid]
 
     def send_result(self, result: dict) -> None:
         try:

@@ -140,6 +140,59 @@ class InferenceServer:
             if not teacher:
                 self.model_iter[player_id] = int(last_iter)
 
+    def load_flat(self, player_id: str, flat: torch.Tensor, names, shapes, last_iter: int = 0):
+        """Hot update from the learner's flat snapshot (runtime/flat_model.py): ONE H2D copy of the flat vector,
+        then ONE native multi-tensor D2D copy into the resident model's tensors."""
+        from ..runtime.flat_model import _copy_many
+        with self._lock:
+            m = self.models[player_id]
+            own = m.state_dict()
+            dev = next(m.parameters()).device
+            flat_dev = flat.to(dev, non_blocking=True)
+            dsts, srcs, off = [], [], 0
+            for k, shp in zip(names, shapes):
+                n = 1
+                for d in shp:
+                    n *= int(d)
+                t = own.get(k)
+                if t is not None and tuple(t.shape) == tuple(shp) and t.dtype == torch.float32:
+                    dsts.append(t)
+                    srcs.append(flat_dev[off:off + n].view(tuple(shp)))
+                off += n
+            with torch.no_grad():
+                _copy_many(dsts, srcs)
+            self.model_iter[player_id] = int(last_iter)
+
+    def attach_model_slot(self, player_id: str, shm_name: str) -> bool:
+        """Co-located learner: read ``player_id``'s published policy straight from its /dev/shm slot (seqlock
+        version, one H2D + one D2D multi-copy per new version; runtime/flat_model.ModelSubscriber)."""
+        import os
+        from ..runtime.flat_model import FlatLayout, ModelSubscriber
+        if not os.path.exists(os.path.join('/dev/shm', shm_name)):
+            return False
+        with self._lock:
+            m = self.models[player_id]
+            sub = ModelSubscriber(m, shm_name)
+            sd = m.policy_state_dict() if hasattr(m, 'policy_state_dict') else m.state_dict()
+            layout = FlatLayout({k: v for k, v in sd.items() if v.dtype == torch.float32})
+            if layout.numel != sub.slot.numel:
+                sub.close()
+                return False
+            sub.bind(layout)
+            self._subscribers = getattr(self, '_subscribers', {})
+            self._subscribers[player_id] = sub
+        return True
+
+    def poll_model_slots(self) -> Dict[str, int]:
+        """Apply any newer published versions; returns {player_id: model_last_iter} of the updated ones."""
+        out = {}
+        for pid, sub in list(getattr(self, '_subscribers', {}).items()):
+            with self._lock:
+                if sub.poll():
+                    self.model_iter[pid] = sub.last_iter
+                    out[pid] = sub.last_iter
+        return out
+
     def add_connection(self, conn: Connection, route: Optional[Tuple[str, str, Optional[str]]] = None):
         """``route`` = (player_id, kind, teacher_id): requests on ``conn`` are bare model inputs for that route
         (kind 'policy', 'teacher' or 'policy+teacher'); None: self-describing envelopes."""

@@ -36,17 +36,21 @@ constexpr int kOOB = 0x7ffffff0;
 #define PIPE_ABL 0
 #endif
 
-template <int BN_, int NS_, int BK_ = 16, int BM_ = 128>
+// NW waves per workgroup (4: 2 x 2 / 4 x 1 waves; 8: the 256-row / 256-column tiles, 2 waves per SIMD at one
+// workgroup per CU - twice the MFMA work per staged byte of the 128 x 128 tile)
+template <int BN_, int NS_, int BK_ = 16, int BM_ = 128, int NW_ = 4>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, NS = NS_, BK = BK_, NT = 256;
-  static constexpr int WN = BN_ >= 128 ? 2 : 1, WM = 4 / WN;
+  static constexpr int BM = BM_, BN = BN_, NS = NS_, BK = BK_, NW = NW_, NT = 64 * NW_;
+  static constexpr int WN = NW_ == 8 ? (BN_ >= 256 ? 4 : (BN_ >= 128 ? 2 : 1)) : (BN_ >= 128 ? 2 : 1);
+  static constexpr int WM = NW_ / WN;
   static constexpr int TM = BM / WM, TN = BN / WN;
   static constexpr int FM = TM / 32, FN = TN / 32;
   static constexpr int RB = BK * 4, SL = BK / 4;              // bytes / 16-B slots per LDS row
   static constexpr int RPI = 1024 / RB;                       // rows per DMA wave-instruction (1 KB)
   static constexpr int A_CH = BM / RPI, B_CH = BN / RPI;      // DMA chunks per stage
-  static constexpr int A_PW = A_CH / 4;                       // A chunks per wave
-  static constexpr int B_PW = B_CH >= 4 ? B_CH / 4 : 1;       // B chunks per wave (waves >= B_CH issue none)
+  static constexpr int A_PW = A_CH / NW;                      // A chunks per wave
+  static constexpr int B_PW = B_CH >= NW ? B_CH / NW : 1;     // B chunks per wave (waves >= B_CH issue none)
+  static_assert(A_PW >= 1 && A_CH % NW == 0, "A chunks must split evenly over the waves");
   static constexpr int STAGE = (BM + BN) * RB;                // bytes per stage array
   // slot swizzle: the 16 rows of a ds_read_b128 lane group on 16 distinct 4-bank groups (64-B rows: XOR with
   // bits 2-3 of the row; 128-B rows: bits 1-3)
@@ -125,13 +129,13 @@ __device__ __forceinline__ void mainloop(char* const (&smem)[C::NS], i32x4 ar, i
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid / C::WN, wn = wid % C::WN;
   const int l32 = lane & 31, h = lane >> 5;
-  const bool b_wave = C::B_CH >= 4 || wid < C::B_CH;
+  const bool b_wave = C::B_CH >= C::NW || wid < C::B_CH;
   auto issue = [&](char* st, int kt) {
 #pragma unroll
-    for (int c = 0; c < C::A_PW; ++c) dma16(ar, st + (wid + 4 * c) * 1024, asrc(c, kt));
+    for (int c = 0; c < C::A_PW; ++c) dma16(ar, st + (wid + C::NW * c) * 1024, asrc(c, kt));
     if (b_wave) {
 #pragma unroll
-      for (int c = 0; c < C::B_PW; ++c) dma16(br, st + C::BM * C::RB + (wid + 4 * c) * 1024, bsrc(c, kt));
+      for (int c = 0; c < C::B_PW; ++c) dma16(br, st + C::BM * C::RB + (wid + C::NW * c) * 1024, bsrc(c, kt));
     }
   };
   auto step = [&](const char* st, char* next, int kt) {
@@ -287,7 +291,7 @@ __device__ __forceinline__ void store_tile_staged(const f16v (&acc)[C::FM][C::FN
       }
     }
     __syncthreads();
-    for (int c = tid; c < 32 * CPR; c += 256) {
+    for (int c = tid; c < 32 * CPR; c += C::NT) {
       const int r = c / CPR, cc = c % CPR;
       const long m = m0 + pw * C::TM + 32 * pi + r;
       const int n = n0 + 8 * cc;

@@ -230,6 +230,7 @@ int wgrad_f32_splits(long R, int N, int K);
 // fp32 product mode of the f32 kernels: 0 = exact-f32 MFMA, 1 = bf16x6 split MFMA (split_mfma.h), split once at
 // LDS staging (default), 2 = the same split done per wave after an fp32 LDS read (A/B reference);
 // APPLESTAR_F32_MFMA=exact / regsplit select 0 / 2
+void set_f32_pipe_variant(int v);   // gemm_f32 split-mode tile / ring variant (A/B switch)
 int f32_mfma_mode();
 void set_f32_mfma_mode(int mode);
 // few-row products of any shape (gemm_small.hip), fp32 (split / exact per f32_mfma_mode) or bf16:

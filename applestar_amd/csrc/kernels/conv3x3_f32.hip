@@ -319,7 +319,7 @@ __global__ __launch_bounds__(256, BM == 128 ? 3 : 2) void conv3x3_f32_pipe_kerne
   int a_pix[C::A_PW], a_ok[C::A_PW], a_c[C::A_PW], b_off[C::B_PW];
 #pragma unroll
   for (int c = 0; c < C::A_PW; ++c) {
-    const int row = C::dma_row(wid + 4 * c, lane);
+    const int row = C::dma_row(wid + C::NW * c, lane);
     const long m = m0 + row;
     a_c[c] = 4 * C::dma_piece(row, lane);
     a_pix[c] = static_cast<int>(m);
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256, BM == 128 ? 3 : 2) void conv3x3_f32_pipe_kerne
   }
 #pragma unroll
   for (int c = 0; c < C::B_PW; ++c) {
-    const int row = C::dma_row(wid + 4 * c, lane);
+    const int row = C::dma_row(wid + C::NW * c, lane);
     b_off[c] = n0 + row < Cout ? ((n0 + row) * K + 4 * C::dma_piece(row, lane)) * 4 : -1;
   }
   const int KT = K / 16;      // Cin % 16 == 0 (host check): every K-step lies inside one tap

@@ -103,14 +103,14 @@ void gemm_bf16_pipe_kernel(const bf16_t* __restrict__ a, const bf16_t* __restric
   int a_off[C::A_PW], a_k[C::A_PW], b_off[C::B_PW], b_k[C::B_PW];
 #pragma unroll
   for (int c = 0; c < C::A_PW; ++c) {
-    const int row = C::dma_row(wid + 4 * c, lane), p = C::dma_piece(row, lane);
+    const int row = C::dma_row(wid + C::NW * c, lane), p = C::dma_piece(row, lane);
     const long m = m0 + row;
     a_k[c] = 8 * p;
     a_off[c] = m < M ? static_cast<int>((m * K + 8 * p) * 2) : -1;
   }
 #pragma unroll
   for (int c = 0; c < C::B_PW; ++c) {
-    const int row = C::dma_row(wid + 4 * c, lane), p = C::dma_piece(row, lane);
+    const int row = C::dma_row(wid + C::NW * c, lane), p = C::dma_piece(row, lane);
     b_k[c] = 8 * p;
     b_off[c] = n0 + row < N ? ((n0 + row) * K + 8 * p) * 2 : -1;
   }

@@ -316,12 +316,12 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 }
 
 // split-MFMA mode: LDS-DMA ring + register split (f32_pipe.h)
-template <int BN, int NS, int BK, bool STAGED = false>
-__global__ __launch_bounds__(256, 3) void gemm_f32_pipe_kernel(const float* __restrict__ a, const float* __restrict__ b,
-                                                            const float* __restrict__ bias,
-                                                            const float* __restrict__ res, float* __restrict__ out,
-                                                            long M, int N, int K, int act) {
-  using C = pipe::Cfg<BN, NS, BK>;
+// NW = 8: the 256 x 256 tile (8 waves of 128 x 64, two per SIMD, one workgroup per CU)
+template <int BN, int NS, int BK, bool STAGED = false, int BM = 128, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 2 : 3) void gemm_f32_pipe_kernel(
+    const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ bias,
+    const float* __restrict__ res, float* __restrict__ out, long M, int N, int K, int act) {
+  using C = pipe::Cfg<BN, NS, BK, BM, NW>;
   __shared__ __attribute__((aligned(16))) char s0[C::STAGE], s1[C::STAGE], s2[NS > 2 ? C::STAGE : 16],
       s3[NS > 3 ? C::STAGE : 16];
   char* const all[4] = {s0, s1, s2, s3};
@@ -338,14 +338,14 @@ __global__ __launch_bounds__(256, 3) void gemm_f32_pipe_kernel(const float* __re
   int a_off[C::A_PW], a_k[C::A_PW], b_off[C::B_PW], b_k[C::B_PW];
 #pragma unroll
   for (int c = 0; c < C::A_PW; ++c) {
-    const int row = C::dma_row(wid + 4 * c, lane), p = C::dma_piece(row, lane);
+    const int row = C::dma_row(wid + C::NW * c, lane), p = C::dma_piece(row, lane);
     const long m = m0 + row;
     a_k[c] = 4 * p;
     a_off[c] = m < M ? static_cast<int>((m * K + 4 * p) * 4) : -1;
   }
 #pragma unroll
   for (int c = 0; c < C::B_PW; ++c) {
-    const int row = C::dma_row(wid + 4 * c, lane), p = C::dma_piece(row, lane);
+    const int row = C::dma_row(wid + C::NW * c, lane), p = C::dma_piece(row, lane);
     b_k[c] = 4 * p;
     b_off[c] = n0 + row < N ? ((n0 + row) * K + 4 * p) * 4 : -1;
   }
@@ -539,13 +539,14 @@ __global__ __launch_bounds__(256) void gemm_bf16_small_kernel(const bf16_t* __re
   }
 }
 
-int pipe_variant() {
-  static const int v = [] {
+int& pipe_variant_ref() {
+  static int v = [] {
     const char* e = std::getenv("APPLESTAR_F32_PIPE");
     return e ? std::atoi(e) : 0;
   }();
   return v;
 }
+int pipe_variant() { return pipe_variant_ref(); }
 
 template <int BN>
 void launch_pipe(const float* a, const float* b, const float* bias, const float* res, float* out, long M, int N, int K,
@@ -555,6 +556,28 @@ void launch_pipe(const float* a, const float* b, const float* bias, const float*
   // (48 KB: 3 workgroups per CU) beat 4 x 16 by 4-7 %, 2 x 32 by 7-10 %, 3 x 32 and 6 x 16 (1 workgroup per CU)
   // by 25-40 % - occupancy, not ring depth, hides the DMA latency
   switch (pipe_variant()) {
+    case 3:
+      if constexpr (BN == 128) {
+        if (N % 256 == 0) {    // 256 x 256 tiles, 8 waves
+          const dim3 g8(static_cast<unsigned>((M + 255) / 256 * (N / 256))), blk8(512);
+          hipLaunchKernelGGL((gemm_f32_pipe_kernel<256, 3, 16, true, 256, 8>), g8, blk8, 0, s, a, b, bias, res, out, M,
+                             N, K, act);
+          break;
+        }
+      }
+      hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 3, 16, true>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act);
+      break;
+    case 4:
+      if constexpr (BN == 128) {
+        if (N % 256 == 0) {    // 256 x 256 tiles, 8 waves, 4-stage ring (128 KB)
+          const dim3 g8(static_cast<unsigned>((M + 255) / 256 * (N / 256))), blk8(512);
+          hipLaunchKernelGGL((gemm_f32_pipe_kernel<256, 4, 16, true, 256, 8>), g8, blk8, 0, s, a, b, bias, res, out, M,
+                             N, K, act);
+          break;
+        }
+      }
+      hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 3, 16, true>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act);
+      break;
     case 1: hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 4, 16>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act); break;
     case 2: hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 2, 32>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act); break;
     default:
@@ -604,6 +627,7 @@ int& mode_ref() {
 }  // namespace
 
 int f32_mfma_mode() { return mode_ref(); }
+void set_f32_pipe_variant(int v) { pipe_variant_ref() = v; }
 void set_f32_mfma_mode(int mode) { mode_ref() = mode >= 0 && mode <= 3 ? mode : 1; }
 
 void gemm_bf16_small(const void* a, const void* b, const float* bias, const void* res, void* out, long M, int N, int K,

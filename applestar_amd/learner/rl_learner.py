@@ -5,8 +5,11 @@ Behaviour of ``distar/agent/default/rl_learner.py`` + ``ctools/worker/learner/le
   load path unless one was given (``learner_comm.py:41-51``);
 * every ``learner_send_model_freq`` iterations (after value pre-training) the *policy* weights
   (no value nets) are published as the ``<player>model`` broadcast with ``model_last_iter`` and
-  ``reset_flag`` (``:53-99``) — here: one D2H copy into a pinned host snapshot on a side stream, then a
-  background thread serializes and publishes, so the training loop never blocks on the network;
+  ``reset_flag`` (``:53-99``) — here as ONE flat fp32 snapshot with a version counter
+  (``runtime/flat_model.py``): one native multi-tensor copy into a flat device buffer, one D2H DMA on a side
+  stream into a pinned ``/dev/shm`` slot that co-located inference servers read directly (H2D + one D2D
+  multi-copy into their resident model), and the same flat tensor pushed as a one-tensor frame for actors on
+  other hosts by a background thread - the training loop never blocks on the network;
 * every ``learner_send_train_info_freq`` iterations rank 0 posts the frames trained; a returned
   ``reset_checkpoint_path`` reloads the model, resets the value networks and value pre-training, and
   re-broadcasts (``:101-137``) — the reset flag is broadcast as a *device* tensor (the reference
@@ -41,6 +44,11 @@ DEFAULT_RL_LEARNER_CONFIG = {
 }
 
 
+def model_slot_name(player_id: str) -> str:
+    """The /dev/shm slot of a player's published policy (runtime/flat_model.SharedModelSlot)."""
+    return f'applestar_model_{player_id}_{os.getuid()}'
+
+
 class LearnerComm:
     def __init__(self, cfg, learner: 'RLLearner'):
         c = cfg.communication
@@ -52,13 +60,11 @@ class LearnerComm:
         self._send_info_freq = int(c.learner_send_train_info_freq)
         self._model_count = 0
         self._info_count = 0
-        self._snapshot: Optional[Dict[str, torch.Tensor]] = None
+        self._publisher = None          # runtime.flat_model.ModelPublisher, built at the first push
         self._pending = threading.Event()
         self._lock = threading.Lock()
         self._meta = (0, False)
         self._stop = False
-        self._stream = torch.cuda.Stream() if learner.device.type == 'cuda' else None
-        self._event = None
         if self._adapter is not None:
             threading.Thread(target=self._publish_loop, daemon=True, name='model-publisher').start()
         self._heartbeat = None
@@ -88,19 +94,11 @@ class LearnerComm:
         sd = {k: v for k, v in learner.model_state_dict().items()
               if 'value_networks' not in k and 'value_encoder' not in k}
         with self._lock:
-            if self._snapshot is None:
-                self._snapshot = {k: torch.empty(v.shape, dtype=v.dtype, pin_memory=v.is_cuda) for k, v in sd.items()}
-            if self._stream is not None:
-                self._stream.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(self._stream):
-                    for k, v in sd.items():
-                        self._snapshot[k].copy_(v.detach(), non_blocking=True)
-                    self._event = torch.cuda.Event()
-                    self._event.record(self._stream)
-            else:
-                for k, v in sd.items():
-                    self._snapshot[k].copy_(v.detach())
-            self._meta = (learner.last_iter.val, reset_flag)
+            if self._publisher is None:
+                from ..runtime.flat_model import ModelPublisher
+                shm = model_slot_name(self.player_id) if learner.device.type == 'cuda' else None
+                self._publisher = ModelPublisher(sd, shm_name=shm)
+            self._publisher.publish(sd, learner.last_iter.val, reset_flag)
         self._pending.set()
 
     def _publish_loop(self):
@@ -109,10 +107,7 @@ class LearnerComm:
                 continue
             self._pending.clear()
             with self._lock:
-                if self._event is not None:
-                    self._event.synchronize()
-                payload = {'model': {k: v.clone() for k, v in self._snapshot.items()},
-                           'model_last_iter': self._meta[0], 'reset_flag': self._meta[1]}
+                payload = self._publisher.payload()      # waits for the D2H; stamps the shared slot's version
             self._adapter.push(payload, self.player_id + 'model', broadcast=True)
 
     # ---------------------------------------------------------------- train info / reset
@@ -144,6 +139,10 @@ class LearnerComm:
             self._heartbeat.stop()
         if self._adapter is not None:
             self._adapter.close()
+        with self._lock:
+            if self._publisher is not None:
+                self._publisher.close(unlink=True)
+                self._publisher = None
 
 
 class SendModelHook(LearnerHook):
