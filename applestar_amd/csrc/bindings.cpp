@@ -1921,6 +1921,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("small_gemm_splitk", &small_gemm_splitk);
   m.def("f32_mfma_mode", &as::f32_mfma_mode);
   m.def("set_f32_pipe_variant", &as::set_f32_pipe_variant);
+  m.def("set_f32_conv_variant", &as::set_f32_conv_variant);
   m.def("set_f32_mfma_mode", &as::set_f32_mfma_mode);
   m.def("conv3x3_f32_supported", &as::conv3x3_f32_supported);
   m.def("varlen_attn_bwd_f32", &varlen_attn_bwd_f32);

@@ -231,6 +231,8 @@ int wgrad_f32_splits(long R, int N, int K);
 // LDS staging (default), 2 = the same split done per wave after an fp32 LDS read (A/B reference);
 // APPLESTAR_F32_MFMA=exact / regsplit select 0 / 2
 void set_f32_pipe_variant(int v);   // gemm_f32 split-mode tile / ring variant (A/B switch)
+int f32_conv_variant();             // conv3x3_f32 split-mode tile variant (A/B switch)
+void set_f32_conv_variant(int v);
 int f32_mfma_mode();
 void set_f32_mfma_mode(int mode);
 // few-row products of any shape (gemm_small.hip), fp32 (split / exact per f32_mfma_mode) or bf16:

@@ -295,12 +295,14 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
 
 // split-MFMA mode: the LDS-DMA ring of f32_pipe.h with the A rows gathered per tap (a lane's DMA piece is 4
 // channels of its row's shifted pixel; taps outside the image read zeros through the buffer range check)
-template <int BN, int NS, int BM = 128, bool STAGED = false>
-__global__ __launch_bounds__(256, BM == 128 ? 3 : 2) void conv3x3_f32_pipe_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                               const float* __restrict__ bias,
-                                                               const float* __restrict__ res, float* __restrict__ out,
-                                                               int B, int H, int W, int Cin, int Cout, int act) {
-  using C = pipe::Cfg<BN, NS, 16, BM>;
+// NW = 8: 256-pixel tiles on 8 waves (each wave 64 x 64 as in the 4-wave tile), the B (weight) stage shared by
+// twice the MFMA work
+template <int BN, int NS, int BM = 128, bool STAGED = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 8 ? 2 : (BM == 128 ? 3 : 2))
+void conv3x3_f32_pipe_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+                             const float* __restrict__ res, float* __restrict__ out, int B, int H, int W, int Cin,
+                             int Cout, int act) {
+  using C = pipe::Cfg<BN, NS, 16, BM, NW>;
   __shared__ __attribute__((aligned(16))) char s0[C::STAGE], s1[C::STAGE], s2[NS > 2 ? C::STAGE : 16],
       s3[NS > 3 ? C::STAGE : 16];
   char* const all[4] = {s0, s1, s2, s3};
@@ -518,6 +520,19 @@ void launch_f32(const float* x, const float* w, const float* bias, const float* 
   const long nwg = (M + 127) / 128 * ((Cout + BN - 1) / BN);
   if (nwg == 0) return;
   const int mode = f32_mfma_mode();
+  if constexpr (BN == 128) {
+    const int cv = f32_conv_variant();
+    if (mode == 1 && (cv == 1 || cv == 2)) {      // 256-pixel tiles on 8 waves (A/B switch)
+      const long nwg8 = (M + 255) / 256 * ((Cout + BN - 1) / BN);
+      if (cv == 1)
+        hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<128, 4, 256, false, 8>), dim3(static_cast<unsigned>(nwg8)),
+                           dim3(512), 0, s, x, w, bias, res, out, B, H, W, Cin, Cout, act);
+      else
+        hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<128, 4, 256, true, 8>), dim3(static_cast<unsigned>(nwg8)),
+                           dim3(512), 0, s, x, w, bias, res, out, B, H, W, Cin, Cout, act);
+      return;
+    }
+  }
   if constexpr (BN == 32) {
     if (mode == 1 && conv_n32_bm256()) {
       const long nwg2 = (M + 255) / 256 * ((Cout + BN - 1) / BN);

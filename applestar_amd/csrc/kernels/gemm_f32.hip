@@ -628,6 +628,16 @@ int& mode_ref() {
 
 int f32_mfma_mode() { return mode_ref(); }
 void set_f32_pipe_variant(int v) { pipe_variant_ref() = v; }
+
+int& conv_variant_ref() {
+  static int v = [] {
+    const char* e = std::getenv("APPLESTAR_F32_CONV_PIPE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+int f32_conv_variant() { return conv_variant_ref(); }
+void set_f32_conv_variant(int v) { conv_variant_ref() = v; }
 void set_f32_mfma_mode(int mode) { mode_ref() = mode >= 0 && mode <= 3 ? mode : 1; }
 
 void gemm_bf16_small(const void* a, const void* b, const float* bias, const void* res, void* out, long M, int N, int K,

@@ -39,9 +39,40 @@ def _native_switch(native: bool):
     return prev
 
 
+@torch.no_grad()
+def _sl_eval(tr, b) -> Dict:
+    """Teacher-forced argmax accuracy of every head on the batch (the selected-units head per labelled step:
+    the reference's SL metrics leave its IoU at 0 in teacher-forced mode, sl_loss.py test_iou off)."""
+    m = tr.model
+    was = m.training
+    m.eval()
+    B = len(b['traj_lens'])
+    H = m.core_lstm.hidden_size
+    z = torch.zeros(B, H, device=tr.device)
+    hs = [(z, z) for _ in range(m.core_lstm.num_layers)]
+    kw = {k: v for k, v in b.items() if k not in ('hidden_state', 'new_episodes')}
+    logits, _, _ = m.sl_train(**kw, hidden_state=hs)
+    act, am = b['action_info'], b['action_mask']
+    out = {}
+    for k in ('action_type', 'delay', 'queued', 'target_unit', 'target_location'):
+        hit = (logits[k].argmax(-1) == act[k].long()).float()
+        msk = am[k].float()
+        out['eval_' + k + '_acc'] = float((hit * msk).sum() / msk.sum().clamp(min=1))
+    su = logits['selected_units']                                        # [B*T, S, N+1]
+    lab = act['selected_units'][:, :su.shape[1]].long()
+    n = b['selected_units_num'].long()
+    valid = (torch.arange(su.shape[1], device=su.device)[None, :] < n[:, None]) & am['selected_units'].bool()[:, None]
+    hit = (su.argmax(-1) == lab).float()
+    out['eval_selected_units_step_acc'] = float((hit * valid).sum() / valid.float().sum().clamp(min=1))
+    m.train(was)
+    return out
+
+
 def sl_overfit_curve(device, steps: int = 300, native: bool = True, batch: int = 2, traj: int = 8,
-                     max_entities: int = 32, lr: float = 1e-3, seed: int = 0, every: int = 1) -> List[Dict]:
-    """Train the SL trainer on ONE fixed batch for ``steps`` iterations; per-step head metrics."""
+                     max_entities: int = 32, lr: float = 1e-3, seed: int = 0, every: int = 1,
+                     eval_every: int = 25) -> List[Dict]:
+    """Train the SL trainer on ONE fixed batch for ``steps`` iterations; per-step loss metrics plus a teacher-
+    forced argmax evaluation of every head every ``eval_every`` steps and at the end."""
     from ..sl.trainer import SLTrainer
     prev = _native_switch(native)
     try:
@@ -53,10 +84,12 @@ def sl_overfit_curve(device, steps: int = 300, native: bool = True, batch: int =
         curve = []
         t0 = time.perf_counter()
         for it in range(steps):
+            ev = _sl_eval(tr, b) if (it % eval_every == 0) else {}
             info = tr.step(dict(b))
-            if it % every == 0 or it == steps - 1:
-                curve.append({'step': it, **{k: float(info[k]) for k in SL_HEAD_METRICS if k in info},
-                              'wall_s': round(time.perf_counter() - t0, 3)})
+            if it % every == 0 or it == steps - 1 or ev:
+                curve.append({'step': it, **{k: float(info[k].detach()) for k in SL_HEAD_METRICS if k in info},
+                              **ev, 'wall_s': round(time.perf_counter() - t0, 3)})
+        curve.append({'step': steps, **_sl_eval(tr, b), 'wall_s': round(time.perf_counter() - t0, 3)})
         return curve
     finally:
         _native_switch(prev)
@@ -100,7 +133,7 @@ def rl_bandit_curve(device, iters: int = 120, native: bool = True, batch: int = 
                 p_rew = probs[..., rew_mask].sum(-1)
                 a = torch.multinomial(probs.reshape(-1, lt.shape[-1]), 1, generator=g).view(T, B)
                 b['action_info']['action_type'] = a
-                b['mask']['actions_mask'] = {k: v.to(device) for k, v in actions_mask(a).items()}
+                b['mask']['actions_mask'] = {k: v.to(device) for k, v in actions_mask(a.cpu()).items()}
                 # the other heads' logits depend on the sampled action type (autoregressive embedding): a second
                 # teacher-forced pass gives the behaviour log-probs of every head and the KL target
                 out = tr.model.rl_learner_forward(**b)

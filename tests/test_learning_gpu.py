@@ -1,0 +1,66 @@
+"""Training learns (VERDICT r4 missing item 1), on one GPU through the production trainers and native kernels, with
+the torch fp32 path on the same GPU as the control curve (runtime/learning_checks.py; curves kept in profiles/ by
+tools/learn_curves.py).
+
+* SL: the SL trainer memorises one fixed synthetic batch (random observations, random labels for every head) -
+  within 300 steps the teacher-forced argmax accuracy of every head (selected units per labelled step) reaches
+  >= 90 %, the loss falls 20x and the location L2 5x; the native curve reaches the thresholds like the torch
+  control.
+* RL: an on-policy bandit through the RL learner (V-trace / UPGO / TD(lambda) / entropy / KL, fused clip + Adam):
+  the policy's mass on the rewarded half of the action types rises from ~0.5, and the winloss value tracks the
+  return (its TD(lambda) loss falls).
+"""
+import pytest
+import torch
+
+from applestar_amd.runtime.learning_checks import rl_bandit_curve, sl_overfit_curve
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device('cuda', 0)
+
+
+def _mean(curve, key, sl):
+    xs = [r[key] for r in curve[sl]]
+    return sum(xs) / len(xs)
+
+
+def _sl_checks(c):
+    first, final = c[0], c[-1]            # teacher-forced argmax evaluations before training and after 300 steps
+    assert first['eval_action_type_acc'] < 0.5
+    for k in ('action_type', 'delay', 'target_unit', 'target_location'):
+        assert final['eval_' + k + '_acc'] >= 0.9, (k, final)
+    assert final['eval_selected_units_step_acc'] >= 0.9, final
+    assert final['eval_selected_units_step_acc'] > first['eval_selected_units_step_acc'] + 0.2
+    train = [r for r in c if 'total_loss' in r]
+    assert _mean(train, 'total_loss', slice(-10, None)) < 0.05 * first['total_loss']
+    assert _mean(train, 'target_location_distance_L2', slice(-10, None)) < 0.2 * first['target_location_distance_L2']
+
+
+def test_sl_native_memorises_fixed_batch():
+    c = sl_overfit_curve(DEV, steps=300, native=True)
+    _sl_checks(c)
+
+
+def test_sl_torch_control_memorises_fixed_batch():
+    c = sl_overfit_curve(DEV, steps=300, native=False)
+    _sl_checks(c)
+
+
+def _rl_checks(c):
+    early, late = slice(0, 10), slice(-10, None)
+    p0, p1 = _mean(c, 'p_rewarded', early), _mean(c, 'p_rewarded', late)
+    assert 0.3 < p0 < 0.7, p0
+    assert p1 > p0 + 0.2, (p0, p1)
+    assert _mean(c, 'frac_rewarded', late) > _mean(c, 'frac_rewarded', early) + 0.1
+    # the critic follows the (rising) return: its TD(lambda) loss falls and its t = 0 value approaches the return
+    assert _mean(c, 'td_loss', late) < _mean(c, 'td_loss', slice(5, 15))
+    gap_late = abs(_mean(c, 'value_mean', late) - _mean(c, 'return_mean', late))
+    assert gap_late < 0.5 * _mean(c, 'return_mean', late), gap_late
+
+
+def test_rl_native_bandit_learns_rewarded_actions():
+    _rl_checks(rl_bandit_curve(DEV, iters=150, native=True))
+
+
+def test_rl_torch_control_bandit_learns_rewarded_actions():
+    _rl_checks(rl_bandit_curve(DEV, iters=150, native=False))
