@@ -948,6 +948,50 @@ at::Tensor conv3x3_f32(const at::Tensor& x, const at::Tensor& wk, const c10::opt
   return out;
 }
 
+// input gradient with the extended epilogue: conv(x) + res + (first res2_rows rows) res2, masked by (mask > 0)
+at::Tensor conv3x3_f32_epi2(const at::Tensor& x, const at::Tensor& wk, const at::Tensor& res,
+                            const c10::optional<at::Tensor>& res2, const c10::optional<at::Tensor>& mask) {
+  check_cuda(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && wk.scalar_type() == at::kFloat && x.dim() == 4 && x.is_contiguous(),
+              "conv3x3_f32_epi2: fp32 NHWC x");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3);
+  TORCH_CHECK(wk.dim() == 4 && wk.size(1) == 3 && wk.size(2) == 3 && wk.size(3) == Cin && wk.is_contiguous(),
+              "conv3x3_f32_epi2: w contiguous [Cout, 3, 3, Cin]");
+  const int64_t Cout = wk.size(0);
+  TORCH_CHECK(as::conv3x3_f32_epi2_supported(static_cast<int>(Cin), static_cast<int>(Cout)),
+              "conv3x3_f32_epi2: shape / mode not covered (Cout % 128, split mode)");
+  TORCH_CHECK(B * H * W * std::max(Cin, Cout) * 4 < 0x7ffffff0LL, "conv3x3_f32_epi2: 32-bit offsets");
+  auto full = [&](const at::Tensor& t, const char* what) {
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.dim() == 4 && t.size(0) == B && t.size(1) == H && t.size(2) == W &&
+                t.size(3) == Cout && t.is_contiguous() && t.device() == x.device(), what);
+  };
+  full(res, "conv3x3_f32_epi2: residual NHWC [B, H, W, Cout]");
+  const float* r2 = nullptr;
+  long r2_rows = 0;
+  if (res2 && res2->defined()) {
+    TORCH_CHECK(res2->scalar_type() == at::kFloat && res2->dim() == 4 && res2->size(0) <= B && res2->size(1) == H &&
+                res2->size(2) == W && res2->size(3) == Cout && res2->is_contiguous() && res2->device() == x.device(),
+                "conv3x3_f32_epi2: res2 NHWC [B2 <= B, H, W, Cout]");
+    r2 = res2->data_ptr<float>();
+    r2_rows = static_cast<long>(res2->size(0) * H * W);
+  }
+  const float* mp = nullptr;
+  if (mask && mask->defined()) {
+    full(*mask, "conv3x3_f32_epi2: mask NHWC [B, H, W, Cout]");
+    mp = mask->data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(x.device().index());
+  auto out = at::empty({B, H, W, Cout}, x.options());
+  as::conv3x3_f32_fwd_epi2(x.data_ptr<float>(), wk.data_ptr<float>(), res.data_ptr<float>(), r2, r2_rows, mp,
+                           out.data_ptr<float>(), static_cast<int>(B), static_cast<int>(H), static_cast<int>(W),
+                           static_cast<int>(Cin), static_cast<int>(Cout), stream());
+  return out;
+}
+
+bool conv3x3_f32_epi2_supported(int64_t cin, int64_t cout) {
+  return as::conv3x3_f32_epi2_supported(static_cast<int>(cin), static_cast<int>(cout));
+}
+
 at::Tensor gemm_f32(const at::Tensor& a, const at::Tensor& b, const c10::optional<at::Tensor>& bias,
                     const c10::optional<at::Tensor>& res, int64_t act) {
   check_cuda(a, "a");
@@ -1907,6 +1951,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("varlen_attn_fwd", &varlen_attn_fwd);
   m.def("varlen_attn_bwd", &varlen_attn_bwd);
   m.def("varlen_attn_fwd_f32", &varlen_attn_fwd_f32);
+  m.def("conv3x3_f32_epi2", &conv3x3_f32_epi2);
+  m.def("conv3x3_f32_epi2_supported", &conv3x3_f32_epi2_supported);
   m.def("conv3x3_f32", &conv3x3_f32);
   m.def("fused_clip_adam", &fused_clip_adam);
   m.def("head_sample", &head_sample);

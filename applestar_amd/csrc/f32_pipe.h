@@ -120,7 +120,9 @@ __device__ __forceinline__ u32v4 frag_bf16(const char* stage, int r, int p) {
 // the stage being read and drains the DMA queue (s_waitcnt vmcnt(0)) before every K-step's first ds_read.
 // BF16: the ring carries bf16 operands (a stage row = 2 BK bf16 = BK / 8 chunks of 16): plain bf16 MFMAs on
 // one fragment read per operand and chunk, no split (gemm_bf16.hip).
-template <class C, class ASrc, class BSrc, bool BF16 = false>
+// DMA_MID: issue the next stage's LDS-DMA between the two halves of the K-step's MFMAs (pinned with
+// sched_barrier) instead of right after the barrier, so the DMA issue overlaps the matrix pipe (A/B switch)
+template <class C, class ASrc, class BSrc, bool BF16 = false, bool DMA_MID = false>
 __device__ __forceinline__ void mainloop(char* const (&smem)[C::NS], i32x4 ar, i32x4 br, int KT, const ASrc& asrc,
                                          const BSrc& bsrc, f16v (&acc)[C::FM][C::FN]) {
   constexpr int NS = C::NS;
@@ -144,7 +146,7 @@ __device__ __forceinline__ void mainloop(char* const (&smem)[C::NS], i32x4 ar, i
     else wait_vm<(NS - 2) * C::A_PW>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    issue(next, kt + NS - 1);
+    if constexpr (!DMA_MID) issue(next, kt + NS - 1);
     if constexpr (BF16) {
 #pragma unroll
       for (int c = 0; c < C::BK / 8; ++c) {
@@ -178,6 +180,18 @@ __device__ __forceinline__ void mainloop(char* const (&smem)[C::NS], i32x4 ar, i
       for (int j = 0; j < C::FN; ++j)
 #pragma unroll
         for (int q = 0; q < 3; ++q) asm volatile("" ::"v"(sb[j].p[q]));
+    } else if constexpr (DMA_MID) {
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) {
+          acc[i][j] = mfma_x6(sb[j], sa[i], acc[i][j]);
+          if (c == 0 && i * C::FN + j == (C::FM * C::FN) / 2 - 1) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue(next, kt + NS - 1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
     } else {
 #pragma unroll
       for (int i = 0; i < C::FM; ++i)
@@ -208,10 +222,19 @@ __device__ __forceinline__ void mainloop(char* const (&smem)[C::NS], i32x4 ar, i
 // Epilogue of a wave's transposed accumulator tiles: lane l32 of tile (i, j) is output row mw + 32 i + l32,
 // registers 4 g .. 4 g + 3 are columns nw + 32 j + 8 g + 4 h + 0..3.  out / res rows have N floats.
 //   v = acc + bias[n] (+ res[m, n] | masked by res[m, n] > 0 for ACT_DRELU), then ReLU for ACT_RELU
+// Extra (input-gradient) terms: + res2[m, n] for rows m < res2_rows (a gradient handed over for the first rows
+// only, e.g. the location head's use of an encoder skip map), then the ReLU mask of the layer input:
+// v = mask[m, n] > 0 ? v : 0.
+struct Epi2 {
+  const float* res2 = nullptr;
+  long res2_rows = 0;
+  const float* mask = nullptr;
+};
+
 template <int FM, int FN>
 __device__ __forceinline__ void store_tile(const f16v (&acc)[FM][FN], float* __restrict__ out,
                                            const float* __restrict__ bias, const float* __restrict__ res, long M,
-                                           int N, long mw, int nw, int act) {
+                                           int N, long mw, int nw, int act, const Epi2 e2 = Epi2()) {
   const int lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
   const bool vec = (N & 3) == 0;
 #pragma unroll
@@ -237,6 +260,15 @@ __device__ __forceinline__ void store_tile(const f16v (&acc)[FM][FN], float* __r
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = act == ACT_DRELU ? (r[q] > 0.f ? v[q] : 0.f) : v[q] + r[q];
           }
+          if (e2.res2 != nullptr && m < e2.res2_rows) {
+            const float4 r2 = *reinterpret_cast<const float4*>(e2.res2 + m * N + n);
+            v[0] += r2.x; v[1] += r2.y; v[2] += r2.z; v[3] += r2.w;
+          }
+          if (e2.mask != nullptr) {
+            const float4 mk = *reinterpret_cast<const float4*>(e2.mask + m * N + n);
+            v[0] = mk.x > 0.f ? v[0] : 0.f; v[1] = mk.y > 0.f ? v[1] : 0.f;
+            v[2] = mk.z > 0.f ? v[2] : 0.f; v[3] = mk.w > 0.f ? v[3] : 0.f;
+          }
           if (act == ACT_RELU)
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = fmaxf(v[q], 0.f);
@@ -247,6 +279,8 @@ __device__ __forceinline__ void store_tile(const f16v (&acc)[FM][FN], float* __r
             if (n + q >= N) continue;
             float x = v[q] + (bias ? bias[n + q] : 0.f);
             if (rrow) x = act == ACT_DRELU ? (rrow[n + q] > 0.f ? x : 0.f) : x + rrow[n + q];
+            if (e2.res2 != nullptr && m < e2.res2_rows) x += e2.res2[m * N + n + q];
+            if (e2.mask != nullptr && !(e2.mask[m * N + n + q] > 0.f)) x = 0.f;
             if (act == ACT_RELU) x = fmaxf(x, 0.f);
             orow[n + q] = x;
           }

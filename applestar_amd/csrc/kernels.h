@@ -225,6 +225,10 @@ void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* re
 bool conv3x3_f32_supported(int Cin, int Cout);
 void conv3x3_f32_fwd(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H,
                      int W, int Cin, int Cout, int act, hipStream_t s);
+// input-gradient conv with out = conv(x) + res + (rows < res2_rows: res2) masked by (mask > 0) (split ring kernel)
+bool conv3x3_f32_epi2_supported(int Cin, int Cout);
+void conv3x3_f32_fwd_epi2(const float* x, const float* w, const float* res, const float* res2, long res2_rows,
+                          const float* mask, float* out, int B, int H, int W, int Cin, int Cout, hipStream_t s);
 int wgrad_f32_splits(long R, int N, int K);
 // out [M, N] = epi(A [M, K] . B [N, K]^T): + bias[n]; res added, or (act == ACT_DRELU) a mask res > 0; ReLU
 // fp32 product mode of the f32 kernels: 0 = exact-f32 MFMA, 1 = bf16x6 split MFMA (split_mfma.h), split once at

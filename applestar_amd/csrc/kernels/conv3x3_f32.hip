@@ -297,11 +297,11 @@ __global__ __launch_bounds__(256) void conv3x3_f32_kernel(const float* __restric
 // channels of its row's shifted pixel; taps outside the image read zeros through the buffer range check)
 // NW = 8: 256-pixel tiles on 8 waves (each wave 64 x 64 as in the 4-wave tile), the B (weight) stage shared by
 // twice the MFMA work
-template <int BN, int NS, int BM = 128, bool STAGED = false, int NW = 4>
+template <int BN, int NS, int BM = 128, bool STAGED = false, int NW = 4, bool DMA_MID = false>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 2 : (BM == 128 ? 3 : 2))
 void conv3x3_f32_pipe_kernel(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
                              const float* __restrict__ res, float* __restrict__ out, int B, int H, int W, int Cin,
-                             int Cout, int act) {
+                             int Cout, int act, const pipe::Epi2 e2 = pipe::Epi2()) {
   using C = pipe::Cfg<BN, NS, 16, BM, NW>;
   __shared__ __attribute__((aligned(16))) char s0[C::STAGE], s1[C::STAGE], s2[NS > 2 ? C::STAGE : 16],
       s3[NS > 3 ? C::STAGE : 16];
@@ -349,12 +349,12 @@ void conv3x3_f32_pipe_kernel(const float* __restrict__ x, const float* __restric
   };
   auto bsrc = [&](int c, int kt) { return b_off[c] >= 0 && kt < KT ? b_off[c] + kt * 64 : pipe::kOOB; };
   f16v acc[C::FM][C::FN];
-  pipe::mainloop<C>(smem, xr, wr, KT, asrc, bsrc, acc);
+  pipe::mainloop<C, decltype(asrc), decltype(bsrc), false, DMA_MID>(smem, xr, wr, KT, asrc, bsrc, acc);
   if constexpr (STAGED) {
     pipe::store_tile_staged<C, float>(acc, smem[0], out, bias, res, M, Cout, m0, n0, act);
   } else {
     const int wm = wid / C::WN, wn = wid % C::WN;
-    pipe::store_tile<C::FM, C::FN>(acc, out, bias, res, M, Cout, m0 + wm * C::TM, n0 + wn * C::TN, act);
+    pipe::store_tile<C::FM, C::FN>(acc, out, bias, res, M, Cout, m0 + wm * C::TM, n0 + wn * C::TN, act, e2);
   }
 }
 
@@ -522,6 +522,11 @@ void launch_f32(const float* x, const float* w, const float* bias, const float* 
   const int mode = f32_mfma_mode();
   if constexpr (BN == 128) {
     const int cv = f32_conv_variant();
+    if (mode == 1 && cv == 3) {                   // DMA issue between the K-step's MFMA halves (A/B switch)
+      hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<128, 3, 128, false, 4, true>), dim3(static_cast<unsigned>(nwg)),
+                         dim3(256), 0, s, x, w, bias, res, out, B, H, W, Cin, Cout, act);
+      return;
+    }
     if (mode == 1 && (cv == 1 || cv == 2)) {      // 256-pixel tiles on 8 waves (A/B switch)
       const long nwg8 = (M + 255) / 256 * ((Cout + BN - 1) / BN);
       if (cv == 1)
@@ -561,6 +566,25 @@ void launch_f32(const float* x, const float* w, const float* bias, const float* 
 }  // namespace
 
 bool conv3x3_f32_supported(int Cin, int Cout) { return Cin % 16 == 0 && Cin > 0 && Cout > 0; }
+
+// the extended input-gradient epilogue (second residual on the first rows + ReLU mask of the layer input) runs on
+// the split ring kernel's register epilogue: 128-multiple output channels, split-MFMA mode
+bool conv3x3_f32_epi2_supported(int Cin, int Cout) {
+  return conv3x3_f32_supported(Cin, Cout) && Cout % 128 == 0 && Cin > 32 && f32_mfma_mode() == 1;
+}
+
+void conv3x3_f32_fwd_epi2(const float* x, const float* w, const float* res, const float* res2, long res2_rows,
+                          const float* mask, float* out, int B, int H, int W, int Cin, int Cout, hipStream_t s) {
+  const long M = static_cast<long>(B) * H * W;
+  const long nwg = (M + 127) / 128 * (Cout / 128);
+  if (nwg == 0) return;
+  pipe::Epi2 e2;
+  e2.res2 = res2;
+  e2.res2_rows = res2_rows;
+  e2.mask = mask;
+  hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<128, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w,
+                     nullptr, res, out, B, H, W, Cin, Cout, 0, e2);
+}
 
 void conv3x3_f32_fwd(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H,
                      int W, int Cin, int Cout, int act, hipStream_t s) {

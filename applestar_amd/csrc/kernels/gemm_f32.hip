@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(const float* __restrict__
 
 // split-MFMA mode: LDS-DMA ring + register split (f32_pipe.h)
 // NW = 8: the 256 x 256 tile (8 waves of 128 x 64, two per SIMD, one workgroup per CU)
-template <int BN, int NS, int BK, bool STAGED = false, int BM = 128, int NW = 4>
+template <int BN, int NS, int BK, bool STAGED = false, int BM = 128, int NW = 4, bool DMA_MID = false>
 __global__ __launch_bounds__(64 * NW, NW == 8 ? 2 : 3) void gemm_f32_pipe_kernel(
     const float* __restrict__ a, const float* __restrict__ b, const float* __restrict__ bias,
     const float* __restrict__ res, float* __restrict__ out, long M, int N, int K, int act) {
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(64 * NW, NW == 8 ? 2 : 3) void gemm_f32_pipe_kernel
     return b_off[c] >= 0 && kt * BK + b_k[c] < K ? b_off[c] + kt * BK * 4 : pipe::kOOB;
   };
   f16v acc[C::FM][C::FN];
-  pipe::mainloop<C>(smem, ar, br, (K + BK - 1) / BK, asrc, bsrc, acc);
+  pipe::mainloop<C, decltype(asrc), decltype(bsrc), false, DMA_MID>(smem, ar, br, (K + BK - 1) / BK, asrc, bsrc, acc);
   if constexpr (STAGED) {
     pipe::store_tile_staged<C, float>(acc, smem[0], out, bias, res, M, N, m0, n0, act);
   } else {
@@ -577,6 +577,10 @@ void launch_pipe(const float* a, const float* b, const float* bias, const float*
         }
       }
       hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 3, 16, true>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act);
+      break;
+    case 5:      // DMA issue between the K-step's MFMA halves
+      hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 3, 16, true, 128, 4, true>), g, blk, 0, s, a, b, bias, res, out, M, N,
+                         K, act);
       break;
     case 1: hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 4, 16>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act); break;
     case 2: hipLaunchKernelGGL((gemm_f32_pipe_kernel<BN, 2, 32>), g, blk, 0, s, a, b, bias, res, out, M, N, K, act); break;

@@ -109,23 +109,30 @@ class _TakeRows(torch.autograd.Function):
     map ran as a strided elementwise kernel (r2bd: ~0.11 ms per 19x20x128 skip, 4 per step)."""
 
     @staticmethod
-    def forward(ctx, x, n):
+    def forward(ctx, x, n, link=None):
         ctx.shape, ctx.stride, ctx.n = x.shape, x.stride(), n
+        ctx.link = link
         return x.narrow(0, 0, n)   # a view: no forward copy
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.link is not None and g.dtype == torch.float32:
+            # hand the gradient to the ResBlock consuming this map (ops/native.py SkipLink): it adds it, NHWC,
+            # to the first n rows of its input gradient; no full-height gradient here, no autograd add
+            nhwc = g.permute(0, 2, 3, 1)
+            ctx.link.g = nhwc if nhwc.is_contiguous() else nhwc.contiguous()
+            return None, None, None
         full = torch.empty_strided(ctx.shape, ctx.stride, dtype=g.dtype, device=g.device)
         full[:ctx.n].copy_(g)
         full[ctx.n:].zero_()
-        return full, None
+        return full, None, None
 
 
 def _take_rows(x, n):
     if x is None:                 # a skip level the fused encoder never materialises (see SpatialEncoder.trunk)
         return None
     if x.dim() == 4 and x.shape[0] > n and x.is_cuda:
-        return _TakeRows.apply(x, n)
+        return _TakeRows.apply(x, n, getattr(x, '_skip_link', None))
     return x[:n]
 
 

@@ -174,7 +174,7 @@ class _LNLSTMRecurrence(torch.autograd.Function):
     @staticmethod
     def forward(ctx, xp, h0, c0, w_hh, lnh_w, lnh_b, lnc_w, lnc_b, w_dtype):
         wq = w_hh.detach().to(w_dtype)
-        wT = wq.t().contiguous()
+        wT = _wT(w_hh, w_dtype)          # a derived form: transposed once per optimizer step, not per layer call
         out, hT, cT, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c = _C.lnlstm_fwd(
             xp.contiguous(), h0.contiguous(), c0.contiguous(), wT, lnh_w.detach(), lnh_b.detach(),
             lnc_w.detach(), lnc_b.detach(), 1e-5)
@@ -185,7 +185,7 @@ class _LNLSTMRecurrence(torch.autograd.Function):
     def backward(ctx, dout, dhT, dcT):
         h0, out, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c, wq, lnh_w, lnc_w = ctx.saved_tensors
         T, B, H = out.shape
-        z = lambda t: torch.zeros(B, H, device=out.device) if t is None else t.float().contiguous()
+        z = lambda t: _zeros_const((B, H), out.device) if t is None else t.float().contiguous()
         dout = torch.zeros_like(out) if dout is None else dout.float().contiguous()
         dgates, dhg, dc_ln, dh0, dc0 = _C.lnlstm_bwd(dout, z(dhT), z(dcT), gates, c_all, xhat_c, rstd_c, xhat_h,
                                                      rstd_h, wq, lnh_w.detach(), lnc_w.detach())
@@ -196,6 +196,19 @@ class _LNLSTMRecurrence(torch.autograd.Function):
         dlnh_w, dlnh_b = _C.ln_affine_grads(dgates.contiguous(), xhat_h.contiguous()).unbind(0)
         dlnc_w, dlnc_b = _C.ln_affine_grads(dc_ln.contiguous(), xhat_c.contiguous()).unbind(0)
         return dgates, dh0, dc0, dw, dlnh_w, dlnh_b, dlnc_w, dlnc_b, None
+
+
+_ZEROS = {}
+
+
+def _zeros_const(shape, device):
+    """A cached all-zero fp32 tensor (read-only input of a kernel, e.g. the LSTM's absent final-state
+    gradients): no fill launch per use.  Callers must never write into it."""
+    key = (tuple(shape), str(device))
+    t = _ZEROS.get(key)
+    if t is None or t._version != 0:
+        t = _ZEROS[key] = torch.zeros(shape, device=device)
+    return t
 
 
 def lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b):
@@ -865,23 +878,52 @@ def _conv_dw(dpre, x, w, b_dtype):
     return dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype), db
 
 
+class SkipLink:
+    """Hands the location head's gradient of an encoder skip map (``model._TakeRows``: the first T*B rows of a
+    ResBlock input) to the backward of the ResBlock that consumes the map, which adds it in its dX conv's
+    epilogue (``conv3x3_f32_epi2``: + res2 on the first rows) - together with the ReLU mask of the map (the
+    previous layer's ReLU): the map then receives ONE gradient, already masked, instead of a full-height
+    copy + tail fill (_TakeRows), an autograd add of the two gradients and a threshold pass (~120 us per
+    19x20x128 level, four levels per fp32 step).  The link rides on the map tensor object itself
+    (``x._skip_link``, set when the ResBlock is called on it), so it can never be picked up by another tensor.
+    Autograd runs the location head's backward (which consumes the heads' outputs) before any encoder
+    ResBlock's (the encoder feeds the heads), so the hand-off is ordered; an unfilled link is a no-op."""
+    __slots__ = ('g',)
+
+    def __init__(self):
+        self.g = None
+
+
+SKIP_LINK = os.environ.get('APPLESTAR_SKIP_LINK', '1') == '1'    # A/B switch
+
+
 class _ResBlock(torch.autograd.Function):
     """relu(conv2(relu(conv1(x))) + x) (res_block.py:50-65) as ONE autograd node: the input gradient of
     conv1 and the skip gradient are summed in the dX conv's epilogue (the residual input of the same MFMA
-    kernel) instead of a separate autograd add over the whole activation."""
+    kernel) instead of a separate autograd add over the whole activation.  fp32: the output is registered as
+    a ReLU output (its consumer may apply the mask, _premasked), and the input gradient takes the location
+    head's hand-over (SkipLink) and the input's own ReLU mask in the same epilogue."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2):
+    def forward(ctx, x, w1, b1, w2, b2, link=None):
         y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1)
         out = _conv3(y1, _conv_w(w2), _w32(b2), x, 1)
         ctx.save_for_backward(x, w1, w2, y1, out)
         ctx.b_dtypes = (b1.dtype, b2.dtype)
+        ctx.link = link
+        ctx.mask_in = False
+        if out.dtype == torch.float32 and SKIP_LINK:
+            _note_relu_out(out)
+            ctx.mask_in = _relu_src(x)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         x, w1, w2, y1, out = ctx.saved_tensors
-        dpre2 = _act_grad(dout, out, True)
+        if out.dtype == torch.float32 and _premasked(out, dout):
+            dpre2 = dout.contiguous()           # the consumer's dX epilogue already applied this block's ReLU
+        else:
+            dpre2 = _act_grad(dout, out, True)
         side = _SideWork(dpre2, dpre2.numel() // dpre2.shape[-1])
         with side.fork():       # weight gradients concurrent with the dX convs
             dw2, db2 = _conv_dw(dpre2, y1, w2, ctx.b_dtypes[1])
@@ -890,9 +932,21 @@ class _ResBlock(torch.autograd.Function):
         with side.fork():
             dw1, db1 = _conv_dw(dpre1, x, w1, ctx.b_dtypes[0])
             db1 = db1.to(ctx.b_dtypes[0])
-        dx = _conv3(dpre1, _conv_wt(w1), None, dpre2, 0)       # + skip gradient, fused
+        g = None
+        if ctx.link is not None:
+            g, ctx.link.g = ctx.link.g, None
+        C = x.shape[-1]
+        if x.dtype == torch.float32 and (g is not None or ctx.mask_in) and _C.conv3x3_f32_epi2_supported(C, C):
+            # + skip gradient + the location head's hand-over (first rows), masked by this input's own ReLU
+            dx = _C.conv3x3_f32_epi2(dpre1, _conv_wt(w1), dpre2, g, x if ctx.mask_in else None)
+            if ctx.mask_in:
+                _MASKED_DX[x.data_ptr()] = (dx, dx._version)
+        else:
+            dx = _conv3(dpre1, _conv_wt(w1), None, dpre2, 0)       # + skip gradient, fused
+            if g is not None:
+                dx[:g.shape[0]] += g
         side.join(dw1, db1, dw2, db2)
-        return dx, dw1, db1, dw2, db2
+        return dx, dw1, db1, dw2, db2, None
 
 
 def _f32_conv_ok(x, w, cin, cout):
@@ -907,7 +961,11 @@ def resblock(x, w1, b1, w2, b2):
     if x.dim() != 4 or b1 is None or b2 is None or tuple(w1.shape) != (C, C, 3, 3) or tuple(w2.shape) != (C, C, 3, 3):
         return None
     if _f32_conv_ok(x, w1, C, C):
-        return from_nhwc(_ResBlock.apply(nhwc(x), w1, b1, w2, b2))
+        link = None
+        if SKIP_LINK and x.is_cuda and _C.conv3x3_f32_epi2_supported(C, C):
+            link = SkipLink()
+            x._skip_link = link          # read by the location head's row view of this map (model._take_rows)
+        return from_nhwc(_ResBlock.apply(nhwc(x), w1, b1, w2, b2, link))
     lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
     if not lowp or not _C.conv3x3_supported(C, C):
         return None

@@ -10,8 +10,8 @@ trainers (native kernels, fused losses, fused clip + Adam):
   weights along the loss gradient cannot memorise random labels.
 * :func:`rl_bandit_curve` - an on-policy contextual bandit through the RL learner: every iteration samples the
   action types of a fixed batch of observations from the CURRENT policy (its own teacher-forced forward), rewards
-  the ``winloss`` field +1 at the steps whose action type lies in a fixed half of the 327 types (even ids) and 0
-  elsewhere, and trains one RL step (V-trace PG + UPGO + TD(lambda) + entropy + KL against the sampling-time
+  the ``winloss`` field +1/T at the steps whose action type lies in a fixed half of the 327 types (even ids) and
+  -1/T elsewhere (returns inside the atan-squashed winloss value's range), and trains one RL step (V-trace PG + UPGO + TD(lambda) + entropy + KL against the sampling-time
   logits).  The policy's probability mass on the rewarded half must rise from ~0.5, and the winloss value must
   track the return (its TD(lambda) loss falls).
 
@@ -61,8 +61,15 @@ def _sl_eval(tr, b) -> Dict:
     su = logits['selected_units']                                        # [B*T, S, N+1]
     lab = act['selected_units'][:, :su.shape[1]].long()
     n = b['selected_units_num'].long()
-    valid = (torch.arange(su.shape[1], device=su.device)[None, :] < n[:, None]) & am['selected_units'].bool()[:, None]
-    hit = (su.argmax(-1) == lab).float()
+    S = su.shape[1]
+    valid = (torch.arange(S, device=su.device)[None, :] < n[:, None]) & am['selected_units'].bool()[:, None]
+    # the SL loss's su_mask (sl/loss.py): at step s the OTHER labelled units are forbidden, so rank the label
+    # against the unlabelled units only
+    lab_v = torch.where(valid, lab, torch.full_like(lab, su.shape[-1]))
+    other = torch.nn.functional.one_hot(lab_v, su.shape[-1] + 1)[..., :-1].bool().any(1)      # [B*T, N+1]
+    forbid = other[:, None, :].expand(-1, S, -1).clone()
+    forbid.scatter_(2, lab.clamp(max=su.shape[-1] - 1)[..., None], False)
+    hit = (su.masked_fill(forbid, float('-inf')).argmax(-1) == lab).float()
     out['eval_selected_units_step_acc'] = float((hit * valid).sum() / valid.float().sum().clamp(min=1))
     m.train(was)
     return out
@@ -106,8 +113,8 @@ def _logp_of(logits: torch.Tensor, a: torch.Tensor) -> torch.Tensor:
     return torch.log_softmax(logits.float(), -1).gather(-1, a.long().unsqueeze(-1)).squeeze(-1)
 
 
-def rl_bandit_curve(device, iters: int = 120, native: bool = True, batch: int = 2, unroll: int = 8,
-                    max_entities: int = 32, lr: float = 1e-4, seed: int = 0) -> List[Dict]:
+def rl_bandit_curve(device, iters: int = 150, native: bool = True, batch: int = 2, unroll: int = 8,
+                    max_entities: int = 32, lr: float = 3e-4, seed: int = 0) -> List[Dict]:
     """On-policy action-type bandit through the RL learner (see the module docstring); per-iteration metrics:
     ``p_rewarded`` (policy mass on the rewarded half, before the update), ``frac_rewarded`` (sampled),
     ``return_mean``, ``value_mean`` (winloss value at t = 0), ``td_loss``, ``pg_loss``."""
@@ -145,7 +152,8 @@ def rl_bandit_curve(device, iters: int = 120, native: bool = True, batch: int = 
                 labels = act['selected_units'][..., :su.shape[2]].clamp(max=su.shape[-1] - 1)
                 blp['selected_units'] = _logp_of(su, labels)
                 reward = dict(base['reward'])
-                r = rew_mask[a].float()
+                # +-1/T per step: returns stay inside the winloss value's (-1, 1) range (atan-squashed baseline)
+                r = (rew_mask[a].float() * 2.0 - 1.0) / T
                 r[-1] = 0.0          # a nonzero last winloss reward would read as "game over" (no bootstrap)
                 reward['winloss'] = r
                 ret = torch.flip(torch.cumsum(torch.flip(r, [0]), 0), [0])        # undiscounted (gamma 1) return
@@ -154,7 +162,8 @@ def rl_bandit_curve(device, iters: int = 120, native: bool = True, batch: int = 
             b['teacher_logit'] = lg
             b['reward'] = reward
             info = tr.step(b)
-            curve.append({'iter': it, 'p_rewarded': float(p_rew.mean()), 'frac_rewarded': float(r[:-1].mean()),
+            curve.append({'iter': it, 'p_rewarded': float(p_rew.mean()),
+                          'frac_rewarded': float(rew_mask[a][:-1].float().mean()),
                           'return_mean': float(ret[0].mean()), 'value_mean': float(v0),
                           'td_loss': float(info['winloss/td']), 'pg_loss': float(info['winloss/total']),
                           'entropy': float(info['entropy/total']), 'kl': float(info['kl/total']),

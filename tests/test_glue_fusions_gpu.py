@@ -1,0 +1,80 @@
+"""Glue fusions of the fp32 learner step vs float64 references (round 5).
+
+* SkipLink (ops/native.py): the location head's gradient of an encoder skip map (model._take_rows) and the map's
+  own ReLU mask are applied in the consuming ResBlock's dX conv epilogue (conv3x3_f32_epi2), so the map gets one
+  pre-masked gradient - no full-height copy, autograd add or threshold pass.
+"""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _err(a, b):
+    return (a.double() - b.double()).abs().max().item()
+
+
+def test_conv3x3_f32_epi2_matches_fp64():
+    """out = conv(x) + res + (first rows) res2, masked by (mask > 0) == float64."""
+    from applestar_amd.ops import native as N
+    C = N.ensure_loaded()
+    torch.manual_seed(0)
+    B, H, W, Ci, Co, B2 = 6, 19, 20, 128, 128, 4
+    x = torch.randn(B, H, W, Ci, device=DEV)
+    w = torch.randn(Co, 3, 3, Ci, device=DEV) / 30
+    res = torch.randn(B, H, W, Co, device=DEV)
+    res2 = torch.randn(B2, H, W, Co, device=DEV)
+    mask = torch.randn(B, H, W, Co, device=DEV).relu()
+    out = C.conv3x3_f32_epi2(x, w, res, res2, mask)
+    ref = torch.nn.functional.conv2d(x.double().cpu().permute(0, 3, 1, 2), w.double().cpu().permute(0, 3, 1, 2),
+                                     padding=1).permute(0, 2, 3, 1) + res.double().cpu()
+    ref[:B2] += res2.double().cpu()
+    ref = torch.where(mask.cpu() > 0, ref, torch.zeros_like(ref))
+    assert _err(out.cpu(), ref) < 1e-5 * max(1.0, ref.abs().max().item())
+    out2 = C.conv3x3_f32_epi2(x, w, res, None, None)                  # plain: conv + res
+    ref2 = torch.nn.functional.conv2d(x.double().cpu().permute(0, 3, 1, 2), w.double().cpu().permute(0, 3, 1, 2),
+                                      padding=1).permute(0, 2, 3, 1) + res.double().cpu()
+    assert _err(out2.cpu(), ref2) < 1e-5 * max(1.0, ref2.abs().max().item())
+
+
+@pytest.mark.parametrize('link', ['1', '0'])
+def test_skip_link_resblock_chain_matches_fp64(link, monkeypatch):
+    """Three fp32 ResBlocks whose inputs are also read (first n rows) by a location-head-like consumer through
+    model._take_rows: every gradient == float64 CPU, with the hand-off on (default) and off."""
+    from applestar_amd.ops import native as N
+    from applestar_amd.models.blocks import ResBlock
+    from applestar_amd.models.model import _take_rows
+    N.ensure_loaded()
+    monkeypatch.setattr(N, 'SKIP_LINK', link == '1')
+    torch.manual_seed(3)
+    C, H, W, B, n = 128, 19, 20, 7, 5
+    blocks = [ResBlock(C) for _ in range(3)]
+    refs = [copy.deepcopy(b).double() for b in blocks]
+    blocks = [b.to(DEV).to(memory_format=torch.channels_last) for b in blocks]
+    x0 = torch.randn(B, C, H, W, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_()
+    x0r = x0.detach().double().cpu().requires_grad_()
+    ws = [torch.randn(n, C, H, W, dtype=torch.float64) for _ in range(3)]
+    wo = torch.randn(B, C, H, W, dtype=torch.float64)
+
+    def run(xin, mods, weights, on_gpu):
+        # as SpatialEncoder.trunk + LocationHead: every block input is a skip map; the row views are taken after
+        # the whole trunk ran (the heads run after the encoder)
+        x, maps = xin, []
+        for m in mods:
+            maps.append(x)
+            x = m(x)
+        loss = (x * (wo.float().to(DEV) if on_gpu else wo)).sum()
+        for mp, wt in zip(maps, weights):
+            rows = _take_rows(mp, n) if on_gpu else mp[:n]
+            loss = loss + (rows * (wt.float().to(DEV) if on_gpu else wt)).sum()
+        return loss
+    run(x0, blocks, ws, True).backward()
+    run(x0r, refs, ws, False).backward()
+    assert _err(x0.grad.cpu(), x0r.grad) < 5e-5 * max(1.0, x0r.grad.abs().max().item())
+    for b, r in zip(blocks, refs):
+        for (name, p), (_, pr) in zip(b.named_parameters(), r.named_parameters()):
+            e = _err(p.grad.cpu(), pr.grad)
+            assert e < 5e-5 * max(1.0, pr.grad.abs().max().item()), (name, e)

@@ -20,17 +20,26 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--sl-steps', type=int, default=300)
     ap.add_argument('--rl-iters', type=int, default=150)
-    ap.add_argument('--rl-lr', type=float, default=1e-4)
+    ap.add_argument('--rl-lr', type=float, default=3e-4)
     ap.add_argument('--out', default='gpurun_out/learn_curves.json')
     ap.add_argument('--no-control', action='store_true')
+    ap.add_argument('--rl-only', action='store_true')
+    ap.add_argument('--rl-lrs', default='', help='comma list: RL learning-rate sweep (native only)')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     res = {}
+    if args.rl_lrs:
+        for lr in [float(x) for x in args.rl_lrs.split(',')]:
+            rl = rl_bandit_curve(dev, iters=args.rl_iters, native=True, lr=lr)
+            res[f'rl_native_lr{lr:g}'] = rl
+            print(json.dumps({'run': f'rl_native_lr{lr:g}', 'first': rl[0], 'mid': rl[len(rl) // 2], 'last': rl[-1]}),
+                  flush=True)
     for native in ([True] if args.no_control else [True, False]):
         tag = 'native' if native else 'torch_control'
-        sl = sl_overfit_curve(dev, steps=args.sl_steps, native=native)
-        res['sl_' + tag] = sl
-        print(json.dumps({'run': 'sl_' + tag, 'first': sl[0], 'last': sl[-1]}), flush=True)
+        if not args.rl_only:
+            sl = sl_overfit_curve(dev, steps=args.sl_steps, native=native)
+            res['sl_' + tag] = sl
+            print(json.dumps({'run': 'sl_' + tag, 'first': sl[0], 'last': sl[-1]}), flush=True)
         rl = rl_bandit_curve(dev, iters=args.rl_iters, native=native, lr=args.rl_lr)
         res['rl_' + tag] = rl
         print(json.dumps({'run': 'rl_' + tag, 'first': rl[0], 'last': rl[-1]}), flush=True)
