@@ -1168,7 +1168,8 @@ std::vector<at::Tensor> small_wgrad(const at::Tensor& dy, const at::Tensor& x, c
   return {dw, db};
 }
 
-std::vector<at::Tensor> wgrad_f32(const at::Tensor& dy, const at::Tensor& x, int64_t cin, bool want_bias) {
+std::vector<at::Tensor> wgrad_f32(const at::Tensor& dy, const at::Tensor& x, int64_t cin, bool want_bias,
+                                  const c10::optional<at::Tensor>& out) {
   check_cuda(dy, "dy");
   check_cuda(x, "x");
   TORCH_CHECK(dy.scalar_type() == at::kFloat && x.scalar_type() == at::kFloat, "wgrad_f32: fp32 dy / x");
@@ -1189,18 +1190,30 @@ std::vector<at::Tensor> wgrad_f32(const at::Tensor& dy, const at::Tensor& x, int
   TORCH_CHECK(R * N * 4 < 0x7ffffff0LL && x.numel() * 4 < 0x7ffffff0LL, "wgrad_f32: tensor too large");
   c10::hip::HIPGuard g(dy.device().index());
   auto opts = dy.options();
-  if (R == 0) return {at::zeros({N, K}, opts), want_bias ? at::zeros({N}, opts) : at::Tensor()};
-  const int S = as::wgrad_f32_splits(R, static_cast<int>(N), static_cast<int>(K));
   const int64_t NK = N * K, stride = NK + (want_bias ? N : 0);
-  auto part = at::empty({S, stride}, opts);
+  // out: a caller-provided flat [N K (+ N)] fp32 result buffer (the deferred weight gradients, ops/native.py)
+  at::Tensor flat;
+  if (out && out->defined()) {
+    TORCH_CHECK(out->scalar_type() == at::kFloat && out->is_contiguous() && out->numel() == stride &&
+                out->device() == dy.device(), "wgrad_f32: out must be a contiguous fp32 [N K (+ N)] buffer");
+    flat = *out;
+  }
+  if (R == 0) {
+    if (flat.defined()) {
+      flat.zero_();
+      return {flat.narrow(0, 0, NK).view({N, K}), want_bias ? flat.narrow(0, NK, N) : at::Tensor()};
+    }
+    return {at::zeros({N, K}, opts), want_bias ? at::zeros({N}, opts) : at::Tensor()};
+  }
+  const int S = as::wgrad_f32_splits(R, static_cast<int>(N), static_cast<int>(K));
+  auto part = (S == 1 && flat.defined()) ? flat.view({1, stride}) : at::empty({S, stride}, opts);
   as::wgrad_f32(dy.data_ptr<float>(), x.data_ptr<float>(), part.data_ptr<float>(),
                 want_bias ? part.data_ptr<float>() + NK : nullptr, stride, R, static_cast<int>(N), static_cast<int>(K),
                 static_cast<int>(H), static_cast<int>(W), static_cast<int>(cin), S, stream());
-  at::Tensor flat;
   if (S == 1) {
-    flat = part.view({stride});
+    if (!flat.defined()) flat = part.view({stride});
   } else {
-    flat = at::empty({stride}, opts);
+    if (!flat.defined()) flat = at::empty({stride}, opts);
     as::column_reduce(part.data_ptr<float>(), flat.data_ptr<float>(), S, static_cast<int>(stride), stream());
   }
   return {flat.narrow(0, 0, NK).view({N, K}), want_bias ? flat.narrow(0, NK, N) : at::Tensor()};
@@ -1958,7 +1971,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_sample", &head_sample);
   m.def("target_unit_sample", &target_unit_sample);
   m.def("fused_adam_chunk", &as::fused_adam_chunk);
-  m.def("wgrad_f32", &wgrad_f32);
+  m.def("wgrad_f32", &wgrad_f32, py::arg("dy"), py::arg("x"), py::arg("cin"), py::arg("want_bias"),
+        py::arg("out") = py::none());
   m.def("gemm_f32", &gemm_f32);
   m.def("gemm_bf16_small", &gemm_bf16_small);
   m.def("gemm_bf16", &gemm_bf16);

@@ -189,6 +189,9 @@ class _LNLSTMRecurrence(torch.autograd.Function):
         dout = torch.zeros_like(out) if dout is None else dout.float().contiguous()
         dgates, dhg, dc_ln, dh0, dc0 = _C.lnlstm_bwd(dout, z(dhT), z(dcT), gates, c_all, xhat_c, rstd_c, xhat_h,
                                                      rstd_h, wq, lnh_w.detach(), lnc_w.detach())
+        # the recurrence is launched (its 8-workgroup rows are dispatched first): the heads' queued weight
+        # gradients now fill the CUs it leaves idle (_Deferred)
+        defer_flush()
         h_prev = torch.cat([h0.float().unsqueeze(0), out[:-1]], 0).view(T * B, H)
         dw = _mm_tn(dhg.view(T * B, 4 * H), h_prev)
         # LN_h / LN_c affine gradients: one column-sum launch each (four products + reductions as torch ops
@@ -650,11 +653,104 @@ def _act_grad(dout, out, relu):
     return torch.ops.aten.threshold_backward(dout, out, 0.0) if relu else dout
 
 
-def _wgrad(dy2d, x, cin, has_b, bf16_out):
-    """(dW, db) of a dense GEMM (cin == 0, x [R, K]) or a 3x3 conv (x NHWC image, Cin = cin) in dy's precision."""
+def _wgrad(dy2d, x, cin, has_b, bf16_out, param=None):
+    """(dW, db) of a dense GEMM (cin == 0, x [R, K]) or a 3x3 conv (x NHWC image, Cin = cin) in dy's precision.
+    ``param``: the weight, when the caller lets the product be deferred (_Deferred: single-use weights only)."""
     if dy2d.dtype == torch.float32:
+        if _Deferred.on and dy2d.is_cuda and param is not None and _single_use(param):
+            return _Deferred.add(dy2d, x, cin, has_b)
         return _C.wgrad_f32(dy2d, x, cin, has_b)
     return _C.wgrad(dy2d, x, cin, has_b, bf16_out)
+
+
+# ---------------------------------------------------------------------------- deferred weight gradients
+DEFER_WGRAD = os.environ.get('APPLESTAR_DEFER_WGRAD', '1') == '1'     # A/B switch
+
+
+_FWD_EPOCH = [0]
+
+
+def _count_use(p) -> None:
+    """Record one forward use of parameter ``p`` in the current step (``_FWD_EPOCH``)."""
+    if isinstance(p, torch.nn.Parameter):
+        u = getattr(p, '_as_uses', None)
+        p._as_uses = (_FWD_EPOCH[0], u[1] + 1) if u is not None and u[0] == _FWD_EPOCH[0] else (_FWD_EPOCH[0], 1)
+
+
+def _single_use(p) -> bool:
+    """``p`` fed exactly one native node in this step's forward: autograd returns that node's gradient as is
+    (a weight used twice would have its gradients summed by autograd, reading a deferred result early)."""
+    u = getattr(p, '_as_uses', None)
+    return u is not None and u == (_FWD_EPOCH[0], 1)
+
+
+class _Deferred:
+    """Weight gradients of the policy heads, run beside the core LSTM's backward (fp32 step).
+
+    The LSTM backward is three latency-bound recurrences on 8 workgroups per batch row (~1 ms in which ~200
+    of the 256 CUs idle); the heads' backward before it is a dX chain whose weight-gradient kernels (the
+    location head's gated ResBlocks, gate GEMMs, up-convolutions, head MLPs: a few ms) lie off its critical
+    path.  Between :func:`defer_begin` (the trainer, before autograd) and the first LSTM backward, every fp32
+    ``_wgrad`` only allocates its result buffer and queues the product (with an event on the stream that
+    produced its operands); the LSTM backward launches its recurrence and then :func:`defer_flush` issues the
+    queue on a side stream, so the products fill the CUs the recurrence leaves idle.  :func:`defer_end` (the
+    trainer, after autograd) makes the main stream wait for them before the gradients are read.  Operands
+    and results are held by the queue and recorded on the side stream (the caching allocator never recycles
+    them early); autograd cannot accumulate in place into a held tensor.  Not while a HIP graph is captured."""
+    on = False
+    q = []
+    streams = {}
+    flushed = None
+
+    @classmethod
+    def add(cls, dy2d, x, cin, has_b):
+        N = dy2d.shape[1]
+        K = 9 * cin if cin > 0 else x.shape[1]
+        out = torch.empty(N * K + (N if has_b else 0), dtype=torch.float32, device=dy2d.device)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(dy2d.device))
+        cls.q.append((ev, dy2d, x, cin, has_b, out))
+        return out[:N * K].view(N, K), (out[N * K:] if has_b else None)
+
+
+def defer_begin(device) -> None:
+    """Start queueing fp32 weight gradients (see :class:`_Deferred`)."""
+    if DEFER_WGRAD and torch.device(device).type == 'cuda' and not torch.cuda.is_current_stream_capturing():
+        _Deferred.on = True
+        _Deferred.q = []
+        _Deferred.flushed = None
+
+
+def defer_flush() -> None:
+    """Issue the queued weight gradients on the side stream (ordered after each operand's producer) and stop
+    queueing."""
+    if not _Deferred.on:
+        return
+    _Deferred.on = False
+    q, _Deferred.q = _Deferred.q, []
+    if not q:
+        return
+    dev = q[0][1].device
+    side = _Deferred.streams.get(dev)
+    if side is None:
+        side = _Deferred.streams[dev] = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(side):
+        for ev, dy2d, x, cin, has_b, out in q:
+            side.wait_event(ev)
+            for t in (dy2d, x, out):
+                t.record_stream(side)
+            _C.wgrad_f32(dy2d, x, cin, has_b, out)
+    _Deferred.flushed = side
+
+
+def defer_end(device) -> None:
+    """Flush anything still queued (no LSTM in this backward) and join the side stream."""
+    if _Deferred.on:
+        defer_flush()
+    side, _Deferred.flushed = _Deferred.flushed, None
+    if side is not None:
+        torch.cuda.current_stream(torch.device(device)).wait_stream(side)
+    _FWD_EPOCH[0] += 1          # the next forward counts weight uses afresh
 
 
 # ---------------------------------------------------------------------------- weight gradients on a side stream
@@ -718,6 +814,7 @@ class _SideWork:
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_nhwc, w_lp, b, res_nhwc, act):
+        _count_use(w_lp)
         wk = w_lp.detach().permute(0, 2, 3, 1)          # [Cout,3,3,Cin]: a view for channels_last weights
         if not wk.is_contiguous():
             wk = wk.contiguous()
@@ -742,7 +839,7 @@ class _Conv3x3(torch.autograd.Function):
         bf = _bf16_grads(w.dtype, ctx.b_dtype)
         side = _SideWork(dpre, dpre.numel() // cout)
         with side.fork():
-            dw, db = _wgrad(dpre.view(-1, cout), x, cin, has_b, bf)   # dW in [Cout,3,3,Cin] (channels_last) order
+            dw, db = _wgrad(dpre.view(-1, cout), x, cin, has_b, bf, w)   # dW in [Cout,3,3,Cin] (channels_last) order
             dw = dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype)
             db = db.to(ctx.b_dtype) if has_b else None
         dx = _conv3(dpre, _conv_wt(w), None, None, 0)
@@ -874,7 +971,7 @@ def _conv_dw(dpre, x, w, b_dtype):
     """dW (in w's dtype) and db of a 3x3 conv; callers cast db to b_dtype (a no-op when both are bf16:
     the cast is then fused into the split reduction)."""
     cout, cin = w.shape[0], w.shape[1]
-    dw, db = _wgrad(dpre.view(-1, cout), x, cin, b_dtype is not None, _bf16_grads(w.dtype, b_dtype))
+    dw, db = _wgrad(dpre.view(-1, cout), x, cin, b_dtype is not None, _bf16_grads(w.dtype, b_dtype), w)
     return dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype), db
 
 
@@ -906,6 +1003,8 @@ class _ResBlock(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, link=None):
+        _count_use(w1)
+        _count_use(w2)
         y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1)
         out = _conv3(y1, _conv_w(w2), _w32(b2), x, 1)
         ctx.save_for_backward(x, w1, w2, y1, out)
@@ -994,6 +1093,8 @@ class _GatedResBlock(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, sp, w1, b1, w2, b2, *gate):
+        for p in (w1, w2, *gate[0::2]):
+            _count_use(p)
         B, H, W, C = x.shape
         y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1)
         y = _conv3(y1, _conv_w(w2), _w32(b2), None, 0)
@@ -1056,7 +1157,7 @@ class _GatedResBlock(torch.autograd.Function):
             # fp32 step: each input gradient on the f32 GEMM with the previous layer's ReLU mask (ACT_DRELU on its
             # saved output) or the skip gradient in the epilogue - no threshold_backward / addmm passes
             for i in (3, 2, 1, 0):
-                dw_i, db_i = _wgrad(d, acts_in[i], 0, True, False)
+                dw_i, db_i = _wgrad(d, acts_in[i], 0, True, False, gws[i])
                 grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
                 if i > 0:
                     d = _C.gemm_f32(d, _wT(gws[i]), None, acts_in[i], 4)
@@ -1341,6 +1442,7 @@ class _Linear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x2, w, b, relu, link=None):
+        _count_use(w)
         ctx.link = link
         R, K = x2.shape
         if SMALL_NATIVE and SPLITK_NATIVE and x2.is_cuda and R <= 2048 and K > F32_SMALL_K_MAX and \
@@ -1400,13 +1502,16 @@ class _Linear(torch.autograd.Function):
         has_b = ctx.b_dtype is not None
         side = _SideWork(dy, dy.shape[0])
         with side.fork():       # dW / db concurrent with the dX GEMM below
-            dw, db = _wgrad(dy, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype))
+            dw, db = _wgrad(dy, x2, 0, has_b, _bf16_grads(w.dtype, ctx.b_dtype), w)
             dw = dw.to(w.dtype)
             db = db.to(ctx.b_dtype) if has_b else None
         dx = None
         g = None
         if ctx.link is not None:
             g, ctx.link.g = ctx.link.g, None
+            if g is not None and (_Deferred.on or _Deferred.flushed is not None):
+                # g is written in place below; queued / side-stream weight gradients may still read it
+                defer_end(g.device)
             if _DEBUG_GRADLINK and g is not None and g._version != ctx.link.version:
                 raise RuntimeError('GradLink: the handed-over residual gradient was modified before the dX GEMM')
         if dy.dtype == torch.float32 and _gemm_f32_ok(dy.shape[0], w.shape[1], dy.shape[1]) and \

@@ -130,10 +130,13 @@ class GradientReducer:
         op = dist.ReduceOp.AVG if self.use_avg else dist.ReduceOp.SUM
         b.handle = dist.all_reduce(buf, op=op, group=self.group, async_op=True)
 
-    def backward(self, loss: torch.Tensor):
+    def backward(self, loss: torch.Tensor, before_copy=None):
         """Gradients of ``loss`` into the bucket views: ``autograd.grad`` + one multi-tensor copy (native on
-        the GPU), at every world size; buckets holding a parameter without a gradient are zeroed first."""
+        the GPU), at every world size; buckets holding a parameter without a gradient are zeroed first.
+        ``before_copy``: called between autograd and the copy (the deferred weight gradients join there)."""
         grads = torch.autograd.grad(loss, self.params, allow_unused=True)
+        if before_copy is not None:
+            before_copy()
         dst, src = [], []
         stale = set()
         for p, g in zip(self.params, grads):

@@ -140,10 +140,18 @@ class TrainEngine:
     # ------------------------------------------------------------------ backward / reduce / update
     def backward(self, loss: torch.Tensor):
         self.reducer.zero_grad(buffers=False)    # backward overwrites every slot (and zeroes unused ones)
-        if self.master is not None:
-            self.master.backward(loss)
-        else:
-            self.reducer.backward(loss)
+        from ..ops import native
+        defer = self.device.type == 'cuda' and self.master is None     # fp32: heads' dW beside the LSTM backward
+        if defer:
+            native.defer_begin(self.device)
+        try:
+            if self.master is not None:
+                self.master.backward(loss)
+            else:
+                self.reducer.backward(loss, before_copy=(lambda: native.defer_end(self.device)) if defer else None)
+        finally:
+            if defer:
+                native.defer_end(self.device)
 
     def _lstm_gate(self):
         """1.0 / 0.0 device scalar: the split LSTM exchange has not / has timed out (ops.native.lstm_exchange_ok)."""

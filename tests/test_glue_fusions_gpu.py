@@ -78,3 +78,39 @@ def test_skip_link_resblock_chain_matches_fp64(link, monkeypatch):
         for (name, p), (_, pr) in zip(b.named_parameters(), r.named_parameters()):
             e = _err(p.grad.cpu(), pr.grad)
             assert e < 5e-5 * max(1.0, pr.grad.abs().max().item()), (name, e)
+
+
+def test_deferred_head_wgrads_equal_inline(monkeypatch):
+    """Deferred weight gradients (ops/native.py _Deferred: the heads' fp32 dW products queued during the heads'
+    backward and issued beside the core LSTM's backward on a side stream) give every parameter the same
+    gradient as the inline products, and the deferral did engage."""
+    from applestar_amd.ops import native as N
+    from applestar_amd.rl.trainer import RLTrainer
+    from applestar_amd.rl.synthetic import rl_batch, to_device
+    N.ensure_loaded()
+    batch = rl_batch(2, 6, max_entities=96, seed=5)
+    grads = {}
+    engaged = {}
+    for defer in (True, False):
+        monkeypatch.setattr(N, 'DEFER_WGRAD', defer)
+        torch.manual_seed(0)
+        tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}},
+                       device=DEV)
+        b = to_device(copy.deepcopy(batch), DEV)
+        queued = []
+        orig = N._Deferred.add.__func__
+
+        def spy(cls, *a):
+            queued.append(1)
+            return orig(cls, *a)
+        monkeypatch.setattr(N._Deferred, 'add', classmethod(spy))
+        out = tr.model.rl_learner_forward(**b)
+        info = tr.loss.compute_loss(out)
+        tr.backward(info['total_loss'])
+        torch.cuda.synchronize()
+        grads[defer] = {n: p.grad.detach().clone() for n, p in tr.model.named_parameters() if p.grad is not None}
+        engaged[defer] = len(queued)
+    assert engaged[True] > 10 and engaged[False] == 0, engaged
+    for n, g in grads[False].items():
+        d = grads[True][n]
+        assert torch.allclose(d, g, rtol=1e-5, atol=1e-7 * max(1.0, float(g.abs().max()))), n
