@@ -140,6 +140,25 @@ class BaseLearner:
             self.call_hooks('after_iter')
             faults.inject('learner_iter')
         self.call_hooks('after_run')
+        self._write_fingerprint()
+
+    def _write_fingerprint(self):
+        """``learner.fingerprint_path`` (a directory): after the run each rank writes {rank, world, iter,
+        weight_hash} there - the data-parallel replica check of tools/rl_train_dp_rehearsal.py."""
+        d = self.cfg.learner.get('fingerprint_path')
+        if not d:
+            return
+        import json
+        os.makedirs(d, exist_ok=True)
+        with torch.no_grad():
+            h = 0
+            for k, v in sorted(self.model.state_dict().items()):
+                if v.is_floating_point():
+                    x = v.detach().float().reshape(-1).cpu()
+                    h = (h * 1000003 + int((x.view(torch.int32).long() * 2654435761 % (1 << 31)).sum())) % (1 << 61)
+        rec = {'rank': self.rank, 'world': self.world_size, 'iter': self.last_iter.val, 'weight_hash': h}
+        with open(os.path.join(d, f'rank{self.rank}.json'), 'w') as f:
+            json.dump(rec, f)
 
     def _log_info(self, info: Dict):
         # one device->host transfer for every logged scalar

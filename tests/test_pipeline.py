@@ -127,3 +127,21 @@ def test_learner_admin_routes(tmp_path, monkeypatch):
     assert lrn.comm is not old_comm and lrn.dataloader is not old_loader
     assert c.get('/rl_learner/status').json['info']['iter'] == 1
     lrn.close()
+
+
+def test_rl_train_two_learner_ranks_identical_replicas(tmp_path):
+    """rl_train itself (coordinator, league, the learner role under torch.distributed.run with
+    two gloo ranks, an actor with fake-env workers and the batched inference server) runs 2 learner iterations;
+    both ranks' weights are then identical (tools/rl_train_dp_rehearsal.py; on a GPU box the same script runs both
+    ranks on the one GPU)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = subprocess.run([sys.executable, os.path.join(root, 'tools', 'rl_train_dp_rehearsal.py'), '--iters', '2',
+                          '--out', str(tmp_path / 'dp2'), '--timeout', '500'], capture_output=True, text=True,
+                         timeout=560)
+    assert res.returncode == 0, (res.stdout[-2000:], res.stderr[-3000:])
+    rec = json.loads(res.stdout.strip().splitlines()[-1])
+    assert rec['replicas_identical'] and rec['iterations'] == [2, 2], rec
