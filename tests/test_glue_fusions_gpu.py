@@ -112,8 +112,11 @@ def test_deferred_head_wgrads_equal_inline(monkeypatch):
         engaged[defer] = len(queued)
     assert engaged[True] > 10 and engaged[False] == 0, engaged
     # a few forward / backward kernels accumulate with fp32 atomics (entity scatter, BO encoder), so two runs
-    # differ in the last bits; a read-before-write hazard would show as garbage, far above this bound
+    # differ in the last bits; a read-before-write hazard would show as garbage, far above this bound. A conv bias
+    # that feeds a normalisation has an (analytically) zero gradient whose float residue is pure noise: the bound
+    # gets a floor of 1e-6 of the largest gradient norm
+    floor = 1e-6 * max(float(g.norm()) for g in grads[False].values())
     for n, g in grads[False].items():
         d = grads[True][n]
-        rel = float((d - g).norm() / g.norm().clamp(min=1e-30))
-        assert torch.isfinite(d).all() and rel < 1e-3, (n, rel)
+        err = float((d - g).norm())
+        assert torch.isfinite(d).all() and err < 1e-3 * float(g.norm()) + floor, (n, err, float(g.norm()))
