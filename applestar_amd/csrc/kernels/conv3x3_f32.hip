@@ -582,8 +582,12 @@ void conv3x3_f32_fwd_epi2(const float* x, const float* w, const float* res, cons
   e2.res2 = res2;
   e2.res2_rows = res2_rows;
   e2.mask = mask;
-  hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<128, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w,
-                     nullptr, res, out, B, H, W, Cin, Cout, 0, e2);
+  if (f32_conv_variant() == 3)
+    hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<128, 3, 128, false, 4, true>), dim3(static_cast<unsigned>(nwg)),
+                       dim3(256), 0, s, x, w, nullptr, res, out, B, H, W, Cin, Cout, 0, e2);
+  else
+    hipLaunchKernelGGL((conv3x3_f32_pipe_kernel<128, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x, w,
+                       nullptr, res, out, B, H, W, Cin, Cout, 0, e2);
 }
 
 void conv3x3_f32_fwd(const float* x, const float* w, const float* bias, const float* res, float* out, int B, int H,

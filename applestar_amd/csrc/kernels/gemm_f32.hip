@@ -635,8 +635,10 @@ void set_f32_pipe_variant(int v) { pipe_variant_ref() = v; }
 
 int& conv_variant_ref() {
   static int v = [] {
+    // default 3 (DMA issue between the MFMA halves): 1.0-1.8 % faster on the learner's 128-channel convs
+    // (profiles/r5d_dma_mid_variants.jsonl); 0 = the plain ring
     const char* e = std::getenv("APPLESTAR_F32_CONV_PIPE");
-    return e ? std::atoi(e) : 0;
+    return e ? std::atoi(e) : 3;
   }();
   return v;
 }

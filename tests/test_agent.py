@@ -213,3 +213,17 @@ def test_trajectory_ring_matches_host_collate():
     small = TrajectoryRing(max(len(f) for f in frames) * 2 + 4096, device='cpu')
     tids = [small.put(f) for f in frames]
     assert tids[-1] in small.ids() and tids[0] not in small.ids() and 1 <= len(small) <= 2
+
+
+def test_transform_obs_matches_golden_digests():
+    """The featurizer reproduces, byte for byte, the digests recorded from the plain per-column implementation
+    (tests/featurize_golden.py) over a FakeSC2Env episode: its speed work changes no value."""
+    import json
+    import tests.featurize_golden as fg
+    with open(fg.GOLDEN) as f:
+        golden = json.load(f)
+    got = fg.episode_digests()
+    assert len(got) == len(golden)
+    for i, (g, r) in enumerate(zip(got, golden)):
+        diff = {k for k in set(g) | set(r) if g.get(k) != r.get(k)}
+        assert not diff, (i, sorted(diff)[:8])

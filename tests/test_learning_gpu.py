@@ -7,8 +7,8 @@ tools/learn_curves.py).
   >= 90 %, the loss falls 20x and the location L2 5x; the native curve reaches the thresholds like the torch
   control.
 * RL: an on-policy bandit through the RL learner (V-trace / UPGO / TD(lambda) / entropy / KL, fused clip + Adam):
-  the policy's mass on the rewarded half of the action types rises from ~0.5, and the winloss value tracks the
-  return (its TD(lambda) loss falls).
+  the policy's mass on the rewarded half of the action types rises from ~0.5 to ~1, and the winloss value at
+  t = 0 climbs to the return.
 """
 import pytest
 import torch
@@ -47,15 +47,21 @@ def test_sl_torch_control_memorises_fixed_batch():
 
 
 def _rl_checks(c):
+    # measured (profiles/r5d_learn_sweep.json, lr 3e-4): p_rewarded 0.50 -> 1.00, frac_rewarded 0.44 -> 1.00,
+    # t = 0 value 0.96 against a return of 0.88 over the last 10 iterations
     early, late = slice(0, 10), slice(-10, None)
     p0, p1 = _mean(c, 'p_rewarded', early), _mean(c, 'p_rewarded', late)
     assert 0.3 < p0 < 0.7, p0
-    assert p1 > p0 + 0.2, (p0, p1)
-    assert _mean(c, 'frac_rewarded', late) > _mean(c, 'frac_rewarded', early) + 0.1
-    # the critic follows the (rising) return: its TD(lambda) loss falls and its t = 0 value approaches the return
-    assert _mean(c, 'td_loss', late) < _mean(c, 'td_loss', slice(5, 15))
-    gap_late = abs(_mean(c, 'value_mean', late) - _mean(c, 'return_mean', late))
-    assert gap_late < 0.5 * _mean(c, 'return_mean', late), gap_late
+    assert p1 > p0 + 0.3, (p0, p1)
+    assert _mean(c, 'frac_rewarded', late) > _mean(c, 'frac_rewarded', early) + 0.25
+    # the critic follows the (rising) return: its t = 0 value climbs from ~0 to within 20 % of the return.  (The
+    # TD(lambda) loss itself need not fall: the per-step return (T - 1 - t) / T of the learned policy varies with
+    # t, which the observations do not encode, while the random policy's returns are ~0.)
+    ret = _mean(c, 'return_mean', late)
+    assert ret > 0.5, ret
+    assert _mean(c, 'value_mean', late) - _mean(c, 'value_mean', early) > 0.5 * ret
+    gap_late = abs(_mean(c, 'value_mean', late) - ret)
+    assert gap_late < 0.2 * ret, (gap_late, ret)
 
 
 def test_rl_native_bandit_learns_rewarded_actions():

@@ -40,9 +40,11 @@ class StubClient:
         from applestar_amd.agent.collate import collate_obs, decollate_output
         t0 = time.perf_counter()
         buf = serialize.dumps({'player_id': 'p', 'kind': self.kind, 'input': model_input})
-        req = serialize.loads(buf)['input']
         t1 = time.perf_counter()
+        req = serialize.loads(buf)['input']
+        t2 = time.perf_counter()
         self.t['request_codec'] += t1 - t0
+        self.t['server_side_decode'] += t2 - t1
         key = self.kind          # one canned answer per kind: the model's own cost is the server's, not ours
         if key not in self._canned:
             with torch.no_grad():
@@ -50,9 +52,9 @@ class StubClient:
                 out = self.model.compute_logp_action(**b) if self.kind == 'policy' else \
                     self.model.compute_teacher_logit(**b)
             self._canned[key] = serialize.dumps(decollate_output(out, 0))
-        t2 = time.perf_counter()
+        t3 = time.perf_counter()
         out = serialize.loads(self._canned[key])
-        self.t['reply_decode'] += time.perf_counter() - t2
+        self.t['reply_decode'] += time.perf_counter() - t3
         return out
 
 
@@ -110,8 +112,17 @@ def main():
         times['featurize'] += time.perf_counter() - t0
         return r
     agent_mod.Agent.step, agent_mod.Agent.collect_data, agent_mod.Agent._pre_process = step, collect, pre
+    from applestar_amd.envs import fake_env
+    orig_env_step = fake_env.FakeSC2Env.step
+
+    def env_step(self, actions):
+        t0 = time.perf_counter()
+        r = orig_env_step(self, actions)
+        times['fake_env_step'] += time.perf_counter() - t0
+        return r
+    fake_env.FakeSC2Env.step = env_step
     prof = cProfile.Profile() if args.cprofile else None
-    t0 = time.perf_counter()
+    t0, c0 = time.perf_counter(), time.process_time()
     if prof:
         prof.enable()
     try:
@@ -120,11 +131,17 @@ def main():
         pass
     if prof:
         prof.disable()
-    wall = time.perf_counter() - t0
+    wall, cpu = time.perf_counter() - t0, time.process_time() - c0
     n = max(n_steps[0], 1)
     res = {k: round(1000 * v / n, 3) for k, v in sorted(times.items())}
     res['traj_serialize'] = round(1000 * ser[0] / n, 3)
     res['wall_per_agent_step_ms'] = round(1000 * wall / n, 3)
+    # process CPU time (one torch thread): insensitive to other tenants of the host, unlike the wall clock
+    res['cpu_per_agent_step_ms'] = round(1000 * cpu / n, 3)
+    # the stub decodes each request as the GPU server would: that decode is the server's cost, not the actor's
+    # ... nor is the stand-in game's own step (SC2 runs in its own process)
+    res['actor_cpu_per_agent_step_ms'] = round(1000 * cpu / n - res.get('server_side_decode', 0.0)
+                                               - res.get('fake_env_step', 0.0), 3)
     res['agent_steps'] = n
     print(json.dumps(res))
     if prof:
