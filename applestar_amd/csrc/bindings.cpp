@@ -95,31 +95,49 @@ at::Tensor reverse_scan(const at::Tensor& a, const at::Tensor& b, const at::Tens
 }
 
 // ---------------------------------------------------------------- gated residual
-at::Tensor gated_residual_fwd(const at::Tensor& y, const at::Tensor& gt, const at::Tensor& sp, const at::Tensor& x) {
+// post (optional): added to the block output in the same pass
+at::Tensor gated_residual_fwd(const at::Tensor& y, const at::Tensor& gt, const at::Tensor& sp, const at::Tensor& x,
+                              const c10::optional<at::Tensor>& post) {
   check_cuda(y, "y");
   check_cuda(gt, "g");
   check_cuda(x, "x");
   TORCH_CHECK(y.scalar_type() == gt.scalar_type() && y.scalar_type() == x.scalar_type(), "gated_residual: dtypes");
   TORCH_CHECK(y.sizes() == gt.sizes() && y.sizes() == x.sizes(), "gated_residual: shapes");
+  TORCH_CHECK(y.is_contiguous() && gt.is_contiguous() && x.is_contiguous(), "gated_residual: contiguous operands");
   TORCH_CHECK(sp.scalar_type() == at::kFloat, "gated_residual: sp fp32");
+  const void* pp = nullptr;
+  if (post && post->defined()) {
+    check_cuda(*post, "post");
+    TORCH_CHECK(post->scalar_type() == y.scalar_type() && post->sizes() == y.sizes() && post->is_contiguous(),
+                "gated_residual: post must match y (dtype, shape, contiguous)");
+    pp = post->data_ptr();
+  }
   c10::hip::HIPGuard g(y.device().index());
   auto out = at::empty_like(y);
-  as::gated_residual_fwd(y.data_ptr(), gt.data_ptr(), sp.data_ptr<float>(), x.data_ptr(), out.data_ptr(), dt(y),
+  as::gated_residual_fwd(y.data_ptr(), gt.data_ptr(), sp.data_ptr<float>(), x.data_ptr(), pp, out.data_ptr(), dt(y),
                          y.numel(), stream());
   return out;
 }
 
+// out: the saved block output (its ReLU mask); with xin (the block input) the mask comes from the recomputed
+// pre-activation instead (the forward carried a post-add, so the saved tensor is not the ReLU output)
 std::vector<at::Tensor> gated_residual_bwd(const at::Tensor& dout, const at::Tensor& y, const at::Tensor& gt,
-                                           const at::Tensor& sp, const at::Tensor& out) {
+                                           const at::Tensor& sp, const at::Tensor& out,
+                                           const c10::optional<at::Tensor>& xin) {
   check_cuda(dout, "dout");
   TORCH_CHECK(dout.scalar_type() == y.scalar_type(), "gated_residual_bwd: dtype");
+  const at::Tensor& mref = (xin && xin->defined()) ? *xin : out;
+  TORCH_CHECK(mref.scalar_type() == y.scalar_type() && mref.sizes() == y.sizes() && mref.is_contiguous() &&
+                  dout.sizes() == y.sizes() && dout.is_contiguous() && y.is_contiguous() && gt.is_contiguous(),
+              "gated_residual_bwd: operands must match y (dtype, shape, contiguous)");
   c10::hip::HIPGuard g(y.device().index());
   auto dy = at::empty_like(y), dg = at::empty_like(y), dx = at::empty_like(y);
   const int nblk = as::elementwise_blocks(y.numel());
   auto part = at::empty({nblk}, y.options().dtype(at::kFloat));
-  as::gated_residual_bwd(dout.data_ptr(), y.data_ptr(), gt.data_ptr(), sp.data_ptr<float>(), out.data_ptr(), dt(y),
-                         dy.data_ptr(), dg.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), y.numel(), nblk,
-                         stream());
+  const bool use_x = xin && xin->defined();
+  as::gated_residual_bwd(dout.data_ptr(), y.data_ptr(), gt.data_ptr(), sp.data_ptr<float>(),
+                         use_x ? nullptr : out.data_ptr(), use_x ? xin->data_ptr() : nullptr, dt(y), dy.data_ptr(),
+                         dg.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), y.numel(), nblk, stream());
   return {dy, dg, dx, part.sum().reshape({1})};
 }
 
@@ -1945,8 +1963,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layer_norm_fwd", &layer_norm_fwd);
   m.def("layer_norm_bwd", &layer_norm_bwd);
   m.def("reverse_scan", &reverse_scan);
-  m.def("gated_residual_fwd", &gated_residual_fwd);
-  m.def("gated_residual_bwd", &gated_residual_bwd);
+  m.def("gated_residual_fwd", &gated_residual_fwd, py::arg("y"), py::arg("g"), py::arg("sp"), py::arg("x"),
+        py::arg("post") = py::none());
+  m.def("gated_residual_bwd", &gated_residual_bwd, py::arg("dout"), py::arg("y"), py::arg("g"), py::arg("sp"),
+        py::arg("out"), py::arg("xin") = py::none());
   m.def("lnlstm_fwd", &lnlstm_fwd);
   m.def("lnlstm_bwd", &lnlstm_bwd);
   m.def("entity_embed_fwd", &entity_embed_fwd);

@@ -45,8 +45,8 @@ void reverse_scan(const float* a, const float* b, const float* init, float* y, i
 
 // ---- elementwise.hip -------------------------------------------------------------------------
 // out = relu(tanh(y * sigmoid(g)) * sp + x)
-void gated_residual_fwd(const void* y, const void* g, const float* sp, const void* x, void* out, int dt, long n,
-                        hipStream_t s);
+void gated_residual_fwd(const void* y, const void* g, const float* sp, const void* x, const void* post, void* out,
+                        int dt, long n, hipStream_t s);
 // value-encoder spatial input: relu(W [sc(8) | own | enemy] + b) per NHWC pixel, one-pass backward
 int vsp_in_channels();
 int vsp_out_channels();
@@ -68,8 +68,9 @@ void loc_in_fwd(const void* y0, const void* p, const float* wp, void* out, long 
 int loc_in_bwd_blocks(long npix);
 void loc_in_bwd(const void* dy, const void* y, const void* p, const float* wp, void* dym, void* dp, float* part,
                 long npix, int HW, int nblk, hipStream_t s);
-void gated_residual_bwd(const void* dout, const void* y, const void* g, const float* sp, const void* out, int dt,
-                        void* dy, void* dg, void* dx, float* dsp_part, long n, int nblk, hipStream_t s);
+void gated_residual_bwd(const void* dout, const void* y, const void* g, const float* sp, const void* out,
+                        const void* xin, int dt, void* dy, void* dg, void* dx, float* dsp_part, long n, int nblk,
+                        hipStream_t s);
 int elementwise_blocks(long n);
 
 // ---- lstm.hip --------------------------------------------------------------------------------

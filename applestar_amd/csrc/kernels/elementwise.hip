@@ -3,7 +3,9 @@
 // gated_residual: the location head's GatedResBlock output  relu(tanh(y * sigmoid(g)) * sp + x)
 // (module_utils.py:224-231) — 5 torch kernels + 4 temporaries per block in the reference, one pass
 // here; the backward recomputes sigmoid/tanh from y, g and writes dy, dg, dx plus per-block partial
-// sums for d(sp) in one pass.
+// sums for d(sp) in one pass.  ``post``: a tensor added to the block output in the same pass (the location head
+// adds the next encoder skip map to every block's output); the backward then takes the ReLU mask from the
+// recomputed pre-activation (``xin`` = the block input) instead of the saved output.
 #include "../common.h"
 #include "../kernels.h"
 
@@ -13,32 +15,36 @@ namespace {
 template <typename T>
 __global__ __launch_bounds__(256) void gated_residual_fwd_kernel(const T* __restrict__ y, const T* __restrict__ g,
                                                                  const float* __restrict__ sp, const T* __restrict__ x,
-                                                                 T* __restrict__ out, long n) {
+                                                                 const T* __restrict__ post, T* __restrict__ out,
+                                                                 long n) {
   const float s = sp[0];
   for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
        i += static_cast<long>(gridDim.x) * blockDim.x) {
     const float yv = Cvt<T>::load(y, i), gv = Cvt<T>::load(g, i), xv = Cvt<T>::load(x, i);
-    const float v = tanhf(yv * sigmoidf_(gv)) * s + xv;
-    Cvt<T>::store(out, i, fmaxf(v, 0.f));
+    const float v = fmaxf(fmaf(tanhf(yv * sigmoidf_(gv)), s, xv), 0.f);
+    Cvt<T>::store(out, i, post != nullptr ? v + Cvt<T>::load(post, i) : v);
   }
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void gated_residual_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ y,
                                                                  const T* __restrict__ g, const float* __restrict__ sp,
-                                                                 const T* __restrict__ out, T* __restrict__ dy,
-                                                                 T* __restrict__ dg, T* __restrict__ dx,
-                                                                 float* __restrict__ dsp_part, long n) {
+                                                                 const T* __restrict__ out, const T* __restrict__ xin,
+                                                                 T* __restrict__ dy, T* __restrict__ dg,
+                                                                 T* __restrict__ dx, float* __restrict__ dsp_part,
+                                                                 long n) {
   __shared__ float red[4];
   const float s = sp[0];
   float acc = 0.f;
   for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
        i += static_cast<long>(gridDim.x) * blockDim.x) {
-    const float o = Cvt<T>::load(out, i);
-    const float d = o > 0.f ? Cvt<T>::load(dout, i) : 0.f;
     const float yv = Cvt<T>::load(y, i), gv = Cvt<T>::load(g, i);
     const float sg = sigmoidf_(gv);
     const float th = tanhf(yv * sg);
+    // the ReLU mask: from the saved output, or (xin: the output carried a post-add) from the recomputed
+    // pre-activation, the forward's exact expression
+    const bool on = xin != nullptr ? fmaf(th, s, Cvt<T>::load(xin, i)) > 0.f : Cvt<T>::load(out, i) > 0.f;
+    const float d = on ? Cvt<T>::load(dout, i) : 0.f;
     acc += d * th;
     const float dpre = d * s * (1.f - th * th);  // d/d(y*sg)
     Cvt<T>::store(dy, i, dpre * sg);
@@ -70,6 +76,7 @@ __global__ __launch_bounds__(256) void gated_residual_fwd_v8_kernel(const bf16_t
                                                                     const bf16_t* __restrict__ g,
                                                                     const float* __restrict__ sp,
                                                                     const bf16_t* __restrict__ x,
+                                                                    const bf16_t* __restrict__ post,
                                                                     bf16_t* __restrict__ out, long n8) {
   const float s = sp[0];
   for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < n8;
@@ -79,7 +86,14 @@ __global__ __launch_bounds__(256) void gated_residual_fwd_v8_kernel(const bf16_t
     gr_unpack8(reinterpret_cast<const uint4*>(g)[i], gv);
     gr_unpack8(reinterpret_cast<const uint4*>(x)[i], xv);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = fmaxf(tanhf(yv[e] * sigmoidf_(gv[e])) * s + xv[e], 0.f);
+    for (int e = 0; e < 8; ++e) o[e] = fmaxf(fmaf(tanhf(yv[e] * sigmoidf_(gv[e])), s, xv[e]), 0.f);
+    if (post != nullptr) {
+      // the block output stays in fp32 until the post-add: one bf16 rounding where the separate add rounded twice
+      float pv[8];
+      gr_unpack8(reinterpret_cast<const uint4*>(post)[i], pv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] += pv[e];
+    }
     reinterpret_cast<uint4*>(out)[i] = gr_pack8(o);
   }
 }
@@ -89,6 +103,7 @@ __global__ __launch_bounds__(256) void gated_residual_bwd_v8_kernel(const bf16_t
                                                                     const bf16_t* __restrict__ g,
                                                                     const float* __restrict__ sp,
                                                                     const bf16_t* __restrict__ out,
+                                                                    const bf16_t* __restrict__ xin,
                                                                     bf16_t* __restrict__ dy, bf16_t* __restrict__ dg,
                                                                     bf16_t* __restrict__ dx,
                                                                     float* __restrict__ dsp_part, long n8) {
@@ -98,15 +113,16 @@ __global__ __launch_bounds__(256) void gated_residual_bwd_v8_kernel(const bf16_t
   for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < n8;
        i += static_cast<long>(gridDim.x) * blockDim.x) {
     float ov[8], dv[8], yv[8], gv[8], ody[8], odg[8], odx[8];
-    gr_unpack8(reinterpret_cast<const uint4*>(out)[i], ov);
+    gr_unpack8(reinterpret_cast<const uint4*>(xin != nullptr ? xin : out)[i], ov);
     gr_unpack8(reinterpret_cast<const uint4*>(dout)[i], dv);
     gr_unpack8(reinterpret_cast<const uint4*>(y)[i], yv);
     gr_unpack8(reinterpret_cast<const uint4*>(g)[i], gv);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float d = ov[e] > 0.f ? dv[e] : 0.f;
       const float sg = sigmoidf_(gv[e]);
       const float th = tanhf(yv[e] * sg);
+      const bool on = xin != nullptr ? fmaf(th, s, ov[e]) > 0.f : ov[e] > 0.f;
+      const float d = on ? dv[e] : 0.f;
       acc += d * th;
       const float dpre = d * s * (1.f - th * th);
       ody[e] = dpre * sg;
@@ -130,42 +146,46 @@ int elementwise_blocks(long n) {
   return static_cast<int>(b < 2048 ? (b < 1 ? 1 : b) : 2048);
 }
 
-void gated_residual_fwd(const void* y, const void* g, const float* sp, const void* x, void* out, int dt, long n,
-                        hipStream_t s) {
+void gated_residual_fwd(const void* y, const void* g, const float* sp, const void* x, const void* post, void* out,
+                        int dt, long n, hipStream_t s) {
   if (dt == DT_BF16 && n % 8 == 0) {
     hipLaunchKernelGGL(gated_residual_fwd_v8_kernel, dim3(elementwise_blocks(n / 8)), dim3(256), 0, s,
                        static_cast<const bf16_t*>(y), static_cast<const bf16_t*>(g), sp, static_cast<const bf16_t*>(x),
-                       static_cast<bf16_t*>(out), n / 8);
+                       static_cast<const bf16_t*>(post), static_cast<bf16_t*>(out), n / 8);
     return;
   }
   dim3 grid(elementwise_blocks(n)), block(256);
   if (dt == DT_BF16)
     hipLaunchKernelGGL(gated_residual_fwd_kernel<bf16_t>, grid, block, 0, s, static_cast<const bf16_t*>(y),
-                       static_cast<const bf16_t*>(g), sp, static_cast<const bf16_t*>(x), static_cast<bf16_t*>(out), n);
+                       static_cast<const bf16_t*>(g), sp, static_cast<const bf16_t*>(x),
+                       static_cast<const bf16_t*>(post), static_cast<bf16_t*>(out), n);
   else
     hipLaunchKernelGGL(gated_residual_fwd_kernel<float>, grid, block, 0, s, static_cast<const float*>(y),
-                       static_cast<const float*>(g), sp, static_cast<const float*>(x), static_cast<float*>(out), n);
+                       static_cast<const float*>(g), sp, static_cast<const float*>(x), static_cast<const float*>(post),
+                       static_cast<float*>(out), n);
 }
 
-void gated_residual_bwd(const void* dout, const void* y, const void* g, const float* sp, const void* out, int dt,
-                        void* dy, void* dg, void* dx, float* dsp_part, long n, int nblk, hipStream_t s) {
+void gated_residual_bwd(const void* dout, const void* y, const void* g, const float* sp, const void* out,
+                        const void* xin, int dt, void* dy, void* dg, void* dx, float* dsp_part, long n, int nblk,
+                        hipStream_t s) {
   dim3 grid(nblk), block(256);
   if (dt == DT_BF16 && n % 8 == 0) {   // nblk (from elementwise_blocks(n)) >= the blocks the 8-wide loop needs
     hipLaunchKernelGGL(gated_residual_bwd_v8_kernel, grid, block, 0, s, static_cast<const bf16_t*>(dout),
                        static_cast<const bf16_t*>(y), static_cast<const bf16_t*>(g), sp,
-                       static_cast<const bf16_t*>(out), static_cast<bf16_t*>(dy), static_cast<bf16_t*>(dg),
-                       static_cast<bf16_t*>(dx), dsp_part, n / 8);
+                       static_cast<const bf16_t*>(out), static_cast<const bf16_t*>(xin), static_cast<bf16_t*>(dy),
+                       static_cast<bf16_t*>(dg), static_cast<bf16_t*>(dx), dsp_part, n / 8);
     return;
   }
   if (dt == DT_BF16)
     hipLaunchKernelGGL(gated_residual_bwd_kernel<bf16_t>, grid, block, 0, s, static_cast<const bf16_t*>(dout),
                        static_cast<const bf16_t*>(y), static_cast<const bf16_t*>(g), sp,
-                       static_cast<const bf16_t*>(out), static_cast<bf16_t*>(dy), static_cast<bf16_t*>(dg),
-                       static_cast<bf16_t*>(dx), dsp_part, n);
+                       static_cast<const bf16_t*>(out), static_cast<const bf16_t*>(xin), static_cast<bf16_t*>(dy),
+                       static_cast<bf16_t*>(dg), static_cast<bf16_t*>(dx), dsp_part, n);
   else
     hipLaunchKernelGGL(gated_residual_bwd_kernel<float>, grid, block, 0, s, static_cast<const float*>(dout),
                        static_cast<const float*>(y), static_cast<const float*>(g), sp, static_cast<const float*>(out),
-                       static_cast<float*>(dy), static_cast<float*>(dg), static_cast<float*>(dx), dsp_part, n);
+                       static_cast<const float*>(xin), static_cast<float*>(dy), static_cast<float*>(dg),
+                       static_cast<float*>(dx), dsp_part, n);
 }
 
 }  // namespace as

@@ -157,15 +157,23 @@ class GatedResBlock(nn.Module):
                                          ConvBlock(dim, dim, 1, act=True), ConvBlock(dim, dim, 1, act=False))
         self.UpdateSP = nn.Parameter(torch.full((1,), 0.1))
 
-    def forward(self, x):
+    def forward(self, x, post=None):
+        """``post``: added to the output (the location head's next skip map), in the output pass when fused."""
         n = ops._native(x)
         if n is not None and n.has('gated_resblock') and FUSED_GATED_RESBLOCK:
-            out = n.gated_resblock(x, self.conv1[0], self.conv2[0], [m[0] for m in self.GateWeightG], self.UpdateSP)
+            out = n.gated_resblock(x, self.conv1[0], self.conv2[0], [m[0] for m in self.GateWeightG], self.UpdateSP,
+                                   post)
             if out is not None:
                 return out
+            if post is not None:
+                out = n.gated_resblock(x, self.conv1[0], self.conv2[0], [m[0] for m in self.GateWeightG],
+                                       self.UpdateSP)
+                if out is not None:
+                    return out + post
         y = self.conv2(self.conv1(x))
         g = self.GateWeightG(x)
-        return ops.gated_residual(y, g, self.UpdateSP, x)
+        out = ops.gated_residual(y, g, self.UpdateSP, x)
+        return out if post is None else out + post
 
 
 class OneHotTable(nn.Module):

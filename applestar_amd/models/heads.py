@@ -386,8 +386,12 @@ class LocationHead(nn.Module):
                 p = p.contiguous(memory_format=torch.channels_last)
             x = F.relu(torch.cat([p.to(skip.dtype), skip], 1))
             x = self.conv1(x)
+        # block i's input is the previous output + skip map -1 - i: the adds after the first ride in the blocks'
+        # output pass (GatedResBlock post)
+        x = x + map_skip[-1]
         for i, blk in enumerate(self.res):
-            x = blk(x + map_skip[len(map_skip) - 1 - i])
+            j = len(map_skip) - 2 - i
+            x = blk(x, map_skip[j] if i + 1 < len(self.res) else None)
         for conv in self.upsample[:-1]:
             x = conv(ops.upsample2x(x))
         last = self.upsample[-1][0]  # 32 -> 1: fused upsample + conv, the 32-ch map never hits HBM

@@ -5,6 +5,7 @@ Shapes/dtypes the kernels do not cover raise instead of silently using torch.
 """
 from __future__ import annotations
 
+import collections
 import os
 import weakref
 
@@ -179,6 +180,7 @@ class _LNLSTMRecurrence(torch.autograd.Function):
             xp.contiguous(), h0.contiguous(), c0.contiguous(), wT, lnh_w.detach(), lnh_b.detach(),
             lnc_w.detach(), lnc_b.detach(), 1e-5)
         ctx.save_for_backward(h0, out, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c, wq.contiguous(), lnh_w, lnc_w)
+        ctx.set_materialize_grads(False)     # unused hT / cT: None (a cached zero) instead of two fills per layer
         return out, hT, cT
 
     @staticmethod
@@ -825,6 +827,8 @@ class _Conv3x3(torch.autograd.Function):
         ctx.save_for_backward(x_nhwc, w_lp, out)
         ctx.act, ctx.has_res = act, res_nhwc is not None
         ctx.b_dtype = b.dtype if b is not None else None
+        if _DEBUG_PREMASK:
+            ctx.site = _fwd_site()
         return out
 
     @staticmethod
@@ -833,6 +837,8 @@ class _Conv3x3(torch.autograd.Function):
         if ctx.act == 'relu' and _premasked(out, dout):
             dpre = dout.contiguous()                       # the consumer's backward applied the mask
         else:
+            if ctx.act == 'relu':
+                _premask_miss(ctx, 'conv3x3', out)
             dpre = _act_grad(dout, out, ctx.act == 'relu')    # one pass: mask + cast + NHWC
         has_b = ctx.b_dtype is not None
         cout, cin = w.shape[0], w.shape[1]
@@ -992,6 +998,8 @@ class SkipLink:
 
 
 SKIP_LINK = os.environ.get('APPLESTAR_SKIP_LINK', '1') == '1'    # A/B switch
+# the location head's skip-map adds in the gated residual blocks' output pass (APPLESTAR_POST_ADD=0: separate adds)
+POST_ADD = os.environ.get('APPLESTAR_POST_ADD', '1') == '1'
 
 
 class _ResBlock(torch.autograd.Function):
@@ -1014,6 +1022,8 @@ class _ResBlock(torch.autograd.Function):
         if out.dtype == torch.float32 and SKIP_LINK:
             _note_relu_out(out)
             ctx.mask_in = _relu_src(x)
+        if _DEBUG_PREMASK:
+            ctx.site = _fwd_site()
         return out
 
     @staticmethod
@@ -1022,6 +1032,7 @@ class _ResBlock(torch.autograd.Function):
         if out.dtype == torch.float32 and _premasked(out, dout):
             dpre2 = dout.contiguous()           # the consumer's dX epilogue already applied this block's ReLU
         else:
+            _premask_miss(ctx, 'resblock', out)
             dpre2 = _act_grad(dout, out, True)
         side = _SideWork(dpre2, dpre2.numel() // dpre2.shape[-1])
         with side.fork():       # weight gradients concurrent with the dX convs
@@ -1092,7 +1103,7 @@ class _GatedResBlock(torch.autograd.Function):
     that sum in its epilogue - no separate whole-activation adds."""
 
     @staticmethod
-    def forward(ctx, x, sp, w1, b1, w2, b2, *gate):
+    def forward(ctx, x, sp, post, w1, b1, w2, b2, *gate):
         for p in (w1, w2, *gate[0::2]):
             _count_use(p)
         B, H, W, C = x.shape
@@ -1121,16 +1132,21 @@ class _GatedResBlock(torch.autograd.Function):
                 gw, gb = gate[2 * i].detach().view(C, C), gate[2 * i + 1].detach()
                 h = torch._addmm_activation(gb, h, gw.t(), use_gelu=False) if i < 3 else torch.addmm(gb, h, gw.t())
                 acts.append(h)
-        out = _C.gated_residual_fwd(y, h.view(B, H, W, C), sp, x)
-        ctx.save_for_backward(x, sp, w1, w2, y1, y, out, *acts[1:], *gate[0::2])
+        # post: the next encoder skip map, added to the block output in the same pass (LocationHead)
+        out = _C.gated_residual_fwd(y, h.view(B, H, W, C), sp, x, post)
+        ctx.save_for_backward(x, sp, w1, w2, y1, y, out if post is None else None, *acts[1:], *gate[0::2])
         ctx.dtypes = (b1.dtype, b2.dtype, gate[1].dtype)
+        ctx.has_post = post is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
         x, sp, w1, w2, y1, y, out, a1, a2, a3, g, gw1, gw2, gw3, gw4 = ctx.saved_tensors
         B, H, W, C = x.shape
-        dy, dg, dx_res, dsp = _C.gated_residual_bwd(dout.contiguous().to(y.dtype), y, g.view(B, H, W, C), sp, out)
+        dout = dout.contiguous().to(y.dtype)
+        # with a post-add the saved output is not the ReLU output: the mask is recomputed from the block input
+        dy, dg, dx_res, dsp = _C.gated_residual_bwd(dout, y, g.view(B, H, W, C), sp, out,
+                                                    x if ctx.has_post else None)
         # gate chain (1x1 convs as GEMMs over the pixels)
         grads_g = []
         d = dg.view(-1, C)
@@ -1185,19 +1201,24 @@ class _GatedResBlock(torch.autograd.Function):
         gate_grads = [None] * 8
         for i, dw_i, db_i in grads_g:
             gate_grads[2 * i], gate_grads[2 * i + 1] = dw_i, db_i
-        return (dx, dsp.to(sp.dtype), dw1, db1, dw2, db2, *gate_grads)
+        return (dx, dsp.to(sp.dtype), dout if ctx.has_post else None, dw1, db1, dw2, db2, *gate_grads)
 
 
-def gated_resblock(x, conv1, conv2, gates, sp):
-    """Fused GatedResBlock (see _GatedResBlock); None when not covered (caller falls back)."""
+def gated_resblock(x, conv1, conv2, gates, sp, post=None):
+    """Fused GatedResBlock (see _GatedResBlock); None when not covered (caller falls back).  ``post``: a tensor of
+    x's shape added to the block output in the same pass (None when it cannot be: the caller adds it)."""
     C = x.shape[1]
     ws = [conv1.weight, conv1.bias, conv2.weight, conv2.bias]
     for gc in gates:
         ws += [gc.weight, gc.bias]
     if x.dim() != 4 or any(t is None for t in ws) or C % 8:
         return None
-    if _f32_conv_ok(x, conv1.weight, C, C) and all(t.dtype == torch.float32 for t in ws):
-        return from_nhwc(_GatedResBlock.apply(nhwc(x), sp.float(), *ws))
+    if post is not None and (post.shape != x.shape or not post.is_contiguous(memory_format=torch.channels_last)
+                             or not POST_ADD):
+        return None
+    if _f32_conv_ok(x, conv1.weight, C, C) and all(t.dtype == torch.float32 for t in ws) and \
+            (post is None or post.dtype == torch.float32):
+        return from_nhwc(_GatedResBlock.apply(nhwc(x), sp.float(), None if post is None else nhwc(post), *ws))
     lowp = x.dtype == torch.bfloat16 or torch.is_autocast_enabled()
     if not lowp or not _C.conv3x3_supported(C, C):
         return None
@@ -1205,8 +1226,9 @@ def gated_resblock(x, conv1, conv2, gates, sp):
     # given: the conv epilogue adds them in fp32
     ws = [t if (t.dtype == torch.bfloat16 or i in (1, 3)) else _CastWeight.apply(t) for i, t in enumerate(ws)]
     xl = nhwc(x.to(torch.bfloat16))
+    pl = None if post is None else nhwc(post.to(torch.bfloat16))
     with torch.autocast('cuda', enabled=False):
-        return from_nhwc(_GatedResBlock.apply(xl, sp.float(), *ws))
+        return from_nhwc(_GatedResBlock.apply(xl, sp.float(), pl, *ws))
 
 
 class _CastWeight(torch.autograd.Function):
@@ -1486,6 +1508,8 @@ class _Linear(torch.autograd.Function):
         ctx.relu = relu
         ctx.b_dtype = b.dtype if b is not None else None
         ctx.mask_in = x2.dtype == torch.float32 and link is None and _relu_src(x2)
+        if _DEBUG_PREMASK:
+            ctx.site = _fwd_site()
         return y
 
     @staticmethod
@@ -1495,6 +1519,7 @@ class _Linear(torch.autograd.Function):
             dy = dy.contiguous().view(y.shape)      # the consumer's dX epilogue applied this ReLU's mask
         elif ctx.relu:
             R, N = y.shape
+            _premask_miss(ctx, 'linear', y)
             dy = _act_grad(dy.view(1, 1, R, N) if dy.is_contiguous() else dy.contiguous().view(1, 1, R, N),
                            y.view(1, 1, R, N), True).view(R, N)
         else:
@@ -1560,6 +1585,22 @@ class _Linear(torch.autograd.Function):
 RELU_LINK = os.environ.get('APPLESTAR_RELU_LINK', '1') == '1'   # A/B switch
 _RELU_OUTS = {}      # data_ptr -> weakref of an fp32 _Linear ReLU output (recorded in forward)
 _MASKED_DX = {}      # data_ptr of such an output -> (dX of its consumer, version): already ReLU-masked
+
+# debug (APPLESTAR_DEBUG_PREMASK=1): ReLU backward passes that could not be folded into a consumer's epilogue,
+# counted by (op, shape, forward call site) - tools/glue_sites.py prints them
+_DEBUG_PREMASK = os.environ.get('APPLESTAR_DEBUG_PREMASK', '0') == '1'
+PREMASK_MISSES = collections.Counter()
+
+
+def _fwd_site():
+    import traceback
+    fr = [f for f in traceback.extract_stack() if 'applestar_amd' in f.filename and 'ops/native.py' not in f.filename]
+    return ' < '.join(f'{f.filename.split("applestar_amd/")[-1]}:{f.lineno}' for f in fr[-2:][::-1])
+
+
+def _premask_miss(ctx, kind, t):
+    if _DEBUG_PREMASK:
+        PREMASK_MISSES[(kind, tuple(t.shape), getattr(ctx, 'site', '?'))] += 1
 
 
 def _relu_src(x2):
@@ -1846,6 +1887,7 @@ class _HeadStats(torch.autograd.Function):
     def forward(ctx, logits, teacher, action):
         out, stats = _C.head_stats_fwd(logits, teacher, action)
         ctx.save_for_backward(logits, teacher, action, stats)
+        ctx.set_materialize_grads(False)
         return out[0], out[1], out[2]
 
     @staticmethod

@@ -120,3 +120,38 @@ def test_deferred_head_wgrads_equal_inline(monkeypatch):
         d = grads[True][n]
         err = float((d - g).norm())
         assert torch.isfinite(d).all() and err < 1e-3 * float(g.norm()) + floor, (n, err, float(g.norm()))
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_gated_resblock_post_add_equals_separate_add(dtype):
+    """GatedResBlock(x, post) (the skip-map add in the block's output pass, the ReLU mask recomputed from the
+    block input in backward) == GatedResBlock(x) + post: forward and every gradient (fp32 to 1e-6 - the same
+    arithmetic; bf16 within one bf16 rounding of the output)."""
+    from applestar_amd.models.blocks import GatedResBlock
+    from applestar_amd.ops import native as N
+    N.ensure_loaded()
+    torch.manual_seed(0)
+    blk = GatedResBlock(128).to(DEV)
+    B, H, W = 6, 19, 20
+    x0 = torch.randn(B, 128, H, W, device=DEV).contiguous(memory_format=torch.channels_last)
+    p0 = torch.randn(B, 128, H, W, device=DEV).contiguous(memory_format=torch.channels_last)
+    go = torch.randn(B, 128, H, W, device=DEV).contiguous(memory_format=torch.channels_last)
+    res = {}
+    for fused in (True, False):
+        blk.zero_grad()
+        x = x0.clone().requires_grad_(True)
+        p = p0.clone().requires_grad_(True)
+        ctx = torch.autocast('cuda', dtype=torch.bfloat16) if dtype == torch.bfloat16 else torch.autocast('cuda',
+                                                                                                         enabled=False)
+        with ctx:
+            y = blk(x, p) if fused else blk(x) + p
+        y.float().backward(go)
+        res[fused] = (y.detach().float(), x.grad.clone(), p.grad.clone(),
+                      {n: q.grad.clone() for n, q in blk.named_parameters()})
+    a, b = res[True], res[False]
+    tol = 1e-6 if dtype == torch.float32 else 1e-2
+    for u, v in zip(a[:3], b[:3]):
+        assert (u - v).abs().max().item() <= tol * max(1.0, v.abs().max().item())
+    for n in a[3]:
+        d = (a[3][n] - b[3][n]).norm().item()
+        assert d <= (1e-6 if dtype == torch.float32 else 2e-2) * max(1e-12, b[3][n].norm().item()), n

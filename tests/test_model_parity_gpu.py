@@ -179,16 +179,128 @@ def test_full_model_bf16_gpu_vs_cpu_fp32(reference):
     if os.path.isdir(OUT_DIR):
         with open(os.path.join(OUT_DIR, 'bf16_grad_group_errors.json'), 'w') as f:
             json.dump(table, f, indent=1, sort_keys=True)
-    # r3b (profiles/r3b_bf16_grad_group_errors.json): 16 of 18 groups within +-15 % of torch's own bf16 error;
-    # the location head (5.8 vs 4.5 %) and the value encoder's 1x1 projection (a 176-parameter layer whose
-    # gradient is a 9.5M-pixel reduction of bf16 products: 25 vs 18 %) are the two above 1.25x
-    # r4: the action-type / delay / queued head groups are additionally allowed their measured native level
-    # (<= 0.11: 0.083 / 0.099 / 0.081 with the round-4 kernels, deterministic) when a run's control happens low
-    floor = {'policy.action_type_head': 0.11, 'policy.delay_head': 0.11, 'policy.queued_head': 0.11}
-    bad = {k: v for k, v in table.items() if v['native_bf16'] > max(1.5 * v['torch_bf16'], floor.get(k, 0.03))}
+    # r3b (profiles/r3b_bf16_grad_group_errors.json): 16 of 18 groups within +-15 % of torch's own bf16 error.
+    # No absolute floors: the control is the max over three runs, and why the head groups sit at 8-10 % in both
+    # paths is pinned down by test_bf16_head_grad_error_is_upstream_amplification below
+    bad = {k: v for k, v in table.items() if v['native_bf16'] > 1.5 * v['torch_bf16']}
     assert not bad, bad
     # and in absolute terms: the big groups (transformer, spatial ResNet, LSTM, heads) within 15 %
     assert all(v['native_bf16'] < 0.15 for k, v in table.items() if k.startswith(('core_lstm', 'policy'))), table
+
+
+def _tensor_leaves(tree, prefix=''):
+    if isinstance(tree, dict):
+        for k, v in tree.items():
+            yield from _tensor_leaves(v, f'{prefix}/{k}')
+    elif isinstance(tree, (list, tuple)):
+        for i, v in enumerate(tree):
+            yield from _tensor_leaves(v, f'{prefix}/{i}')
+    elif torch.is_tensor(tree) and tree.is_floating_point() and tree.requires_grad:
+        yield prefix, tree
+
+
+def _pinned_grad_errors(cpu, batch, ref_grads, pins, native: bool):
+    """Group gradient errors of the bf16 trainer when every model output's upstream gradient is pinned to the
+    fp32 oracle's (the surrogate loss sum_i <out_i, g_i> has exactly the oracle's parameter gradient); also the
+    relative error of the upstream gradients the bf16 step computes itself from the real loss."""
+    from applestar_amd import ops
+    ops.set_native(native)
+    try:
+        tr = RLTrainer(CFG, device='cuda')
+        tr.load_model_state_dict(cpu.state_dict())
+        from applestar_amd.runtime.train_engine import amp_context
+        with amp_context(tr.device, tr.amp_dtype):
+            out = tr.model.rl_learner_forward(**to_device(copy.deepcopy(batch), 'cuda'))
+        leaves = dict(_tensor_leaves(out))
+        # the upstream gradients of the real loss, computed in this path's own precision
+        info = tr.loss.compute_loss(out)
+        names = [k for k in pins if k in leaves]
+        own = torch.autograd.grad(info['total_loss'], [leaves[k] for k in names], retain_graph=True, allow_unused=True)
+        up_err = {}
+        for k, g in zip(names, own):
+            ref = pins[k]
+            if g is not None and float(ref.norm()) > 0:
+                up_err[k] = _rel(g.float(), ref)
+        sur = sum((leaves[k].float() * pins[k].to('cuda', torch.float32)).sum() for k in names)
+        tr.backward(sur)
+        tr._reduce()
+        views = tr.master._master_grad_views()
+        got = {}
+        for p in tr.master.reducer.params:
+            g = views.get(p, p.grad)
+            if g is not None:
+                got[tr.master.names[p]] = g.float()
+        torch.cuda.synchronize()
+    finally:
+        ops.set_native(True)
+    return _group_errors(got, ref_grads), up_err
+
+
+def test_bf16_head_grad_error_not_from_upstream_or_loss(reference):
+    """The 8-10 % bf16 gradient error of the small heads (action type / delay / queued), shared by the native
+    kernels and PyTorch's own autocast path, does not come from the loss: the upstream gradients the bf16 step
+    derives from the real loss are within a few percent of the oracle's, and with every model output's upstream
+    gradient PINNED to the oracle's the head groups keep the same error.  With the upstream pinned, the native
+    path is within 1.5x of the control in EVERY group, no floor (tables in gpurun_out/bf16_pinned_upstream_errors.json;
+    the cause is pinned down by test_bf16_head_grad_error_is_weight_rounding_sensitivity)."""
+    batch, (cpu, ref_out, ref_info, ref_grads) = reference
+    out = cpu.rl_learner_forward(**copy.deepcopy(batch))
+    info = ReinforcementLoss(RLTrainer(CFG).cfg.learner, 'MP0').compute_loss(out)
+    leaves = dict(_tensor_leaves(out))
+    names = list(leaves)
+    gs = torch.autograd.grad(info['total_loss'], [leaves[k] for k in names], allow_unused=True)
+    pins = {k: g.detach() for k, g in zip(names, gs) if g is not None}
+    assert any('target_logit' in k for k in pins) and any('value' in k for k in pins), list(pins)
+    nat, up_nat = _pinned_grad_errors(cpu, batch, ref_grads, pins, native=True)
+    ctl, up_ctl = _pinned_grad_errors(cpu, batch, ref_grads, pins, native=False)
+    table = {k: {'native_bf16_pinned': nat[k], 'torch_bf16_pinned': ctl[k]} for k in nat}
+    ups = {k: {'native_bf16': up_nat.get(k), 'torch_bf16': up_ctl.get(k)} for k in pins}
+    print('pinned-upstream group errors:', json.dumps(table, indent=1, sort_keys=True))
+    print('upstream (d loss / d output) errors of the bf16 paths:', json.dumps(ups, indent=1, sort_keys=True))
+    if os.path.isdir(OUT_DIR):
+        with open(os.path.join(OUT_DIR, 'bf16_pinned_upstream_errors.json'), 'w') as f:
+            json.dump({'pinned_group_errors': table, 'upstream_errors': ups}, f, indent=1, sort_keys=True)
+    # r5g: upstream errors 0.1-1.9 % (native) / 0.1-0.9 % (torch); pinned head groups 0.083 / 0.099 / 0.081 native
+    # vs 0.083 / 0.097 / 0.080 torch - the same as under the real loss
+    for k, v in ups.items():
+        if v['native_bf16'] is not None:
+            assert v['native_bf16'] < 0.05, (k, v)
+    bad = {k: v for k, v in table.items() if v['native_bf16_pinned'] > 1.5 * v['torch_bf16_pinned']}
+    assert not bad, bad
+
+
+def test_bf16_head_grad_error_is_weight_rounding_sensitivity(reference):
+    """Root cause of the shared 8-10 % head-gradient error: the gradient's sensitivity to rounding the weights to
+    bf16 at all.  The fp32 step (fp32 kernels, accurate to ~1e-5 against the oracle with the oracle's weights) run
+    with every weight rounded to bf16 - no bf16 arithmetic anywhere - already moves the head groups' gradients by
+    most of that error: a 2^-9 relative weight perturbation flips the ReLU gates (and max-pool / selection
+    decisions) whose pre-activations sit within that margin of the boundary, and each flipped gate reroutes a whole
+    unit's gradient.  The bf16 paths inherit this from their bf16 compute weights; it is not kernel error."""
+    batch, (cpu, ref_out, ref_info, ref_grads) = reference
+    fp32_cfg = {**CFG, 'learner': {**CFG['learner'], 'amp_dtype': None}}
+    res = {}
+    for tag, rnd in (('fp32_exact_weights', False), ('fp32_bf16_rounded_weights', True)):
+        tr = RLTrainer(fp32_cfg, device='cuda')
+        sd = {k: (v.to(torch.bfloat16).float() if rnd and v.is_floating_point() else v)
+              for k, v in cpu.state_dict().items()}
+        tr.model.load_state_dict(sd)
+        out = tr.model.rl_learner_forward(**to_device(copy.deepcopy(batch), 'cuda'))
+        tr.loss.compute_loss(out)['total_loss'].backward()
+        got = {n: p.grad for n, p in tr.model.named_parameters() if p.grad is not None}
+        res[tag] = _group_errors(got, ref_grads)
+    errs, _, _ = _bf16_grad_errors(cpu, batch, ref_grads, native=True)
+    table = {k: {'fp32_exact_weights': res['fp32_exact_weights'][k],
+                 'fp32_bf16_rounded_weights': res['fp32_bf16_rounded_weights'][k], 'native_bf16': errs[k]}
+             for k in errs}
+    print('weight-rounding sensitivity:', json.dumps(table, indent=1, sort_keys=True))
+    if os.path.isdir(OUT_DIR):
+        with open(os.path.join(OUT_DIR, 'bf16_weight_rounding_sensitivity.json'), 'w') as f:
+            json.dump(table, f, indent=1, sort_keys=True)
+    for k in ('policy.action_type_head', 'policy.delay_head', 'policy.queued_head'):
+        v = table[k]
+        assert v['fp32_exact_weights'] < 1e-3, (k, v)
+        # rounding the weights alone accounts for at least half of the bf16 path's error
+        assert v['fp32_bf16_rounded_weights'] > 0.5 * v['native_bf16'], (k, v)
 
 
 def _trajectory(cfg, batches, steps, w_init, native=True):

@@ -20,7 +20,14 @@ def main():
     ap.add_argument('--precision', default='fp32')
     ap.add_argument('--top', type=int, default=60)
     ap.add_argument('--shapes', action='store_true', help='key the call sites by the first two tensor shapes too')
+    ap.add_argument('--timed', action='store_true',
+                    help='also time every dispatched aten op with stream events and attribute backward ops to their '
+                         'autograd node and its forward call site (anomaly mode keeps the forward stacks)')
+    ap.add_argument('--premask', action='store_true',
+                    help='count the ReLU backward passes not folded into a consumer epilogue, by forward site')
     args = ap.parse_args()
+    if args.premask:
+        os.environ['APPLESTAR_DEBUG_PREMASK'] = '1'
     from applestar_amd.rl.trainer import RLTrainer
     from applestar_amd.rl.synthetic import rl_batch, to_device
     dev = torch.device('cuda', 0)
@@ -90,6 +97,75 @@ def main():
     print('kernel-launching aten calls per iteration by site (TorchDispatchMode; metadata-only ops skipped):')
     for (name, site), n in sorted(sites.items(), key=lambda kv: -kv[1]):
         print(f'{n:6d}  {name:28s} {site}')
+    if args.timed:
+        timed_sites(tr, b, META, args)
+    if args.premask:
+        from applestar_amd.ops import native
+        native.PREMASK_MISSES.clear()
+        tr.step(dict(b))
+        torch.cuda.synchronize()
+        print()
+        print('ReLU backward passes not folded into a consumer epilogue (one iteration):')
+        for (kind, shape, site), n in sorted(native.PREMASK_MISSES.items(), key=lambda kv: -kv[1]):
+            print(f'{n:4d}  {kind:9s} {str(shape):24s} {site}')
+
+
+def _fwd_site(node):
+    """innermost applestar_amd frames of the forward call that created autograd node ``node``"""
+    tb = (getattr(node, 'metadata', None) or {}).get('traceback_')
+    if not tb:
+        return '?'
+    lines = [ln for ln in ''.join(tb).splitlines() if 'applestar_amd/' in ln and 'File' in ln][-2:]
+    out = []
+    for ln in lines[::-1]:
+        f = ln.split('applestar_amd/')[-1]
+        out.append(f.split('"')[0] + ':' + f.split('line ')[-1].split(',')[0])
+    return ' < '.join(out)
+
+
+def timed_sites(tr, b, META, args):
+    """device time of each dispatched aten op (a start / end event pair on the current stream around it),
+    grouped by op and site; ops inside backward carry their autograd node and the node's forward site"""
+    import traceback
+    from torch.utils._python_dispatch import TorchDispatchMode
+    recs = []
+
+    class Timed(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, a=(), kw=None):
+            name = str(func.overloadpacket.__name__)
+            if name in META:
+                return func(*a, **(kw or {}))
+            fr = [f for f in traceback.extract_stack() if 'applestar_amd' in f.filename][-2:]
+            if fr:
+                site = ' < '.join(f'{f.filename.split("applestar_amd/")[-1]}:{f.lineno}' for f in fr[::-1])
+            else:
+                node = torch._C._current_autograd_node()
+                site = f'[{node.name()}] fwd {_fwd_site(node)}' if node is not None else '(no frame)'
+            if args.shapes:
+                site += '  ' + str([tuple(t.shape) for t in a if isinstance(t, torch.Tensor)][:2])
+            st = torch.cuda.current_stream()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            out = func(*a, **(kw or {}))
+            e1.record(st)
+            recs.append((name, site, e0, e1))
+            return out
+    with torch.autograd.set_detect_anomaly(True, check_nan=False):
+        tr.step(dict(b))             # anomaly mode records forward stacks of the nodes
+        torch.cuda.synchronize()
+        with Timed():
+            tr.step(dict(b))
+        torch.cuda.synchronize()
+    agg = collections.defaultdict(lambda: [0.0, 0])
+    for name, site, e0, e1 in recs:
+        agg[(name, site)][0] += e0.elapsed_time(e1)
+        agg[(name, site)][1] += 1
+    total = sum(v[0] for v in agg.values())
+    print()
+    print(f'event-timed aten ops, one iteration: {total:.2f} ms over {len(recs)} ops (includes any stall on the '
+          f'stream between the two events)')
+    for (name, site), (t, n) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:args.top * 2]:
+        print(f'{t:8.3f} ms {n:5d}x  {name:24s} {site}')
 
 
 if __name__ == '__main__':
