@@ -779,6 +779,50 @@ at::Tensor table_grad(const at::Tensor& src, const at::Tensor& idx, int64_t V) {
   return out;
 }
 
+namespace {
+int idx_dtype_code(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kLong: return 0;
+    case at::kInt: return 1;
+    case at::kShort: return 2;
+    case at::kByte: return 3;
+    case at::kChar: return 4;
+    default: TORCH_CHECK(false, "embed_relu: integer index tensor expected");
+  }
+  return 0;
+}
+}  // namespace
+
+// relu(table[clamp(idx)]) -> [U, D] (table fp32 or bf16 [V, D]; idx any integer dtype, contiguous)
+at::Tensor embed_relu_fwd(const at::Tensor& table, const at::Tensor& idx) {
+  check_cuda(table, "table");
+  check_cuda(idx, "idx");
+  TORCH_CHECK(table.dim() == 2 && table.is_contiguous() && idx.is_contiguous(), "embed_relu: contiguous [V, D] table");
+  TORCH_CHECK(table.scalar_type() == at::kFloat || table.scalar_type() == at::kBFloat16, "embed_relu: fp32 / bf16");
+  c10::hip::HIPGuard g(table.device().index());
+  auto out = at::empty({idx.numel(), table.size(1)}, table.options());
+  as::embed_relu_fwd(table.data_ptr(), dt(table), idx.data_ptr(), idx_dtype_code(idx), out.data_ptr(), idx.numel(),
+                     static_cast<int>(table.size(0)), static_cast<int>(table.size(1)), stream());
+  return out;
+}
+
+// d table (fp32 [V, D]) of embed_relu_fwd: rows of dout masked by out > 0, summed per (clamped) index
+at::Tensor embed_relu_bwd(const at::Tensor& dout, const at::Tensor& out, const at::Tensor& idx, int64_t V) {
+  check_cuda(dout, "dout");
+  TORCH_CHECK(dout.sizes() == out.sizes() && dout.scalar_type() == out.scalar_type() && dout.is_contiguous() &&
+                  out.is_contiguous() && out.dim() == 2 && idx.numel() == out.size(0) && idx.is_contiguous(),
+              "embed_relu_bwd: dout / out [U, D] contiguous, idx [U]");
+  TORCH_CHECK(V * out.size(1) <= 16384, "embed_relu_bwd: table too large for LDS accumulation");
+  c10::hip::HIPGuard g(out.device().index());
+  const long U = out.size(0), D = out.size(1);
+  const bool direct = U * D <= 2048;
+  auto dtab = direct ? at::empty({V, D}, out.options().dtype(at::kFloat))
+                     : at::zeros({V, D}, out.options().dtype(at::kFloat));
+  as::embed_relu_bwd(dout.data_ptr(), out.data_ptr(), dt(out), idx.data_ptr(), idx_dtype_code(idx),
+                     dtab.data_ptr<float>(), U, static_cast<int>(V), static_cast<int>(D), direct, stream());
+  return dtab;
+}
+
 // ---------------------------------------------------------------- conv3x3 implicit GEMM (NHWC bf16)
 at::Tensor conv3x3_fwd(const at::Tensor& x, const at::Tensor& wk, const c10::optional<at::Tensor>& bias,
                        const c10::optional<at::Tensor>& res, int64_t act) {
@@ -1963,6 +2007,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layer_norm_fwd", &layer_norm_fwd);
   m.def("layer_norm_bwd", &layer_norm_bwd);
   m.def("reverse_scan", &reverse_scan);
+  m.def("embed_relu_fwd", &embed_relu_fwd);
+  m.def("embed_relu_bwd", &embed_relu_bwd);
   m.def("gated_residual_fwd", &gated_residual_fwd, py::arg("y"), py::arg("g"), py::arg("sp"), py::arg("x"),
         py::arg("post") = py::none());
   m.def("gated_residual_bwd", &gated_residual_bwd, py::arg("dout"), py::arg("y"), py::arg("g"), py::arg("sp"),

@@ -34,6 +34,11 @@ void layer_norm_bwd(const void* dy, int dy_dt, const void* xin, int xin_dt, cons
                     const float* w, const float* mean, const float* rstd, void* dx, int dx_dt,
                     float* dw_part, float* db_part, long rows, int cols, int act, int nblk, hipStream_t s);
 void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s);
+// scalar-encoder embedding + ReLU (idt: 0 int64, 1 int32, 2 int16, 3 uint8, 4 int8; index clamped to [0, V))
+void embed_relu_fwd(const void* table, int dt, const void* idx, int idt, void* out, long U, int V, int D,
+                    hipStream_t s);
+void embed_relu_bwd(const void* dout, const void* out, int dt, const void* idx, int idt, float* dtab, long U, int V,
+                    int D, bool direct, hipStream_t s);
 // nrows <= 1024 only (one pass, no atomics): bf16 output
 void column_reduce_bf16(const float* part, void* out, int nrows, int cols, hipStream_t s);
 int layer_norm_bwd_blocks(long rows);

@@ -17,6 +17,8 @@
 // column_reduce: out[c] = sum_r part[r][c] for the per-block partials of the LayerNorm / upconv
 //   weight gradients.  <= 1024 rows: one 1024-thread block per 64 columns (16 row groups x 4
 //   independent accumulators).  More rows: 256-row slabs per block, fp32 atomics into a zeroed out.
+#include <algorithm>
+
 #include "../common.h"
 #include "../kernels.h"
 
@@ -189,6 +191,51 @@ __global__ __launch_bounds__(256) void table_grad_kernel(const T* __restrict__ s
   for (int i = threadIdx.x; i < VD; i += blockDim.x) {
     const float a = acc[i];
     if (a != 0.f) atomicAdd(out + i, a);
+  }
+}
+
+// Embedding lookup + ReLU of the scalar encoder's small tables (the index column in its stored integer dtype,
+// clamped to [0, V)): out[u][d] = max(table[clamp(idx[u])][d], 0) - one launch instead of the integer cast,
+// clamp, gather and ReLU passes.  The backward sums the ReLU-masked rows into dtable with ONE workgroup for the
+// tiniest batches (LDS accumulation, plain stores: no zero fill of the output) or the LDS-then-global-atomic form.
+template <typename I>
+__device__ __forceinline__ int clamp_idx(const I* idx, long u, int V) {
+  long v = static_cast<long>(idx[u]);
+  return static_cast<int>(v < 0 ? 0 : (v >= V ? V - 1 : v));
+}
+
+template <typename T, typename I>
+__global__ __launch_bounds__(256) void embed_relu_fwd_kernel(const T* __restrict__ table, const I* __restrict__ idx,
+                                                             T* __restrict__ out, long U, int V, int D) {
+  const long total = U * D;
+  for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const long u = i / D;
+    const int d = static_cast<int>(i - u * D);
+    const float v = Cvt<T>::load(table, static_cast<long>(clamp_idx(idx, u, V)) * D + d);
+    Cvt<T>::store(out, i, fmaxf(v, 0.f));
+  }
+}
+
+template <typename T, typename I>
+__global__ __launch_bounds__(256) void embed_relu_bwd_kernel(const T* __restrict__ dout, const T* __restrict__ out,
+                                                             const I* __restrict__ idx, float* __restrict__ dtab,
+                                                             long U, int V, int D, int direct) {
+  extern __shared__ float acc[];
+  const int VD = V * D;
+  for (int i = threadIdx.x; i < VD; i += blockDim.x) acc[i] = 0.f;
+  __syncthreads();
+  const long total = U * D;
+  for (long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
+       i += static_cast<long>(gridDim.x) * blockDim.x) {
+    const long u = i / D;
+    const int d = static_cast<int>(i - u * D);
+    if (Cvt<T>::load(out, i) > 0.f) atomicAdd(&acc[clamp_idx(idx, u, V) * D + d], Cvt<T>::load(dout, i));
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < VD; i += blockDim.x) {
+    if (direct) dtab[i] = acc[i];
+    else if (acc[i] != 0.f) atomicAdd(dtab + i, acc[i]);
   }
 }
 
@@ -421,6 +468,53 @@ void table_grad(const void* src, int dt, const int64_t* idx, float* out, long U,
     hipLaunchKernelGGL(table_grad_kernel<float>, dim3(static_cast<unsigned>(blocks)), dim3(256), lds, s,
                        static_cast<const float*>(src), idx, out, U, V, D);
 }
+
+// idt: 0 int64, 1 int32, 2 int16, 3 uint8, 4 int8
+#define AS_EMB_IDX(IDT, BODY)                                      \
+  switch (IDT) {                                                   \
+    case 0: { using I = int64_t; BODY; } break;                    \
+    case 1: { using I = int32_t; BODY; } break;                    \
+    case 2: { using I = int16_t; BODY; } break;                    \
+    case 3: { using I = uint8_t; BODY; } break;                    \
+    default: { using I = int8_t; BODY; } break;                    \
+  }
+
+void embed_relu_fwd(const void* table, int dt, const void* idx, int idt, void* out, long U, int V, int D,
+                    hipStream_t s) {
+  const long n = U * D;
+  if (n == 0) return;
+  const unsigned blocks = static_cast<unsigned>(std::min<long>((n + 255) / 256, 1024));
+  if (dt == DT_BF16) {
+    AS_EMB_IDX(idt, hipLaunchKernelGGL((embed_relu_fwd_kernel<bf16_t, I>), dim3(blocks), dim3(256), 0, s,
+                                       static_cast<const bf16_t*>(table), static_cast<const I*>(idx),
+                                       static_cast<bf16_t*>(out), U, V, D))
+  } else {
+    AS_EMB_IDX(idt, hipLaunchKernelGGL((embed_relu_fwd_kernel<float, I>), dim3(blocks), dim3(256), 0, s,
+                                       static_cast<const float*>(table), static_cast<const I*>(idx),
+                                       static_cast<float*>(out), U, V, D))
+  }
+}
+
+// direct (one workgroup; tiny U * D): dtab written outright; else dtab must be zeroed and takes one atomic per
+// nonzero LDS slot of each workgroup (~4 elements per thread: the loop is latency-bound, not bandwidth-bound)
+void embed_relu_bwd(const void* dout, const void* out, int dt, const void* idx, int idt, float* dtab, long U, int V,
+                    int D, bool direct, hipStream_t s) {
+  const long n = U * D;
+  long blocks = direct ? 1 : std::min<long>(std::max<long>((n + 1023) / 1024, 1), 256);
+  const size_t lds = static_cast<size_t>(V) * D * sizeof(float);
+  if (dt == DT_BF16) {
+    AS_EMB_IDX(idt, hipLaunchKernelGGL((embed_relu_bwd_kernel<bf16_t, I>), dim3(static_cast<unsigned>(blocks)),
+                                       dim3(256), lds, s, static_cast<const bf16_t*>(dout),
+                                       static_cast<const bf16_t*>(out), static_cast<const I*>(idx), dtab, U, V, D,
+                                       direct ? 1 : 0))
+  } else {
+    AS_EMB_IDX(idt, hipLaunchKernelGGL((embed_relu_bwd_kernel<float, I>), dim3(static_cast<unsigned>(blocks)),
+                                       dim3(256), lds, s, static_cast<const float*>(dout),
+                                       static_cast<const float*>(out), static_cast<const I*>(idx), dtab, U, V, D,
+                                       direct ? 1 : 0))
+  }
+}
+#undef AS_EMB_IDX
 
 void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s) {
   if (nrows <= 1024) {

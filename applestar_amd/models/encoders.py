@@ -144,10 +144,10 @@ class ScalarEncoder(nn.Module):
         for name, kind, n_in, n_out, is_ctx, is_base in SCALAR_MODULES:
             m = self.encode_modules[name]
             if kind == 'emb':
-                # a row gather (native LDS-accumulated backward for the small tables, index_add for
-                # last_action_type) - torch's embedding_dense_backward took 0.9 ms for 390 rows of last_delay
-                idx = x[name].long().clamp(max=n_in - 1)
-                e = F.relu(ops.gather_rows(m.weight, idx.reshape(-1)).view(*idx.shape, -1))
+                # row gather + ReLU: one native launch per direction for the small tables (the index in its stored
+                # dtype, LDS-accumulated masked backward); last_action_type's 327 x 128 table gathers with
+                # index_select - torch's embedding_dense_backward took 0.9 ms for 390 rows of last_delay
+                e = ops.embed_relu(m.weight, x[name])
             elif kind == 'bo':
                 e = m(x['beginning_order'], x['bo_location'])
             else:

@@ -13,13 +13,15 @@ transformer's large products stay on hipBLASLt (faster there, docs/OPEN_ISSUES.m
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from . import reference as ref
 from . import _ext
 
-__all__ = ['linear', 'layer_norm', 'conv2d', 'max_pool2x2', 'segment_sum', 'gather_rows', 'gated_residual', 'lnlstm_layer', 'varlen_attention',
+__all__ = ['linear', 'layer_norm', 'conv2d', 'max_pool2x2', 'segment_sum', 'gather_rows', 'embed_relu', 'gated_residual', 'lnlstm_layer', 'varlen_attention',
            'masked_attention', 'scatter_connection', 'sequence_mask', 'native_enabled', 'set_native', 'upsample2x',
            'upsample_conv_out', 'head_sample', 'target_unit_sample']
 
@@ -45,6 +47,7 @@ def _native(t: torch.Tensor):
     return None
 
 
+EMBED_RELU_NATIVE = os.environ.get('APPLESTAR_EMBED_RELU', '1') == '1'
 sequence_mask = ref.sequence_mask
 masked_attention = ref.masked_attention
 
@@ -129,6 +132,17 @@ def segment_sum(x, cu_seqlens, seg):
         return n.segment_sum(x, cu_seqlens, seg)
     S = cu_seqlens.numel() - 1
     return x.float().new_zeros(S, x.shape[-1]).index_add(0, seg, x.float())
+
+
+def embed_relu(table, idx):
+    """relu(table[idx.long().clamp(max=V - 1)]): one native launch per direction for the small tables."""
+    n = _native(table)
+    if n is not None and n.has('embed_relu') and EMBED_RELU_NATIVE:
+        out = n.embed_relu(table, idx)
+        if out is not None:
+            return out
+    i = idx.long().clamp(max=table.shape[0] - 1)
+    return torch.relu(gather_rows(table, i.reshape(-1)).view(*i.shape, -1))
 
 
 def gather_rows(table, idx):

@@ -28,7 +28,7 @@ _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
                 'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp',
                 'location_input', 'value_spatial_proj', 'spatial_embed_pool', 'value_spatial_proj_pool',
-                'rl_loss'}
+                'rl_loss', 'embed_relu'}
 
 
 def has(name: str) -> bool:
@@ -634,6 +634,34 @@ def gather_rows(table, idx):
     if table.shape[0] * table.shape[1] > 16384:
         return table.index_select(0, idx)
     return _GatherRows.apply(table, idx.long().contiguous())
+
+
+class _EmbedRelu(torch.autograd.Function):
+    """relu(table[clamp(idx, 0, V - 1)]) in one launch; backward: the ReLU-masked rows summed per index in LDS
+    (pool_reduce.hip embed_relu_*).  The scalar encoder's small embedding tables."""
+
+    @staticmethod
+    def forward(ctx, table, idx):
+        out = _C.embed_relu_fwd(table.detach().contiguous(), idx)
+        ctx.save_for_backward(idx, out)
+        ctx.V, ctx.dtype = table.shape[0], table.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        idx, out = ctx.saved_tensors
+        return _C.embed_relu_bwd(dout.to(out.dtype).contiguous(), out, idx, ctx.V).to(ctx.dtype), None
+
+
+def embed_relu(table, idx):
+    """relu(table[clamp(idx, max=V - 1)]) as [*idx.shape, D]; None when the table is too large for the LDS
+    accumulation (caller falls back)."""
+    V, D = table.shape
+    if V * D > 16384 or table.dtype not in (torch.float32, torch.bfloat16) or \
+            idx.dtype not in (torch.int64, torch.int32, torch.int16, torch.uint8, torch.int8):
+        return None
+    out = _EmbedRelu.apply(table, idx.contiguous().reshape(-1))
+    return out.view(*idx.shape, D)
 
 
 # ---------------------------------------------------------------------------- dtype-generic conv / GEMM pieces

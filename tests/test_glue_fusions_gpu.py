@@ -155,3 +155,27 @@ def test_gated_resblock_post_add_equals_separate_add(dtype):
     for n in a[3]:
         d = (a[3][n] - b[3][n]).norm().item()
         assert d <= (1e-6 if dtype == torch.float32 else 2e-2) * max(1e-12, b[3][n].norm().item()), n
+
+
+@pytest.mark.parametrize('idt', [torch.int64, torch.uint8, torch.int32])
+@pytest.mark.parametrize('U', [390, 5000])
+def test_embed_relu_matches_torch(idt, U):
+    """ops.embed_relu (one launch: clamp + gather + ReLU; LDS-accumulated masked backward) == the torch form
+    relu(table[idx.long().clamp(max=V - 1)]), forward exactly and the table gradient to fp32 summation order."""
+    from applestar_amd import ops
+    from applestar_amd.ops import native as N
+    N.ensure_loaded()
+    torch.manual_seed(1)
+    V, D = 128, 64
+    t0 = torch.randn(V, D, device=DEV)
+    hi = 255 if idt == torch.uint8 else V + 20           # indices past the table exercise the clamp
+    idx = torch.randint(0, hi, (U,), device=DEV).to(idt)
+    go = torch.randn(U, D, device=DEV)
+    t1 = t0.clone().requires_grad_(True)
+    out = ops.embed_relu(t1, idx)
+    out.backward(go)
+    t2 = t0.clone().requires_grad_(True)
+    ref = torch.relu(t2[idx.long().clamp(max=V - 1)])
+    ref.backward(go)
+    assert torch.equal(out, ref)
+    assert (t1.grad - t2.grad).abs().max().item() <= 1e-5 * max(1.0, t2.grad.abs().max().item())
