@@ -122,11 +122,13 @@ at::Tensor gated_residual_fwd(const at::Tensor& y, const at::Tensor& gt, const a
 // out: the saved block output (its ReLU mask); with xin (the block input) the mask comes from the recomputed
 // pre-activation instead (the forward carried a post-add, so the saved tensor is not the ReLU output)
 std::vector<at::Tensor> gated_residual_bwd(const at::Tensor& dout, const at::Tensor& y, const at::Tensor& gt,
-                                           const at::Tensor& sp, const at::Tensor& out,
+                                           const at::Tensor& sp, const c10::optional<at::Tensor>& out,
                                            const c10::optional<at::Tensor>& xin) {
   check_cuda(dout, "dout");
   TORCH_CHECK(dout.scalar_type() == y.scalar_type(), "gated_residual_bwd: dtype");
-  const at::Tensor& mref = (xin && xin->defined()) ? *xin : out;
+  const bool use_x = xin && xin->defined();
+  TORCH_CHECK(use_x || (out && out->defined()), "gated_residual_bwd: needs the saved output or the block input");
+  const at::Tensor& mref = use_x ? *xin : *out;
   TORCH_CHECK(mref.scalar_type() == y.scalar_type() && mref.sizes() == y.sizes() && mref.is_contiguous() &&
                   dout.sizes() == y.sizes() && dout.is_contiguous() && y.is_contiguous() && gt.is_contiguous(),
               "gated_residual_bwd: operands must match y (dtype, shape, contiguous)");
@@ -134,9 +136,8 @@ std::vector<at::Tensor> gated_residual_bwd(const at::Tensor& dout, const at::Ten
   auto dy = at::empty_like(y), dg = at::empty_like(y), dx = at::empty_like(y);
   const int nblk = as::elementwise_blocks(y.numel());
   auto part = at::empty({nblk}, y.options().dtype(at::kFloat));
-  const bool use_x = xin && xin->defined();
   as::gated_residual_bwd(dout.data_ptr(), y.data_ptr(), gt.data_ptr(), sp.data_ptr<float>(),
-                         use_x ? nullptr : out.data_ptr(), use_x ? xin->data_ptr() : nullptr, dt(y), dy.data_ptr(),
+                         use_x ? nullptr : out->data_ptr(), use_x ? xin->data_ptr() : nullptr, dt(y), dy.data_ptr(),
                          dg.data_ptr(), dx.data_ptr(), part.data_ptr<float>(), y.numel(), nblk, stream());
   return {dy, dg, dx, part.sum().reshape({1})};
 }
