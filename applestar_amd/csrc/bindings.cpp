@@ -1926,6 +1926,45 @@ void multi_copy(const std::vector<at::Tensor>& dsts, const std::vector<at::Tenso
 // dsts[t] (contiguous, fp32/bf16) <- srcs[t] read through spec[9 t .. 9 t + 8] = {size0..3, stride0..3, base}
 // (element units, relative to srcs[t].data_ptr(); strides may be negative).  Every reachable source offset is
 // checked against the source tensor's own extent before anything is launched.
+// Column-block assembly (as::col_sum): pieces[k] = (dst, dst_col, width, [(src, src_col), ...] (1..3)); every
+// tensor fp32 2-D [rows, *] with unit column stride (row pitch = stride(0)), all on one device.
+void col_sum(const std::vector<at::Tensor>& dsts, const std::vector<int64_t>& dcols, const std::vector<int64_t>& widths,
+             const std::vector<std::vector<at::Tensor>>& srcs, const std::vector<std::vector<int64_t>>& scols) {
+  const size_t P = dsts.size();
+  TORCH_CHECK(P > 0 && P <= as::kColMaxP && dcols.size() == P && widths.size() == P && srcs.size() == P &&
+                  scols.size() == P, "col_sum: 1..32 pieces, matching lists");
+  c10::hip::HIPGuard g(dsts[0].device().index());
+  as::ColSumArgs a;
+  a.npieces = static_cast<int>(P);
+  a.rows = dsts[0].size(0);
+  a.block_start[0] = 0;
+  auto check = [&](const at::Tensor& t, int64_t col, int64_t w) {
+    TORCH_CHECK(t.is_cuda() && t.device() == dsts[0].device() && t.scalar_type() == at::kFloat && t.dim() == 2 &&
+                    t.size(0) == a.rows && t.stride(1) == 1 && col >= 0 && w >= 1 && col + w <= t.size(1) &&
+                    t.stride(0) >= t.size(1) && t.stride(0) < (1L << 31),
+                "col_sum: fp32 [rows, *] tensors with unit column stride, column block in range");
+  };
+  for (size_t p = 0; p < P; ++p) {
+    check(dsts[p], dcols[p], widths[p]);
+    TORCH_CHECK(srcs[p].size() >= 1 && srcs[p].size() <= 3 && scols[p].size() == srcs[p].size(),
+                "col_sum: 1..3 sources per piece");
+    a.dst[p] = dsts[p].data_ptr<float>();
+    a.dld[p] = static_cast<int>(dsts[p].stride(0));
+    a.doff[p] = static_cast<int>(dcols[p]);
+    a.width[p] = static_cast<int>(widths[p]);
+    a.nsrc[p] = static_cast<int>(srcs[p].size());
+    for (size_t k = 0; k < srcs[p].size(); ++k) {
+      check(srcs[p][k], scols[p][k], widths[p]);
+      a.src[p][k] = srcs[p][k].data_ptr<float>();
+      a.sld[p][k] = static_cast<int>(srcs[p][k].stride(0));
+      a.soff[p][k] = static_cast<int>(scols[p][k]);
+    }
+    const long n = a.rows * widths[p];
+    a.block_start[p + 1] = a.block_start[p] + static_cast<int>(std::min<long>((n + 1023) / 1024, 256));
+  }
+  as::col_sum(a, stream());
+}
+
 void multi_strided_copy(const std::vector<at::Tensor>& dsts, const std::vector<at::Tensor>& srcs,
                         const std::vector<int64_t>& spec) {
   TORCH_CHECK(dsts.size() == srcs.size() && spec.size() == 9 * dsts.size(), "multi_strided_copy: list sizes");
@@ -2008,6 +2047,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layer_norm_fwd", &layer_norm_fwd);
   m.def("layer_norm_bwd", &layer_norm_bwd);
   m.def("reverse_scan", &reverse_scan);
+  m.def("col_sum", &col_sum);
   m.def("embed_relu_fwd", &embed_relu_fwd);
   m.def("embed_relu_bwd", &embed_relu_bwd);
   m.def("gated_residual_fwd", &gated_residual_fwd, py::arg("y"), py::arg("g"), py::arg("sp"), py::arg("x"),

@@ -311,6 +311,22 @@ struct CopyArgs {                     // passed by value (< 2 KB of kernel argum
 };
 void multi_copy(const CopyArgs& a, hipStream_t s);
 
+// Column-block assembly over a shared row count (fp32): output piece p is rows x width[p] columns of dst[p] (row
+// pitch dld[p], first column doff[p]) = the sum of nsrc[p] (1..3) column blocks of the sources (pitch sld, first
+// column soff).  Forward: the scalar encoder's three concatenations (embedded / context / baseline) of its module
+// outputs in one launch; backward: each module's gradient as the sum of its slices of the three gradients.
+constexpr int kColMaxP = 32;
+struct ColSumArgs {                    // passed by value (~3 KB of kernel arguments)
+  int npieces;
+  long rows;
+  int block_start[kColMaxP + 1];       // prefix sums of the pieces' workgroup counts
+  float* dst[kColMaxP];
+  int dld[kColMaxP], doff[kColMaxP], width[kColMaxP], nsrc[kColMaxP];
+  const float* src[kColMaxP][3];
+  int sld[kColMaxP][3], soff[kColMaxP][3];
+};
+void col_sum(const ColSumArgs& a, hipStream_t s);
+
 // Strided multi-tensor copy (+ dtype conversion) into contiguous destinations: dst[t][i] for the dst index
 // i = ((i0 * size1 + i1) * size2 + i2) * size3 + i3 reads src[t][base + sum_k ik * stride_k] (strides may be
 // negative: flipped conv weights).  Rebuilds every derived weight form (fp32 biases, transposed GEMM weights,

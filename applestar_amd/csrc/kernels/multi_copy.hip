@@ -144,6 +144,28 @@ void multi_copy(const CopyArgs& a, hipStream_t s) {
   if (nblk > 0) hipLaunchKernelGGL(multi_copy_kernel, dim3(nblk), dim3(256), 0, s, a);
 }
 
+__global__ __launch_bounds__(256) void col_sum_kernel(const ColSumArgs a) {
+  const int b = blockIdx.x;
+  int p = 0;
+  while (p + 1 < a.npieces && a.block_start[p + 1] <= b) ++p;
+  const long n = a.rows * a.width[p];
+  const int w = a.width[p], ns = a.nsrc[p];
+  for (long i = static_cast<long>(b - a.block_start[p]) * 256 + threadIdx.x; i < n;
+       i += static_cast<long>(a.block_start[p + 1] - a.block_start[p]) * 256) {
+    const long r = i / w;
+    const int c = static_cast<int>(i - r * w);
+    float v = a.src[p][0][r * a.sld[p][0] + a.soff[p][0] + c];
+    if (ns > 1) v += a.src[p][1][r * a.sld[p][1] + a.soff[p][1] + c];
+    if (ns > 2) v += a.src[p][2][r * a.sld[p][2] + a.soff[p][2] + c];
+    a.dst[p][r * a.dld[p] + a.doff[p] + c] = v;
+  }
+}
+
+void col_sum(const ColSumArgs& a, hipStream_t s) {
+  const int nblk = a.block_start[a.npieces];
+  if (nblk > 0) hipLaunchKernelGGL(col_sum_kernel, dim3(nblk), dim3(256), 0, s, a);
+}
+
 void multi_strided_copy(const StridedCopyArgs& a, hipStream_t s) {
   const int nblk = a.chunk_start[a.ntensors];
   if (nblk > 0) hipLaunchKernelGGL(strided_copy_kernel, dim3(nblk), dim3(256), 0, s, a);

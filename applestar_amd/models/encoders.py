@@ -158,6 +158,13 @@ class ScalarEncoder(nn.Module):
             if is_base:
                 baseline.append(e)
         embedded.append(self.time_encoder(x['time']).to(embedded[0].dtype))
+        n = ops._native(embedded[0])
+        if n is not None and n.has('col_assemble'):
+            # the three concatenations in one launch, each module's gradient summed from its slices in one
+            flags = [(True, c, b) for *_, c, b in SCALAR_MODULES] + [(True, False, False)]
+            out = n.col_assemble(embedded, [[f[k] for f in flags] for k in range(3)])
+            if out is not None:
+                return out
         return torch.cat(embedded, 1), torch.cat(context, 1), torch.cat(baseline, 1)
 
 

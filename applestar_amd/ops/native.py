@@ -28,7 +28,7 @@ _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
                 'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp',
                 'location_input', 'value_spatial_proj', 'spatial_embed_pool', 'value_spatial_proj_pool',
-                'rl_loss', 'embed_relu'}
+                'rl_loss', 'embed_relu', 'col_assemble'}
 
 
 def has(name: str) -> bool:
@@ -636,6 +636,64 @@ def gather_rows(table, idx):
     return _GatherRows.apply(table, idx.long().contiguous())
 
 
+class _ColAssemble(torch.autograd.Function):
+    """Concatenations of one set of [R, w_i] pieces along columns into several outputs (output j takes the pieces
+    flagged in masks[j], in order) in ONE launch (multi_copy.hip col_sum); backward: each piece's gradient as the sum
+    of its column blocks of the output gradients, one launch - instead of a cat per output and an autograd add per
+    extra use of a piece (the scalar encoder: 3 cats + 12 adds)."""
+
+    @staticmethod
+    def forward(ctx, masks, *pieces):
+        R = pieces[0].shape[0]
+        widths = [p.shape[1] for p in pieces]
+        outs, offs = [], []
+        for m in masks:
+            outs.append(pieces[0].new_empty(R, sum(w for w, f in zip(widths, m) if f)))
+            o, acc = [], 0
+            for w, f in zip(widths, m):
+                o.append(acc if f else -1)
+                acc += w if f else 0
+            offs.append(o)
+        dsts, dcols, ws, srcs, scols = [], [], [], [], []
+        for j, o in enumerate(offs):
+            for i, off in enumerate(o):
+                if off >= 0:
+                    dsts.append(outs[j]), dcols.append(off), ws.append(widths[i])
+                    srcs.append([pieces[i]]), scols.append([0])
+        for k in range(0, len(dsts), 32):
+            _C.col_sum(dsts[k:k + 32], dcols[k:k + 32], ws[k:k + 32], srcs[k:k + 32], scols[k:k + 32])
+        ctx.offs, ctx.widths = offs, widths
+        ctx.set_materialize_grads(False)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *douts):
+        douts = [None if d is None else d.float().contiguous() for d in douts]
+        R = next(d.shape[0] for d in douts if d is not None)
+        grads, dsts, dcols, ws, srcs, scols = [], [], [], [], [], []
+        for i, w in enumerate(ctx.widths):
+            ss = [(douts[j], ctx.offs[j][i]) for j in range(len(douts)) if douts[j] is not None and ctx.offs[j][i] >= 0]
+            if not ss:
+                grads.append(None)
+                continue
+            g = douts[0].new_empty(R, w) if douts[0] is not None else ss[0][0].new_empty(R, w)
+            grads.append(g)
+            dsts.append(g), dcols.append(0), ws.append(w)
+            srcs.append([t for t, _ in ss]), scols.append([c for _, c in ss])
+        for k in range(0, len(dsts), 32):
+            _C.col_sum(dsts[k:k + 32], dcols[k:k + 32], ws[k:k + 32], srcs[k:k + 32], scols[k:k + 32])
+        return (None, *grads)
+
+
+def col_assemble(pieces, masks):
+    """tuple of outputs, output j = cat([p for p, f in zip(pieces, masks[j]) if f], 1); None when not covered."""
+    if not COL_ASSEMBLE or not pieces or \
+            any(p.dtype != torch.float32 or p.dim() != 2 or not p.is_cuda or p.stride(1) != 1 for p in pieces) or \
+            len({p.shape[0] for p in pieces}) != 1:
+        return None
+    return _ColAssemble.apply(tuple(tuple(bool(f) for f in m) for m in masks), *pieces)
+
+
 class _EmbedRelu(torch.autograd.Function):
     """relu(table[clamp(idx, 0, V - 1)]) in one launch; backward: the ReLU-masked rows summed per index in LDS
     (pool_reduce.hip embed_relu_*).  The scalar encoder's small embedding tables."""
@@ -1028,6 +1086,8 @@ class SkipLink:
 SKIP_LINK = os.environ.get('APPLESTAR_SKIP_LINK', '1') == '1'    # A/B switch
 # the location head's skip-map adds in the gated residual blocks' output pass (APPLESTAR_POST_ADD=0: separate adds)
 POST_ADD = os.environ.get('APPLESTAR_POST_ADD', '1') == '1'
+# the scalar encoder's three concatenations in one launch (APPLESTAR_COL_ASSEMBLE=0: torch.cat + autograd adds)
+COL_ASSEMBLE = os.environ.get('APPLESTAR_COL_ASSEMBLE', '1') == '1'
 
 
 class _ResBlock(torch.autograd.Function):

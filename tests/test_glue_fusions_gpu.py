@@ -179,3 +179,29 @@ def test_embed_relu_matches_torch(idt, U):
     ref.backward(go)
     assert torch.equal(out, ref)
     assert (t1.grad - t2.grad).abs().max().item() <= 1e-5 * max(1.0, t2.grad.abs().max().item())
+
+
+def test_col_assemble_matches_cat_and_autograd():
+    """native col_assemble (the scalar encoder's three concatenations in one launch; each piece's gradient summed
+    from its slices in one) == torch.cat per output with autograd's accumulation, exactly."""
+    from applestar_amd.ops import native as N
+    N.ensure_loaded()
+    torch.manual_seed(2)
+    R = 390
+    widths = [64, 32, 32, 128, 128, 64, 32, 128, 128, 64, 64, 64, 64, 32]
+    masks = [[True] * len(widths), [i % 3 == 0 for i in range(len(widths))], [i % 2 == 1 for i in range(len(widths))]]
+    base = [torch.randn(R, w, device=DEV) for w in widths]
+    gos = [torch.randn(R, sum(w for w, f in zip(widths, m) if f), device=DEV) for m in masks]
+    res = []
+    for fused in (True, False):
+        ps = [b.clone().requires_grad_(True) for b in base]
+        if fused:
+            outs = N.col_assemble(ps, masks)
+        else:
+            outs = [torch.cat([p for p, f in zip(ps, m) if f], 1) for m in masks]
+        sum((o * g).sum() for o, g in zip(outs, gos)).backward()
+        res.append(([o.detach() for o in outs], [p.grad for p in ps]))
+    for a, b in zip(res[0][0], res[1][0]):
+        assert torch.equal(a, b)
+    for a, b in zip(res[0][1], res[1][1]):
+        assert (a - b).abs().max().item() <= 1e-6 * max(1.0, b.abs().max().item())
