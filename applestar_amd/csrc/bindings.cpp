@@ -824,6 +824,29 @@ at::Tensor embed_relu_bwd(const at::Tensor& dout, const at::Tensor& out, const a
   return dtab;
 }
 
+// (valid bool [B, N], flat int64 [total], seg int64 [total], cu int32 [B + 1]) of the entity packing
+std::vector<at::Tensor> entity_pack(const at::Tensor& num, int64_t N, int64_t total) {
+  check_cuda(num, "entity_num");
+  TORCH_CHECK(num.dim() == 1 && num.is_contiguous() && (num.scalar_type() == at::kLong || num.scalar_type() == at::kInt),
+              "entity_pack: entity_num int64 / int32 [B]");
+  TORCH_CHECK(N > 0 && total >= 0 && num.size(0) * N < (1L << 31), "entity_pack: sizes");
+  c10::hip::HIPGuard g(num.device().index());
+  const int64_t B = num.size(0);
+  auto o = num.options();
+  auto valid = at::empty({B, N}, o.dtype(at::kBool));
+  auto flat = at::empty({total}, o.dtype(at::kLong));
+  auto seg = at::empty({total}, o.dtype(at::kLong));
+  auto cu = at::empty({B + 1}, o.dtype(at::kInt));
+  if (B == 0) {
+    cu.zero_();
+    return {valid, flat, seg, cu};
+  }
+  as::entity_pack(num.data_ptr(), num.scalar_type() == at::kLong, static_cast<int>(B), static_cast<int>(N), total,
+                  valid.data_ptr<bool>(), flat.data_ptr<int64_t>(), seg.data_ptr<int64_t>(), cu.data_ptr<int>(),
+                  stream());
+  return {valid, flat, seg, cu};
+}
+
 // ---------------------------------------------------------------- conv3x3 implicit GEMM (NHWC bf16)
 at::Tensor conv3x3_fwd(const at::Tensor& x, const at::Tensor& wk, const c10::optional<at::Tensor>& bias,
                        const c10::optional<at::Tensor>& res, int64_t act) {
@@ -2048,6 +2071,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layer_norm_bwd", &layer_norm_bwd);
   m.def("reverse_scan", &reverse_scan);
   m.def("col_sum", &col_sum);
+  m.def("entity_pack", &entity_pack);
   m.def("embed_relu_fwd", &embed_relu_fwd);
   m.def("embed_relu_bwd", &embed_relu_bwd);
   m.def("gated_residual_fwd", &gated_residual_fwd, py::arg("y"), py::arg("g"), py::arg("sp"), py::arg("x"),

@@ -34,6 +34,9 @@ void layer_norm_bwd(const void* dy, int dy_dt, const void* xin, int xin_dt, cons
                     const float* w, const float* mean, const float* rstd, void* dx, int dx_dt,
                     float* dw_part, float* db_part, long rows, int cols, int act, int nblk, hipStream_t s);
 void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s);
+// entity packing tables (valid [B][N], packed -> padded row flat[total], segment seg[total], offsets cu[B + 1])
+void entity_pack(const void* num, bool num64, int B, int N, long total, bool* valid, int64_t* flat, int64_t* seg,
+                 int* cu, hipStream_t s);
 // scalar-encoder embedding + ReLU (idt: 0 int64, 1 int32, 2 int16, 3 uint8, 4 int8; index clamped to [0, V))
 void embed_relu_fwd(const void* table, int dt, const void* idx, int idt, void* out, long U, int V, int D,
                     hipStream_t s);

@@ -239,6 +239,42 @@ __global__ __launch_bounds__(256) void embed_relu_bwd_kernel(const T* __restrict
   }
 }
 
+// Entity packing tables in one launch (one workgroup per observation b; len_b = min(num[b], N) clamped at 0):
+//   valid[b][j] = j < len_b;  cu[b] = sum_{b' < b} len_b' (cu[B] = total);  for the packed rows k = cu[b] + j:
+//   flat[k] = b N + j (packed -> padded row), seg[k] = b.  Rows past `total` (the host's count) are not written.
+// Replaces sequence_mask + nonzero_static + clamp + cumsum + pad + repeat_interleave (~8 launches, 0.2 ms).
+template <typename NT>
+__global__ __launch_bounds__(256) void entity_pack_kernel(const NT* __restrict__ num, int B, int N, long total,
+                                                          bool* __restrict__ valid, int64_t* __restrict__ flat,
+                                                          int64_t* __restrict__ seg, int* __restrict__ cu) {
+  const int b = blockIdx.x;
+  __shared__ long base_s;
+  auto len_of = [&](int i) {
+    const long v = static_cast<long>(num[i]);
+    return v < 0 ? 0L : (v > N ? static_cast<long>(N) : v);
+  };
+  if (threadIdx.x < 64) {
+    long acc = 0;
+    for (int i = threadIdx.x; i < b; i += 64) acc += len_of(i);
+    acc = wave_sum_long(acc);
+    if (threadIdx.x == 0) {
+      base_s = acc;
+      cu[b] = static_cast<int>(acc);
+      if (b == B - 1) cu[B] = static_cast<int>(acc + len_of(b));
+    }
+  }
+  __syncthreads();
+  const long base = base_s, len = len_of(b);
+  for (int j = threadIdx.x; j < N; j += 256) {
+    valid[static_cast<long>(b) * N + j] = j < len;
+    const long k = base + j;
+    if (j < len && k < total) {
+      flat[k] = static_cast<int64_t>(b) * N + j;
+      seg[k] = b;
+    }
+  }
+}
+
 // OutT = bf16_t fuses the cast of the reduced weight gradient to the bf16 compute parameter dtype
 // (one launch instead of reduce + cast, wgrad callers under master weights)
 template <typename OutT>
@@ -515,6 +551,17 @@ void embed_relu_bwd(const void* dout, const void* out, int dt, const void* idx, 
   }
 }
 #undef AS_EMB_IDX
+
+void entity_pack(const void* num, bool num64, int B, int N, long total, bool* valid, int64_t* flat, int64_t* seg,
+                 int* cu, hipStream_t s) {
+  if (B == 0) return;
+  if (num64)
+    hipLaunchKernelGGL(entity_pack_kernel<int64_t>, dim3(B), dim3(256), 0, s, static_cast<const int64_t*>(num), B, N,
+                       total, valid, flat, seg, cu);
+  else
+    hipLaunchKernelGGL(entity_pack_kernel<int>, dim3(B), dim3(256), 0, s, static_cast<const int*>(num), B, N, total,
+                       valid, flat, seg, cu);
+}
 
 void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s) {
   if (nrows <= 1024) {

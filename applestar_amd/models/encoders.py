@@ -235,17 +235,25 @@ class EntityEncoder(nn.Module):
         ``PAD_SEGMENTS * N`` at least the real count) packs to that fixed row count instead, so the
         step's shapes do not depend on the data (HIP-graph capture of the learner step)."""
         B, N = entity_info['unit_type'].shape
-        valid = ops.sequence_mask(entity_num, N)                     # [B,N]
-        if STATIC_SHAPES and valid.is_cuda:
-            return self._forward_static(entity_info, entity_num, valid)
-        if entity_pad is not None and not self.reduce_type.startswith('attention_pool'):
-            return self._forward_padded(entity_info, entity_num, valid, int(entity_pad))
-        if entity_total is not None and valid.is_cuda:
-            flat_index = torch.nonzero_static(valid.reshape(-1), size=int(entity_total)).squeeze(1)
+        padded = entity_pad is not None and not self.reduce_type.startswith('attention_pool')
+        n = ops._native(entity_num) if entity_total is not None and not padded and \
+            not (STATIC_SHAPES and entity_num.is_cuda) else None
+        if n is not None and n.has('entity_pack'):
+            # valid / packed -> padded rows / segments / offsets in one launch
+            valid, flat_index, seg, cu = n.entity_pack(entity_num, N, int(entity_total))
         else:
-            flat_index = valid.reshape(-1).nonzero().squeeze(1)     # packed row -> padded row
-        lens = entity_num.clamp(max=N).to(torch.int32)
-        cu = F.pad(torch.cumsum(lens, 0, dtype=torch.int32), (1, 0))
+            valid = ops.sequence_mask(entity_num, N)                     # [B,N]
+            if STATIC_SHAPES and valid.is_cuda:
+                return self._forward_static(entity_info, entity_num, valid)
+            if padded:
+                return self._forward_padded(entity_info, entity_num, valid, int(entity_pad))
+            seg = None
+            if entity_total is not None and valid.is_cuda:
+                flat_index = torch.nonzero_static(valid.reshape(-1), size=int(entity_total)).squeeze(1)
+            else:
+                flat_index = valid.reshape(-1).nonzero().squeeze(1)     # packed row -> padded row
+            lens = entity_num.clamp(max=N).to(torch.int32)
+            cu = F.pad(torch.cumsum(lens, 0, dtype=torch.int32), (1, 0))
         x = self.embed(entity_info, flat_index)                      # [T,256]
         # the reference's inplace ReLU (entity_encoder.py:84), which also rectifies x used by the mean below,
         # applied by the transformer's closing LayerNorm kernel (no separate pass / mask pass over [T,256])
@@ -258,7 +266,8 @@ class EntityEncoder(nn.Module):
             pooled = self.attention_pool(xp, num=entity_num, mask=valid)
             return entity_embeddings, self.embed_fc(pooled.to(x.dtype)), valid
         # masked mean of relu(transformer output) over real entities (entity_encoder.py:85-87)
-        seg = torch.repeat_interleave(torch.arange(B, device=x.device), lens.long(), output_size=x.shape[0])
+        if seg is None:
+            seg = torch.repeat_interleave(torch.arange(B, device=x.device), lens.long(), output_size=x.shape[0])
         summed = ops.segment_sum(x, cu, seg).to(x.dtype)
         if self.reduce_type == 'constant':
             mean = summed / 512

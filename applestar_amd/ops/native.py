@@ -28,7 +28,7 @@ _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
                 'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp',
                 'location_input', 'value_spatial_proj', 'spatial_embed_pool', 'value_spatial_proj_pool',
-                'rl_loss', 'embed_relu', 'col_assemble'}
+                'rl_loss', 'embed_relu', 'col_assemble', 'entity_pack'}
 
 
 def has(name: str) -> bool:
@@ -634,6 +634,15 @@ def gather_rows(table, idx):
     if table.shape[0] * table.shape[1] > 16384:
         return table.index_select(0, idx)
     return _GatherRows.apply(table, idx.long().contiguous())
+
+
+def entity_pack(entity_num, N: int, total: int):
+    """(valid [B, N] bool, flat [total] int64, seg [total] int64, cu [B + 1] int32) of the packed entity rows in one
+    launch (pool_reduce.hip entity_pack_kernel)."""
+    num = entity_num.reshape(-1)
+    if num.dtype not in (torch.int64, torch.int32):
+        num = num.long()
+    return tuple(_C.entity_pack(num.contiguous(), int(N), int(total)))
 
 
 class _ColAssemble(torch.autograd.Function):

@@ -205,3 +205,22 @@ def test_col_assemble_matches_cat_and_autograd():
         assert torch.equal(a, b)
     for a, b in zip(res[0][1], res[1][1]):
         assert (a - b).abs().max().item() <= 1e-6 * max(1.0, b.abs().max().item())
+
+
+@pytest.mark.parametrize('num_dtype', [torch.int64, torch.int32])
+def test_entity_pack_matches_torch(num_dtype):
+    """native entity_pack (one launch) == sequence_mask / nonzero / cumsum / repeat_interleave."""
+    from applestar_amd.ops import native as N
+    N.ensure_loaded()
+    torch.manual_seed(4)
+    B, Nn = 390, 512
+    num = torch.randint(0, 600, (B,), device=DEV).to(num_dtype)     # some past N: clamped
+    num[3] = 0
+    lens = num.long().clamp(max=Nn)
+    total = int(lens.sum())
+    valid, flat, seg, cu = N.entity_pack(num, Nn, total)
+    rv = torch.arange(Nn, device=DEV)[None, :] < lens[:, None]
+    assert torch.equal(valid, rv)
+    assert torch.equal(flat, rv.reshape(-1).nonzero().squeeze(1))
+    assert torch.equal(seg, torch.repeat_interleave(torch.arange(B, device=DEV), lens))
+    assert torch.equal(cu, torch.nn.functional.pad(torch.cumsum(lens, 0).to(torch.int32), (1, 0)))
