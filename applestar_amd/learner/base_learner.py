@@ -44,7 +44,7 @@ class BaseLearner:
         self.rank = pdist.get_rank()
         self.world_size = pdist.get_world_size()
         use_cuda = bool(lc.use_cuda) and torch.cuda.is_available()
-        self.device = torch.device(f'cuda:{pdist.get_local_rank()}' if use_cuda else 'cpu')
+        self.device = torch.device(f'cuda:{pdist.local_device_index()}' if use_cuda else 'cpu')
         if use_cuda:
             torch.cuda.set_device(self.device)
         self.experiment_name = self.cfg.common.experiment_name

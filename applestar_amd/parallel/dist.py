@@ -37,6 +37,11 @@ def get_local_rank() -> int:
     return int(os.environ.get('LOCAL_RANK', get_rank() % max(torch.cuda.device_count(), 1)))
 
 
+def local_device_index() -> int:
+    """This rank's GPU: LOCAL_RANK modulo the visible devices (several gloo ranks can share one GPU)."""
+    return get_local_rank() % max(torch.cuda.device_count(), 1)
+
+
 def init(backend: Optional[str] = None, init_method: Optional[str] = None, rank: Optional[int] = None,
          world_size: Optional[int] = None, timeout_s: int = 1800) -> tuple:
     """Initialise the default process group if the environment asks for one.  Returns (rank, world)."""
