@@ -50,6 +50,15 @@ def _to(tree, device, non_blocking=True):
     return tree
 
 
+
+def _refresh_forms(model):
+    """New weights are in ``model``'s parameters: rebuild its cached inference weight forms in place (the HIP
+    graphs that captured them read the same buffers)."""
+    reg = getattr(model, '_inference_forms', None)
+    if reg is not None:
+        with torch.no_grad():
+            reg.refresh()
+
 class InferenceClient:
     """Worker-side handle: ``infer(model_input) -> per-sample output`` (blocking).  The connection is bound to
     its route on the server side (``InferenceServer.add_connection(conn, route)``), so a request is the bare
@@ -121,6 +130,11 @@ class InferenceServer:
     # ------------------------------------------------------------------ models
     def set_model(self, player_id: str, model: torch.nn.Module, teacher: bool = False):
         model = model.to(self.device).eval()
+        if self.device.type == 'cuda' and getattr(model, '_inference_forms', None) is None:
+            # bf16 / transposed weight forms cast once per weight version, not inside every graph replay
+            from ..ops import native
+            if native.ensure_loaded() is not None:
+                model._inference_forms = native.attach_inference_forms(model)
         with self._lock:
             (self.teachers if teacher else self.models)[player_id] = model
             self._graphed = {k: v for k, v in self._graphed.items() if player_id not in k[0][::2]}
@@ -137,6 +151,7 @@ class InferenceServer:
                 for k, v in state_dict.items():
                     if k in own and own[k].shape == v.shape:
                         own[k].copy_(v, non_blocking=True)
+            _refresh_forms(m)
             if not teacher:
                 self.model_iter[player_id] = int(last_iter)
 
@@ -161,6 +176,7 @@ class InferenceServer:
                 off += n
             with torch.no_grad():
                 _copy_many(dsts, srcs)
+            _refresh_forms(m)
             self.model_iter[player_id] = int(last_iter)
 
     def attach_model_slot(self, player_id: str, shm_name: str) -> bool:
@@ -189,6 +205,7 @@ class InferenceServer:
         for pid, sub in list(getattr(self, '_subscribers', {}).items()):
             with self._lock:
                 if sub.poll():
+                    _refresh_forms(self.models[pid])
                     self.model_iter[pid] = sub.last_iter
                     out[pid] = sub.last_iter
         return out

@@ -173,8 +173,9 @@ class _LNLSTMRecurrence(torch.autograd.Function):
     """Recurrent part of an LN-LSTM layer: xp [T,B,4H] (already LN_i(x W_ih^T)) -> h [T,B,H]."""
 
     @staticmethod
-    def forward(ctx, xp, h0, c0, w_hh, lnh_w, lnh_b, lnc_w, lnc_b, w_dtype):
-        wq = w_hh.detach().to(w_dtype)
+    def forward(ctx, xp, h0, c0, w_hh, lnh_w, lnh_b, lnc_w, lnc_b, w_dtype, need_bwd=True):
+        # W_hh in the recurrence's dtype, for the backward only (inference skips the cast)
+        wq = w_hh.detach().to(w_dtype) if need_bwd else w_hh.detach()
         wT = _wT(w_hh, w_dtype)          # a derived form: transposed once per optimizer step, not per layer call
         out, hT, cT, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c = _C.lnlstm_fwd(
             xp.contiguous(), h0.contiguous(), c0.contiguous(), wT, lnh_w.detach(), lnh_b.detach(),
@@ -200,7 +201,7 @@ class _LNLSTMRecurrence(torch.autograd.Function):
         # were ~17 launches at ~19 us per LSTM backward, r2dl)
         dlnh_w, dlnh_b = _C.ln_affine_grads(dgates.contiguous(), xhat_h.contiguous()).unbind(0)
         dlnc_w, dlnc_b = _C.ln_affine_grads(dc_ln.contiguous(), xhat_c.contiguous()).unbind(0)
-        return dgates, dh0, dc0, dw, dlnh_w, dlnh_b, dlnc_w, dlnc_b, None
+        return dgates, dh0, dc0, dw, dlnh_w, dlnh_b, dlnc_w, dlnc_b, None, None
 
 
 _ZEROS = {}
@@ -226,11 +227,13 @@ def lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b
     x2 = x.reshape(T * B, -1)
     # bf16 input projection through linear(): its dW takes the split-R MFMA kernel, not a library GEMM that
     # tiles only the 4H x I output over T*B = 24576 rows (the selected-units head's LSTM)
-    xg = linear(x2, w_ih) if x2.dtype == w_ih.dtype and x2.dtype in (torch.bfloat16, torch.float32) else \
-        torch.nn.functional.linear(x2, w_ih)
+    xg = linear(x2, w_ih) if x2.dtype in (torch.bfloat16, torch.float32) and \
+        (x2.dtype == w_ih.dtype or torch.is_autocast_enabled()) else torch.nn.functional.linear(x2, w_ih)
     xp = layer_norm(xg, lni_w, lni_b, out_dtype=torch.float32).view(T, B, 4 * H)
     w_dtype = torch.bfloat16 if torch.is_autocast_enabled() else torch.float32
-    out, hT, cT = _LNLSTMRecurrence.apply(xp, h0.float(), c0.float(), w_hh, lnh_w, lnh_b, lnc_w, lnc_b, w_dtype)
+    need_bwd = torch.is_grad_enabled() and any(t.requires_grad for t in (xp, h0, c0, w_hh, lnh_w, lnh_b, lnc_w, lnc_b))
+    out, hT, cT = _LNLSTMRecurrence.apply(xp, h0.float(), c0.float(), w_hh, lnh_w, lnh_b, lnc_w, lnc_b, w_dtype,
+                                          need_bwd)
     return out, hT, cT
 
 
@@ -1177,8 +1180,8 @@ def resblock(x, w1, b1, w2, b2):
     if not lowp or not _C.conv3x3_supported(C, C):
         return None
     xl = nhwc(x.to(torch.bfloat16))
-    w1l = w1 if w1.dtype == torch.bfloat16 else _CastWeight.apply(w1)
-    w2l = w2 if w2.dtype == torch.bfloat16 else _CastWeight.apply(w2)
+    w1l = w1 if w1.dtype == torch.bfloat16 else _bf16w(w1)
+    w2l = w2 if w2.dtype == torch.bfloat16 else _bf16w(w2)
     with torch.autocast('cuda', enabled=False):
         return from_nhwc(_ResBlock.apply(xl, w1l, b1, w2l, b2))
 
@@ -1321,11 +1324,32 @@ def gated_resblock(x, conv1, conv2, gates, sp, post=None):
         return None
     # conv / GEMM weights and the GEMM biases in bf16 (the per-op path's casts); the conv biases stay as
     # given: the conv epilogue adds them in fp32
-    ws = [t if (t.dtype == torch.bfloat16 or i in (1, 3)) else _CastWeight.apply(t) for i, t in enumerate(ws)]
+    ws = [t if (t.dtype == torch.bfloat16 or i in (1, 3)) else _bf16w(t) for i, t in enumerate(ws)]
     xl = nhwc(x.to(torch.bfloat16))
     pl = None if post is None else nhwc(post.to(torch.bfloat16))
     with torch.autocast('cuda', enabled=False):
         return from_nhwc(_GatedResBlock.apply(xl, sp.float(), pl, *ws))
+
+
+def _bf16w(w):
+    """bf16 compute form of an fp32 weight / bias (autocast semantics).  With autograd: a _CastWeight node (fp32
+    gradient).  Without (actor inference, frozen teachers): a derived form of the parameter, cast once and
+    reused until its weights change - the inference server tags its models' parameters
+    (:func:`attach_inference_forms`) and refreshes the forms in place after every weight update, so the HIP graphs
+    that captured a form's buffer read the new values; untagged tensors are cast per call."""
+    if torch.is_grad_enabled() and w.requires_grad:
+        return _CastWeight.apply(w)
+    return _derived(w, 'bf16', lambda: (w.detach().to(torch.bfloat16).contiguous(), _view_spec(w.detach(), w)
+                                        if w.is_contiguous() else None))
+
+
+def attach_inference_forms(model):
+    """Tag ``model``'s parameters with one DerivedWeights registry (bf16 / fp32 / transposed forms cached across
+    inference calls); returns it - call ``.refresh()`` after loading new weights into the model."""
+    reg = DerivedWeights()
+    for p in model.parameters():
+        p._derived_forms = reg
+    return reg
 
 
 class _CastWeight(torch.autograd.Function):
@@ -1358,7 +1382,7 @@ def conv2d(x, w, b, stride, padding, act, residual):
     if kh == 3 and kw == 3 and padding == 1 and lowp and _C.conv3x3_supported(cin, cout) \
             and _C.conv3x3_supported(cout, cin):
         xl = nhwc(x.to(torch.bfloat16))
-        wl = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
+        wl = w if w.dtype == torch.bfloat16 else _bf16w(w)
         rl = nhwc(residual.to(torch.bfloat16)) if residual is not None else None
         with torch.autocast('cuda', enabled=False):
             return from_nhwc(_Conv3x3.apply(xl, wl, b, rl, act))
@@ -1509,8 +1533,8 @@ def location_input(pf, skip, w, b):
             or cout != C or not _C.loc_in_supported(C, cin - C) or pf.numel() != B * (cin - C) * H * W:
         return None
     w2 = w.view(cout, cin)
-    w2 = w2 if w2.dtype == torch.bfloat16 else _CastWeight.apply(w2)
-    bb = b if b.dtype == torch.bfloat16 else _CastWeight.apply(b)
+    w2 = w2 if w2.dtype == torch.bfloat16 else _bf16w(w2)
+    bb = b if b.dtype == torch.bfloat16 else _bf16w(b)
     with torch.autocast('cuda', enabled=False):
         y = _LocationInput.apply(pf.to(torch.bfloat16).reshape(B, -1).contiguous(), nhwc(skip).view(-1, C), w2, bb,
                                  H * W)
@@ -1909,8 +1933,8 @@ def linear(x, w, b=None, act=None, grad_link=None):
         # instead made both the dX GEMM and the native dW pick slow tiles: +5 ms, r2ap)
         with torch.autocast('cuda', enabled=False):
             xb = x.reshape(R, K).to(torch.bfloat16)
-            wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
-            bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
+            wb = w if w.dtype == torch.bfloat16 else _bf16w(w)
+            bb = None if b is None else (b if b.dtype == torch.bfloat16 else _bf16w(b))
             y = _LinearSplitK.apply(xb, wb, bb, act == 'relu')
         return y.view(*x.shape[:-1], N)
     if lowp and _small_native_ok(x, R, N, K, act) and (R < _WGRAD_MIN_ROWS or N % 8 or K % 8 or act == 'sigmoid'):
@@ -1918,15 +1942,15 @@ def linear(x, w, b=None, act=None, grad_link=None):
         ensure_loaded()
         with torch.autocast('cuda', enabled=False):
             xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
-            wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
+            wb = w if w.dtype == torch.bfloat16 else _bf16w(w)
             y = _SmallLinearNative.apply(xb, wb, b, act)
         return y.view(*x.shape[:-1], N)
     if lowp and x.is_cuda and act in (None, 'relu') and R < _SMALL_LINEAR_ROWS and \
             (R < _WGRAD_MIN_ROWS or N % 8 or K % 8):
         with torch.autocast('cuda', enabled=False):
             xb = x.reshape(R, K).to(torch.bfloat16)
-            wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
-            bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
+            wb = w if w.dtype == torch.bfloat16 else _bf16w(w)
+            bb = None if b is None else (b if b.dtype == torch.bfloat16 else _bf16w(b))
             y = _SmallLinear.apply(xb, wb, bb, act == 'relu')
         return y.view(*x.shape[:-1], N)
     if not lowp and x.dtype == torch.float32 and w.dtype == torch.float32 and x.is_cuda and \
@@ -1969,8 +1993,8 @@ def linear(x, w, b=None, act=None, grad_link=None):
         grad_link.armed, link, xb = x, grad_link, x
     else:
         xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
-    wb = w if w.dtype == torch.bfloat16 else _CastWeight.apply(w)
-    bb = None if b is None else (b if b.dtype == torch.bfloat16 else _CastWeight.apply(b))
+    wb = w if w.dtype == torch.bfloat16 else _bf16w(w)
+    bb = None if b is None else (b if b.dtype == torch.bfloat16 else _bf16w(b))
     with torch.autocast('cuda', enabled=False):
         y = _Linear.apply(xb, wb, bb, act == 'relu', link)
     return y.view(*x.shape[:-1], N)

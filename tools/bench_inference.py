@@ -25,6 +25,10 @@ def main():
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     m = Model({'agent': {'extra_units': True}}).to(dev).eval().to(memory_format=torch.channels_last)
+    if os.environ.get('APPLESTAR_INFERENCE_FORMS', '1') == '1':
+        from applestar_amd.ops import native
+        native.ensure_loaded()
+        native.attach_inference_forms(m)       # as the inference server does (actor/inference.py set_model)
     for B in [int(x) for x in args.batches.split(',')]:
         g = torch.Generator().manual_seed(B)
         en = torch.randint(args.entities // 2, args.entities, (B,), generator=g)

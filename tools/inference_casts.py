@@ -34,6 +34,10 @@ def main():
     from applestar_amd.models import encoders, model as model_mod
     dev = torch.device('cuda', 0)
     m = Model({'agent': {'extra_units': True}}).to(dev).eval().to(memory_format=torch.channels_last)
+    if os.environ.get('APPLESTAR_INFERENCE_FORMS', '1') == '1':
+        from applestar_amd.ops import native
+        native.ensure_loaded()
+        native.attach_inference_forms(m)       # as the inference server does (actor/inference.py set_model)
     B = args.batch
     g = torch.Generator().manual_seed(B)
     en = torch.randint(150, 300, (B,), generator=g)
