@@ -1324,7 +1324,9 @@ def gated_resblock(x, conv1, conv2, gates, sp, post=None):
         return None
     # conv / GEMM weights and the GEMM biases in bf16 (the per-op path's casts); the conv biases stay as
     # given: the conv epilogue adds them in fp32
-    ws = [t if (t.dtype == torch.bfloat16 or i in (1, 3)) else _bf16w(t) for i, t in enumerate(ws)]
+    # (with the one-launch bf16 gate chain the gate biases stay fp32 too: it reads them as fp32)
+    keep = {1, 3} | ({5, 7, 9, 11} if GATE_CHAIN and C == 128 else set())
+    ws = [t if (t.dtype == torch.bfloat16 or i in keep) else _bf16w(t) for i, t in enumerate(ws)]
     xl = nhwc(x.to(torch.bfloat16))
     pl = None if post is None else nhwc(post.to(torch.bfloat16))
     with torch.autocast('cuda', enabled=False):
@@ -1620,9 +1622,9 @@ class _Linear(torch.autograd.Function):
             # (gemm_bf16.hip), bias + ReLU in its epilogue
             y = _C.gemm_bf16(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None, 1 if relu else 0)
         elif relu and b is not None:
-            y = torch._addmm_activation(b, x2, w.t(), use_gelu=False)
+            y = torch._addmm_activation(b.to(x2.dtype), x2, w.t(), use_gelu=False)
         else:
-            y = torch.nn.functional.linear(x2, w, b)
+            y = torch.nn.functional.linear(x2, w, None if b is None else b.to(x2.dtype))
             if relu:
                 y = torch.relu(y)
         ctx.save_for_backward(x2, w, y if relu else None)
@@ -1994,9 +1996,10 @@ def linear(x, w, b=None, act=None, grad_link=None):
     else:
         xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
     wb = w if w.dtype == torch.bfloat16 else _bf16w(w)
-    bb = None if b is None else (b if b.dtype == torch.bfloat16 else _bf16w(b))
+    # the bias as given: the native epilogues add it in fp32 (an fp32 parameter is used as is - no fp32 -> bf16
+    # -> fp32 round trip of casts); _Linear's library fallbacks cast it to the operand dtype themselves
     with torch.autocast('cuda', enabled=False):
-        y = _Linear.apply(xb, wb, bb, act == 'relu', link)
+        y = _Linear.apply(xb, wb, b, act == 'relu', link)
     return y.view(*x.shape[:-1], N)
 
 
