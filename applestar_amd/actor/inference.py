@@ -23,6 +23,7 @@ MI355X design:
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
 from collections import defaultdict, deque
@@ -117,6 +118,13 @@ class InferenceServer:
         self.max_wait = max_wait_ms / 1000.0
         self.max_busy_wait = 0.05       # cap on collecting behind an in-flight batch (seconds)
         self.amp_dtype = amp_dtype if self.device.type == 'cuda' else None
+        # the server's device work (H2D, graph replays, D2H) on a HIGH-priority stream: on a GPU shared with the
+        # learner, the dispatcher starts the actors' small inference kernels ahead of the learner's queued
+        # workgroups, so the agent-step round trip does not wait behind a learner step
+        # (APPLESTAR_INFERENCE_STREAM_PRIORITY=0: the default stream)
+        prio = int(os.environ.get('APPLESTAR_INFERENCE_STREAM_PRIORITY', '-1'))
+        self._stream = torch.cuda.Stream(device=self.device, priority=prio) \
+            if self.device.type == 'cuda' and prio != 0 else None
         self.models: Dict[str, torch.nn.Module] = {}
         self.teachers: Dict[str, torch.nn.Module] = {}
         self.model_iter: Dict[str, int] = defaultdict(int)
@@ -147,11 +155,13 @@ class InferenceServer:
         with self._lock:
             m = (self.teachers if teacher else self.models)[player_id]
             own = m.state_dict()
+            self._weights_begin()
             with torch.no_grad():
                 for k, v in state_dict.items():
                     if k in own and own[k].shape == v.shape:
                         own[k].copy_(v, non_blocking=True)
             _refresh_forms(m)
+            self._weights_end()
             if not teacher:
                 self.model_iter[player_id] = int(last_iter)
 
@@ -174,9 +184,11 @@ class InferenceServer:
                     dsts.append(t)
                     srcs.append(flat_dev[off:off + n].view(tuple(shp)))
                 off += n
+            self._weights_begin()
             with torch.no_grad():
                 _copy_many(dsts, srcs)
             _refresh_forms(m)
+            self._weights_end()
             self.model_iter[player_id] = int(last_iter)
 
     def attach_model_slot(self, player_id: str, shm_name: str) -> bool:
@@ -204,8 +216,10 @@ class InferenceServer:
         out = {}
         for pid, sub in list(getattr(self, '_subscribers', {}).items()):
             with self._lock:
+                self._weights_begin()
                 if sub.poll():
                     _refresh_forms(self.models[pid])
+                self._weights_end()
                     self.model_iter[pid] = sub.last_iter
                     out[pid] = sub.last_iter
         return out
@@ -333,9 +347,23 @@ class InferenceServer:
         self.stats['decollate_s'] += time.perf_counter() - t1
         return res
 
+    def _on_stream(self):
+        return torch.cuda.stream(self._stream) if self._stream is not None else _null()
+
+    def _weights_begin(self):
+        """Before writing a model's weights (any thread): the server's queued work that reads them goes first."""
+        if self._stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._stream)
+
+    def _weights_end(self):
+        """After writing: the server's later work waits for the writes."""
+        if self._stream is not None:
+            self._stream.wait_stream(torch.cuda.current_stream(self.device))
+
     def _forward(self, player_id: str, kind: str, inputs: List[Dict], teacher_id: Optional[str] = None) -> List[Dict]:
         """Synchronous batch of decoded inputs (tests / in-process callers); replies keep the policy logits."""
-        return self._results(self._launch((player_id, kind, teacher_id), inputs=inputs, keep_logits=True))
+        with self._on_stream():
+            return self._results(self._launch((player_id, kind, teacher_id), inputs=inputs, keep_logits=True))
 
     # ------------------------------------------------------------------ serving
     def _finish(self, L: _Launched):
@@ -410,6 +438,10 @@ class InferenceServer:
     def serve_once(self, timeout: float = 0.1) -> int:
         """Collect one dynamic batch per route and launch it; finish (reply to) the batches launched on the
         previous call.  Returns the number of requests launched."""
+        with self._on_stream():
+            return self._serve_once(timeout)
+
+    def _serve_once(self, timeout: float) -> int:
         busy = None
         if self._inflight and self._inflight[-1].event is not None:
             ev = self._inflight[-1].event
@@ -432,8 +464,9 @@ class InferenceServer:
         return served
 
     def drain(self):
-        while self._inflight:
-            self._finish(self._inflight.popleft())
+        with self._on_stream():
+            while self._inflight:
+                self._finish(self._inflight.popleft())
 
     def serve_forever(self, stop_event: Optional[threading.Event] = None):
         while not self._stop and not (stop_event is not None and stop_event.is_set()):
