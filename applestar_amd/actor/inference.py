@@ -217,9 +217,11 @@ class InferenceServer:
         for pid, sub in list(getattr(self, '_subscribers', {}).items()):
             with self._lock:
                 self._weights_begin()
-                if sub.poll():
+                updated = sub.poll()
+                if updated:
                     _refresh_forms(self.models[pid])
                 self._weights_end()
+                if updated:
                     self.model_iter[pid] = sub.last_iter
                     out[pid] = sub.last_iter
         return out
