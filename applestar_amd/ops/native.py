@@ -1341,6 +1341,12 @@ def _bf16w(w):
     that captured a form's buffer read the new values; untagged tensors are cast per call."""
     if torch.is_grad_enabled() and w.requires_grad:
         return _CastWeight.apply(w)
+    if w.dim() == 4 and not w.is_contiguous() and w.is_contiguous(memory_format=torch.channels_last):
+        # a channels_last conv weight: the form keeps that layout ([Cout, kh, kw, Cin] storage, what the conv
+        # kernels read through _conv_w without a copy); returned as the NCHW-logical view of it
+        src = w.detach().permute(0, 2, 3, 1)
+        f = _derived(w, 'bf16_cl', lambda: (src.to(torch.bfloat16).contiguous(), _view_spec(src, w)))
+        return f.permute(0, 3, 1, 2)
     return _derived(w, 'bf16', lambda: (w.detach().to(torch.bfloat16).contiguous(), _view_spec(w.detach(), w)
                                         if w.is_contiguous() else None))
 
