@@ -11,6 +11,8 @@ Parameter names/shapes match ``distar/agent/default/model/obs_encoder/*.py`` and
 """
 from __future__ import annotations
 
+import os
+
 from typing import Dict, List, Tuple, Optional
 
 import torch
@@ -22,7 +24,7 @@ from ..lib import game_data as gd
 from ..lib.features import (MAX_ENTITY_NUM, ENTITY_FIELDS, SPATIAL_ONE_HOT, EFFECT_KEYS, SPATIAL_SIZE, ENTITY_EMBED_DIM,
                             BEGINNING_ORDER_LENGTH)
 from .blocks import FCBlock, ConvBlock, ResBlock, MaxPool2x2, OneHotTable, binary_table, eye_table
-from .transformer import Transformer
+from .transformer import Transformer, dense_segments
 
 SPATIAL_Y, SPATIAL_X = SPATIAL_SIZE
 
@@ -314,8 +316,12 @@ class EntityEncoder(nn.Module):
         B, N = valid.shape
         flat_index = torch.arange(B * N, device=valid.device)
         h = self.embed(entity_info, flat_index).view(B, N, -1)
+        # the native varlen attention over 2B segments (real rows | padding rows) instead of dense masked scores
+        n = ops._native(h)
+        cu = dense_segments(entity_num, N) if n is not None and n.has('varlen_attention') and DENSE_VARLEN and \
+            self.transformer.layers[0].ln_type == 'post' else None
         for layer in self.transformer.layers:
-            h = layer.forward_dense(h, valid)
+            h = layer.forward_dense(h, valid, cu)
         x = F.relu(h)
         vm = valid.unsqueeze(-1).to(x.dtype)
         ee = self.entity_fc(x)
@@ -398,6 +404,8 @@ class SpatialEncoder(nn.Module):
 SCALAR_SIDE_STREAM = True
 # set by runtime.graphs.GraphedPolicy while capturing / replaying: shape-static entity path
 STATIC_SHAPES = False
+# static (graph-captured) entity path: attention on the native varlen kernel over 2B segments
+DENSE_VARLEN = os.environ.get('APPLESTAR_DENSE_VARLEN', '1') == '1'
 # padded packing (EntityEncoder._forward_padded): the padding rows form this many extra segments
 PAD_SEGMENTS = 8
 

@@ -16,6 +16,16 @@ from .. import ops
 from .blocks import FCBlock
 
 
+def dense_segments(lengths: torch.Tensor, N: int) -> torch.Tensor:
+    """int32 cu_seqlens [2B + 1] of a padded [B, N] token batch as 2B varlen segments: row b's first
+    ``lengths[b]`` tokens, then its remaining N - lengths[b] padding tokens."""
+    B = lengths.shape[0]
+    lens = lengths.clamp(0, N).to(torch.int32)
+    starts = torch.arange(B, device=lengths.device, dtype=torch.int32) * N
+    cu = torch.stack([starts, starts + lens], 1).reshape(-1)
+    return torch.cat([cu, cu.new_full((1,), B * N)])
+
+
 class Attention(nn.Module):
     def __init__(self, input_dim: int, head_dim: int, output_dim: int, head_num: int):
         super().__init__()
@@ -29,8 +39,14 @@ class Attention(nn.Module):
         a = ops.varlen_attention(qkv, cu_seqlens, max_len, self.head_num, self.head_dim)
         return self.project(a)
 
-    def forward_dense(self, x, key_mask=None):
+    def forward_dense(self, x, key_mask=None, cu=None):
+        """``cu``: the padded batch as 2B varlen segments (each row's real tokens, then its padding rows as a
+        segment of their own, :func:`dense_segments`): the native varlen kernel instead of dense masked scores.
+        Real rows get the same values; padding rows attend among themselves (finite, discarded downstream)."""
         B, N, _ = x.shape
+        if cu is not None:
+            a = ops.varlen_attention(self.attention_pre(x).reshape(B * N, -1), cu, N, self.head_num, self.head_dim)
+            return self.project(a.view(B, N, -1))
         qkv = self.attention_pre(x).view(B, N, 3, self.head_num, self.head_dim).permute(2, 0, 3, 1, 4)
         a = ops.masked_attention(qkv[0], qkv[1], qkv[2], key_mask)
         a = a.permute(0, 2, 1, 3).reshape(B, N, self.head_num * self.head_dim)
@@ -67,9 +83,9 @@ class TransformerLayer(nn.Module):
             m = blk(m)
         return ops.layer_norm(m, self.layernorm2.weight, self.layernorm2.bias, residual=x, act=act, grad_link=link2)
 
-    def forward_dense(self, x, key_mask=None):
+    def forward_dense(self, x, key_mask=None, cu=None):
         if self.ln_type == 'post':
-            x = self._ln(self.layernorm1, self.attention.forward_dense(x, key_mask), residual=x)
+            x = self._ln(self.layernorm1, self.attention.forward_dense(x, key_mask, cu), residual=x)
             return self._ln(self.layernorm2, self.mlp(x), residual=x)
         x = x + self.attention.forward_dense(self._ln(self.layernorm1, x), key_mask)
         return x + self.mlp(self._ln(self.layernorm2, x))

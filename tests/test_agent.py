@@ -227,3 +227,25 @@ def test_transform_obs_matches_golden_digests():
     for i, (g, r) in enumerate(zip(got, golden)):
         diff = {k for k in set(g) | set(r) if g.get(k) != r.get(k)}
         assert not diff, (i, sorted(diff)[:8])
+
+
+def test_dense_segments_varlen_equals_masked_attention():
+    """The static (graph-captured) entity path runs attention as varlen over 2B segments - each row's real
+    tokens, then its padding tokens (models/transformer.py dense_segments): on every real row it equals the
+    dense masked attention; empty segments (no entities / no padding) are fine."""
+    from applestar_amd.models.transformer import dense_segments
+    from applestar_amd.ops import reference as ref
+    torch.manual_seed(0)
+    B, N, H, D = 4, 16, 2, 8
+    lens = torch.tensor([5, 0, 16, 9])
+    qkv = torch.randn(B, N, 3 * H * D, dtype=torch.float64)
+    cu = dense_segments(lens, N)
+    assert cu.tolist() == [0, 5, 16, 16, 32, 48, 48, 57, 64]
+    a = ref.varlen_attention(qkv.reshape(B * N, -1), cu, N, H, D).view(B, N, -1)
+    q, k, v = qkv.view(B, N, 3, H, D).permute(2, 0, 3, 1, 4)
+    mask = torch.arange(N)[None, :] < lens[:, None]
+    b = ref.masked_attention(q, k, v, mask).permute(0, 2, 1, 3).reshape(B, N, H * D)
+    for i in range(B):
+        n = int(lens[i])
+        assert torch.allclose(a[i, :n], b[i, :n], atol=1e-12), i
+    assert torch.isfinite(a).all()

@@ -224,3 +224,26 @@ def test_entity_pack_matches_torch(num_dtype):
     assert torch.equal(flat, rv.reshape(-1).nonzero().squeeze(1))
     assert torch.equal(seg, torch.repeat_interleave(torch.arange(B, device=DEV), lens))
     assert torch.equal(cu, torch.nn.functional.pad(torch.cumsum(lens, 0).to(torch.int32), (1, 0)))
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_native_varlen_dense_segments_match_masked(dtype):
+    """Native varlen attention over dense_segments (real rows | padding rows, empty segments included) == the
+    dense masked reference on every real row (the graph-captured inference entity path)."""
+    from applestar_amd import ops
+    from applestar_amd.models.transformer import dense_segments
+    from applestar_amd.ops import reference as ref
+    torch.manual_seed(5)
+    B, N, H, D = 4, 512, 2, 128
+    lens = torch.tensor([300, 0, 512, 77], device=DEV)
+    qkv = torch.randn(B, N, 3 * H * D, device=DEV).to(dtype)
+    a = ops.varlen_attention(qkv.reshape(B * N, -1), dense_segments(lens, N), N, H, D).view(B, N, -1).float()
+    q, k, v = qkv.double().view(B, N, 3, H, D).permute(2, 0, 3, 1, 4)
+    mask = torch.arange(N, device=DEV)[None, :] < lens[:, None]
+    b = ref.masked_attention(q, k, v, mask).permute(0, 2, 1, 3).reshape(B, N, H * D)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    for i in range(B):
+        n = int(lens[i])
+        if n:
+            assert (a[i, :n] - b[i, :n]).abs().max().item() < tol * max(1.0, b[i, :n].abs().max().item()), i
+    assert torch.isfinite(a).all()
