@@ -50,10 +50,12 @@ def _learner_main(comm, B, T, gpu, precision, iq):
     orig = lrn._train
 
     def timed(data):
+        t0 = time.time()
         out = orig(data)
         if gpu:
             torch.cuda.synchronize()
-        iq.put((time.time(), lrn.last_iter.val + 1))
+        t1 = time.time()
+        iq.put((t1, lrn.last_iter.val + 1, t1 - t0))
         return out
     lrn._train = timed
     lrn.run(max_iterations=1000000)
@@ -122,12 +124,14 @@ def main():
     t0 = time.time()
     st0 = probe.stats()
     it0 = iters[-1][1] if iters else 0
+    n_rec0 = len(iters)
     srv_stats = lambda: dict(actor._server.stats) if getattr(actor, '_server', None) is not None else {}
     ss0 = srv_stats()
     time.sleep(args.seconds)
     t1 = time.time()
     st1 = probe.stats()
     it1 = iters[-1][1] if iters else 0
+    win = iters[n_rec0:]
     ss1 = srv_stats()
     sd = {k: ss1.get(k, 0.0) - ss0.get(k, 0.0) for k in ss1}
     pushed = st1.get('push', {}).get('MP0traj', 0) - st0.get('push', {}).get('MP0traj', 0)
@@ -140,6 +144,10 @@ def main():
            'actor_agent_steps_per_s_per_env_process': round(pushed * T / dt / max(args.envs, 1), 1),
            'learner_iters_per_s': round(n_it / dt, 3),
            'learner_samples_per_s_fed': round(n_it * B * T / dt, 1),
+           # time inside the learner's train step (incl. the GPU finishing it) vs the whole iteration: the rest is
+           # the learner waiting for / assembling data
+           'learner_train_ms_mean': round(1e3 * sum(r[2] for r in win) / max(len(win), 1), 1),
+           'learner_iter_ms_mean': round(1e3 * dt / max(n_it, 1), 1),
            'fresh_samples_per_s': round(pushed * T / dt, 1),
            'startup_s': round(t0 - t_start, 1),
            'inference_server': {
