@@ -847,6 +847,50 @@ std::vector<at::Tensor> entity_pack(const at::Tensor& num, int64_t N, int64_t to
   return {valid, flat, seg, cu};
 }
 
+// B [N, K] fp32 -> its bf16 fragment planes (uint8 [presplit_b_bytes]) for gemm_f32_psb
+at::Tensor presplit_b(const at::Tensor& b) {
+  check_cuda(b, "b");
+  TORCH_CHECK(b.dim() == 2 && b.scalar_type() == at::kFloat && b.is_contiguous(), "presplit_b: contiguous fp32 [N, K]");
+  c10::hip::HIPGuard g(b.device().index());
+  const int N = static_cast<int>(b.size(0)), K = static_cast<int>(b.size(1));
+  auto out = at::empty({as::presplit_b_bytes(N, K)}, b.options().dtype(at::kByte));
+  as::presplit_b(b.data_ptr<float>(), N, K, out.data_ptr(), stream());
+  return out;
+}
+
+bool gemm_f32_psb_supported(int64_t M, int64_t N, int64_t K) {
+  return as::gemm_f32_psb_supported(M, static_cast<int>(N), static_cast<int>(K));
+}
+
+// act(a [M, K] b^T + bias (+ res)) with b given as its presplit_b planes of an [N, K] matrix
+at::Tensor gemm_f32_psb(const at::Tensor& a, const at::Tensor& bsplit, int64_t N, int64_t K,
+                        const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res, int64_t act) {
+  check_cuda(a, "a");
+  check_cuda(bsplit, "bsplit");
+  TORCH_CHECK(a.scalar_type() == at::kFloat && a.dim() == 2 && a.size(1) == K && a.is_contiguous(),
+              "gemm_f32_psb: contiguous fp32 a [M, K]");
+  TORCH_CHECK(bsplit.scalar_type() == at::kByte && bsplit.numel() == as::presplit_b_bytes(N, K) &&
+                  bsplit.is_contiguous(), "gemm_f32_psb: bsplit must be presplit_b of an [N, K] matrix");
+  TORCH_CHECK(as::gemm_f32_psb_supported(a.size(0), static_cast<int>(N), static_cast<int>(K)),
+              "gemm_f32_psb: N % 128 == 0, K % 4 == 0");
+  const float* bp = nullptr;
+  const float* rp = nullptr;
+  if (bias && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->numel() == N && bias->is_contiguous(), "gemm_f32_psb: bias");
+    bp = bias->data_ptr<float>();
+  }
+  if (res && res->defined()) {
+    TORCH_CHECK(res->scalar_type() == at::kFloat && res->numel() == a.size(0) * N && res->is_contiguous(),
+                "gemm_f32_psb: res [M, N]");
+    rp = res->data_ptr<float>();
+  }
+  c10::hip::HIPGuard g(a.device().index());
+  auto out = at::empty({a.size(0), N}, a.options());
+  as::gemm_f32_psb(a.data_ptr<float>(), bsplit.data_ptr(), bp, rp, out.data_ptr<float>(), a.size(0),
+                   static_cast<int>(N), static_cast<int>(K), static_cast<int>(act), stream());
+  return out;
+}
+
 // ---------------------------------------------------------------- conv3x3 implicit GEMM (NHWC bf16)
 at::Tensor conv3x3_fwd(const at::Tensor& x, const at::Tensor& wk, const c10::optional<at::Tensor>& bias,
                        const c10::optional<at::Tensor>& res, int64_t act) {
@@ -2071,6 +2115,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layer_norm_bwd", &layer_norm_bwd);
   m.def("reverse_scan", &reverse_scan);
   m.def("col_sum", &col_sum);
+  m.def("presplit_b", &presplit_b);
+  m.def("gemm_f32_psb_supported", &gemm_f32_psb_supported);
+  m.def("gemm_f32_psb", &gemm_f32_psb, py::arg("a"), py::arg("bsplit"), py::arg("N"), py::arg("K"),
+        py::arg("bias") = py::none(), py::arg("res") = py::none(), py::arg("act") = 0);
   m.def("entity_pack", &entity_pack);
   m.def("embed_relu_fwd", &embed_relu_fwd);
   m.def("embed_relu_bwd", &embed_relu_bwd);

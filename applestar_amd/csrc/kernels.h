@@ -330,6 +330,14 @@ struct ColSumArgs {                    // passed by value (~3 KB of kernel argum
 };
 void col_sum(const ColSumArgs& a, hipStream_t s);
 
+// fp32 GEMM with the weight operand pre-split into bf16 fragment planes (gemm_f32_psb.hip): presplit_b builds the
+// planes of B [N, K] (presplit_b_bytes(N, K) bytes), gemm_f32_psb runs out = act(A B^T + bias (+ res)) on them
+long presplit_b_bytes(int N, int K);
+void presplit_b(const float* b, int N, int K, void* out, hipStream_t s);
+bool gemm_f32_psb_supported(long M, int N, int K);
+void gemm_f32_psb(const float* a, const void* bsplit, const float* bias, const float* res, float* out, long M, int N,
+                  int K, int act, hipStream_t s);
+
 // Strided multi-tensor copy (+ dtype conversion) into contiguous destinations: dst[t][i] for the dst index
 // i = ((i0 * size1 + i1) * size2 + i2) * size3 + i3 reads src[t][base + sum_k ik * stride_k] (strides may be
 // negative: flipped conv weights).  Rebuilds every derived weight form (fp32 biases, transposed GEMM weights,

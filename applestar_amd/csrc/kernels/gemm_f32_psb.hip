@@ -1,0 +1,187 @@
+// fp32 GEMM  out[M, N] = act(A[M, K] B[N, K]^T + bias (+ res))  with the weight operand PRE-SPLIT (split-MFMA mode).
+//
+// The split ring GEMM (gemm_f32.hip + f32_pipe.h) splits both operands into three bf16 parts in registers, in every
+// wave that reads them: ~44 VALU per fragment, 4 fragments per 24 MFMAs, and the B fragment of a 2 x 2 wave tile is
+// split twice per workgroup.  B is a weight: it changes once per optimizer step and is read by every M-tile.  Here
+// it is split ONCE per step (presplit_b_kernel, a derived weight form) into the MFMA's own fragment order:
+//
+//   planes[nb][kt][p][lane] = 8 bf16 (16 B): part p of B[32 nb + (lane & 31)][16 kt + 8 (lane >> 5) + 0..7]
+//
+// so a wave's fragment of (32-row block nb, 16-deep K-step kt) is three fully coalesced 1-KB loads.  The B
+// fragments bypass LDS: each wave streams its two fragments straight into registers one K-step ahead (inline-asm
+// buffer loads counted with the ring's own vmcnt waits), while the LDS-DMA ring (f32_pipe.h) carries only the A
+// rows (8 KB a stage).  Per K-step a wave splits 2 fragments instead of 4; the LDS traffic per step halves.
+#include "../common.h"
+#include "../kernels.h"
+#include "../split_mfma.h"
+#include "../f32_pipe.h"
+
+namespace as {
+namespace {
+
+using pipe::f16v;
+using pipe::i32x4;
+
+constexpr int kPsbBM = 128, kPsbBN = 128, kPsbNS = 3, kPsbRB = 64;   // 16 fp32 per A row and K-step
+constexpr int kPsbAStage = kPsbBM * kPsbRB;                             // 8 KB of A rows per stage
+
+__global__ __launch_bounds__(256) void presplit_b_kernel(const float* __restrict__ b, int N, int K, int KT, long total,
+                                                         u32v4* __restrict__ out) {
+  const long gid = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
+  if (gid >= total) return;
+  const int lane = static_cast<int>(gid & 63);
+  const long rest = gid >> 6;
+  const int kt = static_cast<int>(rest % KT);
+  const long nb = rest / KT;
+  const long n = nb * 32 + (lane & 31);
+  const int k0 = kt * 16 + 8 * (lane >> 5);
+  float v[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) v[t] = (n < N && k0 + t < K) ? b[n * K + k0 + t] : 0.f;
+  const Split3 s = split8(v);
+  u32v4* o = out + (nb * KT + kt) * 3 * 64 + lane;
+  o[0] = s.p[0];
+  o[64] = s.p[1];
+  o[128] = s.p[2];
+}
+
+// 16 B of a B fragment plane into registers, outside the compiler's waitcnt tracking (counted with the DMA ring)
+__device__ __forceinline__ void bload(u32v4& dst, i32x4 r, int voff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(dst) : "v"(voff), "s"(r) : "memory");
+}
+
+// wait until at most N vector-memory ops are outstanding; ties the B registers about to be read to the wait
+template <int N>
+__device__ __forceinline__ void wait_b(Split3 (&b)[2]) {
+  asm volatile("s_waitcnt vmcnt(%6)"
+               : "+v"(b[0].p[0]), "+v"(b[0].p[1]), "+v"(b[0].p[2]), "+v"(b[1].p[0]), "+v"(b[1].p[1]), "+v"(b[1].p[2])
+               : "n"(N)
+               : "memory");
+}
+
+template <bool STAGED>
+__global__ __launch_bounds__(256, 2) void gemm_f32_psb_kernel(const float* __restrict__ a,
+                                                              const u32v4* __restrict__ bs, int KT,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ res, float* __restrict__ out,
+                                                              long M, int N, int K, int act) {
+  // the staged epilogue reuses stage 0 for 32 x 128 floats (16 KB)
+  using C = pipe::Cfg<kPsbBN, kPsbNS, 16, kPsbBM, 4>;
+  // one ring array (stage = kt % 3, addressed at run time: the DMA is inline asm, so the compiler adds no waits
+  // for it whatever it can prove about the stages); 32 KB so the staged epilogue can take its first 16 KB
+  __shared__ __attribute__((aligned(16))) char ring[4 * kPsbAStage];
+  constexpr int A_PW = kPsbAStage / 1024 / 4;                // A DMA chunks per wave per step (2)
+  const int ntn = (N + kPsbBN - 1) / kPsbBN;
+  const int wg = pipe::xcd_remap();
+  const long m0 = static_cast<long>(wg / ntn) * kPsbBM;
+  const int n0 = (wg % ntn) * kPsbBN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int l32 = lane & 31, h = lane >> 5;
+  const i32x4 ar = pipe::rsrc(a, M * K * 4);
+  const long nbt = (N + 31) / 32;
+  const i32x4 br = pipe::rsrc(bs, nbt * KT * 3 * 1024);
+  // A DMA pieces (the ring's lane-linear, swizzled layout: f32_pipe.h)
+  int a_off[A_PW], a_k[A_PW];
+#pragma unroll
+  for (int c = 0; c < A_PW; ++c) {
+    const int row = C::dma_row(wid + 4 * c, lane), p = C::dma_piece(row, lane);
+    const long m = m0 + row;
+    a_k[c] = 4 * p;
+    a_off[c] = m < M ? static_cast<int>((m * K + 4 * p) * 4) : -1;
+  }
+  auto issue_a = [&](char* st, int kt) {
+#pragma unroll
+    for (int c = 0; c < A_PW; ++c)
+      pipe::dma16(ar, st + (wid + 4 * c) * 1024,
+                  a_off[c] >= 0 && kt < KT && kt * 16 + a_k[c] < K ? a_off[c] + kt * 64 : pipe::kOOB);
+  };
+  // this lane's B fragment j at K-step kt: ((nb KT + kt) 3 + p) KB + 16 lane
+  const int nb0 = (n0 + wn * C::TN) / 32;
+  int b_off[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b_off[j] = nb0 + j < nbt ? static_cast<int>((nb0 + j) * KT * 3 * 1024 + 16 * lane) : -1;
+  auto issue_b = [&](Split3 (&dst)[2], int kt) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bload(dst[j].p[p], br, b_off[j] >= 0 && kt < KT ? b_off[j] + (kt * 3 + p) * 1024 : pipe::kOOB);
+  };
+
+  f16v acc[C::FM][2];
+#pragma unroll
+  for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  Split3 bq[2][2];
+  // issue order per step kt (after its barrier): B(kt + 1), then A(kt + 2).  At the top of step kt the A rows of
+  // kt (issued two steps back) and B(kt) (issued one step back, before A(kt + 1)) must have landed; A(kt + 1) may
+  // stay in flight: vmcnt(A_PW)
+  auto step = [&](const char* st, char* next, int kt, Split3 (&bu)[2], Split3 (&bn)[2]) {
+    wait_b<A_PW>(bu);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue_b(bn, kt + 1);
+    issue_a(next, kt + 2);
+    // one A fragment split at a time (12 live VGPRs instead of 24: the two B register sets take 48)
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i) {
+      const Split3 sa = pipe::frag<C>(st, wm * C::TM + 32 * i + l32, 2 * h);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6(bu[j], sa, acc[i][j]);
+    }
+  };
+  auto stage = [&](int kt) { return ring + (kt % 3) * kPsbAStage; };
+  issue_b(bq[0], 0);
+  issue_a(stage(0), 0);
+  issue_a(stage(1), 1);
+  // unrolled by the 2 register sets (a 6-step unroll - stages and sets all compile-time - blew the register
+  // budget: 500+ VGPRs demanded, 255 spilled)
+  for (int kt = 0; kt < KT; kt += 2) {
+    step(stage(kt), stage(kt + 2), kt, bq[0], bq[1]);
+    if (kt + 1 >= KT) break;
+    step(stage(kt + 1), stage(kt + 3), kt + 1, bq[1], bq[0]);
+  }
+  pipe::wait_vm<0>();
+  if constexpr (STAGED) {
+    pipe::store_tile_staged<C, float>(acc, ring, out, bias, res, M, N, m0, n0, act);
+  } else {
+    pipe::store_tile<C::FM, 2>(acc, out, bias, res, M, N, m0 + wm * C::TM, n0 + wn * C::TN, act);
+  }
+}
+
+}  // namespace
+
+long presplit_b_bytes(int N, int K) {
+  const long nbt = (N + 31) / 32, KT = (K + 15) / 16;
+  return nbt * KT * 3 * 1024;
+}
+
+void presplit_b(const float* b, int N, int K, void* out, hipStream_t s) {
+  const int KT = (K + 15) / 16;
+  const long total = static_cast<long>((N + 31) / 32) * KT * 64;
+  if (total == 0) return;
+  hipLaunchKernelGGL(presplit_b_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, s, b, N, K, KT,
+                     total, static_cast<u32v4*>(out));
+}
+
+// N % 128 == 0 and K % 4 == 0 (the A rows stream in 16-B pieces); B pre-split by presplit_b
+bool gemm_f32_psb_supported(long M, int N, int K) {
+  return N % kPsbBN == 0 && K % 4 == 0 && K > 0 && M > 0 && M * K * 4 < 0x7ffffff0L &&
+         presplit_b_bytes(N, K) < 0x7ffffff0L;
+}
+
+void gemm_f32_psb(const float* a, const void* bsplit, const float* bias, const float* res, float* out, long M, int N,
+                  int K, int act, hipStream_t s) {
+  const long nwg = (M + kPsbBM - 1) / kPsbBM * (N / kPsbBN);
+  if (nwg == 0) return;
+  const int KT = (K + 15) / 16;
+  hipLaunchKernelGGL((gemm_f32_psb_kernel<true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a,
+                     static_cast<const u32v4*>(bsplit), KT, bias, res, out, M, N, K, act);
+}
+
+}  // namespace as

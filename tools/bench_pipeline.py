@@ -36,7 +36,7 @@ def _free_port():
     return p
 
 
-def _learner_main(comm, B, T, gpu, precision, iq):
+def _learner_main(comm, B, T, gpu, precision, iq, graph_step=False):
     import torch
     if not gpu:
         torch.set_num_threads(2)      # CPU rehearsal: leave cores to the env workers and the inference server
@@ -45,6 +45,7 @@ def _learner_main(comm, B, T, gpu, precision, iq):
                      'learner': {'use_cuda': gpu, 'player_id': 'MP0', 'use_value_feature': False,
                                  'amp_dtype': 'bfloat16' if precision == 'bf16' else None,
                                  'data': {'batch_size': B, 'trajectory_length': T, 'buffer_size': 2 * B},
+                                 'graph_step': bool(graph_step),
                                  'log_to_stdout': False},
                      'communication': comm})
     orig = lrn._train
@@ -69,6 +70,7 @@ def main():
     ap.add_argument('--traj-len', type=int, default=64)
     ap.add_argument('--precision', choices=['bf16', 'fp32'], default='bf16')
     ap.add_argument('--workdir', default='/tmp/applestar_pipeline')
+    ap.add_argument('--graph-step', action='store_true', help='the learner replays its whole step as one HIP graph')
     args = ap.parse_args()
     os.makedirs(args.workdir, exist_ok=True)
     os.chdir(args.workdir)
@@ -101,7 +103,7 @@ def main():
     import multiprocessing as mp
     ctx = mp.get_context('spawn')
     iq = ctx.Queue()
-    lp = ctx.Process(target=_learner_main, args=(comm, B, T, gpu, args.precision, iq), daemon=True)
+    lp = ctx.Process(target=_learner_main, args=(comm, B, T, gpu, args.precision, iq, args.graph_step), daemon=True)
     lp.start()
     iters = []          # (wall time, iteration) after each learner iteration
 
@@ -138,6 +140,7 @@ def main():
     dt = t1 - t0
     n_it = it1 - it0
     out = {'metric': 'end-to-end single-GPU RL pipeline', 'envs': args.envs, 'precision': args.precision,
+           'graph_step': bool(args.graph_step),
            'seconds': round(dt, 1), 'traj_len': T, 'batch': B,
            'trajectories_per_s': round(pushed / dt, 2),
            'actor_agent_steps_per_s': round(pushed * T / dt, 1),
