@@ -864,7 +864,8 @@ bool gemm_f32_psb_supported(int64_t M, int64_t N, int64_t K) {
 
 // act(a [M, K] b^T + bias (+ res)) with b given as its presplit_b planes of an [N, K] matrix
 at::Tensor gemm_f32_psb(const at::Tensor& a, const at::Tensor& bsplit, int64_t N, int64_t K,
-                        const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res, int64_t act) {
+                        const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res, int64_t act,
+                        int64_t variant) {
   check_cuda(a, "a");
   check_cuda(bsplit, "bsplit");
   TORCH_CHECK(a.scalar_type() == at::kFloat && a.dim() == 2 && a.size(1) == K && a.is_contiguous(),
@@ -887,8 +888,39 @@ at::Tensor gemm_f32_psb(const at::Tensor& a, const at::Tensor& bsplit, int64_t N
   c10::hip::HIPGuard g(a.device().index());
   auto out = at::empty({a.size(0), N}, a.options());
   as::gemm_f32_psb(a.data_ptr<float>(), bsplit.data_ptr(), bp, rp, out.data_ptr<float>(), a.size(0),
-                   static_cast<int>(N), static_cast<int>(K), static_cast<int>(act), stream());
+                   static_cast<int>(N), static_cast<int>(K), static_cast<int>(act), static_cast<int>(variant), stream());
   return out;
+}
+
+// log-probability of the taken action per head in one launch: logits[h] [..., C_h] (fp32 / bf16, contiguous),
+// actions[h] int64 of the logits' leading shape -> fp32 tensors of that shape
+std::vector<at::Tensor> multi_logp(const std::vector<at::Tensor>& logits, const std::vector<at::Tensor>& actions) {
+  TORCH_CHECK(logits.size() == actions.size() && !logits.empty() && logits.size() <= as::kLogpMaxH,
+              "multi_logp: 1..8 heads");
+  c10::hip::HIPGuard g(logits[0].device().index());
+  as::LogpArgs a;
+  a.nheads = static_cast<int>(logits.size());
+  a.row_start[0] = 0;
+  std::vector<at::Tensor> outs;
+  for (size_t h = 0; h < logits.size(); ++h) {
+    const at::Tensor& l = logits[h];
+    const at::Tensor& ac = actions[h];
+    check_cuda(l, "logits");
+    TORCH_CHECK((l.scalar_type() == at::kFloat || l.scalar_type() == at::kBFloat16) && l.is_contiguous() &&
+                    l.dim() >= 1 && l.size(-1) > 0, "multi_logp: contiguous fp32 / bf16 logits");
+    TORCH_CHECK(ac.scalar_type() == at::kLong && ac.is_contiguous() && ac.device() == l.device() &&
+                    ac.numel() * l.size(-1) == l.numel(), "multi_logp: int64 actions of the logits' leading shape");
+    auto o = at::empty(ac.sizes(), l.options().dtype(at::kFloat));
+    a.logits[h] = l.data_ptr();
+    a.action[h] = ac.data_ptr<int64_t>();
+    a.out[h] = o.data_ptr<float>();
+    a.cols[h] = static_cast<int>(l.size(-1));
+    a.bf16[h] = l.scalar_type() == at::kBFloat16 ? 1 : 0;
+    a.row_start[h + 1] = a.row_start[h] + ac.numel();
+    outs.push_back(o);
+  }
+  as::multi_logp(a, stream());
+  return outs;
 }
 
 // ---------------------------------------------------------------- conv3x3 implicit GEMM (NHWC bf16)
@@ -2115,10 +2147,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("layer_norm_bwd", &layer_norm_bwd);
   m.def("reverse_scan", &reverse_scan);
   m.def("col_sum", &col_sum);
+  m.def("multi_logp", &multi_logp);
   m.def("presplit_b", &presplit_b);
   m.def("gemm_f32_psb_supported", &gemm_f32_psb_supported);
   m.def("gemm_f32_psb", &gemm_f32_psb, py::arg("a"), py::arg("bsplit"), py::arg("N"), py::arg("K"),
-        py::arg("bias") = py::none(), py::arg("res") = py::none(), py::arg("act") = 0);
+        py::arg("bias") = py::none(), py::arg("res") = py::none(), py::arg("act") = 0, py::arg("variant") = 0);
   m.def("entity_pack", &entity_pack);
   m.def("embed_relu_fwd", &embed_relu_fwd);
   m.def("embed_relu_bwd", &embed_relu_bwd);

@@ -330,13 +330,27 @@ struct ColSumArgs {                    // passed by value (~3 KB of kernel argum
 };
 void col_sum(const ColSumArgs& a, hipStream_t s);
 
+// log-probability of the taken action for several heads in one launch (actor inference): head h has rows[h] rows
+// of cols[h] logits (fp32 or bf16: bf16[h]) and an int64 action per row; out[h][r] = logit[a] - logsumexp(row)
+constexpr int kLogpMaxH = 8;
+struct LogpArgs {
+  int nheads;
+  long row_start[kLogpMaxH + 1];       // prefix sums of rows (one wave per row)
+  const void* logits[kLogpMaxH];
+  const int64_t* action[kLogpMaxH];
+  float* out[kLogpMaxH];
+  int cols[kLogpMaxH];
+  unsigned char bf16[kLogpMaxH];
+};
+void multi_logp(const LogpArgs& a, hipStream_t s);
+
 // fp32 GEMM with the weight operand pre-split into bf16 fragment planes (gemm_f32_psb.hip): presplit_b builds the
 // planes of B [N, K] (presplit_b_bytes(N, K) bytes), gemm_f32_psb runs out = act(A B^T + bias (+ res)) on them
 long presplit_b_bytes(int N, int K);
 void presplit_b(const float* b, int N, int K, void* out, hipStream_t s);
 bool gemm_f32_psb_supported(long M, int N, int K);
 void gemm_f32_psb(const float* a, const void* bsplit, const float* bias, const float* res, float* out, long M, int N,
-                  int K, int act, hipStream_t s);
+                  int K, int act, int variant, hipStream_t s);
 
 // Strided multi-tensor copy (+ dtype conversion) into contiguous destinations: dst[t][i] for the dst index
 // i = ((i0 * size1 + i1) * size2 + i2) * size3 + i3 reads src[t][base + sum_k ik * stride_k] (strides may be

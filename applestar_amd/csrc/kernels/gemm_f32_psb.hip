@@ -59,8 +59,10 @@ __device__ __forceinline__ void wait_b(Split3 (&b)[2]) {
                : "memory");
 }
 
-template <bool STAGED>
-__global__ __launch_bounds__(256, 2) void gemm_f32_psb_kernel(const float* __restrict__ a,
+// DB: two B register sets (the next K-step's fragments load during this step's MFMAs: 204 VGPRs, 2 waves / SIMD);
+// else one set, each fragment reloaded right after its last MFMA (3 waves / SIMD)
+template <bool STAGED, bool DB>
+__global__ __launch_bounds__(256, DB ? 2 : 3) void gemm_f32_psb_kernel(const float* __restrict__ a,
                                                               const u32v4* __restrict__ bs, int KT,
                                                               const float* __restrict__ bias,
                                                               const float* __restrict__ res, float* __restrict__ out,
@@ -118,33 +120,63 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_psb_kernel(const float* __res
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   Split3 bq[2][2];
-  // issue order per step kt (after its barrier): B(kt + 1), then A(kt + 2).  At the top of step kt the A rows of
-  // kt (issued two steps back) and B(kt) (issued one step back, before A(kt + 1)) must have landed; A(kt + 1) may
-  // stay in flight: vmcnt(A_PW)
-  auto step = [&](const char* st, char* next, int kt, Split3 (&bu)[2], Split3 (&bn)[2]) {
-    wait_b<A_PW>(bu);
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    issue_b(bn, kt + 1);
-    issue_a(next, kt + 2);
-    // one A fragment split at a time (12 live VGPRs instead of 24: the two B register sets take 48)
-#pragma unroll
-    for (int i = 0; i < C::FM; ++i) {
-      const Split3 sa = pipe::frag<C>(st, wm * C::TM + 32 * i + l32, 2 * h);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6(bu[j], sa, acc[i][j]);
-    }
-  };
   auto stage = [&](int kt) { return ring + (kt % 3) * kPsbAStage; };
-  issue_b(bq[0], 0);
-  issue_a(stage(0), 0);
-  issue_a(stage(1), 1);
-  // unrolled by the 2 register sets (a 6-step unroll - stages and sets all compile-time - blew the register
-  // budget: 500+ VGPRs demanded, 255 spilled)
-  for (int kt = 0; kt < KT; kt += 2) {
-    step(stage(kt), stage(kt + 2), kt, bq[0], bq[1]);
-    if (kt + 1 >= KT) break;
-    step(stage(kt + 1), stage(kt + 3), kt + 1, bq[1], bq[0]);
+  if constexpr (DB) {
+    // issue order per step kt (after its barrier): B(kt + 1), then A(kt + 2).  At the top of step kt the A rows of
+    // kt (issued two steps back) and B(kt) (issued one step back, before A(kt + 1)) must have landed; A(kt + 1)
+    // may stay in flight: vmcnt(A_PW)
+    auto step = [&](const char* st, char* next, int kt, Split3 (&bu)[2], Split3 (&bn)[2]) {
+      wait_b<A_PW>(bu);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      issue_b(bn, kt + 1);
+      issue_a(next, kt + 2);
+#pragma unroll
+      for (int i = 0; i < C::FM; ++i) {
+        const Split3 sa = pipe::frag<C>(st, wm * C::TM + 32 * i + l32, 2 * h);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6(bu[j], sa, acc[i][j]);
+      }
+    };
+    issue_b(bq[0], 0);
+    issue_a(stage(0), 0);
+    issue_a(stage(1), 1);
+    // unrolled by the 2 register sets (a 6-step unroll - stages and sets all compile-time - blew the register
+    // budget: 500+ VGPRs demanded, 255 spilled)
+    for (int kt = 0; kt < KT; kt += 2) {
+      step(stage(kt), stage(kt + 2), kt, bq[0], bq[1]);
+      if (kt + 1 >= KT) break;
+      step(stage(kt + 1), stage(kt + 3), kt + 1, bq[1], bq[0]);
+    }
+  } else {
+    // issue order per step kt: [barrier] MFMAs of fragment 0, B(kt + 1) fragment 0 into its registers, MFMAs of
+    // fragment 1, B(kt + 1) fragment 1, A(kt + 2).  At the top of step kt + 1: A(kt + 1) and B(kt + 1) landed,
+    // A(kt + 2) may stay in flight: vmcnt(A_PW)
+    Split3 (&b)[2] = bq[0];
+    auto load_frag = [&](int j, int kt) {
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bload(b[j].p[p], br, b_off[j] >= 0 && kt < KT ? b_off[j] + (kt * 3 + p) * 1024 : pipe::kOOB);
+    };
+    load_frag(0, 0);
+    load_frag(1, 0);
+    issue_a(stage(0), 0);
+    issue_a(stage(1), 1);
+    for (int kt = 0; kt < KT; ++kt) {
+      wait_b<A_PW>(b);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const char* st = stage(kt);
+      const Split3 sa0 = pipe::frag<C>(st, wm * C::TM + l32, 2 * h);
+      const Split3 sa1 = pipe::frag<C>(st, wm * C::TM + 32 + l32, 2 * h);
+      acc[0][0] = mfma_x6(b[0], sa0, acc[0][0]);
+      acc[1][0] = mfma_x6(b[0], sa1, acc[1][0]);
+      load_frag(0, kt + 1);
+      acc[0][1] = mfma_x6(b[1], sa0, acc[0][1]);
+      acc[1][1] = mfma_x6(b[1], sa1, acc[1][1]);
+      load_frag(1, kt + 1);
+      issue_a(stage(kt + 2), kt + 2);
+    }
   }
   pipe::wait_vm<0>();
   if constexpr (STAGED) {
@@ -175,13 +207,18 @@ bool gemm_f32_psb_supported(long M, int N, int K) {
          presplit_b_bytes(N, K) < 0x7ffffff0L;
 }
 
+// variant: 0 = two B register sets (2 waves / SIMD), 1 = one set (3 waves / SIMD)
 void gemm_f32_psb(const float* a, const void* bsplit, const float* bias, const float* res, float* out, long M, int N,
-                  int K, int act, hipStream_t s) {
+                  int K, int act, int variant, hipStream_t s) {
   const long nwg = (M + kPsbBM - 1) / kPsbBM * (N / kPsbBN);
   if (nwg == 0) return;
   const int KT = (K + 15) / 16;
-  hipLaunchKernelGGL((gemm_f32_psb_kernel<true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a,
-                     static_cast<const u32v4*>(bsplit), KT, bias, res, out, M, N, K, act);
+  if (variant == 1)
+    hipLaunchKernelGGL((gemm_f32_psb_kernel<true, false>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a,
+                       static_cast<const u32v4*>(bsplit), KT, bias, res, out, M, N, K, act);
+  else
+    hipLaunchKernelGGL((gemm_f32_psb_kernel<true, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a,
+                       static_cast<const u32v4*>(bsplit), KT, bias, res, out, M, N, K, act);
 }
 
 }  // namespace as

@@ -185,4 +185,39 @@ void target_unit_sample(const void* e, int e_dt, const float* w1, const float* b
 #undef AS_TU
 }
 
+
+namespace {
+// one wave per row of any head: row max, sum of exp, the taken action's logit
+__global__ __launch_bounds__(256) void multi_logp_kernel(const LogpArgs a) {
+  const long row = static_cast<long>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (row >= a.row_start[a.nheads]) return;
+  int h = 0;
+  while (h + 1 < a.nheads && a.row_start[h + 1] <= row) ++h;
+  const long r = row - a.row_start[h];
+  const int C = a.cols[h], lane = threadIdx.x & 63;
+  const bool b16 = a.bf16[h] != 0;
+  auto ld = [&](long i) {
+    return b16 ? bf2f(static_cast<const bf16_t*>(a.logits[h])[i]) : static_cast<const float*>(a.logits[h])[i];
+  };
+  const long base = r * C;
+  float m = -INFINITY;
+  for (int c = lane; c < C; c += 64) m = fmaxf(m, ld(base + c));
+  m = wave_max(m);
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += __expf(ld(base + c) - m);
+  s = wave_sum(s);
+  if (lane == 0) {
+    long act = a.action[h][r];
+    act = act < 0 ? 0 : (act >= C ? C - 1 : act);
+    a.out[h][r] = ld(base + act) - m - __logf(s);
+  }
+}
+}  // namespace
+
+void multi_logp(const LogpArgs& a, hipStream_t s) {
+  const long rows = a.row_start[a.nheads];
+  if (rows > 0)
+    hipLaunchKernelGGL(multi_logp_kernel, dim3(static_cast<unsigned>((rows + 3) / 4)), dim3(256), 0, s, a);
+}
+
 }  // namespace as

@@ -287,10 +287,7 @@ class Model(nn.Module):
         out, out_state = self._core(lstm_input.unsqueeze(0), hidden_state)
         action, su_num, logit, extra = self.policy(out[0], entity_embeddings, map_skip, scalar_context, entity_num,
                                                    self.temperature, self.race_mask, noise)
-        logp = {}
-        for k, a in action.items():
-            lp = torch.log_softmax(logit[k].float(), dim=-1)
-            logp[k] = lp.gather(-1, a.long().unsqueeze(-1)).squeeze(-1)
+        logp = ops.action_logp(logit, action)
         return {'action_info': action, 'action_logp': logp, 'selected_units_num': su_num,
                 'entity_num': entity_num, 'hidden_state': out_state, 'logit': logit, 'extra_units': extra}
 

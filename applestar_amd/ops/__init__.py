@@ -174,6 +174,22 @@ def varlen_attention(qkv, cu_seqlens, max_len: int, num_heads: int, head_dim: in
     return ref.varlen_attention(qkv, cu_seqlens, max_len, num_heads, head_dim)
 
 
+def action_logp(logits, actions):
+    """{head: log_softmax(logits[head])[actions[head]]} (fp32): one native launch for all heads on the GPU."""
+    keys = list(actions)
+    n = _native(logits[keys[0]]) if keys else None
+    if n is not None and n.has('action_logp') and len(keys) <= 8:
+        ls = [logits[k].contiguous() for k in keys]
+        if all(t.dtype in (torch.float32, torch.bfloat16) for t in ls):
+            outs = n.ensure_loaded().multi_logp(ls, [actions[k].long().contiguous() for k in keys])
+            return dict(zip(keys, outs))
+    out = {}
+    for k in keys:
+        lp = torch.log_softmax(logits[k].float(), dim=-1)
+        out[k] = lp.gather(-1, actions[k].long().unsqueeze(-1)).squeeze(-1)
+    return out
+
+
 def head_stats(logits, teacher, actions):
     """(logp(action), entropy, KL(teacher || logits)) per distribution row, fp32 (K19 fused kernel on GPU)."""
     n = _native(logits)

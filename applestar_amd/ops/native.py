@@ -28,7 +28,7 @@ _IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
                 'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp',
                 'location_input', 'value_spatial_proj', 'spatial_embed_pool', 'value_spatial_proj_pool',
-                'rl_loss', 'embed_relu', 'col_assemble', 'entity_pack'}
+                'rl_loss', 'embed_relu', 'col_assemble', 'entity_pack', 'action_logp'}
 
 
 def has(name: str) -> bool:

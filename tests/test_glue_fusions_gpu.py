@@ -247,3 +247,20 @@ def test_native_varlen_dense_segments_match_masked(dtype):
         if n:
             assert (a[i, :n] - b[i, :n]).abs().max().item() < tol * max(1.0, b[i, :n].abs().max().item()), i
     assert torch.isfinite(a).all()
+
+
+def test_multi_logp_matches_log_softmax_gather():
+    """ops.action_logp (one launch for every head: row max, sum of exp, the taken logit) == log_softmax + gather."""
+    from applestar_amd import ops
+    from applestar_amd.ops import native as N
+    N.ensure_loaded()
+    torch.manual_seed(6)
+    logits = {'a': torch.randn(3, 327, device=DEV), 'b': torch.randn(3, 64, 301, device=DEV).to(torch.bfloat16),
+              'c': torch.randn(3, 24320, device=DEV) * 5}
+    logits['c'][:, 100:] = -1e9
+    acts = {'a': torch.randint(0, 327, (3,), device=DEV), 'b': torch.randint(0, 301, (3, 64), device=DEV),
+            'c': torch.randint(0, 100, (3,), device=DEV)}
+    got = ops.action_logp(logits, acts)
+    for k in logits:
+        ref = torch.log_softmax(logits[k].float(), -1).gather(-1, acts[k].unsqueeze(-1)).squeeze(-1)
+        assert got[k].shape == ref.shape and (got[k] - ref).abs().max().item() < 1e-4, k

@@ -26,7 +26,8 @@ def main():
         ref = (a[:4096].double() @ b.double().t() + bias.double()).relu()
         res = {}
         for name, fn in (('ring', lambda: C.gemm_f32(a, b, bias, None, 1)),
-                         ('psb', lambda: C.gemm_f32_psb(a, bs, Nn, K, bias, None, 1))):
+                         ('psb_db2w', lambda: C.gemm_f32_psb(a, bs, Nn, K, bias, None, 1, 0)),
+                         ('psb_sb', lambda: C.gemm_f32_psb(a, bs, Nn, K, bias, None, 1, 1))):
             out = fn()
             err = (out[:4096].double() - ref).abs()
             for _ in range(3):
@@ -54,7 +55,8 @@ def main():
         t1.record()
         torch.cuda.synchronize()
         print(json.dumps({'shape': [Nn, K], 'presplit_us': round(t0.elapsed_time(t1) * 1e3 / iters, 1),
-                          'speedup': round(res['ring'] / res['psb'], 3)}), flush=True)
+                          'speedup_db2w': round(res['ring'] / res['psb_db2w'], 3),
+                          'speedup_sb': round(res['ring'] / res['psb_sb'], 3)}), flush=True)
 
 
 if __name__ == '__main__':

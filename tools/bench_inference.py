@@ -22,6 +22,7 @@ def main():
     ap.add_argument('--iters', type=int, default=30)
     ap.add_argument('--entities', type=int, default=300)
     ap.add_argument('--graphs', type=int, default=1, help='also time the HIP-graph replay (runtime.graphs.GraphedPolicy)')
+    ap.add_argument('--modes', default='', help='comma list of policy,teacher,policy_graph,teacher_graph (default all)')
     args = ap.parse_args()
     dev = torch.device('cuda', 0)
     m = Model({'agent': {'extra_units': True}}).to(dev).eval().to(memory_format=torch.channels_last)
@@ -43,6 +44,8 @@ def main():
         act_d = {k: v.to(dev) for k, v in act.items()}
         modes = [('policy', False), ('teacher', False)] + ([('policy_graph', True), ('teacher_graph', True)]
                                                            if args.graphs else [])
+        if args.modes:
+            modes = [m for m in modes if m[0] in args.modes.split(',')]
         for name, graphed in modes:
             times = []
             for i in range(args.iters + 3):
@@ -65,7 +68,8 @@ def main():
             times.sort()
             res[name] = {'p50_ms': round(times[len(times) // 2], 2), 'p99_ms': round(times[-1], 2)}
         su = int(out['selected_units_num'].max()) if 'selected_units_num' in out else None
-        print(json.dumps({'batch': B, **res, 'per_env_policy_ms': round(res['policy']['p50_ms'] / B, 3),
+        pol = res.get('policy', res.get('policy_graph', {'p50_ms': float('nan')}))
+        print(json.dumps({'batch': B, **res, 'per_env_policy_ms': round(pol['p50_ms'] / B, 3),
                           'reference_16env_ms': 160.0}), flush=True)
 
 
