@@ -44,7 +44,10 @@ DEFAULT_ACTOR_CONFIG = {
     'actor': {'job_type': 'eval_test', 'league_job_type': 'train', 'gpu_batch_inference': False,
               'env_num': 1, 'episode_num': 1, 'print_freq': 100, 'traj_len': 64, 'use_cuda': False,
               'fake_model': True, 'player_ids': ['model1'], 'agents': {}, 'model_paths': {},
-              'teacher_player_ids': ['none'], 'teacher_model_paths': {}, 'max_wait_ms': 2.0},
+              'teacher_player_ids': ['none'], 'teacher_model_paths': {}, 'max_wait_ms': 2.0,
+              # env workers run at this nice level: on a box shared with a learner / inference server the host
+              # threads that feed the GPU keep their CPU (0: unchanged)
+              'env_nice': 5},
     'env': {'map_name': 'KairosJunction', 'player_ids': ['agent1', 'bot7'], 'races': ['zerg', 'zerg'],
             'realtime': False, 'game_steps_per_episode': 100000, 'fake': None},
     'communication': {'coordinator_ip': '127.0.0.1', 'coordinator_port': 0, 'league_ip': '127.0.0.1',
@@ -222,6 +225,12 @@ def _worker_main(cfg_dict, job, env_id, req_conns, ctrl, result_q, coord):
     """Spawned env worker: CPU featurization + env; model calls go to the parent's server."""
     torch.set_num_threads(1)
     cfg = AttrDict(cfg_dict)
+    nice = int(cfg.actor.get('env_nice', 0) or 0)
+    if nice > 0:
+        try:
+            os.nice(nice)
+        except OSError:
+            pass
     from .inference import InferenceClient
     clients = None
     if req_conns is not None:
