@@ -847,15 +847,24 @@ std::vector<at::Tensor> entity_pack(const at::Tensor& num, int64_t N, int64_t to
   return {valid, flat, seg, cu};
 }
 
-// B [N, K] fp32 -> its bf16 fragment planes (uint8 [presplit_b_bytes]) for gemm_f32_psb
-at::Tensor presplit_b(const at::Tensor& b) {
+// B [N, K] fp32 (or, trans, B^T given as [K, N]) -> its bf16 fragment planes (uint8 [presplit_b_bytes]) for
+// gemm_f32_psb; out: an existing planes buffer of that size to rebuild in place
+at::Tensor presplit_b(const at::Tensor& b, bool trans, const c10::optional<at::Tensor>& out) {
   check_cuda(b, "b");
-  TORCH_CHECK(b.dim() == 2 && b.scalar_type() == at::kFloat && b.is_contiguous(), "presplit_b: contiguous fp32 [N, K]");
+  TORCH_CHECK(b.dim() == 2 && b.scalar_type() == at::kFloat && b.is_contiguous(), "presplit_b: contiguous fp32 matrix");
   c10::hip::HIPGuard g(b.device().index());
-  const int N = static_cast<int>(b.size(0)), K = static_cast<int>(b.size(1));
-  auto out = at::empty({as::presplit_b_bytes(N, K)}, b.options().dtype(at::kByte));
-  as::presplit_b(b.data_ptr<float>(), N, K, out.data_ptr(), stream());
-  return out;
+  const int N = static_cast<int>(trans ? b.size(1) : b.size(0)), K = static_cast<int>(trans ? b.size(0) : b.size(1));
+  const long bytes = as::presplit_b_bytes(N, K);
+  at::Tensor o;
+  if (out && out->defined()) {
+    TORCH_CHECK(out->scalar_type() == at::kByte && out->numel() == bytes && out->is_contiguous() &&
+                    out->device() == b.device(), "presplit_b: out must be a uint8 planes buffer of the right size");
+    o = *out;
+  } else {
+    o = at::empty({bytes}, b.options().dtype(at::kByte));
+  }
+  as::presplit_b(b.data_ptr<float>(), N, K, trans, o.data_ptr(), stream());
+  return o;
 }
 
 bool gemm_f32_psb_supported(int64_t M, int64_t N, int64_t K) {
@@ -2148,7 +2157,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("reverse_scan", &reverse_scan);
   m.def("col_sum", &col_sum);
   m.def("multi_logp", &multi_logp);
-  m.def("presplit_b", &presplit_b);
+  m.def("presplit_b", &presplit_b, py::arg("b"), py::arg("trans") = false, py::arg("out") = py::none());
   m.def("gemm_f32_psb_supported", &gemm_f32_psb_supported);
   m.def("gemm_f32_psb", &gemm_f32_psb, py::arg("a"), py::arg("bsplit"), py::arg("N"), py::arg("K"),
         py::arg("bias") = py::none(), py::arg("res") = py::none(), py::arg("act") = 0, py::arg("variant") = 0);

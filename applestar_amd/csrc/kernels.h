@@ -347,7 +347,7 @@ void multi_logp(const LogpArgs& a, hipStream_t s);
 // fp32 GEMM with the weight operand pre-split into bf16 fragment planes (gemm_f32_psb.hip): presplit_b builds the
 // planes of B [N, K] (presplit_b_bytes(N, K) bytes), gemm_f32_psb runs out = act(A B^T + bias (+ res)) on them
 long presplit_b_bytes(int N, int K);
-void presplit_b(const float* b, int N, int K, void* out, hipStream_t s);
+void presplit_b(const float* b, int N, int K, bool trans, void* out, hipStream_t s);
 bool gemm_f32_psb_supported(long M, int N, int K);
 void gemm_f32_psb(const float* a, const void* bsplit, const float* bias, const float* res, float* out, long M, int N,
                   int K, int act, int variant, hipStream_t s);

@@ -25,8 +25,9 @@ using pipe::i32x4;
 constexpr int kPsbBM = 128, kPsbBN = 128, kPsbNS = 3, kPsbRB = 64;   // 16 fp32 per A row and K-step
 constexpr int kPsbAStage = kPsbBM * kPsbRB;                             // 8 KB of A rows per stage
 
+// trans: the source is B^T ([K][N] row-major, e.g. a weight W [N_out][K_in] whose transpose feeds the dX product)
 __global__ __launch_bounds__(256) void presplit_b_kernel(const float* __restrict__ b, int N, int K, int KT, long total,
-                                                         u32v4* __restrict__ out) {
+                                                         bool trans, u32v4* __restrict__ out) {
   const long gid = static_cast<long>(blockIdx.x) * 256 + threadIdx.x;
   if (gid >= total) return;
   const int lane = static_cast<int>(gid & 63);
@@ -37,7 +38,8 @@ __global__ __launch_bounds__(256) void presplit_b_kernel(const float* __restrict
   const int k0 = kt * 16 + 8 * (lane >> 5);
   float v[8];
 #pragma unroll
-  for (int t = 0; t < 8; ++t) v[t] = (n < N && k0 + t < K) ? b[n * K + k0 + t] : 0.f;
+  for (int t = 0; t < 8; ++t)
+    v[t] = (n < N && k0 + t < K) ? (trans ? b[static_cast<long>(k0 + t) * N + n] : b[n * K + k0 + t]) : 0.f;
   const Split3 s = split8(v);
   u32v4* o = out + (nb * KT + kt) * 3 * 64 + lane;
   o[0] = s.p[0];
@@ -125,8 +127,10 @@ __global__ __launch_bounds__(256, DB ? 2 : 3) void gemm_f32_psb_kernel(const flo
     // issue order per step kt (after its barrier): B(kt + 1), then A(kt + 2).  At the top of step kt the A rows of
     // kt (issued two steps back) and B(kt) (issued one step back, before A(kt + 1)) must have landed; A(kt + 1)
     // may stay in flight: vmcnt(A_PW)
+    // The wait for a register set sits at the END of the step that loaded it (the top of the next step waits for
+    // the same things): a register the compiler carries around the loop (a phi copy at the back edge) is then
+    // never read before its load returned.
     auto step = [&](const char* st, char* next, int kt, Split3 (&bu)[2], Split3 (&bn)[2]) {
-      wait_b<A_PW>(bu);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       issue_b(bn, kt + 1);
@@ -137,10 +141,12 @@ __global__ __launch_bounds__(256, DB ? 2 : 3) void gemm_f32_psb_kernel(const flo
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6(bu[j], sa, acc[i][j]);
       }
+      wait_b<A_PW>(bn);
     };
     issue_b(bq[0], 0);
     issue_a(stage(0), 0);
     issue_a(stage(1), 1);
+    wait_b<A_PW>(bq[0]);
     // unrolled by the 2 register sets (a 6-step unroll - stages and sets all compile-time - blew the register
     // budget: 500+ VGPRs demanded, 255 spilled)
     for (int kt = 0; kt < KT; kt += 2) {
@@ -162,8 +168,8 @@ __global__ __launch_bounds__(256, DB ? 2 : 3) void gemm_f32_psb_kernel(const flo
     load_frag(1, 0);
     issue_a(stage(0), 0);
     issue_a(stage(1), 1);
+    wait_b<A_PW>(b);
     for (int kt = 0; kt < KT; ++kt) {
-      wait_b<A_PW>(b);
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       const char* st = stage(kt);
@@ -176,6 +182,8 @@ __global__ __launch_bounds__(256, DB ? 2 : 3) void gemm_f32_psb_kernel(const flo
       acc[1][1] = mfma_x6(b[1], sa1, acc[1][1]);
       load_frag(1, kt + 1);
       issue_a(stage(kt + 2), kt + 2);
+      // at the end of the step (see the two-set form): B(kt + 1) and A(kt + 1) landed, A(kt + 2) may fly
+      wait_b<A_PW>(b);
     }
   }
   pipe::wait_vm<0>();
@@ -193,12 +201,12 @@ long presplit_b_bytes(int N, int K) {
   return nbt * KT * 3 * 1024;
 }
 
-void presplit_b(const float* b, int N, int K, void* out, hipStream_t s) {
+void presplit_b(const float* b, int N, int K, bool trans, void* out, hipStream_t s) {
   const int KT = (K + 15) / 16;
   const long total = static_cast<long>((N + 31) / 32) * KT * 64;
   if (total == 0) return;
   hipLaunchKernelGGL(presplit_b_kernel, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256), 0, s, b, N, K, KT,
-                     total, static_cast<u32v4*>(out));
+                     total, trans, static_cast<u32v4*>(out));
 }
 
 // N % 128 == 0 and K % 4 == 0 (the A rows stream in 16-B pieces); B pre-split by presplit_b

@@ -995,6 +995,10 @@ class DerivedWeights:
         f = self.forms.get((id(p), key))
         if f is not None and f[3] == self.epoch and f[4] == p._version:
             return f[1]
+        if f is not None and callable(f[2]):
+            f[2](f[1])           # a custom form (e.g. pre-split planes): rebuilt in place by its own kernel
+            f[3], f[4] = self.epoch, p._version
+            return f[1]
         out, spec = make()
         if spec is None or out.data_ptr() == p.data_ptr():
             return out
@@ -1012,12 +1016,16 @@ class DerivedWeights:
         self.epoch += 1
         if not (self.enabled and self.forms):
             return
-        fs = list(self.forms.values())
+        fs = [f for f in self.forms.values() if not callable(f[2])]
         spec = []
         for f in fs:
             spec += f[2]
-        ensure_loaded().multi_strided_copy([f[1] for f in fs], [f[0].detach() for f in fs], spec)
-        for f in fs:
+        if fs:
+            ensure_loaded().multi_strided_copy([f[1] for f in fs], [f[0].detach() for f in fs], spec)
+        for f in self.forms.values():
+            if callable(f[2]):
+                f[2](f[1])
+        for f in self.forms.values():
             f[3], f[4] = self.epoch, f[0]._version
 
 
@@ -1035,6 +1043,27 @@ def _view_spec(view, src):
     pad = 4 - view.dim()
     return [1] * pad + list(view.shape) + [0] * pad + list(view.stride()) + \
         [view.storage_offset() - src.storage_offset()]
+
+
+# fp32 GEMMs on pre-split weight planes (gemm_f32_psb.hip: the weight split once per optimizer step into MFMA
+# fragment-order bf16 planes instead of in every wave of every M-tile); APPLESTAR_GEMM_PSB=0: the split ring GEMM
+GEMM_PSB = os.environ.get('APPLESTAR_GEMM_PSB', '1') == '1'
+GEMM_PSB_VARIANT = int(os.environ.get('APPLESTAR_GEMM_PSB_VARIANT', '1'))
+
+
+def _psb_ok(M, N, K):
+    """The pre-split GEMM replaces the split ring kernel (tile-count rule of gemm_f32; few-row products keep the
+    small-tile kernel): N % 128, K % 4."""
+    return GEMM_PSB and (M + 127) // 128 * ((N + 63) // 64) >= 128 and _C.gemm_f32_psb_supported(M, N, K)
+
+
+def _psb(w, transposed=False):
+    """Pre-split planes of the GEMM B operand: w [N, K] itself, or (transposed) w^T [K_in, N_out] for the dX
+    product; a derived form of a parameter (rebuilt in place by presplit_b after each optimizer step)."""
+    def build(into=None):
+        src = w.detach().reshape(w.shape[0], -1)
+        return _C.presplit_b(src if src.is_contiguous() else src.contiguous(), transposed, into)
+    return _derived(w, 'psbT' if transposed else 'psb', lambda: (build(), build))
 
 
 def _w32(t):
@@ -1615,8 +1644,13 @@ class _Linear(torch.autograd.Function):
                 y = y + b.float()
             y = (torch.relu(y) if relu else y).to(x2.dtype)
         elif x2.dtype == torch.float32 and _gemm_f32_ok(R, w.shape[0], K):
-            # fp32 step: f32-MFMA GEMM with the bias and ReLU in its epilogue (gemm_f32.hip)
-            y = _C.gemm_f32(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None, 1 if relu else 0)
+            # fp32 step: f32-MFMA GEMM with the bias and ReLU in its epilogue (gemm_f32.hip; on the pre-split weight
+            # planes when the shape allows, gemm_f32_psb.hip)
+            bias = _w32(b) if b is not None else None
+            if w.dim() == 2 and _psb_ok(R, w.shape[0], K):
+                y = _C.gemm_f32_psb(x2, _psb(w), w.shape[0], K, bias, None, 1 if relu else 0, GEMM_PSB_VARIANT)
+            else:
+                y = _C.gemm_f32(x2, w.detach().contiguous(), bias, None, 1 if relu else 0)
             if relu and RELU_LINK:
                 _note_relu_out(y)
         elif _bf16_small_ok(x2, R, w.shape[0], K):
@@ -1673,11 +1707,17 @@ class _Linear(torch.autograd.Function):
             # fp32: dX = dY W (+ the handed-over residual gradient) on the f32-MFMA GEMM, out of place; when x is
             # the ReLU output of another fp32 linear, that ReLU's mask is applied here (epilogue mode 4) and
             # the producer's backward skips its own threshold pass (_premasked)
+            psb = w.dim() == 2 and _psb_ok(dy.shape[0], w.shape[1], dy.shape[1])
             if g is None and ctx.mask_in:
-                dx = _C.gemm_f32(dy, _wT(w), None, x2, 4)
+                dx = _C.gemm_f32_psb(dy, _psb(w, True), w.shape[1], w.shape[0], None, x2, 4, GEMM_PSB_VARIANT) if psb \
+                    else _C.gemm_f32(dy, _wT(w), None, x2, 4)
                 _MASKED_DX[x2.data_ptr()] = (dx, dx._version)
             else:
-                dx = _C.gemm_f32(dy, _wT(w), None, None if g is None else g.view(dy.shape[0], w.shape[1]), 0)
+                r = None if g is None else g.view(dy.shape[0], w.shape[1])
+                if psb and r is not None and not r.is_contiguous():
+                    psb = False
+                dx = _C.gemm_f32_psb(dy, _psb(w, True), w.shape[1], w.shape[0], None, r, 0, GEMM_PSB_VARIANT) if psb \
+                    else _C.gemm_f32(dy, _wT(w), None, r, 0)
         elif (g is not None or ctx.needs_input_grad[0]) and _bf16_small_ok(dy, dy.shape[0], w.shape[1], dy.shape[1]) \
                 and (g is None or g.dtype == torch.bfloat16):
             # bf16 step, few rows: dX = dY W (+ the handed-over residual gradient) on the small-tile kernel

@@ -264,3 +264,22 @@ def test_multi_logp_matches_log_softmax_gather():
     for k in logits:
         ref = torch.log_softmax(logits[k].float(), -1).gather(-1, acts[k].unsqueeze(-1)).squeeze(-1)
         assert got[k].shape == ref.shape and (got[k] - ref).abs().max().item() < 1e-4, k
+
+
+@pytest.mark.parametrize('variant', [0, 1])
+@pytest.mark.parametrize('shape', [(1000, 256, 256), (777, 128, 132), (4099, 384, 1000)])
+def test_gemm_f32_psb_matches_fp64(variant, shape):
+    """fp32 GEMM on pre-split weight planes (gemm_f32_psb.hip, both register schemes): relu(A B^T + bias + res)
+    == float64 to fp32 accuracy, ragged M / K included."""
+    from applestar_amd.ops import native as N
+    C = N.ensure_loaded()
+    torch.manual_seed(7)
+    M, Nn, K = shape
+    a = torch.randn(M, K, device=DEV)
+    b = torch.randn(Nn, K, device=DEV) / K ** 0.5
+    bias = torch.randn(Nn, device=DEV)
+    res = torch.randn(M, Nn, device=DEV)
+    out = C.gemm_f32_psb(a, C.presplit_b(b), Nn, K, bias, res, 1, variant)
+    ref = (a.double() @ b.double().t() + bias.double() + res.double()).relu()
+    err = (out.double() - ref).abs().max().item()
+    assert err < 2e-5 * max(1.0, ref.abs().max().item()), err
