@@ -351,6 +351,12 @@ void presplit_b(const float* b, int N, int K, bool trans, void* out, hipStream_t
 bool gemm_f32_psb_supported(long M, int N, int K);
 void gemm_f32_psb(const float* a, const void* bsplit, const float* bias, const float* res, float* out, long M, int N,
                   int K, int act, int variant, hipStream_t s);
+// 3 x 3 conv on the pre-split planes of w [Cout, 3, 3, Cin] (presplit_b of its [Cout, 9 Cin] view); res2 / mask:
+// the input-gradient epilogue extras of conv3x3_f32_fwd_epi2 (nullptr: off)
+bool conv3x3_f32_psb_supported(long M, int Cin, int Cout);
+void conv3x3_f32_psb(const float* x, const void* wsplit, const float* bias, const float* res, const float* res2,
+                     long res2_rows, const float* mask, float* out, int B, int H, int W, int Cin, int Cout, int act,
+                     hipStream_t s);
 
 // Strided multi-tensor copy (+ dtype conversion) into contiguous destinations: dst[t][i] for the dst index
 // i = ((i0 * size1 + i1) * size2 + i2) * size3 + i3 reads src[t][base + sum_k ik * stride_k] (strides may be

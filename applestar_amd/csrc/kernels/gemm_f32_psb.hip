@@ -61,6 +61,49 @@ __device__ __forceinline__ void wait_b(Split3 (&b)[2]) {
                : "memory");
 }
 
+// The one-register-set main loop (128 VGPRs): per K-step kt [barrier] MFMAs of B fragment 0, B(kt + 1) fragment 0
+// into the freed registers, MFMAs of fragment 1, B(kt + 1) fragment 1, then the A rows of kt + 2 into the ring
+// stage read at kt - 1.  The wait for B(kt + 1) / A(kt + 1) sits at the END of step kt (vmcnt(A_PW): A(kt + 2) may
+// fly), so a register the compiler carries around the loop is never copied before its load returned.
+template <class C, int A_PW, class IssueA>
+__device__ __forceinline__ void psb_sb_loop(char* ring, const IssueA& issue_a, i32x4 br, const int (&b_off)[2], int KT,
+                                            f16v (&acc)[2][2], int wm, int l32, int h) {
+  Split3 b[2];
+  auto stage = [&](int kt) { return ring + (kt % 3) * kPsbAStage; };
+  auto load_frag = [&](int j, int kt) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      bload(b[j].p[p], br, b_off[j] >= 0 && kt < KT ? b_off[j] + (kt * 3 + p) * 1024 : pipe::kOOB);
+  };
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  load_frag(0, 0);
+  load_frag(1, 0);
+  issue_a(stage(0), 0);
+  issue_a(stage(1), 1);
+  wait_b<A_PW>(b);
+  for (int kt = 0; kt < KT; ++kt) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    const char* st = stage(kt);
+    const Split3 sa0 = pipe::frag<C>(st, wm * C::TM + l32, 2 * h);
+    const Split3 sa1 = pipe::frag<C>(st, wm * C::TM + 32 + l32, 2 * h);
+    acc[0][0] = mfma_x6(b[0], sa0, acc[0][0]);
+    acc[1][0] = mfma_x6(b[0], sa1, acc[1][0]);
+    load_frag(0, kt + 1);
+    acc[0][1] = mfma_x6(b[1], sa0, acc[0][1]);
+    acc[1][1] = mfma_x6(b[1], sa1, acc[1][1]);
+    load_frag(1, kt + 1);
+    issue_a(stage(kt + 2), kt + 2);
+    wait_b<A_PW>(b);
+  }
+  pipe::wait_vm<0>();
+}
+
 // DB: two B register sets (the next K-step's fragments load during this step's MFMAs: 204 VGPRs, 2 waves / SIMD);
 // else one set, each fragment reloaded right after its last MFMA (3 waves / SIMD)
 template <bool STAGED, bool DB>
@@ -194,6 +237,67 @@ __global__ __launch_bounds__(256, DB ? 2 : 3) void gemm_f32_psb_kernel(const flo
   }
 }
 
+// 3 x 3 / pad 1 convolution (NHWC x [B, H, W, Cin], Cout % 128 == 0, Cin % 16 == 0) on the pre-split weight planes
+// of w [Cout, 3, 3, Cin] (= B [Cout, 9 Cin]); the A rows are the implicit im2col of the ring conv kernel
+// (conv3x3_f32.hip): a lane's DMA piece is 4 channels of its pixel shifted by the K-step's tap, zeros outside
+// the image.  Epilogue: bias / residual / ReLU (/ ReLU-mask of the residual) and the input-gradient extras (Epi2).
+__global__ __launch_bounds__(256, 3) void conv3x3_f32_psb_kernel(const float* __restrict__ x,
+                                                                 const u32v4* __restrict__ bs,
+                                                                 const float* __restrict__ bias,
+                                                                 const float* __restrict__ res,
+                                                                 float* __restrict__ out, int B, int H, int W,
+                                                                 int Cin, int Cout, int act, const pipe::Epi2 e2) {
+  using C = pipe::Cfg<kPsbBN, kPsbNS, 16, kPsbBM, 4>;
+  __shared__ __attribute__((aligned(16))) char ring[4 * kPsbAStage];
+  constexpr int A_PW = kPsbAStage / 1024 / 4;
+  const int HW = H * W;
+  const long M = static_cast<long>(B) * HW;
+  const int K = 9 * Cin, KT = K / 16;
+  const int ntn = Cout / kPsbBN;
+  const int wg = pipe::xcd_remap();
+  const long m0 = static_cast<long>(wg / ntn) * kPsbBM;
+  const int n0 = (wg % ntn) * kPsbBN;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid / C::WN, wn = wid % C::WN;
+  const int l32 = lane & 31, h = lane >> 5;
+  const i32x4 xr = pipe::rsrc(x, M * Cin * 4);
+  const long nbt = Cout / 32;
+  const i32x4 br = pipe::rsrc(bs, nbt * KT * 3 * 1024);
+  int a_pix[A_PW], a_ok[A_PW], a_c[A_PW];
+#pragma unroll
+  for (int c = 0; c < A_PW; ++c) {
+    const int row = C::dma_row(wid + 4 * c, lane);
+    const long m = m0 + row;
+    a_c[c] = 4 * C::dma_piece(row, lane);
+    a_pix[c] = static_cast<int>(m);
+    a_ok[c] = 0;
+    if (m < M) {
+      const int rem = static_cast<int>(m % HW);
+      const int yy = rem / W, xx = rem - yy * W;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int y2 = yy + t / 3 - 1, x2 = xx + t % 3 - 1;
+        a_ok[c] |= (y2 >= 0 && y2 < H && x2 >= 0 && x2 < W) << t;
+      }
+    }
+  }
+  auto issue_a = [&](char* st, int kt) {
+    const int k0 = kt * 16, tap = k0 / Cin, c0 = k0 - tap * Cin;
+    const int shift = (tap / 3 - 1) * W + (tap % 3 - 1);
+#pragma unroll
+    for (int c = 0; c < A_PW; ++c)
+      pipe::dma16(xr, st + (wid + 4 * c) * 1024,
+                  kt < KT && ((a_ok[c] >> tap) & 1) ? ((a_pix[c] + shift) * Cin + c0 + a_c[c]) * 4 : pipe::kOOB);
+  };
+  const int nb0 = (n0 + wn * C::TN) / 32;
+  int b_off[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b_off[j] = static_cast<int>((nb0 + j) * KT * 3 * 1024 + 16 * lane);
+  f16v acc[2][2];
+  psb_sb_loop<C, A_PW>(ring, issue_a, br, b_off, KT, acc, wm, l32, h);
+  pipe::store_tile<2, 2>(acc, out, bias, res, M, Cout, m0 + wm * C::TM, n0 + wn * C::TN, act, e2);
+}
+
 }  // namespace
 
 long presplit_b_bytes(int N, int K) {
@@ -227,6 +331,26 @@ void gemm_f32_psb(const float* a, const void* bsplit, const float* bias, const f
   else
     hipLaunchKernelGGL((gemm_f32_psb_kernel<true, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, a,
                        static_cast<const u32v4*>(bsplit), KT, bias, res, out, M, N, K, act);
+}
+
+// Cout % 128, Cin % 16 (every 16-deep K-step inside one tap), 32-bit offsets
+bool conv3x3_f32_psb_supported(long M, int Cin, int Cout) {
+  return Cout % kPsbBN == 0 && Cin % 16 == 0 && Cin > 0 && M * Cin * 4 < 0x7ffffff0L &&
+         presplit_b_bytes(Cout, 9 * Cin) < 0x7ffffff0L && M * Cout < 0x7ffffff0L;
+}
+
+void conv3x3_f32_psb(const float* x, const void* wsplit, const float* bias, const float* res, const float* res2,
+                     long res2_rows, const float* mask, float* out, int B, int H, int W, int Cin, int Cout, int act,
+                     hipStream_t s) {
+  const long M = static_cast<long>(B) * H * W;
+  const long nwg = (M + kPsbBM - 1) / kPsbBM * (Cout / kPsbBN);
+  if (nwg == 0) return;
+  pipe::Epi2 e2;
+  e2.res2 = res2;
+  e2.res2_rows = res2_rows;
+  e2.mask = mask;
+  hipLaunchKernelGGL(conv3x3_f32_psb_kernel, dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x,
+                     static_cast<const u32v4*>(wsplit), bias, res, out, B, H, W, Cin, Cout, act, e2);
 }
 
 }  // namespace as

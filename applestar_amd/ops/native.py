@@ -738,9 +738,18 @@ def embed_relu(table, idx):
 # Every conv / linear autograd node below runs on bf16 operands (the mixed-precision step: bf16 MFMA kernels) or
 # on fp32 operands (the fp32 step: f32-MFMA kernels conv3x3_f32.hip / wgrad_f32.hip); an fp32 operand is never
 # rounded to bf16.
-def _conv3(x, wk, bias, res, act_code):
-    """3x3 / pad 1 conv on NHWC x with a [Cout, 3, 3, Cin] weight, epilogue act code (_ACT / 4 = ReLU mask)."""
+def _conv3(x, wk, bias, res, act_code, w=None, dx=False, res2=None, mask=None):
+    """3x3 / pad 1 conv on NHWC x with a [Cout, 3, 3, Cin] weight wk, epilogue act code (_ACT / 4 = ReLU mask).
+    ``w``: the conv parameter wk derives from (wk = _conv_w(w), or _conv_wt(w) for ``dx``): fp32 convs with 128-multiple
+    outputs then run on its pre-split planes (gemm_f32_psb.hip conv3x3_f32_psb_kernel).  res2 / mask: the extended
+    input-gradient epilogue (conv3x3_f32_epi2)."""
     if x.dtype == torch.float32:
+        B, H, W, Cin = x.shape
+        Cout = wk.shape[0]
+        if w is not None and CONV_PSB and _C.conv3x3_f32_psb_supported(B * H * W, Cin, Cout):
+            return _C.conv3x3_f32_psb(x, _psb_conv(w, dx), Cout, bias, res, res2, mask, act_code)
+        if res2 is not None or mask is not None:
+            return _C.conv3x3_f32_epi2(x, wk, res, res2, mask)
         return _C.conv3x3_f32(x, wk, bias, res, act_code)
     return _C.conv3x3_fwd(x, wk, bias, res, act_code)
 
@@ -919,7 +928,7 @@ class _Conv3x3(torch.autograd.Function):
         if not wk.is_contiguous():
             wk = wk.contiguous()
         bias = _w32(b) if b is not None else None
-        out = _conv3(x_nhwc, wk, bias, res_nhwc, _ACT[act])
+        out = _conv3(x_nhwc, wk, bias, res_nhwc, _ACT[act], w_lp)
         if act == 'relu' and out.dtype == torch.float32:
             _note_relu_out(out)
         ctx.save_for_backward(x_nhwc, w_lp, out)
@@ -946,7 +955,7 @@ class _Conv3x3(torch.autograd.Function):
             dw, db = _wgrad(dpre.view(-1, cout), x, cin, has_b, bf, w)   # dW in [Cout,3,3,Cin] (channels_last) order
             dw = dw.view(cout, 3, 3, cin).permute(0, 3, 1, 2).to(w.dtype)
             db = db.to(ctx.b_dtype) if has_b else None
-        dx = _conv3(dpre, _conv_wt(w), None, None, 0)
+        dx = _conv3(dpre, _conv_wt(w), None, None, 0, w, True)
         side.join(dw, db)
         return (dx, dw, db, dpre if ctx.has_res else None, None)
 
@@ -1066,6 +1075,19 @@ def _psb(w, transposed=False):
     return _derived(w, 'psbT' if transposed else 'psb', lambda: (build(), build))
 
 
+CONV_PSB = os.environ.get('APPLESTAR_CONV_PSB', '1') == '1'
+
+
+def _psb_conv(w, dx=False):
+    """Pre-split planes of a 3x3 conv's weight operand: [Cout, 3, 3, Cin] (forward) or the flipped transpose
+    [Cin, 3, 3, Cout] (input gradient, built from the _conv_wt form); a derived form of the parameter."""
+    def build(into=None):
+        wk = _conv_wt(w) if dx else _conv_w(w)
+        wk = wk.reshape(wk.shape[0], -1)
+        return _C.presplit_b(wk if wk.is_contiguous() else wk.contiguous(), False, into)
+    return _derived(w, 'psbcT' if dx else 'psbc', lambda: (build(), build))
+
+
 def _w32(t):
     """t as a contiguous fp32 tensor (a bias, a small weight); a derived form for parameters."""
     if t.dtype == torch.float32 and t.is_contiguous():
@@ -1096,8 +1118,8 @@ def _conv_dx_drelu(dpre, w, y):
     """Input gradient of a 3x3 conv whose input y is a ReLU output, already gated by (y > 0): the gate
     is the dX conv's epilogue mode 4 (no separate read-modify-write pass over the activation)."""
     if FUSED_DRELU:
-        return _conv3(dpre, _conv_wt(w), None, y, 4)
-    return _act_grad(_conv3(dpre, _conv_wt(w), None, None, 0), y, True)
+        return _conv3(dpre, _conv_wt(w), None, y, 4, w, True)
+    return _act_grad(_conv3(dpre, _conv_wt(w), None, None, 0, w, True), y, True)
 
 
 def _conv_dw(dpre, x, w, b_dtype):
@@ -1142,8 +1164,8 @@ class _ResBlock(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, link=None):
         _count_use(w1)
         _count_use(w2)
-        y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1)
-        out = _conv3(y1, _conv_w(w2), _w32(b2), x, 1)
+        y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1, w1)
+        out = _conv3(y1, _conv_w(w2), _w32(b2), x, 1, w2)
         ctx.save_for_backward(x, w1, w2, y1, out)
         ctx.b_dtypes = (b1.dtype, b2.dtype)
         ctx.link = link
@@ -1177,11 +1199,11 @@ class _ResBlock(torch.autograd.Function):
         C = x.shape[-1]
         if x.dtype == torch.float32 and (g is not None or ctx.mask_in) and _C.conv3x3_f32_epi2_supported(C, C):
             # + skip gradient + the location head's hand-over (first rows), masked by this input's own ReLU
-            dx = _C.conv3x3_f32_epi2(dpre1, _conv_wt(w1), dpre2, g, x if ctx.mask_in else None)
+            dx = _conv3(dpre1, _conv_wt(w1), None, dpre2, 0, w1, True, g, x if ctx.mask_in else None)
             if ctx.mask_in:
                 _MASKED_DX[x.data_ptr()] = (dx, dx._version)
         else:
-            dx = _conv3(dpre1, _conv_wt(w1), None, dpre2, 0)       # + skip gradient, fused
+            dx = _conv3(dpre1, _conv_wt(w1), None, dpre2, 0, w1, True)       # + skip gradient, fused
             if g is not None:
                 dx[:g.shape[0]] += g
         side.join(dw1, db1, dw2, db2)
@@ -1236,8 +1258,8 @@ class _GatedResBlock(torch.autograd.Function):
         for p in (w1, w2, *gate[0::2]):
             _count_use(p)
         B, H, W, C = x.shape
-        y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1)
-        y = _conv3(y1, _conv_w(w2), _w32(b2), None, 0)
+        y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1, w1)
+        y = _conv3(y1, _conv_w(w2), _w32(b2), None, 0, w2)
         h = x.view(-1, C)
         acts = [h]
         if GATE_CHAIN and C == 128 and x.dtype == torch.bfloat16:
@@ -1325,7 +1347,7 @@ class _GatedResBlock(torch.autograd.Function):
         with side.fork():
             dw1, db1 = _conv_dw(dpre1, x, w1, ctx.dtypes[0])
             db1 = db1.to(ctx.dtypes[0])
-        dx = _conv3(dpre1, _conv_wt(w1), None, dx_gate.view(B, H, W, C).contiguous(), 0)
+        dx = _conv3(dpre1, _conv_wt(w1), None, dx_gate.view(B, H, W, C).contiguous(), 0, w1, True)
         side.join(dw1, db1, dw2, db2)
         gate_grads = [None] * 8
         for i, dw_i, db_i in grads_g:

@@ -283,3 +283,29 @@ def test_gemm_f32_psb_matches_fp64(variant, shape):
     ref = (a.double() @ b.double().t() + bias.double() + res.double()).relu()
     err = (out.double() - ref).abs().max().item()
     assert err < 2e-5 * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize('mode', ['bias_relu', 'res', 'drelu', 'epi2'])
+def test_conv3x3_f32_psb_matches_ring(mode):
+    """fp32 3x3 conv on pre-split weight planes == the ring conv kernel (same split products: to fp32 summation
+    order), every epilogue the learner uses; ragged pixel count."""
+    from applestar_amd.ops import native as N
+    C = N.ensure_loaded()
+    torch.manual_seed(8)
+    B, H, W, Ci, Co = 5, 19, 20, 128, 128
+    x = torch.randn(B, H, W, Ci, device=DEV)
+    w = torch.randn(Co, 3, 3, Ci, device=DEV) / 30
+    bias = torch.randn(Co, device=DEV)
+    res = torch.randn(B, H, W, Co, device=DEV)
+    res2 = torch.randn(3, H, W, Co, device=DEV)
+    mask = torch.randn(B, H, W, Co, device=DEV)
+    ws = C.presplit_b(w.view(Co, -1))
+    if mode == 'bias_relu':
+        got, ref = C.conv3x3_f32_psb(x, ws, Co, bias, None, None, None, 1), C.conv3x3_f32(x, w, bias, None, 1)
+    elif mode == 'res':
+        got, ref = C.conv3x3_f32_psb(x, ws, Co, bias, res, None, None, 0), C.conv3x3_f32(x, w, bias, res, 0)
+    elif mode == 'drelu':
+        got, ref = C.conv3x3_f32_psb(x, ws, Co, None, res, None, None, 4), C.conv3x3_f32(x, w, None, res, 4)
+    else:
+        got, ref = C.conv3x3_f32_psb(x, ws, Co, None, res, res2, mask, 0), C.conv3x3_f32_epi2(x, w, res, res2, mask)
+    assert (got - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
