@@ -867,6 +867,42 @@ at::Tensor presplit_b(const at::Tensor& b, bool trans, const c10::optional<at::T
   return o;
 }
 
+// presplit_b(srcs[i], trans[i], outs[i]) for every i, in launches of up to 48 weights
+void multi_presplit(const std::vector<at::Tensor>& srcs, const std::vector<bool>& trans,
+                    const std::vector<at::Tensor>& outs) {
+  TORCH_CHECK(srcs.size() == trans.size() && srcs.size() == outs.size(), "multi_presplit: list sizes");
+  if (srcs.empty()) return;
+  c10::hip::HIPGuard g(srcs[0].device().index());
+  as::PresplitArgs a;
+  a.n = 0;
+  a.block_start[0] = 0;
+  auto flush = [&]() {
+    if (a.n > 0) as::multi_presplit(a, stream());
+    a.n = 0;
+    a.block_start[0] = 0;
+  };
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    const at::Tensor& b = srcs[i];
+    check_cuda(b, "src");
+    TORCH_CHECK(b.dim() == 2 && b.scalar_type() == at::kFloat && b.is_contiguous(), "multi_presplit: fp32 matrices");
+    const int N = static_cast<int>(trans[i] ? b.size(1) : b.size(0)), K = static_cast<int>(trans[i] ? b.size(0) : b.size(1));
+    TORCH_CHECK(outs[i].scalar_type() == at::kByte && outs[i].is_contiguous() &&
+                    outs[i].numel() == as::presplit_b_bytes(N, K) && outs[i].device() == b.device(),
+                "multi_presplit: out buffer size");
+    const long total = static_cast<long>((N + 31) / 32) * ((K + 15) / 16) * 64;
+    if (total == 0) continue;
+    if (a.n == as::kPresplitMax) flush();
+    a.src[a.n] = b.data_ptr<float>();
+    a.dst[a.n] = outs[i].data_ptr();
+    a.N[a.n] = N;
+    a.K[a.n] = K;
+    a.trans[a.n] = trans[i] ? 1 : 0;
+    a.block_start[a.n + 1] = a.block_start[a.n] + static_cast<int>((total + 255) / 256);
+    ++a.n;
+  }
+  flush();
+}
+
 bool gemm_f32_psb_supported(int64_t M, int64_t N, int64_t K) {
   return as::gemm_f32_psb_supported(M, static_cast<int>(N), static_cast<int>(K));
 }
@@ -2197,6 +2233,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("multi_logp", &multi_logp);
   m.def("presplit_b", &presplit_b, py::arg("b"), py::arg("trans") = false, py::arg("out") = py::none());
   m.def("gemm_f32_psb_supported", &gemm_f32_psb_supported);
+  m.def("multi_presplit", &multi_presplit);
   m.def("conv3x3_f32_psb_supported", &conv3x3_f32_psb_supported);
   m.def("conv3x3_f32_psb", &conv3x3_f32_psb, py::arg("x"), py::arg("wsplit"), py::arg("Cout"),
         py::arg("bias") = py::none(), py::arg("res") = py::none(), py::arg("res2") = py::none(),

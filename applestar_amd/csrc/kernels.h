@@ -349,6 +349,16 @@ void multi_logp(const LogpArgs& a, hipStream_t s);
 long presplit_b_bytes(int N, int K);
 void presplit_b(const float* b, int N, int K, bool trans, void* out, hipStream_t s);
 bool gemm_f32_psb_supported(long M, int N, int K);
+constexpr int kPresplitMax = 48;
+struct PresplitArgs {                    // passed by value (~1.6 KB of kernel arguments)
+  int n;
+  int block_start[kPresplitMax + 1];
+  const float* src[kPresplitMax];
+  void* dst[kPresplitMax];
+  int N[kPresplitMax], K[kPresplitMax];
+  unsigned char trans[kPresplitMax];
+};
+void multi_presplit(const PresplitArgs& a, hipStream_t s);
 void gemm_f32_psb(const float* a, const void* bsplit, const float* bias, const float* res, float* out, long M, int N,
                   int K, int act, int variant, hipStream_t s);
 // 3 x 3 conv on the pre-split planes of w [Cout, 3, 3, Cin] (presplit_b of its [Cout, 9 Cin] view); res2 / mask:

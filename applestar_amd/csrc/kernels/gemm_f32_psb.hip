@@ -47,6 +47,34 @@ __global__ __launch_bounds__(256) void presplit_b_kernel(const float* __restrict
   o[128] = s.p[2];
 }
 
+// many weights' planes in one launch (the per-optimizer-step rebuild of every pre-split form)
+__global__ __launch_bounds__(256) void multi_presplit_kernel(const PresplitArgs a) {
+  const int blk = blockIdx.x;
+  int t = 0;
+  while (t + 1 < a.n && a.block_start[t + 1] <= blk) ++t;
+  const int N = a.N[t], K = a.K[t], KT = (K + 15) / 16;
+  const long total = static_cast<long>((N + 31) / 32) * KT * 64;
+  const long gid = static_cast<long>(blk - a.block_start[t]) * 256 + threadIdx.x;
+  if (gid >= total) return;
+  const float* b = a.src[t];
+  const bool trans = a.trans[t] != 0;
+  const int lane = static_cast<int>(gid & 63);
+  const long rest = gid >> 6;
+  const int kt = static_cast<int>(rest % KT);
+  const long nb = rest / KT;
+  const long n = nb * 32 + (lane & 31);
+  const int k0 = kt * 16 + 8 * (lane >> 5);
+  float v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    v[q] = (n < N && k0 + q < K) ? (trans ? b[static_cast<long>(k0 + q) * N + n] : b[n * K + k0 + q]) : 0.f;
+  const Split3 sp = split8(v);
+  u32v4* o = static_cast<u32v4*>(a.dst[t]) + (nb * KT + kt) * 3 * 64 + lane;
+  o[0] = sp.p[0];
+  o[64] = sp.p[1];
+  o[128] = sp.p[2];
+}
+
 // 16 B of a B fragment plane into registers, outside the compiler's waitcnt tracking (counted with the DMA ring)
 __device__ __forceinline__ void bload(u32v4& dst, i32x4 r, int voff) {
   asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(dst) : "v"(voff), "s"(r) : "memory");
@@ -351,6 +379,11 @@ void conv3x3_f32_psb(const float* x, const void* wsplit, const float* bias, cons
   e2.mask = mask;
   hipLaunchKernelGGL(conv3x3_f32_psb_kernel, dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s, x,
                      static_cast<const u32v4*>(wsplit), bias, res, out, B, H, W, Cin, Cout, act, e2);
+}
+
+void multi_presplit(const PresplitArgs& a, hipStream_t s) {
+  const int nblk = a.block_start[a.n];
+  if (nblk > 0) hipLaunchKernelGGL(multi_presplit_kernel, dim3(nblk), dim3(256), 0, s, a);
 }
 
 }  // namespace as

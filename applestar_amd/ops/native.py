@@ -1031,8 +1031,15 @@ class DerivedWeights:
             spec += f[2]
         if fs:
             ensure_loaded().multi_strided_copy([f[1] for f in fs], [f[0].detach() for f in fs], spec)
+        for f in fs:                # current before the pre-split rebuilds read them (a conv's transposed form)
+            f[3], f[4] = self.epoch, f[0]._version
+        # pre-split weight planes: every form in one batched launch (multi_presplit); other custom forms one by one
+        ps = [f for f in self.forms.values() if callable(f[2]) and getattr(f[2], 'psb_src', None) is not None]
+        if ps:
+            ensure_loaded().multi_presplit([f[2].psb_src() for f in ps], [f[2].psb_trans for f in ps],
+                                           [f[1] for f in ps])
         for f in self.forms.values():
-            if callable(f[2]):
+            if callable(f[2]) and getattr(f[2], 'psb_src', None) is None:
                 f[2](f[1])
         for f in self.forms.values():
             f[3], f[4] = self.epoch, f[0]._version
@@ -1069,9 +1076,13 @@ def _psb_ok(M, N, K):
 def _psb(w, transposed=False):
     """Pre-split planes of the GEMM B operand: w [N, K] itself, or (transposed) w^T [K_in, N_out] for the dX
     product; a derived form of a parameter (rebuilt in place by presplit_b after each optimizer step)."""
+    def src():
+        t = w.detach().reshape(w.shape[0], -1)
+        return t if t.is_contiguous() else t.contiguous()
+
     def build(into=None):
-        src = w.detach().reshape(w.shape[0], -1)
-        return _C.presplit_b(src if src.is_contiguous() else src.contiguous(), transposed, into)
+        return _C.presplit_b(src(), transposed, into)
+    build.psb_src, build.psb_trans = src, transposed        # DerivedWeights.refresh batches these rebuilds
     return _derived(w, 'psbT' if transposed else 'psb', lambda: (build(), build))
 
 
@@ -1081,10 +1092,14 @@ CONV_PSB = os.environ.get('APPLESTAR_CONV_PSB', '1') == '1'
 def _psb_conv(w, dx=False):
     """Pre-split planes of a 3x3 conv's weight operand: [Cout, 3, 3, Cin] (forward) or the flipped transpose
     [Cin, 3, 3, Cout] (input gradient, built from the _conv_wt form); a derived form of the parameter."""
-    def build(into=None):
+    def src():
         wk = _conv_wt(w) if dx else _conv_w(w)
         wk = wk.reshape(wk.shape[0], -1)
-        return _C.presplit_b(wk if wk.is_contiguous() else wk.contiguous(), False, into)
+        return wk if wk.is_contiguous() else wk.contiguous()
+
+    def build(into=None):
+        return _C.presplit_b(src(), False, into)
+    build.psb_src, build.psb_trans = src, False             # DerivedWeights.refresh batches these rebuilds
     return _derived(w, 'psbcT' if dx else 'psbc', lambda: (build(), build))
 
 

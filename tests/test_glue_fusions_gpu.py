@@ -309,3 +309,28 @@ def test_conv3x3_f32_psb_matches_ring(mode):
     else:
         got, ref = C.conv3x3_f32_psb(x, ws, Co, None, res, res2, mask, 0), C.conv3x3_f32_epi2(x, w, res, res2, mask)
     assert (got - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
+
+
+def test_derived_psb_forms_refresh_batched():
+    """The pre-split weight forms are rebuilt in place by ONE batched launch per optimizer step (DerivedWeights
+    .refresh -> multi_presplit): after a weight update + refresh the cached planes equal a fresh presplit_b."""
+    from applestar_amd.ops import native as N
+    C = N.ensure_loaded()
+    torch.manual_seed(9)
+    reg = N.DerivedWeights()
+    lin = torch.nn.Parameter(torch.randn(256, 384, device=DEV))
+    conv = torch.nn.Parameter(torch.randn(128, 128, 3, 3, device=DEV).contiguous(memory_format=torch.channels_last))
+    for p in (lin, conv):
+        p._derived_forms = reg
+    f1, f2, f3 = N._psb(lin), N._psb(lin, True), N._psb_conv(conv, True)
+    ptrs = [t.data_ptr() for t in (f1, f2, f3)]
+    with torch.no_grad():
+        lin.add_(0.5)
+        conv.mul_(-1.0)
+    reg.refresh()
+    g1, g2, g3 = N._psb(lin), N._psb(lin, True), N._psb_conv(conv, True)
+    assert [t.data_ptr() for t in (g1, g2, g3)] == ptrs                     # rebuilt in place (graph-safe)
+    assert torch.equal(g1, C.presplit_b(lin.detach()))
+    assert torch.equal(g2, C.presplit_b(lin.detach(), True))
+    wt = conv.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous().view(128, -1)
+    assert torch.equal(g3, C.presplit_b(wt))

@@ -53,10 +53,11 @@ def _learner_main(comm, B, T, gpu, precision, iq, graph_step=False):
     def timed(data):
         t0 = time.time()
         out = orig(data)
+        th = time.time()                 # the step's host side (launches, Python) is done
         if gpu:
             torch.cuda.synchronize()
         t1 = time.time()
-        iq.put((t1, lrn.last_iter.val + 1, t1 - t0))
+        iq.put((t1, lrn.last_iter.val + 1, t1 - t0, th - t0))
         return out
     lrn._train = timed
     lrn.run(max_iterations=1000000)
@@ -150,6 +151,7 @@ def main():
            # time inside the learner's train step (incl. the GPU finishing it) vs the whole iteration: the rest is
            # the learner waiting for / assembling data
            'learner_train_ms_mean': round(1e3 * sum(r[2] for r in win) / max(len(win), 1), 1),
+           'learner_train_host_ms_mean': round(1e3 * sum(r[3] for r in win) / max(len(win), 1), 1),
            'learner_iter_ms_mean': round(1e3 * dt / max(n_it, 1), 1),
            'fresh_samples_per_s': round(pushed * T / dt, 1),
            'startup_s': round(t0 - t_start, 1),
