@@ -179,15 +179,33 @@ def _post_json(ip: str, port: int, path: str, obj: dict, timeout: float = 30.0):
 
 
 # ----------------------------------------------------------------------------- payload server
+def _recv_into_all(sock: socket.socket, view, n: int, timeout: Optional[float] = None) -> None:
+    """Fill view[:n] from the socket in (usually) ONE blocking ``recv(MSG_WAITALL)``: the kernel copies the whole
+    payload while the GIL stays released.  The chunked loop of a socket with a Python timeout (non-blocking fd,
+    ~64 KB per call, the GIL re-taken for every chunk) starved the learner's launch thread of the GIL while a
+    trajectory was arriving: its step took 280 ms instead of 55 (profiles/r5v_pipeline_learner_threads.txt).
+    ``timeout``: an OS-level receive timeout (SO_RCVTIMEO) instead of Python's, so a dead peer still raises."""
+    prev = sock.gettimeout()
+    if timeout is None:
+        timeout = prev
+    sock.settimeout(None)
+    if timeout:
+        sec = int(timeout)
+        sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVTIMEO, struct.pack('ll', sec, int((timeout - sec) * 1e6)))
+    try:
+        got = 0
+        while got < n:
+            k = sock.recv_into(view[got:n], n - got, socket.MSG_WAITALL)
+            if k == 0:
+                raise ConnectionError('peer closed')
+            got += k
+    finally:
+        sock.settimeout(prev)
+
+
 def _recv_exact(sock: socket.socket, n: int) -> bytearray:
     buf = bytearray(n)
-    view = memoryview(buf)
-    got = 0
-    while got < n:
-        k = sock.recv_into(view[got:], n - got)
-        if k == 0:
-            raise ConnectionError('peer closed')
-        got += k
+    _recv_into_all(sock, memoryview(buf), n)
     return buf
 
 
@@ -268,12 +286,7 @@ def fetch(ip: str, port: int, key: str, timeout: float = 60.0, alloc=None):
             return _recv_exact(s, n)
         buf = alloc(n)
         view = memoryview(buf)[:n]
-        got = 0
-        while got < n:
-            r = s.recv_into(view[got:], n - got)
-            if r == 0:
-                raise ConnectionError('peer closed')
-            got += r
+        _recv_into_all(s, view, n, timeout)
         return view
 
 

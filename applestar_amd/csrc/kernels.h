@@ -341,6 +341,8 @@ struct LogpArgs {
   float* out[kLogpMaxH];
   int cols[kLogpMaxH];
   unsigned char bf16[kLogpMaxH];
+  long blk_start[kLogpMaxH + 1];       // set by multi_logp: first workgroup of each head
+  unsigned char big[kLogpMaxH];        // set by multi_logp: a whole workgroup per row (wide rows)
 };
 void multi_logp(const LogpArgs& a, hipStream_t s);
 

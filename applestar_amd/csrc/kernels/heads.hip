@@ -43,8 +43,10 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   return v;
 }
 
-// inverse-CDF draw over row[0..C) (already scaled / masked, fp32 in `row`): returns the index on every thread
-__device__ int sample_row(const float* __restrict__ row, int C, float u, float* red, float* scan) {
+// inverse-CDF draw over row[0..C) (already scaled / masked, fp32 in `row`: LDS when it fits): returns the index on
+// every thread.  Segment sums are scanned per wave (shuffles) and across the 4 waves through LDS - one barrier where
+// the Hillis-Steele LDS scan took 16.
+__device__ __forceinline__ int sample_row(const float* __restrict__ row, int C, float u, float* red, float* scan) {
   float mx = kNeg * 2.f;
   for (int i = threadIdx.x; i < C; i += kHT) mx = fmaxf(mx, row[i]);
   mx = block_max(mx, red);
@@ -52,22 +54,26 @@ __device__ int sample_row(const float* __restrict__ row, int C, float u, float* 
   const int s0 = threadIdx.x * seg, s1 = min(C, s0 + seg);
   float part = 0.f;
   for (int i = s0; i < s1; ++i) part += __expf(row[i] - mx);
-  scan[threadIdx.x] = part;
-  __syncthreads();
-  // inclusive scan of the 256 segment sums (Hillis-Steele in LDS)
-  for (int off = 1; off < kHT; off <<= 1) {
-    const float add = threadIdx.x >= off ? scan[threadIdx.x - off] : 0.f;
-    __syncthreads();
-    scan[threadIdx.x] += add;
-    __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float incl = part;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(incl, o, kWave);
+    if (lane >= o) incl += y;
   }
-  const float total = scan[kHT - 1];
-  const float target = u * total;
+  float excl = __shfl_up(incl, 1, kWave);   // the neighbour's inclusive value exactly: no gap / overlap by rounding
+  if (lane == 0) excl = 0.f;
+  if (lane == 63) scan[wv] = incl;
   __shared__ int pick;
   if (threadIdx.x == 0) pick = C - 1;
   __syncthreads();
-  const float before = threadIdx.x ? scan[threadIdx.x - 1] : 0.f;
-  if (s0 < s1 && scan[threadIdx.x] > target && before <= target) {
+  float woff = 0.f;
+  for (int w = 0; w < wv; ++w) woff += scan[w];
+  const float total = scan[0] + scan[1] + scan[2] + scan[3];
+  const float target = u * total;
+  incl += woff;
+  const float before = excl + woff;
+  if (s0 < s1 && incl > target && before <= target) {
     float run = before;
     int idx = s1 - 1;
     for (int i = s0; i < s1; ++i) {
@@ -82,6 +88,8 @@ __device__ int sample_row(const float* __restrict__ row, int C, float u, float* 
   return r;
 }
 
+constexpr int kRowLds = 24576;   // rows up to this many logits are staged in LDS (the location head's 24,320)
+
 template <typename TL, typename TW>
 __global__ __launch_bounds__(kHT) void head_sample_kernel(const TL* __restrict__ logits, long ld_logits, int C,
                                                           float inv_t, const uint8_t* __restrict__ mask, long mask_ld,
@@ -90,17 +98,20 @@ __global__ __launch_bounds__(kHT) void head_sample_kernel(const TL* __restrict__
                                                           int D, float* __restrict__ out_logits,
                                                           int64_t* __restrict__ action, float* __restrict__ emb) {
   __shared__ float red[4];
-  __shared__ float scan[kHT];
+  __shared__ float scan[4];
+  __shared__ float srow[kRowLds];
   const int b = blockIdx.x;
   const long len = lens ? lens[b] : C;
   float* row = out_logits + static_cast<long>(b) * C;
+  const bool lds = C <= kRowLds;
   for (int i = threadIdx.x; i < C; i += kHT) {
     float v = ld(logits, static_cast<long>(b) * ld_logits + i) * inv_t;
     if ((mask && !mask[static_cast<long>(b) * mask_ld + i]) || i >= len) v = kNeg;
     row[i] = v;
+    if (lds) srow[i] = v;
   }
   __syncthreads();
-  const int a = sample_row(row, C, u[b], red, scan);
+  const int a = lds ? sample_row(srow, C, u[b], red, scan) : sample_row(row, C, u[b], red, scan);
   if (threadIdx.x == 0) action[b] = a;
   if (table) {
     for (int d = threadIdx.x; d < D; d += kHT)
@@ -188,36 +199,73 @@ void target_unit_sample(const void* e, int e_dt, const float* w1, const float* b
 
 namespace {
 // one wave per row of any head: row max, sum of exp, the taken action's logit
+// (m, s) pairs of an online log-sum-exp: s = sum exp(x - m)
+__device__ __forceinline__ void lse_merge(float& m, float& s, float om, float os) {
+  const float nm = fmaxf(m, om);
+  if (nm == -INFINITY) return;
+  s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + (om == -INFINITY ? 0.f : os * __expf(om - nm));
+  m = nm;
+}
+
+// Narrow heads: one wave per row, 4 rows per workgroup.  Wide heads (the location head's 24,320 logits per row):
+// a whole workgroup per row - one wave per row walked 380 dependent-latency loads per lane twice (~0.4 ms at B = 1).
+// Single pass: an online log-sum-exp per thread, 4 loads in flight, then wave and workgroup merges.
 __global__ __launch_bounds__(256) void multi_logp_kernel(const LogpArgs a) {
-  const long row = static_cast<long>(blockIdx.x) * 4 + (threadIdx.x >> 6);
-  if (row >= a.row_start[a.nheads]) return;
+  __shared__ float red_m[4], red_s[4];
+  const long blk = blockIdx.x;
+  if (blk >= a.blk_start[a.nheads]) return;
   int h = 0;
-  while (h + 1 < a.nheads && a.row_start[h + 1] <= row) ++h;
-  const long r = row - a.row_start[h];
+  while (h + 1 < a.nheads && a.blk_start[h + 1] <= blk) ++h;
+  const long rows_h = a.row_start[h + 1] - a.row_start[h];
+  const bool big = a.big[h] != 0;
+  const long r = big ? blk - a.blk_start[h] : (blk - a.blk_start[h]) * 4 + (threadIdx.x >> 6);
+  if (!big && r >= rows_h) return;          // whole waves (the wide path below keeps every wave)
   const int C = a.cols[h], lane = threadIdx.x & 63;
+  const int t = big ? static_cast<int>(threadIdx.x) : lane, nt = big ? 256 : 64;
   const bool b16 = a.bf16[h] != 0;
   auto ld = [&](long i) {
     return b16 ? bf2f(static_cast<const bf16_t*>(a.logits[h])[i]) : static_cast<const float*>(a.logits[h])[i];
   };
   const long base = r * C;
-  float m = -INFINITY;
-  for (int c = lane; c < C; c += 64) m = fmaxf(m, ld(base + c));
-  m = wave_max(m);
-  float s = 0.f;
-  for (int c = lane; c < C; c += 64) s += __expf(ld(base + c) - m);
-  s = wave_sum(s);
-  if (lane == 0) {
-    long act = a.action[h][r];
-    act = act < 0 ? 0 : (act >= C ? C - 1 : act);
-    a.out[h][r] = ld(base + act) - m - __logf(s);
+  float m = -INFINITY, s = 0.f;
+  int c = t;
+  for (; c + 3 * nt < C; c += 4 * nt) {
+    const float x0 = ld(base + c), x1 = ld(base + c + nt), x2 = ld(base + c + 2 * nt), x3 = ld(base + c + 3 * nt);
+    const float xm = fmaxf(fmaxf(x0, x1), fmaxf(x2, x3));
+    const float nm = fmaxf(m, xm);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - nm)) + __expf(x0 - nm) + __expf(x1 - nm) + __expf(x2 - nm) +
+        __expf(x3 - nm);
+    m = nm;
   }
+  for (; c < C; c += nt) lse_merge(m, s, ld(base + c), 1.f);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lse_merge(m, s, __shfl_xor(m, o, kWave), __shfl_xor(s, o, kWave));
+  if (big) {
+    if (lane == 0) { red_m[threadIdx.x >> 6] = m; red_s[threadIdx.x >> 6] = s; }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    m = red_m[0];
+    s = red_s[0];
+    for (int w = 1; w < 4; ++w) lse_merge(m, s, red_m[w], red_s[w]);
+  } else if (lane != 0) {
+    return;
+  }
+  long act = a.action[h][r];
+  act = act < 0 ? 0 : (act >= C ? C - 1 : act);
+  a.out[h][r] = ld(base + act) - m - __logf(s);
 }
 }  // namespace
 
-void multi_logp(const LogpArgs& a, hipStream_t s) {
-  const long rows = a.row_start[a.nheads];
-  if (rows > 0)
-    hipLaunchKernelGGL(multi_logp_kernel, dim3(static_cast<unsigned>((rows + 3) / 4)), dim3(256), 0, s, a);
+void multi_logp(const LogpArgs& args, hipStream_t s) {
+  LogpArgs a = args;
+  a.blk_start[0] = 0;
+  for (int h = 0; h < a.nheads; ++h) {
+    const long rows = a.row_start[h + 1] - a.row_start[h];
+    a.big[h] = a.cols[h] >= 4096 ? 1 : 0;
+    a.blk_start[h + 1] = a.blk_start[h] + (a.big[h] ? rows : (rows + 3) / 4);
+  }
+  if (a.blk_start[a.nheads] > 0)
+    hipLaunchKernelGGL(multi_logp_kernel, dim3(static_cast<unsigned>(a.blk_start[a.nheads])), dim3(256), 0, s, a);
 }
 
 }  // namespace as

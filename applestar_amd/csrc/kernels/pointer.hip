@@ -12,8 +12,11 @@
 //
 // The fold is exact algebra: query_fc1(ae0 + We2 he + be2) = (Wq1 ae0 + bq1) + Wq1 We2 he + Wq1 be2,
 // so the per-step 1024-d autoregressive embedding never materialises (c0 = Wq1 ae0 + bq1 is one
-// batched GEMM before the launch).  Weights live in registers for all steps (thread i owns row i
-// of Wf / We1, a 32-slice of Wq2, and LSTM gate row i); keys [N+1,32] are staged once in LDS.
+// batched GEMM before the launch).  Weights stay on-chip for all steps: thread i owns row i of Wf / We1 in
+// registers; keys [N+1,32], the Wq2 slices and the LSTM gate weights (wave 0's lane l: rows l and l + 64) are
+// staged once in LDS.  A step has 7 block barriers (was 19): the LSTM cell runs in wave 0 alone on wave
+// reductions, the sampling max / scan exchange wave totals through parity-alternating LDS slots, the owner
+// of the inverse-CDF pick is found by one wave ballot, and every thread keeps the running key sum itself.
 // Semantics match the reference loop: end token masked at step 0, sampled units masked afterwards,
 // su_num = step+1 when the end token is drawn, extra_units = logits > end logit at the last step for
 // rows that never drew the end token.  Rows end independently (a row's later steps are unused).
@@ -29,34 +32,6 @@ constexpr int kF = 256;      // func dim
 constexpr int kMaxN1 = 513;  // 512 entities + end token
 constexpr int kChunk = 3;    // ceil(513 / 256)
 constexpr float kNeg = -1e9f;
-
-__device__ __forceinline__ float block_sum(float v, float* red, int tid) {
-  v = wave_sum(v);
-  if ((tid & 63) == 0) red[tid >> 6] = v;
-  __syncthreads();
-  float r = red[0] + red[1] + red[2] + red[3];
-  __syncthreads();
-  return r;
-}
-
-__device__ __forceinline__ float block_max(float v, float* red, int tid) {
-  v = wave_max(v);
-  if ((tid & 63) == 0) red[tid >> 6] = v;
-  __syncthreads();
-  float r = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  __syncthreads();
-  return r;
-}
-
-// sum over the 128 threads of waves 0-1 (waves 2-3 pass 0)
-__device__ __forceinline__ float sum128(float v, float* red, int tid) {
-  v = wave_sum(v);
-  if ((tid & 63) == 0) red[tid >> 6] = v;
-  __syncthreads();
-  float r = red[0] + red[1];
-  __syncthreads();
-  return r;
-}
 
 template <typename KT>
 __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
@@ -77,16 +52,16 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
   const int en = n1 - 1;
 
   __shared__ float s_key[kMaxN1 * kQ];
+  __shared__ float s_wih[kQ * 4 * kQ];   // [k][gate row]
+  __shared__ float s_whh[kQ * 4 * kQ];
+  __shared__ float s_wq2[32 * kThreads];
   __shared__ uint8_t s_sel[kMaxN1 + 3];
-  __shared__ float s_he[kF];
+  __shared__ __align__(16) float s_he[kF];
   __shared__ float s_x[kF];
   __shared__ float s_qin[kQ];
   __shared__ float s_h[kQ];
   __shared__ float s_q[kQ];
-  __shared__ float s_gates[4 * kQ];
-  __shared__ float s_emb[kQ];
-  __shared__ float s_red[16];
-  __shared__ float s_scan[4];
+  __shared__ float s_red[16];   // two parity halves: 4 wave maxima + 4 wave scan totals each
   __shared__ int s_result;
 
   const long kb = static_cast<long>(b) * key_bstride;
@@ -108,23 +83,28 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
   const float be1_i = be1[tid];
   // qin: thread (o = tid>>3, p = tid&7) owns Wq2[o, p*32 : p*32+32]
   const int qo = tid >> 3, qp = tid & 7;
-  float wq2_s[32];
-#pragma unroll
-  for (int k = 0; k < 32; ++k) wq2_s[k] = wq2[qo * kF + qp * 32 + k];
+  // (in LDS as [k][thread]: conflict-free, and the registers stay below the 256 architectural VGPRs)
+#pragma unroll 4
+  for (int k = 0; k < 32; ++k) s_wq2[k * kThreads + tid] = wq2[qo * kF + qp * 32 + k];
   const float bq2_o = bq2[qo];
-  // LSTM gate row tid (< 128)
-  const int gr = tid < 4 * kQ ? tid : 0;
-  float wih_r[kQ], whh_r[kQ];
-#pragma unroll
-  for (int k = 0; k < kQ; ++k) {
-    wih_r[k] = wih[gr * kQ + k];
-    whh_r[k] = whh[gr * kQ + k];
+  // LSTM: wave 0 runs the whole cell (no block barriers); lane l owns gate rows l and l + 64 (i / f rows in
+  // the first, g / o rows in the second), so LN_i / LN_h statistics are wave reductions and the cell's f / o
+  // inputs arrive from lane l + 32 by a cross-lane read
+  // (the gate weights sit in LDS, k-major so a wave's row reads are conflict-free: the registers are full)
+  const int gr = tid & 63;
+  for (int i = tid; i < 4 * kQ * kQ; i += kThreads) {
+    const int row = i / kQ, k = i % kQ;
+    s_wih[k * 4 * kQ + row] = wih[i];
+    s_whh[k * 4 * kQ + row] = whh[i];
   }
-  const float lniw = lni_w[gr], lnib = lni_b[gr], lnhw = lnh_w[gr], lnhb = lnh_b[gr];
+  const float lniw0 = lni_w[gr], lnib0 = lni_b[gr], lnhw0 = lnh_w[gr], lnhb0 = lnh_b[gr];
+  const float lniw1 = lni_w[gr + 64], lnib1 = lni_b[gr + 64], lnhw1 = lnh_w[gr + 64], lnhb1 = lnh_b[gr + 64];
   const float lncw = lnc_w[tid & 31], lncb = lnc_b[tid & 31];
+  const int nwaves_valid = min((n1 + 64 * kChunk - 1) / (64 * kChunk), kThreads / 64);
 
   float h_state = 0.f, c_state = 0.f;  // lanes 0..31 of wave 0
-  float emb_sum = 0.f;                 // lanes 0..31: running sum of selected keys (dim = lane)
+  float emb_sum = 0.f;                 // lanes 0..31: running sum of the selected keys (dim = lane)
+  float he_sum = 0.f;                  // every thread: We1[tid] . (running key sum), so he needs no exchange
   int cnt = 0;
   bool ended = su_mask[b] == 0;
   int su_num = ended ? 0 : max_steps;
@@ -138,10 +118,19 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
     float acc = c0_i;
     if (step > 0) {
       acc += bf_i;
+      // he read 8 floats at a time, with a scheduling fence per chunk: unfenced, the compiler hoists all 256 LDS
+      // reads ahead of the FMAs and the live values push the weights out to AGPRs
 #pragma unroll
-      for (int j = 0; j < kF / 2; ++j) {
-        const uint32_t w2 = wf_row[j];
-        acc += __uint_as_float(w2 << 16) * s_he[2 * j] + __uint_as_float(w2 & 0xffff0000u) * s_he[2 * j + 1];
+      for (int j = 0; j < kF / 2; j += 4) {
+        const float4 h0 = *reinterpret_cast<const float4*>(s_he + 2 * j);
+        const float4 h1 = *reinterpret_cast<const float4*>(s_he + 2 * j + 4);
+        const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t w2 = wf_row[j + e];
+          acc += __uint_as_float(w2 << 16) * hv[2 * e] + __uint_as_float(w2 & 0xffff0000u) * hv[2 * e + 1];
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     s_x[tid] = fmaxf(acc, 0.f);
@@ -149,47 +138,49 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
     // (b) qin = Wq2 x + bq2
     float part = 0.f;
 #pragma unroll
-    for (int k = 0; k < 32; ++k) part += wq2_s[k] * s_x[qp * 32 + k];
+    for (int k = 0; k < 32; ++k) part += s_wq2[k * kThreads + tid] * s_x[qp * 32 + k];
     part += __shfl_xor(part, 1, kWave);
     part += __shfl_xor(part, 2, kWave);
     part += __shfl_xor(part, 4, kWave);
     if (qp == 0) s_qin[qo] = part + bq2_o;
     __syncthreads();
-    // (c) gates = LN_i(Wih qin) + LN_h(Whh h)
-    float gi = 0.f, gh = 0.f;
-    if (tid < 4 * kQ) {
+    // (c) + (d) gates = LN_i(Wih qin) + LN_h(Whh h), then the cell: wave 0 alone
+    if (tid < 64) {
+      float gi0 = 0.f, gh0 = 0.f, gi1 = 0.f, gh1 = 0.f;
 #pragma unroll
       for (int k = 0; k < kQ; ++k) {
-        gi += wih_r[k] * s_qin[k];
-        gh += whh_r[k] * s_h[k];
+        const float q = s_qin[k], hk = s_h[k];
+        gi0 += s_wih[k * 4 * kQ + gr] * q;
+        gh0 += s_whh[k * 4 * kQ + gr] * hk;
+        gi1 += s_wih[k * 4 * kQ + gr + 64] * q;
+        gh1 += s_whh[k * 4 * kQ + gr + 64] * hk;
       }
-    }
-    const bool gact = tid < 4 * kQ;
-    const float mi = sum128(gact ? gi : 0.f, s_red, tid) * (1.f / (4 * kQ));
-    const float mh = sum128(gact ? gh : 0.f, s_red + 2, tid) * (1.f / (4 * kQ));
-    const float di = gi - mi, dh = gh - mh;
-    const float vi = sum128(gact ? di * di : 0.f, s_red + 4, tid) * (1.f / (4 * kQ));
-    const float vh = sum128(gact ? dh * dh : 0.f, s_red + 6, tid) * (1.f / (4 * kQ));
-    if (gact) s_gates[tid] = di * rsqrtf(vi + eps) * lniw + lnib + dh * rsqrtf(vh + eps) * lnhw + lnhb;
-    __syncthreads();
-    // (d) cell: lanes 0..31
-    if (tid < kQ) {
-      const float ig = sigmoidf_(s_gates[tid]), fg = sigmoidf_(s_gates[kQ + tid]);
-      const float gg = tanhf(s_gates[2 * kQ + tid]), og = sigmoidf_(s_gates[3 * kQ + tid]);
-      const float cp = fg * c_state + ig * gg;
-      float m = cp;
+      const float mi = wave_sum(gi0 + gi1) * (1.f / (4 * kQ));
+      const float mh = wave_sum(gh0 + gh1) * (1.f / (4 * kQ));
+      const float di0 = gi0 - mi, di1 = gi1 - mi, dh0 = gh0 - mh, dh1 = gh1 - mh;
+      const float ri = rsqrtf(wave_sum(di0 * di0 + di1 * di1) * (1.f / (4 * kQ)) + eps);
+      const float rh = rsqrtf(wave_sum(dh0 * dh0 + dh1 * dh1) * (1.f / (4 * kQ)) + eps);
+      const float g0 = di0 * ri * lniw0 + lnib0 + dh0 * rh * lnhw0 + lnhb0;   // row l:      i (l < 32) / f
+      const float g1 = di1 * ri * lniw1 + lnib1 + dh1 * rh * lnhw1 + lnhb1;   // row l + 64: g (l < 32) / o
+      const float gf = __shfl(g0, (tid & 31) + 32, kWave);
+      const float go = __shfl(g1, (tid & 31) + 32, kWave);
+      if (tid < kQ) {
+        const float ig = sigmoidf_(g0), fg = sigmoidf_(gf), gg = tanhf(g1), og = sigmoidf_(go);
+        const float cp = fg * c_state + ig * gg;
+        float m = cp;
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) m += __shfl_xor(m, o, kWave);
-      m *= (1.f / kQ);
-      const float d = cp - m;
-      float v = d * d;
+        for (int o = 16; o > 0; o >>= 1) m += __shfl_xor(m, o, kWave);
+        m *= (1.f / kQ);
+        const float d = cp - m;
+        float v = d * d;
 #pragma unroll
-      for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
-      v *= (1.f / kQ);
-      c_state = d * rsqrtf(v + eps) * lncw + lncb;
-      h_state = og * tanhf(c_state);
-      s_h[tid] = h_state;
-      s_q[tid] = h_state;
+        for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+        v *= (1.f / kQ);
+        c_state = d * rsqrtf(v + eps) * lncw + lncb;
+        h_state = og * tanhf(c_state);
+        s_h[tid] = h_state;   // read next step by this wave only (after the block barriers in between)
+        s_q[tid] = h_state;
+      }
     }
     __syncthreads();
     // (e) logits over this thread's contiguous chunk
@@ -213,7 +204,12 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
       }
       lv[k] = val;
     }
-    const float m = block_max(lmax, s_red, tid);
+    // block max: one barrier (the slots alternate by step parity, so no second barrier guards their reuse)
+    float* red = s_red + 8 * (step & 1);
+    lmax = wave_max(lmax);
+    if ((tid & 63) == 0) red[tid >> 6] = lmax;
+    __syncthreads();
+    const float m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     float es[kChunk];
     float local = 0.f;
 #pragma unroll
@@ -221,34 +217,49 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
       es[k] = (n_base + k < n1) ? __expf(lv[k] - m) : 0.f;
       local += es[k];
     }
-    // (f) inclusive block scan of chunk sums -> inverse-CDF pick
+    // (f) inclusive wave scan of chunk sums, wave totals through LDS -> inverse-CDF pick
     float incl = local;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const float y = __shfl_up(incl, o, kWave);
       if ((tid & 63) >= o) incl += y;
     }
-    if ((tid & 63) == 63) s_scan[tid >> 6] = incl;
+    float* scan = red + 4;
+    if ((tid & 63) == 63) scan[tid >> 6] = incl;
     __syncthreads();
+    const int wv = tid >> 6;
     float wave_off = 0.f;
-    for (int w = 0; w < (tid >> 6); ++w) wave_off += s_scan[w];
-    const float total = s_scan[0] + s_scan[1] + s_scan[2] + s_scan[3];
+    const float total = scan[0] + scan[1] + scan[2] + scan[3];
     const float target = u[static_cast<long>(b) * max_steps + step] * total;
-    float run = wave_off + incl - local;  // exclusive prefix of this thread's chunk
-    // the owner is the LAST thread whose exclusive prefix is <= target (exactly one, despite rounding)
-    const float cand = (n_base < n1 && run <= target) ? static_cast<float>(tid) : -1.f;
-    const int owner = static_cast<int>(block_max(cand, s_red, tid));
-    if (tid == owner) {
-      int pick = -1;
-#pragma unroll
-      for (int k = 0; k < kChunk; ++k) {
-        if (n_base + k < n1 && pick < 0) {
-          run += es[k];
-          if (run > target) pick = n_base + k;
-        }
+    // the owner wave: the last wave with entities whose offset is <= target (every thread computes the same
+    // offsets in the same order); the owner lane: the last lane of that wave whose exclusive prefix is <= target
+    int owner_wave = 0;
+    {
+      float off = 0.f;
+      for (int w = 0; w < nwaves_valid; ++w) {
+        if (w == wv) wave_off = off;
+        if (off <= target) owner_wave = w;
+        off += scan[w];
       }
-      if (pick < 0) pick = min(n_base + kChunk, n1) - 1;
-      s_result = pick;
+      if (wv >= nwaves_valid) wave_off = off;
+    }
+    if (wv == owner_wave) {
+      float run = wave_off + incl - local;  // exclusive prefix of this thread's chunk
+      const bool cand = n_base < n1 && run <= target;
+      const unsigned long long bal = __ballot(cand);
+      const int owner = 63 - __builtin_clzll(bal | 1ull);
+      if ((tid & 63) == owner) {
+        int pick = -1;
+#pragma unroll
+        for (int k = 0; k < kChunk; ++k) {
+          if (n_base + k < n1 && pick < 0) {
+            run += es[k];
+            if (run > target) pick = n_base + k;
+          }
+        }
+        if (pick < 0) pick = min(n_base + kChunk, n1) - 1;
+        s_result = pick;
+      }
     }
     __syncthreads();
     int r = s_result;
@@ -262,7 +273,7 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
       logp_out[static_cast<long>(b) * max_steps + step] = lr - m - __logf(total);
       results[static_cast<long>(b) * max_steps + step] = r;
     }
-    // (g) bookkeeping (uniform across the block)
+    // (g) bookkeeping (uniform across the block); every thread keeps the running key sum itself
     if (tid == 0) s_sel[r] = 1;
     if (r == en) {
       ended = true;
@@ -270,13 +281,13 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
     } else {
       ++cnt;
       if (tid < kQ) emb_sum += s_key[r * kQ + tid];
-    }
-    if (tid < kQ) s_emb[tid] = cnt > 0 ? emb_sum / static_cast<float>(cnt) : 0.f;
-    __syncthreads();
-    // he = relu(We1 emb + be1)
-    float he = be1_i;
+      float d = 0.f;
 #pragma unroll
-    for (int k = 0; k < kQ; ++k) he += we1_row[k] * s_emb[k];
+      for (int k = 0; k < kQ; ++k) d += we1_row[k] * s_key[r * kQ + k];
+      he_sum += d;
+    }
+    // he = relu(We1 emb + be1), emb = key sum / cnt
+    const float he = be1_i + (cnt > 0 ? he_sum / static_cast<float>(cnt) : 0.f);
     s_he[tid] = fmaxf(he, 0.f);
     __syncthreads();
   }

@@ -1296,7 +1296,14 @@ class _GatedResBlock(torch.autograd.Function):
         else:
             for i in range(4):
                 gw, gb = gate[2 * i].detach().view(C, C), gate[2 * i + 1].detach()
-                h = torch._addmm_activation(gb, h, gw.t(), use_gelu=False) if i < 3 else torch.addmm(gb, h, gw.t())
+                R = h.shape[0]
+                if _bf16_small_ok(h, R, C, C) or _bf16_pipe_ok(h, R, C, C):
+                    # the per-op path's kernels (_Linear): fp32 bias in the epilogue, so both paths agree bit for bit
+                    fn = _C.gemm_bf16_small if _bf16_small_ok(h, R, C, C) else _C.gemm_bf16
+                    h = fn(h, gw.contiguous(), _w32(gb), None, 1 if i < 3 else 0)
+                else:
+                    gb = gb.to(h.dtype)
+                    h = torch._addmm_activation(gb, h, gw.t(), use_gelu=False) if i < 3 else torch.addmm(gb, h, gw.t())
                 acts.append(h)
         # post: the next encoder skip map, added to the block output in the same pass (LocationHead)
         out = _C.gated_residual_fwd(y, h.view(B, H, W, C), sp, x, post)
@@ -1391,7 +1398,8 @@ def gated_resblock(x, conv1, conv2, gates, sp, post=None):
     # conv / GEMM weights and the GEMM biases in bf16 (the per-op path's casts); the conv biases stay as
     # given: the conv epilogue adds them in fp32
     # (with the one-launch bf16 gate chain the gate biases stay fp32 too: it reads them as fp32)
-    keep = {1, 3} | ({5, 7, 9, 11} if GATE_CHAIN and C == 128 else set())
+    # (the four-GEMM gate path keeps them fp32 as well: its native GEMMs add an fp32 bias, as the per-op path's do)
+    keep = {1, 3, 5, 7, 9, 11}
     ws = [t if (t.dtype == torch.bfloat16 or i in keep) else _bf16w(t) for i, t in enumerate(ws)]
     xl = nhwc(x.to(torch.bfloat16))
     pl = None if post is None else nhwc(post.to(torch.bfloat16))

@@ -20,6 +20,9 @@ from typing import Dict, Tuple
 import torch
 import torch.nn as nn
 
+# inference graphs: capture the scalar encoder on a side stream (APPLESTAR_GRAPH_SIDE_STREAMS=0: one stream)
+GRAPH_SIDE_STREAMS = os.environ.get('APPLESTAR_GRAPH_SIDE_STREAMS', '0') == '1'
+
 __all__ = ['GraphedSection', 'graphs_enabled']
 
 
@@ -140,7 +143,10 @@ class GraphedPolicy:
                 self._graphs.pop(next(iter(self._graphs)))
             static_in = _tree_clone(kwargs)
             flags = (encoders.STATIC_SHAPES, encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED)
-            encoders.STATIC_SHAPES, encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED = True, False, False
+            # GRAPH_SIDE_STREAMS: the scalar encoder (build-order transformer included) is captured on its own side
+            # stream, forked from and joined into the capture stream, so its kernels overlap the entity / spatial path
+            encoders.STATIC_SHAPES, encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED = \
+                True, GRAPH_SIDE_STREAMS, GRAPH_SIDE_STREAMS
             try:
                 side = torch.cuda.Stream()
                 side.wait_stream(torch.cuda.current_stream())

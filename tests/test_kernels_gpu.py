@@ -1015,8 +1015,12 @@ def test_resmlp_fused_matches_op_by_op():
     assert e_f < 2 * e_r + 1e-4, ('input grad', e_f, e_r)
     for (na, pa), (_, pb), (_, pg) in zip(vb.named_parameters(), ref.named_parameters(), gold.named_parameters()):
         assert pa.grad is not None and pa.grad.dtype == pa.dtype, na
-        e_f, e_r = _err(pa.grad, pg.grad), _err(pb.grad, pg.grad)
-        assert e_f < 2 * e_r + 1e-3 * max(1e-3, pg.grad.abs().max().item()), (na, e_f, e_r)
+        # relative Frobenius error: a max-abs error over a weight gradient behind 16 bf16 residual blocks is set by
+        # single ReLU-mask flips (a 2^-9 perturbation flips pre-activations within that margin of zero, see
+        # test_model_parity_gpu.py::test_bf16_head_grad_error_is_weight_rounding_sensitivity), in either bf16 path
+        rel = lambda a, r: ((a.float() - r.float()).norm() / r.float().norm().clamp_min(1e-30)).item()
+        e_f, e_r = rel(pa.grad, pg.grad), rel(pb.grad, pg.grad)
+        assert e_f < 2 * e_r + 1e-3, (na, e_f, e_r)
 
 
 @pytest.mark.parametrize('B', [6, 5])

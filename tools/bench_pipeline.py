@@ -36,6 +36,30 @@ def _free_port():
     return p
 
 
+def _cgroup_cpu():
+    """cgroup v2 cpu.stat of this job (usage / throttling under a CPU quota), {} when not readable."""
+    try:
+        with open('/sys/fs/cgroup/cpu.stat') as f:
+            d = dict(line.split() for line in f if line.strip())
+        with open('/sys/fs/cgroup/cpu.max') as f:
+            d['max'] = f.read().strip()
+        return d
+    except OSError:
+        return {}
+
+
+def _cg_delta(a, b, dt):
+    if not a or not b:
+        return {}
+    out = {'cpu.max': b.get('max')}
+    for k in ('usage_usec', 'throttled_usec', 'nr_throttled', 'nr_periods'):
+        if k in a and k in b:
+            out[k] = int(b[k]) - int(a[k])
+    if 'usage_usec' in out:
+        out['cpus_used'] = round(out['usage_usec'] / 1e6 / dt, 2)
+    return out
+
+
 def _learner_main(comm, B, T, gpu, precision, iq, graph_step=False):
     import torch
     if not gpu:
@@ -50,14 +74,92 @@ def _learner_main(comm, B, T, gpu, precision, iq, graph_step=False):
                      'communication': comm})
     orig = lrn._train
 
+    prof_at = int(os.environ.get('APPLESTAR_PIPE_PROFILE_AT', '0'))     # cProfile the learner's main thread
+    prof_n = int(os.environ.get('APPLESTAR_PIPE_PROFILE_N', '5'))
+    prof_out = os.environ.get('APPLESTAR_PIPE_PROFILE_OUT', 'learner_profile.txt')
+    state = {'n': 0, 'prof': None}
+
+    def thread_cpu():
+        """{thread id: (name, cpu seconds)} from /proc (Linux)."""
+        out = {}
+        try:
+            for tid in os.listdir('/proc/self/task'):
+                with open(f'/proc/self/task/{tid}/stat') as f:
+                    parts = f.read().rsplit(')', 1)[1].split()
+                with open(f'/proc/self/task/{tid}/comm') as f:
+                    name = f.read().strip()
+                out[int(tid)] = (name, (int(parts[11]) + int(parts[12])) / os.sysconf('SC_CLK_TCK'))
+        except OSError:
+            pass
+        return out
+
+    def sampler(stop, hist):
+        """Every 2 ms: the innermost frame of every Python thread (sampled while this thread holds the GIL)."""
+        import sys as _sys
+        import traceback as _tb
+        names = {}
+        while not stop.is_set():
+            for t in threading.enumerate():
+                names[t.ident] = t.name
+            for ident, fr in _sys._current_frames().items():
+                if ident == threading.get_ident():
+                    continue
+                st = _tb.extract_stack(fr)[-3:]
+                key = (names.get(ident, str(ident)),
+                       ' < '.join(f'{os.path.basename(x.filename)}:{x.lineno}:{x.name}' for x in st[::-1]))
+                hist[key] = hist.get(key, 0) + 1
+            time.sleep(0.002)
+
     def timed(data):
-        t0 = time.time()
+        state['n'] += 1
+        if prof_at and state['n'] == prof_at:
+            import cProfile
+            state['prof'] = cProfile.Profile()
+            state['cpu0'] = thread_cpu()
+            state['wall0'] = time.time()
+            state['hist'] = {}
+            state['stop'] = threading.Event()
+            if os.environ.get('APPLESTAR_PIPE_SAMPLER', '0') == '1':     # perturbs: it takes the GIL every 2 ms
+                threading.Thread(target=sampler, args=(state['stop'], state['hist']), daemon=True,
+                                 name='stack-sampler').start()
+            state['prof'].enable()
+        t0, c0, tc0 = time.time(), time.process_time(), time.thread_time()
+        if gpu:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         out = orig(data)
         th = time.time()                 # the step's host side (launches, Python) is done
         if gpu:
+            e1.record()
             torch.cuda.synchronize()
-        t1 = time.time()
-        iq.put((t1, lrn.last_iter.val + 1, t1 - t0, th - t0))
+        t1, c1, tc1 = time.time(), time.process_time(), time.thread_time()
+        if state['prof'] is not None and state['n'] == prof_at + prof_n - 1:
+            import io
+            import pstats
+            state['prof'].disable()
+            state['stop'].set()
+            cpu1, wall = thread_cpu(), time.time() - state['wall0']
+            buf = io.StringIO()
+            buf.write(f'per-thread CPU over the window ({wall:.2f} s wall):\n')
+            rows = sorted(((c - state['cpu0'].get(t, (n, 0.0))[1], n, t) for t, (n, c) in cpu1.items()), reverse=True)
+            pynames = {t.native_id: t.name for t in threading.enumerate()}
+            for c, n, t in rows[:20]:
+                buf.write(f'  {c:7.3f} s  {n} ({t}) {pynames.get(t, "")}\n')
+            buf.write('\nstack samples of the other Python threads (thread, innermost frames):\n')
+            for (tn, st), c in sorted(state['hist'].items(), key=lambda kv: -kv[1])[:40]:
+                buf.write(f'  {c:6d}  {tn}: {st}\n')
+            buf.write('\n')
+            st = pstats.Stats(state['prof'], stream=buf)
+            st.sort_stats('tottime').print_stats(45)
+            st.sort_stats('cumulative').print_stats(45)
+            with open(prof_out, 'w') as f:
+                f.write(f'{prof_n} learner iterations; cProfile of the main thread below\n' + buf.getvalue())
+            state['prof'] = None
+        # CPU seconds the learner process got during the step (all its threads) and the stream's span between
+        # the step's first and last launch: wall >> cpu and >> gpu = the process waited to be scheduled
+        iq.put((t1, lrn.last_iter.val + 1, t1 - t0, th - t0, c1 - c0,
+                e0.elapsed_time(e1) / 1e3 if gpu else 0.0, tc1 - tc0))
         return out
     lrn._train = timed
     lrn.run(max_iterations=1000000)
@@ -125,6 +227,7 @@ def main():
     while not iters and time.time() - t_start < 600:
         time.sleep(0.5)
     t0 = time.time()
+    cg0 = _cgroup_cpu()
     st0 = probe.stats()
     it0 = iters[-1][1] if iters else 0
     n_rec0 = len(iters)
@@ -152,7 +255,13 @@ def main():
            # the learner waiting for / assembling data
            'learner_train_ms_mean': round(1e3 * sum(r[2] for r in win) / max(len(win), 1), 1),
            'learner_train_host_ms_mean': round(1e3 * sum(r[3] for r in win) / max(len(win), 1), 1),
+           'learner_train_cpu_ms_mean': round(1e3 * sum(r[4] for r in win) / max(len(win), 1), 1),
+           'learner_train_main_thread_cpu_ms_mean': round(1e3 * sum(r[6] for r in win) / max(len(win), 1), 1),
+           'learner_train_stream_ms_mean': round(1e3 * sum(r[5] for r in win) / max(len(win), 1), 1),
            'learner_iter_ms_mean': round(1e3 * dt / max(n_it, 1), 1),
+           'cgroup_cpu': _cg_delta(cg0, _cgroup_cpu(), dt),
+           'affinity_cpus': len(os.sched_getaffinity(0)),
+           'loadavg': open('/proc/loadavg').read().split()[:3],
            'fresh_samples_per_s': round(pushed * T / dt, 1),
            'startup_s': round(t0 - t_start, 1),
            'inference_server': {
