@@ -12,6 +12,7 @@ runs on a side HIP stream one batch ahead of compute (:class:`DevicePrefetcher`)
 """
 from __future__ import annotations
 
+import os
 import queue
 import random
 import threading
@@ -68,11 +69,18 @@ class RLDataLoader:
     # ---------------------------------------------------------------- HBM ring path
     def _ring_loop(self):
         torch.set_num_threads(1)
+        # diagnostics (tools/bench_pipeline.py): 'discard' keeps receiving once the ring is full but drops the frames
+        # (receive cost without the ring insert / H2D copy); 'unpinned' receives into pageable memory
+        mode = os.environ.get('APPLESTAR_RING_DIAG', '')
         while not self._stop.is_set():
+            if mode == 'discard' and len(self._ring) >= self.buffer_size:
+                self._pull(1, raw=True)
+                continue
             with self._avail:
                 while len(self._ring) >= self.buffer_size and not self._stop.is_set():
                     self._avail.wait(0.5)
-            for frame in self._pull(1, raw=True, alloc=self._ring.stage):  # bytes land in pinned staging
+            alloc = None if mode == 'unpinned' else self._ring.stage      # bytes land in pinned staging
+            for frame in self._pull(1, raw=True, alloc=alloc):
                 self._ring.put(frame)
                 with self._avail:
                     self._avail.notify_all()

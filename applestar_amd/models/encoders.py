@@ -153,7 +153,11 @@ class ScalarEncoder(nn.Module):
             elif kind == 'bo':
                 e = m(x['beginning_order'], x['bo_location'])
             else:
-                e = m(x[name].float())
+                v = x[name]
+                # integer feature columns: straight to the bf16 compute dtype under autocast (one cast; via fp32 it was
+                # two launches per module - the linear casts its input anyway, and uint8 / int16 -> fp32 is exact)
+                e = m(v.to(torch.bfloat16) if v.is_cuda and torch.is_autocast_enabled() and not v.is_floating_point()
+                      else v.float())
             embedded.append(e)
             if is_ctx:
                 context.append(e)

@@ -1981,7 +1981,13 @@ class _SmallLinearNative(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x2, w, b, act):
-        y = _C.small_gemm(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None, None, 0, _ACT[act])
+        if SPLITK_NATIVE and x2.shape[1] > F32_SMALL_K_MAX and _ACT[act] in (0, 1, 2):
+            # long reduction (the actor's B = 1..16 spatial-encoder fc, 48,640 wide): split-K slices + an ordered
+            # sum; one workgroup per output tile walked all of K (142 us at B = 1, profiles/r5v_timeline_*)
+            y = _C.small_gemm_splitk(x2, w.detach().contiguous(), _w32(b) if b is not None else None, _ACT[act])
+        else:
+            y = _C.small_gemm(x2, w.detach().contiguous(), _w32(b) if b is not None else None, None, None, 0,
+                              _ACT[act])
         ctx.save_for_backward(x2, w, y if act else None)
         ctx.act, ctx.has_b = act, b is not None
         ctx.b_dtype = b.dtype if b is not None else None
@@ -2012,6 +2018,34 @@ def _small_native_ok(x, R, N, K, act):
         R * K < (1 << 31) and R * N < (1 << 31)
 
 
+_CAST_CACHE = {}      # id(fp32 activation) -> (weakref, version, shape, bf16 copy)
+CAST_CACHE = os.environ.get('APPLESTAR_CAST_CACHE', '1') == '1'
+
+
+def _bf16_rows(x, R, K):
+    """x as a contiguous bf16 [R, K].  An fp32 activation feeding several linears (the core LSTM output, the scalar
+    context: 3-4 heads each) is cast once: the copy is kept while the source tensor object is alive and unmodified
+    (same object, same version counter) - one launch instead of one per consumer."""
+    if x.dtype == torch.bfloat16:
+        return x.reshape(R, K).contiguous()
+    if not (CAST_CACHE and x.is_cuda and x.dtype == torch.float32) or (torch.is_grad_enabled() and x.requires_grad):
+        # (no caching under autograd: an entry would keep the step's graph alive)
+        return x.reshape(R, K).to(torch.bfloat16).contiguous()
+    import weakref
+    e = _CAST_CACHE.get(id(x))
+    if e is not None and e[0]() is x and e[1] == x._version and e[2] == (R, K):
+        return e[3]
+    xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
+    if len(_CAST_CACHE) > 64:
+        for k in [k for k, v in _CAST_CACHE.items() if v[0]() is None]:
+            del _CAST_CACHE[k]
+    try:
+        _CAST_CACHE[id(x)] = (weakref.ref(x), x._version, (R, K), xb)
+    except TypeError:
+        pass
+    return xb
+
+
 def linear(x, w, b=None, act=None, grad_link=None):
     """bf16 act(x W^T + b) over the last dim of x with the native weight gradient when the row count is
     large; other shapes take F.linear (+ the activation).  ``grad_link``: a :class:`GradLink` the residual
@@ -2034,7 +2068,7 @@ def linear(x, w, b=None, act=None, grad_link=None):
         # few rows, odd widths or a sigmoid gate: the native any-shape kernels both ways (gemm_small.hip)
         ensure_loaded()
         with torch.autocast('cuda', enabled=False):
-            xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
+            xb = _bf16_rows(x, R, K)
             wb = w if w.dtype == torch.bfloat16 else _bf16w(w)
             y = _SmallLinearNative.apply(xb, wb, b, act)
         return y.view(*x.shape[:-1], N)
@@ -2085,7 +2119,7 @@ def linear(x, w, b=None, act=None, grad_link=None):
             x.is_contiguous() and x.requires_grad:
         grad_link.armed, link, xb = x, grad_link, x
     else:
-        xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
+        xb = _bf16_rows(x, R, K)
     wb = w if w.dtype == torch.bfloat16 else _bf16w(w)
     # the bias as given: the native epilogues add it in fp32 (an fp32 parameter is used as is - no fp32 -> bf16
     # -> fp32 round trip of casts); _Linear's library fallbacks cast it to the operand dtype themselves

@@ -60,15 +60,19 @@ def _cg_delta(a, b, dt):
     return out
 
 
-def _learner_main(comm, B, T, gpu, precision, iq, graph_step=False):
+def _learner_main(comm, B, T, gpu, precision, iq, graph_step=False, max_reuse=2):
     import torch
+    sw = os.environ.get('APPLESTAR_PIPE_SWITCH')
+    if sw:
+        sys.setswitchinterval(float(sw))     # the GIL hand-over interval of the learner process (default 5 ms)
     if not gpu:
         torch.set_num_threads(2)      # CPU rehearsal: leave cores to the env workers and the inference server
     from applestar_amd.learner.rl_learner import RLLearner
     lrn = RLLearner({'common': {'experiment_name': 'pipeline'},
                      'learner': {'use_cuda': gpu, 'player_id': 'MP0', 'use_value_feature': False,
                                  'amp_dtype': 'bfloat16' if precision == 'bf16' else None,
-                                 'data': {'batch_size': B, 'trajectory_length': T, 'buffer_size': 2 * B},
+                                 'data': {'batch_size': B, 'trajectory_length': T, 'buffer_size': 2 * B,
+                                          'max_reuse': max_reuse},
                                  'graph_step': bool(graph_step),
                                  'log_to_stdout': False},
                      'communication': comm})
@@ -174,6 +178,8 @@ def main():
     ap.add_argument('--precision', choices=['bf16', 'fp32'], default='bf16')
     ap.add_argument('--workdir', default='/tmp/applestar_pipeline')
     ap.add_argument('--graph-step', action='store_true', help='the learner replays its whole step as one HIP graph')
+    ap.add_argument('--max-reuse', type=int, default=2,
+                    help='trainings per trajectory (reference: 2); huge = the ring fills once and ingest stops')
     args = ap.parse_args()
     os.makedirs(args.workdir, exist_ok=True)
     os.chdir(args.workdir)
@@ -206,7 +212,7 @@ def main():
     import multiprocessing as mp
     ctx = mp.get_context('spawn')
     iq = ctx.Queue()
-    lp = ctx.Process(target=_learner_main, args=(comm, B, T, gpu, args.precision, iq, args.graph_step), daemon=True)
+    lp = ctx.Process(target=_learner_main, args=(comm, B, T, gpu, args.precision, iq, args.graph_step, args.max_reuse), daemon=True)
     lp.start()
     iters = []          # (wall time, iteration) after each learner iteration
 
@@ -244,7 +250,8 @@ def main():
     dt = t1 - t0
     n_it = it1 - it0
     out = {'metric': 'end-to-end single-GPU RL pipeline', 'envs': args.envs, 'precision': args.precision,
-           'graph_step': bool(args.graph_step),
+           'graph_step': bool(args.graph_step), 'max_reuse': args.max_reuse,
+           'switch_interval': os.environ.get('APPLESTAR_PIPE_SWITCH'),
            'seconds': round(dt, 1), 'traj_len': T, 'batch': B,
            'trajectories_per_s': round(pushed / dt, 2),
            'actor_agent_steps_per_s': round(pushed * T / dt, 1),
