@@ -13,6 +13,7 @@
 // a pointer read and one memcpy; the header is emitted and parsed without building intermediate JSON objects.
 // Reference counterpart: the reference pickles + lz4-compresses every trajectory (file_helper.py:255-302).
 #include <torch/extension.h>
+#include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 
 #include <algorithm>
@@ -557,6 +558,215 @@ py::object tree_loads(py::object data, bool copy) {
   return d.node();
 }
 
+// ------------------------------------------------------------------------------------------------- trajectory index
+// runtime/traj_ring.py: the learner's ingest thread needs, per trajectory frame, every step's tensor leaves (path,
+// dtype, shape, body offset, bytes).  As json.loads + a Python tree walk that is ~20 ms per 64-step trajectory of
+// GIL-held work (json.loads is one C call the interpreter cannot preempt) - at ~20 trajectories/s it starved the
+// learner's launch thread (profiles/r5x_pipeline_*: 280 ms steps with ingest running, 45 ms without).  Here the
+// header is parsed with the GIL released into one int64 table.
+struct IdxKey {
+  bool is_int = false;
+  std::string s;
+  int64_t i = 0;
+  bool operator==(const IdxKey& o) const { return is_int == o.is_int && i == o.i && s == o.s; }
+};
+struct IdxLeaf {
+  std::vector<IdxKey> path;
+  std::string dt;
+  std::vector<int64_t> shape;
+  int64_t off = 0, nbytes = 0;
+};
+
+struct IndexParser : Decoder {
+  std::vector<IdxKey> path;
+  std::vector<IdxLeaf>* out = nullptr;
+
+  void skip_value() {   // a JSON scalar (a __v__ payload): consumed, not built
+    ws();
+    if (s >= end) fail("truncated header");
+    if (*s == '"') {
+      str();
+      return;
+    }
+    if (lit("null") || lit("true") || lit("false") || lit("NaN") || lit("Infinity") || lit("-Infinity")) return;
+    const char* st = s;
+    if (s < end && (*s == '-' || *s == '+')) ++s;
+    while (s < end && ((*s >= '0' && *s <= '9') || *s == '.' || *s == 'e' || *s == 'E' || *s == '-' || *s == '+')) ++s;
+    if (s == st) fail("bad value");
+  }
+
+  IdxKey key() {
+    IdxKey k;
+    if (peek('"')) {
+      k.s = str();
+    } else {
+      k.is_int = true;
+      k.i = integer();
+    }
+    return k;
+  }
+
+  void node() {
+    expect('{');
+    const std::string tag = str();
+    expect(':');
+    if (tag == "__t__") {
+      IdxLeaf L;
+      L.path = path;
+      expect('[');
+      L.dt = str();
+      at::ScalarType dt;
+      if (!dtype_from_code(L.dt, &dt)) fail("unknown dtype");
+      expect(',');
+      expect('[');
+      if (!peek(']')) {
+        L.shape.push_back(integer());
+        while (peek(',')) {
+          ++s;
+          L.shape.push_back(integer());
+        }
+      }
+      expect(']');
+      expect(',');
+      L.off = integer();
+      expect(',');
+      L.nbytes = integer();
+      expect(']');
+      check_tensor(dt, L.shape, L.off, L.nbytes);
+      out->push_back(std::move(L));
+    } else if (tag == "__d__") {
+      expect('[');
+      bool first = true;
+      while (!peek(']')) {
+        if (!first) expect(',');
+        first = false;
+        expect('[');
+        path.push_back(key());
+        expect(',');
+        node();
+        path.pop_back();
+        expect(']');
+      }
+      expect(']');
+    } else if (tag == "__l__" || tag == "__tu__") {
+      expect('[');
+      bool first = true;
+      int64_t i = 0;
+      while (!peek(']')) {
+        if (!first) expect(',');
+        first = false;
+        IdxKey k;
+        k.is_int = true;
+        k.i = i++;
+        path.push_back(k);
+        node();
+        path.pop_back();
+      }
+      expect(']');
+    } else if (tag == "__v__") {
+      skip_value();
+    } else {
+      fail("unknown node tag");
+    }
+    expect('}');
+  }
+};
+
+constexpr int kIdxMaxDims = 4;
+
+// frame -> (paths, dtype codes, meta int64 [T1, L, 3 + kIdxMaxDims] = body offset, nbytes (-1: absent in that
+//           step), ndim, dims..., body offset of the frame) over the union of the steps' leaves; None when a path
+//           changes dtype or a leaf has more than kIdxMaxDims dims (callers fall back)
+py::object traj_index(py::object data) {
+  py::buffer buf = py::reinterpret_borrow<py::buffer>(data);
+  py::buffer_info info = buf.request();
+  const auto* p = static_cast<const uint8_t*>(info.ptr);
+  const int64_t n = static_cast<int64_t>(info.size * info.itemsize);
+  const int64_t pre = static_cast<int64_t>(kMagicLen) + 9;
+  if (n < pre || std::memcmp(p, kMagic, kMagicLen) != 0) throw py::value_error("not an applestar frame");
+  uint64_t hlen = 0;
+  std::memcpy(&hlen, p + kMagicLen, 8);
+  if (p[kMagicLen + 8] != 0) throw py::value_error("traj_index: compressed frame");
+  if (hlen > static_cast<uint64_t>(n - pre)) throw py::value_error("traj_index: truncated frame");
+  const int64_t pad = (kAlign - (pre + static_cast<int64_t>(hlen)) % kAlign) % kAlign;
+  const int64_t body_start = pre + static_cast<int64_t>(hlen) + pad;
+  if (body_start > n) throw py::value_error("traj_index: truncated frame");
+  std::vector<std::vector<IdxLeaf>> steps;
+  std::map<std::string, int64_t> slot;
+  std::vector<const IdxLeaf*> uni;
+  bool layout_ok = true;
+  {
+    py::gil_scoped_release nogil;
+    IndexParser d;
+    d.s = reinterpret_cast<const char*>(p + pre);
+    d.end = d.s + hlen;
+    d.body = p + body_start;
+    d.body_len = n - body_start;
+    d.copy = false;
+    d.expect('{');
+    if (d.str() != "__l__") d.fail("traj_index: the header is not a step list");
+    d.expect(':');
+    d.expect('[');
+    bool first = true;
+    while (!d.peek(']')) {
+      if (!first) d.expect(',');
+      first = false;
+      steps.emplace_back();
+      d.out = &steps.back();
+      d.node();
+    }
+    d.expect(']');
+    d.expect('}');
+    // the union of the steps' leaves in first-seen order (the last step carries only the observation, the first
+    // the recurrent state); a path must keep its dtype
+    for (const auto& st : steps)
+      for (const IdxLeaf& lf : st) {
+        if (lf.shape.size() > static_cast<size_t>(kIdxMaxDims)) layout_ok = false;
+        std::string k;
+        for (const IdxKey& q : lf.path) k += (q.is_int ? "i" + std::to_string(q.i) : "s" + q.s) + '\x1f';
+        auto it = slot.find(k);
+        if (it == slot.end()) {
+          slot.emplace(k, static_cast<int64_t>(uni.size()));
+          uni.push_back(&lf);
+        } else if (uni[it->second]->dt != lf.dt) {
+          layout_ok = false;
+        }
+      }
+  }
+  if (!layout_ok || steps.empty()) return py::none();
+  const int64_t T1 = static_cast<int64_t>(steps.size()), L = static_cast<int64_t>(uni.size()),
+                W = 3 + kIdxMaxDims;
+  py::array_t<int64_t> meta({T1, L, W});
+  auto* m = meta.mutable_data();
+  for (int64_t i = 0; i < T1 * L; ++i) {
+    int64_t* r = m + i * W;
+    r[0] = 0;
+    r[1] = -1;      // absent in this step
+    r[2] = 0;
+    for (int k = 0; k < kIdxMaxDims; ++k) r[3 + k] = 1;
+  }
+  for (int64_t t = 0; t < T1; ++t)
+    for (const IdxLeaf& lf : steps[t]) {
+      std::string k;
+      for (const IdxKey& q : lf.path) k += (q.is_int ? "i" + std::to_string(q.i) : "s" + q.s) + '\x1f';
+      int64_t* r = m + (t * L + slot[k]) * W;
+      r[0] = lf.off;
+      r[1] = lf.nbytes;
+      r[2] = static_cast<int64_t>(lf.shape.size());
+      for (size_t q = 0; q < lf.shape.size(); ++q) r[3 + q] = lf.shape[q];
+    }
+  py::list paths, dts;
+  for (const IdxLeaf* lfp : uni) {
+    const IdxLeaf& lf = *lfp;
+    py::tuple tp(lf.path.size());
+    for (size_t k = 0; k < lf.path.size(); ++k)
+      tp[k] = lf.path[k].is_int ? py::object(py::int_(lf.path[k].i)) : py::object(py::str(lf.path[k].s));
+    paths.append(tp);
+    dts.append(py::str(lf.dt));
+  }
+  return py::make_tuple(paths, dts, meta, body_start);
+}
+
 // ------------------------------------------------------------------------------------------------- batch collate
 // The inference server's per-batch host path: B request frames -> one pinned staging buffer laid out as the
 // collated batch (agent/collate.py collate_obs: every leaf stacked on a new dim 0; entity_info leaves padded on
@@ -831,6 +1041,8 @@ void register_codec(py::module& m) {
         "applestar frame -> tensor tree (copy=False: tensors alias the buffer)");
   m.def("rows_dumps", &rows_dumps, py::arg("tree"), py::arg("n"), py::arg("trims"),
         "one frame per batch row (row i of every batched leaf, per-path per-row narrowing)");
+  m.def("traj_index", &traj_index, py::arg("data"),
+        "trajectory frame -> (leaf paths, dtype codes, int64 [steps, leaves, 7] offsets / sizes / shapes, body start)");
   m.def("collate_frames", &collate_frames, py::arg("frames"), py::arg("pad_entities") = 0,
         py::arg("device") = py::none(), py::arg("buckets") = std::vector<int64_t>{}, "B request frames -> collated batch (one pinned staging buffer, one H2D)");
 }

@@ -50,20 +50,65 @@ def _leaves(node, path=()):
             yield from _leaves(v, path + (i,))
 
 
-class _Traj:
-    __slots__ = ('start', 'size', 'T', 'leaves', 'entity_counts', 'event', 'uses')
+_W = 7   # per-leaf index row: body offset, nbytes, ndim, 4 dims (csrc/codec.cpp traj_index)
 
-    def __init__(self, start, size, steps):
+
+class _Traj:
+    """A resident trajectory: its arena extent and its leaf index - ``paths`` (leaf paths of a step), ``dts`` (dtype
+    codes), ``meta`` int64 [T + 1, leaves, 7] (offset into the frame body, nbytes, ndim, dims)."""
+    __slots__ = ('start', 'size', 'T', 'paths', 'pidx', 'dts', 'meta', 'entity_counts', 'event', 'uses')
+
+    def __init__(self, start, size, paths, dts, meta):
         self.start, self.size = start, size
-        self.T = len(steps) - 1
-        self.leaves: Dict[tuple, List] = {}
-        for t, st in enumerate(steps):
-            for path, d in _leaves(st):
-                self.leaves.setdefault(path, [None] * len(steps))[t] = d
-        ex = self.leaves[('entity_info', 'x')]
-        self.entity_counts = np.array([d[1][0] for d in ex], dtype=np.int64)
+        self.T = meta.shape[0] - 1
+        self.paths, self.dts, self.meta = paths, dts, meta
+        self.pidx = {p: i for i, p in enumerate(paths)}
+        ex = self.pidx[('entity_info', 'x')]
+        self.entity_counts = meta[:, ex, 3].copy()
         self.event = None
         self.uses = 0
+
+
+def _index_py(steps):
+    """Python form of csrc/codec.cpp traj_index over a parsed header's step list (fallback): the union of the steps'
+    leaves in first-seen order, nbytes -1 where a step lacks a leaf."""
+    pos, paths, dts, rows = {}, [], [], []
+    for t, st in enumerate(steps):
+        for path, d in _leaves(st):
+            if path not in pos:
+                pos[path] = len(paths)
+                paths.append(path)
+                dts.append(d[0])
+            elif dts[pos[path]] != d[0]:
+                raise ValueError(f'trajectory leaf {path} changes dtype')
+            rows.append((t, pos[path], d))
+    meta = np.ones((len(steps), len(paths), _W), dtype=np.int64)
+    meta[:, :, 0], meta[:, :, 1], meta[:, :, 2] = 0, -1, 0
+    for t, i, d in rows:
+        shape = list(d[1])
+        if len(shape) > _W - 3:
+            raise ValueError('trajectory leaf with more than 4 dims')
+        meta[t, i, 0], meta[t, i, 1], meta[t, i, 2] = d[2], d[3], len(shape)
+        meta[t, i, 3:3 + len(shape)] = shape
+    return paths, dts, meta
+
+
+def _native_index(frame):
+    """csrc/codec.cpp traj_index (the header parsed with the GIL released), or None (extension missing, compressed
+    frame, a leaf the table cannot hold) - the caller parses in Python."""
+    try:
+        from ..ops import native
+        C = native._C if native._C is not None else native.ensure_loaded()
+    except Exception:   # noqa: BLE001 - CPU-only installs without the extension
+        return None
+    fn = getattr(C, 'traj_index', None)
+    if fn is None or len(frame) <= len(serialize.MAGIC) + 8 or memoryview(frame)[len(serialize.MAGIC) + 8] != 0:
+        return None
+    r = fn(frame)
+    if r is None:
+        return None
+    paths, dts, meta, body_off = r
+    return [tuple(p) for p in paths], list(dts), meta, int(body_off)
 
 
 def auto_ring_bytes(device, step_peak_gb: float = 20.0, headroom_gb: float = 8.0, fraction: float = 0.75,
@@ -137,13 +182,18 @@ class TrajectoryRing:
         staged = getattr(self, '_staged', None)
         slot = staged[1] if staged is not None and frame is staged[0] else None
         self._staged = None
-        header, body = serialize.parse(frame)
-        steps = header['__l__']
+        idx = _native_index(frame)
+        if idx is not None:
+            paths, dts, meta, body_off = idx
+            body = memoryview(frame)[body_off:]
+        else:
+            header, body = serialize.parse(frame)
+            paths, dts, meta = _index_py(header['__l__'])
         n = len(body)
         body_off = len(frame) - n
         with self._lock:
             start = self._alloc(n)
-            tr = _Traj(start, (n + _ALIGN - 1) // _ALIGN * _ALIGN, steps)
+            tr = _Traj(start, (n + _ALIGN - 1) // _ALIGN * _ALIGN, paths, dts, meta)
             if slot is None:
                 with warnings.catch_warnings():  # read-only source: only ever copied from
                     warnings.simplefilter('ignore')
@@ -192,12 +242,11 @@ class TrajectoryRing:
         N = int(max(tr.entity_counts.max() for tr in trs))
         layout, segs = [], []
         offset = 0
-        paths = list(trs[0].leaves)
-        for path in paths:
-            d0 = trs[0].leaves[path][0]
-            if d0 is None:
+        t0 = trs[0]
+        for li0, path in enumerate(t0.paths):
+            if t0.meta[0, li0, 1] < 0:       # absent in the first step of the first trajectory
                 continue
-            dt = serialize.DTYPES[d0[0]]
+            dt = serialize.DTYPES[t0.dts[li0]]
             esize = torch.empty(0, dtype=torch.uint8 if dt == torch.bool else dt).element_size()
             is_obs = path[0] in OBS_TOP
             is_hidden = path[0] == 'hidden_state'
@@ -211,25 +260,27 @@ class TrajectoryRing:
             elif path in ENTITY_N:
                 row_shape = (N,)
             else:
-                row_shape = tuple(d0[1])
+                m0 = t0.meta[0, li0]
+                row_shape = tuple(int(x) for x in m0[3:3 + m0[2]])
             row_bytes = int(np.prod(row_shape, dtype=np.int64)) * esize
             offset = (offset + _ALIGN - 1) // _ALIGN * _ALIGN
             layout.append((path, dt, (steps * B,) + row_shape, offset, steps))
+            rows = np.arange(steps, dtype=np.int64) * B
             # per (t, b) segments
             for b, tr in enumerate(trs):
-                descs = tr.leaves[path][:steps]
-                offs = np.array([d[2] for d in descs], dtype=np.int64) + tr.start
-                nb = np.array([d[3] for d in descs], dtype=np.int64)
-                rows = np.arange(steps, dtype=np.int64) * B + b
-                dst = offset + rows * row_bytes
+                m = tr.meta[:steps, tr.pidx[path]]            # [steps, 7]
+                offs = m[:, 0] + tr.start
+                nb = m[:, 1]
+                dst = offset + (rows + b) * row_bytes
                 if path in SU_2D:  # [s, n+1] -> [64, N+1]: one segment per source row
-                    for t, d in enumerate(descs):
-                        s, c = (d[1][0], d[1][1]) if len(d[1]) == 2 and d[3] else (0, 0)
-                        if s == 0:
+                    two = (m[:, 2] == 2) & (nb > 0)
+                    for t in np.nonzero(two)[0]:
+                        s_, c = int(m[t, 3]), int(m[t, 4])
+                        if s_ == 0:
                             continue
-                        r = np.arange(s, dtype=np.int64)
+                        r = np.arange(s_, dtype=np.int64)
                         segs.append(np.stack([offs[t] + r * c * esize, dst[t] + r * (N + 1) * esize,
-                                              np.full(s, c * esize, dtype=np.int64)], 1))
+                                              np.full(s_, c * esize, dtype=np.int64)], 1))
                 else:
                     keep = nb > 0
                     segs.append(np.stack([offs[keep], dst[keep], nb[keep]], 1))

@@ -60,7 +60,7 @@ def _cg_delta(a, b, dt):
     return out
 
 
-def _learner_main(comm, B, T, gpu, precision, iq, graph_step=False, max_reuse=2):
+def _learner_main(comm, B, T, gpu, precision, iq, graph_step=False, max_reuse=2, stop_ev=None):
     import torch
     sw = os.environ.get('APPLESTAR_PIPE_SWITCH')
     if sw:
@@ -115,6 +115,8 @@ def _learner_main(comm, B, T, gpu, precision, iq, graph_step=False, max_reuse=2)
             time.sleep(0.002)
 
     def timed(data):
+        if stop_ev is not None and stop_ev.is_set():
+            raise SystemExit(0)         # a normal interpreter exit (atexit handlers run: profiler traces flush)
         state['n'] += 1
         if prof_at and state['n'] == prof_at:
             import cProfile
@@ -212,7 +214,8 @@ def main():
     import multiprocessing as mp
     ctx = mp.get_context('spawn')
     iq = ctx.Queue()
-    lp = ctx.Process(target=_learner_main, args=(comm, B, T, gpu, args.precision, iq, args.graph_step, args.max_reuse), daemon=True)
+    stop_ev = ctx.Event()
+    lp = ctx.Process(target=_learner_main, args=(comm, B, T, gpu, args.precision, iq, args.graph_step, args.max_reuse, stop_ev), daemon=True)
     lp.start()
     iters = []          # (wall time, iteration) after each learner iteration
 
@@ -282,7 +285,10 @@ def main():
            'cpus': os.cpu_count(),
            'data': 'FakeSC2Env observations, random-init policy; learner reuses each trajectory 2x (reference)'}
     print(json.dumps(out), flush=True)
-    lp.terminate()
+    stop_ev.set()
+    lp.join(timeout=30)        # the learner leaves at its next step (a clean exit: traced runs keep their data)
+    if lp.is_alive():
+        lp.terminate()
     try:
         actor.close()
     except Exception:   # noqa: BLE001 - best-effort teardown of the worker processes
