@@ -168,6 +168,11 @@ def run_inference(device, batches=(1, 16), iters=20, entities=300):
     from applestar_amd.runtime.graphs import GraphedPolicy
     out = {}
     m = Model({'agent': {'extra_units': True}}).to(device).eval().to(memory_format=torch.channels_last)
+    # the inference server's configuration (actor/inference.py set_model): the model's parameters carry their cached
+    # bf16 / channels-last compute forms, so the graph reads them instead of casting every weight per call
+    from applestar_amd.ops import native
+    native.ensure_loaded()
+    native.attach_inference_forms(m)
     gp = GraphedPolicy(m, 'compute_logp_action')
     for B in batches:
         g = torch.Generator().manual_seed(B)
