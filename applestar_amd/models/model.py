@@ -387,3 +387,11 @@ class Model(nn.Module):
     def policy_state_dict(self):
         """Actor-facing weights (everything except value networks / value encoder)."""
         return {k: v for k, v in self.state_dict().items() if 'value_networks' not in k and 'value_encoder' not in k}
+
+
+def _install_fast_apply():
+    from ..ops.native import install_fast_apply
+    install_fast_apply(globals(), __name__)
+
+
+_install_fast_apply()

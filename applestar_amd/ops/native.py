@@ -2246,3 +2246,30 @@ def resmlp(x0, params):
     if not torch.is_grad_enabled() or not (x0.requires_grad or any(p.requires_grad for p in params)):
         return _C.resmlp_fwd(x0, list(params), False)[0]
     return _ResMLP.apply(x0, *params)
+
+
+# ---------------------------------------------------------------------------- autograd.Function dispatch
+FAST_APPLY = os.environ.get('APPLESTAR_FAST_APPLY', '1') == '1'
+
+
+def install_fast_apply(namespace: dict, module: str) -> int:
+    """Point ``apply`` of the module's autograd Functions straight at the C++ ``_FunctionBase.apply``.  The Python
+    ``Function.apply`` wrapper runs functorch's ``unwrap_dead_wrappers`` (a pytree walk over every argument) on each
+    call - 141 calls and ~3.9 ms of host time per bf16 learner step (profiles/r6g_host_profile_bf16.txt), a step
+    whose host side is its critical path.  The framework never runs these Functions under functorch transforms
+    (vmap / grad), which is all that wrapper serves; none uses ``setup_context`` or keyword arguments."""
+    if not FAST_APPLY:
+        return 0
+    n = 0
+    base_setup = getattr(torch.autograd.function._SingleLevelFunction, 'setup_context', None)
+    for obj in list(namespace.values()):
+        if not (isinstance(obj, type) and issubclass(obj, torch.autograd.Function) and obj.__module__ == module):
+            continue
+        if 'apply' in obj.__dict__ or getattr(obj, 'setup_context', None) is not base_setup:
+            continue
+        obj.apply = staticmethod(super(torch.autograd.Function, obj).apply)
+        n += 1
+    return n
+
+
+install_fast_apply(globals(), __name__)
