@@ -11,6 +11,8 @@
 // Core LSTM: H=384 -> 384 threads x 4 columns; selected-units LSTM: H=32 -> 64 threads x 2.
 // The backward walks t = T-1..0 and emits d(xp), d(h_{t-1} W^T) (for one dW GEMM afterwards) and
 // the LN_c output gradient (for the affine-parameter reductions).
+#include <cstdlib>
+
 #include "../common.h"
 #include "../kernels.h"
 
@@ -577,7 +579,10 @@ __device__ __forceinline__ void get_granules(const unsigned long long* base, lon
   }
 }
 
-template <int H, int NT, typename TW>
+// GRAN: the partial exchange as {epoch, value} granules (as the backward): every thread writes its partials and
+// polls the 8 x COLS granules it needs - one L2 round trip after the slowest producer, where the flag hand-off
+// (data stores, drain, barrier, flag store, flag poll, barrier, data loads) takes three
+template <int H, int NT, typename TW, bool GRAN>
 __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
     const float* __restrict__ xp, const float* __restrict__ h0, const float* __restrict__ c0,
     const TW* __restrict__ wT, const float* __restrict__ lnh_w, const float* __restrict__ lnh_b,
@@ -633,36 +638,74 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
 #pragma unroll
       for (int k = 0; k < COLS; ++k) acc[k] = fmaf(hv, wv.get(r * COLS + k), acc[k]);
     }
-    // R1 hand-off (the payload is 48 KB per row - too much to poll value by value): write-through data
-    // stores, drain, one flag per producer workgroup; one wave polls the row's 8 flags, then every
-    // thread reads its 16 values with write-through (L1-bypassing) loads - no fences
     const int par = t & 1;
     const unsigned epoch = static_cast<unsigned>(t + 1);
-    unsigned* data = reinterpret_cast<unsigned*>(slab) + (static_cast<long>(par) * Bp + b) * KS * G;
-    unsigned* flags = reinterpret_cast<unsigned*>(slab) + 2L * Bp * KS * G + static_cast<long>(b) * KS;
-#pragma unroll
-    for (int k = 0; k < COLS; ++k)
-      __hip_atomic_store((gu32*)(data + ks * G + tid * COLS + k), __float_as_uint(acc[k]), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) __hip_atomic_store((gu32*)(flags + ks), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid < 64) wait_flags<KS>(flags, epoch, err);
-    __syncthreads();
     float pv[KS][COLS];
+    if constexpr (GRAN) {
+      // data-is-the-flag: a producer can be at most one step ahead (its next partials need this step's h from
+      // every workgroup of the row), so the parity double buffer is never overwritten while still read
+      unsigned long long* gb = slab + (static_cast<long>(par) * Bp + b) * KS * G;
 #pragma unroll
-    for (int q = 0; q < KS; ++q)
+      for (int k = 0; k < COLS; ++k) put_granule(gb + ks * G + tid * COLS + k, epoch, acc[k]);
+      // poll in two halves of the producers with a scheduling fence between them: all 16 granules in flight at
+      // once (32 VGPRs) pushed the 96 register-resident weights into scratch at 3 waves per SIMD
+      // (summed as they arrive, in producer order - the same order as the flag path's sum)
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < COLS; ++k) pv[0][k] = 0.f;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+#pragma unroll
+          for (int q = half * (KS / 2); q < (half + 1) * (KS / 2); ++q)
+#pragma unroll
+            for (int k = 0; k < COLS; ++k) {
+              const unsigned long long x = __hip_atomic_load((gu64*)(gb + q * G + tid * COLS + k), __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
+              pv[0][k] += __uint_as_float(static_cast<unsigned>(x));
+              ok &= static_cast<unsigned>(x >> 32) == epoch;
+            }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (__all(ok)) break;
+        if (spins > kSplitPollLimit) {
+          if ((threadIdx.x & 63) == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    } else {
+      // R1 hand-off: write-through data stores, drain, one flag per producer workgroup; one wave polls the
+      // row's 8 flags, then every thread reads its 16 values with write-through (L1-bypassing) loads
+      unsigned* data = reinterpret_cast<unsigned*>(slab) + (static_cast<long>(par) * Bp + b) * KS * G;
+      unsigned* flags = reinterpret_cast<unsigned*>(slab) + 2L * Bp * KS * G + static_cast<long>(b) * KS;
 #pragma unroll
       for (int k = 0; k < COLS; ++k)
-        pv[q][k] = __uint_as_float(__hip_atomic_load((gu32*)(data + q * G + tid * COLS + k), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT));
+        __hip_atomic_store((gu32*)(data + ks * G + tid * COLS + k), __float_as_uint(acc[k]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store((gu32*)(flags + ks), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid < 64) wait_flags<KS>(flags, epoch, err);
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < KS; ++q)
+#pragma unroll
+        for (int k = 0; k < COLS; ++k)
+          pv[q][k] = __uint_as_float(__hip_atomic_load((gu32*)(data + q * G + tid * COLS + k), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT));
+    }
     float a[COLS];
     float sum = 0.f;
 #pragma unroll
     for (int k = 0; k < COLS; ++k) {
       float v = 0.f;
+      if constexpr (GRAN) {
+        v = pv[0][k];
+      } else {
 #pragma unroll
-      for (int q = 0; q < KS; ++q) v += pv[q][k];
+        for (int q = 0; q < KS; ++q) v += pv[q][k];
+      }
       a[k] = v;
       sum += v;
     }
@@ -908,14 +951,20 @@ void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* w
   if (H == 384 && split != nullptr) {
     const int Bp = (B + 7) / 8 * 8;
     const dim3 grid(Bp * kSplitKS);
-    if (w_dt == DT_BF16)
-      hipLaunchKernelGGL((lnlstm_fwd_split_kernel<384, 768, bf16_t>), grid, dim3(768), 0, s, xp, h0, c0,
-                         static_cast<const bf16_t*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, Bp, eps, out, c_all,
-                         xhat_h, rstd_h, gates, xhat_c, rstd_c, hT, cT, split->slab, split->err);
-    else
-      hipLaunchKernelGGL((lnlstm_fwd_split_kernel<384, 768, float>), grid, dim3(768), 0, s, xp, h0, c0,
-                         static_cast<const float*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, Bp, eps, out, c_all,
-                         xhat_h, rstd_h, gates, xhat_c, rstd_c, hT, cT, split->slab, split->err);
+    static const bool gran = [] {
+      const char* e = std::getenv("APPLESTAR_LSTM_FWD_GRANULE");   // A/B switch, off by default
+      return e != nullptr && e[0] == '1';
+    }();
+#define AS_FWD_SPLIT(TWv, GR)                                                                                    \
+    hipLaunchKernelGGL((lnlstm_fwd_split_kernel<384, 768, TWv, GR>), grid, dim3(768), 0, s, xp, h0, c0,          \
+                       static_cast<const TWv*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, Bp, eps, out, c_all, xhat_h,  \
+                       rstd_h, gates, xhat_c, rstd_c, hT, cT, split->slab, split->err)
+    if (w_dt == DT_BF16) {
+      if (gran) AS_FWD_SPLIT(bf16_t, true); else AS_FWD_SPLIT(bf16_t, false);
+    } else {
+      if (gran) AS_FWD_SPLIT(float, true); else AS_FWD_SPLIT(float, false);
+    }
+#undef AS_FWD_SPLIT
   } else if (H == 384) {
     if (w_dt == DT_BF16)
       hipLaunchKernelGGL((lnlstm_fwd_wide_kernel<384, 768, bf16_t>), dim3(B), dim3(768), 0, s, xp, h0, c0,

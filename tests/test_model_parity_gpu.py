@@ -252,7 +252,12 @@ def test_bf16_head_grad_error_not_from_upstream_or_loss(reference):
     pins = {k: g.detach() for k, g in zip(names, gs) if g is not None}
     assert any('target_logit' in k for k in pins) and any('value' in k for k in pins), list(pins)
     nat, up_nat = _pinned_grad_errors(cpu, batch, ref_grads, pins, native=True)
+    # the control's error on these groups moves run to run (0.04-0.10: atomics-order noise through flipped ReLU
+    # gates); as in test_full_model_bf16_gpu_vs_cpu_fp32, the bound is against the largest of three control runs
     ctl, up_ctl = _pinned_grad_errors(cpu, batch, ref_grads, pins, native=False)
+    for _ in range(2):
+        c2, _ = _pinned_grad_errors(cpu, batch, ref_grads, pins, native=False)
+        ctl = {k: max(ctl[k], c2.get(k, ctl[k])) for k in ctl}
     table = {k: {'native_bf16_pinned': nat[k], 'torch_bf16_pinned': ctl[k]} for k in nat}
     ups = {k: {'native_bf16': up_nat.get(k), 'torch_bf16': up_ctl.get(k)} for k in pins}
     print('pinned-upstream group errors:', json.dumps(table, indent=1, sort_keys=True))

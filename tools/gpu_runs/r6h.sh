@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_glue_fusions_gpu.py tests/test_model_parity_gpu.py tests/test_model_gpu.py -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r6h_pytest.txt 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_glue_fusions_gpu.py tests/test_model_parity_gpu.py tests/test_model_gpu.py -m gpu -q --timeout 200 --timeout-method thread > gpurun_out/r6h_pytest.txt 2>&1; rc=$?
 tail -2 gpurun_out/r6h_pytest.txt; [ $rc -eq 0 ] || exit 1
 b() {  # name precision env...
   N=$1; P=$2; shift 2
