@@ -533,6 +533,18 @@ void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* re
   const bf16_t* rp = static_cast<const bf16_t*>(res);
   bf16_t* op = static_cast<bf16_t*>(out);
   const bool k64 = Cin % 64 == 0;
+  static const bool small_m = [] {
+    const char* e = std::getenv("APPLESTAR_CONV_SMALLM");
+    return e == nullptr || e[0] != '0';
+  }();
+  const long mt = (static_cast<long>(B) * H * W + 127) / 128;
+  if (small_m && Cin % 32 == 0 && Cout % 32 == 0 && mt * ((Cout + 127) / 128) < 64) {
+    // few output tiles (the actor's B = 1..16 forwards: a 19 x 20 map is 3 row tiles - 3 workgroups walking all of
+    // K for ~20 us): 32-wide output tiles give 4x the workgroups
+    if (k64) launch<32, 64>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    else launch<32, 32>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    return;
+  }
   if (use_halo(W, Cin, Cout)) {        // narrow maps: halo window staged once per channel chunk
     int npc = 0;
     halo_pieces(W, &npc);

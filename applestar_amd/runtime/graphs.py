@@ -90,17 +90,36 @@ def _tree_clone(x):
     return x
 
 
-def _tree_copy_(dst, src):
+def _tree_pairs(dst, src, out):
     if torch.is_tensor(dst):
         if dst.shape != src.shape:
             raise ValueError(f'graphed input shape {tuple(src.shape)} != captured {tuple(dst.shape)}')
-        dst.copy_(src, non_blocking=True)
+        out.append((dst, src))
     elif isinstance(dst, dict):
         for k in dst:
-            _tree_copy_(dst[k], src[k])
+            _tree_pairs(dst[k], src[k], out)
     elif isinstance(dst, (list, tuple)):
         for a, b in zip(dst, src):
-            _tree_copy_(a, b)
+            _tree_pairs(a, b, out)
+    return out
+
+
+def _tree_copy_(dst, src):
+    """Refresh the captured inputs.  A policy request has ~70 tensor leaves: one blit per leaf was ~70 copy launches
+    in front of every replay (profiles/r6j_timeline_b1_policy_graph.txt); same-device leaves of one dtype class go
+    through the native multi-tensor copy (raw bytes, 64 leaves per launch)."""
+    dev, rest = [], []
+    for d, s in _tree_pairs(dst, src, []):
+        ok = d.is_cuda and s.is_cuda and d.device == s.device and d.dtype == s.dtype and d.is_contiguous() and \
+            s.is_contiguous()
+        (dev if ok else rest).append((d, s))
+    if len(dev) > 1:
+        from ..ops import native
+        native.ensure_loaded().multi_copy([d for d, _ in dev], [s for _, s in dev])
+    else:
+        rest += dev
+    for d, s in rest:
+        d.copy_(s, non_blocking=True)
 
 
 def _signature(x):
