@@ -28,6 +28,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kQ = 32;       // key / query / LSTM hidden size
+constexpr int kKP = kQ + 1;  // LDS pitch of a key row
 constexpr int kF = 256;      // func dim
 constexpr int kMaxN1 = 513;  // 512 entities + end token
 constexpr int kChunk = 3;    // ceil(513 / 256)
@@ -51,13 +52,15 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
   const int n1 = min(max(static_cast<int>(entity_num[b]), 0) + 1, n1_stride);
   const int en = n1 - 1;
 
-  __shared__ float s_key[kMaxN1 * kQ];
+  // keys at a 33-float pitch: thread t reads entity rows 3t..3t+2, so a 32-float pitch put a wave's 64 lanes on 2
+  // LDS banks (row stride 96 floats = 32 mod 64) - a 32-way conflict on every key read of the logit dot products
+  __shared__ float s_key[kMaxN1 * kKP];
   __shared__ float s_wih[kQ * 4 * kQ];   // [k][gate row]
   __shared__ float s_whh[kQ * 4 * kQ];
   __shared__ float s_wq2[32 * kThreads];
   __shared__ uint8_t s_sel[kMaxN1 + 3];
   __shared__ __align__(16) float s_he[kF];
-  __shared__ float s_x[kF];
+  __shared__ float s_x[kF / 32 * 33];    // 32-float segments at a 33-float pitch (the Wq2 slices read across them)
   __shared__ float s_qin[kQ];
   __shared__ float s_h[kQ];
   __shared__ float s_q[kQ];
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
   __shared__ int s_result;
 
   const long kb = static_cast<long>(b) * key_bstride;
-  for (int i = tid; i < n1 * kQ; i += kThreads) s_key[i] = Cvt<KT>::load(key, kb + i);
+  for (int i = tid; i < n1 * kQ; i += kThreads) s_key[(i / kQ) * kKP + i % kQ] = Cvt<KT>::load(key, kb + i);
   for (int i = tid; i < n1; i += kThreads) s_sel[i] = 0;
 
   // ---- register-resident weights
@@ -133,12 +136,12 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-    s_x[tid] = fmaxf(acc, 0.f);
+    s_x[(tid >> 5) * 33 + (tid & 31)] = fmaxf(acc, 0.f);
     __syncthreads();
     // (b) qin = Wq2 x + bq2
     float part = 0.f;
 #pragma unroll
-    for (int k = 0; k < 32; ++k) part += s_wq2[k * kThreads + tid] * s_x[qp * 32 + k];
+    for (int k = 0; k < 32; ++k) part += s_wq2[k * kThreads + tid] * s_x[qp * 33 + k];
     part += __shfl_xor(part, 1, kWave);
     part += __shfl_xor(part, 2, kWave);
     part += __shfl_xor(part, 4, kWave);
@@ -195,7 +198,7 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
         if (ok) {
           float d = 0.f;
 #pragma unroll
-          for (int c = 0; c < kQ; ++c) d += s_q[c] * s_key[n * kQ + c];
+          for (int c = 0; c < kQ; ++c) d += s_q[c] * s_key[n * kKP + c];
           val = d;
         }
         val *= inv_temp;
@@ -280,10 +283,10 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
       su_num = step + 1;
     } else {
       ++cnt;
-      if (tid < kQ) emb_sum += s_key[r * kQ + tid];
+      if (tid < kQ) emb_sum += s_key[r * kKP + tid];
       float d = 0.f;
 #pragma unroll
-      for (int k = 0; k < kQ; ++k) d += we1_row[k] * s_key[r * kQ + k];
+      for (int k = 0; k < kQ; ++k) d += we1_row[k] * s_key[r * kKP + k];
       he_sum += d;
     }
     // he = relu(We1 emb + be1), emb = key sum / cnt
