@@ -606,6 +606,7 @@ std::vector<at::Tensor> su_sample(const at::Tensor& key, const at::Tensor& c0, c
   TORCH_CHECK(N1 >= 1 && N1 <= 513, "su_sample: N+1 must be in [1, 513]");
   TORCH_CHECK(c0.scalar_type() == at::kFloat && c0.size(0) == B && c0.size(1) == 256, "su_sample: c0 [B,256] fp32");
   TORCH_CHECK(u.scalar_type() == at::kFloat && u.size(0) == B && u.size(1) == max_steps, "su_sample: u [B,steps]");
+  TORCH_CHECK(max_steps >= 1 && max_steps <= 64, "su_sample: 1..64 steps (the kernel stages the uniforms in LDS)");
   TORCH_CHECK(entity_num.scalar_type() == at::kLong && entity_num.numel() == B, "su_sample: entity_num int64 [B]");
   TORCH_CHECK(su_mask.scalar_type() == at::kByte && su_mask.numel() == B, "su_sample: su_mask uint8 [B]");
   TORCH_CHECK(wf.scalar_type() == at::kBFloat16 && wf.size(0) == 256 && wf.size(1) == 256, "su_sample: wf bf16");

@@ -28,7 +28,6 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kQ = 32;       // key / query / LSTM hidden size
-constexpr int kKP = kQ + 1;  // LDS pitch of a key row
 constexpr int kF = 256;      // func dim
 constexpr int kMaxN1 = 513;  // 512 entities + end token
 constexpr int kChunk = 3;    // ceil(513 / 256)
@@ -52,15 +51,15 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
   const int n1 = min(max(static_cast<int>(entity_num[b]), 0) + 1, n1_stride);
   const int en = n1 - 1;
 
-  // keys at a 33-float pitch: thread t reads entity rows 3t..3t+2, so a 32-float pitch put a wave's 64 lanes on 2
-  // LDS banks (row stride 96 floats = 32 mod 64) - a 32-way conflict on every key read of the logit dot products
-  __shared__ float s_key[kMaxN1 * kKP];
+  __shared__ float s_key[kMaxN1 * kQ];
   __shared__ float s_wih[kQ * 4 * kQ];   // [k][gate row]
   __shared__ float s_whh[kQ * 4 * kQ];
   __shared__ float s_wq2[32 * kThreads];
   __shared__ uint8_t s_sel[kMaxN1 + 3];
   __shared__ __align__(16) float s_he[kF];
-  __shared__ float s_x[kF / 32 * 33];    // 32-float segments at a 33-float pitch (the Wq2 slices read across them)
+  __shared__ float s_x[kF];
+  __shared__ float s_u[64];               // the row's uniforms, staged once (a global load per step sat on the
+                                          // critical path of every pointer step)
   __shared__ float s_qin[kQ];
   __shared__ float s_h[kQ];
   __shared__ float s_q[kQ];
@@ -68,8 +67,9 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
   __shared__ int s_result;
 
   const long kb = static_cast<long>(b) * key_bstride;
-  for (int i = tid; i < n1 * kQ; i += kThreads) s_key[(i / kQ) * kKP + i % kQ] = Cvt<KT>::load(key, kb + i);
+  for (int i = tid; i < n1 * kQ; i += kThreads) s_key[i] = Cvt<KT>::load(key, kb + i);
   for (int i = tid; i < n1; i += kThreads) s_sel[i] = 0;
+  for (int i = tid; i < max_steps && i < 64; i += kThreads) s_u[i] = u[static_cast<long>(b) * max_steps + i];
 
   // ---- register-resident weights
   uint32_t wf_row[kF / 2];  // bf16 pairs of Wf[tid, :]
@@ -120,28 +120,37 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
     // (a) x = relu(c0 + [bf + Wf he])
     float acc = c0_i;
     if (step > 0) {
-      acc += bf_i;
-      // he read 8 floats at a time, with a scheduling fence per chunk: unfenced, the compiler hoists all 256 LDS
-      // reads ahead of the FMAs and the live values push the weights out to AGPRs
+      // he read 32 floats (8 LDS reads in flight) per fenced chunk into 4 independent FMA chains: unfenced, the
+      // compiler hoists all 64 reads ahead of the FMAs and the live values push the weights out to AGPRs; one
+      // fence per 8 floats serialised the LDS latency 32 times per step
+      float a4[4] = {bf_i, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int j = 0; j < kF / 2; j += 4) {
-        const float4 h0 = *reinterpret_cast<const float4*>(s_he + 2 * j);
-        const float4 h1 = *reinterpret_cast<const float4*>(s_he + 2 * j + 4);
-        const float hv[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+      for (int j = 0; j < kF / 2; j += 16) {
+        float hv[32];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int q = 0; q < 8; ++q) {
+          const float4 h = *reinterpret_cast<const float4*>(s_he + 2 * j + 4 * q);
+          hv[4 * q] = h.x;
+          hv[4 * q + 1] = h.y;
+          hv[4 * q + 2] = h.z;
+          hv[4 * q + 3] = h.w;
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
           const uint32_t w2 = wf_row[j + e];
-          acc += __uint_as_float(w2 << 16) * hv[2 * e] + __uint_as_float(w2 & 0xffff0000u) * hv[2 * e + 1];
+          a4[e & 3] = fmaf(__uint_as_float(w2 << 16), hv[2 * e], a4[e & 3]);
+          a4[e & 3] = fmaf(__uint_as_float(w2 & 0xffff0000u), hv[2 * e + 1], a4[e & 3]);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      acc += (a4[0] + a4[1]) + (a4[2] + a4[3]);
     }
-    s_x[(tid >> 5) * 33 + (tid & 31)] = fmaxf(acc, 0.f);
+    s_x[tid] = fmaxf(acc, 0.f);
     __syncthreads();
     // (b) qin = Wq2 x + bq2
     float part = 0.f;
 #pragma unroll
-    for (int k = 0; k < 32; ++k) part += s_wq2[k * kThreads + tid] * s_x[qp * 33 + k];
+    for (int k = 0; k < 32; ++k) part += s_wq2[k * kThreads + tid] * s_x[qp * 32 + k];
     part += __shfl_xor(part, 1, kWave);
     part += __shfl_xor(part, 2, kWave);
     part += __shfl_xor(part, 4, kWave);
@@ -198,7 +207,7 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
         if (ok) {
           float d = 0.f;
 #pragma unroll
-          for (int c = 0; c < kQ; ++c) d += s_q[c] * s_key[n * kKP + c];
+          for (int c = 0; c < kQ; ++c) d += s_q[c] * s_key[n * kQ + c];
           val = d;
         }
         val *= inv_temp;
@@ -233,7 +242,7 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
     const int wv = tid >> 6;
     float wave_off = 0.f;
     const float total = scan[0] + scan[1] + scan[2] + scan[3];
-    const float target = u[static_cast<long>(b) * max_steps + step] * total;
+    const float target = s_u[step] * total;
     // the owner wave: the last wave with entities whose offset is <= target (every thread computes the same
     // offsets in the same order); the owner lane: the last lane of that wave whose exclusive prefix is <= target
     int owner_wave = 0;
@@ -283,10 +292,10 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
       su_num = step + 1;
     } else {
       ++cnt;
-      if (tid < kQ) emb_sum += s_key[r * kKP + tid];
+      if (tid < kQ) emb_sum += s_key[r * kQ + tid];
       float d = 0.f;
 #pragma unroll
-      for (int k = 0; k < kQ; ++k) d += we1_row[k] * s_key[r * kKP + k];
+      for (int k = 0; k < kQ; ++k) d += we1_row[k] * s_key[r * kQ + k];
       he_sum += d;
     }
     // he = relu(We1 emb + be1), emb = key sum / cnt
