@@ -143,15 +143,23 @@ class ScalarEncoder(nn.Module):
 
     def forward(self, x: Dict[str, torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         embedded, context, baseline = [], [], []
+        # actor inference under bf16 autocast: every piece in bf16 before the three concatenations (mixed fp32 / bf16
+        # pieces made torch.cat promote all ~16 of them to fp32 - a cast launch each, profiles/r6m_timeline_*)
+        lowp_inf = torch.is_autocast_enabled() and not torch.is_grad_enabled() and \
+            self.position_array.is_cuda
+        if lowp_inf:
+            from ..ops import native
         for name, kind, n_in, n_out, is_ctx, is_base in SCALAR_MODULES:
             m = self.encode_modules[name]
             if kind == 'emb':
                 # row gather + ReLU: one native launch per direction for the small tables (the index in its stored
                 # dtype, LDS-accumulated masked backward); last_action_type's 327 x 128 table gathers with
                 # index_select - torch's embedding_dense_backward took 0.9 ms for 390 rows of last_delay
-                e = ops.embed_relu(m.weight, x[name])
+                e = ops.embed_relu(native._bf16w(m.weight) if lowp_inf else m.weight, x[name])
             elif kind == 'bo':
                 e = m(x['beginning_order'], x['bo_location'])
+                if lowp_inf:
+                    e = e.to(torch.bfloat16)
             else:
                 v = x[name]
                 # integer feature columns: straight to the bf16 compute dtype under autocast (one cast; via fp32 it was
@@ -163,7 +171,7 @@ class ScalarEncoder(nn.Module):
                 context.append(e)
             if is_base:
                 baseline.append(e)
-        embedded.append(self.time_encoder(x['time']).to(embedded[0].dtype))
+        embedded.append(self.time_encoder(x['time']).to(torch.bfloat16 if lowp_inf else embedded[0].dtype))
         n = ops._native(embedded[0])
         if n is not None and n.has('col_assemble'):
             # the three concatenations in one launch, each module's gradient summed from its slices in one
