@@ -617,12 +617,13 @@ std::vector<at::Tensor> su_sample(const at::Tensor& key, const at::Tensor& c0, c
     TORCH_CHECK(t->scalar_type() == at::kFloat, "su_sample: fp32 weights");
   c10::hip::HIPGuard g(key.device().index());
   auto f = key.options().dtype(at::kFloat);
-  auto logits = at::full({B, max_steps, N1}, -1e9, f);
-  auto results = at::zeros({B, max_steps}, key.options().dtype(at::kLong));
-  auto logp = at::zeros({B, max_steps}, f);
+  // every element is written by the kernel (its prologue fills the steps a row does not run)
+  auto logits = at::empty({B, max_steps, N1}, f);
+  auto results = at::empty({B, max_steps}, key.options().dtype(at::kLong));
+  auto logp = at::empty({B, max_steps}, f);
   auto su_num = at::empty({B}, key.options().dtype(at::kLong));
   auto emb = at::empty({B, 32}, f);
-  auto extra = at::zeros({B, extra_units ? N1 : 1}, f);
+  auto extra = extra_units ? at::empty({B, 513}, f) : at::zeros({B, 1}, f);   // [B, 513]: the padded entity width
   as::su_sample(key.data_ptr(), dt(key), N1 * 32, c0.data_ptr<float>(), u.data_ptr<float>(),
                 entity_num.data_ptr<int64_t>(), su_mask.data_ptr<uint8_t>(),
                 reinterpret_cast<const uint16_t*>(wf.data_ptr()), bf.data_ptr<float>(), wq2.data_ptr<float>(),

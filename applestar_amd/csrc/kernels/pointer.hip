@@ -112,6 +112,17 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
   bool ended = su_mask[b] == 0;
   int su_num = ended ? 0 : max_steps;
   if (tid < kQ) s_h[tid] = 0.f;
+  // the outputs of the steps this row will not run (and the padding columns of those it does): -1e9 logits, zero
+  // results / log-probabilities - the host allocates them uninitialised (four fill launches per forward before);
+  // the barrier below orders these stores before the step loop's
+  {
+    const long lbase = static_cast<long>(b) * max_steps * n1_stride;
+    for (long i = tid; i < static_cast<long>(max_steps) * n1_stride; i += kThreads) logits_out[lbase + i] = kNeg;
+    for (int i = tid; i < max_steps; i += kThreads) {
+      results[static_cast<long>(b) * max_steps + i] = 0;
+      logp_out[static_cast<long>(b) * max_steps + i] = 0.f;
+    }
+  }
   __syncthreads();
 
   float lv[kChunk];
@@ -310,11 +321,12 @@ __global__ __launch_bounds__(kThreads, 1) void su_sample_kernel(
     const bool never_ended = su_mask[b] != 0 && !ended;
     float end_logit = 0.f;
     if (never_ended) end_logit = logits_out[(static_cast<long>(b) * max_steps + (max_steps - 1)) * n1_stride + en];
-    for (int n = tid; n < n1_stride; n += kThreads) {
+    // written at the padded width kMaxN1 (the model's [B, 513] extra-units map; zeros past this row's entities)
+    for (int n = tid; n < kMaxN1; n += kThreads) {
       float e = 0.f;
       if (never_ended && n < n1)
         e = logits_out[(static_cast<long>(b) * max_steps + (max_steps - 1)) * n1_stride + n] > end_logit ? 1.f : 0.f;
-      extra_out[static_cast<long>(b) * n1_stride + n] = e;
+      extra_out[static_cast<long>(b) * kMaxN1 + n] = e;
     }
   }
 }

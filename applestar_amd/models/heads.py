@@ -272,9 +272,8 @@ class SelectedUnitsHead(nn.Module):
             self.lstm.layers[0].cell, self.embed_fc1[0].weight, self.embed_fc1[0].bias, temperature,
             MAX_SELECTED_UNITS_NUM, self.extra_units)
         ae = self._ae_update(ae0, emb.to(ae0.dtype))
-        ex = torch.zeros(B, MAX_ENTITY_NUM + 1, device=key.device)
-        if self.extra_units:
-            ex[:, :N1] = extra
+        # the kernel writes the extra-units map at the padded width (zeros past each row's entities)
+        ex = extra if self.extra_units else torch.zeros(B, MAX_ENTITY_NUM + 1, device=key.device)
         return logits, results, ae, su_num, ex
 
     def forward_sample(self, ae0, entity_embedding, entity_num, su_mask, temperature: float = 1.0,

@@ -188,6 +188,13 @@ class Policy(nn.Module):
 
     def forward(self, lstm_output, entity_embeddings, map_skip, scalar_context, entity_num, temperature=1.0,
                 race_mask=None, noise: Optional[Dict[str, torch.Tensor]] = None):
+        if noise is None and lstm_output.is_cuda:
+            # every head's sampling uniforms in two launches (was one torch.rand per head, six launches per step)
+            B = lstm_output.shape[0]
+            u5 = torch.rand(5, B, device=lstm_output.device)
+            noise = {'action_type': u5[0], 'delay': u5[1], 'queued': u5[2], 'target_unit': u5[3],
+                     'target_location': u5[4],
+                     'selected_units': torch.rand(B, MAX_SELECTED_UNITS_NUM, device=lstm_output.device)}
         noise = noise or {}
         logit, action = {}, {}
         logit['action_type'], action['action_type'], emb = self.action_type_head(
