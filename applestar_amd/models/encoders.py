@@ -145,7 +145,7 @@ class ScalarEncoder(nn.Module):
         embedded, context, baseline = [], [], []
         # actor inference under bf16 autocast: every piece in bf16 before the three concatenations (mixed fp32 / bf16
         # pieces made torch.cat promote all ~16 of them to fp32 - a cast launch each, profiles/r6m_timeline_*)
-        lowp_inf = torch.is_autocast_enabled() and not torch.is_grad_enabled() and \
+        lowp_inf = SCALAR_BF16_INFERENCE and torch.is_autocast_enabled() and not torch.is_grad_enabled() and \
             self.position_array.is_cuda
         if lowp_inf:
             from ..ops import native
@@ -414,6 +414,8 @@ class SpatialEncoder(nn.Module):
 
 
 SCALAR_SIDE_STREAM = True
+# bf16 inference: the scalar encoder's concatenated pieces kept in bf16 (APPLESTAR_SCALAR_BF16_INFERENCE=0: as trained)
+SCALAR_BF16_INFERENCE = os.environ.get('APPLESTAR_SCALAR_BF16_INFERENCE', '1') == '1'
 # set by runtime.graphs.GraphedPolicy while capturing / replaying: shape-static entity path
 STATIC_SHAPES = False
 # static (graph-captured) entity path: attention on the native varlen kernel over 2B segments

@@ -125,11 +125,13 @@ def _bf16_grad_errors(cpu, batch, ref_grads, native: bool):
     return _group_errors(got, ref_grads), out, info
 
 
-def _su_logit_spread(cpu, seeds):
-    """Mean selected-units logit error of the bf16 trainer over several batches, native kernels on and off."""
+def _su_logit_spread(cpu, seeds, control_runs: int = 3):
+    """Mean selected-units logit error of the bf16 trainer over several batches, native kernels on and off.  The
+    torch control is not deterministic run to run (0.028-0.039 over four runs of the same batches on one box,
+    r6p), so - as for the gradient groups - its level is the largest of ``control_runs`` runs."""
     from applestar_amd import ops
     res = {}
-    for native in (True, False):
+    for native in [True] + [False] * control_runs:
         ops.set_native(native)
         try:
             tr = RLTrainer(CFG, device='cuda')
@@ -144,7 +146,8 @@ def _su_logit_spread(cpu, seeds):
                 errs.append(_masked_rel(out['target_logit']['selected_units'].float(), ref))
         finally:
             ops.set_native(True)
-        res['native' if native else 'torch'] = sum(errs) / len(errs)
+        key = 'native' if native else 'torch'
+        res[key] = max(res.get(key, 0.0), sum(errs) / len(errs))
     return res
 
 
@@ -171,6 +174,7 @@ def test_full_model_bf16_gpu_vs_cpu_fp32(reference):
     # torch's own autocast 2.1-5.6 %, native 1.8-4.9 %, means 3.4 / 3.1 %), so they are judged on the mean over
     # four batches against the torch control's mean instead of one seed's value
     su = _su_logit_spread(cpu, [3, 0, 1, 2])
+    print('selected-units logit error, mean of four batches:', su)
     assert su['native'] <= max(3e-2, 1.15 * su['torch']), su
     assert _rel(out['value']['winloss'].float(), ref_out['value']['winloss']) < 3e-2
     a, r = float(info['total_loss']), float(ref_info['total_loss'])
