@@ -136,6 +136,11 @@ class GLU(nn.Module):
 
     def forward(self, x, context):
         g = ops.linear(context, self.layer1[0].weight, self.layer1[0].bias, act='sigmoid')
+        if g.dtype == torch.bfloat16 and x.dtype == torch.float32 and x.is_cuda and not torch.is_grad_enabled():
+            # bf16 inference, fp32 x (the core LSTM output): the same fp32 product after an exact upcast of the gate -
+            # torch's mixed-dtype (templated) product kernel ran 37 us at B = 1, these are two ~5 us launches.  (x
+            # rounded to bf16 first instead moved the selected-units logits: test_full_model_bf16_gpu_vs_cpu_fp32)
+            g = g.float()
         return self.layer2(g * x)
 
 

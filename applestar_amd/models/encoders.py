@@ -11,6 +11,7 @@ Parameter names/shapes match ``distar/agent/default/model/obs_encoder/*.py`` and
 """
 from __future__ import annotations
 
+import math
 import os
 
 from typing import Dict, List, Tuple, Optional
@@ -115,6 +116,7 @@ SCALAR_MODULES = [
     ('unit_order_type', 'fc', gd.NUM_UNIT_MIX_ABILITIES, 64, True, False),
 ]
 TIME_DIM = 32
+_TIME_PHASE = {}      # (device, dim) -> the sine phase row (0, pi/2, 0, pi/2, ...) of the bf16 time encoding
 
 
 class ScalarEncoder(nn.Module):
@@ -134,8 +136,19 @@ class ScalarEncoder(nn.Module):
         # the reference registers the build-order transformer after the loop -> last in state_dict
         self.encode_modules['beginning_order'] = BeginningBuildOrderEncoder(64)
 
-    def time_encoder(self, t: torch.Tensor) -> torch.Tensor:
-        ang = t.float().unsqueeze(1) * self.position_array
+    def time_encoder(self, t: torch.Tensor, out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+        pos = self.position_array
+        if out_dtype is not None and out_dtype != torch.float32:
+            # bf16 inference: cos(a) = sin(a + pi/2), so one multiply-add and one sine that writes bf16 (was mul,
+            # sin, cos, two strided copies and a cast: 6 launches); the fp32 phase add rounds far below bf16's step
+            key = (pos.device, pos.shape[-1])
+            ph = _TIME_PHASE.get(key)
+            if ph is None:
+                ph = _TIME_PHASE[key] = torch.zeros(pos.shape[-1], device=pos.device)
+                ph[1::2] = math.pi / 2
+            out = torch.empty(t.shape[0], pos.shape[-1], dtype=out_dtype, device=t.device)
+            return torch.sin(torch.addcmul(ph, t.float().unsqueeze(1), pos), out=out)
+        ang = t.float().unsqueeze(1) * pos
         out = torch.empty_like(ang)
         out[:, 0::2] = torch.sin(ang[:, 0::2])
         out[:, 1::2] = torch.cos(ang[:, 1::2])
@@ -171,7 +184,8 @@ class ScalarEncoder(nn.Module):
                 context.append(e)
             if is_base:
                 baseline.append(e)
-        embedded.append(self.time_encoder(x['time']).to(torch.bfloat16 if lowp_inf else embedded[0].dtype))
+        embedded.append(self.time_encoder(x['time'], torch.bfloat16) if lowp_inf else
+                        self.time_encoder(x['time']).to(embedded[0].dtype))
         n = ops._native(embedded[0])
         if n is not None and n.has('col_assemble'):
             # the three concatenations in one launch, each module's gradient summed from its slices in one
@@ -341,7 +355,7 @@ class EntityEncoder(nn.Module):
         if self.reduce_type.startswith('attention_pool'):
             pooled = self.attention_pool(x * vm, num=entity_num, mask=valid)
             return entity_embeddings, self.embed_fc(pooled.to(x.dtype)), valid
-        summed = (x * vm).float().sum(1)
+        summed = (x * vm).sum(1, dtype=torch.float32)      # fp32 accumulation inside the reduce (no fp32 copy)
         if self.reduce_type == 'constant':
             mean = summed / 512
         else:
