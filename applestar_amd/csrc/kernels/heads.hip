@@ -104,11 +104,26 @@ __global__ __launch_bounds__(kHT) void head_sample_kernel(const TL* __restrict__
   const long len = lens ? lens[b] : C;
   float* row = out_logits + static_cast<long>(b) * C;
   const bool lds = C <= kRowLds;
-  for (int i = threadIdx.x; i < C; i += kHT) {
-    float v = ld(logits, static_cast<long>(b) * ld_logits + i) * inv_t;
-    if ((mask && !mask[static_cast<long>(b) * mask_ld + i]) || i >= len) v = kNeg;
-    row[i] = v;
-    if (lds) srow[i] = v;
+  // 8 independent loads in flight per thread before any store (the 24,320-wide location row is 95 loads per thread:
+  // one at a time, the workgroup waited on memory 75 % of its cycles, profiles/r7c_pmc_inf_b1_a_summary.txt)
+  constexpr int kU = 8;
+  for (int i0 = threadIdx.x; i0 < C; i0 += kHT * kU) {
+    float v[kU];
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const int i = i0 + j * kHT;
+      v[j] = i < C ? ld(logits, static_cast<long>(b) * ld_logits + i) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < kU; ++j) {
+      const int i = i0 + j * kHT;
+      if (i < C) {
+        float x = v[j] * inv_t;
+        if ((mask && !mask[static_cast<long>(b) * mask_ld + i]) || i >= len) x = kNeg;
+        row[i] = x;
+        if (lds) srow[i] = x;
+      }
+    }
   }
   __syncthreads();
   const int a = lds ? sample_row(srow, C, u[b], red, scan) : sample_row(row, C, u[b], red, scan);
