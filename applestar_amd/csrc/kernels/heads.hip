@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kHT) void target_unit_kernel(const TE* __restrict__
                                                           const float* __restrict__ b2, const TK* __restrict__ key,
                                                           int N, const int64_t* __restrict__ lens, float inv_t,
                                                           const float* __restrict__ u, float* __restrict__ out_logits,
-                                                          int64_t* __restrict__ action) {
+                                                          int64_t* __restrict__ action, bool w1_vec) {
   constexpr int IN = 1024, KD = 32;
   __shared__ float red[4];
   __shared__ float scan[kHT];
@@ -151,7 +151,18 @@ __global__ __launch_bounds__(kHT) void target_unit_kernel(const TE* __restrict__
     const int o = threadIdx.x >> 3, part = threadIdx.x & 7;
     float s = 0.f;
     const TE* er = e + static_cast<long>(b) * IN;
-    for (int i = part; i < IN; i += 8) s += w1[o * IN + i] * ld(er, i);
+    if (w1_vec) {
+      // 16-B rows: the 8 lanes of an output read 128 contiguous bytes per load, 32 loads per thread (the scalar loop
+      // below is 128 loads whose wave-wide footprint is 8 scattered 32-B pieces each)
+      const float4* w4 = reinterpret_cast<const float4*>(w1 + o * IN);
+#pragma unroll 4
+      for (int k = part; k < IN / 4; k += 8) {
+        const float4 w = w4[k];
+        s += w.x * ld(er, 4 * k) + w.y * ld(er, 4 * k + 1) + w.z * ld(er, 4 * k + 2) + w.w * ld(er, 4 * k + 3);
+      }
+    } else {
+      for (int i = part; i < IN; i += 8) s += w1[o * IN + i] * ld(er, i);
+    }
     s += __shfl_xor(s, 1, kWave);
     s += __shfl_xor(s, 2, kWave);
     s += __shfl_xor(s, 4, kWave);
@@ -202,7 +213,8 @@ void target_unit_sample(const void* e, int e_dt, const float* w1, const float* b
   if (B <= 0) return;
 #define AS_TU(TE, TK)                                                                                             \
   hipLaunchKernelGGL((target_unit_kernel<TE, TK>), dim3(B), dim3(kHT), 0, s, static_cast<const TE*>(e), w1, b1, w2, \
-                     b2, static_cast<const TK*>(key), N, lens, inv_t, u, out_logits, action)
+                     b2, static_cast<const TK*>(key), N, lens, inv_t, u, out_logits, action, w1_vec)
+  const bool w1_vec = (reinterpret_cast<uintptr_t>(w1) & 15) == 0;
   if (e_dt == DT_BF16) {
     if (key_dt == DT_BF16) AS_TU(bf16_t, bf16_t); else AS_TU(bf16_t, float);
   } else {
