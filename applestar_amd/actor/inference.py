@@ -203,13 +203,29 @@ class InferenceServer:
             sub = ModelSubscriber(m, shm_name)
             sd = m.policy_state_dict() if hasattr(m, 'policy_state_dict') else m.state_dict()
             layout = FlatLayout({k: v for k, v in sd.items() if v.dtype == torch.float32})
-            if layout.numel != sub.slot.numel:
+            try:
+                sub.bind(layout)           # element count AND the (name, shape) hash the publisher stamped
+            except ValueError:
                 sub.close()
                 return False
-            sub.bind(layout)
             self._subscribers = getattr(self, '_subscribers', {})
+            old = self._subscribers.pop(player_id, None)
+            if old is not None:
+                old.close()
             self._subscribers[player_id] = sub
         return True
+
+    def detach_model_slot(self, player_id: str) -> None:
+        """Stop reading ``player_id``'s slot (it went stale, or the network broadcast overtook it)."""
+        with self._lock:
+            sub = getattr(self, '_subscribers', {}).pop(player_id, None)
+        if sub is not None:
+            sub.close()
+
+    def model_slot_state(self, player_id: str) -> Optional[str]:
+        """None (not attached), 'live' or 'stale' (the path now names another publisher's slot)."""
+        sub = getattr(self, '_subscribers', {}).get(player_id)
+        return None if sub is None else ('stale' if sub.stale else 'live')
 
     def poll_model_slots(self) -> Dict[str, int]:
         """Apply any newer published versions; returns {player_id: model_last_iter} of the updated ones."""

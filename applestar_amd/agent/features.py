@@ -28,7 +28,7 @@ from ..lib.features import (SPATIAL_SIZE, SPATIAL_INFO, ENTITY_INFO, EFFECT_LEN,
 from ..lib.game_data import (ACTIONS, NUM_UNIT_TYPES, NUM_UPGRADES, NUM_UNIT_MIX_ABILITIES,
                              NUM_CUMULATIVE_STAT_ACTIONS, BEGINNING_ORDER_ACTIONS, CUMULATIVE_STAT_ACTIONS,
                              UNIT_TYPES_REORDER_ARRAY, BUFFS_REORDER_ARRAY, UPGRADES_REORDER_ARRAY,
-                             ADDON_REORDER_ARRAY, UNIT_ABILITY_REORDER, ABILITY_TO_QUEUE_ACTION, ABILITY_TO_GABILITY,
+                             ADDON_REORDER_ARRAY, UNIT_ABILITY_REORDER, ABILITY_TO_QUEUE_ACTION, RAW_ABILITY_FUNCS,
                              FUNC_ID_TO_ACTION_TYPE_DICT)
 
 MINIMAP_LAYERS = ['height_map', 'visibility_map', 'creep', 'player_relative', 'alerts', 'pathable', 'buildable']
@@ -435,22 +435,28 @@ def _field(msg, name):
 _CANCEL_SLOT = {313, 1039, 305, 307, 309, 1832, 1834, 3672}
 _UNLOAD_UNIT = {410, 415, 397, 1440, 2373, 1409, 914, 3670}
 _FRIVOLOUS = {6, 7}
-_ACTION_BY_GABILITY = defaultdict(dict)
-for _i, _a in enumerate(ACTIONS):
-    if _a['general_ability_id']:
-        _ACTION_BY_GABILITY[_a['general_ability_id']][_a['name'].rsplit('_', 1)[-1]] = _i
+_CMD_TYPE = {'quick': 'raw_cmd', 'pt': 'raw_cmd_pt', 'unit': 'raw_cmd_unit', 'autocast': 'raw_autocast'}
 
 
 def action_type_from_ability(ability_id: int, kind: str) -> Optional[int]:
-    """Map a raw ability id + command kind (quick / pt / unit / autocast) to an action type index."""
+    """Map a raw ability id + command kind (quick / pt / unit / autocast) to an action type index, as the reference's
+    ``transfer_action_type`` (``features.py:862-880``): frivolous abilities drop, unloads become unload-all and slot
+    cancels cancel-quick, a specific ability becomes its general one, then the raw function of that command type.
+    None where the reference prints an invalid ability (no such function, or one outside the action table)."""
     if ability_id in _FRIVOLOUS:
         return None
     if ability_id in _UNLOAD_UNIT:
         ability_id = 3664
     elif ability_id in _CANCEL_SLOT:
         ability_id = 3671
-    g = ABILITY_TO_GABILITY.get(ability_id, ability_id)
-    return _ACTION_BY_GABILITY.get(g, {}).get(kind)
+    fns = RAW_ABILITY_FUNCS.get(ability_id)
+    if not fns:
+        return None
+    gen = next(iter(fns.values()))[1]
+    if gen:
+        ability_id = gen
+    f = RAW_ABILITY_FUNCS.get(ability_id, {}).get(_CMD_TYPE[kind])
+    return FUNC_ID_TO_ACTION_TYPE_DICT.get(f[0]) if f is not None else None
 
 
 @sw.decorate('transform_action')

@@ -9,11 +9,24 @@ and produces a plausible, slowly growing unit population so featurization, varle
 model see realistic entity counts (tens early, hundreds later, capped at 512 after cargo).
 
 Game dynamics are synthetic: actions are accepted (``action_result`` Success with a small error
-rate), units appear/die at random, and the outcome is decided by accumulated "army value" with noise.
+rate), units appear/die at random, and by default the outcome is decided by accumulated "army value" with
+noise - no action influences it.
+
+Learnable mode (``env.fake_learnable: true``) makes the actions matter, so a training run can show that the
+whole pipeline learns (agent -> inference server -> data plane -> HBM ring -> learner -> model push -> actor):
+a fixed quarter of the 327 action types is "rewarded" (:data:`REWARDED_ACTION_TYPES`); an episode lasts
+``fake_episode_agent_steps`` agent steps; player i's rate r_i is the fraction of its steps whose action type is
+rewarded (a bot plays ``fake_bot_rate``, the rate of a uniform policy); player 1 wins with probability
+clip(0.5 + r_1 - r_2, 0, 1).  A uniform policy wins half its games against the bot, a policy that learned the
+set wins all of them.  ``fake_stats_path``: every finished episode appends one JSON line (time, episode, each
+agent slot's rate and result) - the actor-side learning curve.
 """
 from __future__ import annotations
 
+import json
+import os
 import random
+import time
 from typing import Dict, List, Optional
 
 import numpy as np
@@ -22,6 +35,7 @@ from . import raw as R
 from .map_info import get_map_size
 from ..agent.features import transform_action, MINIMAP_LAYERS
 from ..lib.game_data import UNIT_TYPES, UNIT_SPECIFIC_ABILITIES, ABILITY_TO_QUEUE_ACTION, BUFFS, ACTIONS
+from ..lib.game_data import FUNC_ID_TO_ACTION_TYPE_DICT
 
 RANDOM_MAPS = ['KairosJunction', 'KingsCove', 'NewRepugnancy']  # env.py:64
 POSSIBLE_RESULTS = {R.RESULT_VICTORY: 1, R.RESULT_DEFEAT: -1, R.RESULT_TIE: 0, R.RESULT_UNDECIDED: 0}
@@ -31,6 +45,8 @@ _QUEUE_ABILITIES = [a for a in range(len(ABILITY_TO_QUEUE_ACTION)) if int(ABILIT
 _ORDER_ABILITIES = [a for a in UNIT_SPECIFIC_ABILITIES if a]
 _UNIT_POOL = [u for u in UNIT_TYPES if u not in (86, 18, 59)]
 _BUFF_POOL = [b for b in BUFFS if b]
+# learnable mode: the rewarded action types (a fixed quarter of the 327, no_op excluded)
+REWARDED_ACTION_TYPES = frozenset(a for a in range(len(ACTIONS)) if a % 4 == 1)
 
 
 class _PlayerState:
@@ -116,6 +132,10 @@ class FakeSC2Env:
         self._seed = None if seed in (None, 'none') else int(seed)
         self._agent_slots = [i for i, p in enumerate(self._player_ids) if 'bot' not in p]
         self._num_agents = len(self._agent_slots)
+        self._learnable = bool(env.get('fake_learnable', False))
+        self._ep_agent_steps = int(env.get('fake_episode_agent_steps', 32))
+        self._bot_rate = float(env.get('fake_bot_rate', len(REWARDED_ACTION_TYPES) / len(ACTIONS)))
+        self._stats_path = env.get('fake_stats_path', None)
         self._episode_count = 0
         self._rng = np.random.default_rng(self._seed)
         self._done = True
@@ -199,6 +219,8 @@ class FakeSC2Env:
         self._game_loop = 0
         self._next_obs_step = [0] * self._num_agents
         self._action_result = [[0] for _ in range(self._num_agents)]
+        self._steps = [0] * self._num_agents            # learnable mode: agent steps / rewarded steps per slot
+        self._rewarded = [0] * self._num_agents
         self._done = False
         self._game_info = []
         for slot in range(self._num_agents):
@@ -224,6 +246,10 @@ class FakeSC2Env:
                     c, s = transform_action(a)
                     cmds += c
                     skip = max(skip, s) if skip else s
+                if actions[slot]:
+                    self._steps[slot] += 1
+                    at = FUNC_ID_TO_ACTION_TYPE_DICT.get(actions[slot][0].get('func_id'), 0)
+                    self._rewarded[slot] += int(at in REWARDED_ACTION_TYPES)
                 self._next_obs_step[slot] = self._game_loop + max(1, skip)
                 max_skip = max(max_skip, skip)
                 ok = self._rng.random() > self._error_rate
@@ -240,17 +266,44 @@ class FakeSC2Env:
         self._game_loop = target
         return self._observe()
 
+    def _rates(self):
+        """Learnable mode: each player's rewarded-action rate (bots: ``fake_bot_rate``)."""
+        rates = [self._bot_rate, self._bot_rate]
+        for slot, i in enumerate(self._agent_slots):
+            rates[i] = self._rewarded[slot] / max(self._steps[slot], 1)
+        return rates
+
+    def _log_episode(self, rates, res):
+        if not self._stats_path:
+            return
+        line = json.dumps({'t': time.time(), 'pid': os.getpid(), 'episode': self._episode_count,
+                           'agent_steps': list(self._steps),
+                           'rate': [round(rates[i], 4) for i in self._agent_slots],
+                           'win': [int(res[i] == R.RESULT_VICTORY) for i in self._agent_slots]}) + '\n'
+        fd = os.open(self._stats_path, os.O_WRONLY | os.O_APPEND | os.O_CREAT, 0o644)
+        try:
+            os.write(fd, line.encode())      # one O_APPEND write per line: whole lines from many env processes
+        finally:
+            os.close(fd)
+
     def _observe(self):
-        done = self._game_loop >= self._episode_length
+        done = self._game_loop >= self._episode_length or \
+            (self._learnable and max(self._steps) >= self._ep_agent_steps)
         reward = [0] * self._num_agents
         results = None
-        if done:
+        if done and self._learnable:
+            rates = self._rates()
+            p1_wins = self._rng.random() < min(1.0, max(0.0, 0.5 + rates[0] - rates[1]))
+        elif done:
             a, b = self._players[0].army_value, self._players[1].army_value
             p1_wins = (a + self._rng.normal(0, 5)) >= b
+        if done:
             res = [R.RESULT_VICTORY, R.RESULT_DEFEAT] if p1_wins else [R.RESULT_DEFEAT, R.RESULT_VICTORY]
             results = [R.PlayerResult(player_id=1, result=res[0]), R.PlayerResult(player_id=2, result=res[1])]
             for slot in range(self._num_agents):
                 reward[slot] = POSSIBLE_RESULTS[res[self._agent_slots[slot]]]
+            if self._learnable:
+                self._log_episode(rates, res)
             self._done = True
         agent_slots = [s for s in range(self._num_agents) if done or self._next_obs_step[s] <= self._game_loop]
         full = {s: self._observation(self._agent_slots[s], results) for s in range(self._num_agents)}

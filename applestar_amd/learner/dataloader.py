@@ -12,6 +12,7 @@ runs on a side HIP stream one batch ahead of compute (:class:`DevicePrefetcher`)
 """
 from __future__ import annotations
 
+import logging
 import os
 import queue
 import random
@@ -72,16 +73,19 @@ class RLDataLoader:
         # diagnostics (tools/bench_pipeline.py): 'discard' keeps receiving once the ring is full but drops the frames
         # (receive cost without the ring insert / H2D copy); 'unpinned' receives into pageable memory
         mode = os.environ.get('APPLESTAR_RING_DIAG', '')
+        ring = self._ring        # this thread's ring: close() drops self._ring only once the thread has exited
         while not self._stop.is_set():
-            if mode == 'discard' and len(self._ring) >= self.buffer_size:
+            if mode == 'discard' and len(ring) >= self.buffer_size:
                 self._pull(1, raw=True)
                 continue
             with self._avail:
-                while len(self._ring) >= self.buffer_size and not self._stop.is_set():
+                while len(ring) >= self.buffer_size and not self._stop.is_set():
                     self._avail.wait(0.5)
-            alloc = None if mode == 'unpinned' else self._ring.stage      # bytes land in pinned staging
+            alloc = None if mode == 'unpinned' else ring.stage      # bytes land in pinned staging
             for frame in self._pull(1, raw=True, alloc=alloc):
-                self._ring.put(frame)
+                if self._stop.is_set():
+                    break
+                ring.put(frame)
                 with self._avail:
                     self._avail.notify_all()
 
@@ -137,9 +141,11 @@ class RLDataLoader:
         ring = getattr(self, '_ring', None)
         return ring.capacity if ring is not None else None
 
-    def close(self, timeout: float = 5.0):
+    def close(self, timeout: float = 5.0) -> bool:
         """Stop the ingest thread, wait for it, and release the HBM ring (its arena goes back to the caching
-        allocator; the caller may ``torch.cuda.empty_cache()`` before sizing a new ring from free memory)."""
+        allocator; the caller may ``torch.cuda.empty_cache()`` before sizing a new ring from free memory).
+        Returns False when the thread did not exit within ``timeout``: the ring is then kept (the thread may still
+        be inserting a frame into it) and freed by a later ``close``."""
         self._stop.set()
         if getattr(self, '_avail', None) is not None:
             with self._avail:
@@ -147,9 +153,15 @@ class RLDataLoader:
         t = getattr(self, '_thread', None)
         if t is not None and t.is_alive() and t is not threading.current_thread():
             t.join(timeout)
+            if t.is_alive():
+                logging.getLogger(__name__).warning(
+                    'RLDataLoader.close: ingest thread still running after %.1f s; keeping its ring', timeout)
+                self._iter = iter(())
+                return False
         self._iter = iter(())
         if getattr(self, '_ring', None) is not None:
             self._ring = None
+        return True
 
 
 class SyntheticRLDataLoader:

@@ -44,9 +44,11 @@ DEFAULT_RL_LEARNER_CONFIG = {
 }
 
 
-def model_slot_name(player_id: str) -> str:
-    """The /dev/shm slot of a player's published policy (runtime/flat_model.SharedModelSlot)."""
-    return f'applestar_model_{player_id}_{os.getuid()}'
+def model_slot_name(player_id: str, experiment: str = '') -> str:
+    """The /dev/shm slot of a player's published policy (runtime/flat_model.SharedModelSlot): per experiment, player
+    and user, so two experiments on one host that both train ``MP0`` never share a slot."""
+    exp = ''.join(ch if ch.isalnum() or ch in '-_.' else '_' for ch in str(experiment)) or 'default'
+    return f'applestar_model_{exp}_{player_id}_{os.getuid()}'
 
 
 class LearnerComm:
@@ -96,7 +98,8 @@ class LearnerComm:
         with self._lock:
             if self._publisher is None:
                 from ..runtime.flat_model import ModelPublisher
-                shm = model_slot_name(self.player_id) if learner.device.type == 'cuda' else None
+                shm = (model_slot_name(self.player_id, self.cfg.common.get('experiment_name', ''))
+                       if learner.device.type == 'cuda' else None)
                 self._publisher = ModelPublisher(sd, shm_name=shm)
             self._publisher.publish(sd, learner.last_iter.val, reset_flag)
         self._pending.set()
@@ -241,8 +244,8 @@ class RLLearner(BaseLearner):
         # the new one is sized, and the new ring keeps the old capacity: sizing it from mem_get_info while the old
         # ~hundreds-of-GB arena is still allocated would shrink it to the floor
         keep_bytes = getattr(self.dataloader, 'ring_bytes', None)
-        if hasattr(self.dataloader, 'close'):
-            self.dataloader.close()
+        if hasattr(self.dataloader, 'close') and self.dataloader.close() is False:
+            self.dataloader.close(timeout=30.0)   # the ingest thread was mid-frame: its ring must go first
         self.dataloader = None
         if self.device.type == 'cuda':
             torch.cuda.synchronize(self.device)

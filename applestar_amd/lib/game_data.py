@@ -69,6 +69,13 @@ UNIT_ABILITY_REORDER[0] = 0
 
 FUNC_ID_TO_ACTION_TYPE_DICT = {a['func_id']: i for i, a in enumerate(ACTIONS)}
 
+# raw ability id -> {command type: (func id, general ability id)} from the pysc2 raw function table
+# (distar/pysc2/lib/actions.py:1183-1763 RAW_ABILITY_IDS; every ability has at most one function per command type
+# and one general id, so the table is order-free): replay decoding (agent/features.py action_type_from_ability)
+RAW_ABILITY_FUNCS = {}
+for _fid, _name, _ftype, _ab, _gen in _RAW['raw_functions']:
+    RAW_ABILITY_FUNCS.setdefault(_ab, {})[_ftype] = (_fid, _gen)
+
 # queue actions: every Train_* / Research* action, indexed from 1 (0 = no-op)
 QUEUE_ACTIONS = [i for i, a in enumerate(ACTIONS) if 'Train_' in a['name'] or 'Research' in a['name']]
 # later entries sharing a general ability overwrite earlier ones (reference dict-insertion order)

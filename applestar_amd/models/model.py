@@ -116,9 +116,10 @@ class _TakeRows(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        if ctx.link is not None and g.dtype == torch.float32:
+        if ctx.link is not None and g.dtype == torch.float32 and not ctx.link.consumed:
             # hand the gradient to the ResBlock consuming this map (ops/native.py SkipLink): it adds it, NHWC,
-            # to the first n rows of its input gradient; no full-height gradient here, no autograd add
+            # to the first n rows of its input gradient; no full-height gradient here, no autograd add.  A link
+            # whose ResBlock backward already ran (consumed) falls through to the ordinary gradient below
             nhwc = g.permute(0, 2, 3, 1)
             ctx.link.g = nhwc if nhwc.is_contiguous() else nhwc.contiguous()
             return None, None, None

@@ -787,10 +787,33 @@ def _count_use(p) -> None:
 
 
 def _single_use(p) -> bool:
-    """``p`` fed exactly one native node in this step's forward: autograd returns that node's gradient as is
-    (a weight used twice would have its gradients summed by autograd, reading a deferred result early)."""
+    """``p`` fed exactly one native node in this step's forward AND has exactly one consumer in this step's
+    autograd graph (``single_consumer_params``, checked by :func:`defer_begin`): autograd returns that node's
+    gradient as is.  A weight with a second consumer - another native node, or an uncounted path such as
+    ``F.linear`` or a torch fallback - would have its gradients summed by autograd on the main stream into a
+    buffer the side stream has not written yet."""
     u = getattr(p, '_as_uses', None)
-    return u is not None and u == (_FWD_EPOCH[0], 1)
+    return u is not None and u == (_FWD_EPOCH[0], 1) and getattr(p, '_as_one_consumer', -1) == _FWD_EPOCH[0]
+
+
+def single_consumer_params(root) -> list:
+    """The leaf tensors that exactly ONE edge of ``root``'s autograd graph reaches (their AccumulateGrad node has
+    one producer of its gradient).  One iterative walk over the graph.  Visited nodes are held in ``seen`` (node
+    wrappers are created on access: an id is unique only while its object lives)."""
+    counts, seen, stack = {}, {}, [root.grad_fn] if root.grad_fn is not None else []
+    while stack:
+        fn = stack.pop()
+        for nxt, _ in fn.next_functions:
+            if nxt is None:
+                continue
+            if type(nxt).__name__ == 'AccumulateGrad':
+                k = id(nxt)
+                c = counts.get(k)
+                counts[k] = (nxt, 1) if c is None else (nxt, c[1] + 1)
+            elif id(nxt) not in seen:
+                seen[id(nxt)] = nxt
+                stack.append(nxt)
+    return [node.variable for node, c in counts.values() if c == 1]
 
 
 class _Deferred:
@@ -822,9 +845,13 @@ class _Deferred:
         return out[:N * K].view(N, K), (out[N * K:] if has_b else None)
 
 
-def defer_begin(device) -> None:
-    """Start queueing fp32 weight gradients (see :class:`_Deferred`)."""
+def defer_begin(device, loss=None) -> None:
+    """Start queueing fp32 weight gradients (see :class:`_Deferred`).  ``loss``: the root of the backward about to
+    run; only parameters with one consumer in its graph may be deferred (without it nothing is)."""
     if DEFER_WGRAD and torch.device(device).type == 'cuda' and not torch.cuda.is_current_stream_capturing():
+        if loss is not None:
+            for p in single_consumer_params(loss):
+                p._as_one_consumer = _FWD_EPOCH[0]
         _Deferred.on = True
         _Deferred.q = []
         _Deferred.flushed = None
@@ -1154,11 +1181,15 @@ class SkipLink:
     19x20x128 level, four levels per fp32 step).  The link rides on the map tensor object itself
     (``x._skip_link``, set when the ResBlock is called on it), so it can never be picked up by another tensor.
     Autograd runs the location head's backward (which consumes the heads' outputs) before any encoder
-    ResBlock's (the encoder feeds the heads), so the hand-off is ordered; an unfilled link is a no-op."""
-    __slots__ = ('g',)
+    ResBlock's (the encoder feeds the heads), so the hand-off is normally ordered.  The order is not relied on:
+    the ResBlock's backward marks the link ``consumed``, and a ``_TakeRows`` backward that finds it consumed
+    returns its full-height gradient through autograd instead (an ordinary add; the map's producer then sees an
+    unmasked gradient and applies its own ReLU mask), so a late hand-over is never dropped."""
+    __slots__ = ('g', 'consumed')
 
     def __init__(self):
         self.g = None
+        self.consumed = False
 
 
 SKIP_LINK = os.environ.get('APPLESTAR_SKIP_LINK', '1') == '1'    # A/B switch
@@ -1211,6 +1242,7 @@ class _ResBlock(torch.autograd.Function):
         g = None
         if ctx.link is not None:
             g, ctx.link.g = ctx.link.g, None
+            ctx.link.consumed = True          # a later _TakeRows backward takes the autograd path (SkipLink)
         C = x.shape[-1]
         if x.dtype == torch.float32 and (g is not None or ctx.mask_in) and _C.conv3x3_f32_epi2_supported(C, C):
             # + skip gradient + the location head's hand-over (first rows), masked by this input's own ReLU

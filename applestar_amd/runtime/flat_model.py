@@ -12,17 +12,22 @@ every 4 iterations (``distar/ctools/worker/learner/learner_comm.py:53-99``); act
   a side stream.  The host buffer is either private (the cross-host path pushes it as a single tensor over the
   data plane) or a :class:`SharedModelSlot` in ``/dev/shm`` that co-located inference servers read directly;
 * :class:`SharedModelSlot` - POSIX shared memory: a 64-byte header (seqlock ``version``: odd while a copy is in
-  flight; ``model_last_iter``; ``reset_flag``) followed by the flat fp32 payload, registered with the HIP runtime
+  flight; ``model_last_iter``; ``reset_flag``; payload size; the publisher's random ``session`` id; a hash of the
+  layout's names and shapes) followed by the flat fp32 payload, registered with the HIP runtime
   (``hipHostRegister``) in every process that maps it, so both the learner's D2H and the reader's H2D are DMAs;
 * :class:`ModelSubscriber` (inference server) - ``poll``: when the version moved, ONE H2D DMA of the flat payload
   into a device buffer, a version re-check (a torn read is dropped and retried next poll), then ONE native
   multi-tensor D2D copy into the resident model's parameters (captured HIP graphs stay valid: the parameters are
-  updated in place).
+  updated in place).  A subscriber is bound to ONE publisher session: ``poll`` reports the slot ``stale`` when the
+  file was replaced (another inode at the path: a restarted learner, ``reset_comm_setting``), when a new publisher
+  re-created it in place (another session id) or when the layout hash no longer matches; the caller then re-attaches
+  or falls back to the network broadcast (actor/comm.py).
 
 A ~116 MB policy moves as one DMA each way instead of ~430 per-tensor copies, a clone and a pickle/TCP frame.
 """
 from __future__ import annotations
 
+import hashlib
 import mmap
 import os
 import struct
@@ -32,7 +37,7 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 _HEADER = 64
-_HDR = struct.Struct('<qqqq')        # version, model_last_iter, reset_flag, payload elements
+_HDR = struct.Struct('<qqqqQQ')      # version, model_last_iter, reset_flag, payload elements, session, layout hash
 
 
 class FlatLayout:
@@ -64,6 +69,15 @@ class FlatLayout:
     def signature(self) -> Tuple:
         return tuple(zip(self.names, self.shapes))
 
+    def digest(self) -> int:
+        """64-bit hash of the (name, shape) order: two layouts with equal element counts but different tensors
+        never match."""
+        h = hashlib.blake2b(digest_size=8)
+        for k, s in zip(self.names, self.shapes):
+            h.update(k.encode())
+            h.update(struct.pack(f'<{len(s) + 1}q', len(s), *s))
+        return int.from_bytes(h.digest(), 'little')
+
 
 def _copy_many(dsts: List[torch.Tensor], srcs: List[torch.Tensor]) -> None:
     """One native multi-tensor launch on GPU tensors (torch foreach copy elsewhere).  Pairs whose strides differ
@@ -80,7 +94,7 @@ def _copy_many(dsts: List[torch.Tensor], srcs: List[torch.Tensor]) -> None:
 class SharedModelSlot:
     """``/dev/shm/<name>``: 64-B header + ``numel`` fp32 payload; pinned (hipHostRegister) in this process."""
 
-    def __init__(self, name: str, numel: int, create: bool = False):
+    def __init__(self, name: str, numel: int, create: bool = False, layout_hash: int = 0):
         self.path = os.path.join('/dev/shm', name)
         nbytes = _HEADER + 4 * int(numel)
         if create:
@@ -94,13 +108,18 @@ class SharedModelSlot:
                 os.close(fd)
                 raise ValueError(f'{self.path} holds fewer than {numel} elements')
         self._mm = mmap.mmap(fd, nbytes)
+        self.inode = os.fstat(fd).st_ino
         os.close(fd)
         self.numel = int(numel)
+        self.session = int.from_bytes(os.urandom(8), 'little') if create else 0
+        self.layout_hash = int(layout_hash)
         buf = torch.frombuffer(self._mm, dtype=torch.uint8)
         self.header = buf[:_HEADER]
         self.payload = buf[_HEADER:].view(torch.float32)
         if create:
             self._write_header(0, 0, 0)
+        else:
+            self.session, self.layout_hash = self.read_header()[4:6]
         self._registered = False
         if torch.cuda.is_available():
             rc = int(torch.cuda.cudart().cudaHostRegister(buf.data_ptr(), nbytes, 0))
@@ -108,10 +127,18 @@ class SharedModelSlot:
         self._base = buf
 
     def _write_header(self, version: int, last_iter: int, reset: int) -> None:
-        self._mm[0:_HDR.size] = _HDR.pack(int(version), int(last_iter), int(reset), self.numel)
+        self._mm[0:_HDR.size] = _HDR.pack(int(version), int(last_iter), int(reset), self.numel, self.session,
+                                          self.layout_hash)
 
-    def read_header(self) -> Tuple[int, int, int, int]:
+    def read_header(self) -> Tuple[int, int, int, int, int, int]:
         return _HDR.unpack(self._mm[0:_HDR.size])
+
+    def replaced(self) -> bool:
+        """True when the path no longer names the mapped file (unlinked, or re-created as another inode)."""
+        try:
+            return os.stat(self.path).st_ino != self.inode
+        except FileNotFoundError:
+            return True
 
     def begin_write(self) -> int:
         v = self.read_header()[0]
@@ -145,7 +172,8 @@ class ModelPublisher:
         dev = next(iter(state_dict.values())).device
         self.device = dev
         self.flat_dev = torch.empty(self.layout.numel, dtype=torch.float32, device=dev)
-        self.slot = SharedModelSlot(shm_name, self.layout.numel, create=True) if shm_name else None
+        self.slot = SharedModelSlot(shm_name, self.layout.numel, create=True,
+                                    layout_hash=self.layout.digest()) if shm_name else None
         if self.slot is not None:
             self.flat_host = self.slot.payload
         else:
@@ -219,6 +247,7 @@ class ModelSubscriber:
         self.flat_dev = torch.empty(self.slot.numel, dtype=torch.float32, device=self.device)
         self._dsts: List[torch.Tensor] = []
         self._srcs: List[torch.Tensor] = []
+        self.stale = False
 
     @staticmethod
     def _numel_of(shm_name: str) -> int:
@@ -227,8 +256,9 @@ class ModelSubscriber:
 
     def bind(self, layout: FlatLayout) -> None:
         """The publisher's layout (e.g. built from the same model class's policy state dict); only tensors
-        present in the resident model with equal shapes are updated."""
-        if layout.numel != self.slot.numel:
+        present in the resident model with equal shapes are updated.  The slot must carry the same layout
+        (element count AND the hash of every name and shape)."""
+        if layout.numel != self.slot.numel or layout.digest() != self.slot.layout_hash:
             raise ValueError('ModelSubscriber: layout does not match the shared slot')
         self.layout = layout
         views = layout.views(self.flat_dev)
@@ -241,9 +271,12 @@ class ModelSubscriber:
 
     def poll(self) -> bool:
         """Load the newest version if one was published since the last poll; True when the model changed."""
-        if self.layout is None:
+        if self.layout is None or self.stale:
             return False
-        v, it, reset, _ = self.slot.read_header()
+        v, it, reset, _, session, lhash = self.slot.read_header()
+        if session != self.slot.session or lhash != self.slot.layout_hash or self.slot.replaced():
+            self.stale = True                 # another publisher owns the path now: re-attach (actor/comm.py)
+            return False
         if v % 2 or v == self.version:
             return False
         self.flat_dev.copy_(self.slot.payload, non_blocking=True)

@@ -143,7 +143,7 @@ class TrainEngine:
         from ..ops import native
         defer = self.device.type == 'cuda' and self.master is None     # fp32: heads' dW beside the LSTM backward
         if defer:
-            native.defer_begin(self.device)
+            native.defer_begin(self.device, loss)
         try:
             if self.master is not None:
                 self.master.backward(loss)

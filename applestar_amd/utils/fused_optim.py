@@ -164,6 +164,9 @@ class FusedClipAdam:
         """Host side of the next step: step counts, bias corrections (uploaded when ``device_hparams``)."""
         self._ensure_table()
         self._host_hp = self.hparams()
+        # the fused kernel replaces torch.optim's step: record the call where LRScheduler.step() looks for it (its
+        # "lr_scheduler.step() before optimizer.step()" warning otherwise fires on every run)
+        self.opt._opt_called = True
         if self.clip is not None:
             self.clip.step += 1
         if self.device_hparams:

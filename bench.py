@@ -56,9 +56,9 @@ def _fp32_products():
             'fp32-accurate bf16x6 split MFMA (exact 3-way bf16 split, 6 partial products, fp32 accumulation)')
 
 
-def _make_trainer(args, precision, device):
+def _make_trainer(args, precision, device, mode=None):
     amp = 'bfloat16' if precision == 'bf16' else None
-    if args.mode == 'rl':
+    if (mode or args.mode) == 'rl':
         from applestar_amd.rl.trainer import RLTrainer
         return RLTrainer({'learner': {'use_value_feature': True, 'graph_step': args.graph, 'amp_dtype': amp},
                           'model': {'enable_baselines': ['winloss']}}, device=device)
@@ -68,14 +68,14 @@ def _make_trainer(args, precision, device):
                      device=device)
 
 
-def run_learner(args, precision, rank, world, device, host_batches):
+def run_learner(args, precision, rank, world, device, host_batches, mode=None):
     """W untimed warm-up steps, then exactly K timed steps between barrier + synchronize pairs."""
     from applestar_amd.parallel import dist as pdist
     from applestar_amd.runtime.prefetch import DevicePrefetcher
     gpu = device.type == 'cuda'
     torch.manual_seed(1234 + rank)
     t_build = time.perf_counter()
-    trainer = _make_trainer(args, precision, device)
+    trainer = _make_trainer(args, precision, device, mode)
     if rank == 0:
         _log(f'[{precision}] trainer built in {time.perf_counter() - t_build:.1f} s')
 
@@ -213,6 +213,9 @@ def main():
                     help='rl: the headline RL learner step; sl: supervised learner step (reference 384 samples/s/GPU)')
     ap.add_argument('--graph', action='store_true', help='replay the learner step from HIP graphs (runtime/step_graph.py)')
     ap.add_argument('--inference', type=int, default=1, help='1: also time the actor agent step at B=1 and B=16')
+    ap.add_argument('--sl', type=int, default=1,
+                    help='1 (rl mode): also time the fp32 SL learner step on the same config -> "sl_fp32" '
+                         '(reference 384 samples/s/GPU)')
     ap.add_argument('--conv-benchmark', type=int, default=-1,
                     help='1/0: force MIOpen find-mode autotuning of convolutions on/off (-1: trainer default)')
     args = ap.parse_args()
@@ -239,6 +242,14 @@ def main():
 
     precisions = ['fp32', 'bf16'] if args.precision == 'both' else [args.precision]
     results = {p: run_learner(args, p, rank, world, device, host_batches) for p in precisions}
+    if args.sl and args.mode == 'rl':
+        # the supervised learner step (distar/agent/default/sl_learner.py) on the same per-GPU batch, fp32 like the
+        # reference's, reported beside the headline so the 384 samples/s/GPU comparison is observed by the driver
+        sl_batches = [pin_tree(sl_batch(args.batch, args.unroll, max_entities=args.max_entities, seed=1000 * rank + i))
+                      if gpu else sl_batch(args.batch, args.unroll, max_entities=args.max_entities, seed=1000 * rank + i)
+                      for i in range(args.n_batches)]
+        results['sl_fp32'] = run_learner(args, 'fp32', rank, world, device, sl_batches, mode='sl')
+        del sl_batches
     inference = None
     if args.inference and gpu and rank == 0 and args.mode == 'rl':
         try:
@@ -251,7 +262,7 @@ def main():
         samples_per_step = args.batch * args.unroll * world
         base = (BASELINE_PER_GPU if args.mode == 'rl' else SL_BASELINE_PER_GPU) * world
 
-        def summary(p):
+        def summary(p, base=base):
             r = results[p]
             v = samples_per_step * args.steps / r['elapsed_s']
             return v, {'value': round(v, 2), 'ms_per_step': round(r['ms_per_step'], 3),
@@ -298,6 +309,10 @@ def main():
         }
         if len(precisions) > 1:
             out['mixed_bf16'] = summary('bf16')[1]
+        if 'sl_fp32' in results:
+            out['sl_fp32'] = {'metric': 'SL learner samples/sec (AlphaStar policy, fp32)',
+                              **summary('sl_fp32', base=SL_BASELINE_PER_GPU * world)[1],
+                              'baseline_note': 'vs_baseline = per-GPU samples/s / 384 (reference SL learner, fp32, A100)'}
         if inference is not None:
             out['inference_p50_ms'] = inference
             out['inference_note'] = ('actor agent step (compute_logp_action incl. sampling), bf16, HIP-graph replay; '

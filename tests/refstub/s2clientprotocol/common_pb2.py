@@ -13,3 +13,7 @@ class _Any:
     def Name(self, *a): return ''
 def __getattr__(name):
     return _Any()
+
+
+# real enum values of common.proto
+NoRace, Terran, Zerg, Protoss, Random = 0, 1, 2, 3, 4      # Race

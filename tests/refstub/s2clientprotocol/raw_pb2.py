@@ -13,3 +13,9 @@ class _Any:
     def Name(self, *a): return ''
 def __getattr__(name):
     return _Any()
+
+
+# real enum values of raw.proto
+Self, Ally, Neutral, Enemy = 1, 2, 3, 4                    # Alliance
+Visible, Snapshot, Hidden = 1, 2, 3                        # DisplayType
+CloakedUnknown, Cloaked, CloakedDetected, NotCloaked, CloakedAllied = 0, 1, 2, 3, 4   # CloakState

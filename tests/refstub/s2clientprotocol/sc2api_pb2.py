@@ -13,3 +13,9 @@ class _Any:
     def Name(self, *a): return ''
 def __getattr__(name):
     return _Any()
+
+
+# real enum values of sc2api.proto (the reference's featurizer / agent compare against these)
+Participant, Computer, Observer = 1, 2, 3                  # PlayerType
+Victory, Defeat, Tie, Undecided = 1, 2, 3, 4               # Result
+Terran, Zerg, Protoss, Random = 1, 2, 3, 4                 # Race (common.proto, re-exported)

@@ -106,3 +106,34 @@ def test_fake_env_contract():
     env = FakeSC2Env({'env': {'player_ids': ['agent1', 'bot7'], 'game_steps_per_episode': 100}})
     obs, _, _ = env.reset()
     assert set(obs) == {0} and obs[0]['opponent_obs'] is not None
+
+
+def test_fake_env_learnable_mode_rewards_the_action_set(tmp_path):
+    """Learnable FakeSC2Env: the result depends on the share of rewarded action types; each
+    finished episode is logged to fake_stats_path."""
+    import json
+    from applestar_amd.envs.fake_env import REWARDED_ACTION_TYPES
+    from applestar_amd.lib.game_data import ACTIONS
+    plain = [a for a in range(1, len(ACTIONS)) if not ACTIONS[a]['target_unit'] and not ACTIONS[a]['target_location']]
+    good = next(a for a in plain if a in REWARDED_ACTION_TYPES)
+    bad = next(a for a in plain if a not in REWARDED_ACTION_TYPES)
+    stats = tmp_path / 'stats.jsonl'
+    wins = {}
+    for name, at in (('good', good), ('bad', bad)):
+        env = FakeSC2Env({'env': {'player_ids': ['agent1', 'bot7'], 'fake_learnable': True,
+                                  'fake_episode_agent_steps': 8, 'random_seed': 0, 'fake_stats_path': str(stats)}})
+        n = 0
+        for ep in range(40):
+            env.reset()
+            done, steps = False, 0
+            while not done:
+                _, reward, done = env.step({0: [{'func_id': ACTIONS[at]['func_id'], 'skip_steps': 4,
+                                                 'unit_tags': [], 'queued': 0}]})
+                steps += 1
+            assert steps == 8
+            n += reward[0] > 0
+        wins[name] = n / 40
+    # rate 1 vs the bot's ~0.25: p(win) = 1; rate 0: p(win) = 0.25
+    assert wins['good'] == 1.0 and wins['bad'] < 0.5, wins
+    lines = [json.loads(x) for x in stats.read_text().splitlines()]
+    assert len(lines) == 80 and lines[0]['rate'] == [1.0] and lines[-1]['rate'] == [0.0]

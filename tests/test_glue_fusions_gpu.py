@@ -80,6 +80,45 @@ def test_skip_link_resblock_chain_matches_fp64(link, monkeypatch):
             assert e < 5e-5 * max(1.0, pr.grad.abs().max().item()), (name, e)
 
 
+def test_skip_link_late_takerows_backward_matches_fp64():
+    """the hand-over must not depend on autograd's order.  The trunk's backward runs FIRST (every
+    ResBlock consumes an empty link), the row views' backward second: their gradients take the autograd path and
+    every gradient still equals float64."""
+    from applestar_amd.ops import native as N
+    from applestar_amd.models.blocks import ResBlock
+    from applestar_amd.models.model import _take_rows
+    N.ensure_loaded()
+    torch.manual_seed(4)
+    C, H, W, B, n = 128, 19, 20, 6, 4
+    blocks = [ResBlock(C) for _ in range(2)]
+    refs = [copy.deepcopy(b).double() for b in blocks]
+    blocks = [b.to(DEV).to(memory_format=torch.channels_last) for b in blocks]
+    x0 = torch.randn(B, C, H, W, device=DEV).contiguous(memory_format=torch.channels_last).requires_grad_()
+    x0r = x0.detach().double().cpu().requires_grad_()
+    ws = [torch.randn(n, C, H, W, dtype=torch.float64) for _ in range(2)]
+    wo = torch.randn(B, C, H, W, dtype=torch.float64)
+
+    def run(xin, mods, on_gpu):
+        x, maps = xin, []
+        for m in mods:
+            maps.append(x)
+            x = m(x)
+        trunk = (x * (wo.float().to(DEV) if on_gpu else wo)).sum()
+        rows = sum(((_take_rows(mp, n) if on_gpu else mp[:n]) * (wt.float().to(DEV) if on_gpu else wt)).sum()
+                   for mp, wt in zip(maps, ws))
+        return trunk, rows
+    t, r = run(x0, blocks, True)
+    t.backward(retain_graph=True)          # every ResBlock backward runs before any _TakeRows backward
+    r.backward()
+    t, r = run(x0r, refs, False)
+    (t + r).backward()
+    assert _err(x0.grad.cpu(), x0r.grad) < 5e-5 * max(1.0, x0r.grad.abs().max().item())
+    for b, rf in zip(blocks, refs):
+        for (name, p), (_, pr) in zip(b.named_parameters(), rf.named_parameters()):
+            e = _err(p.grad.cpu(), pr.grad)
+            assert e < 5e-5 * max(1.0, pr.grad.abs().max().item()), (name, e)
+
+
 def test_deferred_head_wgrads_equal_inline(monkeypatch):
     """Deferred weight gradients (ops/native.py _Deferred: the heads' fp32 dW products queued during the heads'
     backward and issued beside the core LSTM's backward on a side stream) give every parameter the same

@@ -174,11 +174,13 @@ def test_full_model_bf16_gpu_vs_cpu_fp32(reference):
     # torch's own autocast 2.1-5.6 %, native 1.8-4.9 %, means 3.4 / 3.1 %), so they are judged on the mean over
     # four batches against the torch control's mean instead of one seed's value
     # Over round 5's boxes the four-batch mean was 0.028-0.039 for the torch control and 0.0297-0.0343 for the native
-    # path (it moves box to box with the conv routing and library tile choice).  The bound clears both ranges and
-    # still fails a real regression: rounding the core output to bf16 in front of a GLU gave 0.0407 (r7a).
+    # path.  The check is an absolute ceiling that sits above the native path's measured range and below the one real
+    # regression seen (rounding the core output to bf16 in front of a GLU: 0.0407, r7a) - it does not widen with the
+    # control - plus a relative bound against the control's noise level.
     su = _su_logit_spread(cpu, [3, 0, 1, 2])
     print('selected-units logit error, mean of four batches:', su)
-    assert su['native'] <= max(3.75e-2, 1.25 * su['torch']), su
+    assert su['native'] <= 0.036, su
+    assert su['native'] <= 1.25 * su['torch'], su
     assert _rel(out['value']['winloss'].float(), ref_out['value']['winloss']) < 3e-2
     a, r = float(info['total_loss']), float(ref_info['total_loss'])
     assert abs(a - r) <= 2e-2 * max(1.0, abs(r)), (a, r)

@@ -241,3 +241,37 @@ def test_stopwatch_and_alphastar_table():
     r.update_var({'winloss/action_type': 0.5, 'total_loss': 2.0, 'kl/total': 0.1})
     txt = r.get_vars_text()
     assert 'winloss' in txt and '0.5' in txt and 'total_loss' in txt
+
+
+def test_take_rows_consumed_skip_link_returns_full_gradient():
+    """SkipLink hand-over (ops/native.py): an unconsumed link takes the gradient (no autograd gradient here); a
+    link whose ResBlock backward already ran returns the ordinary full-height gradient instead of dropping it."""
+    import torch
+    from applestar_amd.models.model import _TakeRows
+    from applestar_amd.ops.native import SkipLink
+    for consumed in (False, True):
+        x = torch.randn(5, 3, 2, 2, requires_grad=True)
+        link = SkipLink()
+        link.consumed = consumed
+        _TakeRows.apply(x, 2, link).sum().backward()
+        if consumed:
+            assert link.g is None and torch.equal(x.grad[:2], torch.ones(2, 3, 2, 2)) and not x.grad[2:].any()
+        else:
+            assert x.grad is None and link.g.shape == (2, 2, 2, 3)
+
+
+def test_single_consumer_params_counts_every_autograd_use():
+    """Deferred fp32 weight gradients (ops/native.py _Deferred) are allowed only for parameters with ONE consumer in
+    the step's autograd graph: a weight also reached through an uncounted path (F.linear, a view) is excluded."""
+    import torch
+    from applestar_amd.ops.native import single_consumer_params
+    a = torch.nn.Parameter(torch.randn(4, 4))
+    b = torch.nn.Parameter(torch.randn(4, 4))
+    c = torch.nn.Parameter(torch.randn(4))
+    x = torch.randn(3, 4)
+    y = torch.nn.functional.linear(torch.relu(x @ a.t()), b, c)
+    loss = y.sum() + (x @ b.t()).sum()          # b: a second consumer through another op
+    ids = {id(p) for p in single_consumer_params(loss)}
+    assert id(a) in ids and id(c) in ids and id(b) not in ids
+    y2 = (x @ a.t()).sum() + a.t().sum()         # a view of a: two edges into its AccumulateGrad
+    assert id(a) not in {id(p) for p in single_consumer_params(y2)}

@@ -14,6 +14,8 @@ Sources:
   distar/pysc2/lib/units.py, upgrades.py          unit / upgrade enum names (ids -> names for logs)
   distar/envs/map_info.py:8-258                   MAPS (bnet name, path, cropped / full size)
   distar/pysc2/run_configs/lib.py:36-…            SC2 VERSIONS (game version -> build, data hash)
+  distar/pysc2/lib/actions.py:1183-1757           _RAW_FUNCTIONS (func id, name, command type, ability id,
+                                                  general ability id): replay decoding (reverse_raw_action)
 """
 import ast
 import json
@@ -53,6 +55,29 @@ def _enum_classes(path):
     return out
 
 
+def _raw_functions(path):
+    """[[func_id, name, function_type, ability_id, general_id], ...] of the ``_RAW_FUNCTIONS`` list, in list order."""
+    tree = ast.parse(open(path).read())
+    for node in tree.body:
+        if isinstance(node, ast.Assign) and getattr(node.targets[0], 'id', None) == '_RAW_FUNCTIONS':
+            out = []
+            for call in node.value.elts:
+                kind = call.func.attr
+                args = call.args
+                fid, name, ftype = ast.literal_eval(args[0]), ast.literal_eval(args[1]), args[2].id
+                if kind == 'raw_ability':
+                    ab = ast.literal_eval(args[3])
+                    gen = ast.literal_eval(args[4]) if len(args) > 4 else 0
+                    for kw in call.keywords:
+                        if kw.arg == 'general_id':
+                            gen = ast.literal_eval(kw.value)
+                else:                                       # raw_ui_func: no ability
+                    ab, gen = 0, 0
+                out.append([fid, name, ftype, ab, gen])
+            return out
+    raise ValueError('_RAW_FUNCTIONS not found')
+
+
 def _versions(path):
     tree = ast.parse(open(path).read())
     out = []
@@ -87,6 +112,7 @@ def main():
         'unit_enums': _enum_classes(os.path.join(REF, 'distar/pysc2/lib/units.py')),
         'upgrade_enums': _enum_classes(os.path.join(REF, 'distar/pysc2/lib/upgrades.py'))['Upgrades'],
         'sc2_versions': _versions(os.path.join(REF, 'distar/pysc2/run_configs/lib.py')),
+        'raw_functions': _raw_functions(os.path.join(REF, 'distar/pysc2/lib/actions.py')),
         'maps': {k: list(v) for k, v in _literal(_assignments(os.path.join(REF, 'distar/envs/map_info.py'))['MAPS']).items()},
     }
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
