@@ -280,7 +280,29 @@ class Model(nn.Module):
         return cache[name]
 
     def _encode(self, spatial_info, entity_info, scalar_info, entity_num, entity_total=None, entity_pad=None):
-        return self.encoder(spatial_info, entity_info, scalar_info, entity_num, entity_total, entity_pad)
+        out = self.encoder(spatial_info, entity_info, scalar_info, entity_num, entity_total, entity_pad)
+        if getattr(self, 'phase_cut', False) and torch.is_grad_enabled() and \
+                not (out[0].is_cuda and torch.cuda.is_current_stream_capturing()):
+            # the two-phase backward (parallel/dp.py backward_phased): everything downstream of the encoders (core
+            # LSTM, heads, critics) reads detached leaf copies of the encoders' outputs, so backward phase 1 stops at
+            # them; phase 2 runs the encoders' backward from the (encoder output, leaf gradient) pairs in ONE
+            # autograd call (the outputs are not independent: each skip map feeds the next, the entity embeddings feed
+            # the spatial scatter).  A skip map's SkipLink rides along on its leaf.
+            pairs = []
+
+            def cut(t):
+                if not torch.is_tensor(t) or not t.requires_grad:
+                    return t
+                leaf = t.detach().requires_grad_()
+                if getattr(t, '_skip_link', None) is not None:
+                    leaf._skip_link = t._skip_link
+                pairs.append((t, leaf))
+                return leaf
+            lstm_input, scalar_context, baseline_feature, entity_embeddings, map_skip = out
+            out = (cut(lstm_input), cut(scalar_context), cut(baseline_feature), cut(entity_embeddings),
+                   [cut(m) for m in map_skip])
+            self.encoder_boundary = pairs
+        return out
 
     def _core(self, lstm_input_seq, hidden_state):
         state = [(h.float(), c.float()) for h, c in hidden_state]

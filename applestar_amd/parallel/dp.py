@@ -15,6 +15,16 @@ small - 132 MB of fp32 gradients on an 8-GPU ring moves 2 x 7/8 x 132 MB per lin
 the 150-300 GB/s an xGMI ring sustains, against a 30-90 ms step.  Buckets default to 32 MB so the copy of
 one bucket and the reduction of the previous one pipeline inside RCCL; the whole reduction is two to five
 calls.
+
+Two-phase backward (``backward_phased``, multi-rank by default): the step's autograd graph is cut at the encoders'
+outputs - downstream modules read detached leaf copies of them (``Model._encode``, ``encoder_boundary`` holds the
+(output, leaf) pairs).  Phase 1 differentiates the loss w.r.t. everything downstream of the cut (core LSTM, heads,
+critics: ~12 M of the ~31 M parameters) AND the leaves; those parameters' gradients are then final, so their
+buckets are copied and their all-reduce is issued right away, and runs on RCCL's stream while phase 2 (the
+encoders' backward from every (output, leaf gradient) pair, one autograd call) computes.  No per-parameter hooks: two
+``autograd.grad`` calls and one multi-tensor copy per phase.  The buckets are built per phase (phase-1 parameters
+first), so no bucket mixes the two.  ``comm_dtype=torch.bfloat16`` sends bf16 on the wire (half the bytes;
+averaged by RCCL, converted back into the fp32 buckets).
 """
 from __future__ import annotations
 
@@ -68,7 +78,8 @@ class _Bucket:
 
 class GradientReducer:
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 32.0,
-                 comm_dtype: Optional[torch.dtype] = None, group=None, overlap: bool = True):
+                 comm_dtype: Optional[torch.dtype] = None, group=None, overlap: bool = True,
+                 phase_of=None):
         self.group = group
         self.world = pdist.get_world_size()
         self.overlap = overlap
@@ -78,26 +89,33 @@ class GradientReducer:
         self.params = params
         self.buckets: List[_Bucket] = []
         self._owner = {}
+        # phase_of(p) -> 0 (downstream of the encoders: final after backward phase 1) or 1 (the encoders); every
+        # parameter in phase 0 without one
+        ph = [int(phase_of(p)) if phase_of is not None else 0 for p in params]
+        self.phase_params = [[p for p, k in zip(params, ph) if k == i] for i in (0, 1)]
+        self.phase_buckets: List[List[_Bucket]] = [[], []]
         # backward visits layers roughly in reverse registration order; parameters of different dtypes
         # (bf16 GEMM weights + fp32 norm affines under master weights) go to separate bucket chains so
         # the interleaving does not fragment the buckets
         limit = int(bucket_mb * 1024 * 1024)
-        keys = []
-        for p in reversed(params):
-            if (p.dtype, p.device) not in keys:
-                keys.append((p.dtype, p.device))
-        for key in keys:
-            cur, cur_bytes = [], 0
-            for p in reversed(params):
-                if (p.dtype, p.device) != key:
-                    continue
-                if cur and cur_bytes + p.numel() * p.element_size() > limit:
-                    self._add_bucket(cur)
-                    cur, cur_bytes = [], 0
-                cur.append(p)
-                cur_bytes += p.numel() * p.element_size()
-            if cur:
-                self._add_bucket(cur)
+        for phase in (0, 1):
+            keys = []
+            members = [p for p, k in zip(params, ph) if k == phase]
+            for p in reversed(members):
+                if (p.dtype, p.device) not in keys:
+                    keys.append((p.dtype, p.device))
+            for key in keys:
+                cur, cur_bytes = [], 0
+                for p in reversed(members):
+                    if (p.dtype, p.device) != key:
+                        continue
+                    if cur and cur_bytes + p.numel() * p.element_size() > limit:
+                        self.phase_buckets[phase].append(self._add_bucket(cur))
+                        cur, cur_bytes = [], 0
+                    cur.append(p)
+                    cur_bytes += p.numel() * p.element_size()
+                if cur:
+                    self.phase_buckets[phase].append(self._add_bucket(cur))
         self._hooks = []
         self.use_avg = self.world > 1 and dist.get_backend(group) == 'nccl'
 
@@ -112,6 +130,7 @@ class GradientReducer:
             self._owner[p] = b
             off += n
         self.buckets.append(b)
+        return b
 
     @property
     def num_buckets(self) -> int:
@@ -137,18 +156,42 @@ class GradientReducer:
         grads = torch.autograd.grad(loss, self.params, allow_unused=True)
         if before_copy is not None:
             before_copy()
+        self._store(self.params, grads, self.buckets)
+
+    def _store(self, params, grads, buckets):
         dst, src = [], []
         stale = set()
-        for p, g in zip(self.params, grads):
+        for p, g in zip(params, grads):
             if g is not None:
                 dst.append(p.grad)
                 src.append(g)
             else:
                 stale.add(id(self._owner[p]))
-        for b in self.buckets:
+        for b in buckets:
             if id(b) in stale:
                 b.flat.zero_()
         copy_into(dst, src)
+
+    def backward_phased(self, loss: torch.Tensor, boundary, before_copy=None):
+        """Two-phase backward (module docstring): phase 1 = the loss w.r.t. the phase-0 parameters and the
+        boundary leaves; their buckets are filled and (multi-rank) their all-reduce issued; phase 2 = the encoder
+        outputs, with the leaves' gradients, w.r.t. the phase-1 parameters.  ``boundary``: the (encoder output,
+        leaf) pairs of ``Model.encoder_boundary``.  ``before_copy`` runs before the first copy."""
+        p0, p1 = self.phase_params
+        outs, leaves = [o for o, _ in boundary], [lf for _, lf in boundary]
+        g = torch.autograd.grad(loss, p0 + leaves, allow_unused=True)
+        if before_copy is not None:
+            before_copy()
+        self._store(p0, g[:len(p0)], self.phase_buckets[0])
+        for b in self.phase_buckets[0]:
+            self._launch(b)               # RCCL's stream, beside the encoders' backward below
+        roots = [(t, gt) for t, gt in zip(outs, g[len(p0):]) if gt is not None]
+        if roots and p1:
+            g2 = torch.autograd.grad([t for t, _ in roots], p1, grad_outputs=[gt for _, gt in roots],
+                                     allow_unused=True)
+        else:
+            g2 = [None] * len(p1)
+        self._store(p1, g2, self.phase_buckets[1])
 
     def zero_grad(self, buffers: bool = True):
         """Reset the per-step state; ``buffers=False`` leaves the bucket memory alone (``backward`` overwrites

@@ -35,7 +35,7 @@ def lowp_parameter_names(model: nn.Module) -> List[str]:
 
 
 class MasterWeights:
-    def __init__(self, model: nn.Module, bucket_mb: float = 32.0, comm_dtype=None):
+    def __init__(self, model: nn.Module, bucket_mb: float = 32.0, comm_dtype=None, phase_of=None):
         self.model = model
         params = dict(model.named_parameters())
         lowp = set(lowp_parameter_names(model))
@@ -44,8 +44,11 @@ class MasterWeights:
             p = params[n]
             p.data = p.data.to(torch.bfloat16)  # keeps strides (channels_last conv weights)
         self.params = [p for p in model.parameters() if p.requires_grad]
-        self.reducer = GradientReducer(self.params, bucket_mb=bucket_mb, comm_dtype=comm_dtype)
+        self.reducer = GradientReducer(self.params, bucket_mb=bucket_mb, comm_dtype=comm_dtype, phase_of=phase_of)
         self.reducer.keep_comm = True
+        # gradients on the wire: fp32 (default) or bf16 (half the bytes; averaged by RCCL, widened back to fp32)
+        self.comm_dtype = comm_dtype if comm_dtype == torch.bfloat16 else None
+        self._pending = []
         # fp32 master in bucket order: master slice i <-> bf16 bucket i (same per-parameter offsets)
         self.lowp_buckets = [b for b in self.reducer.buckets if b.flat.dtype == torch.bfloat16]
         n = sum(b.flat.numel() for b in self.lowp_buckets)
@@ -67,6 +70,10 @@ class MasterWeights:
                 p.data = view  # the module computes with a view of the flat bf16 storage
                 o2 += m
             off += k
+        # the master range of the phase-0 parameters (parallel/dp.py backward_phased): buckets are built phase by
+        # phase, so it is the prefix [0, n0)
+        ph0 = set(id(b) for b in self.reducer.phase_buckets[0])
+        self.master_n0 = sum(k for b, _, k in self._slices if id(b) in ph0)
         self.fp32_params = [p for b in self.reducer.buckets if b.flat.dtype != torch.bfloat16 for p in b.params]
         self.opt_params = [self.master] + self.fp32_params
         # fp32 biases / transposed GEMM weights / flipped conv weights the kernels read: rebuilt in one launch
@@ -85,7 +92,7 @@ class MasterWeights:
     def zero_grad(self):
         self.reducer.zero_grad()
 
-    def backward(self, loss: torch.Tensor):
+    def backward(self, loss: torch.Tensor, boundary=None):
         """Backward straight into the fp32 master gradient, with the same launches at every world size:
         ``autograd.grad`` (no per-parameter ``AccumulateGrad`` add into zeroed buckets) and ONE native
         multi-tensor copy that writes every bf16 gradient, converted, into its fp32 master-grad slot (and the
@@ -93,38 +100,79 @@ class MasterWeights:
         buffers (fp32 reduction of the bf16 gradients; parallel/dp.py explains why the collective is not
         overlapped with backward through per-parameter hooks)."""
         self._direct = False
+        self._pending = []
+        self._phase0_issued = False
         if not loss.is_cuda:
             self.reducer.backward(loss)
             return
-        grads = torch.autograd.grad(loss, self.reducer.params, allow_unused=True)
+        if boundary is None:
+            grads = torch.autograd.grad(loss, self.reducer.params, allow_unused=True)
+            self._store(self.reducer.params, grads, None)
+            self._direct = True
+            return
+        # two phases (parallel/dp.py backward_phased): the phase-0 master range and fp32 buckets are final after
+        # phase 1; their all-reduce is issued before the encoders' backward
+        p0, p1 = self.reducer.phase_params
+        outs, leaves = [o for o, _ in boundary], [lf for _, lf in boundary]
+        g = torch.autograd.grad(loss, p0 + leaves, allow_unused=True)
+        self._store(p0, g[:len(p0)], 0)
+        self._direct = True
+        self._issue(0)
+        self._phase0_issued = True
+        roots = [(t, gt) for t, gt in zip(outs, g[len(p0):]) if gt is not None]
+        g2 = torch.autograd.grad([t for t, _ in roots], p1, grad_outputs=[gt for _, gt in roots],
+                                 allow_unused=True) if roots and p1 else [None] * len(p1)
+        self._store(p1, g2, 1)
+
+    def _store(self, params, grads, phase):
+        """Every gradient, converted, into its fp32 master-grad slot (fp32 ones into their buckets); ``phase``:
+        which master range / fp32 buckets these parameters own (None: all)."""
         mg = self._master_grad_views()
         dst, src = [], []
-        for p, g in zip(self.reducer.params, grads):
+        for p, g in zip(params, grads):
             if g is not None:
                 dst.append(mg.get(p, p.grad))
                 src.append(g)
-        if len(dst) < len(self.reducer.params):   # unused parameters (e.g. value pre-training) get zeros
-            self.master.grad.zero_()
-            for b in self.reducer.buckets:
-                if b.flat.dtype != torch.bfloat16:
-                    b.flat.zero_()
+        if len(dst) < len(params):   # unused parameters (e.g. value pre-training) get zeros
+            lo, hi = self._range(phase)
+            self.master.grad[lo:hi].zero_()
+            for b in self._fp32_buckets(phase):
+                b.flat.zero_()
         copy_into(dst, src)
-        self._direct = True
 
-    def reduce_flat(self):
-        """All-reduce (average) the whole fp32 master gradient and the fp32 buckets: one RCCL call each,
-        issued back to back (async) and then waited for."""
+    def _range(self, phase):
+        n = self.master.grad.numel()
+        return (0, n) if phase is None else ((0, self.master_n0) if phase == 0 else (self.master_n0, n))
+
+    def _fp32_buckets(self, phase):
+        bs = self.reducer.buckets if phase is None else self.reducer.phase_buckets[phase]
+        return [b for b in bs if b.flat.dtype != torch.bfloat16]
+
+    def _issue(self, phase):
+        """Async all-reduce (AVG) of one phase's master range + fp32 buckets (None: everything)."""
         import torch.distributed as dist
         if self.reducer.world == 1:
             return
-        bufs = [self.master.grad] + [b.flat for b in self.reducer.buckets if b.flat.dtype != torch.bfloat16]
-        avg = self.reducer.use_avg
-        op = dist.ReduceOp.AVG if avg else dist.ReduceOp.SUM
-        handles = [dist.all_reduce(buf, op=op, group=self.reducer.group, async_op=True) for buf in bufs]
-        for h, buf in zip(handles, bufs):
+        lo, hi = self._range(phase)
+        bufs = ([self.master.grad[lo:hi]] if hi > lo else []) + [b.flat for b in self._fp32_buckets(phase)]
+        op = dist.ReduceOp.AVG if self.reducer.use_avg else dist.ReduceOp.SUM
+        for buf in bufs:
+            wire = buf.to(self.comm_dtype) if self.comm_dtype is not None and buf.dtype != self.comm_dtype else buf
+            self._pending.append((dist.all_reduce(wire, op=op, group=self.reducer.group, async_op=True), buf, wire))
+
+    def reduce_flat(self):
+        """All-reduce (average) the fp32 master gradient and the fp32 buckets: one RCCL call each, issued back to
+        back (async) and then waited for; after a two-phase backward only phase 1's ranges are still to issue."""
+        if self.reducer.world == 1:
+            return
+        self._issue(1 if getattr(self, '_phase0_issued', False) else None)
+        for h, buf, wire in self._pending:
             h.wait()
-            if not avg:
+            if wire is not buf:
+                buf.copy_(wire)
+            if not self.reducer.use_avg:
                 buf.div_(self.reducer.world)
+        self._pending = []
 
     def segments(self):
         """(offset, numel) of every bf16 parameter inside the flat master, in master order (per-layer pieces

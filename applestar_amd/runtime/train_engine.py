@@ -71,16 +71,21 @@ class TrainEngine:
         self.params = [p for p in self.model.parameters() if p.requires_grad]
         self.amp_dtype = lc.get('amp_dtype')
         comm = getattr(torch, lc.comm_dtype) if lc.get('comm_dtype') else None
+        # the two-phase backward (parallel/dp.py backward_phased): encoder parameters are phase 1, everything
+        # downstream of the encoders' outputs (core LSTM, heads, critics, value encoder) phase 0
+        enc = {id(p) for n, p in self.model.named_parameters() if n.startswith('encoder.')}
+        phase_of = (lambda p: 1 if id(p) in enc else 0)
+        self.model.phase_cut = self._phased()
         use_master = lc.get('master_weights', None)
         if use_master is None:
             use_master = self.device.type == 'cuda' and self.amp_dtype == 'bfloat16'
         self.master = None
         if use_master:
-            self.master = MasterWeights(self.model, bucket_mb=lc.bucket_mb, comm_dtype=comm)
+            self.master = MasterWeights(self.model, bucket_mb=lc.bucket_mb, comm_dtype=comm, phase_of=phase_of)
             self.reducer = self.master.reducer
             self.opt_params = self.master.opt_params
         else:
-            self.reducer = GradientReducer(self.params, bucket_mb=lc.bucket_mb, comm_dtype=comm)
+            self.reducer = GradientReducer(self.params, bucket_mb=lc.bucket_mb, comm_dtype=comm, phase_of=phase_of)
             self.opt_params = self.params
         # fp32 step: the weights' derived forms built once per optimizer step (MasterWeights owns its own registry)
         self.derived = None
@@ -138,17 +143,34 @@ class TrainEngine:
         return g
 
     # ------------------------------------------------------------------ backward / reduce / update
+    def _phased(self) -> bool:
+        """Two-phase backward with the downstream buckets' all-reduce issued between the phases: multi-rank
+        (``learner.overlap_backward``, default on), or forced on one rank by APPLESTAR_PHASED_BACKWARD=1 (tests).
+        Decided once (the model then cuts its forward graph at the encoders' outputs, ``Model._encode``); a
+        forward that made the cut must be followed by the phased backward, which ``backward`` ensures: it runs
+        the two phases exactly when the forward left (output, leaf) pairs."""
+        forced = os.environ.get('APPLESTAR_PHASED_BACKWARD', '')
+        if forced:
+            return forced == '1'
+        return pdist.get_world_size() > 1 and bool(self.cfg.learner.get('overlap_backward', True))
+
     def backward(self, loss: torch.Tensor):
         self.reducer.zero_grad(buffers=False)    # backward overwrites every slot (and zeroes unused ones)
         from ..ops import native
+        boundary = getattr(self.model, 'encoder_boundary', None)
+        self.model.encoder_boundary = None
+        phased = bool(boundary)
         defer = self.device.type == 'cuda' and self.master is None     # fp32: heads' dW beside the LSTM backward
         if defer:
             native.defer_begin(self.device, loss)
         try:
+            join = (lambda: native.defer_end(self.device)) if defer else None
             if self.master is not None:
-                self.master.backward(loss)
+                self.master.backward(loss, boundary if phased else None)
+            elif phased:
+                self.reducer.backward_phased(loss, boundary, before_copy=join)
             else:
-                self.reducer.backward(loss, before_copy=(lambda: native.defer_end(self.device)) if defer else None)
+                self.reducer.backward(loss, before_copy=join)
         finally:
             if defer:
                 native.defer_end(self.device)

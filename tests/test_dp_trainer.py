@@ -112,3 +112,78 @@ def test_rl_trainer_data_parallel(world, tmp_path):
     assert r0['step2'] != r0['init']
     assert res[1]['drifted'] != r0['drifted']           # the reset really had something to undo
     assert r0['reset'] == {k: v for k, v in r0['step2'].items()}
+
+
+def test_phased_backward_equals_single_phase(monkeypatch):
+    """The two-phase backward (parallel/dp.py backward_phased: loss -> downstream parameters + encoder outputs,
+    then encoder outputs -> encoder parameters) writes the same bucket gradients as one autograd.grad."""
+    from applestar_amd.rl.trainer import RLTrainer
+    from applestar_amd.rl.synthetic import rl_batch
+    torch.set_num_threads(2)
+    grads = {}
+    for mode in ('0', '1'):
+        monkeypatch.setenv('APPLESTAR_PHASED_BACKWARD', mode)
+        torch.manual_seed(0)
+        tr = RLTrainer({'learner': {'use_value_feature': True, 'bucket_mb': 4},
+                        'model': {'enable_baselines': ['winloss']}}, device='cpu')
+        assert tr.reducer.phase_params[0] and tr.reducer.phase_params[1]
+        out = tr.model.rl_learner_forward(**rl_batch(1, 2, max_entities=16, seed=3))
+        tr.backward(tr.loss.compute_loss(out)['total_loss'])
+        grads[mode] = {n: p.grad.clone() for n, p in tr.model.named_parameters() if p.requires_grad}
+    assert grads['0'].keys() == grads['1'].keys()
+    bad = [n for n in grads['0'] if not torch.allclose(grads['0'][n], grads['1'][n], rtol=1e-5, atol=1e-7)]
+    assert not bad, bad[:5]
+    assert any(n.startswith('encoder.') and grads['1'][n].abs().sum() > 0 for n in grads['1'])
+
+
+def _wire_worker(rank, world, port, comm, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)
+    from applestar_amd.parallel import dist as pdist
+    from applestar_amd.rl.trainer import RLTrainer
+    from applestar_amd.rl.synthetic import rl_batch
+    pdist.init(backend='gloo')
+    torch.manual_seed(0)
+    tr = RLTrainer({'learner': {'use_value_feature': True, 'bucket_mb': 4, 'comm_dtype': comm},
+                    'model': {'enable_baselines': ['winloss']}}, device='cpu')
+    batch = rl_batch(1, 2, max_entities=16, seed=10 + rank)
+    # this rank's own gradient, one plain autograd.grad over the uncut graph (the reference for the average)
+    params = [p for p in tr.model.parameters() if p.requires_grad]
+    assert tr.model.phase_cut
+    tr.model.phase_cut = False
+    loss = tr.loss.compute_loss(tr.model.rl_learner_forward(**rl_batch(1, 2, max_entities=16, seed=10 + rank)))
+    tr.model.phase_cut = True
+    local = torch.autograd.grad(loss['total_loss'], params, allow_unused=True)
+    local = torch.cat([(g if g is not None else torch.zeros_like(p)).reshape(-1) for g, p in zip(local, params)])
+    allg = [torch.zeros_like(local) for _ in range(world)]
+    torch.distributed.all_gather(allg, local)
+    ref = torch.stack(allg).mean(0)
+    # the trainer's phased backward (multi-rank default) + bucket all-reduce
+    out = tr.model.rl_learner_forward(**batch)
+    tr.backward(tr.loss.compute_loss(out)['total_loss'])
+    tr._reduce()
+    got = torch.cat([p.grad.reshape(-1) for p in params])
+    q.put({'rank': rank, 'err': float((got - ref).abs().max()), 'scale': float(ref.abs().max()),
+           'sum': float(got.double().sum())})
+    pdist.finalize()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize('comm', [None, 'bfloat16'])
+def test_phased_allreduce_world2_matches_average(comm):
+    """World 2 (gloo): the phased backward with its early all-reduce of the downstream buckets gives every rank
+    the average of the ranks' own gradients - exactly on the fp32 wire, within bf16 rounding on the bf16 wire -
+    and identical reduced gradients on both ranks."""
+    port = _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_wire_worker, args=(r, 2, port, comm, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=500) for _ in range(2)], key=lambda r: r['rank'])
+    for p in procs:
+        p.join(timeout=60)
+    tol = 1e-5 if comm is None else 2 ** -7
+    for r in res:
+        assert r['err'] <= tol * r['scale'], r
+    assert res[0]['sum'] == res[1]['sum']

@@ -108,6 +108,8 @@ def main():
     ap.add_argument('--workdir', default='/tmp/applestar_learn')
     ap.add_argument('--out', default=None)
     args = ap.parse_args()
+    if args.out:
+        args.out = os.path.abspath(args.out)      # before the chdir below
     os.makedirs(args.workdir, exist_ok=True)
     os.chdir(args.workdir)
     stats_path = os.path.join(args.workdir, f'episodes_{os.getpid()}.jsonl')
@@ -133,7 +135,7 @@ def main():
     srv = make_server('127.0.0.1', lport, create_league_app(league), threaded=True)
     threading.Thread(target=srv.serve_forever, daemon=True).start()
     comm = {'coordinator_ip': '127.0.0.1', 'coordinator_port': cport, 'league_ip': '127.0.0.1',
-            'league_port': lport, 'learner_send_model_freq': 2, 'learner_send_train_info_freq': 1000,
+            'league_port': lport, 'learner_send_model_freq': 10, 'learner_send_train_info_freq': 1000,
             'actor_ask_for_job_interval': 3600, 'actor_model_update_interval': 2}
     import multiprocessing as mp
     ctx = mp.get_context('spawn')
@@ -177,6 +179,8 @@ def main():
     before = [e for e in eps_all if e['t'] < t0]
     eps = [e for e in eps_all if t0 <= e['t'] <= t1]
     curve = _bins(eps, t0, args.bin)
+    if len(curve) > 2 and curve[-1]['episodes'] < 0.5 * curve[-2]['episodes']:
+        curve = curve[:-1]               # the partial bin after the window
     it_curve = [{'t_s': round(t - t0, 1), 'iter': it, **rec} for t, it, rec in iters if t >= t0]
     first = curve[0] if curve else {}
     last = curve[-1] if curve else {}
