@@ -208,6 +208,9 @@ class InferenceServer:
             except ValueError:
                 sub.close()
                 return False
+            if sub.stale:                  # left behind by a learner that exited: not this run's weights
+                sub.close()
+                return False
             self._subscribers = getattr(self, '_subscribers', {})
             old = self._subscribers.pop(player_id, None)
             if old is not None:

@@ -1004,6 +1004,40 @@ at::Tensor conv3x3_f32_psb(const at::Tensor& x, const at::Tensor& wsplit, int64_
   return out;
 }
 
+at::Tensor conv3x3_f32_v2(const at::Tensor& x, const at::Tensor& wsplit, int64_t Cout,
+                           const c10::optional<at::Tensor>& bias, const c10::optional<at::Tensor>& res,
+                           const c10::optional<at::Tensor>& res2, const c10::optional<at::Tensor>& mask, int64_t act,
+                          int64_t variant) {
+  check_cuda(x, "x");
+  check_cuda(wsplit, "wsplit");
+  TORCH_CHECK(x.scalar_type() == at::kFloat && x.dim() == 4 && x.is_contiguous(), "conv3x3_f32_psb: NHWC fp32 x");
+  const int64_t B = x.size(0), H = x.size(1), W = x.size(2), Cin = x.size(3), M = B * H * W;
+  TORCH_CHECK(as::conv3x3_f32_psb_supported(M, static_cast<int>(Cin), static_cast<int>(Cout)),
+              "conv3x3_f32_psb: Cout % 128, Cin % 16");
+  TORCH_CHECK(wsplit.scalar_type() == at::kByte && wsplit.is_contiguous() &&
+                  wsplit.numel() == as::presplit_b_bytes(static_cast<int>(Cout), static_cast<int>(9 * Cin)),
+              "conv3x3_f32_psb: wsplit must be presplit_b of the [Cout, 9 Cin] weight");
+  auto fp = [&](const c10::optional<at::Tensor>& t, int64_t rows, const char* what) -> const float* {
+    if (!t || !t->defined()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->device() == x.device() &&
+                    (rows < 0 ? t->numel() == Cout : (t->numel() % Cout == 0 && t->numel() / Cout <= rows)), what);
+    return t->data_ptr<float>();
+  };
+  const float* bp = fp(bias, -1, "conv3x3_f32_psb: bias [Cout]");
+  const float* rp = fp(res, M, "conv3x3_f32_psb: res [B, H, W, Cout]");
+  if (rp) TORCH_CHECK(res->numel() == M * Cout, "conv3x3_f32_psb: res [B, H, W, Cout]");
+  const float* r2 = fp(res2, M, "conv3x3_f32_psb: res2 [b <= B, H, W, Cout]");
+  const float* mk = fp(mask, M, "conv3x3_f32_psb: mask [B, H, W, Cout]");
+  if (mk) TORCH_CHECK(mask->numel() == M * Cout, "conv3x3_f32_psb: mask [B, H, W, Cout]");
+  c10::hip::HIPGuard g(x.device().index());
+  auto out = at::empty({B, H, W, Cout}, x.options());
+  as::conv3x3_f32_v2(x.data_ptr<float>(), wsplit.data_ptr(), bp, rp, r2, r2 ? res2->numel() / Cout : 0, mk,
+                      out.data_ptr<float>(), static_cast<int>(B), static_cast<int>(H), static_cast<int>(W),
+                      static_cast<int>(Cin), static_cast<int>(Cout), static_cast<int>(act),
+                     static_cast<int>(variant), stream());
+  return out;
+}
+
 bool conv3x3_f32_psb_supported(int64_t M, int64_t Cin, int64_t Cout) {
   return as::conv3x3_f32_psb_supported(M, static_cast<int>(Cin), static_cast<int>(Cout));
 }
@@ -2240,6 +2274,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv3x3_f32_psb", &conv3x3_f32_psb, py::arg("x"), py::arg("wsplit"), py::arg("Cout"),
         py::arg("bias") = py::none(), py::arg("res") = py::none(), py::arg("res2") = py::none(),
         py::arg("mask") = py::none(), py::arg("act") = 0);
+  m.def("conv3x3_f32_v2", &conv3x3_f32_v2, py::arg("x"), py::arg("wsplit"), py::arg("Cout"),
+        py::arg("bias") = py::none(), py::arg("res") = py::none(), py::arg("res2") = py::none(),
+        py::arg("mask") = py::none(), py::arg("act") = 0, py::arg("variant") = 0);
   m.def("gemm_f32_psb", &gemm_f32_psb, py::arg("a"), py::arg("bsplit"), py::arg("N"), py::arg("K"),
         py::arg("bias") = py::none(), py::arg("res") = py::none(), py::arg("act") = 0, py::arg("variant") = 0);
   m.def("entity_pack", &entity_pack);

@@ -369,6 +369,12 @@ bool conv3x3_f32_psb_supported(long M, int Cin, int Cout);
 void conv3x3_f32_psb(const float* x, const void* wsplit, const float* bias, const float* res, const float* res2,
                      long res2_rows, const float* mask, float* out, int B, int H, int W, int Cin, int Cout, int act,
                      hipStream_t s);
+// the same product with both operands staged through the LDS ring (conv3x3_f32_v2.hip; same support predicate)
+void conv3x3_f32_v2(const float* x, const void* wsplit, const float* bias, const float* res, const float* res2,
+                    long res2_rows, const float* mask, float* out, int B, int H, int W, int Cin, int Cout, int act,
+                    int variant, hipStream_t s);
+void gemm_f32_v2(const float* a, const void* bsplit, const float* bias, const float* res, float* out, long M, int N,
+                 int K, int act, int variant, hipStream_t s);
 
 // Strided multi-tensor copy (+ dtype conversion) into contiguous destinations: dst[t][i] for the dst index
 // i = ((i0 * size1 + i1) * size2 + i2) * size3 + i3 reads src[t][base + sum_k ik * stride_k] (strides may be

@@ -347,9 +347,13 @@ bool gemm_f32_psb_supported(long M, int N, int K) {
          presplit_b_bytes(N, K) < 0x7ffffff0L;
 }
 
-// variant: 0 = two B register sets (2 waves / SIMD), 1 = one set (3 waves / SIMD)
+// variant: 0 = two B register sets (2 waves / SIMD), 1 = one set (3 waves / SIMD); >= 10: gemm_f32_v2 variant - 10
 void gemm_f32_psb(const float* a, const void* bsplit, const float* bias, const float* res, float* out, long M, int N,
                   int K, int act, int variant, hipStream_t s) {
+  if (variant >= 10) {        // both operands staged through the LDS ring (conv3x3_f32_v2.hip), variant - 10
+    gemm_f32_v2(a, bsplit, bias, res, out, M, N, K, act, variant - 10, s);
+    return;
+  }
   const long nwg = (M + kPsbBM - 1) / kPsbBM * (N / kPsbBN);
   if (nwg == 0) return;
   const int KT = (K + 15) / 16;
@@ -367,9 +371,24 @@ bool conv3x3_f32_psb_supported(long M, int Cin, int Cout) {
          presplit_b_bytes(Cout, 9 * Cin) < 0x7ffffff0L && M * Cout < 0x7ffffff0L;
 }
 
+// APPLESTAR_CONV_V2: the design with both operands staged through the LDS ring (conv3x3_f32_v2.hip) and its
+// variant (default 2: 4 x 1 waves, 2 stages, 4 workgroups per CU: 218 vs 235 us on the ResBlock conv,
+// profiles/r8d_conv_v2.jsonl); -1 = the register-streamed weight planes below
+int conv_v2_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("APPLESTAR_CONV_V2");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+
 void conv3x3_f32_psb(const float* x, const void* wsplit, const float* bias, const float* res, const float* res2,
                      long res2_rows, const float* mask, float* out, int B, int H, int W, int Cin, int Cout, int act,
                      hipStream_t s) {
+  if (conv_v2_variant() >= 0) {
+    conv3x3_f32_v2(x, wsplit, bias, res, res2, res2_rows, mask, out, B, H, W, Cin, Cout, act, conv_v2_variant(), s);
+    return;
+  }
   const long M = static_cast<long>(B) * H * W;
   const long nwg = (M + kPsbBM - 1) / kPsbBM * (Cout / kPsbBN);
   if (nwg == 0) return;

@@ -13,15 +13,17 @@ every 4 iterations (``distar/ctools/worker/learner/learner_comm.py:53-99``); act
   data plane) or a :class:`SharedModelSlot` in ``/dev/shm`` that co-located inference servers read directly;
 * :class:`SharedModelSlot` - POSIX shared memory: a 64-byte header (seqlock ``version``: odd while a copy is in
   flight; ``model_last_iter``; ``reset_flag``; payload size; the publisher's random ``session`` id; a hash of the
-  layout's names and shapes) followed by the flat fp32 payload, registered with the HIP runtime
+  layout's names and shapes; the publisher's pid) followed by the flat fp32 payload, registered with the HIP runtime
   (``hipHostRegister``) in every process that maps it, so both the learner's D2H and the reader's H2D are DMAs;
 * :class:`ModelSubscriber` (inference server) - ``poll``: when the version moved, ONE H2D DMA of the flat payload
   into a device buffer, a version re-check (a torn read is dropped and retried next poll), then ONE native
   multi-tensor D2D copy into the resident model's parameters (captured HIP graphs stay valid: the parameters are
   updated in place).  A subscriber is bound to ONE publisher session: ``poll`` reports the slot ``stale`` when the
   file was replaced (another inode at the path: a restarted learner, ``reset_comm_setting``), when a new publisher
-  re-created it in place (another session id) or when the layout hash no longer matches; the caller then re-attaches
-  or falls back to the network broadcast (actor/comm.py).
+  re-created it in place (another session id), when the layout hash no longer matches or when the publishing
+  process has exited (a slot left behind by a crashed or terminated learner is never attached either: it would
+  serve that run's last weights to the next run's actors); the caller then re-attaches or falls back to the network
+  broadcast (actor/comm.py).
 
 A ~116 MB policy moves as one DMA each way instead of ~430 per-tensor copies, a clone and a pickle/TCP frame.
 """
@@ -37,7 +39,8 @@ from typing import Dict, List, Optional, Tuple
 import torch
 
 _HEADER = 64
-_HDR = struct.Struct('<qqqqQQ')      # version, model_last_iter, reset_flag, payload elements, session, layout hash
+# version, model_last_iter, reset_flag, payload elements, session, layout hash, publisher pid
+_HDR = struct.Struct('<qqqqQQq')
 
 
 class FlatLayout:
@@ -113,13 +116,14 @@ class SharedModelSlot:
         self.numel = int(numel)
         self.session = int.from_bytes(os.urandom(8), 'little') if create else 0
         self.layout_hash = int(layout_hash)
+        self.owner_pid = os.getpid() if create else 0
         buf = torch.frombuffer(self._mm, dtype=torch.uint8)
         self.header = buf[:_HEADER]
         self.payload = buf[_HEADER:].view(torch.float32)
         if create:
             self._write_header(0, 0, 0)
         else:
-            self.session, self.layout_hash = self.read_header()[4:6]
+            self.session, self.layout_hash, self.owner_pid = self.read_header()[4:7]
         self._registered = False
         if torch.cuda.is_available():
             rc = int(torch.cuda.cudart().cudaHostRegister(buf.data_ptr(), nbytes, 0))
@@ -128,10 +132,23 @@ class SharedModelSlot:
 
     def _write_header(self, version: int, last_iter: int, reset: int) -> None:
         self._mm[0:_HDR.size] = _HDR.pack(int(version), int(last_iter), int(reset), self.numel, self.session,
-                                          self.layout_hash)
+                                          self.layout_hash, self.owner_pid)
 
-    def read_header(self) -> Tuple[int, int, int, int, int, int]:
+    def read_header(self) -> Tuple[int, int, int, int, int, int, int]:
         return _HDR.unpack(self._mm[0:_HDR.size])
+
+    def owner_alive(self) -> bool:
+        """The publishing process still runs (co-located: one pid namespace)."""
+        pid = int(self.read_header()[6])
+        if pid <= 0:
+            return False
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            return False
+        except PermissionError:       # exists, another user's
+            return True
+        return True
 
     def replaced(self) -> bool:
         """True when the path no longer names the mapped file (unlinked, or re-created as another inode)."""
@@ -247,7 +264,7 @@ class ModelSubscriber:
         self.flat_dev = torch.empty(self.slot.numel, dtype=torch.float32, device=self.device)
         self._dsts: List[torch.Tensor] = []
         self._srcs: List[torch.Tensor] = []
-        self.stale = False
+        self.stale = not self.slot.owner_alive()     # a dead learner's slot is never read
 
     @staticmethod
     def _numel_of(shm_name: str) -> int:
@@ -273,8 +290,9 @@ class ModelSubscriber:
         """Load the newest version if one was published since the last poll; True when the model changed."""
         if self.layout is None or self.stale:
             return False
-        v, it, reset, _, session, lhash = self.slot.read_header()
-        if session != self.slot.session or lhash != self.slot.layout_hash or self.slot.replaced():
+        v, it, reset, _, session, lhash, _ = self.slot.read_header()
+        if session != self.slot.session or lhash != self.slot.layout_hash or self.slot.replaced() or \
+                not self.slot.owner_alive():
             self.stale = True                 # another publisher owns the path now: re-attach (actor/comm.py)
             return False
         if v % 2 or v == self.version:

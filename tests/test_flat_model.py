@@ -202,3 +202,27 @@ def test_actor_reattaches_recreated_slot_and_falls_back_to_broadcast():
     finally:
         srv.detach_model_slot('MP0')
         pub.close(unlink=True)
+
+
+def test_slot_of_exited_learner_is_not_attached(tmp_path):
+    """A slot a terminated learner left in /dev/shm (no unlink) still holds that run's last weights: the next
+    run's inference server must not attach it (the publisher's pid is in the header)."""
+    import subprocess
+    import sys
+    from applestar_amd.actor.inference import InferenceServer
+    name = _name('dead')
+    code = ("import os, sys, torch; sys.path.insert(0, %r)\n"
+            "from applestar_amd.models.model import Model\n"
+            "from applestar_amd.runtime.flat_model import ModelPublisher\n"
+            "m = Model({}); sd = m.policy_state_dict(); p = ModelPublisher(sd, shm_name=%r)\n"
+            "p.publish(sd, last_iter=7); p.wait(); os._exit(0)\n") % (os.path.dirname(os.path.dirname(
+                os.path.abspath(__file__))), name)
+    subprocess.run([sys.executable, '-c', code], check=True, timeout=300)
+    try:
+        assert os.path.exists('/dev/shm/' + name)
+        _, b = _models('cpu')
+        srv = InferenceServer(device='cpu', amp_dtype=None)
+        srv.set_model('MP0', b)
+        assert not srv.attach_model_slot('MP0', name) and srv.model_slot_state('MP0') is None
+    finally:
+        os.unlink('/dev/shm/' + name)

@@ -305,11 +305,11 @@ def test_multi_logp_matches_log_softmax_gather():
         assert got[k].shape == ref.shape and (got[k] - ref).abs().max().item() < 1e-4, k
 
 
-@pytest.mark.parametrize('variant', [0, 1])
+@pytest.mark.parametrize('variant', [0, 1, 10, 12, 14])
 @pytest.mark.parametrize('shape', [(1000, 256, 256), (777, 128, 132), (4099, 384, 1000)])
 def test_gemm_f32_psb_matches_fp64(variant, shape):
-    """fp32 GEMM on pre-split weight planes (gemm_f32_psb.hip, both register schemes): relu(A B^T + bias + res)
-    == float64 to fp32 accuracy, ragged M / K included."""
+    """fp32 GEMM on pre-split weight planes (gemm_f32_psb.hip, both register schemes; >= 10: both operands through
+    the LDS ring, conv3x3_f32_v2.hip): relu(A B^T + bias + res) == float64 to fp32 accuracy, ragged M / K included."""
     from applestar_amd.ops import native as N
     C = N.ensure_loaded()
     torch.manual_seed(7)
@@ -348,6 +348,31 @@ def test_conv3x3_f32_psb_matches_ring(mode):
     else:
         got, ref = C.conv3x3_f32_psb(x, ws, Co, None, res, res2, mask, 0), C.conv3x3_f32_epi2(x, w, res, res2, mask)
     assert (got - ref).abs().max().item() <= 1e-5 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.parametrize('variant', [0, 1, 2, 3, 4])
+@pytest.mark.parametrize('shape', [(5, 19, 20, 128, 128), (3, 9, 13, 64, 256), (2, 38, 40, 32, 128)])
+def test_conv3x3_f32_v2_variants_match_fp64(variant, shape):
+    """The ring-staged split conv (conv3x3_f32_v2.hip, every variant: wave layouts 4x1 / 2x2, 2-4 stages, 16- / 32-deep
+    K-steps) == float64 with the full epilogue (bias, residual, first-rows hand-over, ReLU mask); ragged pixel
+    counts, Cin 32 / 64 / 128, two column tiles."""
+    from applestar_amd.ops import native as N
+    C = N.ensure_loaded()
+    torch.manual_seed(10)
+    B, H, W, Ci, Co = shape
+    x = torch.randn(B, H, W, Ci, device=DEV)
+    w = torch.randn(Co, 3, 3, Ci, device=DEV) / (9 * Ci) ** 0.5
+    bias = torch.randn(Co, device=DEV)
+    res = torch.randn(B, H, W, Co, device=DEV)
+    res2 = torch.randn(1, H, W, Co, device=DEV)
+    mask = torch.randn(B, H, W, Co, device=DEV)
+    got = C.conv3x3_f32_v2(x, C.presplit_b(w.reshape(Co, -1).contiguous()), Co, bias, res, res2, mask, 0, variant)
+    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double().permute(0, 3, 1, 2),
+                                     bias.double(), padding=1).permute(0, 2, 3, 1) + res.double()
+    ref[:1] += res2.double()
+    ref = torch.where(mask > 0, ref, torch.zeros_like(ref))
+    err = (got.double() - ref).abs().max().item()
+    assert err < 2e-5 * max(1.0, ref.abs().max().item()), err
 
 
 def test_derived_psb_forms_refresh_batched():

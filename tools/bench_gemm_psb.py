@@ -27,7 +27,10 @@ def main():
         res = {}
         for name, fn in (('ring', lambda: C.gemm_f32(a, b, bias, None, 1)),
                          ('psb_db2w', lambda: C.gemm_f32_psb(a, bs, Nn, K, bias, None, 1, 0)),
-                         ('psb_sb', lambda: C.gemm_f32_psb(a, bs, Nn, K, bias, None, 1, 1))):
+                         ('psb_sb', lambda: C.gemm_f32_psb(a, bs, Nn, K, bias, None, 1, 1)),
+                         ('v2_ns3', lambda: C.gemm_f32_psb(a, bs, Nn, K, bias, None, 1, 10)),
+                         ('v2_ns2', lambda: C.gemm_f32_psb(a, bs, Nn, K, bias, None, 1, 12)),
+                         ('v2_k32', lambda: C.gemm_f32_psb(a, bs, Nn, K, bias, None, 1, 14))):
             out = fn()
             err = (out[:4096].double() - ref).abs()
             for _ in range(3):
@@ -56,7 +59,9 @@ def main():
         torch.cuda.synchronize()
         print(json.dumps({'shape': [Nn, K], 'presplit_us': round(t0.elapsed_time(t1) * 1e3 / iters, 1),
                           'speedup_db2w': round(res['ring'] / res['psb_db2w'], 3),
-                          'speedup_sb': round(res['ring'] / res['psb_sb'], 3)}), flush=True)
+                          'speedup_sb': round(res['ring'] / res['psb_sb'], 3),
+                          'best_v2_vs_psb': round(min(res['psb_db2w'], res['psb_sb']) /
+                                                  min(res['v2_ns3'], res['v2_ns2'], res['v2_k32']), 3)}), flush=True)
 
 
 if __name__ == '__main__':

@@ -38,13 +38,13 @@ def _free_port():
     return p
 
 
-def _learner_main(comm, B, T, precision, lr, iq, stop_ev):
+def _learner_main(comm, B, T, precision, lr, iq, stop_ev, exp):
     import torch
     from applestar_amd.learner.rl_learner import RLLearner
     gpu = torch.cuda.is_available()
     if not gpu:
         torch.set_num_threads(2)
-    lrn = RLLearner({'common': {'experiment_name': 'learn_pipeline'},
+    lrn = RLLearner({'common': {'experiment_name': exp},
                      'learner': {'use_cuda': gpu, 'player_id': 'MP0', 'use_value_feature': False,
                                  'learning_rate': lr,
                                  'amp_dtype': 'bfloat16' if precision == 'bf16' else None,
@@ -141,8 +141,9 @@ def main():
     ctx = mp.get_context('spawn')
     iq = ctx.Queue()
     stop_ev = ctx.Event()
+    exp = f'learn_pipeline_{os.getpid()}'     # this run's own model slot (runtime/flat_model.py)
     lp = ctx.Process(target=_learner_main, args=(comm, args.batch, args.traj_len, args.precision, args.lr, iq,
-                                                 stop_ev), daemon=True)
+                                                 stop_ev, exp), daemon=True)
     lp.start()
     iters = []
 
@@ -150,7 +151,7 @@ def main():
         while True:
             iters.append(iq.get())
     threading.Thread(target=drain, daemon=True).start()
-    actor = Actor({'common': {'experiment_name': 'learn_pipeline'},
+    actor = Actor({'common': {'experiment_name': exp},
                    'actor': {'job_type': 'train', 'env_num': args.envs, 'gpu_batch_inference': True,
                              'traj_len': args.traj_len, 'episode_num': 10 ** 9, 'print_freq': 10 ** 9},
                    'env': {'game_steps_per_episode': 10 ** 9, 'fake': True, 'fake_learnable': True,
