@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(const float* __restrict_
 // read 32 consecutive floats of one row).  The conv form's X piece of a lane is a fixed 4-channel group of one tap
 // (the lane's column is the same in every stage); its row's image coordinates advance by 16 rows per issued step.
 template <int BN, int BK, bool CONV, int NS>
-__global__ __launch_bounds__(256, ((BN == 128 && BK == 128) || BN == 32) ? 2 : 3) void wgrad_f32_pipe_kernel(const float* __restrict__ dy,
+__global__ __launch_bounds__(256, ((BN == 128 && BK >= 128) || BN == 32) ? 2 : 3) void wgrad_f32_pipe_kernel(const float* __restrict__ dy,
                                                                 const float* __restrict__ x,
                                                                 float* __restrict__ dw_part, float* __restrict__ db_part,
                                                                 long part_stride, long R, int N, int K, int H, int W,
@@ -346,23 +346,40 @@ __global__ __launch_bounds__(256, ((BN == 128 && BK == 128) || BN == 32) ? 2 : 3
     for (int sub = 0; sub < SUB; ++sub) {
       const float* A = reinterpret_cast<const float*>(st) + (16 * sub + 8 * h) * BN + wn * TN + l32;
       const float* Bt = reinterpret_cast<const float*>(st + A_BYTES) + (16 * sub + 8 * h) * BK + wk * TK + l32;
-      float av[FN][8], bv[FK][8];
+      float av[FN][8];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) {
+      for (int t = 0; t < 8; ++t)
 #pragma unroll
         for (int i = 0; i < FN; ++i) av[i][t] = A[t * BN + 32 * i];
-#pragma unroll
-        for (int j = 0; j < FK; ++j) bv[j][t] = Bt[t * BK + 32 * j];
-      }
-      Split3 sa[FN], sb[FK];
+      Split3 sa[FN];
 #pragma unroll
       for (int i = 0; i < FN; ++i) sa[i] = split8(av[i]);
+      if constexpr (FK <= 2) {
+        float bv[FK][8];
 #pragma unroll
-      for (int j = 0; j < FK; ++j) sb[j] = split8(bv[j]);
+        for (int t = 0; t < 8; ++t)
 #pragma unroll
-      for (int i = 0; i < FN; ++i)
+          for (int j = 0; j < FK; ++j) bv[j][t] = Bt[t * BK + 32 * j];
+        Split3 sb[FK];
 #pragma unroll
-        for (int j = 0; j < FK; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+        for (int j = 0; j < FK; ++j) sb[j] = split8(bv[j]);
+#pragma unroll
+        for (int i = 0; i < FN; ++i)
+#pragma unroll
+          for (int j = 0; j < FK; ++j) acc[i][j] = mfma_x6(sa[i], sb[j], acc[i][j]);
+      } else {
+        // the wide tile (64 x 128 per wave: 2 dY + 4 X fragments per 48 MFMAs, 25 % less split VALU per MFMA than
+        // 64 x 64): X fragments streamed one at a time
+#pragma unroll
+        for (int j = 0; j < FK; ++j) {
+          float bv[8];
+#pragma unroll
+          for (int t = 0; t < 8; ++t) bv[t] = Bt[t * BK + 32 * j];
+          const Split3 sb = split8(bv);
+#pragma unroll
+          for (int i = 0; i < FN; ++i) acc[i][j] = mfma_x6(sa[i], sb, acc[i][j]);
+        }
+      }
       if (do_bias) {
 #pragma unroll
         for (int i = 0; i < FN; ++i)
@@ -406,6 +423,192 @@ __global__ __launch_bounds__(256, ((BN == 128 && BK == 128) || BN == 32) ? 2 : 3
   }
 }
 
+// Split-once staging (the 128 x 128 tiles of the split-MFMA mode, APPLESTAR_WGRAD_STG): in the ring kernel above every
+// wave splits each fragment it reads, and in its 2 x 2 wave layout every dY and every X fragment is split by two
+// waves - the split is ~80 % of the loop's VALU (9-11 VALU per MFMA, profiles/r8h_pmc_wgrad_*).  Here each fp32
+// value of a stage is split ONCE per workgroup into three bf16 planes stored in MFMA fragment order, which the
+// waves then read with one conflict-free ds_read_b128 per plane:
+//
+//   fp32 ring F[2] (16 reduction rows x (128 dY + 128 X) columns, LDS-DMA as loaded)
+//   planes P[2]: P[p][block(4)][half(2)][lane(32)] x 16 B for dY and for X (24 KB per stage)
+//   step kt: wait F(kt + 1) -> s_barrier -> DMA F(kt + 2) into F(kt)'s slot -> split F(kt + 1) into P(kt + 1)
+//            (thread t: column t % 128, rows 8 (t / 128) .. + 7, of dY and of X) beside MFMA(kt) on P(kt)
+// so the split of the next step and the products of this one share a barrier interval.  80 KB of LDS: 2
+// workgroups per CU.  db: each thread's dY column sums, the two row halves combined through LDS at the end.
+template <bool CONV>
+__global__ __launch_bounds__(256, 2) void wgrad_f32_stg_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                                              float* __restrict__ dw_part, float* __restrict__ db_part,
+                                                              long part_stride, long R, int N, int K, int H, int W,
+                                                              int Cin, long rows_per_split, int tiles_n, int tiles_k) {
+  constexpr int BN = 128, BK = 128, RS = 16;
+  constexpr int A_BYTES = RS * BN * 4, B_BYTES = RS * BK * 4, FST = A_BYTES + B_BYTES;     // 16 KB fp32 stage
+  constexpr int A_PW = A_BYTES / 4096, B_PW = B_BYTES / 4096;                          // 2 + 2 DMA per wave
+  constexpr int A_CPR = BN / 4, B_CPR = BK / 4, A_RPI = 64 / A_CPR, B_RPI = 64 / B_CPR;
+  constexpr int PL = 4 * 2 * 32 * 16;          // one plane of one operand: 4 blocks x 2 halves x 32 lanes x 16 B
+  constexpr int PST = 2 * 3 * PL;               // planes of a stage (dY then X): 24 KB
+  __shared__ __attribute__((aligned(16))) char F[2 * FST];
+  __shared__ __attribute__((aligned(16))) char P[2 * PST];      // 80 KB in all: 2 workgroups per CU
+
+  const int wg = pipe::xcd_remap();
+  const int tk = wg % tiles_k;
+  const int tn = (wg / tiles_k) % tiles_n;
+  const int s = wg / (tiles_k * tiles_n);
+  const int n0 = tn * BN, k0 = tk * BK;
+  const long r_begin = static_cast<long>(s) * rows_per_split;
+  const long r_end = r_begin + rows_per_split < R ? r_begin + rows_per_split : R;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wid >> 1, wk = wid & 1;
+  const int l32 = lane & 31, h = lane >> 5;
+  const long HW = static_cast<long>(H) * W;
+  const pipe::i32x4 yr = pipe::rsrc(dy, R * N * 4), xr = pipe::rsrc(x, CONV ? R * Cin * 4 : R * K * 4);
+
+  // DMA pieces (the ring kernel's): fixed column per lane, row (within a step) per chunk
+  const int a_col = n0 + 4 * (lane % A_CPR), b_col = k0 + 4 * (lane % B_CPR);
+  int a_row[A_PW], b_row[B_PW];
+#pragma unroll
+  for (int c = 0; c < A_PW; ++c) a_row[c] = (wid + 4 * c) * A_RPI + lane / A_CPR;
+#pragma unroll
+  for (int c = 0; c < B_PW; ++c) b_row[c] = (wid + 4 * c) * B_RPI + lane / B_CPR;
+  int b_c = b_col, b_dy = 0, b_dx = 0;
+  if (CONV) {
+    const int tap = b_col / Cin;
+    b_c = b_col - tap * Cin;
+    b_dy = tap / 3 - 1;
+    b_dx = tap % 3 - 1;
+  }
+  const bool a_ok = a_col < N, b_ok = b_col < K;
+  int py[B_PW], px[B_PW];
+  const int adv_y = RS / W, adv_x = RS % W;
+  if (CONV) {
+#pragma unroll
+    for (int c = 0; c < B_PW; ++c) {
+      const int rem = static_cast<int>((r_begin + b_row[c]) % HW);
+      py[c] = rem / W;
+      px[c] = rem - py[c] * W;
+    }
+  }
+  const long nsteps = r_end > r_begin ? (r_end - r_begin + RS - 1) / RS : 0;
+  auto issue = [&](long kt) {
+    char* st = F + (kt & 1) * FST;
+    const long r0 = r_begin + kt * RS;
+#pragma unroll
+    for (int c = 0; c < A_PW; ++c) {
+      const long r = r0 + a_row[c];
+      pipe::dma16(yr, st + (wid + 4 * c) * 1024,
+                  (kt < nsteps && a_ok && r < r_end) ? (static_cast<int>(r) * N + a_col) * 4 : pipe::kOOB);
+    }
+#pragma unroll
+    for (int c = 0; c < B_PW; ++c) {
+      const long r = r0 + b_row[c];
+      int off = pipe::kOOB;
+      if (CONV) {
+        const int yy = py[c] + b_dy, xx = px[c] + b_dx;
+        if (kt < nsteps && b_ok && r < r_end && yy >= 0 && yy < H && xx >= 0 && xx < W)
+          off = ((static_cast<int>(r) + b_dy * W + b_dx) * Cin + b_c) * 4;
+        px[c] += adv_x;
+        py[c] += adv_y;
+        if (px[c] >= W) { px[c] -= W; ++py[c]; }
+        while (py[c] >= H) py[c] -= H;
+      } else if (kt < nsteps && b_ok && r < r_end) {
+        off = (static_cast<int>(r) * K + b_col) * 4;
+      }
+      pipe::dma16(xr, st + A_BYTES + (wid + 4 * c) * 1024, off);
+    }
+  };
+
+  // split work of this thread: column sc of dY and of X, rows 8 sh .. 8 sh + 7 of the stage
+  const int sc = tid & (BN - 1), sh = tid >> 7;
+  const bool do_bias = db_part != nullptr && tk == 0;
+  float bsum = 0.f;
+  auto split_stage = [&](long j) {
+    const float* fa = reinterpret_cast<const float*>(F + (j & 1) * FST);
+    const float* fb = fa + RS * BN;
+    char* pa = P + (j & 1) * PST;
+    char* pb = pa + 3 * PL;
+    float va[8], vb[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      va[q] = fa[(8 * sh + q) * BN + sc];
+      vb[q] = fb[(8 * sh + q) * BK + sc];
+    }
+    const Split3 sa = split8(va), sb = split8(vb);
+    const int slot = (((sc >> 5) * 2 + sh) * 32 + (sc & 31)) * 16;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      *reinterpret_cast<u32v4*>(pa + p * PL + slot) = sa.p[p];
+      *reinterpret_cast<u32v4*>(pb + p * PL + slot) = sb.p[p];
+    }
+    if (do_bias) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) bsum += va[q];
+    }
+  };
+
+  f16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  if (nsteps > 0) {
+    issue(0);
+    issue(1);
+    pipe::wait_vm<A_PW + B_PW>();          // this wave's pieces of step 0
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    split_stage(0);
+  }
+  for (long kt = 0; kt < nsteps; ++kt) {
+    // F(kt + 1) landed (this wave's pieces, then everyone's); everyone finished split(kt) (P(kt) complete, F(kt)
+    // free) and MFMA(kt - 1) (P(kt + 1)'s slot free)
+    pipe::wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    issue(kt + 2);
+    if (kt + 1 < nsteps) split_stage(kt + 1);
+    const char* pa = P + (kt & 1) * PST;
+    const char* pb = pa + 3 * PL;
+    Split3 fa[2], fb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        const int off = p * PL + (((wn * 2 + i) * 2 + h) * 32 + l32) * 16;
+        fa[i].p[p] = *reinterpret_cast<const u32v4*>(pa + off);
+        fb[i].p[p] = *reinterpret_cast<const u32v4*>(pb + p * PL + (((wk * 2 + i) * 2 + h) * 32 + l32) * 16);
+      }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6(fa[i], fb[j], acc[i][j]);
+  }
+  pipe::wait_vm<0>();
+
+  // accumulator (i, j) register e: n = n0 + wn 64 + 32 i + (e&3) + 8 (e>>2) + 4 h, k = k0 + wk 64 + 32 j + l32
+  float* outp = dw_part + static_cast<long>(s) * part_stride;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = k0 + wk * 64 + 32 * j + l32;
+      if (k >= K) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int n = n0 + wn * 64 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (n < N) outp[static_cast<long>(n) * K + k] = acc[i][j][e];
+      }
+    }
+  if (do_bias) {
+    float* bred = reinterpret_cast<float*>(F);      // the ring is idle: every DMA landed (wait_vm<0> above)
+    __syncthreads();
+    if (sh == 1) bred[sc] = bsum;
+    __syncthreads();
+    if (sh == 0 && n0 + sc < N) db_part[static_cast<long>(s) * part_stride + n0 + sc] = bsum + bred[sc];
+  }
+}
+
 // The 32-wide ring kernel is opt-in (APPLESTAR_WGRAD32_PIPE=1): on the learner's narrow convs it measured
 // 5-13 % slower than the register-staged kernel (76x80 64->32: 1358 vs 1283 us; 19x20 32->32: 66.7 vs
 // 59.2 us; profiles/r3v2_wgrad32_ab.jsonl) - 60 KB of stages hold it at 2 workgroups per CU.
@@ -417,12 +620,28 @@ bool wgrad_f32_pipe32_off() {
   return off;
 }
 
+// APPLESTAR_WGRAD_STG=0: the 128 x 128 tiles on the per-wave-split ring kernel instead of split-once staging
+bool wgrad_stg() {
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_WGRAD_STG");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 template <int BN, int BK, bool CONV>
 void launch(const float* dy, const float* x, float* dwp, float* dbp, long ps, long R, int N, int K, int H, int W,
             int Cin, int S, long rps, hipStream_t st) {
   const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
   const long nwg = static_cast<long>(tn) * tk * S;
-  if constexpr (BN >= 32 && BK <= 128) {
+  if constexpr (BN == 128 && BK == 128) {
+    if (f32_mfma_mode() == 1 && wgrad_stg()) {
+      hipLaunchKernelGGL((wgrad_f32_stg_kernel<CONV>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x, dwp,
+                         dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
+      return;
+    }
+  }
+  if constexpr (BN >= 32 && (BK <= 128 || (BN == 128 && BK == 256))) {
     if (f32_mfma_mode() == 1 && !(BN == 32 && wgrad_f32_pipe32_off())) {
       hipLaunchKernelGGL((wgrad_f32_pipe_kernel<BN, BK, CONV, 3>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st,
                          dy, x, dwp, dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
@@ -448,9 +667,18 @@ bool wgrad32_bk256() {
   }();
   return on;
 }
+// APPLESTAR_WGRAD_WIDE=1: 128 x 256 tiles (each wave 64 x 128) for N >= 128, K >= 256 in split-MFMA mode
+bool wgrad_wide() {
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_WGRAD_WIDE");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
 // the K tile: a wave covers >= 32 columns (2 waves along K for BN >= 64, 4 for the 32-wide N tile)
 int pick_k(int k, int bn) {
   if (bn == 32) return (k >= 256 && wgrad32_bk256()) ? 256 : 128;
+  if (bn == 128 && k >= 256 && wgrad_wide() && f32_mfma_mode() == 1) return 256;
   return k <= 64 ? 64 : 128;
 }
 
@@ -493,7 +721,7 @@ void wgrad_f32(const float* dy, const float* x, float* dw_part, float* db_part, 
     else launch<BNv, BKv, false>(dy, x, dw_part, db_part, part_stride, R, N, K, H, W, Cin, S, rps, st);     \
     return;                                                                                \
   }
-  AS_WGF(128, 128) AS_WGF(128, 64) AS_WGF(64, 128) AS_WGF(64, 64) AS_WGF(32, 128) AS_WGF(32, 256)
+  AS_WGF(128, 128) AS_WGF(128, 64) AS_WGF(64, 128) AS_WGF(64, 64) AS_WGF(32, 128) AS_WGF(32, 256) AS_WGF(128, 256)
 #undef AS_WGF
 }
 

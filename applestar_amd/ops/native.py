@@ -767,7 +767,7 @@ def _wgrad(dy2d, x, cin, has_b, bf16_out, param=None):
     ``param``: the weight, when the caller lets the product be deferred (_Deferred: single-use weights only)."""
     if dy2d.dtype == torch.float32:
         if _Deferred.on and dy2d.is_cuda and param is not None and _single_use(param):
-            return _Deferred.add(dy2d, x, cin, has_b)
+            return _Deferred.add(dy2d, x, cin, has_b, param)
         return _C.wgrad_f32(dy2d, x, cin, has_b)
     return _C.wgrad(dy2d, x, cin, has_b, bf16_out)
 
@@ -793,13 +793,19 @@ def _single_use(p) -> bool:
     ``F.linear`` or a torch fallback - would have its gradients summed by autograd on the main stream into a
     buffer the side stream has not written yet."""
     u = getattr(p, '_as_uses', None)
-    return u is not None and u == (_FWD_EPOCH[0], 1) and getattr(p, '_as_one_consumer', -1) == _FWD_EPOCH[0]
+    return u is not None and u == (_FWD_EPOCH[0], 1) and getattr(p, '_as_one_consumer', False)
 
 
 def single_consumer_params(root) -> list:
     """The leaf tensors that exactly ONE edge of ``root``'s autograd graph reaches (their AccumulateGrad node has
-    one producer of its gradient).  One iterative walk over the graph.  Visited nodes are held in ``seen`` (node
-    wrappers are created on access: an id is unique only while its object lives)."""
+    one producer of its gradient)."""
+    return [t for t, c in _consumer_counts(root).values() if c == 1]
+
+
+def _consumer_counts(root) -> dict:
+    """{id(AccumulateGrad node): (leaf tensor, edges reaching it)} over ``root``'s autograd graph: one iterative
+    walk.  Visited nodes are held in ``seen`` (node wrappers are created on access: an id is unique only while its
+    object lives)."""
     counts, seen, stack = {}, {}, [root.grad_fn] if root.grad_fn is not None else []
     while stack:
         fn = stack.pop()
@@ -813,7 +819,7 @@ def single_consumer_params(root) -> list:
             elif id(nxt) not in seen:
                 seen[id(nxt)] = nxt
                 stack.append(nxt)
-    return [node.variable for node, c in counts.values() if c == 1]
+    return {k: (node.variable, c) for k, (node, c) in counts.items()}
 
 
 class _Deferred:
@@ -834,24 +840,58 @@ class _Deferred:
     streams = {}
     flushed = None
 
+    issued = []          # (param, dW view): checked against what autograd returns (defer_verify)
+    walks = 0            # graph walks so far (single_consumer_params), one per REWALK deferral steps
+    steps = 0
+
     @classmethod
-    def add(cls, dy2d, x, cin, has_b):
+    def add(cls, dy2d, x, cin, has_b, param=None):
         N = dy2d.shape[1]
         K = 9 * cin if cin > 0 else x.shape[1]
         out = torch.empty(N * K + (N if has_b else 0), dtype=torch.float32, device=dy2d.device)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(dy2d.device))
         cls.q.append((ev, dy2d, x, cin, has_b, out))
-        return out[:N * K].view(N, K), (out[N * K:] if has_b else None)
+        dw = out[:N * K].view(N, K)
+        if param is not None:
+            cls.issued.append((param, dw))
+        return dw, (out[N * K:] if has_b else None)
+
+
+# the single-consumer walk (defer_begin) runs on the first deferral step and then every DEFER_REWALK steps (a walk of
+# the ~2,000-node graph is ~1-2 ms of host time the GPU would wait for between the loss and the backward); every step
+# defer_verify checks what autograd actually returned, so a weight that gained a second consumer in between fails
+# loudly instead of receiving a half-written gradient.  APPLESTAR_DEFER_CHECK=1: walk every step.
+DEFER_REWALK = 1 if os.environ.get('APPLESTAR_DEFER_CHECK', '0') == '1' else 256
+
+
+def defer_verify(params, grads) -> None:
+    """Every deferred weight gradient must reach the buckets exactly as the native node returned it: autograd adds
+    a second consumer's gradient by replacing it (another tensor) or in place (a version bump)."""
+    issued, _Deferred.issued = _Deferred.issued, []
+    if not issued:
+        return
+    got = {id(p): g for p, g in zip(params, grads)}
+    for p, dw in issued:
+        g = got.get(id(p))
+        if g is None:
+            continue
+        if g.data_ptr() != dw.data_ptr() or g._version != dw._version:
+            p._as_one_consumer = False
+            raise RuntimeError('deferred fp32 weight gradient was accumulated by autograd (a second consumer of the '
+                               f'weight {tuple(p.shape)}): run with APPLESTAR_DEFER_WGRAD=0 or APPLESTAR_DEFER_CHECK=1')
 
 
 def defer_begin(device, loss=None) -> None:
     """Start queueing fp32 weight gradients (see :class:`_Deferred`).  ``loss``: the root of the backward about to
     run; only parameters with one consumer in its graph may be deferred (without it nothing is)."""
     if DEFER_WGRAD and torch.device(device).type == 'cuda' and not torch.cuda.is_current_stream_capturing():
-        if loss is not None:
-            for p in single_consumer_params(loss):
-                p._as_one_consumer = _FWD_EPOCH[0]
+        if loss is not None and _Deferred.steps % DEFER_REWALK == 0:
+            for t, c in _consumer_counts(loss).values():
+                t._as_one_consumer = c == 1
+            _Deferred.walks += 1
+        _Deferred.steps += 1
+        _Deferred.issued = []
         _Deferred.on = True
         _Deferred.q = []
         _Deferred.flushed = None

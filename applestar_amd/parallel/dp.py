@@ -117,6 +117,9 @@ class GradientReducer:
                 if cur:
                     self.phase_buckets[phase].append(self._add_bucket(cur))
         self._hooks = []
+        # called with (params, autograd's gradients) before they are copied into the buckets (the deferred weight
+        # gradients' check, ops/native.py defer_verify)
+        self.grad_hook = None
         self.use_avg = self.world > 1 and dist.get_backend(group) == 'nccl'
 
     def _add_bucket(self, params):
@@ -159,6 +162,8 @@ class GradientReducer:
         self._store(self.params, grads, self.buckets)
 
     def _store(self, params, grads, buckets):
+        if self.grad_hook is not None:
+            self.grad_hook(params, grads)
         dst, src = [], []
         stale = set()
         for p, g in zip(params, grads):

@@ -87,6 +87,9 @@ class TrainEngine:
         else:
             self.reducer = GradientReducer(self.params, bucket_mb=lc.bucket_mb, comm_dtype=comm, phase_of=phase_of)
             self.opt_params = self.params
+            if self.device.type == 'cuda':
+                from ..ops.native import defer_verify
+                self.reducer.grad_hook = defer_verify
         # fp32 step: the weights' derived forms built once per optimizer step (MasterWeights owns its own registry)
         self.derived = None
         if self.master is None and self.device.type == 'cuda' and \
