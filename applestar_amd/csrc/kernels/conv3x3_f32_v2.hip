@@ -22,12 +22,12 @@ namespace {
 using pipe::f16v;
 using pipe::i32x4;
 
-constexpr int kV2BM = 128, kV2BN = 128;
+constexpr int kV2BM = 128;
 
 // SUB: 16-deep MFMA K-steps per ring stage (1: 20 KB stages; 2: 40 KB, half the barriers and DMA bookkeeping)
 // CONV: the implicit im2col of a 3x3 / pad 1 conv over NHWC x [B, H, W, Cin] (K = 9 Cin); else a dense GEMM with
 // A = x [Mg, Kg] row-major (Kg % 4 == 0; the pre-split planes are zero past Kg)
-template <int WM, int NS, int SUB = 1, bool CONV = true>
+template <int WM, int NS, int SUB = 1, bool CONV = true, int kV2BN = 128>
 __global__ __launch_bounds__(256, 2) void conv3x3_f32_v2_kernel(const float* __restrict__ x,
                                                                 const u32v4* __restrict__ bs,
                                                                 const float* __restrict__ bias,
@@ -41,7 +41,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_f32_v2_kernel(const float* __r
   constexpr int kV2Stage = kV2A + SUB * kV2B1;
   using CA = pipe::Cfg<kV2BN, NS, BK, kV2BM, 4>;     // the activation half of the ring: rows, swizzle, DMA pieces
   constexpr int WN = 4 / WM, TM = kV2BM / WM, TN = kV2BN / WN, FM = TM / 32, FN = TN / 32;
-  constexpr int A_PW = kV2A / 1024 / 4, B_PW = SUB * kV2B1 / 1024 / 4;   // DMA pieces per wave per stage
+  // DMA pieces per wave per stage: A_PW activation pieces; the QB weight pieces are dealt round-robin (wave w takes
+  // pieces w, w + 4, ...: 3 each for 128 columns, 2 / 1 for 64 - the waits are then vmcnt(0), NS = 2)
+  constexpr int A_PW = kV2A / 1024 / 4, QB = SUB * kV2B1 / 1024, B_PW = (QB + 3) / 4;
+  static_assert(QB % 4 == 0 || NS == 2, "uneven weight pieces need the 2-stage ring");
   __shared__ __attribute__((aligned(16))) char ring[NS * kV2Stage];
   const int HW = H * W;
   const long M = CONV ? static_cast<long>(B) * HW : Mg;
@@ -78,11 +81,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_f32_v2_kernel(const float* __r
       }
     }
   }
-  // weight pieces: stage chunk q = B_PW wid + c = (16-deep sub-step q / 12, column block q % 12 / 3, plane q % 3)
+  // weight pieces: stage chunk q = wid + 4 c = (16-deep sub-step q / QB1, column block q % QB1 / 3, plane q % 3)
+  constexpr int QB1 = kV2B1 / 1024;
   int b_off[B_PW];
 #pragma unroll
   for (int c = 0; c < B_PW; ++c) {
-    const int q = B_PW * wid + c, sub = q / 12, r = q % 12;
+    const int q = wid + 4 * c, sub = q / QB1, r = q % QB1;
     b_off[c] = static_cast<int>(((n0 / 32 + r / 3) * KT16 * 3 + sub * 3 + r % 3) * 1024 + 16 * lane);
   }
   auto stage = [&](int kt) { return ring + (kt % NS) * kV2Stage; };
@@ -104,7 +108,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_f32_v2_kernel(const float* __r
     }
 #pragma unroll
     for (int c = 0; c < B_PW; ++c)
-      pipe::dma16(br, st + kV2A + (B_PW * wid + c) * 1024, kt < KT ? b_off[c] + kt * SUB * 3 * 1024 : pipe::kOOB);
+      if (QB % 4 == 0 || wid + 4 * c < QB)            // wave-uniform
+        pipe::dma16(br, st + kV2A + (wid + 4 * c) * 1024, kt < KT ? b_off[c] + kt * SUB * 3 * 1024 : pipe::kOOB);
   };
   f16v acc[FM][FN];
 #pragma unroll
@@ -146,13 +151,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_f32_v2_kernel(const float* __r
   pipe::store_tile<FM, FN>(acc, out, bias, res, M, Cout, m0 + wm * TM, n0 + wn * TN, act, e2);
 }
 
-template <int WM, int NS, int SUB = 1>
+template <int WM, int NS, int SUB = 1, int BN = 128>
 void launch_v2(const float* x, const void* ws, const float* bias, const float* res, const pipe::Epi2& e2, float* out,
                int B, int H, int W, int Cin, int Cout, int act, hipStream_t s) {
   const long M = static_cast<long>(B) * H * W;
-  const long nwg = (M + kV2BM - 1) / kV2BM * (Cout / kV2BN);
-  hipLaunchKernelGGL((conv3x3_f32_v2_kernel<WM, NS, SUB, true>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, s,
-                     x, static_cast<const u32v4*>(ws), bias, res, out, B, H, W, Cin, Cout, act, e2, 0L, 0);
+  const long nwg = (M + kV2BM - 1) / kV2BM * (Cout / BN);
+  hipLaunchKernelGGL((conv3x3_f32_v2_kernel<WM, NS, SUB, true, BN>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0,
+                     s, x, static_cast<const u32v4*>(ws), bias, res, out, B, H, W, Cin, Cout, act, e2, 0L, 0);
 }
 
 }  // namespace
@@ -167,6 +172,11 @@ void conv3x3_f32_v2(const float* x, const void* wsplit, const float* bias, const
   e2.res2 = res2;
   e2.res2_rows = res2_rows;
   e2.mask = mask;
+  if (Cout % 128 != 0) {        // 64 / 32 output channels: 128 x 64 / 128 x 32 tiles (each wave 32 rows), 2 stages
+    if (Cout % 64 == 0) launch_v2<4, 2, 1, 64>(x, wsplit, bias, res, e2, out, B, H, W, Cin, Cout, act, s);
+    else launch_v2<4, 2, 1, 32>(x, wsplit, bias, res, e2, out, B, H, W, Cin, Cout, act, s);
+    return;
+  }
   switch (variant) {
     case 1: launch_v2<4, 4>(x, wsplit, bias, res, e2, out, B, H, W, Cin, Cout, act, s); break;
     case 2: launch_v2<4, 2>(x, wsplit, bias, res, e2, out, B, H, W, Cin, Cout, act, s); break;
@@ -186,7 +196,7 @@ void conv3x3_f32_v2(const float* x, const void* wsplit, const float* bias, const
 // N % 128 == 0, K % 4 == 0): variant 2 = 4 x 1 waves, 2 stages (0: 3 stages; 4: 32-deep K-steps, K % 32 == 0)
 void gemm_f32_v2(const float* a, const void* bsplit, const float* bias, const float* res, float* out, long M, int N,
                  int K, int act, int variant, hipStream_t s) {
-  const long nwg = (M + kV2BM - 1) / kV2BM * (N / kV2BN);
+  const long nwg = (M + kV2BM - 1) / kV2BM * (N / 128);
   if (nwg == 0) return;
   const pipe::Epi2 e2;
   const auto* bs = static_cast<const u32v4*>(bsplit);

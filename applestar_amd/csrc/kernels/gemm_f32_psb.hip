@@ -365,9 +365,11 @@ void gemm_f32_psb(const float* a, const void* bsplit, const float* bias, const f
                        static_cast<const u32v4*>(bsplit), KT, bias, res, out, M, N, K, act);
 }
 
-// Cout % 128, Cin % 16 (every 16-deep K-step inside one tap), 32-bit offsets
+int conv_v2_variant();
+// Cout % 128 (or 64 / 32 on the ring-staged kernel), Cin % 16 (every 16-deep K-step inside one tap), 32-bit offsets
 bool conv3x3_f32_psb_supported(long M, int Cin, int Cout) {
-  return Cout % kPsbBN == 0 && Cin % 16 == 0 && Cin > 0 && M * Cin * 4 < 0x7ffffff0L &&
+  return (Cout % kPsbBN == 0 || ((Cout == 64 || Cout == 32) && conv_v2_variant() >= 0)) && Cin % 16 == 0 && Cin > 0 &&
+         M * Cin * 4 < 0x7ffffff0L &&
          presplit_b_bytes(Cout, 9 * Cin) < 0x7ffffff0L && M * Cout < 0x7ffffff0L;
 }
 

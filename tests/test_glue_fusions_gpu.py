@@ -351,7 +351,8 @@ def test_conv3x3_f32_psb_matches_ring(mode):
 
 
 @pytest.mark.parametrize('variant', [0, 1, 2, 3, 4])
-@pytest.mark.parametrize('shape', [(5, 19, 20, 128, 128), (3, 9, 13, 64, 256), (2, 38, 40, 32, 128)])
+@pytest.mark.parametrize('shape', [(5, 19, 20, 128, 128), (3, 9, 13, 64, 256), (2, 38, 40, 32, 128),
+                                   (3, 38, 40, 128, 64), (2, 21, 17, 32, 64), (3, 19, 20, 32, 32), (2, 17, 23, 64, 32)])
 def test_conv3x3_f32_v2_variants_match_fp64(variant, shape):
     """The ring-staged split conv (conv3x3_f32_v2.hip, every variant: wave layouts 4x1 / 2x2, 2-4 stages, 16- / 32-deep
     K-steps) == float64 with the full epilogue (bias, residual, first-rows hand-over, ReLU mask); ragged pixel
