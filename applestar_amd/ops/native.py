@@ -1328,6 +1328,7 @@ GATE_CHAIN = os.environ.get('APPLESTAR_GATE_CHAIN', '1') == '1'
 # the fp32 step's gate chain in one launch per direction (gate_chain.hip gate_chain_f32_kernel): measured equal to the
 # four f32 GEMMs on the step (profiles/r4z_gate_chain_f32.txt), off by default
 GATE_CHAIN_F32 = os.environ.get('APPLESTAR_GATE_CHAIN_F32', '0') == '1'
+GATE_PSB = os.environ.get('APPLESTAR_GATE_PSB', '1') == '1'       # A/B: the fp32 gate GEMMs on pre-split planes
 
 
 class _GatedResBlock(torch.autograd.Function):
@@ -1362,8 +1363,11 @@ class _GatedResBlock(torch.autograd.Function):
             h = acts[-1]
         elif x.dtype == torch.float32 and _gemm_f32_ok(h.shape[0], C, C):
             # fp32 step: the four gate layers on the f32 GEMM with bias (+ ReLU) in the epilogue
+            psb = GATE_PSB and _psb_ok(h.shape[0], C, C)     # the pre-split weight planes (gemm_f32_psb.hip)
             for i in range(4):
-                h = _C.gemm_f32(h, gate[2 * i].detach().view(C, C), _w32(gate[2 * i + 1]), None, 1 if i < 3 else 0)
+                gw, gb, act = gate[2 * i], _w32(gate[2 * i + 1]), 1 if i < 3 else 0
+                h = _C.gemm_f32_psb(h, _psb(gw), C, C, gb, None, act, GEMM_PSB_VARIANT) if psb \
+                    else _C.gemm_f32(h, gw.detach().view(C, C), gb, None, act)
                 acts.append(h)
         else:
             for i in range(4):
@@ -1417,12 +1421,17 @@ class _GatedResBlock(torch.autograd.Function):
         elif x.dtype == torch.float32 and _gemm_f32_ok(d.shape[0], C, C):
             # fp32 step: each input gradient on the f32 GEMM with the previous layer's ReLU mask (ACT_DRELU on its
             # saved output) or the skip gradient in the epilogue - no threshold_backward / addmm passes
+            psb = GATE_PSB and _psb_ok(d.shape[0], C, C)
+
+            def dgemm(d, i, r, mode):
+                return _C.gemm_f32_psb(d, _psb(gws[i], True), C, C, None, r, mode, GEMM_PSB_VARIANT) if psb \
+                    else _C.gemm_f32(d, _wT(gws[i]), None, r, mode)
             for i in (3, 2, 1, 0):
                 dw_i, db_i = _wgrad(d, acts_in[i], 0, True, False, gws[i])
                 grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
                 if i > 0:
-                    d = _C.gemm_f32(d, _wT(gws[i]), None, acts_in[i], 4)
-            dx_gate = _C.gemm_f32(d, _wT(gws[0]), None, dx_res.view(-1, C).contiguous(), 0)
+                    d = dgemm(d, i, acts_in[i], 4)
+            dx_gate = dgemm(d, 0, dx_res.view(-1, C).contiguous(), 0)
         else:
             for i in (3, 2, 1, 0):
                 dw_i, db_i = _wgrad(d, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))

@@ -1,16 +1,14 @@
-"""Find host <-> GPU synchronisations inside one learner step (the bench's fp32 RL step by default).
+"""Host <-> device synchronisations inside one learner step: every op that makes the host wait for the GPU
+(``torch.cuda.set_sync_debug_mode``) with the framework call site that issued it, counted per site.
 
-A synchronising call (``.item()``, a pageable H2D/D2H copy, ``nonzero``, ...) makes the host wait for the GPU
-to drain its queue; afterwards the GPU idles while the host issues the next kernels.  torch's sync debug mode
-reports every such call; this tool records the Python stack of each report during W+1 steps and prints the
-call sites of the last step, most frequent first.
+    python tools/sync_audit.py [--precision fp32|bf16] [--mode rl|sl] [--steps 2]
 
-    python tools/sync_audit.py [--precision fp32|bf16] [--mode rl|sl] [--warmup 3] [--depth 6]
+A sync in the middle of the step drains the launch queue: the GPU idles while the host catches up (the largest
+idle gaps of ``tools/prof_gaps.py``).  Run after warm-up, so one-off syncs (allocation, autotuning) are excluded.
 """
-from __future__ import annotations
-
 import argparse
 import collections
+import json
 import os
 import sys
 import traceback
@@ -25,61 +23,47 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--precision', choices=['fp32', 'bf16'], default='fp32')
     ap.add_argument('--mode', choices=['rl', 'sl'], default='rl')
+    ap.add_argument('--steps', type=int, default=2)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--depth', type=int, default=6)
-    ap.add_argument('--graph', action='store_true')
     args = ap.parse_args()
+    import bench
     from applestar_amd.rl.synthetic import rl_batch, sl_batch
-    from applestar_amd.runtime.prefetch import DevicePrefetcher
-    from applestar_amd.runtime.prefetch import pin_tree
+    from applestar_amd.runtime.prefetch import DevicePrefetcher, pin_tree
     device = torch.device('cuda', 0)
-    amp = 'bfloat16' if args.precision == 'bf16' else None
-    if args.mode == 'rl':
-        from applestar_amd.rl.trainer import RLTrainer
-        trainer = RLTrainer({'learner': {'use_value_feature': True, 'graph_step': args.graph, 'amp_dtype': amp},
-                             'model': {'enable_baselines': ['winloss']}}, device=device)
-        batches = [pin_tree(rl_batch(6, 64, seed=i)) for i in range(2)]
-    else:
-        from applestar_amd.sl.trainer import SLTrainer
-        trainer = SLTrainer({'learner': {'ignore_steps': 0, 'amp_dtype': amp,
-                                         'data': {'batch_size': 6, 'trajectory_length': 64}}}, device=device)
-        batches = [pin_tree(sl_batch(6, 64, seed=i)) for i in range(2)]
+    mk = rl_batch if args.mode == 'rl' else sl_batch
+    batches = [pin_tree(mk(6, 64, max_entities=512, seed=i)) for i in range(2)]
+    ns = argparse.Namespace(mode=args.mode, graph=False, batch=6, unroll=64)
+    trainer = bench._make_trainer(ns, args.precision, device, args.mode)
 
     def source():
         i = 0
         while True:
             yield batches[i % 2]
             i += 1
-
     it = DevicePrefetcher(source(), device)
     for _ in range(args.warmup):
         trainer.step(next(it))
     torch.cuda.synchronize()
-
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sites = collections.Counter()
-    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    examples = {}
 
-    def record(message, category, filename, lineno, file=None, line=None):
-        if 'synchroniz' not in str(message):
-            return
-        st = [f for f in traceback.extract_stack()[:-1] if 'warnings.py' not in f.filename]
-        own = [f for f in st if f.filename.startswith(here) and 'sync_audit' not in f.filename]
-        key = ' <- '.join(f'{os.path.relpath(f.filename, here)}:{f.lineno} {f.name}' for f in reversed(own[-args.depth:]))
-        sites[(str(message).split('\n')[0][:60], key)] += 1
-
-    old = warnings.showwarning
-    warnings.showwarning = record
+    def show(message, category, filename, lineno, file=None, line=None):
+        stack = [f for f in traceback.extract_stack()[:-1] if f.filename.startswith(root) and 'sync_audit' not in f.filename]
+        key = ' <- '.join(f'{os.path.relpath(f.filename, root)}:{f.lineno}' for f in reversed(stack[-4:]))
+        sites[key] += 1
+        examples.setdefault(key, str(message)[:120])
+    warnings.showwarning = show
     warnings.simplefilter('always')
     torch.cuda.set_sync_debug_mode('warn')
-    b = next(it)
-    trainer.step(b)
+    for _ in range(args.steps):
+        trainer.step(next(it))
     torch.cuda.set_sync_debug_mode('default')
-    warnings.showwarning = old
     torch.cuda.synchronize()
-    total = sum(sites.values())
-    print(f'{total} synchronising calls in one {args.mode} {args.precision} step')
-    for (msg, key), n in sites.most_common():
-        print(f'{n:5d}  {msg}\n       {key}')
+    print(json.dumps({'precision': args.precision, 'mode': args.mode, 'steps': args.steps,
+                      'syncs_per_step': sum(sites.values()) / args.steps}))
+    for k, n in sites.most_common():
+        print(f'{n / args.steps:6.1f}/step  {k}\n         {examples[k]}')
 
 
 if __name__ == '__main__':
