@@ -518,6 +518,14 @@ void launch(const bf16_t* x, const bf16_t* w, const float* bias, const bf16_t* r
                      bias, res, out, B, H, W, Cin, Cout, act);
 }
 
+bool small_m_bk128() {   // APPLESTAR_CONV_SMALLM_BK=64: the 64-wide K-steps (A/B)
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_CONV_SMALLM_BK");
+    return e == nullptr || std::atoi(e) != 64;
+  }();
+  return on;
+}
+
 }  // namespace
 
 bool conv3x3_supported(int Cin, int Cout) {  // (the host wrapper also bounds B*H*W*Cin*2 < 2^31)
@@ -540,8 +548,12 @@ void conv3x3_fwd(const void* x, const void* w, const float* bias, const void* re
   const long mt = (static_cast<long>(B) * H * W + 127) / 128;
   if (small_m && Cin % 32 == 0 && Cout % 32 == 0 && mt * ((Cout + 127) / 128) < 64) {
     // few output tiles (the actor's B = 1..16 forwards: a 19 x 20 map is 3 row tiles - 3 workgroups walking all of
-    // K for ~20 us): 32-wide output tiles give 4x the workgroups
-    if (k64) launch<32, 64>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    // K for ~20 us): 32-wide output tiles give 4x the workgroups.  Each K-step of these few workgroups waits out a
+    // whole memory latency, so 128-wide K-steps (Cin % 128) halve the dependent chain.  (A split-K form - fp32
+    // partials reduced by the last-arriving workgroup - measured slower, 22 vs 15 us: the device-scope release /
+    // acquire fences around the partials write back and invalidate the L2, profiles/r8v_timeline_b1_splitk_conv.txt)
+    if (Cin % 128 == 0 && small_m_bk128()) launch<32, 128>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
+    else if (k64) launch<32, 64>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
     else launch<32, 32>(xp, wp, bias, rp, op, B, H, W, Cin, Cout, act, s);
     return;
   }

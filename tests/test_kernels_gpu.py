@@ -458,6 +458,25 @@ def test_conv3x3_mfma_matches_fp32(cin, cout, H, W, act, res):
         assert _err(a, ref) < 3e-2 * max(1.0, ref.abs().max().item())
 
 
+@pytest.mark.parametrize('cin,cout,H,W', [(128, 128, 19, 20), (64, 128, 38, 40), (32, 32, 38, 40), (128, 64, 9, 9)])
+def test_conv3x3_few_tiles(cin, cout, H, W):
+    """The actor's B = 1 convs (few output tiles: 32-wide N tiles, 128-wide K-steps when Cin % 128 == 0) against
+    an fp32 conv with bias + residual + ReLU; repeated calls give identical outputs."""
+    from applestar_amd.ops import native
+    C = native.ensure_loaded()
+    torch.manual_seed(3)
+    x = torch.randn(1, H, W, cin, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(cout, 3, 3, cin, device=DEV) / (3 * cin ** 0.5)).to(torch.bfloat16)
+    b = 0.1 * torch.randn(cout, device=DEV)
+    r = torch.randn(1, H, W, cout, device=DEV).to(torch.bfloat16)
+    y = C.conv3x3_fwd(x, w, b, r, 1)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w.float().permute(0, 3, 1, 2), b, padding=1)
+    ref = torch.relu(ref.permute(0, 2, 3, 1) + r.float())
+    assert _err(y, ref) < 2e-2 * max(1.0, ref.abs().max().item())
+    for _ in range(3):
+        assert torch.equal(C.conv3x3_fwd(x, w, b, r, 1), y)
+
+
 @pytest.mark.parametrize('cin,cout,H,W', [(128, 128, 19, 20), (64, 128, 38, 40), (128, 64, 38, 40),
                                           (256, 128, 9, 9), (32, 32, 7, 5), (128, 128, 76, 80)])
 def test_conv3x3_drelu_epilogue(cin, cout, H, W):
