@@ -765,11 +765,29 @@ def _act_grad(dout, out, relu):
 def _wgrad(dy2d, x, cin, has_b, bf16_out, param=None):
     """(dW, db) of a dense GEMM (cin == 0, x [R, K]) or a 3x3 conv (x NHWC image, Cin = cin) in dy's precision.
     ``param``: the weight, when the caller lets the product be deferred (_Deferred: single-use weights only)."""
+    if _ABL_NO_WGRAD:
+        return _abl_zero_wgrad(dy2d, x, cin, has_b, bf16_out)
     if dy2d.dtype == torch.float32:
         if _Deferred.on and dy2d.is_cuda and param is not None and _single_use(param):
             return _Deferred.add(dy2d, x, cin, has_b, param)
         return _C.wgrad_f32(dy2d, x, cin, has_b)
     return _C.wgrad(dy2d, x, cin, has_b, bf16_out)
+
+
+# timing ablation only (tools/host_gpu_timeline.py): every weight gradient of the native kernels is a cached zero
+# tensor, no launch - the step without its weight-gradient work, i.e. how much of it the side streams hide
+_ABL_NO_WGRAD = os.environ.get('APPLESTAR_ABL_NO_WGRAD', '0') == '1'
+_ABL_ZEROS = {}
+
+
+def _abl_zero_wgrad(dy2d, x, cin, has_b, bf16_out):
+    N, K = dy2d.shape[1], (9 * cin if cin else x.shape[-1])
+    dt = dy2d.dtype if dy2d.dtype == torch.float32 or not bf16_out else torch.bfloat16
+    key = (N, K, dt, dy2d.device)
+    if key not in _ABL_ZEROS:
+        _ABL_ZEROS[key] = (torch.zeros(N, K, dtype=dt, device=dy2d.device), torch.zeros(N, dtype=dt, device=dy2d.device))
+    dw, db = _ABL_ZEROS[key]
+    return dw, (db if has_b else None)
 
 
 # ---------------------------------------------------------------------------- deferred weight gradients
