@@ -148,6 +148,47 @@ __device__ __forceinline__ void mm_nt_pre(const float* A, const WPre& r, float* 
   __syncthreads();
 }
 
+// the backward's form: weight only (no bias), staged [n][k] for dA = dY W
+template <int K, int N, typename WT>
+__device__ __forceinline__ void prefetch_w(const void* W, WPre& r) {
+  static_assert(N * K % 256 == 0 && N * K / 256 <= kPre, "prefetch shape");
+#pragma unroll
+  for (int j = 0; j < N * K / 256; ++j) r.w[j] = ldw<WT>(W, threadIdx.x + 256 * j);
+}
+// the first half of mm_nn on prefetched weights: stage them (row pitch K + 1) and wait; the caller may then issue the
+// next prefetch into r before calling mm_nn_compute
+template <int K, int N>
+__device__ __forceinline__ void mm_nn_stage(const WPre& r, float* wb) {
+#pragma unroll
+  for (int j = 0; j < N * K / 256; ++j) {
+    const int i = threadIdx.x + 256 * j, n = i / K, k = i - n * K;
+    wb[n * (K + 1) + k] = r.w[j];
+  }
+  __syncthreads();
+}
+template <int K, int N>
+__device__ __forceinline__ void mm_nn_compute(const float* dY, float* dA, const float* wb) {
+  constexpr int KP = K / 2;
+  for (int o = threadIdx.x; o < (L / 2) * KP; o += 256) {
+    const int t = 2 * (o / KP), k = 2 * (o % KP);
+    float a00 = 0.f, a01 = 0.f, a10 = 0.f, a11 = 0.f;
+#pragma unroll 8
+    for (int n = 0; n < N; ++n) {
+      const float y0 = dY[t * N + n], y1 = dY[(t + 1) * N + n];
+      const float w0 = wb[n * (K + 1) + k], w1 = wb[n * (K + 1) + k + 1];
+      a00 += y0 * w0;
+      a01 += y0 * w1;
+      a10 += y1 * w0;
+      a11 += y1 * w1;
+    }
+    dA[t * K + k] = a00;
+    dA[t * K + k + 1] = a01;
+    dA[(t + 1) * K + k] = a10;
+    dA[(t + 1) * K + k + 1] = a11;
+  }
+  __syncthreads();
+}
+
 // LayerNorm over 64 features with the affine parameters already in registers (lane = feature)
 __device__ __forceinline__ void layer_norm64_r(const float* X, float g, float bta, float* U, float* mu, float* rs) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -415,6 +456,8 @@ __global__ __launch_bounds__(256) void bo_bwd_kernel(const void* __restrict__ bo
   // `replicas` copies (reduced afterwards) so ~B / replicas workgroups, not all B, contend per address
   grad += (b % replicas) * static_cast<long>(kBoGradSize);
   for (int i = tid; i < L * D; i += 256) s.dX[i] = dmean[b * D + (i % D)] * (1.f / L);
+  WPre pf;                                   // the next mm_nn's weight, loaded one phase ahead (as the forward)
+  prefetch_w<HID, D, WT>(wts.w2[NL - 1], pf);
   __syncthreads();
   for (int l = NL - 1; l >= 0; --l) {
     const float* rec = save + (b * NL + l) * REC;
@@ -424,13 +467,17 @@ __global__ __launch_bounds__(256) void bo_bwd_kernel(const void* __restrict__ bo
     for (int i = tid; i < L * HID; i += 256) s.A[i] = rec[R_H1 + i];
     __syncthreads();
     mm_grad<HID, D>(s.dT, s.A, gl + G_W2, gl + G_B2);
-    mm_nn<HID, D, WT>(s.dT, wts.w2[l], s.dH, s.wb);
+    mm_nn_stage<HID, D>(pf, s.wb);
+    prefetch_w<D, HID, WT>(wts.w1[l], pf);
+    mm_nn_compute<HID, D>(s.dT, s.dH, s.wb);
     for (int i = tid; i < L * HID; i += 256) s.dH[i] = s.A[i] > 0.f ? s.dH[i] : 0.f;         // dH1 (pre-act)
     __syncthreads();
     for (int i = tid; i < L * D; i += 256) s.A[i] = rec[R_U2 + i];
     __syncthreads();
     mm_grad<D, HID>(s.dH, s.A, gl + G_W1, gl + G_B1);
-    mm_nn<D, HID, WT>(s.dH, wts.w1[l], s.dT, s.wb);                                           // dU2
+    mm_nn_stage<D, HID>(pf, s.wb);
+    prefetch_w<16, D, WT>(wts.wp[l], pf);
+    mm_nn_compute<D, HID>(s.dH, s.dT, s.wb);                                                   // dU2
     layer_norm64_bwd(rec + R_XMID, rec + R_MU2, rec + R_RS2, wts.ln2w[l], s.dT, s.dX, gl + G_LN2W, gl + G_LN2B);
     // ---- attention branch: xmid = xin + (softmax(q k^T / sqrt 8) v) Wp^T + bp
     for (int i = tid; i < L * 16; i += 256) s.A[i] = rec[R_O + i];
@@ -438,7 +485,9 @@ __global__ __launch_bounds__(256) void bo_bwd_kernel(const void* __restrict__ bo
     for (int i = tid; i < NH * L * L; i += 256) s.P[i] = rec[R_P + i];
     __syncthreads();
     mm_grad<16, D>(s.dX, s.A, gl + G_WP, gl + G_BP);
-    mm_nn<16, D, WT>(s.dX, wts.wp[l], s.dO, s.wb);
+    mm_nn_stage<16, D>(pf, s.wb);
+    prefetch_w<D, QD, WT>(wts.wqkv[l], pf);
+    mm_nn_compute<16, D>(s.dX, s.dO, s.wb);
     for (int i = tid; i < NH * L * L; i += 256) {          // dP[h][t][u] = dO[t][h] . V[u][h]
       const int h = i / (L * L), t = (i / L) % L, u = i % L;
       float acc = 0.f;
@@ -474,7 +523,9 @@ __global__ __launch_bounds__(256) void bo_bwd_kernel(const void* __restrict__ bo
     for (int i = tid; i < L * D; i += 256) s.A[i] = rec[R_U1 + i];
     __syncthreads();
     mm_grad<D, QD>(s.dQKV, s.A, gl + G_WQKV, gl + G_BQKV);
-    mm_nn<D, QD, WT>(s.dQKV, wts.wqkv[l], s.dT, s.wb);                                        // dU1
+    mm_nn_stage<D, QD>(pf, s.wb);
+    if (l > 0) prefetch_w<HID, D, WT>(wts.w2[l - 1], pf);
+    mm_nn_compute<D, QD>(s.dQKV, s.dT, s.wb);                                                  // dU1
     layer_norm64_bwd(rec + R_XIN, rec + R_MU1, rec + R_RS1, wts.ln1w[l], s.dT, s.dX, gl + G_LN1W, gl + G_LN1B);
   }
   // ---- embedding: x0 = relu(pre); pre = b0 + sum of the selected W0 columns
