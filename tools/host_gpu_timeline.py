@@ -50,9 +50,12 @@ def main():
             mark(name + '<')
             return r
         setattr(obj, attr, g)
-    for n, m in tr.model.named_children():
+    for n, m in tr.model.named_modules():
+        if not n or n.count('.') > 1 or (n.count('.') == 1 and not n.startswith('policy.')):
+            continue        # the model's children and the policy heads
         m.register_forward_pre_hook(lambda mod, inp, n=n: mark('fwd:' + n + '>'))
         m.register_forward_hook(lambda mod, inp, out, n=n: mark('fwd:' + n + '<'))
+    wrap(tr.model.policy.selected_units_head, 'forward_teacher', 'fwd:policy.selected_units_head.teacher')
     wrap(tr.loss, 'compute_loss', 'loss')
     wrap(tr, 'backward', 'backward')
     wrap(tr, '_reduce', 'reduce')
