@@ -900,14 +900,19 @@ def defer_verify(params, grads) -> None:
                                f'weight {tuple(p.shape)}): run with APPLESTAR_DEFER_WGRAD=0 or APPLESTAR_DEFER_CHECK=1')
 
 
-def defer_begin(device, loss=None) -> None:
+def defer_begin(device, loss=None, owner=None) -> None:
     """Start queueing fp32 weight gradients (see :class:`_Deferred`).  ``loss``: the root of the backward about to
-    run; only parameters with one consumer in its graph may be deferred (without it nothing is)."""
+    run; only parameters with one consumer in its graph may be deferred (without it nothing is).  ``owner``: the
+    object whose steps these are (the trainer): the graph is walked on ITS first step and every DEFER_REWALK-th
+    after, so a second trainer in the process (new parameters) is walked on its own first step."""
     if DEFER_WGRAD and torch.device(device).type == 'cuda' and not torch.cuda.is_current_stream_capturing():
-        if loss is not None and _Deferred.steps % DEFER_REWALK == 0:
+        steps = getattr(owner, '_defer_steps', 0) if owner is not None else _Deferred.steps
+        if loss is not None and steps % DEFER_REWALK == 0:
             for t, c in _consumer_counts(loss).values():
                 t._as_one_consumer = c == 1
             _Deferred.walks += 1
+        if owner is not None:
+            owner._defer_steps = steps + 1
         _Deferred.steps += 1
         _Deferred.issued = []
         _Deferred.on = True

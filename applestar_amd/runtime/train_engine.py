@@ -165,7 +165,7 @@ class TrainEngine:
         phased = bool(boundary)
         defer = self.device.type == 'cuda' and self.master is None     # fp32: heads' dW beside the LSTM backward
         if defer:
-            native.defer_begin(self.device, loss)
+            native.defer_begin(self.device, loss, owner=self)
         try:
             join = (lambda: native.defer_end(self.device)) if defer else None
             if self.master is not None:

@@ -388,7 +388,10 @@ def _count_native(monkeypatch, names):
         f = getattr(C, n)
 
         def wrap(*a, _f=f, _n=n):
-            calls[_n].append((a[3] is not None if _n == 'gemm_f32' else None, a[4] if _n == 'gemm_f32' else None,
+            # (residual given, epilogue act, rows): gemm_f32(a, b, bias, res, act), gemm_f32_psb(a, planes, N, K,
+            # bias, res, act, variant)
+            ri, ai = {'gemm_f32': (3, 4), 'gemm_f32_psb': (5, 6)}.get(_n, (None, None))
+            calls[_n].append((a[ri] is not None if ri is not None else None, a[ai] if ai is not None else None,
                               int(a[0].shape[0]) if torch.is_tensor(a[0]) else None))
             return _f(*a)
         monkeypatch.setattr(C, n, wrap)
@@ -404,14 +407,14 @@ def test_fp32_benchmark_composition_matches_cpu(monkeypatch):
     batch = rl_batch(2, 16, max_entities=300, seed=11)
     assert int(batch['entity_num'].max()) > 128
     cpu, ref_out, ref_info, ref_grads = _cpu_reference(batch)
-    calls = _count_native(monkeypatch, ['gemm_f32', 'varlen_attn_fwd_f32', 'varlen_attn_bwd_f32'])
+    calls = _count_native(monkeypatch, ['gemm_f32', 'gemm_f32_psb', 'varlen_attn_fwd_f32', 'varlen_attn_bwd_f32'])
     tr = RLTrainer({**CFG, 'learner': {**CFG['learner'], 'amp_dtype': None}}, device='cuda')
     tr.model.load_state_dict(cpu.state_dict())
     out = tr.model.rl_learner_forward(**to_device(copy.deepcopy(batch), 'cuda'))
     info = tr.loss.compute_loss(out)
     info['total_loss'].backward()
     torch.cuda.synchronize()
-    g = calls['gemm_f32']
+    g = calls['gemm_f32'] + calls['gemm_f32_psb']                  # the split ring or the pre-split-plane kernel
     assert len(g) >= 12, len(g)                                    # transformer linears fwd + dX on the f32 GEMM
     assert any(e[1] == 4 for e in g), 'no ReLU-mask (ACT_DRELU) dX epilogue'
     assert any(e[0] and e[1] == 0 for e in g), 'no residual (GradLink) dX epilogue'
