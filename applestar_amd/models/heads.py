@@ -263,7 +263,10 @@ class SelectedUnitsHead(nn.Module):
         key, _ = self.keys(entity_embedding, entity_num)
         B, N1, _ = key.shape
         q1 = self.query_fc1[0]
-        c0 = F.linear(ae0.float(), q1.weight.float(), q1.bias.float())
+        # fp32 like the sampler's other inputs, on the few-row native GEMM outside autocast (under autocast
+        # F.linear re-cast the 256 x 1024 weight to bf16 in every replayed graph: 4 extra launches)
+        with torch.autocast('cuda', enabled=False):
+            c0 = native.linear_f32_rows(ae0.float(), q1.weight, q1.bias)
         if u is None:
             u = torch.rand(B, MAX_SELECTED_UNITS_NUM, device=key.device)
         wf, bf = self._folded_query()

@@ -511,6 +511,16 @@ def varlen_attention(qkv, cu_seqlens, max_len: int, num_heads: int, head_dim: in
     return _VarlenAttention.apply(qkv.contiguous(), cu, int(max_len), int(num_heads))
 
 
+def linear_f32_rows(x, w, b=None):
+    """fp32 x W^T + b without autograd (inference): the native f32 GEMM when it takes the shape (few rows: one wave
+    per 32 x 32 tile), else torch.addmm; the weight / bias read as fp32 derived forms."""
+    C = ensure_loaded()
+    R, K = x.shape
+    if x.is_cuda and _gemm_f32_ok(R, w.shape[0], K):
+        return C.gemm_f32(x.contiguous(), _w32(w), None if b is None else _w32(b), None, 0)
+    return torch.addmm(b.float(), x, w.float().t()) if b is not None else x @ w.float().t()
+
+
 def su_sample(key, c0, u, entity_num, su_mask, wf_bf16, bf, wq2, bq2, cell, we1, be1, temperature: float,
               max_steps: int, extra_units: bool):
     """Persistent selected-units sampler (inference only; see csrc/kernels/pointer.hip)."""
