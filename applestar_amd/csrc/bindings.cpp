@@ -2111,9 +2111,10 @@ void multi_copy(const std::vector<at::Tensor>& dsts, const std::vector<at::Tenso
     const at::Tensor& s = srcs[i];
     TORCH_CHECK(d.is_cuda() && s.is_cuda() && d.sizes() == s.sizes(), "multi_copy: GPU tensors of equal shape");
     const bool same = d.scalar_type() == s.scalar_type();
+    const auto st = s.scalar_type();
     const bool ok = d.strides() == s.strides() && d.is_non_overlapping_and_dense() &&
                     (same || ((d.scalar_type() == at::kFloat || d.scalar_type() == at::kBFloat16) &&
-                              (s.scalar_type() == at::kFloat || s.scalar_type() == at::kBFloat16)));
+                              (st == at::kFloat || st == at::kBFloat16 || st == at::kByte || st == at::kShort)));
     if (!ok) {
       at::Tensor dd = d;
       dd.copy_(s);
@@ -2132,7 +2133,8 @@ void multi_copy(const std::vector<at::Tensor>& dsts, const std::vector<at::Tenso
       a.chunk_start[t + 1] = a.chunk_start[t] + static_cast<int>((a.n[t] + as::kCopyRawChunk - 1) / as::kCopyRawChunk);
     } else {
       a.n[t] = n;
-      a.dts[t] = static_cast<unsigned char>((s.scalar_type() == at::kFloat ? 1 : 0) | (d.scalar_type() == at::kFloat ? 2 : 0));
+      a.dts[t] = static_cast<unsigned char>((st == at::kFloat ? 1 : 0) | (d.scalar_type() == at::kFloat ? 2 : 0) |
+                                            (st == at::kByte ? 8 : 0) | (st == at::kShort ? 16 : 0));
       a.chunk_start[t + 1] = a.chunk_start[t] + static_cast<int>((n + as::kCopyChunk - 1) / as::kCopyChunk);
     }
     if (a.ntensors == as::kCopyMaxT) flush();

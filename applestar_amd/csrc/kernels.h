@@ -310,7 +310,8 @@ struct CopyArgs {                     // passed by value (< 2 KB of kernel argum
   const void* src[kCopyMaxT];
   void* dst[kCopyMaxT];
   long n[kCopyMaxT];                  // elements (raw: bytes)
-  unsigned char dts[kCopyMaxT];       // bit 0: src fp32, bit 1: dst fp32 (else bf16), bit 2: raw bytes, same dtype
+  unsigned char dts[kCopyMaxT];       // bit 0: src fp32, bit 1: dst fp32 (else bf16), bit 2: raw bytes, same dtype,
+                                      // bit 3 / 4: src uint8 / int16 (converting copies)
 };
 void multi_copy(const CopyArgs& a, hipStream_t s);
 

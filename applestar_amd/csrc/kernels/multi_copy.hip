@@ -10,6 +10,13 @@
 namespace as {
 namespace {
 
+// element i of a converting copy's source: fp32, bf16, or an integer feature column (uint8 / int16, exact in fp32)
+__device__ __forceinline__ float copy_src(const void* src, long i, unsigned char dts) {
+  if (dts & 8) return static_cast<float>(static_cast<const unsigned char*>(src)[i]);
+  if (dts & 16) return static_cast<float>(static_cast<const short*>(src)[i]);
+  return (dts & 1) ? static_cast<const float*>(src)[i] : bf2f(static_cast<const bf16_t*>(src)[i]);
+}
+
 __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyArgs a) {
   const int b = blockIdx.x;
   int t = 0;
@@ -43,16 +50,14 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyArgs a) {
   }
   const long i0 = static_cast<long>(b - a.chunk_start[t]) * kCopyChunk;
   const long i1 = i0 + kCopyChunk < a.n[t] ? i0 + kCopyChunk : a.n[t];
-  const bool sf = (a.dts[t] & 1) != 0, df = (a.dts[t] & 2) != 0;
+  const bool df = (a.dts[t] & 2) != 0;
+  const unsigned char dts = a.dts[t];
   if (i1 - i0 == kCopyChunk) {
     // a full chunk: the thread's 32 elements loaded before any is stored (see the raw path)
     constexpr int U = static_cast<int>(kCopyChunk / 256);
     float v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long i = i0 + threadIdx.x + 256 * u;
-      v[u] = sf ? static_cast<const float*>(src)[i] : bf2f(static_cast<const bf16_t*>(src)[i]);
-    }
+    for (int u = 0; u < U; ++u) v[u] = copy_src(src, i0 + threadIdx.x + 256 * u, dts);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const long i = i0 + threadIdx.x + 256 * u;
@@ -62,7 +67,7 @@ __global__ __launch_bounds__(256) void multi_copy_kernel(const CopyArgs a) {
     return;
   }
   for (long i = i0 + threadIdx.x; i < i1; i += 256) {
-    const float v = sf ? static_cast<const float*>(src)[i] : bf2f(static_cast<const bf16_t*>(src)[i]);
+    const float v = copy_src(src, i, dts);
     if (df) static_cast<float*>(dst)[i] = v;
     else static_cast<bf16_t*>(dst)[i] = f2bf(v);
   }

@@ -162,6 +162,9 @@ class ScalarEncoder(nn.Module):
             self.position_array.is_cuda
         if lowp_inf:
             from ..ops import native
+        # the integer feature columns of the fc modules cast to the compute dtype in ONE multi-tensor launch (was a
+        # cast launch per module: 6-7 per forward, in the actor's graph and in the learner step alike)
+        pre = _cast_int_features(x, [name for name, kind, *_ in SCALAR_MODULES if kind not in ('emb', 'bo')])
         for name, kind, n_in, n_out, is_ctx, is_base in SCALAR_MODULES:
             m = self.encode_modules[name]
             if kind == 'emb':
@@ -173,6 +176,8 @@ class ScalarEncoder(nn.Module):
                 e = m(x['beginning_order'], x['bo_location'])
                 if lowp_inf:
                     e = e.to(torch.bfloat16)
+            elif name in pre:
+                e = m(pre[name])
             else:
                 v = x[name]
                 # integer feature columns: straight to the bf16 compute dtype under autocast (one cast; via fp32 it was
@@ -194,6 +199,23 @@ class ScalarEncoder(nn.Module):
             if out is not None:
                 return out
         return torch.cat(embedded, 1), torch.cat(context, 1), torch.cat(baseline, 1)
+
+
+def _cast_int_features(x: Dict[str, torch.Tensor], names) -> Dict[str, torch.Tensor]:
+    """{name: x[name] in the compute dtype} for the integer (uint8 / int16) GPU feature columns among ``names``:
+    bf16 under autocast, else fp32 (both exact for these ranges), all in one native multi-tensor copy; {} off the
+    GPU or without the extension (the per-module casts stay)."""
+    names = [n for n in names if n in x and x[n].is_cuda and x[n].dtype in (torch.uint8, torch.int16)
+             and x[n].is_contiguous()]
+    if len(names) < 2:
+        return {}
+    n = ops._native(x[names[0]])
+    if n is None:
+        return {}
+    dt = torch.bfloat16 if torch.is_autocast_enabled() else torch.float32
+    dst = [torch.empty(x[k].shape, dtype=dt, device=x[k].device) for k in names]
+    n.ensure_loaded().multi_copy(dst, [x[k] for k in names])
+    return dict(zip(names, dst))
 
 
 def entity_field_layout() -> List[Tuple[str, str, int, int]]:

@@ -738,6 +738,23 @@ def test_copy_into_strided_sources_without_copy_launches():
         assert torch.equal(d, s.float())
 
 
+def test_multi_copy_integer_sources_convert_exactly():
+    """uint8 / int16 feature columns -> bf16 / fp32 in one launch (the scalar encoder's casts), values exact;
+    int32 falls back to copy_."""
+    from applestar_amd.ops import native
+    C = native.ensure_loaded()
+    torch.manual_seed(19)
+    srcs = [torch.randint(0, 256, (1, 260), device=DEV, dtype=torch.uint8),
+            torch.randint(-300, 300, (390, 90), device=DEV, dtype=torch.int16),
+            torch.randint(0, 256, (9000,), device=DEV, dtype=torch.uint8),
+            torch.randint(-200, 200, (17, 5), device=DEV, dtype=torch.int32)]
+    for dt in (torch.bfloat16, torch.float32):
+        dsts = [torch.empty(s.shape, device=DEV, dtype=dt) for s in srcs]
+        C.multi_copy(dsts, srcs)
+        for d, s in zip(dsts, srcs):
+            assert torch.equal(d, s.to(dt)), (dt, s.dtype)
+
+
 def test_multi_copy_raw_bytes_any_dtype():
     """Equal-dtype pairs travel as raw bytes (the graph step's batch refresh): int64 / int32 / bool / uint8 /
     fp16 / fp32 leaves, odd byte counts and views at unaligned offsets (byte path), > 64 MB leaves (many
