@@ -336,6 +336,16 @@ long wgrad_target_wg() {
   return v;
 }
 
+// few-row products (R < 2048): at least this many rows per slice (APPLESTAR_WGRAD_SMALL_R_BF16; 0 = one slice).
+// Unlike the fp32 kernels (wgrad_f32.hip) the bf16 step did not move with 96 (26.95 / 27.10 vs 27.00 / 26.98 ms): off
+long wgrad_small_r_rows() {
+  static const long v = [] {
+    const char* e = std::getenv("APPLESTAR_WGRAD_SMALL_R_BF16");
+    return e ? std::atol(e) : 0L;
+  }();
+  return v;
+}
+
 int wgrad_splits(long R, int N, int K) {
   const int BN = pick_bn(N), BK = pick_bk(K);
   const long tiles = static_cast<long>((N + BN - 1) / BN) * ((K + BK - 1) / BK);
@@ -343,7 +353,8 @@ int wgrad_splits(long R, int N, int K) {
   long S = (target + tiles - 1) / tiles;               // ~target workgroups: 2 resident per CU
   // at least 256 rows (4 stages) per slice; short reductions (R < 2048, e.g. the 390-row policy / value
   // MLP gradients) take one slice so no partial-sum pass is launched at all
-  const long max_s = R < 2048 ? 1 : (R + 255) / 256;
+  const long small = wgrad_small_r_rows();
+  const long max_s = R < 2048 ? (small > 0 && R >= 2 * small ? R / small : 1) : (R + 255) / 256;
   if (S > max_s) S = max_s;
   const long max_part = (8L << 20) / (static_cast<long>(N) * K);  // partials <= 32 MB (their sum is a pass)
   if (S > max_part) S = max_part;

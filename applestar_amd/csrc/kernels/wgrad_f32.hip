@@ -435,19 +435,35 @@ __global__ __launch_bounds__(256, ((BN == 128 && BK >= 128) || BN == 32) ? 2 : 3
 //            (thread t: column t % 128, rows 8 (t / 128) .. + 7, of dY and of X) beside MFMA(kt) on P(kt)
 // so the split of the next step and the products of this one share a barrier interval.  80 KB of LDS: 2
 // workgroups per CU.  db: each thread's dY column sums, the two row halves combined through LDS at the end.
-template <bool CONV>
-__global__ __launch_bounds__(256, 2) void wgrad_f32_stg_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+// Narrow N tiles (BN = 32 / 64: the 76x80 / 19x20 convs with 32 / 64 output channels, round 6): the same stages
+// with the four waves along K (each wave 32 (BN = 32) or 64 x 32 of the tile), the dY stage DMA'd by the first
+// A_N waves, and dY split by the first 2 BN threads; 50 / 60 KB of LDS (3 / 2 workgroups per CU).
+template <int BN>
+struct StgCfg {
+  static constexpr int BK = 128, RS = 16;
+  static constexpr int WN = BN == 128 ? 2 : 1, WK = 4 / WN;
+  static constexpr int FN = BN / (32 * WN), FK = BK / (32 * WK);   // 32 x 32 blocks per wave along N / K
+  static constexpr int A_BYTES = RS * BN * 4, B_BYTES = RS * BK * 4, FST = A_BYTES + B_BYTES;
+  static constexpr int A_N = A_BYTES / 1024, B_N = B_BYTES / 1024;  // 1 KB DMA wave-instructions per stage
+  static constexpr int A_PW = (A_N + 3) / 4, B_PW = B_N / 4;
+  static constexpr int A_CPR = BN / 4, B_CPR = BK / 4, A_RPI = 64 / A_CPR, B_RPI = 64 / B_CPR;
+  static constexpr int PLA = (BN / 32) * 2 * 32 * 16, PLB = (BK / 32) * 2 * 32 * 16;   // one plane of dY / X
+  static constexpr int PST = 3 * (PLA + PLB);
+  static constexpr int OCC = BN == 32 ? 3 : 2;
+  static_assert(B_N % 4 == 0 && (A_N % 4 == 0 || A_N < 4), "stage DMA split");
+};
+
+template <int BN, bool CONV>
+__global__ __launch_bounds__(256, StgCfg<BN>::OCC) void wgrad_f32_stg_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                               float* __restrict__ dw_part, float* __restrict__ db_part,
                                                               long part_stride, long R, int N, int K, int H, int W,
                                                               int Cin, long rows_per_split, int tiles_n, int tiles_k) {
-  constexpr int BN = 128, BK = 128, RS = 16;
-  constexpr int A_BYTES = RS * BN * 4, B_BYTES = RS * BK * 4, FST = A_BYTES + B_BYTES;     // 16 KB fp32 stage
-  constexpr int A_PW = A_BYTES / 4096, B_PW = B_BYTES / 4096;                          // 2 + 2 DMA per wave
-  constexpr int A_CPR = BN / 4, B_CPR = BK / 4, A_RPI = 64 / A_CPR, B_RPI = 64 / B_CPR;
-  constexpr int PL = 4 * 2 * 32 * 16;          // one plane of one operand: 4 blocks x 2 halves x 32 lanes x 16 B
-  constexpr int PST = 2 * 3 * PL;               // planes of a stage (dY then X): 24 KB
+  using C = StgCfg<BN>;
+  constexpr int BK = C::BK, RS = C::RS, A_BYTES = C::A_BYTES, FST = C::FST, A_PW = C::A_PW, B_PW = C::B_PW;
+  constexpr int A_CPR = C::A_CPR, B_CPR = C::B_CPR, A_RPI = C::A_RPI, B_RPI = C::B_RPI;
+  constexpr int PLA = C::PLA, PLB = C::PLB, PST = C::PST, FN = C::FN, FK = C::FK;
   __shared__ __attribute__((aligned(16))) char F[2 * FST];
-  __shared__ __attribute__((aligned(16))) char P[2 * PST];      // 80 KB in all: 2 workgroups per CU
+  __shared__ __attribute__((aligned(16))) char P[2 * PST];
 
   const int wg = pipe::xcd_remap();
   const int tk = wg % tiles_k;
@@ -457,10 +473,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32_stg_kernel(const float* __re
   const long r_begin = static_cast<long>(s) * rows_per_split;
   const long r_end = r_begin + rows_per_split < R ? r_begin + rows_per_split : R;
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wn = wid >> 1, wk = wid & 1;
+  const int wn = wid / C::WK, wk = wid % C::WK;
   const int l32 = lane & 31, h = lane >> 5;
   const long HW = static_cast<long>(H) * W;
   const pipe::i32x4 yr = pipe::rsrc(dy, R * N * 4), xr = pipe::rsrc(x, CONV ? R * Cin * 4 : R * K * 4);
+  // waves past the dY stage's A_N DMA instructions (BN = 32) issue only their X pieces
+  const bool a_wave = A_PW * 4 == C::A_N || wid < C::A_N;
 
   // DMA pieces (the ring kernel's): fixed column per lane, row (within a step) per chunk
   const int a_col = n0 + 4 * (lane % A_CPR), b_col = k0 + 4 * (lane % B_CPR);
@@ -491,11 +509,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32_stg_kernel(const float* __re
   auto issue = [&](long kt) {
     char* st = F + (kt & 1) * FST;
     const long r0 = r_begin + kt * RS;
+    if (a_wave) {
 #pragma unroll
-    for (int c = 0; c < A_PW; ++c) {
-      const long r = r0 + a_row[c];
-      pipe::dma16(yr, st + (wid + 4 * c) * 1024,
-                  (kt < nsteps && a_ok && r < r_end) ? (static_cast<int>(r) * N + a_col) * 4 : pipe::kOOB);
+      for (int c = 0; c < A_PW; ++c) {
+        const long r = r0 + a_row[c];
+        pipe::dma16(yr, st + (wid + 4 * c) * 1024,
+                    (kt < nsteps && a_ok && r < r_end) ? (static_cast<int>(r) * N + a_col) * 4 : pipe::kOOB);
+      }
     }
 #pragma unroll
     for (int c = 0; c < B_PW; ++c) {
@@ -516,46 +536,53 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32_stg_kernel(const float* __re
     }
   };
 
-  // split work of this thread: column sc of dY and of X, rows 8 sh .. 8 sh + 7 of the stage
-  const int sc = tid & (BN - 1), sh = tid >> 7;
+  // split work of this thread: column sc of X, rows 8 sh .. 8 sh + 7 of the stage; column ac of dY (rows 8 ah ..)
+  // for the first 2 BN threads
+  const int sc = tid & (BK - 1), sh = tid >> 7;
+  const int ac = tid & (BN - 1), ah = tid / BN;
+  const bool a_split = tid < 2 * BN;
   const bool do_bias = db_part != nullptr && tk == 0;
   float bsum = 0.f;
   auto split_stage = [&](long j) {
     const float* fa = reinterpret_cast<const float*>(F + (j & 1) * FST);
     const float* fb = fa + RS * BN;
     char* pa = P + (j & 1) * PST;
-    char* pb = pa + 3 * PL;
-    float va[8], vb[8];
+    char* pb = pa + 3 * PLA;
+    float vb[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      va[q] = fa[(8 * sh + q) * BN + sc];
-      vb[q] = fb[(8 * sh + q) * BK + sc];
-    }
-    const Split3 sa = split8(va), sb = split8(vb);
-    const int slot = (((sc >> 5) * 2 + sh) * 32 + (sc & 31)) * 16;
+    for (int q = 0; q < 8; ++q) vb[q] = fb[(8 * sh + q) * BK + sc];
+    const Split3 sb = split8(vb);
+    const int bslot = (((sc >> 5) * 2 + sh) * 32 + (sc & 31)) * 16;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      *reinterpret_cast<u32v4*>(pa + p * PL + slot) = sa.p[p];
-      *reinterpret_cast<u32v4*>(pb + p * PL + slot) = sb.p[p];
-    }
-    if (do_bias) {
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<u32v4*>(pb + p * PLB + bslot) = sb.p[p];
+    if (a_split) {
+      float va[8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) bsum += va[q];
+      for (int q = 0; q < 8; ++q) va[q] = fa[(8 * ah + q) * BN + ac];
+      const Split3 sa = split8(va);
+      const int aslot = (((ac >> 5) * 2 + ah) * 32 + (ac & 31)) * 16;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<u32v4*>(pa + p * PLA + aslot) = sa.p[p];
+      if (do_bias) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) bsum += va[q];
+      }
     }
   };
 
-  f16v acc[2][2];
+  f16v acc[FN][FK];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FK; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
   if (nsteps > 0) {
     issue(0);
     issue(1);
-    pipe::wait_vm<A_PW + B_PW>();          // this wave's pieces of step 0
+    if (a_wave) pipe::wait_vm<A_PW + B_PW>();          // this wave's pieces of step 0
+    else pipe::wait_vm<B_PW>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     split_stage(0);
@@ -569,43 +596,45 @@ __global__ __launch_bounds__(256, 2) void wgrad_f32_stg_kernel(const float* __re
     issue(kt + 2);
     if (kt + 1 < nsteps) split_stage(kt + 1);
     const char* pa = P + (kt & 1) * PST;
-    const char* pb = pa + 3 * PL;
-    Split3 fa[2], fb[2];
+    const char* pb = pa + 3 * PLA;
+    Split3 fa[FN], fb[FK];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FN; ++i)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
-        const int off = p * PL + (((wn * 2 + i) * 2 + h) * 32 + l32) * 16;
-        fa[i].p[p] = *reinterpret_cast<const u32v4*>(pa + off);
-        fb[i].p[p] = *reinterpret_cast<const u32v4*>(pb + p * PL + (((wk * 2 + i) * 2 + h) * 32 + l32) * 16);
-      }
+      for (int p = 0; p < 3; ++p)
+        fa[i].p[p] = *reinterpret_cast<const u32v4*>(pa + p * PLA + (((wn * FN + i) * 2 + h) * 32 + l32) * 16);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < FK; ++j)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma_x6(fa[i], fb[j], acc[i][j]);
+      for (int p = 0; p < 3; ++p)
+        fb[j].p[p] = *reinterpret_cast<const u32v4*>(pb + p * PLB + (((wk * FK + j) * 2 + h) * 32 + l32) * 16);
+#pragma unroll
+    for (int i = 0; i < FN; ++i)
+#pragma unroll
+      for (int j = 0; j < FK; ++j) acc[i][j] = mfma_x6(fa[i], fb[j], acc[i][j]);
   }
   pipe::wait_vm<0>();
 
-  // accumulator (i, j) register e: n = n0 + wn 64 + 32 i + (e&3) + 8 (e>>2) + 4 h, k = k0 + wk 64 + 32 j + l32
+  // accumulator (i, j) register e: n = n0 + wn 32 FN + 32 i + (e&3) + 8 (e>>2) + 4 h, k = k0 + wk 32 FK + 32 j + l32
   float* outp = dw_part + static_cast<long>(s) * part_stride;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FN; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int k = k0 + wk * 64 + 32 * j + l32;
+    for (int j = 0; j < FK; ++j) {
+      const int k = k0 + wk * 32 * FK + 32 * j + l32;
       if (k >= K) continue;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int n = n0 + wn * 64 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int n = n0 + wn * 32 * FN + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (n < N) outp[static_cast<long>(n) * K + k] = acc[i][j][e];
       }
     }
   if (do_bias) {
     float* bred = reinterpret_cast<float*>(F);      // the ring is idle: every DMA landed (wait_vm<0> above)
     __syncthreads();
-    if (sh == 1) bred[sc] = bsum;
+    if (a_split && ah == 1) bred[ac] = bsum;
     __syncthreads();
-    if (sh == 0 && n0 + sc < N) db_part[static_cast<long>(s) * part_stride + n0 + sc] = bsum + bred[sc];
+    if (a_split && ah == 0 && n0 + ac < N) db_part[static_cast<long>(s) * part_stride + n0 + ac] = bsum + bred[ac];
   }
 }
 
@@ -629,15 +658,26 @@ bool wgrad_stg() {
   return on;
 }
 
+// APPLESTAR_WGRAD_STG_NARROW=1: the 32 / 64-wide N tiles on split-once staging too.  Measured slower than the
+// per-wave-split kernels on every narrow learner shape (76x80 64 -> 32: 1266 vs 1142 us, 32 -> 64: 1142 vs 959 us;
+// fp32 step 55.25 / 55.35 vs 54.79 / 54.74 ms; profiles/r10b_wgrad32_stg_narrow_{on,off}.jsonl): off
+bool wgrad_stg_narrow() {
+  static const bool on = [] {
+    const char* e = std::getenv("APPLESTAR_WGRAD_STG_NARROW");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 template <int BN, int BK, bool CONV>
 void launch(const float* dy, const float* x, float* dwp, float* dbp, long ps, long R, int N, int K, int H, int W,
             int Cin, int S, long rps, hipStream_t st) {
   const int tn = (N + BN - 1) / BN, tk = (K + BK - 1) / BK;
   const long nwg = static_cast<long>(tn) * tk * S;
-  if constexpr (BN == 128 && BK == 128) {
-    if (f32_mfma_mode() == 1 && wgrad_stg()) {
-      hipLaunchKernelGGL((wgrad_f32_stg_kernel<CONV>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x, dwp,
-                         dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
+  if constexpr (BK == 128) {
+    if (f32_mfma_mode() == 1 && wgrad_stg() && (BN == 128 || wgrad_stg_narrow())) {
+      hipLaunchKernelGGL((wgrad_f32_stg_kernel<BN, CONV>), dim3(static_cast<unsigned>(nwg)), dim3(256), 0, st, dy, x,
+                         dwp, dbp, ps, R, N, K, H, W, Cin, rps, tn, tk);
       return;
     }
   }
@@ -695,12 +735,26 @@ long wgrad_f32_target_wg() {
   return v;
 }
 
+// few-row products (R < 2048: the heads' / critics' MLPs at R = 384 / 390 - 33 weight gradients per fp32 step, each
+// ~4 workgroups walking all R rows in ~32 us): slices of at least this many rows plus one column reduction
+// (APPLESTAR_WGRAD_SMALL_R; 0 = one slice).  fp32 step 54.50 / 54.30 ms (0) -> 53.96 / 53.89 (48), 54.08 / 54.03
+// (96), 54.21 / 54.31 (192) on one box (profiles/r10c_bench_small_r.txt)
+long wgrad_f32_small_r_rows() {
+  static const long v = [] {
+    const char* e = std::getenv("APPLESTAR_WGRAD_SMALL_R");
+    return e ? std::atol(e) : 48L;
+  }();
+  return v;
+}
+
 int wgrad_f32_splits(long R, int N, int K) {
   const int bn = pick(N), bk = pick_k(K, bn);
   const long tiles = static_cast<long>((N + bn - 1) / bn) * ((K + bk - 1) / bk);
   const long target = wgrad_f32_target_wg();
   long S = (target + tiles - 1) / tiles;                 // ~target workgroups
-  const long max_s = R < 2048 ? 1 : (R + 127) / 128;     // >= 4 stages per slice
+  const long small = wgrad_f32_small_r_rows();
+  const long max_s = R < 2048 ? (small > 0 && R >= 2 * small ? R / small : 1)
+                              : (R + 127) / 128;         // >= 4 stages per slice
   if (S > max_s) S = max_s;
   const long max_part = (16L << 20) / (static_cast<long>(N) * K);   // partials <= 64 MB
   if (S > max_part) S = max_part;

@@ -1,6 +1,7 @@
 """fp32 weight gradients with a <= 32-wide output (N tile 32): time per call and error vs float64 on a row
 subsample, for the A/B of the 32-wide LDS-DMA ring kernel (run once with APPLESTAR_WGRAD32_PIPE=0 for the
 register-staged kernel, APPLESTAR_WGRAD32_PIPE=1 for the ring; the switch is read once per process).
+Round 6: the split-once staging kernel for 32 / 64-wide N tiles is the default (APPLESTAR_WGRAD_STG_NARROW=0: off).
 
     python tools/bench_wgrad32.py > out.jsonl
 """
@@ -15,8 +16,9 @@ from tools.bench_f32_kernels import timed  # noqa: E402
 
 # learner shapes whose Cout / N <= 32: location-head 76x80 64->32 and 16->16 convs, the 19x20 32->32 conv, a
 # 32-wide dense product and a 16-wide one
-CONV = [(384, 76, 80, 64, 32), (390, 76, 80, 16, 16), (390, 19, 20, 32, 32), (384, 152, 160, 32, 16)]
-DENSE = [(100000, 32, 256), (199680, 16, 64)]
+CONV = [(384, 76, 80, 64, 32), (390, 76, 80, 16, 16), (390, 19, 20, 32, 32), (384, 152, 160, 32, 16),
+        (390, 76, 80, 32, 64), (384, 38, 40, 128, 64), (390, 38, 40, 16, 32)]
+DENSE = [(100000, 32, 256), (199680, 16, 64), (100000, 64, 256)]
 
 
 def err(out, ref):
@@ -29,6 +31,8 @@ def main():
     C = native.ensure_loaded()
     C.set_f32_mfma_mode(1)
     mode = 'ring' if os.environ.get('APPLESTAR_WGRAD32_PIPE', '0') == '1' else 'regstaged'
+    if os.environ.get('APPLESTAR_WGRAD_STG_NARROW', '1') != '0':
+        mode = 'stg_narrow'
     if os.environ.get('APPLESTAR_WGRAD32_BK', '128') == '256':
         mode += '_bk256'
     torch.manual_seed(0)

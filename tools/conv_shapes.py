@@ -39,9 +39,12 @@ class Timed:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--out', default='gpurun_out/conv_shapes.txt')
+    ap.add_argument('--names', default='conv3x3_fwd,wgrad,act_grad_nhwc,maxpool2_fwd,maxpool2_bwd,conv3x3_f32,'
+                    'conv3x3_f32_v2,conv3x3_f32_psb,conv3x3_f32_epi2,wgrad_f32,gemm_f32,gemm_f32_psb')
+    ap.add_argument('--precision', choices=['fp32', 'bf16'], default='fp32')
     args = ap.parse_args()
     C = native.ensure_loaded()
-    names = ['conv3x3_fwd', 'wgrad', 'act_grad_nhwc', 'maxpool2_fwd', 'maxpool2_bwd']
+    names = [n for n in args.names.split(',') if hasattr(C, n)]
 
     class Proxy:
         pass
@@ -54,7 +57,10 @@ def main():
         setattr(proxy, n, t.wrap(n))
     native._C = proxy
     dev = torch.device('cuda', 0)
-    tr = RLTrainer({'learner': {'use_value_feature': True}, 'model': {'enable_baselines': ['winloss']}}, device=dev)
+    lcfg = {'use_value_feature': True}
+    if args.precision == 'bf16':
+        lcfg['amp_dtype'] = 'bfloat16'
+    tr = RLTrainer({'learner': lcfg, 'model': {'enable_baselines': ['winloss']}}, device=dev)
     h = rl_batch(6, 64, seed=0)
     b = to_device(h, dev)
     b['entity_total'] = entity_total_hint(h)

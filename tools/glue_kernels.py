@@ -61,7 +61,14 @@ def main():
             if kind is None:
                 continue
             dur = getattr(k, 'duration', 0)
-            key = f'{kind:16s} {e.name:28s} {site or "(no frame)"}'
+            if site is None:     # no framework frame: name the CPU op chain (and any stack frame at all)
+                chain, p = [], e
+                while p is not None and len(chain) < 5:
+                    chain.append(p.name)
+                    p = p.cpu_parent
+                fr = next((f for f in (e.stack or []) if 'torch/' not in f), None)
+                site = '(no frame) ' + ' < '.join(chain[1:]) + (f' @ {fr}' if fr else '')
+            key = f'{kind:16s} {e.name:28s} {site}'
             sites[key][0] += 1
             sites[key][1] += dur
             kinds[kind][0] += 1
