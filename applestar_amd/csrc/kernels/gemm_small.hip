@@ -167,15 +167,16 @@ __global__ __launch_bounds__(256) void small_nt_kernel(const T* __restrict__ a, 
 
 // dW tile (rows n0 .. n0 + 31 of dW = columns of dY, columns k0 .. k0 + 31 = columns of X); the workgroups of the
 // first column tile also produce db.  lane (l32, h): dY column n0 + l32 and X column k0 + l32 at rows
-// 16 s + 8 h .. + 7 of reduction step s (wave w takes steps w, w + 4, ...): every load instruction reads 32
-// consecutive elements of one row (coalesced).
-template <typename T, typename TO, int SPLIT>
-__global__ __launch_bounds__(256) void small_tn_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+// 16 s + 8 h .. + 7 of reduction step s (wave w takes steps w, w + NW, ...): every load instruction reads 32
+// consecutive elements of one row (coalesced).  NW = 16 waves once the reduction has >= 32 steps (R >= 512,
+// small_tn_waves): each wave's loop is a chain of dependent L2 round trips, so more waves = shorter chains.
+template <typename T, typename TO, int SPLIT, int NW>
+__global__ __launch_bounds__(64 * NW) void small_tn_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                        const T* __restrict__ ymask, int mask_mode,
                                                        TO* __restrict__ dw, TO* __restrict__ db, long R, int N,
                                                        int K, int tiles_k) {
-  __shared__ float red[3][16][64];
-  __shared__ float dbs[4][64];
+  __shared__ float red[NW - 1][16][64];
+  __shared__ float dbs[NW][64];
   const int tk = blockIdx.x % tiles_k, tn = blockIdx.x / tiles_k;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, l32 = lane & 31, h = lane >> 5;
   const int n = tn * 32 + l32, k = tk * 32 + l32;
@@ -200,9 +201,9 @@ __global__ __launch_bounds__(256) void small_tn_kernel(const T* __restrict__ dy,
   };
   float ca[8], cb[8];
   load(w, ca, cb);
-  for (long s = w; s < RT; s += 4) {
+  for (long s = w; s < RT; s += NW) {
     float na[8], nb[8];
-    load(s + 4, na, nb);
+    load(s + NW, na, nb);
 #pragma unroll
     for (int j = 0; j < 8; ++j) dsum += ca[j];
     step_mfma<T, SPLIT>(ca, cb, acc);
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(256) void small_tn_kernel(const T* __restrict__ dy,
   if (want_db && h == 0 && nok) {
     float t = 0.f;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) t += dbs[q][l32] + dbs[q][l32 + 32];
+    for (int q = 0; q < NW; ++q) t += dbs[q][l32] + dbs[q][l32 + 32];
     Cvt<TO>::store(db, n, t);
   }
   if (!nok) return;
@@ -229,7 +230,10 @@ __global__ __launch_bounds__(256) void small_tn_kernel(const T* __restrict__ dy,
     for (int q = 0; q < 4; ++q) {
       const int e = 4 * g + q, kk = tk * 32 + 8 * g + 4 * h + q;
       if (kk >= K) continue;
-      Cvt<TO>::store(dw, static_cast<long>(n) * K + kk, acc[e] + red[0][e][lane] + red[1][e][lane] + red[2][e][lane]);
+      float v = acc[e];
+#pragma unroll
+      for (int q = 0; q < NW - 1; ++q) v += red[q][e][lane];
+      Cvt<TO>::store(dw, static_cast<long>(n) * K + kk, v);
     }
   }
 }
@@ -343,30 +347,48 @@ void small_nt(const void* a, const void* b, const float* bias, const void* res, 
   }
 }
 
-void small_tn(const void* dy, const void* x, const void* ymask, int mask_mode, void* dw, void* db, long R, int N,
-              int K, bool bf16_in, bool bf16_out, hipStream_t s) {
+// waves per workgroup of small_tn: 16 when the reduction has >= 32 steps (R >= 512), else 4
+// (APPLESTAR_SMALL_TN_WAVES = 4 | 16 forces one)
+int small_tn_waves(long R) {
+  static const int forced = [] {
+    const char* e = std::getenv("APPLESTAR_SMALL_TN_WAVES");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced == 4 || forced == 16) return forced;
+  return (R + 15) / 16 >= 32 ? 16 : 4;
+}
+
+template <int NW>
+void small_tn_launch(const void* dy, const void* x, const void* ymask, int mask_mode, void* dw, void* db, long R,
+                     int N, int K, bool bf16_in, bool bf16_out, hipStream_t s) {
   const int tk = (K + 31) / 32;
   const long nwg = static_cast<long>((N + 31) / 32) * tk;
   if (nwg == 0) return;
-  const dim3 g(static_cast<unsigned>(nwg)), blk(256);
+  const dim3 g(static_cast<unsigned>(nwg)), blk(64 * NW);
   if (bf16_in) {
     if (bf16_out)
-      hipLaunchKernelGGL((small_tn_kernel<bf16_t, bf16_t, 0>), g, blk, 0, s, static_cast<const bf16_t*>(dy),
+      hipLaunchKernelGGL((small_tn_kernel<bf16_t, bf16_t, 0, NW>), g, blk, 0, s, static_cast<const bf16_t*>(dy),
                          static_cast<const bf16_t*>(x), static_cast<const bf16_t*>(ymask), mask_mode,
                          static_cast<bf16_t*>(dw), static_cast<bf16_t*>(db), R, N, K, tk);
     else
-      hipLaunchKernelGGL((small_tn_kernel<bf16_t, float, 0>), g, blk, 0, s, static_cast<const bf16_t*>(dy),
+      hipLaunchKernelGGL((small_tn_kernel<bf16_t, float, 0, NW>), g, blk, 0, s, static_cast<const bf16_t*>(dy),
                          static_cast<const bf16_t*>(x), static_cast<const bf16_t*>(ymask), mask_mode,
                          static_cast<float*>(dw), static_cast<float*>(db), R, N, K, tk);
   } else if (f32_mfma_mode() == 0) {
-    hipLaunchKernelGGL((small_tn_kernel<float, float, 0>), g, blk, 0, s, static_cast<const float*>(dy),
+    hipLaunchKernelGGL((small_tn_kernel<float, float, 0, NW>), g, blk, 0, s, static_cast<const float*>(dy),
                        static_cast<const float*>(x), static_cast<const float*>(ymask), mask_mode,
                        static_cast<float*>(dw), static_cast<float*>(db), R, N, K, tk);
   } else {
-    hipLaunchKernelGGL((small_tn_kernel<float, float, 1>), g, blk, 0, s, static_cast<const float*>(dy),
+    hipLaunchKernelGGL((small_tn_kernel<float, float, 1, NW>), g, blk, 0, s, static_cast<const float*>(dy),
                        static_cast<const float*>(x), static_cast<const float*>(ymask), mask_mode,
                        static_cast<float*>(dw), static_cast<float*>(db), R, N, K, tk);
   }
+}
+
+void small_tn(const void* dy, const void* x, const void* ymask, int mask_mode, void* dw, void* db, long R, int N,
+              int K, bool bf16_in, bool bf16_out, hipStream_t s) {
+  if (small_tn_waves(R) == 16) small_tn_launch<16>(dy, x, ymask, mask_mode, dw, db, R, N, K, bf16_in, bf16_out, s);
+  else small_tn_launch<4>(dy, x, ymask, mask_mode, dw, db, R, N, K, bf16_in, bf16_out, s);
 }
 
 }  // namespace as
