@@ -930,8 +930,15 @@ def defer_begin(device, loss=None, owner=None) -> None:
         _Deferred.flushed = None
 
 
+# side streams the deferred weight gradients are spread over (APPLESTAR_DEFER_STREAMS, default 1): each product goes
+# to the stream with the least queued work (rows x N x K plus a per-launch constant).  Measured: 2 streams neutral
+# (54.89 / 54.66 vs 54.66 / 54.68 ms), 3 slower (55.24 / 55.25; profiles/r10f_bench_defer_streams.txt) - the
+# products already fill the CUs the recurrence leaves idle, and more queues than the box's 4 hardware queues share
+DEFER_STREAMS = max(1, int(os.environ.get('APPLESTAR_DEFER_STREAMS', '1')))
+
+
 def defer_flush() -> None:
-    """Issue the queued weight gradients on the side stream (ordered after each operand's producer) and stop
+    """Issue the queued weight gradients on the side stream(s) (ordered after each operand's producer) and stop
     queueing."""
     if not _Deferred.on:
         return
@@ -940,25 +947,30 @@ def defer_flush() -> None:
     if not q:
         return
     dev = q[0][1].device
-    side = _Deferred.streams.get(dev)
-    if side is None:
-        side = _Deferred.streams[dev] = torch.cuda.Stream(device=dev)
-    with torch.cuda.stream(side):
-        for ev, dy2d, x, cin, has_b, out in q:
+    sides = _Deferred.streams.get(dev)
+    if sides is None:
+        sides = _Deferred.streams[dev] = [torch.cuda.Stream(device=dev) for _ in range(DEFER_STREAMS)]
+    load = [0] * len(sides)
+    for ev, dy2d, x, cin, has_b, out in q:
+        i = min(range(len(sides)), key=load.__getitem__)
+        load[i] += dy2d.shape[0] * out.numel() + (1 << 22)
+        side = sides[i]
+        with torch.cuda.stream(side):
             side.wait_event(ev)
             for t in (dy2d, x, out):
                 t.record_stream(side)
             _C.wgrad_f32(dy2d, x, cin, has_b, out)
-    _Deferred.flushed = side
+    _Deferred.flushed = [s for s, n in zip(sides, load) if n]
 
 
 def defer_end(device) -> None:
-    """Flush anything still queued (no LSTM in this backward) and join the side stream."""
+    """Flush anything still queued (no LSTM in this backward) and join the side stream(s)."""
     if _Deferred.on:
         defer_flush()
-    side, _Deferred.flushed = _Deferred.flushed, None
-    if side is not None:
-        torch.cuda.current_stream(torch.device(device)).wait_stream(side)
+    sides, _Deferred.flushed = _Deferred.flushed, None
+    main = torch.cuda.current_stream(torch.device(device))
+    for side in sides or ():
+        main.wait_stream(side)
     _FWD_EPOCH[0] += 1          # the next forward counts weight uses afresh
 
 
