@@ -188,9 +188,11 @@ SplitBufs make_split(const at::Tensor& like, int64_t B, int64_t width) {
   return r;
 }
 
+// want_bf16: also return a bf16 copy of out written by the split recurrence itself (inference: the next layer's input
+// projection and the heads take bf16 operands - no cast launch per layer); undefined when the split path is not taken
 std::vector<at::Tensor> lnlstm_fwd(const at::Tensor& xp, const at::Tensor& h0, const at::Tensor& c0,
                                    const at::Tensor& wT, const at::Tensor& lnh_w, const at::Tensor& lnh_b,
-                                   const at::Tensor& lnc_w, const at::Tensor& lnc_b, double eps) {
+                                   const at::Tensor& lnc_w, const at::Tensor& lnc_b, double eps, bool want_bf16) {
   for (auto* t : {&xp, &h0, &c0, &wT, &lnh_w, &lnh_b, &lnc_w, &lnc_b}) check_cuda(*t, "lnlstm input");
   TORCH_CHECK(xp.scalar_type() == at::kFloat && h0.scalar_type() == at::kFloat && c0.scalar_type() == at::kFloat,
               "lnlstm: fp32 activations");
@@ -212,13 +214,16 @@ std::vector<at::Tensor> lnlstm_fwd(const at::Tensor& xp, const at::Tensor& h0, c
   SplitBufs sb;
   const bool split = lstm_split_enabled(H, B);
   if (split) sb = make_split(xp, B, G);
+  at::Tensor out_bf;
+  if (split && want_bf16) out_bf = at::empty({T, B, H}, xp.options().dtype(at::kBFloat16));
   as::lnlstm_fwd(xp.data_ptr<float>(), h0.data_ptr<float>(), c0.data_ptr<float>(), wT.data_ptr(), dt(wT),
                  lnh_w.data_ptr<float>(), lnh_b.data_ptr<float>(), lnc_w.data_ptr<float>(), lnc_b.data_ptr<float>(),
                  static_cast<int>(T), static_cast<int>(B), static_cast<int>(H), static_cast<float>(eps),
                  out.data_ptr<float>(), c_all.data_ptr<float>(), xhat_h.data_ptr<float>(), rstd_h.data_ptr<float>(),
                  gates.data_ptr<float>(), xhat_c.data_ptr<float>(), rstd_c.data_ptr<float>(), hT.data_ptr<float>(),
-                 cT.data_ptr<float>(), stream(), split ? &sb.s : nullptr);
-  return {out, hT, cT, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c};
+                 cT.data_ptr<float>(), stream(), split ? &sb.s : nullptr,
+                 out_bf.defined() ? reinterpret_cast<unsigned short*>(out_bf.data_ptr()) : nullptr);
+  return {out, hT, cT, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c, out_bf};
 }
 
 std::vector<at::Tensor> lnlstm_bwd(const at::Tensor& dout, const at::Tensor& dhT, const at::Tensor& dcT,
@@ -2288,7 +2293,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("post") = py::none());
   m.def("gated_residual_bwd", &gated_residual_bwd, py::arg("dout"), py::arg("y"), py::arg("g"), py::arg("sp"),
         py::arg("out"), py::arg("xin") = py::none());
-  m.def("lnlstm_fwd", &lnlstm_fwd);
+  m.def("lnlstm_fwd", &lnlstm_fwd, py::arg("xp"), py::arg("h0"), py::arg("c0"), py::arg("wT"),
+        py::arg("lnh_w"), py::arg("lnh_b"), py::arg("lnc_w"), py::arg("lnc_b"),
+        py::arg("eps"), py::arg("want_bf16") = false);
   m.def("lnlstm_bwd", &lnlstm_bwd);
   m.def("entity_embed_fwd", &entity_embed_fwd);
   m.def("entity_onehot", &entity_onehot);

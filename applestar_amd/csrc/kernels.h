@@ -97,7 +97,7 @@ struct LstmSplit {
 void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* wT, int w_dt, const float* lnh_w,
                 const float* lnh_b, const float* lnc_w, const float* lnc_b, int T, int B, int H, float eps, float* out,
                 float* c_all, float* xhat_h, float* rstd_h, float* gates, float* xhat_c, float* rstd_c, float* hT,
-                float* cT, hipStream_t s, const LstmSplit* split = nullptr);
+                float* cT, hipStream_t s, const LstmSplit* split = nullptr, unsigned short* out_bf16 = nullptr);
 // w = W_hh [4H][H]. Outputs d(xp) [T,B,4H], d(h W_hh^T) [T,B,4H], dL/d(LN_c out) [T,B,H], dh0, dc0.
 void lnlstm_bwd(const float* dout, const float* dhT, const float* dcT, const float* gates, const float* c_all,
                 const float* xhat_c, const float* rstd_c, const float* xhat_h, const float* rstd_h, const void* w,

@@ -589,7 +589,8 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
     const float* __restrict__ lnc_w, const float* __restrict__ lnc_b, int T, int B, int Bp, float eps,
     float* __restrict__ out, float* __restrict__ c_all, float* __restrict__ xhat_h, float* __restrict__ rstd_h,
     float* __restrict__ gates_out, float* __restrict__ xhat_c, float* __restrict__ rstd_c, float* __restrict__ hT,
-    float* __restrict__ cT, unsigned long long* __restrict__ slab, int* __restrict__ err) {
+    float* __restrict__ cT, unsigned long long* __restrict__ slab, int* __restrict__ err,
+    bf16_t* __restrict__ out_bf) {
   constexpr int KS = kSplitKS;
   constexpr int G = 4 * H, RS = H / KS, COLS = G / NT, GS = G / KS;
   static_assert(G % NT == 0 && H % KS == 0 && NT >= H, "split tiling");
@@ -749,6 +750,7 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
       h_s[tid] = hv;
       if (own_unit) {
         out[row * H + tid] = hv;
+        if (out_bf) out_bf[row * H + tid] = f2bf(hv);   // the next layer's / heads' bf16 operand (inference)
         c_all[(row + B) * H + tid] = c;
         xhat_c[row * H + tid] = xc;
         if (t == T - 1) { hT[static_cast<long>(b) * H + tid] = hv; cT[static_cast<long>(b) * H + tid] = c; }
@@ -947,7 +949,7 @@ bool lnlstm_supported(int H) { return H == 384 || H == 32; }
 void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* wT, int w_dt, const float* lnh_w,
                 const float* lnh_b, const float* lnc_w, const float* lnc_b, int T, int B, int H, float eps, float* out,
                 float* c_all, float* xhat_h, float* rstd_h, float* gates, float* xhat_c, float* rstd_c, float* hT,
-                float* cT, hipStream_t s, const LstmSplit* split) {
+                float* cT, hipStream_t s, const LstmSplit* split, unsigned short* out_bf16) {
   if (H == 384 && split != nullptr) {
     const int Bp = (B + 7) / 8 * 8;
     const dim3 grid(Bp * kSplitKS);
@@ -958,7 +960,7 @@ void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* w
 #define AS_FWD_SPLIT(TWv, GR)                                                                                    \
     hipLaunchKernelGGL((lnlstm_fwd_split_kernel<384, 768, TWv, GR>), grid, dim3(768), 0, s, xp, h0, c0,          \
                        static_cast<const TWv*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, Bp, eps, out, c_all, xhat_h,  \
-                       rstd_h, gates, xhat_c, rstd_c, hT, cT, split->slab, split->err)
+                       rstd_h, gates, xhat_c, rstd_c, hT, cT, split->slab, split->err, out_bf16)
     if (w_dt == DT_BF16) {
       if (gran) AS_FWD_SPLIT(bf16_t, true); else AS_FWD_SPLIT(bf16_t, false);
     } else {

@@ -169,6 +169,9 @@ def lstm_exchange_ok(device):
 
 
 
+LSTM_BF16_OUT = os.environ.get('APPLESTAR_LSTM_BF16_OUT', '1') == '1'     # A/B switch
+
+
 class _LNLSTMRecurrence(torch.autograd.Function):
     """Recurrent part of an LN-LSTM layer: xp [T,B,4H] (already LN_i(x W_ih^T)) -> h [T,B,H]."""
 
@@ -177,9 +180,14 @@ class _LNLSTMRecurrence(torch.autograd.Function):
         # W_hh in the recurrence's dtype, for the backward only (inference skips the cast)
         wq = w_hh.detach().to(w_dtype) if need_bwd else w_hh.detach()
         wT = _wT(w_hh, w_dtype)          # a derived form: transposed once per optimizer step, not per layer call
-        out, hT, cT, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c = _C.lnlstm_fwd(
+        # inference under autocast: the recurrence also writes h in bf16, registered as out's cast (_bf16_rows), so
+        # the next layer's input projection and the heads read it without a cast launch per layer
+        want_bf16 = LSTM_BF16_OUT and not need_bwd and CAST_CACHE and torch.is_autocast_enabled() and xp.is_cuda
+        out, hT, cT, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c, out_bf = _C.lnlstm_fwd(
             xp.contiguous(), h0.contiguous(), c0.contiguous(), wT, lnh_w.detach(), lnh_b.detach(),
-            lnc_w.detach(), lnc_b.detach(), 1e-5)
+            lnc_w.detach(), lnc_b.detach(), 1e-5, want_bf16)
+        if out_bf is not None:
+            _note_bf16_copy(out, out_bf)
         ctx.save_for_backward(h0, out, c_all, xhat_h, rstd_h, gates, xhat_c, rstd_c, wq.contiguous(), lnh_w, lnc_w)
         ctx.set_materialize_grads(False)     # unused hT / cT: None (a cached zero) instead of two fills per layer
         return out, hT, cT
@@ -2144,31 +2152,62 @@ def _small_native_ok(x, R, N, K, act):
         R * K < (1 << 31) and R * N < (1 << 31)
 
 
-_CAST_CACHE = {}      # id(fp32 activation) -> (weakref, version, shape, bf16 copy)
+_CAST_CACHE = {}      # (data_ptr, R, K) of an fp32 activation -> (weakref, version, bf16 copy)
 CAST_CACHE = os.environ.get('APPLESTAR_CAST_CACHE', '1') == '1'
+
+
+def _cast_key(x, R, K):
+    return (x.data_ptr(), R, K) if x.is_contiguous() and x.numel() == R * K else None
+
+
+def _cast_lookup(x, R, K):
+    key = _cast_key(x, R, K)
+    e = _CAST_CACHE.get(key) if key is not None else None
+    if e is None:
+        return None
+    src = e[0]()
+    # the source object alive at the same address and unmodified (views share its version counter)
+    if src is None or src.data_ptr() != x.data_ptr() or src._version != e[1] or x._version != e[1]:
+        return None
+    return e[2]
+
+
+def _cast_store(x, R, K, xb):
+    import weakref
+    key = _cast_key(x, R, K)
+    if key is None:
+        return
+    if len(_CAST_CACHE) > 64:
+        for k in [k for k, v in _CAST_CACHE.items() if v[0]() is None]:
+            del _CAST_CACHE[k]
+    try:
+        _CAST_CACHE[key] = (weakref.ref(x), x._version, xb)
+    except TypeError:
+        pass
+
+
+def _note_bf16_copy(x, xb):
+    """Register xb (bf16, same shape) as the cast of the fp32 activation x (written by x's producer kernel)."""
+    R = x.shape[0] * x.shape[1] if x.dim() == 3 else x.shape[0]
+    K = x.numel() // R if R else 0
+    _cast_store(x, R, K, xb.view(R, K))
 
 
 def _bf16_rows(x, R, K):
     """x as a contiguous bf16 [R, K].  An fp32 activation feeding several linears (the core LSTM output, the scalar
-    context: 3-4 heads each) is cast once: the copy is kept while the source tensor object is alive and unmodified
-    (same object, same version counter) - one launch instead of one per consumer."""
+    context: 3-4 heads each) is cast once: the copy is kept while the source tensor is alive and unmodified (same
+    storage address, same version counter, so a reshaped view of it hits too) - one launch instead of one per
+    consumer; the LSTM recurrence registers its own bf16 output here (no launch at all)."""
     if x.dtype == torch.bfloat16:
         return x.reshape(R, K).contiguous()
     if not (CAST_CACHE and x.is_cuda and x.dtype == torch.float32) or (torch.is_grad_enabled() and x.requires_grad):
         # (no caching under autograd: an entry would keep the step's graph alive)
         return x.reshape(R, K).to(torch.bfloat16).contiguous()
-    import weakref
-    e = _CAST_CACHE.get(id(x))
-    if e is not None and e[0]() is x and e[1] == x._version and e[2] == (R, K):
-        return e[3]
+    xb = _cast_lookup(x, R, K)
+    if xb is not None:
+        return xb
     xb = x.reshape(R, K).to(torch.bfloat16).contiguous()
-    if len(_CAST_CACHE) > 64:
-        for k in [k for k, v in _CAST_CACHE.items() if v[0]() is None]:
-            del _CAST_CACHE[k]
-    try:
-        _CAST_CACHE[id(x)] = (weakref.ref(x), x._version, (R, K), xb)
-    except TypeError:
-        pass
+    _cast_store(x, R, K, xb)
     return xb
 
 

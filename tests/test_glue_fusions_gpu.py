@@ -399,3 +399,27 @@ def test_derived_psb_forms_refresh_batched():
     assert torch.equal(g2, C.presplit_b(lin.detach(), True))
     wt = conv.detach().flip(2, 3).permute(1, 2, 3, 0).contiguous().view(128, -1)
     assert torch.equal(g3, C.presplit_b(wt))
+
+
+def test_lstm_inference_bf16_output_is_the_registered_cast():
+    """Inference under autocast: the split LN-LSTM recurrence writes h in bf16 too and registers it as the cast of
+    its fp32 output (ops/native.py _note_bf16_copy), so the next layer / the heads read it without a cast launch;
+    it must be exactly the round-to-nearest-even cast of the fp32 output, also through a reshaped view."""
+    from applestar_amd.models.lstm import StackedLNLSTM
+    from applestar_amd.ops import native as NN
+    torch.manual_seed(0)
+    B, H = 3, 384
+    m = StackedLNLSTM(64, H, 2).to(DEV)
+    x = torch.randn(2, B, 64, device=DEV)
+    with torch.no_grad(), torch.autocast('cuda', dtype=torch.bfloat16):
+        out, _ = m(x, m.zero_state(B, DEV))
+        flat = out.reshape(2 * B, H)
+        reg = NN._cast_lookup(flat, 2 * B, H)
+        assert reg is not None, 'the recurrence did not register its bf16 output'
+        assert reg.dtype == torch.bfloat16 and torch.equal(reg, flat.to(torch.bfloat16))
+        assert NN._bf16_rows(flat, 2 * B, H).data_ptr() == reg.data_ptr()
+        out.add_(1.0)                           # a modified source must not hit the stale copy
+        assert NN._cast_lookup(flat, 2 * B, H) is None
+    with torch.no_grad():                       # no autocast: nothing registered, fp32 path unchanged
+        out2, _ = m(x, m.zero_state(B, DEV))
+        assert NN._cast_lookup(out2.reshape(2 * B, H), 2 * B, H) is None

@@ -176,11 +176,16 @@ def test_full_model_bf16_gpu_vs_cpu_fp32(reference):
     # Over round 5's boxes the four-batch mean was 0.028-0.039 for the torch control and 0.0297-0.0343 for the native
     # path.  The check is an absolute ceiling that sits above the native path's measured range and below the one real
     # regression seen (rounding the core output to bf16 in front of a GLU: 0.0407, r7a) - it does not widen with the
-    # control - plus a relative bound against the control's noise level.
+    # control.  The control is reported, not bounded against: it moves box to box as well (its max of three runs was
+    # 0.0271 on the round-6 box where the native value was 0.0343 - a 1.25x relative bound failed there - and 0.0372
+    # on the next run of the same tree), and the native forward is bit-identical across reruns and under allocator
+    # poisoning (tools/diag/poison_probe.py, profiles/r10g_poison_probe_fwd.txt: no read of unwritten memory), so its
+    # box-to-box spread is not an uninitialised read in these kernels.
     su = _su_logit_spread(cpu, [3, 0, 1, 2])
-    print('selected-units logit error, mean of four batches:', su)
+    props = torch.cuda.get_device_properties(0)
+    print('selected-units logit error, mean of four batches:', su, 'device CUs', props.multi_processor_count,
+          getattr(props, 'gcnArchName', ''))
     assert su['native'] <= 0.036, su
-    assert su['native'] <= 1.25 * su['torch'], su
     assert _rel(out['value']['winloss'].float(), ref_out['value']['winloss']) < 3e-2
     a, r = float(info['total_loss']), float(ref_info['total_loss'])
     assert abs(a - r) <= 2e-2 * max(1.0, abs(r)), (a, r)
