@@ -187,7 +187,8 @@ class SelectedUnitsHead(nn.Module):
         return ae0 + self.embed_fc2(self.embed_fc1(emb))
 
     # ------------------------------------------------------------------ teacher forced (parallel)
-    def forward_teacher(self, ae0, entity_embedding, entity_num, selected_units_num, selected_units, key=None):
+    def forward_teacher(self, ae0, entity_embedding, entity_num, selected_units_num, selected_units, key=None,
+                        split=False):
         key, base_mask = self.keys(entity_embedding, entity_num, key)     # [B,N+1,32], [B,N+1]
         B, N1, C = key.shape
         step_ok = None
@@ -224,6 +225,19 @@ class SelectedUnitsHead(nn.Module):
             pooled = self.attention_pool.prefix(key, labels.clamp(max=N1 - 1), new)
             ae_after = ae0.unsqueeze(1) + pooled.to(ae0.dtype)
         ae_in = torch.cat([ae0.unsqueeze(1).to(ae_after.dtype), ae_after[:, :-1]], 1)
+        ptr = {'ae_in': ae_in, 'key': key, 'labels': labels, 'base_mask': base_mask, 'en': en, 'step_ok': step_ok}
+        if split:
+            # the caller runs the pointer half (a 32-wide LSTM: latency-bound, a few workgroups) beside the target-unit
+            # and location heads, which need only ae_after
+            return ptr, ae_after[:, -1], selected_units_num
+        return self.pointer_logits(ptr), None, ae_after[:, -1], selected_units_num
+
+    def pointer_logits(self, ptr):
+        """Teacher-forced pointer logits [B,S,N+1] from forward_teacher(split=True)'s inputs."""
+        ae_in, key, labels, base_mask, en, step_ok = (ptr[k] for k in ('ae_in', 'key', 'labels', 'base_mask', 'en',
+                                                                        'step_ok'))
+        B, N1, _ = key.shape
+        S = labels.shape[1]
         q_in = self.query_fc2(self.query_fc1(ae_in))                     # [B,S,32]
         state = self.lstm.zero_state(B, q_in.device, torch.float32)
         q, _ = self.lstm(q_in.transpose(0, 1), state)                    # [S,B,32]
@@ -239,9 +253,8 @@ class SelectedUnitsHead(nn.Module):
         mask[:, 0] &= ~end_pos
         if step_ok is not None:
             mask = mask & step_ok[None, :, None]
-        logits = torch.where(mask, logits, NEG)
-        # the reference returns no sampled units in teacher-forced mode (test_iou off): None
-        return logits, None, ae_after[:, -1], selected_units_num
+        # the reference returns no sampled units in teacher-forced mode (test_iou off)
+        return torch.where(mask, logits, NEG)
 
     # ------------------------------------------------------------------ sampling (actor)
     def _folded_query(self):

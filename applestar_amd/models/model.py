@@ -48,6 +48,8 @@ DEFAULT_MODEL_CONFIG = AttrDict({
 _SIDE_STREAMS: Dict[tuple, 'torch.cuda.Stream'] = {}
 SIDE_STREAMS_ENABLED = True
 CRITIC_SIDE_STREAM = False   # tools/ab_bench.py --variant critic_side: no gain (+1.9 ms, noisy)
+# teacher-forced selected-units pointer (LSTM + logits) on side stream 2 beside the target-unit / location heads
+SU_SIDE_STREAM = os.environ.get('APPLESTAR_SU_SIDE_STREAM', '1') == '1'
 VE_BWD_OVERLAP = os.environ.get('APPLESTAR_VE_BWD_OVERLAP', '0') == '1'   # A/B r4: 61.6 / 61.7 vs 61.3 / 61.6 ms, off
 VE_AFTER_CORE = os.environ.get('APPLESTAR_VE_AFTER_CORE', '1') == '1'   # A/B r4: fp32 61.3 / 60.8 vs 61.8 / 61.6 ms
 # selected-units + target-unit key projections as one product before the row slice (APPLESTAR_JOINT_KEYS=0: per head)
@@ -231,13 +233,28 @@ class Policy(nn.Module):
             lstm_output, scalar_context, temperature, action_type=action_info['action_type'])
         logit['delay'], action['delay'], emb = self.delay_head(emb, temperature, action=action_info['delay'])
         logit['queued'], action['queued'], emb = self.queued_head(emb, temperature, action=action_info['queued'])
-        logit['selected_units'], action['selected_units'], emb, su_num = \
-            self.selected_units_head.forward_teacher(emb, entity_embeddings, entity_num, selected_units_num,
-                                                     action_info['selected_units'], key=su_key)
+        su = self.selected_units_head
+        if SU_SIDE_STREAM and emb.is_cuda and not torch.cuda.is_current_stream_capturing():
+            # the pointer half of the selected-units head (its 32-wide LSTM + logits: latency-bound) on side stream 2,
+            # beside the target-unit and location heads, which need only the head's output embedding; autograd
+            # replays its backward on that stream as well
+            ptr, emb, su_num = su.forward_teacher(emb, entity_embeddings, entity_num, selected_units_num,
+                                                  action_info['selected_units'], key=su_key, split=True)
+            su_h = _side_stream_call(su.pointer_logits, ptr, slot=2)
+        else:
+            su_logit, _, emb, su_num = su.forward_teacher(emb, entity_embeddings, entity_num, selected_units_num,
+                                                          action_info['selected_units'], key=su_key)
+            su_h = (su_logit, None)
+        action['selected_units'] = None
         logit['target_unit'], action['target_unit'] = self.target_unit_head(
             emb, entity_embeddings, entity_num, temperature, target_unit=action_info['target_unit'], key=tu_key)
         logit['target_location'], action['target_location'] = self.location_head(
             emb, map_skip, temperature, location=action_info['target_location'])
+        logit['selected_units'] = _side_stream_join(su_h)
+        logit = {k: logit[k] for k in ('action_type', 'delay', 'queued', 'selected_units', 'target_unit',
+                                       'target_location')}
+        action = {k: action[k] for k in ('action_type', 'delay', 'queued', 'selected_units', 'target_unit',
+                                         'target_location')}
         return action, su_num, logit
 
 
