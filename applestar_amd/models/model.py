@@ -47,7 +47,14 @@ DEFAULT_MODEL_CONFIG = AttrDict({
 
 _SIDE_STREAMS: Dict[tuple, 'torch.cuda.Stream'] = {}
 SIDE_STREAMS_ENABLED = True
-CRITIC_SIDE_STREAM = False   # tools/ab_bench.py --variant critic_side: no gain (+1.9 ms, noisy)
+# the critics on the value encoder's side stream (beside the policy heads): r2 measured no gain (+1.9 ms, noisy); on
+# the round-6 tree fp32 53.26 / 53.00 -> 51.98 / 52.07 ms, bf16 neutral to +0.1 ms (profiles/r10j_bench_critic_tu_side.txt,
+# r10k_*): APPLESTAR_CRITIC_SIDE_STREAM = fp32 (default: the fp32 step only) | 1 | 0
+_CRITIC_SIDE = os.environ.get('APPLESTAR_CRITIC_SIDE_STREAM', 'fp32')
+CRITIC_SIDE_STREAM = _CRITIC_SIDE == '1'
+CRITIC_SIDE_STREAM_FP32 = _CRITIC_SIDE in ('1', 'fp32')
+# the target-unit head behind the selected-units pointer on side stream 2: fp32 -0.07 / bf16 -0.15 ms (same file)
+TU_SIDE_STREAM = os.environ.get('APPLESTAR_TU_SIDE_STREAM', '1') == '1'
 # teacher-forced selected-units pointer (LSTM + logits) on side stream 2 beside the target-unit / location heads
 SU_SIDE_STREAM = os.environ.get('APPLESTAR_SU_SIDE_STREAM', '1') == '1'
 VE_BWD_OVERLAP = os.environ.get('APPLESTAR_VE_BWD_OVERLAP', '0') == '1'   # A/B r4: 61.6 / 61.7 vs 61.3 / 61.6 ms, off
@@ -246,10 +253,17 @@ class Policy(nn.Module):
                                                           action_info['selected_units'], key=su_key)
             su_h = (su_logit, None)
         action['selected_units'] = None
-        logit['target_unit'], action['target_unit'] = self.target_unit_head(
-            emb, entity_embeddings, entity_num, temperature, target_unit=action_info['target_unit'], key=tu_key)
+        tu_in = {'emb': emb, 'ee': entity_embeddings, 'en': entity_num, 'tu': action_info['target_unit'],
+                 'key': tu_key}
+        tu_head = lambda d: self.target_unit_head(d['emb'], d['ee'], d['en'], temperature, target_unit=d['tu'],
+                                                  key=d['key'])
+        if TU_SIDE_STREAM and su_h[1] is not None:
+            tu_h = _side_stream_call(tu_head, tu_in, slot=2)
+        else:
+            tu_h = (tu_head(tu_in), None)
         logit['target_location'], action['target_location'] = self.location_head(
             emb, map_skip, temperature, location=action_info['target_location'])
+        logit['target_unit'], action['target_unit'] = _side_stream_join(tu_h)
         logit['selected_units'] = _side_stream_join(su_h)
         logit = {k: logit[k] for k in ('action_type', 'delay', 'queued', 'selected_units', 'target_unit',
                                        'target_location')}
@@ -401,7 +415,8 @@ class Model(nn.Module):
         # stream, so the overlap is kept): the critic below reads vf on the main stream
         vf_out = _side_stream_join(vf) if isinstance(vf, tuple) else vf
         critic_in = {'lstm': critic_input, 'vf': vf_out, 'bf': baseline_feature}
-        values_h = _side_stream_call(critic, critic_in) if CRITIC_SIDE_STREAM else (critic(critic_in), None)
+        critic_side = CRITIC_SIDE_STREAM or (CRITIC_SIDE_STREAM_FP32 and not torch.is_autocast_enabled())
+        values_h = _side_stream_call(critic, critic_in) if critic_side else (critic(critic_in), None)
         keys = self.policy.joint_keys(entity_embeddings, n) if JOINT_KEYS else None
         _, _, logits = self.policy.train_forward(
             lstm_output[:n], entity_embeddings[:n], [_take_rows(m, n) for m in map_skip], scalar_context[:n],
