@@ -101,6 +101,17 @@ class ActionTypeHead(nn.Module):
         embedding = self.glu1(e1, scalar_context) + self.glu2(lstm_output, scalar_context)
         return logits, action_type, embedding
 
+    # teacher-forced halves (Policy.train_forward): the logits do not feed the autoregressive embedding, so they can
+    # run on a side stream while the embedding chain continues
+    def teacher_logits(self, lstm_output, scalar_context, temperature: float = 1.0):
+        return self.action_fc(self.res(self.project(lstm_output)), scalar_context) / temperature
+
+    def teacher_embedding(self, lstm_output, scalar_context, action_type):
+        w1 = self.action_map_fc1[0]
+        e1 = F.relu(w1.weight.t().index_select(0, action_type.long().reshape(-1)).view(*action_type.shape, -1)
+                    + w1.bias)
+        return self.glu1(self.action_map_fc2(e1), scalar_context) + self.glu2(lstm_output, scalar_context)
+
 
 class _ArgMLPHead(nn.Module):
     """Shared shape of DelayHead / QueuedHead (action_arg_head.py:27-86)."""
@@ -131,6 +142,15 @@ class _ArgMLPHead(nn.Module):
         w = self.embed_fc1[0]
         e = F.relu(w.weight.t().index_select(0, action.long().reshape(-1)).view(*action.shape, -1) + w.bias)
         return logits, action, embedding + self.embed_fc2(e)
+
+    def teacher_logits(self, embedding, temperature: float = 1.0):
+        logits = self.fc3(self.fc2(self.fc1(embedding)))
+        return logits / temperature if self.use_temperature else logits
+
+    def teacher_embedding(self, embedding, action):
+        w = self.embed_fc1[0]
+        e = F.relu(w.weight.t().index_select(0, action.long().reshape(-1)).view(*action.shape, -1) + w.bias)
+        return embedding + self.embed_fc2(e)
 
 
 class DelayHead(_ArgMLPHead):

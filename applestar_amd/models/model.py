@@ -55,6 +55,8 @@ CRITIC_SIDE_STREAM = _CRITIC_SIDE == '1'
 CRITIC_SIDE_STREAM_FP32 = _CRITIC_SIDE in ('1', 'fp32')
 # the target-unit head behind the selected-units pointer on side stream 2: fp32 -0.07 / bf16 -0.15 ms (same file)
 TU_SIDE_STREAM = os.environ.get('APPLESTAR_TU_SIDE_STREAM', '1') == '1'
+# teacher-forced action-type / delay / queued logits on side stream 2 beside the embedding chain (A/B switch)
+HEAD_LOGITS_SIDE_STREAM = os.environ.get('APPLESTAR_HEAD_LOGITS_SIDE', '1') == '1'
 # teacher-forced selected-units pointer (LSTM + logits) on side stream 2 beside the target-unit / location heads
 SU_SIDE_STREAM = os.environ.get('APPLESTAR_SU_SIDE_STREAM', '1') == '1'
 VE_BWD_OVERLAP = os.environ.get('APPLESTAR_VE_BWD_OVERLAP', '0') == '1'   # A/B r4: 61.6 / 61.7 vs 61.3 / 61.6 ms, off
@@ -236,10 +238,29 @@ class Policy(nn.Module):
         """``keys``: (selected-units, target-unit) key projections from :meth:`joint_keys` (else per head)."""
         logit, action = {}, {}
         su_key, tu_key = keys if keys is not None else (None, None)
-        logit['action_type'], action['action_type'], emb = self.action_type_head(
-            lstm_output, scalar_context, temperature, action_type=action_info['action_type'])
-        logit['delay'], action['delay'], emb = self.delay_head(emb, temperature, action=action_info['delay'])
-        logit['queued'], action['queued'], emb = self.queued_head(emb, temperature, action=action_info['queued'])
+        if HEAD_LOGITS_SIDE_STREAM and lstm_output.is_cuda and SU_SIDE_STREAM and \
+                not torch.cuda.is_current_stream_capturing():
+            # teacher forcing: the action-type / delay / queued logits branches do not feed the autoregressive
+            # embedding chain - they run on side stream 2 (before the selected-units pointer) while the chain continues
+            at, dh, qh = self.action_type_head, self.delay_head, self.queued_head
+            heads_h = [('action_type', _side_stream_call(
+                lambda d: at.teacher_logits(d['x'], d['c'], temperature), {'x': lstm_output, 'c': scalar_context},
+                slot=2))]
+            emb = at.teacher_embedding(lstm_output, scalar_context, action_info['action_type'])
+            heads_h.append(('delay', _side_stream_call(lambda d: dh.teacher_logits(d['e'], temperature), {'e': emb},
+                                                       slot=2)))
+            emb = dh.teacher_embedding(emb, action_info['delay'])
+            heads_h.append(('queued', _side_stream_call(lambda d: qh.teacher_logits(d['e'], temperature), {'e': emb},
+                                                        slot=2)))
+            emb = qh.teacher_embedding(emb, action_info['queued'])
+            for k, _ in heads_h:
+                action[k] = action_info[k]
+        else:
+            heads_h = []
+            logit['action_type'], action['action_type'], emb = self.action_type_head(
+                lstm_output, scalar_context, temperature, action_type=action_info['action_type'])
+            logit['delay'], action['delay'], emb = self.delay_head(emb, temperature, action=action_info['delay'])
+            logit['queued'], action['queued'], emb = self.queued_head(emb, temperature, action=action_info['queued'])
         su = self.selected_units_head
         if SU_SIDE_STREAM and emb.is_cuda and not torch.cuda.is_current_stream_capturing():
             # the pointer half of the selected-units head (its 32-wide LSTM + logits: latency-bound) on side stream 2,
@@ -265,6 +286,8 @@ class Policy(nn.Module):
             emb, map_skip, temperature, location=action_info['target_location'])
         logit['target_unit'], action['target_unit'] = _side_stream_join(tu_h)
         logit['selected_units'] = _side_stream_join(su_h)
+        for k, h in heads_h:
+            logit[k] = _side_stream_join(h)
         logit = {k: logit[k] for k in ('action_type', 'delay', 'queued', 'selected_units', 'target_unit',
                                        'target_location')}
         action = {k: action[k] for k in ('action_type', 'delay', 'queued', 'selected_units', 'target_unit',

@@ -29,6 +29,7 @@ def set_variant(name, on):
     elif name == 'critic_side':
         from applestar_amd.models import model
         model.CRITIC_SIDE_STREAM = on
+        model.CRITIC_SIDE_STREAM_FP32 = on
     elif name == 'scalar_side':
         from applestar_amd.models import encoders
         encoders.SCALAR_SIDE_STREAM = on
