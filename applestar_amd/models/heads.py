@@ -14,6 +14,7 @@ Two execution modes per head:
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -163,6 +164,10 @@ class QueuedHead(_ArgMLPHead):
         super().__init__(2, use_temperature=True)
 
 
+# teacher-forced split (Policy.train_forward): the earlier steps' embedding update goes with the pointer half (A/B)
+SU_AE_SIDE = os.environ.get('APPLESTAR_SU_AE_SIDE', '1') == '1'
+
+
 class SelectedUnitsHead(nn.Module):
     """Pointer network over entities + end token (action_arg_head.py:89-328)."""
 
@@ -240,6 +245,13 @@ class SelectedUnitsHead(nn.Module):
             run_cnt = torch.cumsum(new.int(), 1)
             div = torch.where((selected_units_num != 0)[:, None], run_cnt.clamp(min=1), torch.ones_like(run_cnt))
             emb = run_sum / div.unsqueeze(-1).to(run_sum.dtype)          # embedding after step i
+            if split and SU_AE_SIDE:
+                # the caller runs the pointer half (a 32-wide LSTM: latency-bound, a few workgroups) beside the
+                # target-unit and location heads, which need only the last step's embedding: the [B, S - 1, 1024]
+                # embedding update of the earlier steps (the pointer's queries) moves there too
+                ptr = {'ae0': ae0, 'emb_prev': emb[:, :-1], 'key': key, 'labels': labels, 'base_mask': base_mask,
+                       'en': en, 'step_ok': step_ok}
+                return ptr, self._ae_update(ae0, emb[:, -1]), selected_units_num
             ae_after = self._ae_update(ae0.unsqueeze(1), emb)            # [B,S,1024]
         else:  # attention pooling over the selected set after each step (prefix softmax, all steps at once)
             pooled = self.attention_pool.prefix(key, labels.clamp(max=N1 - 1), new)
@@ -247,15 +259,17 @@ class SelectedUnitsHead(nn.Module):
         ae_in = torch.cat([ae0.unsqueeze(1).to(ae_after.dtype), ae_after[:, :-1]], 1)
         ptr = {'ae_in': ae_in, 'key': key, 'labels': labels, 'base_mask': base_mask, 'en': en, 'step_ok': step_ok}
         if split:
-            # the caller runs the pointer half (a 32-wide LSTM: latency-bound, a few workgroups) beside the target-unit
-            # and location heads, which need only ae_after
             return ptr, ae_after[:, -1], selected_units_num
         return self.pointer_logits(ptr), None, ae_after[:, -1], selected_units_num
 
     def pointer_logits(self, ptr):
         """Teacher-forced pointer logits [B,S,N+1] from forward_teacher(split=True)'s inputs."""
-        ae_in, key, labels, base_mask, en, step_ok = (ptr[k] for k in ('ae_in', 'key', 'labels', 'base_mask', 'en',
-                                                                        'step_ok'))
+        key, labels, base_mask, en, step_ok = (ptr[k] for k in ('key', 'labels', 'base_mask', 'en', 'step_ok'))
+        ae_in = ptr.get('ae_in')
+        if ae_in is None:
+            ae0 = ptr['ae0']
+            ae_prev = self._ae_update(ae0.unsqueeze(1), ptr['emb_prev'])     # [B,S-1,1024]
+            ae_in = torch.cat([ae0.unsqueeze(1).to(ae_prev.dtype), ae_prev], 1)
         B, N1, _ = key.shape
         S = labels.shape[1]
         q_in = self.query_fc2(self.query_fc1(ae_in))                     # [B,S,32]

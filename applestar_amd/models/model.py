@@ -57,6 +57,10 @@ CRITIC_SIDE_STREAM_FP32 = _CRITIC_SIDE in ('1', 'fp32')
 TU_SIDE_STREAM = os.environ.get('APPLESTAR_TU_SIDE_STREAM', '1') == '1'
 # teacher-forced action-type / delay / queued logits on side stream 2 beside the embedding chain (A/B switch)
 HEAD_LOGITS_SIDE_STREAM = os.environ.get('APPLESTAR_HEAD_LOGITS_SIDE', '1') == '1'
+# the heads' joint entity key projection on side stream 2 beside the core LSTM: slower (fp32 52.3 / 53.2 vs 51.2 /
+# 51.0 ms, profiles/r10m_bench_keys_side.txt) - a ~200k-row product beside the split recurrence delays the residency
+# of its 8-workgroup rows; off (APPLESTAR_KEYS_SIDE=1 turns it on)
+KEYS_SIDE = os.environ.get('APPLESTAR_KEYS_SIDE', '0') == '1'
 # teacher-forced selected-units pointer (LSTM + logits) on side stream 2 beside the target-unit / location heads
 SU_SIDE_STREAM = os.environ.get('APPLESTAR_SU_SIDE_STREAM', '1') == '1'
 VE_BWD_OVERLAP = os.environ.get('APPLESTAR_VE_BWD_OVERLAP', '0') == '1'   # A/B r4: 61.6 / 61.7 vs 61.3 / 61.6 ms, off
@@ -412,6 +416,11 @@ class Model(nn.Module):
             # issued right behind the core LSTM's inputs: the value encoder's forward runs on its side stream
             # while the latency-bound recurrence occupies a few dozen CUs (A/B switch)
             vf = _side_stream_call(self.value_encoder, value_feature)
+        ev_keys = None
+        if KEYS_SIDE and JOINT_KEYS and lstm_input.is_cuda and SIDE_STREAMS_ENABLED and \
+                not torch.cuda.is_current_stream_capturing():
+            ev_keys = torch.cuda.Event()
+            ev_keys.record(torch.cuda.current_stream(lstm_input.device))
         out, _ = self._core(lstm_input.view(T + 1, B, -1), h0)
         if self._use_value_feature and vf is None:
             # VE_BWD_OVERLAP: created AFTER the core LSTM (so autograd issues its backward before the LSTM's: the
@@ -440,7 +449,14 @@ class Model(nn.Module):
         critic_in = {'lstm': critic_input, 'vf': vf_out, 'bf': baseline_feature}
         critic_side = CRITIC_SIDE_STREAM or (CRITIC_SIDE_STREAM_FP32 and not torch.is_autocast_enabled())
         values_h = _side_stream_call(critic, critic_in) if critic_side else (critic(critic_in), None)
-        keys = self.policy.joint_keys(entity_embeddings, n) if JOINT_KEYS else None
+        if ev_keys is not None:
+            # the heads' entity key projections depend only on the encoders: issued after the core LSTM (autograd
+            # then runs their backward before the recurrence's, beside it) on side stream 2, ordered on the GPU only
+            # behind the event recorded before the LSTM - the product runs beside the recurrence
+            keys = _side_stream_join(_side_stream_call(lambda d: self.policy.joint_keys(d['ee'], n),
+                                                       {'ee': entity_embeddings}, slot=2, after=ev_keys))
+        else:
+            keys = self.policy.joint_keys(entity_embeddings, n) if JOINT_KEYS else None
         _, _, logits = self.policy.train_forward(
             lstm_output[:n], entity_embeddings[:n], [_take_rows(m, n) for m in map_skip], scalar_context[:n],
             entity_num[:n], flat_action, flat_su_num, self.temperature, keys=keys)
