@@ -279,7 +279,7 @@ __global__ __launch_bounds__(256) void entity_pack_kernel(const NT* __restrict__
 // (one launch instead of reduce + cast, wgrad callers under master weights)
 template <typename OutT>
 __global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __restrict__ part, OutT* __restrict__ out,
-                                                             int nrows, int cols) {
+                                                             int nrows, int cols, long rstride) {
   __shared__ float red[16][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
@@ -287,12 +287,12 @@ __global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __rest
   if (c < cols) {
     int r = g;
     for (; r + 48 < nrows; r += 64) {
-      s0 += part[static_cast<long>(r) * cols + c];
-      s1 += part[static_cast<long>(r + 16) * cols + c];
-      s2 += part[static_cast<long>(r + 32) * cols + c];
-      s3 += part[static_cast<long>(r + 48) * cols + c];
+      s0 += part[static_cast<long>(r) * rstride + c];
+      s1 += part[static_cast<long>(r + 16) * rstride + c];
+      s2 += part[static_cast<long>(r + 32) * rstride + c];
+      s3 += part[static_cast<long>(r + 48) * rstride + c];
     }
-    for (; r < nrows; r += 16) s0 += part[static_cast<long>(r) * cols + c];
+    for (; r < nrows; r += 16) s0 += part[static_cast<long>(r) * rstride + c];
   }
   red[g][threadIdx.x & 63] = (s0 + s1) + (s2 + s3);
   __syncthreads();
@@ -305,9 +305,11 @@ __global__ __launch_bounds__(1024) void column_reduce_kernel(const float* __rest
   }
 }
 
-// grid (ceil(cols/64), ceil(nrows/256)); out zeroed beforehand
-__global__ __launch_bounds__(256) void column_reduce_atomic_kernel(const float* __restrict__ part,
-                                                                   float* __restrict__ out, int nrows, int cols) {
+// first pass of a long reduction (nrows > 1024): grid (ceil(cols/64), ceil(nrows/256)); workgroup (cb, rb) sums rows
+// 256 rb .. 256 rb + 255 of its 64 columns in a fixed order and writes the sum over the chunk's FIRST row (rows only
+// it reads), so the second pass (column_reduce_kernel with rstride = 256 cols) is deterministic too.  Replaced a zero
+// fill + atomicAdd pass whose summation order varied run to run (tools/diag/poison_probe.py).
+__global__ __launch_bounds__(256) void column_reduce_chunk_kernel(float* __restrict__ part, int nrows, int cols) {
   __shared__ float red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int g = threadIdx.x >> 6;
@@ -325,8 +327,9 @@ __global__ __launch_bounds__(256) void column_reduce_atomic_kernel(const float* 
   }
   red[g][threadIdx.x & 63] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (g == 0 && c < cols) atomicAdd(out + c, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                                 red[3][threadIdx.x]);
+  if (g == 0 && c < cols)
+    part[static_cast<long>(r0) * cols + c] = (red[0][threadIdx.x] + red[1][threadIdx.x]) +
+                                             (red[2][threadIdx.x] + red[3][threadIdx.x]);
 }
 
 
@@ -563,19 +566,23 @@ void entity_pack(const void* num, bool num64, int B, int N, long total, bool* va
                        valid, flat, seg, cu);
 }
 
+// part is scratch: a long reduction (> 1024 rows) overwrites the first row of every 256-row chunk
 void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s) {
   if (nrows <= 1024) {
-    hipLaunchKernelGGL(column_reduce_kernel<float>, dim3((cols + 63) / 64), dim3(1024), 0, s, part, out, nrows, cols);
+    hipLaunchKernelGGL(column_reduce_kernel<float>, dim3((cols + 63) / 64), dim3(1024), 0, s, part, out, nrows, cols,
+                       static_cast<long>(cols));
     return;
   }
-  (void)hipMemsetAsync(out, 0, static_cast<size_t>(cols) * sizeof(float), s);
-  hipLaunchKernelGGL(column_reduce_atomic_kernel, dim3((cols + 63) / 64, (nrows + 255) / 256), dim3(256), 0, s, part,
-                     out, nrows, cols);
+  const int nchunk = (nrows + 255) / 256;
+  hipLaunchKernelGGL(column_reduce_chunk_kernel, dim3((cols + 63) / 64, nchunk), dim3(256), 0, s,
+                     const_cast<float*>(part), nrows, cols);
+  hipLaunchKernelGGL(column_reduce_kernel<float>, dim3((cols + 63) / 64), dim3(1024), 0, s, part, out, nchunk, cols,
+                     256L * cols);
 }
 
 void column_reduce_bf16(const float* part, void* out, int nrows, int cols, hipStream_t s) {
   hipLaunchKernelGGL(column_reduce_kernel<bf16_t>, dim3((cols + 63) / 64), dim3(1024), 0, s, part,
-                     static_cast<bf16_t*>(out), nrows, cols);
+                     static_cast<bf16_t*>(out), nrows, cols, static_cast<long>(cols));
 }
 
 int ln_affine_slices(long R) { return static_cast<int>((R + kAffRows - 1) / kAffRows); }

@@ -2025,3 +2025,22 @@ def test_target_unit_fused_matches_torch(edtype):
     assert torch.equal(valid, lf > -1e8)
     assert _err(lf[valid], lr_[valid]) < 2e-4 * max(1.0, lr_[valid].abs().max().item())
     _same_or_boundary(af.cpu(), ar_.cpu(), lr_.cpu(), u.cpu())
+
+
+def test_wgrad_f32_long_reduction_is_deterministic():
+    """A split-R fp32 weight gradient with more than 1,024 slices takes the two-pass chunked column reduction
+    (pool_reduce.hip column_reduce_chunk_kernel): fixed summation order - bit-identical across launches (the former
+    zero fill + atomicAdd pass was not) - and within the usual bound of float64."""
+    from applestar_amd.ops import native
+    C = native.ensure_loaded()
+    torch.manual_seed(3)
+    R, N, K = 300000, 128, 128
+    dy = torch.randn(R, N, device=DEV)
+    x = torch.randn(R, K, device=DEV)
+    dw1, db1 = C.wgrad_f32(dy, x, 0, True)
+    dw2, db2 = C.wgrad_f32(dy, x, 0, True)
+    assert torch.equal(dw1, dw2) and torch.equal(db1, db2)
+    ref = dy[:20000].double().cpu().t() @ x[:20000].double().cpu()
+    part = C.wgrad_f32(dy[:20000].contiguous(), x[:20000].contiguous(), 0, False)[0]
+    assert float((part.double().cpu() - ref).abs().max()) < 1e-3 * 20000 ** 0.5
+    assert float((db1.double().cpu() - dy.double().cpu().sum(0)).abs().max()) < 1e-3 * R ** 0.5
