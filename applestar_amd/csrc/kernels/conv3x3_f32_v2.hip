@@ -173,6 +173,19 @@ void conv3x3_f32_v2(const float* x, const void* wsplit, const float* bias, const
   e2.res2_rows = res2_rows;
   e2.mask = mask;
   if (Cout % 128 != 0) {        // 64 / 32 output channels: 128 x 64 / 128 x 32 tiles (each wave 32 rows), 2 stages
+    // 32-deep K-steps per stage (half the barriers / DMA bookkeeping): 32 outputs 858 -> 743 us on the location
+    // head's 76 x 80 64 -> 32 conv, but 64 outputs slower (574 -> 607, 634 -> 729 us; profiles/r10r_conv_narrow_sub*.jsonl)
+    // - so by default for 32 outputs only (APPLESTAR_CONV_V2_NARROW_SUB = 1: never, 2: both widths)
+    static const int sub_mode = [] {
+      const char* e = std::getenv("APPLESTAR_CONV_V2_NARROW_SUB");
+      return e ? std::atoi(e) : 0;
+    }();
+    const bool sub2 = Cin % 32 == 0 && (sub_mode == 2 || (sub_mode == 0 && Cout % 64 != 0));
+    if (sub2) {
+      if (Cout % 64 == 0) launch_v2<4, 2, 2, 64>(x, wsplit, bias, res, e2, out, B, H, W, Cin, Cout, act, s);
+      else launch_v2<4, 2, 2, 32>(x, wsplit, bias, res, e2, out, B, H, W, Cin, Cout, act, s);
+      return;
+    }
     if (Cout % 64 == 0) launch_v2<4, 2, 1, 64>(x, wsplit, bias, res, e2, out, B, H, W, Cin, Cout, act, s);
     else launch_v2<4, 2, 1, 32>(x, wsplit, bias, res, e2, out, B, H, W, Cin, Cout, act, s);
     return;

@@ -21,6 +21,8 @@ def main():
     C = native.ensure_loaded()
     torch.manual_seed(0)
     shapes = [(390, 19, 20, 128, 128), (384, 19, 20, 128, 128)]
+    if os.environ.get('CONV_SHAPES'):          # e.g. "384,38,40,128,64;384,76,80,64,32"
+        shapes = [tuple(int(v) for v in t.split(',')) for t in os.environ['CONV_SHAPES'].split(';')]
     for B, H, W, Ci, Co in shapes:
         x = torch.randn(B, H, W, Ci, device='cuda').relu()
         w = torch.randn(Co, 3, 3, Ci, device='cuda') / (9 * Ci) ** 0.5
