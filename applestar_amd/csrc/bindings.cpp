@@ -775,6 +775,25 @@ at::Tensor segment_sum(const at::Tensor& x, const at::Tensor& cu) {  // x [T,C],
   return out;
 }
 
+// x [B,N,C] bf16 / fp32, valid [B,N] bool, num [B] int64 / int32 -> [B,C] in x's dtype (inference, no autograd)
+at::Tensor entity_mean_pool(const at::Tensor& x, const at::Tensor& valid, const at::Tensor& num) {
+  check_cuda(x, "x");
+  check_cuda(valid, "valid");
+  check_cuda(num, "num");
+  TORCH_CHECK(x.dim() == 3 && x.is_contiguous() && (x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat),
+              "entity_mean_pool: contiguous x [B, N, C] bf16 / fp32");
+  TORCH_CHECK(valid.scalar_type() == at::kBool && valid.is_contiguous() && valid.size(0) == x.size(0) &&
+                  valid.size(1) == x.size(1) && valid.dim() == 2, "entity_mean_pool: valid [B, N] bool");
+  TORCH_CHECK((num.scalar_type() == at::kLong || num.scalar_type() == at::kInt) && num.numel() == x.size(0) &&
+                  num.is_contiguous(), "entity_mean_pool: num [B] int64 / int32");
+  c10::hip::HIPGuard g(x.device().index());
+  auto out = at::empty({x.size(0), x.size(2)}, x.options());
+  as::entity_mean_pool(x.data_ptr(), dt(x), valid.data_ptr<bool>(), num.data_ptr(), num.scalar_type() == at::kLong,
+                       out.data_ptr(), static_cast<int>(x.size(0)), static_cast<int>(x.size(1)),
+                       static_cast<int>(x.size(2)), stream());
+  return out;
+}
+
 at::Tensor table_grad(const at::Tensor& src, const at::Tensor& idx, int64_t V) {  // src [U,D], idx [U] int64
   check_cuda(src, "src");
   check_cuda(idx, "idx");
@@ -2346,6 +2365,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spatial_embed_pool_fwd", &spatial_embed_pool_fwd);
   m.def("spatial_pool_supported", [](int64_t h, int64_t w) { return as::spatial_pool_supported(static_cast<int>(h), static_cast<int>(w)); });
   m.def("segment_sum", &segment_sum);
+  m.def("entity_mean_pool", &entity_mean_pool);
   m.def("table_grad", &table_grad);
   m.def("conv3x3_fwd", &conv3x3_fwd);
   m.def("wgrad", &wgrad, py::arg("dy"), py::arg("x"), py::arg("cin"), py::arg("want_bias"),

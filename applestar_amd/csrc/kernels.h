@@ -217,6 +217,9 @@ void maxpool2_bwd_relu(const void* dy, const uint8_t* pos, const void* y, void* 
                        hipStream_t s, bool f32 = false);
 // out [S, C] fp32 = per-segment row sums of x [T, C] (segments cu[s]..cu[s+1]); C <= 1024, C % 4 == 0
 void segment_sum(const void* x, int dt, const int* cu, float* out, int S, int C, hipStream_t s);
+// mean over valid rows of x [B,N,C] (bf16 / fp32, fp32 accumulation) / max(num[b], 1) -> out [B,C] in x's dtype
+void entity_mean_pool(const void* x, int dt, const bool* valid, const void* num, bool num64, void* out, int B, int N,
+                      int C, hipStream_t s);
 // LayerNorm affine gradients: per row slice s of ln_affine_slices(R), part[s] = [sum dy*xh (C) | sum dy (C)]
 // (fp32 [R, C] inputs); reduce the slices with column_reduce when there are several
 int ln_affine_slices(long R);

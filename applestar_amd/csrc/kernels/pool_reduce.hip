@@ -485,6 +485,56 @@ void maxpool2_bwd(const void* dy, const uint8_t* pos, void* dx, int dt, int B, i
                        pos, static_cast<float*>(dx), B, H, W, C, static_cast<const float*>(mask));
 }
 
+namespace {
+// mean over the valid entity rows of x [B, N, C] (valid [B, N] bool, count num[b] clamped to >= 1), fp32 accumulation,
+// output in x's dtype: the static (graphed) inference path's entity pooling in one launch (was mask cast, multiply,
+// sum, count clamp / cast, divide and the output cast: seven small launches per forward).  grid (B, C / 64): the four
+// waves take every 4th row of the 64 columns, then sum through LDS in a fixed order.
+template <typename T, typename TN>
+__global__ __launch_bounds__(256) void entity_mean_pool_kernel(const T* __restrict__ x, const bool* __restrict__ valid,
+                                                               const TN* __restrict__ num, T* __restrict__ out, int N,
+                                                               int C) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.x, c = blockIdx.y * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
+  float a0 = 0.f, a1 = 0.f;
+  if (c < C) {
+    int n = w;
+    for (; n + 4 < N; n += 8) {
+      const long r0 = static_cast<long>(b) * N + n, r1 = r0 + 4;
+      const float v0 = Cvt<T>::load(x, r0 * C + c), v1 = Cvt<T>::load(x, r1 * C + c);
+      a0 += valid[r0] ? v0 : 0.f;
+      a1 += valid[r1] ? v1 : 0.f;
+    }
+    for (; n < N; n += 4) {
+      const long r = static_cast<long>(b) * N + n;
+      a0 += valid[r] ? Cvt<T>::load(x, r * C + c) : 0.f;
+    }
+  }
+  red[w][threadIdx.x & 63] = a0 + a1;
+  __syncthreads();
+  if (w == 0 && c < C) {
+    const long cnt = static_cast<long>(num[b]);
+    const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    Cvt<T>::store(out, static_cast<long>(b) * C + c, s / static_cast<float>(cnt > 1 ? cnt : 1));
+  }
+}
+}  // namespace
+
+void entity_mean_pool(const void* x, int dt, const bool* valid, const void* num, bool num64, void* out, int B, int N,
+                      int C, hipStream_t s) {
+  if (B == 0 || C == 0) return;
+  const dim3 g(B, (C + 63) / 64);
+#define AS_EMP(T, TN)                                                                                            \
+  hipLaunchKernelGGL((entity_mean_pool_kernel<T, TN>), g, dim3(256), 0, s, static_cast<const T*>(x), valid,      \
+                     static_cast<const TN*>(num), static_cast<T*>(out), N, C)
+  if (dt == DT_BF16) {
+    if (num64) AS_EMP(bf16_t, int64_t); else AS_EMP(bf16_t, int);
+  } else {
+    if (num64) AS_EMP(float, int64_t); else AS_EMP(float, int);
+  }
+#undef AS_EMP
+}
+
 void segment_sum(const void* x, int dt, const int* cu, float* out, int S, int C, hipStream_t s) {
   if (S == 0) return;
   if (dt == DT_BF16)

@@ -377,6 +377,11 @@ class EntityEncoder(nn.Module):
         if self.reduce_type.startswith('attention_pool'):
             pooled = self.attention_pool(x * vm, num=entity_num, mask=valid)
             return entity_embeddings, self.embed_fc(pooled.to(x.dtype)), valid
+        if n is not None and n.has('entity_mean_pool') and self.reduce_type != 'constant' and \
+                not (torch.is_grad_enabled() and x.requires_grad):
+            mean = n.entity_mean_pool(x, valid, entity_num)     # mask + sum + count + divide + cast in one launch
+            if mean is not None:
+                return entity_embeddings, self.embed_fc(mean), valid
         summed = (x * vm).sum(1, dtype=torch.float32)      # fp32 accumulation inside the reduce (no fp32 copy)
         if self.reduce_type == 'constant':
             mean = summed / 512

@@ -24,7 +24,7 @@ def ensure_loaded():
     return _C
 
 
-_IMPLEMENTED = {'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
+_IMPLEMENTED = {'entity_mean_pool', 'layer_norm', 'gated_residual', 'reverse_scan', 'lnlstm_layer', 'entity_embed', 'upsample2x',
                 'spatial_embed', 'varlen_attention', 'su_sample', 'upsample_conv_out', 'maxpool2x2', 'segment_sum',
                 'gather_rows', 'conv2d', 'linear', 'resblock', 'gated_resblock', 'head_stats', 'bo_encoder', 'resmlp',
                 'location_input', 'value_spatial_proj', 'spatial_embed_pool', 'value_spatial_proj_pool',
@@ -223,6 +223,15 @@ def _zeros_const(shape, device):
     if t is None or t._version != 0:
         t = _ZEROS[key] = torch.zeros(shape, device=device)
     return t
+
+
+def entity_mean_pool(x, valid, num):
+    """Mean of x [B,N,C] over the valid rows (valid [B,N] bool), divided by max(num, 1), in x's dtype with fp32
+    accumulation: one launch (inference only - no autograd node)."""
+    if valid.dtype != torch.bool or num.dtype not in (torch.int64, torch.int32) or x.dtype not in (torch.float32,
+                                                                                                  torch.bfloat16):
+        return None
+    return ensure_loaded().entity_mean_pool(x.contiguous(), valid.contiguous(), num.contiguous())
 
 
 def lnlstm_layer(x, h0, c0, w_ih, w_hh, lni_w, lni_b, lnh_w, lnh_b, lnc_w, lnc_b):

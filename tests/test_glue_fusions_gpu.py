@@ -423,3 +423,22 @@ def test_lstm_inference_bf16_output_is_the_registered_cast():
     with torch.no_grad():                       # no autocast: nothing registered, fp32 path unchanged
         out2, _ = m(x, m.zero_state(B, DEV))
         assert NN._cast_lookup(out2.reshape(2 * B, H), 2 * B, H) is None
+
+
+@pytest.mark.parametrize('dt', [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize('num_dt', [torch.int64, torch.int32])
+def test_entity_mean_pool_matches_torch(dt, num_dt):
+    """The inference path's entity pooling in one launch (pool_reduce.hip entity_mean_pool_kernel) == the masked sum
+    / max(count, 1) with fp32 accumulation, cast to x's dtype; rows with no entity give zeros."""
+    from applestar_amd.ops import native as NN
+    torch.manual_seed(4)
+    B, N, C = 5, 77, 256
+    x = torch.randn(B, N, C, device=DEV).relu().to(dt)
+    num = torch.tensor([0, 1, 13, 77, 40], device=DEV, dtype=num_dt)
+    valid = torch.arange(N, device=DEV)[None, :] < num[:, None].long()
+    got = NN.entity_mean_pool(x, valid, num)
+    ref = (x.float() * valid.unsqueeze(-1)).sum(1) / num.clamp(min=1).unsqueeze(1).float()
+    assert got.dtype == dt and got.shape == (B, C)
+    tol = 1e-6 if dt == torch.float32 else 8e-3
+    assert (got.float() - ref).abs().max().item() <= tol * max(1.0, ref.abs().max().item())
+    assert torch.equal(got[0].float(), torch.zeros(C, device=DEV))
