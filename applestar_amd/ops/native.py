@@ -1391,6 +1391,41 @@ GATE_CHAIN = os.environ.get('APPLESTAR_GATE_CHAIN', '1') == '1'
 # four f32 GEMMs on the step (profiles/r4z_gate_chain_f32.txt), off by default
 GATE_CHAIN_F32 = os.environ.get('APPLESTAR_GATE_CHAIN_F32', '0') == '1'
 GATE_PSB = os.environ.get('APPLESTAR_GATE_PSB', '1') == '1'       # A/B: the fp32 gate GEMMs on pre-split planes
+# the fp32 gate chain (four K = 128 GEMMs: pipeline-bound, ~70 us each) on its own stream beside the conv branch, forward
+# and backward: neutral (51.18 / 51.23 / 51.12 vs 51.16 / 51.17 / 51.19 ms, profiles/r10x_bench_gate_side.txt - the convs
+# already fill the chip); off, APPLESTAR_GATE_SIDE=1 turns it on
+GATE_SIDE = os.environ.get('APPLESTAR_GATE_SIDE', '0') == '1'
+_GATE_STREAMS = {}
+
+
+class _GateSide:
+    """Run a block of launches on the gated blocks' side stream (ordered after the main stream's work so far) and join:
+    ``with g.run(): ...`` then ``g.join(*outs)`` makes the main stream wait and marks the outputs as used there."""
+
+    def __init__(self, ref, on):
+        self.on = on and ref.is_cuda and not torch.cuda.is_current_stream_capturing()
+        if self.on:
+            self.main = torch.cuda.current_stream(ref.device)
+            key = ref.device.index
+            if key not in _GATE_STREAMS:
+                _GATE_STREAMS[key] = torch.cuda.Stream(ref.device)
+            self.side = _GATE_STREAMS[key]
+
+    def run(self, *inputs):
+        if not self.on:
+            return _NULL_CTX
+        self.side.wait_stream(self.main)
+        for t in inputs:
+            if t is not None:
+                t.record_stream(self.side)
+        return torch.cuda.stream(self.side)
+
+    def join(self, *outs):
+        if self.on:
+            self.main.wait_stream(self.side)
+            for t in outs:
+                if t is not None:
+                    t.record_stream(self.main)
 
 
 class _GatedResBlock(torch.autograd.Function):
@@ -1408,10 +1443,13 @@ class _GatedResBlock(torch.autograd.Function):
         for p in (w1, w2, *gate[0::2]):
             _count_use(p)
         B, H, W, C = x.shape
-        y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1, w1)
-        y = _conv3(y1, _conv_w(w2), _w32(b2), None, 0, w2)
         h = x.view(-1, C)
         acts = [h]
+        gate_join = None
+        gate_first = GATE_SIDE and x.dtype == torch.float32 and x.is_cuda and not GATE_CHAIN_F32
+        if not gate_first:
+            y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1, w1)
+            y = _conv3(y1, _conv_w(w2), _w32(b2), None, 0, w2)
         if GATE_CHAIN and C == 128 and x.dtype == torch.bfloat16:
             # the four gate layers in one launch, activation tile resident in LDS (gate_chain.hip)
             acts += _C.gate_chain(h, [gate[2 * i].detach().view(C, C) for i in range(4)],
@@ -1424,13 +1462,19 @@ class _GatedResBlock(torch.autograd.Function):
                                       [_w32(gate[2 * i + 1]) for i in range(4)], [None] * 4, [None] * 4, 0b0111)
             h = acts[-1]
         elif x.dtype == torch.float32 and _gemm_f32_ok(h.shape[0], C, C):
-            # fp32 step: the four gate layers on the f32 GEMM with bias (+ ReLU) in the epilogue
+            # fp32 step: the four gate layers on the f32 GEMM with bias (+ ReLU) in the epilogue - on the gate stream,
+            # beside the two 3x3 convs above (independent branches of the block)
             psb = GATE_PSB and _psb_ok(h.shape[0], C, C)     # the pre-split weight planes (gemm_f32_psb.hip)
-            for i in range(4):
-                gw, gb, act = gate[2 * i], _w32(gate[2 * i + 1]), 1 if i < 3 else 0
-                h = _C.gemm_f32_psb(h, _psb(gw), C, C, gb, None, act, GEMM_PSB_VARIANT) if psb \
-                    else _C.gemm_f32(h, gw.detach().view(C, C), gb, None, act)
-                acts.append(h)
+            pw = [_psb(gate[2 * i]) if psb else gate[2 * i].detach().view(C, C) for i in range(4)]   # (main stream)
+            pb = [_w32(gate[2 * i + 1]) for i in range(4)]
+            gs = _GateSide(x, GATE_SIDE)
+            with gs.run(x):
+                for i in range(4):
+                    act = 1 if i < 3 else 0
+                    h = _C.gemm_f32_psb(h, pw[i], C, C, pb[i], None, act, GEMM_PSB_VARIANT) if psb \
+                        else _C.gemm_f32(h, pw[i], pb[i], None, act)
+                    acts.append(h)
+            gate_join = gs      # joined after the convs are issued (a join here would order them behind the chain)
         else:
             for i in range(4):
                 gw, gb = gate[2 * i].detach().view(C, C), gate[2 * i + 1].detach()
@@ -1443,6 +1487,13 @@ class _GatedResBlock(torch.autograd.Function):
                     gb = gb.to(h.dtype)
                     h = torch._addmm_activation(gb, h, gw.t(), use_gelu=False) if i < 3 else torch.addmm(gb, h, gw.t())
                 acts.append(h)
+        if gate_first:
+            # the convs after the gate chain's issue: the gate stream waited only for x's producer, so its GEMMs run
+            # beside these
+            y1 = _conv3(x, _conv_w(w1), _w32(b1), None, 1, w1)
+            y = _conv3(y1, _conv_w(w2), _w32(b2), None, 0, w2)
+        if gate_join is not None:
+            gate_join.join(*acts[1:])
         # post: the next encoder skip map, added to the block output in the same pass (LocationHead)
         out = _C.gated_residual_fwd(y, h.view(B, H, W, C), sp, x, post)
         ctx.save_for_backward(x, sp, w1, w2, y1, y, out if post is None else None, *acts[1:], *gate[0::2])
@@ -1460,6 +1511,7 @@ class _GatedResBlock(torch.autograd.Function):
                                                     x if ctx.has_post else None)
         # gate chain (1x1 convs as GEMMs over the pixels)
         grads_g = []
+        gate_bwd = None
         d = dg.view(-1, C)
         acts_in = [x.view(-1, C), a1, a2, a3]
         gws = [gw1, gw2, gw3, gw4]
@@ -1484,16 +1536,22 @@ class _GatedResBlock(torch.autograd.Function):
             # fp32 step: each input gradient on the f32 GEMM with the previous layer's ReLU mask (ACT_DRELU on its
             # saved output) or the skip gradient in the epilogue - no threshold_backward / addmm passes
             psb = GATE_PSB and _psb_ok(d.shape[0], C, C)
+            pwt = [_psb(gws[i], True) if psb else _wT(gws[i]) for i in range(4)]      # (main stream)
 
             def dgemm(d, i, r, mode):
-                return _C.gemm_f32_psb(d, _psb(gws[i], True), C, C, None, r, mode, GEMM_PSB_VARIANT) if psb \
-                    else _C.gemm_f32(d, _wT(gws[i]), None, r, mode)
-            for i in (3, 2, 1, 0):
-                dw_i, db_i = _wgrad(d, acts_in[i], 0, True, False, gws[i])
-                grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
-                if i > 0:
-                    d = dgemm(d, i, acts_in[i], 4)
-            dx_gate = dgemm(d, 0, dx_res.view(-1, C).contiguous(), 0)
+                return _C.gemm_f32_psb(d, pwt[i], C, C, None, r, mode, GEMM_PSB_VARIANT) if psb \
+                    else _C.gemm_f32(d, pwt[i], None, r, mode)
+            # the gate chain's backward on the gate stream, beside the conv branch's dX below; joined before the
+            # conv1 dX kernel that adds dx_gate in its epilogue
+            gate_bwd = _GateSide(x, GATE_SIDE)
+            dxr = dx_res.view(-1, C).contiguous()
+            with gate_bwd.run(d, dxr, *acts_in):
+                for i in (3, 2, 1, 0):
+                    dw_i, db_i = _wgrad(d, acts_in[i], 0, True, False, gws[i])
+                    grads_g.append((i, dw_i.view_as(gws[i]).to(gws[i].dtype), db_i.to(ctx.dtypes[2])))
+                    if i > 0:
+                        d = dgemm(d, i, acts_in[i], 4)
+                dx_gate = dgemm(d, 0, dxr, 0)
         else:
             for i in (3, 2, 1, 0):
                 dw_i, db_i = _wgrad(d, acts_in[i], 0, True, _bf16_grads(gws[i].dtype, ctx.dtypes[2]))
@@ -1512,6 +1570,8 @@ class _GatedResBlock(torch.autograd.Function):
         with side.fork():
             dw1, db1 = _conv_dw(dpre1, x, w1, ctx.dtypes[0])
             db1 = db1.to(ctx.dtypes[0])
+        if gate_bwd is not None:
+            gate_bwd.join(dx_gate, *[t for _, dw_i, db_i in grads_g for t in (dw_i, db_i)])
         dx = _conv3(dpre1, _conv_wt(w1), None, dx_gate.view(B, H, W, C).contiguous(), 0, w1, True)
         side.join(dw1, db1, dw2, db2)
         gate_grads = [None] * 8
