@@ -519,6 +519,52 @@ at::Tensor spatial_gather_rows(const at::Tensor& dpre, const at::Tensor& ex, con
   return drows;
 }
 
+// the fused embed + pool stage's backward without the full-resolution dpre (fp32): dy, y [B, H/2, W/2, 32] fp32 (pooled
+// gradient, pooled ReLU output), pos [B, H/2, W/2, 32] uint8 (per-channel argmax in the 2x2 window)
+std::vector<at::Tensor> spatial_dense_wgrad_pooled(const std::vector<at::Tensor>& planes,
+                                                   const std::vector<at::Tensor>& effects, const at::Tensor& dy,
+                                                   const at::Tensor& y, const at::Tensor& pos) {
+  auto sp = make_planes(planes, effects);
+  const int64_t B = planes[0].size(0), H = planes[0].size(1), W = planes[0].size(2);
+  const int64_t L = effects[0].size(1);
+  for (auto* t : {&dy, &y, &pos}) check_cuda(*t, "pooled operand");
+  TORCH_CHECK(H % 2 == 0 && W % 2 == 0, "spatial_dense_wgrad_pooled: even H, W");
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat && pos.scalar_type() == at::kByte,
+              "spatial_dense_wgrad_pooled: fp32 dy / y, uint8 pos");
+  for (auto* t : {&dy, &y, &pos})
+    TORCH_CHECK(t->is_contiguous() && t->numel() == B * (H / 2) * (W / 2) * 32, "spatial_dense_wgrad_pooled: [B,H/2,W/2,32]");
+  c10::hip::HIPGuard g(dy.device().index());
+  const int nb = as::spatial_wgrad_blocks(static_cast<int>(B));
+  auto f32 = dy.options().dtype(at::kFloat);
+  auto part = at::empty({nb, 32 * 24 + 32}, f32);
+  as::spatial_dense_wgrad_pooled(sp, dy.data_ptr<float>(), y.data_ptr<float>(), pos.data_ptr<uint8_t>(),
+                                 part.data_ptr<float>(), static_cast<int>(B), static_cast<int>(H), static_cast<int>(W),
+                                 static_cast<int>(L), stream());
+  auto red = at::empty({32 * 24 + 32}, f32);
+  as::column_reduce(part.data_ptr<float>(), red.data_ptr<float>(), nb, 32 * 24 + 32, stream());
+  return {red.narrow(0, 0, 32 * 24).view({32, 24}), red.narrow(0, 32 * 24, 32)};
+}
+
+at::Tensor spatial_gather_rows_pooled(const at::Tensor& dy, const at::Tensor& y, const at::Tensor& pos,
+                                      const at::Tensor& ex, const at::Tensor& ey, const at::Tensor& entity_num, int64_t N,
+                                      int64_t H, int64_t W) {
+  for (auto* t : {&dy, &y, &pos}) check_cuda(*t, "pooled operand");
+  TORCH_CHECK(dy.scalar_type() == at::kFloat && y.scalar_type() == at::kFloat && pos.scalar_type() == at::kByte &&
+                  dy.is_contiguous() && y.is_contiguous() && pos.is_contiguous() && dy.dim() == 4 && dy.size(3) == 32 &&
+                  y.sizes() == dy.sizes() && pos.sizes() == dy.sizes() && dy.size(1) == H / 2 && dy.size(2) == W / 2,
+              "spatial_gather_rows_pooled: fp32 dy / y, uint8 pos [B,H/2,W/2,32]");
+  TORCH_CHECK(ex.scalar_type() == at::kByte && ey.scalar_type() == at::kByte && entity_num.scalar_type() == at::kLong,
+              "spatial_gather_rows_pooled: uint8 ex / ey, int64 entity_num");
+  const int64_t B = dy.size(0);
+  TORCH_CHECK(ex.numel() == B * N && ey.numel() == B * N && entity_num.numel() == B, "spatial_gather_rows_pooled: rows");
+  c10::hip::HIPGuard g(dy.device().index());
+  auto drows = at::empty({B, N, 32}, dy.options());
+  as::gather_rows_pooled(dy.data_ptr<float>(), y.data_ptr<float>(), pos.data_ptr<uint8_t>(), ex.data_ptr<uint8_t>(),
+                         ey.data_ptr<uint8_t>(), entity_num.data_ptr<int64_t>(), drows.data_ptr<float>(),
+                         static_cast<int>(B), static_cast<int>(N), static_cast<int>(H), static_cast<int>(W), stream());
+  return drows;
+}
+
 at::Tensor spatial_dense_input(const std::vector<at::Tensor>& planes, const std::vector<at::Tensor>& effects,
                                const at::Tensor& bits, int64_t x_dtype) {
   auto sp = make_planes(planes, effects);
@@ -2365,6 +2411,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("spatial_embed_pool_fwd", &spatial_embed_pool_fwd);
   m.def("spatial_pool_supported", [](int64_t h, int64_t w) { return as::spatial_pool_supported(static_cast<int>(h), static_cast<int>(w)); });
   m.def("segment_sum", &segment_sum);
+  m.def("spatial_dense_wgrad_pooled", &spatial_dense_wgrad_pooled);
+  m.def("spatial_gather_rows_pooled", &spatial_gather_rows_pooled);
   m.def("entity_mean_pool", &entity_mean_pool);
   m.def("table_grad", &table_grad);
   m.def("conv3x3_fwd", &conv3x3_fwd);

@@ -153,6 +153,12 @@ void spatial_embed_pool(const SpatialPlanes& sp, const float* wd, const float* b
 int spatial_wgrad_blocks(int B);
 void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, const void* gate, int dt, float* part, int B, int H,
                          int W, int L, hipStream_t s);
+// pooled form (the fused embed + max-pool stage's backward, fp32): dpre from the pooled gradient dy, the pooled ReLU
+// output y and the per-channel argmax pos ([B, H/2, W/2, 32] each) on the fly
+void spatial_dense_wgrad_pooled(const SpatialPlanes& sp, const float* dy, const float* y, const uint8_t* pos,
+                                float* part, int B, int H, int W, int L, hipStream_t s);
+void gather_rows_pooled(const float* dy, const float* y, const uint8_t* pos, const uint8_t* ex, const uint8_t* ey,
+                        const int64_t* entity_num, float* drows, int B, int N, int H, int W, hipStream_t s);
 
 // ---- attention.hip ---------------------------------------------------------------------------
 // Packed varlen MHA, head dim 128, bf16. qkv [T][3][H][128], cu [S+1] int32, out [T][H][128],

@@ -1063,10 +1063,17 @@ __global__ __launch_bounds__(256) void spatial_dense_wgrad_mfma_kernel(SpatialPl
 // dpre = d0 + d1 + d2) makes dW = sum_p (d0 + d1 + d2)[p][n] X[p][c] three bf16 MFMAs per step, each product exact,
 // accumulated in fp32.  The scalar fp32 kernel above streams the same 2.4 GB of dpre / gate at ~1 ms per step with a
 // select-add per column; the planes are staged transposed (channel-major) in LDS like the bf16 image.
+// POOLED (the fused embed + max-pool stage's backward): dpre is not materialised - each pixel's value is the pooled
+// gradient dpre = pdy[window] where the window's per-channel argmax (ppos) is this pixel and the pooled ReLU output
+// (py) is positive, else 0 (pdy / py / ppos [B, H/2, W/2, 32]); it replaces a maxpool2_bwd_relu pass that wrote the
+// 1.2 GB full-resolution dpre this kernel and the row gather then read back.
+template <bool POOLED>
 __global__ __launch_bounds__(256) void spatial_dense_wgrad_mfma_f32_kernel(SpatialPlanes sp, const float* __restrict__ dpre,
                                                                            const float* __restrict__ gate,
                                                                            float* __restrict__ part, int H, int W, int L,
-                                                                           int tiles, int wg_per_obs) {
+                                                                           int tiles, int wg_per_obs,
+                                                                           const float* __restrict__ py,
+                                                                           const uint8_t* __restrict__ ppos) {
   __shared__ __attribute__((aligned(16))) bf16_t dT[3][32 * kSpP];
   __shared__ __attribute__((aligned(16))) uint32_t msk[kSpTile];
   __shared__ __attribute__((aligned(16))) uint16_t hgt[kSpTile];
@@ -1098,7 +1105,17 @@ __global__ __launch_bounds__(256) void spatial_dense_wgrad_mfma_f32_kernel(Spati
     {  // split dpre^T planes: thread = (pixel pair, 16-channel half); tail pixels are zero (clamped loads + select)
       const int pp = 2 * (tid & 127), h16 = 16 * (tid >> 7);
       const bool ok0 = pp < np, ok1 = pp + 1 < np;
-      const long r0 = (base + (ok0 ? pp : 0)) * 32 + h16, r1 = (base + (ok1 ? pp + 1 : 0)) * 32 + h16;
+      long r0 = (base + (ok0 ? pp : 0)) * 32 + h16, r1 = (base + (ok1 ? pp + 1 : 0)) * 32 + h16;
+      uint32_t t0 = 0, t1 = 0;
+      if constexpr (POOLED) {   // the pooled pixel of each of the two pixels, and its position in the 2x2 window
+        const int q0 = p0 + (ok0 ? pp : 0), q1 = p0 + (ok1 ? pp + 1 : 0);
+        const int y0 = q0 / W, x0 = q0 - y0 * W, y1 = q1 / W, x1 = q1 - y1 * W;
+        const long ob = static_cast<long>(b) * (H >> 1);
+        r0 = ((ob + (y0 >> 1)) * (W >> 1) + (x0 >> 1)) * 32 + h16;
+        r1 = ((ob + (y1 >> 1)) * (W >> 1) + (x1 >> 1)) * 32 + h16;
+        t0 = static_cast<uint32_t>((y0 & 1) * 2 + (x0 & 1));
+        t1 = static_cast<uint32_t>((y1 & 1) * 2 + (x1 & 1));
+      }
       uint32_t* d0 = reinterpret_cast<uint32_t*>(dT[0]);
       uint32_t* d1 = reinterpret_cast<uint32_t*>(dT[1]);
       uint32_t* d2 = reinterpret_cast<uint32_t*>(dT[2]);
@@ -1107,7 +1124,22 @@ __global__ __launch_bounds__(256) void spatial_dense_wgrad_mfma_f32_kernel(Spati
         float4 a = *reinterpret_cast<const float4*>(dpre + r0 + 4 * k);
         float4 c = *reinterpret_cast<const float4*>(dpre + r1 + 4 * k);
         float4 ga = make_float4(1.f, 1.f, 1.f, 1.f), gc = ga;
-        if (gate != nullptr) {
+        if constexpr (POOLED) {
+          // gate > 0 <=> this pixel is the channel's argmax in its window and the pooled ReLU output is positive
+          const float4 ya = *reinterpret_cast<const float4*>(py + r0 + 4 * k);
+          const float4 yc = *reinterpret_cast<const float4*>(py + r1 + 4 * k);
+          const uint32_t pa = *reinterpret_cast<const uint32_t*>(ppos + r0 + 4 * k);
+          const uint32_t pc = *reinterpret_cast<const uint32_t*>(ppos + r1 + 4 * k);
+          const float yav[4] = {ya.x, ya.y, ya.z, ya.w}, ycv[4] = {yc.x, yc.y, yc.z, yc.w};
+          float gav[4], gcv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            gav[j] = (((pa >> (8 * j)) & 0xffu) == t0 && yav[j] > 0.f) ? 1.f : 0.f;
+            gcv[j] = (((pc >> (8 * j)) & 0xffu) == t1 && ycv[j] > 0.f) ? 1.f : 0.f;
+          }
+          ga = make_float4(gav[0], gav[1], gav[2], gav[3]);
+          gc = make_float4(gcv[0], gcv[1], gcv[2], gcv[3]);
+        } else if (gate != nullptr) {
           ga = *reinterpret_cast<const float4*>(gate + r0 + 4 * k);
           gc = *reinterpret_cast<const float4*>(gate + r1 + 4 * k);
         }
@@ -1344,12 +1376,55 @@ void spatial_dense_wgrad(const SpatialPlanes& sp, const void* dpre, const void* 
     hipLaunchKernelGGL(spatial_dense_wgrad_kernel<bf16_t>, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256), 0, s, sp,
                        static_cast<const bf16_t*>(dpre), static_cast<const bf16_t*>(gate), part, H, W, L, tiles, kSpWgPerObs);
   else if (spatial_mfma())
-    hipLaunchKernelGGL(spatial_dense_wgrad_mfma_f32_kernel, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256), 0, s,
-                       sp, static_cast<const float*>(dpre), static_cast<const float*>(gate), part, H, W, L, tiles,
-                       kSpWgPerObs);
+    hipLaunchKernelGGL(spatial_dense_wgrad_mfma_f32_kernel<false>, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256),
+                       0, s, sp, static_cast<const float*>(dpre), static_cast<const float*>(gate), part, H, W, L, tiles,
+                       kSpWgPerObs, nullptr, nullptr);
   else
     hipLaunchKernelGGL(spatial_dense_wgrad_kernel<float>, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256), 0, s, sp,
                        static_cast<const float*>(dpre), static_cast<const float*>(gate), part, H, W, L, tiles, kSpWgPerObs);
+}
+
+void spatial_dense_wgrad_pooled(const SpatialPlanes& sp, const float* dy, const float* y, const uint8_t* pos,
+                                float* part, int B, int H, int W, int L, hipStream_t s) {
+  const int tiles = (H * W + kSpTile - 1) / kSpTile;
+  if (B == 0) return;
+  hipLaunchKernelGGL(spatial_dense_wgrad_mfma_f32_kernel<true>, dim3(static_cast<unsigned>(B) * kSpWgPerObs), dim3(256),
+                     0, s, sp, dy, nullptr, part, H, W, L, tiles, kSpWgPerObs, y, pos);
+}
+
+namespace {
+// rows gather of the pooled form (see spatial_dense_wgrad_mfma_f32_kernel<true>): an entity at full-resolution (x, y)
+// takes the pooled gradient of its window where that channel's argmax is its pixel and the pooled output is positive
+__global__ __launch_bounds__(256) void gather_rows_pooled_kernel(const float* __restrict__ dy, const float* __restrict__ yp,
+                                                                 const uint8_t* __restrict__ pos,
+                                                                 const uint8_t* __restrict__ ex,
+                                                                 const uint8_t* __restrict__ ey,
+                                                                 const int64_t* __restrict__ entity_num,
+                                                                 float* __restrict__ drows, int B, int N, int H, int W) {
+  const long i = static_cast<long>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= static_cast<long>(B) * N * 32) return;
+  const int c = static_cast<int>(i & 31);
+  const long bn = i >> 5;
+  const int b = static_cast<int>(bn / N);
+  const int n = static_cast<int>(bn % N);
+  float v = 0.f;
+  if (n < entity_num[b]) {
+    int x = ex[bn], y = ey[bn];
+    x = x < W ? x : W - 1;
+    y = y < H ? y : H - 1;
+    const long o = ((static_cast<long>(b) * (H >> 1) + (y >> 1)) * (W >> 1) + (x >> 1)) * 32 + c;
+    if (pos[o] == static_cast<uint8_t>((y & 1) * 2 + (x & 1)) && yp[o] > 0.f) v = dy[o];
+  }
+  drows[i] = v;
+}
+}  // namespace
+
+void gather_rows_pooled(const float* dy, const float* y, const uint8_t* pos, const uint8_t* ex, const uint8_t* ey,
+                        const int64_t* entity_num, float* drows, int B, int N, int H, int W, hipStream_t s) {
+  const long n = static_cast<long>(B) * N * 32;
+  if (n == 0) return;
+  hipLaunchKernelGGL(gather_rows_pooled_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, s, dy, y, pos,
+                     ex, ey, entity_num, drows, B, N, H, W);
 }
 
 void relu_cast(const float* x, void* y, int dt, long n, hipStream_t s) {

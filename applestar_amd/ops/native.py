@@ -422,6 +422,14 @@ class _SpatialEmbedPool(torch.autograd.Function):
         pooled, pos, ex, ey, entity_num, *tensors = ctx.saved_tensors
         planes, effects = list(tensors[:ctx.n_planes]), list(tensors[ctx.n_planes:])
         H, W = ctx.HW
+        if POOLED_BWD and pooled.dtype == torch.float32 and H % 2 == 0 and W % 2 == 0:
+            # fp32: the row gather and the dense weight gradient compute dpre from the pooled gradient, the argmax bytes
+            # and the pooled ReLU output on the fly - no 1.2 GB full-resolution dpre written and read back twice
+            dy = dpooled.to(torch.float32).contiguous()
+            drows = _C.spatial_gather_rows_pooled(dy, pooled.contiguous(), pos.contiguous(), ex, ey, entity_num, ctx.N,
+                                                  H, W).to(ctx.rows_dtype)
+            dw, db = _C.spatial_dense_wgrad_pooled(planes, effects, dy, pooled.contiguous(), pos.contiguous())
+            return (dw, db, drows) + (None,) * (4 + len(tensors))
         dpre = _C.maxpool2_bwd_relu(dpooled.to(pooled.dtype).contiguous(), pos, pooled, H, W)
         drows = _C.spatial_gather_rows(dpre, ex, ey, entity_num, ctx.N).to(ctx.rows_dtype)
         dw, db = _C.spatial_dense_wgrad(planes, effects, dpre)
@@ -429,6 +437,8 @@ class _SpatialEmbedPool(torch.autograd.Function):
 
 
 SPATIAL_POOL_FUSED_F32 = os.environ.get('APPLESTAR_SPATIAL_POOL_FUSED_F32', '1') == '1'
+# the fp32 fused embed + pool backward without the full-resolution dpre (spatial.hip *_pooled; A/B switch)
+POOLED_BWD = os.environ.get('APPLESTAR_POOLED_BWD', '1') == '1'
 
 
 def spatial_embed_pool(spatial_info, rows, entity_x, entity_y, entity_num, w_dense, bias):
