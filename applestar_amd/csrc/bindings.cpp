@@ -183,7 +183,9 @@ SplitBufs make_split(const at::Tensor& like, int64_t B, int64_t width) {
   const int64_t Bp = (B + 7) / 8 * 8;
   // granules [2, Bp, 8, width] u64 (backward) or data [2, Bp, 8, width] u32 + flags [Bp, 8] (forward):
   // one zeroed buffer sized for either
-  r.slab = at::zeros({2 * Bp * 8 * width + Bp * 8}, like.options().dtype(at::kLong));
+  const int64_t KS = std::getenv("APPLESTAR_LSTM_KS") != nullptr && std::atoi(std::getenv("APPLESTAR_LSTM_KS")) == 16
+                       ? 16 : 8;     // workgroups per row (lstm.hip lstm_ks)
+  r.slab = at::zeros({2 * Bp * KS * width + Bp * KS}, like.options().dtype(at::kLong));
   r.s = {reinterpret_cast<unsigned long long*>(r.slab.data_ptr<int64_t>()), lstm_split_err(like.device()).data_ptr<int>()};
   return r;
 }

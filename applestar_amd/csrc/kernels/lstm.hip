@@ -520,6 +520,17 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_kernel(
 // The poll is bounded: after kSplitPollLimit passes it sets *err and continues (garbage, but the grid drains).
 constexpr int kSplitKS = 8;
 
+// workgroups per batch row (APPLESTAR_LSTM_KS = 8 | 16): 16 halves each workgroup's W_hh slice (48 weights per thread)
+// and the per-step GEMV, at twice the partials exchanged per step.  Measured slower: fp32 50.55 / 50.52 vs 50.28 / 50.20
+// ms (profiles/r10za_bench_lstm_ks.txt) - the exchange, not the GEMV, sets the step; 8 stays the default
+int lstm_ks() {
+  static const int v = [] {
+    const char* e = std::getenv("APPLESTAR_LSTM_KS");
+    return (e != nullptr && std::atoi(e) == 16) ? 16 : 8;
+  }();
+  return v;
+}
+
 // poll budget of the cross-workgroup exchange (each pass sleeps ~64 clocks plus one L2 round trip: ~2^20
 // passes is ~1 s).  Running out sets the sticky device flag (bindings: lstm_split_flag), which the trainers
 // read with the step's logged scalars: the optimizer update of that step is gated to zero and the learner
@@ -582,7 +593,7 @@ __device__ __forceinline__ void get_granules(const unsigned long long* base, lon
 // GRAN: the partial exchange as {epoch, value} granules (as the backward): every thread writes its partials and
 // polls the 8 x COLS granules it needs - one L2 round trip after the slowest producer, where the flag hand-off
 // (data stores, drain, barrier, flag store, flag poll, barrier, data loads) takes three
-template <int H, int NT, typename TW, bool GRAN>
+template <int H, int NT, typename TW, bool GRAN, int KS_ = kSplitKS>
 __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
     const float* __restrict__ xp, const float* __restrict__ h0, const float* __restrict__ c0,
     const TW* __restrict__ wT, const float* __restrict__ lnh_w, const float* __restrict__ lnh_b,
@@ -591,7 +602,7 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
     float* __restrict__ gates_out, float* __restrict__ xhat_c, float* __restrict__ rstd_c, float* __restrict__ hT,
     float* __restrict__ cT, unsigned long long* __restrict__ slab, int* __restrict__ err,
     bf16_t* __restrict__ out_bf) {
-  constexpr int KS = kSplitKS;
+  constexpr int KS = KS_;
   constexpr int G = 4 * H, RS = H / KS, COLS = G / NT, GS = G / KS;
   static_assert(G % NT == 0 && H % KS == 0 && NT >= H, "split tiling");
   __shared__ float h_s[H];
@@ -765,7 +776,7 @@ __global__ __launch_bounds__(NT) void lnlstm_fwd_split_kernel(
 }
 
 // w: W_hh [4H][H] row-major
-template <int H, int NT, typename TW>
+template <int H, int NT, typename TW, int KS_ = kSplitKS>
 __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
     const float* __restrict__ dout, const float* __restrict__ dhT, const float* __restrict__ dcT,
     const float* __restrict__ gates, const float* __restrict__ c_all, const float* __restrict__ xhat_c,
@@ -773,7 +784,7 @@ __global__ __launch_bounds__(NT) void lnlstm_bwd_split_kernel(
     const TW* __restrict__ w, const float* __restrict__ lnh_w, const float* __restrict__ lnc_w, int T, int B, int Bp,
     float* __restrict__ dgates, float* __restrict__ dhg, float* __restrict__ dc_ln, float* __restrict__ dh0,
     float* __restrict__ dc0, unsigned long long* __restrict__ slab, int* __restrict__ err) {
-  constexpr int KS = kSplitKS;
+  constexpr int KS = KS_;
   constexpr int G = 4 * H, COLS = G / NT, JS = G / KS, RH = NT / H, JR = JS / RH, RS = H / KS;
   static_assert(NT % H == 0 && JS % RH == 0 && G % NT == 0, "split tiling");
   __shared__ float dh_s[H];
@@ -952,19 +963,22 @@ void lnlstm_fwd(const float* xp, const float* h0, const float* c0, const void* w
                 float* cT, hipStream_t s, const LstmSplit* split, unsigned short* out_bf16) {
   if (H == 384 && split != nullptr) {
     const int Bp = (B + 7) / 8 * 8;
-    const dim3 grid(Bp * kSplitKS);
+    const int ks = lstm_ks();
+    const dim3 grid(Bp * ks);
     static const bool gran = [] {
       const char* e = std::getenv("APPLESTAR_LSTM_FWD_GRANULE");   // A/B switch, off by default
       return e != nullptr && e[0] == '1';
     }();
-#define AS_FWD_SPLIT(TWv, GR)                                                                                    \
-    hipLaunchKernelGGL((lnlstm_fwd_split_kernel<384, 768, TWv, GR>), grid, dim3(768), 0, s, xp, h0, c0,          \
+#define AS_FWD_SPLIT(TWv, GR, KSv)                                                                               \
+    hipLaunchKernelGGL((lnlstm_fwd_split_kernel<384, 768, TWv, GR, KSv>), grid, dim3(768), 0, s, xp, h0, c0,     \
                        static_cast<const TWv*>(wT), lnh_w, lnh_b, lnc_w, lnc_b, T, B, Bp, eps, out, c_all, xhat_h,  \
                        rstd_h, gates, xhat_c, rstd_c, hT, cT, split->slab, split->err, out_bf16)
-    if (w_dt == DT_BF16) {
-      if (gran) AS_FWD_SPLIT(bf16_t, true); else AS_FWD_SPLIT(bf16_t, false);
+    if (ks == 16) {
+      if (w_dt == DT_BF16) AS_FWD_SPLIT(bf16_t, false, 16); else AS_FWD_SPLIT(float, false, 16);
+    } else if (w_dt == DT_BF16) {
+      if (gran) AS_FWD_SPLIT(bf16_t, true, 8); else AS_FWD_SPLIT(bf16_t, false, 8);
     } else {
-      if (gran) AS_FWD_SPLIT(float, true); else AS_FWD_SPLIT(float, false);
+      if (gran) AS_FWD_SPLIT(float, true, 8); else AS_FWD_SPLIT(float, false, 8);
     }
 #undef AS_FWD_SPLIT
   } else if (H == 384) {
@@ -988,15 +1002,18 @@ void lnlstm_bwd(const float* dout, const float* dhT, const float* dcT, const flo
                 float* dc_ln, float* dh0, float* dc0, hipStream_t s, const LstmSplit* split) {
   if (H == 384 && split != nullptr) {
     const int Bp = (B + 7) / 8 * 8;
-    const dim3 grid(Bp * kSplitKS);
-    if (w_dt == DT_BF16)
-      hipLaunchKernelGGL((lnlstm_bwd_split_kernel<384, 768, bf16_t>), grid, dim3(768), 0, s, dout, dhT, dcT, gates,
-                         c_all, xhat_c, rstd_c, xhat_h, rstd_h, static_cast<const bf16_t*>(w), lnh_w, lnc_w, T, B, Bp,
-                         dgates, dhg, dc_ln, dh0, dc0, split->slab, split->err);
-    else
-      hipLaunchKernelGGL((lnlstm_bwd_split_kernel<384, 768, float>), grid, dim3(768), 0, s, dout, dhT, dcT, gates,
-                         c_all, xhat_c, rstd_c, xhat_h, rstd_h, static_cast<const float*>(w), lnh_w, lnc_w, T, B, Bp,
-                         dgates, dhg, dc_ln, dh0, dc0, split->slab, split->err);
+    const int ks = lstm_ks();
+    const dim3 grid(Bp * ks);
+#define AS_BWD_SPLIT(TWv, KSv)                                                                                   \
+    hipLaunchKernelGGL((lnlstm_bwd_split_kernel<384, 768, TWv, KSv>), grid, dim3(768), 0, s, dout, dhT, dcT, gates,  \
+                       c_all, xhat_c, rstd_c, xhat_h, rstd_h, static_cast<const TWv*>(w), lnh_w, lnc_w, T, B, Bp,    \
+                       dgates, dhg, dc_ln, dh0, dc0, split->slab, split->err)
+    if (ks == 16) {
+      if (w_dt == DT_BF16) AS_BWD_SPLIT(bf16_t, 16); else AS_BWD_SPLIT(float, 16);
+    } else {
+      if (w_dt == DT_BF16) AS_BWD_SPLIT(bf16_t, 8); else AS_BWD_SPLIT(float, 8);
+    }
+#undef AS_BWD_SPLIT
   } else if (H == 384)
     bwd_launch<384, 768, 2>(dout, dhT, dcT, gates, c_all, xhat_c, rstd_c, xhat_h, rstd_h, w, w_dt, lnh_w, lnc_w, T, B,
                             dgates, dhg, dc_ln, dh0, dc0, s);
