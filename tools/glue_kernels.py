@@ -20,6 +20,7 @@ def main():
     ap.add_argument('--precision', choices=['fp32', 'bf16'], default='fp32')
     ap.add_argument('--match', default='Fill,copy,threshold,CUDAFunctor_add,copyBuffer,CatArray,where,Mul')
     ap.add_argument('--top', type=int, default=40)
+    ap.add_argument('--shapes', action='store_true', help='key the sites by the launching op\'s input shapes too')
     args = ap.parse_args()
     import bench
     from applestar_amd.rl.synthetic import rl_batch
@@ -38,7 +39,8 @@ def main():
         tr.step(next(it))
     torch.cuda.synchronize()
     from torch.profiler import profile, ProfilerActivity
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True,
+                 record_shapes=args.shapes) as prof:
         tr.step(next(it))
         torch.cuda.synchronize()
     keys = [k for k in args.match.split(',') if k]
@@ -69,6 +71,8 @@ def main():
                 fr = next((f for f in (e.stack or []) if 'torch/' not in f), None)
                 site = '(no frame) ' + ' < '.join(chain[1:]) + (f' @ {fr}' if fr else '')
             key = f'{kind:16s} {e.name:28s} {site}'
+            if args.shapes:
+                key += f'  {[tuple(x) for x in (e.input_shapes or []) if x][:2]}'
             sites[key][0] += 1
             sites[key][1] += dur
             kinds[kind][0] += 1
