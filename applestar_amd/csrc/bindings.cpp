@@ -740,7 +740,8 @@ at::Tensor upconv1_fwd(const at::Tensor& x_nhwc, const at::Tensor& w, const at::
   return y;
 }
 
-std::vector<at::Tensor> upconv1_bwd(const at::Tensor& x_nhwc, const at::Tensor& w, const at::Tensor& dy) {
+std::vector<at::Tensor> upconv1_bwd(const at::Tensor& x_nhwc, const at::Tensor& w, const at::Tensor& dy,
+                                    bool relu_mask) {
   check_cuda(x_nhwc, "x");
   check_cuda(w, "w");
   check_cuda(dy, "dy");
@@ -757,7 +758,7 @@ std::vector<at::Tensor> upconv1_bwd(const at::Tensor& x_nhwc, const at::Tensor& 
   auto dwb = at::empty({as::upconv1_channels() * 9 + 1}, dy.options());
   as::upconv1_bwd(x_nhwc.data_ptr(), dt(x_nhwc), w.data_ptr<float>(), dy.data_ptr<float>(), dx.data_ptr(),
                   part.data_ptr<float>(), dwb.data_ptr<float>(), static_cast<int>(B), static_cast<int>(H),
-                  static_cast<int>(W), stream());
+                  static_cast<int>(W), stream(), relu_mask);
   return {dx, dwb};
 }
 
@@ -2405,7 +2406,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("segment_copy", &segment_copy);
   m.def("conv_wt", &conv_wt);
   m.def("upconv1_fwd", &upconv1_fwd);
-  m.def("upconv1_bwd", &upconv1_bwd);
+  m.def("upconv1_bwd", &upconv1_bwd, py::arg("x_nhwc"), py::arg("w"), py::arg("dy"), py::arg("relu_mask") = false);
   m.def("maxpool2_fwd", &maxpool2_fwd);
   m.def("maxpool2_bwd", &maxpool2_bwd, py::arg("dy"), py::arg("pos"), py::arg("H"), py::arg("W"),
         py::arg("mask") = py::none());

@@ -209,7 +209,7 @@ void upconv1_fwd(const void* x, int x_dt, const float* w, const float* bias, flo
                  hipStream_t s);
 // dx NHWC (x's dtype), dwb [289] = (dW[32*9], db); part [upconv1_tiles, 289] scratch
 void upconv1_bwd(const void* x, int x_dt, const float* w, const float* dy, void* dx, float* part, float* dwb, int B,
-                 int Hl, int Wl, hipStream_t s);
+                 int Hl, int Wl, hipStream_t s, bool relu_mask = false);
 }  // namespace as
 
 namespace as {

@@ -158,7 +158,8 @@ __device__ __forceinline__ float tap_weight(int p, int q, int n_in) {
 template <typename T>
 __global__ __launch_bounds__(kThreads) void upconv1_bwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                               const float* __restrict__ dy, T* __restrict__ dx,
-                                                              float* __restrict__ part, int Hl, int Wl) {
+                                                              float* __restrict__ part, int Hl, int Wl,
+                                                              int relu_mask) {
   __shared__ float dy_s[DR][DCP];
   __shared__ float dz_s[kK][kThreads];
   __shared__ float x_s[kC][kThreads + 1];
@@ -222,7 +223,8 @@ __global__ __launch_bounds__(kThreads) void upconv1_bwd_kernel(const T* __restri
       float s = 0.f;
 #pragma unroll
       for (int k = 0; k < kK; ++k) s = fmaf(w[c * kK + k], dz[k], s);
-      g[c] = s;
+      // x is a ReLU output: its mask (x > 0) = relu'(pre) is applied here, the producer skips its threshold pass
+      g[c] = (relu_mask && !(v[c] > 0.f)) ? 0.f : s;
     }
     store_px(dx + px, g);
   }
@@ -269,15 +271,15 @@ void upconv1_fwd(const void* x, int x_dt, const float* w, const float* bias, flo
 }
 
 void upconv1_bwd(const void* x, int x_dt, const float* w, const float* dy, void* dx, float* part, float* dwb, int B,
-                 int Hl, int Wl, hipStream_t s) {
+                 int Hl, int Wl, hipStream_t s, bool relu_mask) {
   const dim3 grid((Wl + LW - 1) / LW, (Hl + LH - 1) / LH, B);
   const long tiles = upconv1_tiles(B, Hl, Wl);
   if (x_dt == DT_BF16)
     hipLaunchKernelGGL(upconv1_bwd_kernel<bf16_t>, grid, dim3(kThreads), 0, s, static_cast<const bf16_t*>(x), w, dy,
-                       static_cast<bf16_t*>(dx), part, Hl, Wl);
+                       static_cast<bf16_t*>(dx), part, Hl, Wl, relu_mask ? 1 : 0);
   else
     hipLaunchKernelGGL(upconv1_bwd_kernel<float>, grid, dim3(kThreads), 0, s, static_cast<const float*>(x), w, dy,
-                       static_cast<float*>(dx), part, Hl, Wl);
+                       static_cast<float*>(dx), part, Hl, Wl, relu_mask ? 1 : 0);
   column_reduce(part, dwb, static_cast<int>(tiles), kC * kK + 1, s);
 }
 

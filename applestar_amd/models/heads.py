@@ -166,6 +166,8 @@ class QueuedHead(_ArgMLPHead):
 
 # teacher-forced split (Policy.train_forward): the earlier steps' embedding update goes with the pointer half (A/B)
 SU_AE_SIDE = os.environ.get('APPLESTAR_SU_AE_SIDE', '1') == '1'
+# ... and its queries over the earlier steps take query_fc1 folded into embed_fc2 (SelectedUnitsHead._query_in_folded)
+SU_FOLD = os.environ.get('APPLESTAR_SU_FOLD', '1') == '1'
 
 
 class SelectedUnitsHead(nn.Module):
@@ -266,13 +268,17 @@ class SelectedUnitsHead(nn.Module):
         """Teacher-forced pointer logits [B,S,N+1] from forward_teacher(split=True)'s inputs."""
         key, labels, base_mask, en, step_ok = (ptr[k] for k in ('key', 'labels', 'base_mask', 'en', 'step_ok'))
         ae_in = ptr.get('ae_in')
+        q_h = None
         if ae_in is None:
             ae0 = ptr['ae0']
-            ae_prev = self._ae_update(ae0.unsqueeze(1), ptr['emb_prev'])     # [B,S-1,1024]
-            ae_in = torch.cat([ae0.unsqueeze(1).to(ae_prev.dtype), ae_prev], 1)
+            if SU_FOLD and not self.query_fc1.norm:
+                q_h = self._query_in_folded(ae0, ptr['emb_prev'])            # [B,S,256]
+            else:
+                ae_prev = self._ae_update(ae0.unsqueeze(1), ptr['emb_prev'])     # [B,S-1,1024]
+                ae_in = torch.cat([ae0.unsqueeze(1).to(ae_prev.dtype), ae_prev], 1)
         B, N1, _ = key.shape
         S = labels.shape[1]
-        q_in = self.query_fc2(self.query_fc1(ae_in))                     # [B,S,32]
+        q_in = self.query_fc2(self.query_fc1(ae_in) if q_h is None else q_h)   # [B,S,32]
         state = self.lstm.zero_state(B, q_in.device, torch.float32)
         q, _ = self.lstm(q_in.transpose(0, 1), state)                    # [S,B,32]
         logits = torch.bmm(q.transpose(0, 1).float(), key.float().transpose(1, 2))  # [B,S,N+1]
@@ -289,6 +295,23 @@ class SelectedUnitsHead(nn.Module):
             mask = mask & step_ok[None, :, None]
         # the reference returns no sampled units in teacher-forced mode (test_iou off)
         return torch.where(mask, logits, NEG)
+
+    def _query_in_folded(self, ae0, emb_prev):
+        """relu(query_fc1([ae0, ae0 + embed_fc2(embed_fc1(emb_prev))])) [B,S,256] without the [B, S-1, 1024] embedding
+        update: query_fc1 is linear, so Wq (ae0 + We2 h + be2) + bq = (Wq ae0 + bq) + (Wq We2) h + Wq be2 - one
+        256 x 256 product over the earlier steps instead of two 1024-wide ones, and neither the 1024-wide
+        intermediates nor their gradients reach HBM (the sampler's fold, pointer.hip, in the training graph).
+        Same function (fp32 products reassociated); gradients reach Wq, We2, be2 through the fold."""
+        q1, e2 = self.query_fc1[0], self.embed_fc2[0]
+        h = self.embed_fc1(emb_prev)                                     # [B,S-1,256]
+        dt = torch.promote_types(q1.weight.dtype, torch.float32)
+        with torch.autocast(ae0.device.type, enabled=False):             # the fold itself in (at least) fp32
+            wq = q1.weight.to(dt)
+            wf = wq @ e2.weight.to(dt)                                   # [256,256]
+            bf = wq @ e2.bias.to(dt)                                     # [256]
+        p0 = ops.linear(ae0, q1.weight, q1.bias)                         # [B,256]
+        pp = ops.linear(h, wf, bf) + p0.unsqueeze(1)                     # [B,S-1,256]
+        return F.relu(torch.cat([p0.unsqueeze(1), pp.to(p0.dtype)], 1))
 
     # ------------------------------------------------------------------ sampling (actor)
     def _folded_query(self):

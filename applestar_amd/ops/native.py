@@ -565,6 +565,9 @@ def su_sample(key, c0, u, entity_num, su_mask, wf_bf16, bf, wq2, bq2, cell, we1,
 
 
 # ---------------------------------------------------------------------------- upsample x2 + conv -> 1 ch
+UPCONV_RELU = os.environ.get('APPLESTAR_UPCONV_RELU', '1') == '1'   # A/B switch
+
+
 class _UpsampleConvOut(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x_nhwc, w, b):
@@ -574,12 +577,17 @@ class _UpsampleConvOut(torch.autograd.Function):
         ctx.save_for_backward(x_nhwc, w32)
         ctx.has_bias = b is not None
         ctx.w_shape, ctx.w_dtype = w.shape, w.dtype
+        # an fp32 ReLU conv output as input: dX takes its mask in the kernel (the conv skips its threshold pass)
+        relu_in = UPCONV_RELU and x_nhwc.dtype == torch.float32 and x_nhwc.is_contiguous() and _relu_src(x_nhwc)
+        ctx.x_ptr = x_nhwc.data_ptr() if relu_in else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x_nhwc, w32 = ctx.saved_tensors
-        dx, dwb = _C.upconv1_bwd(x_nhwc, w32, dy.float().contiguous())
+        dx, dwb = _C.upconv1_bwd(x_nhwc, w32, dy.float().contiguous(), ctx.x_ptr is not None)
+        if ctx.x_ptr is not None:
+            _MASKED_DX[ctx.x_ptr] = (dx, dx._version)
         dw = dwb[:-1].view(ctx.w_shape).to(ctx.w_dtype)
         db = dwb[-1:].to(ctx.w_dtype) if ctx.has_bias else None
         return dx, dw, db

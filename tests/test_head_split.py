@@ -49,3 +49,32 @@ def test_selected_units_split_matches_forward_teacher(reduce_type):
     ptr, emb2, _ = su.forward_teacher(ae0, ee, en, sun, sel, split=True)
     assert _close(emb2, emb, 1e-5)
     assert _close(su.pointer_logits(ptr), logits, 1e-5)
+
+
+def test_selected_units_folded_queries_gradients_match():
+    """The split pointer half takes query_fc1 folded into embed_fc2 (SU_FOLD): the loss gradients of every head
+    parameter and of the input embedding match the unsplit (unfolded) head's."""
+    torch.manual_seed(3)
+    su = heads.SelectedUnitsHead()
+    B, N = 4, 20
+    ae0, ee = torch.randn(B, 1024), torch.randn(B, N, 256)
+    en = torch.tensor([3, 20, 9, 1])
+    sun = torch.tensor([2, 64, 4, 0])
+    sel = torch.randint(0, N, (B, 64))
+    sel[torch.arange(B), sun.clamp(max=63)] = en
+    grads = []
+    for split in (False, True):
+        su.zero_grad()
+        a = ae0.clone().requires_grad_()
+        if split:
+            ptr, emb, _ = su.forward_teacher(a, ee, en, sun, sel, split=True)
+            logits = su.pointer_logits(ptr)
+        else:
+            logits, _, emb, _ = su.forward_teacher(a, ee, en, sun, sel)
+        w = torch.linspace(-1, 1, logits.shape[-1])
+        (torch.where(logits > -1e8, logits, 0) * w).sum().backward(retain_graph=True)
+        (emb * emb).mean().backward()
+        grads.append([a.grad.clone()] + [p.grad.clone() if p.grad is not None else torch.zeros_like(p)
+                                         for p in su.parameters()])
+    for g0, g1 in zip(*grads):
+        assert _close(g1, g0, 2e-5), float((g1 - g0).abs().max())

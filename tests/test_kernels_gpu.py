@@ -1420,12 +1420,13 @@ print("ok")
     assert out.returncode == 0 and out.stdout.strip().endswith('ok'), out.stderr[-2000:]
 
 
-@pytest.mark.parametrize('between', ['maxpool', 'upsample'])
+@pytest.mark.parametrize('between', ['maxpool', 'upsample', 'upconv'])
 @pytest.mark.parametrize('extra_consumer', [False, True])
 def test_conv_relu_mask_handoff_f32(between, extra_consumer):
-    """fp32 conv(ReLU) -> maxpool / bilinear x2 -> conv: the pool / upsample backward applies the first conv's ReLU
-    mask and the conv backward skips its threshold pass (ops/native.py _premasked); with a second consumer of the
-    ReLU output the summed gradient takes the mask as usual.  Both vs float64."""
+    """fp32 conv(ReLU) -> maxpool / bilinear x2 -> conv (or the fused bilinear x2 + conv 32 -> 1, upconv1): the pool /
+    upsample / upconv backward applies the first conv's ReLU mask and the conv backward skips its threshold pass
+    (ops/native.py _premasked); with a second consumer of the ReLU output the summed gradient takes the mask as
+    usual.  Both vs float64."""
     from applestar_amd import ops
     torch.manual_seed(12)
     cl = torch.channels_last
@@ -1437,6 +1438,14 @@ def test_conv_relu_mask_handoff_f32(between, extra_consumer):
 
     def net(x, w1, b1, w2, ref):
         h = ops.conv2d(x, w1, b1, 1, 1, act='relu') if not ref else torch.relu(torch.nn.functional.conv2d(x, w1, b1, 1, 1))
+        if between == 'upconv':
+            if not ref:
+                y = N.upsample_conv_out(h, w2[:1], None)
+            else:
+                up = torch.nn.functional.interpolate(h, scale_factor=2.0, mode='bilinear', align_corners=False)
+                y = torch.nn.functional.conv2d(up, w2[:1], None, 1, 1)
+            out = (y * y).sum()
+            return out + (h * h).sum() if extra_consumer else out
         if between == 'maxpool':
             m = N.maxpool2x2(h) if not ref else torch.nn.functional.max_pool2d(h, 2, 2)
         else:
@@ -1447,6 +1456,7 @@ def test_conv_relu_mask_handoff_f32(between, extra_consumer):
         return out + (h * h).sum() if extra_consumer else out
     net(x, w1, b1, w2, False).backward()
     net(*ts, True).backward()
+    assert not N._MASKED_DX, 'the producer did not consume the hand-off'
     for name, a, r in zip(('dx', 'dw1', 'db1', 'dw2'), (x, w1, b1, w2), ts):
         e = _err(a.grad.cpu(), r.grad)
         assert e < 3e-5 * max(1.0, r.grad.abs().max().item()), (name, e)
