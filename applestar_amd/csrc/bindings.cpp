@@ -57,7 +57,7 @@ std::vector<at::Tensor> layer_norm_fwd(const at::Tensor& x, const c10::optional<
 
 std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& xin, const at::Tensor& y,
                                        const at::Tensor& w, const at::Tensor& mean, const at::Tensor& rstd,
-                                       int64_t dx_dtype, int64_t act) {
+                                       int64_t dx_dtype, int64_t act, const c10::optional<at::Tensor>& mask_src) {
   check_cuda(dy, "dy");
   check_cuda(xin, "xin");
   const int64_t C = xin.size(-1);
@@ -68,11 +68,19 @@ std::vector<at::Tensor> layer_norm_bwd(const at::Tensor& dy, const at::Tensor& x
   auto part = at::empty({nblk, 2 * C}, xin.options().dtype(at::kFloat));
   auto dwb = at::empty({2 * C}, xin.options().dtype(at::kFloat));
   const at::Tensor& yy = act != 0 ? y : dy;
+  at::Tensor dxm;
+  if (mask_src.has_value()) {
+    TORCH_CHECK(mask_src->scalar_type() == at::kFloat && mask_src->is_contiguous() && mask_src->numel() == rows * C,
+                "layer_norm_bwd: mask_src fp32 contiguous, x's size");
+    dxm = at::empty(xin.sizes(), xin.options().dtype(at::kFloat));
+  }
   as::layer_norm_bwd(dy.data_ptr(), dt(dy), xin.data_ptr(), dt(xin), yy.data_ptr(), dt(yy), w.data_ptr<float>(),
                      mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr(), dt(dx),
                      part.data_ptr<float>(), part.data_ptr<float>() + C, rows, static_cast<int>(C),
-                     static_cast<int>(act), nblk, stream());
+                     static_cast<int>(act), nblk, stream(), dxm.defined() ? mask_src->data_ptr<float>() : nullptr,
+                     dxm.defined() ? dxm.data_ptr<float>() : nullptr);
   as::column_reduce(part.data_ptr<float>(), dwb.data_ptr<float>(), nblk, static_cast<int>(2 * C), stream());
+  if (dxm.defined()) return {dx, dwb.narrow(0, 0, C), dwb.narrow(0, C, C), dxm};
   return {dx, dwb.narrow(0, 0, C), dwb.narrow(0, C, C)};
 }
 
@@ -2338,7 +2346,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "applestar_amd HIP kernels for gfx950 (MI355X)";
   register_codec(m);
   m.def("layer_norm_fwd", &layer_norm_fwd);
-  m.def("layer_norm_bwd", &layer_norm_bwd);
+  m.def("layer_norm_bwd", &layer_norm_bwd, py::arg("dy"), py::arg("xin"), py::arg("y"), py::arg("w"), py::arg("mean"),
+        py::arg("rstd"), py::arg("dx_dtype"), py::arg("act"), py::arg("mask_src") = py::none());
   m.def("reverse_scan", &reverse_scan);
   m.def("col_sum", &col_sum);
   m.def("multi_logp", &multi_logp);

@@ -29,10 +29,12 @@ struct EntityFields {
 void layer_norm_fwd(const void* x, int x_dt, const void* res, int res_dt, const float* w, const float* b,
                     void* y, int y_dt, float* xsum, float* mean, float* rstd, long rows, int cols, float eps,
                     int act, hipStream_t s);
-// dx (fp32 or bf16) and per-block partial dw/db [nblk, cols] (reduced by layer_norm_bwd_reduce).
+// dx (fp32 or bf16) and per-block partial dw/db [nblk, cols] (reduced by layer_norm_bwd_reduce).  msrc / dxm
+// (optional, fp32): dxm = dx masked by (msrc > 0), for an x that is a ReLU output.
 void layer_norm_bwd(const void* dy, int dy_dt, const void* xin, int xin_dt, const void* y, int y_dt,
                     const float* w, const float* mean, const float* rstd, void* dx, int dx_dt,
-                    float* dw_part, float* db_part, long rows, int cols, int act, int nblk, hipStream_t s);
+                    float* dw_part, float* db_part, long rows, int cols, int act, int nblk, hipStream_t s,
+                    const float* msrc = nullptr, float* dxm = nullptr);
 void column_reduce(const float* part, float* out, int nrows, int cols, hipStream_t s);
 // entity packing tables (valid [B][N], packed -> padded row flat[total], segment seg[total], offsets cu[B + 1])
 void entity_pack(const void* num, bool num64, int B, int N, long total, bool* valid, int64_t* flat, int64_t* seg,

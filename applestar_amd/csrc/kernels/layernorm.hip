@@ -123,7 +123,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
                                                      const TY* __restrict__ y, const float* __restrict__ w,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
                                                      TO* __restrict__ dx, float* __restrict__ dw_part,
-                                                     float* __restrict__ db_part, long rows, int act) {
+                                                     float* __restrict__ db_part, long rows, int act,
+                                                     const float* __restrict__ msrc, float* __restrict__ dxm) {
   constexpr int C = VPT * kWave;
   __shared__ float red[4][2][C];
   const int lane = threadIdx.x & 63;
@@ -162,6 +163,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const TD* __restrict__ dy, 
 #pragma unroll
     for (int i = 0; i < VPT; ++i) o[i] = rs * (g[i] * wv[i] - s1 - xh[i] * s2);
     store_row<VPT>(dx, base, lane, o);
+    if (dxm) {
+      // x is an fp32 ReLU output: its masked gradient as a second output (the residual branch keeps dx unmasked)
+      float m[VPT];
+      load_row<VPT>(msrc, base, lane, m);
+#pragma unroll
+      for (int i = 0; i < VPT; ++i) o[i] = m[i] > 0.f ? o[i] : 0.f;
+      store_row<VPT>(dxm, base, lane, o);
+    }
   }
   store_row<VPT>(&red[wib][0][0], 0, lane, dwa);
   store_row<VPT>(&red[wib][1][0], 0, lane, dba);
@@ -203,12 +212,12 @@ void fwd_dispatch(const void* x, int x_dt, const void* res, int res_dt, const fl
 template <int VPT>
 void bwd_dispatch(const void* dy, int dy_dt, const void* xin, int xin_dt, const void* y, int y_dt, const float* w,
                   const float* mean, const float* rstd, void* dx, int dx_dt, float* dwp, float* dbp, long rows,
-                  int act, int nblk, hipStream_t s) {
+                  int act, int nblk, hipStream_t s, const float* msrc, float* dxm) {
   dim3 grid(nblk), block(256);
 #define LN_BWD(TD, TX, TY, TO)                                                                           \
   hipLaunchKernelGGL((ln_bwd_kernel<VPT, TD, TX, TY, TO>), grid, block, 0, s, static_cast<const TD*>(dy), \
                      static_cast<const TX*>(xin), static_cast<const TY*>(y), w, mean, rstd, static_cast<TO*>(dx), \
-                     dwp, dbp, rows, act)
+                     dwp, dbp, rows, act, msrc, dxm)
   // y dtype == dy dtype in every use (y is the forward output, dy its gradient)
   if (dy_dt == DT_F32 && xin_dt == DT_F32 && dx_dt == DT_F32) LN_BWD(float, float, float, float);
   else if (dy_dt == DT_F32 && xin_dt == DT_BF16 && dx_dt == DT_BF16) LN_BWD(float, bf16_t, float, bf16_t);
@@ -249,9 +258,9 @@ void layer_norm_fwd(const void* x, int x_dt, const void* res, int res_dt, const 
 
 void layer_norm_bwd(const void* dy, int dy_dt, const void* xin, int xin_dt, const void* y, int y_dt, const float* w,
                     const float* mean, const float* rstd, void* dx, int dx_dt, float* dw_part, float* db_part,
-                    long rows, int cols, int act, int nblk, hipStream_t s) {
+                    long rows, int cols, int act, int nblk, hipStream_t s, const float* msrc, float* dxm) {
   VPT_SWITCH(cols, bwd_dispatch, dy, dy_dt, xin, xin_dt, y, y_dt, w, mean, rstd, dx, dx_dt, dw_part, db_part, rows,
-             act, nblk, s);
+             act, nblk, s, msrc, dxm);
 }
 
 }  // namespace as

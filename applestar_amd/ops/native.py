@@ -84,6 +84,9 @@ class GradLink:
         self.version = None
 
 
+LN_RELU_MASK = os.environ.get('APPLESTAR_LN_RELU_MASK', '1') == '1'   # A/B switch
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, res, w, b, act, eps, out_dtype, link=None):
@@ -91,7 +94,10 @@ class _LayerNorm(torch.autograd.Function):
         res_c = res.contiguous() if res is not None else None
         y, mean, rstd, xsum = _C.layer_norm_fwd(x_c, res_c, w, b, _dt_code(out_dtype), eps, _ACT[act], True)
         xin = xsum if res is not None else x_c
-        ctx.save_for_backward(xin, y, w, mean, rstd)
+        # residual LN over an fp32 ReLU output (the transformer FFN's last layer): the backward writes x's gradient
+        # masked as a second output beside the residual's unmasked one, so the ReLU's producer skips its threshold
+        ctx.mask_x = LN_RELU_MASK and res is not None and x_c.dtype == torch.float32 and _relu_src(x_c)
+        ctx.save_for_backward(xin, y, w, mean, rstd, x_c if ctx.mask_x else None)
         ctx.act = act
         ctx.has_res = res is not None
         ctx.x_dtype = x.dtype
@@ -101,16 +107,21 @@ class _LayerNorm(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        xin, y, w, mean, rstd = ctx.saved_tensors
+        xin, y, w, mean, rstd, xm = ctx.saved_tensors
         dy = dy.contiguous()
-        dx, dw, db = _C.layer_norm_bwd(dy, xin, y, w, mean, rstd, _dt_code(ctx.x_dtype), _ACT[ctx.act])
+        dxm = None
+        if xm is not None and ctx.needs_input_grad[0]:
+            dx, dw, db, dxm = _C.layer_norm_bwd(dy, xin, y, w, mean, rstd, _dt_code(ctx.x_dtype), _ACT[ctx.act], xm)
+            _MASKED_DX[xm.data_ptr()] = (dxm, dxm._version)
+        else:
+            dx, dw, db = _C.layer_norm_bwd(dy, xin, y, w, mean, rstd, _dt_code(ctx.x_dtype), _ACT[ctx.act])
         dres = None
         if ctx.has_res:
             dres = dx if ctx.res_dtype == ctx.x_dtype else dx.to(ctx.res_dtype)
             if ctx.link is not None and ctx.needs_input_grad[1]:
                 ctx.link.g, dres = dres, None      # added by the branch linear's dX GEMM (GradLink)
                 ctx.link.version = ctx.link.g._version if _DEBUG_GRADLINK else None
-        return dx, dres, dw, db, None, None, None, None
+        return dx if dxm is None else dxm, dres, dw, db, None, None, None, None
 
 
 def layer_norm(x, w, b, residual=None, act=None, eps=1e-5, out_dtype=None, grad_link=None):

@@ -1420,6 +1420,40 @@ print("ok")
     assert out.returncode == 0 and out.stdout.strip().endswith('ok'), out.stderr[-2000:]
 
 
+@pytest.mark.parametrize('linked', [False, True])
+def test_residual_ln_relu_mask_handoff_f32(linked):
+    """Transformer FFN shape: x -> relu(x W1^T + b1) -> relu(. W2^T + b2) = m -> LN(m + x).  The residual LayerNorm's
+    backward writes m's gradient masked by (m > 0) as a second output (ops/native.py LN_RELU_MASK) and the second
+    linear skips its threshold pass; the residual gradient stays unmasked (through autograd, or handed to the first
+    linear's dX GEMM with a GradLink).  Every gradient vs float64."""
+    from applestar_amd import ops
+    torch.manual_seed(14)
+    R, C, Hd = 3000, 256, 512
+    x = torch.randn(R, C, device=DEV).requires_grad_()
+    w1 = (torch.randn(Hd, C, device=DEV) / C ** 0.5).requires_grad_()
+    b1 = (0.1 * torch.randn(Hd, device=DEV)).requires_grad_()
+    w2 = (torch.randn(C, Hd, device=DEV) / Hd ** 0.5).requires_grad_()
+    b2 = (0.1 * torch.randn(C, device=DEV)).requires_grad_()
+    lw = (1 + 0.1 * torch.randn(C, device=DEV)).requires_grad_()
+    lb = (0.1 * torch.randn(C, device=DEV)).requires_grad_()
+    ts = [_f64(t) for t in (x, w1, b1, w2, b2, lw, lb)]
+    link = ops.grad_link(x) if linked else None
+    h = N.linear(x, w1, b1, act='relu', grad_link=link)
+    m = N.linear(h, w2, b2, act='relu')
+    assert N._relu_src(m)
+    y = N.layer_norm(m, lw, lb, residual=x, grad_link=link)
+    xs, w1s, b1s, w2s, b2s, lws, lbs = ts
+    ms = torch.relu(torch.relu(xs @ w1s.t() + b1s) @ w2s.t() + b2s)
+    ys = torch.nn.functional.layer_norm(ms + xs, (C,), lws, lbs)
+    g = torch.randn(R, C, dtype=torch.float64)
+    y.backward(g.float().to(DEV))
+    ys.backward(g)
+    assert not N._MASKED_DX, 'the producer did not consume the hand-off'
+    for name, a, r in zip(('dx', 'dw1', 'db1', 'dw2', 'db2', 'dlw', 'dlb'), (x, w1, b1, w2, b2, lw, lb), ts):
+        e = _err(a.grad.cpu(), r.grad)
+        assert e < 3e-5 * max(1.0, r.grad.abs().max().item()), (name, e)
+
+
 @pytest.mark.parametrize('between', ['maxpool', 'upsample', 'upconv'])
 @pytest.mark.parametrize('extra_consumer', [False, True])
 def test_conv_relu_mask_handoff_f32(between, extra_consumer):
