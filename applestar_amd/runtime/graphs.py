@@ -14,6 +14,8 @@ argument, else ``APPLESTAR_GRAPHS=1``); anything else calls the module directly.
 """
 from __future__ import annotations
 
+import contextlib
+import gc
 import os
 from typing import Dict, Tuple
 
@@ -24,6 +26,22 @@ import torch.nn as nn
 GRAPH_SIDE_STREAMS = os.environ.get('APPLESTAR_GRAPH_SIDE_STREAMS', '0') == '1'
 
 __all__ = ['GraphedSection', 'graphs_enabled']
+
+
+@contextlib.contextmanager
+def gc_paused():
+    """Python's cyclic garbage collector paused while a HIP graph is captured (collected once before).  A collection
+    inside the capture runs the destructors of unrelated garbage from earlier eager steps against the capturing
+    process - one aborted the whole-step capture of test_graphed_train_step_matches_eager mid-forward
+    ("Garbage-collecting" frame on the aborting thread)."""
+    was = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def graphs_enabled() -> bool:
@@ -71,7 +89,7 @@ class GraphedSection:
             if len(self._graphs) >= self.max_signatures:   # shapes keep changing: not a static section
                 return self.module(*args)
             sample = tuple(a.detach().clone().requires_grad_(a.requires_grad) for a in args)
-            with torch.autocast('cuda', dtype=sig[-1], enabled=sig[-2], cache_enabled=False):
+            with torch.autocast('cuda', dtype=sig[-1], enabled=sig[-2], cache_enabled=False), gc_paused():
                 g = torch.cuda.make_graphed_callables(_Holder(self.module), sample, num_warmup_iters=self.warmup,
                                                       allow_unused_input=True)
             self._graphs[sig] = g
@@ -174,7 +192,7 @@ class GraphedPolicy:
                         self._run(static_in)
                 torch.cuda.current_stream().wait_stream(side)
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
+                with gc_paused(), torch.cuda.graph(g):
                     static_out = self._run(static_in)
             finally:
                 encoders.STATIC_SHAPES, encoders.SCALAR_SIDE_STREAM, model_mod.SIDE_STREAMS_ENABLED = flags

@@ -39,6 +39,8 @@ from typing import Callable, Dict, Optional, Tuple
 
 import torch
 
+from .graphs import gc_paused
+
 __all__ = ['GraphedTrainStep', 'batch_signature']
 
 
@@ -157,7 +159,7 @@ class GraphedTrainStep:
         if not self.side_streams:
             encoders.SCALAR_SIDE_STREAM = model_mod.SIDE_STREAMS_ENABLED = False
         try:
-            with torch.cuda.graph(e.fb, pool=self._pool):
+            with gc_paused(), torch.cuda.graph(e.fb, pool=self._pool):
                 info = self.fwd_bwd(e.static_in)
                 e.keys = sorted(k for k, v in info.items() if torch.is_tensor(v) and v.numel() == 1)
                 e.packed = torch.stack([info[k].detach().float().reshape(()) for k in e.keys]) if e.keys else None
@@ -169,7 +171,7 @@ class GraphedTrainStep:
         e.upd = None
         if not self.single_graph:
             e.upd = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(e.upd, pool=self._pool):
+            with gc_paused(), torch.cuda.graph(e.upd, pool=self._pool):
                 e.grad_norm = self.update().detach().float().reshape(())
         self.captures += 1
         self._graphs[key] = e
