@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import math
 import os
+import weakref
 
 from typing import Dict, List, Tuple, Optional
 
@@ -311,6 +312,8 @@ class EntityEncoder(nn.Module):
         ee = self.entity_fc(x)
         entity_embeddings = ee.new_zeros(B * N, ee.shape[-1])
         entity_embeddings = entity_embeddings.index_copy(0, flat_index, ee).view(B, N, -1)
+        # the packed rows behind the padded output, for a consumer that projects them directly (Encoder.forward)
+        self._packed = (weakref.ref(entity_embeddings), ee, flat_index)
         if self.reduce_type.startswith('attention_pool'):
             xp = x.new_zeros(B * N, x.shape[-1]).index_copy(0, flat_index, x).view(B, N, -1)
             pooled = self.attention_pool(xp, num=entity_num, mask=valid)
@@ -455,6 +458,9 @@ class SpatialEncoder(nn.Module):
 
 
 SCALAR_SIDE_STREAM = True
+# the spatial scatter projection over the packed entity rows (APPLESTAR_PACKED_SCATTER=0: over the padded rows + mask);
+# fp32 only: fp32 49.25 / 48.92 vs 49.23 / 49.31 ms, bf16 neutral within its noise (profiles/r10zm_bench_packed_scatter.txt)
+PACKED_SCATTER = os.environ.get('APPLESTAR_PACKED_SCATTER', '1') == '1'
 # bf16 inference: the scalar encoder's concatenated pieces kept in bf16 (APPLESTAR_SCALAR_BF16_INFERENCE=0: as trained)
 SCALAR_BF16_INFERENCE = os.environ.get('APPLESTAR_SCALAR_BF16_INFERENCE', '1') == '1'
 # set by runtime.graphs.GraphedPolicy while capturing / replaying: shape-static entity path
@@ -489,7 +495,16 @@ class Encoder(nn.Module):
             (self.scalar_encoder(scalar_info), None)
         entity_embeddings, embedded_entity, entity_mask = self.entity_encoder(entity_info, entity_num, entity_total,
                                                                               entity_pad)
-        proj = self.scatter_project(entity_embeddings) * entity_mask.unsqueeze(2).to(entity_embeddings.dtype)
+        pk, self.entity_encoder._packed = getattr(self.entity_encoder, '_packed', None), None
+        if PACKED_SCATTER and pk is not None and pk[0]() is entity_embeddings and not torch.is_autocast_enabled():
+            # the scatter projection over the packed entity rows, zero-padded afterwards (its padded rows were masked
+            # to zero anyway): half the rows of the GEMMs, and the padded 256-wide embeddings then have one consumer
+            # in training (the heads' keys), so autograd sums no two [B * N, 256] input gradients
+            B, N = entity_embeddings.shape[:2]
+            p = self.scatter_project(pk[1])
+            proj = p.new_zeros(B * N, p.shape[-1]).index_copy(0, pk[2], p).view(B, N, -1)
+        else:
+            proj = self.scatter_project(entity_embeddings) * entity_mask.unsqueeze(2).to(entity_embeddings.dtype)
         n = ops._native(proj) if proj.is_cuda else None
         if n is not None and n.has('spatial_embed'):
             embedded_spatial, map_skip = self.spatial_encoder.forward_native(
